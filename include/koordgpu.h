@@ -1,0 +1,303 @@
+/*
+ * koordgpu.h — C ABI of the MI355X scheduling evaluator (libkoordgpu.so).
+ *
+ * This is the drop-in boundary for koord-scheduler's per-pod Filter/Score
+ * sweep.  A Go cgo shim or any C/C++ host calls it.
+ * Plain C types only: caller-owned flat arrays, int status codes, no torch or
+ * HIP types in any signature.
+ *
+ * What each entry point replaces in the reference (xulinfei1996/koordinator,
+ * paths relative to its root; "upstream" = k8s.io/kubernetes v1.24.15):
+ *
+ *   ks_create          plugin construction through PluginFactoryProxy
+ *                      (pkg/scheduler/frameworkext/framework_extender_factory.go:209-221)
+ *                      for LoadAwareScheduling (pkg/scheduler/plugins/loadaware/load_aware.go:76-110),
+ *                      NodeResourcesFit (upstream noderesources/fit.go NewFit) and
+ *                      ElasticQuota (pkg/scheduler/plugins/elasticquota/plugin.go:102);
+ *                      args mirror pkg/scheduler/apis/config/types.go:30-62.
+ *   ks_load_nodes      scheduler cache snapshot (upstream Cache.UpdateSnapshot) + the
+ *   ks_update_nodes    LoadAware NodeMetric lister / podAssignCache state
+ *                      (load_aware.go:133,278; pod_assign_cache.go:53-117).
+ *   ks_load_quotas     GroupQuotaManager QuotaInfo used/runtime
+ *                      (pkg/scheduler/plugins/elasticquota/core/group_quota_manager.go:259-326).
+ *   ks_schedule        the per-pod cycle (upstream schedule_one.go schedulePod:
+ *                      PreFilter -> findNodesThatPassFilters -> prioritizeNodes -> selectHost)
+ *                      followed by Reserve (framework_extender.go:457; load_aware.go:260;
+ *                      elasticquota/plugin.go:323), for a batch of pods in queue order,
+ *                      with exact one-pod-at-a-time semantics.
+ *   ks_eval_pod_debug  one pod's Filter + Score over every node without Reserve
+ *                      (framework_extender.go:204 RunFilterPluginsWithNominatedPods,
+ *                      :237 RunScorePlugins) — the parity/debug entry point.
+ *
+ * Semantics pinned by this ABI: percentageOfNodesToScore=100 (every node is
+ * evaluated), and selectHost ties are broken by the LOWEST node index (the
+ * reference picks uniformly at random among ties).
+ *
+ * Quantities are int64 after the host's resource.Quantity conversion exactly as
+ * the reference does it: cpu -> MilliValue(), everything else -> Value()
+ * (pkg/scheduler/plugins/loadaware/helper.go:146-151).  Values must be in
+ * [0, 2^56); larger values are rejected with KS_EINVAL.
+ */
+#ifndef KOORDGPU_H
+#define KOORDGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KS_ABI_VERSION 1
+
+#define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
+#define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
+
+/* ---- status codes ---- */
+#define KS_OK 0
+#define KS_EINVAL (-1)       /* bad argument / value out of supported range   */
+#define KS_EHIP (-2)         /* HIP runtime error                               */
+#define KS_ESTATE (-3)       /* call out of order (e.g. schedule before load)   */
+#define KS_EUNSUPPORTED (-4) /* configuration not supported by this build       */
+#define KS_ENOMEM (-5)
+
+/* ---- NodeResourcesFit scoring strategy (pkg/scheduler/apis/config/types.go:84-92) ---- */
+#define KS_LEAST_ALLOCATED 0
+#define KS_MOST_ALLOCATED 1
+
+/* ---- per-node LoadAware flags (ks_node_cols.la_flags) ----
+ * Resolved by the host from the NodeMetric object, node annotations and the
+ * plugin args, exactly at the points the reference reads them. */
+#define KS_LA_HAS_METRIC 0x01u          /* nodeMetricLister.Get found it (load_aware.go:133,278)          */
+#define KS_LA_EXPIRED 0x02u             /* isNodeMetricExpired(nm, NodeMetricExpirationSeconds) (helper.go:36) */
+#define KS_LA_HAS_STATUS_METRIC 0x04u   /* nm.Status.NodeMetric != nil (load_aware.go:174)                */
+#define KS_LA_FILTER_USAGE_PRESENT 0x08u /* filter profile's nodeUsage != nil (load_aware.go:195-208)     */
+#define KS_LA_AGGREGATED_FILTER 0x10u   /* filter profile uses AggregatedUsage (reason string variant)    */
+#define KS_LA_NODE_THR_NONEMPTY 0x20u   /* len(usageThresholds) > 0 (load_aware.go:159)                   */
+#define KS_LA_PROD_THR_NONEMPTY 0x40u   /* len(ProdUsageThresholds) > 0 (load_aware.go:148)               */
+#define KS_LA_HAS_PODS_METRIC 0x80u     /* len(nm.Status.PodsMetric) > 0 (load_aware.go:227)              */
+
+/* ---- per-pod flags (ks_pod_cols.flags) ---- */
+#define KS_POD_PROD 0x01u            /* GetPodPriorityClassWithDefault == koord-prod (apis/extension/priority_utils.go:26) */
+#define KS_POD_DAEMONSET 0x02u       /* isDaemonSetPod(ownerRefs) (loadaware/helper.go:188)          */
+#define KS_POD_NONPREEMPTIBLE 0x04u  /* extension.IsPodNonPreemptible (elasticquota/plugin.go:236)   */
+#define KS_POD_SCALAR_KEYS 0x08u     /* podRequest.ScalarResources has at least one key (upstream fitsRequest) */
+
+/* ---- per-node filter reason bits (ks_eval_pod_debug) ---- */
+#define KS_R_FIT_PODS 0x001u      /* "Too many pods"                                    */
+#define KS_R_FIT_CPU 0x002u       /* "Insufficient cpu"                                 */
+#define KS_R_FIT_MEMORY 0x004u    /* "Insufficient memory"                              */
+#define KS_R_FIT_EPHEMERAL 0x008u /* "Insufficient ephemeral-storage"                   */
+#define KS_R_FIT_SCALAR 0x010u    /* "Insufficient <scalar>"                            */
+#define KS_R_LA_CPU 0x020u        /* ErrReasonUsageExceedThreshold cpu (load_aware.go:45) */
+#define KS_R_LA_MEMORY 0x040u     /* ErrReasonUsageExceedThreshold memory               */
+#define KS_R_LA_AGGREGATED 0x080u /* the failure used ErrReasonAggregatedUsageExceedThreshold */
+#define KS_R_LA_PROD 0x100u       /* the failure came from filterProdUsage              */
+
+/* ---- per-pod result status (ks_result.status) ---- */
+#define KS_S_SCHEDULED 0x0u
+#define KS_S_QUOTA 0x1u                /* ElasticQuota PreFilter: "Insufficient quotas"            */
+#define KS_S_QUOTA_NONPREEMPTIBLE 0x2u /* ElasticQuota PreFilter: "Insufficient non-preemptible quotas" */
+#define KS_S_QUOTA_PARENT 0x4u         /* checkQuotaRecursive rejected at a parent                 */
+#define KS_S_UNSCHEDULABLE 0x8u        /* no node passed Filter                                    */
+
+/* score plugin slots for ks_eval_pod_debug's per-plugin score matrix */
+#define KS_SCORE_FIT 0
+#define KS_SCORE_LOADAWARE 1
+#define KS_NUM_SCORE_PLUGINS 2
+
+/* NodeResourcesFitArgs.scoringStrategy (upstream apis/config/types.go; the profile in
+ * config/manager/scheduler-config.yaml:17-31). A weight of 0 means "not listed". */
+typedef struct ks_fit_args {
+  int32_t enable_filter;
+  int32_t enable_score;
+  int32_t strategy; /* KS_LEAST_ALLOCATED | KS_MOST_ALLOCATED */
+  int32_t _pad0;
+  int64_t weight_cpu;
+  int64_t weight_memory;
+  int64_t weight_ephemeral;
+  int64_t weight_scalar[KS_MAX_SCALARS];
+  int64_t plugin_weight; /* profile score weight */
+} ks_fit_args;
+
+/* LoadAwareSchedulingArgs (pkg/scheduler/apis/config/types.go:30-62) after
+ * SetDefaults_LoadAwareSchedulingArgs (v1beta2/defaults.go:77-100).  Per-node
+ * thresholds (custom-usage-thresholds annotation, aggregated profile) are
+ * resolved by the host into ks_node_cols; only the pod-independent knobs that
+ * the sweep needs live here.  Only cpu and memory may carry weights. */
+typedef struct ks_loadaware_args {
+  int32_t enable_filter;
+  int32_t enable_score;
+  int32_t filter_expired_node_metrics; /* FilterExpiredNodeMetrics (load_aware.go:141) */
+  int32_t score_according_prod_usage;  /* ScoreAccordingProdUsage (load_aware.go:294)  */
+  int64_t weight_cpu;                  /* ResourceWeights[cpu]; 0 = not listed          */
+  int64_t weight_memory;
+  int64_t scaling_cpu;                 /* EstimatedScalingFactors                        */
+  int64_t scaling_memory;
+  int64_t plugin_weight;
+} ks_loadaware_args;
+
+/* ElasticQuotaArgs (pkg/scheduler/apis/config/types.go) */
+typedef struct ks_quota_args {
+  int32_t enable;
+  int32_t enable_check_parent_quota; /* EnableCheckParentQuota (plugin.go:250) */
+} ks_quota_args;
+
+typedef struct ks_config {
+  int32_t abi_version; /* = KS_ABI_VERSION */
+  int32_t device;      /* HIP device ordinal */
+  ks_fit_args fit;
+  ks_loadaware_args loadaware;
+  ks_quota_args quota;
+  int32_t batch_pods;  /* pods evaluated per sweep pass (0 = default 64, max 64) */
+  int32_t candidates;  /* candidate node chunks kept per pod per pass (0 = default 32, max 64) */
+  int32_t profile;     /* 1 = bracket every kernel with HIP events (ks_get_stats) */
+  int32_t _pad1;
+} ks_config;
+
+/* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
+ * upstream framework.NodeInfo (Allocatable/Requested/NonZeroRequested/Pods).
+ * The LoadAware block is the host-side reduction of NodeMetric + podAssignCache
+ * documented in DESIGN.md §2 (reference: load_aware.go:123-376, helper.go:36-186). */
+typedef struct ks_node_cols {
+  const int64_t *alloc_milli_cpu;
+  const int64_t *alloc_memory;
+  const int64_t *alloc_ephemeral;
+  const int32_t *allowed_pods;
+  const int64_t *req_milli_cpu;   /* NodeInfo.Requested */
+  const int64_t *req_memory;
+  const int64_t *req_ephemeral;
+  const int32_t *pod_count;       /* len(NodeInfo.Pods) */
+  const int64_t *nonzero_milli_cpu; /* NodeInfo.NonZeroRequested */
+  const int64_t *nonzero_memory;
+  const int64_t *alloc_scalar[KS_MAX_SCALARS]; /* NULL = slot unused (treated as 0) */
+  const int64_t *req_scalar[KS_MAX_SCALARS];
+  /* LoadAwareScheduling */
+  const uint32_t *la_flags;        /* KS_LA_* */
+  const int64_t *la_alloc_milli_cpu; /* EstimateNode() allocatable (estimator/default_estimator.go:110-129) */
+  const int64_t *la_alloc_memory;
+  const int64_t *la_term_milli_cpu;  /* Σ assigned-estimated + node usage (load_aware.go:294-325), all pods */
+  const int64_t *la_term_memory;
+  const int64_t *la_prod_term_milli_cpu; /* same with filterProdPod=true (prod pod, ScoreAccordingProdUsage) */
+  const int64_t *la_prod_term_memory;
+  const int32_t *la_thr_cpu;          /* filter usage thresholds, 0 = skip (load_aware.go:185-187) */
+  const int32_t *la_thr_memory;
+  const int32_t *la_prod_thr_cpu;     /* prod usage thresholds, 0 = skip */
+  const int32_t *la_prod_thr_memory;
+  const int64_t *la_total_milli_cpu;  /* EstimateNode allocatable .MilliValue() (load_aware.go:214) */
+  const int64_t *la_total_milli_memory;
+  const int64_t *la_usage_milli_cpu;  /* filter profile usage .MilliValue() (node or aggregated) */
+  const int64_t *la_usage_milli_memory;
+  const int64_t *la_prod_usage_milli_cpu; /* Σ prod pod usages .MilliValue() (load_aware.go:231-248) */
+  const int64_t *la_prod_usage_milli_memory;
+} ks_node_cols;
+
+/* Pending pods, queue order, structure-of-arrays. */
+typedef struct ks_pod_cols {
+  const int64_t *req_milli_cpu;  /* upstream computePodResourceRequest (Fit PreFilter) */
+  const int64_t *req_memory;
+  const int64_t *req_ephemeral;
+  const int64_t *req_scalar[KS_MAX_SCALARS]; /* NULL = 0 */
+  const int64_t *nonzero_milli_cpu; /* non-zero request (100m / 200Mi defaults) for Fit score + NonZeroRequested */
+  const int64_t *nonzero_memory;
+  const uint32_t *flags;          /* KS_POD_* */
+  /* EstimatePod inputs (estimator/default_estimator.go:57-108): request/limit of the
+   * priority-translated resource name (resource.go:53-58), plus the value used when
+   * the quantity is zero (250 / 209715200 / 0). */
+  const int64_t *la_req_cpu;
+  const int64_t *la_lim_cpu;
+  const int64_t *la_dflt_cpu;
+  const int64_t *la_req_memory;
+  const int64_t *la_lim_memory;
+  const int64_t *la_dflt_memory;
+  /* ElasticQuota */
+  const int32_t *quota;           /* quota row, -1 = no quota (plugin.go:211-215) */
+  const uint32_t *quota_mask;     /* bit d: dimension d present in PodRequestsAndLimits keys */
+  const int64_t *quota_req[KS_QUOTA_DIMS];
+} ks_pod_cols;
+
+/* ElasticQuota table: QuotaInfo.CalculateInfo per quota (core/quota_info.go). */
+typedef struct ks_quota_cols {
+  const int32_t *parent;          /* parent row, -1 = child of root (plugin_helper.go:292) */
+  const uint32_t *limit_mask;     /* keys of getQuotaInfoUsedLimit (Runtime, or Max if !EnableRuntimeQuota) */
+  const int64_t *limit[KS_QUOTA_DIMS];
+  const int64_t *used[KS_QUOTA_DIMS];
+  const uint32_t *min_mask;       /* keys of CalculateInfo.Min */
+  const int64_t *min[KS_QUOTA_DIMS];
+  const int64_t *nonpreemptible_used[KS_QUOTA_DIMS];
+} ks_quota_cols;
+
+typedef struct ks_result {
+  int32_t node;    /* chosen node index, -1 if not scheduled */
+  uint32_t status; /* KS_S_* */
+  int64_t score;   /* total weighted score of the chosen node */
+} ks_result;
+
+/* Mutable node state after commits (read back for parity). */
+typedef struct ks_node_state {
+  int64_t *req_milli_cpu;
+  int64_t *req_memory;
+  int64_t *req_ephemeral;
+  int32_t *pod_count;
+  int64_t *nonzero_milli_cpu;
+  int64_t *nonzero_memory;
+  int64_t *req_scalar[KS_MAX_SCALARS]; /* NULL = skip */
+  int64_t *la_term_milli_cpu;
+  int64_t *la_term_memory;
+  int64_t *la_prod_term_milli_cpu;
+  int64_t *la_prod_term_memory;
+} ks_node_state;
+
+typedef struct ks_stats {
+  int64_t passes;          /* sweep passes executed by the last ks_schedule* call */
+  int64_t cut_passes;      /* passes ended early because a pod's candidates were exhausted */
+  int64_t rescans;         /* dirty-chunk rescans done by the commit kernel */
+  double sweep_ms;         /* summed HIP-event time of the sweep kernels */
+  double select_ms;        /* summed HIP-event time of the candidate-selection kernels */
+  double commit_ms;        /* summed HIP-event time of the commit kernels */
+  double total_ms;         /* wall time of the last call on the device stream */
+  int64_t sweep_launches;
+  int64_t sweep_bytes;     /* algorithmic bytes one sweep launch reads/writes */
+} ks_stats;
+
+typedef struct ks_ctx ks_ctx;
+
+/* Returns KS_OK and *out on success.  On failure *out is NULL and
+ * ks_last_error(NULL) describes the problem. */
+int ks_create(const ks_config *cfg, ks_ctx **out);
+void ks_destroy(ks_ctx *ctx);
+const char *ks_last_error(const ks_ctx *ctx);
+
+int ks_load_nodes(ks_ctx *ctx, const ks_node_cols *nodes, int64_t n);
+/* Informer deltas: rows[i] replaces node idx[i]; arrays in `rows` have length m. */
+int ks_update_nodes(ks_ctx *ctx, const int32_t *idx, const ks_node_cols *rows, int64_t m);
+int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
+
+/* Schedule `p` pods in order with commits; out[i] for pod i. Host buffers. */
+int ks_schedule(ks_ctx *ctx, const ks_pod_cols *pods, int32_t p, ks_result *out);
+
+/* Device-resident variant: stage pods once (host buffers copied to HBM), then
+ * schedule the staged batch; results stay in HBM until ks_fetch_results. */
+int ks_stage_pods(ks_ctx *ctx, const ks_pod_cols *pods, int32_t p);
+int ks_schedule_staged(ks_ctx *ctx);
+int ks_fetch_results(ks_ctx *ctx, ks_result *out, int32_t p);
+
+/* Snapshot save/restore of the mutable node + quota state (for repeatable benches). */
+int ks_checkpoint(ks_ctx *ctx);
+int ks_restore(ks_ctx *ctx);
+
+/* Evaluate pod 0 of `pod` against every node without Reserve.
+ * reasons[n] gets KS_R_* bits (0 = feasible); scores[n*KS_NUM_SCORE_PLUGINS+k]
+ * the un-weighted plugin-k score (0 for infeasible nodes); total[n] the weighted
+ * sum (-1 for infeasible). Any output pointer may be NULL. */
+int ks_eval_pod_debug(ks_ctx *ctx, const ks_pod_cols *pod, uint32_t *reasons, int64_t *scores,
+                      int64_t *total);
+
+int ks_read_nodes(ks_ctx *ctx, ks_node_state *out);
+int ks_read_quota_used(ks_ctx *ctx, int64_t *used /* q*KS_QUOTA_DIMS, row-major */);
+int ks_get_stats(const ks_ctx *ctx, ks_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KOORDGPU_H */

@@ -1,0 +1,241 @@
+"""ctypes mirror of include/koordgpu.h (the C ABI of libkoordgpu.so).
+
+Plain data layout only — every struct here is field-for-field identical to the
+header, so the same SoA buffers can be handed to the HIP library and to the CPU
+oracle.  Keep in sync with include/koordgpu.h (tests/test_abi.py checks sizes).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+KS_ABI_VERSION = 1
+KS_MAX_SCALARS = 4
+KS_QUOTA_DIMS = 8
+
+KS_OK = 0
+KS_EINVAL = -1
+KS_EHIP = -2
+KS_ESTATE = -3
+KS_EUNSUPPORTED = -4
+KS_ENOMEM = -5
+
+KS_LEAST_ALLOCATED = 0
+KS_MOST_ALLOCATED = 1
+
+KS_LA_HAS_METRIC = 0x01
+KS_LA_EXPIRED = 0x02
+KS_LA_HAS_STATUS_METRIC = 0x04
+KS_LA_FILTER_USAGE_PRESENT = 0x08
+KS_LA_AGGREGATED_FILTER = 0x10
+KS_LA_NODE_THR_NONEMPTY = 0x20
+KS_LA_PROD_THR_NONEMPTY = 0x40
+KS_LA_HAS_PODS_METRIC = 0x80
+
+KS_POD_PROD = 0x01
+KS_POD_DAEMONSET = 0x02
+KS_POD_NONPREEMPTIBLE = 0x04
+KS_POD_SCALAR_KEYS = 0x08
+
+KS_R_FIT_PODS = 0x001
+KS_R_FIT_CPU = 0x002
+KS_R_FIT_MEMORY = 0x004
+KS_R_FIT_EPHEMERAL = 0x008
+KS_R_FIT_SCALAR = 0x010
+KS_R_LA_CPU = 0x020
+KS_R_LA_MEMORY = 0x040
+KS_R_LA_AGGREGATED = 0x080
+KS_R_LA_PROD = 0x100
+
+KS_S_SCHEDULED = 0x0
+KS_S_QUOTA = 0x1
+KS_S_QUOTA_NONPREEMPTIBLE = 0x2
+KS_S_QUOTA_PARENT = 0x4
+KS_S_UNSCHEDULABLE = 0x8
+
+KS_SCORE_FIT = 0
+KS_SCORE_LOADAWARE = 1
+KS_NUM_SCORE_PLUGINS = 2
+
+P64 = C.POINTER(C.c_int64)
+P32 = C.POINTER(C.c_int32)
+PU32 = C.POINTER(C.c_uint32)
+
+
+class KsFitArgs(C.Structure):
+    _fields_ = [
+        ("enable_filter", C.c_int32),
+        ("enable_score", C.c_int32),
+        ("strategy", C.c_int32),
+        ("_pad0", C.c_int32),
+        ("weight_cpu", C.c_int64),
+        ("weight_memory", C.c_int64),
+        ("weight_ephemeral", C.c_int64),
+        ("weight_scalar", C.c_int64 * KS_MAX_SCALARS),
+        ("plugin_weight", C.c_int64),
+    ]
+
+
+class KsLoadAwareArgs(C.Structure):
+    _fields_ = [
+        ("enable_filter", C.c_int32),
+        ("enable_score", C.c_int32),
+        ("filter_expired_node_metrics", C.c_int32),
+        ("score_according_prod_usage", C.c_int32),
+        ("weight_cpu", C.c_int64),
+        ("weight_memory", C.c_int64),
+        ("scaling_cpu", C.c_int64),
+        ("scaling_memory", C.c_int64),
+        ("plugin_weight", C.c_int64),
+    ]
+
+
+class KsQuotaArgs(C.Structure):
+    _fields_ = [("enable", C.c_int32), ("enable_check_parent_quota", C.c_int32)]
+
+
+class KsConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32),
+        ("device", C.c_int32),
+        ("fit", KsFitArgs),
+        ("loadaware", KsLoadAwareArgs),
+        ("quota", KsQuotaArgs),
+        ("batch_pods", C.c_int32),
+        ("candidates", C.c_int32),
+        ("profile", C.c_int32),
+        ("_pad1", C.c_int32),
+    ]
+
+
+NODE_COLS = [
+    ("alloc_milli_cpu", P64),
+    ("alloc_memory", P64),
+    ("alloc_ephemeral", P64),
+    ("allowed_pods", P32),
+    ("req_milli_cpu", P64),
+    ("req_memory", P64),
+    ("req_ephemeral", P64),
+    ("pod_count", P32),
+    ("nonzero_milli_cpu", P64),
+    ("nonzero_memory", P64),
+    ("alloc_scalar", P64 * KS_MAX_SCALARS),
+    ("req_scalar", P64 * KS_MAX_SCALARS),
+    ("la_flags", PU32),
+    ("la_alloc_milli_cpu", P64),
+    ("la_alloc_memory", P64),
+    ("la_term_milli_cpu", P64),
+    ("la_term_memory", P64),
+    ("la_prod_term_milli_cpu", P64),
+    ("la_prod_term_memory", P64),
+    ("la_thr_cpu", P32),
+    ("la_thr_memory", P32),
+    ("la_prod_thr_cpu", P32),
+    ("la_prod_thr_memory", P32),
+    ("la_total_milli_cpu", P64),
+    ("la_total_milli_memory", P64),
+    ("la_usage_milli_cpu", P64),
+    ("la_usage_milli_memory", P64),
+    ("la_prod_usage_milli_cpu", P64),
+    ("la_prod_usage_milli_memory", P64),
+]
+
+
+class KsNodeCols(C.Structure):
+    _fields_ = NODE_COLS
+
+
+POD_COLS = [
+    ("req_milli_cpu", P64),
+    ("req_memory", P64),
+    ("req_ephemeral", P64),
+    ("req_scalar", P64 * KS_MAX_SCALARS),
+    ("nonzero_milli_cpu", P64),
+    ("nonzero_memory", P64),
+    ("flags", PU32),
+    ("la_req_cpu", P64),
+    ("la_lim_cpu", P64),
+    ("la_dflt_cpu", P64),
+    ("la_req_memory", P64),
+    ("la_lim_memory", P64),
+    ("la_dflt_memory", P64),
+    ("quota", P32),
+    ("quota_mask", PU32),
+    ("quota_req", P64 * KS_QUOTA_DIMS),
+]
+
+
+class KsPodCols(C.Structure):
+    _fields_ = POD_COLS
+
+
+QUOTA_COLS = [
+    ("parent", P32),
+    ("limit_mask", PU32),
+    ("limit", P64 * KS_QUOTA_DIMS),
+    ("used", P64 * KS_QUOTA_DIMS),
+    ("min_mask", PU32),
+    ("min", P64 * KS_QUOTA_DIMS),
+    ("nonpreemptible_used", P64 * KS_QUOTA_DIMS),
+]
+
+
+class KsQuotaCols(C.Structure):
+    _fields_ = QUOTA_COLS
+
+
+class KsResult(C.Structure):
+    _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64)]
+
+
+NODE_STATE_COLS = [
+    ("req_milli_cpu", P64),
+    ("req_memory", P64),
+    ("req_ephemeral", P64),
+    ("pod_count", P32),
+    ("nonzero_milli_cpu", P64),
+    ("nonzero_memory", P64),
+    ("req_scalar", P64 * KS_MAX_SCALARS),
+    ("la_term_milli_cpu", P64),
+    ("la_term_memory", P64),
+    ("la_prod_term_milli_cpu", P64),
+    ("la_prod_term_memory", P64),
+]
+
+
+class KsNodeState(C.Structure):
+    _fields_ = NODE_STATE_COLS
+
+
+class KsStats(C.Structure):
+    _fields_ = [
+        ("passes", C.c_int64),
+        ("cut_passes", C.c_int64),
+        ("rescans", C.c_int64),
+        ("sweep_ms", C.c_double),
+        ("select_ms", C.c_double),
+        ("commit_ms", C.c_double),
+        ("total_ms", C.c_double),
+        ("sweep_launches", C.c_int64),
+        ("sweep_bytes", C.c_int64),
+    ]
+
+
+# every symbol include/koordgpu.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = [
+    "ks_create",
+    "ks_destroy",
+    "ks_last_error",
+    "ks_load_nodes",
+    "ks_update_nodes",
+    "ks_load_quotas",
+    "ks_schedule",
+    "ks_stage_pods",
+    "ks_schedule_staged",
+    "ks_fetch_results",
+    "ks_checkpoint",
+    "ks_restore",
+    "ks_eval_pod_debug",
+    "ks_read_nodes",
+    "ks_read_quota_used",
+    "ks_get_stats",
+]

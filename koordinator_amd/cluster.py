@@ -1,0 +1,247 @@
+"""Structure-of-arrays tables for the C ABI (host side).
+
+``NodeTable`` / ``PodTable`` / ``QuotaTable`` own numpy columns laid out exactly
+as ``ks_node_cols`` / ``ks_pod_cols`` / ``ks_quota_cols`` expect and build the
+ctypes pointer structs on demand.  This is the Python stand-in for what the Go
+cgo shim does at informer time: NodeInfo fields come from the
+scheduler cache snapshot, the ``la_*`` block from the LoadAware reduction in
+:mod:`.ingest`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import abi
+
+NODE_I64 = [
+    "alloc_milli_cpu", "alloc_memory", "alloc_ephemeral",
+    "req_milli_cpu", "req_memory", "req_ephemeral",
+    "nonzero_milli_cpu", "nonzero_memory",
+    "la_alloc_milli_cpu", "la_alloc_memory",
+    "la_term_milli_cpu", "la_term_memory", "la_prod_term_milli_cpu", "la_prod_term_memory",
+    "la_total_milli_cpu", "la_total_milli_memory",
+    "la_usage_milli_cpu", "la_usage_milli_memory",
+    "la_prod_usage_milli_cpu", "la_prod_usage_milli_memory",
+]
+NODE_I32 = ["allowed_pods", "pod_count", "la_thr_cpu", "la_thr_memory", "la_prod_thr_cpu", "la_prod_thr_memory"]
+NODE_U32 = ["la_flags"]
+
+POD_I64 = [
+    "req_milli_cpu", "req_memory", "req_ephemeral",
+    "nonzero_milli_cpu", "nonzero_memory",
+    "la_req_cpu", "la_lim_cpu", "la_dflt_cpu", "la_req_memory", "la_lim_memory", "la_dflt_memory",
+]
+POD_I32 = ["quota"]
+POD_U32 = ["flags", "quota_mask"]
+
+STATE_I64 = [
+    "req_milli_cpu", "req_memory", "req_ephemeral", "nonzero_milli_cpu", "nonzero_memory",
+    "la_term_milli_cpu", "la_term_memory", "la_prod_term_milli_cpu", "la_prod_term_memory",
+]
+
+MAX_QUANTITY = 1 << 56  # ks ABI supported range
+
+
+def _p64(a: np.ndarray):
+    return a.ctypes.data_as(abi.P64)
+
+
+def _p32(a: np.ndarray):
+    return a.ctypes.data_as(abi.P32)
+
+
+def _pu32(a: np.ndarray):
+    return a.ctypes.data_as(abi.PU32)
+
+
+class _Table:
+    I64: list = []
+    I32: list = []
+    U32: list = []
+    N_SCALAR_ARRAYS: tuple = ()
+
+    def __init__(self, n: int):
+        self.n = int(n)
+        for name in self.I64:
+            setattr(self, name, np.zeros(self.n, np.int64))
+        for name in self.I32:
+            setattr(self, name, np.zeros(self.n, np.int32))
+        for name in self.U32:
+            setattr(self, name, np.zeros(self.n, np.uint32))
+
+    def columns(self) -> Dict[str, np.ndarray]:
+        return {k: getattr(self, k) for k in self.I64 + self.I32 + self.U32}
+
+    def _fix(self):
+        for name in self.I64:
+            a = getattr(self, name)
+            if a.dtype != np.int64 or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, np.int64))
+        for name in self.I32:
+            a = getattr(self, name)
+            if a.dtype != np.int32 or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, np.int32))
+        for name in self.U32:
+            a = getattr(self, name)
+            if a.dtype != np.uint32 or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, np.uint32))
+
+
+class NodeTable(_Table):
+    I64 = NODE_I64
+    I32 = NODE_I32
+    U32 = NODE_U32
+
+    def __init__(self, n: int):
+        super().__init__(n)
+        self.alloc_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
+        self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
+
+    def copy(self) -> "NodeTable":
+        t = NodeTable(self.n)
+        for k, v in self.columns().items():
+            setattr(t, k, v.copy())
+        t.alloc_scalar = self.alloc_scalar.copy()
+        t.req_scalar = self.req_scalar.copy()
+        return t
+
+    def rows(self, idx) -> "NodeTable":
+        idx = np.asarray(idx)
+        t = NodeTable(len(idx))
+        for k, v in self.columns().items():
+            setattr(t, k, np.ascontiguousarray(v[idx]))
+        t.alloc_scalar = np.ascontiguousarray(self.alloc_scalar[:, idx])
+        t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
+        return t
+
+    def check_range(self) -> None:
+        for name in NODE_I64:
+            a = getattr(self, name)
+            if a.size and (a.min() < 0 or a.max() >= MAX_QUANTITY):
+                raise ValueError(f"{name} outside [0, 2^56)")
+
+    def ks(self) -> abi.KsNodeCols:
+        self._fix()
+        self.alloc_scalar = np.ascontiguousarray(self.alloc_scalar, np.int64)
+        self.req_scalar = np.ascontiguousarray(self.req_scalar, np.int64)
+        c = abi.KsNodeCols()
+        for name in NODE_I64:
+            setattr(c, name, _p64(getattr(self, name)))
+        for name in NODE_I32:
+            setattr(c, name, _p32(getattr(self, name)))
+        c.la_flags = _pu32(self.la_flags)
+        for k in range(abi.KS_MAX_SCALARS):
+            c.alloc_scalar[k] = _p64(self.alloc_scalar[k])
+            c.req_scalar[k] = _p64(self.req_scalar[k])
+        c._keep = self  # keep arrays alive with the struct
+        return c
+
+
+class PodTable(_Table):
+    I64 = POD_I64
+    I32 = POD_I32
+    U32 = POD_U32
+
+    def __init__(self, n: int):
+        super().__init__(n)
+        self.quota[:] = -1
+        self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
+        self.quota_req = np.zeros((abi.KS_QUOTA_DIMS, self.n), np.int64)
+
+    def rows(self, idx) -> "PodTable":
+        idx = np.asarray(idx)
+        t = PodTable(len(idx))
+        for k, v in self.columns().items():
+            setattr(t, k, np.ascontiguousarray(v[idx]))
+        t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
+        t.quota_req = np.ascontiguousarray(self.quota_req[:, idx])
+        return t
+
+    def ks(self) -> abi.KsPodCols:
+        self._fix()
+        self.req_scalar = np.ascontiguousarray(self.req_scalar, np.int64)
+        self.quota_req = np.ascontiguousarray(self.quota_req, np.int64)
+        c = abi.KsPodCols()
+        for name in POD_I64:
+            setattr(c, name, _p64(getattr(self, name)))
+        c.quota = _p32(self.quota)
+        c.flags = _pu32(self.flags)
+        c.quota_mask = _pu32(self.quota_mask)
+        for k in range(abi.KS_MAX_SCALARS):
+            c.req_scalar[k] = _p64(self.req_scalar[k])
+        for d in range(abi.KS_QUOTA_DIMS):
+            c.quota_req[d] = _p64(self.quota_req[d])
+        c._keep = self
+        return c
+
+
+class QuotaTable:
+    def __init__(self, q: int):
+        self.q = int(q)
+        self.parent = np.full(self.q, -1, np.int32)
+        self.limit_mask = np.zeros(self.q, np.uint32)
+        self.min_mask = np.zeros(self.q, np.uint32)
+        self.limit = np.zeros((abi.KS_QUOTA_DIMS, self.q), np.int64)
+        self.used = np.zeros((abi.KS_QUOTA_DIMS, self.q), np.int64)
+        self.min = np.zeros((abi.KS_QUOTA_DIMS, self.q), np.int64)
+        self.nonpreemptible_used = np.zeros((abi.KS_QUOTA_DIMS, self.q), np.int64)
+
+    def copy(self) -> "QuotaTable":
+        t = QuotaTable(self.q)
+        for k in ("parent", "limit_mask", "min_mask", "limit", "used", "min", "nonpreemptible_used"):
+            setattr(t, k, getattr(self, k).copy())
+        return t
+
+    def ks(self) -> abi.KsQuotaCols:
+        c = abi.KsQuotaCols()
+        self.parent = np.ascontiguousarray(self.parent, np.int32)
+        c.parent = _p32(self.parent)
+        c.limit_mask = _pu32(self.limit_mask)
+        c.min_mask = _pu32(self.min_mask)
+        for name in ("limit", "used", "min", "nonpreemptible_used"):
+            arr = np.ascontiguousarray(getattr(self, name), np.int64)
+            setattr(self, name, arr)
+            field = getattr(c, name)
+            for d in range(abi.KS_QUOTA_DIMS):
+                field[d] = _p64(arr[d])
+        c._keep = self
+        return c
+
+
+class NodeState:
+    """Host buffers for ks_read_nodes / ko_read_nodes."""
+
+    def __init__(self, n: int):
+        self.n = n
+        for name in STATE_I64:
+            setattr(self, name, np.zeros(n, np.int64))
+        self.pod_count = np.zeros(n, np.int32)
+        self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, n), np.int64)
+
+    def ks(self) -> abi.KsNodeState:
+        s = abi.KsNodeState()
+        for name in STATE_I64:
+            setattr(s, name, _p64(getattr(self, name)))
+        s.pod_count = _p32(self.pod_count)
+        for k in range(abi.KS_MAX_SCALARS):
+            s.req_scalar[k] = _p64(self.req_scalar[k])
+        s._keep = self
+        return s
+
+    def as_dict(self) -> Dict[str, np.ndarray]:
+        d = {k: getattr(self, k) for k in STATE_I64}
+        d["pod_count"] = self.pod_count
+        d["req_scalar"] = self.req_scalar
+        return d
+
+
+def results_to_numpy(res) -> Dict[str, np.ndarray]:
+    arr = np.ctypeslib.as_array(res)
+    return {
+        "node": np.array([r.node for r in res], np.int32) if arr.dtype.names is None else arr["node"].copy(),
+        "status": np.array([r.status for r in res], np.uint32) if arr.dtype.names is None else arr["status"].copy(),
+        "score": np.array([r.score for r in res], np.int64) if arr.dtype.names is None else arr["score"].copy(),
+    }

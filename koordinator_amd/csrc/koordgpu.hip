@@ -1,0 +1,1342 @@
+// koordgpu.hip — MI355X (gfx950) scheduling evaluator behind the C ABI in include/koordgpu.h.
+//
+// Pipeline for ks_schedule (one "pass" = up to 64 queued pods):
+//
+//   sweep_kernel    streams the node SoA once per pod group, evaluates Filter+Score for every
+//                   (pod, node) with the reference's int64 formulas, and reduces each 64-node
+//                   chunk to its best (score, lowest index) per pod          -> chunk maxima
+//   select_kernel   per pod: the K best chunks (exact top-K by key)          -> candidate lists
+//   commit_kernel   ONE wave walks the pass's pods in queue order: quota admission, pick the best
+//                   candidate whose chunk no earlier pod of the pass touched, re-scan touched
+//                   chunks exactly, Reserve (NodeInfo/assign-cache/quota updates)  -> results
+//
+// Exactness: a pod's best node is max(best untouched node, best touched node).  Untouched nodes
+// keep their snapshot score, so chunk maxima of untouched chunks are exact; touched chunks are
+// re-scanned with the current state.  When every candidate chunk of a pod is touched and their
+// re-scanned best is below the K-th snapshot key, an untouched chunk outside the list could win:
+// the pass is cut there and the next pass re-sweeps from that pod.  Results are therefore
+// identical to scheduling one pod at a time (oracle/koord_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ks_device.h"
+
+using namespace ks;
+
+// ------------------------------------------------------------------------------------------
+// prep kernels
+// ------------------------------------------------------------------------------------------
+
+// usage := int64(math.Round(float64(used.MilliValue()) / float64(total.MilliValue()) * 100))
+// (load_aware.go:214,248); threshold 0 and zero total are skipped (:185-192)
+__device__ __forceinline__ bool usage_exceeds(int64_t used, int64_t total, int32_t thr) {
+  if (thr == 0 || total == 0) return false;
+  const int64_t usage = (int64_t)::round((double)used / (double)total * 100.0);
+  return usage >= thr;
+}
+
+// Per-node LoadAware filter/score flags; pod-dependent only through prod / daemonset.
+__global__ void prep_nodes_kernel(DevNodes d, int64_t n, int32_t filter_expired) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t f = d.la_flags[i];
+  uint32_t bits = 0;
+  if (!(f & KS_LA_HAS_METRIC) || (f & KS_LA_EXPIRED)) bits |= kLaZeroScore;  // load_aware.go:278-289
+  const bool pass_all = !(f & KS_LA_HAS_METRIC) || (filter_expired && (f & KS_LA_EXPIRED));
+  uint32_t r_np = 0, r_p = 0;
+  if (!pass_all) {
+    // filterNodeUsage (load_aware.go:173-224)
+    if ((f & KS_LA_NODE_THR_NONEMPTY) && (f & KS_LA_HAS_STATUS_METRIC) && (f & KS_LA_FILTER_USAGE_PRESENT)) {
+      const uint32_t agg = (f & KS_LA_AGGREGATED_FILTER) ? KS_R_LA_AGGREGATED : 0u;
+      if (usage_exceeds(d.la_usage_cpu[i], d.la_total_cpu[i], d.la_thr_cpu[i]))
+        r_np = KS_R_LA_CPU | agg;
+      else if (usage_exceeds(d.la_usage_mem[i], d.la_total_mem[i], d.la_thr_mem[i]))
+        r_np = KS_R_LA_MEMORY | agg;
+    }
+    if (f & KS_LA_PROD_THR_NONEMPTY) {
+      // filterProdUsage (load_aware.go:226-254)
+      if (f & KS_LA_HAS_PODS_METRIC) {
+        if (usage_exceeds(d.la_pusage_cpu[i], d.la_total_cpu[i], d.la_pthr_cpu[i]))
+          r_p = KS_R_LA_CPU | KS_R_LA_PROD;
+        else if (usage_exceeds(d.la_pusage_mem[i], d.la_total_mem[i], d.la_pthr_mem[i]))
+          r_p = KS_R_LA_MEMORY | KS_R_LA_PROD;
+      }
+    } else {
+      r_p = r_np;  // prod pods fall back to the node-usage path (load_aware.go:148-168)
+    }
+  }
+  if (r_np) bits |= kLaFailNonProd | (r_np << kLaReasonNonProdShift);
+  if (r_p) bits |= kLaFailProd | (r_p << kLaReasonProdShift);
+  d.la_bits[i] = bits;
+}
+
+struct DevPodCols {
+  int64_t *cpu, *mem, *eph, *nzcpu, *nzmem;
+  int64_t *sc[KS_MAX_SCALARS];
+  uint32_t *flags;
+  int32_t *quota;
+  int64_t *la_req_cpu, *la_lim_cpu, *la_dflt_cpu, *la_req_mem, *la_lim_mem, *la_dflt_mem;
+};
+
+// estimatedUsedByResource (estimator/default_estimator.go:73-108)
+__device__ __forceinline__ int64_t estimated_used(int64_t req, int64_t lim, int64_t sf, int64_t dflt) {
+  int64_t q;
+  if (lim > req) {
+    sf = 100;
+    q = lim;
+  } else {
+    q = req;
+  }
+  if (q == 0) return dflt;
+  int64_t est = (int64_t)::round((double)q * (double)sf / 100.0);
+  if (lim > 0 && est > lim) est = lim;
+  return est;
+}
+
+__global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t sf_cpu, int64_t sf_mem) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  PodRec r;
+  r.cpu = s.cpu[i];
+  r.mem = s.mem[i];
+  r.eph = s.eph[i];
+  r.nzcpu = s.nzcpu[i];
+  r.nzmem = s.nzmem[i];
+  r.est_cpu = estimated_used(s.la_req_cpu[i], s.la_lim_cpu[i], sf_cpu, s.la_dflt_cpu[i]);
+  r.est_mem = estimated_used(s.la_req_mem[i], s.la_lim_mem[i], sf_mem, s.la_dflt_mem[i]);
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) r.sc[k] = s.sc[k][i];
+  uint32_t fl = s.flags[i] & 0xffu;
+  if (r.cpu == 0 && r.mem == 0 && r.eph == 0 && !(fl & KS_POD_SCALAR_KEYS)) fl |= kPodAllZero;
+  r.flags = fl;
+  r.quota = s.quota[i];
+  r._pad[0] = r._pad[1] = r._pad[2] = 0;
+  out[i] = r;
+}
+
+// ------------------------------------------------------------------------------------------
+// sweep: chunk maxima
+// ------------------------------------------------------------------------------------------
+
+struct SweepArgs {
+  DevNodes d;
+  Cfg c;
+  const PodRec* __restrict__ pods;
+  const int32_t* __restrict__ cursor;
+  uint32_t* __restrict__ out;  // [nchunks][64]: lane p = best local key of pod p in the chunk
+  int64_t n, nchunks;
+  int32_t total_pods, batch, ppw;
+};
+
+// local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
+template <int NSC>
+__global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor);
+  const int32_t groups = (np + a.ppw - 1) / a.ppw;
+  const int64_t nwork = a.nchunks * groups;
+  for (int64_t w = wave; w < nwork; w += nwaves) {
+    const int64_t c = w / groups;
+    const int32_t g = (int32_t)(w - c * groups);
+    const int64_t node = c * 64 + lane;
+    NodeReg<NSC> r;
+    load_node<NSC>(a.d, node, node < a.n, r);
+    const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
+    uint32_t res = 0;
+    for (int32_t p = p0; p < p1; ++p) {
+      const PodRec pod = a.pods[cursor + p];
+      const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
+      const uint32_t key = o.reasons ? 0u : (((uint32_t)(o.total + 1) << 6) | (uint32_t)(63 - lane));
+      const uint32_t m = wave_max_u32(key);
+      res = (lane == p) ? m : res;
+    }
+    if (lane >= p0 && lane < p1) a.out[c * 64 + lane] = res;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// select: top-K chunks per pod
+// ------------------------------------------------------------------------------------------
+
+struct SelectArgs {
+  const uint32_t* __restrict__ in;  // sweep output
+  const int32_t* __restrict__ cursor;
+  uint32_t* cand_chunk;             // [64][K]
+  uint64_t* cand_key;               // [64][K]
+  uint64_t* cand_bound;             // [64]
+  int32_t* cand_count;              // [64]
+  int64_t nchunks;
+  int32_t total_pods, batch, k;
+};
+
+__device__ __forceinline__ uint64_t entry_gkey(uint32_t loc, int64_t chunk) {
+  if (loc == 0) return 0;
+  const int64_t node = chunk * 64 + (63 - (int64_t)(loc & 63u));
+  return ((uint64_t)(loc >> 6) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)node);
+}
+
+__global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
+  const int lane = threadIdx.x;
+  const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor);
+  const int32_t p = blockIdx.x;
+  if (p >= np) return;
+  const int32_t K = a.k;
+  // pass 1: feasible count and max score
+  int32_t cnt = 0;
+  uint32_t hmax = 0;
+  for (int64_t e = lane; e < a.nchunks; e += 64) {
+    const uint32_t h = a.in[e * 64 + p] >> 6;
+    cnt += h != 0;
+    hmax = h > hmax ? h : hmax;
+  }
+  cnt = wave_sum_i32(cnt);
+  hmax = wave_max_u32(hmax);
+  uint32_t t = 1;  // admit h >= t
+  int32_t need_eq = 0x7fffffff;
+  bool exhaustive = cnt <= K;
+  if (!exhaustive) {
+    // largest t with count(h >= t) >= K
+    uint32_t lo = 1, hi = hmax;
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo + 1) / 2;
+      int32_t c = 0;
+      for (int64_t e = lane; e < a.nchunks; e += 64) c += (a.in[e * 64 + p] >> 6) >= mid;
+      c = wave_sum_i32(c);
+      if (c >= K) lo = mid;
+      else hi = mid - 1;
+    }
+    t = lo;
+    int32_t gt = 0;
+    for (int64_t e = lane; e < a.nchunks; e += 64) gt += (a.in[e * 64 + p] >> 6) > t;
+    gt = wave_sum_i32(gt);
+    need_eq = K - gt;
+  }
+  // compaction: every h > t, plus the first need_eq entries (chunk order) with h == t
+  int32_t base = 0, eq_taken = 0;
+  uint64_t bound = 0;
+  const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  for (int64_t e0 = 0; e0 < a.nchunks; e0 += 64) {
+    const int64_t e = e0 + lane;
+    const uint32_t loc = e < a.nchunks ? a.in[e * 64 + p] : 0u;
+    const uint32_t h = loc >> 6;
+    const bool is_gt = h > t;
+    const bool is_eq = (h == t) && h != 0;
+    const uint64_t beq = __ballot(is_eq);
+    const int32_t eq_rank = eq_taken + __popcll(beq & lanemask_lt);
+    const bool take_eq = is_eq && eq_rank < need_eq;
+    const bool take = is_gt || take_eq;
+    const uint64_t btake = __ballot(take);
+    if (take) {
+      const int32_t pos = base + __popcll(btake & lanemask_lt);
+      const uint64_t key = entry_gkey(loc, e);
+      a.cand_chunk[p * K + pos] = (uint32_t)e;
+      a.cand_key[p * K + pos] = key;
+      if (take_eq && eq_rank == need_eq - 1) bound = key;
+    }
+    base += __popcll(btake);
+    eq_taken += __popcll(beq);
+  }
+  bound = wave_max_u64(bound);  // only one lane holds a non-zero bound
+  if (lane == 0) {
+    a.cand_count[p] = base;
+    a.cand_bound[p] = exhaustive ? 0ull : bound;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// commit: sequential exact selection + Reserve, one wave
+// ------------------------------------------------------------------------------------------
+
+struct CommitArgs {
+  DevNodes d;
+  Cfg c;
+  const PodRec* __restrict__ pods;
+  DevPodQuota pq;
+  DevQuotas q;
+  int32_t* cursor;
+  const uint32_t* __restrict__ cand_chunk;
+  const uint64_t* __restrict__ cand_key;
+  const uint64_t* __restrict__ cand_bound;
+  const int32_t* __restrict__ cand_count;
+  ks_result* results;
+  unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans
+  int64_t n, nchunks;
+  int32_t total_pods, batch, k, nwords;
+};
+
+struct CommitSmem {
+  MutState slots[kMaxBatch];
+  uint8_t dmap[kMaxBatch][64];  // dirty entry -> lane -> slot (0xFF none)
+};
+
+template <int NSC>
+__device__ __forceinline__ uint64_t rescan_chunk(const CommitArgs& a, const CommitSmem& sm, const PodRec& pod,
+                                                 int64_t chunk, int32_t dentry) {
+  const int lane = threadIdx.x;
+  const int64_t node = chunk * 64 + lane;
+  NodeReg<NSC> r;
+  load_node<NSC>(a.d, node, node < a.n, r);
+  const uint8_t s = sm.dmap[dentry][lane];
+  if (s != 0xFF) apply_mut<NSC>(r, sm.slots[s]);
+  const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
+  const uint64_t key = o.reasons ? 0ull : gkey(o.total, node);
+  return wave_max_u64(key);
+}
+
+template <int NSC>
+__device__ __forceinline__ uint64_t rescore_slots(const CommitArgs& a, const CommitSmem& sm, const PodRec& pod,
+                                                  int32_t nslots) {
+  const int lane = threadIdx.x;
+  uint64_t key = 0;
+  if (lane < nslots) {
+    const int64_t node = sm.slots[lane].node;
+    NodeReg<NSC> r;
+    load_node<NSC>(a.d, node, 1, r);
+    apply_mut<NSC>(r, sm.slots[lane]);
+    const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
+    key = o.reasons ? 0ull : gkey(o.total, node);
+  }
+  return wave_max_u64(key);
+}
+
+// ElasticQuota PreFilter admission for one pod (plugin.go:210-255, plugin_helper.go:281-319);
+// lane d checks resource dimension d.
+__device__ __forceinline__ uint32_t quota_admit(const CommitArgs& a, int32_t gp, int32_t quota, uint32_t flags) {
+  const int lane = threadIdx.x;
+  const uint32_t pmask = a.pq.mask[gp];
+  const int64_t req = lane < KS_QUOTA_DIMS ? a.pq.req[lane < KS_QUOTA_DIMS ? lane : 0][gp] : 0;
+  const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
+  {
+    const int64_t* row = a.q.used + (int64_t)quota * KS_QUOTA_DIMS;
+    const bool lim = in_pod && ((a.q.limit_mask[quota] >> lane) & 1u);
+    const bool bad = lim && (req + row[lane] > a.q.limit[(int64_t)quota * KS_QUOTA_DIMS + lane]);
+    if (__ballot(bad)) return KS_S_QUOTA;
+  }
+  if (flags & KS_POD_NONPREEMPTIBLE) {
+    const bool mn = in_pod && ((a.q.min_mask[quota] >> lane) & 1u);
+    const bool bad = mn && (req + a.q.npused[(int64_t)quota * KS_QUOTA_DIMS + lane] >
+                            a.q.min[(int64_t)quota * KS_QUOTA_DIMS + lane]);
+    if (__ballot(bad)) return KS_S_QUOTA_NONPREEMPTIBLE;
+  }
+  if (a.c.quota_parent) {
+    for (int32_t cur = quota; cur >= 0; cur = a.q.parent[cur]) {
+      const bool lim = in_pod && ((a.q.limit_mask[cur] >> lane) & 1u);
+      const bool bad = lim && (req + a.q.used[(int64_t)cur * KS_QUOTA_DIMS + lane] >
+                               a.q.limit[(int64_t)cur * KS_QUOTA_DIMS + lane]);
+      if (__ballot(bad)) return KS_S_QUOTA | KS_S_QUOTA_PARENT;
+    }
+  }
+  return 0;
+}
+
+__device__ __forceinline__ void quota_reserve(const CommitArgs& a, int32_t gp, int32_t quota, uint32_t flags) {
+  const int lane = threadIdx.x;
+  if (lane >= KS_QUOTA_DIMS) return;
+  const uint32_t pmask = a.pq.mask[gp];
+  if (!((pmask >> lane) & 1u)) return;
+  const int64_t req = a.pq.req[lane][gp];
+  for (int32_t cur = quota; cur >= 0; cur = a.q.parent[cur]) {
+    a.q.used[(int64_t)cur * KS_QUOTA_DIMS + lane] += req;
+    if (flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(int64_t)cur * KS_QUOTA_DIMS + lane] += req;
+  }
+}
+
+template <int NSC>
+__global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  CommitSmem& sm = *reinterpret_cast<CommitSmem*>(smem_raw);
+  uint32_t* dirty_bits = reinterpret_cast<uint32_t*>(smem_raw + sizeof(CommitSmem));
+  const int lane = threadIdx.x;
+  const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor0 >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor0);
+  const int32_t K = a.k;
+  for (int32_t w = lane; w < a.nwords; w += 64) dirty_bits[w] = 0;
+  __syncthreads();
+
+  int32_t nslots = 0, ndirty = 0;
+  int32_t dchunk = -1;  // lane d: chunk id of dirty entry d
+  int32_t processed = np;
+  unsigned long long rescans = 0;
+  for (int32_t j = 0; j < np; ++j) {
+    const int32_t gp = cursor0 + j;
+    const PodRec pod = a.pods[gp];
+    if (a.c.quota_enable && pod.quota >= 0) {
+      const uint32_t st = quota_admit(a, gp, pod.quota, pod.flags);
+      if (st) {
+        if (lane == 0) a.results[gp] = ks_result{-1, st, 0};
+        continue;
+      }
+    }
+    const int32_t cnt = a.cand_count[j];
+    const bool valid = lane < cnt;
+    const uint32_t chunk = valid ? a.cand_chunk[j * K + lane] : 0u;
+    const uint64_t key = valid ? a.cand_key[j * K + lane] : 0ull;
+    const bool dirty = valid && ((dirty_bits[chunk >> 5] >> (chunk & 31u)) & 1u);
+    uint64_t best = wave_max_u64(valid && !dirty ? key : 0ull);
+    const bool any_clean = best != 0;
+    uint64_t need = __ballot(dirty && key > best);
+    while (need) {
+      const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? key : 0ull);
+      const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && key == kmax)) - 1;
+      const int64_t c = (int64_t)(uint32_t)__shfl((int)chunk, sel, 64);
+      const int32_t d = __ffsll((long long)__ballot(lane < ndirty && dchunk == (int32_t)c)) - 1;
+      const uint64_t v = rescan_chunk<NSC>(a, sm, pod, c, d);
+      ++rescans;
+      best = v > best ? v : best;
+      need &= ~(1ull << sel);
+      need &= __ballot(key > best);
+    }
+    if (!a.c.monotone && nslots) {
+      const uint64_t v = rescore_slots<NSC>(a, sm, pod, nslots);
+      best = v > best ? v : best;
+    }
+    if (!any_clean && cnt == K && best < a.cand_bound[j]) {
+      processed = j;  // an untouched chunk outside the list may win: re-sweep from pod j
+      break;
+    }
+    if (best == 0) {
+      if (lane == 0) a.results[gp] = ks_result{-1, KS_S_UNSCHEDULABLE, 0};
+      continue;
+    }
+    const int64_t node = gkey_node(best);
+    const int64_t score = gkey_score(best);
+    const int32_t c = (int32_t)(node >> 6);
+    const int ln = (int)(node & 63);
+    int32_t d = __ffsll((long long)__ballot(lane < ndirty && dchunk == c)) - 1;
+    if (d < 0) {
+      d = ndirty++;
+      if (lane == d) dchunk = c;
+      sm.dmap[d][lane] = 0xFF;
+      if (lane == 0) dirty_bits[c >> 5] |= 1u << (c & 31);
+    }
+    __syncthreads();
+    int32_t s = sm.dmap[d][ln];
+    if (s == 0xFF) {
+      s = nslots++;
+      if (lane == 0) {
+        MutState m;
+        m.req_cpu = a.d.req_cpu[node];
+        m.req_mem = a.d.req_mem[node];
+        m.req_eph = a.d.req_eph[node];
+        m.nz_cpu = a.d.nz_cpu[node];
+        m.nz_mem = a.d.nz_mem[node];
+#pragma unroll
+        for (int k = 0; k < KS_MAX_SCALARS; ++k) m.req_sc[k] = k < NSC ? a.d.req_sc[k][node] : 0;
+        m.term_cpu = a.d.la_term_cpu[node];
+        m.term_mem = a.d.la_term_mem[node];
+        m.pterm_cpu = a.d.la_pterm_cpu[node];
+        m.pterm_mem = a.d.la_pterm_mem[node];
+        m.pod_count = a.d.pod_count[node];
+        m.node = (int32_t)node;
+        sm.slots[s] = m;
+        sm.dmap[d][ln] = (uint8_t)s;
+      }
+    }
+    if (lane == 0) {
+      // NodeInfo.AddPod + podAssignCache.assign (load_aware.go:260, pod_assign_cache.go:53)
+      MutState& m = sm.slots[s];
+      m.req_cpu += pod.cpu;
+      m.req_mem += pod.mem;
+      m.req_eph += pod.eph;
+      m.nz_cpu += pod.nzcpu;
+      m.nz_mem += pod.nzmem;
+#pragma unroll
+      for (int k = 0; k < NSC; ++k) m.req_sc[k] += pod.sc[k];
+      m.pod_count += 1;
+      m.term_cpu += pod.est_cpu;
+      m.term_mem += pod.est_mem;
+      if (pod.flags & KS_POD_PROD) {
+        m.pterm_cpu += pod.est_cpu;
+        m.pterm_mem += pod.est_mem;
+      }
+      a.results[gp] = ks_result{(int32_t)node, KS_S_SCHEDULED, score};
+    }
+    if (a.c.quota_enable && pod.quota >= 0) quota_reserve(a, gp, pod.quota, pod.flags);
+    __syncthreads();
+  }
+  __syncthreads();
+  // write the touched nodes back
+  if (lane < nslots) {
+    const MutState m = sm.slots[lane];
+    const int64_t node = m.node;
+    a.d.req_cpu[node] = m.req_cpu;
+    a.d.req_mem[node] = m.req_mem;
+    a.d.req_eph[node] = m.req_eph;
+    a.d.nz_cpu[node] = m.nz_cpu;
+    a.d.nz_mem[node] = m.nz_mem;
+#pragma unroll
+    for (int k = 0; k < NSC; ++k) a.d.req_sc[k][node] = m.req_sc[k];
+    a.d.pod_count[node] = m.pod_count;
+    a.d.la_term_cpu[node] = m.term_cpu;
+    a.d.la_term_mem[node] = m.term_mem;
+    a.d.la_pterm_cpu[node] = m.pterm_cpu;
+    a.d.la_pterm_mem[node] = m.pterm_mem;
+  }
+  if (lane == 0) {
+    *a.cursor = cursor0 + processed;
+    atomicAdd(&a.counters[0], 1ull);
+    if (processed < np) atomicAdd(&a.counters[1], 1ull);
+    atomicAdd(&a.counters[2], rescans);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// debug evaluation of one pod over every node (no Reserve)
+// ------------------------------------------------------------------------------------------
+
+template <int NSC>
+__global__ void eval_debug_kernel(DevNodes d, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
+                                  int64_t* scores, int64_t* total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  NodeReg<NSC> r;
+  load_node<NSC>(d, i, 1, r);
+  const PodRec p = *pod;
+  const EvalOut o = eval_pod_node<NSC, true>(c, p, r);
+  reasons[i] = o.reasons;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
+  total[i] = o.reasons ? -1 : o.total;
+}
+
+// scatter m staged rows into the node columns (informer deltas)
+__global__ void scatter_rows_kernel(void* const* dst_cols, const void* const* src_cols, const int32_t* widths,
+                                    int32_t ncols, const int32_t* idx, int64_t m) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int64_t to = idx[i];
+  for (int32_t k = 0; k < ncols; ++k) {
+    if (widths[k] == 8)
+      ((int64_t*)dst_cols[k])[to] = ((const int64_t*)src_cols[k])[i];
+    else
+      ((int32_t*)dst_cols[k])[to] = ((const int32_t*)src_cols[k])[i];
+  }
+}
+
+// ==========================================================================================
+// host side
+// ==========================================================================================
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct Col {
+  void** dev;       // address of the DevNodes pointer field
+  int32_t width;    // bytes per element
+  bool mutable_;    // changed by commits (checkpointed)
+};
+
+}  // namespace
+
+struct ks_ctx {
+  ks_config cfg{};
+  Cfg kc{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // nodes
+  int64_t n = 0, npad = 0, nchunks = 0;
+  int nsc = 0;
+  DevNodes d{};
+  std::vector<Col> cols;
+  void* node_blob = nullptr;
+  void* ckpt_blob = nullptr;
+  size_t mut_bytes = 0;
+  // quotas
+  DevQuotas q{};
+  void* quota_blob = nullptr;
+  int64_t* quota_used_ckpt = nullptr;
+  int64_t* quota_npused_ckpt = nullptr;
+  // pods
+  int32_t np = 0, pod_cap = 0;
+  PodRec* pods = nullptr;
+  DevPodQuota pq{};
+  void* pod_blob = nullptr;
+  DevPodCols pstage{};
+  ks_result* results = nullptr;
+  // pass scratch
+  uint32_t* sweep_out = nullptr;
+  uint32_t* cand_chunk = nullptr;
+  uint64_t* cand_key = nullptr;
+  uint64_t* cand_bound = nullptr;
+  int32_t* cand_count = nullptr;
+  int32_t* cursor = nullptr;
+  unsigned long long* counters = nullptr;
+  int32_t batch = 64, k = 32;
+  // debug
+  PodRec* dbg_pod = nullptr;
+  // stats
+  ks_stats stats{};
+  std::vector<hipEvent_t> ev_pool;
+};
+
+#define KS_FAIL(ctx, code, ...)                                        \
+  do {                                                                 \
+    char buf_[512];                                                    \
+    snprintf(buf_, sizeof(buf_), __VA_ARGS__);                         \
+    (ctx)->err = buf_;                                                 \
+    return (code);                                                     \
+  } while (0)
+
+#define HIPCHK(ctx, expr)                                                                    \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) KS_FAIL(ctx, KS_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+static int dev_alloc(ks_ctx* ctx, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) KS_FAIL(ctx, KS_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  return KS_OK;
+}
+
+static void dev_free(void*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+static Cfg make_cfg(const ks_config& c, int nsc) {
+  Cfg k{};
+  k.fit_filter = c.fit.enable_filter;
+  k.fit_score = c.fit.enable_score;
+  k.fit_most = c.fit.strategy == KS_MOST_ALLOCATED;
+  k.nsc = nsc;
+  k.fw_cpu = c.fit.weight_cpu;
+  k.fw_mem = c.fit.weight_memory;
+  k.fw_eph = c.fit.weight_ephemeral;
+  for (int i = 0; i < KS_MAX_SCALARS; ++i) k.fw_sc[i] = c.fit.weight_scalar[i];
+  k.fit_pw = c.fit.plugin_weight;
+  k.la_filter = c.loadaware.enable_filter;
+  k.la_score = c.loadaware.enable_score;
+  k.la_filter_expired = c.loadaware.filter_expired_node_metrics;
+  k.la_prod_usage = c.loadaware.score_according_prod_usage;
+  k.lw_cpu = c.loadaware.weight_cpu;
+  k.lw_mem = c.loadaware.weight_memory;
+  k.la_pw = c.loadaware.plugin_weight;
+  k.scaling_cpu = c.loadaware.scaling_cpu;
+  k.scaling_mem = c.loadaware.scaling_memory;
+  k.quota_enable = c.quota.enable;
+  k.quota_parent = c.quota.enable_check_parent_quota;
+  // LeastAllocated Fit + LoadAware: a commit only raises requested/estimated usage, so a node's
+  // key can only drop and its Filter can only start failing.
+  k.monotone = c.fit.strategy == KS_LEAST_ALLOCATED || !c.fit.enable_score;
+  return k;
+}
+
+// C-ABI entry points: declared extern "C" in include/koordgpu.h, so these definitions have C linkage.
+
+const char* ks_last_error(const ks_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int ks_create(const ks_config* cfg, ks_ctx** out) {
+  if (out) *out = nullptr;
+  if (!cfg || !out) {
+    g_create_error = "ks_create: null argument";
+    return KS_EINVAL;
+  }
+  if (cfg->abi_version != KS_ABI_VERSION) {
+    g_create_error = "ks_create: ABI version mismatch";
+    return KS_EINVAL;
+  }
+  const ks_loadaware_args& la = cfg->loadaware;
+  if (la.weight_cpu < 0 || la.weight_cpu > 100 || la.weight_memory < 0 || la.weight_memory > 100 ||
+      (la.enable_score && la.weight_cpu + la.weight_memory == 0)) {
+    g_create_error = "ks_create: LoadAware resource weights must be in [1,100] (validation_pluginargs.go:60-70)";
+    return KS_EINVAL;
+  }
+  const int64_t max_total = 100 * (std::max<int64_t>(cfg->fit.plugin_weight, 0) +
+                                   std::max<int64_t>(cfg->loadaware.plugin_weight, 0));
+  if (cfg->fit.plugin_weight < 0 || cfg->loadaware.plugin_weight < 0 || max_total >= (1 << 25)) {
+    g_create_error = "ks_create: plugin weights out of supported range";
+    return KS_EINVAL;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    g_create_error = "ks_create: no HIP device available";
+    return KS_EHIP;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    g_create_error = "ks_create: device ordinal out of range";
+    return KS_EINVAL;
+  }
+  ks_ctx* ctx = new ks_ctx();
+  ctx->cfg = *cfg;
+  ctx->device = cfg->device;
+  ctx->batch = cfg->batch_pods > 0 ? std::min(cfg->batch_pods, kMaxBatch) : 64;
+  ctx->k = cfg->candidates > 0 ? std::min(cfg->candidates, kMaxCand) : 32;
+  if (hipSetDevice(ctx->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    g_create_error = "ks_create: cannot create HIP stream";
+    delete ctx;
+    return KS_EHIP;
+  }
+  void* p = nullptr;
+  size_t cand_bytes = (size_t)kMaxBatch * kMaxCand;
+  if (dev_alloc(ctx, &p, cand_bytes * 4) != KS_OK) goto fail;
+  ctx->cand_chunk = (uint32_t*)p;
+  if (dev_alloc(ctx, &p, cand_bytes * 8) != KS_OK) goto fail;
+  ctx->cand_key = (uint64_t*)p;
+  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  ctx->cand_bound = (uint64_t*)p;
+  if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
+  ctx->cand_count = (int32_t*)p;
+  if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
+  ctx->cursor = (int32_t*)p;
+  if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
+  ctx->counters = (unsigned long long*)p;
+  if (dev_alloc(ctx, &p, sizeof(PodRec)) != KS_OK) goto fail;
+  ctx->dbg_pod = (PodRec*)p;
+  *out = ctx;
+  return KS_OK;
+fail:
+  g_create_error = ctx->err;
+  ks_destroy(ctx);
+  return KS_ENOMEM;
+}
+
+void ks_destroy(ks_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  dev_free(ctx->node_blob);
+  dev_free(ctx->ckpt_blob);
+  dev_free(ctx->quota_blob);
+  void* p;
+  p = ctx->pod_blob; dev_free(p);
+  p = ctx->sweep_out; dev_free(p);
+  p = ctx->cand_chunk; dev_free(p);
+  p = ctx->cand_key; dev_free(p);
+  p = ctx->cand_bound; dev_free(p);
+  p = ctx->cand_count; dev_free(p);
+  p = ctx->cursor; dev_free(p);
+  p = ctx->counters; dev_free(p);
+  p = ctx->dbg_pod; dev_free(p);
+  for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+static void build_col_table(ks_ctx* ctx) {
+  DevNodes& d = ctx->d;
+  ctx->cols.clear();
+  auto add = [&](void* field, int w, bool mut) { ctx->cols.push_back(Col{(void**)field, w, mut}); };
+  // mutable columns first (contiguous -> one checkpoint copy)
+  add(&d.req_cpu, 8, true);
+  add(&d.req_mem, 8, true);
+  add(&d.req_eph, 8, true);
+  add(&d.nz_cpu, 8, true);
+  add(&d.nz_mem, 8, true);
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) add(&d.req_sc[k], 8, true);
+  add(&d.la_term_cpu, 8, true);
+  add(&d.la_term_mem, 8, true);
+  add(&d.la_pterm_cpu, 8, true);
+  add(&d.la_pterm_mem, 8, true);
+  add(&d.pod_count, 4, true);
+  // read-only columns
+  add(&d.alloc_cpu, 8, false);
+  add(&d.alloc_mem, 8, false);
+  add(&d.alloc_eph, 8, false);
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) add(&d.alloc_sc[k], 8, false);
+  add(&d.la_alloc_cpu, 8, false);
+  add(&d.la_alloc_mem, 8, false);
+  add(&d.la_total_cpu, 8, false);
+  add(&d.la_total_mem, 8, false);
+  add(&d.la_usage_cpu, 8, false);
+  add(&d.la_usage_mem, 8, false);
+  add(&d.la_pusage_cpu, 8, false);
+  add(&d.la_pusage_mem, 8, false);
+  add(&d.allowed_pods, 4, false);
+  add(&d.la_flags, 4, false);
+  add(&d.la_thr_cpu, 4, false);
+  add(&d.la_thr_mem, 4, false);
+  add(&d.la_pthr_cpu, 4, false);
+  add(&d.la_pthr_mem, 4, false);
+  add(&d.la_bits, 4, false);
+}
+
+// host source pointers in the same order as build_col_table (NULL = zeros)
+static std::vector<const void*> host_cols(const ks_node_cols* c) {
+  std::vector<const void*> v;
+  v.push_back(c->req_milli_cpu);
+  v.push_back(c->req_memory);
+  v.push_back(c->req_ephemeral);
+  v.push_back(c->nonzero_milli_cpu);
+  v.push_back(c->nonzero_memory);
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) v.push_back(c->req_scalar[k]);
+  v.push_back(c->la_term_milli_cpu);
+  v.push_back(c->la_term_memory);
+  v.push_back(c->la_prod_term_milli_cpu);
+  v.push_back(c->la_prod_term_memory);
+  v.push_back(c->pod_count);
+  v.push_back(c->alloc_milli_cpu);
+  v.push_back(c->alloc_memory);
+  v.push_back(c->alloc_ephemeral);
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) v.push_back(c->alloc_scalar[k]);
+  v.push_back(c->la_alloc_milli_cpu);
+  v.push_back(c->la_alloc_memory);
+  v.push_back(c->la_total_milli_cpu);
+  v.push_back(c->la_total_milli_memory);
+  v.push_back(c->la_usage_milli_cpu);
+  v.push_back(c->la_usage_milli_memory);
+  v.push_back(c->la_prod_usage_milli_cpu);
+  v.push_back(c->la_prod_usage_milli_memory);
+  v.push_back(c->allowed_pods);
+  v.push_back(c->la_flags);
+  v.push_back(c->la_thr_cpu);
+  v.push_back(c->la_thr_memory);
+  v.push_back(c->la_prod_thr_cpu);
+  v.push_back(c->la_prod_thr_memory);
+  v.push_back(nullptr);  // la_bits: derived on device
+  return v;
+}
+
+static int check_range64(ks_ctx* ctx, const int64_t* p, int64_t n, const char* what) {
+  if (!p) return KS_OK;
+  const int64_t lim = (int64_t)1 << 56;
+  for (int64_t i = 0; i < n; ++i)
+    if (p[i] < 0 || p[i] >= lim) KS_FAIL(ctx, KS_EINVAL, "%s[%lld]=%lld outside [0, 2^56)", what, (long long)i, (long long)p[i]);
+  return KS_OK;
+}
+
+static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
+  if (!c->alloc_milli_cpu || !c->alloc_memory || !c->allowed_pods || !c->req_milli_cpu || !c->req_memory ||
+      !c->pod_count || !c->nonzero_milli_cpu || !c->nonzero_memory || !c->la_flags)
+    KS_FAIL(ctx, KS_EINVAL, "ks_node_cols: required column missing");
+  const int64_t* cols64[] = {c->alloc_milli_cpu, c->alloc_memory, c->alloc_ephemeral, c->req_milli_cpu, c->req_memory,
+                             c->req_ephemeral, c->nonzero_milli_cpu, c->nonzero_memory, c->la_alloc_milli_cpu,
+                             c->la_alloc_memory, c->la_term_milli_cpu, c->la_term_memory, c->la_prod_term_milli_cpu,
+                             c->la_prod_term_memory};
+  for (const int64_t* col : cols64)
+    if (check_range64(ctx, col, n, "node quantity") != KS_OK) return KS_EINVAL;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) {
+    if (check_range64(ctx, c->alloc_scalar[k], n, "alloc_scalar") != KS_OK) return KS_EINVAL;
+    if (check_range64(ctx, c->req_scalar[k], n, "req_scalar") != KS_OK) return KS_EINVAL;
+  }
+  return KS_OK;
+}
+
+static int upload_prep_nodes(ks_ctx* ctx) {
+  const int threads = 256;
+  const int blocks = (int)((ctx->n + threads - 1) / threads);
+  if (blocks > 0)
+    hipLaunchKernelGGL(prep_nodes_kernel, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->n,
+                       ctx->cfg.loadaware.filter_expired_node_metrics);
+  HIPCHK(ctx, hipGetLastError());
+  return KS_OK;
+}
+
+int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
+  if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
+  if (validate_nodes(ctx, nodes, n) != KS_OK) return KS_EINVAL;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  dev_free(ctx->node_blob);
+  dev_free(ctx->ckpt_blob);
+  void* p = ctx->sweep_out;
+  dev_free(p);
+  ctx->sweep_out = nullptr;
+  ctx->n = n;
+  ctx->nchunks = (n + 63) / 64;
+  if (ctx->nchunks == 0) ctx->nchunks = 1;
+  ctx->npad = ctx->nchunks * 64;
+  int nsc = 0;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k)
+    if (nodes->alloc_scalar[k] || ctx->cfg.fit.weight_scalar[k]) nsc = k + 1;
+  ctx->nsc = nsc <= 0 ? 0 : (nsc <= 2 ? 2 : 4);
+  ctx->kc = make_cfg(ctx->cfg, ctx->nsc);
+  build_col_table(ctx);
+  size_t total = 0, mut = 0;
+  for (const Col& c : ctx->cols) {
+    total += (size_t)ctx->npad * c.width;
+    if (c.mutable_) mut += (size_t)ctx->npad * c.width;
+  }
+  ctx->mut_bytes = mut;
+  if (dev_alloc(ctx, &ctx->node_blob, total) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemsetAsync(ctx->node_blob, 0, total, ctx->stream));
+  char* base = (char*)ctx->node_blob;
+  std::vector<const void*> src = host_cols(nodes);
+  for (size_t i = 0; i < ctx->cols.size(); ++i) {
+    *ctx->cols[i].dev = base;
+    if (src[i] && n > 0)
+      HIPCHK(ctx, hipMemcpyAsync(base, src[i], (size_t)n * ctx->cols[i].width, hipMemcpyHostToDevice, ctx->stream));
+    base += (size_t)ctx->npad * ctx->cols[i].width;
+  }
+  if (dev_alloc(ctx, &p, (size_t)ctx->nchunks * 64 * 4) != KS_OK) return KS_ENOMEM;
+  ctx->sweep_out = (uint32_t*)p;
+  if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, int64_t m) {
+  if (!ctx || !idx || !rows || m < 0) return ctx ? (ctx->err = "ks_update_nodes: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_update_nodes before ks_load_nodes");
+  if (m == 0) return KS_OK;
+  for (int64_t i = 0; i < m; ++i)
+    if (idx[i] < 0 || idx[i] >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: idx[%lld]=%d out of range", (long long)i, idx[i]);
+  if (validate_nodes(ctx, rows, m) != KS_OK) return KS_EINVAL;
+  std::vector<const void*> src = host_cols(rows);
+  std::vector<void*> dst;
+  std::vector<int32_t> widths;
+  std::vector<size_t> offs;
+  size_t bytes = 0;
+  for (size_t i = 0; i < ctx->cols.size(); ++i) {
+    if (!src[i]) continue;
+    dst.push_back(*ctx->cols[i].dev);
+    widths.push_back(ctx->cols[i].width);
+    offs.push_back(bytes);
+    bytes += ((size_t)m * ctx->cols[i].width + 15) / 16 * 16;
+  }
+  const size_t ncols = dst.size();
+  const size_t meta = ncols * (sizeof(void*) * 2 + 4) + (size_t)m * 4 + 64;
+  std::vector<char> host(bytes + meta);
+  void* dbuf = nullptr;
+  if (dev_alloc(ctx, &dbuf, bytes + meta) != KS_OK) return KS_ENOMEM;
+  std::vector<const void*> srcdev(ncols);
+  size_t j = 0;
+  for (size_t i = 0; i < ctx->cols.size(); ++i) {
+    if (!src[i]) continue;
+    memcpy(host.data() + offs[j], src[i], (size_t)m * ctx->cols[i].width);
+    srcdev[j] = (char*)dbuf + offs[j];
+    ++j;
+  }
+  char* mp = host.data() + bytes;
+  memcpy(mp, dst.data(), ncols * sizeof(void*));
+  memcpy(mp + ncols * sizeof(void*), srcdev.data(), ncols * sizeof(void*));
+  memcpy(mp + 2 * ncols * sizeof(void*), widths.data(), ncols * 4);
+  const size_t idx_off = bytes + 2 * ncols * sizeof(void*) + ((ncols * 4 + 15) / 16) * 16;
+  memcpy(host.data() + idx_off, idx, (size_t)m * 4);
+  HIPCHK(ctx, hipMemcpyAsync(dbuf, host.data(), host.size(), hipMemcpyHostToDevice, ctx->stream));
+  char* dm = (char*)dbuf + bytes;
+  const int threads = 256;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)((m + threads - 1) / threads)), dim3(threads), 0, ctx->stream,
+                     (void* const*)dm, (const void* const*)(dm + ncols * sizeof(void*)),
+                     (const int32_t*)(dm + 2 * ncols * sizeof(void*)), (int32_t)ncols,
+                     (const int32_t*)((char*)dbuf + idx_off), m);
+  HIPCHK(ctx, hipGetLastError());
+  if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  (void)hipFree(dbuf);
+  return KS_OK;
+}
+
+int ks_load_quotas(ks_ctx* ctx, const ks_quota_cols* qc, int32_t nq) {
+  if (!ctx || !qc || nq < 0) return ctx ? (ctx->err = "ks_load_quotas: bad args", KS_EINVAL) : KS_EINVAL;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  dev_free(ctx->quota_blob);
+  const size_t rows = (size_t)(nq > 0 ? nq : 1);
+  const size_t tbl = rows * KS_QUOTA_DIMS * 8;
+  const size_t bytes = rows * 12 + 16 + tbl * 6;
+  if (dev_alloc(ctx, &ctx->quota_blob, bytes) != KS_OK) return KS_ENOMEM;
+  std::vector<char> h(bytes, 0);
+  char* b = h.data();
+  int32_t* parent = (int32_t*)b;
+  uint32_t* lmask = (uint32_t*)(b + rows * 4);
+  uint32_t* mmask = (uint32_t*)(b + rows * 8);
+  const size_t toff = (rows * 12 + 15) / 16 * 16;
+  int64_t* limit = (int64_t*)(b + toff);
+  int64_t* used = limit + rows * KS_QUOTA_DIMS;
+  int64_t* mn = used + rows * KS_QUOTA_DIMS;
+  int64_t* np = mn + rows * KS_QUOTA_DIMS;
+  for (int32_t i = 0; i < nq; ++i) {
+    parent[i] = qc->parent ? qc->parent[i] : -1;
+    if (parent[i] >= nq || parent[i] == i) KS_FAIL(ctx, KS_EINVAL, "quota %d: bad parent %d", i, parent[i]);
+    lmask[i] = qc->limit_mask ? qc->limit_mask[i] : 0;
+    mmask[i] = qc->min_mask ? qc->min_mask[i] : 0;
+    for (int d = 0; d < KS_QUOTA_DIMS; ++d) {
+      const size_t o = (size_t)i * KS_QUOTA_DIMS + d;
+      limit[o] = qc->limit[d] ? qc->limit[d][i] : 0;
+      used[o] = qc->used[d] ? qc->used[d][i] : 0;
+      mn[o] = qc->min[d] ? qc->min[d][i] : 0;
+      np[o] = qc->nonpreemptible_used[d] ? qc->nonpreemptible_used[d][i] : 0;
+    }
+  }
+  // parent chains must terminate (no cycles)
+  for (int32_t i = 0; i < nq; ++i) {
+    int32_t cur = i, steps = 0;
+    while (cur >= 0 && steps <= nq) cur = parent[cur], ++steps;
+    if (cur >= 0) KS_FAIL(ctx, KS_EINVAL, "quota %d: parent chain has a cycle", i);
+  }
+  HIPCHK(ctx, hipMemcpyAsync(ctx->quota_blob, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+  char* d = (char*)ctx->quota_blob;
+  ctx->q.q = nq;
+  ctx->q.parent = (int32_t*)d;
+  ctx->q.limit_mask = (uint32_t*)(d + rows * 4);
+  ctx->q.min_mask = (uint32_t*)(d + rows * 8);
+  ctx->q.limit = (int64_t*)(d + toff);
+  ctx->q.used = ctx->q.limit + rows * KS_QUOTA_DIMS;
+  ctx->q.min = ctx->q.used + rows * KS_QUOTA_DIMS;
+  ctx->q.npused = ctx->q.min + rows * KS_QUOTA_DIMS;
+  ctx->quota_used_ckpt = ctx->q.npused + rows * KS_QUOTA_DIMS;
+  ctx->quota_npused_ckpt = ctx->quota_used_ckpt + rows * KS_QUOTA_DIMS;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
+  if (p <= ctx->pod_cap && ctx->pod_blob) return KS_OK;
+  dev_free(ctx->pod_blob);
+  const int32_t cap = std::max<int32_t>(p, 64);
+  const size_t rec = (size_t)cap * sizeof(PodRec);
+  const size_t res = ((size_t)cap * sizeof(ks_result) + 255) / 256 * 256;
+  const size_t col8 = ((size_t)cap * 8 + 255) / 256 * 256;
+  const size_t col4 = ((size_t)cap * 4 + 255) / 256 * 256;
+  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 qreq[8] = 23 int64 cols; flags quota qmask = 3 x32
+  const size_t bytes = rec + res + col8 * 23 + col4 * 3;
+  if (dev_alloc(ctx, &ctx->pod_blob, bytes) != KS_OK) return KS_ENOMEM;
+  char* b = (char*)ctx->pod_blob;
+  ctx->pods = (PodRec*)b;
+  b += rec;
+  ctx->results = (ks_result*)b;
+  b += res;
+  DevPodCols& s = ctx->pstage;
+  int64_t** c8[] = {&s.cpu, &s.mem, &s.eph, &s.nzcpu, &s.nzmem, &s.sc[0], &s.sc[1], &s.sc[2], &s.sc[3],
+                    &s.la_req_cpu, &s.la_lim_cpu, &s.la_dflt_cpu, &s.la_req_mem, &s.la_lim_mem, &s.la_dflt_mem};
+  for (int64_t** f : c8) {
+    *f = (int64_t*)b;
+    b += col8;
+  }
+  for (int d = 0; d < KS_QUOTA_DIMS; ++d) {
+    ctx->pq.req[d] = (int64_t*)b;
+    b += col8;
+  }
+  s.flags = (uint32_t*)b;
+  b += col4;
+  s.quota = (int32_t*)b;
+  b += col4;
+  ctx->pq.mask = (uint32_t*)b;
+  ctx->pod_cap = cap;
+  return KS_OK;
+}
+
+static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* dst) {
+  // copy host columns into the staging area, then build PodRec on device
+  DevPodCols& s = ctx->pstage;
+  auto cp8 = [&](int64_t* d, const int64_t* h) -> hipError_t {
+    if (h) return hipMemcpyAsync(d, h, (size_t)p * 8, hipMemcpyHostToDevice, ctx->stream);
+    return hipMemsetAsync(d, 0, (size_t)p * 8, ctx->stream);
+  };
+  HIPCHK(ctx, cp8(s.cpu, pc->req_milli_cpu));
+  HIPCHK(ctx, cp8(s.mem, pc->req_memory));
+  HIPCHK(ctx, cp8(s.eph, pc->req_ephemeral));
+  HIPCHK(ctx, cp8(s.nzcpu, pc->nonzero_milli_cpu));
+  HIPCHK(ctx, cp8(s.nzmem, pc->nonzero_memory));
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) HIPCHK(ctx, cp8(s.sc[k], pc->req_scalar[k]));
+  HIPCHK(ctx, cp8(s.la_req_cpu, pc->la_req_cpu));
+  HIPCHK(ctx, cp8(s.la_lim_cpu, pc->la_lim_cpu));
+  HIPCHK(ctx, cp8(s.la_dflt_cpu, pc->la_dflt_cpu));
+  HIPCHK(ctx, cp8(s.la_req_mem, pc->la_req_memory));
+  HIPCHK(ctx, cp8(s.la_lim_mem, pc->la_lim_memory));
+  HIPCHK(ctx, cp8(s.la_dflt_mem, pc->la_dflt_memory));
+  for (int d = 0; d < KS_QUOTA_DIMS; ++d) HIPCHK(ctx, cp8(ctx->pq.req[d], pc->quota_req[d]));
+  if (pc->flags) HIPCHK(ctx, hipMemcpyAsync(s.flags, pc->flags, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(s.flags, 0, (size_t)p * 4, ctx->stream));
+  if (pc->quota) HIPCHK(ctx, hipMemcpyAsync(s.quota, pc->quota, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(s.quota, 0xFF, (size_t)p * 4, ctx->stream));
+  if (pc->quota_mask) HIPCHK(ctx, hipMemcpyAsync(ctx->pq.mask, pc->quota_mask, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(ctx->pq.mask, 0, (size_t)p * 4, ctx->stream));
+  const int threads = 256;
+  hipLaunchKernelGGL(prep_pods_kernel, dim3((p + threads - 1) / threads), dim3(threads), 0, ctx->stream, s, dst, p,
+                     ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory);
+  HIPCHK(ctx, hipGetLastError());
+  return KS_OK;
+}
+
+static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
+  const int64_t* cols[] = {pc->req_milli_cpu, pc->req_memory, pc->req_ephemeral, pc->nonzero_milli_cpu,
+                           pc->nonzero_memory, pc->la_req_cpu, pc->la_lim_cpu, pc->la_req_memory, pc->la_lim_memory};
+  for (const int64_t* c : cols)
+    if (check_range64(ctx, c, p, "pod quantity") != KS_OK) return KS_EINVAL;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k)
+    if (check_range64(ctx, pc->req_scalar[k], p, "pod scalar") != KS_OK) return KS_EINVAL;
+  if (pc->quota) {
+    for (int32_t i = 0; i < p; ++i)
+      if (pc->quota[i] >= ctx->q.q || pc->quota[i] < -1)
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: quota row %d out of range (loaded %d)", i, pc->quota[i], ctx->q.q);
+  }
+  for (int k = ctx->nsc; k < KS_MAX_SCALARS; ++k) {
+    if (!pc->req_scalar[k]) continue;
+    for (int32_t i = 0; i < p; ++i)
+      if (pc->req_scalar[k][i] != 0) KS_FAIL(ctx, KS_EINVAL, "pod %d requests scalar slot %d with no node column", i, k);
+  }
+  return KS_OK;
+}
+
+int ks_stage_pods(ks_ctx* ctx, const ks_pod_cols* pods, int32_t p) {
+  if (!ctx || !pods || p < 0) return ctx ? (ctx->err = "ks_stage_pods: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_stage_pods before ks_load_nodes");
+  if (ctx->cfg.quota.enable && pods->quota && !ctx->quota_blob)
+    KS_FAIL(ctx, KS_ESTATE, "ElasticQuota enabled but ks_load_quotas not called");
+  if (validate_pods(ctx, pods, p) != KS_OK) return KS_EINVAL;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ensure_pod_capacity(ctx, p) != KS_OK) return KS_ENOMEM;
+  if (p > 0 && stage_pods_to(ctx, pods, p, ctx->pods) != KS_OK) return KS_EHIP;
+  ctx->np = p;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+static hipEvent_t take_event(ks_ctx* ctx, size_t i) {
+  while (ctx->ev_pool.size() <= i) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ctx->ev_pool.push_back(e);
+  }
+  return ctx->ev_pool[i];
+}
+
+template <int NSC>
+static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
+  auto rec = [&](int kind) {
+    if (!evs) return;
+    hipEvent_t e = take_event(ctx, *evn);
+    (void)hipEventRecord(e, ctx->stream);
+    evs->push_back({kind, (*evn)++});
+  };
+  SweepArgs sa;
+  sa.d = ctx->d;
+  sa.c = ctx->kc;
+  sa.pods = ctx->pods;
+  sa.cursor = ctx->cursor;
+  sa.out = ctx->sweep_out;
+  sa.n = ctx->n;
+  sa.nchunks = ctx->nchunks;
+  sa.total_pods = ctx->np;
+  sa.batch = ctx->batch;
+  sa.ppw = ppw;
+  rec(0);
+  hipLaunchKernelGGL(sweep_kernel<NSC>, dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  rec(0);
+  SelectArgs se;
+  se.in = ctx->sweep_out;
+  se.cursor = ctx->cursor;
+  se.cand_chunk = ctx->cand_chunk;
+  se.cand_key = ctx->cand_key;
+  se.cand_bound = ctx->cand_bound;
+  se.cand_count = ctx->cand_count;
+  se.nchunks = ctx->nchunks;
+  se.total_pods = ctx->np;
+  se.batch = ctx->batch;
+  se.k = ctx->k;
+  rec(1);
+  hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64), 0, ctx->stream, se);
+  rec(1);
+  CommitArgs ca;
+  ca.d = ctx->d;
+  ca.c = ctx->kc;
+  ca.pods = ctx->pods;
+  ca.pq = ctx->pq;
+  ca.q = ctx->q;
+  ca.cursor = ctx->cursor;
+  ca.cand_chunk = ctx->cand_chunk;
+  ca.cand_key = ctx->cand_key;
+  ca.cand_bound = ctx->cand_bound;
+  ca.cand_count = ctx->cand_count;
+  ca.results = ctx->results;
+  ca.counters = ctx->counters;
+  ca.n = ctx->n;
+  ca.nchunks = ctx->nchunks;
+  ca.total_pods = ctx->np;
+  ca.batch = ctx->batch;
+  ca.k = ctx->k;
+  ca.nwords = (int32_t)((ctx->nchunks + 31) / 32);
+  const size_t smem = sizeof(CommitSmem) + (size_t)ca.nwords * 4;
+  rec(2);
+  hipLaunchKernelGGL(commit_kernel<NSC>, dim3(1), dim3(64), smem, ctx->stream, ca);
+  rec(2);
+}
+
+static int schedule_staged_impl(ks_ctx* ctx) {
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "schedule before ks_load_nodes");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  ctx->stats = ks_stats{};
+  const int32_t np = ctx->np;
+  if (np == 0) return KS_OK;
+  const size_t smem = sizeof(CommitSmem) + (size_t)((ctx->nchunks + 31) / 32) * 4;
+  if (smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld)", (long long)ctx->n);
+  // pods per wave: aim for >= ~4096 waves per sweep
+  int32_t ppw = 64;
+  while (ppw > 4 && ctx->nchunks * (ctx->batch / ppw) < 4096) ppw >>= 1;
+  if (ppw > ctx->batch) ppw = ctx->batch;
+  const int64_t nwork = ctx->nchunks * ((ctx->batch + ppw - 1) / ppw);
+  const int sweep_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048));
+  hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
+  HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 64, ctx->stream));
+  HIPCHK(ctx, hipEventRecord(t0, ctx->stream));
+  std::vector<std::pair<int, size_t>> evs;
+  size_t evn = 2;
+  int32_t host_cursor = 0;
+  int rounds = 0;
+  while (host_cursor < np) {
+    const int32_t remaining = np - host_cursor;
+    const int32_t g = std::min<int32_t>((remaining + ctx->batch - 1) / ctx->batch, 256);
+    for (int32_t i = 0; i < g; ++i) {
+      auto* ev = ctx->cfg.profile ? &evs : nullptr;
+      switch (ctx->nsc) {
+        case 0: launch_pass<0>(ctx, ppw, sweep_blocks, ev, &evn); break;
+        case 2: launch_pass<2>(ctx, ppw, sweep_blocks, ev, &evn); break;
+        default: launch_pass<4>(ctx, ppw, sweep_blocks, ev, &evn); break;
+      }
+    }
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(&host_cursor, ctx->cursor, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (++rounds > 1000000) KS_FAIL(ctx, KS_EHIP, "schedule made no progress");
+  }
+  HIPCHK(ctx, hipEventRecord(t1, ctx->stream));
+  unsigned long long cnt[3] = {0, 0, 0};
+  HIPCHK(ctx, hipMemcpyAsync(cnt, ctx->counters, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, t0, t1);
+  ctx->stats.total_ms = ms;
+  ctx->stats.passes = (int64_t)cnt[0];
+  ctx->stats.cut_passes = (int64_t)cnt[1];
+  ctx->stats.rescans = (int64_t)cnt[2];
+  for (size_t i = 0; i + 1 < evs.size(); i += 2) {
+    float e = 0;
+    (void)hipEventElapsedTime(&e, ctx->ev_pool[evs[i].second], ctx->ev_pool[evs[i + 1].second]);
+    if (evs[i].first == 0) {
+      ctx->stats.sweep_ms += e;
+      ctx->stats.sweep_launches += 1;
+    } else if (evs[i].first == 1) {
+      ctx->stats.select_ms += e;
+    } else {
+      ctx->stats.commit_ms += e;
+    }
+  }
+  // algorithmic bytes of one full sweep launch: node columns read once per pod group + outputs
+  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16;
+  const int64_t groups = (ctx->batch + ppw - 1) / ppw;
+  ctx->stats.sweep_bytes = ctx->n * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + ctx->nchunks * 64 * 4;
+  return KS_OK;
+}
+
+int ks_schedule_staged(ks_ctx* ctx) {
+  if (!ctx) return KS_EINVAL;
+  return schedule_staged_impl(ctx);
+}
+
+int ks_fetch_results(ks_ctx* ctx, ks_result* out, int32_t p) {
+  if (!ctx || !out || p < 0 || p > ctx->np) return ctx ? (ctx->err = "ks_fetch_results: bad args", KS_EINVAL) : KS_EINVAL;
+  if (p == 0) return KS_OK;
+  HIPCHK(ctx, hipMemcpyAsync(out, ctx->results, (size_t)p * sizeof(ks_result), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_schedule(ks_ctx* ctx, const ks_pod_cols* pods, int32_t p, ks_result* out) {
+  int rc = ks_stage_pods(ctx, pods, p);
+  if (rc != KS_OK) return rc;
+  rc = ks_schedule_staged(ctx);
+  if (rc != KS_OK) return rc;
+  return ks_fetch_results(ctx, out, p);
+}
+
+int ks_checkpoint(ks_ctx* ctx) {
+  if (!ctx || !ctx->node_blob) return ctx ? (ctx->err = "ks_checkpoint before ks_load_nodes", KS_ESTATE) : KS_EINVAL;
+  if (!ctx->ckpt_blob && dev_alloc(ctx, &ctx->ckpt_blob, ctx->mut_bytes) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->ckpt_blob, ctx->node_blob, ctx->mut_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->quota_blob) {
+    const size_t tb = (size_t)(ctx->q.q > 0 ? ctx->q.q : 1) * KS_QUOTA_DIMS * 8;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->quota_used_ckpt, ctx->q.used, tb, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->quota_npused_ckpt, ctx->q.npused, tb, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_restore(ks_ctx* ctx) {
+  if (!ctx || !ctx->ckpt_blob) return ctx ? (ctx->err = "ks_restore without ks_checkpoint", KS_ESTATE) : KS_EINVAL;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->node_blob, ctx->ckpt_blob, ctx->mut_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->quota_blob) {
+    const size_t tb = (size_t)(ctx->q.q > 0 ? ctx->q.q : 1) * KS_QUOTA_DIMS * 8;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->q.used, ctx->quota_used_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->q.npused, ctx->quota_npused_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t* scores, int64_t* total) {
+  if (!ctx || !pod) return ctx ? (ctx->err = "ks_eval_pod_debug: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_eval_pod_debug before ks_load_nodes");
+  if (validate_pods(ctx, pod, 1) != KS_OK) return KS_EINVAL;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ensure_pod_capacity(ctx, 1) != KS_OK) return KS_ENOMEM;
+  if (stage_pods_to(ctx, pod, 1, ctx->dbg_pod) != KS_OK) return KS_EHIP;
+  const int64_t n = ctx->n;
+  void* buf = nullptr;
+  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8) + 64;
+  if (dev_alloc(ctx, &buf, bytes) != KS_OK) return KS_ENOMEM;
+  uint32_t* dr = (uint32_t*)buf;
+  int64_t* ds = (int64_t*)((char*)buf + ((size_t)n * 4 + 15) / 16 * 16);
+  int64_t* dt = ds + (size_t)n * KS_NUM_SCORE_PLUGINS;
+  const int threads = 256;
+  const int blocks = (int)((n + threads - 1) / threads);
+  if (blocks > 0) {
+    switch (ctx->nsc) {
+      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->kc, ctx->dbg_pod, n, dr, ds, dt); break;
+      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->kc, ctx->dbg_pod, n, dr, ds, dt); break;
+      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->kc, ctx->dbg_pod, n, dr, ds, dt); break;
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && reasons && n) e = hipMemcpyAsync(reasons, dr, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess && scores && n) e = hipMemcpyAsync(scores, ds, (size_t)n * 8 * KS_NUM_SCORE_PLUGINS, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess && total && n) e = hipMemcpyAsync(total, dt, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(buf);
+  if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "ks_eval_pod_debug: %s", hipGetErrorString(e));
+  return KS_OK;
+}
+
+int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
+  if (!ctx || !o) return ctx ? (ctx->err = "ks_read_nodes: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_read_nodes before ks_load_nodes");
+  const size_t n = (size_t)ctx->n;
+  auto cp = [&](void* h, const void* d, size_t w) -> hipError_t {
+    if (!h || !n) return hipSuccess;
+    return hipMemcpyAsync(h, d, n * w, hipMemcpyDeviceToHost, ctx->stream);
+  };
+  HIPCHK(ctx, cp(o->req_milli_cpu, ctx->d.req_cpu, 8));
+  HIPCHK(ctx, cp(o->req_memory, ctx->d.req_mem, 8));
+  HIPCHK(ctx, cp(o->req_ephemeral, ctx->d.req_eph, 8));
+  HIPCHK(ctx, cp(o->pod_count, ctx->d.pod_count, 4));
+  HIPCHK(ctx, cp(o->nonzero_milli_cpu, ctx->d.nz_cpu, 8));
+  HIPCHK(ctx, cp(o->nonzero_memory, ctx->d.nz_mem, 8));
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) HIPCHK(ctx, cp(o->req_scalar[k], ctx->d.req_sc[k], 8));
+  HIPCHK(ctx, cp(o->la_term_milli_cpu, ctx->d.la_term_cpu, 8));
+  HIPCHK(ctx, cp(o->la_term_memory, ctx->d.la_term_mem, 8));
+  HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, ctx->d.la_pterm_cpu, 8));
+  HIPCHK(ctx, cp(o->la_prod_term_memory, ctx->d.la_pterm_mem, 8));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_read_quota_used(ks_ctx* ctx, int64_t* used) {
+  if (!ctx || !used) return ctx ? (ctx->err = "ks_read_quota_used: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->quota_blob || ctx->q.q == 0) return KS_OK;
+  HIPCHK(ctx, hipMemcpyAsync(used, ctx->q.used, (size_t)ctx->q.q * KS_QUOTA_DIMS * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_get_stats(const ks_ctx* ctx, ks_stats* out) {
+  if (!ctx || !out) return KS_EINVAL;
+  *out = ctx->stats;
+  return KS_OK;
+}
+

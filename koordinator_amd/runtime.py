@@ -1,0 +1,183 @@
+"""ctypes binding of libkoordgpu.so — the product path.
+
+``Evaluator`` owns one ``ks_ctx`` (one scheduler profile on one GPU).  There
+is no CPU fallback: if the in-tree HIP library is missing or no GPU is visible
+the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+from .cluster import NodeState, NodeTable, PodTable, QuotaTable
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkoordgpu.so")
+CSRC = os.path.join(HERE, "csrc")
+
+RESULT_DTYPE = np.dtype([("node", "<i4"), ("status", "<u4"), ("score", "<i8")])
+
+
+class KsError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"ks error {rc}: {msg}")
+        self.rc = rc
+
+
+def build(force: bool = False) -> str:
+    """Compile libkoordgpu.so for gfx950 in-tree (hipcc)."""
+    args = ["make", "-s", "-C", CSRC]
+    if force:
+        args.append("-B")
+    subprocess.check_call(args)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} is not built; run koordinator_amd.runtime.build() (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.ks_create.argtypes = [C.POINTER(abi.KsConfig), C.POINTER(vp)]
+    L.ks_destroy.argtypes = [vp]
+    L.ks_destroy.restype = None
+    L.ks_last_error.argtypes = [vp]
+    L.ks_last_error.restype = C.c_char_p
+    L.ks_load_nodes.argtypes = [vp, C.POINTER(abi.KsNodeCols), C.c_int64]
+    L.ks_update_nodes.argtypes = [vp, abi.P32, C.POINTER(abi.KsNodeCols), C.c_int64]
+    L.ks_load_quotas.argtypes = [vp, C.POINTER(abi.KsQuotaCols), C.c_int32]
+    L.ks_schedule.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
+    L.ks_stage_pods.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32]
+    L.ks_schedule_staged.argtypes = [vp]
+    L.ks_fetch_results.argtypes = [vp, C.POINTER(abi.KsResult), C.c_int32]
+    L.ks_checkpoint.argtypes = [vp]
+    L.ks_restore.argtypes = [vp]
+    L.ks_eval_pod_debug.argtypes = [vp, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
+    L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
+    L.ks_read_quota_used.argtypes = [vp, abi.P64]
+    L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
+    for name in abi.EXPORTED_SYMBOLS:
+        if name not in ("ks_destroy", "ks_last_error"):
+            getattr(L, name).restype = C.c_int
+    _lib = L
+    return L
+
+
+class Evaluator:
+    """One scheduler profile's device-resident node snapshot + the sweep/commit pipeline."""
+
+    def __init__(self, cfg: abi.KsConfig, nodes: Optional[NodeTable] = None, quotas: Optional[QuotaTable] = None):
+        self.L = lib()
+        self.cfg = cfg
+        h = C.c_void_p()
+        rc = self.L.ks_create(C.byref(cfg), C.byref(h))
+        if rc != abi.KS_OK:
+            raise KsError(rc, self.L.ks_last_error(None).decode())
+        self.h = h
+        self.n = 0
+        self.nq = 0
+        self.np_staged = 0
+        if nodes is not None:
+            self.load_nodes(nodes)
+        if quotas is not None:
+            self.load_quotas(quotas)
+
+    def _chk(self, rc: int):
+        if rc != abi.KS_OK:
+            raise KsError(rc, self.L.ks_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ks_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def load_nodes(self, nodes: NodeTable):
+        cols = nodes.ks()
+        self._chk(self.L.ks_load_nodes(self.h, C.byref(cols), nodes.n))
+        self.n = nodes.n
+
+    def update_nodes(self, idx, rows: NodeTable):
+        idx = np.ascontiguousarray(idx, np.int32)
+        cols = rows.ks()
+        self._chk(self.L.ks_update_nodes(self.h, idx.ctypes.data_as(abi.P32), C.byref(cols), rows.n))
+
+    def load_quotas(self, quotas: QuotaTable):
+        cols = quotas.ks()
+        self._chk(self.L.ks_load_quotas(self.h, C.byref(cols), quotas.q))
+        self.nq = quotas.q
+
+    def schedule(self, pods: PodTable) -> dict:
+        out = np.zeros(max(pods.n, 1), RESULT_DTYPE)
+        cols = pods.ks()
+        self._chk(self.L.ks_schedule(self.h, C.byref(cols), pods.n, out.ctypes.data_as(C.POINTER(abi.KsResult))))
+        out = out[: pods.n]
+        return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy()}
+
+    def stage(self, pods: PodTable):
+        cols = pods.ks()
+        self._chk(self.L.ks_stage_pods(self.h, C.byref(cols), pods.n))
+        self.np_staged = pods.n
+
+    def schedule_staged(self):
+        self._chk(self.L.ks_schedule_staged(self.h))
+
+    def fetch(self) -> dict:
+        out = np.zeros(max(self.np_staged, 1), RESULT_DTYPE)
+        self._chk(self.L.ks_fetch_results(self.h, out.ctypes.data_as(C.POINTER(abi.KsResult)), self.np_staged))
+        out = out[: self.np_staged]
+        return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy()}
+
+    def checkpoint(self):
+        self._chk(self.L.ks_checkpoint(self.h))
+
+    def restore(self):
+        self._chk(self.L.ks_restore(self.h))
+
+    def eval_pod(self, pod: PodTable):
+        reasons = np.zeros(max(self.n, 1), np.uint32)
+        scores = np.zeros(max(self.n, 1) * abi.KS_NUM_SCORE_PLUGINS, np.int64)
+        total = np.zeros(max(self.n, 1), np.int64)
+        cols = pod.ks()
+        self._chk(self.L.ks_eval_pod_debug(self.h, C.byref(cols), reasons.ctypes.data_as(abi.PU32),
+                                           scores.ctypes.data_as(abi.P64), total.ctypes.data_as(abi.P64)))
+        n = self.n
+        return reasons[:n], scores[: n * abi.KS_NUM_SCORE_PLUGINS].reshape(n, abi.KS_NUM_SCORE_PLUGINS), total[:n]
+
+    def read_nodes(self) -> NodeState:
+        st = NodeState(self.n)
+        s = st.ks()
+        self._chk(self.L.ks_read_nodes(self.h, C.byref(s)))
+        return st
+
+    def read_quota_used(self) -> np.ndarray:
+        used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)
+        self._chk(self.L.ks_read_quota_used(self.h, used.ctypes.data_as(abi.P64)))
+        return used[: self.nq * abi.KS_QUOTA_DIMS].reshape(self.nq, abi.KS_QUOTA_DIMS)
+
+    def stats(self) -> dict:
+        s = abi.KsStats()
+        self._chk(self.L.ks_get_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in abi.KsStats._fields_}

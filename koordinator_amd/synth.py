@@ -1,0 +1,182 @@
+"""Synthetic clusters for the benchmark configurations.
+
+All generators are deterministic (numpy PCG64, seed 20261015 by default) and
+emit the structure-of-arrays tables the C ABI consumes, i.e. what the Go host
+would produce from a scheduler-cache snapshot plus NodeMetric objects:
+
+* C1  500 nodes, 1k pods, NodeResourcesFit + LoadAwareScheduling
+* C2  5k nodes, 10k pods, + ElasticQuota admission (32 leaf quotas under root,
+      limits sized so roughly a tenth of the pods are rejected)
+* C5  100k nodes, C1 pod distribution (the multi-GPU sharding config)
+
+Node model: allocatable cpu ∈ {32,48,64,96} cores, memory ∈ {128,256,384,512}
+GiB, ephemeral 1 TiB, 110 pods; already-running pods give requested ≈ U(0,0.5)
+of allocatable; NodeMetric usage cpu ~ U(0,0.75)·alloc, memory ~ U(0,0.95)·alloc,
+reported at the frozen "now" (so nothing is expired and no assigned pod is
+counted twice); batch-cpu / batch-memory allocatable (koordlet batch resource)
+= 40 % of allocatable.
+
+Pod model: 70 % default-priority pods (Burstable → koord-prod by QoS, priority_utils.go:26-47)
+and 20 % explicit koord-prod pods requesting cpu ∈ {250m..8000m step 250m} and
+memory ∈ {256Mi..16Gi step 256Mi}, 30 % of them with limit = 1.5 × request;
+10 % koord-batch pods requesting the same shapes as kubernetes.io/batch-cpu
+(milli-cores as a plain integer) and kubernetes.io/batch-memory.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+from .cluster import NodeTable, PodTable, QuotaTable
+from .config import BATCH_CPU, BATCH_MEMORY, CPU, MEMORY, ElasticQuotaArgs, NodeResourcesFitArgs, SchedulerProfile
+
+SEED = 20261015
+GI = 1 << 30
+MI = 1 << 20
+DEFAULT_MILLI_CPU_LA = 250  # loadaware estimator DefaultMilliCPURequest
+DEFAULT_MEMORY_LA = 200 * MI
+DEFAULT_MILLI_CPU_NZ = 100  # upstream schedutil.DefaultMilliCPURequest (non-zero request)
+DEFAULT_MEMORY_NZ = 200 * MI
+
+SLOT_BATCH_CPU = 0
+SLOT_BATCH_MEMORY = 1
+
+QDIM_CPU, QDIM_MEMORY, QDIM_BATCH_CPU, QDIM_BATCH_MEMORY = 0, 1, 2, 3
+
+
+@dataclass
+class Workload:
+    name: str
+    profile: SchedulerProfile
+    nodes: NodeTable
+    pods: PodTable
+    quotas: Optional[QuotaTable]
+
+    @property
+    def cfg(self) -> abi.KsConfig:
+        return self.profile.to_ks_config()
+
+
+def koord_profile(with_quota: bool = False, batch_pods: int = 0, candidates: int = 0) -> SchedulerProfile:
+    """NodeResourcesFit (LeastAllocated cpu/memory/batch-cpu/batch-memory, weight 1 each:
+    config/manager/scheduler-config.yaml:17-31) + LoadAwareScheduling defaults."""
+    fit = NodeResourcesFitArgs(resources={CPU: 1, MEMORY: 1, BATCH_CPU: 1, BATCH_MEMORY: 1})
+    return SchedulerProfile(fit=fit, quota=ElasticQuotaArgs() if with_quota else None,
+                            batch_pods=batch_pods, candidates=candidates)
+
+
+def make_nodes(n: int, rng: np.random.Generator, thresholds=(65, 95)) -> NodeTable:
+    t = NodeTable(n)
+    cores = rng.choice(np.array([32, 48, 64, 96], np.int64), n)
+    mem_gi = rng.choice(np.array([128, 256, 384, 512], np.int64), n)
+    t.alloc_milli_cpu[:] = cores * 1000
+    t.alloc_memory[:] = mem_gi * GI
+    t.alloc_ephemeral[:] = 1024 * GI
+    t.allowed_pods[:] = 110
+    t.pod_count[:] = rng.integers(0, 60, n)
+    frac_c = rng.uniform(0.0, 0.5, n)
+    frac_m = rng.uniform(0.0, 0.5, n)
+    t.req_milli_cpu[:] = (t.alloc_milli_cpu * frac_c).astype(np.int64)
+    t.req_memory[:] = (t.alloc_memory * frac_m).astype(np.int64) // MI * MI
+    t.req_ephemeral[:] = rng.integers(0, 64, n) * GI
+    t.nonzero_milli_cpu[:] = t.req_milli_cpu + t.pod_count * 0  # every running pod declared requests
+    t.nonzero_memory[:] = t.req_memory
+    # koordlet batch resources (kubernetes.io/batch-cpu in milli-cores, batch-memory in bytes)
+    t.alloc_scalar[SLOT_BATCH_CPU] = t.alloc_milli_cpu * 4 // 10
+    t.alloc_scalar[SLOT_BATCH_MEMORY] = t.alloc_memory * 4 // 10
+    t.req_scalar[SLOT_BATCH_CPU] = (t.alloc_scalar[SLOT_BATCH_CPU] * rng.uniform(0, 0.3, n)).astype(np.int64)
+    t.req_scalar[SLOT_BATCH_MEMORY] = (t.alloc_scalar[SLOT_BATCH_MEMORY] * rng.uniform(0, 0.3, n)).astype(np.int64)
+    # NodeMetric: usage, frozen now, nothing expired, no assigned-not-reported pods
+    use_c = (t.alloc_milli_cpu * rng.uniform(0.0, 0.75, n)).astype(np.int64)
+    use_m = (t.alloc_memory * rng.uniform(0.0, 0.95, n)).astype(np.int64)
+    prod_share = rng.uniform(0.3, 0.9, n)
+    t.la_flags[:] = (abi.KS_LA_HAS_METRIC | abi.KS_LA_HAS_STATUS_METRIC | abi.KS_LA_FILTER_USAGE_PRESENT
+                     | abi.KS_LA_NODE_THR_NONEMPTY | abi.KS_LA_HAS_PODS_METRIC)
+    t.la_alloc_milli_cpu[:] = t.alloc_milli_cpu
+    t.la_alloc_memory[:] = t.alloc_memory
+    t.la_term_milli_cpu[:] = use_c
+    t.la_term_memory[:] = use_m
+    t.la_prod_term_milli_cpu[:] = (use_c * prod_share).astype(np.int64)
+    t.la_prod_term_memory[:] = (use_m * prod_share).astype(np.int64)
+    t.la_thr_cpu[:] = thresholds[0]
+    t.la_thr_memory[:] = thresholds[1]
+    t.la_total_milli_cpu[:] = t.alloc_milli_cpu
+    t.la_total_milli_memory[:] = t.alloc_memory * 1000
+    t.la_usage_milli_cpu[:] = use_c
+    t.la_usage_milli_memory[:] = use_m * 1000
+    t.la_prod_usage_milli_cpu[:] = t.la_prod_term_milli_cpu
+    t.la_prod_usage_milli_memory[:] = t.la_prod_term_memory * 1000
+    return t
+
+
+def make_pods(p: int, rng: np.random.Generator, n_quotas: int = 0) -> PodTable:
+    t = PodTable(p)
+    cpu = rng.integers(1, 33, p) * 250
+    mem = rng.integers(1, 65, p) * 256 * MI
+    has_lim = rng.random(p) < 0.3
+    lim_cpu = np.where(has_lim, cpu * 3 // 2, 0)
+    lim_mem = np.where(has_lim, mem * 3 // 2, 0)
+    kind = rng.choice(np.array([0, 1, 2]), p, p=[0.7, 0.2, 0.1])  # 0 default, 1 explicit prod, 2 batch
+    batch = kind == 2
+    t.flags[:] = np.where(batch, 0, abi.KS_POD_PROD).astype(np.uint32)
+    t.flags[batch] |= abi.KS_POD_SCALAR_KEYS
+    t.req_milli_cpu[:] = np.where(batch, 0, cpu)
+    t.req_memory[:] = np.where(batch, 0, mem)
+    t.req_scalar[SLOT_BATCH_CPU] = np.where(batch, cpu, 0)
+    t.req_scalar[SLOT_BATCH_MEMORY] = np.where(batch, mem, 0)
+    t.nonzero_milli_cpu[:] = np.where(batch, DEFAULT_MILLI_CPU_NZ, cpu)
+    t.nonzero_memory[:] = np.where(batch, DEFAULT_MEMORY_NZ, mem)
+    # EstimatePod: translated resource (batch pods -> batch-cpu / batch-memory) request/limit
+    t.la_req_cpu[:] = cpu
+    t.la_lim_cpu[:] = lim_cpu
+    t.la_req_memory[:] = mem
+    t.la_lim_memory[:] = lim_mem
+    t.la_dflt_cpu[:] = DEFAULT_MILLI_CPU_LA
+    t.la_dflt_memory[:] = DEFAULT_MEMORY_LA
+    if n_quotas:
+        t.quota[:] = rng.integers(0, n_quotas, p)
+        t.quota_req[QDIM_CPU] = t.req_milli_cpu
+        t.quota_req[QDIM_MEMORY] = t.req_memory
+        t.quota_req[QDIM_BATCH_CPU] = t.req_scalar[SLOT_BATCH_CPU]
+        t.quota_req[QDIM_BATCH_MEMORY] = t.req_scalar[SLOT_BATCH_MEMORY]
+        t.quota_mask[:] = np.where(batch, (1 << QDIM_BATCH_CPU) | (1 << QDIM_BATCH_MEMORY),
+                                   (1 << QDIM_CPU) | (1 << QDIM_MEMORY)).astype(np.uint32)
+    return t
+
+
+def make_quotas(pods: PodTable, n_quotas: int, rng: np.random.Generator, admit_frac: float = 0.9) -> QuotaTable:
+    """Leaf quotas directly under root whose runtime limits admit ~admit_frac of demand."""
+    q = QuotaTable(n_quotas)
+    q.limit_mask[:] = (1 << QDIM_CPU) | (1 << QDIM_MEMORY) | (1 << QDIM_BATCH_CPU) | (1 << QDIM_BATCH_MEMORY)
+    for d in (QDIM_CPU, QDIM_MEMORY, QDIM_BATCH_CPU, QDIM_BATCH_MEMORY):
+        has = pods.quota >= 0
+        demand = np.bincount(pods.quota[has], weights=pods.quota_req[d][has].astype(np.float64), minlength=n_quotas)
+        q.limit[d] = (demand * admit_frac * rng.uniform(0.95, 1.05, n_quotas)).astype(np.int64)
+    q.min_mask[:] = q.limit_mask
+    q.min[:] = q.limit // 2
+    return q
+
+
+def c1(seed: int = SEED, n_nodes: int = 500, n_pods: int = 1000, **kw) -> Workload:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = make_nodes(n_nodes, rng)
+    pods = make_pods(n_pods, rng)
+    return Workload("C1", koord_profile(**kw), nodes, pods, None)
+
+
+def c2(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, n_quotas: int = 32, **kw) -> Workload:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = make_nodes(n_nodes, rng)
+    pods = make_pods(n_pods, rng, n_quotas)
+    quotas = make_quotas(pods, n_quotas, rng)
+    return Workload("C2", koord_profile(with_quota=True, **kw), nodes, pods, quotas)
+
+
+def c5(seed: int = SEED, n_nodes: int = 100_000, n_pods: int = 1_000_000, **kw) -> Workload:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = make_nodes(n_nodes, rng)
+    pods = make_pods(n_pods, rng)
+    return Workload("C5", koord_profile(**kw), nodes, pods, None)

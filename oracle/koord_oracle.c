@@ -1,0 +1,618 @@
+/*
+ * koord_oracle.c — CPU restatement of koord-scheduler's per-pod sweep.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity oracle and the CPU
+ * baseline timer.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product (libkoordgpu.so) never does.
+ *
+ * It consumes the same structure-of-arrays layout as the C ABI
+ * (include/koordgpu.h) and restates, in plain scalar C, the reference code:
+ *
+ *   NodeResourcesFit Filter  upstream k8s v1.24 noderesources/fit.go fitsRequest
+ *                            (in-tree proxy: pkg/scheduler/plugins/reservation/plugin.go:445-496)
+ *   NodeResourcesFit Score   upstream resource_allocation.go + least_allocated.go / most_allocated.go
+ *                            (in-tree copies: pkg/scheduler/plugins/nodenumaresource/least_allocated.go:30-58,
+ *                             most_allocated.go:30-62)
+ *   LoadAware Filter         pkg/scheduler/plugins/loadaware/load_aware.go:123-254
+ *   LoadAware Score          load_aware.go:269-397 (scorer :378-386, leastRequestedScore :388-397)
+ *   EstimatePod              loadaware/estimator/default_estimator.go:57-108
+ *   Reserve                  load_aware.go:260 -> pod_assign_cache.go:53; upstream NodeInfo.AddPod;
+ *                            elasticquota/plugin.go:323 -> core/group_quota_manager.go:798,620-655
+ *   ElasticQuota PreFilter   elasticquota/plugin.go:210-255, plugin_helper.go:281-319
+ *   Sweep driver             upstream schedule_one.go (schedulePod, findNodesThatPassFilters,
+ *                            prioritizeNodes, selectHost) with percentageOfNodesToScore=100 and
+ *                            lowest-index tie-break; Parallelizer pkg/util/parallelize/parallelism.go:29-49
+ *
+ * Floating point sites keep Go's operation order (compile with
+ * -ffp-contract=off, no -ffast-math).  Go math.Round == C round().
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/koordgpu.h"
+
+#define MAX_NODE_SCORE 100 /* framework.MaxNodeScore */
+
+/* ------------------------------------------------------------------ */
+/* scorers                                                             */
+/* ------------------------------------------------------------------ */
+
+/* load_aware.go:388-397 and nodenumaresource/least_allocated.go:45-54 */
+int64_t ko_least_requested_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * MAX_NODE_SCORE) / capacity;
+}
+
+/* nodenumaresource/most_allocated.go:50-62 */
+int64_t ko_most_requested_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) requested = capacity;
+  return (requested * MAX_NODE_SCORE) / capacity;
+}
+
+/* estimator/default_estimator.go:73-108 (estimatedUsedByResource).
+ * req/lim: the translated resource's request/limit value; dflt: value returned
+ * when the chosen quantity is zero. */
+int64_t ko_estimated_used(int64_t req, int64_t lim, int64_t scaling_factor, int64_t dflt) {
+  int64_t quantity;
+  if (lim > req) { /* limitQuantity.Cmp(requestQuantity) > 0 */
+    scaling_factor = 100;
+    quantity = lim;
+  } else {
+    quantity = req;
+  }
+  if (quantity == 0) return dflt;
+  int64_t est = (int64_t)round((double)quantity * (double)scaling_factor / 100.0);
+  if (lim > 0 && est > lim) est = lim;
+  return est;
+}
+
+/* ------------------------------------------------------------------ */
+/* scheduler state                                                     */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+  int64_t *alloc_cpu, *alloc_mem, *alloc_eph;
+  int32_t *allowed_pods;
+  int64_t *req_cpu, *req_mem, *req_eph;
+  int32_t *pod_count;
+  int64_t *nz_cpu, *nz_mem;
+  int64_t *alloc_sc[KS_MAX_SCALARS], *req_sc[KS_MAX_SCALARS];
+  uint32_t *la_flags;
+  int64_t *la_alloc_cpu, *la_alloc_mem;
+  int64_t *la_term_cpu, *la_term_mem, *la_pterm_cpu, *la_pterm_mem;
+  int32_t *la_thr_cpu, *la_thr_mem, *la_pthr_cpu, *la_pthr_mem;
+  int64_t *la_total_cpu, *la_total_mem, *la_usage_cpu, *la_usage_mem, *la_pusage_cpu, *la_pusage_mem;
+} ko_nodes;
+
+typedef struct {
+  int32_t parent;
+  uint32_t limit_mask, min_mask;
+  int64_t limit[KS_QUOTA_DIMS], used[KS_QUOTA_DIMS], min[KS_QUOTA_DIMS], npused[KS_QUOTA_DIMS];
+} ko_quota;
+
+typedef struct ko_pool ko_pool;
+
+typedef struct ko_sched {
+  ks_config cfg;
+  int64_t n;
+  ko_nodes nd;
+  void *blob;
+  int32_t nq;
+  ko_quota *q;
+  /* per-call scratch */
+  uint8_t *feasible;
+  int64_t *total;
+  ko_pool *pool;
+  int nthreads;
+} ko_sched;
+
+/* pod view for one pod (values pulled out of ks_pod_cols) */
+typedef struct {
+  int64_t cpu, mem, eph, sc[KS_MAX_SCALARS];
+  int64_t nzcpu, nzmem;
+  uint32_t flags;
+  int64_t est_cpu, est_mem;
+  int32_t quota;
+  uint32_t qmask;
+  int64_t qreq[KS_QUOTA_DIMS];
+} ko_pod;
+
+static int64_t colv64(const int64_t *c, int64_t i) { return c ? c[i] : 0; }
+static uint32_t colvu32(const uint32_t *c, int64_t i) { return c ? c[i] : 0; }
+
+static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod *p) {
+  memset(p, 0, sizeof(*p));
+  p->cpu = colv64(pc->req_milli_cpu, i);
+  p->mem = colv64(pc->req_memory, i);
+  p->eph = colv64(pc->req_ephemeral, i);
+  for (int k = 0; k < KS_MAX_SCALARS; k++) p->sc[k] = colv64(pc->req_scalar[k], i);
+  p->nzcpu = colv64(pc->nonzero_milli_cpu, i);
+  p->nzmem = colv64(pc->nonzero_memory, i);
+  p->flags = colvu32(pc->flags, i);
+  p->est_cpu = ko_estimated_used(colv64(pc->la_req_cpu, i), colv64(pc->la_lim_cpu, i),
+                                 s->cfg.loadaware.scaling_cpu, colv64(pc->la_dflt_cpu, i));
+  p->est_mem = ko_estimated_used(colv64(pc->la_req_memory, i), colv64(pc->la_lim_memory, i),
+                                 s->cfg.loadaware.scaling_memory, colv64(pc->la_dflt_memory, i));
+  p->quota = pc->quota ? pc->quota[i] : -1;
+  p->qmask = colvu32(pc->quota_mask, i);
+  for (int d = 0; d < KS_QUOTA_DIMS; d++) p->qreq[d] = colv64(pc->quota_req[d], i);
+}
+
+/* ------------------------------------------------------------------ */
+/* Filter                                                              */
+/* ------------------------------------------------------------------ */
+
+/* upstream fitsRequest (noderesources/fit.go); returns KS_R_FIT_* bits */
+static uint32_t fit_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
+  const ko_nodes *d = &s->nd;
+  uint32_t r = 0;
+  if ((int64_t)d->pod_count[n] + 1 > (int64_t)d->allowed_pods[n]) r |= KS_R_FIT_PODS;
+  if (p->cpu == 0 && p->mem == 0 && p->eph == 0 && !(p->flags & KS_POD_SCALAR_KEYS)) return r;
+  if (p->cpu > d->alloc_cpu[n] - d->req_cpu[n]) r |= KS_R_FIT_CPU;
+  if (p->mem > d->alloc_mem[n] - d->req_mem[n]) r |= KS_R_FIT_MEMORY;
+  if (p->eph > d->alloc_eph[n] - d->req_eph[n]) r |= KS_R_FIT_EPHEMERAL;
+  for (int k = 0; k < KS_MAX_SCALARS; k++) {
+    if (p->sc[k] == 0) continue; /* resource not in podRequest.ScalarResources */
+    if (p->sc[k] > d->alloc_sc[k][n] - d->req_sc[k][n]) r |= KS_R_FIT_SCALAR;
+  }
+  return r;
+}
+
+/* usage := int64(math.Round(float64(used.MilliValue()) / float64(total.MilliValue()) * 100)) */
+static int usage_exceeds(int64_t used_milli, int64_t total_milli, int32_t thr) {
+  if (thr == 0) return 0;
+  if (total_milli == 0) return 0; /* total.IsZero() -> continue */
+  int64_t usage = (int64_t)round((double)used_milli / (double)total_milli * 100.0);
+  return usage >= thr;
+}
+
+/* load_aware.go:123-254; returns KS_R_LA_* bits (one resource reported, cpu first) */
+static uint32_t la_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
+  const ko_nodes *d = &s->nd;
+  if (p->flags & KS_POD_DAEMONSET) return 0;
+  uint32_t f = d->la_flags[n];
+  if (!(f & KS_LA_HAS_METRIC)) return 0;
+  if (s->cfg.loadaware.filter_expired_node_metrics && (f & KS_LA_EXPIRED)) return 0;
+  if ((f & KS_LA_PROD_THR_NONEMPTY) && (p->flags & KS_POD_PROD)) {
+    /* filterProdUsage */
+    if (!(f & KS_LA_HAS_PODS_METRIC)) return 0;
+    if (usage_exceeds(d->la_pusage_cpu[n], d->la_total_cpu[n], d->la_pthr_cpu[n])) return KS_R_LA_CPU | KS_R_LA_PROD;
+    if (usage_exceeds(d->la_pusage_mem[n], d->la_total_mem[n], d->la_pthr_mem[n])) return KS_R_LA_MEMORY | KS_R_LA_PROD;
+    return 0;
+  }
+  if (!(f & KS_LA_NODE_THR_NONEMPTY)) return 0;
+  /* filterNodeUsage */
+  if (!(f & KS_LA_HAS_STATUS_METRIC)) return 0;
+  if (!(f & KS_LA_FILTER_USAGE_PRESENT)) return 0;
+  uint32_t agg = (f & KS_LA_AGGREGATED_FILTER) ? KS_R_LA_AGGREGATED : 0;
+  if (usage_exceeds(d->la_usage_cpu[n], d->la_total_cpu[n], d->la_thr_cpu[n])) return KS_R_LA_CPU | agg;
+  if (usage_exceeds(d->la_usage_mem[n], d->la_total_mem[n], d->la_thr_mem[n])) return KS_R_LA_MEMORY | agg;
+  return 0;
+}
+
+static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n) {
+  uint32_t r = 0;
+  if (s->cfg.fit.enable_filter) r |= fit_filter(s, p, n);
+  if (s->cfg.loadaware.enable_filter) r |= la_filter(s, p, n);
+  return r;
+}
+
+/* ------------------------------------------------------------------ */
+/* Score                                                               */
+/* ------------------------------------------------------------------ */
+
+/* upstream resourceAllocationScorer.score with LeastAllocated/MostAllocated */
+static int64_t fit_score(const ko_sched *s, const ko_pod *p, int64_t n) {
+  const ko_nodes *d = &s->nd;
+  const ks_fit_args *a = &s->cfg.fit;
+  int64_t node_score = 0, weight_sum = 0;
+  int most = a->strategy == KS_MOST_ALLOCATED;
+#define FIT_TERM(W, ALLOC, REQ)                                                              \
+  do {                                                                                       \
+    int64_t al_ = (ALLOC), rq_ = (REQ);                                                      \
+    if ((W) != 0 && al_ != 0) {                                                              \
+      int64_t sc_ = most ? ko_most_requested_score(rq_, al_) : ko_least_requested_score(rq_, al_); \
+      node_score += sc_ * (W);                                                               \
+      weight_sum += (W);                                                                     \
+    }                                                                                        \
+  } while (0)
+  FIT_TERM(a->weight_cpu, d->alloc_cpu[n], d->nz_cpu[n] + p->nzcpu);
+  FIT_TERM(a->weight_memory, d->alloc_mem[n], d->nz_mem[n] + p->nzmem);
+  FIT_TERM(a->weight_ephemeral, d->alloc_eph[n], d->req_eph[n] + p->eph);
+  for (int k = 0; k < KS_MAX_SCALARS; k++) {
+    if (p->sc[k] == 0) continue; /* scalar not requested by the pod -> (0, 0), bypassed */
+    FIT_TERM(a->weight_scalar[k], d->alloc_sc[k][n], d->req_sc[k][n] + p->sc[k]);
+  }
+#undef FIT_TERM
+  if (weight_sum == 0) return 0;
+  return node_score / weight_sum;
+}
+
+/* load_aware.go:269-335 on the reduced node term, scorer :378-386 */
+static int64_t la_score(const ko_sched *s, const ko_pod *p, int64_t n) {
+  const ko_nodes *d = &s->nd;
+  const ks_loadaware_args *a = &s->cfg.loadaware;
+  uint32_t f = d->la_flags[n];
+  if (!(f & KS_LA_HAS_METRIC)) return 0;
+  if (f & KS_LA_EXPIRED) return 0;
+  int prod = (p->flags & KS_POD_PROD) && a->score_according_prod_usage;
+  int64_t used_cpu = p->est_cpu + (prod ? d->la_pterm_cpu[n] : d->la_term_cpu[n]);
+  int64_t used_mem = p->est_mem + (prod ? d->la_pterm_mem[n] : d->la_term_mem[n]);
+  int64_t node_score = 0, weight_sum = 0;
+  if (a->weight_cpu) {
+    node_score += ko_least_requested_score(used_cpu, d->la_alloc_cpu[n]) * a->weight_cpu;
+    weight_sum += a->weight_cpu;
+  }
+  if (a->weight_memory) {
+    node_score += ko_least_requested_score(used_mem, d->la_alloc_mem[n]) * a->weight_memory;
+    weight_sum += a->weight_memory;
+  }
+  if (weight_sum == 0) return 0; /* rejected by validation in the reference */
+  return node_score / weight_sum;
+}
+
+static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_out, int64_t *la_out) {
+  int64_t t = 0, fs = 0, ls = 0;
+  if (s->cfg.fit.enable_score) {
+    fs = fit_score(s, p, n);
+    t += fs * s->cfg.fit.plugin_weight;
+  }
+  if (s->cfg.loadaware.enable_score) {
+    ls = la_score(s, p, n);
+    t += ls * s->cfg.loadaware.plugin_weight;
+  }
+  if (fit_out) *fit_out = fs;
+  if (la_out) *la_out = ls;
+  return t;
+}
+
+/* ------------------------------------------------------------------ */
+/* ElasticQuota PreFilter + Reserve                                    */
+/* ------------------------------------------------------------------ */
+
+/* quotav1.LessThanOrEqual(Mask(Add(req, used), names(req)), limit): compares only keys of
+ * `limit` that are also present in the masked sum. */
+static int quota_fits(const ko_quota *q, const ko_pod *p) {
+  for (int d = 0; d < KS_QUOTA_DIMS; d++) {
+    if (!((q->limit_mask >> d) & 1u)) continue;
+    if (!((p->qmask >> d) & 1u)) continue;
+    if (p->qreq[d] + q->used[d] > q->limit[d]) return 0;
+  }
+  return 1;
+}
+
+static uint32_t quota_prefilter(const ko_sched *s, const ko_pod *p) {
+  if (!s->cfg.quota.enable || p->quota < 0) return 0;
+  const ko_quota *q = &s->q[p->quota];
+  if (!quota_fits(q, p)) return KS_S_QUOTA;
+  if (p->flags & KS_POD_NONPREEMPTIBLE) {
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) {
+      if (!((q->min_mask >> d) & 1u)) continue;
+      if (!((p->qmask >> d) & 1u)) continue;
+      if (p->qreq[d] + q->npused[d] > q->min[d]) return KS_S_QUOTA_NONPREEMPTIBLE;
+    }
+  }
+  if (s->cfg.quota.enable_check_parent_quota) {
+    /* checkQuotaRecursive: the pod's own quota first, then each ancestor below root */
+    for (int32_t cur = p->quota; cur >= 0; cur = s->q[cur].parent) {
+      if (!quota_fits(&s->q[cur], p)) return KS_S_QUOTA | KS_S_QUOTA_PARENT;
+    }
+  }
+  return 0;
+}
+
+/* updatePodUsedNoLock -> updateGroupDeltaUsedNoLock: used += request along the chain */
+static void quota_reserve(ko_sched *s, const ko_pod *p) {
+  if (!s->cfg.quota.enable || p->quota < 0) return;
+  for (int32_t cur = p->quota; cur >= 0; cur = s->q[cur].parent) {
+    ko_quota *q = &s->q[cur];
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) {
+      if (!((p->qmask >> d) & 1u)) continue;
+      q->used[d] += p->qreq[d];
+      if (p->flags & KS_POD_NONPREEMPTIBLE) q->npused[d] += p->qreq[d];
+    }
+  }
+}
+
+/* NodeInfo.AddPod (upstream) + podAssignCache.assign (pod_assign_cache.go:53) */
+static void node_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
+  ko_nodes *d = &s->nd;
+  d->req_cpu[n] += p->cpu;
+  d->req_mem[n] += p->mem;
+  d->req_eph[n] += p->eph;
+  for (int k = 0; k < KS_MAX_SCALARS; k++) d->req_sc[k][n] += p->sc[k];
+  d->nz_cpu[n] += p->nzcpu;
+  d->nz_mem[n] += p->nzmem;
+  d->pod_count[n] += 1;
+  /* the freshly assigned pod has no PodMetric, so estimatedAssignedPodUsed counts
+   * its estimate (load_aware.go:350-355) in every later Score on this node. */
+  d->la_term_cpu[n] += p->est_cpu;
+  d->la_term_mem[n] += p->est_mem;
+  if (p->flags & KS_POD_PROD) {
+    d->la_pterm_cpu[n] += p->est_cpu;
+    d->la_pterm_mem[n] += p->est_mem;
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* Parallelizer: workqueue.ParallelizeUntil(ctx, 16, n, f, chunk)       */
+/* ------------------------------------------------------------------ */
+
+typedef void (*ko_piece_fn)(void *arg, int64_t lo, int64_t hi);
+
+struct ko_pool {
+  int workers;
+  pthread_t *th;
+  pthread_mutex_t mu;
+  pthread_cond_t cv_start, cv_done;
+  int64_t generation;
+  int shutdown;
+  int active;
+  /* current job */
+  ko_piece_fn fn;
+  void *arg;
+  int64_t pieces, chunk;
+  atomic_llong next;
+};
+
+static void run_chunks(ko_pool *pl) {
+  for (;;) {
+    int64_t lo = atomic_fetch_add(&pl->next, pl->chunk);
+    if (lo >= pl->pieces) break;
+    int64_t hi = lo + pl->chunk;
+    if (hi > pl->pieces) hi = pl->pieces;
+    pl->fn(pl->arg, lo, hi);
+  }
+}
+
+static void *pool_main(void *v) {
+  ko_pool *pl = (ko_pool *)v;
+  int64_t seen = 0;
+  for (;;) {
+    pthread_mutex_lock(&pl->mu);
+    while (pl->generation == seen && !pl->shutdown) pthread_cond_wait(&pl->cv_start, &pl->mu);
+    if (pl->shutdown) {
+      pthread_mutex_unlock(&pl->mu);
+      return NULL;
+    }
+    seen = pl->generation;
+    pthread_mutex_unlock(&pl->mu);
+    run_chunks(pl);
+    pthread_mutex_lock(&pl->mu);
+    if (--pl->active == 0) pthread_cond_signal(&pl->cv_done);
+    pthread_mutex_unlock(&pl->mu);
+  }
+}
+
+static ko_pool *pool_create(int workers) {
+  ko_pool *pl = (ko_pool *)calloc(1, sizeof(ko_pool));
+  pl->workers = workers;
+  pthread_mutex_init(&pl->mu, NULL);
+  pthread_cond_init(&pl->cv_start, NULL);
+  pthread_cond_init(&pl->cv_done, NULL);
+  if (workers > 1) {
+    pl->th = (pthread_t *)calloc((size_t)workers - 1, sizeof(pthread_t));
+    for (int i = 0; i < workers - 1; i++) pthread_create(&pl->th[i], NULL, pool_main, pl);
+  }
+  return pl;
+}
+
+static void pool_destroy(ko_pool *pl) {
+  if (!pl) return;
+  pthread_mutex_lock(&pl->mu);
+  pl->shutdown = 1;
+  pthread_cond_broadcast(&pl->cv_start);
+  pthread_mutex_unlock(&pl->mu);
+  for (int i = 0; i < pl->workers - 1; i++) pthread_join(pl->th[i], NULL);
+  free(pl->th);
+  free(pl);
+}
+
+/* chunkSizeFor (parallelism.go:34-44): max(1, min(sqrt(n), n/parallelism+1)) */
+static int64_t chunk_size_for(int64_t n, int parallelism) {
+  int64_t s = (int64_t)sqrt((double)n);
+  int64_t r = n / parallelism + 1;
+  if (s > r) s = r;
+  else if (s < 1) s = 1;
+  return s;
+}
+
+static void pool_until(ko_pool *pl, int64_t pieces, ko_piece_fn fn, void *arg) {
+  if (pieces <= 0) return;
+  pl->fn = fn;
+  pl->arg = arg;
+  pl->pieces = pieces;
+  pl->chunk = chunk_size_for(pieces, pl->workers < 16 ? 16 : pl->workers);
+  atomic_store(&pl->next, 0);
+  if (pl->workers <= 1) {
+    run_chunks(pl);
+    return;
+  }
+  pthread_mutex_lock(&pl->mu);
+  pl->active = pl->workers - 1;
+  pl->generation++;
+  pthread_cond_broadcast(&pl->cv_start);
+  pthread_mutex_unlock(&pl->mu);
+  run_chunks(pl); /* the calling goroutine participates */
+  pthread_mutex_lock(&pl->mu);
+  while (pl->active > 0) pthread_cond_wait(&pl->cv_done, &pl->mu);
+  pthread_mutex_unlock(&pl->mu);
+}
+
+/* ------------------------------------------------------------------ */
+/* public oracle API                                                   */
+/* ------------------------------------------------------------------ */
+
+#define NCOL64 (20 + 2 * KS_MAX_SCALARS)
+
+ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int nthreads) {
+  ko_sched *s = (ko_sched *)calloc(1, sizeof(ko_sched));
+  s->cfg = *cfg;
+  s->n = n;
+  size_t nn = (size_t)(n > 0 ? n : 1);
+  s->blob = calloc(nn, NCOL64 * 8 + 8 * 4 + 4);
+  char *b = (char *)s->blob;
+#define TAKE64(f) (s->nd.f = (int64_t *)b, b += nn * 8)
+#define TAKE32(f) (s->nd.f = (int32_t *)b, b += nn * 4)
+  TAKE64(alloc_cpu); TAKE64(alloc_mem); TAKE64(alloc_eph);
+  TAKE64(req_cpu); TAKE64(req_mem); TAKE64(req_eph);
+  TAKE64(nz_cpu); TAKE64(nz_mem);
+  for (int k = 0; k < KS_MAX_SCALARS; k++) { TAKE64(alloc_sc[k]); TAKE64(req_sc[k]); }
+  TAKE64(la_alloc_cpu); TAKE64(la_alloc_mem);
+  TAKE64(la_term_cpu); TAKE64(la_term_mem); TAKE64(la_pterm_cpu); TAKE64(la_pterm_mem);
+  TAKE64(la_total_cpu); TAKE64(la_total_mem); TAKE64(la_usage_cpu); TAKE64(la_usage_mem);
+  TAKE64(la_pusage_cpu); TAKE64(la_pusage_mem);
+  TAKE32(allowed_pods); TAKE32(pod_count);
+  TAKE32(la_thr_cpu); TAKE32(la_thr_mem); TAKE32(la_pthr_cpu); TAKE32(la_pthr_mem);
+  s->nd.la_flags = (uint32_t *)b;
+  b += nn * 4;
+#undef TAKE64
+#undef TAKE32
+#define CP64(dst, src) do { if (src) memcpy(s->nd.dst, src, (size_t)n * 8); } while (0)
+#define CP32(dst, src) do { if (src) memcpy(s->nd.dst, src, (size_t)n * 4); } while (0)
+  CP64(alloc_cpu, nc->alloc_milli_cpu); CP64(alloc_mem, nc->alloc_memory); CP64(alloc_eph, nc->alloc_ephemeral);
+  CP32(allowed_pods, nc->allowed_pods);
+  CP64(req_cpu, nc->req_milli_cpu); CP64(req_mem, nc->req_memory); CP64(req_eph, nc->req_ephemeral);
+  CP32(pod_count, nc->pod_count);
+  CP64(nz_cpu, nc->nonzero_milli_cpu); CP64(nz_mem, nc->nonzero_memory);
+  for (int k = 0; k < KS_MAX_SCALARS; k++) { CP64(alloc_sc[k], nc->alloc_scalar[k]); CP64(req_sc[k], nc->req_scalar[k]); }
+  CP32(la_flags, (const int32_t *)nc->la_flags);
+  CP64(la_alloc_cpu, nc->la_alloc_milli_cpu); CP64(la_alloc_mem, nc->la_alloc_memory);
+  CP64(la_term_cpu, nc->la_term_milli_cpu); CP64(la_term_mem, nc->la_term_memory);
+  CP64(la_pterm_cpu, nc->la_prod_term_milli_cpu); CP64(la_pterm_mem, nc->la_prod_term_memory);
+  CP32(la_thr_cpu, nc->la_thr_cpu); CP32(la_thr_mem, nc->la_thr_memory);
+  CP32(la_pthr_cpu, nc->la_prod_thr_cpu); CP32(la_pthr_mem, nc->la_prod_thr_memory);
+  CP64(la_total_cpu, nc->la_total_milli_cpu); CP64(la_total_mem, nc->la_total_milli_memory);
+  CP64(la_usage_cpu, nc->la_usage_milli_cpu); CP64(la_usage_mem, nc->la_usage_milli_memory);
+  CP64(la_pusage_cpu, nc->la_prod_usage_milli_cpu); CP64(la_pusage_mem, nc->la_prod_usage_milli_memory);
+#undef CP64
+#undef CP32
+  s->feasible = (uint8_t *)calloc(nn, 1);
+  s->total = (int64_t *)calloc(nn, 8);
+  s->nthreads = nthreads < 1 ? 1 : nthreads;
+  s->pool = pool_create(s->nthreads);
+  return s;
+}
+
+void ko_destroy(ko_sched *s) {
+  if (!s) return;
+  pool_destroy(s->pool);
+  free(s->blob);
+  free(s->q);
+  free(s->feasible);
+  free(s->total);
+  free(s);
+}
+
+int ko_load_quotas(ko_sched *s, const ks_quota_cols *qc, int32_t nq) {
+  free(s->q);
+  s->nq = nq;
+  s->q = (ko_quota *)calloc((size_t)(nq > 0 ? nq : 1), sizeof(ko_quota));
+  for (int32_t i = 0; i < nq; i++) {
+    ko_quota *q = &s->q[i];
+    q->parent = qc->parent ? qc->parent[i] : -1;
+    q->limit_mask = colvu32(qc->limit_mask, i);
+    q->min_mask = colvu32(qc->min_mask, i);
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) {
+      q->limit[d] = colv64(qc->limit[d], i);
+      q->used[d] = colv64(qc->used[d], i);
+      q->min[d] = colv64(qc->min[d], i);
+      q->npused[d] = colv64(qc->nonpreemptible_used[d], i);
+    }
+  }
+  return 0;
+}
+
+typedef struct {
+  ko_sched *s;
+  const ko_pod *p;
+} sweep_arg;
+
+static void filter_piece(void *v, int64_t lo, int64_t hi) {
+  sweep_arg *a = (sweep_arg *)v;
+  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = filter_node(a->s, a->p, n) == 0;
+}
+
+static void score_piece(void *v, int64_t lo, int64_t hi) {
+  sweep_arg *a = (sweep_arg *)v;
+  for (int64_t n = lo; n < hi; n++)
+    a->s->total[n] = a->s->feasible[n] ? total_score(a->s, a->p, n, NULL, NULL) : -1;
+}
+
+/* one scheduling cycle per pod, in order (scheduleOne loop) */
+int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) {
+  for (int32_t i = 0; i < np; i++) {
+    ko_pod p;
+    load_pod(s, pc, i, &p);
+    out[i].node = -1;
+    out[i].score = 0;
+    out[i].status = quota_prefilter(s, &p);
+    if (out[i].status) continue;
+    sweep_arg a = {s, &p};
+    pool_until(s->pool, s->n, filter_piece, &a);
+    pool_until(s->pool, s->n, score_piece, &a);
+    /* prioritizeNodes sum + selectHost: max score, lowest index on ties */
+    int64_t best = -1, best_n = -1;
+    for (int64_t n = 0; n < s->n; n++) {
+      if (s->total[n] > best) {
+        best = s->total[n];
+        best_n = n;
+      }
+    }
+    if (best_n < 0) {
+      out[i].status = KS_S_UNSCHEDULABLE;
+      continue;
+    }
+    out[i].node = (int32_t)best_n;
+    out[i].score = best;
+    node_reserve(s, &p, best_n);
+    quota_reserve(s, &p);
+  }
+  return 0;
+}
+
+int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *scores, int64_t *total) {
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  for (int64_t n = 0; n < s->n; n++) {
+    uint32_t r = filter_node(s, &p, n);
+    int64_t fs = 0, ls = 0, t = -1;
+    if (!r) t = total_score(s, &p, n, &fs, &ls);
+    if (reasons) reasons[n] = r;
+    if (scores) {
+      scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = r ? 0 : fs;
+      scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = r ? 0 : ls;
+    }
+    if (total) total[n] = t;
+  }
+  return 0;
+}
+
+int ko_read_nodes(const ko_sched *s, ks_node_state *o) {
+  size_t b8 = (size_t)s->n * 8, b4 = (size_t)s->n * 4;
+  if (o->req_milli_cpu) memcpy(o->req_milli_cpu, s->nd.req_cpu, b8);
+  if (o->req_memory) memcpy(o->req_memory, s->nd.req_mem, b8);
+  if (o->req_ephemeral) memcpy(o->req_ephemeral, s->nd.req_eph, b8);
+  if (o->pod_count) memcpy(o->pod_count, s->nd.pod_count, b4);
+  if (o->nonzero_milli_cpu) memcpy(o->nonzero_milli_cpu, s->nd.nz_cpu, b8);
+  if (o->nonzero_memory) memcpy(o->nonzero_memory, s->nd.nz_mem, b8);
+  for (int k = 0; k < KS_MAX_SCALARS; k++)
+    if (o->req_scalar[k]) memcpy(o->req_scalar[k], s->nd.req_sc[k], b8);
+  if (o->la_term_milli_cpu) memcpy(o->la_term_milli_cpu, s->nd.la_term_cpu, b8);
+  if (o->la_term_memory) memcpy(o->la_term_memory, s->nd.la_term_mem, b8);
+  if (o->la_prod_term_milli_cpu) memcpy(o->la_prod_term_milli_cpu, s->nd.la_pterm_cpu, b8);
+  if (o->la_prod_term_memory) memcpy(o->la_prod_term_memory, s->nd.la_pterm_mem, b8);
+  return 0;
+}
+
+int ko_read_quota_used(const ko_sched *s, int64_t *used) {
+  for (int32_t i = 0; i < s->nq; i++)
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) used[(size_t)i * KS_QUOTA_DIMS + d] = s->q[i].used[d];
+  return 0;
+}

@@ -1,0 +1,107 @@
+"""ctypes wrapper of oracle/libkoord_oracle.so — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (parity checker), __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  Consumes the same SoA tables as the HIP library
+(koordinator_amd.cluster), so both sides see byte-identical inputs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from koordinator_amd import abi
+from koordinator_amd.cluster import NodeState, NodeTable, PodTable, QuotaTable
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "koord_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.ko_create.restype = C.c_void_p
+        L.ko_create.argtypes = [C.POINTER(abi.KsConfig), C.POINTER(abi.KsNodeCols), C.c_int64, C.c_int]
+        L.ko_destroy.argtypes = [C.c_void_p]
+        L.ko_load_quotas.argtypes = [C.c_void_p, C.POINTER(abi.KsQuotaCols), C.c_int32]
+        L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
+        L.ko_eval_pod.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
+        L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
+        L.ko_read_quota_used.argtypes = [C.c_void_p, abi.P64]
+        L.ko_least_requested_score.restype = C.c_int64
+        L.ko_least_requested_score.argtypes = [C.c_int64, C.c_int64]
+        L.ko_most_requested_score.restype = C.c_int64
+        L.ko_most_requested_score.argtypes = [C.c_int64, C.c_int64]
+        L.ko_estimated_used.restype = C.c_int64
+        L.ko_estimated_used.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int64]
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    """Sequential one-pod-at-a-time scheduler on the CPU (reduced form)."""
+
+    def __init__(self, cfg: abi.KsConfig, nodes: NodeTable, quotas: QuotaTable | None = None, nthreads: int = 1):
+        self.L = lib()
+        self.cfg = cfg
+        self.n = nodes.n
+        self._cols = nodes.ks()
+        self.h = self.L.ko_create(C.byref(cfg), C.byref(self._cols), nodes.n, int(nthreads))
+        self.nq = 0
+        if quotas is not None:
+            self._q = quotas.ks()
+            self.L.ko_load_quotas(self.h, C.byref(self._q), quotas.q)
+            self.nq = quotas.q
+
+    def close(self):
+        if self.h:
+            self.L.ko_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def schedule(self, pods: PodTable):
+        out = (abi.KsResult * max(pods.n, 1))()
+        cols = pods.ks()
+        self.L.ko_schedule(self.h, C.byref(cols), pods.n, out)
+        arr = np.frombuffer(out, dtype=np.dtype([("node", "<i4"), ("status", "<u4"), ("score", "<i8")]), count=pods.n)
+        return {"node": arr["node"].copy(), "status": arr["status"].copy(), "score": arr["score"].copy()}
+
+    def eval_pod(self, pod: PodTable):
+        reasons = np.zeros(self.n, np.uint32)
+        scores = np.zeros(self.n * abi.KS_NUM_SCORE_PLUGINS, np.int64)
+        total = np.zeros(self.n, np.int64)
+        cols = pod.ks()
+        self.L.ko_eval_pod(self.h, C.byref(cols), reasons.ctypes.data_as(abi.PU32),
+                           scores.ctypes.data_as(abi.P64), total.ctypes.data_as(abi.P64))
+        return reasons, scores.reshape(self.n, abi.KS_NUM_SCORE_PLUGINS), total
+
+    def read_nodes(self) -> NodeState:
+        st = NodeState(self.n)
+        s = st.ks()
+        self.L.ko_read_nodes(self.h, C.byref(s))
+        return st
+
+    def read_quota_used(self) -> np.ndarray:
+        used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)
+        self.L.ko_read_quota_used(self.h, used.ctypes.data_as(abi.P64))
+        return used[: self.nq * abi.KS_QUOTA_DIMS].reshape(self.nq, abi.KS_QUOTA_DIMS)
