@@ -26,8 +26,11 @@
  * Floating point sites keep Go's operation order (compile with
  * -ffp-contract=off, no -ffast-math).  Go math.Round == C round().
  */
+#define _GNU_SOURCE
 #include <math.h>
 #include <pthread.h>
+#include <sched.h>
+#include <time.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -349,11 +352,9 @@ typedef void (*ko_piece_fn)(void *arg, int64_t lo, int64_t hi);
 struct ko_pool {
   int workers;
   pthread_t *th;
-  pthread_mutex_t mu;
-  pthread_cond_t cv_start, cv_done;
-  int64_t generation;
-  int shutdown;
-  int active;
+  atomic_llong generation;
+  atomic_int active;
+  atomic_int shutdown;
   /* current job */
   ko_piece_fn fn;
   void *arg;
@@ -371,31 +372,41 @@ static void run_chunks(ko_pool *pl) {
   }
 }
 
+/* Spin briefly, then yield, then nap: dedicated workers with goroutine-like
+ * dispatch latency (~1 us) while a scheduling loop is running. */
+static void backoff(long *spins) {
+  ++*spins;
+  if (*spins < 4000) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  } else if (*spins < 8000) {
+    sched_yield();
+  } else {
+    struct timespec ts = {0, 50000};
+    nanosleep(&ts, NULL);
+  }
+}
+
 static void *pool_main(void *v) {
   ko_pool *pl = (ko_pool *)v;
-  int64_t seen = 0;
+  long long seen = 0;
   for (;;) {
-    pthread_mutex_lock(&pl->mu);
-    while (pl->generation == seen && !pl->shutdown) pthread_cond_wait(&pl->cv_start, &pl->mu);
-    if (pl->shutdown) {
-      pthread_mutex_unlock(&pl->mu);
-      return NULL;
-    }
-    seen = pl->generation;
-    pthread_mutex_unlock(&pl->mu);
+    long spins = 0;
+    while (atomic_load(&pl->generation) == seen && !atomic_load(&pl->shutdown)) backoff(&spins);
+    if (atomic_load(&pl->shutdown)) return NULL;
+    seen = atomic_load(&pl->generation);
     run_chunks(pl);
-    pthread_mutex_lock(&pl->mu);
-    if (--pl->active == 0) pthread_cond_signal(&pl->cv_done);
-    pthread_mutex_unlock(&pl->mu);
+    atomic_fetch_sub(&pl->active, 1);
   }
 }
 
 static ko_pool *pool_create(int workers) {
   ko_pool *pl = (ko_pool *)calloc(1, sizeof(ko_pool));
   pl->workers = workers;
-  pthread_mutex_init(&pl->mu, NULL);
-  pthread_cond_init(&pl->cv_start, NULL);
-  pthread_cond_init(&pl->cv_done, NULL);
+  atomic_store(&pl->generation, 0);
+  atomic_store(&pl->active, 0);
+  atomic_store(&pl->shutdown, 0);
   if (workers > 1) {
     pl->th = (pthread_t *)calloc((size_t)workers - 1, sizeof(pthread_t));
     for (int i = 0; i < workers - 1; i++) pthread_create(&pl->th[i], NULL, pool_main, pl);
@@ -405,10 +416,7 @@ static ko_pool *pool_create(int workers) {
 
 static void pool_destroy(ko_pool *pl) {
   if (!pl) return;
-  pthread_mutex_lock(&pl->mu);
-  pl->shutdown = 1;
-  pthread_cond_broadcast(&pl->cv_start);
-  pthread_mutex_unlock(&pl->mu);
+  atomic_store(&pl->shutdown, 1);
   for (int i = 0; i < pl->workers - 1; i++) pthread_join(pl->th[i], NULL);
   free(pl->th);
   free(pl);
@@ -434,15 +442,13 @@ static void pool_until(ko_pool *pl, int64_t pieces, ko_piece_fn fn, void *arg) {
     run_chunks(pl);
     return;
   }
-  pthread_mutex_lock(&pl->mu);
-  pl->active = pl->workers - 1;
-  pl->generation++;
-  pthread_cond_broadcast(&pl->cv_start);
-  pthread_mutex_unlock(&pl->mu);
+  atomic_store(&pl->active, pl->workers - 1);
+  atomic_fetch_add(&pl->generation, 1);
   run_chunks(pl); /* the calling goroutine participates */
-  pthread_mutex_lock(&pl->mu);
-  while (pl->active > 0) pthread_cond_wait(&pl->cv_done, &pl->mu);
-  pthread_mutex_unlock(&pl->mu);
+  long spins = 0;
+  while (atomic_load(&pl->active) > 0) {
+    if (++spins > 100000) sched_yield();
+  }
 }
 
 /* ------------------------------------------------------------------ */
