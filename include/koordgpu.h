@@ -258,6 +258,8 @@ typedef struct ks_stats {
   double total_ms;         /* wall time of the last call on the device stream */
   int64_t sweep_launches;
   int64_t sweep_bytes;     /* algorithmic bytes one sweep launch reads/writes */
+  int64_t slot_misses;     /* commits whose node row was not prefetched (one extra HBM round trip) */
+  int64_t diag[8];         /* diagnostic build only (KS_COMMIT_STAMPS): commit-phase cycle sums */
 } ks_stats;
 
 typedef struct ks_ctx ks_ctx;

@@ -217,6 +217,8 @@ class KsStats(C.Structure):
         ("total_ms", C.c_double),
         ("sweep_launches", C.c_int64),
         ("sweep_bytes", C.c_int64),
+        ("slot_misses", C.c_int64),
+        ("diag", C.c_int64 * 8),
     ]
 
 

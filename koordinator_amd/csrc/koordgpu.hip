@@ -120,7 +120,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
 }
 
 // ------------------------------------------------------------------------------------------
-// sweep: chunk maxima
+// sweep: per (pod, 64-node chunk) best and runner-up
 // ------------------------------------------------------------------------------------------
 
 struct SweepArgs {
@@ -128,7 +128,7 @@ struct SweepArgs {
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
-  uint32_t* __restrict__ out;  // [nchunks][64]: lane p = best local key of pod p in the chunk
+  uint2* __restrict__ out;  // [nchunks][64]: lane p = {best, runner-up} local keys of pod p
   int64_t n, nchunks;
   int32_t total_pods, batch, ppw;
 };
@@ -151,34 +151,36 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     NodeReg<NSC> r;
     load_node<NSC>(a.d, node, node < a.n, r);
     const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
-    uint32_t res = 0;
+    uint32_t best = 0, second = 0;
     for (int32_t p = p0; p < p1; ++p) {
       const PodRec pod = a.pods[cursor + p];
       const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
       const uint32_t key = o.reasons ? 0u : (((uint32_t)(o.total + 1) << 6) | (uint32_t)(63 - lane));
-      const uint32_t m = wave_max_u32(key);
-      res = (lane == p) ? m : res;
+      const uint32_t m1 = wave_max_u32(key);
+      const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
+      best = (lane == p) ? m1 : best;
+      second = (lane == p) ? m2 : second;
     }
-    if (lane >= p0 && lane < p1) a.out[c * 64 + lane] = res;
+    if (lane >= p0 && lane < p1) a.out[c * 64 + lane] = make_uint2(best, second);
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// select: top-K chunks per pod
+// select: top-K chunks per pod (by chunk best)
 // ------------------------------------------------------------------------------------------
 
 struct SelectArgs {
-  const uint32_t* __restrict__ in;  // sweep output
+  const uint2* __restrict__ in;  // sweep output
   const int32_t* __restrict__ cursor;
-  uint32_t* cand_chunk;             // [64][K]
-  uint64_t* cand_key;               // [64][K]
-  uint64_t* cand_bound;             // [64]
-  int32_t* cand_count;              // [64]
+  uint32_t* cand_chunk;          // [64][K]
+  uint2* cand_t;                 // [64][K] {best, runner-up} local keys
+  uint64_t* cand_bound;          // [64]
+  int32_t* cand_count;           // [64]
   int64_t nchunks;
   int32_t total_pods, batch, k;
 };
 
-__device__ __forceinline__ uint64_t entry_gkey(uint32_t loc, int64_t chunk) {
+__device__ __forceinline__ uint64_t local_gkey(uint32_t loc, int64_t chunk) {
   if (loc == 0) return 0;
   const int64_t node = chunk * 64 + (63 - (int64_t)(loc & 63u));
   return ((uint64_t)(loc >> 6) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)node);
@@ -192,11 +194,10 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   const int32_t p = blockIdx.x;
   if (p >= np) return;
   const int32_t K = a.k;
-  // pass 1: feasible count and max score
   int32_t cnt = 0;
   uint32_t hmax = 0;
   for (int64_t e = lane; e < a.nchunks; e += 64) {
-    const uint32_t h = a.in[e * 64 + p] >> 6;
+    const uint32_t h = a.in[e * 64 + p].x >> 6;
     cnt += h != 0;
     hmax = h > hmax ? h : hmax;
   }
@@ -204,32 +205,31 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   hmax = wave_max_u32(hmax);
   uint32_t t = 1;  // admit h >= t
   int32_t need_eq = 0x7fffffff;
-  bool exhaustive = cnt <= K;
+  const bool exhaustive = cnt <= K;
   if (!exhaustive) {
-    // largest t with count(h >= t) >= K
-    uint32_t lo = 1, hi = hmax;
+    uint32_t lo = 1, hi = hmax;  // largest t with count(h >= t) >= K
     while (lo < hi) {
       const uint32_t mid = lo + (hi - lo + 1) / 2;
       int32_t c = 0;
-      for (int64_t e = lane; e < a.nchunks; e += 64) c += (a.in[e * 64 + p] >> 6) >= mid;
+      for (int64_t e = lane; e < a.nchunks; e += 64) c += (a.in[e * 64 + p].x >> 6) >= mid;
       c = wave_sum_i32(c);
       if (c >= K) lo = mid;
       else hi = mid - 1;
     }
     t = lo;
     int32_t gt = 0;
-    for (int64_t e = lane; e < a.nchunks; e += 64) gt += (a.in[e * 64 + p] >> 6) > t;
+    for (int64_t e = lane; e < a.nchunks; e += 64) gt += (a.in[e * 64 + p].x >> 6) > t;
     gt = wave_sum_i32(gt);
     need_eq = K - gt;
   }
-  // compaction: every h > t, plus the first need_eq entries (chunk order) with h == t
+  // every h > t, plus the first need_eq entries (chunk order) with h == t
   int32_t base = 0, eq_taken = 0;
   uint64_t bound = 0;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   for (int64_t e0 = 0; e0 < a.nchunks; e0 += 64) {
     const int64_t e = e0 + lane;
-    const uint32_t loc = e < a.nchunks ? a.in[e * 64 + p] : 0u;
-    const uint32_t h = loc >> 6;
+    const uint2 loc = e < a.nchunks ? a.in[e * 64 + p] : make_uint2(0u, 0u);
+    const uint32_t h = loc.x >> 6;
     const bool is_gt = h > t;
     const bool is_eq = (h == t) && h != 0;
     const uint64_t beq = __ballot(is_eq);
@@ -239,10 +239,9 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
     const uint64_t btake = __ballot(take);
     if (take) {
       const int32_t pos = base + __popcll(btake & lanemask_lt);
-      const uint64_t key = entry_gkey(loc, e);
       a.cand_chunk[p * K + pos] = (uint32_t)e;
-      a.cand_key[p * K + pos] = key;
-      if (take_eq && eq_rank == need_eq - 1) bound = key;
+      a.cand_t[p * K + pos] = loc;
+      if (take_eq && eq_rank == need_eq - 1) bound = local_gkey(loc.x, e);
     }
     base += __popcll(btake);
     eq_taken += __popcll(beq);
@@ -255,8 +254,10 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// commit: sequential exact selection + Reserve, one wave
+// commit: sequential exact selection + Reserve, one wave, pass state resident in LDS
 // ------------------------------------------------------------------------------------------
+
+constexpr int kQuotaLdsRows = 128;  // quota tables up to this size are cached in LDS for the pass
 
 struct CommitArgs {
   DevNodes d;
@@ -266,144 +267,262 @@ struct CommitArgs {
   DevQuotas q;
   int32_t* cursor;
   const uint32_t* __restrict__ cand_chunk;
-  const uint64_t* __restrict__ cand_key;
+  const uint2* __restrict__ cand_t;
   const uint64_t* __restrict__ cand_bound;
   const int32_t* __restrict__ cand_count;
   ks_result* results;
-  unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans
+  unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot global loads
   int64_t n, nchunks;
-  int32_t total_pods, batch, k, nwords;
+  int32_t total_pods, batch, k;
 };
 
-struct CommitSmem {
-  MutState slots[kMaxBatch];
-  uint8_t dmap[kMaxBatch][64];  // dirty entry -> lane -> slot (0xFF none)
+// LDS image of one pass (fixed part); the candidate arrays, the optional quota cache and the
+// chunk -> dirty-entry map follow it (carved by CommitLayout, same arithmetic on host and device).
+template <int NSC>
+struct __attribute__((aligned(16))) CommitLds {
+  NodeReg<NSC> slot[kMaxBatch];   // rows of nodes touched in this pass (authoritative)
+  NodeReg<NSC> pred[2][kMaxBatch];  // snapshot rows of each pod's two best candidate nodes
+  PodRec pods[kMaxBatch];
+  uint64_t cand_bound[kMaxBatch];
+  int32_t cand_count[kMaxBatch];
+  int32_t slot_node[kMaxBatch];
+  int32_t pred_node[2][kMaxBatch];
+  uint32_t pq_mask[kMaxBatch];
+  int64_t pq_req[kMaxBatch][KS_QUOTA_DIMS];
+  uint8_t dmap[kMaxBatch][64];    // dirty entry -> lane in chunk -> slot (0xFF none)
+};
+
+struct QuotaRowsLds {
+  int32_t parent[kQuotaLdsRows];
+  uint32_t limit_mask[kQuotaLdsRows], min_mask[kQuotaLdsRows];
+  int64_t limit[kQuotaLdsRows * KS_QUOTA_DIMS], used[kQuotaLdsRows * KS_QUOTA_DIMS];
+  int64_t min[kQuotaLdsRows * KS_QUOTA_DIMS], npused[kQuotaLdsRows * KS_QUOTA_DIMS];
+};
+
+struct CommitLayout {
+  size_t cand_t, cand_chunk, quota, dentry, total;
 };
 
 template <int NSC>
-__device__ __forceinline__ uint64_t rescan_chunk(const CommitArgs& a, const CommitSmem& sm, const PodRec& pod,
+__host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc) {
+  CommitLayout L;
+  size_t o = (sizeof(CommitLds<NSC>) + 15) / 16 * 16;
+  L.cand_t = o;
+  o += (size_t)kMaxBatch * k * sizeof(uint2);
+  L.cand_chunk = o;
+  o += ((size_t)kMaxBatch * k * 4 + 15) / 16 * 16;
+  L.quota = o;
+  if (qc) o += (sizeof(QuotaRowsLds) + 15) / 16 * 16;
+  L.dentry = o;
+  o += (size_t)(nchunks + 15) / 16 * 16;
+  L.total = o;
+  return L;
+}
+
+template <int NSC>
+__device__ __forceinline__ uint64_t rescan_chunk(const CommitArgs& a, const CommitLds<NSC>& sm, const PodRec& pod,
                                                  int64_t chunk, int32_t dentry) {
   const int lane = threadIdx.x;
   const int64_t node = chunk * 64 + lane;
   NodeReg<NSC> r;
-  load_node<NSC>(a.d, node, node < a.n, r);
   const uint8_t s = sm.dmap[dentry][lane];
-  if (s != 0xFF) apply_mut<NSC>(r, sm.slots[s]);
+  if (s != 0xFF) r = sm.slot[s];
+  else load_node<NSC>(a.d, node, node < a.n, r);
   const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
-  const uint64_t key = o.reasons ? 0ull : gkey(o.total, node);
-  return wave_max_u64(key);
+  return wave_max_u64(o.reasons ? 0ull : gkey(o.total, node));
 }
 
-template <int NSC>
-__device__ __forceinline__ uint64_t rescore_slots(const CommitArgs& a, const CommitSmem& sm, const PodRec& pod,
-                                                  int32_t nslots) {
+// ElasticQuota PreFilter (plugin.go:210-255, plugin_helper.go:281-319); lane d checks dimension d.
+// Q is either the LDS cache (QuotaRowsLds*) or the global table; templated so each path keeps
+// its own address space (ds_* vs global_* loads).
+template <typename P32, typename PU32, typename P64>
+__device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU32 min_mask, P64 limit, P64 used,
+                                                P64 minv, P64 npused, bool check_parent, int32_t quota,
+                                                uint32_t flags, uint32_t pmask, int64_t req) {
   const int lane = threadIdx.x;
-  uint64_t key = 0;
-  if (lane < nslots) {
-    const int64_t node = sm.slots[lane].node;
-    NodeReg<NSC> r;
-    load_node<NSC>(a.d, node, 1, r);
-    apply_mut<NSC>(r, sm.slots[lane]);
-    const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
-    key = o.reasons ? 0ull : gkey(o.total, node);
-  }
-  return wave_max_u64(key);
-}
-
-// ElasticQuota PreFilter admission for one pod (plugin.go:210-255, plugin_helper.go:281-319);
-// lane d checks resource dimension d.
-__device__ __forceinline__ uint32_t quota_admit(const CommitArgs& a, int32_t gp, int32_t quota, uint32_t flags) {
-  const int lane = threadIdx.x;
-  const uint32_t pmask = a.pq.mask[gp];
-  const int64_t req = lane < KS_QUOTA_DIMS ? a.pq.req[lane < KS_QUOTA_DIMS ? lane : 0][gp] : 0;
   const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
+  const int ld = lane < KS_QUOTA_DIMS ? lane : 0;
   {
-    const int64_t* row = a.q.used + (int64_t)quota * KS_QUOTA_DIMS;
-    const bool lim = in_pod && ((a.q.limit_mask[quota] >> lane) & 1u);
-    const bool bad = lim && (req + row[lane] > a.q.limit[(int64_t)quota * KS_QUOTA_DIMS + lane]);
+    const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
+    const bool bad = in_pod && ((limit_mask[quota] >> lane) & 1u) && (req + used[o] > limit[o]);
     if (__ballot(bad)) return KS_S_QUOTA;
   }
   if (flags & KS_POD_NONPREEMPTIBLE) {
-    const bool mn = in_pod && ((a.q.min_mask[quota] >> lane) & 1u);
-    const bool bad = mn && (req + a.q.npused[(int64_t)quota * KS_QUOTA_DIMS + lane] >
-                            a.q.min[(int64_t)quota * KS_QUOTA_DIMS + lane]);
+    const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
+    const bool bad = in_pod && ((min_mask[quota] >> lane) & 1u) && (req + npused[o] > minv[o]);
     if (__ballot(bad)) return KS_S_QUOTA_NONPREEMPTIBLE;
   }
-  if (a.c.quota_parent) {
-    for (int32_t cur = quota; cur >= 0; cur = a.q.parent[cur]) {
-      const bool lim = in_pod && ((a.q.limit_mask[cur] >> lane) & 1u);
-      const bool bad = lim && (req + a.q.used[(int64_t)cur * KS_QUOTA_DIMS + lane] >
-                               a.q.limit[(int64_t)cur * KS_QUOTA_DIMS + lane]);
+  if (check_parent) {
+    for (int32_t cur = quota; cur >= 0; cur = parent[cur]) {
+      const size_t o = (size_t)cur * KS_QUOTA_DIMS + ld;
+      const bool bad = in_pod && ((limit_mask[cur] >> lane) & 1u) && (req + used[o] > limit[o]);
       if (__ballot(bad)) return KS_S_QUOTA | KS_S_QUOTA_PARENT;
     }
   }
   return 0;
 }
 
-__device__ __forceinline__ void quota_reserve(const CommitArgs& a, int32_t gp, int32_t quota, uint32_t flags) {
+// Copy a 16-byte aligned LDS struct with one 16-byte move per lane.
+template <typename T>
+__device__ __forceinline__ void lds_copy(T& dst, const T& src) {
+  static_assert(sizeof(T) % 16 == 0, "LDS row copy needs 16-byte multiples");
+  constexpr int n16 = (int)(sizeof(T) / 16);
   const int lane = threadIdx.x;
-  if (lane >= KS_QUOTA_DIMS) return;
-  const uint32_t pmask = a.pq.mask[gp];
-  if (!((pmask >> lane) & 1u)) return;
-  const int64_t req = a.pq.req[lane][gp];
-  for (int32_t cur = quota; cur >= 0; cur = a.q.parent[cur]) {
-    a.q.used[(int64_t)cur * KS_QUOTA_DIMS + lane] += req;
-    if (flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(int64_t)cur * KS_QUOTA_DIMS + lane] += req;
-  }
+  if (lane < n16) reinterpret_cast<uint4*>(&dst)[lane] = reinterpret_cast<const uint4*>(&src)[lane];
 }
 
-template <int NSC>
+template <int NSC, bool QC>
 __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  CommitSmem& sm = *reinterpret_cast<CommitSmem*>(smem_raw);
-  uint32_t* dirty_bits = reinterpret_cast<uint32_t*>(smem_raw + sizeof(CommitSmem));
+  CommitLds<NSC>& sm = *reinterpret_cast<CommitLds<NSC>*>(smem_raw);
+  const int32_t K = a.k;
+  const CommitLayout lay = commit_layout<NSC>(K, a.nchunks, QC);
+  uint2* cand_t = reinterpret_cast<uint2*>(smem_raw + lay.cand_t);
+  uint32_t* cand_chunk = reinterpret_cast<uint32_t*>(smem_raw + lay.cand_chunk);
+  QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
+  uint8_t* dentry_of_chunk = smem_raw + lay.dentry;
   const int lane = threadIdx.x;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor0 >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor0);
-  const int32_t K = a.k;
-  for (int32_t w = lane; w < a.nwords; w += 64) dirty_bits[w] = 0;
+#ifdef KS_COMMIT_STAMPS
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tlast = __builtin_amdgcn_s_memtime();
+#define KS_STAMP(i)                                    \
+  do {                                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - tlast;                               \
+    tlast = t_;                                        \
+  } while (0)
+#else
+#define KS_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
+  // ---- prefetch the whole pass into LDS (one burst of independent loads) ----
+  if (lane < np) {
+    sm.pods[lane] = a.pods[cursor0 + lane];
+    sm.cand_count[lane] = a.cand_count[lane];
+    sm.cand_bound[lane] = a.cand_bound[lane];
+    const int32_t gp = cursor0 + lane;
+    sm.pq_mask[lane] = a.pq.mask[gp];
+#pragma unroll
+    for (int d = 0; d < KS_QUOTA_DIMS; ++d) sm.pq_req[lane][d] = a.pq.req[d][gp];
+  }
+  for (int32_t i = lane; i < np * K; i += 64) {
+    cand_chunk[i] = a.cand_chunk[i];
+    cand_t[i] = a.cand_t[i];
+  }
+  for (int64_t c = lane; c < a.nchunks; c += 64) dentry_of_chunk[c] = 0xFF;
+  if (QC) {
+    for (int32_t r = lane; r < a.q.q; r += 64) {
+      qlds->parent[r] = a.q.parent[r];
+      qlds->limit_mask[r] = a.q.limit_mask[r];
+      qlds->min_mask[r] = a.q.min_mask[r];
+    }
+    for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
+      qlds->limit[i] = a.q.limit[i];
+      qlds->used[i] = a.q.used[i];
+      qlds->min[i] = a.q.min[i];
+      qlds->npused[i] = a.q.npused[i];
+    }
+  }
   __syncthreads();
+  // predicted winners of each pod = its two best snapshot candidates; prefetch those rows
+  if (lane < np) {
+    const int32_t cnt = sm.cand_count[lane];
+    uint64_t b0 = 0, b1 = 0;
+    for (int32_t k = 0; k < cnt; ++k) {
+      const uint64_t g = local_gkey(cand_t[lane * K + k].x, cand_chunk[lane * K + k]);
+      if (g > b0) {
+        b1 = b0;
+        b0 = g;
+      } else if (g > b1) {
+        b1 = g;
+      }
+    }
+    const int64_t n0 = b0 ? gkey_node(b0) : -1, n1 = b1 ? gkey_node(b1) : -1;
+    sm.pred_node[0][lane] = (int32_t)n0;
+    sm.pred_node[1][lane] = (int32_t)n1;
+    if (n0 >= 0) load_node<NSC>(a.d, n0, 1, sm.pred[0][lane]);
+    if (n1 >= 0) load_node<NSC>(a.d, n1, 1, sm.pred[1][lane]);
+  }
+  __syncthreads();
+  KS_STAMP(0);
 
   int32_t nslots = 0, ndirty = 0;
-  int32_t dchunk = -1;  // lane d: chunk id of dirty entry d
   int32_t processed = np;
-  unsigned long long rescans = 0;
+  unsigned long long rescans = 0, misses = 0;
   for (int32_t j = 0; j < np; ++j) {
     const int32_t gp = cursor0 + j;
-    const PodRec pod = a.pods[gp];
-    if (a.c.quota_enable && pod.quota >= 0) {
-      const uint32_t st = quota_admit(a, gp, pod.quota, pod.flags);
+    const PodRec pod = sm.pods[j];
+    const bool has_quota = a.c.quota_enable && pod.quota >= 0;
+    const uint32_t pmask = sm.pq_mask[j];
+    const int64_t qreq = sm.pq_req[j][lane & (KS_QUOTA_DIMS - 1)];
+    if (has_quota) {
+      const uint32_t st =
+          QC ? quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
+                           qlds->npused, a.c.quota_parent, pod.quota, pod.flags, pmask, qreq)
+             : quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
+                           a.c.quota_parent, pod.quota, pod.flags, pmask, qreq);
       if (st) {
         if (lane == 0) a.results[gp] = ks_result{-1, st, 0};
+        KS_STAMP(1);
         continue;
       }
     }
-    const int32_t cnt = a.cand_count[j];
+    KS_STAMP(1);
+    // nodes touched earlier in this pass: exact current keys from their LDS rows
+    uint64_t best_mod = 0;
+    if (nslots) {
+      uint64_t key = 0;
+      if (lane < nslots) {
+        const NodeReg<NSC> r = sm.slot[lane];
+        const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
+        key = o.reasons ? 0ull : gkey(o.total, sm.slot_node[lane]);
+      }
+      best_mod = wave_max_u64(key);
+    }
+    KS_STAMP(2);
+    // untouched nodes: chunk best / runner-up from the snapshot
+    const int32_t cnt = sm.cand_count[j];
     const bool valid = lane < cnt;
-    const uint32_t chunk = valid ? a.cand_chunk[j * K + lane] : 0u;
-    const uint64_t key = valid ? a.cand_key[j * K + lane] : 0ull;
-    const bool dirty = valid && ((dirty_bits[chunk >> 5] >> (chunk & 31u)) & 1u);
-    uint64_t best = wave_max_u64(valid && !dirty ? key : 0ull);
-    const bool any_clean = best != 0;
-    uint64_t need = __ballot(dirty && key > best);
+    const uint32_t chunk = valid ? cand_chunk[j * K + lane] : 0u;
+    const uint2 t = valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
+    const uint32_t de = valid ? dentry_of_chunk[chunk] : 0xFFu;
+    uint64_t u = local_gkey(t.x, chunk), ub = 0;
+    bool exact = valid;
+    if (valid && de != 0xFFu) {
+      if (sm.dmap[de][63 - (t.x & 63u)] != 0xFF) {           // best node touched
+        if (t.y == 0) {
+          u = 0;                                             // no other feasible node in the chunk
+        } else if (sm.dmap[de][63 - (t.y & 63u)] == 0xFF) {
+          u = local_gkey(t.y, chunk);                        // runner-up untouched: exact
+        } else {
+          exact = false;                                     // both touched: < runner-up, unknown
+          ub = local_gkey(t.y, chunk);
+          u = 0;
+        }
+      }
+    }
+    uint64_t best = wave_max_u64(exact ? u : 0ull);
+    uint64_t need = __ballot(!exact && valid && ub > best);
     while (need) {
-      const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? key : 0ull);
-      const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && key == kmax)) - 1;
+      const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? ub : 0ull);
+      const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && ub == kmax)) - 1;
       const int64_t c = (int64_t)(uint32_t)__shfl((int)chunk, sel, 64);
-      const int32_t d = __ffsll((long long)__ballot(lane < ndirty && dchunk == (int32_t)c)) - 1;
+      const int32_t d = (int32_t)(uint32_t)__shfl((int)de, sel, 64);
       const uint64_t v = rescan_chunk<NSC>(a, sm, pod, c, d);
       ++rescans;
-      best = v > best ? v : best;
+      best = umax64(best, v);
       need &= ~(1ull << sel);
-      need &= __ballot(key > best);
+      need &= __ballot(ub > best);
     }
-    if (!a.c.monotone && nslots) {
-      const uint64_t v = rescore_slots<NSC>(a, sm, pod, nslots);
-      best = v > best ? v : best;
-    }
-    if (!any_clean && cnt == K && best < a.cand_bound[j]) {
-      processed = j;  // an untouched chunk outside the list may win: re-sweep from pod j
+    best = umax64(best, best_mod);
+    KS_STAMP(3);
+    if (cnt == K && best < sm.cand_bound[j]) {
+      processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep
       break;
     }
     if (best == 0) {
@@ -414,82 +533,89 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
     const int64_t score = gkey_score(best);
     const int32_t c = (int32_t)(node >> 6);
     const int ln = (int)(node & 63);
-    int32_t d = __ffsll((long long)__ballot(lane < ndirty && dchunk == c)) - 1;
-    if (d < 0) {
+    // LDS operations of one wave execute in order, so no barrier is needed between the
+    // lane-0 / cooperative writes below and the next pod's reads.
+    int32_t d = dentry_of_chunk[c];
+    if (d == 0xFF) {
       d = ndirty++;
-      if (lane == d) dchunk = c;
       sm.dmap[d][lane] = 0xFF;
-      if (lane == 0) dirty_bits[c >> 5] |= 1u << (c & 31);
+      if (lane == 0) dentry_of_chunk[c] = (uint8_t)d;
     }
-    __syncthreads();
     int32_t s = sm.dmap[d][ln];
     if (s == 0xFF) {
       s = nslots++;
+      if (sm.pred_node[0][j] == node) {
+        lds_copy(sm.slot[s], sm.pred[0][j]);
+        asm volatile("" ::: "memory");
+      } else if (sm.pred_node[1][j] == node) {
+        lds_copy(sm.slot[s], sm.pred[1][j]);
+        asm volatile("" ::: "memory");
+      } else {
+        ++misses;
+        if (lane == 0) load_node<NSC>(a.d, node, 1, sm.slot[s]);
+      }
       if (lane == 0) {
-        MutState m;
-        m.req_cpu = a.d.req_cpu[node];
-        m.req_mem = a.d.req_mem[node];
-        m.req_eph = a.d.req_eph[node];
-        m.nz_cpu = a.d.nz_cpu[node];
-        m.nz_mem = a.d.nz_mem[node];
-#pragma unroll
-        for (int k = 0; k < KS_MAX_SCALARS; ++k) m.req_sc[k] = k < NSC ? a.d.req_sc[k][node] : 0;
-        m.term_cpu = a.d.la_term_cpu[node];
-        m.term_mem = a.d.la_term_mem[node];
-        m.pterm_cpu = a.d.la_pterm_cpu[node];
-        m.pterm_mem = a.d.la_pterm_mem[node];
-        m.pod_count = a.d.pod_count[node];
-        m.node = (int32_t)node;
-        sm.slots[s] = m;
+        sm.slot_node[s] = (int32_t)node;
         sm.dmap[d][ln] = (uint8_t)s;
       }
     }
+    asm volatile("" ::: "memory");
     if (lane == 0) {
-      // NodeInfo.AddPod + podAssignCache.assign (load_aware.go:260, pod_assign_cache.go:53)
-      MutState& m = sm.slots[s];
-      m.req_cpu += pod.cpu;
-      m.req_mem += pod.mem;
-      m.req_eph += pod.eph;
-      m.nz_cpu += pod.nzcpu;
-      m.nz_mem += pod.nzmem;
-#pragma unroll
-      for (int k = 0; k < NSC; ++k) m.req_sc[k] += pod.sc[k];
-      m.pod_count += 1;
-      m.term_cpu += pod.est_cpu;
-      m.term_mem += pod.est_mem;
-      if (pod.flags & KS_POD_PROD) {
-        m.pterm_cpu += pod.est_cpu;
-        m.pterm_mem += pod.est_mem;
-      }
+      reserve_row<NSC>(sm.slot[s], pod);
       a.results[gp] = ks_result{(int32_t)node, KS_S_SCHEDULED, score};
     }
-    if (a.c.quota_enable && pod.quota >= 0) quota_reserve(a, gp, pod.quota, pod.flags);
-    __syncthreads();
+    if (has_quota && lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u)) {
+      // updatePodUsedNoLock -> updateGroupDeltaUsedNoLock (group_quota_manager.go:620-655)
+      if (QC) {
+        for (int32_t cur = pod.quota; cur >= 0; cur = qlds->parent[cur]) {
+          qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+          if (pod.flags & KS_POD_NONPREEMPTIBLE) qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+        }
+      } else {
+        for (int32_t cur = pod.quota; cur >= 0; cur = a.q.parent[cur]) {
+          a.q.used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+          if (pod.flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+        }
+      }
+    }
+    KS_STAMP(4);
   }
   __syncthreads();
-  // write the touched nodes back
+  KS_STAMP(5);
+  // ---- write back touched nodes and quota usage ----
   if (lane < nslots) {
-    const MutState m = sm.slots[lane];
-    const int64_t node = m.node;
-    a.d.req_cpu[node] = m.req_cpu;
-    a.d.req_mem[node] = m.req_mem;
-    a.d.req_eph[node] = m.req_eph;
-    a.d.nz_cpu[node] = m.nz_cpu;
-    a.d.nz_mem[node] = m.nz_mem;
+    const NodeReg<NSC> r = sm.slot[lane];
+    const int64_t node = sm.slot_node[lane];
+    a.d.req_cpu[node] = r.alloc_cpu - r.free_cpu;
+    a.d.req_mem[node] = r.alloc_mem - r.free_mem;
+    a.d.req_eph[node] = r.req_eph;
+    a.d.nz_cpu[node] = r.nz_cpu;
+    a.d.nz_mem[node] = r.nz_mem;
 #pragma unroll
-    for (int k = 0; k < NSC; ++k) a.d.req_sc[k][node] = m.req_sc[k];
-    a.d.pod_count[node] = m.pod_count;
-    a.d.la_term_cpu[node] = m.term_cpu;
-    a.d.la_term_mem[node] = m.term_mem;
-    a.d.la_pterm_cpu[node] = m.pterm_cpu;
-    a.d.la_pterm_mem[node] = m.pterm_mem;
+    for (int k = 0; k < NSC; ++k) a.d.req_sc[k][node] = r.req_sc[k];
+    a.d.pod_count[node] = r.pod_count;
+    a.d.la_term_cpu[node] = r.term_cpu;
+    a.d.la_term_mem[node] = r.term_mem;
+    a.d.la_pterm_cpu[node] = r.pterm_cpu;
+    a.d.la_pterm_mem[node] = r.pterm_mem;
+  }
+  if (QC) {
+    for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
+      a.q.used[i] = qlds->used[i];
+      a.q.npused[i] = qlds->npused[i];
+    }
   }
   if (lane == 0) {
     *a.cursor = cursor0 + processed;
     atomicAdd(&a.counters[0], 1ull);
     if (processed < np) atomicAdd(&a.counters[1], 1ull);
     atomicAdd(&a.counters[2], rescans);
+    atomicAdd(&a.counters[3], misses);
+#ifdef KS_COMMIT_STAMPS
+    for (int i = 0; i < 6; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
+#endif
   }
+#undef KS_STAMP
 }
 
 // ------------------------------------------------------------------------------------------
@@ -568,9 +694,9 @@ struct ks_ctx {
   DevPodCols pstage{};
   ks_result* results = nullptr;
   // pass scratch
-  uint32_t* sweep_out = nullptr;
+  uint2* sweep_out = nullptr;
   uint32_t* cand_chunk = nullptr;
-  uint64_t* cand_key = nullptr;
+  uint2* cand_t = nullptr;
   uint64_t* cand_bound = nullptr;
   int32_t* cand_count = nullptr;
   int32_t* cursor = nullptr;
@@ -687,14 +813,14 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   if (dev_alloc(ctx, &p, cand_bytes * 4) != KS_OK) goto fail;
   ctx->cand_chunk = (uint32_t*)p;
   if (dev_alloc(ctx, &p, cand_bytes * 8) != KS_OK) goto fail;
-  ctx->cand_key = (uint64_t*)p;
+  ctx->cand_t = (uint2*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_bound = (uint64_t*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_count = (int32_t*)p;
   if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
   ctx->cursor = (int32_t*)p;
-  if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, 256) != KS_OK) goto fail;
   ctx->counters = (unsigned long long*)p;
   if (dev_alloc(ctx, &p, sizeof(PodRec)) != KS_OK) goto fail;
   ctx->dbg_pod = (PodRec*)p;
@@ -716,7 +842,7 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->pod_blob; dev_free(p);
   p = ctx->sweep_out; dev_free(p);
   p = ctx->cand_chunk; dev_free(p);
-  p = ctx->cand_key; dev_free(p);
+  p = ctx->cand_t; dev_free(p);
   p = ctx->cand_bound; dev_free(p);
   p = ctx->cand_count; dev_free(p);
   p = ctx->cursor; dev_free(p);
@@ -851,8 +977,12 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (ctx->nchunks == 0) ctx->nchunks = 1;
   ctx->npad = ctx->nchunks * 64;
   int nsc = 0;
-  for (int k = 0; k < KS_MAX_SCALARS; ++k)
-    if (nodes->alloc_scalar[k] || ctx->cfg.fit.weight_scalar[k]) nsc = k + 1;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) {
+    bool used = ctx->cfg.fit.weight_scalar[k] != 0;
+    for (int64_t i = 0; !used && nodes->alloc_scalar[k] && i < n; ++i) used = nodes->alloc_scalar[k][i] != 0;
+    for (int64_t i = 0; !used && nodes->req_scalar[k] && i < n; ++i) used = nodes->req_scalar[k][i] != 0;
+    if (used) nsc = k + 1;
+  }
   ctx->nsc = nsc <= 0 ? 0 : (nsc <= 2 ? 2 : 4);
   ctx->kc = make_cfg(ctx->cfg, ctx->nsc);
   build_col_table(ctx);
@@ -872,8 +1002,8 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
       HIPCHK(ctx, hipMemcpyAsync(base, src[i], (size_t)n * ctx->cols[i].width, hipMemcpyHostToDevice, ctx->stream));
     base += (size_t)ctx->npad * ctx->cols[i].width;
   }
-  if (dev_alloc(ctx, &p, (size_t)ctx->nchunks * 64 * 4) != KS_OK) return KS_ENOMEM;
-  ctx->sweep_out = (uint32_t*)p;
+  if (dev_alloc(ctx, &p, (size_t)ctx->nchunks * 64 * 8) != KS_OK) return KS_ENOMEM;
+  ctx->sweep_out = (uint2*)p;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
@@ -1122,7 +1252,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   se.in = ctx->sweep_out;
   se.cursor = ctx->cursor;
   se.cand_chunk = ctx->cand_chunk;
-  se.cand_key = ctx->cand_key;
+  se.cand_t = ctx->cand_t;
   se.cand_bound = ctx->cand_bound;
   se.cand_count = ctx->cand_count;
   se.nchunks = ctx->nchunks;
@@ -1140,7 +1270,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.q = ctx->q;
   ca.cursor = ctx->cursor;
   ca.cand_chunk = ctx->cand_chunk;
-  ca.cand_key = ctx->cand_key;
+  ca.cand_t = ctx->cand_t;
   ca.cand_bound = ctx->cand_bound;
   ca.cand_count = ctx->cand_count;
   ca.results = ctx->results;
@@ -1150,10 +1280,13 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.total_pods = ctx->np;
   ca.batch = ctx->batch;
   ca.k = ctx->k;
-  ca.nwords = (int32_t)((ctx->nchunks + 31) / 32);
-  const size_t smem = sizeof(CommitSmem) + (size_t)ca.nwords * 4;
+  const bool qcache = ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows;
+  const size_t smem = commit_layout<NSC>(ctx->k, ctx->nchunks, qcache).total;
   rec(2);
-  hipLaunchKernelGGL(commit_kernel<NSC>, dim3(1), dim3(64), smem, ctx->stream, ca);
+  if (qcache)
+    hipLaunchKernelGGL((commit_kernel<NSC, true>), dim3(1), dim3(64), smem, ctx->stream, ca);
+  else
+    hipLaunchKernelGGL((commit_kernel<NSC, false>), dim3(1), dim3(64), smem, ctx->stream, ca);
   rec(2);
 }
 
@@ -1163,8 +1296,26 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   ctx->stats = ks_stats{};
   const int32_t np = ctx->np;
   if (np == 0) return KS_OK;
-  const size_t smem = sizeof(CommitSmem) + (size_t)((ctx->nchunks + 31) / 32) * 4;
-  if (smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld)", (long long)ctx->n);
+  {
+    const bool qcache = ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows;
+    size_t smem = 0;
+    hipError_t e = hipSuccess;
+    auto setattr = [&](const void* fn, size_t bytes) {
+      if (e == hipSuccess) e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    };
+    switch (ctx->nsc) {
+      case 0: smem = commit_layout<0>(ctx->k, ctx->nchunks, qcache).total; break;
+      case 2: smem = commit_layout<2>(ctx->k, ctx->nchunks, qcache).total; break;
+      default: smem = commit_layout<4>(ctx->k, ctx->nchunks, qcache).total; break;
+    }
+    if (smem <= 160 * 1024) {
+      if (ctx->nsc == 0) qcache ? setattr((const void*)commit_kernel<0, true>, smem) : setattr((const void*)commit_kernel<0, false>, smem);
+      else if (ctx->nsc == 2) qcache ? setattr((const void*)commit_kernel<2, true>, smem) : setattr((const void*)commit_kernel<2, false>, smem);
+      else qcache ? setattr((const void*)commit_kernel<4, true>, smem) : setattr((const void*)commit_kernel<4, false>, smem);
+    }
+    if (smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes)", (long long)ctx->n);
+    if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
+  }
   // pods per wave: aim for >= ~4096 waves per sweep
   int32_t ppw = 64;
   while (ppw > 4 && ctx->nchunks * (ctx->batch / ppw) < 4096) ppw >>= 1;
@@ -1173,7 +1324,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   const int sweep_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048));
   hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
-  HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 64, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 256, ctx->stream));
   HIPCHK(ctx, hipEventRecord(t0, ctx->stream));
   std::vector<std::pair<int, size_t>> evs;
   size_t evn = 2;
@@ -1196,7 +1347,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     if (++rounds > 1000000) KS_FAIL(ctx, KS_EHIP, "schedule made no progress");
   }
   HIPCHK(ctx, hipEventRecord(t1, ctx->stream));
-  unsigned long long cnt[3] = {0, 0, 0};
+  unsigned long long cnt[16] = {0};
   HIPCHK(ctx, hipMemcpyAsync(cnt, ctx->counters, sizeof(cnt), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   float ms = 0;
@@ -1205,6 +1356,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   ctx->stats.passes = (int64_t)cnt[0];
   ctx->stats.cut_passes = (int64_t)cnt[1];
   ctx->stats.rescans = (int64_t)cnt[2];
+  ctx->stats.slot_misses = (int64_t)cnt[3];
+  for (int i = 0; i < 8; ++i) ctx->stats.diag[i] = (int64_t)cnt[8 + i];
   for (size_t i = 0; i + 1 < evs.size(); i += 2) {
     float e = 0;
     (void)hipEventElapsedTime(&e, ctx->ev_pool[evs[i].second], ctx->ev_pool[evs[i + 1].second]);

@@ -90,17 +90,9 @@ struct DevQuotas {
   int64_t *limit, *used, *min, *npused;  // [q][KS_QUOTA_DIMS]
 };
 
-// Mutable node state carried by commit-kernel slots.
-struct MutState {
-  int64_t req_cpu, req_mem, req_eph, nz_cpu, nz_mem;
-  int64_t req_sc[KS_MAX_SCALARS];
-  int64_t term_cpu, term_mem, pterm_cpu, pterm_mem;
-  int32_t pod_count, node;
-};
-
 // One node in registers, with node-only precomputation done once per pass.
 template <int NSC>
-struct NodeReg {
+struct __attribute__((aligned(16))) NodeReg {
   int64_t alloc_cpu, alloc_mem, alloc_eph;
   int64_t free_cpu, free_mem, free_eph;
   int64_t nz_cpu, nz_mem, req_eph;
@@ -111,6 +103,7 @@ struct NodeReg {
   uint32_t la_bits;
   int32_t pods_full;
   int32_t allowed;
+  int32_t pod_count;
   int32_t valid;
 };
 
@@ -169,7 +162,8 @@ __device__ __forceinline__ void load_node(const DevNodes& d, int64_t n, int vali
   r.free_mem = r.alloc_mem - req_mem;
   r.free_eph = r.alloc_eph - r.req_eph;
   r.allowed = d.allowed_pods[n];
-  r.pods_full = ((int64_t)d.pod_count[n] + 1 > (int64_t)r.allowed) || !valid;
+  r.pod_count = d.pod_count[n];
+  r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !valid;
   r.nz_cpu = d.nz_cpu[n];
   r.nz_mem = d.nz_mem[n];
 #pragma unroll
@@ -192,22 +186,27 @@ __device__ __forceinline__ void load_node(const DevNodes& d, int64_t n, int vali
   r.rcp_lmem = rcp100(r.la_alloc_mem);
 }
 
-// Overlay the mutable fields of a commit slot onto a loaded node.
+// Reserve: NodeInfo.AddPod (upstream framework/types.go) + podAssignCache.assign
+// (load_aware.go:260, pod_assign_cache.go:53): the new pod has no PodMetric, so its
+// estimate counts in every later Score on this node (load_aware.go:350-355).
 template <int NSC>
-__device__ __forceinline__ void apply_mut(NodeReg<NSC>& r, const MutState& m) {
-  r.pods_full = ((int64_t)m.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
-  r.free_cpu = r.alloc_cpu - m.req_cpu;
-  r.free_mem = r.alloc_mem - m.req_mem;
-  r.req_eph = m.req_eph;
-  r.free_eph = r.alloc_eph - m.req_eph;
-  r.nz_cpu = m.nz_cpu;
-  r.nz_mem = m.nz_mem;
+__device__ __forceinline__ void reserve_row(NodeReg<NSC>& r, const PodRec& p) {
+  r.free_cpu -= p.cpu;
+  r.free_mem -= p.mem;
+  r.free_eph -= p.eph;
+  r.req_eph += p.eph;
 #pragma unroll
-  for (int k = 0; k < NSC; ++k) r.req_sc[k] = m.req_sc[k];
-  r.term_cpu = m.term_cpu;
-  r.term_mem = m.term_mem;
-  r.pterm_cpu = m.pterm_cpu;
-  r.pterm_mem = m.pterm_mem;
+  for (int k = 0; k < NSC; ++k) r.req_sc[k] += p.sc[k];
+  r.nz_cpu += p.nzcpu;
+  r.nz_mem += p.nzmem;
+  r.pod_count += 1;
+  r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
+  r.term_cpu += p.est_cpu;
+  r.term_mem += p.est_mem;
+  if (p.flags & KS_POD_PROD) {
+    r.pterm_cpu += p.est_cpu;
+    r.pterm_mem += p.est_mem;
+  }
 }
 
 struct EvalOut {
@@ -286,23 +285,44 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   return o;
 }
 
-// Wave-wide reductions (64 lanes).
+// Wave-wide reductions (64 lanes), result wave-uniform.
+// DPP within each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror),
+// then the four row maxima through readlane into SGPRs.  Requires all 64 lanes active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    uint32_t o = __shfl_xor(v, off, 64);
-    v = o > v ? o : v;
-  }
-  return v;
+  v = umax32(v, dpp32<0xB1>(v));
+  v = umax32(v, dpp32<0x4E>(v));
+  v = umax32(v, dpp32<0x141>(v));
+  v = umax32(v, dpp32<0x140>(v));
+  const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+  return umax32(umax32(r0, r1), umax32(r2, r3));
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = dpp32<CTRL>((uint32_t)v), hi = dpp32<CTRL>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    uint64_t o = __shfl_xor((unsigned long long)v, off, 64);
-    v = o > v ? o : v;
-  }
-  return v;
+  v = umax64(v, dpp64<0xB1>(v));
+  v = umax64(v, dpp64<0x4E>(v));
+  v = umax64(v, dpp64<0x141>(v));
+  v = umax64(v, dpp64<0x140>(v));
+  return umax64(umax64(readlane64(v, 0), readlane64(v, 16)), umax64(readlane64(v, 32), readlane64(v, 48)));
 }
 
 __device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {

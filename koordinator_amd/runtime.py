@@ -17,7 +17,7 @@ from . import abi
 from .cluster import NodeState, NodeTable, PodTable, QuotaTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkoordgpu.so")
+LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
 CSRC = os.path.join(HERE, "csrc")
 
 RESULT_DTYPE = np.dtype([("node", "<i4"), ("status", "<u4"), ("score", "<i8")])
@@ -180,4 +180,6 @@ class Evaluator:
     def stats(self) -> dict:
         s = abi.KsStats()
         self._chk(self.L.ks_get_stats(self.h, C.byref(s)))
-        return {k: getattr(s, k) for k, _ in abi.KsStats._fields_}
+        out = {k: getattr(s, k) for k, _ in abi.KsStats._fields_}
+        out["diag"] = list(s.diag)
+        return out

@@ -1,0 +1,18 @@
+"""Diagnostic: per-phase cycle split of the commit kernel (needs libkoordgpu_diag.so, -DKS_COMMIT_STAMPS)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("KS_LIB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "koordinator_amd", "libkoordgpu_diag.so"))
+from koordinator_amd import runtime, synth
+w = synth.c2()
+cfg = w.cfg
+cfg.profile = 1
+ev = runtime.Evaluator(cfg, w.nodes, w.quotas)
+ev.stage(w.pods)
+ev.checkpoint()
+for i in range(3):
+    ev.restore(); ev.schedule_staged(); st = ev.stats()
+names = ["prefetch", "quota", "slot_rescore", "candidates+rescans", "commit", "loop_exit"]
+tot = sum(st["diag"][:6])
+print({k: st[k] for k in ("passes", "cut_passes", "rescans", "slot_misses", "sweep_ms", "select_ms", "commit_ms", "total_ms")})
+for n, v in zip(names, st["diag"][:6]):
+    print(f"{n:20s} {v:14d} cycles  {100.0*v/max(tot,1):6.2f}%  {v/10000:10.1f} cyc/pod")
