@@ -1195,10 +1195,20 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
       if (pc->quota[i] >= ctx->q.q || pc->quota[i] < -1)
         KS_FAIL(ctx, KS_EINVAL, "pod %d: quota row %d out of range (loaded %d)", i, pc->quota[i], ctx->q.q);
   }
+  // a pod requesting a scalar slot no node advertises still has to be evaluated against the
+  // (zero) allocatable of that slot: widen the kernels' scalar template to cover it
+  int need = ctx->nsc;
   for (int k = ctx->nsc; k < KS_MAX_SCALARS; ++k) {
     if (!pc->req_scalar[k]) continue;
     for (int32_t i = 0; i < p; ++i)
-      if (pc->req_scalar[k][i] != 0) KS_FAIL(ctx, KS_EINVAL, "pod %d requests scalar slot %d with no node column", i, k);
+      if (pc->req_scalar[k][i] != 0) {
+        need = k + 1;
+        break;
+      }
+  }
+  if (need > ctx->nsc) {
+    ctx->nsc = need <= 2 ? 2 : 4;
+    ctx->kc.nsc = ctx->nsc;
   }
   return KS_OK;
 }

@@ -1,0 +1,83 @@
+"""The C ABI boundary: header/ctypes layout agreement and library exports (CPU-only)."""
+import ctypes as C
+import os
+import subprocess
+
+import pytest
+
+from koordinator_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "koordinator_amd", "libkoordgpu.so")
+
+
+@pytest.fixture(scope="module")
+def probe(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("abi") / "probe"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "abi_probe.c"), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode().split("\n")
+    return dict(line.split() for line in out if line.strip())
+
+
+STRUCTS = {
+    "ks_fit_args": abi.KsFitArgs, "ks_loadaware_args": abi.KsLoadAwareArgs, "ks_quota_args": abi.KsQuotaArgs,
+    "ks_config": abi.KsConfig, "ks_node_cols": abi.KsNodeCols, "ks_pod_cols": abi.KsPodCols,
+    "ks_quota_cols": abi.KsQuotaCols, "ks_result": abi.KsResult, "ks_node_state": abi.KsNodeState,
+    "ks_stats": abi.KsStats,
+}
+
+
+@pytest.mark.parametrize("name", sorted(STRUCTS))
+def test_struct_sizes_match_header(probe, name):
+    assert int(probe[name]) == C.sizeof(STRUCTS[name])
+
+
+def test_field_offsets_match_header(probe):
+    for key, v in probe.items():
+        if "." not in key:
+            continue
+        sname, field = key.split(".")
+        assert getattr(STRUCTS[sname], field).offset == int(v), key
+
+
+def test_library_exports_every_header_symbol():
+    if not os.path.exists(LIB):
+        pytest.skip("libkoordgpu.so not built (run __graft_entry__.build())")
+    nm = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
+    exported = {line.split()[-1] for line in nm.splitlines() if " T " in line}
+    with open(os.path.join(ROOT, "include", "koordgpu.h")) as f:
+        header = f.read()
+    declared = {s for s in abi.EXPORTED_SYMBOLS if f" {s}(" in header or f"*{s}(" in header}
+    assert declared == set(abi.EXPORTED_SYMBOLS)
+    assert set(abi.EXPORTED_SYMBOLS) <= exported
+
+
+def test_library_loads_and_reports_missing_gpu():
+    """dlopen works without a GPU; ks_create fails loudly (no CPU fallback) when no device is visible."""
+    if not os.path.exists(LIB):
+        pytest.skip("libkoordgpu.so not built")
+    from koordinator_amd import runtime
+
+    L = runtime.lib()
+    for s in abi.EXPORTED_SYMBOLS:
+        assert hasattr(L, s)
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    with pytest.raises(runtime.KsError) as ei:
+        runtime.Evaluator(abi.KsConfig(abi_version=abi.KS_ABI_VERSION))
+    assert "device" in str(ei.value).lower()
+
+
+def test_abi_version_checked():
+    if not os.path.exists(LIB):
+        pytest.skip("libkoordgpu.so not built")
+    from koordinator_amd import runtime
+
+    L = runtime.lib()
+    h = C.c_void_p()
+    cfg = abi.KsConfig(abi_version=999)
+    assert L.ks_create(C.byref(cfg), C.byref(h)) == abi.KS_EINVAL
+    assert b"ABI" in L.ks_last_error(None)
