@@ -278,19 +278,21 @@ struct CommitArgs {
 
 // LDS image of one pass (fixed part); the candidate arrays, the optional quota cache and the
 // chunk -> dirty-entry map follow it (carved by CommitLayout, same arithmetic on host and device).
+// LDS image of one pass (fixed part); the candidate arrays, the optional quota cache, the
+// per-chunk touched masks and the node->slot hash follow it (carved by commit_layout, the same
+// arithmetic on host and device).
 template <int NSC>
 struct __attribute__((aligned(16))) CommitLds {
-  NodeReg<NSC> slot[kMaxBatch];   // rows of nodes touched in this pass (authoritative)
   NodeReg<NSC> pred[2][kMaxBatch];  // snapshot rows of each pod's two best candidate nodes
   PodRec pods[kMaxBatch];
+  ks_result res[kMaxBatch];         // results buffered for one coalesced store at the end
   uint64_t cand_bound[kMaxBatch];
   int32_t cand_count[kMaxBatch];
-  int32_t slot_node[kMaxBatch];
-  int32_t pred_node[2][kMaxBatch];
   uint32_t pq_mask[kMaxBatch];
   int64_t pq_req[kMaxBatch][KS_QUOTA_DIMS];
-  uint8_t dmap[kMaxBatch][64];    // dirty entry -> lane in chunk -> slot (0xFF none)
 };
+
+constexpr int kSlotHash = 128;  // open-addressing node -> slot table (>= 2 x max slots)
 
 struct QuotaRowsLds {
   int32_t parent[kQuotaLdsRows];
@@ -300,7 +302,7 @@ struct QuotaRowsLds {
 };
 
 struct CommitLayout {
-  size_t cand_t, cand_chunk, quota, dentry, total;
+  size_t cand_t, cand_chunk, quota, hash, touched, total;
 };
 
 template <int NSC>
@@ -313,28 +315,16 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += ((size_t)kMaxBatch * k * 4 + 15) / 16 * 16;
   L.quota = o;
   if (qc) o += (sizeof(QuotaRowsLds) + 15) / 16 * 16;
-  L.dentry = o;
-  o += (size_t)(nchunks + 15) / 16 * 16;
+  L.hash = o;
+  o += (size_t)kSlotHash * 8;
+  L.touched = o;
+  o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
   L.total = o;
   return L;
 }
 
-template <int NSC>
-__device__ __forceinline__ uint64_t rescan_chunk(const CommitArgs& a, const CommitLds<NSC>& sm, const PodRec& pod,
-                                                 int64_t chunk, int32_t dentry) {
-  const int lane = threadIdx.x;
-  const int64_t node = chunk * 64 + lane;
-  NodeReg<NSC> r;
-  const uint8_t s = sm.dmap[dentry][lane];
-  if (s != 0xFF) r = sm.slot[s];
-  else load_node<NSC>(a.d, node, node < a.n, r);
-  const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
-  return wave_max_u64(o.reasons ? 0ull : gkey(o.total, node));
-}
-
 // ElasticQuota PreFilter (plugin.go:210-255, plugin_helper.go:281-319); lane d checks dimension d.
-// Q is either the LDS cache (QuotaRowsLds*) or the global table; templated so each path keeps
-// its own address space (ds_* vs global_* loads).
+// Templated on the pointer types so the LDS cache and the global table keep their address spaces.
 template <typename P32, typename PU32, typename P64>
 __device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU32 min_mask, P64 limit, P64 used,
                                                 P64 minv, P64 npused, bool check_parent, int32_t quota,
@@ -362,13 +352,84 @@ __device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU3
   return 0;
 }
 
-// Copy a 16-byte aligned LDS struct with one 16-byte move per lane.
-template <typename T>
-__device__ __forceinline__ void lds_copy(T& dst, const T& src) {
-  static_assert(sizeof(T) % 16 == 0, "LDS row copy needs 16-byte multiples");
-  constexpr int n16 = (int)(sizeof(T) / 16);
+// Move a NodeReg held in lane `src`'s registers to every lane (field by field, ds_bpermute).
+template <int NSC>
+__device__ __forceinline__ NodeReg<NSC> shfl_row(const NodeReg<NSC>& r, int src) {
+  NodeReg<NSC> o;
+  auto s64 = [&](int64_t v) { return (int64_t)__shfl((long long)v, src, 64); };
+  auto sf = [&](float v) { return __shfl(v, src, 64); };
+  auto si = [&](int32_t v) { return __shfl(v, src, 64); };
+  o.alloc_cpu = s64(r.alloc_cpu);
+  o.alloc_mem = s64(r.alloc_mem);
+  o.alloc_eph = s64(r.alloc_eph);
+  o.free_cpu = s64(r.free_cpu);
+  o.free_mem = s64(r.free_mem);
+  o.free_eph = s64(r.free_eph);
+  o.nz_cpu = s64(r.nz_cpu);
+  o.nz_mem = s64(r.nz_mem);
+  o.req_eph = s64(r.req_eph);
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) {
+    o.alloc_sc[k] = s64(r.alloc_sc[k]);
+    o.req_sc[k] = s64(r.req_sc[k]);
+    o.rcp_sc[k] = sf(r.rcp_sc[k]);
+  }
+  o.la_alloc_cpu = s64(r.la_alloc_cpu);
+  o.la_alloc_mem = s64(r.la_alloc_mem);
+  o.term_cpu = s64(r.term_cpu);
+  o.term_mem = s64(r.term_mem);
+  o.pterm_cpu = s64(r.pterm_cpu);
+  o.pterm_mem = s64(r.pterm_mem);
+  o.rcp_cpu = sf(r.rcp_cpu);
+  o.rcp_mem = sf(r.rcp_mem);
+  o.rcp_eph = sf(r.rcp_eph);
+  o.rcp_lcpu = sf(r.rcp_lcpu);
+  o.rcp_lmem = sf(r.rcp_lmem);
+  o.la_bits = (uint32_t)si((int32_t)r.la_bits);
+  o.pods_full = si(r.pods_full);
+  o.allowed = si(r.allowed);
+  o.pod_count = si(r.pod_count);
+  o.valid = si(r.valid);
+  return o;
+}
+
+__device__ __forceinline__ uint32_t slot_hash(int64_t node) { return ((uint32_t)node * 2654435761u) >> 25; }  // 7 bits
+
+__device__ __forceinline__ int32_t hash_find(const int2* h, int64_t node) {
+  uint32_t i = slot_hash(node);
+  for (int probe = 0; probe < kSlotHash; ++probe, i = (i + 1) & (kSlotHash - 1)) {
+    const int2 e = h[i];
+    if (e.x == (int32_t)node) return e.y;
+    if (e.x < 0) return -1;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void hash_insert(int2* h, int64_t node, int32_t slot) {
+  uint32_t i = slot_hash(node);
+  while (h[i].x >= 0) i = (i + 1) & (kSlotHash - 1);
+  h[i] = make_int2((int32_t)node, slot);
+}
+
+// Re-scan a touched chunk exactly: untouched nodes from HBM, touched ones from their slot lane.
+template <int NSC>
+__device__ __forceinline__ uint64_t rescan_chunk(const CommitArgs& a, const int2* hash, const NodeReg<NSC>& srow,
+                                                 const PodRec& pod, int64_t chunk, uint64_t touched_mask) {
   const int lane = threadIdx.x;
-  if (lane < n16) reinterpret_cast<uint4*>(&dst)[lane] = reinterpret_cast<const uint4*>(&src)[lane];
+  const int64_t node = chunk * 64 + lane;
+  NodeReg<NSC> r;
+  load_node<NSC>(a.d, node, node < a.n, r);
+  // the slots of the touched lanes, one at a time (uniform loop over the mask)
+  uint64_t m = touched_mask;
+  while (m) {
+    const int l = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const int32_t s = hash_find(hash, chunk * 64 + l);
+    const NodeReg<NSC> t = shfl_row<NSC>(srow, s);
+    if (lane == l) r = t;
+  }
+  const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
+  return wave_max_u64(o.reasons ? 0ull : gkey(o.total, node));
 }
 
 template <int NSC, bool QC>
@@ -380,7 +441,8 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
   uint2* cand_t = reinterpret_cast<uint2*>(smem_raw + lay.cand_t);
   uint32_t* cand_chunk = reinterpret_cast<uint32_t*>(smem_raw + lay.cand_chunk);
   QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
-  uint8_t* dentry_of_chunk = smem_raw + lay.dentry;
+  int2* hash = reinterpret_cast<int2*>(smem_raw + lay.hash);
+  unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
   const int lane = threadIdx.x;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor0 >= a.total_pods) return;
@@ -400,7 +462,7 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
   } while (0)
 #endif
 
-  // ---- prefetch the whole pass into LDS (one burst of independent loads) ----
+  // ---- prefetch the whole pass into LDS / registers (one burst of independent loads) ----
   if (lane < np) {
     sm.pods[lane] = a.pods[cursor0 + lane];
     sm.cand_count[lane] = a.cand_count[lane];
@@ -414,7 +476,8 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
     cand_chunk[i] = a.cand_chunk[i];
     cand_t[i] = a.cand_t[i];
   }
-  for (int64_t c = lane; c < a.nchunks; c += 64) dentry_of_chunk[c] = 0xFF;
+  for (int64_t c = lane; c < a.nchunks; c += 64) touched[c] = 0ull;
+  for (int32_t i = lane; i < kSlotHash; i += 64) hash[i] = make_int2(-1, -1);
   if (QC) {
     for (int32_t r = lane; r < a.q.q; r += 64) {
       qlds->parent[r] = a.q.parent[r];
@@ -429,7 +492,9 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
     }
   }
   __syncthreads();
-  // predicted winners of each pod = its two best snapshot candidates; prefetch those rows
+  // predicted winners of each pod (lane = pod) = its two best snapshot candidates; rows to LDS
+  int32_t pnode0 = -1, pnode1 = -1;
+  uint64_t pkey0 = 0;
   if (lane < np) {
     const int32_t cnt = sm.cand_count[lane];
     uint64_t b0 = 0, b1 = 0;
@@ -442,20 +507,22 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
         b1 = g;
       }
     }
-    const int64_t n0 = b0 ? gkey_node(b0) : -1, n1 = b1 ? gkey_node(b1) : -1;
-    sm.pred_node[0][lane] = (int32_t)n0;
-    sm.pred_node[1][lane] = (int32_t)n1;
-    if (n0 >= 0) load_node<NSC>(a.d, n0, 1, sm.pred[0][lane]);
-    if (n1 >= 0) load_node<NSC>(a.d, n1, 1, sm.pred[1][lane]);
+    pnode0 = b0 ? (int32_t)gkey_node(b0) : -1;
+    pnode1 = b1 ? (int32_t)gkey_node(b1) : -1;
+    pkey0 = b0;
+    if (pnode0 >= 0) load_node<NSC>(a.d, pnode0, 1, sm.pred[0][lane]);
+    if (pnode1 >= 0) load_node<NSC>(a.d, pnode1, 1, sm.pred[1][lane]);
   }
   __syncthreads();
   KS_STAMP(0);
 
-  int32_t nslots = 0, ndirty = 0;
+  // slot s lives in lane s's registers: the current row of the s-th node touched in this pass
+  NodeReg<NSC> srow;
+  int32_t snode = -1;
+  int32_t nslots = 0;
   int32_t processed = np;
   unsigned long long rescans = 0, misses = 0;
   for (int32_t j = 0; j < np; ++j) {
-    const int32_t gp = cursor0 + j;
     const PodRec pod = sm.pods[j];
     const bool has_quota = a.c.quota_enable && pod.quota >= 0;
     const uint32_t pmask = sm.pq_mask[j];
@@ -467,37 +534,45 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
              : quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
                            a.c.quota_parent, pod.quota, pod.flags, pmask, qreq);
       if (st) {
-        if (lane == 0) a.results[gp] = ks_result{-1, st, 0};
+        if (lane == 0) sm.res[j] = ks_result{-1, st, 0};
         KS_STAMP(1);
         continue;
       }
     }
     KS_STAMP(1);
-    // nodes touched earlier in this pass: exact current keys from their LDS rows
-    uint64_t best_mod = 0;
-    if (nslots) {
-      uint64_t key = 0;
-      if (lane < nslots) {
-        const NodeReg<NSC> r = sm.slot[lane];
-        const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
-        key = o.reasons ? 0ull : gkey(o.total, sm.slot_node[lane]);
+    const int32_t b0 = __builtin_amdgcn_readlane(pnode0, j);
+    uint64_t best = 0;
+    bool resolved = false;
+    if (a.c.monotone) {
+      // Monotone profiles: a commit can only lower a node's key, so the pod's snapshot-best node is
+      // still the exact argmax whenever no earlier pod of this pass touched it.
+      if (b0 < 0) {
+        resolved = true;  // nothing feasible in the snapshot, and nothing can become feasible
+      } else if (!((touched[b0 >> 6] >> (b0 & 63)) & 1ull)) {
+        best = readlane64(pkey0, j);
+        resolved = true;
       }
-      best_mod = wave_max_u64(key);
     }
-    KS_STAMP(2);
-    // untouched nodes: chunk best / runner-up from the snapshot
-    const int32_t cnt = sm.cand_count[j];
-    const bool valid = lane < cnt;
-    const uint32_t chunk = valid ? cand_chunk[j * K + lane] : 0u;
-    const uint2 t = valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
-    const uint32_t de = valid ? dentry_of_chunk[chunk] : 0xFFu;
-    uint64_t u = local_gkey(t.x, chunk), ub = 0;
-    bool exact = valid;
-    if (valid && de != 0xFFu) {
-      if (sm.dmap[de][63 - (t.x & 63u)] != 0xFF) {           // best node touched
+    if (!resolved) {
+      // nodes touched earlier in this pass: exact current keys from their slot registers
+      uint64_t key_mod = 0;
+      if (lane < nslots) {
+        const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, srow);
+        key_mod = o.reasons ? 0ull : gkey(o.total, snode);
+      }
+      KS_STAMP(2);
+      // untouched nodes: chunk best / runner-up from the snapshot
+      const int32_t cnt = sm.cand_count[j];
+      const bool valid = lane < cnt;
+      const uint32_t chunk = valid ? cand_chunk[j * K + lane] : 0u;
+      const uint2 t = valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
+      const uint64_t tm = valid ? touched[chunk] : 0ull;
+      uint64_t u = local_gkey(t.x, chunk), ub = 0;
+      bool exact = valid;
+      if (valid && ((tm >> (63 - (t.x & 63u))) & 1ull)) {    // best node touched
         if (t.y == 0) {
           u = 0;                                             // no other feasible node in the chunk
-        } else if (sm.dmap[de][63 - (t.y & 63u)] == 0xFF) {
+        } else if (!((tm >> (63 - (t.y & 63u))) & 1ull)) {
           u = local_gkey(t.y, chunk);                        // runner-up untouched: exact
         } else {
           exact = false;                                     // both touched: < runner-up, unknown
@@ -505,65 +580,50 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
           u = 0;
         }
       }
-    }
-    uint64_t best = wave_max_u64(exact ? u : 0ull);
-    uint64_t need = __ballot(!exact && valid && ub > best);
-    while (need) {
-      const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? ub : 0ull);
-      const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && ub == kmax)) - 1;
-      const int64_t c = (int64_t)(uint32_t)__shfl((int)chunk, sel, 64);
-      const int32_t d = (int32_t)(uint32_t)__shfl((int)de, sel, 64);
-      const uint64_t v = rescan_chunk<NSC>(a, sm, pod, c, d);
-      ++rescans;
-      best = umax64(best, v);
-      need &= ~(1ull << sel);
-      need &= __ballot(ub > best);
-    }
-    best = umax64(best, best_mod);
-    KS_STAMP(3);
-    if (cnt == K && best < sm.cand_bound[j]) {
-      processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep
-      break;
+      best = wave_max_u64(umax64(exact ? u : 0ull, key_mod));
+      uint64_t need = __ballot(!exact && valid && ub > best);
+      while (need) {
+        const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? ub : 0ull);
+        const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && ub == kmax)) - 1;
+        const int64_t c = (int64_t)(uint32_t)__shfl((int)chunk, sel, 64);
+        const uint64_t v = rescan_chunk<NSC>(a, hash, srow, pod, c, touched[c]);
+        ++rescans;
+        best = umax64(best, v);
+        need &= ~(1ull << sel);
+        need &= __ballot(ub > best);
+      }
+      KS_STAMP(3);
+      if (cnt == K && best < sm.cand_bound[j]) {
+        processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep
+        break;
+      }
     }
     if (best == 0) {
-      if (lane == 0) a.results[gp] = ks_result{-1, KS_S_UNSCHEDULABLE, 0};
+      if (lane == 0) sm.res[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0};
       continue;
     }
     const int64_t node = gkey_node(best);
     const int64_t score = gkey_score(best);
-    const int32_t c = (int32_t)(node >> 6);
-    const int ln = (int)(node & 63);
-    // LDS operations of one wave execute in order, so no barrier is needed between the
-    // lane-0 / cooperative writes below and the next pod's reads.
-    int32_t d = dentry_of_chunk[c];
-    if (d == 0xFF) {
-      d = ndirty++;
-      sm.dmap[d][lane] = 0xFF;
-      if (lane == 0) dentry_of_chunk[c] = (uint8_t)d;
-    }
-    int32_t s = sm.dmap[d][ln];
-    if (s == 0xFF) {
+    int32_t s = __ffsll((long long)__ballot(snode == (int32_t)node)) - 1;
+    if (s < 0) {
       s = nslots++;
-      if (sm.pred_node[0][j] == node) {
-        lds_copy(sm.slot[s], sm.pred[0][j]);
-        asm volatile("" ::: "memory");
-      } else if (sm.pred_node[1][j] == node) {
-        lds_copy(sm.slot[s], sm.pred[1][j]);
-        asm volatile("" ::: "memory");
+      if (b0 == (int32_t)node) {
+        if (lane == s) srow = sm.pred[0][j];
+      } else if (__builtin_amdgcn_readlane(pnode1, j) == (int32_t)node) {
+        if (lane == s) srow = sm.pred[1][j];
       } else {
         ++misses;
-        if (lane == 0) load_node<NSC>(a.d, node, 1, sm.slot[s]);
+        if (lane == s) load_node<NSC>(a.d, node, 1, srow);
       }
+      if (lane == s) snode = (int32_t)node;
       if (lane == 0) {
-        sm.slot_node[s] = (int32_t)node;
-        sm.dmap[d][ln] = (uint8_t)s;
+        atomicOr(&touched[node >> 6], 1ull << (node & 63));
+        hash_insert(hash, node, s);
       }
     }
-    asm volatile("" ::: "memory");
-    if (lane == 0) {
-      reserve_row<NSC>(sm.slot[s], pod);
-      a.results[gp] = ks_result{(int32_t)node, KS_S_SCHEDULED, score};
-    }
+    // Reserve on the slot's registers: NodeInfo.AddPod + podAssignCache.assign
+    if (lane == s) reserve_row<NSC>(srow, pod);
+    if (lane == 0) sm.res[j] = ks_result{(int32_t)node, KS_S_SCHEDULED, score};
     if (has_quota && lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u)) {
       // updatePodUsedNoLock -> updateGroupDeltaUsedNoLock (group_quota_manager.go:620-655)
       if (QC) {
@@ -582,22 +642,22 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
   }
   __syncthreads();
   KS_STAMP(5);
-  // ---- write back touched nodes and quota usage ----
+  // ---- write back results, touched nodes and quota usage ----
+  if (lane < processed) a.results[cursor0 + lane] = sm.res[lane];
   if (lane < nslots) {
-    const NodeReg<NSC> r = sm.slot[lane];
-    const int64_t node = sm.slot_node[lane];
-    a.d.req_cpu[node] = r.alloc_cpu - r.free_cpu;
-    a.d.req_mem[node] = r.alloc_mem - r.free_mem;
-    a.d.req_eph[node] = r.req_eph;
-    a.d.nz_cpu[node] = r.nz_cpu;
-    a.d.nz_mem[node] = r.nz_mem;
+    const int64_t node = snode;
+    a.d.req_cpu[node] = srow.alloc_cpu - srow.free_cpu;
+    a.d.req_mem[node] = srow.alloc_mem - srow.free_mem;
+    a.d.req_eph[node] = srow.req_eph;
+    a.d.nz_cpu[node] = srow.nz_cpu;
+    a.d.nz_mem[node] = srow.nz_mem;
 #pragma unroll
-    for (int k = 0; k < NSC; ++k) a.d.req_sc[k][node] = r.req_sc[k];
-    a.d.pod_count[node] = r.pod_count;
-    a.d.la_term_cpu[node] = r.term_cpu;
-    a.d.la_term_mem[node] = r.term_mem;
-    a.d.la_pterm_cpu[node] = r.pterm_cpu;
-    a.d.la_pterm_mem[node] = r.pterm_mem;
+    for (int k = 0; k < NSC; ++k) a.d.req_sc[k][node] = srow.req_sc[k];
+    a.d.pod_count[node] = srow.pod_count;
+    a.d.la_term_cpu[node] = srow.term_cpu;
+    a.d.la_term_mem[node] = srow.term_mem;
+    a.d.la_pterm_cpu[node] = srow.pterm_cpu;
+    a.d.la_pterm_mem[node] = srow.pterm_mem;
   }
   if (QC) {
     for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
