@@ -115,7 +115,21 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   if (r.cpu == 0 && r.mem == 0 && r.eph == 0 && !(fl & KS_POD_SCALAR_KEYS)) fl |= kPodAllZero;
   r.flags = fl;
   r.quota = s.quota[i];
-  r._pad[0] = r._pad[1] = r._pad[2] = 0;
+  r.h_nzcpu = r.nzcpu * 100;
+  r.h_nzmem = r.nzmem * 100;
+  r.h_eph = r.eph * 100;
+  r.h_est_cpu = r.est_cpu * 100;
+  r.h_est_mem = r.est_mem * 100;
+  r.f_nzcpu = i64_to_f32(r.nzcpu);
+  r.f_nzmem = i64_to_f32(r.nzmem);
+  r.f_eph = i64_to_f32(r.eph);
+  r.f_est_cpu = i64_to_f32(r.est_cpu);
+  r.f_est_mem = i64_to_f32(r.est_mem);
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) {
+    r.h_sc[k] = r.sc[k] * 100;
+    r.f_sc[k] = i64_to_f32(r.sc[k]);
+  }
+  r._fpad[0] = r._fpad[1] = r._fpad[2] = 0.0f;
   out[i] = r;
 }
 
@@ -124,7 +138,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
 // ------------------------------------------------------------------------------------------
 
 struct SweepArgs {
-  DevNodes d;
+  const DevNodes* __restrict__ dn;
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
@@ -137,7 +151,8 @@ struct SweepArgs {
 template <int NSC>
 __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar)
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor >= a.total_pods) return;
@@ -149,11 +164,14 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     const int32_t g = (int32_t)(w - c * groups);
     const int64_t node = c * 64 + lane;
     NodeReg<NSC> r;
-    load_node<NSC>(a.d, node, node < a.n, r);
+    {
+      const DevNodes d = *a.dn;
+      load_node<NSC>(a.c, d, node, node < a.n, r);
+    }
     const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
     uint32_t best = 0, second = 0;
     for (int32_t p = p0; p < p1; ++p) {
-      const PodRec pod = a.pods[cursor + p];
+      const PodRec pod = load_pod_uniform(a.pods + cursor + p);
       const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
       const uint32_t key = o.reasons ? 0u : (((uint32_t)(o.total + 1) << 6) | (uint32_t)(63 - lane));
       const uint32_t m1 = wave_max_u32(key);
@@ -175,6 +193,7 @@ struct SelectArgs {
   uint32_t* cand_chunk;          // [64][K]
   uint2* cand_t;                 // [64][K] {best, runner-up} local keys
   uint64_t* cand_bound;          // [64]
+  uint64_t* cand_top;            // [64] the pod's snapshot-best key over every chunk
   int32_t* cand_count;           // [64]
   int64_t nchunks;
   int32_t total_pods, batch, k;
@@ -196,13 +215,17 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   const int32_t K = a.k;
   int32_t cnt = 0;
   uint32_t hmax = 0;
+  uint64_t top = 0;
   for (int64_t e = lane; e < a.nchunks; e += 64) {
-    const uint32_t h = a.in[e * 64 + p].x >> 6;
+    const uint32_t loc = a.in[e * 64 + p].x;
+    const uint32_t h = loc >> 6;
     cnt += h != 0;
     hmax = h > hmax ? h : hmax;
+    top = umax64(top, local_gkey(loc, e));
   }
   cnt = wave_sum_i32(cnt);
   hmax = wave_max_u32(hmax);
+  top = wave_max_u64(top);
   uint32_t t = 1;  // admit h >= t
   int32_t need_eq = 0x7fffffff;
   const bool exhaustive = cnt <= K;
@@ -250,49 +273,73 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   if (lane == 0) {
     a.cand_count[p] = base;
     a.cand_bound[p] = exhaustive ? 0ull : bound;
+    a.cand_top[p] = top;
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // commit: sequential exact selection + Reserve, one wave, pass state resident in LDS
 // ------------------------------------------------------------------------------------------
+//
+// Slot s (the s-th node touched in this pass) is an LDS row of score Terms + Filter headrooms,
+// updated in place by every Reserve.  Building a slot and Reserve are lane-parallel (lane t owns
+// term t).  For pod j the wave evaluates every slot at once (lane = slot; touched nodes exact)
+// and takes the best untouched node from the candidate lists (snapshot keys, exact for untouched
+// nodes).  Monotone profiles skip the slot evaluation whenever the pod's snapshot-best node is
+// still untouched (a commit can only lower keys).  Pod j+1's quota admission and candidate
+// resolution depend only on state pod j has finished changing, so they run right after pod j's
+// Reserve, and the row of pod j+1's best untouched candidate is put in flight from HBM then.
 
 constexpr int kQuotaLdsRows = 128;  // quota tables up to this size are cached in LDS for the pass
+constexpr int kCommitThreads = 256; // 4 waves load the pass; wave 0 alone runs the sequential loop
+
+// fields of a raw node row (lane f of a row load holds field f)
+enum RowField : int {
+  RF_REQ_CPU = 0, RF_REQ_MEM = 1, RF_REQ_EPH = 2, RF_NZ_CPU = 3, RF_NZ_MEM = 4, RF_REQ_SC = 5,  // 5..8
+  RF_TERM_CPU = 9, RF_TERM_MEM = 10, RF_PTERM_CPU = 11, RF_PTERM_MEM = 12, RF_POD_COUNT = 13,
+  RF_ALLOC_CPU = 14, RF_ALLOC_MEM = 15, RF_ALLOC_EPH = 16, RF_ALLOC_SC = 17,  // 17..20
+  RF_LA_ALLOC_CPU = 21, RF_LA_ALLOC_MEM = 22, RF_ALLOWED = 23, RF_LA_BITS = 24,
+  RF_N = 25
+};
+
+// slot-row terms and headrooms
+enum SlotTerm : int { ST_CPU = 0, ST_MEM = 1, ST_EPH = 2, ST_SC = 3, ST_LCPU = 7, ST_LMEM = 8, ST_PLCPU = 9, ST_PLMEM = 10, ST_N = 11 };
+enum SlotFree : int { SF_CPU = 0, SF_MEM = 1, SF_EPH = 2, SF_SC = 3, SF_N = 7 };
+
+struct __attribute__((aligned(16))) SlotRow {
+  Term t[12];
+  int64_t free[8];
+  uint32_t la_bits;
+  int32_t fit_ws, pods_full, allowed, pod_count, valid;
+  int32_t _pad[14];  // 528 B: consecutive rows start 4 banks apart (lane = slot reads conflict-free)
+};
+static_assert(sizeof(SlotRow) == 528, "SlotRow layout");
+
+// Device column of each row field (built by the host at ks_load_nodes).
+struct RowCol {
+  const void* p;
+  int32_t width;
+  int32_t _pad;
+};
 
 struct CommitArgs {
-  DevNodes d;
+  const DevNodes* __restrict__ dn;
   Cfg c;
   const PodRec* __restrict__ pods;
   DevPodQuota pq;
   DevQuotas q;
+  const RowCol* __restrict__ rowcols;  // [RF_N]
   int32_t* cursor;
   const uint32_t* __restrict__ cand_chunk;
   const uint2* __restrict__ cand_t;
   const uint64_t* __restrict__ cand_bound;
+  const uint64_t* __restrict__ cand_top;
   const int32_t* __restrict__ cand_count;
   ks_result* results;
-  unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot global loads
+  unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot row misses [14] fast picks
   int64_t n, nchunks;
   int32_t total_pods, batch, k;
 };
-
-// LDS image of one pass (fixed part); the candidate arrays, the optional quota cache and the
-// chunk -> dirty-entry map follow it (carved by CommitLayout, same arithmetic on host and device).
-// LDS image of one pass (fixed part); the candidate arrays, the optional quota cache, the
-// per-chunk touched masks and the node->slot hash follow it (carved by commit_layout, the same
-// arithmetic on host and device).
-template <int NSC>
-struct __attribute__((aligned(16))) CommitLds {
-  NodeReg<NSC> pred[2][kMaxBatch];  // snapshot rows of each pod's two best candidate nodes
-  PodRec pods[kMaxBatch];
-  ks_result res[kMaxBatch];         // results buffered for one coalesced store at the end
-  uint64_t cand_bound[kMaxBatch];
-  int32_t cand_count[kMaxBatch];
-  uint32_t pq_mask[kMaxBatch];
-  int64_t pq_req[kMaxBatch][KS_QUOTA_DIMS];
-};
-
-constexpr int kSlotHash = 128;  // open-addressing node -> slot table (>= 2 x max slots)
 
 struct QuotaRowsLds {
   int32_t parent[kQuotaLdsRows];
@@ -302,21 +349,32 @@ struct QuotaRowsLds {
 };
 
 struct CommitLayout {
-  size_t cand_t, cand_chunk, quota, hash, touched, total;
+  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, quota, touched, total;
 };
 
-template <int NSC>
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+
 __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc) {
   CommitLayout L;
-  size_t o = (sizeof(CommitLds<NSC>) + 15) / 16 * 16;
+  size_t o = 0;
+  L.rows = o;
+  o += (size_t)kMaxBatch * sizeof(SlotRow);
+  L.pods = o;
+  o += (size_t)kMaxBatch * sizeof(PodRec);
+  L.res = o;
+  o += align16((size_t)kMaxBatch * sizeof(ks_result));
+  L.raw = o;
+  o += 32 * 8;  // one raw row being turned into a slot row
+  L.rawtop = o;
+  o += (size_t)kMaxBatch * 32 * 8;  // raw row of each pod's snapshot-best node, prefetched per pass
+  L.pqreq = o;
+  o += (size_t)kMaxBatch * KS_QUOTA_DIMS * 8;
   L.cand_t = o;
   o += (size_t)kMaxBatch * k * sizeof(uint2);
   L.cand_chunk = o;
-  o += ((size_t)kMaxBatch * k * 4 + 15) / 16 * 16;
+  o += align16((size_t)kMaxBatch * k * 4);
   L.quota = o;
-  if (qc) o += (sizeof(QuotaRowsLds) + 15) / 16 * 16;
-  L.hash = o;
-  o += (size_t)kSlotHash * 8;
+  if (qc) o += align16(sizeof(QuotaRowsLds));
   L.touched = o;
   o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
   L.total = o;
@@ -324,126 +382,141 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
 }
 
 // ElasticQuota PreFilter (plugin.go:210-255, plugin_helper.go:281-319); lane d checks dimension d.
-// Templated on the pointer types so the LDS cache and the global table keep their address spaces.
+// The leaf's used/limit/mask reads are independent, so they are issued together.
 template <typename P32, typename PU32, typename P64>
 __device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU32 min_mask, P64 limit, P64 used,
                                                 P64 minv, P64 npused, bool check_parent, int32_t quota,
                                                 uint32_t flags, uint32_t pmask, int64_t req) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
   const int ld = lane < KS_QUOTA_DIMS ? lane : 0;
+  const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
   {
-    const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
-    const bool bad = in_pod && ((limit_mask[quota] >> lane) & 1u) && (req + used[o] > limit[o]);
+    const uint32_t lm = limit_mask[quota];
+    const int64_t u = used[o], l = limit[o];
+    const bool bad = in_pod && ((lm >> lane) & 1u) && (req + u > l);
     if (__ballot(bad)) return KS_S_QUOTA;
   }
   if (flags & KS_POD_NONPREEMPTIBLE) {
-    const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
-    const bool bad = in_pod && ((min_mask[quota] >> lane) & 1u) && (req + npused[o] > minv[o]);
+    const uint32_t mm = min_mask[quota];
+    const int64_t u = npused[o], m = minv[o];
+    const bool bad = in_pod && ((mm >> lane) & 1u) && (req + u > m);
     if (__ballot(bad)) return KS_S_QUOTA_NONPREEMPTIBLE;
   }
   if (check_parent) {
-    for (int32_t cur = quota; cur >= 0; cur = parent[cur]) {
-      const size_t o = (size_t)cur * KS_QUOTA_DIMS + ld;
-      const bool bad = in_pod && ((limit_mask[cur] >> lane) & 1u) && (req + used[o] > limit[o]);
+    for (int32_t cur = parent[quota]; cur >= 0; cur = parent[cur]) {
+      const size_t oc = (size_t)cur * KS_QUOTA_DIMS + ld;
+      const bool bad = in_pod && ((limit_mask[cur] >> lane) & 1u) && (req + used[oc] > limit[oc]);
       if (__ballot(bad)) return KS_S_QUOTA | KS_S_QUOTA_PARENT;
     }
   }
   return 0;
 }
 
-// Move a NodeReg held in lane `src`'s registers to every lane (field by field, ds_bpermute).
+// One row field of node `node`, lane f loading field f (4-byte columns zero-extended).
+__device__ __forceinline__ int64_t load_field(const void* p, int32_t w, int64_t node) {
+  if (w == 8) return gld((const int64_t*)p + node);
+  return (int64_t)(uint64_t)gld((const uint32_t*)p + node);
+}
+
+// NodeReg of one slot row (lane-private LDS reads).
 template <int NSC>
-__device__ __forceinline__ NodeReg<NSC> shfl_row(const NodeReg<NSC>& r, int src) {
-  NodeReg<NSC> o;
-  auto s64 = [&](int64_t v) { return (int64_t)__shfl((long long)v, src, 64); };
-  auto sf = [&](float v) { return __shfl(v, src, 64); };
-  auto si = [&](int32_t v) { return __shfl(v, src, 64); };
-  o.alloc_cpu = s64(r.alloc_cpu);
-  o.alloc_mem = s64(r.alloc_mem);
-  o.alloc_eph = s64(r.alloc_eph);
-  o.free_cpu = s64(r.free_cpu);
-  o.free_mem = s64(r.free_mem);
-  o.free_eph = s64(r.free_eph);
-  o.nz_cpu = s64(r.nz_cpu);
-  o.nz_mem = s64(r.nz_mem);
-  o.req_eph = s64(r.req_eph);
+__device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
+  r.free_cpu = s.free[SF_CPU];
+  r.free_mem = s.free[SF_MEM];
+  r.free_eph = s.free[SF_EPH];
+  r.t_cpu = s.t[ST_CPU];
+  r.t_mem = s.t[ST_MEM];
+  r.t_eph = s.t[ST_EPH];
 #pragma unroll
   for (int k = 0; k < NSC; ++k) {
-    o.alloc_sc[k] = s64(r.alloc_sc[k]);
-    o.req_sc[k] = s64(r.req_sc[k]);
-    o.rcp_sc[k] = sf(r.rcp_sc[k]);
+    r.free_sc[k] = s.free[SF_SC + k];
+    r.t_sc[k] = s.t[ST_SC + k];
   }
-  o.la_alloc_cpu = s64(r.la_alloc_cpu);
-  o.la_alloc_mem = s64(r.la_alloc_mem);
-  o.term_cpu = s64(r.term_cpu);
-  o.term_mem = s64(r.term_mem);
-  o.pterm_cpu = s64(r.pterm_cpu);
-  o.pterm_mem = s64(r.pterm_mem);
-  o.rcp_cpu = sf(r.rcp_cpu);
-  o.rcp_mem = sf(r.rcp_mem);
-  o.rcp_eph = sf(r.rcp_eph);
-  o.rcp_lcpu = sf(r.rcp_lcpu);
-  o.rcp_lmem = sf(r.rcp_lmem);
-  o.la_bits = (uint32_t)si((int32_t)r.la_bits);
-  o.pods_full = si(r.pods_full);
-  o.allowed = si(r.allowed);
-  o.pod_count = si(r.pod_count);
-  o.valid = si(r.valid);
-  return o;
+  r.t_lcpu = s.t[ST_LCPU];
+  r.t_lmem = s.t[ST_LMEM];
+  r.t_plcpu = s.t[ST_PLCPU];
+  r.t_plmem = s.t[ST_PLMEM];
+  r.la_bits = s.la_bits;
+  r.fit_ws = s.fit_ws;
+  r.pods_full = s.pods_full;
+  r.allowed = s.allowed;
+  r.pod_count = s.pod_count;
+  r.valid = s.valid;
 }
 
-__device__ __forceinline__ uint32_t slot_hash(int64_t node) { return ((uint32_t)node * 2654435761u) >> 25; }  // 7 bits
+// Untouched-candidate resolution of one pod (lane k = candidate k), against the current touched masks.
+struct Cands {
+  uint64_t u;      // exact best untouched key of the lane's chunk (0 = none / unknown)
+  uint64_t ub;     // upper bound when inexact (best and runner-up both touched)
+  uint32_t chunk;
+  bool exact, valid;
+  uint64_t umax;   // wave max of the exact u
+  bool fast;       // monotone profile and the pod's snapshot-best node is untouched
+};
 
-__device__ __forceinline__ int32_t hash_find(const int2* h, int64_t node) {
-  uint32_t i = slot_hash(node);
-  for (int probe = 0; probe < kSlotHash; ++probe, i = (i + 1) & (kSlotHash - 1)) {
-    const int2 e = h[i];
-    if (e.x == (int32_t)node) return e.y;
-    if (e.x < 0) return -1;
+__device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const uint2* cand_t,
+                                               const unsigned long long* touched, int32_t j, int32_t K,
+                                               int32_t cnt) {
+  const int lane = threadIdx.x & 63;
+  Cands r;
+  r.valid = lane < cnt;
+  r.chunk = r.valid ? cand_chunk[j * K + lane] : 0u;
+  const uint2 t = r.valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
+  const uint64_t tm = r.valid ? touched[r.chunk] : 0ull;
+  r.u = local_gkey(t.x, r.chunk);
+  r.fast = false;
+  r.ub = 0;
+  r.exact = r.valid;
+  if (r.valid && ((tm >> (63 - (t.x & 63u))) & 1ull)) {  // chunk best touched
+    if (t.y == 0) {
+      r.u = 0;                                           // no other feasible node in the chunk
+    } else if (!((tm >> (63 - (t.y & 63u))) & 1ull)) {
+      r.u = local_gkey(t.y, r.chunk);                    // runner-up untouched: exact
+    } else {
+      r.exact = false;                                   // both touched: below the runner-up, unknown
+      r.ub = local_gkey(t.y, r.chunk);
+      r.u = 0;
+    }
   }
-  return -1;
+  r.umax = wave_max_u64(r.exact ? r.u : 0ull);
+  return r;
 }
 
-__device__ __forceinline__ void hash_insert(int2* h, int64_t node, int32_t slot) {
-  uint32_t i = slot_hash(node);
-  while (h[i].x >= 0) i = (i + 1) & (kSlotHash - 1);
-  h[i] = make_int2((int32_t)node, slot);
-}
-
-// Re-scan a touched chunk exactly: untouched nodes from HBM, touched ones from their slot lane.
+// Re-scan a candidate chunk's untouched nodes exactly for one pod (lane = node); touched nodes are
+// covered by the slot evaluation.
 template <int NSC>
-__device__ __forceinline__ uint64_t rescan_chunk(const CommitArgs& a, const int2* hash, const NodeReg<NSC>& srow,
-                                                 const PodRec& pod, int64_t chunk, uint64_t touched_mask) {
-  const int lane = threadIdx.x;
+__device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const Cfg& cfg, const PodRec& pod,
+                                                     int64_t chunk, uint64_t touched_mask) {
+  const int lane = threadIdx.x & 63;
   const int64_t node = chunk * 64 + lane;
   NodeReg<NSC> r;
-  load_node<NSC>(a.d, node, node < a.n, r);
-  // the slots of the touched lanes, one at a time (uniform loop over the mask)
-  uint64_t m = touched_mask;
-  while (m) {
-    const int l = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    const int32_t s = hash_find(hash, chunk * 64 + l);
-    const NodeReg<NSC> t = shfl_row<NSC>(srow, s);
-    if (lane == l) r = t;
+  {
+    const DevNodes d = *a.dn;
+    load_node<NSC>(cfg, d, node, node < a.n, r);
   }
-  const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
-  return wave_max_u64(o.reasons ? 0ull : gkey(o.total, node));
+  const EvalOut o = eval_pod_node<NSC, false>(cfg, pod, r);
+  const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
+  return wave_max_u64(skip ? 0ull : gkey(o.total, node));
 }
 
 template <int NSC, bool QC>
-__global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
+__global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  CommitLds<NSC>& sm = *reinterpret_cast<CommitLds<NSC>*>(smem_raw);
   const int32_t K = a.k;
-  const CommitLayout lay = commit_layout<NSC>(K, a.nchunks, QC);
+  const CommitLayout lay = commit_layout(K, a.nchunks, QC);
+  SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
+  PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
+  ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
+  int64_t* raw = reinterpret_cast<int64_t*>(smem_raw + lay.raw);
+  int64_t* rawtop = reinterpret_cast<int64_t*>(smem_raw + lay.rawtop);
+  int64_t* pqreq = reinterpret_cast<int64_t*>(smem_raw + lay.pqreq);
   uint2* cand_t = reinterpret_cast<uint2*>(smem_raw + lay.cand_t);
   uint32_t* cand_chunk = reinterpret_cast<uint32_t*>(smem_raw + lay.cand_chunk);
   QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
-  int2* hash = reinterpret_cast<int2*>(smem_raw + lay.hash);
   unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor0 >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor0);
@@ -462,202 +535,305 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
   } while (0)
 #endif
 
-  // ---- prefetch the whole pass into LDS / registers (one burst of independent loads) ----
-  if (lane < np) {
-    sm.pods[lane] = a.pods[cursor0 + lane];
-    sm.cand_count[lane] = a.cand_count[lane];
-    sm.cand_bound[lane] = a.cand_bound[lane];
-    const int32_t gp = cursor0 + lane;
-    sm.pq_mask[lane] = a.pq.mask[gp];
-#pragma unroll
-    for (int d = 0; d < KS_QUOTA_DIMS; ++d) sm.pq_req[lane][d] = a.pq.req[d][gp];
-  }
-  for (int32_t i = lane; i < np * K; i += 64) {
+  // ---- load the pass into LDS with all four waves (independent loads, one burst) ----
+  for (int32_t i = tid; i < np * K; i += kCommitThreads) {
     cand_chunk[i] = a.cand_chunk[i];
     cand_t[i] = a.cand_t[i];
   }
-  for (int64_t c = lane; c < a.nchunks; c += 64) touched[c] = 0ull;
-  for (int32_t i = lane; i < kSlotHash; i += 64) hash[i] = make_int2(-1, -1);
+  for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += kCommitThreads) {
+    const int32_t p = i / KS_QUOTA_DIMS, dd = i - p * KS_QUOTA_DIMS;
+    pqreq[i] = a.pq.req[dd][cursor0 + p];
+  }
+  {
+    const int64_t* src = reinterpret_cast<const int64_t*>(a.pods + cursor0);
+    int64_t* dst = reinterpret_cast<int64_t*>(spods);
+    const int32_t words = np * (int32_t)(sizeof(PodRec) / 8);
+    for (int32_t i = tid; i < words; i += kCommitThreads) dst[i] = src[i];
+  }
+  for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
+  // raw row of every pod's snapshot-best node (the monotone fast path's winner): all loads in flight together
+  for (int32_t i = tid; i < np * RF_N; i += kCommitThreads) {
+    const int32_t p = i / RF_N, f = i - p * RF_N;
+    const uint64_t top = a.cand_top[p];
+    if (top) {
+      const RowCol rc = a.rowcols[f];
+      rawtop[p * 32 + f] = load_field(rc.p, rc.width, gkey_node(top));
+    }
+  }
   if (QC) {
-    for (int32_t r = lane; r < a.q.q; r += 64) {
+    for (int32_t r = tid; r < a.q.q; r += kCommitThreads) {
       qlds->parent[r] = a.q.parent[r];
       qlds->limit_mask[r] = a.q.limit_mask[r];
       qlds->min_mask[r] = a.q.min_mask[r];
     }
-    for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
+    for (int32_t i = tid; i < a.q.q * KS_QUOTA_DIMS; i += kCommitThreads) {
       qlds->limit[i] = a.q.limit[i];
       qlds->used[i] = a.q.used[i];
       qlds->min[i] = a.q.min[i];
       qlds->npused[i] = a.q.npused[i];
     }
   }
-  __syncthreads();
-  // predicted winners of each pod (lane = pod) = its two best snapshot candidates; rows to LDS
-  int32_t pnode0 = -1, pnode1 = -1;
-  uint64_t pkey0 = 0;
-  if (lane < np) {
-    const int32_t cnt = sm.cand_count[lane];
-    uint64_t b0 = 0, b1 = 0;
-    for (int32_t k = 0; k < cnt; ++k) {
-      const uint64_t g = local_gkey(cand_t[lane * K + k].x, cand_chunk[lane * K + k]);
-      if (g > b0) {
-        b1 = b0;
-        b0 = g;
-      } else if (g > b1) {
-        b1 = g;
-      }
-    }
-    pnode0 = b0 ? (int32_t)gkey_node(b0) : -1;
-    pnode1 = b1 ? (int32_t)gkey_node(b1) : -1;
-    pkey0 = b0;
-    if (pnode0 >= 0) load_node<NSC>(a.d, pnode0, 1, sm.pred[0][lane]);
-    if (pnode1 >= 0) load_node<NSC>(a.d, pnode1, 1, sm.pred[1][lane]);
+  // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
+  int32_t my_cnt = 0, my_quota = -1;
+  uint32_t my_flags = 0, my_pmask = 0;
+  uint64_t my_bound = 0, my_top = 0;
+  if (tid < 64 && lane < np) {
+    my_cnt = a.cand_count[lane];
+    my_bound = a.cand_bound[lane];
+    my_top = a.cand_top[lane];
+    my_pmask = a.pq.mask[cursor0 + lane];
+    my_quota = a.pods[cursor0 + lane].quota;
+    my_flags = a.pods[cursor0 + lane].flags;
+  }
+  // lane f < RF_N: the column of row field f
+  const void* my_col = nullptr;
+  int32_t my_w = 8;
+  if (tid < RF_N) {
+    my_col = a.rowcols[lane].p;
+    my_w = a.rowcols[lane].width;
   }
   __syncthreads();
+  if (tid >= 64) return;  // waves 1-3 are done; wave 0 runs the sequential loop alone
   KS_STAMP(0);
+  // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
+  // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
+  Cfg cfg = a.c;
+  {
+    int32_t* w = reinterpret_cast<int32_t*>(&cfg);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(Cfg) / 4); ++i) asm volatile("" : "+s"(w[i]));
+  }
 
-  // slot s lives in lane s's registers: the current row of the s-th node touched in this pass
-  NodeReg<NSC> srow;
-  int32_t snode = -1;
+  // ---- per-lane roles in slot construction and Reserve (lane t < ST_N: term t; ST_N.. : headrooms) ----
+  // term t: capacity / requested raw fields, and the PodRec words of its Reserve delta (x1, x100)
+  int32_t t_cap = 0, t_req = 0, t_pw = -1, t_pw100 = -1;
+  bool t_prod_only = false;
+  switch (lane) {
+    case ST_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_NZ_CPU; t_pw = 3; t_pw100 = 12; break;
+    case ST_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_NZ_MEM; t_pw = 4; t_pw100 = 13; break;
+    case ST_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 14; break;
+    case ST_SC + 0: case ST_SC + 1: case ST_SC + 2: case ST_SC + 3:
+      t_cap = RF_ALLOC_SC + (lane - ST_SC); t_req = RF_REQ_SC + (lane - ST_SC); t_pw = 7 + (lane - ST_SC); t_pw100 = 17 + (lane - ST_SC); break;
+    case ST_LCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_TERM_CPU; t_pw = 5; t_pw100 = 15; break;
+    case ST_LMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_TERM_MEM; t_pw = 6; t_pw100 = 16; break;
+    case ST_PLCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_PTERM_CPU; t_pw = 5; t_pw100 = 15; t_prod_only = true; break;
+    case ST_PLMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_PTERM_MEM; t_pw = 6; t_pw100 = 16; t_prod_only = true; break;
+    default: break;
+  }
+  // headroom lane ST_N + i: free[i] = alloc - Requested, Reserve subtracts the pod's raw request
+  const int32_t fi = lane - ST_N;
+  int32_t f_alloc = 0, f_req = 0, f_pw = 0;
+  switch (fi) {
+    case SF_CPU: f_alloc = RF_ALLOC_CPU; f_req = RF_REQ_CPU; f_pw = 0; break;
+    case SF_MEM: f_alloc = RF_ALLOC_MEM; f_req = RF_REQ_MEM; f_pw = 1; break;
+    case SF_EPH: f_alloc = RF_ALLOC_EPH; f_req = RF_REQ_EPH; f_pw = 2; break;
+    case SF_SC + 0: case SF_SC + 1: case SF_SC + 2: case SF_SC + 3:
+      f_alloc = RF_ALLOC_SC + (fi - SF_SC); f_req = RF_REQ_SC + (fi - SF_SC); f_pw = 7 + (fi - SF_SC); break;
+    default: break;
+  }
+  constexpr int kLaneCounts = ST_N + SF_N;  // lane: pod count / flags of the row
+  const bool monotone = cfg.monotone != 0;
+
+  int32_t snode = -1;  // lane s: node of slot s
   int32_t nslots = 0;
   int32_t processed = np;
-  unsigned long long rescans = 0, misses = 0;
-  for (int32_t j = 0; j < np; ++j) {
-    const PodRec pod = sm.pods[j];
-    const bool has_quota = a.c.quota_enable && pod.quota >= 0;
-    const uint32_t pmask = sm.pq_mask[j];
-    const int64_t qreq = sm.pq_req[j][lane & (KS_QUOTA_DIMS - 1)];
-    if (has_quota) {
-      const uint32_t st =
-          QC ? quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
-                           qlds->npused, a.c.quota_parent, pod.quota, pod.flags, pmask, qreq)
-             : quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
-                           a.c.quota_parent, pod.quota, pod.flags, pmask, qreq);
-      if (st) {
-        if (lane == 0) sm.res[j] = ks_result{-1, st, 0};
-        KS_STAMP(1);
-        continue;
-      }
-    }
-    KS_STAMP(1);
-    const int32_t b0 = __builtin_amdgcn_readlane(pnode0, j);
-    uint64_t best = 0;
-    bool resolved = false;
-    if (a.c.monotone) {
-      // Monotone profiles: a commit can only lower a node's key, so the pod's snapshot-best node is
-      // still the exact argmax whenever no earlier pod of this pass touched it.
-      if (b0 < 0) {
-        resolved = true;  // nothing feasible in the snapshot, and nothing can become feasible
-      } else if (!((touched[b0 >> 6] >> (b0 & 63)) & 1ull)) {
-        best = readlane64(pkey0, j);
-        resolved = true;
-      }
-    }
-    if (!resolved) {
-      // nodes touched earlier in this pass: exact current keys from their slot registers
-      uint64_t key_mod = 0;
-      if (lane < nslots) {
-        const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, srow);
-        key_mod = o.reasons ? 0ull : gkey(o.total, snode);
-      }
-      KS_STAMP(2);
-      // untouched nodes: chunk best / runner-up from the snapshot
-      const int32_t cnt = sm.cand_count[j];
-      const bool valid = lane < cnt;
-      const uint32_t chunk = valid ? cand_chunk[j * K + lane] : 0u;
-      const uint2 t = valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
-      const uint64_t tm = valid ? touched[chunk] : 0ull;
-      uint64_t u = local_gkey(t.x, chunk), ub = 0;
-      bool exact = valid;
-      if (valid && ((tm >> (63 - (t.x & 63u))) & 1ull)) {    // best node touched
-        if (t.y == 0) {
-          u = 0;                                             // no other feasible node in the chunk
-        } else if (!((tm >> (63 - (t.y & 63u))) & 1ull)) {
-          u = local_gkey(t.y, chunk);                        // runner-up untouched: exact
-        } else {
-          exact = false;                                     // both touched: < runner-up, unknown
-          ub = local_gkey(t.y, chunk);
-          u = 0;
+  uint32_t rescans = 0, misses = 0, fast = 0;
+  // speculative raw row of the next pod's best untouched candidate (lane f = field f)
+  int64_t spec_val = 0;
+  int32_t spec_node = -1;
+
+  auto admit = [&](int32_t j) -> uint32_t {
+    const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
+    if (!cfg.quota_enable || qrow < 0) return 0u;
+    const uint32_t flags = __builtin_amdgcn_readlane(my_flags, j);
+    const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
+    const int64_t req = pqreq[j * KS_QUOTA_DIMS + (lane & (KS_QUOTA_DIMS - 1))];
+    return QC ? quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
+                            qlds->npused, cfg.quota_parent, qrow, flags, pmask, req)
+              : quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
+                            cfg.quota_parent, qrow, flags, pmask, req);
+  };
+  uint32_t st_next = 0;
+  Cands cn{};
+  auto lookahead = [&](int32_t j) {
+    st_next = admit(j);
+    if (st_next) return;
+    if (monotone) {
+      const uint64_t top = readlane64(my_top, j);
+      if (top != 0) {
+        const int32_t tn = (int32_t)gkey_node(top);
+        if (!((touched[tn >> 6] >> (tn & 63)) & 1ull)) {
+          cn.fast = true;  // its row is in rawtop[j]
+          cn.umax = top;
+          return;
         }
       }
-      best = wave_max_u64(umax64(exact ? u : 0ull, key_mod));
-      uint64_t need = __ballot(!exact && valid && ub > best);
+    }
+    cn = resolve_cands(cand_chunk, cand_t, touched, j, K, __builtin_amdgcn_readlane(my_cnt, j));
+#ifndef KS_NO_SPEC
+    if (cn.umax) {
+      const int32_t node = (int32_t)gkey_node(cn.umax);
+      if (node != spec_node) {
+        spec_node = node;
+        if (lane < RF_N) spec_val = load_field(my_col, my_w, node);
+      }
+    }
+#endif
+  };
+  lookahead(0);
+  KS_STAMP(1);
+
+  for (int32_t j = 0; j < np; ++j) {
+    const uint32_t st = st_next;
+    const Cands cj = cn;
+    if (st) {
+      if (lane == 0) sres[j] = ks_result{-1, st, 0};
+      goto next_pod;
+    }
+    {
+    uint64_t best;
+    if (cj.fast) {
+      best = cj.umax;  // the snapshot-best node is untouched: commits only lower keys, so it wins
+      ++fast;
+      KS_STAMP(2);
+    } else {
+      // pod j: LDS broadcast into VGPRs; flags scalar so the plugin branches stay wave-uniform
+      PodRec pod = spods[j];
+      pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
+      // ---- every touched node exactly (lane = slot), untouched from the candidates ----
+      uint64_t key_mod = 0;
+      if (lane < nslots) {
+        NodeReg<NSC> r;
+        slot_to_reg<NSC>(rows[lane], r);
+        const EvalOut o = eval_pod_node<NSC, false>(cfg, pod, r);
+        key_mod = o.reasons ? 0ull : gkey(o.total, snode);
+      }
+      best = umax64(cj.umax, wave_max_u64(key_mod));
+      KS_STAMP(2);
+      uint64_t need = __ballot(!cj.exact && cj.valid && cj.ub > best);
       while (need) {
-        const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? ub : 0ull);
-        const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && ub == kmax)) - 1;
-        const int64_t c = (int64_t)(uint32_t)__shfl((int)chunk, sel, 64);
-        const uint64_t v = rescan_chunk<NSC>(a, hash, srow, pod, c, touched[c]);
+        const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? cj.ub : 0ull);
+        const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && cj.ub == kmax)) - 1;
+        const int64_t c = (int64_t)(uint32_t)__shfl((int)cj.chunk, sel, 64);
+        const uint64_t v = rescan_untouched<NSC>(a, cfg, pod, c, touched[c]);
         ++rescans;
         best = umax64(best, v);
         need &= ~(1ull << sel);
-        need &= __ballot(ub > best);
+        need &= __ballot(cj.ub > best);
       }
-      KS_STAMP(3);
-      if (cnt == K && best < sm.cand_bound[j]) {
-        processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep
+      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, j);
+      if (cnt == K && best < readlane64(my_bound, j)) {
+        processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep from j
         break;
       }
+      KS_STAMP(3);
     }
     if (best == 0) {
-      if (lane == 0) sm.res[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0};
-      continue;
+      if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0};
+      goto next_pod;
     }
-    const int64_t node = gkey_node(best);
+    const int32_t node = (int32_t)gkey_node(best);
     const int64_t score = gkey_score(best);
-    int32_t s = __ffsll((long long)__ballot(snode == (int32_t)node)) - 1;
+    const uint32_t pflags = __builtin_amdgcn_readlane(my_flags, j);
+    const int64_t* podw = reinterpret_cast<const int64_t*>(&spods[j]);
+    // ---- Reserve: NodeInfo.AddPod + podAssignCache.assign on the slot row (lane = term) ----
+    int32_t s = __ffsll((long long)__ballot(snode == node)) - 1;
+    SlotRow* row;
     if (s < 0) {
       s = nslots++;
-      if (b0 == (int32_t)node) {
-        if (lane == s) srow = sm.pred[0][j];
-      } else if (__builtin_amdgcn_readlane(pnode1, j) == (int32_t)node) {
-        if (lane == s) srow = sm.pred[1][j];
+      row = &rows[s];
+      const int64_t* src = raw;
+      if (node == (int32_t)gkey_node(readlane64(my_top, j))) {
+        src = rawtop + j * 32;  // prefetched at pass start
       } else {
-        ++misses;
-        if (lane == s) load_node<NSC>(a.d, node, 1, srow);
+        int64_t v = spec_val;
+        if (node != spec_node) {
+          ++misses;
+          if (lane < RF_N) v = load_field(my_col, my_w, node);
+        }
+        if (lane < RF_N) raw[lane] = v;
       }
-      if (lane == s) snode = (int32_t)node;
-      if (lane == 0) {
-        atomicOr(&touched[node >> 6], 1ull << (node & 63));
-        hash_insert(hash, node, s);
+      if (lane == s) snode = node;
+      if (lane == 0) touched[node >> 6] |= 1ull << (node & 63);
+      // build the slot row with the pod already reserved on it (lane-parallel)
+      if (lane < ST_N) {
+        Term t;
+        const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+        term_set(t, src[t_cap], src[t_req] + (take ? podw[t_pw] : 0));
+        row->t[lane] = t;
+      } else if (lane < ST_N + SF_N) {
+        row->free[fi] = src[f_alloc] - src[f_req] - podw[f_pw];
+      } else if (lane == kLaneCounts) {
+        const int32_t allowed = (int32_t)src[RF_ALLOWED];
+        const int32_t pc = (int32_t)src[RF_POD_COUNT] + 1;
+        row->la_bits = (uint32_t)src[RF_LA_BITS];
+        row->allowed = allowed;
+        row->pod_count = pc;
+        row->pods_full = (int64_t)pc + 1 > (int64_t)allowed;
+        row->valid = 1;
+        row->fit_ws = (src[RF_ALLOC_CPU] != 0 ? cfg.fw_cpu : 0) + (src[RF_ALLOC_MEM] != 0 ? cfg.fw_mem : 0) +
+                      (src[RF_ALLOC_EPH] != 0 ? cfg.fw_eph : 0);
+      }
+    } else {
+      row = &rows[s];
+      if (lane < ST_N) {
+        if (!t_prod_only || (pflags & KS_POD_PROD)) term_take(row->t[lane], podw[t_pw], podw[t_pw100]);
+      } else if (lane < ST_N + SF_N) {
+        row->free[fi] -= podw[f_pw];
+      } else if (lane == kLaneCounts) {
+        const int32_t pc = row->pod_count + 1;
+        row->pod_count = pc;
+        row->pods_full = (int64_t)pc + 1 > (int64_t)row->allowed;
       }
     }
-    // Reserve on the slot's registers: NodeInfo.AddPod + podAssignCache.assign
-    if (lane == s) reserve_row<NSC>(srow, pod);
-    if (lane == 0) sm.res[j] = ks_result{(int32_t)node, KS_S_SCHEDULED, score};
-    if (has_quota && lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u)) {
-      // updatePodUsedNoLock -> updateGroupDeltaUsedNoLock (group_quota_manager.go:620-655)
-      if (QC) {
-        for (int32_t cur = pod.quota; cur >= 0; cur = qlds->parent[cur]) {
-          qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
-          if (pod.flags & KS_POD_NONPREEMPTIBLE) qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
-        }
-      } else {
-        for (int32_t cur = pod.quota; cur >= 0; cur = a.q.parent[cur]) {
-          a.q.used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
-          if (pod.flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score};
+    {
+      const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
+      if (cfg.quota_enable && qrow >= 0) {
+        const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
+        if (lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u)) {
+          // updatePodUsedNoLock -> updateGroupDeltaUsedNoLock (group_quota_manager.go:620-655)
+          const int64_t qreq = pqreq[j * KS_QUOTA_DIMS + lane];
+          const bool np_ = (pflags & KS_POD_NONPREEMPTIBLE) != 0;
+          if (QC) {
+            for (int32_t cur = qrow; cur >= 0; cur = qlds->parent[cur]) {
+              qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+              if (np_) qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+            }
+          } else {
+            for (int32_t cur = qrow; cur >= 0; cur = a.q.parent[cur]) {
+              a.q.used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+              if (np_) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+            }
+          }
         }
       }
     }
     KS_STAMP(4);
+    }
+  next_pod:
+    if (j + 1 < np) lookahead(j + 1);
+    KS_STAMP(1);
   }
-  __syncthreads();
   KS_STAMP(5);
-  // ---- write back results, touched nodes and quota usage ----
-  if (lane < processed) a.results[cursor0 + lane] = sm.res[lane];
+  // ---- write back: results, touched rows, quota usage ----
+  if (lane < processed) a.results[cursor0 + lane] = sres[lane];
   if (lane < nslots) {
+    const DevNodes d = *a.dn;
+    const SlotRow& r = rows[lane];
     const int64_t node = snode;
-    a.d.req_cpu[node] = srow.alloc_cpu - srow.free_cpu;
-    a.d.req_mem[node] = srow.alloc_mem - srow.free_mem;
-    a.d.req_eph[node] = srow.req_eph;
-    a.d.nz_cpu[node] = srow.nz_cpu;
-    a.d.nz_mem[node] = srow.nz_mem;
+    gst(d.req_cpu + node, r.t[ST_CPU].c - r.free[SF_CPU]);
+    gst(d.req_mem + node, r.t[ST_MEM].c - r.free[SF_MEM]);
+    gst(d.req_eph + node, r.t[ST_EPH].c - r.free[SF_EPH]);
+    gst(d.nz_cpu + node, term_requested(r.t[ST_CPU]));
+    gst(d.nz_mem + node, term_requested(r.t[ST_MEM]));
 #pragma unroll
-    for (int k = 0; k < NSC; ++k) a.d.req_sc[k][node] = srow.req_sc[k];
-    a.d.pod_count[node] = srow.pod_count;
-    a.d.la_term_cpu[node] = srow.term_cpu;
-    a.d.la_term_mem[node] = srow.term_mem;
-    a.d.la_pterm_cpu[node] = srow.pterm_cpu;
-    a.d.la_pterm_mem[node] = srow.pterm_mem;
+    for (int k = 0; k < KS_MAX_SCALARS; ++k) gst(d.req_sc[k] + node, r.t[ST_SC + k].c - r.free[SF_SC + k]);
+    gst(d.pod_count + node, r.pod_count);
+    gst(d.la_term_cpu + node, term_requested(r.t[ST_LCPU]));
+    gst(d.la_term_mem + node, term_requested(r.t[ST_LMEM]));
+    gst(d.la_pterm_cpu + node, term_requested(r.t[ST_PLCPU]));
+    gst(d.la_pterm_mem + node, term_requested(r.t[ST_PLMEM]));
   }
   if (QC) {
     for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
@@ -669,8 +845,9 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs a) {
     *a.cursor = cursor0 + processed;
     atomicAdd(&a.counters[0], 1ull);
     if (processed < np) atomicAdd(&a.counters[1], 1ull);
-    atomicAdd(&a.counters[2], rescans);
-    atomicAdd(&a.counters[3], misses);
+    atomicAdd(&a.counters[2], (unsigned long long)rescans);
+    atomicAdd(&a.counters[3], (unsigned long long)misses);
+    atomicAdd(&a.counters[14], (unsigned long long)fast);  // ks_stats.diag[6]: monotone fast picks
 #ifdef KS_COMMIT_STAMPS
     for (int i = 0; i < 6; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
 #endif
@@ -688,7 +865,7 @@ __global__ void eval_debug_kernel(DevNodes d, Cfg c, const PodRec* pod, int64_t 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   NodeReg<NSC> r;
-  load_node<NSC>(d, i, 1, r);
+  load_node<NSC>(c, d, i, 1, r);
   const PodRec p = *pod;
   const EvalOut o = eval_pod_node<NSC, true>(c, p, r);
   reasons[i] = o.reasons;
@@ -758,10 +935,13 @@ struct ks_ctx {
   uint32_t* cand_chunk = nullptr;
   uint2* cand_t = nullptr;
   uint64_t* cand_bound = nullptr;
+  uint64_t* cand_top = nullptr;
   int32_t* cand_count = nullptr;
   int32_t* cursor = nullptr;
   unsigned long long* counters = nullptr;
   int32_t batch = 64, k = 32;
+  RowCol* rowcols = nullptr;  // [RF_N] device column of each slot-row field
+  DevNodes* dnodes = nullptr;  // device copy of d (the hot kernels read column pointers from it)
   // debug
   PodRec* dbg_pod = nullptr;
   // stats
@@ -801,20 +981,18 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.fit_score = c.fit.enable_score;
   k.fit_most = c.fit.strategy == KS_MOST_ALLOCATED;
   k.nsc = nsc;
-  k.fw_cpu = c.fit.weight_cpu;
-  k.fw_mem = c.fit.weight_memory;
-  k.fw_eph = c.fit.weight_ephemeral;
-  for (int i = 0; i < KS_MAX_SCALARS; ++i) k.fw_sc[i] = c.fit.weight_scalar[i];
-  k.fit_pw = c.fit.plugin_weight;
+  k.fw_cpu = (int32_t)c.fit.weight_cpu;
+  k.fw_mem = (int32_t)c.fit.weight_memory;
+  k.fw_eph = (int32_t)c.fit.weight_ephemeral;
+  for (int i = 0; i < KS_MAX_SCALARS; ++i) k.fw_sc[i] = (int32_t)c.fit.weight_scalar[i];
+  k.fit_pw = (int32_t)c.fit.plugin_weight;
   k.la_filter = c.loadaware.enable_filter;
   k.la_score = c.loadaware.enable_score;
   k.la_filter_expired = c.loadaware.filter_expired_node_metrics;
   k.la_prod_usage = c.loadaware.score_according_prod_usage;
-  k.lw_cpu = c.loadaware.weight_cpu;
-  k.lw_mem = c.loadaware.weight_memory;
-  k.la_pw = c.loadaware.plugin_weight;
-  k.scaling_cpu = c.loadaware.scaling_cpu;
-  k.scaling_mem = c.loadaware.scaling_memory;
+  k.lw_cpu = (int32_t)c.loadaware.weight_cpu;
+  k.lw_mem = (int32_t)c.loadaware.weight_memory;
+  k.la_pw = (int32_t)c.loadaware.plugin_weight;
   k.quota_enable = c.quota.enable;
   k.quota_parent = c.quota.enable_check_parent_quota;
   // LeastAllocated Fit + LoadAware: a commit only raises requested/estimated usage, so a node's
@@ -842,6 +1020,17 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
       (la.enable_score && la.weight_cpu + la.weight_memory == 0)) {
     g_create_error = "ks_create: LoadAware resource weights must be in [1,100] (validation_pluginargs.go:60-70)";
     return KS_EINVAL;
+  }
+  {
+    // upstream ValidateNodeResourcesFitArgs: every listed resource weight in [1, 100] (0 = not listed)
+    const ks_fit_args& fa = cfg->fit;
+    bool ok = fa.weight_cpu >= 0 && fa.weight_cpu <= 100 && fa.weight_memory >= 0 && fa.weight_memory <= 100 &&
+              fa.weight_ephemeral >= 0 && fa.weight_ephemeral <= 100;
+    for (int k = 0; k < KS_MAX_SCALARS; ++k) ok = ok && fa.weight_scalar[k] >= 0 && fa.weight_scalar[k] <= 100;
+    if (!ok) {
+      g_create_error = "ks_create: NodeResourcesFit resource weights must be in [1,100] (upstream ValidateNodeResourcesFitArgs)";
+      return KS_EINVAL;
+    }
   }
   const int64_t max_total = 100 * (std::max<int64_t>(cfg->fit.plugin_weight, 0) +
                                    std::max<int64_t>(cfg->loadaware.plugin_weight, 0));
@@ -876,6 +1065,8 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->cand_t = (uint2*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_bound = (uint64_t*)p;
+  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  ctx->cand_top = (uint64_t*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_count = (int32_t*)p;
   if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
@@ -904,10 +1095,13 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->cand_chunk; dev_free(p);
   p = ctx->cand_t; dev_free(p);
   p = ctx->cand_bound; dev_free(p);
+  p = ctx->cand_top; dev_free(p);
   p = ctx->cand_count; dev_free(p);
   p = ctx->cursor; dev_free(p);
   p = ctx->counters; dev_free(p);
   p = ctx->dbg_pod; dev_free(p);
+  p = ctx->rowcols; dev_free(p);
+  p = ctx->dnodes; dev_free(p);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1012,6 +1206,46 @@ static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
   return KS_OK;
 }
 
+// Device table of the slot-row fields' columns (RowField order), read by the commit kernel.
+static int upload_rowcols(ks_ctx* ctx) {
+  const DevNodes& d = ctx->d;
+  RowCol h[RF_N] = {};
+  auto set = [&](int f, const void* p, int w) { h[f].p = p; h[f].width = w; };
+  set(RF_REQ_CPU, d.req_cpu, 8);
+  set(RF_REQ_MEM, d.req_mem, 8);
+  set(RF_REQ_EPH, d.req_eph, 8);
+  set(RF_NZ_CPU, d.nz_cpu, 8);
+  set(RF_NZ_MEM, d.nz_mem, 8);
+  for (int k = 0; k < 4; ++k) set(RF_REQ_SC + k, d.req_sc[k], 8);
+  set(RF_TERM_CPU, d.la_term_cpu, 8);
+  set(RF_TERM_MEM, d.la_term_mem, 8);
+  set(RF_PTERM_CPU, d.la_pterm_cpu, 8);
+  set(RF_PTERM_MEM, d.la_pterm_mem, 8);
+  set(RF_POD_COUNT, d.pod_count, 4);
+  set(RF_ALLOC_CPU, d.alloc_cpu, 8);
+  set(RF_ALLOC_MEM, d.alloc_mem, 8);
+  set(RF_ALLOC_EPH, d.alloc_eph, 8);
+  for (int k = 0; k < 4; ++k) set(RF_ALLOC_SC + k, d.alloc_sc[k], 8);
+  set(RF_LA_ALLOC_CPU, d.la_alloc_cpu, 8);
+  set(RF_LA_ALLOC_MEM, d.la_alloc_mem, 8);
+  set(RF_ALLOWED, d.allowed_pods, 4);
+  set(RF_LA_BITS, d.la_bits, 4);
+  if (!ctx->rowcols) {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, sizeof(h)) != KS_OK) return KS_ENOMEM;
+    ctx->rowcols = (RowCol*)p;
+  }
+  if (!ctx->dnodes) {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, sizeof(DevNodes)) != KS_OK) return KS_ENOMEM;
+    ctx->dnodes = (DevNodes*)p;
+  }
+  HIPCHK(ctx, hipMemcpyAsync(ctx->rowcols, h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->dnodes, &ctx->d, sizeof(DevNodes), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
 static int upload_prep_nodes(ks_ctx* ctx) {
   const int threads = 256;
   const int blocks = (int)((ctx->n + threads - 1) / threads);
@@ -1064,6 +1298,7 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   }
   if (dev_alloc(ctx, &p, (size_t)ctx->nchunks * 64 * 8) != KS_OK) return KS_ENOMEM;
   ctx->sweep_out = (uint2*)p;
+  if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
@@ -1296,6 +1531,12 @@ static hipEvent_t take_event(ks_ctx* ctx, size_t i) {
   return ctx->ev_pool[i];
 }
 
+// Quota rows are cached in LDS for the pass when the table is small enough and the LDS image fits.
+static bool commit_qcache(const ks_ctx* ctx) {
+  if (!(ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows)) return false;
+  return commit_layout(ctx->k, ctx->nchunks, true).total <= 160 * 1024;
+}
+
 template <int NSC>
 static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
   auto rec = [&](int kind) {
@@ -1305,7 +1546,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
     evs->push_back({kind, (*evn)++});
   };
   SweepArgs sa;
-  sa.d = ctx->d;
+  sa.dn = ctx->dnodes;
   sa.c = ctx->kc;
   sa.pods = ctx->pods;
   sa.cursor = ctx->cursor;
@@ -1324,6 +1565,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   se.cand_chunk = ctx->cand_chunk;
   se.cand_t = ctx->cand_t;
   se.cand_bound = ctx->cand_bound;
+  se.cand_top = ctx->cand_top;
   se.cand_count = ctx->cand_count;
   se.nchunks = ctx->nchunks;
   se.total_pods = ctx->np;
@@ -1333,7 +1575,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64), 0, ctx->stream, se);
   rec(1);
   CommitArgs ca;
-  ca.d = ctx->d;
+  ca.dn = ctx->dnodes;
   ca.c = ctx->kc;
   ca.pods = ctx->pods;
   ca.pq = ctx->pq;
@@ -1342,6 +1584,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.cand_chunk = ctx->cand_chunk;
   ca.cand_t = ctx->cand_t;
   ca.cand_bound = ctx->cand_bound;
+  ca.cand_top = ctx->cand_top;
   ca.cand_count = ctx->cand_count;
   ca.results = ctx->results;
   ca.counters = ctx->counters;
@@ -1350,13 +1593,14 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.total_pods = ctx->np;
   ca.batch = ctx->batch;
   ca.k = ctx->k;
-  const bool qcache = ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows;
-  const size_t smem = commit_layout<NSC>(ctx->k, ctx->nchunks, qcache).total;
+  ca.rowcols = ctx->rowcols;
+  const bool qcache = commit_qcache(ctx);
+  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache).total;
   rec(2);
   if (qcache)
-    hipLaunchKernelGGL((commit_kernel<NSC, true>), dim3(1), dim3(64), smem, ctx->stream, ca);
+    hipLaunchKernelGGL((commit_kernel<NSC, true>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
   else
-    hipLaunchKernelGGL((commit_kernel<NSC, false>), dim3(1), dim3(64), smem, ctx->stream, ca);
+    hipLaunchKernelGGL((commit_kernel<NSC, false>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
   rec(2);
 }
 
@@ -1367,23 +1611,17 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   const int32_t np = ctx->np;
   if (np == 0) return KS_OK;
   {
-    const bool qcache = ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows;
-    size_t smem = 0;
+    const bool qcache = commit_qcache(ctx);
+    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache).total;
+    if (smem > 160 * 1024)
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
     hipError_t e = hipSuccess;
-    auto setattr = [&](const void* fn, size_t bytes) {
-      if (e == hipSuccess) e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    auto setattr = [&](const void* fn) {
+      if (e == hipSuccess) e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     };
-    switch (ctx->nsc) {
-      case 0: smem = commit_layout<0>(ctx->k, ctx->nchunks, qcache).total; break;
-      case 2: smem = commit_layout<2>(ctx->k, ctx->nchunks, qcache).total; break;
-      default: smem = commit_layout<4>(ctx->k, ctx->nchunks, qcache).total; break;
-    }
-    if (smem <= 160 * 1024) {
-      if (ctx->nsc == 0) qcache ? setattr((const void*)commit_kernel<0, true>, smem) : setattr((const void*)commit_kernel<0, false>, smem);
-      else if (ctx->nsc == 2) qcache ? setattr((const void*)commit_kernel<2, true>, smem) : setattr((const void*)commit_kernel<2, false>, smem);
-      else qcache ? setattr((const void*)commit_kernel<4, true>, smem) : setattr((const void*)commit_kernel<4, false>, smem);
-    }
-    if (smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes)", (long long)ctx->n);
+    if (ctx->nsc == 0) qcache ? setattr((const void*)commit_kernel<0, true>) : setattr((const void*)commit_kernel<0, false>);
+    else if (ctx->nsc == 2) qcache ? setattr((const void*)commit_kernel<2, true>) : setattr((const void*)commit_kernel<2, false>);
+    else qcache ? setattr((const void*)commit_kernel<4, true>) : setattr((const void*)commit_kernel<4, false>);
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
   }
   // pods per wave: aim for >= ~4096 waves per sweep

@@ -40,13 +40,13 @@ constexpr uint32_t kLaFailProd = 0x4u;      // Filter fails for prod pods when p
 constexpr int kLaReasonNonProdShift = 8;    // KS_R_LA_* reason bits for the non-prod case
 constexpr int kLaReasonProdShift = 20;      // KS_R_LA_* reason bits for the prod case
 
-// Kernel-constant view of ks_config.
+// Kernel-constant view of ks_config (int32: weights are validated to small ranges in ks_create,
+// which keeps the sweep's SGPR footprint small).
 struct Cfg {
   int32_t fit_filter, fit_score, fit_most, nsc;
-  int64_t fw_cpu, fw_mem, fw_eph, fw_sc[KS_MAX_SCALARS], fit_pw;
+  int32_t fw_cpu, fw_mem, fw_eph, fw_sc[KS_MAX_SCALARS], fit_pw;
   int32_t la_filter, la_score, la_filter_expired, la_prod_usage;
-  int64_t lw_cpu, lw_mem, la_pw;
-  int64_t scaling_cpu, scaling_mem;
+  int32_t lw_cpu, lw_mem, la_pw;
   int32_t quota_enable, quota_parent;
   int32_t monotone;  // commits can only lower a node's key (LeastAllocated + LoadAware)
 };
@@ -67,15 +67,57 @@ struct DevNodes {
   uint32_t *la_bits;  // derived by prep_nodes_kernel
 };
 
-// Per-pod record read by the sweep with scalar loads (AoS, 128 B).
+// Per-pod record read by the sweep with scalar loads (AoS, 192 B).  The x100 and f32 copies feed
+// the exact score terms (see term_least below).
 struct __attribute__((aligned(16))) PodRec {
-  int64_t cpu, mem, eph, nzcpu, nzmem, est_cpu, est_mem;
-  int64_t sc[KS_MAX_SCALARS];
-  uint32_t flags;
-  int32_t quota;
-  int64_t _pad[3];
+  int64_t cpu, mem, eph, nzcpu, nzmem, est_cpu, est_mem;  // words 0..6
+  int64_t sc[KS_MAX_SCALARS];                              // words 7..10
+  uint32_t flags;                                          // word 11 (lo)
+  int32_t quota;                                           // word 11 (hi)
+  // 100 x the score-term requests (nzcpu, nzmem, eph, est_cpu, est_mem, sc[k])
+  int64_t h_nzcpu, h_nzmem, h_eph, h_est_cpu, h_est_mem;   // words 12..16
+  int64_t h_sc[KS_MAX_SCALARS];                            // words 17..20
+  float f_nzcpu, f_nzmem, f_eph, f_est_cpu, f_est_mem;     // f32 of the same requests
+  float f_sc[KS_MAX_SCALARS];
+  float _fpad[3];
 };
-static_assert(sizeof(PodRec) == 128, "PodRec must stay 128 B");
+static_assert(sizeof(PodRec) == 224, "PodRec layout");
+
+// Explicit global (addrspace 1) accesses for pointers read from memory: without the cast hipcc
+// emits flat_load, which counts on lgkmcnt too, so every later LDS wait would also wait for the
+// HBM load (the commit kernel overlaps its row prefetch with LDS work).
+template <typename T>
+__device__ __forceinline__ T gld(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(const __attribute__((address_space(1))) T*)p;
+#else
+  return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void gst(T* p, T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *(__attribute__((address_space(1))) T*)p = v;
+#else
+  *p = v;
+#endif
+}
+
+// Wave-uniform pod record through the constant address space: the compiler emits scalar loads
+// (s_load) into SGPRs, so every branch on pod fields is a scalar branch.
+__device__ __forceinline__ PodRec load_pod_uniform(const PodRec* p) {
+  PodRec r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) int64_t* ConstWords;
+  const ConstWords src = (ConstWords)p;
+  int64_t* dst = reinterpret_cast<int64_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(PodRec) / 8); ++i) dst[i] = src[i];
+#else
+  r = *p;
+#endif
+  return r;
+}
 
 // Quota request columns for the commit kernel (SoA).
 struct DevPodQuota {
@@ -90,58 +132,93 @@ struct DevQuotas {
   int64_t *limit, *used, *min, *npused;  // [q][KS_QUOTA_DIMS]
 };
 
-// One node in registers, with node-only precomputation done once per pass.
+// One score term's node side: capacity c, headroom h = c - requested_on_node, and the derived
+// 100*h, f32(h), 100/c used by term_least / term_most.  For c == 0 the headroom is offset by
+// -2^62 so the term scores 0 without a branch (leastRequestedScore's capacity == 0 case) while
+// the requested value stays recoverable (term_requested).
+struct Term {
+  int64_t c, h, h100;
+  float fh, rcp;
+};
+
+__device__ __forceinline__ float i64_to_f32(int64_t v) {
+  // |v| < 2^62: hi part exact in f32 up to 2^24, the sum within 2^-23 relative
+  return __builtin_fmaf((float)(int32_t)(v >> 32), 4294967296.0f, (float)(uint32_t)v);
+}
+
+__device__ __forceinline__ float rcp100(int64_t cap) {
+  // ~100 / cap in f32 (v_rcp_f32, 1 ulp); cap == 0 never reaches a divide (guarded by callers).
+  return cap > 0 ? 100.0f * __builtin_amdgcn_rcpf(i64_to_f32(cap)) : 0.0f;
+}
+
+constexpr int64_t kNoCap = -((int64_t)1 << 62);
+
+__device__ __forceinline__ void term_set(Term& t, int64_t cap, int64_t requested) {
+  t.c = cap;
+  t.h = cap - requested + (cap != 0 ? 0 : kNoCap);
+  t.h100 = cap != 0 ? (cap - requested) * 100 : 0;
+  t.fh = i64_to_f32(t.h);
+  t.rcp = rcp100(cap);
+}
+
+__device__ __forceinline__ int64_t term_requested(const Term& t) { return t.c - t.h + (t.c != 0 ? 0 : kNoCap); }
+
+// Reserve: the node's requested grows by r (x100 and f32 copies kept in step).
+__device__ __forceinline__ void term_take(Term& t, int64_t r, int64_t r100) {
+  t.h -= r;
+  t.h100 -= r100;
+  t.fh = i64_to_f32(t.h);
+}
+
+// leastRequestedScore(requested = c - h + p, c) (load_aware.go:388-397, least_allocated.go:45-54):
+// 0 if c == 0 or requested > c, else floor((h - p) * 100 / c).  The quotient is estimated in f32
+// (|error| < 1e-4 for 0 <= h - p <= c < 2^56, so the truncated estimate is within one of the
+// floor) and corrected exactly with r = 100(h - p) - q c in int64.  Branch-free.
+__device__ __forceinline__ int32_t term_least(const Term& t, int64_t p, int64_t p100, float fp) {
+  int32_t q = (int32_t)((t.fh - fp) * t.rcp);
+  const int64_t r = t.h100 - (p100 + (int64_t)q * t.c);
+  q += (r >= t.c) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return (t.h >= p) ? q : 0;
+}
+
+// mostRequestedScore(requested, c) (most_allocated.go:50-62): requested clamped to c, then
+// floor(requested * 100 / c); requested = c - (h - p).
+__device__ __forceinline__ int32_t term_most(const Term& t, int64_t p, int64_t p100, float fp) {
+  const bool over = p > t.h;  // requested > capacity: clamp -> 100
+  const int64_t d100 = t.c * 100 - (t.h100 - p100);
+  int32_t q = (int32_t)((i64_to_f32(t.c) - (t.fh - fp)) * t.rcp);
+  const int64_t r = d100 - (int64_t)q * t.c;
+  q += (r >= t.c) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return t.c == 0 ? 0 : (over ? 100 : q);
+}
+
+// One node in registers, with node-only precomputation done once per load.
 template <int NSC>
 struct __attribute__((aligned(16))) NodeReg {
-  int64_t alloc_cpu, alloc_mem, alloc_eph;
-  int64_t free_cpu, free_mem, free_eph;
-  int64_t nz_cpu, nz_mem, req_eph;
-  int64_t alloc_sc[NSC > 0 ? NSC : 1], req_sc[NSC > 0 ? NSC : 1];
-  int64_t la_alloc_cpu, la_alloc_mem, term_cpu, term_mem, pterm_cpu, pterm_mem;
-  float rcp_cpu, rcp_mem, rcp_eph, rcp_lcpu, rcp_lmem;
-  float rcp_sc[NSC > 0 ? NSC : 1];
+  int64_t free_cpu, free_mem, free_eph;       // Allocatable - Requested (Fit Filter)
+  int64_t free_sc[NSC > 0 ? NSC : 1];
+  Term t_cpu, t_mem;                           // Fit cpu/memory: NonZeroRequested (upstream resource_allocation.go)
+  Term t_eph;                                  // Fit ephemeral-storage: Requested
+  Term t_sc[NSC > 0 ? NSC : 1];                // Fit scalars: Requested
+  Term t_lcpu, t_lmem, t_plcpu, t_plmem;       // LoadAware: EstimateNode alloc - node term (all / prod)
   uint32_t la_bits;
+  int32_t fit_ws;                              // Σ weights of cpu/mem/eph terms with capacity != 0
   int32_t pods_full;
   int32_t allowed;
   int32_t pod_count;
   int32_t valid;
 };
 
-__device__ __forceinline__ float rcp100(int64_t cap) {
-  // 100 / cap in f32; cap == 0 never reaches the divide (guarded by callers)
-  uint64_t u = (uint64_t)cap;
-  float f = (float)(uint32_t)(u >> 32) * 4294967296.0f + (float)(uint32_t)u;
-  return cap > 0 ? 100.0f / f : 0.0f;
-}
-
-// floor(d * 100 / cap) for 0 <= d <= cap < 2^56, rcp = rcp100(cap).
-__device__ __forceinline__ int64_t div100(int64_t d, int64_t cap, float rcp) {
-  uint64_t u = (uint64_t)d;
-  float df = (float)(uint32_t)(u >> 32) * 4294967296.0f + (float)(uint32_t)u;
-  int32_t q = (int32_t)(df * rcp);
-  int64_t r = d * 100 - (int64_t)q * cap;
-  q += (r >= cap) ? 1 : 0;
-  q -= (r < 0) ? 1 : 0;
-  return q;
-}
-
-// leastRequestedScore (load_aware.go:388-397; least_allocated.go:45-54)
-__device__ __forceinline__ int64_t least_req(int64_t requested, int64_t cap, float rcp) {
-  if (cap == 0 || requested > cap) return 0;
-  return div100(cap - requested, cap, rcp);
-}
-
-// mostRequestedScore (most_allocated.go:50-62)
-__device__ __forceinline__ int64_t most_req(int64_t requested, int64_t cap, float rcp) {
-  if (cap == 0) return 0;
-  if (requested > cap) requested = cap;
-  return div100(requested, cap, rcp);
+template <int NSC>
+__device__ __forceinline__ int32_t node_fit_ws(const Cfg& c, const NodeReg<NSC>& r) {
+  return (r.t_cpu.c != 0 ? c.fw_cpu : 0) + (r.t_mem.c != 0 ? c.fw_mem : 0) + (r.t_eph.c != 0 ? c.fw_eph : 0);
 }
 
 // exact floor(num / den) for the weighted means of [0,100] scores
 // (0 <= num < 2^24, 0 < den, quotient <= 100): f32 estimate + exact correction
-__device__ __forceinline__ int64_t small_div(int64_t num, int64_t den) {
-  const int32_t n32 = (int32_t)num, d32 = (int32_t)den;
+__device__ __forceinline__ int32_t small_div(int32_t n32, int32_t d32) {
   int32_t q = (int32_t)((float)n32 * __builtin_amdgcn_rcpf((float)d32));
   const int32_t r = n32 - q * d32;
   q += (r >= d32) ? 1 : 0;
@@ -149,41 +226,51 @@ __device__ __forceinline__ int64_t small_div(int64_t num, int64_t den) {
   return q;
 }
 
+// Build a NodeReg from the node's fields (shared by load_node and the commit's raw rows).
 template <int NSC>
-__device__ __forceinline__ void load_node(const DevNodes& d, int64_t n, int valid, NodeReg<NSC>& r) {
+__device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int valid, int64_t alloc_cpu,
+                                          int64_t alloc_mem, int64_t alloc_eph, int64_t req_cpu, int64_t req_mem,
+                                          int64_t req_eph, int64_t nz_cpu, int64_t nz_mem, const int64_t* alloc_sc,
+                                          const int64_t* req_sc, int64_t la_alloc_cpu, int64_t la_alloc_mem,
+                                          int64_t term_cpu, int64_t term_mem, int64_t pterm_cpu, int64_t pterm_mem,
+                                          uint32_t la_bits, int32_t allowed, int32_t pod_count) {
   r.valid = valid;
-  if (!valid) n = 0;
-  r.alloc_cpu = d.alloc_cpu[n];
-  r.alloc_mem = d.alloc_mem[n];
-  r.alloc_eph = d.alloc_eph[n];
-  const int64_t req_cpu = d.req_cpu[n], req_mem = d.req_mem[n];
-  r.req_eph = d.req_eph[n];
-  r.free_cpu = r.alloc_cpu - req_cpu;
-  r.free_mem = r.alloc_mem - req_mem;
-  r.free_eph = r.alloc_eph - r.req_eph;
-  r.allowed = d.allowed_pods[n];
-  r.pod_count = d.pod_count[n];
-  r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !valid;
-  r.nz_cpu = d.nz_cpu[n];
-  r.nz_mem = d.nz_mem[n];
+  r.free_cpu = alloc_cpu - req_cpu;
+  r.free_mem = alloc_mem - req_mem;
+  r.free_eph = alloc_eph - req_eph;
+  term_set(r.t_cpu, alloc_cpu, nz_cpu);
+  term_set(r.t_mem, alloc_mem, nz_mem);
+  term_set(r.t_eph, alloc_eph, req_eph);
 #pragma unroll
   for (int k = 0; k < NSC; ++k) {
-    r.alloc_sc[k] = d.alloc_sc[k][n];
-    r.req_sc[k] = d.req_sc[k][n];
-    r.rcp_sc[k] = rcp100(r.alloc_sc[k]);
+    r.free_sc[k] = alloc_sc[k] - req_sc[k];
+    term_set(r.t_sc[k], alloc_sc[k], req_sc[k]);
   }
-  r.la_bits = d.la_bits[n];
-  r.la_alloc_cpu = d.la_alloc_cpu[n];
-  r.la_alloc_mem = d.la_alloc_mem[n];
-  r.term_cpu = d.la_term_cpu[n];
-  r.term_mem = d.la_term_mem[n];
-  r.pterm_cpu = d.la_pterm_cpu[n];
-  r.pterm_mem = d.la_pterm_mem[n];
-  r.rcp_cpu = rcp100(r.alloc_cpu);
-  r.rcp_mem = rcp100(r.alloc_mem);
-  r.rcp_eph = rcp100(r.alloc_eph);
-  r.rcp_lcpu = rcp100(r.la_alloc_cpu);
-  r.rcp_lmem = rcp100(r.la_alloc_mem);
+  term_set(r.t_lcpu, la_alloc_cpu, term_cpu);
+  term_set(r.t_lmem, la_alloc_mem, term_mem);
+  term_set(r.t_plcpu, la_alloc_cpu, pterm_cpu);
+  term_set(r.t_plmem, la_alloc_mem, pterm_mem);
+  r.la_bits = la_bits;
+  r.allowed = allowed;
+  r.pod_count = pod_count;
+  r.pods_full = ((int64_t)pod_count + 1 > (int64_t)allowed) || !valid;
+  r.fit_ws = node_fit_ws<NSC>(c, r);
+}
+
+template <int NSC>
+__device__ __forceinline__ void load_node(const Cfg& c, const DevNodes& d, int64_t n, int valid, NodeReg<NSC>& r) {
+  if (!valid) n = 0;
+  int64_t asc[NSC > 0 ? NSC : 1], rsc[NSC > 0 ? NSC : 1];
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) {
+    asc[k] = gld(d.alloc_sc[k] + n);
+    rsc[k] = gld(d.req_sc[k] + n);
+  }
+  make_node<NSC>(c, r, valid, gld(d.alloc_cpu + n), gld(d.alloc_mem + n), gld(d.alloc_eph + n), gld(d.req_cpu + n),
+                 gld(d.req_mem + n), gld(d.req_eph + n), gld(d.nz_cpu + n), gld(d.nz_mem + n), asc, rsc,
+                 gld(d.la_alloc_cpu + n), gld(d.la_alloc_mem + n), gld(d.la_term_cpu + n), gld(d.la_term_mem + n),
+                 gld(d.la_pterm_cpu + n), gld(d.la_pterm_mem + n), gld(d.la_bits + n), gld(d.allowed_pods + n),
+                 gld(d.pod_count + n));
 }
 
 // Reserve: NodeInfo.AddPod (upstream framework/types.go) + podAssignCache.assign
@@ -194,94 +281,106 @@ __device__ __forceinline__ void reserve_row(NodeReg<NSC>& r, const PodRec& p) {
   r.free_cpu -= p.cpu;
   r.free_mem -= p.mem;
   r.free_eph -= p.eph;
-  r.req_eph += p.eph;
+  term_take(r.t_cpu, p.nzcpu, p.h_nzcpu);
+  term_take(r.t_mem, p.nzmem, p.h_nzmem);
+  term_take(r.t_eph, p.eph, p.h_eph);
 #pragma unroll
-  for (int k = 0; k < NSC; ++k) r.req_sc[k] += p.sc[k];
-  r.nz_cpu += p.nzcpu;
-  r.nz_mem += p.nzmem;
+  for (int k = 0; k < NSC; ++k) {
+    r.free_sc[k] -= p.sc[k];
+    term_take(r.t_sc[k], p.sc[k], p.h_sc[k]);
+  }
   r.pod_count += 1;
   r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
-  r.term_cpu += p.est_cpu;
-  r.term_mem += p.est_mem;
+  term_take(r.t_lcpu, p.est_cpu, p.h_est_cpu);
+  term_take(r.t_lmem, p.est_mem, p.h_est_mem);
   if (p.flags & KS_POD_PROD) {
-    r.pterm_cpu += p.est_cpu;
-    r.pterm_mem += p.est_mem;
+    term_take(r.t_plcpu, p.est_cpu, p.h_est_cpu);
+    term_take(r.t_plmem, p.est_mem, p.h_est_mem);
   }
 }
 
 struct EvalOut {
   uint32_t reasons;  // KS_R_* (0 = feasible)
-  int64_t fit, la, total;
+  int32_t fit, la, total;
 };
 
-// Filter + Score of one (pod, node).  DEBUG=false computes only what the sweep
-// needs (feasible + total); DEBUG=true also fills reasons and per-plugin scores.
+// Filter + Score of one (pod, node).  DEBUG=false computes feasibility (reasons != 0) and the
+// total without branches on node data; DEBUG=true also fills every reason bit and the
+// per-plugin scores (which it computes for infeasible nodes too; callers mask them).
 template <int NSC, bool DEBUG>
 __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, const NodeReg<NSC>& r) {
   EvalOut o;
-  o.reasons = 0;
-  o.fit = 0;
-  o.la = 0;
-  o.total = 0;
   uint32_t rs = 0;
   if (c.fit_filter) {
-    if (r.pods_full) rs |= KS_R_FIT_PODS;
-    if (!(p.flags & kPodAllZero)) {
-      if (p.cpu > r.free_cpu) rs |= KS_R_FIT_CPU;
-      if (p.mem > r.free_mem) rs |= KS_R_FIT_MEMORY;
-      if (p.eph > r.free_eph) rs |= KS_R_FIT_EPHEMERAL;
+    if (DEBUG) {
+      if (r.pods_full) rs |= KS_R_FIT_PODS;
+      if (!(p.flags & kPodAllZero)) {
+        if (p.cpu > r.free_cpu) rs |= KS_R_FIT_CPU;
+        if (p.mem > r.free_mem) rs |= KS_R_FIT_MEMORY;
+        if (p.eph > r.free_eph) rs |= KS_R_FIT_EPHEMERAL;
 #pragma unroll
-      for (int k = 0; k < NSC; ++k)
-        if (p.sc[k] != 0 && p.sc[k] > r.alloc_sc[k] - r.req_sc[k]) rs |= KS_R_FIT_SCALAR;
+        for (int k = 0; k < NSC; ++k)
+          if (p.sc[k] != 0 && p.sc[k] > r.free_sc[k]) rs |= KS_R_FIT_SCALAR;
+      }
+    } else {
+      bool bad = r.pods_full != 0;
+      if (!(p.flags & kPodAllZero)) {
+        bad |= (p.cpu > r.free_cpu) | (p.mem > r.free_mem) | (p.eph > r.free_eph);
+#pragma unroll
+        for (int k = 0; k < NSC; ++k)
+          if (p.sc[k] != 0) bad |= p.sc[k] > r.free_sc[k];
+      }
+      rs = bad ? KS_R_FIT_PODS : 0u;
     }
-  } else if (!r.valid) {
-    rs |= KS_R_FIT_PODS;
+  } else {
+    rs = r.valid ? 0u : KS_R_FIT_PODS;
   }
   if (c.la_filter && !(p.flags & KS_POD_DAEMONSET)) {
     const bool prod_path = (p.flags & KS_POD_PROD) != 0;
     const uint32_t failbit = prod_path ? kLaFailProd : kLaFailNonProd;
-    if (r.la_bits & failbit) {
-      if (DEBUG)
-        rs |= (r.la_bits >> (prod_path ? kLaReasonProdShift : kLaReasonNonProdShift)) & 0x1ffu;
-      else
-        rs |= KS_R_LA_CPU;
+    if (DEBUG) {
+      if (r.la_bits & failbit) rs |= (r.la_bits >> (prod_path ? kLaReasonProdShift : kLaReasonNonProdShift)) & 0x1ffu;
+    } else {
+      rs |= (r.la_bits & failbit) ? KS_R_LA_CPU : 0u;
     }
   }
   o.reasons = rs;
-  if (!DEBUG && rs) return o;
+  o.fit = 0;
+  o.la = 0;
+  int32_t total = 0;
   if (c.fit_score) {
-    int64_t ns = 0, ws = 0;
-    auto term = [&](int64_t w, int64_t alloc, int64_t req, float rcp) {
-      if (w != 0 && alloc != 0) {
-        ns += (c.fit_most ? most_req(req, alloc, rcp) : least_req(req, alloc, rcp)) * w;
-        ws += w;
+    int32_t ns = 0, ws = r.fit_ws;
+    auto term = [&](int32_t w, const Term& t, int64_t pr, int64_t pr100, float fpr) {
+      if (w != 0) {
+        const int32_t s = c.fit_most ? term_most(t, pr, pr100, fpr) : term_least(t, pr, pr100, fpr);
+        ns += (w == 1) ? s : s * w;
       }
     };
-    term(c.fw_cpu, r.alloc_cpu, r.nz_cpu + p.nzcpu, r.rcp_cpu);
-    term(c.fw_mem, r.alloc_mem, r.nz_mem + p.nzmem, r.rcp_mem);
-    term(c.fw_eph, r.alloc_eph, r.req_eph + p.eph, r.rcp_eph);
+    term(c.fw_cpu, r.t_cpu, p.nzcpu, p.h_nzcpu, p.f_nzcpu);
+    term(c.fw_mem, r.t_mem, p.nzmem, p.h_nzmem, p.f_nzmem);
+    term(c.fw_eph, r.t_eph, p.eph, p.h_eph, p.f_eph);
 #pragma unroll
-    for (int k = 0; k < NSC; ++k)
-      if (p.sc[k] != 0) term(c.fw_sc[k], r.alloc_sc[k], r.req_sc[k] + p.sc[k], r.rcp_sc[k]);
-    o.fit = ws ? small_div(ns, ws) : 0;
-    o.total += o.fit * c.fit_pw;
+    for (int k = 0; k < NSC; ++k) {
+      if (p.sc[k] != 0 && c.fw_sc[k] != 0) {  // scalar skipped when the pod does not request it
+        term(c.fw_sc[k], r.t_sc[k], p.sc[k], p.h_sc[k], p.f_sc[k]);
+        ws += r.t_sc[k].c != 0 ? c.fw_sc[k] : 0;
+      }
+    }
+    o.fit = ws > 0 ? small_div(ns, ws > 0 ? ws : 1) : 0;
+    total += o.fit * c.fit_pw;
   }
-  if (c.la_score && !(r.la_bits & kLaZeroScore)) {
+  if (c.la_score) {
     const bool prod = (p.flags & KS_POD_PROD) && c.la_prod_usage;
-    const int64_t ucpu = p.est_cpu + (prod ? r.pterm_cpu : r.term_cpu);
-    const int64_t umem = p.est_mem + (prod ? r.pterm_mem : r.term_mem);
-    int64_t ns = 0, ws = 0;
-    if (c.lw_cpu) {
-      ns += least_req(ucpu, r.la_alloc_cpu, r.rcp_lcpu) * c.lw_cpu;
-      ws += c.lw_cpu;
-    }
-    if (c.lw_mem) {
-      ns += least_req(umem, r.la_alloc_mem, r.rcp_lmem) * c.lw_mem;
-      ws += c.lw_mem;
-    }
-    o.la = ws ? small_div(ns, ws) : 0;
-    o.total += o.la * c.la_pw;
+    const Term& tc = prod ? r.t_plcpu : r.t_lcpu;
+    const Term& tm = prod ? r.t_plmem : r.t_lmem;
+    int32_t ns = 0;
+    if (c.lw_cpu) ns += term_least(tc, p.est_cpu, p.h_est_cpu, p.f_est_cpu) * c.lw_cpu;
+    if (c.lw_mem) ns += term_least(tm, p.est_mem, p.h_est_mem, p.f_est_mem) * c.lw_mem;
+    const int32_t la = small_div(ns, c.lw_cpu + c.lw_mem);
+    o.la = (r.la_bits & kLaZeroScore) ? 0 : la;
+    total += o.la * c.la_pw;
   }
+  o.total = total;
   return o;
 }
 

@@ -11,8 +11,8 @@ ev.stage(w.pods)
 ev.checkpoint()
 for i in range(3):
     ev.restore(); ev.schedule_staged(); st = ev.stats()
-names = ["prefetch", "quota", "slot_rescore", "candidates+rescans", "commit", "loop_exit"]
+names = ["prefetch", "lookahead(quota+cands)", "slot_eval", "rescans+cut", "reserve", "loop_exit"]
 tot = sum(st["diag"][:6])
-print({k: st[k] for k in ("passes", "cut_passes", "rescans", "slot_misses", "sweep_ms", "select_ms", "commit_ms", "total_ms")})
+print({k: st[k] for k in ("passes", "cut_passes", "rescans", "slot_misses", "sweep_ms", "select_ms", "commit_ms", "total_ms")}, "fast_picks", st["diag"][6])
 for n, v in zip(names, st["diag"][:6]):
     print(f"{n:20s} {v:14d} cycles  {100.0*v/max(tot,1):6.2f}%  {v/10000:10.1f} cyc/pod")
