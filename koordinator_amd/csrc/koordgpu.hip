@@ -142,7 +142,7 @@ struct SweepArgs {
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
-  uint2* __restrict__ out;  // [nchunks][64]: lane p = {best, runner-up} local keys of pod p
+  uint2* __restrict__ out;  // [64 pods][nchunks]: {best, runner-up} local keys (pod-major: select reads a row)
   int64_t n, nchunks;
   int32_t total_pods, batch, ppw;
 };
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       best = (lane == p) ? m1 : best;
       second = (lane == p) ? m2 : second;
     }
-    if (lane >= p0 && lane < p1) a.out[c * 64 + lane] = make_uint2(best, second);
+    if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
   }
 }
 
@@ -205,7 +205,12 @@ __device__ __forceinline__ uint64_t local_gkey(uint32_t loc, int64_t chunk) {
   return ((uint64_t)(loc >> 6) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)node);
 }
 
+// One wave per pod: the pod's row of chunk keys is staged in LDS once (coalesced), then the K-th
+// largest chunk score is found from an LDS histogram (binary search over the LDS copy when the
+// score range exceeds the histogram).
+constexpr int kSelHistBins = 1024;
 __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint2 srow[];  // [nchunks]
   const int lane = threadIdx.x;
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor >= a.total_pods) return;
@@ -213,16 +218,19 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   const int32_t p = blockIdx.x;
   if (p >= np) return;
   const int32_t K = a.k;
+  const uint2* in = a.in + (size_t)p * a.nchunks;
   int32_t cnt = 0;
   uint32_t hmax = 0;
   uint64_t top = 0;
   for (int64_t e = lane; e < a.nchunks; e += 64) {
-    const uint32_t loc = a.in[e * 64 + p].x;
-    const uint32_t h = loc >> 6;
+    const uint2 loc = in[e];
+    srow[e] = loc;
+    const uint32_t h = loc.x >> 6;
     cnt += h != 0;
     hmax = h > hmax ? h : hmax;
-    top = umax64(top, local_gkey(loc, e));
+    top = umax64(top, local_gkey(loc.x, e));
   }
+  __syncthreads();
   cnt = wave_sum_i32(cnt);
   hmax = wave_max_u32(hmax);
   top = wave_max_u64(top);
@@ -230,20 +238,68 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   int32_t need_eq = 0x7fffffff;
   const bool exhaustive = cnt <= K;
   if (!exhaustive) {
-    uint32_t lo = 1, hi = hmax;  // largest t with count(h >= t) >= K
-    while (lo < hi) {
-      const uint32_t mid = lo + (hi - lo + 1) / 2;
-      int32_t c = 0;
-      for (int64_t e = lane; e < a.nchunks; e += 64) c += (a.in[e * 64 + p].x >> 6) >= mid;
-      c = wave_sum_i32(c);
-      if (c >= K) lo = mid;
-      else hi = mid - 1;
+    if (hmax < kSelHistBins) {
+      // histogram of chunk scores (LDS atomics), then the largest t with count(h >= t) >= K by a
+      // suffix scan over the bins (lane l owns bins [l*B, l*B+B))
+      uint32_t* hist = reinterpret_cast<uint32_t*>(srow + a.nchunks);
+      constexpr int B = kSelHistBins / 64;
+#pragma unroll
+      for (int i = 0; i < B; ++i) hist[lane * B + i] = 0u;
+      __syncthreads();
+      for (int64_t e = lane; e < a.nchunks; e += 64) {
+        const uint32_t h = srow[e].x >> 6;
+        if (h) atomicAdd(&hist[h], 1u);
+      }
+      __syncthreads();
+      uint32_t mine[B];
+      uint32_t part = 0;
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        mine[i] = hist[lane * B + i];
+        part += mine[i];
+      }
+      // inclusive suffix sum of the per-lane partials: count of h in bins >= lane*B
+      uint32_t suf = part;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_down(suf, off, 64);
+        suf += (lane + off < 64) ? v : 0u;
+      }
+      // the lane holding t: suf(lane) >= K and suf(lane+1) < K
+      const uint32_t suf_next = suf - part;
+      const bool here = suf >= (uint32_t)K && suf_next < (uint32_t)K;
+      uint32_t tl = 0, gtl = 0;
+      if (here) {
+        uint32_t acc = suf_next;
+        for (int i = B - 1; i >= 0; --i) {
+          if (acc + mine[i] >= (uint32_t)K) {
+            tl = (uint32_t)(lane * B + i);
+            gtl = acc;  // count of h > t
+            break;
+          }
+          acc += mine[i];
+        }
+      }
+      const uint64_t hb = __ballot(here);
+      const int src = __ffsll((long long)hb) - 1;
+      t = (uint32_t)__shfl((int)tl, src, 64);
+      need_eq = K - (int32_t)__shfl((int)gtl, src, 64);
+    } else {
+      uint32_t lo = 1, hi = hmax;  // largest t with count(h >= t) >= K
+      while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo + 1) / 2;
+        int32_t c = 0;
+        for (int64_t e = lane; e < a.nchunks; e += 64) c += (srow[e].x >> 6) >= mid;
+        c = wave_sum_i32(c);
+        if (c >= K) lo = mid;
+        else hi = mid - 1;
+      }
+      t = lo;
+      int32_t gt = 0;
+      for (int64_t e = lane; e < a.nchunks; e += 64) gt += (srow[e].x >> 6) > t;
+      gt = wave_sum_i32(gt);
+      need_eq = K - gt;
     }
-    t = lo;
-    int32_t gt = 0;
-    for (int64_t e = lane; e < a.nchunks; e += 64) gt += (a.in[e * 64 + p].x >> 6) > t;
-    gt = wave_sum_i32(gt);
-    need_eq = K - gt;
   }
   // every h > t, plus the first need_eq entries (chunk order) with h == t
   int32_t base = 0, eq_taken = 0;
@@ -251,7 +307,7 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   for (int64_t e0 = 0; e0 < a.nchunks; e0 += 64) {
     const int64_t e = e0 + lane;
-    const uint2 loc = e < a.nchunks ? a.in[e * 64 + p] : make_uint2(0u, 0u);
+    const uint2 loc = e < a.nchunks ? srow[e] : make_uint2(0u, 0u);
     const uint32_t h = loc.x >> 6;
     const bool is_gt = h > t;
     const bool is_eq = (h == t) && h != 0;
@@ -302,18 +358,21 @@ enum RowField : int {
   RF_N = 25
 };
 
-// slot-row terms and headrooms
-enum SlotTerm : int { ST_CPU = 0, ST_MEM = 1, ST_EPH = 2, ST_SC = 3, ST_LCPU = 7, ST_LMEM = 8, ST_PLCPU = 9, ST_PLMEM = 10, ST_N = 11 };
-enum SlotFree : int { SF_CPU = 0, SF_MEM = 1, SF_EPH = 2, SF_SC = 3, SF_N = 7 };
+// slot-row terms: score terms 0..10, then the Filter headrooms (Allocatable - Requested) stored as
+// Terms too (only .h is read), so building a row and Reserve are one lane-uniform code path
+enum SlotTerm : int {
+  ST_CPU = 0, ST_MEM = 1, ST_EPH = 2, ST_SC = 3, ST_LCPU = 7, ST_LMEM = 8, ST_PLCPU = 9, ST_PLMEM = 10,
+  ST_FREE_CPU = 11, ST_FREE_MEM = 12, ST_FREE_EPH = 13, ST_FREE_SC = 14,  // 14..17
+  ST_N = 18
+};
 
 struct __attribute__((aligned(16))) SlotRow {
-  Term t[12];
-  int64_t free[8];
+  Term t[ST_N];
   uint32_t la_bits;
-  int32_t fit_ws, pods_full, allowed, pod_count, valid;
-  int32_t _pad[14];  // 528 B: consecutive rows start 4 banks apart (lane = slot reads conflict-free)
+  int32_t fit_ws, allowed, pod_count;
 };
-static_assert(sizeof(SlotRow) == 528, "SlotRow layout");
+// 592 B = 37 x 16 B: consecutive rows start 5 x 16 B apart mod 256 B, so lane = slot ds_read_b128 is conflict-free
+static_assert(sizeof(SlotRow) == 592, "SlotRow layout");
 
 // Device column of each row field (built by the host at ks_load_nodes).
 struct RowCol {
@@ -386,12 +445,13 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
 template <typename P32, typename PU32, typename P64>
 __device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU32 min_mask, P64 limit, P64 used,
                                                 P64 minv, P64 npused, bool check_parent, int32_t quota,
-                                                uint32_t flags, uint32_t pmask, int64_t req) {
+                                                uint32_t flags, uint32_t pmask, int64_t req,
+                                                bool skip_leaf = false) {
   const int lane = threadIdx.x & 63;
   const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
   const int ld = lane < KS_QUOTA_DIMS ? lane : 0;
   const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
-  {
+  if (!skip_leaf) {
     const uint32_t lm = limit_mask[quota];
     const int64_t u = used[o], l = limit[o];
     const bool bad = in_pod && ((lm >> lane) & 1u) && (req + u > l);
@@ -422,15 +482,15 @@ __device__ __forceinline__ int64_t load_field(const void* p, int32_t w, int64_t 
 // NodeReg of one slot row (lane-private LDS reads).
 template <int NSC>
 __device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
-  r.free_cpu = s.free[SF_CPU];
-  r.free_mem = s.free[SF_MEM];
-  r.free_eph = s.free[SF_EPH];
+  r.free_cpu = s.t[ST_FREE_CPU].h;
+  r.free_mem = s.t[ST_FREE_MEM].h;
+  r.free_eph = s.t[ST_FREE_EPH].h;
   r.t_cpu = s.t[ST_CPU];
   r.t_mem = s.t[ST_MEM];
   r.t_eph = s.t[ST_EPH];
 #pragma unroll
   for (int k = 0; k < NSC; ++k) {
-    r.free_sc[k] = s.free[SF_SC + k];
+    r.free_sc[k] = s.t[ST_FREE_SC + k].h;
     r.t_sc[k] = s.t[ST_SC + k];
   }
   r.t_lcpu = s.t[ST_LCPU];
@@ -439,10 +499,10 @@ __device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
   r.t_plmem = s.t[ST_PLMEM];
   r.la_bits = s.la_bits;
   r.fit_ws = s.fit_ws;
-  r.pods_full = s.pods_full;
   r.allowed = s.allowed;
   r.pod_count = s.pod_count;
-  r.valid = s.valid;
+  r.pods_full = (int64_t)s.pod_count + 1 > (int64_t)s.allowed;
+  r.valid = 1;
 }
 
 // Untouched-candidate resolution of one pod (lane k = candidate k), against the current touched masks.
@@ -603,11 +663,14 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
 #pragma unroll
     for (int i = 0; i < (int)(sizeof(Cfg) / 4); ++i) asm volatile("" : "+s"(w[i]));
   }
+  int32_t Kc = K;
+  asm volatile("" : "+s"(Kc));
 
-  // ---- per-lane roles in slot construction and Reserve (lane t < ST_N: term t; ST_N.. : headrooms) ----
-  // term t: capacity / requested raw fields, and the PodRec words of its Reserve delta (x1, x100)
-  int32_t t_cap = 0, t_req = 0, t_pw = -1, t_pw100 = -1;
-  bool t_prod_only = false;
+  // ---- per-lane roles in slot construction and Reserve: lane t < ST_N owns slot term t ----
+  // capacity / requested raw fields, the PodRec words of its Reserve delta (x1, x100), and whether a
+  // zero capacity disables the term (score terms) or not (headrooms)
+  int32_t t_cap = 0, t_req = 0, t_pw = 0, t_pw100 = 0;
+  bool t_prod_only = false, t_score = true;
   switch (lane) {
     case ST_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_NZ_CPU; t_pw = 3; t_pw100 = 12; break;
     case ST_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_NZ_MEM; t_pw = 4; t_pw100 = 13; break;
@@ -618,20 +681,15 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     case ST_LMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_TERM_MEM; t_pw = 6; t_pw100 = 16; break;
     case ST_PLCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_PTERM_CPU; t_pw = 5; t_pw100 = 15; t_prod_only = true; break;
     case ST_PLMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_PTERM_MEM; t_pw = 6; t_pw100 = 16; t_prod_only = true; break;
+    case ST_FREE_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_REQ_CPU; t_pw = 0; t_pw100 = 0; t_score = false; break;
+    case ST_FREE_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_REQ_MEM; t_pw = 1; t_pw100 = 1; t_score = false; break;
+    case ST_FREE_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 2; t_score = false; break;
+    case ST_FREE_SC + 0: case ST_FREE_SC + 1: case ST_FREE_SC + 2: case ST_FREE_SC + 3:
+      t_cap = RF_ALLOC_SC + (lane - ST_FREE_SC); t_req = RF_REQ_SC + (lane - ST_FREE_SC);
+      t_pw = 7 + (lane - ST_FREE_SC); t_pw100 = t_pw; t_score = false; break;
     default: break;
   }
-  // headroom lane ST_N + i: free[i] = alloc - Requested, Reserve subtracts the pod's raw request
-  const int32_t fi = lane - ST_N;
-  int32_t f_alloc = 0, f_req = 0, f_pw = 0;
-  switch (fi) {
-    case SF_CPU: f_alloc = RF_ALLOC_CPU; f_req = RF_REQ_CPU; f_pw = 0; break;
-    case SF_MEM: f_alloc = RF_ALLOC_MEM; f_req = RF_REQ_MEM; f_pw = 1; break;
-    case SF_EPH: f_alloc = RF_ALLOC_EPH; f_req = RF_REQ_EPH; f_pw = 2; break;
-    case SF_SC + 0: case SF_SC + 1: case SF_SC + 2: case SF_SC + 3:
-      f_alloc = RF_ALLOC_SC + (fi - SF_SC); f_req = RF_REQ_SC + (fi - SF_SC); f_pw = 7 + (fi - SF_SC); break;
-    default: break;
-  }
-  constexpr int kLaneCounts = ST_N + SF_N;  // lane: pod count / flags of the row
+  constexpr int kLaneCounts = ST_N;  // lane: pod count / flags of the row
   const bool monotone = cfg.monotone != 0;
 
   int32_t snode = -1;  // lane s: node of slot s
@@ -656,20 +714,48 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   uint32_t st_next = 0;
   Cands cn{};
   auto lookahead = [&](int32_t j) {
-    st_next = admit(j);
-    if (st_next) return;
-    if (monotone) {
-      const uint64_t top = readlane64(my_top, j);
-      if (top != 0) {
-        const int32_t tn = (int32_t)gkey_node(top);
-        if (!((touched[tn >> 6] >> (tn & 63)) & 1ull)) {
-          cn.fast = true;  // its row is in rawtop[j]
-          cn.umax = top;
-          return;
+    const uint64_t top = monotone ? readlane64(my_top, j) : 0ull;
+    const int32_t tn = top ? (int32_t)gkey_node(top) : 0;
+    if (QC) {
+      // every LDS read of the admission and of the fast check issued together (one latency)
+      const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
+      const bool has_q = cfg.quota_enable && qrow >= 0;
+      const int32_t qr = has_q ? qrow : 0;
+      const int ld = lane & (KS_QUOTA_DIMS - 1);
+      const size_t o = (size_t)qr * KS_QUOTA_DIMS + ld;
+      const int64_t req = pqreq[j * KS_QUOTA_DIMS + ld];
+      const uint32_t lm = qlds->limit_mask[qr];
+      const int64_t u = qlds->used[o], l = qlds->limit[o];
+      const uint64_t tw = touched[tn >> 6];
+      st_next = 0;
+      if (has_q) {
+        const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
+        const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
+        if (__ballot(in_pod && ((lm >> lane) & 1u) && (req + u > l))) {
+          st_next = KS_S_QUOTA;
+        } else {
+          const uint32_t flags = __builtin_amdgcn_readlane(my_flags, j);
+          st_next = quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
+                                qlds->npused, cfg.quota_parent, qrow, flags & KS_POD_NONPREEMPTIBLE, pmask, req,
+                                /*skip_leaf=*/true);
         }
       }
+      if (st_next) return;
+      if (top && !((tw >> (tn & 63)) & 1ull)) {
+        cn.fast = true;  // its row is in rawtop[j]
+        cn.umax = top;
+        return;
+      }
+    } else {
+      st_next = admit(j);
+      if (st_next) return;
+      if (top && !((touched[tn >> 6] >> (tn & 63)) & 1ull)) {
+        cn.fast = true;
+        cn.umax = top;
+        return;
+      }
     }
-    cn = resolve_cands(cand_chunk, cand_t, touched, j, K, __builtin_amdgcn_readlane(my_cnt, j));
+    cn = resolve_cands(cand_chunk, cand_t, touched, j, Kc, __builtin_amdgcn_readlane(my_cnt, j));
 #ifndef KS_NO_SPEC
     if (cn.umax) {
       const int32_t node = (int32_t)gkey_node(cn.umax);
@@ -722,7 +808,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         need &= __ballot(cj.ub > best);
       }
       const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, j);
-      if (cnt == K && best < readlane64(my_bound, j)) {
+      if (cnt == Kc && best < readlane64(my_bound, j)) {
         processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep from j
         break;
       }
@@ -755,35 +841,31 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       }
       if (lane == s) snode = node;
       if (lane == 0) touched[node >> 6] |= 1ull << (node & 63);
-      // build the slot row with the pod already reserved on it (lane-parallel)
+      // build the slot row with the pod already reserved on it (lane-parallel, one code path)
+      const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+      const int64_t cap = src[t_cap], req = src[t_req] + (take ? podw[t_pw] : 0);
       if (lane < ST_N) {
         Term t;
-        const bool take = !t_prod_only || (pflags & KS_POD_PROD);
-        term_set(t, src[t_cap], src[t_req] + (take ? podw[t_pw] : 0));
+        t.c = cap;
+        t.h = cap - req + ((cap != 0 || !t_score) ? 0 : kNoCap);
+        t.h100 = cap != 0 ? (cap - req) * 100 : 0;
+        t.fh = i64_to_f32(t.h);
+        t.rcp = rcp100(cap);
         row->t[lane] = t;
-      } else if (lane < ST_N + SF_N) {
-        row->free[fi] = src[f_alloc] - src[f_req] - podw[f_pw];
       } else if (lane == kLaneCounts) {
-        const int32_t allowed = (int32_t)src[RF_ALLOWED];
-        const int32_t pc = (int32_t)src[RF_POD_COUNT] + 1;
         row->la_bits = (uint32_t)src[RF_LA_BITS];
-        row->allowed = allowed;
-        row->pod_count = pc;
-        row->pods_full = (int64_t)pc + 1 > (int64_t)allowed;
-        row->valid = 1;
+        row->allowed = (int32_t)src[RF_ALLOWED];
+        row->pod_count = (int32_t)src[RF_POD_COUNT] + 1;
         row->fit_ws = (src[RF_ALLOC_CPU] != 0 ? cfg.fw_cpu : 0) + (src[RF_ALLOC_MEM] != 0 ? cfg.fw_mem : 0) +
                       (src[RF_ALLOC_EPH] != 0 ? cfg.fw_eph : 0);
       }
     } else {
       row = &rows[s];
+      const bool take = !t_prod_only || (pflags & KS_POD_PROD);
       if (lane < ST_N) {
-        if (!t_prod_only || (pflags & KS_POD_PROD)) term_take(row->t[lane], podw[t_pw], podw[t_pw100]);
-      } else if (lane < ST_N + SF_N) {
-        row->free[fi] -= podw[f_pw];
+        if (take) term_take(row->t[lane], podw[t_pw], podw[t_pw100]);
       } else if (lane == kLaneCounts) {
-        const int32_t pc = row->pod_count + 1;
-        row->pod_count = pc;
-        row->pods_full = (int64_t)pc + 1 > (int64_t)row->allowed;
+        row->pod_count += 1;
       }
     }
     if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score};
@@ -822,13 +904,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const DevNodes d = *a.dn;
     const SlotRow& r = rows[lane];
     const int64_t node = snode;
-    gst(d.req_cpu + node, r.t[ST_CPU].c - r.free[SF_CPU]);
-    gst(d.req_mem + node, r.t[ST_MEM].c - r.free[SF_MEM]);
-    gst(d.req_eph + node, r.t[ST_EPH].c - r.free[SF_EPH]);
+    gst(d.req_cpu + node, r.t[ST_FREE_CPU].c - r.t[ST_FREE_CPU].h);
+    gst(d.req_mem + node, r.t[ST_FREE_MEM].c - r.t[ST_FREE_MEM].h);
+    gst(d.req_eph + node, r.t[ST_FREE_EPH].c - r.t[ST_FREE_EPH].h);
     gst(d.nz_cpu + node, term_requested(r.t[ST_CPU]));
     gst(d.nz_mem + node, term_requested(r.t[ST_MEM]));
 #pragma unroll
-    for (int k = 0; k < KS_MAX_SCALARS; ++k) gst(d.req_sc[k] + node, r.t[ST_SC + k].c - r.free[SF_SC + k]);
+    for (int k = 0; k < KS_MAX_SCALARS; ++k) gst(d.req_sc[k] + node, r.t[ST_FREE_SC + k].c - r.t[ST_FREE_SC + k].h);
     gst(d.pod_count + node, r.pod_count);
     gst(d.la_term_cpu + node, term_requested(r.t[ST_LCPU]));
     gst(d.la_term_mem + node, term_requested(r.t[ST_LMEM]));
@@ -1572,7 +1654,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   se.batch = ctx->batch;
   se.k = ctx->k;
   rec(1);
-  hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64), 0, ctx->stream, se);
+  hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64), (size_t)ctx->nchunks * sizeof(uint2) + kSelHistBins * 4, ctx->stream, se);
   rec(1);
   CommitArgs ca;
   ca.dn = ctx->dnodes;
@@ -1623,6 +1705,10 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     else if (ctx->nsc == 2) qcache ? setattr((const void*)commit_kernel<2, true>) : setattr((const void*)commit_kernel<2, false>);
     else qcache ? setattr((const void*)commit_kernel<4, true>) : setattr((const void*)commit_kernel<4, false>);
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
+    const size_t sel_smem = (size_t)ctx->nchunks * sizeof(uint2) + kSelHistBins * 4;
+    if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
+    e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_smem);
+    if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(select LDS %zu): %s", sel_smem, hipGetErrorString(e));
   }
   // pods per wave: aim for >= ~4096 waves per sweep
   int32_t ppw = 64;
