@@ -227,6 +227,21 @@ typedef struct ks_quota_cols {
   const int64_t *nonpreemptible_used[KS_QUOTA_DIMS];
 } ks_quota_cols;
 
+/* ElasticQuota tree for RefreshRuntime (pkg/scheduler/plugins/elasticquota/core/group_quota_manager.go:259-326):
+ * one row per quota of the tree (the system / default quotas excluded, as the reference does),
+ * values per resource dimension (cpu -> MilliValue, others -> Value). */
+typedef struct ks_quota_tree {
+  const int32_t *parent;          /* parent row, -1 = child of the root quota */
+  const uint8_t *allow_lent;      /* AllowLentResource (quota label allow-lent-resource, default true) */
+  const uint32_t *max_mask;       /* keys of CalculateInfo.Max */
+  const int64_t *max[KS_QUOTA_DIMS];
+  const int64_t *min[KS_QUOTA_DIMS];           /* Min (= AutoScaleMin; scale-min-quota not modelled) */
+  const int64_t *shared_weight[KS_QUOTA_DIMS]; /* NULL = Max (annotation shared-weight absent) */
+  const int64_t *guaranteed[KS_QUOTA_DIMS];    /* NULL = 0 (feature ElasticQuotaGuaranteeUsage off) */
+  const int64_t *self_request[KS_QUOTA_DIMS];  /* Σ PodRequestsAndLimits of the quota's own pods */
+  int64_t cluster_total[KS_QUOTA_DIMS];        /* totalResourceExceptSystemAndDefaultUsed */
+} ks_quota_tree;
+
 typedef struct ks_result {
   int32_t node;    /* chosen node index, -1 if not scheduled */
   uint32_t status; /* KS_S_* */
@@ -274,6 +289,16 @@ int ks_load_nodes(ks_ctx *ctx, const ks_node_cols *nodes, int64_t n);
 /* Informer deltas: rows[i] replaces node idx[i]; arrays in `rows` have length m. */
 int ks_update_nodes(ks_ctx *ctx, const int32_t *idx, const ks_node_cols *rows, int64_t m);
 int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
+
+/* RefreshRuntime for every quota of the tree at once, on the device
+ * (replaces GroupQuotaManager.RefreshRuntime, group_quota_manager.go:259-326, with the request
+ * aggregation of recursiveUpdateGroupTreeWithDeltaRequest :184-226 and the water-filling of
+ * runtime_quota_calculator.go:111-168).  runtime[i*KS_QUOTA_DIMS+d] and runtime_mask[i] (the
+ * calculators' resource keys = union of all Max keys) are written when non-NULL.  When quotas
+ * with the same row count are loaded, the runtime also becomes their admission limit
+ * (ElasticQuota PreFilter with EnableRuntimeQuota, plugin.go:221-223 / plugin_helper.go:314-319). */
+int ks_refresh_quota_runtime(ks_ctx *ctx, const ks_quota_tree *tree, int32_t q, int64_t *runtime,
+                             uint32_t *runtime_mask);
 
 /* Schedule `p` pods in order with commits; out[i] for pod i. Host buffers. */
 int ks_schedule(ks_ctx *ctx, const ks_pod_cols *pods, int32_t p, ks_result *out);

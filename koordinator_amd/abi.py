@@ -183,6 +183,20 @@ class KsQuotaCols(C.Structure):
     _fields_ = QUOTA_COLS
 
 
+class KsQuotaTree(C.Structure):
+    _fields_ = [
+        ("parent", P32),
+        ("allow_lent", C.POINTER(C.c_uint8)),
+        ("max_mask", PU32),
+        ("max", P64 * KS_QUOTA_DIMS),
+        ("min", P64 * KS_QUOTA_DIMS),
+        ("shared_weight", P64 * KS_QUOTA_DIMS),
+        ("guaranteed", P64 * KS_QUOTA_DIMS),
+        ("self_request", P64 * KS_QUOTA_DIMS),
+        ("cluster_total", C.c_int64 * KS_QUOTA_DIMS),
+    ]
+
+
 class KsResult(C.Structure):
     _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64)]
 
@@ -230,6 +244,7 @@ EXPORTED_SYMBOLS = [
     "ks_load_nodes",
     "ks_update_nodes",
     "ks_load_quotas",
+    "ks_refresh_quota_runtime",
     "ks_schedule",
     "ks_stage_pods",
     "ks_schedule_staged",

@@ -211,6 +211,49 @@ class QuotaTable:
         return c
 
 
+class QuotaTree:
+    """ElasticQuota tree for ks_refresh_quota_runtime (one row per quota; values [dim][quota]).
+
+    Mirrors the QuotaInfo fields RefreshRuntime reads (pkg/scheduler/plugins/elasticquota/core/
+    quota_info.go CalculateInfo: Max, Min/AutoScaleMin, SharedWeight, Guaranteed, the quota's own
+    pods' Request) plus AllowLentResource and the tree's total resource."""
+
+    def __init__(self, q: int):
+        self.q = int(q)
+        self.parent = np.full(self.q, -1, np.int32)
+        self.allow_lent = np.ones(self.q, np.uint8)
+        self.max_mask = np.zeros(self.q, np.uint32)
+        D = abi.KS_QUOTA_DIMS
+        self.max = np.zeros((D, self.q), np.int64)
+        self.min = np.zeros((D, self.q), np.int64)
+        self.shared_weight: Optional[np.ndarray] = None  # None = Max
+        self.guaranteed = np.zeros((D, self.q), np.int64)
+        self.self_request = np.zeros((D, self.q), np.int64)
+        self.cluster_total = np.zeros(D, np.int64)
+
+    def ks(self) -> abi.KsQuotaTree:
+        c = abi.KsQuotaTree()
+        self.parent = np.ascontiguousarray(self.parent, np.int32)
+        self.allow_lent = np.ascontiguousarray(self.allow_lent, np.uint8)
+        self.max_mask = np.ascontiguousarray(self.max_mask, np.uint32)
+        c.parent = _p32(self.parent)
+        c.allow_lent = self.allow_lent.ctypes.data_as(C.POINTER(C.c_uint8))
+        c.max_mask = _pu32(self.max_mask)
+        for name in ("max", "min", "guaranteed", "self_request", "shared_weight"):
+            arr = getattr(self, name)
+            if arr is None:
+                continue
+            arr = np.ascontiguousarray(arr, np.int64)
+            setattr(self, name, arr)
+            field = getattr(c, name)
+            for d in range(abi.KS_QUOTA_DIMS):
+                field[d] = _p64(arr[d])
+        for d in range(abi.KS_QUOTA_DIMS):
+            c.cluster_total[d] = int(self.cluster_total[d])
+        c._keep = self
+        return c
+
+
 class NodeState:
     """Host buffers for ks_read_nodes / ko_read_nodes."""
 

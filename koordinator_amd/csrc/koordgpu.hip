@@ -938,6 +938,140 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// ElasticQuota RefreshRuntime for the whole tree (group_quota_manager.go:259-326)
+// ------------------------------------------------------------------------------------------
+//
+// One wave per resource dimension.  Per-quota state lives in LDS ([dims][n] int64 x3).  The host
+// lays the tree out breadth-first (children of one parent contiguous) with depth levels and
+// sibling groups, so the wave can (1) aggregate requests bottom-up a level at a time
+// (recursiveUpdateGroupTreeWithDeltaRequest :184-226: ChildRequest = own pods + children's limited
+// requests; a non-lending quota asks for at least Min; limited = min(Request, Max) on Max's keys,
+// quota_info.go:217-228) and (2) run redistribution / iterationForRedistribution
+// (runtime_quota_calculator.go:111-168) for each sibling group top-down, lanes over siblings.
+// The float64 share int64(float64(w)*float64(total)/float64(Σw) + 0.5) is computed with IEEE
+// double ops in Go's order (-ffp-contract=off).
+
+struct QrtArgs {
+  int32_t n, ngroups, nlevels, dim0, ndims;
+  uint32_t keys;                  // union of all Max keys (the calculators' resource keys)
+  const int32_t* __restrict__ order;      // breadth-first quota order
+  const int32_t* __restrict__ level_off;  // [nlevels+1] ranges of `order` by depth (depth 1 first)
+  const int32_t* __restrict__ grp_parent; // [ngroups] parent quota of sibling group g (-1 = root)
+  const int32_t* __restrict__ grp_off;    // [ngroups+1] ranges of `order` holding group g
+  const int32_t* __restrict__ parent;
+  const uint8_t* __restrict__ allow;
+  const uint32_t* __restrict__ maxmask;
+  const int64_t* __restrict__ mx;         // [n][KS_QUOTA_DIMS]
+  const int64_t* __restrict__ mn;
+  const int64_t* __restrict__ sw;
+  const int64_t* __restrict__ guar;
+  const int64_t* __restrict__ selfreq;
+  const int64_t* __restrict__ total;      // [KS_QUOTA_DIMS]
+  int64_t* __restrict__ runtime;          // [n][KS_QUOTA_DIMS]
+};
+
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(512) void quota_runtime_kernel(QrtArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int64_t qlds[];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int d = a.dim0 + w;
+  if (w >= a.ndims || d >= KS_QUOTA_DIMS) return;
+  const int32_t n = a.n;
+  int64_t* creq = qlds + (size_t)w * 3 * n;  // ChildRequest, then the limited request
+  int64_t* rt = creq + n;                    // runtime
+  int64_t* lreq = rt + n;                    // limited request
+  const bool key = (a.keys >> d) & 1u;
+  for (int32_t q = lane; q < n; q += 64) {
+    const int64_t s = a.selfreq[(size_t)q * KS_QUOTA_DIMS + d];
+    creq[q] = s > 0 ? s : 0;
+    rt[q] = 0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // (1) requests, deepest level first
+  for (int32_t l = a.nlevels - 1; l >= 0; --l) {
+    for (int32_t i = a.level_off[l] + lane; i < a.level_off[l + 1]; i += 64) {
+      const int32_t q = a.order[i];
+      const size_t o = (size_t)q * KS_QUOTA_DIMS + d;
+      int64_t req = creq[q];
+      if (!a.allow[q] && a.mn[o] > req) req = a.mn[o];
+      if (((a.maxmask[q] >> d) & 1u) && req > a.mx[o]) req = a.mx[o];
+      lreq[q] = req;
+      const int32_t p = a.parent[q];
+      if (p >= 0) atomicAdd((unsigned long long*)&creq[p], (unsigned long long)req);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // (2) runtime, sibling groups in breadth-first order (a parent's runtime precedes its children)
+  for (int32_t g = 0; g < a.ngroups && key; ++g) {
+    const int32_t p = a.grp_parent[g];
+    int64_t tot = p < 0 ? a.total[d] : rt[p];
+    const int32_t b0 = a.grp_off[g], b1 = a.grp_off[g + 1];
+    int64_t used = 0, tsw = 0;
+    for (int32_t i = b0 + lane; i < b1; i += 64) {
+      const int32_t c = a.order[i];
+      const size_t o = (size_t)c * KS_QUOTA_DIMS + d;
+      int64_t m = a.mn[o];
+      if (a.guar[o] > m) m = a.guar[o];
+      const int64_t r = lreq[c];
+      int64_t v;
+      if (r > m) {
+        v = m;
+        tsw += a.sw[o];
+        creq[c] = 1;  // reused: "still adjusting"
+      } else {
+        v = a.allow[c] ? r : m;
+        creq[c] = 0;
+      }
+      rt[c] = v;
+      used += v;
+    }
+    used = wave_sum_i64(used);
+    tsw = wave_sum_i64(tsw);
+    int64_t part = tot - used;
+    if (part > 0) {
+      while (tsw > 0) {
+        int64_t npart = 0, nsw = 0, nadj = 0;
+        for (int32_t i = b0 + lane; i < b1; i += 64) {
+          const int32_t c = a.order[i];
+          if (!creq[c]) continue;
+          const size_t o = (size_t)c * KS_QUOTA_DIMS + d;
+          const int64_t wgt = a.sw[o];
+          const int64_t delta = (int64_t)((double)wgt * (double)part / (double)tsw + 0.5);
+          int64_t v = rt[c] + delta;
+          const int64_t r = lreq[c];
+          if (v < r) {
+            nsw += wgt;
+            nadj += 1;
+          } else {
+            npart += v - r;
+            v = r;
+            creq[c] = 0;
+          }
+          rt[c] = v;
+        }
+        npart = wave_sum_i64(npart);
+        nsw = wave_sum_i64(nsw);
+        nadj = wave_sum_i64(nadj);
+        if (!(npart > 0 && nadj > 0)) break;
+        part = npart;
+        tsw = nsw;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  for (int32_t q = lane; q < n; q += 64) a.runtime[(size_t)q * KS_QUOTA_DIMS + d] = key ? rt[q] : 0;
+}
+
+// ------------------------------------------------------------------------------------------
 // debug evaluation of one pod over every node (no Reserve)
 // ------------------------------------------------------------------------------------------
 
@@ -1488,6 +1622,138 @@ int ks_load_quotas(ks_ctx* ctx, const ks_quota_cols* qc, int32_t nq) {
   ctx->quota_used_ckpt = ctx->q.npused + rows * KS_QUOTA_DIMS;
   ctx->quota_npused_ckpt = ctx->quota_used_ckpt + rows * KS_QUOTA_DIMS;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_refresh_quota_runtime(ks_ctx* ctx, const ks_quota_tree* t, int32_t nq, int64_t* runtime, uint32_t* runtime_mask) {
+  if (!ctx || !t || nq < 0) return ctx ? (ctx->err = "ks_refresh_quota_runtime: bad args", KS_EINVAL) : KS_EINVAL;
+  if (nq == 0) return KS_OK;
+  if (!t->parent || !t->max_mask) KS_FAIL(ctx, KS_EINVAL, "ks_quota_tree: parent and max_mask are required");
+  const int D = KS_QUOTA_DIMS;
+  // breadth-first layout: sibling groups contiguous, depth levels
+  std::vector<std::vector<int32_t>> kids(nq + 1);  // kids[nq] = children of the root
+  for (int32_t i = 0; i < nq; ++i) {
+    const int32_t p = t->parent[i];
+    if (p < -1 || p >= nq || p == i) KS_FAIL(ctx, KS_EINVAL, "quota %d: bad parent %d", i, p);
+    kids[p < 0 ? nq : p].push_back(i);
+  }
+  std::vector<int32_t> order, level_off, grp_parent, grp_off, depth(nq, -1);
+  order.reserve(nq);
+  grp_parent.push_back(-1);
+  grp_off.push_back(0);
+  for (int32_t c : kids[nq]) order.push_back(c), depth[c] = 0;
+  grp_off.push_back((int32_t)order.size());
+  for (size_t i = 0; i < order.size(); ++i) {
+    const int32_t q = order[i];
+    if (kids[q].empty()) continue;
+    grp_parent.push_back(q);
+    for (int32_t c : kids[q]) order.push_back(c), depth[c] = depth[q] + 1;
+    grp_off.push_back((int32_t)order.size());
+  }
+  if ((int32_t)order.size() != nq) KS_FAIL(ctx, KS_EINVAL, "ks_quota_tree: parent links form a cycle");
+  int32_t nlevels = 0;
+  for (int32_t q : order) nlevels = std::max(nlevels, depth[q] + 1);
+  level_off.assign(nlevels + 1, 0);
+  {
+    // `order` is breadth-first, so depths are non-decreasing along it
+    int32_t l = 0;
+    for (int32_t i = 0; i < nq; ++i)
+      while (depth[order[i]] >= l) level_off[l++] = i;
+    while (l <= nlevels) level_off[l++] = nq;
+  }
+  const int32_t ngroups = (int32_t)grp_parent.size();
+  uint32_t keys = 0;
+  for (int32_t i = 0; i < nq; ++i) keys |= t->max_mask[i];
+  keys &= (1u << D) - 1u;
+  // pack: int64 tables first, then int32/u8 metadata
+  const size_t tbl = (size_t)nq * D;
+  std::vector<int64_t> h64(tbl * 6 + D, 0);
+  int64_t* mx = h64.data();
+  int64_t* mn = mx + tbl;
+  int64_t* sw = mn + tbl;
+  int64_t* gu = sw + tbl;
+  int64_t* sr = gu + tbl;
+  int64_t* rtout = sr + tbl;
+  int64_t* tot = rtout + tbl;
+  for (int32_t i = 0; i < nq; ++i)
+    for (int d = 0; d < D; ++d) {
+      const size_t o = (size_t)i * D + d;
+      mx[o] = t->max[d] ? t->max[d][i] : 0;
+      mn[o] = t->min[d] ? t->min[d][i] : 0;
+      sw[o] = t->shared_weight[d] ? t->shared_weight[d][i] : mx[o];
+      gu[o] = t->guaranteed[d] ? t->guaranteed[d][i] : 0;
+      sr[o] = t->self_request[d] ? t->self_request[d][i] : 0;
+      for (int64_t v : {mx[o], mn[o], sw[o], gu[o], sr[o]})
+        if (v < 0 || v >= ((int64_t)1 << 56)) KS_FAIL(ctx, KS_EINVAL, "quota %d dim %d: value outside [0, 2^56)", i, d);
+    }
+  for (int d = 0; d < D; ++d) tot[d] = t->cluster_total[d];
+  std::vector<int32_t> h32;
+  auto put = [&](const std::vector<int32_t>& v) { size_t o = h32.size(); h32.insert(h32.end(), v.begin(), v.end()); return o; };
+  const size_t o_order = put(order), o_lvl = put(level_off), o_gp = put(grp_parent), o_go = put(grp_off);
+  const size_t o_par = put(std::vector<int32_t>(t->parent, t->parent + nq));
+  std::vector<int32_t> mm(nq);
+  for (int32_t i = 0; i < nq; ++i) mm[i] = (int32_t)t->max_mask[i];
+  const size_t o_mm = put(mm);
+  std::vector<int32_t> al(nq);
+  for (int32_t i = 0; i < nq; ++i) al[i] = t->allow_lent ? (t->allow_lent[i] ? 1 : 0) : 1;
+  const size_t o_al = h32.size();
+  h32.resize(h32.size() + (nq + 3) / 4, 0);
+  memcpy(h32.data() + o_al, std::vector<uint8_t>(al.begin(), al.end()).data(), nq);
+  const size_t b64 = h64.size() * 8, b32 = h32.size() * 4;
+  void* dbuf = nullptr;
+  if (dev_alloc(ctx, &dbuf, b64 + b32) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemcpyAsync(dbuf, h64.data(), b64, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync((char*)dbuf + b64, h32.data(), b32, hipMemcpyHostToDevice, ctx->stream));
+  const int64_t* d64 = (const int64_t*)dbuf;
+  const int32_t* d32 = (const int32_t*)((char*)dbuf + b64);
+  QrtArgs qa;
+  qa.n = nq;
+  qa.ngroups = ngroups;
+  qa.nlevels = nlevels;
+  qa.keys = keys;
+  qa.order = d32 + o_order;
+  qa.level_off = d32 + o_lvl;
+  qa.grp_parent = d32 + o_gp;
+  qa.grp_off = d32 + o_go;
+  qa.parent = d32 + o_par;
+  qa.maxmask = (const uint32_t*)(d32 + o_mm);
+  qa.allow = (const uint8_t*)(d32 + o_al);
+  qa.mx = d64;
+  qa.mn = d64 + tbl;
+  qa.sw = d64 + 2 * tbl;
+  qa.guar = d64 + 3 * tbl;
+  qa.selfreq = d64 + 4 * tbl;
+  qa.runtime = (int64_t*)d64 + 5 * tbl;
+  qa.total = d64 + 6 * tbl;
+  // one wave per dimension; as many dimensions per launch as LDS holds (3 x int64 per quota)
+  const size_t per_dim = (size_t)nq * 3 * 8;
+  int dims_per = (int)std::min<size_t>(D, (160 * 1024) / per_dim);
+  if (dims_per < 1) {
+    (void)hipFree(dbuf);
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "quota tree too large for the runtime kernel's LDS (%d quotas)", nq);
+  }
+  hipError_t e = hipFuncSetAttribute((const void*)quota_runtime_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(per_dim * dims_per));
+  for (int d0 = 0; e == hipSuccess && d0 < D; d0 += dims_per) {
+    qa.dim0 = d0;
+    qa.ndims = std::min(dims_per, D - d0);
+    hipLaunchKernelGGL(quota_runtime_kernel, dim3(1), dim3(64 * qa.ndims), per_dim * qa.ndims, ctx->stream, qa);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(rtout, qa.runtime, tbl * 8, hipMemcpyDeviceToHost, ctx->stream);
+  // install as the admission limit of the loaded quota table (EnableRuntimeQuota)
+  if (e == hipSuccess && ctx->quota_blob && ctx->q.q == nq) {
+    e = hipMemcpyAsync(ctx->q.limit, qa.runtime, tbl * 8, hipMemcpyDeviceToDevice, ctx->stream);
+    std::vector<uint32_t> lm(nq, keys);
+    if (e == hipSuccess) e = hipMemcpyAsync(ctx->q.limit_mask, lm.data(), (size_t)nq * 4, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(dbuf);
+  if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "ks_refresh_quota_runtime: %s", hipGetErrorString(e));
+  if (runtime) memcpy(runtime, rtout, tbl * 8);
+  if (runtime_mask)
+    for (int32_t i = 0; i < nq; ++i) runtime_mask[i] = keys;
   return KS_OK;
 }
 

@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import NodeState, NodeTable, PodTable, QuotaTable
+from .cluster import NodeState, NodeTable, PodTable, QuotaTable, QuotaTree
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
@@ -57,6 +57,7 @@ def lib() -> C.CDLL:
     L.ks_load_nodes.argtypes = [vp, C.POINTER(abi.KsNodeCols), C.c_int64]
     L.ks_update_nodes.argtypes = [vp, abi.P32, C.POINTER(abi.KsNodeCols), C.c_int64]
     L.ks_load_quotas.argtypes = [vp, C.POINTER(abi.KsQuotaCols), C.c_int32]
+    L.ks_refresh_quota_runtime.argtypes = [vp, C.POINTER(abi.KsQuotaTree), C.c_int32, abi.P64, abi.PU32]
     L.ks_schedule.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
     L.ks_stage_pods.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32]
     L.ks_schedule_staged.argtypes = [vp]
@@ -128,6 +129,16 @@ class Evaluator:
         cols = quotas.ks()
         self._chk(self.L.ks_load_quotas(self.h, C.byref(cols), quotas.q))
         self.nq = quotas.q
+
+    def refresh_quota_runtime(self, tree: QuotaTree):
+        """RefreshRuntime for every quota (on the device); installs it as the admission limit of the
+        loaded quota table when the row counts agree.  Returns (runtime [dim][quota], mask)."""
+        rt = np.zeros((max(tree.q, 1), abi.KS_QUOTA_DIMS), np.int64)
+        mask = np.zeros(max(tree.q, 1), np.uint32)
+        cols = tree.ks()
+        self._chk(self.L.ks_refresh_quota_runtime(self.h, C.byref(cols), tree.q, rt.ctypes.data_as(abi.P64),
+                                                  mask.ctypes.data_as(abi.PU32)))
+        return rt[: tree.q].T.copy(), mask[: tree.q]
 
     def schedule(self, pods: PodTable) -> dict:
         out = np.zeros(max(pods.n, 1), RESULT_DTYPE)

@@ -5,10 +5,10 @@
 #define O(T, f) printf("%s.%s %zu\n", #T, #f, offsetof(T, f))
 int main(void) {
   P(ks_fit_args); P(ks_loadaware_args); P(ks_quota_args); P(ks_config); P(ks_node_cols); P(ks_pod_cols);
-  P(ks_quota_cols); P(ks_result); P(ks_node_state); P(ks_stats);
+  P(ks_quota_cols); P(ks_quota_tree); P(ks_result); P(ks_node_state); P(ks_stats);
   O(ks_config, fit); O(ks_config, loadaware); O(ks_config, quota); O(ks_config, batch_pods); O(ks_config, profile);
   O(ks_node_cols, alloc_scalar); O(ks_node_cols, la_flags); O(ks_node_cols, la_prod_usage_milli_memory);
   O(ks_pod_cols, flags); O(ks_pod_cols, quota_req); O(ks_quota_cols, nonpreemptible_used);
-  O(ks_stats, sweep_ms); O(ks_stats, diag);
+  O(ks_quota_tree, max); O(ks_quota_tree, self_request); O(ks_quota_tree, cluster_total); O(ks_stats, sweep_ms); O(ks_stats, diag);
   return 0;
 }
