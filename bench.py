@@ -103,6 +103,10 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--shard", action="store_true",
+                    help="shard the nodes over the ranks (RCCL allgather of per-shard candidates, SURVEY §8e); "
+                         "default for --gpus N is N independent replicas")
+    ap.add_argument("--vshards", type=int, default=1, help="virtual shards per GPU (exercises the merge on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,7 +122,8 @@ def main():
 
     from koordinator_amd import runtime
 
-    w = build_workload(args.config, seed=20261015 + rank)
+    # replicas schedule their own cluster (seed + rank); shards split one shared cluster
+    w = build_workload(args.config, seed=20261015 + (0 if args.shard else rank))
     prof = w.profile
     prof.device = local_rank if world > 1 else 0
     prof.batch_pods = args.batch_pods
@@ -126,6 +131,13 @@ def main():
     cfg = prof.to_ks_config()
     cfg.profile = 0 if args.no_profile else 1
     ev = runtime.Evaluator(cfg, w.nodes, w.quotas)
+    if args.shard or args.vshards > 1:
+        uid = None
+        if world > 1:
+            box = [runtime.shard_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        ev.shard(world if args.shard else 1, rank if args.shard else 0, uid, args.vshards)
     ev.stage(w.pods)
     ev.checkpoint()
 
@@ -162,7 +174,7 @@ def main():
     res = ev.fetch()
 
     n_pods, n_nodes = w.pods.n, w.nodes.n
-    total_pods = n_pods * args.steps * world
+    total_pods = n_pods * args.steps * (1 if args.shard else world)
     value = total_pods / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
     out = None
@@ -173,7 +185,8 @@ def main():
             # algorithmic bytes per sweep launch: every node column the enabled plugins read, once
             # (B_node), + the pass's pod records + the chunk-maxima output
             b_node = 8 * 15 + 4 * 3 + 16 * 2  # LA+Fit columns + batch-cpu/batch-memory scalar columns
-            algo = n_nodes * b_node + 64 * 128 + ((n_nodes + 63) // 64) * 64 * 4
+            local_nodes = n_nodes // (world if args.shard else 1)  # one rank sweeps its shard
+            algo = local_nodes * b_node + 64 * 128 + ((local_nodes + 63) // 64) * 64 * 4
             achieved = algo / avg_s / 1e9
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
@@ -188,14 +201,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.shard else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
             "config": {"workload": f"{w.name}: {n_pods} pods x {n_nodes} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
                                    f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else ""),
                        "pods_per_step": n_pods, "nodes": n_nodes, "percentage_of_nodes_to_score": 100,
-                       "parallelism": f"replicas{world}" if world > 1 else "single-gpu",
+                       "parallelism": (f"node-shards{world}x{args.vshards}" if args.shard or args.vshards > 1
+                                       else (f"replicas{world}" if world > 1 else "single-gpu")),
                        "batch_pods": cfg.batch_pods or 64, "candidates": cfg.candidates or 32},
             "node_evals_per_s": round(value * n_nodes, 1),
             "placed_per_step": int((res["status"] == 0).sum()),

@@ -52,6 +52,7 @@ extern "C" {
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
+#define KS_SHARD_ID_BYTES 128 /* opaque RCCL unique id (ks_shard_unique_id) */
 
 /* ---- status codes ---- */
 #define KS_OK 0
@@ -323,6 +324,18 @@ int ks_eval_pod_debug(ks_ctx *ctx, const ks_pod_cols *pod, uint32_t *reasons, in
 int ks_read_nodes(ks_ctx *ctx, ks_node_state *out);
 int ks_read_quota_used(ks_ctx *ctx, int64_t *used /* q*KS_QUOTA_DIMS, row-major */);
 int ks_get_stats(const ks_ctx *ctx, ks_stats *out);
+
+/* Node sharding over GPUs (one process per GPU).  The node table stays replicated
+ * (every rank applies the same commits); shard s = rank * virtual_shards + v sweeps and selects
+ * over its contiguous node-chunk range, the per-shard top-K candidate lists are exchanged with
+ * one RCCL allgather per pass, and a merge kernel rebuilds exactly the list a single sweep would
+ * give, so placements are identical for any shard count.  Replaces the reference's single-process
+ * Parallelizer over nodes (pkg/util/parallelize/parallelism.go:29-49 / upstream
+ * findNodesThatPassFilters + prioritizeNodes).  ks_shard_unique_id is called on rank 0 and the
+ * bytes broadcast by the host; virtual_shards > 1 splits one GPU's range into several shards
+ * (exercises the merge on one GPU). */
+int ks_shard_unique_id(uint8_t *out /* KS_SHARD_ID_BYTES */);
+int ks_shard_init(ks_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *unique_id, int32_t virtual_shards);
 
 #ifdef __cplusplus
 }

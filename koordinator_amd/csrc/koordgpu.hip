@@ -25,6 +25,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "ks_device.h"
 
 using namespace ks;
@@ -144,6 +146,7 @@ struct SweepArgs {
   const int32_t* __restrict__ cursor;
   uint2* __restrict__ out;  // [64 pods][nchunks]: {best, runner-up} local keys (pod-major: select reads a row)
   int64_t n, nchunks;
+  int64_t c0, c1;  // this shard's chunk range
   int32_t total_pods, batch, ppw;
 };
 
@@ -158,9 +161,9 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
   const int32_t groups = (np + a.ppw - 1) / a.ppw;
-  const int64_t nwork = a.nchunks * groups;
+  const int64_t nwork = (a.c1 - a.c0) * groups;
   for (int64_t w = wave; w < nwork; w += nwaves) {
-    const int64_t c = w / groups;
+    const int64_t c = a.c0 + w / groups;
     const int32_t g = (int32_t)(w - c * groups);
     const int64_t node = c * 64 + lane;
     NodeReg<NSC> r;
@@ -195,7 +198,9 @@ struct SelectArgs {
   uint64_t* cand_bound;          // [64]
   uint64_t* cand_top;            // [64] the pod's snapshot-best key over every chunk
   int32_t* cand_count;           // [64]
-  int64_t nchunks;
+  int32_t* cand_total;           // [64] feasible chunks in this range (before the top-K cut)
+  int64_t nchunks;               // row stride of the sweep output
+  int64_t c0, c1;                // chunk range selected over
   int32_t total_pods, batch, k;
 };
 
@@ -218,17 +223,18 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   const int32_t p = blockIdx.x;
   if (p >= np) return;
   const int32_t K = a.k;
-  const uint2* in = a.in + (size_t)p * a.nchunks;
+  const int64_t nc = a.c1 - a.c0;  // LDS row index e <-> chunk c0 + e
+  const uint2* in = a.in + (size_t)p * a.nchunks + a.c0;
   int32_t cnt = 0;
   uint32_t hmax = 0;
   uint64_t top = 0;
-  for (int64_t e = lane; e < a.nchunks; e += 64) {
+  for (int64_t e = lane; e < nc; e += 64) {
     const uint2 loc = in[e];
     srow[e] = loc;
     const uint32_t h = loc.x >> 6;
     cnt += h != 0;
     hmax = h > hmax ? h : hmax;
-    top = umax64(top, local_gkey(loc.x, e));
+    top = umax64(top, local_gkey(loc.x, a.c0 + e));
   }
   __syncthreads();
   cnt = wave_sum_i32(cnt);
@@ -241,12 +247,12 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
     if (hmax < kSelHistBins) {
       // histogram of chunk scores (LDS atomics), then the largest t with count(h >= t) >= K by a
       // suffix scan over the bins (lane l owns bins [l*B, l*B+B))
-      uint32_t* hist = reinterpret_cast<uint32_t*>(srow + a.nchunks);
+      uint32_t* hist = reinterpret_cast<uint32_t*>(srow + nc);
       constexpr int B = kSelHistBins / 64;
 #pragma unroll
       for (int i = 0; i < B; ++i) hist[lane * B + i] = 0u;
       __syncthreads();
-      for (int64_t e = lane; e < a.nchunks; e += 64) {
+      for (int64_t e = lane; e < nc; e += 64) {
         const uint32_t h = srow[e].x >> 6;
         if (h) atomicAdd(&hist[h], 1u);
       }
@@ -289,14 +295,14 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
       while (lo < hi) {
         const uint32_t mid = lo + (hi - lo + 1) / 2;
         int32_t c = 0;
-        for (int64_t e = lane; e < a.nchunks; e += 64) c += (srow[e].x >> 6) >= mid;
+        for (int64_t e = lane; e < nc; e += 64) c += (srow[e].x >> 6) >= mid;
         c = wave_sum_i32(c);
         if (c >= K) lo = mid;
         else hi = mid - 1;
       }
       t = lo;
       int32_t gt = 0;
-      for (int64_t e = lane; e < a.nchunks; e += 64) gt += (srow[e].x >> 6) > t;
+      for (int64_t e = lane; e < nc; e += 64) gt += (srow[e].x >> 6) > t;
       gt = wave_sum_i32(gt);
       need_eq = K - gt;
     }
@@ -305,9 +311,9 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   int32_t base = 0, eq_taken = 0;
   uint64_t bound = 0;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  for (int64_t e0 = 0; e0 < a.nchunks; e0 += 64) {
+  for (int64_t e0 = 0; e0 < nc; e0 += 64) {
     const int64_t e = e0 + lane;
-    const uint2 loc = e < a.nchunks ? srow[e] : make_uint2(0u, 0u);
+    const uint2 loc = e < nc ? srow[e] : make_uint2(0u, 0u);
     const uint32_t h = loc.x >> 6;
     const bool is_gt = h > t;
     const bool is_eq = (h == t) && h != 0;
@@ -318,14 +324,154 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
     const uint64_t btake = __ballot(take);
     if (take) {
       const int32_t pos = base + __popcll(btake & lanemask_lt);
-      a.cand_chunk[p * K + pos] = (uint32_t)e;
+      a.cand_chunk[p * K + pos] = (uint32_t)(a.c0 + e);
       a.cand_t[p * K + pos] = loc;
-      if (take_eq && eq_rank == need_eq - 1) bound = local_gkey(loc.x, e);
+      if (take_eq && eq_rank == need_eq - 1) bound = local_gkey(loc.x, a.c0 + e);
     }
     base += __popcll(btake);
     eq_taken += __popcll(beq);
   }
   bound = wave_max_u64(bound);  // only one lane holds a non-zero bound
+  if (lane == 0) {
+    a.cand_count[p] = base;
+    a.cand_total[p] = cnt;
+    a.cand_bound[p] = exhaustive ? 0ull : bound;
+    a.cand_top[p] = top;
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------
+// merge: per-shard candidate lists -> the list a single select over every chunk would produce
+// ------------------------------------------------------------------------------------------
+//
+// Shards own contiguous chunk ranges in shard order, so concatenating the shard lists keeps
+// global chunk order.  A shard's list holds every chunk above its own K-th score t_s <= t (the
+// global K-th score) and its first equal-score chunks, so the union holds every chunk above t and
+// the first need_eq = K - #(h > t) chunks equal to t in global chunk order: the same selection
+// rule applied to the union reproduces the single-GPU list, bound and top exactly.
+
+struct CandSlot {  // one shard's select output inside the gather buffer (byte offsets)
+  size_t chunk, t, count, total, top, bytes;
+};
+
+__host__ __device__ inline CandSlot cand_slot_layout(int32_t k) {
+  CandSlot L;
+  size_t o = 0;
+  L.chunk = o;
+  o += (size_t)kMaxBatch * k * 4;
+  L.t = o;
+  o += (size_t)kMaxBatch * k * 8;
+  L.count = o;
+  o += kMaxBatch * 4;
+  L.total = o;
+  o += kMaxBatch * 4;
+  L.top = o;
+  o += kMaxBatch * 8;
+  L.bytes = (o + 255) / 256 * 256;
+  return L;
+}
+
+struct MergeArgs {
+  const unsigned char* __restrict__ gather;  // [nslots] CandSlot blocks
+  const int32_t* __restrict__ cursor;
+  uint32_t* cand_chunk;
+  uint2* cand_t;
+  uint64_t* cand_bound;
+  uint64_t* cand_top;
+  int32_t* cand_count;
+  int32_t nslots, total_pods, batch, k;
+};
+
+__global__ __launch_bounds__(64) void merge_kernel(MergeArgs a) {
+  const int lane = threadIdx.x;
+  const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor);
+  const int32_t p = blockIdx.x;
+  if (p >= np) return;
+  const int32_t K = a.k;
+  const CandSlot L = cand_slot_layout(K);
+  int32_t total = 0;
+  uint64_t top = 0;
+  for (int32_t s = 0; s < a.nslots; ++s) {
+    const unsigned char* b = a.gather + (size_t)s * L.bytes;
+    total += reinterpret_cast<const int32_t*>(b + L.total)[p];
+    top = umax64(top, reinterpret_cast<const uint64_t*>(b + L.top)[p]);
+  }
+  // the union, in shard order, walked 64 entries at a time
+  auto entry = [&](int32_t s, int32_t i, uint32_t& chunk, uint2& t) {
+    const unsigned char* b = a.gather + (size_t)s * L.bytes;
+    chunk = reinterpret_cast<const uint32_t*>(b + L.chunk)[p * K + i];
+    t = reinterpret_cast<const uint2*>(b + L.t)[p * K + i];
+  };
+  uint32_t t_thr = 1;
+  int32_t need_eq = 0x7fffffff;
+  const bool exhaustive = total <= K;
+  if (!exhaustive) {
+    uint32_t hmax = 0;
+    for (int32_t s = 0; s < a.nslots; ++s) {
+      const int32_t cnt = reinterpret_cast<const int32_t*>(a.gather + (size_t)s * L.bytes + L.count)[p];
+      for (int32_t i = lane; i < cnt; i += 64) {
+        uint32_t c;
+        uint2 t;
+        entry(s, i, c, t);
+        hmax = umax32(hmax, t.x >> 6);
+      }
+    }
+    hmax = wave_max_u32(hmax);
+    auto count_ge = [&](uint32_t x, bool strict) {
+      int32_t n = 0;
+      for (int32_t s = 0; s < a.nslots; ++s) {
+        const int32_t cnt = reinterpret_cast<const int32_t*>(a.gather + (size_t)s * L.bytes + L.count)[p];
+        for (int32_t i = lane; i < cnt; i += 64) {
+          uint32_t c;
+          uint2 t;
+          entry(s, i, c, t);
+          const uint32_t h = t.x >> 6;
+          n += strict ? (h > x) : (h >= x);
+        }
+      }
+      return wave_sum_i32(n);
+    };
+    uint32_t lo = 1, hi = hmax;  // largest t with count(h >= t) >= K
+    while (lo < hi) {
+      const uint32_t mid = lo + (hi - lo + 1) / 2;
+      if (count_ge(mid, false) >= K) lo = mid;
+      else hi = mid - 1;
+    }
+    t_thr = lo;
+    need_eq = K - count_ge(t_thr, true);
+  }
+  int32_t base = 0, eq_taken = 0;
+  uint64_t bound = 0;
+  const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  for (int32_t s = 0; s < a.nslots; ++s) {
+    const int32_t cnt = reinterpret_cast<const int32_t*>(a.gather + (size_t)s * L.bytes + L.count)[p];
+    for (int32_t i0 = 0; i0 < cnt; i0 += 64) {
+      const int32_t i = i0 + lane;
+      uint32_t c = 0;
+      uint2 t = make_uint2(0u, 0u);
+      if (i < cnt) entry(s, i, c, t);
+      const uint32_t h = t.x >> 6;
+      const bool is_gt = h > t_thr;
+      const bool is_eq = (h == t_thr) && h != 0;
+      const uint64_t beq = __ballot(is_eq);
+      const int32_t eq_rank = eq_taken + __popcll(beq & lanemask_lt);
+      const bool take_eq = is_eq && eq_rank < need_eq;
+      const bool take = is_gt || take_eq;
+      const uint64_t btake = __ballot(take);
+      if (take) {
+        const int32_t pos = base + __popcll(btake & lanemask_lt);
+        a.cand_chunk[p * K + pos] = c;
+        a.cand_t[p * K + pos] = t;
+        if (take_eq && eq_rank == need_eq - 1) bound = local_gkey(t.x, c);
+      }
+      base += __popcll(btake);
+      eq_taken += __popcll(beq);
+    }
+  }
+  bound = wave_max_u64(bound);
   if (lane == 0) {
     a.cand_count[p] = base;
     a.cand_bound[p] = exhaustive ? 0ull : bound;
@@ -1152,6 +1298,12 @@ struct ks_ctx {
   uint2* cand_t = nullptr;
   uint64_t* cand_bound = nullptr;
   uint64_t* cand_top = nullptr;
+  int32_t* cand_total = nullptr;
+  // node sharding: shard s = rank * vshards + v owns chunks [s*nchunks/S, (s+1)*nchunks/S)
+  int32_t nranks = 1, rank = 0, vshards = 1;
+  ncclComm_t comm = nullptr;
+  unsigned char* gather = nullptr;  // [nranks * vshards] CandSlot blocks
+  size_t gather_bytes = 0;
   int32_t* cand_count = nullptr;
   int32_t* cursor = nullptr;
   unsigned long long* counters = nullptr;
@@ -1284,6 +1436,8 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_top = (uint64_t*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
+  ctx->cand_total = (int32_t*)p;
+  if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_count = (int32_t*)p;
   if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
   ctx->cursor = (int32_t*)p;
@@ -1312,6 +1466,9 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->cand_t; dev_free(p);
   p = ctx->cand_bound; dev_free(p);
   p = ctx->cand_top; dev_free(p);
+  p = ctx->cand_total; dev_free(p);
+  p = ctx->gather; dev_free(p);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   p = ctx->cand_count; dev_free(p);
   p = ctx->cursor; dev_free(p);
   p = ctx->counters; dev_free(p);
@@ -1893,6 +2050,8 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
     (void)hipEventRecord(e, ctx->stream);
     evs->push_back({kind, (*evn)++});
   };
+  const int32_t S = ctx->nranks * ctx->vshards;
+  auto shard_lo = [&](int32_t sh) { return ctx->nchunks * sh / S; };
   SweepArgs sa;
   sa.dn = ctx->dnodes;
   sa.c = ctx->kc;
@@ -1901,6 +2060,8 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.out = ctx->sweep_out;
   sa.n = ctx->n;
   sa.nchunks = ctx->nchunks;
+  sa.c0 = shard_lo(ctx->rank * ctx->vshards);
+  sa.c1 = shard_lo((ctx->rank + 1) * ctx->vshards);
   sa.total_pods = ctx->np;
   sa.batch = ctx->batch;
   sa.ppw = ppw;
@@ -1910,17 +2071,55 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   SelectArgs se;
   se.in = ctx->sweep_out;
   se.cursor = ctx->cursor;
-  se.cand_chunk = ctx->cand_chunk;
-  se.cand_t = ctx->cand_t;
-  se.cand_bound = ctx->cand_bound;
-  se.cand_top = ctx->cand_top;
-  se.cand_count = ctx->cand_count;
   se.nchunks = ctx->nchunks;
   se.total_pods = ctx->np;
   se.batch = ctx->batch;
   se.k = ctx->k;
+  const CandSlot L = cand_slot_layout(ctx->k);
   rec(1);
-  hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64), (size_t)ctx->nchunks * sizeof(uint2) + kSelHistBins * 4, ctx->stream, se);
+  for (int32_t v = 0; v < ctx->vshards; ++v) {
+    const int32_t sh = ctx->rank * ctx->vshards + v;
+    se.c0 = shard_lo(sh);
+    se.c1 = shard_lo(sh + 1);
+    if (S == 1) {
+      se.cand_chunk = ctx->cand_chunk;
+      se.cand_t = ctx->cand_t;
+      se.cand_bound = ctx->cand_bound;
+      se.cand_top = ctx->cand_top;
+      se.cand_count = ctx->cand_count;
+      se.cand_total = ctx->cand_total;
+    } else {
+      unsigned char* b = ctx->gather + (size_t)sh * L.bytes;
+      se.cand_chunk = (uint32_t*)(b + L.chunk);
+      se.cand_t = (uint2*)(b + L.t);
+      se.cand_bound = ctx->cand_bound;  // recomputed by the merge
+      se.cand_top = (uint64_t*)(b + L.top);
+      se.cand_count = (int32_t*)(b + L.count);
+      se.cand_total = (int32_t*)(b + L.total);
+    }
+    hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64),
+                       (size_t)(se.c1 - se.c0) * sizeof(uint2) + kSelHistBins * 4, ctx->stream, se);
+  }
+  if (S > 1) {
+    if (ctx->nranks > 1) {
+      // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
+      const size_t bytes = (size_t)ctx->vshards * L.bytes;
+      (void)ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, ctx->stream);
+    }
+    MergeArgs ma;
+    ma.gather = ctx->gather;
+    ma.cursor = ctx->cursor;
+    ma.cand_chunk = ctx->cand_chunk;
+    ma.cand_t = ctx->cand_t;
+    ma.cand_bound = ctx->cand_bound;
+    ma.cand_top = ctx->cand_top;
+    ma.cand_count = ctx->cand_count;
+    ma.nslots = S;
+    ma.total_pods = ctx->np;
+    ma.batch = ctx->batch;
+    ma.k = ctx->k;
+    hipLaunchKernelGGL(merge_kernel, dim3(ctx->batch), dim3(64), 0, ctx->stream, ma);
+  }
   rec(1);
   CommitArgs ca;
   ca.dn = ctx->dnodes;
@@ -1975,12 +2174,24 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
     e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_smem);
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(select LDS %zu): %s", sel_smem, hipGetErrorString(e));
+    const size_t gb = (size_t)ctx->nranks * ctx->vshards * cand_slot_layout(ctx->k).bytes;
+    if (ctx->nranks * ctx->vshards > 1 && ctx->gather_bytes < gb) {
+      void* g = ctx->gather;
+      dev_free(g);
+      ctx->gather = nullptr;
+      if (dev_alloc(ctx, &g, gb) != KS_OK) return KS_ENOMEM;
+      HIPCHK(ctx, hipMemsetAsync(g, 0, gb, ctx->stream));
+      ctx->gather = (unsigned char*)g;
+      ctx->gather_bytes = gb;
+    }
   }
   // pods per wave: aim for >= ~4096 waves per sweep
+  const int64_t S = (int64_t)ctx->nranks * ctx->vshards;
+  const int64_t local_chunks = ctx->nchunks * (ctx->rank + 1) * ctx->vshards / S - ctx->nchunks * ctx->rank * ctx->vshards / S;
   int32_t ppw = 64;
-  while (ppw > 4 && ctx->nchunks * (ctx->batch / ppw) < 4096) ppw >>= 1;
+  while (ppw > 4 && local_chunks * (ctx->batch / ppw) < 4096) ppw >>= 1;
   if (ppw > ctx->batch) ppw = ctx->batch;
-  const int64_t nwork = ctx->nchunks * ((ctx->batch + ppw - 1) / ppw);
+  const int64_t nwork = std::max<int64_t>(local_chunks, 1) * ((ctx->batch + ppw - 1) / ppw);
   const int sweep_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048));
   hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
@@ -2033,7 +2244,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   // algorithmic bytes of one full sweep launch: node columns read once per pod group + outputs
   int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16;
   const int64_t groups = (ctx->batch + ppw - 1) / ppw;
-  ctx->stats.sweep_bytes = ctx->n * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + ctx->nchunks * 64 * 4;
+  ctx->stats.sweep_bytes = local_chunks * 64 * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + local_chunks * 64 * 4;
   return KS_OK;
 }
 
@@ -2144,6 +2355,36 @@ int ks_read_quota_used(ks_ctx* ctx, int64_t* used) {
   if (!ctx->quota_blob || ctx->q.q == 0) return KS_OK;
   HIPCHK(ctx, hipMemcpyAsync(used, ctx->q.used, (size_t)ctx->q.q * KS_QUOTA_DIMS * 8, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_shard_unique_id(uint8_t* out) {
+  if (!out) return KS_EINVAL;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return KS_EHIP;
+  static_assert(sizeof(id) == KS_SHARD_ID_BYTES, "ncclUniqueId size");
+  memcpy(out, &id, sizeof(id));
+  return KS_OK;
+}
+
+int ks_shard_init(ks_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* unique_id, int32_t virtual_shards) {
+  if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || virtual_shards < 1 || nranks * virtual_shards > 1024)
+    return ctx ? (ctx->err = "ks_shard_init: bad args", KS_EINVAL) : KS_EINVAL;
+  if (nranks > 1 && !unique_id) KS_FAIL(ctx, KS_EINVAL, "ks_shard_init: nranks > 1 needs the rank-0 unique id");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ctx->comm) {
+    (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+  }
+  if (nranks > 1) {
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
+    if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  }
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  ctx->vshards = virtual_shards;
   return KS_OK;
 }
 

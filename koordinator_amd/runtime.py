@@ -68,11 +68,23 @@ def lib() -> C.CDLL:
     L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
     L.ks_read_quota_used.argtypes = [vp, abi.P64]
     L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
+    L.ks_shard_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+    L.ks_shard_init.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32]
     for name in abi.EXPORTED_SYMBOLS:
         if name not in ("ks_destroy", "ks_last_error"):
             getattr(L, name).restype = C.c_int
     _lib = L
     return L
+
+
+def shard_unique_id() -> bytes:
+    """RCCL unique id for ks_shard_init (call on rank 0, broadcast the bytes to the other ranks)."""
+    L = lib()
+    buf = (C.c_uint8 * abi.KS_SHARD_ID_BYTES)()
+    rc = L.ks_shard_unique_id(buf)
+    if rc != abi.KS_OK:
+        raise KsError(rc, "ncclGetUniqueId failed")
+    return bytes(buf)
 
 
 class Evaluator:
@@ -129,6 +141,13 @@ class Evaluator:
         cols = quotas.ks()
         self._chk(self.L.ks_load_quotas(self.h, C.byref(cols), quotas.q))
         self.nq = quotas.q
+
+    def shard(self, nranks: int = 1, rank: int = 0, unique_id: Optional[bytes] = None, virtual_shards: int = 1):
+        """Node sharding: this rank sweeps its chunk range; candidates are exchanged by RCCL allgather."""
+        uid = None
+        if unique_id is not None:
+            uid = (C.c_uint8 * abi.KS_SHARD_ID_BYTES).from_buffer_copy(unique_id)
+        self._chk(self.L.ks_shard_init(self.h, nranks, rank, uid, virtual_shards))
 
     def refresh_quota_runtime(self, tree: QuotaTree):
         """RefreshRuntime for every quota (on the device); installs it as the admission limit of the
