@@ -48,11 +48,13 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 1
+#define KS_ABI_VERSION 2
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
 #define KS_SHARD_ID_BYTES 128 /* opaque RCCL unique id (ks_shard_unique_id) */
+#define KS_RSV_DIMS (3 + KS_MAX_SCALARS) /* reservation resources: cpu, memory, ephemeral-storage, scalar[k] */
+#define KS_RSV_CLASSES 64 /* pod match classes (ks_reservation_cols.owner_classes bits) */
 
 /* ---- status codes ---- */
 #define KS_OK 0
@@ -83,6 +85,7 @@ extern "C" {
 #define KS_POD_DAEMONSET 0x02u       /* isDaemonSetPod(ownerRefs) (loadaware/helper.go:188)          */
 #define KS_POD_NONPREEMPTIBLE 0x04u  /* extension.IsPodNonPreemptible (elasticquota/plugin.go:236)   */
 #define KS_POD_SCALAR_KEYS 0x08u     /* podRequest.ScalarResources has at least one key (upstream fitsRequest) */
+#define KS_POD_RSV_AFFINITY 0x10u    /* GetRequiredReservationAffinity != nil (reservation/transformer.go:51, stateData.hasAffinity) */
 
 /* ---- per-node filter reason bits (ks_eval_pod_debug) ---- */
 #define KS_R_FIT_PODS 0x001u      /* "Too many pods"                                    */
@@ -94,6 +97,8 @@ extern "C" {
 #define KS_R_LA_MEMORY 0x040u     /* ErrReasonUsageExceedThreshold memory               */
 #define KS_R_LA_AGGREGATED 0x080u /* the failure used ErrReasonAggregatedUsageExceedThreshold */
 #define KS_R_LA_PROD 0x100u       /* the failure came from filterProdUsage              */
+#define KS_R_RSV_AFFINITY 0x200u  /* ErrReasonReservationAffinity: no matched reservation (reservation/plugin.go:236,343) */
+#define KS_R_RSV_NO_FIT 0x400u    /* filterWithReservations: no matched reservation satisfies the pod (plugin.go:425-437) */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -105,7 +110,15 @@ extern "C" {
 /* score plugin slots for ks_eval_pod_debug's per-plugin score matrix */
 #define KS_SCORE_FIT 0
 #define KS_SCORE_LOADAWARE 1
-#define KS_NUM_SCORE_PLUGINS 2
+#define KS_SCORE_RESERVATION 2 /* after DefaultNormalizeScore (reservation/scoring.go:126-131) */
+#define KS_NUM_SCORE_PLUGINS 3
+
+/* ---- reservation flags (ks_reservation_cols.flags) ---- */
+#define KS_RSV_UNSCHEDULABLE 0x1u /* ReservationInfo.IsUnschedulable (transformer.go:113)              */
+#define KS_RSV_ALLOCATE_ONCE 0x2u /* IsAllocateOnce (transformer.go:109, plugin.go:523)                */
+#define KS_RSV_POLICY_DEFAULT 0u    /* ReservationAllocatePolicy (ks_reservation_cols.policy) */
+#define KS_RSV_POLICY_ALIGNED 1u
+#define KS_RSV_POLICY_RESTRICTED 2u
 
 /* NodeResourcesFitArgs.scoringStrategy (upstream apis/config/types.go; the profile in
  * config/manager/scheduler-config.yaml:17-31). A weight of 0 means "not listed". */
@@ -144,6 +157,17 @@ typedef struct ks_quota_args {
   int32_t enable_check_parent_quota; /* EnableCheckParentQuota (plugin.go:250) */
 } ks_quota_args;
 
+/* Reservation plugin (pkg/scheduler/plugins/reservation): profile score weight
+ * (config/manager/scheduler-config.yaml: 5000).  The device ranks nodes by the exact
+ * lexicographic order the normalized score induces, which requires
+ * plugin_weight > 100 * (fit.plugin_weight + loadaware.plugin_weight);
+ * other weights are rejected with KS_EUNSUPPORTED. */
+typedef struct ks_reservation_args {
+  int32_t enable;
+  int32_t _pad0;
+  int64_t plugin_weight;
+} ks_reservation_args;
+
 typedef struct ks_config {
   int32_t abi_version; /* = KS_ABI_VERSION */
   int32_t device;      /* HIP device ordinal */
@@ -154,6 +178,7 @@ typedef struct ks_config {
   int32_t candidates;  /* candidate node chunks kept per pod per pass (0 = default 32, max 64) */
   int32_t profile;     /* 1 = bracket every kernel with HIP events (ks_get_stats) */
   int32_t _pad1;
+  ks_reservation_args reservation;
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -215,6 +240,11 @@ typedef struct ks_pod_cols {
   const int32_t *quota;           /* quota row, -1 = no quota (plugin.go:211-215) */
   const uint32_t *quota_mask;     /* bit d: dimension d present in PodRequestsAndLimits keys */
   const int64_t *quota_req[KS_QUOTA_DIMS];
+  /* Reservation: the pod's match class (-1 = matches no reservation; NULL = all -1).  Pods
+   * whose MatchReservationOwners / reservation-affinity outcome is identical for every
+   * reservation share a class (matchReservation, transformer.go:349-373); reserve pods
+   * themselves are not scheduled through this entry point. */
+  const int32_t *rsv_class;
 } ks_pod_cols;
 
 /* ElasticQuota table: QuotaInfo.CalculateInfo per quota (core/quota_info.go). */
@@ -243,10 +273,31 @@ typedef struct ks_quota_tree {
   int64_t cluster_total[KS_QUOTA_DIMS];        /* totalResourceExceptSystemAndDefaultUsed */
 } ks_quota_tree;
 
+/* Available reservations (reservationCache.forEachAvailableReservationOnNode,
+ * reservation/cache.go:256-291), one row per reservation; rows of the same node are visited
+ * in table order (the canonical order for the reference's map iteration).  ReservationInfo
+ * fields: frameworkext/reservation_info.go:37-115.  The reserve pod in NodeInfo requests
+ * exactly `allocatable` (reservationutil.NewReservePod). */
+typedef struct ks_reservation_cols {
+  const int32_t *node;            /* Status.NodeName as node row */
+  const uint64_t *owner_classes;  /* bit c: pods of class c match (owners + reservation affinity) */
+  const uint32_t *flags;          /* KS_RSV_* */
+  const uint32_t *policy;         /* KS_RSV_POLICY_* (GetAllocatePolicy) */
+  const int64_t *order;           /* label reservation-order parsed (scoring.go:162-181); 0 = none */
+  const uint32_t *key_mask;       /* bit d: dimension d is a key of Allocatable (= ResourceNames) */
+  const int64_t *allocatable[KS_RSV_DIMS];
+  const int64_t *allocated[KS_RSV_DIMS];  /* NULL = 0 */
+  const int32_t *assigned;        /* len(AssignedPods); NULL = 0 */
+  const int64_t *reserve_nonzero_milli_cpu; /* reserve pod's NonZeroRequested; NULL = from allocatable */
+  const int64_t *reserve_nonzero_memory;
+} ks_reservation_cols;
+
 typedef struct ks_result {
   int32_t node;    /* chosen node index, -1 if not scheduled */
   uint32_t status; /* KS_S_* */
   int64_t score;   /* total weighted score of the chosen node */
+  int32_t reservation; /* reservation row the pod was assumed into (Reserve, plugin.go:532-570), -1 = none */
+  int32_t _pad0;
 } ks_result;
 
 /* Mutable node state after commits (read back for parity). */
@@ -290,6 +341,15 @@ int ks_load_nodes(ks_ctx *ctx, const ks_node_cols *nodes, int64_t n);
 /* Informer deltas: rows[i] replaces node idx[i]; arrays in `rows` have length m. */
 int ks_update_nodes(ks_ctx *ctx, const int32_t *idx, const ks_node_cols *rows, int64_t m);
 int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
+
+/* Reservation cache snapshot (reservation/cache.go:104-291) for the Reservation plugin's
+ * BeforePreFilter restore (transformer.go:41-307), Filter (plugin.go:311-496), PreScore
+ * nomination (scoring.go:42-101, nominator.go:134-192), Score/NormalizeScore (scoring.go:103-203)
+ * and Reserve (plugin.go:532-570 -> cache.go:171-192 -> reservation_info.go:379-388).
+ * Node columns stay the reference's NodeInfo (reserve pods included); call after ks_load_nodes. */
+int ks_load_reservations(ks_ctx *ctx, const ks_reservation_cols *rsv, int32_t r);
+/* Allocated (r*KS_RSV_DIMS, row-major) and len(AssignedPods) after commits; NULL = skip. */
+int ks_read_reservations(ks_ctx *ctx, int64_t *allocated, int32_t *assigned);
 
 /* RefreshRuntime for every quota of the tree at once, on the device
  * (replaces GroupQuotaManager.RefreshRuntime, group_quota_manager.go:259-326, with the request

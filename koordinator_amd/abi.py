@@ -8,9 +8,11 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 1
+KS_ABI_VERSION = 2
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
+KS_RSV_DIMS = 3 + KS_MAX_SCALARS
+KS_RSV_CLASSES = 64
 
 KS_OK = 0
 KS_EINVAL = -1
@@ -35,6 +37,7 @@ KS_POD_PROD = 0x01
 KS_POD_DAEMONSET = 0x02
 KS_POD_NONPREEMPTIBLE = 0x04
 KS_POD_SCALAR_KEYS = 0x08
+KS_POD_RSV_AFFINITY = 0x10
 
 KS_R_FIT_PODS = 0x001
 KS_R_FIT_CPU = 0x002
@@ -45,6 +48,8 @@ KS_R_LA_CPU = 0x020
 KS_R_LA_MEMORY = 0x040
 KS_R_LA_AGGREGATED = 0x080
 KS_R_LA_PROD = 0x100
+KS_R_RSV_AFFINITY = 0x200
+KS_R_RSV_NO_FIT = 0x400
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -54,7 +59,14 @@ KS_S_UNSCHEDULABLE = 0x8
 
 KS_SCORE_FIT = 0
 KS_SCORE_LOADAWARE = 1
-KS_NUM_SCORE_PLUGINS = 2
+KS_SCORE_RESERVATION = 2
+KS_NUM_SCORE_PLUGINS = 3
+
+KS_RSV_UNSCHEDULABLE = 0x1
+KS_RSV_ALLOCATE_ONCE = 0x2
+KS_RSV_POLICY_DEFAULT = 0
+KS_RSV_POLICY_ALIGNED = 1
+KS_RSV_POLICY_RESTRICTED = 2
 
 P64 = C.POINTER(C.c_int64)
 P32 = C.POINTER(C.c_int32)
@@ -93,6 +105,10 @@ class KsQuotaArgs(C.Structure):
     _fields_ = [("enable", C.c_int32), ("enable_check_parent_quota", C.c_int32)]
 
 
+class KsReservationArgs(C.Structure):
+    _fields_ = [("enable", C.c_int32), ("_pad0", C.c_int32), ("plugin_weight", C.c_int64)]
+
+
 class KsConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -104,6 +120,7 @@ class KsConfig(C.Structure):
         ("candidates", C.c_int32),
         ("profile", C.c_int32),
         ("_pad1", C.c_int32),
+        ("reservation", KsReservationArgs),
     ]
 
 
@@ -161,6 +178,7 @@ POD_COLS = [
     ("quota", P32),
     ("quota_mask", PU32),
     ("quota_req", P64 * KS_QUOTA_DIMS),
+    ("rsv_class", P32),
 ]
 
 
@@ -197,8 +215,28 @@ class KsQuotaTree(C.Structure):
     ]
 
 
+class KsReservationCols(C.Structure):
+    _fields_ = [
+        ("node", P32),
+        ("owner_classes", C.POINTER(C.c_uint64)),
+        ("flags", PU32),
+        ("policy", PU32),
+        ("order", P64),
+        ("key_mask", PU32),
+        ("allocatable", P64 * KS_RSV_DIMS),
+        ("allocated", P64 * KS_RSV_DIMS),
+        ("assigned", P32),
+        ("reserve_nonzero_milli_cpu", P64),
+        ("reserve_nonzero_memory", P64),
+    ]
+
+
 class KsResult(C.Structure):
-    _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64)]
+    _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64), ("reservation", C.c_int32),
+                ("_pad0", C.c_int32)]
+
+
+RESULT_DTYPE_FIELDS = [("node", "<i4"), ("status", "<u4"), ("score", "<i8"), ("reservation", "<i4"), ("_pad0", "<i4")]
 
 
 NODE_STATE_COLS = [
@@ -244,6 +282,8 @@ EXPORTED_SYMBOLS = [
     "ks_load_nodes",
     "ks_update_nodes",
     "ks_load_quotas",
+    "ks_load_reservations",
+    "ks_read_reservations",
     "ks_refresh_quota_runtime",
     "ks_schedule",
     "ks_stage_pods",

@@ -34,7 +34,7 @@ POD_I64 = [
     "nonzero_milli_cpu", "nonzero_memory",
     "la_req_cpu", "la_lim_cpu", "la_dflt_cpu", "la_req_memory", "la_lim_memory", "la_dflt_memory",
 ]
-POD_I32 = ["quota"]
+POD_I32 = ["quota", "rsv_class"]
 POD_U32 = ["flags", "quota_mask"]
 
 STATE_I64 = [
@@ -148,6 +148,7 @@ class PodTable(_Table):
     def __init__(self, n: int):
         super().__init__(n)
         self.quota[:] = -1
+        self.rsv_class[:] = -1
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.quota_req = np.zeros((abi.KS_QUOTA_DIMS, self.n), np.int64)
 
@@ -168,6 +169,7 @@ class PodTable(_Table):
         for name in POD_I64:
             setattr(c, name, _p64(getattr(self, name)))
         c.quota = _p32(self.quota)
+        c.rsv_class = _p32(self.rsv_class)
         c.flags = _pu32(self.flags)
         c.quota_mask = _pu32(self.quota_mask)
         for k in range(abi.KS_MAX_SCALARS):
@@ -254,6 +256,51 @@ class QuotaTree:
         return c
 
 
+class ReservationTable:
+    """Available reservations (ks_reservation_cols): one row per ReservationInfo
+    (pkg/scheduler/frameworkext/reservation_info.go:37-115); resources [dim][row] with dims
+    cpu (milli), memory, ephemeral-storage, scalar[k]."""
+
+    def __init__(self, r: int):
+        self.r = int(r)
+        D = abi.KS_RSV_DIMS
+        self.node = np.zeros(self.r, np.int32)
+        self.owner_classes = np.zeros(self.r, np.uint64)
+        self.flags = np.zeros(self.r, np.uint32)
+        self.policy = np.zeros(self.r, np.uint32)
+        self.order = np.zeros(self.r, np.int64)
+        self.key_mask = np.zeros(self.r, np.uint32)
+        self.allocatable = np.zeros((D, self.r), np.int64)
+        self.allocated = np.zeros((D, self.r), np.int64)
+        self.assigned = np.zeros(self.r, np.int32)
+
+    def copy(self) -> "ReservationTable":
+        t = ReservationTable(self.r)
+        for k in ("node", "owner_classes", "flags", "policy", "order", "key_mask", "allocatable", "allocated",
+                  "assigned"):
+            setattr(t, k, getattr(self, k).copy())
+        return t
+
+    def ks(self) -> abi.KsReservationCols:
+        c = abi.KsReservationCols()
+        for name, dt in (("node", np.int32), ("owner_classes", np.uint64), ("flags", np.uint32),
+                         ("policy", np.uint32), ("order", np.int64), ("key_mask", np.uint32),
+                         ("assigned", np.int32), ("allocatable", np.int64), ("allocated", np.int64)):
+            setattr(self, name, np.ascontiguousarray(getattr(self, name), dt))
+        c.node = _p32(self.node)
+        c.owner_classes = self.owner_classes.ctypes.data_as(C.POINTER(C.c_uint64))
+        c.flags = _pu32(self.flags)
+        c.policy = _pu32(self.policy)
+        c.order = _p64(self.order)
+        c.key_mask = _pu32(self.key_mask)
+        c.assigned = _p32(self.assigned)
+        for d in range(abi.KS_RSV_DIMS):
+            c.allocatable[d] = _p64(self.allocatable[d])
+            c.allocated[d] = _p64(self.allocated[d])
+        c._keep = self
+        return c
+
+
 class NodeState:
     """Host buffers for ks_read_nodes / ko_read_nodes."""
 
@@ -287,4 +334,6 @@ def results_to_numpy(res) -> Dict[str, np.ndarray]:
         "node": np.array([r.node for r in res], np.int32) if arr.dtype.names is None else arr["node"].copy(),
         "status": np.array([r.status for r in res], np.uint32) if arr.dtype.names is None else arr["status"].copy(),
         "score": np.array([r.score for r in res], np.int64) if arr.dtype.names is None else arr["score"].copy(),
+        "reservation": np.array([r.reservation for r in res], np.int32) if arr.dtype.names is None
+        else arr["reservation"].copy(),
     }

@@ -119,6 +119,7 @@ class SchedulerProfile:
     loadaware: Optional[LoadAwareSchedulingArgs] = field(default_factory=LoadAwareSchedulingArgs)
     loadaware_weight: int = 1
     quota: Optional[ElasticQuotaArgs] = None
+    reservation_weight: Optional[int] = None  # Reservation plugin score weight (koord profile: 5000); None = off
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -171,6 +172,9 @@ class SchedulerProfile:
             c.loadaware.scaling_cpu = la.estimated_scaling_factors.get(CPU, 0)
             c.loadaware.scaling_memory = la.estimated_scaling_factors.get(MEMORY, 0)
             c.loadaware.plugin_weight = self.loadaware_weight
+        if self.reservation_weight is not None:
+            c.reservation.enable = 1
+            c.reservation.plugin_weight = int(self.reservation_weight)
         if self.quota is not None:
             c.quota.enable = 1
             c.quota.enable_check_parent_quota = 1 if self.quota.enable_check_parent_quota else 0

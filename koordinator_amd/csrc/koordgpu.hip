@@ -28,6 +28,7 @@
 #include <rccl/rccl.h>
 
 #include "ks_device.h"
+#include "ks_rsv.h"
 
 using namespace ks;
 
@@ -84,6 +85,7 @@ struct DevPodCols {
   uint32_t *flags;
   int32_t *quota;
   int64_t *la_req_cpu, *la_lim_cpu, *la_dflt_cpu, *la_req_mem, *la_lim_mem, *la_dflt_mem;
+  int32_t *rsv_class;
 };
 
 // estimatedUsedByResource (estimator/default_estimator.go:73-108)
@@ -131,7 +133,13 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
     r.h_sc[k] = r.sc[k] * 100;
     r.f_sc[k] = i64_to_f32(r.sc[k]);
   }
-  r._fpad[0] = r._fpad[1] = r._fpad[2] = 0.0f;
+  r.rsv_class = s.rsv_class[i];
+  uint32_t keys = 0;
+  const int64_t dims[3] = {r.cpu, r.mem, r.eph};
+  for (int d = 0; d < 3; ++d) keys |= dims[d] != 0 ? (1u << d) : 0u;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) keys |= r.sc[k] != 0 ? (1u << (3 + k)) : 0u;
+  r.rsv_keys = keys;
+  r._fpad = 0.0f;
   out[i] = r;
 }
 
@@ -141,6 +149,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
 
 struct SweepArgs {
   const DevNodes* __restrict__ dn;
+  const DevRsv* __restrict__ rv;
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
@@ -151,7 +160,7 @@ struct SweepArgs {
 };
 
 // local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
-template <int NSC>
+template <int NSC, bool RSV>
 __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const int lane = threadIdx.x & 63;
   // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar)
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     uint32_t best = 0, second = 0;
     for (int32_t p = p0; p < p1; ++p) {
       const PodRec pod = load_pod_uniform(a.pods + cursor + p);
-      const EvalOut o = eval_pod_node<NSC, false>(a.c, pod, r);
+      const EvalOut o = eval_full<NSC, false, false, true, RSV>(a.c, a.rv, pod, r, node);
       const uint32_t key = o.reasons ? 0u : (((uint32_t)(o.total + 1) << 6) | (uint32_t)(63 - lane));
       const uint32_t m1 = wave_max_u32(key);
       const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
@@ -500,8 +509,8 @@ enum RowField : int {
   RF_REQ_CPU = 0, RF_REQ_MEM = 1, RF_REQ_EPH = 2, RF_NZ_CPU = 3, RF_NZ_MEM = 4, RF_REQ_SC = 5,  // 5..8
   RF_TERM_CPU = 9, RF_TERM_MEM = 10, RF_PTERM_CPU = 11, RF_PTERM_MEM = 12, RF_POD_COUNT = 13,
   RF_ALLOC_CPU = 14, RF_ALLOC_MEM = 15, RF_ALLOC_EPH = 16, RF_ALLOC_SC = 17,  // 17..20
-  RF_LA_ALLOC_CPU = 21, RF_LA_ALLOC_MEM = 22, RF_ALLOWED = 23, RF_LA_BITS = 24,
-  RF_N = 25
+  RF_LA_ALLOC_CPU = 21, RF_LA_ALLOC_MEM = 22, RF_ALLOWED = 23, RF_LA_BITS = 24, RF_RSV_CLS = 25,
+  RF_N = 26
 };
 
 // slot-row terms: score terms 0..10, then the Filter headrooms (Allocatable - Requested) stored as
@@ -529,6 +538,7 @@ struct RowCol {
 
 struct CommitArgs {
   const DevNodes* __restrict__ dn;
+  const DevRsv* __restrict__ rv;
   Cfg c;
   const PodRec* __restrict__ pods;
   DevPodQuota pq;
@@ -554,7 +564,7 @@ struct QuotaRowsLds {
 };
 
 struct CommitLayout {
-  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, quota, touched, total;
+  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, quota, touched, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
@@ -578,6 +588,8 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += (size_t)kMaxBatch * k * sizeof(uint2);
   L.cand_chunk = o;
   o += align16((size_t)kMaxBatch * k * 4);
+  L.scls = o;
+  o += (size_t)kMaxBatch * 8;  // per slot: owner classes of the node's matchable reservations
   L.quota = o;
   if (qc) o += align16(sizeof(QuotaRowsLds));
   L.touched = o;
@@ -649,6 +661,7 @@ __device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
   r.pod_count = s.pod_count;
   r.pods_full = (int64_t)s.pod_count + 1 > (int64_t)s.allowed;
   r.valid = 1;
+  r.rsv_cls = 0;
 }
 
 // Untouched-candidate resolution of one pod (lane k = candidate k), against the current touched masks.
@@ -691,7 +704,7 @@ __device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const
 
 // Re-scan a candidate chunk's untouched nodes exactly for one pod (lane = node); touched nodes are
 // covered by the slot evaluation.
-template <int NSC>
+template <int NSC, bool RSV>
 __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const Cfg& cfg, const PodRec& pod,
                                                      int64_t chunk, uint64_t touched_mask) {
   const int lane = threadIdx.x & 63;
@@ -701,12 +714,12 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
     const DevNodes d = *a.dn;
     load_node<NSC>(cfg, d, node, node < a.n, r);
   }
-  const EvalOut o = eval_pod_node<NSC, false>(cfg, pod, r);
+  const EvalOut o = eval_full<NSC, false, false, false, RSV>(cfg, a.rv, pod, r, node);
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
   return wave_max_u64(skip ? 0ull : gkey(o.total, node));
 }
 
-template <int NSC, bool QC>
+template <int NSC, bool QC, bool RSV>
 __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
@@ -721,6 +734,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   uint32_t* cand_chunk = reinterpret_cast<uint32_t*>(smem_raw + lay.cand_chunk);
   QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
   unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
+  uint64_t* scls = reinterpret_cast<uint64_t*>(smem_raw + lay.scls);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -816,23 +830,25 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   // capacity / requested raw fields, the PodRec words of its Reserve delta (x1, x100), and whether a
   // zero capacity disables the term (score terms) or not (headrooms)
   int32_t t_cap = 0, t_req = 0, t_pw = 0, t_pw100 = 0;
+  int32_t t_rdim = -1;  // reservation restore dimension of the lane's term: 0..6 Requested, 8/9 NonZero cpu/memory
   bool t_prod_only = false, t_score = true;
   switch (lane) {
-    case ST_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_NZ_CPU; t_pw = 3; t_pw100 = 12; break;
-    case ST_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_NZ_MEM; t_pw = 4; t_pw100 = 13; break;
-    case ST_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 14; break;
+    case ST_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_NZ_CPU; t_pw = 3; t_pw100 = 12; t_rdim = 8; break;
+    case ST_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_NZ_MEM; t_pw = 4; t_pw100 = 13; t_rdim = 9; break;
+    case ST_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 14; t_rdim = 2; break;
     case ST_SC + 0: case ST_SC + 1: case ST_SC + 2: case ST_SC + 3:
-      t_cap = RF_ALLOC_SC + (lane - ST_SC); t_req = RF_REQ_SC + (lane - ST_SC); t_pw = 7 + (lane - ST_SC); t_pw100 = 17 + (lane - ST_SC); break;
+      t_cap = RF_ALLOC_SC + (lane - ST_SC); t_req = RF_REQ_SC + (lane - ST_SC); t_pw = 7 + (lane - ST_SC); t_pw100 = 17 + (lane - ST_SC);
+      t_rdim = 3 + (lane - ST_SC); break;
     case ST_LCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_TERM_CPU; t_pw = 5; t_pw100 = 15; break;
     case ST_LMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_TERM_MEM; t_pw = 6; t_pw100 = 16; break;
     case ST_PLCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_PTERM_CPU; t_pw = 5; t_pw100 = 15; t_prod_only = true; break;
     case ST_PLMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_PTERM_MEM; t_pw = 6; t_pw100 = 16; t_prod_only = true; break;
-    case ST_FREE_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_REQ_CPU; t_pw = 0; t_pw100 = 0; t_score = false; break;
-    case ST_FREE_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_REQ_MEM; t_pw = 1; t_pw100 = 1; t_score = false; break;
-    case ST_FREE_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 2; t_score = false; break;
+    case ST_FREE_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_REQ_CPU; t_pw = 0; t_pw100 = 0; t_score = false; t_rdim = 0; break;
+    case ST_FREE_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_REQ_MEM; t_pw = 1; t_pw100 = 1; t_score = false; t_rdim = 1; break;
+    case ST_FREE_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 2; t_score = false; t_rdim = 2; break;
     case ST_FREE_SC + 0: case ST_FREE_SC + 1: case ST_FREE_SC + 2: case ST_FREE_SC + 3:
       t_cap = RF_ALLOC_SC + (lane - ST_FREE_SC); t_req = RF_REQ_SC + (lane - ST_FREE_SC);
-      t_pw = 7 + (lane - ST_FREE_SC); t_pw100 = t_pw; t_score = false; break;
+      t_pw = 7 + (lane - ST_FREE_SC); t_pw100 = t_pw; t_score = false; t_rdim = 3 + (lane - ST_FREE_SC); break;
     default: break;
   }
   constexpr int kLaneCounts = ST_N;  // lane: pod count / flags of the row
@@ -919,7 +935,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const uint32_t st = st_next;
     const Cands cj = cn;
     if (st) {
-      if (lane == 0) sres[j] = ks_result{-1, st, 0};
+      if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0};
       goto next_pod;
     }
     {
@@ -932,12 +948,14 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       // pod j: LDS broadcast into VGPRs; flags scalar so the plugin branches stay wave-uniform
       PodRec pod = spods[j];
       pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
+      pod.rsv_class = __builtin_amdgcn_readfirstlane(pod.rsv_class);
       // ---- every touched node exactly (lane = slot), untouched from the candidates ----
       uint64_t key_mod = 0;
       if (lane < nslots) {
         NodeReg<NSC> r;
         slot_to_reg<NSC>(rows[lane], r);
-        const EvalOut o = eval_pod_node<NSC, false>(cfg, pod, r);
+        r.rsv_cls = scls[lane];
+        const EvalOut o = eval_full<NSC, false, true, false, RSV>(cfg, a.rv, pod, r, snode);
         key_mod = o.reasons ? 0ull : gkey(o.total, snode);
       }
       best = umax64(cj.umax, wave_max_u64(key_mod));
@@ -947,7 +965,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? cj.ub : 0ull);
         const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && cj.ub == kmax)) - 1;
         const int64_t c = (int64_t)(uint32_t)__shfl((int)cj.chunk, sel, 64);
-        const uint64_t v = rescan_untouched<NSC>(a, cfg, pod, c, touched[c]);
+        const uint64_t v = rescan_untouched<NSC, RSV>(a, cfg, pod, c, touched[c]);
         ++rescans;
         best = umax64(best, v);
         need &= ~(1ull << sel);
@@ -961,7 +979,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       KS_STAMP(3);
     }
     if (best == 0) {
-      if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0};
+      if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0, -1, 0};
       goto next_pod;
     }
     const int32_t node = (int32_t)gkey_node(best);
@@ -971,6 +989,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     // ---- Reserve: NodeInfo.AddPod + podAssignCache.assign on the slot row (lane = term) ----
     int32_t s = __ffsll((long long)__ballot(snode == node)) - 1;
     SlotRow* row;
+    // Reservation Reserve needs the node's pre-pod row: when the pod's class matches one of the
+    // node's reservations the row is built / kept without the pod, nominated on, then taken.
+    const int32_t pcls = RSV ? __builtin_amdgcn_readfirstlane(spods[j].rsv_class) : -1;
+    bool rsvc = false;
     if (s < 0) {
       s = nslots++;
       row = &rows[s];
@@ -987,8 +1009,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       }
       if (lane == s) snode = node;
       if (lane == 0) touched[node >> 6] |= 1ull << (node & 63);
+      const uint64_t ncl = (uint64_t)src[RF_RSV_CLS];
+      rsvc = pcls >= 0 && pcls < 64 && ((ncl >> pcls) & 1ull);
+      if (lane == 0) scls[s] = ncl;
       // build the slot row with the pod already reserved on it (lane-parallel, one code path)
-      const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+      const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
       const int64_t cap = src[t_cap], req = src[t_req] + (take ? podw[t_pw] : 0);
       if (lane < ST_N) {
         Term t;
@@ -1001,20 +1026,76 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       } else if (lane == kLaneCounts) {
         row->la_bits = (uint32_t)src[RF_LA_BITS];
         row->allowed = (int32_t)src[RF_ALLOWED];
-        row->pod_count = (int32_t)src[RF_POD_COUNT] + 1;
+        row->pod_count = (int32_t)src[RF_POD_COUNT] + (rsvc ? 0 : 1);
         row->fit_ws = (src[RF_ALLOC_CPU] != 0 ? cfg.fw_cpu : 0) + (src[RF_ALLOC_MEM] != 0 ? cfg.fw_mem : 0) +
                       (src[RF_ALLOC_EPH] != 0 ? cfg.fw_eph : 0);
       }
     } else {
       row = &rows[s];
-      const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+      rsvc = pcls >= 0 && pcls < 64 && ((scls[s] >> pcls) & 1ull);
+      const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
       if (lane < ST_N) {
         if (take) term_take(row->t[lane], podw[t_pw], podw[t_pw100]);
+      } else if (lane == kLaneCounts) {
+        if (!rsvc) row->pod_count += 1;
+      }
+    }
+    int32_t nom_row = -1;
+    int64_t fitla_pref = -1;  // Fit + LoadAware total of a preferred (ordered) chosen node
+    if (RSV && rsvc) {
+      // NominateReservation on the pre-pod state, Reserve into it (AddAssignedPod), then the pod
+      PodRec pod = spods[j];
+      pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
+      pod.rsv_class = pcls;
+      NodeReg<NSC> nr;
+      slot_to_reg<NSC>(*row, nr);
+      nr.rsv_cls = scls[s];
+      RsvDelta<NSC> dl;
+      const RsvOut ro = rsv_eval<NSC, true>(*a.rv, pod, nr, node, dl);
+      const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);
+      if (ro.hi >= kRsvOrderBase) {
+        rsv_apply<NSC>(nr, dl, 1);
+        fitla_pref = eval_pod_node<NSC, false>(cfg, pod, nr).total;
+      }
+      int64_t dd = 0;
+      if (nom >= 0) {
+        const RsvReserve rr = rsv_reserve_delta<true>(*a.rv, pod, nom);
+#pragma unroll
+        for (int d = 0; d < kRsvDims; ++d) {
+          dd = (t_rdim == d) ? rr.dreq[d] : dd;
+          if (lane == d && rr.add[d] != 0)
+            atomicAdd((unsigned long long*)(a.rv->allocd + (int64_t)d * a.rv->nr + nom), (unsigned long long)rr.add[d]);
+        }
+        dd = (t_rdim == 8) ? rr.dnz[0] : (t_rdim == 9) ? rr.dnz[1] : dd;
+        if (lane == 0) atomicAdd(a.rv->assigned + nom, 1);
+        __threadfence();
+        if (rr.now_ineligible) {
+          const uint64_t ncl = rsv_node_classes<true>(*a.rv, node);
+          if (lane == 0) {
+            scls[s] = ncl;
+            atomicExch((unsigned long long*)(a.rv->ncls + node), (unsigned long long)ncl);
+          }
+          __threadfence();
+        }
+        nom_row = a.rv->rowid[nom];
+      }
+      const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+      if (lane < ST_N) {
+        const int64_t v = (take ? podw[t_pw] : 0) + dd;
+        const int64_t v100 = (take ? podw[t_pw100] : 0) + dd * 100;
+        if (take || dd != 0) term_take(row->t[lane], v, v100);
       } else if (lane == kLaneCounts) {
         row->pod_count += 1;
       }
     }
-    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score};
+    int64_t score_out = score;
+    if (RSV) {
+      // the chosen node holds the maximum normalized Reservation score: 100 if hi > 0, else 0
+      const int64_t hi = score / cfg.rsv_F;
+      const int64_t fitla = hi >= kRsvOrderBase ? fitla_pref : score - hi * cfg.rsv_F;
+      score_out = fitla + (hi > 0 ? a.rv->w100 : 0);
+    }
+    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, 0};
     {
       const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
       if (cfg.quota_enable && qrow >= 0) {
@@ -1222,18 +1303,93 @@ __global__ __launch_bounds__(512) void quota_runtime_kernel(QrtArgs a) {
 // ------------------------------------------------------------------------------------------
 
 template <int NSC>
-__global__ void eval_debug_kernel(DevNodes d, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
-                                  int64_t* scores, int64_t* total) {
+__global__ void eval_debug_kernel(DevNodes d, const DevRsv* rv, Cfg c, const PodRec* pod, int64_t n,
+                                  uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   NodeReg<NSC> r;
   load_node<NSC>(c, d, i, 1, r);
   const PodRec p = *pod;
-  const EvalOut o = eval_pod_node<NSC, true>(c, p, r);
+  RsvOut ro;
+  const EvalOut o = eval_full<NSC, true, false, false>(c, rv, p, r, i, &ro);
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
-  total[i] = o.reasons ? -1 : o.total;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
+  total[i] = o.reasons ? -1 : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw;  // Fit + LoadAware part
+  raw[i] = ro.raw;
+  hiord[i] = ro.hiord;
+}
+
+// Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and DefaultNormalizeScore
+// (normalize_score.go:24-52) over the feasible nodes for the debug path (one block).
+__global__ __launch_bounds__(1024) void rsv_normalize_debug_kernel(int64_t n, const uint32_t* reasons,
+                                                                   const int32_t* raw, const int32_t* hiord,
+                                                                   int64_t* scores, int64_t* total, int64_t w) {
+  __shared__ unsigned long long s_pref, s_max;
+  if (threadIdx.x == 0) {
+    s_pref = 0;
+    s_max = 0;
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (reasons[i]) continue;
+    if (hiord[i] > 0)  // larger hiord = smaller order label; ties to the lowest index
+      atomicMax(&s_pref, ((unsigned long long)hiord[i] << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+  }
+  __syncthreads();
+  const bool has_pref = s_pref != 0;
+  const int64_t pref = has_pref ? (int64_t)(0xFFFFFFFFull - (s_pref & 0xFFFFFFFFull)) : -1;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (reasons[i]) continue;
+    atomicMax(&s_max, (unsigned long long)(i == pref ? 1000 : raw[i]));
+  }
+  __syncthreads();
+  const int64_t mx = (int64_t)s_max;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (reasons[i]) continue;
+    const int64_t rs = i == pref ? 1000 : raw[i];
+    const int64_t sc = mx == 0 ? rs : 100 * rs / mx;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = sc;
+    total[i] += sc * w;
+  }
+}
+
+// Base restore of the reservation table (ks_rsv.h): add (sign = +1) or remove (-1) every eligible
+// reservation's unmatched replacement (transformer.go:266-307) on the node columns; with classes != 0
+// also (re)compute the node's matchable owner-class union.  idx = NULL: nodes [0, count).
+__global__ void rsv_base_kernel(DevNodes d, DevRsv rv, const int32_t* idx, int64_t count, int64_t sign, int32_t classes) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  const int64_t n = idx ? idx[t] : t;
+  const int64_t b = rv.beg[n], e = rv.beg[n + 1];
+  int64_t dq[kRsvDims] = {0, 0, 0, 0, 0, 0, 0}, dz[2] = {0, 0};
+  uint64_t cls = 0;
+  for (int64_t i = b; i < e; ++i) {
+    const uint32_t meta = rv.meta[i];
+    const int32_t a = rv.assigned[i];
+    const bool ao = (meta & KS_RSV_ALLOCATE_ONCE) != 0;
+    if (!(ao && a > 0) && !(meta & KS_RSV_UNSCHEDULABLE)) cls |= rv.cls[i];
+    if (ao || a <= 0) continue;  // not eligible, or no assigned pods: not restored as unmatched
+    int64_t rem[kRsvDims];
+    bool nzr = false;
+    for (int dd = 0; dd < kRsvDims; ++dd) {
+      const int64_t v = rv.alloc[dd * rv.nr + i] - rv.allocd[dd * rv.nr + i];
+      rem[dd] = v > 0 ? v : 0;
+      nzr |= rem[dd] != 0;
+    }
+    for (int dd = 0; dd < kRsvDims; ++dd) dq[dd] += (nzr ? rem[dd] : 0) - rv.alloc[dd * rv.nr + i];
+    const uint32_t keys = rsv_keys(meta);
+    dz[0] += (nzr ? ((keys & 1u) ? rem[0] : kDefaultMilliCPU) : 0) - rv.rnz[i];
+    dz[1] += (nzr ? ((keys & 2u) ? rem[1] : kDefaultMemory) : 0) - rv.rnz[rv.nr + i];
+  }
+  d.req_cpu[n] += sign * dq[0];
+  d.req_mem[n] += sign * dq[1];
+  d.req_eph[n] += sign * dq[2];
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) d.req_sc[k][n] += sign * dq[3 + k];
+  d.nz_cpu[n] += sign * dz[0];
+  d.nz_mem[n] += sign * dz[1];
+  if (classes) d.rsv_cls[n] = cls;
 }
 
 // scatter m staged rows into the node columns (informer deltas)
@@ -1310,6 +1466,16 @@ struct ks_ctx {
   int32_t batch = 64, k = 32;
   RowCol* rowcols = nullptr;  // [RF_N] device column of each slot-row field
   DevNodes* dnodes = nullptr;  // device copy of d (the hot kernels read column pointers from it)
+  // reservations (ks_rsv.h)
+  void* rsv_blob = nullptr;
+  DevRsv rv{};               // host copy of the device table
+  DevRsv* drv = nullptr;     // device copy (kernels read it through a pointer)
+  bool rsv_based = false;    // node columns hold the base restore of rv
+  int64_t* rsv_allocd_ckpt = nullptr;
+  int32_t* rsv_assigned_ckpt = nullptr;
+  int32_t rsv_ndist = 0;     // distinct order labels
+  int32_t rsv_nrows = 0;     // caller rows
+  std::vector<int32_t> rsv_perm;  // CSR position -> caller row
   // debug
   PodRec* dbg_pod = nullptr;
   // stats
@@ -1366,6 +1532,11 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   // LeastAllocated Fit + LoadAware: a commit only raises requested/estimated usage, so a node's
   // key can only drop and its Filter can only start failing.
   k.monotone = c.fit.strategy == KS_LEAST_ALLOCATED || !c.fit.enable_score;
+  k.rsv = c.reservation.enable ? 1 : 0;
+  k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
+                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0)) + 1);
+  // a commit into a reservation can raise that node's Reservation score for later pods
+  if (k.rsv) k.monotone = 0;
   return k;
 }
 
@@ -1405,6 +1576,15 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   if (cfg->fit.plugin_weight < 0 || cfg->loadaware.plugin_weight < 0 || max_total >= (1 << 25)) {
     g_create_error = "ks_create: plugin weights out of supported range";
     return KS_EINVAL;
+  }
+  if (cfg->reservation.enable) {
+    const int64_t fitla = 100 * ((cfg->fit.enable_score ? cfg->fit.plugin_weight : 0) +
+                                 (cfg->loadaware.enable_score ? cfg->loadaware.plugin_weight : 0));
+    if (cfg->reservation.plugin_weight <= fitla || cfg->reservation.plugin_weight > ((int64_t)1 << 40) ||
+        (fitla + 1) * (kRsvOrderBase + 1) >= (1 << 26)) {
+      g_create_error = "ks_create: Reservation plugin weight must exceed 100 x (Fit + LoadAware weights) (ks_rsv.h ranking)";
+      return KS_EUNSUPPORTED;
+    }
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -1475,6 +1655,8 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->dbg_pod; dev_free(p);
   p = ctx->rowcols; dev_free(p);
   p = ctx->dnodes; dev_free(p);
+  p = ctx->drv; dev_free(p);
+  dev_free(ctx->rsv_blob);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1495,6 +1677,7 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.la_term_mem, 8, true);
   add(&d.la_pterm_cpu, 8, true);
   add(&d.la_pterm_mem, 8, true);
+  add(&d.rsv_cls, 8, true);
   add(&d.pod_count, 4, true);
   // read-only columns
   add(&d.alloc_cpu, 8, false);
@@ -1531,6 +1714,7 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->la_term_memory);
   v.push_back(c->la_prod_term_milli_cpu);
   v.push_back(c->la_prod_term_memory);
+  v.push_back(nullptr);  // rsv_cls: derived from the reservation table
   v.push_back(c->pod_count);
   v.push_back(c->alloc_milli_cpu);
   v.push_back(c->alloc_memory);
@@ -1603,6 +1787,7 @@ static int upload_rowcols(ks_ctx* ctx) {
   set(RF_LA_ALLOC_MEM, d.la_alloc_mem, 8);
   set(RF_ALLOWED, d.allowed_pods, 4);
   set(RF_LA_BITS, d.la_bits, 4);
+  set(RF_RSV_CLS, d.rsv_cls, 8);
   if (!ctx->rowcols) {
     void* p = nullptr;
     if (dev_alloc(ctx, &p, sizeof(h)) != KS_OK) return KS_ENOMEM;
@@ -1629,6 +1814,8 @@ static int upload_prep_nodes(ks_ctx* ctx) {
   return KS_OK;
 }
 
+static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
+
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
   if (validate_nodes(ctx, nodes, n) != KS_OK) return KS_EINVAL;
@@ -1639,6 +1826,8 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   void* p = ctx->sweep_out;
   dev_free(p);
   ctx->sweep_out = nullptr;
+  ctx->rsv_based = false;  // fresh columns (a loaded reservation table is dropped: reload it)
+  ctx->rsv_nrows = 0;
   ctx->n = n;
   ctx->nchunks = (n + 63) / 64;
   if (ctx->nchunks == 0) ctx->nchunks = 1;
@@ -1673,7 +1862,156 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   ctx->sweep_out = (uint2*)p;
   if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
+  if (ctx->cfg.reservation.enable && rsv_install(ctx, nullptr, 0) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+static int rsv_launch_base(ks_ctx* ctx, const int32_t* didx, int64_t count, int64_t sign, int32_t classes) {
+  if (count <= 0) return KS_OK;
+  hipLaunchKernelGGL(rsv_base_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, ctx->stream, ctx->d, ctx->rv,
+                     didx, count, sign, classes);
+  HIPCHK(ctx, hipGetLastError());
+  return KS_OK;
+}
+
+// Upload the reservation table (CSR by node), add its base restore to the node columns.
+static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
+  constexpr int D = kRsvDims;
+  if (nr > 0 && (!rc || !rc->node || !rc->owner_classes || !rc->key_mask))
+    KS_FAIL(ctx, KS_EINVAL, "ks_reservation_cols: node, owner_classes and key_mask are required");
+  for (int32_t r = 0; r < nr; ++r) {
+    if (rc->node[r] < 0 || rc->node[r] >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "reservation %d: node %d out of range", r, rc->node[r]);
+    if (rc->assigned && rc->assigned[r] < 0) KS_FAIL(ctx, KS_EINVAL, "reservation %d: negative assigned count", r);
+    if (rc->key_mask[r] >> D) KS_FAIL(ctx, KS_EINVAL, "reservation %d: key_mask has bits beyond KS_RSV_DIMS", r);
+  }
+  for (int d = 0; d < D; ++d) {
+    if (check_range64(ctx, rc ? rc->allocatable[d] : nullptr, nr, "reservation allocatable") != KS_OK) return KS_EINVAL;
+    if (check_range64(ctx, rc ? rc->allocated[d] : nullptr, nr, "reservation allocated") != KS_OK) return KS_EINVAL;
+  }
+  if (nr > 0) {
+    if (check_range64(ctx, rc->reserve_nonzero_milli_cpu, nr, "reserve_nonzero_milli_cpu") != KS_OK) return KS_EINVAL;
+    if (check_range64(ctx, rc->reserve_nonzero_memory, nr, "reserve_nonzero_memory") != KS_OK) return KS_EINVAL;
+  }
+  // order labels -> composite ranks (smaller label = larger hi)
+  std::vector<int64_t> ords;
+  for (int32_t r = 0; r < nr; ++r)
+    if (rc->order && rc->order[r] != 0) ords.push_back(rc->order[r]);
+  std::sort(ords.begin(), ords.end());
+  ords.erase(std::unique(ords.begin(), ords.end()), ords.end());
+  const int64_t ndist = (int64_t)ords.size();
+  if ((int64_t)(kRsvOrderBase + ndist + 1) * ctx->kc.rsv_F >= ((int64_t)1 << 26))
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "too many distinct reservation order labels (%lld) for the key width", (long long)ndist);
+  // remove the previous table's base restore
+  if (ctx->rsv_based) {
+    if (rsv_launch_base(ctx, nullptr, ctx->n, -1, 0) != KS_OK) return KS_EHIP;
+    ctx->rsv_based = false;
+  }
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<int32_t> perm(nr);
+  for (int32_t r = 0; r < nr; ++r) perm[r] = r;
+  std::stable_sort(perm.begin(), perm.end(), [&](int32_t x, int32_t y) { return rc->node[x] < rc->node[y]; });
+  const size_t m = (size_t)(nr > 0 ? nr : 1);
+  auto al16 = [](size_t x) { return (x + 15) / 16 * 16; };
+  const size_t o_beg = 0, o_cls = al16((size_t)(ctx->npad + 1) * 4), o_meta = o_cls + al16(m * 8),
+               o_ohi = o_meta + al16(m * 4), o_alloc = o_ohi + al16(m * 4), o_allocd = o_alloc + al16(D * m * 8),
+               o_asg = o_allocd + al16(D * m * 8), o_rnz = o_asg + al16(m * 4), o_row = o_rnz + al16(2 * m * 8),
+               o_ck_allocd = o_row + al16(m * 4), o_ck_asg = o_ck_allocd + al16(D * m * 8),
+               bytes = o_ck_asg + al16(m * 4);
+  std::vector<char> h(bytes, 0);
+  int32_t* beg = (int32_t*)(h.data() + o_beg);
+  uint64_t* cls = (uint64_t*)(h.data() + o_cls);
+  uint32_t* meta = (uint32_t*)(h.data() + o_meta);
+  int32_t* ohi = (int32_t*)(h.data() + o_ohi);
+  int64_t* alloc = (int64_t*)(h.data() + o_alloc);
+  int64_t* allocd = (int64_t*)(h.data() + o_allocd);
+  int32_t* asg = (int32_t*)(h.data() + o_asg);
+  int64_t* rnz = (int64_t*)(h.data() + o_rnz);
+  int32_t* rowid = (int32_t*)(h.data() + o_row);
+  for (int32_t i = 0; i < nr; ++i) beg[rc->node[perm[i]] + 1]++;
+  for (int64_t n = 0; n < ctx->npad; ++n) beg[n + 1] += beg[n];
+  for (int32_t i = 0; i < nr; ++i) {
+    const int32_t r = perm[i];
+    rowid[i] = r;
+    cls[i] = rc->owner_classes[r];
+    const uint32_t flags = rc->flags ? rc->flags[r] & 0xfu : 0u;
+    const uint32_t pol = rc->policy ? std::min<uint32_t>(rc->policy[r], 0xfu) : 0u;
+    meta[i] = flags | (pol << 4) | (rc->key_mask[r] << 8);
+    const int64_t o = rc->order ? rc->order[r] : 0;
+    if (o != 0) {
+      const int64_t rank = std::lower_bound(ords.begin(), ords.end(), o) - ords.begin();
+      ohi[i] = (int32_t)(kRsvOrderBase + (ndist - 1 - rank));
+    }
+    for (int d = 0; d < D; ++d) {
+      alloc[(size_t)d * m + i] = rc->allocatable[d] ? rc->allocatable[d][r] : 0;
+      allocd[(size_t)d * m + i] = rc->allocated[d] ? rc->allocated[d][r] : 0;
+    }
+    asg[i] = rc->assigned ? rc->assigned[r] : 0;
+    // reserve pod's NonZeroRequested (one container with the allocatable as requests by default)
+    const uint32_t keys = rc->key_mask[r];
+    rnz[i] = rc->reserve_nonzero_milli_cpu ? rc->reserve_nonzero_milli_cpu[r]
+                                           : ((keys & 1u) ? alloc[i] : kDefaultMilliCPU);
+    rnz[m + i] = rc->reserve_nonzero_memory ? rc->reserve_nonzero_memory[r]
+                                            : ((keys & 2u) ? alloc[m + i] : kDefaultMemory);
+  }
+  dev_free(ctx->rsv_blob);
+  if (dev_alloc(ctx, &ctx->rsv_blob, bytes) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_blob, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+  char* b = (char*)ctx->rsv_blob;
+  DevRsv& rv = ctx->rv;
+  rv.beg = (const int32_t*)(b + o_beg);
+  rv.cls = (const uint64_t*)(b + o_cls);
+  rv.meta = (const uint32_t*)(b + o_meta);
+  rv.ohi = (const int32_t*)(b + o_ohi);
+  rv.alloc = (const int64_t*)(b + o_alloc);
+  rv.allocd = (int64_t*)(b + o_allocd);
+  rv.assigned = (int32_t*)(b + o_asg);
+  rv.rnz = (const int64_t*)(b + o_rnz);
+  rv.rowid = (const int32_t*)(b + o_row);
+  rv.ncls = ctx->d.rsv_cls;
+  rv.nr = (int64_t)m;  // row stride of the [dim][row] tables
+  rv.w100 = 100 * ctx->cfg.reservation.plugin_weight;
+  ctx->rsv_allocd_ckpt = (int64_t*)(b + o_ck_allocd);
+  ctx->rsv_assigned_ckpt = (int32_t*)(b + o_ck_asg);
+  ctx->rsv_ndist = (int32_t)ndist;
+  ctx->rsv_nrows = nr;
+  ctx->rsv_perm = perm;
+  if (!ctx->drv) {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, sizeof(DevRsv)) != KS_OK) return KS_ENOMEM;
+    ctx->drv = (DevRsv*)p;
+  }
+  HIPCHK(ctx, hipMemcpyAsync(ctx->drv, &ctx->rv, sizeof(DevRsv), hipMemcpyHostToDevice, ctx->stream));
+  if (rsv_launch_base(ctx, nullptr, ctx->n, +1, 1) != KS_OK) return KS_EHIP;
+  ctx->rsv_based = true;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_load_reservations(ks_ctx* ctx, const ks_reservation_cols* rsv, int32_t r) {
+  if (!ctx || r < 0 || (r > 0 && !rsv)) return ctx ? (ctx->err = "ks_load_reservations: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_load_reservations before ks_load_nodes");
+  if (!ctx->cfg.reservation.enable) KS_FAIL(ctx, KS_ESTATE, "ks_load_reservations: the Reservation plugin is not enabled");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  return rsv_install(ctx, rsv, r);
+}
+
+int ks_read_reservations(ks_ctx* ctx, int64_t* allocated, int32_t* assigned) {
+  if (!ctx) return KS_EINVAL;
+  const int32_t nr = ctx->rsv_nrows;
+  if (nr == 0 || !ctx->rsv_blob) return KS_OK;
+  const size_t m = (size_t)ctx->rv.nr;
+  std::vector<int64_t> ad(kRsvDims * m);
+  std::vector<int32_t> as(m);
+  HIPCHK(ctx, hipMemcpyAsync(ad.data(), ctx->rv.allocd, ad.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(as.data(), ctx->rv.assigned, m * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  for (int32_t i = 0; i < nr; ++i) {
+    const int32_t r = ctx->rsv_perm[i];
+    if (allocated)
+      for (int d = 0; d < kRsvDims; ++d) allocated[(size_t)r * kRsvDims + d] = ad[(size_t)d * m + i];
+    if (assigned) assigned[r] = as[i];
+  }
   return KS_OK;
 }
 
@@ -1683,6 +2021,12 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
   if (m == 0) return KS_OK;
   for (int64_t i = 0; i < m; ++i)
     if (idx[i] < 0 || idx[i] >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: idx[%lld]=%d out of range", (long long)i, idx[i]);
+  if (ctx->rsv_based) {
+    std::vector<int32_t> sorted(idx, idx + m);
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+      KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: duplicate node index with reservations loaded");
+  }
   if (validate_nodes(ctx, rows, m) != KS_OK) return KS_EINVAL;
   std::vector<const void*> src = host_cols(rows);
   std::vector<void*> dst;
@@ -1723,6 +2067,8 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
                      (const int32_t*)(dm + 2 * ncols * sizeof(void*)), (int32_t)ncols,
                      (const int32_t*)((char*)dbuf + idx_off), m);
   HIPCHK(ctx, hipGetLastError());
+  // the replaced rows are the reference's NodeInfo: add the reservation base restore again
+  if (ctx->rsv_based && rsv_launch_base(ctx, (const int32_t*)((char*)dbuf + idx_off), m, +1, 0) != KS_OK) return KS_EHIP;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   (void)hipFree(dbuf);
@@ -1922,8 +2268,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   const size_t res = ((size_t)cap * sizeof(ks_result) + 255) / 256 * 256;
   const size_t col8 = ((size_t)cap * 8 + 255) / 256 * 256;
   const size_t col4 = ((size_t)cap * 4 + 255) / 256 * 256;
-  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 qreq[8] = 23 int64 cols; flags quota qmask = 3 x32
-  const size_t bytes = rec + res + col8 * 23 + col4 * 3;
+  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 qreq[8] = 23 int64 cols; flags quota qmask rsv_class = 4 x32
+  const size_t bytes = rec + res + col8 * 23 + col4 * 4;
   if (dev_alloc(ctx, &ctx->pod_blob, bytes) != KS_OK) return KS_ENOMEM;
   char* b = (char*)ctx->pod_blob;
   ctx->pods = (PodRec*)b;
@@ -1946,6 +2292,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   s.quota = (int32_t*)b;
   b += col4;
   ctx->pq.mask = (uint32_t*)b;
+  b += col4;
+  s.rsv_class = (int32_t*)b;
   ctx->pod_cap = cap;
   return KS_OK;
 }
@@ -1976,6 +2324,8 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
   else HIPCHK(ctx, hipMemsetAsync(s.quota, 0xFF, (size_t)p * 4, ctx->stream));
   if (pc->quota_mask) HIPCHK(ctx, hipMemcpyAsync(ctx->pq.mask, pc->quota_mask, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(ctx->pq.mask, 0, (size_t)p * 4, ctx->stream));
+  if (pc->rsv_class) HIPCHK(ctx, hipMemcpyAsync(s.rsv_class, pc->rsv_class, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(s.rsv_class, 0xFF, (size_t)p * 4, ctx->stream));
   const int threads = 256;
   hipLaunchKernelGGL(prep_pods_kernel, dim3((p + threads - 1) / threads), dim3(threads), 0, ctx->stream, s, dst, p,
                      ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory);
@@ -1990,6 +2340,11 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
     if (check_range64(ctx, c, p, "pod quantity") != KS_OK) return KS_EINVAL;
   for (int k = 0; k < KS_MAX_SCALARS; ++k)
     if (check_range64(ctx, pc->req_scalar[k], p, "pod scalar") != KS_OK) return KS_EINVAL;
+  if (pc->rsv_class) {
+    for (int32_t i = 0; i < p; ++i)
+      if (pc->rsv_class[i] < -1 || pc->rsv_class[i] >= KS_RSV_CLASSES)
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: reservation class %d outside [-1, %d)", i, pc->rsv_class[i], KS_RSV_CLASSES);
+  }
   if (pc->quota) {
     for (int32_t i = 0; i < p; ++i)
       if (pc->quota[i] >= ctx->q.q || pc->quota[i] < -1)
@@ -2054,6 +2409,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   auto shard_lo = [&](int32_t sh) { return ctx->nchunks * sh / S; };
   SweepArgs sa;
   sa.dn = ctx->dnodes;
+  sa.rv = ctx->drv;
   sa.c = ctx->kc;
   sa.pods = ctx->pods;
   sa.cursor = ctx->cursor;
@@ -2066,7 +2422,10 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.batch = ctx->batch;
   sa.ppw = ppw;
   rec(0);
-  hipLaunchKernelGGL(sweep_kernel<NSC>, dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  if (ctx->kc.rsv)
+    hipLaunchKernelGGL((sweep_kernel<NSC, true>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  else
+    hipLaunchKernelGGL((sweep_kernel<NSC, false>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
   rec(0);
   SelectArgs se;
   se.in = ctx->sweep_out;
@@ -2123,6 +2482,7 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   rec(1);
   CommitArgs ca;
   ca.dn = ctx->dnodes;
+  ca.rv = ctx->drv;
   ca.c = ctx->kc;
   ca.pods = ctx->pods;
   ca.pq = ctx->pq;
@@ -2144,10 +2504,17 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   const bool qcache = commit_qcache(ctx);
   const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache).total;
   rec(2);
-  if (qcache)
-    hipLaunchKernelGGL((commit_kernel<NSC, true>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
-  else
-    hipLaunchKernelGGL((commit_kernel<NSC, false>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
+  if (ctx->kc.rsv) {
+    if (qcache)
+      hipLaunchKernelGGL((commit_kernel<NSC, true, true>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
+    else
+      hipLaunchKernelGGL((commit_kernel<NSC, false, true>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
+  } else {
+    if (qcache)
+      hipLaunchKernelGGL((commit_kernel<NSC, true, false>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
+    else
+      hipLaunchKernelGGL((commit_kernel<NSC, false, false>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
+  }
   rec(2);
 }
 
@@ -2166,9 +2533,16 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     auto setattr = [&](const void* fn) {
       if (e == hipSuccess) e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     };
-    if (ctx->nsc == 0) qcache ? setattr((const void*)commit_kernel<0, true>) : setattr((const void*)commit_kernel<0, false>);
-    else if (ctx->nsc == 2) qcache ? setattr((const void*)commit_kernel<2, true>) : setattr((const void*)commit_kernel<2, false>);
-    else qcache ? setattr((const void*)commit_kernel<4, true>) : setattr((const void*)commit_kernel<4, false>);
+    const bool rs = ctx->kc.rsv != 0;
+#define KS_SETATTR(N)                                                                       \
+  do {                                                                                      \
+    if (rs) qcache ? setattr((const void*)commit_kernel<N, true, true>) : setattr((const void*)commit_kernel<N, false, true>); \
+    else qcache ? setattr((const void*)commit_kernel<N, true, false>) : setattr((const void*)commit_kernel<N, false, false>); \
+  } while (0)
+    if (ctx->nsc == 0) KS_SETATTR(0);
+    else if (ctx->nsc == 2) KS_SETATTR(2);
+    else KS_SETATTR(4);
+#undef KS_SETATTR
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
     const size_t sel_smem = (size_t)ctx->nchunks * sizeof(uint2) + kSelHistBins * 4;
     if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
@@ -2242,7 +2616,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     }
   }
   // algorithmic bytes of one full sweep launch: node columns read once per pod group + outputs
-  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16;
+  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16 + (ctx->kc.rsv ? 8 : 0);
   const int64_t groups = (ctx->batch + ppw - 1) / ppw;
   ctx->stats.sweep_bytes = local_chunks * 64 * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + local_chunks * 64 * 4;
   return KS_OK;
@@ -2278,6 +2652,10 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->quota_used_ckpt, ctx->q.used, tb, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->quota_npused_ckpt, ctx->q.npused, tb, hipMemcpyDeviceToDevice, ctx->stream));
   }
+  if (ctx->rsv_blob) {
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_allocd_ckpt, ctx->rv.allocd, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -2289,6 +2667,10 @@ int ks_restore(ks_ctx* ctx) {
     const size_t tb = (size_t)(ctx->q.q > 0 ? ctx->q.q : 1) * KS_QUOTA_DIMS * 8;
     HIPCHK(ctx, hipMemcpyAsync(ctx->q.used, ctx->quota_used_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->q.npused, ctx->quota_npused_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
+  }
+  if (ctx->rsv_blob) {
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
@@ -2303,19 +2685,24 @@ int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, in
   if (stage_pods_to(ctx, pod, 1, ctx->dbg_pod) != KS_OK) return KS_EHIP;
   const int64_t n = ctx->n;
   void* buf = nullptr;
-  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8) + 64;
+  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8) + 64;
   if (dev_alloc(ctx, &buf, bytes) != KS_OK) return KS_ENOMEM;
   uint32_t* dr = (uint32_t*)buf;
   int64_t* ds = (int64_t*)((char*)buf + ((size_t)n * 4 + 15) / 16 * 16);
   int64_t* dt = ds + (size_t)n * KS_NUM_SCORE_PLUGINS;
+  int32_t* draw = (int32_t*)(dt + n);
+  int32_t* dhi = draw + n;
   const int threads = 256;
   const int blocks = (int)((n + threads - 1) / threads);
   if (blocks > 0) {
     switch (ctx->nsc) {
-      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->kc, ctx->dbg_pod, n, dr, ds, dt); break;
-      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->kc, ctx->dbg_pod, n, dr, ds, dt); break;
-      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->kc, ctx->dbg_pod, n, dr, ds, dt); break;
+      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi); break;
+      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi); break;
+      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi); break;
     }
+    if (ctx->kc.rsv)
+      hipLaunchKernelGGL(rsv_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, draw, dhi, ds, dt,
+                         ctx->cfg.reservation.plugin_weight);
   }
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && reasons && n) e = hipMemcpyAsync(reasons, dr, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream);
@@ -2335,6 +2722,8 @@ int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
     if (!h || !n) return hipSuccess;
     return hipMemcpyAsync(h, d, n * w, hipMemcpyDeviceToHost, ctx->stream);
   };
+  // the columns hold the reservation base restore: report the reference's NodeInfo
+  if (ctx->rsv_based && rsv_launch_base(ctx, nullptr, ctx->n, -1, 0) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, cp(o->req_milli_cpu, ctx->d.req_cpu, 8));
   HIPCHK(ctx, cp(o->req_memory, ctx->d.req_mem, 8));
   HIPCHK(ctx, cp(o->req_ephemeral, ctx->d.req_eph, 8));
@@ -2346,6 +2735,7 @@ int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
   HIPCHK(ctx, cp(o->la_term_memory, ctx->d.la_term_mem, 8));
   HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, ctx->d.la_pterm_cpu, 8));
   HIPCHK(ctx, cp(o->la_prod_term_memory, ctx->d.la_pterm_mem, 8));
+  if (ctx->rsv_based && rsv_launch_base(ctx, nullptr, ctx->n, +1, 0) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }

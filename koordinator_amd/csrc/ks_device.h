@@ -49,6 +49,8 @@ struct Cfg {
   int32_t lw_cpu, lw_mem, la_pw;
   int32_t quota_enable, quota_parent;
   int32_t monotone;  // commits can only lower a node's key (LeastAllocated + LoadAware)
+  int32_t rsv;       // Reservation plugin enabled
+  int32_t rsv_F;     // key radix: key total = hi * rsv_F + (Fit + LoadAware weighted total), see ks_rsv.h
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -65,6 +67,7 @@ struct DevNodes {
   int32_t *la_thr_cpu, *la_thr_mem, *la_pthr_cpu, *la_pthr_mem;
   int64_t *la_total_cpu, *la_total_mem, *la_usage_cpu, *la_usage_mem, *la_pusage_cpu, *la_pusage_mem;
   uint32_t *la_bits;  // derived by prep_nodes_kernel
+  uint64_t *rsv_cls;  // union of the owner classes of the node's matchable reservations (ks_rsv.h)
 };
 
 // Per-pod record read by the sweep with scalar loads (AoS, 192 B).  The x100 and f32 copies feed
@@ -79,7 +82,9 @@ struct __attribute__((aligned(16))) PodRec {
   int64_t h_sc[KS_MAX_SCALARS];                            // words 17..20
   float f_nzcpu, f_nzmem, f_eph, f_est_cpu, f_est_mem;     // f32 of the same requests
   float f_sc[KS_MAX_SCALARS];
-  float _fpad[3];
+  int32_t rsv_class;  // reservation match class (-1 = none)
+  uint32_t rsv_keys;  // bit d: request dimension d is non-zero (a key of the pod's requests)
+  float _fpad;
 };
 static_assert(sizeof(PodRec) == 224, "PodRec layout");
 
@@ -209,6 +214,7 @@ struct __attribute__((aligned(16))) NodeReg {
   int32_t allowed;
   int32_t pod_count;
   int32_t valid;
+  uint64_t rsv_cls;                            // owner classes of matchable reservations (0 = none)
 };
 
 template <int NSC>
@@ -255,6 +261,7 @@ __device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int val
   r.pod_count = pod_count;
   r.pods_full = ((int64_t)pod_count + 1 > (int64_t)allowed) || !valid;
   r.fit_ws = node_fit_ws<NSC>(c, r);
+  r.rsv_cls = 0;
 }
 
 template <int NSC>
@@ -271,6 +278,7 @@ __device__ __forceinline__ void load_node(const Cfg& c, const DevNodes& d, int64
                  gld(d.la_alloc_cpu + n), gld(d.la_alloc_mem + n), gld(d.la_term_cpu + n), gld(d.la_term_mem + n),
                  gld(d.la_pterm_cpu + n), gld(d.la_pterm_mem + n), gld(d.la_bits + n), gld(d.allowed_pods + n),
                  gld(d.pod_count + n));
+  if (c.rsv && valid) r.rsv_cls = gld(d.rsv_cls + n);
 }
 
 // Reserve: NodeInfo.AddPod (upstream framework/types.go) + podAssignCache.assign

@@ -1,0 +1,331 @@
+// ks_rsv.h — Reservation plugin on the device (pkg/scheduler/plugins/reservation).
+//
+// Node columns hold the "base" NodeInfo: the reference's NodeInfo (reserve pods included) with
+// every eligible reservation that has assigned pods already replaced by its remainder, i.e. the
+// restoreUnmatchedReservations step (transformer.go:266-307) applied as if no reservation matched
+// the pod.  That part is pod-independent.  For a (pod, node) pair whose pod class matches some of
+// the node's reservations, rsv_eval turns the base into the pod's restored NodeInfo
+// (restoreMatchedReservation :241-264 for the matched ones, undoing their unmatched step), and
+// derives nodeRState.podRequested / rAllocated for fitsNode (plugin.go:445-496), the Reservation
+// Filter (:311-440), the nomination (nominator.go:134-192, FilterReservation plugin.go:503-530)
+// and scoreReservation (scoring.go:183-203).
+//
+// Score ranking.  Reservation's Score is 1000 on the PreScore-preferred node (lowest order label
+// among feasible nodes, scoring.go:87-96), the nominated reservation's score elsewhere, then
+// DefaultNormalizeScore(100) and weight w (5000).  With w > 100 * (Fit + LoadAware weights) the
+// weighted totals order nodes exactly by (hi, Fit+LoadAware total, lowest index) where
+// hi = 101 + rank of the node's best order label (larger for smaller labels) when it has an ordered
+// matched reservation, else the raw score (0..100): the preferred node scores 100*w and every other
+// node at most 10*w + (Fit+LA), and without a preferred node floor(100*raw/max) is strictly
+// increasing in raw for max <= 100.  So the key total is hi * F + (Fit+LA) with F = max(Fit+LA)+1,
+// which depends on the node alone: untouched nodes keep their snapshot keys under commits exactly
+// as for the other plugins.  Ordered nodes drop the Fit+LA part (hi * F alone): among equal order
+// labels the preferred node is the lowest index (scoring.go:87-96), not the best Fit+LA.  The
+// chosen node's reference total is (Fit+LA) + 100*w when hi > 0 (it holds the maximum raw score or
+// is the preferred node) and (Fit+LA) otherwise.
+#pragma once
+
+#include "ks_device.h"
+
+namespace ks {
+
+constexpr int kRsvDims = KS_RSV_DIMS;
+constexpr int64_t kDefaultMilliCPU = 100;                 // schedutil.DefaultMilliCPURequest
+constexpr int64_t kDefaultMemory = 200ll * 1024 * 1024;   // schedutil.DefaultMemoryRequest
+constexpr int32_t kRsvOrderBase = 101;                    // hi of an ordered node > any raw score
+
+// meta word: flags (KS_RSV_*) | policy << 4 | key_mask << 8
+__device__ __forceinline__ uint32_t rsv_policy(uint32_t m) { return (m >> 4) & 0xfu; }
+__device__ __forceinline__ uint32_t rsv_keys(uint32_t m) { return (m >> 8) & 0xffu; }
+
+// Reservation table in CSR order (rows of node n at [beg[n], beg[n+1]), table order within a node).
+struct DevRsv {
+  const int32_t* beg;     // [npad + 1]
+  const uint64_t* cls;    // owner classes
+  const uint32_t* meta;
+  const int32_t* ohi;     // kRsvOrderBase + (#distinct orders - 1 - rank of the order label); 0 = none
+  const int64_t* alloc;   // [kRsvDims][nr]
+  int64_t* allocd;        // [kRsvDims][nr]  mutable (Reserve)
+  int32_t* assigned;      // [nr]            mutable (Reserve)
+  const int64_t* rnz;     // [2][nr] reserve pod NonZeroRequested cpu / memory
+  uint64_t* ncls;         // = DevNodes.rsv_cls
+  const int32_t* rowid;   // CSR position -> caller row
+  int64_t nr;
+  int64_t w100;           // 100 * plugin weight
+};
+
+// Mutable reservation fields read inside the commit kernel go around the CU's L1 (agent-scope
+// relaxed loads = global_load sc1): the same wave wrote them a few pods earlier.
+template <bool FRESH, typename T>
+__device__ __forceinline__ T rld(const T* p) {
+  if (FRESH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return gld(p);
+}
+
+__device__ __forceinline__ int64_t pod_dim(const PodRec& p, int d) {
+  return d == 0 ? p.cpu : d == 1 ? p.mem : d == 2 ? p.eph : p.sc[d - 3];
+}
+
+// exact floor(100 * req / cap) for 0 <= req <= cap < 2^56 (f32 estimate + int64 correction)
+__device__ __forceinline__ int32_t pct_floor(int64_t req, int64_t cap) {
+  int32_t q = (int32_t)(i64_to_f32(req) * 100.0f * __builtin_amdgcn_rcpf(i64_to_f32(cap)));
+  const int64_t r = req * 100 - (int64_t)q * cap;
+  q += (r >= cap) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return q;
+}
+
+// Per-(pod, node) restore deltas relative to the base NodeInfo.
+template <int NSC>
+struct RsvDelta {
+  int64_t dreq[3 + NSC];  // Requested (cpu, memory, ephemeral, scalars)
+  int64_t dnz[2];         // NonZeroRequested
+  int32_t nm;             // len(matched)
+};
+
+struct RsvOut {
+  uint32_t reasons;  // KS_R_RSV_*
+  int32_t hi;        // ranking key component (see header)
+  int32_t raw;       // scoreReservation of the nominated reservation (0 = none)
+  int32_t hiord;     // kRsvOrderBase+... of the node's best order label over matched (0 = none)
+  int32_t nom;       // nominated reservation, CSR position (-1 = none)
+};
+
+template <bool FRESH>
+__device__ __forceinline__ bool rsv_matches(const DevRsv& rv, int64_t i, int32_t cls, uint32_t& meta, int32_t& a) {
+  meta = gld(rv.meta + i);
+  a = rld<FRESH>(rv.assigned + i);
+  const bool eligible = !((meta & KS_RSV_ALLOCATE_ONCE) && a > 0);  // transformer.go:109
+  return eligible && !(meta & KS_RSV_UNSCHEDULABLE) && ((gld(rv.cls + i) >> cls) & 1ull);
+}
+
+// scoreReservation (scoring.go:183-203): MostAllocated over the non-zero allocatable dims
+template <bool FRESH>
+__device__ __forceinline__ int32_t rsv_score(const DevRsv& rv, const PodRec& p, int64_t i) {
+  int32_t s = 0, w = 0;
+#pragma unroll
+  for (int d = 0; d < kRsvDims; ++d) {
+    const int64_t al = gld(rv.alloc + d * rv.nr + i);
+    if (al == 0) continue;
+    ++w;
+    const int64_t req = pod_dim(p, d) + rld<FRESH>(rv.allocd + d * rv.nr + i);
+    if (req <= al) s += pct_floor(req, al);
+  }
+  return w ? s / w : 0;
+}
+
+// BeforePreFilter restore + Reservation Filter + nomination for one (pod, node); r is the base row.
+template <int NSC, bool FRESH>
+__device__ __forceinline__ RsvOut rsv_eval(const DevRsv& rv, const PodRec& p, const NodeReg<NSC>& r, int64_t node,
+                                        RsvDelta<NSC>& dl) {
+  constexpr int D = 3 + NSC;
+  const int32_t cls = p.rsv_class;
+  const int64_t b = gld(rv.beg + node), e = gld(rv.beg + node + 1);
+  int64_t dpre[D], ral[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) dl.dreq[d] = dpre[d] = ral[d] = 0;
+  dl.dnz[0] = dl.dnz[1] = 0;
+  int32_t nm = 0, hiord = 0;
+  for (int64_t i = b; i < e; ++i) {
+    uint32_t meta;
+    int32_t a;
+    if (!rsv_matches<FRESH>(rv, i, cls, meta, a)) continue;
+    ++nm;
+    hiord = max(hiord, gld(rv.ohi + i));
+    int64_t rem[kRsvDims];
+    bool nzr = false;
+#pragma unroll
+    for (int d = 0; d < kRsvDims; ++d) {
+      const int64_t v = gld(rv.alloc + d * rv.nr + i) - rld<FRESH>(rv.allocd + d * rv.nr + i);
+      rem[d] = v > 0 ? v : 0;  // quotav1.SubtractWithNonNegativeResult
+      nzr |= rem[d] != 0;
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int64_t al = gld(rv.alloc + d * rv.nr + i);
+      const int64_t kept = nzr ? rem[d] : 0;
+      dl.dreq[d] -= a > 0 ? kept : al;  // matched: reserve pod removed; base had it replaced by `kept`
+      dpre[d] += a > 0 ? al - kept : 0; // podRequested: this one is not in the pod's unmatched set
+      ral[d] += rld<FRESH>(rv.allocd + d * rv.nr + i);
+    }
+    const uint32_t keys = rsv_keys(meta);
+    const int64_t nzc = nzr ? ((keys & 1u) ? rem[0] : kDefaultMilliCPU) : 0;
+    const int64_t nzm = nzr ? ((keys & 2u) ? rem[1] : kDefaultMemory) : 0;
+    dl.dnz[0] -= a > 0 ? nzc : gld(rv.rnz + i);
+    dl.dnz[1] -= a > 0 ? nzm : gld(rv.rnz + rv.nr + i);
+  }
+  dl.nm = nm;
+  RsvOut o{0u, 0, 0, hiord, -1};
+  const bool aff = (p.flags & KS_POD_RSV_AFFINITY) != 0;
+  if (nm == 0) {
+    o.reasons = aff ? KS_R_RSV_AFFINITY : 0u;
+    return o;
+  }
+  // fitsNode (plugin.go:445-496): pods check on the restored NodeInfo, resources against
+  // Allocatable - (podRequested - rRemained - rAllocated)
+  const bool pods_bad = (int64_t)(r.pod_count - nm) - nm + 1 > (int64_t)r.allowed;
+  const bool all_zero = (p.flags & kPodAllZero) != 0;
+  int64_t slack[D];
+  slack[0] = r.free_cpu - dpre[0] + ral[0];
+  slack[1] = r.free_mem - dpre[1] + ral[1];
+  slack[2] = r.free_eph - dpre[2] + ral[2];
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) slack[3 + k] = r.free_sc[k] - dpre[3 + k] + ral[3 + k];
+  int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0;
+  for (int64_t i = b; i < e; ++i) {
+    uint32_t meta;
+    int32_t a;
+    if (!rsv_matches<FRESH>(rv, i, cls, meta, a)) continue;
+    // filterWithReservations body for one reservation (plugin.go:386-422)
+    const uint32_t names = rsv_keys(meta) & p.rsv_keys;
+    bool ok = names != 0 && !pods_bad;
+    if (ok && !all_zero) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int64_t pd = pod_dim(p, d);
+        if (d >= 3 && pd == 0) continue;  // podRequest.ScalarResources keys
+        const int64_t rrem = gld(rv.alloc + d * rv.nr + i) - rld<FRESH>(rv.allocd + d * rv.nr + i);
+        ok = ok && !(pd > slack[d] + rrem);
+      }
+    }
+    const uint32_t pol = rsv_policy(meta);
+    if (pol == KS_RSV_POLICY_RESTRICTED) {
+#pragma unroll
+      for (int d = 0; d < kRsvDims; ++d) {
+        if (!((names >> d) & 1u)) continue;
+        int64_t rem = gld(rv.alloc + d * rv.nr + i) - rld<FRESH>(rv.allocd + d * rv.nr + i);
+        rem = rem > 0 ? rem : 0;
+        ok = ok && !(pod_dim(p, d) > rem);
+      }
+    } else if (pol != KS_RSV_POLICY_DEFAULT && pol != KS_RSV_POLICY_ALIGNED) {
+      ok = false;
+    }
+    if (!ok) continue;
+    // NominateReservation: lowest order label first (strict, table order), else best score
+    const int32_t oh = gld(rv.ohi + i);
+    const int32_t sc = rsv_score<FRESH>(rv, p, i);
+    if (oh > best_o) {
+      best_o = oh;
+      nom_o = (int32_t)i;
+      raw_o = sc;
+    }
+    if (sc > best_s) {
+      best_s = sc;
+      nom_s = (int32_t)i;
+    }
+  }
+  o.nom = nom_o >= 0 ? nom_o : nom_s;
+  o.raw = nom_o >= 0 ? raw_o : (nom_s >= 0 ? best_s : 0);
+  o.hi = hiord > 0 ? hiord : o.raw;
+  o.reasons = (aff && o.nom < 0) ? KS_R_RSV_NO_FIT : 0u;
+  return o;
+}
+
+// base row <-> the pod's restored row (sign = +1 apply, -1 undo; exact in int64)
+template <int NSC>
+__device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& dl, int64_t sign) {
+  r.free_cpu -= sign * dl.dreq[0];
+  r.free_mem -= sign * dl.dreq[1];
+  r.free_eph -= sign * dl.dreq[2];
+  term_take(r.t_eph, sign * dl.dreq[2], sign * dl.dreq[2] * 100);
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) {
+    r.free_sc[k] -= sign * dl.dreq[3 + k];
+    term_take(r.t_sc[k], sign * dl.dreq[3 + k], sign * dl.dreq[3 + k] * 100);
+  }
+  term_take(r.t_cpu, sign * dl.dnz[0], sign * dl.dnz[0] * 100);
+  term_take(r.t_mem, sign * dl.dnz[1], sign * dl.dnz[1] * 100);
+  r.pod_count -= (int32_t)sign * dl.nm;
+  r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
+}
+
+// Filter + Score of one (pod, node) with the Reservation plugin: total = hi * F + Fit/LA total.
+// r must be the base row; with UNDO it is returned unchanged (the sweep reuses it across pods).
+template <int NSC, bool DEBUG, bool FRESH, bool UNDO, bool RSV = true>
+__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const DevRsv* rvp, const PodRec& p, NodeReg<NSC>& r,
+                                             int64_t node, RsvOut* info = nullptr) {
+  if (!RSV || !c.rsv || (p.rsv_class < 0 && !(p.flags & KS_POD_RSV_AFFINITY))) {
+    if (info) *info = RsvOut{0u, 0, 0, 0, -1};
+    return eval_pod_node<NSC, DEBUG>(c, p, r);
+  }
+  const bool slow = p.rsv_class >= 0 && p.rsv_class < 64 && ((r.rsv_cls >> p.rsv_class) & 1ull);
+  RsvDelta<NSC> dl;
+  RsvOut ro{(p.flags & KS_POD_RSV_AFFINITY) ? KS_R_RSV_AFFINITY : 0u, 0, 0, 0, -1};
+  if (slow) {
+    ro = rsv_eval<NSC, FRESH>(*rvp, p, r, node, dl);
+    rsv_apply<NSC>(r, dl, 1);
+  }
+  EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
+  if (UNDO && slow) rsv_apply<NSC>(r, dl, -1);
+  // a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
+  // NodeNames, plugin.go:235-246) before any Filter plugin runs
+  o.reasons = ro.reasons == KS_R_RSV_AFFINITY ? ro.reasons : (o.reasons | ro.reasons);
+  // the preferred node is the lowest INDEX among equal order labels, whatever its Fit/LoadAware
+  // total: ordered nodes rank by hi alone (ties to the lower index through the key's node bits)
+  o.total = ro.hi >= kRsvOrderBase ? ro.hi * c.rsv_F : o.total + ro.hi * c.rsv_F;
+  if (info) *info = ro;
+  return o;
+}
+
+// Reserve into reservation i (plugin.go:532-570 -> reservation_info.go:379-388): the change of the
+// node's base restore (unmatched remainder of i before / after) for each Requested / NonZero dim.
+struct RsvReserve {
+  int64_t dreq[kRsvDims];
+  int64_t dnz[2];
+  int64_t add[kRsvDims];  // Allocated += Mask(pod requests, ResourceNames)
+  bool now_ineligible;    // AllocateOnce: skipped from now on (transformer.go:109)
+};
+
+template <bool FRESH>
+__device__ __forceinline__ RsvReserve rsv_reserve_delta(const DevRsv& rv, const PodRec& p, int64_t i) {
+  RsvReserve o;
+  const uint32_t meta = gld(rv.meta + i);
+  const uint32_t keys = rsv_keys(meta);
+  const int32_t a_old = rld<FRESH>(rv.assigned + i);
+  const bool ao = (meta & KS_RSV_ALLOCATE_ONCE) != 0;
+  int64_t al[kRsvDims], ro[kRsvDims], rn[kRsvDims];
+  bool nz_old = false, nz_new = false;
+#pragma unroll
+  for (int d = 0; d < kRsvDims; ++d) {
+    al[d] = gld(rv.alloc + d * rv.nr + i);
+    const int64_t ad = rld<FRESH>(rv.allocd + d * rv.nr + i);
+    o.add[d] = ((keys >> d) & 1u) ? pod_dim(p, d) : 0;
+    const int64_t vo = al[d] - ad, vn = al[d] - (ad + o.add[d]);
+    ro[d] = vo > 0 ? vo : 0;
+    rn[d] = vn > 0 ? vn : 0;
+    nz_old |= ro[d] != 0;
+    nz_new |= rn[d] != 0;
+  }
+  // base contribution U(r) = eligible && assigned > 0 ? [rem != 0] * rem - alloc : 0
+#pragma unroll
+  for (int d = 0; d < kRsvDims; ++d) {
+    const int64_t u_old = a_old > 0 ? (nz_old ? ro[d] : 0) - al[d] : 0;
+    const int64_t u_new = !ao ? (nz_new ? rn[d] : 0) - al[d] : 0;
+    o.dreq[d] = u_new - u_old;
+  }
+  const int64_t rnzc = gld(rv.rnz + i), rnzm = gld(rv.rnz + rv.nr + i);
+  const int64_t oc = nz_old ? ((keys & 1u) ? ro[0] : kDefaultMilliCPU) : 0;
+  const int64_t om = nz_old ? ((keys & 2u) ? ro[1] : kDefaultMemory) : 0;
+  const int64_t nc = nz_new ? ((keys & 1u) ? rn[0] : kDefaultMilliCPU) : 0;
+  const int64_t nmm = nz_new ? ((keys & 2u) ? rn[1] : kDefaultMemory) : 0;
+  o.dnz[0] = (!ao ? nc - rnzc : 0) - (a_old > 0 ? oc - rnzc : 0);
+  o.dnz[1] = (!ao ? nmm - rnzm : 0) - (a_old > 0 ? om - rnzm : 0);
+  o.now_ineligible = ao;
+  return o;
+}
+
+// union of owner classes of the node's matchable reservations
+template <bool FRESH>
+__device__ __forceinline__ uint64_t rsv_node_classes(const DevRsv& rv, int64_t node) {
+  const int64_t b = gld(rv.beg + node), e = gld(rv.beg + node + 1);
+  uint64_t m = 0;
+  for (int64_t i = b; i < e; ++i) {
+    const uint32_t meta = gld(rv.meta + i);
+    const int32_t a = rld<FRESH>(rv.assigned + i);
+    if (((meta & KS_RSV_ALLOCATE_ONCE) && a > 0) || (meta & KS_RSV_UNSCHEDULABLE)) continue;
+    m |= gld(rv.cls + i);
+  }
+  return m;
+}
+
+}  // namespace ks

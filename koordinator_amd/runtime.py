@@ -14,13 +14,13 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import NodeState, NodeTable, PodTable, QuotaTable, QuotaTree
+from .cluster import NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
 CSRC = os.path.join(HERE, "csrc")
 
-RESULT_DTYPE = np.dtype([("node", "<i4"), ("status", "<u4"), ("score", "<i8")])
+RESULT_DTYPE = np.dtype(abi.RESULT_DTYPE_FIELDS)
 
 
 class KsError(RuntimeError):
@@ -57,6 +57,8 @@ def lib() -> C.CDLL:
     L.ks_load_nodes.argtypes = [vp, C.POINTER(abi.KsNodeCols), C.c_int64]
     L.ks_update_nodes.argtypes = [vp, abi.P32, C.POINTER(abi.KsNodeCols), C.c_int64]
     L.ks_load_quotas.argtypes = [vp, C.POINTER(abi.KsQuotaCols), C.c_int32]
+    L.ks_load_reservations.argtypes = [vp, C.POINTER(abi.KsReservationCols), C.c_int32]
+    L.ks_read_reservations.argtypes = [vp, abi.P64, abi.P32]
     L.ks_refresh_quota_runtime.argtypes = [vp, C.POINTER(abi.KsQuotaTree), C.c_int32, abi.P64, abi.PU32]
     L.ks_schedule.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
     L.ks_stage_pods.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32]
@@ -90,7 +92,8 @@ def shard_unique_id() -> bytes:
 class Evaluator:
     """One scheduler profile's device-resident node snapshot + the sweep/commit pipeline."""
 
-    def __init__(self, cfg: abi.KsConfig, nodes: Optional[NodeTable] = None, quotas: Optional[QuotaTable] = None):
+    def __init__(self, cfg: abi.KsConfig, nodes: Optional[NodeTable] = None, quotas: Optional[QuotaTable] = None,
+                 reservations: Optional[ReservationTable] = None):
         self.L = lib()
         self.cfg = cfg
         h = C.c_void_p()
@@ -100,11 +103,14 @@ class Evaluator:
         self.h = h
         self.n = 0
         self.nq = 0
+        self.nr = 0
         self.np_staged = 0
         if nodes is not None:
             self.load_nodes(nodes)
         if quotas is not None:
             self.load_quotas(quotas)
+        if reservations is not None:
+            self.load_reservations(reservations)
 
     def _chk(self, rc: int):
         if rc != abi.KS_OK:
@@ -142,6 +148,19 @@ class Evaluator:
         self._chk(self.L.ks_load_quotas(self.h, C.byref(cols), quotas.q))
         self.nq = quotas.q
 
+    def load_reservations(self, rs: ReservationTable):
+        cols = rs.ks()
+        self._chk(self.L.ks_load_reservations(self.h, C.byref(cols), rs.r))
+        self.nr = rs.r
+
+    def read_reservations(self):
+        """(allocated [r][KS_RSV_DIMS], assigned [r]) after commits"""
+        allocated = np.zeros(max(self.nr, 1) * abi.KS_RSV_DIMS, np.int64)
+        assigned = np.zeros(max(self.nr, 1), np.int32)
+        self._chk(self.L.ks_read_reservations(self.h, allocated.ctypes.data_as(abi.P64),
+                                              assigned.ctypes.data_as(abi.P32)))
+        return allocated[: self.nr * abi.KS_RSV_DIMS].reshape(self.nr, abi.KS_RSV_DIMS), assigned[: self.nr]
+
     def shard(self, nranks: int = 1, rank: int = 0, unique_id: Optional[bytes] = None, virtual_shards: int = 1):
         """Node sharding: this rank sweeps its chunk range; candidates are exchanged by RCCL allgather."""
         uid = None
@@ -164,7 +183,8 @@ class Evaluator:
         cols = pods.ks()
         self._chk(self.L.ks_schedule(self.h, C.byref(cols), pods.n, out.ctypes.data_as(C.POINTER(abi.KsResult))))
         out = out[: pods.n]
-        return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy()}
+        return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy(),
+                "reservation": out["reservation"].copy()}
 
     def stage(self, pods: PodTable):
         cols = pods.ks()
@@ -178,7 +198,8 @@ class Evaluator:
         out = np.zeros(max(self.np_staged, 1), RESULT_DTYPE)
         self._chk(self.L.ks_fetch_results(self.h, out.ctypes.data_as(C.POINTER(abi.KsResult)), self.np_staged))
         out = out[: self.np_staged]
-        return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy()}
+        return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy(),
+                "reservation": out["reservation"].copy()}
 
     def checkpoint(self):
         self._chk(self.L.ks_checkpoint(self.h))

@@ -7,6 +7,8 @@ would produce from a scheduler-cache snapshot plus NodeMetric objects:
 * C1  500 nodes, 1k pods, NodeResourcesFit + LoadAwareScheduling
 * C2  5k nodes, 10k pods, + ElasticQuota admission (32 leaf quotas under root,
       limits sized so roughly a tenth of the pods are rejected)
+* C4  20k nodes with 50k reservations (make_reservations), 10k pods of which 60 % belong to one
+      of 16 reservation owner classes, NodeResourcesFit + LoadAwareScheduling + Reservation (weight 5000)
 * C5  100k nodes, C1 pod distribution (the multi-GPU sharding config)
 
 Node model: allocatable cpu ∈ {32,48,64,96} cores, memory ∈ {128,256,384,512}
@@ -30,7 +32,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import NodeTable, PodTable, QuotaTable
+from .cluster import NodeTable, PodTable, QuotaTable, ReservationTable
 from .config import BATCH_CPU, BATCH_MEMORY, CPU, MEMORY, ElasticQuotaArgs, NodeResourcesFitArgs, SchedulerProfile
 
 SEED = 20261015
@@ -54,17 +56,21 @@ class Workload:
     nodes: NodeTable
     pods: PodTable
     quotas: Optional[QuotaTable]
+    reservations: Optional[ReservationTable] = None
 
     @property
     def cfg(self) -> abi.KsConfig:
         return self.profile.to_ks_config()
 
 
-def koord_profile(with_quota: bool = False, batch_pods: int = 0, candidates: int = 0) -> SchedulerProfile:
+def koord_profile(with_quota: bool = False, batch_pods: int = 0, candidates: int = 0,
+                  with_reservation: bool = False) -> SchedulerProfile:
     """NodeResourcesFit (LeastAllocated cpu/memory/batch-cpu/batch-memory, weight 1 each:
-    config/manager/scheduler-config.yaml:17-31) + LoadAwareScheduling defaults."""
+    config/manager/scheduler-config.yaml:17-31) + LoadAwareScheduling defaults (+ Reservation, weight
+    5000 in the same profile)."""
     fit = NodeResourcesFitArgs(resources={CPU: 1, MEMORY: 1, BATCH_CPU: 1, BATCH_MEMORY: 1})
     return SchedulerProfile(fit=fit, quota=ElasticQuotaArgs() if with_quota else None,
+                            reservation_weight=5000 if with_reservation else None,
                             batch_pods=batch_pods, candidates=candidates)
 
 
@@ -160,6 +166,56 @@ def make_quotas(pods: PodTable, n_quotas: int, rng: np.random.Generator, admit_f
     return q
 
 
+def make_reservations(nodes: NodeTable, r: int, rng: np.random.Generator, n_classes: int = 16,
+                      order_frac: float = 0.03, assigned_frac: float = 0.25) -> ReservationTable:
+    """Available reservations spread uniformly over the nodes (~r/n per node).  Each reserves
+    cpu ∈ {2,4,8} cores with 2 or 4 GiB memory per core (keys cpu + memory), belongs to one owner
+    class (10 % to two), 5 % are unschedulable, 20 % AllocateOnce, policies Default 60 % / Aligned
+    25 % / Restricted 15 %, a few carry a reservation-order label, and a quarter already hold 1-3
+    assigned pods using part of them.  The reserve pods and the assigned pods are added to the
+    nodes' NodeInfo (requested, non-zero requested, pod count) as the scheduler cache holds them."""
+    t = ReservationTable(r)
+    t.node[:] = rng.integers(0, nodes.n, r)
+    cls = rng.integers(0, n_classes, r).astype(np.uint64)
+    two = rng.random(r) < 0.1
+    cls2 = rng.integers(0, n_classes, r).astype(np.uint64)
+    t.owner_classes[:] = (np.uint64(1) << cls) | np.where(two, np.uint64(1) << cls2, np.uint64(0))
+    u = rng.random(r)
+    t.flags[:] = np.where(u < 0.05, abi.KS_RSV_UNSCHEDULABLE, np.where(u < 0.25, abi.KS_RSV_ALLOCATE_ONCE, 0))
+    t.policy[:] = rng.choice(np.array([abi.KS_RSV_POLICY_DEFAULT, abi.KS_RSV_POLICY_ALIGNED,
+                                       abi.KS_RSV_POLICY_RESTRICTED], np.uint32), r, p=[0.6, 0.25, 0.15])
+    t.order[:] = np.where(rng.random(r) < order_frac, rng.integers(1, 1000, r), 0)
+    t.key_mask[:] = 0b11
+    cores = rng.choice(np.array([2, 4, 8], np.int64), r)
+    t.allocatable[0] = cores * 1000
+    t.allocatable[1] = cores * rng.choice(np.array([2, 4], np.int64), r) * GI
+    has = rng.random(r) < assigned_frac
+    t.assigned[:] = np.where(has, rng.integers(1, 4, r), 0)
+    frac = rng.choice(np.array([1, 2, 3, 4], np.int64), r)
+    t.allocated[0] = np.where(has, t.allocatable[0] * frac // 4, 0)
+    t.allocated[1] = np.where(has, t.allocatable[1] * frac // 4 // MI * MI, 0)
+    add_cpu = t.allocatable[0] + t.allocated[0]
+    add_mem = t.allocatable[1] + t.allocated[1]
+    nodes.req_milli_cpu[:] += np.bincount(t.node, weights=add_cpu, minlength=nodes.n).astype(np.int64)
+    nodes.req_memory[:] += np.bincount(t.node, weights=add_mem.astype(np.float64), minlength=nodes.n).astype(np.int64)
+    nodes.nonzero_milli_cpu[:] += np.bincount(t.node, weights=add_cpu, minlength=nodes.n).astype(np.int64)
+    nodes.nonzero_memory[:] += np.bincount(t.node, weights=add_mem.astype(np.float64), minlength=nodes.n).astype(np.int64)
+    nodes.pod_count[:] += np.bincount(t.node, weights=1 + t.assigned, minlength=nodes.n).astype(np.int32)
+    return t
+
+
+def reservation_pods(pods: PodTable, rng: np.random.Generator, n_classes: int = 16, class_frac: float = 0.6,
+                     affinity_frac: float = 0.05) -> PodTable:
+    """Give pods an owner class (matching reservations of that class) and, for a few, a required
+    reservation affinity."""
+    p = pods.n
+    classed = rng.random(p) < class_frac
+    pods.rsv_class[:] = np.where(classed, rng.integers(0, n_classes, p), -1)
+    aff = classed & (rng.random(p) < affinity_frac)
+    pods.flags[aff] |= abi.KS_POD_RSV_AFFINITY
+    return pods
+
+
 def c1(seed: int = SEED, n_nodes: int = 500, n_pods: int = 1000, **kw) -> Workload:
     rng = np.random.Generator(np.random.PCG64(seed))
     nodes = make_nodes(n_nodes, rng)
@@ -173,6 +229,17 @@ def c2(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, n_quotas: int
     pods = make_pods(n_pods, rng, n_quotas)
     quotas = make_quotas(pods, n_quotas, rng)
     return Workload("C2", koord_profile(with_quota=True, **kw), nodes, pods, quotas)
+
+
+def c4(seed: int = SEED, n_nodes: int = 20_000, n_reservations: int = 50_000, n_pods: int = 10_000, **kw) -> Workload:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = make_nodes(n_nodes, rng)
+    # other running pods use up to a quarter of the node; the reservations come on top
+    for col in ("req_milli_cpu", "req_memory", "nonzero_milli_cpu", "nonzero_memory"):
+        setattr(nodes, col, getattr(nodes, col) // 2)
+    rs = make_reservations(nodes, n_reservations, rng)
+    pods = reservation_pods(make_pods(n_pods, rng), rng)
+    return Workload("C4", koord_profile(with_reservation=True, **kw), nodes, pods, None, rs)
 
 
 def c5(seed: int = SEED, n_nodes: int = 100_000, n_pods: int = 1_000_000, **kw) -> Workload:

@@ -19,6 +19,13 @@
  *   Reserve                  load_aware.go:260 -> pod_assign_cache.go:53; upstream NodeInfo.AddPod;
  *                            elasticquota/plugin.go:323 -> core/group_quota_manager.go:798,620-655
  *   ElasticQuota PreFilter   elasticquota/plugin.go:210-255, plugin_helper.go:281-319
+ *   Reservation              BeforePreFilter restore reservation/transformer.go:41-307 (matchReservation
+ *                            :349-373), PreFilter plugin.go:215-248, Filter :311-375, filterWithReservations
+ *                            :377-440, fitsNode :445-496, FilterReservation :503-530, PreScore
+ *                            scoring.go:42-101, NominateReservation nominator.go:134-192, Score
+ *                            scoring.go:103-131, scoreReservation :183-203, findMostPreferredReservationByOrder
+ *                            :162-181, DefaultNormalizeScore frameworkext/normalize_score.go:24-52, Reserve
+ *                            plugin.go:532-570 -> reservation_info.go:379-388
  *   Sweep driver             upstream schedule_one.go (schedulePod, findNodesThatPassFilters,
  *                            prioritizeNodes, selectHost) with percentageOfNodesToScore=100 and
  *                            lowest-index tie-break; Parallelizer pkg/util/parallelize/parallelism.go:29-49
@@ -39,6 +46,10 @@
 #include "../include/koordgpu.h"
 
 #define MAX_NODE_SCORE 100 /* framework.MaxNodeScore */
+#define KO_D KS_RSV_DIMS
+#define DEFAULT_MILLI_CPU 100                 /* schedutil.DefaultMilliCPURequest */
+#define DEFAULT_MEMORY (200LL * 1024 * 1024)  /* schedutil.DefaultMemoryRequest */
+#define MOST_PREFERRED_SCORE 1000             /* reservation/scoring.go:39 */
 
 /* ------------------------------------------------------------------ */
 /* scorers                                                             */
@@ -101,6 +112,18 @@ typedef struct {
 
 typedef struct ko_pool ko_pool;
 
+/* reservation cache: rows in caller order, CSR by node (rows of a node in table order) */
+typedef struct {
+  int32_t nr;
+  int32_t *beg, *row;
+  int32_t *node, *assigned;
+  uint64_t *cls;
+  uint32_t *flags, *policy, *keys;
+  int64_t *order;
+  int64_t *alloc, *allocd; /* nr * KO_D */
+  int64_t *rnz;            /* nr * 2: reserve pod NonZeroRequested cpu, memory */
+} ko_rsv;
+
 typedef struct ko_sched {
   ks_config cfg;
   int64_t n;
@@ -113,6 +136,10 @@ typedef struct ko_sched {
   int64_t *total;
   ko_pool *pool;
   int nthreads;
+  ko_rsv rv;
+  int32_t *nom;     /* per node: nominated reservation row (-1) */
+  int64_t *rraw;    /* per node: Reservation raw score */
+  int64_t *rord;    /* per node: findMostPreferredReservationByOrder over matched (0 = none) */
 } ko_sched;
 
 /* pod view for one pod (values pulled out of ks_pod_cols) */
@@ -124,7 +151,16 @@ typedef struct {
   int32_t quota;
   uint32_t qmask;
   int64_t qreq[KS_QUOTA_DIMS];
+  int32_t rcls;  /* reservation match class, -1 = none */
+  uint32_t keys; /* bit d: request dimension d is a key of the pod's requests (value != 0) */
 } ko_pod;
+
+/* NodeInfo values the Fit plugin reads, after the Reservation restore */
+typedef struct {
+  int64_t req[KO_D];
+  int64_t nz[2];
+  int64_t pods;
+} ko_eff;
 
 static int64_t colv64(const int64_t *c, int64_t i) { return c ? c[i] : 0; }
 static uint32_t colvu32(const uint32_t *c, int64_t i) { return c ? c[i] : 0; }
@@ -145,6 +181,27 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
   p->quota = pc->quota ? pc->quota[i] : -1;
   p->qmask = colvu32(pc->quota_mask, i);
   for (int d = 0; d < KS_QUOTA_DIMS; d++) p->qreq[d] = colv64(pc->quota_req[d], i);
+  p->rcls = pc->rsv_class ? pc->rsv_class[i] : -1;
+  int64_t v[KO_D] = {p->cpu, p->mem, p->eph};
+  for (int k = 0; k < KS_MAX_SCALARS; k++) v[3 + k] = p->sc[k];
+  for (int d = 0; d < KO_D; d++)
+    if (v[d] != 0) p->keys |= 1u << d;
+}
+
+static int64_t pod_dim(const ko_pod *p, int d) { return d == 0 ? p->cpu : d == 1 ? p->mem : d == 2 ? p->eph : p->sc[d - 3]; }
+
+static int64_t node_alloc_dim(const ko_nodes *nd, int64_t n, int d) {
+  return d == 0 ? nd->alloc_cpu[n] : d == 1 ? nd->alloc_mem[n] : d == 2 ? nd->alloc_eph[n] : nd->alloc_sc[d - 3][n];
+}
+
+static void node_eff(const ko_nodes *nd, int64_t n, ko_eff *e) {
+  e->req[0] = nd->req_cpu[n];
+  e->req[1] = nd->req_mem[n];
+  e->req[2] = nd->req_eph[n];
+  for (int k = 0; k < KS_MAX_SCALARS; k++) e->req[3 + k] = nd->req_sc[k][n];
+  e->nz[0] = nd->nz_cpu[n];
+  e->nz[1] = nd->nz_mem[n];
+  e->pods = nd->pod_count[n];
 }
 
 /* ------------------------------------------------------------------ */
@@ -152,17 +209,17 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
 /* ------------------------------------------------------------------ */
 
 /* upstream fitsRequest (noderesources/fit.go); returns KS_R_FIT_* bits */
-static uint32_t fit_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
+static uint32_t fit_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   const ko_nodes *d = &s->nd;
   uint32_t r = 0;
-  if ((int64_t)d->pod_count[n] + 1 > (int64_t)d->allowed_pods[n]) r |= KS_R_FIT_PODS;
+  if (e->pods + 1 > (int64_t)d->allowed_pods[n]) r |= KS_R_FIT_PODS;
   if (p->cpu == 0 && p->mem == 0 && p->eph == 0 && !(p->flags & KS_POD_SCALAR_KEYS)) return r;
-  if (p->cpu > d->alloc_cpu[n] - d->req_cpu[n]) r |= KS_R_FIT_CPU;
-  if (p->mem > d->alloc_mem[n] - d->req_mem[n]) r |= KS_R_FIT_MEMORY;
-  if (p->eph > d->alloc_eph[n] - d->req_eph[n]) r |= KS_R_FIT_EPHEMERAL;
+  if (p->cpu > d->alloc_cpu[n] - e->req[0]) r |= KS_R_FIT_CPU;
+  if (p->mem > d->alloc_mem[n] - e->req[1]) r |= KS_R_FIT_MEMORY;
+  if (p->eph > d->alloc_eph[n] - e->req[2]) r |= KS_R_FIT_EPHEMERAL;
   for (int k = 0; k < KS_MAX_SCALARS; k++) {
     if (p->sc[k] == 0) continue; /* resource not in podRequest.ScalarResources */
-    if (p->sc[k] > d->alloc_sc[k][n] - d->req_sc[k][n]) r |= KS_R_FIT_SCALAR;
+    if (p->sc[k] > d->alloc_sc[k][n] - e->req[3 + k]) r |= KS_R_FIT_SCALAR;
   }
   return r;
 }
@@ -199,9 +256,9 @@ static uint32_t la_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
   return 0;
 }
 
-static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n) {
+static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   uint32_t r = 0;
-  if (s->cfg.fit.enable_filter) r |= fit_filter(s, p, n);
+  if (s->cfg.fit.enable_filter) r |= fit_filter(s, p, n, e);
   if (s->cfg.loadaware.enable_filter) r |= la_filter(s, p, n);
   return r;
 }
@@ -211,7 +268,7 @@ static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n) {
 /* ------------------------------------------------------------------ */
 
 /* upstream resourceAllocationScorer.score with LeastAllocated/MostAllocated */
-static int64_t fit_score(const ko_sched *s, const ko_pod *p, int64_t n) {
+static int64_t fit_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   const ko_nodes *d = &s->nd;
   const ks_fit_args *a = &s->cfg.fit;
   int64_t node_score = 0, weight_sum = 0;
@@ -225,12 +282,12 @@ static int64_t fit_score(const ko_sched *s, const ko_pod *p, int64_t n) {
       weight_sum += (W);                                                                     \
     }                                                                                        \
   } while (0)
-  FIT_TERM(a->weight_cpu, d->alloc_cpu[n], d->nz_cpu[n] + p->nzcpu);
-  FIT_TERM(a->weight_memory, d->alloc_mem[n], d->nz_mem[n] + p->nzmem);
-  FIT_TERM(a->weight_ephemeral, d->alloc_eph[n], d->req_eph[n] + p->eph);
+  FIT_TERM(a->weight_cpu, d->alloc_cpu[n], e->nz[0] + p->nzcpu);
+  FIT_TERM(a->weight_memory, d->alloc_mem[n], e->nz[1] + p->nzmem);
+  FIT_TERM(a->weight_ephemeral, d->alloc_eph[n], e->req[2] + p->eph);
   for (int k = 0; k < KS_MAX_SCALARS; k++) {
     if (p->sc[k] == 0) continue; /* scalar not requested by the pod -> (0, 0), bypassed */
-    FIT_TERM(a->weight_scalar[k], d->alloc_sc[k][n], d->req_sc[k][n] + p->sc[k]);
+    FIT_TERM(a->weight_scalar[k], d->alloc_sc[k][n], e->req[3 + k] + p->sc[k]);
   }
 #undef FIT_TERM
   if (weight_sum == 0) return 0;
@@ -260,10 +317,11 @@ static int64_t la_score(const ko_sched *s, const ko_pod *p, int64_t n) {
   return node_score / weight_sum;
 }
 
-static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_out, int64_t *la_out) {
+static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *fit_out,
+                           int64_t *la_out) {
   int64_t t = 0, fs = 0, ls = 0;
   if (s->cfg.fit.enable_score) {
-    fs = fit_score(s, p, n);
+    fs = fit_score(s, p, n, e);
     t += fs * s->cfg.fit.plugin_weight;
   }
   if (s->cfg.loadaware.enable_score) {
@@ -321,6 +379,190 @@ static void quota_reserve(ko_sched *s, const ko_pod *p) {
       if (p->flags & KS_POD_NONPREEMPTIBLE) q->npused[d] += p->qreq[d];
     }
   }
+}
+
+/* ------------------------------------------------------------------ */
+/* Reservation                                                         */
+/* ------------------------------------------------------------------ */
+
+/* transformer.go:103-111: available (the table holds only available ones), not
+ * AllocateOnce-and-already-used */
+static int rsv_eligible(const ko_rsv *rv, int32_t r) {
+  return !((rv->flags[r] & KS_RSV_ALLOCATE_ONCE) && rv->assigned[r] > 0);
+}
+
+/* transformer.go:113: !isReservedPod && !IsUnschedulable && matchReservation */
+static int rsv_matched(const ko_rsv *rv, const ko_pod *p, int32_t r) {
+  return rsv_eligible(rv, r) && !(rv->flags[r] & KS_RSV_UNSCHEDULABLE) && p->rcls >= 0 &&
+         p->rcls < KS_RSV_CLASSES && ((rv->cls[r] >> p->rcls) & 1u);
+}
+
+/* schedutil.GetNonzeroRequests of one container's requests */
+static void nonzero_of(const int64_t *v, uint32_t keys, int64_t out[2]) {
+  out[0] = (keys & 1u) ? v[0] : DEFAULT_MILLI_CPU;
+  out[1] = (keys & 2u) ? v[1] : DEFAULT_MEMORY;
+}
+
+typedef struct {
+  int has;          /* node is in stateData.nodeReservationStates */
+  int nmatched;     /* len(nodeRState.matched) */
+  ko_eff e;         /* NodeInfo after the restore */
+  int64_t preq[KO_D];   /* nodeRState.podRequested */
+  int64_t ralloc[KO_D]; /* nodeRState.rAllocated */
+} ko_rstate;
+
+/* prepareMatchReservationState.processNode (transformer.go:81-190) for one node */
+static void rsv_restore(const ko_sched *s, const ko_pod *p, int64_t n, ko_rstate *st) {
+  const ko_rsv *rv = &s->rv;
+  memset(st, 0, sizeof(*st));
+  node_eff(&s->nd, n, &st->e);
+  if (!s->cfg.reservation.enable || rv->nr == 0) return;
+  int nm = 0, nu = 0;
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    int32_t r = rv->row[i];
+    if (!rsv_eligible(rv, r)) continue;
+    if (rsv_matched(rv, p, r)) nm++;
+    else if (rv->assigned[r] > 0) nu++;
+  }
+  if (nm == 0 && nu == 0) return;
+  if ((p->flags & KS_POD_RSV_AFFINITY) && nm == 0) return; /* :135-137 */
+  st->has = 1;
+  st->nmatched = nm;
+  ko_eff *e = &st->e;
+  /* restoreUnmatchedReservations (:266-292) -> updateNodeInfoRequested (:294-307) */
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    int32_t r = rv->row[i];
+    if (!rsv_eligible(rv, r) || rsv_matched(rv, p, r) || rv->assigned[r] <= 0) continue;
+    const int64_t *al = rv->alloc + (size_t)r * KO_D, *ad = rv->allocd + (size_t)r * KO_D;
+    for (int d = 0; d < KO_D; d++) e->req[d] -= al[d];
+    e->nz[0] -= rv->rnz[2 * r];
+    e->nz[1] -= rv->rnz[2 * r + 1];
+    int64_t rem[KO_D];
+    int nonzero = 0;
+    for (int d = 0; d < KO_D; d++) {
+      int64_t v = al[d] - ad[d];
+      rem[d] = v > 0 ? v : 0; /* quotav1.SubtractWithNonNegativeResult */
+      nonzero |= rem[d] != 0;
+    }
+    if (nonzero) {
+      int64_t nz[2];
+      for (int d = 0; d < KO_D; d++) e->req[d] += rem[d];
+      nonzero_of(rem, rv->keys[r], nz);
+      e->nz[0] += nz[0];
+      e->nz[1] += nz[1];
+    }
+  }
+  memcpy(st->preq, e->req, sizeof(st->preq)); /* :151-152 */
+  /* restoreMatchedReservation (:241-264): NodeInfo.RemovePod(reservePod); rAllocated (:168) */
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    int32_t r = rv->row[i];
+    if (!rsv_matched(rv, p, r)) continue;
+    const int64_t *al = rv->alloc + (size_t)r * KO_D, *ad = rv->allocd + (size_t)r * KO_D;
+    for (int d = 0; d < KO_D; d++) {
+      e->req[d] -= al[d];
+      st->ralloc[d] += ad[d];
+    }
+    e->nz[0] -= rv->rnz[2 * r];
+    e->nz[1] -= rv->rnz[2 * r + 1];
+    e->pods -= 1;
+  }
+}
+
+/* fitsNode (plugin.go:445-496) without preemption; r = -1 for the nil reservation */
+static int rsv_fits_node(const ko_sched *s, const ko_pod *p, int64_t n, const ko_rstate *st, int32_t r) {
+  const ko_rsv *rv = &s->rv;
+  if (st->e.pods - st->nmatched + 1 > (int64_t)s->nd.allowed_pods[n]) return 0;
+  if (p->cpu == 0 && p->mem == 0 && p->eph == 0 && !(p->flags & KS_POD_SCALAR_KEYS)) return 1;
+  for (int d = 0; d < KO_D; d++) {
+    int64_t pd = pod_dim(p, d);
+    if (d >= 3 && pd == 0) continue; /* podRequest.ScalarResources keys */
+    int64_t rrem = r >= 0 ? rv->alloc[(size_t)r * KO_D + d] - rv->allocd[(size_t)r * KO_D + d] : 0;
+    if (pd > node_alloc_dim(&s->nd, n, d) - (st->preq[d] - rrem - st->ralloc[d])) return 0;
+  }
+  return 1;
+}
+
+/* filterWithReservations (plugin.go:377-440) body for one reservation: satisfied? */
+static int rsv_satisfies(const ko_sched *s, const ko_pod *p, int64_t n, const ko_rstate *st, int32_t r) {
+  const ko_rsv *rv = &s->rv;
+  uint32_t names = rv->keys[r] & p->keys; /* Intersection(ResourceNames, podRequests names) */
+  if (!names) return 0;
+  int node_fits = rsv_fits_node(s, p, n, st, r);
+  uint32_t pol = rv->policy[r];
+  if (pol == KS_RSV_POLICY_DEFAULT || pol == KS_RSV_POLICY_ALIGNED) return node_fits;
+  if (pol == KS_RSV_POLICY_RESTRICTED) {
+    /* requests = Mask(podRequests, ResourceNames) <= rRemained = alloc - Mask(allocated, names) (>= 0) */
+    for (int d = 0; d < KO_D; d++) {
+      if (!((names >> d) & 1u)) continue;
+      int64_t rem = rv->alloc[(size_t)r * KO_D + d] - rv->allocd[(size_t)r * KO_D + d];
+      if (rem < 0) rem = 0;
+      if (pod_dim(p, d) > rem) return 0;
+    }
+    return node_fits;
+  }
+  return 0;
+}
+
+/* Reservation Filter for a non-reserve pod (plugin.go:335-372) -> KS_R_RSV_* */
+static uint32_t rsv_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_rstate *st) {
+  if (!s->cfg.reservation.enable || !(p->flags & KS_POD_RSV_AFFINITY)) return 0;
+  if (!st->has || st->nmatched == 0) return KS_R_RSV_AFFINITY; /* PreFilter NodeNames / :342-344 */
+  const ko_rsv *rv = &s->rv;
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    int32_t r = rv->row[i];
+    if (rsv_matched(rv, p, r) && rsv_satisfies(s, p, n, st, r)) return 0;
+  }
+  return KS_R_RSV_NO_FIT;
+}
+
+/* scoreReservation (scoring.go:183-203); MilliValue on both sides gives the same floor */
+static int64_t rsv_score(const ko_rsv *rv, const ko_pod *p, int32_t r) {
+  int64_t w = 0, sum = 0;
+  for (int d = 0; d < KO_D; d++) {
+    int64_t cap = rv->alloc[(size_t)r * KO_D + d];
+    if (cap == 0) continue; /* quotav1.RemoveZeros */
+    w++;
+    int64_t req = pod_dim(p, d) + rv->allocd[(size_t)r * KO_D + d];
+    if (req <= cap) sum += MAX_NODE_SCORE * req / cap;
+  }
+  return w ? sum / w : 0;
+}
+
+/* NominateReservation (nominator.go:134-192): FilterReservation survivors, lowest order label
+ * first (findMostPreferredReservationByOrder), else the highest scoreReservation (ties: table
+ * order).  Also returns the node's preferred order over every matched reservation (PreScore :65). */
+static int32_t rsv_nominate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_rstate *st, int64_t *node_order) {
+  const ko_rsv *rv = &s->rv;
+  int64_t mo = INT64_MAX, bo = INT64_MAX, bs = -1;
+  int32_t by_order = -1, by_score = -1;
+  if (node_order) *node_order = 0;
+  if (!st->has || st->nmatched == 0) return -1;
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    int32_t r = rv->row[i];
+    if (!rsv_matched(rv, p, r)) continue;
+    int64_t o = rv->order[r];
+    if (o != 0 && mo > o) mo = o;
+    if (!rsv_satisfies(s, p, n, st, r)) continue; /* FilterReservation (plugin.go:503-530) */
+    if (o != 0 && bo > o) {
+      bo = o;
+      by_order = r;
+    }
+    int64_t sc = rsv_score(rv, p, r);
+    if (sc > bs) {
+      bs = sc;
+      by_score = r;
+    }
+  }
+  if (node_order && mo != INT64_MAX) *node_order = mo;
+  return by_order >= 0 ? by_order : by_score;
+}
+
+/* Reserve (plugin.go:532-570) -> ReservationInfo.AddAssignedPod: Allocated += Mask(req, names) */
+static void rsv_reserve(ko_sched *s, const ko_pod *p, int32_t r) {
+  ko_rsv *rv = &s->rv;
+  for (int d = 0; d < KO_D; d++)
+    if ((rv->keys[r] >> d) & 1u) rv->allocd[(size_t)r * KO_D + d] += pod_dim(p, d);
+  rv->assigned[r] += 1;
 }
 
 /* NodeInfo.AddPod (upstream) + podAssignCache.assign (pod_assign_cache.go:53) */
@@ -501,6 +743,10 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
 #undef CP32
   s->feasible = (uint8_t *)calloc(nn, 1);
   s->total = (int64_t *)calloc(nn, 8);
+  s->nom = (int32_t *)calloc(nn, 4);
+  s->rraw = (int64_t *)calloc(nn, 8);
+  s->rord = (int64_t *)calloc(nn, 8);
+  s->rv.beg = (int32_t *)calloc(nn + 1, 4);
   s->nthreads = nthreads < 1 ? 1 : nthreads;
   s->pool = pool_create(s->nthreads);
   return s;
@@ -513,7 +759,68 @@ void ko_destroy(ko_sched *s) {
   free(s->q);
   free(s->feasible);
   free(s->total);
+  free(s->nom);
+  free(s->rraw);
+  free(s->rord);
+  ko_rsv *rv = &s->rv;
+  free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
+  free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
   free(s);
+}
+
+/* reservation cache snapshot; rows must reference valid nodes (returns -1 otherwise) */
+int ko_load_reservations(ko_sched *s, const ks_reservation_cols *rc, int32_t nr) {
+  ko_rsv *rv = &s->rv;
+  free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
+  free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
+  size_t m = (size_t)(nr > 0 ? nr : 1);
+  rv->nr = nr;
+  rv->row = (int32_t *)calloc(m, 4);
+  rv->node = (int32_t *)calloc(m, 4);
+  rv->assigned = (int32_t *)calloc(m, 4);
+  rv->cls = (uint64_t *)calloc(m, 8);
+  rv->flags = (uint32_t *)calloc(m, 4);
+  rv->policy = (uint32_t *)calloc(m, 4);
+  rv->keys = (uint32_t *)calloc(m, 4);
+  rv->order = (int64_t *)calloc(m, 8);
+  rv->alloc = (int64_t *)calloc(m * KO_D, 8);
+  rv->allocd = (int64_t *)calloc(m * KO_D, 8);
+  rv->rnz = (int64_t *)calloc(m * 2, 8);
+  memset(rv->beg, 0, (size_t)(s->n + 1) * 4);
+  for (int32_t r = 0; r < nr; r++) {
+    int32_t n = rc->node[r];
+    if (n < 0 || n >= s->n) return -1;
+    rv->node[r] = n;
+    rv->beg[n + 1]++;
+    rv->cls[r] = rc->owner_classes ? rc->owner_classes[r] : 0;
+    rv->flags[r] = colvu32(rc->flags, r);
+    rv->policy[r] = colvu32(rc->policy, r);
+    rv->keys[r] = colvu32(rc->key_mask, r);
+    rv->order[r] = colv64(rc->order, r);
+    rv->assigned[r] = rc->assigned ? rc->assigned[r] : 0;
+    for (int d = 0; d < KO_D; d++) {
+      rv->alloc[(size_t)r * KO_D + d] = colv64(rc->allocatable[d], r);
+      rv->allocd[(size_t)r * KO_D + d] = colv64(rc->allocated[d], r);
+    }
+    int64_t nz[2];
+    nonzero_of(rv->alloc + (size_t)r * KO_D, rv->keys[r], nz);
+    rv->rnz[2 * r] = rc->reserve_nonzero_milli_cpu ? rc->reserve_nonzero_milli_cpu[r] : nz[0];
+    rv->rnz[2 * r + 1] = rc->reserve_nonzero_memory ? rc->reserve_nonzero_memory[r] : nz[1];
+  }
+  for (int64_t n = 0; n < s->n; n++) rv->beg[n + 1] += rv->beg[n];
+  int32_t *fill = (int32_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 4);
+  for (int32_t r = 0; r < nr; r++) {
+    int32_t n = rv->node[r];
+    rv->row[rv->beg[n] + fill[n]++] = r;
+  }
+  free(fill);
+  return 0;
+}
+
+int ko_read_reservations(const ko_sched *s, int64_t *allocated, int32_t *assigned) {
+  if (allocated) memcpy(allocated, s->rv.allocd, (size_t)s->rv.nr * KO_D * 8);
+  if (assigned) memcpy(assigned, s->rv.assigned, (size_t)s->rv.nr * 4);
+  return 0;
 }
 
 int ko_load_quotas(ko_sched *s, const ks_quota_cols *qc, int32_t nq) {
@@ -540,15 +847,62 @@ typedef struct {
   const ko_pod *p;
 } sweep_arg;
 
-static void filter_piece(void *v, int64_t lo, int64_t hi) {
-  sweep_arg *a = (sweep_arg *)v;
-  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = filter_node(a->s, a->p, n) == 0;
+/* BeforePreFilter restore + Filter for one node; the Reservation PreScore per-node part
+ * (nomination, node order) for feasible ones.  Returns the KS_R_* bits. */
+static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_out, int64_t *la_out) {
+  ko_rstate st;
+  rsv_restore(s, p, n, &st);
+  uint32_t r = rsv_filter(s, p, n, &st);
+  /* a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
+   * NodeNames, plugin.go:235-246) before any Filter plugin runs */
+  if (r != KS_R_RSV_AFFINITY) r |= filter_node(s, p, n, &st.e);
+  s->nom[n] = -1;
+  s->rraw[n] = 0;
+  s->rord[n] = 0;
+  if (r) {
+    s->total[n] = -1;
+    return r;
+  }
+  s->total[n] = total_score(s, p, n, &st.e, fit_out, la_out);
+  if (s->cfg.reservation.enable) {
+    int32_t nom = rsv_nominate(s, p, n, &st, &s->rord[n]);
+    s->nom[n] = nom;
+    s->rraw[n] = nom >= 0 ? rsv_score(&s->rv, p, nom) : 0;
+  }
+  return 0;
 }
 
-static void score_piece(void *v, int64_t lo, int64_t hi) {
+static void filter_piece(void *v, int64_t lo, int64_t hi) {
   sweep_arg *a = (sweep_arg *)v;
-  for (int64_t n = lo; n < hi; n++)
-    a->s->total[n] = a->s->feasible[n] ? total_score(a->s, a->p, n, NULL, NULL) : -1;
+  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = eval_node(a->s, a->p, n, NULL, NULL) == 0;
+}
+
+/* Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and
+ * DefaultNormalizeScore (normalize_score.go:24-52) over the feasible nodes, weighted into total[].
+ * norm (optional) receives the normalized per-node score. */
+static void rsv_normalize(ko_sched *s, int64_t *norm) {
+  if (!s->cfg.reservation.enable) return;
+  int64_t sel = INT64_MAX, pref = -1, mx = 0;
+  for (int64_t n = 0; n < s->n; n++)
+    if (s->total[n] >= 0 && s->rord[n] != 0 && sel > s->rord[n]) {
+      sel = s->rord[n];
+      pref = n;
+    }
+  for (int64_t n = 0; n < s->n; n++) {
+    if (s->total[n] < 0) continue;
+    int64_t raw = n == pref ? MOST_PREFERRED_SCORE : s->rraw[n];
+    s->rraw[n] = raw;
+    if (raw > mx) mx = raw;
+  }
+  for (int64_t n = 0; n < s->n; n++) {
+    if (s->total[n] < 0) {
+      if (norm) norm[n] = 0;
+      continue;
+    }
+    int64_t sc = mx == 0 ? s->rraw[n] : MAX_NODE_SCORE * s->rraw[n] / mx;
+    if (norm) norm[n] = sc;
+    s->total[n] += sc * s->cfg.reservation.plugin_weight;
+  }
 }
 
 /* one scheduling cycle per pod, in order (scheduleOne loop) */
@@ -558,11 +912,13 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     load_pod(s, pc, i, &p);
     out[i].node = -1;
     out[i].score = 0;
+    out[i].reservation = -1;
+    out[i]._pad0 = 0;
     out[i].status = quota_prefilter(s, &p);
     if (out[i].status) continue;
     sweep_arg a = {s, &p};
     pool_until(s->pool, s->n, filter_piece, &a);
-    pool_until(s->pool, s->n, score_piece, &a);
+    rsv_normalize(s, NULL);
     /* prioritizeNodes sum + selectHost: max score, lowest index on ties */
     int64_t best = -1, best_n = -1;
     for (int64_t n = 0; n < s->n; n++) {
@@ -577,6 +933,10 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     }
     out[i].node = (int32_t)best_n;
     out[i].score = best;
+    if (s->nom[best_n] >= 0) {
+      out[i].reservation = s->nom[best_n];
+      rsv_reserve(s, &p, s->nom[best_n]);
+    }
     node_reserve(s, &p, best_n);
     quota_reserve(s, &p);
   }
@@ -587,16 +947,22 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
   ko_pod p;
   load_pod(s, pc, 0, &p);
   for (int64_t n = 0; n < s->n; n++) {
-    uint32_t r = filter_node(s, &p, n);
-    int64_t fs = 0, ls = 0, t = -1;
-    if (!r) t = total_score(s, &p, n, &fs, &ls);
+    int64_t fs = 0, ls = 0;
+    uint32_t r = eval_node(s, &p, n, &fs, &ls);
     if (reasons) reasons[n] = r;
     if (scores) {
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = r ? 0 : fs;
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = r ? 0 : ls;
+      scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
     }
-    if (total) total[n] = t;
   }
+  int64_t *norm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
+  rsv_normalize(s, norm);
+  for (int64_t n = 0; n < s->n; n++) {
+    if (scores && s->cfg.reservation.enable) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = norm[n];
+    if (total) total[n] = s->total[n];
+  }
+  free(norm);
   return 0;
 }
 

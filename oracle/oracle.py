@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 from koordinator_amd import abi
-from koordinator_amd.cluster import NodeState, NodeTable, PodTable, QuotaTable
+from koordinator_amd.cluster import NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
@@ -39,6 +39,8 @@ def lib():
         L.ko_create.argtypes = [C.POINTER(abi.KsConfig), C.POINTER(abi.KsNodeCols), C.c_int64, C.c_int]
         L.ko_destroy.argtypes = [C.c_void_p]
         L.ko_load_quotas.argtypes = [C.c_void_p, C.POINTER(abi.KsQuotaCols), C.c_int32]
+        L.ko_load_reservations.argtypes = [C.c_void_p, C.POINTER(abi.KsReservationCols), C.c_int32]
+        L.ko_read_reservations.argtypes = [C.c_void_p, abi.P64, abi.P32]
         L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
         L.ko_eval_pod.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
         L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
@@ -56,7 +58,8 @@ def lib():
 class Oracle:
     """Sequential one-pod-at-a-time scheduler on the CPU (reduced form)."""
 
-    def __init__(self, cfg: abi.KsConfig, nodes: NodeTable, quotas: QuotaTable | None = None, nthreads: int = 1):
+    def __init__(self, cfg: abi.KsConfig, nodes: NodeTable, quotas: QuotaTable | None = None, nthreads: int = 1,
+                 reservations: ReservationTable | None = None):
         self.L = lib()
         self.cfg = cfg
         self.n = nodes.n
@@ -67,6 +70,12 @@ class Oracle:
             self._q = quotas.ks()
             self.L.ko_load_quotas(self.h, C.byref(self._q), quotas.q)
             self.nq = quotas.q
+        self.nr = 0
+        if reservations is not None:
+            self._r = reservations.ks()
+            if self.L.ko_load_reservations(self.h, C.byref(self._r), reservations.r) != 0:
+                raise ValueError("reservation row references an unknown node")
+            self.nr = reservations.r
 
     def close(self):
         if self.h:
@@ -83,8 +92,9 @@ class Oracle:
         out = (abi.KsResult * max(pods.n, 1))()
         cols = pods.ks()
         self.L.ko_schedule(self.h, C.byref(cols), pods.n, out)
-        arr = np.frombuffer(out, dtype=np.dtype([("node", "<i4"), ("status", "<u4"), ("score", "<i8")]), count=pods.n)
-        return {"node": arr["node"].copy(), "status": arr["status"].copy(), "score": arr["score"].copy()}
+        arr = np.frombuffer(out, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS), count=pods.n)
+        return {"node": arr["node"].copy(), "status": arr["status"].copy(), "score": arr["score"].copy(),
+                "reservation": arr["reservation"].copy()}
 
     def eval_pod(self, pod: PodTable):
         reasons = np.zeros(self.n, np.uint32)
@@ -100,6 +110,12 @@ class Oracle:
         s = st.ks()
         self.L.ko_read_nodes(self.h, C.byref(s))
         return st
+
+    def read_reservations(self):
+        allocated = np.zeros(max(self.nr, 1) * abi.KS_RSV_DIMS, np.int64)
+        assigned = np.zeros(max(self.nr, 1), np.int32)
+        self.L.ko_read_reservations(self.h, allocated.ctypes.data_as(abi.P64), assigned.ctypes.data_as(abi.P32))
+        return allocated[: self.nr * abi.KS_RSV_DIMS].reshape(self.nr, abi.KS_RSV_DIMS), assigned[: self.nr]
 
     def read_quota_used(self) -> np.ndarray:
         used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)

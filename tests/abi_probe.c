@@ -6,9 +6,12 @@
 int main(void) {
   P(ks_fit_args); P(ks_loadaware_args); P(ks_quota_args); P(ks_config); P(ks_node_cols); P(ks_pod_cols);
   P(ks_quota_cols); P(ks_quota_tree); P(ks_result); P(ks_node_state); P(ks_stats);
+  P(ks_reservation_args); P(ks_reservation_cols);
   O(ks_config, fit); O(ks_config, loadaware); O(ks_config, quota); O(ks_config, batch_pods); O(ks_config, profile);
   O(ks_node_cols, alloc_scalar); O(ks_node_cols, la_flags); O(ks_node_cols, la_prod_usage_milli_memory);
   O(ks_pod_cols, flags); O(ks_pod_cols, quota_req); O(ks_quota_cols, nonpreemptible_used);
   O(ks_quota_tree, max); O(ks_quota_tree, self_request); O(ks_quota_tree, cluster_total); O(ks_stats, sweep_ms); O(ks_stats, diag);
+  O(ks_config, reservation); O(ks_pod_cols, rsv_class); O(ks_result, reservation); O(ks_reservation_cols, allocatable);
+  O(ks_reservation_cols, allocated); O(ks_reservation_cols, assigned); O(ks_reservation_cols, reserve_nonzero_memory);
   return 0;
 }

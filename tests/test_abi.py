@@ -24,7 +24,8 @@ STRUCTS = {
     "ks_fit_args": abi.KsFitArgs, "ks_loadaware_args": abi.KsLoadAwareArgs, "ks_quota_args": abi.KsQuotaArgs,
     "ks_config": abi.KsConfig, "ks_node_cols": abi.KsNodeCols, "ks_pod_cols": abi.KsPodCols,
     "ks_quota_cols": abi.KsQuotaCols, "ks_quota_tree": abi.KsQuotaTree, "ks_result": abi.KsResult, "ks_node_state": abi.KsNodeState,
-    "ks_stats": abi.KsStats,
+    "ks_stats": abi.KsStats, "ks_reservation_args": abi.KsReservationArgs,
+    "ks_reservation_cols": abi.KsReservationCols,
 }
 
 

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU iteration for the Reservation row: its parity tests, then the whole gpu suite, then a short C2 bench.
+set -o pipefail
+OUT=gpurun_out/${1:-rsv}
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_reservation.py -x -v --timeout 180 --timeout-method thread > $OUT/pytest_rsv.log 2>&1 || { echo "rsv pytest failed"; tail -60 $OUT/pytest_rsv.log; exit 1; }
+tail -3 $OUT/pytest_rsv.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 300 python -u bench.py --no-cpu-baseline ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
