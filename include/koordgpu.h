@@ -86,6 +86,13 @@ extern "C" {
 #define KS_POD_NONPREEMPTIBLE 0x04u  /* extension.IsPodNonPreemptible (elasticquota/plugin.go:236)   */
 #define KS_POD_SCALAR_KEYS 0x08u     /* podRequest.ScalarResources has at least one key (upstream fitsRequest) */
 #define KS_POD_RSV_AFFINITY 0x10u    /* GetRequiredReservationAffinity != nil (reservation/transformer.go:51, stateData.hasAffinity) */
+#define KS_POD_CPU_BIND 0x20u        /* NodeNUMAResource preFilterState.requestCPUBind (nodenumaresource/plugin.go:236-262):
+                                        cpuset allocation is not supported by this build (KS_EUNSUPPORTED) */
+
+/* ---- per-node NodeNUMAResource flags (ks_node_cols.numa_flags) ---- */
+#define KS_NUMA_INVALID_RATIO 0x1u   /* GetNodeResourceAmplificationRatio returned an error (plugin.go:348-351)   */
+#define KS_NUMA_CPU_BIND_POLICY 0x2u /* node CPU bind policy label != None (GetNodeCPUBindPolicy): unsupported   */
+#define KS_NUMA_TOPOLOGY_POLICY 0x4u /* NUMA topology policy != None (getNUMATopologyPolicy): unsupported         */
 
 /* ---- per-node filter reason bits (ks_eval_pod_debug) ---- */
 #define KS_R_FIT_PODS 0x001u      /* "Too many pods"                                    */
@@ -99,6 +106,8 @@ extern "C" {
 #define KS_R_LA_PROD 0x100u       /* the failure came from filterProdUsage              */
 #define KS_R_RSV_AFFINITY 0x200u  /* ErrReasonReservationAffinity: no matched reservation (reservation/plugin.go:236,343) */
 #define KS_R_RSV_NO_FIT 0x400u    /* filterWithReservations: no matched reservation satisfies the pod (plugin.go:425-437) */
+#define KS_R_NUMA_AMPLIFIED_CPU 0x800u  /* ErrInsufficientAmplifiedCPU (nodenumaresource/plugin.go:369-371)       */
+#define KS_R_NUMA_INVALID_RATIO 0x1000u /* ErrInvalidCPUAmplificationRatio (plugin.go:348-351)                    */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -111,7 +120,8 @@ extern "C" {
 #define KS_SCORE_FIT 0
 #define KS_SCORE_LOADAWARE 1
 #define KS_SCORE_RESERVATION 2 /* after DefaultNormalizeScore (reservation/scoring.go:126-131) */
-#define KS_NUM_SCORE_PLUGINS 3
+#define KS_SCORE_NUMA 3        /* NodeNUMAResource scoreWithAmplifiedCPUs (nodenumaresource/scoring.go:98-114) */
+#define KS_NUM_SCORE_PLUGINS 4
 
 /* ---- reservation flags (ks_reservation_cols.flags) ---- */
 #define KS_RSV_UNSCHEDULABLE 0x1u /* ReservationInfo.IsUnschedulable (transformer.go:113)              */
@@ -168,6 +178,17 @@ typedef struct ks_reservation_args {
   int64_t plugin_weight;
 } ks_reservation_args;
 
+/* NodeNUMAResourceArgs.ScoringStrategy (pkg/scheduler/apis/config/types.go; defaults
+ * v1beta2/defaults.go:107-136: LeastAllocated, cpu 1, memory 1).  Pods that request a cpuset
+ * (KS_POD_CPU_BIND) and nodes with a CPU-bind or NUMA topology policy are not supported. */
+typedef struct ks_numa_args {
+  int32_t enable;
+  int32_t strategy; /* KS_LEAST_ALLOCATED | KS_MOST_ALLOCATED */
+  int64_t weight_cpu;
+  int64_t weight_memory;
+  int64_t plugin_weight;
+} ks_numa_args;
+
 typedef struct ks_config {
   int32_t abi_version; /* = KS_ABI_VERSION */
   int32_t device;      /* HIP device ordinal */
@@ -179,6 +200,7 @@ typedef struct ks_config {
   int32_t profile;     /* 1 = bracket every kernel with HIP events (ks_get_stats) */
   int32_t _pad1;
   ks_reservation_args reservation;
+  ks_numa_args numa;
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -216,6 +238,10 @@ typedef struct ks_node_cols {
   const int64_t *la_usage_milli_memory;
   const int64_t *la_prod_usage_milli_cpu; /* Σ prod pod usages .MilliValue() (load_aware.go:231-248) */
   const int64_t *la_prod_usage_milli_memory;
+  /* NodeNUMAResource */
+  const double *numa_cpu_amplification; /* node annotation cpu amplification ratio; NULL / <= 1 = none */
+  const int32_t *numa_cpuset_cpus;      /* CPUs allocated to cpuset pods: GetAvailableCPUs' allocated.Size() */
+  const uint32_t *numa_flags;           /* KS_NUMA_* */
 } ks_node_cols;
 
 /* Pending pods, queue order, structure-of-arrays. */

@@ -38,6 +38,11 @@ KS_POD_DAEMONSET = 0x02
 KS_POD_NONPREEMPTIBLE = 0x04
 KS_POD_SCALAR_KEYS = 0x08
 KS_POD_RSV_AFFINITY = 0x10
+KS_POD_CPU_BIND = 0x20
+
+KS_NUMA_INVALID_RATIO = 0x1
+KS_NUMA_CPU_BIND_POLICY = 0x2
+KS_NUMA_TOPOLOGY_POLICY = 0x4
 
 KS_R_FIT_PODS = 0x001
 KS_R_FIT_CPU = 0x002
@@ -50,6 +55,8 @@ KS_R_LA_AGGREGATED = 0x080
 KS_R_LA_PROD = 0x100
 KS_R_RSV_AFFINITY = 0x200
 KS_R_RSV_NO_FIT = 0x400
+KS_R_NUMA_AMPLIFIED_CPU = 0x800
+KS_R_NUMA_INVALID_RATIO = 0x1000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -60,7 +67,8 @@ KS_S_UNSCHEDULABLE = 0x8
 KS_SCORE_FIT = 0
 KS_SCORE_LOADAWARE = 1
 KS_SCORE_RESERVATION = 2
-KS_NUM_SCORE_PLUGINS = 3
+KS_SCORE_NUMA = 3
+KS_NUM_SCORE_PLUGINS = 4
 
 KS_RSV_UNSCHEDULABLE = 0x1
 KS_RSV_ALLOCATE_ONCE = 0x2
@@ -109,6 +117,11 @@ class KsReservationArgs(C.Structure):
     _fields_ = [("enable", C.c_int32), ("_pad0", C.c_int32), ("plugin_weight", C.c_int64)]
 
 
+class KsNumaArgs(C.Structure):
+    _fields_ = [("enable", C.c_int32), ("strategy", C.c_int32), ("weight_cpu", C.c_int64),
+                ("weight_memory", C.c_int64), ("plugin_weight", C.c_int64)]
+
+
 class KsConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -121,6 +134,7 @@ class KsConfig(C.Structure):
         ("profile", C.c_int32),
         ("_pad1", C.c_int32),
         ("reservation", KsReservationArgs),
+        ("numa", KsNumaArgs),
     ]
 
 
@@ -154,6 +168,9 @@ NODE_COLS = [
     ("la_usage_milli_memory", P64),
     ("la_prod_usage_milli_cpu", P64),
     ("la_prod_usage_milli_memory", P64),
+    ("numa_cpu_amplification", C.POINTER(C.c_double)),
+    ("numa_cpuset_cpus", P32),
+    ("numa_flags", PU32),
 ]
 
 

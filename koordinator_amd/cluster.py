@@ -26,8 +26,9 @@ NODE_I64 = [
     "la_usage_milli_cpu", "la_usage_milli_memory",
     "la_prod_usage_milli_cpu", "la_prod_usage_milli_memory",
 ]
-NODE_I32 = ["allowed_pods", "pod_count", "la_thr_cpu", "la_thr_memory", "la_prod_thr_cpu", "la_prod_thr_memory"]
-NODE_U32 = ["la_flags"]
+NODE_I32 = ["allowed_pods", "pod_count", "la_thr_cpu", "la_thr_memory", "la_prod_thr_cpu", "la_prod_thr_memory",
+            "numa_cpuset_cpus"]
+NODE_U32 = ["la_flags", "numa_flags"]
 
 POD_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral",
@@ -99,6 +100,7 @@ class NodeTable(_Table):
         super().__init__(n)
         self.alloc_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
+        self.numa_cpu_amplification = np.zeros(self.n, np.float64)  # <= 1: not amplified
 
     def copy(self) -> "NodeTable":
         t = NodeTable(self.n)
@@ -106,6 +108,7 @@ class NodeTable(_Table):
             setattr(t, k, v.copy())
         t.alloc_scalar = self.alloc_scalar.copy()
         t.req_scalar = self.req_scalar.copy()
+        t.numa_cpu_amplification = self.numa_cpu_amplification.copy()
         return t
 
     def rows(self, idx) -> "NodeTable":
@@ -115,6 +118,7 @@ class NodeTable(_Table):
             setattr(t, k, np.ascontiguousarray(v[idx]))
         t.alloc_scalar = np.ascontiguousarray(self.alloc_scalar[:, idx])
         t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
+        t.numa_cpu_amplification = np.ascontiguousarray(self.numa_cpu_amplification[idx])
         return t
 
     def check_range(self) -> None:
@@ -133,6 +137,9 @@ class NodeTable(_Table):
         for name in NODE_I32:
             setattr(c, name, _p32(getattr(self, name)))
         c.la_flags = _pu32(self.la_flags)
+        c.numa_flags = _pu32(self.numa_flags)
+        self.numa_cpu_amplification = np.ascontiguousarray(self.numa_cpu_amplification, np.float64)
+        c.numa_cpu_amplification = self.numa_cpu_amplification.ctypes.data_as(C.POINTER(C.c_double))
         for k in range(abi.KS_MAX_SCALARS):
             c.alloc_scalar[k] = _p64(self.alloc_scalar[k])
             c.req_scalar[k] = _p64(self.req_scalar[k])

@@ -105,6 +105,13 @@ class NodeResourcesFitArgs:
 
 
 @dataclass
+class NodeNUMAResourceArgs:
+    """NodeNUMAResourceArgs.ScoringStrategy after v1beta2 defaults (defaults.go:107-136)."""
+    strategy: str = "LeastAllocated"
+    resources: Dict[str, int] = field(default_factory=lambda: {CPU: 1, MEMORY: 1})
+
+
+@dataclass
 class ElasticQuotaArgs:
     enable_runtime_quota: bool = True
     enable_check_parent_quota: bool = False
@@ -120,6 +127,8 @@ class SchedulerProfile:
     loadaware_weight: int = 1
     quota: Optional[ElasticQuotaArgs] = None
     reservation_weight: Optional[int] = None  # Reservation plugin score weight (koord profile: 5000); None = off
+    numa: Optional[NodeNUMAResourceArgs] = None
+    numa_weight: int = 1
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -172,6 +181,15 @@ class SchedulerProfile:
             c.loadaware.scaling_cpu = la.estimated_scaling_factors.get(CPU, 0)
             c.loadaware.scaling_memory = la.estimated_scaling_factors.get(MEMORY, 0)
             c.loadaware.plugin_weight = self.loadaware_weight
+        if self.numa is not None:
+            c.numa.enable = 1
+            c.numa.strategy = abi.KS_MOST_ALLOCATED if self.numa.strategy == "MostAllocated" else abi.KS_LEAST_ALLOCATED
+            for name, w in self.numa.resources.items():
+                if name not in (CPU, MEMORY):
+                    raise ValidationError(f"NodeNUMAResource weight on {name} is not supported (cpu/memory only)")
+            c.numa.weight_cpu = self.numa.resources.get(CPU, 0)
+            c.numa.weight_memory = self.numa.resources.get(MEMORY, 0)
+            c.numa.plugin_weight = self.numa_weight
         if self.reservation_weight is not None:
             c.reservation.enable = 1
             c.reservation.plugin_weight = int(self.reservation_weight)

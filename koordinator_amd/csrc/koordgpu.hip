@@ -76,6 +76,15 @@ __global__ void prep_nodes_kernel(DevNodes d, int64_t n, int32_t filter_expired)
   }
   if (r_np) bits |= kLaFailNonProd | (r_np << kLaReasonNonProdShift);
   if (r_p) bits |= kLaFailProd | (r_p << kLaReasonProdShift);
+  // NodeNUMAResource: Amplify(allocated, ratio) = int64(math.Ceil(float64(allocated) * ratio)), ratio > 1
+  // (apis/extension/node_resource_amplification.go:170-175)
+  const double ratio = d.numa_ratio[i];
+  const int64_t A = (int64_t)d.numa_cpus[i] * 1000;
+  const bool amp = ratio > 1.0;
+  d.numa_amilli[i] = A;
+  d.numa_off[i] = amp ? (int64_t)::ceil((double)A * ratio) - A : 0;
+  if (amp) bits |= kNumaAmp;
+  if (d.numa_flags[i] & KS_NUMA_INVALID_RATIO) bits |= kNumaInvalid;
   d.la_bits[i] = bits;
 }
 
@@ -140,6 +149,12 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   for (int k = 0; k < KS_MAX_SCALARS; ++k) keys |= r.sc[k] != 0 ? (1u << (3 + k)) : 0u;
   r.rsv_keys = keys;
   r._fpad = 0.0f;
+  if (keys == 0) r.flags |= kPodReqZero;
+  r.h_cpu = r.cpu * 100;
+  r.h_mem = r.mem * 100;
+  r.f_cpu = i64_to_f32(r.cpu);
+  r.f_mem = i64_to_f32(r.mem);
+  r._pad2 = 0;
   out[i] = r;
 }
 
@@ -160,7 +175,7 @@ struct SweepArgs {
 };
 
 // local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
-template <int NSC, bool RSV>
+template <int NSC, int FEAT>
 __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const int lane = threadIdx.x & 63;
   // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar)
@@ -184,7 +199,8 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     uint32_t best = 0, second = 0;
     for (int32_t p = p0; p < p1; ++p) {
       const PodRec pod = load_pod_uniform(a.pods + cursor + p);
-      const EvalOut o = eval_full<NSC, false, false, true, RSV>(a.c, a.rv, pod, r, node);
+      const EvalOut o = eval_full<NSC, false, true, FEAT>(
+          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); });
       const uint32_t key = o.reasons ? 0u : (((uint32_t)(o.total + 1) << 6) | (uint32_t)(63 - lane));
       const uint32_t m1 = wave_max_u32(key);
       const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
@@ -510,7 +526,9 @@ enum RowField : int {
   RF_TERM_CPU = 9, RF_TERM_MEM = 10, RF_PTERM_CPU = 11, RF_PTERM_MEM = 12, RF_POD_COUNT = 13,
   RF_ALLOC_CPU = 14, RF_ALLOC_MEM = 15, RF_ALLOC_EPH = 16, RF_ALLOC_SC = 17,  // 17..20
   RF_LA_ALLOC_CPU = 21, RF_LA_ALLOC_MEM = 22, RF_ALLOWED = 23, RF_LA_BITS = 24, RF_RSV_CLS = 25,
-  RF_N = 26
+  RF_RSV_BEG = 26, RF_RSV_END = 27,  // the node's reservation range [beg, end) in the CSR table
+  RF_NUMA_A = 28, RF_NUMA_OFF = 29,   // NodeNUMAResource cpuset milli-CPUs and amplification offset
+  RF_N = 30
 };
 
 // slot-row terms: score terms 0..10, then the Filter headrooms (Allocatable - Requested) stored as
@@ -518,7 +536,8 @@ enum RowField : int {
 enum SlotTerm : int {
   ST_CPU = 0, ST_MEM = 1, ST_EPH = 2, ST_SC = 3, ST_LCPU = 7, ST_LMEM = 8, ST_PLCPU = 9, ST_PLMEM = 10,
   ST_FREE_CPU = 11, ST_FREE_MEM = 12, ST_FREE_EPH = 13, ST_FREE_SC = 14,  // 14..17
-  ST_N = 18
+  ST_NCPU = 18, ST_NMEM = 19,  // NodeNUMAResource: Requested (+ amplified cpuset part) cpu / memory
+  ST_N = 20
 };
 
 struct __attribute__((aligned(16))) SlotRow {
@@ -526,8 +545,8 @@ struct __attribute__((aligned(16))) SlotRow {
   uint32_t la_bits;
   int32_t fit_ws, allowed, pod_count;
 };
-// 592 B = 37 x 16 B: consecutive rows start 5 x 16 B apart mod 256 B, so lane = slot ds_read_b128 is conflict-free
-static_assert(sizeof(SlotRow) == 592, "SlotRow layout");
+// 656 B = 41 x 16 B (an odd number of 16 B units): lane = slot ds_read_b128 is conflict-free
+static_assert(sizeof(SlotRow) == 656, "SlotRow layout");
 
 // Device column of each row field (built by the host at ks_load_nodes).
 struct RowCol {
@@ -554,6 +573,8 @@ struct CommitArgs {
   unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot row misses [14] fast picks
   int64_t n, nchunks;
   int32_t total_pods, batch, k;
+  int32_t rcap;        // reservations cached in LDS per slot (0 = none)
+  int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
 };
 
 struct QuotaRowsLds {
@@ -564,12 +585,12 @@ struct QuotaRowsLds {
 };
 
 struct CommitLayout {
-  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, quota, touched, total;
+  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, quota, touched, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 
-__host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc) {
+__host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0) {
   CommitLayout L;
   size_t o = 0;
   L.rows = o;
@@ -590,6 +611,12 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += align16((size_t)kMaxBatch * k * 4);
   L.scls = o;
   o += (size_t)kMaxBatch * 8;  // per slot: owner classes of the node's matchable reservations
+  L.snuma = o;
+  o += (size_t)kMaxBatch * 16;  // per slot: NodeNUMAResource cpuset milli-CPUs, amplification offset
+  L.srcnt = o;
+  o += (size_t)kMaxBatch * 8;  // per slot: reservations cached (-1 = on the HBM table), CSR begin
+  L.srec = o;
+  o += align16(rsv_bytes);     // per slot: the node's reservations (RsvRec, rcap each)
   L.quota = o;
   if (qc) o += align16(sizeof(QuotaRowsLds));
   L.touched = o;
@@ -655,6 +682,10 @@ __device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
   r.t_lmem = s.t[ST_LMEM];
   r.t_plcpu = s.t[ST_PLCPU];
   r.t_plmem = s.t[ST_PLMEM];
+  r.t_ncpu = s.t[ST_NCPU];
+  r.t_nmem = s.t[ST_NMEM];
+  r.numa_A = 0;
+  r.numa_off = 0;
   r.la_bits = s.la_bits;
   r.fit_ws = s.fit_ws;
   r.allowed = s.allowed;
@@ -704,7 +735,7 @@ __device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const
 
 // Re-scan a candidate chunk's untouched nodes exactly for one pod (lane = node); touched nodes are
 // covered by the slot evaluation.
-template <int NSC, bool RSV>
+template <int NSC, int FEAT>
 __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const Cfg& cfg, const PodRec& pod,
                                                      int64_t chunk, uint64_t touched_mask) {
   const int lane = threadIdx.x & 63;
@@ -714,16 +745,18 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
     const DevNodes d = *a.dn;
     load_node<NSC>(cfg, d, node, node < a.n, r);
   }
-  const EvalOut o = eval_full<NSC, false, false, false, RSV>(cfg, a.rv, pod, r, node);
+  const EvalOut o = eval_full<NSC, false, false, FEAT>(
+      cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); });
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
   return wave_max_u64(skip ? 0ull : gkey(o.total, node));
 }
 
-template <int NSC, bool QC, bool RSV>
+template <int NSC, bool QC, int FEAT>
 __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
+  constexpr bool RSV = (FEAT & 1) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
-  const CommitLayout lay = commit_layout(K, a.nchunks, QC);
+  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes);
   SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
   PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
   ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
@@ -735,6 +768,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
   unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
   uint64_t* scls = reinterpret_cast<uint64_t*>(smem_raw + lay.scls);
+  int64_t* snuma = reinterpret_cast<int64_t*>(smem_raw + lay.snuma);
+  int32_t* srcnt = reinterpret_cast<int32_t*>(smem_raw + lay.srcnt);
+  int32_t* srbeg = srcnt + kMaxBatch;
+  constexpr int RD = 3 + NSC;
+  RsvRec<RD>* srec = reinterpret_cast<RsvRec<RD>*>(smem_raw + lay.srec);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -849,6 +887,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     case ST_FREE_SC + 0: case ST_FREE_SC + 1: case ST_FREE_SC + 2: case ST_FREE_SC + 3:
       t_cap = RF_ALLOC_SC + (lane - ST_FREE_SC); t_req = RF_REQ_SC + (lane - ST_FREE_SC);
       t_pw = 7 + (lane - ST_FREE_SC); t_pw100 = t_pw; t_score = false; t_rdim = 3 + (lane - ST_FREE_SC); break;
+    case ST_NCPU: t_cap = RF_ALLOC_CPU; t_req = RF_REQ_CPU; t_pw = 0; t_pw100 = kPodWordHCpu; t_rdim = 0; break;
+    case ST_NMEM: t_cap = RF_ALLOC_MEM; t_req = RF_REQ_MEM; t_pw = 1; t_pw100 = kPodWordHMem; t_rdim = 1; break;
     default: break;
   }
   constexpr int kLaneCounts = ST_N;  // lane: pod count / flags of the row
@@ -955,7 +995,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         NodeReg<NSC> r;
         slot_to_reg<NSC>(rows[lane], r);
         r.rsv_cls = scls[lane];
-        const EvalOut o = eval_full<NSC, false, true, false, RSV>(cfg, a.rv, pod, r, snode);
+        r.numa_A = snuma[2 * lane];
+        r.numa_off = snuma[2 * lane + 1];
+        const EvalOut o = eval_full<NSC, false, false, FEAT>(cfg, pod, r, [&](RsvDelta<NSC>& dl) {
+          const int32_t c = srcnt[lane];
+          if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
+          return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
+        });
         key_mod = o.reasons ? 0ull : gkey(o.total, snode);
       }
       best = umax64(cj.umax, wave_max_u64(key_mod));
@@ -965,7 +1011,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? cj.ub : 0ull);
         const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && cj.ub == kmax)) - 1;
         const int64_t c = (int64_t)(uint32_t)__shfl((int)cj.chunk, sel, 64);
-        const uint64_t v = rescan_untouched<NSC, RSV>(a, cfg, pod, c, touched[c]);
+        const uint64_t v = rescan_untouched<NSC, FEAT>(a, cfg, pod, c, touched[c]);
         ++rescans;
         best = umax64(best, v);
         need &= ~(1ull << sel);
@@ -991,7 +1037,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     SlotRow* row;
     // Reservation Reserve needs the node's pre-pod row: when the pod's class matches one of the
     // node's reservations the row is built / kept without the pod, nominated on, then taken.
-    const int32_t pcls = RSV ? __builtin_amdgcn_readfirstlane(spods[j].rsv_class) : -1;
+    const int32_t pcls = (RSV && cfg.rsv) ? __builtin_amdgcn_readfirstlane(spods[j].rsv_class) : -1;
     bool rsvc = false;
     if (s < 0) {
       s = nslots++;
@@ -1011,10 +1057,43 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       if (lane == 0) touched[node >> 6] |= 1ull << (node & 63);
       const uint64_t ncl = (uint64_t)src[RF_RSV_CLS];
       rsvc = pcls >= 0 && pcls < 64 && ((ncl >> pcls) & 1ull);
-      if (lane == 0) scls[s] = ncl;
+      if (lane == 0) {
+        scls[s] = ncl;
+        snuma[2 * s] = src[RF_NUMA_A];
+        snuma[2 * s + 1] = src[RF_NUMA_OFF];
+      }
+      if (RSV && cfg.rsv) {
+        // the node's reservations into LDS (lane = record word), unless too many or too wide
+        const int32_t rb = (int32_t)src[RF_RSV_BEG], cnt = (int32_t)src[RF_RSV_END] - rb;
+        int32_t mode = -1;
+        if (cnt <= a.rcap) {
+          constexpr int W = (int)(sizeof(RsvRec<RD>) / 8);
+          int64_t* dst = reinterpret_cast<int64_t*>(srec + s * a.rcap);
+          const DevRsv& rv = *a.rv;
+          for (int t = lane; t < cnt * W; t += 64) {
+            const int rr = t / W, w = t - rr * W;
+            const int64_t i = rb + rr;
+            int64_t v;
+            if (w == 0) v = (int64_t)gld(rv.cls + i);
+            else if (w == 1) v = (int64_t)(((uint64_t)(uint32_t)gld(rv.ohi + i) << 32) | gld(rv.meta + i));
+            else if (w == 2) v = (int64_t)(uint32_t)gld(rv.assigned + i);
+            else if (w < 3 + RD) v = gld(rv.alloc + (int64_t)(w - 3) * rv.nr + i);
+            else if (w < 3 + 2 * RD) v = gld(rv.allocd + (int64_t)(w - 3 - RD) * rv.nr + i);
+            else v = gld(rv.rnz + (int64_t)(w - 3 - 2 * RD) * rv.nr + i);
+            dst[t] = v;
+          }
+          const bool wide = __ballot(lane < cnt && rsv_ndims(srec[s * a.rcap + (lane < cnt ? lane : 0)].meta) > RD) != 0;
+          mode = wide ? -1 : cnt;
+        }
+        if (lane == 0) {
+          srcnt[s] = mode;
+          srbeg[s] = rb;
+        }
+      }
       // build the slot row with the pod already reserved on it (lane-parallel, one code path)
       const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
-      const int64_t cap = src[t_cap], req = src[t_req] + (take ? podw[t_pw] : 0);
+      const int64_t cap = src[t_cap],
+                    req = src[t_req] + (take ? podw[t_pw] : 0) + (lane == ST_NCPU ? src[RF_NUMA_OFF] : 0);
       if (lane < ST_N) {
         Term t;
         t.c = cap;
@@ -1050,34 +1129,57 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       NodeReg<NSC> nr;
       slot_to_reg<NSC>(*row, nr);
       nr.rsv_cls = scls[s];
+      nr.numa_A = snuma[2 * s];
+      nr.numa_off = snuma[2 * s + 1];
       RsvDelta<NSC> dl;
-      const RsvOut ro = rsv_eval<NSC, true>(*a.rv, pod, nr, node, dl);
-      const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);
+      const int32_t mode = srcnt[s];
+      const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s]};
+      RsvOut ro;
+      if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl);
+      else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl);
+      const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);  // view index
       if (ro.hi >= kRsvOrderBase) {
         rsv_apply<NSC>(nr, dl, 1);
-        fitla_pref = eval_pod_node<NSC, false>(cfg, pod, nr).total;
+        EvalOut e2 = eval_pod_node<NSC, false>(cfg, pod, nr);
+        if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
+        fitla_pref = e2.total;
       }
       int64_t dd = 0;
       if (nom >= 0) {
-        const RsvReserve rr = rsv_reserve_delta<true>(*a.rv, pod, nom);
+        RsvReserve rr;
+        int64_t gi;
+        if (mode >= 0) {
+          rr = rsv_reserve_delta(lv, pod, nom);
+          gi = lv.csr(nom);
+        } else {
+          const RsvG<true> gv(*a.rv, node);
+          rr = rsv_reserve_delta(gv, pod, nom);
+          gi = gv.csr(nom);
+        }
+        RsvRec<RD>* rec = srec + s * a.rcap + nom;
 #pragma unroll
         for (int d = 0; d < kRsvDims; ++d) {
           dd = (t_rdim == d) ? rr.dreq[d] : dd;
-          if (lane == d && rr.add[d] != 0)
-            atomicAdd((unsigned long long*)(a.rv->allocd + (int64_t)d * a.rv->nr + nom), (unsigned long long)rr.add[d]);
+          if (lane == d && rr.add[d] != 0) {
+            // the HBM table stays current for the next pass; the LDS copy for this one
+            atomicAdd((unsigned long long*)(a.rv->allocd + (int64_t)d * a.rv->nr + gi), (unsigned long long)rr.add[d]);
+            if (mode >= 0 && d < RD) rec->allocd[d] += rr.add[d];
+          }
         }
         dd = (t_rdim == 8) ? rr.dnz[0] : (t_rdim == 9) ? rr.dnz[1] : dd;
-        if (lane == 0) atomicAdd(a.rv->assigned + nom, 1);
-        __threadfence();
+        if (lane == 0) {
+          atomicAdd(a.rv->assigned + gi, 1);
+          if (mode >= 0) rec->assigned += 1;
+        }
+        if (mode < 0) __threadfence();
         if (rr.now_ineligible) {
-          const uint64_t ncl = rsv_node_classes<true>(*a.rv, node);
+          const uint64_t ncl = mode >= 0 ? rsv_node_classes(lv) : rsv_node_classes(RsvG<true>(*a.rv, node));
           if (lane == 0) {
             scls[s] = ncl;
             atomicExch((unsigned long long*)(a.rv->ncls + node), (unsigned long long)ncl);
           }
-          __threadfence();
         }
-        nom_row = a.rv->rowid[nom];
+        nom_row = a.rv->rowid[gi];
       }
       const bool take = !t_prod_only || (pflags & KS_POD_PROD);
       if (lane < ST_N) {
@@ -1089,7 +1191,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       }
     }
     int64_t score_out = score;
-    if (RSV) {
+    if (RSV && cfg.rsv) {
       // the chosen node holds the maximum normalized Reservation score: 100 if hi > 0, else 0
       const int64_t hi = score / cfg.rsv_F;
       const int64_t fitla = hi >= kRsvOrderBase ? fitla_pref : score - hi * cfg.rsv_F;
@@ -1311,12 +1413,15 @@ __global__ void eval_debug_kernel(DevNodes d, const DevRsv* rv, Cfg c, const Pod
   load_node<NSC>(c, d, i, 1, r);
   const PodRec p = *pod;
   RsvOut ro;
-  const EvalOut o = eval_full<NSC, true, false, false>(c, rv, p, r, i, &ro);
+  const EvalOut o = eval_full<NSC, true, false, 3>(
+      c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); }, &ro);
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
-  total[i] = o.reasons ? -1 : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw;  // Fit + LoadAware part
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
+  // Fit + LoadAware + NUMA part (the Reservation part is added by rsv_normalize_debug_kernel)
+  total[i] = o.reasons ? -1 : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw;
   raw[i] = ro.raw;
   hiord[i] = ro.hiord;
 }
@@ -1532,9 +1637,15 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   // LeastAllocated Fit + LoadAware: a commit only raises requested/estimated usage, so a node's
   // key can only drop and its Filter can only start failing.
   k.monotone = c.fit.strategy == KS_LEAST_ALLOCATED || !c.fit.enable_score;
+  k.numa = c.numa.enable ? 1 : 0;
+  k.numa_most = c.numa.strategy == KS_MOST_ALLOCATED;
+  k.nw_cpu = (int32_t)c.numa.weight_cpu;
+  k.nw_mem = (int32_t)c.numa.weight_memory;
+  k.numa_pw = c.numa.enable ? (int32_t)c.numa.plugin_weight : 0;
+  if (k.numa && k.numa_most) k.monotone = 0;
   k.rsv = c.reservation.enable ? 1 : 0;
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
-                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0)) + 1);
+                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw) + 1);
   // a commit into a reservation can raise that node's Reservation score for later pods
   if (k.rsv) k.monotone = 0;
   return k;
@@ -1577,9 +1688,18 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
     g_create_error = "ks_create: plugin weights out of supported range";
     return KS_EINVAL;
   }
+  if (cfg->numa.enable) {
+    const ks_numa_args& na = cfg->numa;
+    if (na.weight_cpu < 0 || na.weight_cpu > 100 || na.weight_memory < 0 || na.weight_memory > 100 ||
+        na.plugin_weight < 0 || na.plugin_weight > 1000 || (na.strategy != KS_LEAST_ALLOCATED && na.strategy != KS_MOST_ALLOCATED)) {
+      g_create_error = "ks_create: NodeNUMAResource args out of range";
+      return KS_EINVAL;
+    }
+  }
   if (cfg->reservation.enable) {
     const int64_t fitla = 100 * ((cfg->fit.enable_score ? cfg->fit.plugin_weight : 0) +
-                                 (cfg->loadaware.enable_score ? cfg->loadaware.plugin_weight : 0));
+                                 (cfg->loadaware.enable_score ? cfg->loadaware.plugin_weight : 0) +
+                                 (cfg->numa.enable ? cfg->numa.plugin_weight : 0));
     if (cfg->reservation.plugin_weight <= fitla || cfg->reservation.plugin_weight > ((int64_t)1 << 40) ||
         (fitla + 1) * (kRsvOrderBase + 1) >= (1 << 26)) {
       g_create_error = "ks_create: Reservation plugin weight must exceed 100 x (Fit + LoadAware weights) (ks_rsv.h ranking)";
@@ -1699,6 +1819,11 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.la_pthr_cpu, 4, false);
   add(&d.la_pthr_mem, 4, false);
   add(&d.la_bits, 4, false);
+  add(&d.numa_ratio, 8, false);
+  add(&d.numa_amilli, 8, false);
+  add(&d.numa_off, 8, false);
+  add(&d.numa_cpus, 4, false);
+  add(&d.numa_flags, 4, false);
 }
 
 // host source pointers in the same order as build_col_table (NULL = zeros)
@@ -1735,6 +1860,11 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->la_prod_thr_cpu);
   v.push_back(c->la_prod_thr_memory);
   v.push_back(nullptr);  // la_bits: derived on device
+  v.push_back(c->numa_cpu_amplification);
+  v.push_back(nullptr);  // numa_amilli: derived on device
+  v.push_back(nullptr);  // numa_off: derived on device
+  v.push_back(c->numa_cpuset_cpus);
+  v.push_back(c->numa_flags);
   return v;
 }
 
@@ -1759,6 +1889,17 @@ static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
   for (int k = 0; k < KS_MAX_SCALARS; ++k) {
     if (check_range64(ctx, c->alloc_scalar[k], n, "alloc_scalar") != KS_OK) return KS_EINVAL;
     if (check_range64(ctx, c->req_scalar[k], n, "req_scalar") != KS_OK) return KS_EINVAL;
+  }
+  if (ctx->cfg.numa.enable) {
+    for (int64_t i = 0; c->numa_flags && i < n; ++i)
+      if (c->numa_flags[i] & (KS_NUMA_CPU_BIND_POLICY | KS_NUMA_TOPOLOGY_POLICY))
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: NodeNUMAResource CPU-bind / NUMA topology policies are not supported", (long long)i);
+    for (int64_t i = 0; c->numa_cpuset_cpus && i < n; ++i)
+      if (c->numa_cpuset_cpus[i] < 0 || c->numa_cpuset_cpus[i] > (1 << 20))
+        KS_FAIL(ctx, KS_EINVAL, "node %lld: numa_cpuset_cpus out of range", (long long)i);
+    for (int64_t i = 0; c->numa_cpu_amplification && i < n; ++i)
+      if (!(c->numa_cpu_amplification[i] <= 1024.0))  // also rejects NaN
+        KS_FAIL(ctx, KS_EINVAL, "node %lld: cpu amplification ratio out of range", (long long)i);
   }
   return KS_OK;
 }
@@ -1788,6 +1929,10 @@ static int upload_rowcols(ks_ctx* ctx) {
   set(RF_ALLOWED, d.allowed_pods, 4);
   set(RF_LA_BITS, d.la_bits, 4);
   set(RF_RSV_CLS, d.rsv_cls, 8);
+  set(RF_RSV_BEG, ctx->rv.beg ? (const void*)ctx->rv.beg : (const void*)d.la_bits, 4);
+  set(RF_RSV_END, ctx->rv.beg ? (const void*)(ctx->rv.beg + 1) : (const void*)d.la_bits, 4);
+  set(RF_NUMA_A, d.numa_amilli, 8);
+  set(RF_NUMA_OFF, d.numa_off, 8);
   if (!ctx->rowcols) {
     void* p = nullptr;
     if (dev_alloc(ctx, &p, sizeof(h)) != KS_OK) return KS_ENOMEM;
@@ -1818,7 +1963,7 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
 
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
-  if (validate_nodes(ctx, nodes, n) != KS_OK) return KS_EINVAL;
+  if (int rc = validate_nodes(ctx, nodes, n); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   dev_free(ctx->node_blob);
@@ -1936,7 +2081,10 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
     cls[i] = rc->owner_classes[r];
     const uint32_t flags = rc->flags ? rc->flags[r] & 0xfu : 0u;
     const uint32_t pol = rc->policy ? std::min<uint32_t>(rc->policy[r], 0xfu) : 0u;
-    meta[i] = flags | (pol << 4) | (rc->key_mask[r] << 8);
+    int32_t nd = 0;
+    for (int d = 0; d < D; ++d)
+      if ((rc->allocatable[d] && rc->allocatable[d][r]) || (rc->allocated[d] && rc->allocated[d][r])) nd = d + 1;
+    meta[i] = flags | (pol << 4) | (rc->key_mask[r] << 8) | ((uint32_t)nd << 16);
     const int64_t o = rc->order ? rc->order[r] : 0;
     if (o != 0) {
       const int64_t rank = std::lower_bound(ords.begin(), ords.end(), o) - ords.begin();
@@ -1982,6 +2130,7 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
     ctx->drv = (DevRsv*)p;
   }
   HIPCHK(ctx, hipMemcpyAsync(ctx->drv, &ctx->rv, sizeof(DevRsv), hipMemcpyHostToDevice, ctx->stream));
+  if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;  // row fields RF_RSV_BEG / RF_RSV_END
   if (rsv_launch_base(ctx, nullptr, ctx->n, +1, 1) != KS_OK) return KS_EHIP;
   ctx->rsv_based = true;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2027,7 +2176,7 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
     if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
       KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: duplicate node index with reservations loaded");
   }
-  if (validate_nodes(ctx, rows, m) != KS_OK) return KS_EINVAL;
+  if (int rc = validate_nodes(ctx, rows, m); rc != KS_OK) return rc;
   std::vector<const void*> src = host_cols(rows);
   std::vector<void*> dst;
   std::vector<int32_t> widths;
@@ -2340,6 +2489,11 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
     if (check_range64(ctx, c, p, "pod quantity") != KS_OK) return KS_EINVAL;
   for (int k = 0; k < KS_MAX_SCALARS; ++k)
     if (check_range64(ctx, pc->req_scalar[k], p, "pod scalar") != KS_OK) return KS_EINVAL;
+  if (ctx->cfg.numa.enable && pc->flags) {
+    for (int32_t i = 0; i < p; ++i)
+      if (pc->flags[i] & KS_POD_CPU_BIND)
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: cpuset (cpu-bind) allocation is not supported by this build", i);
+  }
   if (pc->rsv_class) {
     for (int32_t i = 0; i < p; ++i)
       if (pc->rsv_class[i] < -1 || pc->rsv_class[i] >= KS_RSV_CLASSES)
@@ -2373,7 +2527,7 @@ int ks_stage_pods(ks_ctx* ctx, const ks_pod_cols* pods, int32_t p) {
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_stage_pods before ks_load_nodes");
   if (ctx->cfg.quota.enable && pods->quota && !ctx->quota_blob)
     KS_FAIL(ctx, KS_ESTATE, "ElasticQuota enabled but ks_load_quotas not called");
-  if (validate_pods(ctx, pods, p) != KS_OK) return KS_EINVAL;
+  if (int rc = validate_pods(ctx, pods, p); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ensure_pod_capacity(ctx, p) != KS_OK) return KS_ENOMEM;
   if (p > 0 && stage_pods_to(ctx, pods, p, ctx->pods) != KS_OK) return KS_EHIP;
@@ -2395,6 +2549,31 @@ static hipEvent_t take_event(ks_ctx* ctx, size_t i) {
 static bool commit_qcache(const ks_ctx* ctx) {
   if (!(ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows)) return false;
   return commit_layout(ctx->k, ctx->nchunks, true).total <= 160 * 1024;
+}
+
+// kernel variant: 0 = Fit/LoadAware/Quota, 1 = + Reservation, 3 = + Reservation + NodeNUMAResource
+static int kernel_feat(const ks_ctx* ctx) { return ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0); }
+
+static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {
+  return (size_t)kMaxBatch * rcap * 8 * (size_t)(3 + 2 * (3 + ctx->nsc) + 2);  // sizeof(RsvRec<3+nsc>)
+}
+
+// Reservations cached per commit slot: as many as fit next to the rest of the commit layout (<= 8);
+// the quota-row cache yields to it when both do not fit.
+static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
+  *qcache = commit_qcache(ctx);
+  if (!ctx->kc.rsv) return 0;
+  auto fit = [&](bool qc) {
+    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0).total + 64;
+    const size_t avail = base < 160 * 1024 ? 160 * 1024 - base : 0;
+    return (int32_t)std::min<size_t>(8, avail / rsv_cache_bytes(ctx, 1));
+  };
+  int32_t r = fit(*qcache);
+  if (*qcache && r < 4) {
+    *qcache = false;
+    r = fit(false);
+  }
+  return r;
 }
 
 template <int NSC>
@@ -2422,10 +2601,13 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.batch = ctx->batch;
   sa.ppw = ppw;
   rec(0);
-  if (ctx->kc.rsv)
-    hipLaunchKernelGGL((sweep_kernel<NSC, true>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  const int feat = kernel_feat(ctx);
+  if (feat == 3)
+    hipLaunchKernelGGL((sweep_kernel<NSC, 3>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  else if (feat == 1)
+    hipLaunchKernelGGL((sweep_kernel<NSC, 1>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
   else
-    hipLaunchKernelGGL((sweep_kernel<NSC, false>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    hipLaunchKernelGGL((sweep_kernel<NSC, 0>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
   rec(0);
   SelectArgs se;
   se.in = ctx->sweep_out;
@@ -2501,20 +2683,22 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.batch = ctx->batch;
   ca.k = ctx->k;
   ca.rowcols = ctx->rowcols;
-  const bool qcache = commit_qcache(ctx);
-  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache).total;
+  bool qcache = false;
+  ca.rcap = commit_rcap(ctx, &qcache);
+  ca.rsv_bytes = (int32_t)rsv_cache_bytes(ctx, ca.rcap);
+  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes).total;
   rec(2);
-  if (ctx->kc.rsv) {
-    if (qcache)
-      hipLaunchKernelGGL((commit_kernel<NSC, true, true>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
-    else
-      hipLaunchKernelGGL((commit_kernel<NSC, false, true>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
-  } else {
-    if (qcache)
-      hipLaunchKernelGGL((commit_kernel<NSC, true, false>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
-    else
-      hipLaunchKernelGGL((commit_kernel<NSC, false, false>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);
-  }
+#define KS_COMMIT(F)                                                                                          \
+  do {                                                                                                        \
+    if (qcache)                                                                                               \
+      hipLaunchKernelGGL((commit_kernel<NSC, true, F>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca);  \
+    else                                                                                                      \
+      hipLaunchKernelGGL((commit_kernel<NSC, false, F>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca); \
+  } while (0)
+  if (feat == 3) KS_COMMIT(3);
+  else if (feat == 1) KS_COMMIT(1);
+  else KS_COMMIT(0);
+#undef KS_COMMIT
   rec(2);
 }
 
@@ -2525,19 +2709,21 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   const int32_t np = ctx->np;
   if (np == 0) return KS_OK;
   {
-    const bool qcache = commit_qcache(ctx);
-    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache).total;
+    bool qcache = false;
+    const int32_t rcap = commit_rcap(ctx, &qcache);
+    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap)).total;
     if (smem > 160 * 1024)
       KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
     hipError_t e = hipSuccess;
     auto setattr = [&](const void* fn) {
       if (e == hipSuccess) e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     };
-    const bool rs = ctx->kc.rsv != 0;
-#define KS_SETATTR(N)                                                                       \
-  do {                                                                                      \
-    if (rs) qcache ? setattr((const void*)commit_kernel<N, true, true>) : setattr((const void*)commit_kernel<N, false, true>); \
-    else qcache ? setattr((const void*)commit_kernel<N, true, false>) : setattr((const void*)commit_kernel<N, false, false>); \
+    const int feat = kernel_feat(ctx);
+#define KS_SETATTR(N)                                                                                                         \
+  do {                                                                                                                        \
+    if (feat == 3) qcache ? setattr((const void*)commit_kernel<N, true, 3>) : setattr((const void*)commit_kernel<N, false, 3>); \
+    else if (feat == 1) qcache ? setattr((const void*)commit_kernel<N, true, 1>) : setattr((const void*)commit_kernel<N, false, 1>); \
+    else qcache ? setattr((const void*)commit_kernel<N, true, 0>) : setattr((const void*)commit_kernel<N, false, 0>); \
   } while (0)
     if (ctx->nsc == 0) KS_SETATTR(0);
     else if (ctx->nsc == 2) KS_SETATTR(2);
@@ -2616,7 +2802,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     }
   }
   // algorithmic bytes of one full sweep launch: node columns read once per pod group + outputs
-  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16 + (ctx->kc.rsv ? 8 : 0);
+  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16 + (ctx->kc.rsv ? 8 : 0) + (ctx->kc.numa ? 16 : 0);
   const int64_t groups = (ctx->batch + ppw - 1) / ppw;
   ctx->stats.sweep_bytes = local_chunks * 64 * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + local_chunks * 64 * 4;
   return KS_OK;
@@ -2679,7 +2865,7 @@ int ks_restore(ks_ctx* ctx) {
 int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t* scores, int64_t* total) {
   if (!ctx || !pod) return ctx ? (ctx->err = "ks_eval_pod_debug: bad args", KS_EINVAL) : KS_EINVAL;
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_eval_pod_debug before ks_load_nodes");
-  if (validate_pods(ctx, pod, 1) != KS_OK) return KS_EINVAL;
+  if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ensure_pod_capacity(ctx, 1) != KS_OK) return KS_ENOMEM;
   if (stage_pods_to(ctx, pod, 1, ctx->dbg_pod) != KS_OK) return KS_EHIP;

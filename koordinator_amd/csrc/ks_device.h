@@ -20,6 +20,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/koordgpu.h"
@@ -32,6 +33,8 @@ constexpr int kMaxCand = 64;   // candidate chunks per pod
 
 // internal pod flag: podRequest is all-zero with no scalar keys (fitsRequest early return)
 constexpr uint32_t kPodAllZero = 0x100u;
+// internal pod flag: every request value is zero (quotav1.IsZero, NodeNUMAResource PreFilter skip)
+constexpr uint32_t kPodReqZero = 0x200u;
 
 // la_bits (prep_nodes_kernel output)
 constexpr uint32_t kLaZeroScore = 0x1u;     // Score returns 0 (no NodeMetric / expired)
@@ -39,6 +42,8 @@ constexpr uint32_t kLaFailNonProd = 0x2u;   // Filter fails for non-prod (or no 
 constexpr uint32_t kLaFailProd = 0x4u;      // Filter fails for prod pods when prod thresholds exist
 constexpr int kLaReasonNonProdShift = 8;    // KS_R_LA_* reason bits for the non-prod case
 constexpr int kLaReasonProdShift = 20;      // KS_R_LA_* reason bits for the prod case
+constexpr uint32_t kNumaAmp = 1u << 30;     // NodeNUMAResource: cpu amplification ratio > 1
+constexpr uint32_t kNumaInvalid = 1u << 31; // NodeNUMAResource: invalid amplification annotation
 
 // Kernel-constant view of ks_config (int32: weights are validated to small ranges in ks_create,
 // which keeps the sweep's SGPR footprint small).
@@ -50,7 +55,8 @@ struct Cfg {
   int32_t quota_enable, quota_parent;
   int32_t monotone;  // commits can only lower a node's key (LeastAllocated + LoadAware)
   int32_t rsv;       // Reservation plugin enabled
-  int32_t rsv_F;     // key radix: key total = hi * rsv_F + (Fit + LoadAware weighted total), see ks_rsv.h
+  int32_t rsv_F;     // key radix: key total = hi * rsv_F + (Fit + LoadAware + NUMA weighted total), see ks_rsv.h
+  int32_t numa, numa_most, nw_cpu, nw_mem, numa_pw;  // NodeNUMAResource
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -68,6 +74,11 @@ struct DevNodes {
   int64_t *la_total_cpu, *la_total_mem, *la_usage_cpu, *la_usage_mem, *la_pusage_cpu, *la_pusage_mem;
   uint32_t *la_bits;  // derived by prep_nodes_kernel
   uint64_t *rsv_cls;  // union of the owner classes of the node's matchable reservations (ks_rsv.h)
+  double *numa_ratio;       // NodeNUMAResource inputs: cpu amplification ratio, cpuset CPUs, flags
+  int32_t *numa_cpus;
+  uint32_t *numa_flags;
+  int64_t *numa_amilli;     // derived: cpuset CPUs x 1000
+  int64_t *numa_off;        // derived: Amplify(cpuset milli, ratio) - cpuset milli (ratio > 1), else 0
 };
 
 // Per-pod record read by the sweep with scalar loads (AoS, 192 B).  The x100 and f32 copies feed
@@ -85,8 +96,14 @@ struct __attribute__((aligned(16))) PodRec {
   int32_t rsv_class;  // reservation match class (-1 = none)
   uint32_t rsv_keys;  // bit d: request dimension d is non-zero (a key of the pod's requests)
   float _fpad;
+  int64_t h_cpu, h_mem;  // 100 x the Requested cpu / memory (NodeNUMAResource score)
+  float f_cpu, f_mem;
+  int64_t _pad2;
 };
-static_assert(sizeof(PodRec) == 224, "PodRec layout");
+static_assert(sizeof(PodRec) == 256, "PodRec layout");
+// PodRec int64 word indices read by the commit kernel's lane-parallel Reserve
+constexpr int kPodWordHCpu = (int)(offsetof(PodRec, h_cpu) / 8), kPodWordHMem = (int)(offsetof(PodRec, h_mem) / 8);
+static_assert(offsetof(PodRec, h_nzcpu) == 12 * 8 && offsetof(PodRec, h_sc) == 17 * 8, "PodRec word layout");
 
 // Explicit global (addrspace 1) accesses for pointers read from memory: without the cast hipcc
 // emits flat_load, which counts on lgkmcnt too, so every later LDS wait would also wait for the
@@ -208,6 +225,8 @@ struct __attribute__((aligned(16))) NodeReg {
   Term t_eph;                                  // Fit ephemeral-storage: Requested
   Term t_sc[NSC > 0 ? NSC : 1];                // Fit scalars: Requested
   Term t_lcpu, t_lmem, t_plcpu, t_plmem;       // LoadAware: EstimateNode alloc - node term (all / prod)
+  Term t_ncpu, t_nmem;                         // NodeNUMAResource: Requested (+ amplified cpuset part for cpu)
+  int64_t numa_A, numa_off;                    // cpuset milli-CPUs, Amplify(A) - A
   uint32_t la_bits;
   int32_t fit_ws;                              // Σ weights of cpu/mem/eph terms with capacity != 0
   int32_t pods_full;
@@ -239,7 +258,8 @@ __device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int val
                                           int64_t req_eph, int64_t nz_cpu, int64_t nz_mem, const int64_t* alloc_sc,
                                           const int64_t* req_sc, int64_t la_alloc_cpu, int64_t la_alloc_mem,
                                           int64_t term_cpu, int64_t term_mem, int64_t pterm_cpu, int64_t pterm_mem,
-                                          uint32_t la_bits, int32_t allowed, int32_t pod_count) {
+                                          uint32_t la_bits, int32_t allowed, int32_t pod_count, int64_t numa_A = 0,
+                                          int64_t numa_off = 0) {
   r.valid = valid;
   r.free_cpu = alloc_cpu - req_cpu;
   r.free_mem = alloc_mem - req_mem;
@@ -262,6 +282,10 @@ __device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int val
   r.pods_full = ((int64_t)pod_count + 1 > (int64_t)allowed) || !valid;
   r.fit_ws = node_fit_ws<NSC>(c, r);
   r.rsv_cls = 0;
+  r.numa_A = numa_A;
+  r.numa_off = numa_off;
+  term_set(r.t_ncpu, alloc_cpu, req_cpu + numa_off);
+  term_set(r.t_nmem, alloc_mem, req_mem);
 }
 
 template <int NSC>
@@ -273,11 +297,16 @@ __device__ __forceinline__ void load_node(const Cfg& c, const DevNodes& d, int64
     asc[k] = gld(d.alloc_sc[k] + n);
     rsc[k] = gld(d.req_sc[k] + n);
   }
+  int64_t na = 0, no = 0;
+  if (c.numa) {
+    na = gld(d.numa_amilli + n);
+    no = gld(d.numa_off + n);
+  }
   make_node<NSC>(c, r, valid, gld(d.alloc_cpu + n), gld(d.alloc_mem + n), gld(d.alloc_eph + n), gld(d.req_cpu + n),
                  gld(d.req_mem + n), gld(d.req_eph + n), gld(d.nz_cpu + n), gld(d.nz_mem + n), asc, rsc,
                  gld(d.la_alloc_cpu + n), gld(d.la_alloc_mem + n), gld(d.la_term_cpu + n), gld(d.la_term_mem + n),
                  gld(d.la_pterm_cpu + n), gld(d.la_pterm_mem + n), gld(d.la_bits + n), gld(d.allowed_pods + n),
-                 gld(d.pod_count + n));
+                 gld(d.pod_count + n), na, no);
   if (c.rsv && valid) r.rsv_cls = gld(d.rsv_cls + n);
 }
 
@@ -299,6 +328,8 @@ __device__ __forceinline__ void reserve_row(NodeReg<NSC>& r, const PodRec& p) {
   }
   r.pod_count += 1;
   r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
+  term_take(r.t_ncpu, p.cpu, p.h_cpu);
+  term_take(r.t_nmem, p.mem, p.h_mem);
   term_take(r.t_lcpu, p.est_cpu, p.h_est_cpu);
   term_take(r.t_lmem, p.est_mem, p.h_est_mem);
   if (p.flags & KS_POD_PROD) {
@@ -310,6 +341,7 @@ __device__ __forceinline__ void reserve_row(NodeReg<NSC>& r, const PodRec& p) {
 struct EvalOut {
   uint32_t reasons;  // KS_R_* (0 = feasible)
   int32_t fit, la, total;
+  int32_t numa;
 };
 
 // Filter + Score of one (pod, node).  DEBUG=false computes feasibility (reasons != 0) and the
@@ -355,6 +387,7 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   o.reasons = rs;
   o.fit = 0;
   o.la = 0;
+  o.numa = 0;
   int32_t total = 0;
   if (c.fit_score) {
     int32_t ns = 0, ws = r.fit_ws;
@@ -390,6 +423,39 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   }
   o.total = total;
   return o;
+}
+
+// NodeNUMAResource for a pod without cpu bind on a topology-policy-None node: filterAmplifiedCPUs
+// (nodenumaresource/plugin.go:340-373) and scoreWithAmplifiedCPUs (scoring.go:98-114) with the
+// resourceAllocationScorer over cpu / memory Requested (:206-242).
+template <int NSC, bool DEBUG>
+__device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const NodeReg<NSC>& r, EvalOut& o) {
+  if (p.flags & kPodReqZero) return;  // PreFilter skip
+  uint32_t rs = 0;
+  if (p.cpu != 0) {
+    if (r.la_bits & kNumaInvalid) {
+      rs = KS_R_NUMA_INVALID_RATIO;
+    } else if (r.la_bits & kNumaAmp) {
+      const int64_t requested = r.t_ncpu.c - r.free_cpu;  // alloc - (alloc - Requested)
+      const bool amp = requested >= r.numa_A && r.numa_A > 0;
+      if (p.cpu > r.free_cpu - (amp ? r.numa_off : 0)) rs = KS_R_NUMA_AMPLIFIED_CPU;
+    }
+  }
+  o.reasons |= DEBUG ? rs : (rs ? KS_R_FIT_PODS : 0u);
+  Term tc = r.t_ncpu;
+  if (p.cpu == 0) term_take(tc, -r.numa_off, -r.numa_off * 100);  // a cpu-less pod scores the plain Requested
+  int32_t ns = 0, ws = 0;
+  if (c.nw_cpu && tc.c != 0) {
+    ns += (c.numa_most ? term_most(tc, p.cpu, p.h_cpu, p.f_cpu) : term_least(tc, p.cpu, p.h_cpu, p.f_cpu)) * c.nw_cpu;
+    ws += c.nw_cpu;
+  }
+  if (c.nw_mem && r.t_nmem.c != 0) {
+    ns += (c.numa_most ? term_most(r.t_nmem, p.mem, p.h_mem, p.f_mem) : term_least(r.t_nmem, p.mem, p.h_mem, p.f_mem)) *
+          c.nw_mem;
+    ws += c.nw_mem;
+  }
+  o.numa = ws > 0 ? small_div(ns, ws) : 0;
+  o.total += o.numa * c.numa_pw;
 }
 
 // Wave-wide reductions (64 lanes), result wave-uniform.

@@ -91,68 +91,115 @@ struct RsvOut {
   int32_t nom;       // nominated reservation, CSR position (-1 = none)
 };
 
+// ---- views of one node's reservations ----
+// RsvG: the CSR table in HBM (FRESH: the mutable fields around the CU's L1).
+// RsvL: the commit kernel's LDS copy of a touched node's reservations (D = 3 + NSC dims kept; a node
+// whose reservations use a dimension beyond D stays on RsvG).  Index i runs over [0, n()).
 template <bool FRESH>
-__device__ __forceinline__ bool rsv_matches(const DevRsv& rv, int64_t i, int32_t cls, uint32_t& meta, int32_t& a) {
-  meta = gld(rv.meta + i);
-  a = rld<FRESH>(rv.assigned + i);
+struct RsvG {
+  const DevRsv& rv;
+  int64_t b, e;
+  __device__ __forceinline__ RsvG(const DevRsv& r, int64_t node) : rv(r), b(gld(r.beg + node)), e(gld(r.beg + node + 1)) {}
+  __device__ __forceinline__ int64_t n() const { return e - b; }
+  __device__ __forceinline__ uint32_t meta(int64_t i) const { return gld(rv.meta + b + i); }
+  __device__ __forceinline__ int32_t assigned(int64_t i) const { return rld<FRESH>(rv.assigned + b + i); }
+  __device__ __forceinline__ uint64_t cls(int64_t i) const { return gld(rv.cls + b + i); }
+  __device__ __forceinline__ int32_t ohi(int64_t i) const { return gld(rv.ohi + b + i); }
+  __device__ __forceinline__ int64_t alloc(int d, int64_t i) const { return gld(rv.alloc + d * rv.nr + b + i); }
+  __device__ __forceinline__ int64_t allocd(int d, int64_t i) const { return rld<FRESH>(rv.allocd + d * rv.nr + b + i); }
+  __device__ __forceinline__ int64_t rnz(int k, int64_t i) const { return gld(rv.rnz + k * rv.nr + b + i); }
+  __device__ __forceinline__ int32_t csr(int64_t i) const { return (int32_t)(b + i); }
+};
+
+template <int D>
+struct __attribute__((aligned(8))) RsvRec {
+  uint64_t cls;
+  uint32_t meta;
+  int32_t ohi;
+  int32_t assigned, _pad;
+  int64_t alloc[D], allocd[D], rnz[2];
+};
+
+template <int D>
+struct RsvL {
+  const RsvRec<D>* rec;
+  int32_t cnt, b;
+  __device__ __forceinline__ int64_t n() const { return cnt; }
+  __device__ __forceinline__ uint32_t meta(int64_t i) const { return rec[i].meta; }
+  __device__ __forceinline__ int32_t assigned(int64_t i) const { return rec[i].assigned; }
+  __device__ __forceinline__ uint64_t cls(int64_t i) const { return rec[i].cls; }
+  __device__ __forceinline__ int32_t ohi(int64_t i) const { return rec[i].ohi; }
+  __device__ __forceinline__ int64_t alloc(int d, int64_t i) const { return d < D ? rec[i].alloc[d] : 0; }
+  __device__ __forceinline__ int64_t allocd(int d, int64_t i) const { return d < D ? rec[i].allocd[d] : 0; }
+  __device__ __forceinline__ int64_t rnz(int k, int64_t i) const { return rec[i].rnz[k]; }
+  __device__ __forceinline__ int32_t csr(int64_t i) const { return b + (int32_t)i; }
+};
+
+// meta bits 16..19: 1 + the highest dimension with a non-zero allocatable / allocated (0 = none)
+__device__ __forceinline__ int32_t rsv_ndims(uint32_t m) { return (int32_t)((m >> 16) & 0xfu); }
+
+template <typename V>
+__device__ __forceinline__ bool rsv_matches(const V& v, int64_t i, int32_t cls, uint32_t& meta, int32_t& a) {
+  meta = v.meta(i);
+  a = v.assigned(i);
   const bool eligible = !((meta & KS_RSV_ALLOCATE_ONCE) && a > 0);  // transformer.go:109
-  return eligible && !(meta & KS_RSV_UNSCHEDULABLE) && ((gld(rv.cls + i) >> cls) & 1ull);
+  return eligible && !(meta & KS_RSV_UNSCHEDULABLE) && ((v.cls(i) >> cls) & 1ull);
 }
 
 // scoreReservation (scoring.go:183-203): MostAllocated over the non-zero allocatable dims
-template <bool FRESH>
-__device__ __forceinline__ int32_t rsv_score(const DevRsv& rv, const PodRec& p, int64_t i) {
+template <typename V>
+__device__ __forceinline__ int32_t rsv_score(const V& v, const PodRec& p, int64_t i) {
   int32_t s = 0, w = 0;
 #pragma unroll
   for (int d = 0; d < kRsvDims; ++d) {
-    const int64_t al = gld(rv.alloc + d * rv.nr + i);
+    const int64_t al = v.alloc(d, i);
     if (al == 0) continue;
     ++w;
-    const int64_t req = pod_dim(p, d) + rld<FRESH>(rv.allocd + d * rv.nr + i);
+    const int64_t req = pod_dim(p, d) + v.allocd(d, i);
     if (req <= al) s += pct_floor(req, al);
   }
   return w ? s / w : 0;
 }
 
 // BeforePreFilter restore + Reservation Filter + nomination for one (pod, node); r is the base row.
-template <int NSC, bool FRESH>
-__device__ __forceinline__ RsvOut rsv_eval(const DevRsv& rv, const PodRec& p, const NodeReg<NSC>& r, int64_t node,
-                                        RsvDelta<NSC>& dl) {
+// RsvOut.nom is the view index of the nominated reservation.
+template <int NSC, typename V>
+__device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const NodeReg<NSC>& r, RsvDelta<NSC>& dl) {
   constexpr int D = 3 + NSC;
   const int32_t cls = p.rsv_class;
-  const int64_t b = gld(rv.beg + node), e = gld(rv.beg + node + 1);
+  const int64_t cnt = v.n();
   int64_t dpre[D], ral[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) dl.dreq[d] = dpre[d] = ral[d] = 0;
   dl.dnz[0] = dl.dnz[1] = 0;
   int32_t nm = 0, hiord = 0;
-  for (int64_t i = b; i < e; ++i) {
+  for (int64_t i = 0; i < cnt; ++i) {
     uint32_t meta;
     int32_t a;
-    if (!rsv_matches<FRESH>(rv, i, cls, meta, a)) continue;
+    if (!rsv_matches(v, i, cls, meta, a)) continue;
     ++nm;
-    hiord = max(hiord, gld(rv.ohi + i));
+    hiord = max(hiord, v.ohi(i));
     int64_t rem[kRsvDims];
     bool nzr = false;
 #pragma unroll
     for (int d = 0; d < kRsvDims; ++d) {
-      const int64_t v = gld(rv.alloc + d * rv.nr + i) - rld<FRESH>(rv.allocd + d * rv.nr + i);
-      rem[d] = v > 0 ? v : 0;  // quotav1.SubtractWithNonNegativeResult
+      const int64_t x = v.alloc(d, i) - v.allocd(d, i);
+      rem[d] = x > 0 ? x : 0;  // quotav1.SubtractWithNonNegativeResult
       nzr |= rem[d] != 0;
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const int64_t al = gld(rv.alloc + d * rv.nr + i);
+      const int64_t al = v.alloc(d, i);
       const int64_t kept = nzr ? rem[d] : 0;
       dl.dreq[d] -= a > 0 ? kept : al;  // matched: reserve pod removed; base had it replaced by `kept`
       dpre[d] += a > 0 ? al - kept : 0; // podRequested: this one is not in the pod's unmatched set
-      ral[d] += rld<FRESH>(rv.allocd + d * rv.nr + i);
+      ral[d] += v.allocd(d, i);
     }
     const uint32_t keys = rsv_keys(meta);
     const int64_t nzc = nzr ? ((keys & 1u) ? rem[0] : kDefaultMilliCPU) : 0;
     const int64_t nzm = nzr ? ((keys & 2u) ? rem[1] : kDefaultMemory) : 0;
-    dl.dnz[0] -= a > 0 ? nzc : gld(rv.rnz + i);
-    dl.dnz[1] -= a > 0 ? nzm : gld(rv.rnz + rv.nr + i);
+    dl.dnz[0] -= a > 0 ? nzc : v.rnz(0, i);
+    dl.dnz[1] -= a > 0 ? nzm : v.rnz(1, i);
   }
   dl.nm = nm;
   RsvOut o{0u, 0, 0, hiord, -1};
@@ -172,10 +219,10 @@ __device__ __forceinline__ RsvOut rsv_eval(const DevRsv& rv, const PodRec& p, co
 #pragma unroll
   for (int k = 0; k < NSC; ++k) slack[3 + k] = r.free_sc[k] - dpre[3 + k] + ral[3 + k];
   int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0;
-  for (int64_t i = b; i < e; ++i) {
+  for (int64_t i = 0; i < cnt; ++i) {
     uint32_t meta;
     int32_t a;
-    if (!rsv_matches<FRESH>(rv, i, cls, meta, a)) continue;
+    if (!rsv_matches(v, i, cls, meta, a)) continue;
     // filterWithReservations body for one reservation (plugin.go:386-422)
     const uint32_t names = rsv_keys(meta) & p.rsv_keys;
     bool ok = names != 0 && !pods_bad;
@@ -184,7 +231,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const DevRsv& rv, const PodRec& p, co
       for (int d = 0; d < D; ++d) {
         const int64_t pd = pod_dim(p, d);
         if (d >= 3 && pd == 0) continue;  // podRequest.ScalarResources keys
-        const int64_t rrem = gld(rv.alloc + d * rv.nr + i) - rld<FRESH>(rv.allocd + d * rv.nr + i);
+        const int64_t rrem = v.alloc(d, i) - v.allocd(d, i);
         ok = ok && !(pd > slack[d] + rrem);
       }
     }
@@ -193,7 +240,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const DevRsv& rv, const PodRec& p, co
 #pragma unroll
       for (int d = 0; d < kRsvDims; ++d) {
         if (!((names >> d) & 1u)) continue;
-        int64_t rem = gld(rv.alloc + d * rv.nr + i) - rld<FRESH>(rv.allocd + d * rv.nr + i);
+        int64_t rem = v.alloc(d, i) - v.allocd(d, i);
         rem = rem > 0 ? rem : 0;
         ok = ok && !(pod_dim(p, d) > rem);
       }
@@ -202,8 +249,8 @@ __device__ __forceinline__ RsvOut rsv_eval(const DevRsv& rv, const PodRec& p, co
     }
     if (!ok) continue;
     // NominateReservation: lowest order label first (strict, table order), else best score
-    const int32_t oh = gld(rv.ohi + i);
-    const int32_t sc = rsv_score<FRESH>(rv, p, i);
+    const int32_t oh = v.ohi(i);
+    const int32_t sc = rsv_score(v, p, i);
     if (oh > best_o) {
       best_o = oh;
       nom_o = (int32_t)i;
@@ -235,27 +282,36 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
   }
   term_take(r.t_cpu, sign * dl.dnz[0], sign * dl.dnz[0] * 100);
   term_take(r.t_mem, sign * dl.dnz[1], sign * dl.dnz[1] * 100);
+  term_take(r.t_ncpu, sign * dl.dreq[0], sign * dl.dreq[0] * 100);
+  term_take(r.t_nmem, sign * dl.dreq[1], sign * dl.dreq[1] * 100);
   r.pod_count -= (int32_t)sign * dl.nm;
   r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
 }
 
 // Filter + Score of one (pod, node) with the Reservation plugin: total = hi * F + Fit/LA total.
 // r must be the base row; with UNDO it is returned unchanged (the sweep reuses it across pods).
-template <int NSC, bool DEBUG, bool FRESH, bool UNDO, bool RSV = true>
-__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const DevRsv* rvp, const PodRec& p, NodeReg<NSC>& r,
-                                             int64_t node, RsvOut* info = nullptr) {
+// rsv(dl) runs rsv_eval on the node's reservation view; it is called only when the pod's class
+// matches one of them.
+// FEAT: bit 0 Reservation, bit 1 NodeNUMAResource compiled in (the Cfg flags switch them at run time).
+template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F>
+__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv,
+                                             RsvOut* info = nullptr) {
+  constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0;
   if (!RSV || !c.rsv || (p.rsv_class < 0 && !(p.flags & KS_POD_RSV_AFFINITY))) {
     if (info) *info = RsvOut{0u, 0, 0, 0, -1};
-    return eval_pod_node<NSC, DEBUG>(c, p, r);
+    EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
+    if (NUMA && c.numa) numa_eval<NSC, DEBUG>(c, p, r, o);
+    return o;
   }
   const bool slow = p.rsv_class >= 0 && p.rsv_class < 64 && ((r.rsv_cls >> p.rsv_class) & 1ull);
   RsvDelta<NSC> dl;
   RsvOut ro{(p.flags & KS_POD_RSV_AFFINITY) ? KS_R_RSV_AFFINITY : 0u, 0, 0, 0, -1};
   if (slow) {
-    ro = rsv_eval<NSC, FRESH>(*rvp, p, r, node, dl);
+    ro = rsv(dl);
     rsv_apply<NSC>(r, dl, 1);
   }
   EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
+  if (NUMA && c.numa) numa_eval<NSC, DEBUG>(c, p, r, o);
   if (UNDO && slow) rsv_apply<NSC>(r, dl, -1);
   // a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
   // NodeNames, plugin.go:235-246) before any Filter plugin runs
@@ -267,8 +323,9 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const DevRsv* rvp, co
   return o;
 }
 
-// Reserve into reservation i (plugin.go:532-570 -> reservation_info.go:379-388): the change of the
-// node's base restore (unmatched remainder of i before / after) for each Requested / NonZero dim.
+// Reserve into reservation i of the view (plugin.go:532-570 -> reservation_info.go:379-388): the
+// change of the node's base restore (unmatched remainder of i before / after) for each Requested /
+// NonZero dim, and the Allocated increment.
 struct RsvReserve {
   int64_t dreq[kRsvDims];
   int64_t dnz[2];
@@ -276,19 +333,19 @@ struct RsvReserve {
   bool now_ineligible;    // AllocateOnce: skipped from now on (transformer.go:109)
 };
 
-template <bool FRESH>
-__device__ __forceinline__ RsvReserve rsv_reserve_delta(const DevRsv& rv, const PodRec& p, int64_t i) {
+template <typename V>
+__device__ __forceinline__ RsvReserve rsv_reserve_delta(const V& v, const PodRec& p, int64_t i) {
   RsvReserve o;
-  const uint32_t meta = gld(rv.meta + i);
+  const uint32_t meta = v.meta(i);
   const uint32_t keys = rsv_keys(meta);
-  const int32_t a_old = rld<FRESH>(rv.assigned + i);
+  const int32_t a_old = v.assigned(i);
   const bool ao = (meta & KS_RSV_ALLOCATE_ONCE) != 0;
   int64_t al[kRsvDims], ro[kRsvDims], rn[kRsvDims];
   bool nz_old = false, nz_new = false;
 #pragma unroll
   for (int d = 0; d < kRsvDims; ++d) {
-    al[d] = gld(rv.alloc + d * rv.nr + i);
-    const int64_t ad = rld<FRESH>(rv.allocd + d * rv.nr + i);
+    al[d] = v.alloc(d, i);
+    const int64_t ad = v.allocd(d, i);
     o.add[d] = ((keys >> d) & 1u) ? pod_dim(p, d) : 0;
     const int64_t vo = al[d] - ad, vn = al[d] - (ad + o.add[d]);
     ro[d] = vo > 0 ? vo : 0;
@@ -303,7 +360,7 @@ __device__ __forceinline__ RsvReserve rsv_reserve_delta(const DevRsv& rv, const 
     const int64_t u_new = !ao ? (nz_new ? rn[d] : 0) - al[d] : 0;
     o.dreq[d] = u_new - u_old;
   }
-  const int64_t rnzc = gld(rv.rnz + i), rnzm = gld(rv.rnz + rv.nr + i);
+  const int64_t rnzc = v.rnz(0, i), rnzm = v.rnz(1, i);
   const int64_t oc = nz_old ? ((keys & 1u) ? ro[0] : kDefaultMilliCPU) : 0;
   const int64_t om = nz_old ? ((keys & 2u) ? ro[1] : kDefaultMemory) : 0;
   const int64_t nc = nz_new ? ((keys & 1u) ? rn[0] : kDefaultMilliCPU) : 0;
@@ -315,15 +372,14 @@ __device__ __forceinline__ RsvReserve rsv_reserve_delta(const DevRsv& rv, const 
 }
 
 // union of owner classes of the node's matchable reservations
-template <bool FRESH>
-__device__ __forceinline__ uint64_t rsv_node_classes(const DevRsv& rv, int64_t node) {
-  const int64_t b = gld(rv.beg + node), e = gld(rv.beg + node + 1);
+template <typename V>
+__device__ __forceinline__ uint64_t rsv_node_classes(const V& v) {
   uint64_t m = 0;
-  for (int64_t i = b; i < e; ++i) {
-    const uint32_t meta = gld(rv.meta + i);
-    const int32_t a = rld<FRESH>(rv.assigned + i);
+  for (int64_t i = 0; i < v.n(); ++i) {
+    const uint32_t meta = v.meta(i);
+    const int32_t a = v.assigned(i);
     if (((meta & KS_RSV_ALLOCATE_ONCE) && a > 0) || (meta & KS_RSV_UNSCHEDULABLE)) continue;
-    m |= gld(rv.cls + i);
+    m |= v.cls(i);
   }
   return m;
 }

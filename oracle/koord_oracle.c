@@ -26,6 +26,10 @@
  *                            scoring.go:103-131, scoreReservation :183-203, findMostPreferredReservationByOrder
  *                            :162-181, DefaultNormalizeScore frameworkext/normalize_score.go:24-52, Reserve
  *                            plugin.go:532-570 -> reservation_info.go:379-388
+ *   NodeNUMAResource         PreFilter nodenumaresource/plugin.go:219-269 (skip / cpu-bind), Filter :275-338,
+ *                            filterAmplifiedCPUs :340-373, Score scoring.go:55-114 (scoreWithAmplifiedCPUs),
+ *                            resourceAllocationScorer :187-242, Amplify apis/extension/node_resource_amplification.go:170-175
+ *                            (topology policy None and non-cpuset pods only)
  *   Sweep driver             upstream schedule_one.go (schedulePod, findNodesThatPassFilters,
  *                            prioritizeNodes, selectHost) with percentageOfNodesToScore=100 and
  *                            lowest-index tie-break; Parallelizer pkg/util/parallelize/parallelism.go:29-49
@@ -102,6 +106,9 @@ typedef struct {
   int64_t *la_term_cpu, *la_term_mem, *la_pterm_cpu, *la_pterm_mem;
   int32_t *la_thr_cpu, *la_thr_mem, *la_pthr_cpu, *la_pthr_mem;
   int64_t *la_total_cpu, *la_total_mem, *la_usage_cpu, *la_usage_mem, *la_pusage_cpu, *la_pusage_mem;
+  double *numa_ratio;
+  int32_t *numa_cpus;
+  uint32_t *numa_flags;
 } ko_nodes;
 
 typedef struct {
@@ -152,6 +159,7 @@ typedef struct {
   uint32_t qmask;
   int64_t qreq[KS_QUOTA_DIMS];
   int32_t rcls;  /* reservation match class, -1 = none */
+  int reqzero;   /* quotav1.IsZero(PodRequestsAndLimits) (NodeNUMAResource PreFilter skip) */
   uint32_t keys; /* bit d: request dimension d is a key of the pod's requests (value != 0) */
 } ko_pod;
 
@@ -186,6 +194,7 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
   for (int k = 0; k < KS_MAX_SCALARS; k++) v[3 + k] = p->sc[k];
   for (int d = 0; d < KO_D; d++)
     if (v[d] != 0) p->keys |= 1u << d;
+  p->reqzero = p->keys == 0;
 }
 
 static int64_t pod_dim(const ko_pod *p, int d) { return d == 0 ? p->cpu : d == 1 ? p->mem : d == 2 ? p->eph : p->sc[d - 3]; }
@@ -256,10 +265,63 @@ static uint32_t la_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
   return 0;
 }
 
+/* extension.Amplify: int64(math.Ceil(float64(origin) * float64(ratio))) for ratio > 1 */
+static int64_t amplify(int64_t origin, double ratio) {
+  if (ratio <= 1) return origin;
+  return (int64_t)ceil((double)origin * ratio);
+}
+
+/* NodeNUMAResource Filter for a pod without cpu bind on a topology-policy-None node:
+ * filterAmplifiedCPUs (plugin.go:340-373) on the (restored) NodeInfo */
+static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+  const ko_nodes *d = &s->nd;
+  if (p->reqzero) return 0; /* PreFilter skip */
+  if (p->cpu == 0) return 0;
+  if (d->numa_flags[n] & KS_NUMA_INVALID_RATIO) return KS_R_NUMA_INVALID_RATIO;
+  double ratio = d->numa_ratio[n];
+  if (ratio <= 1) return 0;
+  int64_t allocated = (int64_t)d->numa_cpus[n] * 1000;
+  int64_t requested = e->req[0];
+  if (requested >= allocated && allocated > 0) {
+    requested -= allocated;
+    requested += amplify(allocated, ratio);
+  }
+  if (p->cpu > d->alloc_cpu[n] - requested) return KS_R_NUMA_AMPLIFIED_CPU;
+  return 0;
+}
+
+/* scoreWithAmplifiedCPUs (scoring.go:98-114) -> resourceAllocationScorer.score (:206-221) */
+static int64_t numa_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+  const ko_nodes *d = &s->nd;
+  const ks_numa_args *a = &s->cfg.numa;
+  if (p->reqzero) return 0;
+  int64_t req_cpu = e->req[0];
+  double ratio = d->numa_ratio[n];
+  if (p->cpu != 0 && ratio > 1) {
+    int64_t allocated = (int64_t)d->numa_cpus[n] * 1000;
+    req_cpu = req_cpu - allocated + amplify(allocated, ratio);
+  }
+  int most = a->strategy == KS_MOST_ALLOCATED;
+  int64_t node_score = 0, weight_sum = 0;
+  if (a->weight_cpu && d->alloc_cpu[n] != 0) {
+    int64_t rq = req_cpu + p->cpu, cap = d->alloc_cpu[n];
+    node_score += (most ? ko_most_requested_score(rq, cap) : ko_least_requested_score(rq, cap)) * a->weight_cpu;
+    weight_sum += a->weight_cpu;
+  }
+  if (a->weight_memory && d->alloc_mem[n] != 0) {
+    int64_t rq = e->req[1] + p->mem, cap = d->alloc_mem[n];
+    node_score += (most ? ko_most_requested_score(rq, cap) : ko_least_requested_score(rq, cap)) * a->weight_memory;
+    weight_sum += a->weight_memory;
+  }
+  if (weight_sum == 0) return 0;
+  return node_score / weight_sum;
+}
+
 static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   uint32_t r = 0;
   if (s->cfg.fit.enable_filter) r |= fit_filter(s, p, n, e);
   if (s->cfg.loadaware.enable_filter) r |= la_filter(s, p, n);
+  if (s->cfg.numa.enable) r |= numa_filter(s, p, n, e);
   return r;
 }
 
@@ -318,8 +380,13 @@ static int64_t la_score(const ko_sched *s, const ko_pod *p, int64_t n) {
 }
 
 static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *fit_out,
-                           int64_t *la_out) {
-  int64_t t = 0, fs = 0, ls = 0;
+                           int64_t *la_out, int64_t *numa_out) {
+  int64_t t = 0, fs = 0, ls = 0, ns = 0;
+  if (s->cfg.numa.enable) {
+    ns = numa_score(s, p, n, e);
+    t += ns * s->cfg.numa.plugin_weight;
+  }
+  if (numa_out) *numa_out = ns;
   if (s->cfg.fit.enable_score) {
     fs = fit_score(s, p, n, e);
     t += fs * s->cfg.fit.plugin_weight;
@@ -704,7 +771,7 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   s->cfg = *cfg;
   s->n = n;
   size_t nn = (size_t)(n > 0 ? n : 1);
-  s->blob = calloc(nn, NCOL64 * 8 + 8 * 4 + 4);
+  s->blob = calloc(nn, NCOL64 * 8 + 8 * 4 + 4 + 4 + 4);
   char *b = (char *)s->blob;
 #define TAKE64(f) (s->nd.f = (int64_t *)b, b += nn * 8)
 #define TAKE32(f) (s->nd.f = (int32_t *)b, b += nn * 4)
@@ -720,6 +787,10 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   TAKE32(la_thr_cpu); TAKE32(la_thr_mem); TAKE32(la_pthr_cpu); TAKE32(la_pthr_mem);
   s->nd.la_flags = (uint32_t *)b;
   b += nn * 4;
+  s->nd.numa_flags = (uint32_t *)b;
+  b += nn * 4;
+  TAKE32(numa_cpus);
+  s->nd.numa_ratio = (double *)calloc(nn, 8);
 #undef TAKE64
 #undef TAKE32
 #define CP64(dst, src) do { if (src) memcpy(s->nd.dst, src, (size_t)n * 8); } while (0)
@@ -739,6 +810,9 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   CP64(la_total_cpu, nc->la_total_milli_cpu); CP64(la_total_mem, nc->la_total_milli_memory);
   CP64(la_usage_cpu, nc->la_usage_milli_cpu); CP64(la_usage_mem, nc->la_usage_milli_memory);
   CP64(la_pusage_cpu, nc->la_prod_usage_milli_cpu); CP64(la_pusage_mem, nc->la_prod_usage_milli_memory);
+  CP32(numa_cpus, nc->numa_cpuset_cpus);
+  CP32(numa_flags, (const int32_t *)nc->numa_flags);
+  if (nc->numa_cpu_amplification) memcpy(s->nd.numa_ratio, nc->numa_cpu_amplification, (size_t)n * 8);
 #undef CP64
 #undef CP32
   s->feasible = (uint8_t *)calloc(nn, 1);
@@ -756,6 +830,7 @@ void ko_destroy(ko_sched *s) {
   if (!s) return;
   pool_destroy(s->pool);
   free(s->blob);
+  free(s->nd.numa_ratio);
   free(s->q);
   free(s->feasible);
   free(s->total);
@@ -849,7 +924,8 @@ typedef struct {
 
 /* BeforePreFilter restore + Filter for one node; the Reservation PreScore per-node part
  * (nomination, node order) for feasible ones.  Returns the KS_R_* bits. */
-static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_out, int64_t *la_out) {
+static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_out, int64_t *la_out,
+                          int64_t *numa_out) {
   ko_rstate st;
   rsv_restore(s, p, n, &st);
   uint32_t r = rsv_filter(s, p, n, &st);
@@ -863,7 +939,7 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_
     s->total[n] = -1;
     return r;
   }
-  s->total[n] = total_score(s, p, n, &st.e, fit_out, la_out);
+  s->total[n] = total_score(s, p, n, &st.e, fit_out, la_out, numa_out);
   if (s->cfg.reservation.enable) {
     int32_t nom = rsv_nominate(s, p, n, &st, &s->rord[n]);
     s->nom[n] = nom;
@@ -874,7 +950,7 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_
 
 static void filter_piece(void *v, int64_t lo, int64_t hi) {
   sweep_arg *a = (sweep_arg *)v;
-  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = eval_node(a->s, a->p, n, NULL, NULL) == 0;
+  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = eval_node(a->s, a->p, n, NULL, NULL, NULL) == 0;
 }
 
 /* Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and
@@ -947,13 +1023,14 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
   ko_pod p;
   load_pod(s, pc, 0, &p);
   for (int64_t n = 0; n < s->n; n++) {
-    int64_t fs = 0, ls = 0;
-    uint32_t r = eval_node(s, &p, n, &fs, &ls);
+    int64_t fs = 0, ls = 0, ns = 0;
+    uint32_t r = eval_node(s, &p, n, &fs, &ls, &ns);
     if (reasons) reasons[n] = r;
     if (scores) {
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = r ? 0 : fs;
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = r ? 0 : ls;
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
+      scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = r ? 0 : ns;
     }
   }
   int64_t *norm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
