@@ -55,6 +55,7 @@ extern "C" {
 #define KS_SHARD_ID_BYTES 128 /* opaque RCCL unique id (ks_shard_unique_id) */
 #define KS_RSV_DIMS (3 + KS_MAX_SCALARS) /* reservation resources: cpu, memory, ephemeral-storage, scalar[k] */
 #define KS_RSV_CLASSES 64 /* pod match classes (ks_reservation_cols.owner_classes bits) */
+#define KS_MAX_GPUS 8     /* GPU minors per node (ks_device_cols); minor = slot index */
 
 /* ---- status codes ---- */
 #define KS_OK 0
@@ -88,6 +89,9 @@ extern "C" {
 #define KS_POD_RSV_AFFINITY 0x10u    /* GetRequiredReservationAffinity != nil (reservation/transformer.go:51, stateData.hasAffinity) */
 #define KS_POD_CPU_BIND 0x20u        /* NodeNUMAResource preFilterState.requestCPUBind (nodenumaresource/plugin.go:236-262):
                                         cpuset allocation is not supported by this build (KS_EUNSUPPORTED) */
+#define KS_POD_GPU_CORE 0x40u        /* DeviceShare: the converted GPU request has a gpu-core key (deviceshare/utils.go:96-146) */
+#define KS_POD_GPU_MEMORY 0x80u      /* DeviceShare: gpu-memory given (ratio derived per node, devicehandler_gpu.go:71-89);
+                                        otherwise gpu-memory-ratio given (memory derived) */
 
 /* ---- per-node NodeNUMAResource flags (ks_node_cols.numa_flags) ---- */
 #define KS_NUMA_INVALID_RATIO 0x1u   /* GetNodeResourceAmplificationRatio returned an error (plugin.go:348-351)   */
@@ -108,6 +112,8 @@ extern "C" {
 #define KS_R_RSV_NO_FIT 0x400u    /* filterWithReservations: no matched reservation satisfies the pod (plugin.go:425-437) */
 #define KS_R_NUMA_AMPLIFIED_CPU 0x800u  /* ErrInsufficientAmplifiedCPU (nodenumaresource/plugin.go:369-371)       */
 #define KS_R_NUMA_INVALID_RATIO 0x1000u /* ErrInvalidCPUAmplificationRatio (plugin.go:348-351)                    */
+#define KS_R_DEV_INSUFFICIENT 0x2000u   /* DeviceShare "Insufficient gpu devices" (device_allocator.go:453-456)  */
+#define KS_R_DEV_NO_GPU 0x4000u         /* DeviceShare: node has no (healthy) GPU (devicehandler_gpu.go:41-50)  */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -121,7 +127,11 @@ extern "C" {
 #define KS_SCORE_LOADAWARE 1
 #define KS_SCORE_RESERVATION 2 /* after DefaultNormalizeScore (reservation/scoring.go:126-131) */
 #define KS_SCORE_NUMA 3        /* NodeNUMAResource scoreWithAmplifiedCPUs (nodenumaresource/scoring.go:98-114) */
-#define KS_NUM_SCORE_PLUGINS 4
+#define KS_SCORE_DEVICESHARE 4 /* after DefaultNormalizeScore (deviceshare/scoring.go:95-97) */
+#define KS_NUM_SCORE_PLUGINS 5
+
+/* ---- per-node DeviceShare flags (ks_device_cols.flags) ---- */
+#define KS_DEV_PRESENT 0x1u /* nodeDeviceCache.getNodeDevice != nil (deviceshare/plugin.go:286-289) */
 
 /* ---- reservation flags (ks_reservation_cols.flags) ---- */
 #define KS_RSV_UNSCHEDULABLE 0x1u /* ReservationInfo.IsUnschedulable (transformer.go:113)              */
@@ -189,6 +199,18 @@ typedef struct ks_numa_args {
   int64_t plugin_weight;
 } ks_numa_args;
 
+/* DeviceShareArgs.ScoringStrategy (defaults v1beta2/defaults.go:187-207: LeastAllocated,
+ * gpu-memory-ratio 1 (rdma / fpga weights do not apply to GPUs)).  GPU devices only: no
+ * allocate hints, joint allocation, NUMA affinity, VFs or device-holding reservations. */
+typedef struct ks_deviceshare_args {
+  int32_t enable;
+  int32_t strategy; /* KS_LEAST_ALLOCATED | KS_MOST_ALLOCATED */
+  int64_t weight_gpu_core;
+  int64_t weight_gpu_memory;
+  int64_t weight_gpu_memory_ratio;
+  int64_t plugin_weight;
+} ks_deviceshare_args;
+
 typedef struct ks_config {
   int32_t abi_version; /* = KS_ABI_VERSION */
   int32_t device;      /* HIP device ordinal */
@@ -201,6 +223,7 @@ typedef struct ks_config {
   int32_t _pad1;
   ks_reservation_args reservation;
   ks_numa_args numa;
+  ks_deviceshare_args deviceshare;
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -271,6 +294,11 @@ typedef struct ks_pod_cols {
    * reservation share a class (matchReservation, transformer.go:349-373); reserve pods
    * themselves are not scheduled through this entry point. */
   const int32_t *rsv_class;
+  /* DeviceShare: the pod's converted GPU request (GetPodDeviceRequests, utils.go:232-252; nvidia.com/gpu
+   * and koordinator.sh/gpu converted to core + ratio by the host); NULL = no GPU request */
+  const int64_t *gpu_core;
+  const int64_t *gpu_memory;
+  const int64_t *gpu_memory_ratio;
 } ks_pod_cols;
 
 /* ElasticQuota table: QuotaInfo.CalculateInfo per quota (core/quota_info.go). */
@@ -318,12 +346,25 @@ typedef struct ks_reservation_cols {
   const int64_t *reserve_nonzero_memory;
 } ks_reservation_cols;
 
+/* Node GPU devices (nodeDeviceCache, deviceshare/device_cache.go): per minor k the device total and
+ * the used amount (deviceTotal / deviceUsed) of gpu-core, gpu-memory, gpu-memory-ratio.  A minor
+ * whose totals are all zero is absent / unhealthy. */
+typedef struct ks_device_cols {
+  const uint32_t *flags; /* KS_DEV_* */
+  const int64_t *total_core[KS_MAX_GPUS];
+  const int64_t *total_memory[KS_MAX_GPUS];
+  const int64_t *total_ratio[KS_MAX_GPUS];
+  const int64_t *used_core[KS_MAX_GPUS];   /* NULL = 0 */
+  const int64_t *used_memory[KS_MAX_GPUS];
+  const int64_t *used_ratio[KS_MAX_GPUS];
+} ks_device_cols;
+
 typedef struct ks_result {
   int32_t node;    /* chosen node index, -1 if not scheduled */
   uint32_t status; /* KS_S_* */
   int64_t score;   /* total weighted score of the chosen node */
   int32_t reservation; /* reservation row the pod was assumed into (Reserve, plugin.go:532-570), -1 = none */
-  int32_t _pad0;
+  uint32_t gpu_minors; /* DeviceShare Reserve: bit k = GPU minor k allocated (plugin.go:377-430) */
 } ks_result;
 
 /* Mutable node state after commits (read back for parity). */
@@ -367,6 +408,12 @@ int ks_load_nodes(ks_ctx *ctx, const ks_node_cols *nodes, int64_t n);
 /* Informer deltas: rows[i] replaces node idx[i]; arrays in `rows` have length m. */
 int ks_update_nodes(ks_ctx *ctx, const int32_t *idx, const ks_node_cols *rows, int64_t m);
 int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
+
+/* GPU devices of the loaded nodes (deviceshare nodeDeviceCache, device_cache.go:44-160); call after
+ * ks_load_nodes.  Reserve (plugin.go:377-430 -> updateCacheUsed) adds each allocation to used. */
+int ks_load_devices(ks_ctx *ctx, const ks_device_cols *dev, int64_t n);
+/* used amounts after commits, [k*n + node] for minor k; NULL = skip */
+int ks_read_devices(ks_ctx *ctx, int64_t *used_core, int64_t *used_memory, int64_t *used_ratio);
 
 /* Reservation cache snapshot (reservation/cache.go:104-291) for the Reservation plugin's
  * BeforePreFilter restore (transformer.go:41-307), Filter (plugin.go:311-496), PreScore

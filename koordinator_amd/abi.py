@@ -11,6 +11,7 @@ import ctypes as C
 KS_ABI_VERSION = 2
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
+KS_MAX_GPUS = 8
 KS_RSV_DIMS = 3 + KS_MAX_SCALARS
 KS_RSV_CLASSES = 64
 
@@ -39,6 +40,9 @@ KS_POD_NONPREEMPTIBLE = 0x04
 KS_POD_SCALAR_KEYS = 0x08
 KS_POD_RSV_AFFINITY = 0x10
 KS_POD_CPU_BIND = 0x20
+KS_POD_GPU_CORE = 0x40
+KS_POD_GPU_MEMORY = 0x80
+KS_DEV_PRESENT = 0x1
 
 KS_NUMA_INVALID_RATIO = 0x1
 KS_NUMA_CPU_BIND_POLICY = 0x2
@@ -57,6 +61,8 @@ KS_R_RSV_AFFINITY = 0x200
 KS_R_RSV_NO_FIT = 0x400
 KS_R_NUMA_AMPLIFIED_CPU = 0x800
 KS_R_NUMA_INVALID_RATIO = 0x1000
+KS_R_DEV_INSUFFICIENT = 0x2000
+KS_R_DEV_NO_GPU = 0x4000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -68,7 +74,8 @@ KS_SCORE_FIT = 0
 KS_SCORE_LOADAWARE = 1
 KS_SCORE_RESERVATION = 2
 KS_SCORE_NUMA = 3
-KS_NUM_SCORE_PLUGINS = 4
+KS_SCORE_DEVICESHARE = 4
+KS_NUM_SCORE_PLUGINS = 5
 
 KS_RSV_UNSCHEDULABLE = 0x1
 KS_RSV_ALLOCATE_ONCE = 0x2
@@ -122,6 +129,11 @@ class KsNumaArgs(C.Structure):
                 ("weight_memory", C.c_int64), ("plugin_weight", C.c_int64)]
 
 
+class KsDeviceShareArgs(C.Structure):
+    _fields_ = [("enable", C.c_int32), ("strategy", C.c_int32), ("weight_gpu_core", C.c_int64),
+                ("weight_gpu_memory", C.c_int64), ("weight_gpu_memory_ratio", C.c_int64), ("plugin_weight", C.c_int64)]
+
+
 class KsConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -135,6 +147,7 @@ class KsConfig(C.Structure):
         ("_pad1", C.c_int32),
         ("reservation", KsReservationArgs),
         ("numa", KsNumaArgs),
+        ("deviceshare", KsDeviceShareArgs),
     ]
 
 
@@ -196,6 +209,9 @@ POD_COLS = [
     ("quota_mask", PU32),
     ("quota_req", P64 * KS_QUOTA_DIMS),
     ("rsv_class", P32),
+    ("gpu_core", P64),
+    ("gpu_memory", P64),
+    ("gpu_memory_ratio", P64),
 ]
 
 
@@ -248,12 +264,25 @@ class KsReservationCols(C.Structure):
     ]
 
 
+class KsDeviceCols(C.Structure):
+    _fields_ = [
+        ("flags", PU32),
+        ("total_core", P64 * KS_MAX_GPUS),
+        ("total_memory", P64 * KS_MAX_GPUS),
+        ("total_ratio", P64 * KS_MAX_GPUS),
+        ("used_core", P64 * KS_MAX_GPUS),
+        ("used_memory", P64 * KS_MAX_GPUS),
+        ("used_ratio", P64 * KS_MAX_GPUS),
+    ]
+
+
 class KsResult(C.Structure):
     _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64), ("reservation", C.c_int32),
-                ("_pad0", C.c_int32)]
+                ("gpu_minors", C.c_uint32)]
 
 
-RESULT_DTYPE_FIELDS = [("node", "<i4"), ("status", "<u4"), ("score", "<i8"), ("reservation", "<i4"), ("_pad0", "<i4")]
+RESULT_DTYPE_FIELDS = [("node", "<i4"), ("status", "<u4"), ("score", "<i8"), ("reservation", "<i4"),
+                       ("gpu_minors", "<u4")]
 
 
 NODE_STATE_COLS = [
@@ -299,6 +328,8 @@ EXPORTED_SYMBOLS = [
     "ks_load_nodes",
     "ks_update_nodes",
     "ks_load_quotas",
+    "ks_load_devices",
+    "ks_read_devices",
     "ks_load_reservations",
     "ks_read_reservations",
     "ks_refresh_quota_runtime",

@@ -34,6 +34,7 @@ POD_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral",
     "nonzero_milli_cpu", "nonzero_memory",
     "la_req_cpu", "la_lim_cpu", "la_dflt_cpu", "la_req_memory", "la_lim_memory", "la_dflt_memory",
+    "gpu_core", "gpu_memory", "gpu_memory_ratio",
 ]
 POD_I32 = ["quota", "rsv_class"]
 POD_U32 = ["flags", "quota_mask"]
@@ -259,6 +260,37 @@ class QuotaTree:
                 field[d] = _p64(arr[d])
         for d in range(abi.KS_QUOTA_DIMS):
             c.cluster_total[d] = int(self.cluster_total[d])
+        c._keep = self
+        return c
+
+
+class DeviceTable:
+    """GPU devices per node (ks_device_cols): [minor][node] arrays of total / used gpu-core,
+    gpu-memory, gpu-memory-ratio (deviceshare nodeDeviceCache deviceTotal / deviceUsed)."""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+        G = abi.KS_MAX_GPUS
+        self.flags = np.zeros(self.n, np.uint32)
+        for name in ("total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio"):
+            setattr(self, name, np.zeros((G, self.n), np.int64))
+
+    def copy(self) -> "DeviceTable":
+        t = DeviceTable(self.n)
+        for k in ("flags", "total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio"):
+            setattr(t, k, getattr(self, k).copy())
+        return t
+
+    def ks(self) -> abi.KsDeviceCols:
+        c = abi.KsDeviceCols()
+        self.flags = np.ascontiguousarray(self.flags, np.uint32)
+        c.flags = _pu32(self.flags)
+        for name in ("total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio"):
+            arr = np.ascontiguousarray(getattr(self, name), np.int64)
+            setattr(self, name, arr)
+            field = getattr(c, name)
+            for k in range(abi.KS_MAX_GPUS):
+                field[k] = _p64(arr[k])
         c._keep = self
         return c
 

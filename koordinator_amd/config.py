@@ -25,6 +25,9 @@ MEMORY = "memory"
 EPHEMERAL = "ephemeral-storage"
 BATCH_CPU = "kubernetes.io/batch-cpu"
 BATCH_MEMORY = "kubernetes.io/batch-memory"
+GPU_CORE = "koordinator.sh/gpu-core"
+GPU_MEMORY = "koordinator.sh/gpu-memory"
+GPU_MEMORY_RATIO = "koordinator.sh/gpu-memory-ratio"
 
 DEFAULT_NODE_METRIC_EXPIRATION_SECONDS = 180
 DEFAULT_RESOURCE_WEIGHTS = {CPU: 1, MEMORY: 1}
@@ -112,6 +115,14 @@ class NodeNUMAResourceArgs:
 
 
 @dataclass
+class DeviceShareArgs:
+    """DeviceShareArgs.ScoringStrategy after v1beta2 defaults (defaults.go:187-207): LeastAllocated,
+    gpu-memory-ratio weight 1."""
+    strategy: str = "LeastAllocated"
+    resources: Dict[str, int] = field(default_factory=lambda: {GPU_MEMORY_RATIO: 1})
+
+
+@dataclass
 class ElasticQuotaArgs:
     enable_runtime_quota: bool = True
     enable_check_parent_quota: bool = False
@@ -129,6 +140,8 @@ class SchedulerProfile:
     reservation_weight: Optional[int] = None  # Reservation plugin score weight (koord profile: 5000); None = off
     numa: Optional[NodeNUMAResourceArgs] = None
     numa_weight: int = 1
+    deviceshare: Optional[DeviceShareArgs] = None
+    deviceshare_weight: int = 1
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -190,6 +203,17 @@ class SchedulerProfile:
             c.numa.weight_cpu = self.numa.resources.get(CPU, 0)
             c.numa.weight_memory = self.numa.resources.get(MEMORY, 0)
             c.numa.plugin_weight = self.numa_weight
+        if self.deviceshare is not None:
+            d = self.deviceshare
+            c.deviceshare.enable = 1
+            c.deviceshare.strategy = abi.KS_MOST_ALLOCATED if d.strategy == "MostAllocated" else abi.KS_LEAST_ALLOCATED
+            for name in d.resources:
+                if name not in (GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, "koordinator.sh/rdma", "koordinator.sh/fpga"):
+                    raise ValidationError(f"DeviceShare weight on {name} is not supported")
+            c.deviceshare.weight_gpu_core = d.resources.get(GPU_CORE, 0)
+            c.deviceshare.weight_gpu_memory = d.resources.get(GPU_MEMORY, 0)
+            c.deviceshare.weight_gpu_memory_ratio = d.resources.get(GPU_MEMORY_RATIO, 0)
+            c.deviceshare.plugin_weight = self.deviceshare_weight
         if self.reservation_weight is not None:
             c.reservation.enable = 1
             c.reservation.plugin_weight = int(self.reservation_weight)

@@ -29,6 +29,7 @@
 
 #include "ks_device.h"
 #include "ks_rsv.h"
+#include "ks_dev.h"
 
 using namespace ks;
 
@@ -95,6 +96,7 @@ struct DevPodCols {
   int32_t *quota;
   int64_t *la_req_cpu, *la_lim_cpu, *la_dflt_cpu, *la_req_mem, *la_lim_mem, *la_dflt_mem;
   int32_t *rsv_class;
+  int64_t *gpu_core, *gpu_mem, *gpu_ratio;
 };
 
 // estimatedUsedByResource (estimator/default_estimator.go:73-108)
@@ -154,7 +156,10 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   r.h_mem = r.mem * 100;
   r.f_cpu = i64_to_f32(r.cpu);
   r.f_mem = i64_to_f32(r.mem);
-  r._pad2 = 0;
+  r.gpu_core = s.gpu_core[i];
+  r.gpu_mem = s.gpu_mem[i];
+  r.gpu_ratio = s.gpu_ratio[i];
+  if (r.gpu_core != 0 || r.gpu_mem != 0 || r.gpu_ratio != 0) r.flags |= kPodHasGpu;
   out[i] = r;
 }
 
@@ -165,6 +170,9 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
 struct SweepArgs {
   const DevNodes* __restrict__ dn;
   const DevRsv* __restrict__ rv;
+  const DevDev* __restrict__ dv;
+  unsigned long long* dev_M;  // [64] DeviceShare: (max raw << 32) | ~witness node per pod of the pass
+  int32_t phase;              // 0: reduce dev_M only (DeviceShare), 1: chunk keys
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
@@ -200,13 +208,23 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     for (int32_t p = p0; p < p1; ++p) {
       const PodRec pod = load_pod_uniform(a.pods + cursor + p);
       const EvalOut o = eval_full<NSC, false, true, FEAT>(
-          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); });
-      const uint32_t key = o.reasons ? 0u : (((uint32_t)(o.total + 1) << 6) | (uint32_t)(63 - lane));
+          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+          [&]() { return dev_eval<false>(a.c, pod, DevGView{*a.dv, node}); });
+      if ((FEAT & 4) && a.phase == 0) {
+        // DeviceShare normalization max over the feasible nodes, witness = lowest index holding it
+        const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | (0xFFFFFFFFull - (uint64_t)node));
+        const uint64_t m = wave_max_u64(mk);
+        if (lane == 0 && m) atomicMax(a.dev_M + p, (unsigned long long)m);
+        continue;
+      }
+      const int32_t M = (FEAT & 4) ? (int32_t)(a.dev_M[p] >> 32) : 0;
+      const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane));
       const uint32_t m1 = wave_max_u32(key);
       const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
       best = (lane == p) ? m1 : best;
       second = (lane == p) ? m2 : second;
     }
+    if ((FEAT & 4) && a.phase == 0) continue;
     if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
   }
 }
@@ -558,6 +576,8 @@ struct RowCol {
 struct CommitArgs {
   const DevNodes* __restrict__ dn;
   const DevRsv* __restrict__ rv;
+  const DevDev* __restrict__ dv;
+  const unsigned long long* __restrict__ dev_M;  // [64] DeviceShare normalization max + witness (sweep phase 0)
   Cfg c;
   const PodRec* __restrict__ pods;
   DevPodQuota pq;
@@ -575,6 +595,7 @@ struct CommitArgs {
   int32_t total_pods, batch, k;
   int32_t rcap;        // reservations cached in LDS per slot (0 = none)
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
+  int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
 };
 
 struct QuotaRowsLds {
@@ -585,12 +606,13 @@ struct QuotaRowsLds {
 };
 
 struct CommitLayout {
-  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, quota, touched, total;
+  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, quota, touched, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 
-__host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0) {
+__host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0,
+                                                      size_t dev_bytes = 0) {
   CommitLayout L;
   size_t o = 0;
   L.rows = o;
@@ -617,6 +639,8 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += (size_t)kMaxBatch * 8;  // per slot: reservations cached (-1 = on the HBM table), CSR begin
   L.srec = o;
   o += align16(rsv_bytes);     // per slot: the node's reservations (RsvRec, rcap each)
+  L.sdev = o;
+  o += align16(dev_bytes);     // per slot: GPU totals / used [3][kGpus] + present flag
   L.quota = o;
   if (qc) o += align16(sizeof(QuotaRowsLds));
   L.touched = o;
@@ -737,7 +761,7 @@ __device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const
 // covered by the slot evaluation.
 template <int NSC, int FEAT>
 __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const Cfg& cfg, const PodRec& pod,
-                                                     int64_t chunk, uint64_t touched_mask) {
+                                                     int64_t chunk, uint64_t touched_mask, int32_t M) {
   const int lane = threadIdx.x & 63;
   const int64_t node = chunk * 64 + lane;
   NodeReg<NSC> r;
@@ -746,9 +770,10 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
     load_node<NSC>(cfg, d, node, node < a.n, r);
   }
   const EvalOut o = eval_full<NSC, false, false, FEAT>(
-      cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); });
+      cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+      [&]() { return dev_eval<false>(cfg, pod, DevGView{*a.dv, node}); });
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
-  return wave_max_u64(skip ? 0ull : gkey(o.total, node));
+  return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
 }
 
 template <int NSC, bool QC, int FEAT>
@@ -756,7 +781,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   constexpr bool RSV = (FEAT & 1) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
-  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes);
+  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes);
   SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
   PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
   ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
@@ -773,6 +798,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   int32_t* srbeg = srcnt + kMaxBatch;
   constexpr int RD = 3 + NSC;
   RsvRec<RD>* srec = reinterpret_cast<RsvRec<RD>*>(smem_raw + lay.srec);
+  constexpr bool DEV = (FEAT & 4) != 0;
+  constexpr int DW = 3 * kGpus;  // int64 words of one slot's GPU totals (and of its used amounts)
+  int64_t* sdev_tot = reinterpret_cast<int64_t*>(smem_raw + lay.sdev);
+  int64_t* sdev_use = sdev_tot + kMaxBatch * DW;
+  int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kMaxBatch * DW);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -834,11 +864,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
   int32_t my_cnt = 0, my_quota = -1;
   uint32_t my_flags = 0, my_pmask = 0;
-  uint64_t my_bound = 0, my_top = 0;
+  uint64_t my_bound = 0, my_top = 0, my_devM = 0;
   if (tid < 64 && lane < np) {
     my_cnt = a.cand_count[lane];
     my_bound = a.cand_bound[lane];
     my_top = a.cand_top[lane];
+    if (DEV) my_devM = a.dev_M[lane];
     my_pmask = a.pq.mask[cursor0 + lane];
     my_quota = a.pods[cursor0 + lane].quota;
     my_flags = a.pods[cursor0 + lane].flags;
@@ -980,6 +1011,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     }
     {
     uint64_t best;
+    int32_t Muse = 0;  // DeviceShare normalization max used for this pod
     if (cj.fast) {
       best = cj.umax;  // the snapshot-best node is untouched: commits only lower keys, so it wins
       ++fast;
@@ -991,19 +1023,43 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       pod.rsv_class = __builtin_amdgcn_readfirstlane(pod.rsv_class);
       // ---- every touched node exactly (lane = slot), untouched from the candidates ----
       uint64_t key_mod = 0;
+      EvalOut o{};
+      bool feas = false;
       if (lane < nslots) {
         NodeReg<NSC> r;
         slot_to_reg<NSC>(rows[lane], r);
         r.rsv_cls = scls[lane];
         r.numa_A = snuma[2 * lane];
         r.numa_off = snuma[2 * lane + 1];
-        const EvalOut o = eval_full<NSC, false, false, FEAT>(cfg, pod, r, [&](RsvDelta<NSC>& dl) {
-          const int32_t c = srcnt[lane];
-          if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
-          return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
-        });
-        key_mod = o.reasons ? 0ull : gkey(o.total, snode);
+        o = eval_full<NSC, false, false, FEAT>(
+            cfg, pod, r,
+            [&](RsvDelta<NSC>& dl) {
+              const int32_t c = srcnt[lane];
+              if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
+              return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
+            },
+            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane * DW, sdev_use + lane * DW, sdev_pres[lane] != 0}); });
+        feas = o.reasons == 0;
       }
+      if (DEV && cfg.dev) {
+        // DeviceShare normalization: the untouched nodes' max is the sweep's M while its witness is
+        // untouched; the touched nodes are current.  If the pod's max changes, cut the pass here.
+        const uint64_t mk = readlane64(my_devM, j);
+        const int32_t Msw = (int32_t)(mk >> 32);
+        const int32_t Mt = (int32_t)wave_max_u32(feas ? (uint32_t)o.dev_raw + 1u : 0u) - 1;
+        if (mk == 0) {
+          Muse = Mt < 0 ? 0 : Mt;  // no untouched node is feasible: only the touched ones compete
+        } else {
+          const int64_t wn = (int64_t)(0xFFFFFFFFull - (mk & 0xFFFFFFFFull));
+          const bool wt = ((touched[wn >> 6] >> (wn & 63)) & 1ull) != 0;
+          if (wt ? (Mt != Msw) : (Mt > Msw)) {
+            processed = j;
+            break;
+          }
+          Muse = Msw;
+        }
+      }
+      if (feas) key_mod = gkey(key_total(cfg, o, Muse), snode);
       best = umax64(cj.umax, wave_max_u64(key_mod));
       KS_STAMP(2);
       uint64_t need = __ballot(!cj.exact && cj.valid && cj.ub > best);
@@ -1011,7 +1067,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? cj.ub : 0ull);
         const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && cj.ub == kmax)) - 1;
         const int64_t c = (int64_t)(uint32_t)__shfl((int)cj.chunk, sel, 64);
-        const uint64_t v = rescan_untouched<NSC, FEAT>(a, cfg, pod, c, touched[c]);
+        const uint64_t v = rescan_untouched<NSC, FEAT>(a, cfg, pod, c, touched[c], Muse);
         ++rescans;
         best = umax64(best, v);
         need &= ~(1ull << sel);
@@ -1061,6 +1117,17 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         scls[s] = ncl;
         snuma[2 * s] = src[RF_NUMA_A];
         snuma[2 * s + 1] = src[RF_NUMA_OFF];
+      }
+      if (DEV && cfg.dev) {
+        // the node's GPU totals / used / present flag into LDS (lane = word)
+        const DevDev& dv = *a.dv;
+        int64_t v = 0;
+        if (lane < DW) v = gld(dv.total + (int64_t)lane * dv.npad + node);
+        else if (lane < 2 * DW) v = gld(dv.used + (int64_t)(lane - DW) * dv.npad + node);
+        else if (lane == 2 * DW) v = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
+        if (lane < DW) sdev_tot[s * DW + lane] = v;
+        else if (lane < 2 * DW) sdev_use[s * DW + lane - DW] = v;
+        else if (lane == 2 * DW) sdev_pres[s] = (int32_t)v;
       }
       if (RSV && cfg.rsv) {
         // the node's reservations into LDS (lane = record word), unless too many or too wide
@@ -1143,6 +1210,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         EvalOut e2 = eval_pod_node<NSC, false>(cfg, pod, nr);
         if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
         fitla_pref = e2.total;
+        if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
+          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DW, sdev_pres[s] != 0});
+          fitla_pref += cfg.dev_pw * (Muse == 0 ? dd.raw : small_div(100 * dd.raw, Muse));
+        }
       }
       int64_t dd = 0;
       if (nom >= 0) {
@@ -1197,7 +1268,23 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       const int64_t fitla = hi >= kRsvOrderBase ? fitla_pref : score - hi * cfg.rsv_F;
       score_out = fitla + (hi > 0 ? a.rv->w100 : 0);
     }
-    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, 0};
+    uint32_t gminors = 0;
+    if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
+      // DeviceShare Reserve: allocate the minors on the pre-pod GPU state, add the request per instance
+      PodRec pod = spods[j];
+      pod.flags = pflags;
+      GpuReq g;
+      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DW, sdev_pres[s] != 0}, &g);
+      gminors = __builtin_amdgcn_readfirstlane(dd.minors);
+      if (lane < DW && ((gminors >> (lane % kGpus)) & 1u)) {
+        const int q = lane / kGpus;
+        const int64_t add = q == 0 ? (g.has_core ? g.core : 0) : (q == 1 ? g.mem : g.ratio);
+        const int64_t nv = sdev_use[s * DW + lane] + add;
+        sdev_use[s * DW + lane] = nv;
+        gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
+      }
+    }
+    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors};
     {
       const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
       if (cfg.quota_enable && qrow >= 0) {
@@ -1405,16 +1492,18 @@ __global__ __launch_bounds__(512) void quota_runtime_kernel(QrtArgs a) {
 // ------------------------------------------------------------------------------------------
 
 template <int NSC>
-__global__ void eval_debug_kernel(DevNodes d, const DevRsv* rv, Cfg c, const PodRec* pod, int64_t n,
-                                  uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord) {
+__global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, Cfg c, const PodRec* pod, int64_t n,
+                                  uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
+                                  int32_t* draw) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   NodeReg<NSC> r;
   load_node<NSC>(c, d, i, 1, r);
   const PodRec p = *pod;
   RsvOut ro;
-  const EvalOut o = eval_full<NSC, true, false, 3>(
-      c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); }, &ro);
+  const EvalOut o = eval_full<NSC, true, false, 7>(
+      c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
+      [&]() { return dev_eval<false>(c, p, DevGView{*dv, i}); }, &ro);
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
@@ -1424,6 +1513,27 @@ __global__ void eval_debug_kernel(DevNodes d, const DevRsv* rv, Cfg c, const Pod
   total[i] = o.reasons ? -1 : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw;
   raw[i] = ro.raw;
   hiord[i] = ro.hiord;
+  draw[i] = o.dev_raw;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
+}
+
+// DeviceShare NormalizeScore (DefaultNormalizeScore(100), scoring.go:95-97) for the debug path (one block)
+__global__ __launch_bounds__(1024) void dev_normalize_debug_kernel(int64_t n, const uint32_t* reasons,
+                                                                   const int32_t* draw, int64_t* scores,
+                                                                   int64_t* total, int64_t w) {
+  __shared__ int32_t s_max;
+  if (threadIdx.x == 0) s_max = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (!reasons[i]) atomicMax(&s_max, draw[i]);
+  __syncthreads();
+  const int64_t mx = s_max;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (reasons[i]) continue;
+    const int64_t sc = mx == 0 ? draw[i] : 100 * (int64_t)draw[i] / mx;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = sc;
+    total[i] += sc * w;
+  }
 }
 
 // Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and DefaultNormalizeScore
@@ -1581,6 +1691,13 @@ struct ks_ctx {
   int32_t rsv_ndist = 0;     // distinct order labels
   int32_t rsv_nrows = 0;     // caller rows
   std::vector<int32_t> rsv_perm;  // CSR position -> caller row
+  // DeviceShare GPUs (ks_dev.h)
+  void* dev_blob = nullptr;
+  DevDev dv{};
+  DevDev* ddv = nullptr;
+  bool dev_loaded = false;
+  int64_t* dev_used_ckpt = nullptr;
+  unsigned long long* dev_M = nullptr;  // [64] per pass
   // debug
   PodRec* dbg_pod = nullptr;
   // stats
@@ -1643,9 +1760,16 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.nw_mem = (int32_t)c.numa.weight_memory;
   k.numa_pw = c.numa.enable ? (int32_t)c.numa.plugin_weight : 0;
   if (k.numa && k.numa_most) k.monotone = 0;
+  k.dev = c.deviceshare.enable ? 1 : 0;
+  k.dev_most = c.deviceshare.strategy == KS_MOST_ALLOCATED;
+  k.dw_core = (int32_t)c.deviceshare.weight_gpu_core;
+  k.dw_mem = (int32_t)c.deviceshare.weight_gpu_memory;
+  k.dw_ratio = (int32_t)c.deviceshare.weight_gpu_memory_ratio;
+  k.dev_pw = c.deviceshare.enable ? (int32_t)c.deviceshare.plugin_weight : 0;
+  if (k.dev) k.monotone = 0;  // a commit changes the pod's DeviceShare normalization max
   k.rsv = c.reservation.enable ? 1 : 0;
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
-                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw) + 1);
+                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw) + 1);
   // a commit into a reservation can raise that node's Reservation score for later pods
   if (k.rsv) k.monotone = 0;
   return k;
@@ -1696,10 +1820,20 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
       return KS_EINVAL;
     }
   }
+  if (cfg->deviceshare.enable) {
+    const ks_deviceshare_args& da = cfg->deviceshare;
+    if (da.weight_gpu_core < 0 || da.weight_gpu_core > 100 || da.weight_gpu_memory < 0 || da.weight_gpu_memory > 100 ||
+        da.weight_gpu_memory_ratio < 0 || da.weight_gpu_memory_ratio > 100 || da.plugin_weight < 0 ||
+        da.plugin_weight > 1000 || (da.strategy != KS_LEAST_ALLOCATED && da.strategy != KS_MOST_ALLOCATED)) {
+      g_create_error = "ks_create: DeviceShare args out of range";
+      return KS_EINVAL;
+    }
+  }
   if (cfg->reservation.enable) {
     const int64_t fitla = 100 * ((cfg->fit.enable_score ? cfg->fit.plugin_weight : 0) +
                                  (cfg->loadaware.enable_score ? cfg->loadaware.plugin_weight : 0) +
-                                 (cfg->numa.enable ? cfg->numa.plugin_weight : 0));
+                                 (cfg->numa.enable ? cfg->numa.plugin_weight : 0) +
+                                 (cfg->deviceshare.enable ? cfg->deviceshare.plugin_weight : 0));
     if (cfg->reservation.plugin_weight <= fitla || cfg->reservation.plugin_weight > ((int64_t)1 << 40) ||
         (fitla + 1) * (kRsvOrderBase + 1) >= (1 << 26)) {
       g_create_error = "ks_create: Reservation plugin weight must exceed 100 x (Fit + LoadAware weights) (ks_rsv.h ranking)";
@@ -1745,6 +1879,8 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->counters = (unsigned long long*)p;
   if (dev_alloc(ctx, &p, sizeof(PodRec)) != KS_OK) goto fail;
   ctx->dbg_pod = (PodRec*)p;
+  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  ctx->dev_M = (unsigned long long*)p;
   *out = ctx;
   return KS_OK;
 fail:
@@ -1777,6 +1913,9 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->dnodes; dev_free(p);
   p = ctx->drv; dev_free(p);
   dev_free(ctx->rsv_blob);
+  p = ctx->ddv; dev_free(p);
+  dev_free(ctx->dev_blob);
+  p = ctx->dev_M; dev_free(p);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1960,6 +2099,7 @@ static int upload_prep_nodes(ks_ctx* ctx) {
 }
 
 static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
+static int dev_install(ks_ctx* ctx, const ks_device_cols* dc);
 
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
@@ -2008,6 +2148,7 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
   if (ctx->cfg.reservation.enable && rsv_install(ctx, nullptr, 0) != KS_OK) return KS_EHIP;
+  if (ctx->cfg.deviceshare.enable && dev_install(ctx, nullptr) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -2134,6 +2275,72 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
   if (rsv_launch_base(ctx, nullptr, ctx->n, +1, 1) != KS_OK) return KS_EHIP;
   ctx->rsv_based = true;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+// Upload the GPU device table ([3][kGpus][npad] totals / used + flags); dc == NULL: no device info.
+static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
+  const size_t np = (size_t)ctx->npad, words = 3 * (size_t)kGpus * np;
+  const size_t o_flags = 0, o_total = (np * 4 + 15) / 16 * 16, o_used = o_total + words * 8, o_ck = o_used + words * 8,
+               bytes = o_ck + words * 8;
+  std::vector<char> h(bytes, 0);
+  uint32_t* flags = (uint32_t*)(h.data() + o_flags);
+  int64_t* total = (int64_t*)(h.data() + o_total);
+  int64_t* used = (int64_t*)(h.data() + o_used);
+  if (dc) {
+    for (int k = 0; k < kGpus; ++k) {
+      const int64_t* cols[6] = {dc->total_core[k], dc->total_memory[k], dc->total_ratio[k],
+                                dc->used_core[k], dc->used_memory[k], dc->used_ratio[k]};
+      for (int c = 0; c < 6; ++c)
+        if (check_range64(ctx, cols[c], ctx->n, "device quantity") != KS_OK) return KS_EINVAL;
+      for (int64_t n = 0; n < ctx->n; ++n)
+        for (int q = 0; q < 3; ++q) {
+          total[((size_t)q * kGpus + k) * np + n] = cols[q] ? cols[q][n] : 0;
+          used[((size_t)q * kGpus + k) * np + n] = cols[3 + q] ? cols[3 + q][n] : 0;
+        }
+    }
+    for (int64_t n = 0; n < ctx->n; ++n) flags[n] = dc->flags ? dc->flags[n] : 0;
+  }
+  dev_free(ctx->dev_blob);
+  if (dev_alloc(ctx, &ctx->dev_blob, bytes) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->dev_blob, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+  char* b = (char*)ctx->dev_blob;
+  ctx->dv.flags = (const uint32_t*)(b + o_flags);
+  ctx->dv.total = (const int64_t*)(b + o_total);
+  ctx->dv.used = (int64_t*)(b + o_used);
+  ctx->dv.npad = (int64_t)np;
+  ctx->dev_used_ckpt = (int64_t*)(b + o_ck);
+  if (!ctx->ddv) {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, sizeof(DevDev)) != KS_OK) return KS_ENOMEM;
+    ctx->ddv = (DevDev*)p;
+  }
+  HIPCHK(ctx, hipMemcpyAsync(ctx->ddv, &ctx->dv, sizeof(DevDev), hipMemcpyHostToDevice, ctx->stream));
+  ctx->dev_loaded = dc != nullptr;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_load_devices(ks_ctx* ctx, const ks_device_cols* dev, int64_t n) {
+  if (!ctx || !dev) return ctx ? (ctx->err = "ks_load_devices: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_load_devices before ks_load_nodes");
+  if (n != ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_load_devices: %lld rows for %lld nodes", (long long)n, (long long)ctx->n);
+  if (!ctx->cfg.deviceshare.enable) KS_FAIL(ctx, KS_ESTATE, "ks_load_devices: the DeviceShare plugin is not enabled");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  return dev_install(ctx, dev);
+}
+
+int ks_read_devices(ks_ctx* ctx, int64_t* used_core, int64_t* used_memory, int64_t* used_ratio) {
+  if (!ctx) return KS_EINVAL;
+  if (!ctx->dev_blob) return KS_OK;
+  const size_t np = (size_t)ctx->npad, n = (size_t)ctx->n;
+  std::vector<int64_t> u(3 * (size_t)kGpus * np);
+  HIPCHK(ctx, hipMemcpyAsync(u.data(), ctx->dv.used, u.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  int64_t* outs[3] = {used_core, used_memory, used_ratio};
+  for (int q = 0; q < 3; ++q)
+    if (outs[q])
+      for (int k = 0; k < kGpus; ++k) memcpy(outs[q] + (size_t)k * n, u.data() + ((size_t)q * kGpus + k) * np, n * 8);
   return KS_OK;
 }
 
@@ -2417,8 +2624,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   const size_t res = ((size_t)cap * sizeof(ks_result) + 255) / 256 * 256;
   const size_t col8 = ((size_t)cap * 8 + 255) / 256 * 256;
   const size_t col4 = ((size_t)cap * 4 + 255) / 256 * 256;
-  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 qreq[8] = 23 int64 cols; flags quota qmask rsv_class = 4 x32
-  const size_t bytes = rec + res + col8 * 23 + col4 * 4;
+  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 qreq[8] = 26 int64 cols; flags quota qmask rsv_class = 4 x32
+  const size_t bytes = rec + res + col8 * 26 + col4 * 4;
   if (dev_alloc(ctx, &ctx->pod_blob, bytes) != KS_OK) return KS_ENOMEM;
   char* b = (char*)ctx->pod_blob;
   ctx->pods = (PodRec*)b;
@@ -2427,7 +2634,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   b += res;
   DevPodCols& s = ctx->pstage;
   int64_t** c8[] = {&s.cpu, &s.mem, &s.eph, &s.nzcpu, &s.nzmem, &s.sc[0], &s.sc[1], &s.sc[2], &s.sc[3],
-                    &s.la_req_cpu, &s.la_lim_cpu, &s.la_dflt_cpu, &s.la_req_mem, &s.la_lim_mem, &s.la_dflt_mem};
+                    &s.la_req_cpu, &s.la_lim_cpu, &s.la_dflt_cpu, &s.la_req_mem, &s.la_lim_mem, &s.la_dflt_mem,
+                    &s.gpu_core, &s.gpu_mem, &s.gpu_ratio};
   for (int64_t** f : c8) {
     *f = (int64_t*)b;
     b += col8;
@@ -2466,6 +2674,9 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
   HIPCHK(ctx, cp8(s.la_req_mem, pc->la_req_memory));
   HIPCHK(ctx, cp8(s.la_lim_mem, pc->la_lim_memory));
   HIPCHK(ctx, cp8(s.la_dflt_mem, pc->la_dflt_memory));
+  HIPCHK(ctx, cp8(s.gpu_core, pc->gpu_core));
+  HIPCHK(ctx, cp8(s.gpu_mem, pc->gpu_memory));
+  HIPCHK(ctx, cp8(s.gpu_ratio, pc->gpu_memory_ratio));
   for (int d = 0; d < KS_QUOTA_DIMS; ++d) HIPCHK(ctx, cp8(ctx->pq.req[d], pc->quota_req[d]));
   if (pc->flags) HIPCHK(ctx, hipMemcpyAsync(s.flags, pc->flags, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.flags, 0, (size_t)p * 4, ctx->stream));
@@ -2484,7 +2695,8 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
 
 static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
   const int64_t* cols[] = {pc->req_milli_cpu, pc->req_memory, pc->req_ephemeral, pc->nonzero_milli_cpu,
-                           pc->nonzero_memory, pc->la_req_cpu, pc->la_lim_cpu, pc->la_req_memory, pc->la_lim_memory};
+                           pc->nonzero_memory, pc->la_req_cpu, pc->la_lim_cpu, pc->la_req_memory, pc->la_lim_memory,
+                           pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio};
   for (const int64_t* c : cols)
     if (check_range64(ctx, c, p, "pod quantity") != KS_OK) return KS_EINVAL;
   for (int k = 0; k < KS_MAX_SCALARS; ++k)
@@ -2552,7 +2764,11 @@ static bool commit_qcache(const ks_ctx* ctx) {
 }
 
 // kernel variant: 0 = Fit/LoadAware/Quota, 1 = + Reservation, 3 = + Reservation + NodeNUMAResource
-static int kernel_feat(const ks_ctx* ctx) { return ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0); }
+static int kernel_feat(const ks_ctx* ctx) { return ctx->kc.dev ? 7 : (ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0)); }
+
+static size_t dev_cache_bytes(const ks_ctx* ctx) {
+  return ctx->kc.dev ? (size_t)kMaxBatch * (2 * 3 * kGpus * 8 + 4) : 0;
+}
 
 static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {
   return (size_t)kMaxBatch * rcap * 8 * (size_t)(3 + 2 * (3 + ctx->nsc) + 2);  // sizeof(RsvRec<3+nsc>)
@@ -2564,7 +2780,7 @@ static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
   *qcache = commit_qcache(ctx);
   if (!ctx->kc.rsv) return 0;
   auto fit = [&](bool qc) {
-    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0).total + 64;
+    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx)).total + 64;
     const size_t avail = base < 160 * 1024 ? 160 * 1024 - base : 0;
     return (int32_t)std::min<size_t>(8, avail / rsv_cache_bytes(ctx, 1));
   };
@@ -2602,7 +2818,19 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.ppw = ppw;
   rec(0);
   const int feat = kernel_feat(ctx);
-  if (feat == 3)
+  sa.dv = ctx->ddv;
+  sa.dev_M = ctx->dev_M;
+  sa.phase = 1;
+  if (feat == 7) {
+    // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys
+    (void)hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream);
+    sa.phase = 0;
+    hipLaunchKernelGGL((sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    if (ctx->nranks > 1)
+      (void)ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ctx->stream);
+    sa.phase = 1;
+    hipLaunchKernelGGL((sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  } else if (feat == 3)
     hipLaunchKernelGGL((sweep_kernel<NSC, 3>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
   else if (feat == 1)
     hipLaunchKernelGGL((sweep_kernel<NSC, 1>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
@@ -2686,7 +2914,10 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   bool qcache = false;
   ca.rcap = commit_rcap(ctx, &qcache);
   ca.rsv_bytes = (int32_t)rsv_cache_bytes(ctx, ca.rcap);
-  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes).total;
+  ca.dev_bytes = (int32_t)dev_cache_bytes(ctx);
+  ca.dv = ctx->ddv;
+  ca.dev_M = ctx->dev_M;
+  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes).total;
   rec(2);
 #define KS_COMMIT(F)                                                                                          \
   do {                                                                                                        \
@@ -2695,7 +2926,8 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
     else                                                                                                      \
       hipLaunchKernelGGL((commit_kernel<NSC, false, F>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca); \
   } while (0)
-  if (feat == 3) KS_COMMIT(3);
+  if (feat == 7) KS_COMMIT(7);
+  else if (feat == 3) KS_COMMIT(3);
   else if (feat == 1) KS_COMMIT(1);
   else KS_COMMIT(0);
 #undef KS_COMMIT
@@ -2711,7 +2943,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   {
     bool qcache = false;
     const int32_t rcap = commit_rcap(ctx, &qcache);
-    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap)).total;
+    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx)).total;
     if (smem > 160 * 1024)
       KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
     hipError_t e = hipSuccess;
@@ -2721,7 +2953,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     const int feat = kernel_feat(ctx);
 #define KS_SETATTR(N)                                                                                                         \
   do {                                                                                                                        \
-    if (feat == 3) qcache ? setattr((const void*)commit_kernel<N, true, 3>) : setattr((const void*)commit_kernel<N, false, 3>); \
+    if (feat == 7) qcache ? setattr((const void*)commit_kernel<N, true, 7>) : setattr((const void*)commit_kernel<N, false, 7>); \
+    else if (feat == 3) qcache ? setattr((const void*)commit_kernel<N, true, 3>) : setattr((const void*)commit_kernel<N, false, 3>); \
     else if (feat == 1) qcache ? setattr((const void*)commit_kernel<N, true, 1>) : setattr((const void*)commit_kernel<N, false, 1>); \
     else qcache ? setattr((const void*)commit_kernel<N, true, 0>) : setattr((const void*)commit_kernel<N, false, 0>); \
   } while (0)
@@ -2802,7 +3035,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     }
   }
   // algorithmic bytes of one full sweep launch: node columns read once per pod group + outputs
-  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16 + (ctx->kc.rsv ? 8 : 0) + (ctx->kc.numa ? 16 : 0);
+  int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16 + (ctx->kc.rsv ? 8 : 0) + (ctx->kc.numa ? 16 : 0) +
+                   (ctx->kc.dev ? 4 + 2 * 3 * kGpus * 8 : 0);
   const int64_t groups = (ctx->batch + ppw - 1) / ppw;
   ctx->stats.sweep_bytes = local_chunks * 64 * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + local_chunks * 64 * 4;
   return KS_OK;
@@ -2838,6 +3072,8 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->quota_used_ckpt, ctx->q.used, tb, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->quota_npused_ckpt, ctx->q.npused, tb, hipMemcpyDeviceToDevice, ctx->stream));
   }
+  if (ctx->dev_blob)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dev_used_ckpt, ctx->dv.used, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_allocd_ckpt, ctx->rv.allocd, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -2854,6 +3090,8 @@ int ks_restore(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->q.used, ctx->quota_used_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->q.npused, ctx->quota_npused_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
   }
+  if (ctx->dev_blob)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dv.used, ctx->dev_used_ckpt, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -2871,21 +3109,25 @@ int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, in
   if (stage_pods_to(ctx, pod, 1, ctx->dbg_pod) != KS_OK) return KS_EHIP;
   const int64_t n = ctx->n;
   void* buf = nullptr;
-  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8) + 64;
+  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4) + 64;
   if (dev_alloc(ctx, &buf, bytes) != KS_OK) return KS_ENOMEM;
   uint32_t* dr = (uint32_t*)buf;
   int64_t* ds = (int64_t*)((char*)buf + ((size_t)n * 4 + 15) / 16 * 16);
   int64_t* dt = ds + (size_t)n * KS_NUM_SCORE_PLUGINS;
   int32_t* draw = (int32_t*)(dt + n);
   int32_t* dhi = draw + n;
+  int32_t* ddraw = dhi + n;
   const int threads = 256;
   const int blocks = (int)((n + threads - 1) / threads);
   if (blocks > 0) {
     switch (ctx->nsc) {
-      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi); break;
-      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi); break;
-      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi); break;
+      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
+      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
+      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
     }
+    if (ctx->kc.dev)
+      hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,
+                         ctx->cfg.deviceshare.plugin_weight);
     if (ctx->kc.rsv)
       hipLaunchKernelGGL(rsv_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, draw, dhi, ds, dt,
                          ctx->cfg.reservation.plugin_weight);

@@ -35,6 +35,8 @@ constexpr int kMaxCand = 64;   // candidate chunks per pod
 constexpr uint32_t kPodAllZero = 0x100u;
 // internal pod flag: every request value is zero (quotav1.IsZero, NodeNUMAResource PreFilter skip)
 constexpr uint32_t kPodReqZero = 0x200u;
+// internal pod flag: the pod has a GPU request (DeviceShare preparePod: skip = false)
+constexpr uint32_t kPodHasGpu = 0x400u;
 
 // la_bits (prep_nodes_kernel output)
 constexpr uint32_t kLaZeroScore = 0x1u;     // Score returns 0 (no NodeMetric / expired)
@@ -57,6 +59,7 @@ struct Cfg {
   int32_t rsv;       // Reservation plugin enabled
   int32_t rsv_F;     // key radix: key total = hi * rsv_F + (Fit + LoadAware + NUMA weighted total), see ks_rsv.h
   int32_t numa, numa_most, nw_cpu, nw_mem, numa_pw;  // NodeNUMAResource
+  int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw;  // DeviceShare (GPU)
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -98,9 +101,9 @@ struct __attribute__((aligned(16))) PodRec {
   float _fpad;
   int64_t h_cpu, h_mem;  // 100 x the Requested cpu / memory (NodeNUMAResource score)
   float f_cpu, f_mem;
-  int64_t _pad2;
+  int64_t gpu_core, gpu_mem, gpu_ratio;  // DeviceShare: converted GPU request
 };
-static_assert(sizeof(PodRec) == 256, "PodRec layout");
+static_assert(sizeof(PodRec) == 272, "PodRec layout");
 // PodRec int64 word indices read by the commit kernel's lane-parallel Reserve
 constexpr int kPodWordHCpu = (int)(offsetof(PodRec, h_cpu) / 8), kPodWordHMem = (int)(offsetof(PodRec, h_mem) / 8);
 static_assert(offsetof(PodRec, h_nzcpu) == 12 * 8 && offsetof(PodRec, h_sc) == 17 * 8, "PodRec word layout");
@@ -166,6 +169,15 @@ struct Term {
 __device__ __forceinline__ float i64_to_f32(int64_t v) {
   // |v| < 2^62: hi part exact in f32 up to 2^24, the sum within 2^-23 relative
   return __builtin_fmaf((float)(int32_t)(v >> 32), 4294967296.0f, (float)(uint32_t)v);
+}
+
+// exact floor(100 * num / cap) for 0 <= num <= cap < 2^56, cap > 0 (f32 estimate + int64 correction)
+__device__ __forceinline__ int32_t pct_floor_i64(int64_t num, int64_t cap) {
+  int32_t q = (int32_t)(i64_to_f32(num) * 100.0f * __builtin_amdgcn_rcpf(i64_to_f32(cap)));
+  const int64_t r = num * 100 - (int64_t)q * cap;
+  q += (r >= cap) ? 1 : 0;
+  q -= (r < 0) ? 1 : 0;
+  return q;
 }
 
 __device__ __forceinline__ float rcp100(int64_t cap) {
@@ -340,8 +352,10 @@ __device__ __forceinline__ void reserve_row(NodeReg<NSC>& r, const PodRec& p) {
 
 struct EvalOut {
   uint32_t reasons;  // KS_R_* (0 = feasible)
-  int32_t fit, la, total;
+  int32_t fit, la, total;  // total: Fit + LoadAware + NodeNUMAResource (weighted)
   int32_t numa;
+  int32_t dev_raw;         // DeviceShare raw score (normalized in key_total)
+  int32_t hi;              // Reservation ranking component (ks_rsv.h)
 };
 
 // Filter + Score of one (pod, node).  DEBUG=false computes feasibility (reasons != 0) and the
@@ -388,6 +402,8 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   o.fit = 0;
   o.la = 0;
   o.numa = 0;
+  o.dev_raw = 0;
+  o.hi = 0;
   int32_t total = 0;
   if (c.fit_score) {
     int32_t ns = 0, ws = r.fit_ws;

@@ -66,14 +66,7 @@ __device__ __forceinline__ int64_t pod_dim(const PodRec& p, int d) {
   return d == 0 ? p.cpu : d == 1 ? p.mem : d == 2 ? p.eph : p.sc[d - 3];
 }
 
-// exact floor(100 * req / cap) for 0 <= req <= cap < 2^56 (f32 estimate + int64 correction)
-__device__ __forceinline__ int32_t pct_floor(int64_t req, int64_t cap) {
-  int32_t q = (int32_t)(i64_to_f32(req) * 100.0f * __builtin_amdgcn_rcpf(i64_to_f32(cap)));
-  const int64_t r = req * 100 - (int64_t)q * cap;
-  q += (r >= cap) ? 1 : 0;
-  q -= (r < 0) ? 1 : 0;
-  return q;
-}
+__device__ __forceinline__ int32_t pct_floor(int64_t req, int64_t cap) { return pct_floor_i64(req, cap); }
 
 // Per-(pod, node) restore deltas relative to the base NodeInfo.
 template <int NSC>
@@ -292,15 +285,22 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
 // r must be the base row; with UNDO it is returned unchanged (the sweep reuses it across pods).
 // rsv(dl) runs rsv_eval on the node's reservation view; it is called only when the pod's class
 // matches one of them.
-// FEAT: bit 0 Reservation, bit 1 NodeNUMAResource compiled in (the Cfg flags switch them at run time).
-template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F>
-__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv,
+// FEAT: bit 0 Reservation, bit 1 NodeNUMAResource, bit 2 DeviceShare compiled in (the Cfg flags
+// switch them at run time).  dev() returns the node's DevOut (ks_dev.h).  The key total is
+// key_total(c, o, M) with M the pod's DeviceShare normalization max.
+template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G>
+__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& dev,
                                              RsvOut* info = nullptr) {
-  constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0;
+  constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0, DEV = (FEAT & 4) != 0;
   if (!RSV || !c.rsv || (p.rsv_class < 0 && !(p.flags & KS_POD_RSV_AFFINITY))) {
     if (info) *info = RsvOut{0u, 0, 0, 0, -1};
     EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
     if (NUMA && c.numa) numa_eval<NSC, DEBUG>(c, p, r, o);
+    if (DEV && c.dev && (p.flags & kPodHasGpu)) {
+      const auto d = dev();
+      o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
+      o.dev_raw = d.raw;
+    }
     return o;
   }
   const bool slow = p.rsv_class >= 0 && p.rsv_class < 64 && ((r.rsv_cls >> p.rsv_class) & 1ull);
@@ -313,14 +313,28 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
   EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
   if (NUMA && c.numa) numa_eval<NSC, DEBUG>(c, p, r, o);
   if (UNDO && slow) rsv_apply<NSC>(r, dl, -1);
+  if (DEV && c.dev && (p.flags & kPodHasGpu)) {
+    const auto d = dev();
+    o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
+    o.dev_raw = d.raw;
+  }
   // a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
   // NodeNames, plugin.go:235-246) before any Filter plugin runs
   o.reasons = ro.reasons == KS_R_RSV_AFFINITY ? ro.reasons : (o.reasons | ro.reasons);
-  // the preferred node is the lowest INDEX among equal order labels, whatever its Fit/LoadAware
-  // total: ordered nodes rank by hi alone (ties to the lower index through the key's node bits)
-  o.total = ro.hi >= kRsvOrderBase ? ro.hi * c.rsv_F : o.total + ro.hi * c.rsv_F;
+  o.hi = ro.hi;
   if (info) *info = ro;
   return o;
+}
+
+// Key total of a feasible node: Fit + LoadAware + NUMA + DeviceShare normalized with the pod's max M,
+// then the Reservation ranking.  The preferred node is the lowest INDEX among equal order labels,
+// whatever its other scores: ordered nodes rank by hi alone (ties to the lower index through the
+// key's node bits).
+__device__ __forceinline__ int32_t key_total(const Cfg& c, const EvalOut& o, int32_t M) {
+  int32_t t = o.total;
+  if (c.dev) t += c.dev_pw * (M == 0 ? o.dev_raw : small_div(100 * o.dev_raw, M));
+  if (c.rsv) t = o.hi >= kRsvOrderBase ? o.hi * c.rsv_F : t + o.hi * c.rsv_F;
+  return t;
 }
 
 // Reserve into reservation i of the view (plugin.go:532-570 -> reservation_info.go:379-388): the

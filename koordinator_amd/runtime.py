@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
+from .cluster import DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
@@ -59,6 +59,8 @@ def lib() -> C.CDLL:
     L.ks_load_quotas.argtypes = [vp, C.POINTER(abi.KsQuotaCols), C.c_int32]
     L.ks_load_reservations.argtypes = [vp, C.POINTER(abi.KsReservationCols), C.c_int32]
     L.ks_read_reservations.argtypes = [vp, abi.P64, abi.P32]
+    L.ks_load_devices.argtypes = [vp, C.POINTER(abi.KsDeviceCols), C.c_int64]
+    L.ks_read_devices.argtypes = [vp, abi.P64, abi.P64, abi.P64]
     L.ks_refresh_quota_runtime.argtypes = [vp, C.POINTER(abi.KsQuotaTree), C.c_int32, abi.P64, abi.PU32]
     L.ks_schedule.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
     L.ks_stage_pods.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32]
@@ -93,7 +95,7 @@ class Evaluator:
     """One scheduler profile's device-resident node snapshot + the sweep/commit pipeline."""
 
     def __init__(self, cfg: abi.KsConfig, nodes: Optional[NodeTable] = None, quotas: Optional[QuotaTable] = None,
-                 reservations: Optional[ReservationTable] = None):
+                 reservations: Optional[ReservationTable] = None, devices: Optional[DeviceTable] = None):
         self.L = lib()
         self.cfg = cfg
         h = C.c_void_p()
@@ -111,6 +113,8 @@ class Evaluator:
             self.load_quotas(quotas)
         if reservations is not None:
             self.load_reservations(reservations)
+        if devices is not None:
+            self.load_devices(devices)
 
     def _chk(self, rc: int):
         if rc != abi.KS_OK:
@@ -153,6 +157,17 @@ class Evaluator:
         self._chk(self.L.ks_load_reservations(self.h, C.byref(cols), rs.r))
         self.nr = rs.r
 
+    def load_devices(self, dev: DeviceTable):
+        cols = dev.ks()
+        self._chk(self.L.ks_load_devices(self.h, C.byref(cols), dev.n))
+
+    def read_devices(self):
+        """(used_core, used_memory, used_ratio), each [KS_MAX_GPUS][n]"""
+        G = abi.KS_MAX_GPUS
+        out = [np.zeros(G * max(self.n, 1), np.int64) for _ in range(3)]
+        self._chk(self.L.ks_read_devices(self.h, *[o.ctypes.data_as(abi.P64) for o in out]))
+        return tuple(o[: G * self.n].reshape(G, self.n) for o in out)
+
     def read_reservations(self):
         """(allocated [r][KS_RSV_DIMS], assigned [r]) after commits"""
         allocated = np.zeros(max(self.nr, 1) * abi.KS_RSV_DIMS, np.int64)
@@ -184,7 +199,7 @@ class Evaluator:
         self._chk(self.L.ks_schedule(self.h, C.byref(cols), pods.n, out.ctypes.data_as(C.POINTER(abi.KsResult))))
         out = out[: pods.n]
         return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy(),
-                "reservation": out["reservation"].copy()}
+                "reservation": out["reservation"].copy(), "gpu_minors": out["gpu_minors"].copy()}
 
     def stage(self, pods: PodTable):
         cols = pods.ks()
@@ -199,7 +214,7 @@ class Evaluator:
         self._chk(self.L.ks_fetch_results(self.h, out.ctypes.data_as(C.POINTER(abi.KsResult)), self.np_staged))
         out = out[: self.np_staged]
         return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy(),
-                "reservation": out["reservation"].copy()}
+                "reservation": out["reservation"].copy(), "gpu_minors": out["gpu_minors"].copy()}
 
     def checkpoint(self):
         self._chk(self.L.ks_checkpoint(self.h))

@@ -216,6 +216,44 @@ def reservation_pods(pods: PodTable, rng: np.random.Generator, n_classes: int = 
     return pods
 
 
+def make_devices(nodes: NodeTable, rng: np.random.Generator, gpu_frac: float = 0.9) -> "DeviceTable":
+    """GPU devices (DeviceShare): 90 % of the nodes carry 8 (or 4) GPUs of 80 GiB (gpu-core 100,
+    gpu-memory-ratio 100 each), some already partly used by running GPU pods; the rest have no
+    device information.  A few nodes carry an unhealthy minor (zero totals)."""
+    from .cluster import DeviceTable
+    n = nodes.n
+    d = DeviceTable(n)
+    has = rng.random(n) < gpu_frac
+    d.flags[:] = np.where(has, abi.KS_DEV_PRESENT, 0)
+    count = np.where(rng.random(n) < 0.75, 8, 4)
+    for k in range(abi.KS_MAX_GPUS):
+        on = has & (k < count) & (rng.random(n) > 0.01)
+        d.total_core[k] = np.where(on, 100, 0)
+        d.total_ratio[k] = np.where(on, 100, 0)
+        d.total_memory[k] = np.where(on, 80 * GI, 0)
+        used = on & (rng.random(n) < 0.3)
+        part = rng.choice(np.array([25, 50, 100], np.int64), n)
+        d.used_core[k] = np.where(used, part, 0)
+        d.used_ratio[k] = np.where(used, part, 0)
+        d.used_memory[k] = np.where(used, part * 80 * GI // 100, 0)
+    return d
+
+
+def gpu_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4) -> PodTable:
+    """40 % of the pods request GPUs: whole devices (nvidia.com/gpu 1, 2, 4 -> core = ratio = 100 x n),
+    half a GPU by ratio, or a memory amount (gpu-memory, ratio derived per node)."""
+    p = pods.n
+    g = rng.random(p) < frac
+    kind = rng.choice(np.array([0, 1, 2, 3, 4]), p, p=[0.35, 0.2, 0.1, 0.2, 0.15])
+    whole = np.array([100, 200, 400, 50, 0])[kind]
+    pods.gpu_core[:] = np.where(g & (kind < 4), whole, 0)
+    pods.gpu_memory_ratio[:] = np.where(g & (kind < 4), whole, 0)
+    pods.gpu_memory[:] = np.where(g & (kind == 4), rng.choice(np.array([10, 20, 40], np.int64), p) * GI, 0)
+    pods.flags[:] |= np.where(g & (kind < 4), abi.KS_POD_GPU_CORE, 0).astype(np.uint32)
+    pods.flags[:] |= np.where(g & (kind == 4), abi.KS_POD_GPU_MEMORY, 0).astype(np.uint32)
+    return pods
+
+
 def c1(seed: int = SEED, n_nodes: int = 500, n_pods: int = 1000, **kw) -> Workload:
     rng = np.random.Generator(np.random.PCG64(seed))
     nodes = make_nodes(n_nodes, rng)

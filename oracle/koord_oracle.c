@@ -30,6 +30,12 @@
  *                            filterAmplifiedCPUs :340-373, Score scoring.go:55-114 (scoreWithAmplifiedCPUs),
  *                            resourceAllocationScorer :187-242, Amplify apis/extension/node_resource_amplification.go:170-175
  *                            (topology policy None and non-cpuset pods only)
+ *   DeviceShare (GPU)        PreFilter deviceshare/plugin.go:150-157 -> preparePod / GetPodDeviceRequests utils.go:203-252,
+ *                            Filter plugin.go:272-322 -> AutopilotAllocator.Allocate device_allocator.go:94-132,
+ *                            GPUHandler.CalcDesiredRequestsAndCount devicehandler_gpu.go:40-98, defaultAllocateDevices
+ *                            device_allocator.go:392-462, scoreDevices / sortDeviceResourcesByMinor device_resources.go:171-208,
+ *                            Score scoring.go:34-89 -> scoreNode :228-253, NormalizeScore :95-97, Reserve plugin.go:377-430
+ *                            (GPU devices only: no hints, joint allocation, NUMA affinity, VFs)
  *   Sweep driver             upstream schedule_one.go (schedulePod, findNodesThatPassFilters,
  *                            prioritizeNodes, selectHost) with percentageOfNodesToScore=100 and
  *                            lowest-index tie-break; Parallelizer pkg/util/parallelize/parallelism.go:29-49
@@ -119,6 +125,15 @@ typedef struct {
 
 typedef struct ko_pool ko_pool;
 
+#define KO_GPUS KS_MAX_GPUS
+/* nodeDeviceCache: per node and GPU minor, deviceTotal / deviceUsed of (core, memory, ratio) */
+typedef struct {
+  int loaded;
+  uint32_t *flags;
+  int64_t *total; /* [n][KO_GPUS][3] */
+  int64_t *used;  /* [n][KO_GPUS][3] */
+} ko_dev;
+
 /* reservation cache: rows in caller order, CSR by node (rows of a node in table order) */
 typedef struct {
   int32_t nr;
@@ -147,6 +162,8 @@ typedef struct ko_sched {
   int32_t *nom;     /* per node: nominated reservation row (-1) */
   int64_t *rraw;    /* per node: Reservation raw score */
   int64_t *rord;    /* per node: findMostPreferredReservationByOrder over matched (0 = none) */
+  ko_dev dv;
+  int64_t *draw;    /* per node: DeviceShare raw score */
 } ko_sched;
 
 /* pod view for one pod (values pulled out of ks_pod_cols) */
@@ -160,6 +177,8 @@ typedef struct {
   int64_t qreq[KS_QUOTA_DIMS];
   int32_t rcls;  /* reservation match class, -1 = none */
   int reqzero;   /* quotav1.IsZero(PodRequestsAndLimits) (NodeNUMAResource PreFilter skip) */
+  int64_t gpu[3]; /* converted GPU request: core, memory, ratio */
+  int has_gpu;
   uint32_t keys; /* bit d: request dimension d is a key of the pod's requests (value != 0) */
 } ko_pod;
 
@@ -195,6 +214,10 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
   for (int d = 0; d < KO_D; d++)
     if (v[d] != 0) p->keys |= 1u << d;
   p->reqzero = p->keys == 0;
+  p->gpu[0] = colv64(pc->gpu_core, i);
+  p->gpu[1] = colv64(pc->gpu_memory, i);
+  p->gpu[2] = colv64(pc->gpu_memory_ratio, i);
+  p->has_gpu = p->gpu[0] != 0 || p->gpu[1] != 0 || p->gpu[2] != 0;
 }
 
 static int64_t pod_dim(const ko_pod *p, int d) { return d == 0 ? p->cpu : d == 1 ? p->mem : d == 2 ? p->eph : p->sc[d - 3]; }
@@ -632,6 +655,137 @@ static void rsv_reserve(ko_sched *s, const ko_pod *p, int32_t r) {
   rv->assigned[r] += 1;
 }
 
+/* ------------------------------------------------------------------ */
+/* DeviceShare (GPU)                                                   */
+/* ------------------------------------------------------------------ */
+
+static const int64_t *dev_total(const ko_sched *s, int64_t n, int k) { return s->dv.total + ((size_t)n * KO_GPUS + k) * 3; }
+static const int64_t *dev_used(const ko_sched *s, int64_t n, int k) { return s->dv.used + ((size_t)n * KO_GPUS + k) * 3; }
+
+/* a GPU instance: the request per instance and how many (GPUHandler.CalcDesiredRequestsAndCount
+ * after fillGPUTotalMem); returns KS_R_DEV_NO_GPU when the node has no healthy GPU */
+typedef struct {
+  int64_t req[3]; /* core, memory, ratio */
+  int has_core;
+  int desired;
+} ko_gpureq;
+
+static uint32_t dev_prepare(const ko_sched *s, const ko_pod *p, int64_t n, ko_gpureq *g) {
+  int64_t total_mem = -1;
+  for (int k = 0; k < KO_GPUS; k++) {
+    const int64_t *t = dev_total(s, n, k);
+    if (t[0] || t[1] || t[2]) {
+      total_mem = t[1];
+      break;
+    }
+  }
+  if (total_mem < 0) return KS_R_DEV_NO_GPU;
+  int64_t core = p->gpu[0], mem = p->gpu[1], ratio = p->gpu[2];
+  if (p->flags & KS_POD_GPU_MEMORY)
+    ratio = (int64_t)((double)mem / (double)total_mem * 100); /* memoryBytesToRatio */
+  else
+    mem = ratio * total_mem / 100; /* memoryRatioToBytes */
+  g->has_core = (p->flags & KS_POD_GPU_CORE) != 0;
+  g->desired = 1;
+  if (ratio > 100 && ratio % 100 == 0) {
+    g->desired = (int)(ratio / 100);
+    core /= g->desired;
+    mem /= g->desired;
+    ratio /= g->desired;
+  }
+  g->req[0] = core;
+  g->req[1] = mem;
+  g->req[2] = ratio;
+  return 0;
+}
+
+static int64_t dev_weight(const ko_sched *s, int r) {
+  const ks_deviceshare_args *a = &s->cfg.deviceshare;
+  return r == 0 ? a->weight_gpu_core : r == 1 ? a->weight_gpu_memory : a->weight_gpu_memory_ratio;
+}
+
+/* resourceAllocationScorer over (requested, allocatable) pairs (scoring.go:254-308) */
+static int64_t dev_scorer(const ko_sched *s, const int64_t *total, const int64_t *free, const int64_t *podreq) {
+  int most = s->cfg.deviceshare.strategy == KS_MOST_ALLOCATED;
+  int64_t node_score = 0, weight_sum = 0;
+  for (int r = 0; r < 3; r++) {
+    int64_t w = dev_weight(s, r);
+    if (w == 0 || total[r] == 0) continue;
+    int64_t req = total[r];
+    if (total[r] >= free[r]) req = total[r] - free[r] + podreq[r];
+    node_score += (most ? ko_most_requested_score(req, total[r]) : ko_least_requested_score(req, total[r])) * w;
+    weight_sum += w;
+  }
+  return weight_sum ? node_score / weight_sum : 0;
+}
+
+/* defaultAllocateDevices: the free minors sorted by (scoreDevice desc, minor asc), the first `desired`
+ * that satisfy LessThanOrEqual(request, free).  Returns the minor mask, 0 if fewer fit. */
+static uint32_t dev_allocate(const ko_sched *s, int64_t n, const ko_gpureq *g) {
+  int64_t sc[KO_GPUS];
+  int ok[KO_GPUS];
+  int64_t podreq[3] = {g->has_core ? g->req[0] : 0, g->req[1], g->req[2]};
+  for (int k = 0; k < KO_GPUS; k++) {
+    const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
+    int64_t free[3] = {t[0] - u[0], t[1] - u[1], t[2] - u[2]};
+    ok[k] = 0;
+    sc[k] = 0;
+    if (!(t[0] || t[1] || t[2])) continue;           /* no such minor */
+    if (!(free[0] || free[1] || free[2])) continue;  /* fully used: dropped from deviceFree */
+    int fits = (!g->has_core || g->req[0] <= free[0]) && g->req[1] <= free[1] && g->req[2] <= free[2];
+    ok[k] = fits;
+    sc[k] = dev_scorer(s, t, free, podreq);
+  }
+  uint32_t mask = 0;
+  for (int got = 0; got < g->desired; got++) {
+    int best = -1;
+    for (int k = 0; k < KO_GPUS; k++)
+      if (ok[k] && !((mask >> k) & 1u) && (best < 0 || sc[k] > sc[best])) best = k;
+    if (best < 0) return 0;
+    mask |= 1u << best;
+  }
+  return mask;
+}
+
+/* DeviceShare Filter; *raw gets the node score (scoreNode) when feasible */
+static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *raw) {
+  *raw = 0;
+  if (!s->cfg.deviceshare.enable || !p->has_gpu) return 0;
+  if (!s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return 0; /* no device info: pass, score 0 */
+  ko_gpureq g;
+  uint32_t r = dev_prepare(s, p, n, &g);
+  if (r) return r;
+  if (!dev_allocate(s, n, &g)) return KS_R_DEV_INSUFFICIENT;
+  int64_t total[3] = {0, 0, 0}, free[3] = {0, 0, 0};
+  for (int k = 0; k < KO_GPUS; k++) {
+    const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
+    if (!(t[0] || t[1] || t[2])) continue;
+    int64_t f[3] = {t[0] - u[0], t[1] - u[1], t[2] - u[2]};
+    for (int q = 0; q < 3; q++) total[q] += t[q];
+    if (f[0] || f[1] || f[2])
+      for (int q = 0; q < 3; q++) free[q] += f[q];
+  }
+  int64_t podreq[3] = {g.has_core ? g.req[0] : 0, g.req[1], g.req[2]};
+  *raw = dev_scorer(s, total, free, podreq);
+  return 0;
+}
+
+/* Reserve -> nodeDevice.updateCacheUsed: used += the allocation on each chosen minor */
+static uint32_t dev_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
+  if (!s->cfg.deviceshare.enable || !p->has_gpu || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return 0;
+  ko_gpureq g;
+  if (dev_prepare(s, p, n, &g)) return 0;
+  uint32_t mask = dev_allocate(s, n, &g);
+  for (int k = 0; k < KO_GPUS; k++) {
+    if (!((mask >> k) & 1u)) continue;
+    int64_t *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
+    if (g.has_core) u[0] += g.req[0];
+    u[1] += g.req[1];
+    u[2] += g.req[2];
+  }
+  return mask;
+}
+
 /* NodeInfo.AddPod (upstream) + podAssignCache.assign (pod_assign_cache.go:53) */
 static void node_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
   ko_nodes *d = &s->nd;
@@ -820,6 +974,7 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   s->nom = (int32_t *)calloc(nn, 4);
   s->rraw = (int64_t *)calloc(nn, 8);
   s->rord = (int64_t *)calloc(nn, 8);
+  s->draw = (int64_t *)calloc(nn, 8);
   s->rv.beg = (int32_t *)calloc(nn + 1, 4);
   s->nthreads = nthreads < 1 ? 1 : nthreads;
   s->pool = pool_create(s->nthreads);
@@ -837,6 +992,10 @@ void ko_destroy(ko_sched *s) {
   free(s->nom);
   free(s->rraw);
   free(s->rord);
+  free(s->draw);
+  free(s->dv.flags);
+  free(s->dv.total);
+  free(s->dv.used);
   ko_rsv *rv = &s->rv;
   free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
   free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
@@ -892,6 +1051,43 @@ int ko_load_reservations(ko_sched *s, const ks_reservation_cols *rc, int32_t nr)
   return 0;
 }
 
+int ko_load_devices(ko_sched *s, const ks_device_cols *dc) {
+  size_t nn = (size_t)(s->n > 0 ? s->n : 1);
+  free(s->dv.flags);
+  free(s->dv.total);
+  free(s->dv.used);
+  s->dv.flags = (uint32_t *)calloc(nn, 4);
+  s->dv.total = (int64_t *)calloc(nn * KO_GPUS * 3, 8);
+  s->dv.used = (int64_t *)calloc(nn * KO_GPUS * 3, 8);
+  for (int64_t n = 0; n < s->n; n++) {
+    s->dv.flags[n] = colvu32(dc->flags, n);
+    for (int k = 0; k < KO_GPUS; k++) {
+      int64_t *t = s->dv.total + ((size_t)n * KO_GPUS + k) * 3, *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
+      t[0] = colv64(dc->total_core[k], n);
+      t[1] = colv64(dc->total_memory[k], n);
+      t[2] = colv64(dc->total_ratio[k], n);
+      u[0] = colv64(dc->used_core[k], n);
+      u[1] = colv64(dc->used_memory[k], n);
+      u[2] = colv64(dc->used_ratio[k], n);
+    }
+  }
+  s->dv.loaded = 1;
+  return 0;
+}
+
+/* used amounts, [k*n + node] per minor k */
+int ko_read_devices(const ko_sched *s, int64_t *used_core, int64_t *used_memory, int64_t *used_ratio) {
+  for (int64_t n = 0; n < s->n; n++)
+    for (int k = 0; k < KO_GPUS; k++) {
+      const int64_t *u = s->dv.used ? dev_used(s, n, k) : NULL;
+      size_t o = (size_t)k * s->n + n;
+      if (used_core) used_core[o] = u ? u[0] : 0;
+      if (used_memory) used_memory[o] = u ? u[1] : 0;
+      if (used_ratio) used_ratio[o] = u ? u[2] : 0;
+    }
+  return 0;
+}
+
 int ko_read_reservations(const ko_sched *s, int64_t *allocated, int32_t *assigned) {
   if (allocated) memcpy(allocated, s->rv.allocd, (size_t)s->rv.nr * KO_D * 8);
   if (assigned) memcpy(assigned, s->rv.assigned, (size_t)s->rv.nr * 4);
@@ -929,9 +1125,11 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_
   ko_rstate st;
   rsv_restore(s, p, n, &st);
   uint32_t r = rsv_filter(s, p, n, &st);
+  int64_t draw = 0;
   /* a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
    * NodeNames, plugin.go:235-246) before any Filter plugin runs */
-  if (r != KS_R_RSV_AFFINITY) r |= filter_node(s, p, n, &st.e);
+  if (r != KS_R_RSV_AFFINITY) r |= filter_node(s, p, n, &st.e) | dev_eval(s, p, n, &draw);
+  s->draw[n] = r ? 0 : draw;
   s->nom[n] = -1;
   s->rraw[n] = 0;
   s->rord[n] = 0;
@@ -956,6 +1154,23 @@ static void filter_piece(void *v, int64_t lo, int64_t hi) {
 /* Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and
  * DefaultNormalizeScore (normalize_score.go:24-52) over the feasible nodes, weighted into total[].
  * norm (optional) receives the normalized per-node score. */
+/* DeviceShare NormalizeScore = DefaultNormalizeScore(100) over the feasible nodes, weighted into total[] */
+static void dev_normalize(ko_sched *s, int64_t *norm) {
+  if (!s->cfg.deviceshare.enable) return;
+  int64_t mx = 0;
+  for (int64_t n = 0; n < s->n; n++)
+    if (s->total[n] >= 0 && s->draw[n] > mx) mx = s->draw[n];
+  for (int64_t n = 0; n < s->n; n++) {
+    if (s->total[n] < 0) {
+      if (norm) norm[n] = 0;
+      continue;
+    }
+    int64_t sc = mx == 0 ? s->draw[n] : MAX_NODE_SCORE * s->draw[n] / mx;
+    if (norm) norm[n] = sc;
+    s->total[n] += sc * s->cfg.deviceshare.plugin_weight;
+  }
+}
+
 static void rsv_normalize(ko_sched *s, int64_t *norm) {
   if (!s->cfg.reservation.enable) return;
   int64_t sel = INT64_MAX, pref = -1, mx = 0;
@@ -989,11 +1204,12 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     out[i].node = -1;
     out[i].score = 0;
     out[i].reservation = -1;
-    out[i]._pad0 = 0;
+    out[i].gpu_minors = 0;
     out[i].status = quota_prefilter(s, &p);
     if (out[i].status) continue;
     sweep_arg a = {s, &p};
     pool_until(s->pool, s->n, filter_piece, &a);
+    dev_normalize(s, NULL);
     rsv_normalize(s, NULL);
     /* prioritizeNodes sum + selectHost: max score, lowest index on ties */
     int64_t best = -1, best_n = -1;
@@ -1013,6 +1229,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
       out[i].reservation = s->nom[best_n];
       rsv_reserve(s, &p, s->nom[best_n]);
     }
+    out[i].gpu_minors = dev_reserve(s, &p, best_n);
     node_reserve(s, &p, best_n);
     quota_reserve(s, &p);
   }
@@ -1034,12 +1251,16 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
     }
   }
   int64_t *norm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
+  int64_t *dnorm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
+  dev_normalize(s, dnorm);
   rsv_normalize(s, norm);
   for (int64_t n = 0; n < s->n; n++) {
     if (scores && s->cfg.reservation.enable) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = norm[n];
+    if (scores) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = s->cfg.deviceshare.enable ? dnorm[n] : 0;
     if (total) total[n] = s->total[n];
   }
   free(norm);
+  free(dnorm);
   return 0;
 }
 

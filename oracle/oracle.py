@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 from koordinator_amd import abi
-from koordinator_amd.cluster import NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
+from koordinator_amd.cluster import DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
@@ -41,6 +41,8 @@ def lib():
         L.ko_load_quotas.argtypes = [C.c_void_p, C.POINTER(abi.KsQuotaCols), C.c_int32]
         L.ko_load_reservations.argtypes = [C.c_void_p, C.POINTER(abi.KsReservationCols), C.c_int32]
         L.ko_read_reservations.argtypes = [C.c_void_p, abi.P64, abi.P32]
+        L.ko_load_devices.argtypes = [C.c_void_p, C.POINTER(abi.KsDeviceCols)]
+        L.ko_read_devices.argtypes = [C.c_void_p, abi.P64, abi.P64, abi.P64]
         L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
         L.ko_eval_pod.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
         L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
@@ -59,7 +61,7 @@ class Oracle:
     """Sequential one-pod-at-a-time scheduler on the CPU (reduced form)."""
 
     def __init__(self, cfg: abi.KsConfig, nodes: NodeTable, quotas: QuotaTable | None = None, nthreads: int = 1,
-                 reservations: ReservationTable | None = None):
+                 reservations: ReservationTable | None = None, devices: DeviceTable | None = None):
         self.L = lib()
         self.cfg = cfg
         self.n = nodes.n
@@ -76,6 +78,9 @@ class Oracle:
             if self.L.ko_load_reservations(self.h, C.byref(self._r), reservations.r) != 0:
                 raise ValueError("reservation row references an unknown node")
             self.nr = reservations.r
+        if devices is not None:
+            self._d = devices.ks()
+            self.L.ko_load_devices(self.h, C.byref(self._d))
 
     def close(self):
         if self.h:
@@ -94,7 +99,7 @@ class Oracle:
         self.L.ko_schedule(self.h, C.byref(cols), pods.n, out)
         arr = np.frombuffer(out, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS), count=pods.n)
         return {"node": arr["node"].copy(), "status": arr["status"].copy(), "score": arr["score"].copy(),
-                "reservation": arr["reservation"].copy()}
+                "reservation": arr["reservation"].copy(), "gpu_minors": arr["gpu_minors"].copy()}
 
     def eval_pod(self, pod: PodTable):
         reasons = np.zeros(self.n, np.uint32)
@@ -116,6 +121,12 @@ class Oracle:
         assigned = np.zeros(max(self.nr, 1), np.int32)
         self.L.ko_read_reservations(self.h, allocated.ctypes.data_as(abi.P64), assigned.ctypes.data_as(abi.P32))
         return allocated[: self.nr * abi.KS_RSV_DIMS].reshape(self.nr, abi.KS_RSV_DIMS), assigned[: self.nr]
+
+    def read_devices(self):
+        G = abi.KS_MAX_GPUS
+        out = [np.zeros(G * max(self.n, 1), np.int64) for _ in range(3)]
+        self.L.ko_read_devices(self.h, *[o.ctypes.data_as(abi.P64) for o in out])
+        return tuple(o[: G * self.n].reshape(G, self.n) for o in out)
 
     def read_quota_used(self) -> np.ndarray:
         used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)
