@@ -41,6 +41,8 @@ def build_workload(name: str, seed: int):
         return synth.c2(seed=seed)
     if name == "c1":
         return synth.c1(seed=seed)
+    if name == "c3":
+        return synth.c3(seed=seed)
     if name == "c4":
         return synth.c4(seed=seed)
     if name == "c5":
@@ -57,15 +59,16 @@ def cpu_baseline(w, gpu_res, budget_s: float):
     # estimate the prefix that fits the budget from a short probe
     probe = min(w.pods.n, 500)
     rs = w.reservations
+    dv = w.devices
     o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None)
+               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None)
     t = time.perf_counter()
     r_probe = o.schedule(w.pods.rows(range(probe)))
     dt = time.perf_counter() - t
     o.close()
     n_sample = w.pods.n if dt * w.pods.n / probe <= budget_s else max(probe, int(budget_s * probe / dt))
     o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None)
+               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None)
     t = time.perf_counter()
     r = o.schedule(w.pods.rows(range(n_sample)))
     dt = time.perf_counter() - t
@@ -73,7 +76,8 @@ def cpu_baseline(w, gpu_res, budget_s: float):
     parity = bool(np.array_equal(r["node"], gpu_res["node"][:n_sample])
                   and np.array_equal(r["status"], gpu_res["status"][:n_sample])
                   and np.array_equal(r["score"], gpu_res["score"][:n_sample])
-                  and np.array_equal(r["reservation"], gpu_res["reservation"][:n_sample]))
+                  and np.array_equal(r["reservation"], gpu_res["reservation"][:n_sample])
+                  and np.array_equal(r["gpu_minors"], gpu_res["gpu_minors"][:n_sample]))
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -103,7 +107,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="do not bracket kernels with HIP events")
@@ -136,7 +140,7 @@ def main():
     prof.candidates = args.candidates
     cfg = prof.to_ks_config()
     cfg.profile = 0 if args.no_profile else 1
-    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations)
+    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices)
     if args.shard or args.vshards > 1:
         uid = None
         if world > 1:
@@ -193,6 +197,9 @@ def main():
             b_node = 8 * 15 + 4 * 3 + 16 * 2  # LA+Fit columns + batch-cpu/batch-memory scalar columns
             local_nodes = n_nodes // (world if args.shard else 1)  # one rank sweeps its shard
             algo = local_nodes * b_node + 64 * 128 + ((local_nodes + 63) // 64) * 64 * 4
+            if w.devices is not None:
+                # + NUMA amplification columns (16 B) and the GPU table (flags + 2 x 3 x 8 int64)
+                algo += local_nodes * (16 + 4 + 2 * 3 * 8 * 8)
             if w.reservations is not None:
                 # + the owner-class column and the reservation table (CSR offsets, classes, meta, order rank,
                 # allocatable/allocated x7, assigned, reserve-pod non-zero x2) read once
@@ -217,7 +224,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{w.name}: {n_pods} pods x {n_nodes} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
                                    f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
-                                   + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else ""),
+                                   + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else "")
+                                   + (" + NodeNUMAResource(non-cpuset) + DeviceShare(GPU, 8x80GiB/node)" if w.devices is not None else ""),
                        "pods_per_step": n_pods, "nodes": n_nodes, "percentage_of_nodes_to_score": 100,
                        "parallelism": (f"node-shards{world}x{args.vshards}" if args.shard or args.vshards > 1
                                        else (f"replicas{world}" if world > 1 else "single-gpu")),
@@ -225,6 +233,7 @@ def main():
             "node_evals_per_s": round(value * n_nodes, 1),
             "placed_per_step": int((res["status"] == 0).sum()),
             "into_reservations_per_step": int((res["reservation"] >= 0).sum()),
+            "gpu_pods_placed_per_step": int((res["gpu_minors"] != 0).sum()),
             "passes_per_step": agg["passes"] / args.steps,
             "cut_passes_per_step": agg["cut_passes"] / args.steps,
             "rescans_per_step": agg["rescans"] / args.steps,

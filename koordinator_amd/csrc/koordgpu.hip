@@ -2816,26 +2816,32 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.total_pods = ctx->np;
   sa.batch = ctx->batch;
   sa.ppw = ppw;
-  rec(0);
   const int feat = kernel_feat(ctx);
   sa.dv = ctx->ddv;
   sa.dev_M = ctx->dev_M;
   sa.phase = 1;
   if (feat == 7) {
-    // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys
+    // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
+    // each launch is timed on its own (the roofline is per sweep launch)
     (void)hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream);
     sa.phase = 0;
+    rec(0);
     hipLaunchKernelGGL((sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    rec(0);
     if (ctx->nranks > 1)
       (void)ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ctx->stream);
     sa.phase = 1;
+    rec(0);
     hipLaunchKernelGGL((sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
-  } else if (feat == 3)
-    hipLaunchKernelGGL((sweep_kernel<NSC, 3>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
-  else if (feat == 1)
-    hipLaunchKernelGGL((sweep_kernel<NSC, 1>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
-  else
-    hipLaunchKernelGGL((sweep_kernel<NSC, 0>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  } else {
+    rec(0);
+    if (feat == 3)
+      hipLaunchKernelGGL((sweep_kernel<NSC, 3>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    else if (feat == 1)
+      hipLaunchKernelGGL((sweep_kernel<NSC, 1>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    else
+      hipLaunchKernelGGL((sweep_kernel<NSC, 0>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+  }
   rec(0);
   SelectArgs se;
   se.in = ctx->sweep_out;

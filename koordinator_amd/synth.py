@@ -7,6 +7,11 @@ would produce from a scheduler-cache snapshot plus NodeMetric objects:
 * C1  500 nodes, 1k pods, NodeResourcesFit + LoadAwareScheduling
 * C2  5k nodes, 10k pods, + ElasticQuota admission (32 leaf quotas under root,
       limits sized so roughly a tenth of the pods are rejected)
+* C3  5k nodes with 8 (or 4) 80 GiB GPUs each (make_devices) and cpu amplification ratios with
+      cpuset-held CPUs (NodeNUMAResource); 10k pods, 40 % requesting GPUs (whole devices 1/2/4, half a
+      GPU by ratio, or a gpu-memory amount); Fit + LoadAware + NodeNUMAResource + DeviceShare.  The
+      reference's C3 also has cpuset (LSR) pods and GPU+RDMA joint allocation, which this build
+      does not model
 * C4  20k nodes with 50k reservations (make_reservations), 10k pods of which 60 % belong to one
       of 16 reservation owner classes, NodeResourcesFit + LoadAwareScheduling + Reservation (weight 5000)
 * C5  100k nodes, C1 pod distribution (the multi-GPU sharding config)
@@ -57,6 +62,7 @@ class Workload:
     pods: PodTable
     quotas: Optional[QuotaTable]
     reservations: Optional[ReservationTable] = None
+    devices: Optional["DeviceTable"] = None
 
     @property
     def cfg(self) -> abi.KsConfig:
@@ -267,6 +273,23 @@ def c2(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, n_quotas: int
     pods = make_pods(n_pods, rng, n_quotas)
     quotas = make_quotas(pods, n_quotas, rng)
     return Workload("C2", koord_profile(with_quota=True, **kw), nodes, pods, quotas)
+
+
+def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, **kw) -> Workload:
+    from .config import GPU_MEMORY_RATIO, DeviceShareArgs, NodeNUMAResourceArgs
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = make_nodes(n_nodes, rng)
+    ratio = rng.choice(np.array([0.0, 1.0, 1.5, 2.0]), n_nodes)
+    amp = ratio > 1
+    nodes.numa_cpu_amplification[:] = ratio
+    nodes.alloc_milli_cpu[amp] = np.ceil(nodes.alloc_milli_cpu[amp] * ratio[amp]).astype(np.int64)
+    nodes.numa_cpuset_cpus[:] = np.where(rng.random(n_nodes) < 0.5, rng.integers(0, 16, n_nodes), 0)
+    devs = make_devices(nodes, rng)
+    pods = gpu_pods(make_pods(n_pods, rng), rng)
+    prof = koord_profile(**kw)
+    prof.numa = NodeNUMAResourceArgs()
+    prof.deviceshare = DeviceShareArgs(resources={GPU_MEMORY_RATIO: 1})
+    return Workload("C3", prof, nodes, pods, None, None, devs)
 
 
 def c4(seed: int = SEED, n_nodes: int = 20_000, n_reservations: int = 50_000, n_pods: int = 10_000, **kw) -> Workload:
