@@ -50,6 +50,27 @@ def build_workload(name: str, seed: int):
     raise SystemExit(f"unknown config {name}")
 
 
+def pmc_traffic(config: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary for this config
+    (profiles/rNN_<config>_traffic.json, written by tools/pmc_traffic.sh + tools/traffic.py from
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command); None when absent."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"r*_{config}_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    n = b = 0
+    for k, v in t.get("kernels", {}).items():
+        if kernel in k:
+            n += v["launches"]
+            b += v["hbm_bytes_per_launch"] * v["launches"]
+    if not n:
+        return None, None
+    return round(b / n), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+
+
 def cpu_baseline(w, gpu_res, budget_s: float):
     """Time the CPU oracle (port of the reference loop) on a bounded prefix of the workload."""
     from oracle.oracle import Oracle
@@ -205,8 +226,9 @@ def main():
                 # allocatable/allocated x7, assigned, reserve-pod non-zero x2) read once
                 algo += local_nodes * (8 + 4) + w.reservations.r * (8 + 4 + 4 + 7 * 8 * 2 + 4 + 16)
             achieved = algo / avg_s / 1e9
+            traffic, traffic_src = pmc_traffic(args.config, "sweep_kernel")
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
                         "kernel": "sweep_kernel", "avg_launch_us": round(avg_s * 1e6, 3),
                         "algorithmic_bytes_per_launch": algo, "bytes_incl_pod_group_rereads": sweep_bytes}
         out = {

@@ -186,8 +186,13 @@ struct SweepArgs {
 template <int NSC, int FEAT>
 __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const int lane = threadIdx.x & 63;
-  // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar)
-  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar).
+  // XCD-aware: blocks are dealt round-robin over the 8 XCDs, so block b works as virtual block
+  // (b % 8) * (grid / 8) + b / 8 — each XCD gets a contiguous run of work items, i.e. every pod
+  // group of a node chunk is swept on one XCD and the chunk's columns are fetched into one L2 only.
+  // The host launches a multiple of 8 blocks.
+  const uint32_t vblock = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int64_t wave = (int64_t)vblock * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor >= a.total_pods) return;
@@ -2991,7 +2996,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   while (ppw > 4 && local_chunks * (ctx->batch / ppw) < 4096) ppw >>= 1;
   if (ppw > ctx->batch) ppw = ctx->batch;
   const int64_t nwork = std::max<int64_t>(local_chunks, 1) * ((ctx->batch + ppw - 1) / ppw);
-  const int sweep_blocks = (int)std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048));
+  const int sweep_blocks = (int)((std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048)) + 7) & ~7ll);  // % 8 == 0 (XCD swizzle)
   hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 256, ctx->stream));

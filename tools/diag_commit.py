@@ -1,13 +1,14 @@
 """Diagnostic: per-phase cycle split of the commit kernel (needs libkoordgpu_diag.so, -DKS_COMMIT_STAMPS).
-usage: python tools/diag_commit.py [c2|c4]"""
+usage: python tools/diag_commit.py [c2|c3|c4]"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("KS_LIB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "koordinator_amd", "libkoordgpu_diag.so"))
 from koordinator_amd import runtime, synth
-w = synth.c4() if (len(sys.argv) > 1 and sys.argv[1] == "c4") else synth.c2()
+which = sys.argv[1] if len(sys.argv) > 1 else "c2"
+w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4}[which]()
 cfg = w.cfg
 cfg.profile = 1
-ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations)
+ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices)
 ev.stage(w.pods)
 ev.checkpoint()
 for i in range(3):
