@@ -20,8 +20,8 @@ LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(HERE, "koord_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(HERE, f) for f in ("koord_oracle.c", "cpu_accumulator.c", "cpu_accumulator.h")]
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", HERE])
     return LIB_PATH
 
@@ -53,8 +53,59 @@ def lib():
         L.ko_most_requested_score.argtypes = [C.c_int64, C.c_int64]
         L.ko_estimated_used.restype = C.c_int64
         L.ko_estimated_used.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int64]
+        L.ko_take_cpus.restype = C.c_int
+        L.ko_take_cpus.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                   C.c_int, C.c_void_p]
+        L.ko_spread_order.restype = C.c_int
+        L.ko_spread_order.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.ko_topo_finish.argtypes = [C.c_void_p]
         _lib = L
     return _lib
+
+
+KO_MAX_CPUS = 256
+EXCL = {"None": 0, "PCPULevel": 1, "NUMANodeLevel": 2}
+BIND = {"FullPCPUs": 1, "SpreadByPCPUs": 2}
+STRATEGY = {"Most": 0, "Least": 1}
+
+
+class KoTopo(C.Structure):
+    _fields_ = [("ncpus", C.c_int), ("core", C.c_int * KO_MAX_CPUS), ("node", C.c_int * KO_MAX_CPUS),
+                ("socket", C.c_int * KO_MAX_CPUS), ("num_cores", C.c_int), ("num_nodes", C.c_int),
+                ("num_sockets", C.c_int)]
+
+
+def topo_from_ids(core, node, socket) -> KoTopo:
+    t = KoTopo()
+    t.ncpus = len(core)
+    for i in range(len(core)):
+        t.core[i], t.node[i], t.socket[i] = int(core[i]), int(node[i]), int(socket[i])
+    lib().ko_topo_finish(C.byref(t))
+    return t
+
+
+def take_cpus(t: KoTopo, avail, needed: int, bind: str, excl: str = "None", strategy: str = "Most",
+              max_ref: int = 1, refcount=None, alloc_excl=None):
+    """takeCPUs on the oracle; returns the sorted CPU list or None on error."""
+    n = t.ncpus
+    av = np.zeros(KO_MAX_CPUS, np.uint8)
+    av[:n] = np.asarray(avail, np.uint8)[:n]
+    rc = np.zeros(KO_MAX_CPUS, np.int32)
+    if refcount is not None:
+        rc[:n] = refcount
+    ex = np.full(KO_MAX_CPUS, -1, np.int8)
+    if alloc_excl is not None:
+        ex[:n] = alloc_excl
+    out = np.zeros(KO_MAX_CPUS, np.uint8)
+    rv = lib().ko_take_cpus(C.byref(t), max_ref, av.ctypes.data, rc.ctypes.data, ex.ctypes.data, needed,
+                            BIND[bind], EXCL[excl], STRATEGY[strategy], out.ctypes.data)
+    return None if rv != 0 else [int(c) for c in np.nonzero(out[:n])[0]]
+
+
+def spread_order(t: KoTopo, strategy: str = "Most"):
+    out = np.zeros(KO_MAX_CPUS, np.int32)
+    k = lib().ko_spread_order(C.byref(t), STRATEGY[strategy], out.ctypes.data)
+    return [int(x) for x in out[:k]]
 
 
 class Oracle:
