@@ -82,23 +82,27 @@ def cpu_baseline(w, gpu_res, budget_s: float):
     rs = w.reservations
     dv = w.devices
     o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None)
+               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None,
+               cpu_state=w.cpus.copy() if w.cpus is not None else None)
     t = time.perf_counter()
     r_probe = o.schedule(w.pods.rows(range(probe)))
     dt = time.perf_counter() - t
     o.close()
     n_sample = w.pods.n if dt * w.pods.n / probe <= budget_s else max(probe, int(budget_s * probe / dt))
     o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None)
+               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None,
+               cpu_state=w.cpus.copy() if w.cpus is not None else None)
     t = time.perf_counter()
     r = o.schedule(w.pods.rows(range(n_sample)))
     dt = time.perf_counter() - t
+    cs = o.fetch_cpusets(n_sample) if w.cpus is not None else None
     o.close()
     parity = bool(np.array_equal(r["node"], gpu_res["node"][:n_sample])
                   and np.array_equal(r["status"], gpu_res["status"][:n_sample])
                   and np.array_equal(r["score"], gpu_res["score"][:n_sample])
                   and np.array_equal(r["reservation"], gpu_res["reservation"][:n_sample])
-                  and np.array_equal(r["gpu_minors"], gpu_res["gpu_minors"][:n_sample]))
+                  and np.array_equal(r["gpu_minors"], gpu_res["gpu_minors"][:n_sample])
+                  and (cs is None or np.array_equal(cs, gpu_res["cpusets"][:n_sample])))
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -151,7 +155,7 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from koordinator_amd import runtime
+    from koordinator_amd import abi, runtime
 
     # replicas schedule their own cluster (seed + rank); shards split one shared cluster
     w = build_workload(args.config, seed=20261015 + (0 if args.shard else rank))
@@ -161,7 +165,7 @@ def main():
     prof.candidates = args.candidates
     cfg = prof.to_ks_config()
     cfg.profile = 0 if args.no_profile else 1
-    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices)
+    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices, w.cpus)
     if args.shard or args.vshards > 1:
         uid = None
         if world > 1:
@@ -203,6 +207,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     res = ev.fetch()
+    if w.cpus is not None:
+        res["cpusets"] = ev.fetch_cpusets(w.pods.n)
 
     n_pods, n_nodes = w.pods.n, w.nodes.n
     total_pods = n_pods * args.steps * (1 if args.shard else world)
@@ -247,7 +253,7 @@ def main():
             "config": {"workload": f"{w.name}: {n_pods} pods x {n_nodes} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
                                    f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
                                    + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else "")
-                                   + (" + NodeNUMAResource(non-cpuset) + DeviceShare(GPU, 8x80GiB/node)" if w.devices is not None else ""),
+                                   + (" + NodeNUMAResource(amplified CPUs, cpuset pods) + DeviceShare(GPU, 8x80GiB/node)" if w.devices is not None else ""),
                        "pods_per_step": n_pods, "nodes": n_nodes, "percentage_of_nodes_to_score": 100,
                        "parallelism": (f"node-shards{world}x{args.vshards}" if args.shard or args.vshards > 1
                                        else (f"replicas{world}" if world > 1 else "single-gpu")),
@@ -256,6 +262,7 @@ def main():
             "placed_per_step": int((res["status"] == 0).sum()),
             "into_reservations_per_step": int((res["reservation"] >= 0).sum()),
             "gpu_pods_placed_per_step": int((res["gpu_minors"] != 0).sum()),
+            "cpuset_pods_placed_per_step": int(((res["status"] == 0) & ((w.pods.flags & abi.KS_POD_CPU_BIND) != 0)).sum()),
             "passes_per_step": agg["passes"] / args.steps,
             "cut_passes_per_step": agg["cut_passes"] / args.steps,
             "rescans_per_step": agg["rescans"] / args.steps,

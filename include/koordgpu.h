@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 2
+#define KS_ABI_VERSION 3
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -56,6 +56,8 @@ extern "C" {
 #define KS_RSV_DIMS (3 + KS_MAX_SCALARS) /* reservation resources: cpu, memory, ephemeral-storage, scalar[k] */
 #define KS_RSV_CLASSES 64 /* pod match classes (ks_reservation_cols.owner_classes bits) */
 #define KS_MAX_GPUS 8     /* GPU minors per node (ks_device_cols); minor = slot index */
+#define KS_MAX_CPUS 256   /* logical CPUs per node topology (ks_cpu_topology); CPU ids 0..ncpus-1 */
+#define KS_CPU_WORDS 4    /* uint64 words of a CPU set (bit c = CPU c) */
 
 /* ---- status codes ---- */
 #define KS_OK 0
@@ -88,7 +90,9 @@ extern "C" {
 #define KS_POD_SCALAR_KEYS 0x08u     /* podRequest.ScalarResources has at least one key (upstream fitsRequest) */
 #define KS_POD_RSV_AFFINITY 0x10u    /* GetRequiredReservationAffinity != nil (reservation/transformer.go:51, stateData.hasAffinity) */
 #define KS_POD_CPU_BIND 0x20u        /* NodeNUMAResource preFilterState.requestCPUBind (nodenumaresource/plugin.go:236-262):
-                                        cpuset allocation is not supported by this build (KS_EUNSUPPORTED) */
+                                        a preferred FullPCPUs / SpreadByPCPUs policy of an LSE/LSR prod pod with a whole-CPU
+                                        request; policy and exclusive policy in ks_pod_cols.cpu_bind.  A required bind
+                                        policy (resourceSpec.requiredCPUBindPolicy) is not supported (KS_EUNSUPPORTED) */
 #define KS_POD_GPU_CORE 0x40u        /* DeviceShare: the converted GPU request has a gpu-core key (deviceshare/utils.go:96-146) */
 #define KS_POD_GPU_MEMORY 0x80u      /* DeviceShare: gpu-memory given (ratio derived per node, devicehandler_gpu.go:71-89);
                                         otherwise gpu-memory-ratio given (memory derived) */
@@ -97,6 +101,17 @@ extern "C" {
 #define KS_NUMA_INVALID_RATIO 0x1u   /* GetNodeResourceAmplificationRatio returned an error (plugin.go:348-351)   */
 #define KS_NUMA_CPU_BIND_POLICY 0x2u /* node CPU bind policy label != None (GetNodeCPUBindPolicy): unsupported   */
 #define KS_NUMA_TOPOLOGY_POLICY 0x4u /* NUMA topology policy != None (getNUMATopologyPolicy): unsupported         */
+#define KS_NUMA_ALLOC_LEAST 0x8u     /* label numa-allocate-strategy = LeastAllocated (GetNUMAAllocateStrategy, util.go:30-36) */
+#define KS_NUMA_ALLOC_MOST 0x10u     /* label numa-allocate-strategy = MostAllocated                                */
+
+/* ---- pod cpuset request (ks_pod_cols.cpu_bind, with KS_POD_CPU_BIND) ---- */
+#define KS_CPU_BIND_FULL_PCPUS 1u       /* schedulingconfig.CPUBindPolicyFullPCPUs     */
+#define KS_CPU_BIND_SPREAD_BY_PCPUS 2u  /* schedulingconfig.CPUBindPolicySpreadByPCPUs */
+#define KS_CPU_BIND_POLICY_MASK 0x3u
+#define KS_CPU_EXCL_SHIFT 2             /* bits 2-3: preferredCPUExclusivePolicy */
+#define KS_CPU_EXCL_NONE 0u
+#define KS_CPU_EXCL_PCPU_LEVEL 1u
+#define KS_CPU_EXCL_NUMA_NODE_LEVEL 2u
 
 /* ---- per-node filter reason bits (ks_eval_pod_debug) ---- */
 #define KS_R_FIT_PODS 0x001u      /* "Too many pods"                                    */
@@ -114,6 +129,7 @@ extern "C" {
 #define KS_R_NUMA_INVALID_RATIO 0x1000u /* ErrInvalidCPUAmplificationRatio (plugin.go:348-351)                    */
 #define KS_R_DEV_INSUFFICIENT 0x2000u   /* DeviceShare "Insufficient gpu devices" (device_allocator.go:453-456)  */
 #define KS_R_DEV_NO_GPU 0x4000u         /* DeviceShare: node has no (healthy) GPU (devicehandler_gpu.go:41-50)  */
+#define KS_R_NUMA_INVALID_TOPOLOGY 0x8000u /* ErrInvalidCPUTopology: cpu-bind pod on a node without a valid CPU topology (plugin.go:296-301) */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -121,6 +137,9 @@ extern "C" {
 #define KS_S_QUOTA_NONPREEMPTIBLE 0x2u /* ElasticQuota PreFilter: "Insufficient non-preemptible quotas" */
 #define KS_S_QUOTA_PARENT 0x4u         /* checkQuotaRecursive rejected at a parent                 */
 #define KS_S_UNSCHEDULABLE 0x8u        /* no node passed Filter                                    */
+#define KS_S_RESERVE_FAILED 0x10u      /* a Reserve plugin failed on the selected node and every plugin unreserved
+                                          (NodeNUMAResource Allocate: "not enough cpus available", resource_manager.go:333-335);
+                                          node = the selected node, nothing is applied */
 
 /* score plugin slots for ks_eval_pod_debug's per-plugin score matrix */
 #define KS_SCORE_FIT 0
@@ -189,14 +208,19 @@ typedef struct ks_reservation_args {
 } ks_reservation_args;
 
 /* NodeNUMAResourceArgs.ScoringStrategy (pkg/scheduler/apis/config/types.go; defaults
- * v1beta2/defaults.go:107-136: LeastAllocated, cpu 1, memory 1).  Pods that request a cpuset
- * (KS_POD_CPU_BIND) and nodes with a CPU-bind or NUMA topology policy are not supported. */
+ * v1beta2/defaults.go:107-136: LeastAllocated, cpu 1, memory 1).  Nodes with a CPU-bind or NUMA
+ * topology policy are not supported; cpuset pods (KS_POD_CPU_BIND) are, on nodes whose CPU
+ * topology and allocation state were given to ks_load_cpu_state. */
 typedef struct ks_numa_args {
   int32_t enable;
   int32_t strategy; /* KS_LEAST_ALLOCATED | KS_MOST_ALLOCATED */
   int64_t weight_cpu;
   int64_t weight_memory;
   int64_t plugin_weight;
+  /* NUMAScoringStrategy.Type: the default NUMA allocate strategy of the CPU accumulator
+   * (GetDefaultNUMAAllocateStrategy, util.go:22-28): KS_MOST_ALLOCATED -> NUMAMostAllocated, else NUMALeastAllocated */
+  int32_t numa_scoring_strategy;
+  int32_t _pad0;
 } ks_numa_args;
 
 /* DeviceShareArgs.ScoringStrategy (defaults v1beta2/defaults.go:187-207: LeastAllocated,
@@ -299,6 +323,10 @@ typedef struct ks_pod_cols {
   const int64_t *gpu_core;
   const int64_t *gpu_memory;
   const int64_t *gpu_memory_ratio;
+  /* NodeNUMAResource cpuset request with KS_POD_CPU_BIND: KS_CPU_BIND_* | exclusive policy << KS_CPU_EXCL_SHIFT
+   * (preferredCPUBindPolicy after the args default, preferredCPUExclusivePolicy); numCPUsNeeded =
+   * req_milli_cpu / 1000 (a multiple of 1000).  NULL = none */
+  const uint32_t *cpu_bind;
 } ks_pod_cols;
 
 /* ElasticQuota table: QuotaInfo.CalculateInfo per quota (core/quota_info.go). */
@@ -359,6 +387,27 @@ typedef struct ks_device_cols {
   const int64_t *used_ratio[KS_MAX_GPUS];
 } ks_device_cols;
 
+/* A node CPU topology (CPUTopology, nodenumaresource/cpu_topology.go:27-33, built from the
+ * NodeResourceTopology): CPU c has core / NUMA node / socket ids (ids < KS_MAX_CPUS, at most 8 CPUs
+ * per core).  Nodes refer to a topology by index, so identical machines share one entry. */
+typedef struct ks_cpu_topology {
+  int32_t ncpus;
+  int32_t core[KS_MAX_CPUS];
+  int32_t numa_node[KS_MAX_CPUS];
+  int32_t socket[KS_MAX_CPUS];
+} ks_cpu_topology;
+
+/* Per-node CPU allocation state (NodeAllocation, node_allocation.go:37-177) as CPU sets of
+ * KS_CPU_WORDS words per node ([node*KS_CPU_WORDS + w]).  maxRefCount is 1 (every allocated CPU is
+ * unavailable).  The cpuset millicores of ks_node_cols.numa_cpuset_cpus must match |allocated|. */
+typedef struct ks_cpu_state_cols {
+  const int32_t *topology;      /* index into the topology table, -1 = no valid topology */
+  const uint64_t *allocated;    /* allocatedCPUs */
+  const uint64_t *excl_pcpu;    /* allocated with CPUExclusivePolicy PCPULevel; NULL = none */
+  const uint64_t *excl_numa;    /* allocated with CPUExclusivePolicy NUMANodeLevel; NULL = none */
+  const uint64_t *reserved;     /* kubelet reserved CPUs (TopologyOptions.ReservedCPUs); NULL = none */
+} ks_cpu_state_cols;
+
 typedef struct ks_result {
   int32_t node;    /* chosen node index, -1 if not scheduled */
   uint32_t status; /* KS_S_* */
@@ -414,6 +463,17 @@ int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
 int ks_load_devices(ks_ctx *ctx, const ks_device_cols *dev, int64_t n);
 /* used amounts after commits, [k*n + node] for minor k; NULL = skip */
 int ks_read_devices(ks_ctx *ctx, int64_t *used_core, int64_t *used_memory, int64_t *used_ratio);
+
+/* CPU topologies and per-node CPU allocation state for cpuset pods (NodeNUMAResource
+ * resourceManager / NodeAllocation, resource_manager.go:58-401); call after ks_load_nodes.  Reserve of
+ * a KS_POD_CPU_BIND pod allocates its CPUs with the CPU accumulator (takeCPUs, cpu_accumulator.go:86-232)
+ * and adds them to the node's allocation (NodeAllocation.addPodAllocation, node_allocation.go:75-100). */
+int ks_load_cpu_state(ks_ctx *ctx, const ks_cpu_topology *topologies, int32_t ntopo, const ks_cpu_state_cols *state);
+/* CPU sets after commits, [node*KS_CPU_WORDS + w]; NULL = skip */
+int ks_read_cpu_state(ks_ctx *ctx, uint64_t *allocated, uint64_t *excl_pcpu, uint64_t *excl_numa);
+/* The CPUs allocated to each pod of the last ks_schedule / ks_schedule_staged call ([pod*KS_CPU_WORDS + w],
+ * zero for pods without a cpuset), the PodAllocation.CPUSet written by PreBind */
+int ks_fetch_cpusets(ks_ctx *ctx, uint64_t *out, int32_t p);
 
 /* Reservation cache snapshot (reservation/cache.go:104-291) for the Reservation plugin's
  * BeforePreFilter restore (transformer.go:41-307), Filter (plugin.go:311-496), PreScore

@@ -8,10 +8,12 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 2
+KS_ABI_VERSION = 3
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
+KS_MAX_CPUS = 256
+KS_CPU_WORDS = 4
 KS_RSV_DIMS = 3 + KS_MAX_SCALARS
 KS_RSV_CLASSES = 64
 
@@ -47,6 +49,16 @@ KS_DEV_PRESENT = 0x1
 KS_NUMA_INVALID_RATIO = 0x1
 KS_NUMA_CPU_BIND_POLICY = 0x2
 KS_NUMA_TOPOLOGY_POLICY = 0x4
+KS_NUMA_ALLOC_LEAST = 0x8
+KS_NUMA_ALLOC_MOST = 0x10
+
+KS_CPU_BIND_FULL_PCPUS = 1
+KS_CPU_BIND_SPREAD_BY_PCPUS = 2
+KS_CPU_BIND_POLICY_MASK = 0x3
+KS_CPU_EXCL_SHIFT = 2
+KS_CPU_EXCL_NONE = 0
+KS_CPU_EXCL_PCPU_LEVEL = 1
+KS_CPU_EXCL_NUMA_NODE_LEVEL = 2
 
 KS_R_FIT_PODS = 0x001
 KS_R_FIT_CPU = 0x002
@@ -63,12 +75,14 @@ KS_R_NUMA_AMPLIFIED_CPU = 0x800
 KS_R_NUMA_INVALID_RATIO = 0x1000
 KS_R_DEV_INSUFFICIENT = 0x2000
 KS_R_DEV_NO_GPU = 0x4000
+KS_R_NUMA_INVALID_TOPOLOGY = 0x8000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
 KS_S_QUOTA_NONPREEMPTIBLE = 0x2
 KS_S_QUOTA_PARENT = 0x4
 KS_S_UNSCHEDULABLE = 0x8
+KS_S_RESERVE_FAILED = 0x10
 
 KS_SCORE_FIT = 0
 KS_SCORE_LOADAWARE = 1
@@ -126,7 +140,8 @@ class KsReservationArgs(C.Structure):
 
 class KsNumaArgs(C.Structure):
     _fields_ = [("enable", C.c_int32), ("strategy", C.c_int32), ("weight_cpu", C.c_int64),
-                ("weight_memory", C.c_int64), ("plugin_weight", C.c_int64)]
+                ("weight_memory", C.c_int64), ("plugin_weight", C.c_int64), ("numa_scoring_strategy", C.c_int32),
+                ("_pad0", C.c_int32)]
 
 
 class KsDeviceShareArgs(C.Structure):
@@ -212,6 +227,7 @@ POD_COLS = [
     ("gpu_core", P64),
     ("gpu_memory", P64),
     ("gpu_memory_ratio", P64),
+    ("cpu_bind", PU32),
 ]
 
 
@@ -276,6 +292,19 @@ class KsDeviceCols(C.Structure):
     ]
 
 
+class KsCpuTopology(C.Structure):
+    _fields_ = [("ncpus", C.c_int32), ("core", C.c_int32 * KS_MAX_CPUS), ("numa_node", C.c_int32 * KS_MAX_CPUS),
+                ("socket", C.c_int32 * KS_MAX_CPUS)]
+
+
+PU64 = C.POINTER(C.c_uint64)
+
+
+class KsCpuStateCols(C.Structure):
+    _fields_ = [("topology", P32), ("allocated", PU64), ("excl_pcpu", PU64), ("excl_numa", PU64),
+                ("reserved", PU64)]
+
+
 class KsResult(C.Structure):
     _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64), ("reservation", C.c_int32),
                 ("gpu_minors", C.c_uint32)]
@@ -330,6 +359,9 @@ EXPORTED_SYMBOLS = [
     "ks_load_quotas",
     "ks_load_devices",
     "ks_read_devices",
+    "ks_load_cpu_state",
+    "ks_read_cpu_state",
+    "ks_fetch_cpusets",
     "ks_load_reservations",
     "ks_read_reservations",
     "ks_refresh_quota_runtime",

@@ -37,7 +37,7 @@ POD_I64 = [
     "gpu_core", "gpu_memory", "gpu_memory_ratio",
 ]
 POD_I32 = ["quota", "rsv_class"]
-POD_U32 = ["flags", "quota_mask"]
+POD_U32 = ["flags", "quota_mask", "cpu_bind"]
 
 STATE_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral", "nonzero_milli_cpu", "nonzero_memory",
@@ -180,6 +180,7 @@ class PodTable(_Table):
         c.rsv_class = _p32(self.rsv_class)
         c.flags = _pu32(self.flags)
         c.quota_mask = _pu32(self.quota_mask)
+        c.cpu_bind = _pu32(self.cpu_bind)
         for k in range(abi.KS_MAX_SCALARS):
             c.req_scalar[k] = _p64(self.req_scalar[k])
         for d in range(abi.KS_QUOTA_DIMS):
@@ -291,6 +292,86 @@ class DeviceTable:
             field = getattr(c, name)
             for k in range(abi.KS_MAX_GPUS):
                 field[k] = _p64(arr[k])
+        c._keep = self
+        return c
+
+
+def cpu_topology(core, numa_node, socket) -> abi.KsCpuTopology:
+    """ks_cpu_topology from per-CPU ids (CPU c = index c)."""
+    t = abi.KsCpuTopology()
+    t.ncpus = len(core)
+    for i in range(len(core)):
+        t.core[i], t.numa_node[i], t.socket[i] = int(core[i]), int(numa_node[i]), int(socket[i])
+    return t
+
+
+def regular_topology(sockets: int, nodes_per_socket: int, cores_per_node: int, cpus_per_core: int) -> abi.KsCpuTopology:
+    """CPU ids in (socket, node, core, thread) order, like buildCPUTopologyForTest
+    (nodenumaresource/cpu_accumulator_test.go:30-57)."""
+    core, node, sock = [], [], []
+    cid = nid = 0
+    for s in range(sockets):
+        for _ in range(nodes_per_socket):
+            for _ in range(cores_per_node):
+                for _ in range(cpus_per_core):
+                    core.append(cid)
+                    node.append(nid)
+                    sock.append(s)
+                cid += 1
+            nid += 1
+    return cpu_topology(core, node, sock)
+
+
+def cpu_mask(cpus) -> np.ndarray:
+    """CPU list -> KS_CPU_WORDS uint64 words."""
+    m = np.zeros(abi.KS_CPU_WORDS, np.uint64)
+    for c in cpus:
+        m[c >> 6] |= np.uint64(1) << np.uint64(c & 63)
+    return m
+
+
+def mask_cpus(m) -> list:
+    out = []
+    for w in range(abi.KS_CPU_WORDS):
+        v = int(m[w])
+        for b in range(64):
+            if (v >> b) & 1:
+                out.append(w * 64 + b)
+    return out
+
+
+class CpuState:
+    """ks_cpu_state_cols + the topology table: per node a topology index (-1 = none) and CPU sets
+    [node][KS_CPU_WORDS] (allocated, allocated with PCPULevel / NUMANodeLevel exclusivity, reserved)."""
+
+    def __init__(self, n: int, topologies=()):
+        self.n = int(n)
+        self.topologies = list(topologies)
+        self.topology = np.full(self.n, -1, np.int32)
+        W = abi.KS_CPU_WORDS
+        for k in ("allocated", "excl_pcpu", "excl_numa", "reserved"):
+            setattr(self, k, np.zeros((self.n, W), np.uint64))
+
+    def copy(self) -> "CpuState":
+        t = CpuState(self.n, self.topologies)
+        for k in ("topology", "allocated", "excl_pcpu", "excl_numa", "reserved"):
+            setattr(t, k, getattr(self, k).copy())
+        return t
+
+    def topo_array(self):
+        arr = (abi.KsCpuTopology * max(len(self.topologies), 1))()
+        for i, t in enumerate(self.topologies):
+            arr[i] = t
+        return arr
+
+    def ks(self) -> abi.KsCpuStateCols:
+        c = abi.KsCpuStateCols()
+        self.topology = np.ascontiguousarray(self.topology, np.int32)
+        c.topology = _p32(self.topology)
+        for k in ("allocated", "excl_pcpu", "excl_numa", "reserved"):
+            arr = np.ascontiguousarray(getattr(self, k), np.uint64)
+            setattr(self, k, arr)
+            setattr(c, k, arr.ctypes.data_as(abi.PU64))
         c._keep = self
         return c
 

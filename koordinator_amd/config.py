@@ -112,6 +112,9 @@ class NodeNUMAResourceArgs:
     """NodeNUMAResourceArgs.ScoringStrategy after v1beta2 defaults (defaults.go:107-136)."""
     strategy: str = "LeastAllocated"
     resources: Dict[str, int] = field(default_factory=lambda: {CPU: 1, MEMORY: 1})
+    # NUMAScoringStrategy.Type: the CPU accumulator's default NUMA allocate strategy
+    # (GetDefaultNUMAAllocateStrategy, nodenumaresource/util.go:22-28)
+    numa_scoring_strategy: str = "LeastAllocated"
 
 
 @dataclass
@@ -203,6 +206,8 @@ class SchedulerProfile:
             c.numa.weight_cpu = self.numa.resources.get(CPU, 0)
             c.numa.weight_memory = self.numa.resources.get(MEMORY, 0)
             c.numa.plugin_weight = self.numa_weight
+            c.numa.numa_scoring_strategy = (abi.KS_MOST_ALLOCATED if self.numa.numa_scoring_strategy == "MostAllocated"
+                                            else abi.KS_LEAST_ALLOCATED)
         if self.deviceshare is not None:
             d = self.deviceshare
             c.deviceshare.enable = 1

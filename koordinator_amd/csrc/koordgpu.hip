@@ -30,6 +30,7 @@
 #include "ks_device.h"
 #include "ks_rsv.h"
 #include "ks_dev.h"
+#include "ks_cpuset.h"
 
 using namespace ks;
 
@@ -97,6 +98,7 @@ struct DevPodCols {
   int64_t *la_req_cpu, *la_lim_cpu, *la_dflt_cpu, *la_req_mem, *la_lim_mem, *la_dflt_mem;
   int32_t *rsv_class;
   int64_t *gpu_core, *gpu_mem, *gpu_ratio;
+  uint32_t* cpu_bind;
 };
 
 // estimatedUsedByResource (estimator/default_estimator.go:73-108)
@@ -150,7 +152,6 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   for (int d = 0; d < 3; ++d) keys |= dims[d] != 0 ? (1u << d) : 0u;
   for (int k = 0; k < KS_MAX_SCALARS; ++k) keys |= r.sc[k] != 0 ? (1u << (3 + k)) : 0u;
   r.rsv_keys = keys;
-  r._fpad = 0.0f;
   if (keys == 0) r.flags |= kPodReqZero;
   r.h_cpu = r.cpu * 100;
   r.h_mem = r.mem * 100;
@@ -160,6 +161,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   r.gpu_mem = s.gpu_mem[i];
   r.gpu_ratio = s.gpu_ratio[i];
   if (r.gpu_core != 0 || r.gpu_mem != 0 || r.gpu_ratio != 0) r.flags |= kPodHasGpu;
+  r.cpu_bind = (r.flags & KS_POD_CPU_BIND) ? ((s.cpu_bind[i] & 0xFu) | ((uint32_t)(r.cpu / 1000) << 8)) : 0u;
   out[i] = r;
 }
 
@@ -551,7 +553,8 @@ enum RowField : int {
   RF_LA_ALLOC_CPU = 21, RF_LA_ALLOC_MEM = 22, RF_ALLOWED = 23, RF_LA_BITS = 24, RF_RSV_CLS = 25,
   RF_RSV_BEG = 26, RF_RSV_END = 27,  // the node's reservation range [beg, end) in the CSR table
   RF_NUMA_A = 28, RF_NUMA_OFF = 29,   // NodeNUMAResource cpuset milli-CPUs and amplification offset
-  RF_N = 30
+  RF_NUMA_RATIO = 30, RF_CPU_FREE = 31,  // cpu amplification ratio (f64 bits), available CPUs (i32, -1 = no topology)
+  RF_N = 32
 };
 
 // slot-row terms: score terms 0..10, then the Filter headrooms (Allocatable - Requested) stored as
@@ -598,6 +601,8 @@ struct CommitArgs {
   unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot row misses [14] fast picks
   int64_t n, nchunks;
   int32_t total_pods, batch, k;
+  int2* cpuset_list;   // (pod, node) of every cpu-bind Reserve, in placement order (ks_cpuset.h)
+  int32_t* cpuset_n;
   int32_t rcap;        // reservations cached in LDS per slot (0 = none)
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
   int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
@@ -639,7 +644,7 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   L.scls = o;
   o += (size_t)kMaxBatch * 8;  // per slot: owner classes of the node's matchable reservations
   L.snuma = o;
-  o += (size_t)kMaxBatch * 16;  // per slot: NodeNUMAResource cpuset milli-CPUs, amplification offset
+  o += (size_t)kMaxBatch * 32;  // per slot: NodeNUMAResource cpuset milli-CPUs, amplification offset, ratio, free CPUs
   L.srcnt = o;
   o += (size_t)kMaxBatch * 8;  // per slot: reservations cached (-1 = on the HBM table), CSR begin
   L.srec = o;
@@ -1034,8 +1039,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         NodeReg<NSC> r;
         slot_to_reg<NSC>(rows[lane], r);
         r.rsv_cls = scls[lane];
-        r.numa_A = snuma[2 * lane];
-        r.numa_off = snuma[2 * lane + 1];
+        r.numa_A = snuma[4 * lane];
+        r.numa_off = snuma[4 * lane + 1];
+        r.numa_ratio = __longlong_as_double(snuma[4 * lane + 2]);
+        r.cpu_free = (int32_t)snuma[4 * lane + 3];
         o = eval_full<NSC, false, false, FEAT>(
             cfg, pod, r,
             [&](RsvDelta<NSC>& dl) {
@@ -1094,6 +1101,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const uint32_t pflags = __builtin_amdgcn_readlane(my_flags, j);
     const int64_t* podw = reinterpret_cast<const int64_t*>(&spods[j]);
     // ---- Reserve: NodeInfo.AddPod + podAssignCache.assign on the slot row (lane = term) ----
+    // a cpu-bind pod first needs numCPUsNeeded available CPUs on the node (resource_manager.go:333-335)
+    const bool cpubind = (FEAT & 2) && cfg.cpuset && (pflags & KS_POD_CPU_BIND);
+    const int32_t cpu_need = cpubind ? (int32_t)(__builtin_amdgcn_readfirstlane(spods[j].cpu_bind) >> 8) : 0;
     int32_t s = __ffsll((long long)__ballot(snode == node)) - 1;
     SlotRow* row;
     // Reservation Reserve needs the node's pre-pod row: when the pod's class matches one of the
@@ -1114,14 +1124,22 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         }
         if (lane < RF_N) raw[lane] = v;
       }
+      if (cpubind && (int32_t)src[RF_CPU_FREE] < cpu_need) {
+        // NodeNUMAResource Reserve -> Allocate: not enough CPUs; every plugin unreserves
+        --nslots;
+        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0};
+        goto next_pod;
+      }
       if (lane == s) snode = node;
       if (lane == 0) touched[node >> 6] |= 1ull << (node & 63);
       const uint64_t ncl = (uint64_t)src[RF_RSV_CLS];
       rsvc = pcls >= 0 && pcls < 64 && ((ncl >> pcls) & 1ull);
       if (lane == 0) {
         scls[s] = ncl;
-        snuma[2 * s] = src[RF_NUMA_A];
-        snuma[2 * s + 1] = src[RF_NUMA_OFF];
+        snuma[4 * s] = src[RF_NUMA_A];
+        snuma[4 * s + 1] = src[RF_NUMA_OFF];
+        snuma[4 * s + 2] = src[RF_NUMA_RATIO];
+        snuma[4 * s + 3] = (int64_t)(int32_t)src[RF_CPU_FREE];
       }
       if (DEV && cfg.dev) {
         // the node's GPU totals / used / present flag into LDS (lane = word)
@@ -1182,6 +1200,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
                       (src[RF_ALLOC_EPH] != 0 ? cfg.fw_eph : 0);
       }
     } else {
+      if (cpubind && (int32_t)snuma[4 * s + 3] < cpu_need) {
+        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0};
+        goto next_pod;
+      }
       row = &rows[s];
       rsvc = pcls >= 0 && pcls < 64 && ((scls[s] >> pcls) & 1ull);
       const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
@@ -1201,8 +1223,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       NodeReg<NSC> nr;
       slot_to_reg<NSC>(*row, nr);
       nr.rsv_cls = scls[s];
-      nr.numa_A = snuma[2 * s];
-      nr.numa_off = snuma[2 * s + 1];
+      nr.numa_A = snuma[4 * s];
+      nr.numa_off = snuma[4 * s + 1];
+      nr.numa_ratio = __longlong_as_double(snuma[4 * s + 2]);
+      nr.cpu_free = (int32_t)snuma[4 * s + 3];
       RsvDelta<NSC> dl;
       const int32_t mode = srcnt[s];
       const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s]};
@@ -1289,6 +1313,21 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
       }
     }
+    if (cpubind) {
+      // NodeAllocation.addPodAllocation of numCPUsNeeded CPUs: the cpuset millicores A grow, the
+      // amplification offset Amplify(A) - A is re-derived (the CPU ids are chosen by cpuset_kernel)
+      const int64_t A0 = snuma[4 * s], off0 = snuma[4 * s + 1];
+      const double ratio = __longlong_as_double(snuma[4 * s + 2]);
+      const int64_t A1 = A0 + (int64_t)cpu_need * 1000;
+      const int64_t off1 = ratio > 1.0 ? (int64_t)::ceil((double)A1 * ratio) - A1 : 0;
+      if (lane == ST_NCPU) term_take(row->t[ST_NCPU], off1 - off0, (off1 - off0) * 100);
+      if (lane == 0) {
+        snuma[4 * s] = A1;
+        snuma[4 * s + 1] = off1;
+        snuma[4 * s + 3] -= cpu_need;
+        a.cpuset_list[atomicAdd(a.cpuset_n, 1)] = make_int2(cursor0 + j, node);
+      }
+    }
     if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors};
     {
       const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
@@ -1337,6 +1376,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     gst(d.la_term_mem + node, term_requested(r.t[ST_LMEM]));
     gst(d.la_pterm_cpu + node, term_requested(r.t[ST_PLCPU]));
     gst(d.la_pterm_mem + node, term_requested(r.t[ST_PLMEM]));
+    if ((FEAT & 2) && cfg.cpuset) {
+      gst(d.numa_amilli + node, snuma[4 * lane]);
+      gst(d.numa_off + node, snuma[4 * lane + 1]);
+      gst(d.numa_cpus + node, (int32_t)(snuma[4 * lane] / 1000));
+      gst(d.cpu_free + node, (int32_t)snuma[4 * lane + 3]);
+    }
   }
   if (QC) {
     for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
@@ -1578,6 +1623,58 @@ __global__ __launch_bounds__(1024) void rsv_normalize_debug_kernel(int64_t n, co
 // Base restore of the reservation table (ks_rsv.h): add (sign = +1) or remove (-1) every eligible
 // reservation's unmatched replacement (transformer.go:266-307) on the node columns; with classes != 0
 // also (re)compute the node's matchable owner-class union.  idx = NULL: nodes [0, count).
+// ------------------------------------------------------------------------------------------
+// NodeNUMAResource cpusets: the CPU ids of every cpu-bind Reserve, per node in placement order
+// ------------------------------------------------------------------------------------------
+//
+// One thread per node.  The block stages the (pod, node) list through LDS; a thread runs takeCPUs
+// (ks_cpuset.h) for each of its node's entries in list order and adds the CPUs to the node's
+// allocation (NodeAllocation.addPodAllocation, node_allocation.go:75-100: allocated, exclusive policy).
+constexpr int kCpusetStage = 1024;
+
+__global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* list, const int32_t* count_p,
+                                                     const PodRec* pods, CpuSet* out, const uint32_t* numa_flags,
+                                                     int32_t default_most, int64_t n) {
+  __shared__ int2 stage[kCpusetStage];
+  const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t count = *count_p;
+  uint64_t keys[KS_MAX_CPUS];
+  for (int32_t base = 0; base < count; base += kCpusetStage) {
+    const int32_t m = min(kCpusetStage, count - base);
+    for (int32_t i = threadIdx.x; i < m; i += blockDim.x) stage[i] = list[base + i];
+    __syncthreads();
+    for (int32_t i = 0; i < m && node < n; ++i) {
+      if (stage[i].y != (int32_t)node) continue;
+      const int32_t pod = stage[i].x;
+      const int32_t tid = cpu.topo_id[node];
+      if (tid < 0) continue;  // unreachable: the Filter rejects nodes without a topology
+      const CpuTopo& t = cpu.topo[tid];
+      const uint32_t cb = pods[pod].cpu_bind;
+      const uint32_t nf = numa_flags[node];
+      CpuAcc a;
+      a.t = &t;
+      const CpuSet alloc = cpu.allocated[node], xp = cpu.excl_pcpu[node], xn = cpu.excl_numa[node];
+      a.al = cs_andnot(cs_andnot(t.all, alloc), cpu.reserved[node]);
+      a.res = cs_zero();
+      a.exc_cores = cs_zero();
+      a.exc_nodes = 0;
+      for (int w = 0; w < kCpuW; ++w) {
+        for (uint64_t b = xp.w[w]; b; b &= b - 1) cs_add(a.exc_cores, t.core_of[w * 64 + __builtin_ctzll(b)]);
+        for (uint64_t b = xn.w[w]; b; b &= b - 1) a.exc_nodes |= 1ull << t.node_of[w * 64 + __builtin_ctzll(b)];
+      }
+      a.excl = (int32_t)((cb >> KS_CPU_EXCL_SHIFT) & 3u);
+      a.most = (nf & KS_NUMA_ALLOC_MOST) ? true : ((nf & KS_NUMA_ALLOC_LEAST) ? false : default_most != 0);
+      a.needed = (int32_t)(cb >> 8);
+      if (!take_cpus(a, (int)(cb & KS_CPU_BIND_POLICY_MASK), keys)) a.res = cs_zero();  // unreachable (count checked)
+      cpu.allocated[node] = cs_or(alloc, a.res);
+      if (a.excl == KS_CPU_EXCL_PCPU_LEVEL) cpu.excl_pcpu[node] = cs_or(xp, a.res);
+      if (a.excl == KS_CPU_EXCL_NUMA_NODE_LEVEL) cpu.excl_numa[node] = cs_or(xn, a.res);
+      out[pod] = a.res;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void rsv_base_kernel(DevNodes d, DevRsv rv, const int32_t* idx, int64_t count, int64_t sign, int32_t classes) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= count) return;
@@ -1703,6 +1800,16 @@ struct ks_ctx {
   bool dev_loaded = false;
   int64_t* dev_used_ckpt = nullptr;
   unsigned long long* dev_M = nullptr;  // [64] per pass
+  // NodeNUMAResource cpusets (ks_cpuset.h)
+  void* cpu_blob = nullptr;
+  DevCpu cpu{};
+  bool cpu_loaded = false;
+  std::vector<int32_t> cpu_cpc;          // CPUsPerCore of each loaded topology
+  CpuSet* cpu_ckpt = nullptr;            // allocated / excl_pcpu / excl_numa at ks_checkpoint
+  int2* cpuset_list = nullptr;           // [pod_cap] (pod, node) of every cpu-bind Reserve
+  int32_t* cpuset_n = nullptr;
+  CpuSet* cpuset_out = nullptr;          // [pod_cap] CPUs allocated per pod of the last schedule
+  int32_t cpuset_cap = 0;
   // debug
   PodRec* dbg_pod = nullptr;
   // stats
@@ -1738,6 +1845,7 @@ static void dev_free(void*& p) {
 
 static Cfg make_cfg(const ks_config& c, int nsc) {
   Cfg k{};
+  k.cpuset = c.numa.enable ? 1 : 0;  // cpu-bind pods: topology check, amplified request, Reserve counts
   k.fit_filter = c.fit.enable_filter;
   k.fit_score = c.fit.enable_score;
   k.fit_most = c.fit.strategy == KS_MOST_ALLOCATED;
@@ -1921,6 +2029,8 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->ddv; dev_free(p);
   dev_free(ctx->dev_blob);
   p = ctx->dev_M; dev_free(p);
+  dev_free(ctx->cpu_blob);
+  p = ctx->cpuset_list; dev_free(p);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1942,7 +2052,11 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.la_pterm_cpu, 8, true);
   add(&d.la_pterm_mem, 8, true);
   add(&d.rsv_cls, 8, true);
+  add(&d.numa_amilli, 8, true);
+  add(&d.numa_off, 8, true);
   add(&d.pod_count, 4, true);
+  add(&d.numa_cpus, 4, true);
+  add(&d.cpu_free, 4, true);
   // read-only columns
   add(&d.alloc_cpu, 8, false);
   add(&d.alloc_mem, 8, false);
@@ -1964,9 +2078,6 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.la_pthr_mem, 4, false);
   add(&d.la_bits, 4, false);
   add(&d.numa_ratio, 8, false);
-  add(&d.numa_amilli, 8, false);
-  add(&d.numa_off, 8, false);
-  add(&d.numa_cpus, 4, false);
   add(&d.numa_flags, 4, false);
 }
 
@@ -1984,7 +2095,11 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->la_prod_term_milli_cpu);
   v.push_back(c->la_prod_term_memory);
   v.push_back(nullptr);  // rsv_cls: derived from the reservation table
+  v.push_back(nullptr);  // numa_amilli: derived on device
+  v.push_back(nullptr);  // numa_off: derived on device
   v.push_back(c->pod_count);
+  v.push_back(c->numa_cpuset_cpus);
+  v.push_back(nullptr);  // cpu_free: ks_load_cpu_state (-1 = no CPU topology)
   v.push_back(c->alloc_milli_cpu);
   v.push_back(c->alloc_memory);
   v.push_back(c->alloc_ephemeral);
@@ -2005,9 +2120,6 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->la_prod_thr_memory);
   v.push_back(nullptr);  // la_bits: derived on device
   v.push_back(c->numa_cpu_amplification);
-  v.push_back(nullptr);  // numa_amilli: derived on device
-  v.push_back(nullptr);  // numa_off: derived on device
-  v.push_back(c->numa_cpuset_cpus);
   v.push_back(c->numa_flags);
   return v;
 }
@@ -2077,6 +2189,8 @@ static int upload_rowcols(ks_ctx* ctx) {
   set(RF_RSV_END, ctx->rv.beg ? (const void*)(ctx->rv.beg + 1) : (const void*)d.la_bits, 4);
   set(RF_NUMA_A, d.numa_amilli, 8);
   set(RF_NUMA_OFF, d.numa_off, 8);
+  set(RF_NUMA_RATIO, d.numa_ratio, 8);
+  set(RF_CPU_FREE, d.cpu_free, 4);
   if (!ctx->rowcols) {
     void* p = nullptr;
     if (dev_alloc(ctx, &p, sizeof(h)) != KS_OK) return KS_ENOMEM;
@@ -2148,6 +2262,8 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
       HIPCHK(ctx, hipMemcpyAsync(base, src[i], (size_t)n * ctx->cols[i].width, hipMemcpyHostToDevice, ctx->stream));
     base += (size_t)ctx->npad * ctx->cols[i].width;
   }
+  HIPCHK(ctx, hipMemsetAsync(ctx->d.cpu_free, 0xFF, (size_t)ctx->npad * 4, ctx->stream));  // no CPU topology yet
+  ctx->cpu_loaded = false;
   if (dev_alloc(ctx, &p, (size_t)ctx->nchunks * 64 * 8) != KS_OK) return KS_ENOMEM;
   ctx->sweep_out = (uint2*)p;
   if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;
@@ -2346,6 +2462,170 @@ int ks_read_devices(ks_ctx* ctx, int64_t* used_core, int64_t* used_memory, int64
   for (int q = 0; q < 3; ++q)
     if (outs[q])
       for (int k = 0; k < kGpus; ++k) memcpy(outs[q] + (size_t)k * n, u.data() + ((size_t)q * kGpus + k) * np, n * 8);
+  return KS_OK;
+}
+
+// Dense form of one ks_cpu_topology (ids in ascending order -> indices); checks the shape assumptions.
+static int build_cpu_topo(ks_ctx* ctx, const ks_cpu_topology& in, int32_t ti, CpuTopo& t) {
+  memset(&t, 0, sizeof(t));
+  const int nc = in.ncpus;
+  if (nc <= 0 || nc > KS_MAX_CPUS) KS_FAIL(ctx, KS_EINVAL, "cpu topology %d: ncpus %d outside (0, %d]", ti, nc, KS_MAX_CPUS);
+  std::vector<int32_t> cores(in.core, in.core + nc), nodes(in.numa_node, in.numa_node + nc), socks(in.socket, in.socket + nc);
+  for (int c = 0; c < nc; ++c)
+    if (in.core[c] < 0 || in.numa_node[c] < 0 || in.socket[c] < 0)
+      KS_FAIL(ctx, KS_EINVAL, "cpu topology %d: negative id for CPU %d", ti, c);
+  auto uniq = [](std::vector<int32_t>& v) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); };
+  uniq(cores);
+  uniq(nodes);
+  uniq(socks);
+  if ((int)nodes.size() > kMaxNumaNodes || (int)socks.size() > kMaxNumaNodes)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "cpu topology %d: more than %d NUMA nodes or sockets", ti, kMaxNumaNodes);
+  if (socks.size() > 12)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "cpu topology %d: more than 12 sockets (Go's sort order is only stable up to 12)", ti);
+  auto idx = [](const std::vector<int32_t>& v, int32_t x) { return (int)(std::lower_bound(v.begin(), v.end(), x) - v.begin()); };
+  std::vector<int> core_n(cores.size(), -1), core_s(cores.size(), -1), node_s(nodes.size(), -1), core_cnt(cores.size(), 0);
+  for (int c = 0; c < nc; ++c) {
+    const int k = idx(cores, in.core[c]), nn = idx(nodes, in.numa_node[c]), ss = idx(socks, in.socket[c]);
+    t.core_of[c] = (uint8_t)k;
+    t.node_of[c] = (uint8_t)nn;
+    t.sock_of[c] = (uint8_t)ss;
+    if ((core_n[k] >= 0 && core_n[k] != nn) || (core_s[k] >= 0 && core_s[k] != ss) || (node_s[nn] >= 0 && node_s[nn] != ss))
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "cpu topology %d: a core spans NUMA nodes / sockets or a NUMA node spans sockets", ti);
+    core_n[k] = nn;
+    core_s[k] = ss;
+    node_s[nn] = ss;
+    if (++core_cnt[k] > 8) KS_FAIL(ctx, KS_EUNSUPPORTED, "cpu topology %d: more than 8 CPUs per core", ti);
+    cs_add(t.core_mask[k], c);
+    cs_add(t.node_mask[nn], c);
+    cs_add(t.sock_mask[ss], c);
+    cs_add(t.all, c);
+  }
+  for (size_t k = 0; k < cores.size(); ++k) {
+    t.core_node[k] = (uint8_t)core_n[k];
+    t.core_sock[k] = (uint8_t)core_s[k];
+  }
+  for (size_t nn = 0; nn < nodes.size(); ++nn) t.node_sock[nn] = (uint8_t)node_s[nn];
+  // CPUTopologyBuilder counts (cpu_topology.go:45-70): cores are distinct per (socket, node, core)
+  std::vector<std::tuple<int, int, int>> trip;
+  std::vector<std::pair<int, int>> pairs;
+  for (int c = 0; c < nc; ++c) {
+    trip.emplace_back(in.socket[c], in.numa_node[c], in.core[c]);
+    pairs.emplace_back(in.socket[c], in.numa_node[c]);
+  }
+  std::sort(trip.begin(), trip.end());
+  trip.erase(std::unique(trip.begin(), trip.end()), trip.end());
+  std::sort(pairs.begin(), pairs.end());
+  pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
+  t.ncpus = nc;
+  t.ncores = (int32_t)cores.size();
+  t.nnodes = (int32_t)nodes.size();
+  t.nsockets = (int32_t)socks.size();
+  if ((int)trip.size() != t.ncores || (int)pairs.size() != t.nnodes)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "cpu topology %d: core / NUMA ids are not unique across sockets", ti);
+  t.cpc = nc / t.ncores;
+  t.cpn = nc / t.nnodes;
+  t.cps = nc / t.nsockets;
+  return KS_OK;
+}
+
+int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, const ks_cpu_state_cols* st) {
+  if (!ctx || ntopo < 0 || (ntopo > 0 && !topos) || !st || !st->topology || !st->allocated)
+    return ctx ? (ctx->err = "ks_load_cpu_state: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_load_cpu_state before ks_load_nodes");
+  if (!ctx->cfg.numa.enable) KS_FAIL(ctx, KS_ESTATE, "ks_load_cpu_state: the NodeNUMAResource plugin is not enabled");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int64_t n = ctx->n, np = ctx->npad;
+  std::vector<CpuTopo> tt((size_t)std::max(ntopo, 1));
+  std::vector<int32_t> cpc;
+  for (int32_t i = 0; i < ntopo; ++i) {
+    if (int rc = build_cpu_topo(ctx, topos[i], i, tt[i]); rc != KS_OK) return rc;
+    cpc.push_back(tt[i].cpc);
+  }
+  std::vector<int32_t> tid((size_t)np, -1), freec((size_t)np, -1), ncpu((size_t)np, 0);
+  std::vector<CpuSet> al((size_t)np, cs_zero()), xp((size_t)np, cs_zero()), xn((size_t)np, cs_zero()), rs((size_t)np, cs_zero());
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t ti = st->topology[i];
+    if (ti < -1 || ti >= ntopo) KS_FAIL(ctx, KS_EINVAL, "node %lld: cpu topology %d out of range", (long long)i, ti);
+    auto rd = [&](const uint64_t* p) {
+      CpuSet c = cs_zero();
+      if (p) memcpy(c.w, p + i * kCpuW, sizeof(c.w));
+      return c;
+    };
+    al[i] = rd(st->allocated);
+    xp[i] = rd(st->excl_pcpu);
+    xn[i] = rd(st->excl_numa);
+    rs[i] = rd(st->reserved);
+    tid[i] = ti;
+    if (ti >= 0) {
+      const CpuSet& all = tt[ti].all;
+      if (cs_count(cs_andnot(cs_or(cs_or(al[i], xp[i]), cs_or(xn[i], rs[i])), all)) != 0)
+        KS_FAIL(ctx, KS_EINVAL, "node %lld: CPU set outside its topology", (long long)i);
+      if (cs_count(cs_andnot(cs_or(xp[i], xn[i]), al[i])) != 0 || cs_count(cs_and(xp[i], xn[i])) != 0)
+        KS_FAIL(ctx, KS_EINVAL, "node %lld: exclusive CPU sets must be disjoint subsets of allocated", (long long)i);
+      freec[i] = cs_count(cs_andnot(all, cs_or(al[i], rs[i])));
+    } else if (cs_count(al[i]) != 0) {
+      KS_FAIL(ctx, KS_EINVAL, "node %lld: allocated CPUs without a topology", (long long)i);
+    }
+    ncpu[i] = cs_count(al[i]);  // the cpuset millicores of filterAmplifiedCPUs are |allocated| x 1000
+  }
+  dev_free(ctx->cpu_blob);
+  ctx->cpu_loaded = false;
+  const size_t tb = align16(tt.size() * sizeof(CpuTopo)), ib = align16((size_t)np * 4), sb = (size_t)np * sizeof(CpuSet);
+  if (dev_alloc(ctx, &ctx->cpu_blob, tb + ib + sb * 7) != KS_OK) return KS_ENOMEM;
+  char* b = (char*)ctx->cpu_blob;
+  DevCpu& c = ctx->cpu;
+  c.topo = (const CpuTopo*)b;
+  HIPCHK(ctx, hipMemcpyAsync(b, tt.data(), tt.size() * sizeof(CpuTopo), hipMemcpyHostToDevice, ctx->stream));
+  b += tb;
+  c.topo_id = (const int32_t*)b;
+  HIPCHK(ctx, hipMemcpyAsync(b, tid.data(), (size_t)np * 4, hipMemcpyHostToDevice, ctx->stream));
+  b += ib;
+  CpuSet* sets[4] = {nullptr, nullptr, nullptr, nullptr};
+  const std::vector<CpuSet>* srcs[4] = {&al, &xp, &xn, &rs};
+  for (int q = 0; q < 4; ++q) {
+    sets[q] = (CpuSet*)b;
+    HIPCHK(ctx, hipMemcpyAsync(b, srcs[q]->data(), sb, hipMemcpyHostToDevice, ctx->stream));
+    b += sb;
+  }
+  c.allocated = sets[0];
+  c.excl_pcpu = sets[1];
+  c.excl_numa = sets[2];
+  c.reserved = sets[3];
+  ctx->cpu_ckpt = (CpuSet*)b;  // 3 x [npad]
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cpu_ckpt, c.allocated, sb * 3, hipMemcpyDeviceToDevice, ctx->stream));
+  c.npad = np;
+  c.ntopo = ntopo;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->d.cpu_free, freec.data(), (size_t)np * 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->d.numa_cpus, ncpu.data(), (size_t)np * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;  // re-derive the cpuset millicores and offsets
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->cpu_cpc = cpc;
+  ctx->cpu_loaded = true;
+  return KS_OK;
+}
+
+int ks_read_cpu_state(ks_ctx* ctx, uint64_t* allocated, uint64_t* excl_pcpu, uint64_t* excl_numa) {
+  if (!ctx) return KS_EINVAL;
+  if (!ctx->cpu_loaded) return KS_OK;
+  const size_t n = (size_t)ctx->n;
+  uint64_t* outs[3] = {allocated, excl_pcpu, excl_numa};
+  const CpuSet* srcs[3] = {ctx->cpu.allocated, ctx->cpu.excl_pcpu, ctx->cpu.excl_numa};
+  for (int q = 0; q < 3; ++q)
+    if (outs[q] && n) HIPCHK(ctx, hipMemcpyAsync(outs[q], srcs[q], n * sizeof(CpuSet), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_fetch_cpusets(ks_ctx* ctx, uint64_t* out, int32_t p) {
+  if (!ctx || (p > 0 && !out) || p < 0) return ctx ? (ctx->err = "ks_fetch_cpusets: bad args", KS_EINVAL) : KS_EINVAL;
+  if (p > ctx->np) KS_FAIL(ctx, KS_EINVAL, "ks_fetch_cpusets: %d pods requested, %d scheduled", p, ctx->np);
+  if (p == 0) return KS_OK;
+  if (!ctx->cpuset_out || ctx->cpuset_cap < p) {
+    memset(out, 0, (size_t)p * sizeof(CpuSet));
+    return KS_OK;
+  }
+  HIPCHK(ctx, hipMemcpyAsync(out, ctx->cpuset_out, (size_t)p * sizeof(CpuSet), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
 
@@ -2629,8 +2909,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   const size_t res = ((size_t)cap * sizeof(ks_result) + 255) / 256 * 256;
   const size_t col8 = ((size_t)cap * 8 + 255) / 256 * 256;
   const size_t col4 = ((size_t)cap * 4 + 255) / 256 * 256;
-  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 qreq[8] = 26 int64 cols; flags quota qmask rsv_class = 4 x32
-  const size_t bytes = rec + res + col8 * 26 + col4 * 4;
+  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 qreq[8] = 26 int64 cols; flags quota qmask rsv_class cpu_bind = 5 x32
+  const size_t bytes = rec + res + col8 * 26 + col4 * 5;
   if (dev_alloc(ctx, &ctx->pod_blob, bytes) != KS_OK) return KS_ENOMEM;
   char* b = (char*)ctx->pod_blob;
   ctx->pods = (PodRec*)b;
@@ -2656,6 +2936,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   ctx->pq.mask = (uint32_t*)b;
   b += col4;
   s.rsv_class = (int32_t*)b;
+  b += col4;
+  s.cpu_bind = (uint32_t*)b;
   ctx->pod_cap = cap;
   return KS_OK;
 }
@@ -2691,6 +2973,8 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
   else HIPCHK(ctx, hipMemsetAsync(ctx->pq.mask, 0, (size_t)p * 4, ctx->stream));
   if (pc->rsv_class) HIPCHK(ctx, hipMemcpyAsync(s.rsv_class, pc->rsv_class, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.rsv_class, 0xFF, (size_t)p * 4, ctx->stream));
+  if (pc->cpu_bind) HIPCHK(ctx, hipMemcpyAsync(s.cpu_bind, pc->cpu_bind, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(s.cpu_bind, 0, (size_t)p * 4, ctx->stream));
   const int threads = 256;
   hipLaunchKernelGGL(prep_pods_kernel, dim3((p + threads - 1) / threads), dim3(threads), 0, ctx->stream, s, dst, p,
                      ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory);
@@ -2707,9 +2991,23 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
   for (int k = 0; k < KS_MAX_SCALARS; ++k)
     if (check_range64(ctx, pc->req_scalar[k], p, "pod scalar") != KS_OK) return KS_EINVAL;
   if (ctx->cfg.numa.enable && pc->flags) {
-    for (int32_t i = 0; i < p; ++i)
-      if (pc->flags[i] & KS_POD_CPU_BIND)
-        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: cpuset (cpu-bind) allocation is not supported by this build", i);
+    for (int32_t i = 0; i < p; ++i) {
+      if (!(pc->flags[i] & KS_POD_CPU_BIND)) continue;
+      if (!pc->cpu_bind) KS_FAIL(ctx, KS_EINVAL, "pod %d: KS_POD_CPU_BIND without ks_pod_cols.cpu_bind", i);
+      const uint32_t cb = pc->cpu_bind[i], pol = cb & KS_CPU_BIND_POLICY_MASK, ex = (cb >> KS_CPU_EXCL_SHIFT) & 3u;
+      const int64_t cpu = pc->req_milli_cpu ? pc->req_milli_cpu[i] : 0;
+      if ((pol != KS_CPU_BIND_FULL_PCPUS && pol != KS_CPU_BIND_SPREAD_BY_PCPUS) || ex > KS_CPU_EXCL_NUMA_NODE_LEVEL || (cb >> 4))
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: cpu_bind 0x%x invalid", i, cb);
+      if (cpu <= 0 || cpu % 1000 != 0 || cpu / 1000 > KS_MAX_CPUS)
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
+      // takeCPUs' FullPCPUs fallback can take a whole core past numCPUsNeeded when the request is not a
+      // whole number of cores (cpu_accumulator.go:163-175); the count-only commit does not model that
+      if (pol == KS_CPU_BIND_FULL_PCPUS)
+        for (int32_t cpc : ctx->cpu_cpc)
+          if (cpc > 1 && (cpu / 1000) % cpc != 0)
+            KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: FullPCPUs request of %lld CPUs is not a whole number of %d-thread cores", i,
+                    (long long)(cpu / 1000), cpc);
+    }
   }
   if (pc->rsv_class) {
     for (int32_t i = 0; i < p; ++i)
@@ -2928,6 +3226,8 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.dev_bytes = (int32_t)dev_cache_bytes(ctx);
   ca.dv = ctx->ddv;
   ca.dev_M = ctx->dev_M;
+  ca.cpuset_list = ctx->cpuset_list;
+  ca.cpuset_n = ctx->cpuset_n;
   const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes).total;
   rec(2);
 #define KS_COMMIT(F)                                                                                          \
@@ -2997,7 +3297,23 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   if (ppw > ctx->batch) ppw = ctx->batch;
   const int64_t nwork = std::max<int64_t>(local_chunks, 1) * ((ctx->batch + ppw - 1) / ppw);
   const int sweep_blocks = (int)((std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048)) + 7) & ~7ll);  // % 8 == 0 (XCD swizzle)
+  if (ctx->cfg.numa.enable && ctx->cpuset_cap < np) {
+    // (pod, node) list + its count + the per-pod CPU sets of this call
+    void* p = ctx->cpuset_list;
+    dev_free(p);
+    ctx->cpuset_list = nullptr;
+    const int32_t cap = std::max<int32_t>(np, 64);
+    if (dev_alloc(ctx, &p, (size_t)cap * 8 + 16 + (size_t)cap * sizeof(CpuSet)) != KS_OK) return KS_ENOMEM;
+    ctx->cpuset_list = (int2*)p;
+    ctx->cpuset_n = (int32_t*)((char*)p + (size_t)cap * 8);
+    ctx->cpuset_out = (CpuSet*)((char*)p + (size_t)cap * 8 + 16);
+    ctx->cpuset_cap = cap;
+  }
   hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
+  if (ctx->cpuset_list) {
+    HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_out, 0, (size_t)np * sizeof(CpuSet), ctx->stream));
+  }
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 256, ctx->stream));
   HIPCHK(ctx, hipEventRecord(t0, ctx->stream));
@@ -3020,6 +3336,14 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(&host_cursor, ctx->cursor, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (++rounds > 1000000) KS_FAIL(ctx, KS_EHIP, "schedule made no progress");
+  }
+  if (ctx->cpu_loaded && ctx->n > 0) {
+    // the CPU ids of the pass's cpu-bind Reserves (ks_cpuset.h), per node in placement order
+    hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
+                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const PodRec*)ctx->pods,
+                       ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
+                       (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+    HIPCHK(ctx, hipGetLastError());
   }
   HIPCHK(ctx, hipEventRecord(t1, ctx->stream));
   unsigned long long cnt[16] = {0};
@@ -3085,6 +3409,8 @@ int ks_checkpoint(ks_ctx* ctx) {
   }
   if (ctx->dev_blob)
     HIPCHK(ctx, hipMemcpyAsync(ctx->dev_used_ckpt, ctx->dv.used, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->cpu_loaded)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->cpu_ckpt, ctx->cpu.allocated, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_allocd_ckpt, ctx->rv.allocd, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -3103,6 +3429,8 @@ int ks_restore(ks_ctx* ctx) {
   }
   if (ctx->dev_blob)
     HIPCHK(ctx, hipMemcpyAsync(ctx->dv.used, ctx->dev_used_ckpt, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->cpu_loaded)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->cpu.allocated, ctx->cpu_ckpt, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));

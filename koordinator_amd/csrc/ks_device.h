@@ -59,6 +59,7 @@ struct Cfg {
   int32_t rsv;       // Reservation plugin enabled
   int32_t rsv_F;     // key radix: key total = hi * rsv_F + (Fit + LoadAware + NUMA weighted total), see ks_rsv.h
   int32_t numa, numa_most, nw_cpu, nw_mem, numa_pw;  // NodeNUMAResource
+  int32_t cpuset;    // CPU state loaded: cpu-bind pods are evaluated (ks_cpuset.h)
   int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw;  // DeviceShare (GPU)
 };
 
@@ -82,6 +83,7 @@ struct DevNodes {
   uint32_t *numa_flags;
   int64_t *numa_amilli;     // derived: cpuset CPUs x 1000
   int64_t *numa_off;        // derived: Amplify(cpuset milli, ratio) - cpuset milli (ratio > 1), else 0
+  int32_t *cpu_free;        // available CPUs for cpuset pods (ks_cpuset.h), -1 = no valid CPU topology
 };
 
 // Per-pod record read by the sweep with scalar loads (AoS, 192 B).  The x100 and f32 copies feed
@@ -98,7 +100,7 @@ struct __attribute__((aligned(16))) PodRec {
   float f_sc[KS_MAX_SCALARS];
   int32_t rsv_class;  // reservation match class (-1 = none)
   uint32_t rsv_keys;  // bit d: request dimension d is non-zero (a key of the pod's requests)
-  float _fpad;
+  uint32_t cpu_bind;  // KS_POD_CPU_BIND pods: KS_CPU_BIND_* | exclusive << KS_CPU_EXCL_SHIFT | numCPUsNeeded << 8
   int64_t h_cpu, h_mem;  // 100 x the Requested cpu / memory (NodeNUMAResource score)
   float f_cpu, f_mem;
   int64_t gpu_core, gpu_mem, gpu_ratio;  // DeviceShare: converted GPU request
@@ -239,6 +241,8 @@ struct __attribute__((aligned(16))) NodeReg {
   Term t_lcpu, t_lmem, t_plcpu, t_plmem;       // LoadAware: EstimateNode alloc - node term (all / prod)
   Term t_ncpu, t_nmem;                         // NodeNUMAResource: Requested (+ amplified cpuset part for cpu)
   int64_t numa_A, numa_off;                    // cpuset milli-CPUs, Amplify(A) - A
+  double numa_ratio;                           // cpu amplification ratio (amplifies a cpu-bind pod's request)
+  int32_t cpu_free;                            // available CPUs for cpuset pods, -1 = no valid CPU topology
   uint32_t la_bits;
   int32_t fit_ws;                              // Σ weights of cpu/mem/eph terms with capacity != 0
   int32_t pods_full;
@@ -271,7 +275,7 @@ __device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int val
                                           const int64_t* req_sc, int64_t la_alloc_cpu, int64_t la_alloc_mem,
                                           int64_t term_cpu, int64_t term_mem, int64_t pterm_cpu, int64_t pterm_mem,
                                           uint32_t la_bits, int32_t allowed, int32_t pod_count, int64_t numa_A = 0,
-                                          int64_t numa_off = 0) {
+                                          int64_t numa_off = 0, double numa_ratio = 0.0, int32_t cpu_free = -1) {
   r.valid = valid;
   r.free_cpu = alloc_cpu - req_cpu;
   r.free_mem = alloc_mem - req_mem;
@@ -296,6 +300,8 @@ __device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int val
   r.rsv_cls = 0;
   r.numa_A = numa_A;
   r.numa_off = numa_off;
+  r.numa_ratio = numa_ratio;
+  r.cpu_free = cpu_free;
   term_set(r.t_ncpu, alloc_cpu, req_cpu + numa_off);
   term_set(r.t_nmem, alloc_mem, req_mem);
 }
@@ -310,15 +316,21 @@ __device__ __forceinline__ void load_node(const Cfg& c, const DevNodes& d, int64
     rsc[k] = gld(d.req_sc[k] + n);
   }
   int64_t na = 0, no = 0;
+  double nr = 0.0;
+  int32_t cf = -1;
   if (c.numa) {
     na = gld(d.numa_amilli + n);
     no = gld(d.numa_off + n);
+    if (c.cpuset) {
+      nr = gld(d.numa_ratio + n);
+      cf = gld(d.cpu_free + n);
+    }
   }
   make_node<NSC>(c, r, valid, gld(d.alloc_cpu + n), gld(d.alloc_mem + n), gld(d.alloc_eph + n), gld(d.req_cpu + n),
                  gld(d.req_mem + n), gld(d.req_eph + n), gld(d.nz_cpu + n), gld(d.nz_mem + n), asc, rsc,
                  gld(d.la_alloc_cpu + n), gld(d.la_alloc_mem + n), gld(d.la_term_cpu + n), gld(d.la_term_mem + n),
                  gld(d.la_pterm_cpu + n), gld(d.la_pterm_mem + n), gld(d.la_bits + n), gld(d.allowed_pods + n),
-                 gld(d.pod_count + n), na, no);
+                 gld(d.pod_count + n), na, no, nr, cf);
   if (c.rsv && valid) r.rsv_cls = gld(d.rsv_cls + n);
 }
 
@@ -441,12 +453,22 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   return o;
 }
 
-// NodeNUMAResource for a pod without cpu bind on a topology-policy-None node: filterAmplifiedCPUs
-// (nodenumaresource/plugin.go:340-373) and scoreWithAmplifiedCPUs (scoring.go:98-114) with the
-// resourceAllocationScorer over cpu / memory Requested (:206-242).
+// NodeNUMAResource on a topology-policy-None node: filterAmplifiedCPUs (nodenumaresource/plugin.go:340-373),
+// for a cpu-bind pod the CPU topology check (:296-301; the trial Allocate runs only for a required bind
+// policy, :318-327), and scoreWithAmplifiedCPUs (scoring.go:98-114) with the resourceAllocationScorer over
+// cpu / memory Requested (:206-242).  A cpu-bind pod's request is amplified on a node with ratio > 1
+// (plugin.go:357-359 and getResourceOptions :503-506).
 template <int NSC, bool DEBUG>
 __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const NodeReg<NSC>& r, EvalOut& o) {
   if (p.flags & kPodReqZero) return;  // PreFilter skip
+  const bool bind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
+  int64_t pc = p.cpu, pc100 = p.h_cpu;
+  float pcf = p.f_cpu;
+  if (bind && (r.la_bits & kNumaAmp)) {
+    pc = (int64_t)::ceil((double)p.cpu * r.numa_ratio);  // extension.Amplify
+    pc100 = pc * 100;
+    pcf = i64_to_f32(pc);
+  }
   uint32_t rs = 0;
   if (p.cpu != 0) {
     if (r.la_bits & kNumaInvalid) {
@@ -454,15 +476,16 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
     } else if (r.la_bits & kNumaAmp) {
       const int64_t requested = r.t_ncpu.c - r.free_cpu;  // alloc - (alloc - Requested)
       const bool amp = requested >= r.numa_A && r.numa_A > 0;
-      if (p.cpu > r.free_cpu - (amp ? r.numa_off : 0)) rs = KS_R_NUMA_AMPLIFIED_CPU;
+      if (pc > r.free_cpu - (amp ? r.numa_off : 0)) rs = KS_R_NUMA_AMPLIFIED_CPU;
     }
   }
+  if (bind && rs == 0 && r.cpu_free < 0) rs = KS_R_NUMA_INVALID_TOPOLOGY;
   o.reasons |= DEBUG ? rs : (rs ? KS_R_FIT_PODS : 0u);
   Term tc = r.t_ncpu;
   if (p.cpu == 0) term_take(tc, -r.numa_off, -r.numa_off * 100);  // a cpu-less pod scores the plain Requested
   int32_t ns = 0, ws = 0;
   if (c.nw_cpu && tc.c != 0) {
-    ns += (c.numa_most ? term_most(tc, p.cpu, p.h_cpu, p.f_cpu) : term_least(tc, p.cpu, p.h_cpu, p.f_cpu)) * c.nw_cpu;
+    ns += (c.numa_most ? term_most(tc, pc, pc100, pcf) : term_least(tc, pc, pc100, pcf)) * c.nw_cpu;
     ws += c.nw_cpu;
   }
   if (c.nw_mem && r.t_nmem.c != 0) {

@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
+from .cluster import CpuState, DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
@@ -61,6 +61,9 @@ def lib() -> C.CDLL:
     L.ks_read_reservations.argtypes = [vp, abi.P64, abi.P32]
     L.ks_load_devices.argtypes = [vp, C.POINTER(abi.KsDeviceCols), C.c_int64]
     L.ks_read_devices.argtypes = [vp, abi.P64, abi.P64, abi.P64]
+    L.ks_load_cpu_state.argtypes = [vp, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
+    L.ks_read_cpu_state.argtypes = [vp, abi.PU64, abi.PU64, abi.PU64]
+    L.ks_fetch_cpusets.argtypes = [vp, abi.PU64, C.c_int32]
     L.ks_refresh_quota_runtime.argtypes = [vp, C.POINTER(abi.KsQuotaTree), C.c_int32, abi.P64, abi.PU32]
     L.ks_schedule.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
     L.ks_stage_pods.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32]
@@ -95,7 +98,8 @@ class Evaluator:
     """One scheduler profile's device-resident node snapshot + the sweep/commit pipeline."""
 
     def __init__(self, cfg: abi.KsConfig, nodes: Optional[NodeTable] = None, quotas: Optional[QuotaTable] = None,
-                 reservations: Optional[ReservationTable] = None, devices: Optional[DeviceTable] = None):
+                 reservations: Optional[ReservationTable] = None, devices: Optional[DeviceTable] = None,
+                 cpu_state: Optional[CpuState] = None):
         self.L = lib()
         self.cfg = cfg
         h = C.c_void_p()
@@ -115,6 +119,8 @@ class Evaluator:
             self.load_reservations(reservations)
         if devices is not None:
             self.load_devices(devices)
+        if cpu_state is not None:
+            self.load_cpu_state(cpu_state)
 
     def _chk(self, rc: int):
         if rc != abi.KS_OK:
@@ -160,6 +166,25 @@ class Evaluator:
     def load_devices(self, dev: DeviceTable):
         cols = dev.ks()
         self._chk(self.L.ks_load_devices(self.h, C.byref(cols), dev.n))
+
+    def load_cpu_state(self, st: CpuState):
+        """CPU topologies + per-node allocation for cpuset (KS_POD_CPU_BIND) pods."""
+        cols = st.ks()
+        topos = st.topo_array()
+        self._chk(self.L.ks_load_cpu_state(self.h, topos, len(st.topologies), C.byref(cols)))
+
+    def read_cpu_state(self):
+        """(allocated, excl_pcpu, excl_numa), each [n][KS_CPU_WORDS] uint64"""
+        W = abi.KS_CPU_WORDS
+        out = [np.zeros((max(self.n, 1), W), np.uint64) for _ in range(3)]
+        self._chk(self.L.ks_read_cpu_state(self.h, *[o.ctypes.data_as(abi.PU64) for o in out]))
+        return tuple(o[: self.n] for o in out)
+
+    def fetch_cpusets(self, p: int) -> np.ndarray:
+        """[p][KS_CPU_WORDS] uint64: the CPUs each pod of the last schedule call was allocated."""
+        out = np.zeros((max(p, 1), abi.KS_CPU_WORDS), np.uint64)
+        self._chk(self.L.ks_fetch_cpusets(self.h, out.ctypes.data_as(abi.PU64), p))
+        return out[:p]
 
     def read_devices(self):
         """(used_core, used_memory, used_ratio), each [KS_MAX_GPUS][n]"""

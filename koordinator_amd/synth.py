@@ -37,7 +37,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import NodeTable, PodTable, QuotaTable, ReservationTable
+from .cluster import CpuState, DeviceTable, NodeTable, PodTable, QuotaTable, ReservationTable, cpu_mask, regular_topology
 from .config import BATCH_CPU, BATCH_MEMORY, CPU, MEMORY, ElasticQuotaArgs, NodeResourcesFitArgs, SchedulerProfile
 
 SEED = 20261015
@@ -63,6 +63,7 @@ class Workload:
     quotas: Optional[QuotaTable]
     reservations: Optional[ReservationTable] = None
     devices: Optional["DeviceTable"] = None
+    cpus: Optional[CpuState] = None
 
     @property
     def cfg(self) -> abi.KsConfig:
@@ -260,6 +261,72 @@ def gpu_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4) -> Pod
     return pods
 
 
+# node CPU topologies by core count: (sockets, NUMA nodes per socket, cores per NUMA node, threads per core)
+CPU_TOPOLOGIES = {32: (2, 1, 8, 2), 48: (2, 1, 12, 2), 64: (2, 2, 8, 2), 96: (2, 2, 12, 2)}
+
+
+def make_cpu_state(nodes: NodeTable, rng: np.random.Generator, cores=None, no_topology: float = 0.05,
+                   max_alloc: float = 0.3, label_frac: float = 0.2) -> CpuState:
+    """NodeResourceTopology-derived CPU state: a regular topology per node (by its core count), a
+    fragmented set of already-allocated CPUs (exclusive policy None / PCPULevel / NUMANodeLevel), kubelet
+    reserved CPUs 0-1 on a third of the nodes, and numa-allocate-strategy labels on some nodes.  Node
+    Requested cpu and numa_cpuset_cpus are raised to include the allocated cpusets."""
+    n = nodes.n
+    cores = np.asarray(cores if cores is not None else nodes.alloc_milli_cpu // 1000)
+    keys = sorted(CPU_TOPOLOGIES)
+    st = CpuState(n, [regular_topology(*CPU_TOPOLOGIES[k]) for k in keys])
+    W = abi.KS_CPU_WORDS
+    for i in range(n):
+        c = int(cores[i])
+        if c not in CPU_TOPOLOGIES or rng.random() < no_topology:
+            continue
+        st.topology[i] = keys.index(c)
+        resv = [0, 1] if rng.random() < 0.33 else []
+        free = np.array([x for x in range(c) if x not in resv])
+        k = int(rng.integers(0, int(max_alloc * c) + 1))
+        taken = rng.choice(free, k, replace=False) if k else np.zeros(0, np.int64)
+        pol = rng.choice(np.array([0, 1, 2]), len(taken), p=[0.6, 0.3, 0.1])
+        st.allocated[i] = cpu_mask(taken)
+        st.excl_pcpu[i] = cpu_mask(taken[pol == 1])
+        st.excl_numa[i] = cpu_mask(taken[pol == 2])
+        st.reserved[i] = cpu_mask(resv)
+        nodes.numa_cpuset_cpus[i] = len(taken)
+        nodes.req_milli_cpu[i] += len(taken) * 1000
+        nodes.nonzero_milli_cpu[i] += len(taken) * 1000
+    lab = rng.random(n) < label_frac
+    nodes.numa_flags[:] |= np.where(lab, np.where(rng.random(n) < 0.5, abi.KS_NUMA_ALLOC_MOST, abi.KS_NUMA_ALLOC_LEAST),
+                                    0).astype(np.uint32)
+    assert st.allocated.shape == (n, W)
+    return st
+
+
+def cpuset_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4, exclude=None) -> PodTable:
+    """LSR/LSE prod pods with a preferred cpuset: 4-16 CPUs (FullPCPUs requests in whole 2-thread cores),
+    70 % FullPCPUs / 30 % SpreadByPCPUs, exclusive policy None / PCPULevel / NUMANodeLevel."""
+    p = pods.n
+    sel = rng.random(p) < frac
+    if exclude is not None:
+        sel &= ~np.asarray(exclude)
+    full = rng.random(p) < 0.7
+    k = np.where(full, 2 * rng.integers(2, 9, p), rng.integers(4, 17, p))
+    excl = rng.choice(np.array([0, 1, 2]), p, p=[0.6, 0.25, 0.15])
+    bind = np.where(full, abi.KS_CPU_BIND_FULL_PCPUS, abi.KS_CPU_BIND_SPREAD_BY_PCPUS) | (excl << abi.KS_CPU_EXCL_SHIFT)
+    cpu = k * 1000
+    pods.cpu_bind[:] = np.where(sel, bind, 0).astype(np.uint32)
+    pods.flags[:] = np.where(sel, (pods.flags & ~np.uint32(abi.KS_POD_SCALAR_KEYS)) | abi.KS_POD_PROD | abi.KS_POD_CPU_BIND,
+                             pods.flags).astype(np.uint32)
+    mem = np.where(pods.req_memory > 0, pods.req_memory, pods.req_scalar[SLOT_BATCH_MEMORY])
+    pods.req_milli_cpu[:] = np.where(sel, cpu, pods.req_milli_cpu)
+    pods.req_memory[:] = np.where(sel, mem, pods.req_memory)
+    pods.nonzero_milli_cpu[:] = np.where(sel, cpu, pods.nonzero_milli_cpu)
+    pods.nonzero_memory[:] = np.where(sel, mem, pods.nonzero_memory)
+    pods.la_req_cpu[:] = np.where(sel, cpu, pods.la_req_cpu)
+    pods.la_lim_cpu[:] = np.where(sel, 0, pods.la_lim_cpu)
+    for slot in (SLOT_BATCH_CPU, SLOT_BATCH_MEMORY):
+        pods.req_scalar[slot] = np.where(sel, 0, pods.req_scalar[slot])
+    return pods
+
+
 def c1(seed: int = SEED, n_nodes: int = 500, n_pods: int = 1000, **kw) -> Workload:
     rng = np.random.Generator(np.random.PCG64(seed))
     nodes = make_nodes(n_nodes, rng)
@@ -281,15 +348,17 @@ def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, **kw) -> Wor
     nodes = make_nodes(n_nodes, rng)
     ratio = rng.choice(np.array([0.0, 1.0, 1.5, 2.0]), n_nodes)
     amp = ratio > 1
+    cores = nodes.alloc_milli_cpu // 1000
     nodes.numa_cpu_amplification[:] = ratio
     nodes.alloc_milli_cpu[amp] = np.ceil(nodes.alloc_milli_cpu[amp] * ratio[amp]).astype(np.int64)
-    nodes.numa_cpuset_cpus[:] = np.where(rng.random(n_nodes) < 0.5, rng.integers(0, 16, n_nodes), 0)
+    cpus = make_cpu_state(nodes, rng, cores=cores)
     devs = make_devices(nodes, rng)
     pods = gpu_pods(make_pods(n_pods, rng), rng)
+    pods = cpuset_pods(pods, rng, 0.4 / 0.6, exclude=pods.gpu_memory_ratio + pods.gpu_memory > 0)
     prof = koord_profile(**kw)
     prof.numa = NodeNUMAResourceArgs()
     prof.deviceshare = DeviceShareArgs(resources={GPU_MEMORY_RATIO: 1})
-    return Workload("C3", prof, nodes, pods, None, None, devs)
+    return Workload("C3", prof, nodes, pods, None, None, devs, cpus)
 
 
 def c4(seed: int = SEED, n_nodes: int = 20_000, n_reservations: int = 50_000, n_pods: int = 10_000, **kw) -> Workload:

@@ -54,6 +54,7 @@
 #include <string.h>
 
 #include "../include/koordgpu.h"
+#include "cpu_accumulator.h"
 
 #define MAX_NODE_SCORE 100 /* framework.MaxNodeScore */
 #define KO_D KS_RSV_DIMS
@@ -164,6 +165,16 @@ typedef struct ko_sched {
   int64_t *rord;    /* per node: findMostPreferredReservationByOrder over matched (0 = none) */
   ko_dev dv;
   int64_t *draw;    /* per node: DeviceShare raw score */
+  /* NodeNUMAResource cpusets: topologies, per node topology / allocated / exclusive policy / reserved */
+  int cpu_loaded;
+  int32_t ntopo;
+  ko_topo *topos;
+  int32_t *topo_of;   /* [n], -1 = none */
+  uint8_t *cpu_alloc; /* [n][KO_MAX_CPUS] */
+  int8_t *cpu_excl;   /* [n][KO_MAX_CPUS]: KO_EXCL_* of an allocated CPU, -1 = free */
+  uint8_t *cpu_resv;  /* [n][KO_MAX_CPUS] */
+  uint64_t *cpusets;  /* [np][KS_CPU_WORDS] of the last ko_schedule */
+  int32_t cpusets_cap;
 } ko_sched;
 
 /* pod view for one pod (values pulled out of ks_pod_cols) */
@@ -180,6 +191,8 @@ typedef struct {
   int64_t gpu[3]; /* converted GPU request: core, memory, ratio */
   int has_gpu;
   uint32_t keys; /* bit d: request dimension d is a key of the pod's requests (value != 0) */
+  uint32_t bind;  /* cpu-bind pod (preFilterState.requestCPUBind): ks_pod_cols.cpu_bind, else 0 */
+  int32_t needed; /* numCPUsNeeded */
 } ko_pod;
 
 /* NodeInfo values the Fit plugin reads, after the Reservation restore */
@@ -218,6 +231,10 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
   p->gpu[1] = colv64(pc->gpu_memory, i);
   p->gpu[2] = colv64(pc->gpu_memory_ratio, i);
   p->has_gpu = p->gpu[0] != 0 || p->gpu[1] != 0 || p->gpu[2] != 0;
+  if (s->cfg.numa.enable && (p->flags & KS_POD_CPU_BIND) && pc->cpu_bind) {
+    p->bind = pc->cpu_bind[i];
+    p->needed = (int32_t)(p->cpu / 1000);
+  }
 }
 
 static int64_t pod_dim(const ko_pod *p, int d) { return d == 0 ? p->cpu : d == 1 ? p->mem : d == 2 ? p->eph : p->sc[d - 3]; }
@@ -294,22 +311,32 @@ static int64_t amplify(int64_t origin, double ratio) {
   return (int64_t)ceil((double)origin * ratio);
 }
 
-/* NodeNUMAResource Filter for a pod without cpu bind on a topology-policy-None node:
- * filterAmplifiedCPUs (plugin.go:340-373) on the (restored) NodeInfo */
-static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+/* filterAmplifiedCPUs (plugin.go:340-373) on the (restored) NodeInfo; a cpu-bind pod's request is amplified */
+static uint32_t numa_filter_amplified(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   const ko_nodes *d = &s->nd;
-  if (p->reqzero) return 0; /* PreFilter skip */
   if (p->cpu == 0) return 0;
   if (d->numa_flags[n] & KS_NUMA_INVALID_RATIO) return KS_R_NUMA_INVALID_RATIO;
   double ratio = d->numa_ratio[n];
   if (ratio <= 1) return 0;
+  int64_t pod_cpu = p->bind ? amplify(p->cpu, ratio) : p->cpu;
   int64_t allocated = (int64_t)d->numa_cpus[n] * 1000;
   int64_t requested = e->req[0];
   if (requested >= allocated && allocated > 0) {
     requested -= allocated;
     requested += amplify(allocated, ratio);
   }
-  if (p->cpu > d->alloc_cpu[n] - requested) return KS_R_NUMA_AMPLIFIED_CPU;
+  if (pod_cpu > d->alloc_cpu[n] - requested) return KS_R_NUMA_AMPLIFIED_CPU;
+  return 0;
+}
+
+/* NodeNUMAResource Filter on a topology-policy-None node (plugin.go:275-338): the amplified-CPU check,
+ * then for a cpu-bind pod a valid CPU topology (:296-301).  Preferred bind policies run no trial Allocate
+ * (:318-327 is for a required policy, which the evaluator refuses). */
+static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+  if (p->reqzero) return 0; /* PreFilter skip */
+  uint32_t r = numa_filter_amplified(s, p, n, e);
+  if (r) return r;
+  if (p->bind && !(s->cpu_loaded && s->topo_of[n] >= 0)) return KS_R_NUMA_INVALID_TOPOLOGY;
   return 0;
 }
 
@@ -320,14 +347,16 @@ static int64_t numa_score(const ko_sched *s, const ko_pod *p, int64_t n, const k
   if (p->reqzero) return 0;
   int64_t req_cpu = e->req[0];
   double ratio = d->numa_ratio[n];
+  int64_t pod_cpu = p->cpu;
   if (p->cpu != 0 && ratio > 1) {
     int64_t allocated = (int64_t)d->numa_cpus[n] * 1000;
     req_cpu = req_cpu - allocated + amplify(allocated, ratio);
+    if (p->bind) pod_cpu = amplify(p->cpu, ratio); /* getResourceOptions :503-506 */
   }
   int most = a->strategy == KS_MOST_ALLOCATED;
   int64_t node_score = 0, weight_sum = 0;
   if (a->weight_cpu && d->alloc_cpu[n] != 0) {
-    int64_t rq = req_cpu + p->cpu, cap = d->alloc_cpu[n];
+    int64_t rq = req_cpu + pod_cpu, cap = d->alloc_cpu[n];
     node_score += (most ? ko_most_requested_score(rq, cap) : ko_least_requested_score(rq, cap)) * a->weight_cpu;
     weight_sum += a->weight_cpu;
   }
@@ -996,6 +1025,7 @@ void ko_destroy(ko_sched *s) {
   free(s->dv.flags);
   free(s->dv.total);
   free(s->dv.used);
+  free(s->topos); free(s->topo_of); free(s->cpu_alloc); free(s->cpu_excl); free(s->cpu_resv); free(s->cpusets);
   ko_rsv *rv = &s->rv;
   free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
   free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
@@ -1048,6 +1078,72 @@ int ko_load_reservations(ko_sched *s, const ks_reservation_cols *rc, int32_t nr)
     rv->row[rv->beg[n] + fill[n]++] = r;
   }
   free(fill);
+  return 0;
+}
+
+int ko_load_cpu_state(ko_sched *s, const ks_cpu_topology *topos, int32_t ntopo, const ks_cpu_state_cols *st) {
+  size_t nn = (size_t)(s->n > 0 ? s->n : 1);
+  free(s->topos); free(s->topo_of); free(s->cpu_alloc); free(s->cpu_excl); free(s->cpu_resv);
+  s->topos = (ko_topo *)calloc((size_t)(ntopo > 0 ? ntopo : 1), sizeof(ko_topo));
+  for (int32_t i = 0; i < ntopo; i++) {
+    s->topos[i].ncpus = topos[i].ncpus;
+    for (int c = 0; c < topos[i].ncpus; c++) {
+      s->topos[i].core[c] = topos[i].core[c];
+      s->topos[i].node[c] = topos[i].numa_node[c];
+      s->topos[i].socket[c] = topos[i].socket[c];
+    }
+    ko_topo_finish(&s->topos[i]);
+  }
+  s->ntopo = ntopo;
+  s->topo_of = (int32_t *)calloc(nn, 4);
+  s->cpu_alloc = (uint8_t *)calloc(nn * KO_MAX_CPUS, 1);
+  s->cpu_excl = (int8_t *)malloc(nn * KO_MAX_CPUS);
+  memset(s->cpu_excl, -1, nn * KO_MAX_CPUS);
+  s->cpu_resv = (uint8_t *)calloc(nn * KO_MAX_CPUS, 1);
+  for (int64_t n = 0; n < s->n; n++) {
+    s->topo_of[n] = st->topology[n];
+    int cnt = 0;
+    for (int c = 0; c < KO_MAX_CPUS; c++) {
+      const uint64_t bit = 1ull << (c & 63);
+      const size_t w = (size_t)n * KS_CPU_WORDS + (c >> 6);
+      const size_t o = (size_t)n * KO_MAX_CPUS + c;
+      if (st->allocated[w] & bit) {
+        s->cpu_alloc[o] = 1;
+        cnt++;
+        s->cpu_excl[o] = (st->excl_pcpu && (st->excl_pcpu[w] & bit)) ? KO_EXCL_PCPU
+                         : (st->excl_numa && (st->excl_numa[w] & bit)) ? KO_EXCL_NUMA : KO_EXCL_NONE;
+      }
+      if (st->reserved && (st->reserved[w] & bit)) s->cpu_resv[o] = 1;
+    }
+    s->nd.numa_cpus[n] = cnt; /* filterAmplifiedCPUs: allocated.CPUs().Size() */
+  }
+  s->cpu_loaded = 1;
+  return 0;
+}
+
+/* CPU sets [node*KS_CPU_WORDS + w] */
+int ko_read_cpu_state(const ko_sched *s, uint64_t *allocated, uint64_t *excl_pcpu, uint64_t *excl_numa) {
+  for (int64_t n = 0; n < s->n; n++)
+    for (int w = 0; w < KS_CPU_WORDS; w++) {
+      uint64_t a = 0, xp = 0, xn = 0;
+      for (int b = 0; s->cpu_loaded && b < 64; b++) {
+        const size_t o = (size_t)n * KO_MAX_CPUS + w * 64 + b;
+        if (!s->cpu_alloc[o]) continue;
+        a |= 1ull << b;
+        if (s->cpu_excl[o] == KO_EXCL_PCPU) xp |= 1ull << b;
+        if (s->cpu_excl[o] == KO_EXCL_NUMA) xn |= 1ull << b;
+      }
+      const size_t i = (size_t)n * KS_CPU_WORDS + w;
+      if (allocated) allocated[i] = a;
+      if (excl_pcpu) excl_pcpu[i] = xp;
+      if (excl_numa) excl_numa[i] = xn;
+    }
+  return 0;
+}
+
+int ko_fetch_cpusets(const ko_sched *s, uint64_t *out, int32_t p) {
+  if (p > s->cpusets_cap) return -1;
+  if (p > 0) memcpy(out, s->cpusets, (size_t)p * KS_CPU_WORDS * 8);
   return 0;
 }
 
@@ -1196,8 +1292,49 @@ static void rsv_normalize(ko_sched *s, int64_t *norm) {
   }
 }
 
+/* NodeNUMAResource Reserve for a cpu-bind pod (plugin.go:376-429): resourceManager.Allocate ->
+ * allocateCPUSet (resource_manager.go:314-380: available = CPUs - allocated - reserved, too few -> error;
+ * takeCPUs) then Update -> NodeAllocation.addPodAllocation (node_allocation.go:75-100). */
+static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod) {
+  if (!s->cpu_loaded || s->topo_of[n] < 0) return -1;
+  const ko_topo *t = &s->topos[s->topo_of[n]];
+  uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
+  int8_t *ex = s->cpu_excl + (size_t)n * KO_MAX_CPUS;
+  uint8_t avail[KO_MAX_CPUS], res[KO_MAX_CPUS];
+  int navail = 0;
+  for (int c = 0; c < t->ncpus; c++) {
+    avail[c] = !al[c] && !rs[c];
+    navail += avail[c];
+  }
+  if (navail < p->needed) return -1;
+  uint32_t nf = s->nd.numa_flags[n];
+  int strategy = (nf & KS_NUMA_ALLOC_MOST) ? KO_NUMA_MOST
+                 : (nf & KS_NUMA_ALLOC_LEAST) ? KO_NUMA_LEAST
+                 : (s->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED ? KO_NUMA_MOST : KO_NUMA_LEAST);
+  int excl_policy = (int)((p->bind >> KS_CPU_EXCL_SHIFT) & 3u);
+  int bind = (p->bind & KS_CPU_BIND_POLICY_MASK) == KS_CPU_BIND_FULL_PCPUS ? KO_BIND_FULL_PCPUS : KO_BIND_SPREAD_BY_PCPUS;
+  if (ko_take_cpus(t, 1, avail, NULL, ex, p->needed, bind, excl_policy, strategy, res) != 0) return -1;
+  uint64_t *o = s->cpusets + (size_t)pod * KS_CPU_WORDS;
+  int taken = 0;
+  for (int c = 0; c < t->ncpus; c++) {
+    if (!res[c]) continue;
+    al[c] = 1;
+    ex[c] = (int8_t)excl_policy;
+    o[c >> 6] |= 1ull << (c & 63);
+    taken++;
+  }
+  s->nd.numa_cpus[n] += taken;
+  return 0;
+}
+
 /* one scheduling cycle per pod, in order (scheduleOne loop) */
 int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) {
+  if (np > s->cpusets_cap) {
+    free(s->cpusets);
+    s->cpusets = (uint64_t *)calloc((size_t)np * KS_CPU_WORDS, 8);
+    s->cpusets_cap = np;
+  }
+  if (np > 0) memset(s->cpusets, 0, (size_t)np * KS_CPU_WORDS * 8);
   for (int32_t i = 0; i < np; i++) {
     ko_pod p;
     load_pod(s, pc, i, &p);
@@ -1225,6 +1362,12 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     }
     out[i].node = (int32_t)best_n;
     out[i].score = best;
+    if (p.bind && cpu_reserve(s, &p, best_n, i) != 0) {
+      /* NodeNUMAResource Reserve -> Allocate failed: every Reserve plugin unreserves */
+      out[i].status = KS_S_RESERVE_FAILED;
+      out[i].score = 0;
+      continue;
+    }
     if (s->nom[best_n] >= 0) {
       out[i].reservation = s->nom[best_n];
       rsv_reserve(s, &p, s->nom[best_n]);

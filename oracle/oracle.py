@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 from koordinator_amd import abi
-from koordinator_amd.cluster import DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
+from koordinator_amd.cluster import CpuState, DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
@@ -43,6 +43,9 @@ def lib():
         L.ko_read_reservations.argtypes = [C.c_void_p, abi.P64, abi.P32]
         L.ko_load_devices.argtypes = [C.c_void_p, C.POINTER(abi.KsDeviceCols)]
         L.ko_read_devices.argtypes = [C.c_void_p, abi.P64, abi.P64, abi.P64]
+        L.ko_load_cpu_state.argtypes = [C.c_void_p, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
+        L.ko_read_cpu_state.argtypes = [C.c_void_p, abi.PU64, abi.PU64, abi.PU64]
+        L.ko_fetch_cpusets.argtypes = [C.c_void_p, abi.PU64, C.c_int32]
         L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
         L.ko_eval_pod.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
         L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
@@ -112,7 +115,8 @@ class Oracle:
     """Sequential one-pod-at-a-time scheduler on the CPU (reduced form)."""
 
     def __init__(self, cfg: abi.KsConfig, nodes: NodeTable, quotas: QuotaTable | None = None, nthreads: int = 1,
-                 reservations: ReservationTable | None = None, devices: DeviceTable | None = None):
+                 reservations: ReservationTable | None = None, devices: DeviceTable | None = None,
+                 cpu_state: CpuState | None = None):
         self.L = lib()
         self.cfg = cfg
         self.n = nodes.n
@@ -132,6 +136,10 @@ class Oracle:
         if devices is not None:
             self._d = devices.ks()
             self.L.ko_load_devices(self.h, C.byref(self._d))
+        if cpu_state is not None:
+            self._cs = cpu_state.ks()
+            self._ct = cpu_state.topo_array()
+            self.L.ko_load_cpu_state(self.h, self._ct, len(cpu_state.topologies), C.byref(self._cs))
 
     def close(self):
         if self.h:
@@ -178,6 +186,20 @@ class Oracle:
         out = [np.zeros(G * max(self.n, 1), np.int64) for _ in range(3)]
         self.L.ko_read_devices(self.h, *[o.ctypes.data_as(abi.P64) for o in out])
         return tuple(o[: G * self.n].reshape(G, self.n) for o in out)
+
+    def read_cpu_state(self):
+        W = abi.KS_CPU_WORDS
+        out = [np.zeros((max(self.n, 1), W), np.uint64) for _ in range(3)]
+        self.L.ko_read_cpu_state(self.h, *[o.ctypes.data_as(abi.PU64) for o in out])
+        return tuple(o[: self.n] for o in out)
+
+    def fetch_cpusets(self, p: int) -> np.ndarray:
+        if not self.h:
+            raise ValueError("oracle closed")
+        out = np.zeros((max(p, 1), abi.KS_CPU_WORDS), np.uint64)
+        if self.L.ko_fetch_cpusets(self.h, out.ctypes.data_as(abi.PU64), p) != 0:
+            raise ValueError("no cpusets for that many pods")
+        return out[:p]
 
     def read_quota_used(self) -> np.ndarray:
         used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)

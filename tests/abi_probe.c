@@ -13,5 +13,9 @@ int main(void) {
   O(ks_quota_tree, max); O(ks_quota_tree, self_request); O(ks_quota_tree, cluster_total); O(ks_stats, sweep_ms); O(ks_stats, diag);
   O(ks_config, reservation); O(ks_pod_cols, rsv_class); O(ks_result, reservation); O(ks_reservation_cols, allocatable);
   O(ks_reservation_cols, allocated); O(ks_reservation_cols, assigned); O(ks_reservation_cols, reserve_nonzero_memory);
+  P(ks_numa_args); P(ks_deviceshare_args); P(ks_device_cols); P(ks_cpu_topology); P(ks_cpu_state_cols);
+  O(ks_config, numa); O(ks_config, deviceshare); O(ks_numa_args, numa_scoring_strategy); O(ks_pod_cols, gpu_core);
+  O(ks_pod_cols, cpu_bind); O(ks_cpu_topology, numa_node); O(ks_cpu_topology, socket); O(ks_cpu_state_cols, reserved);
+  O(ks_node_cols, numa_flags); O(ks_result, gpu_minors);
   return 0;
 }

@@ -25,7 +25,9 @@ STRUCTS = {
     "ks_config": abi.KsConfig, "ks_node_cols": abi.KsNodeCols, "ks_pod_cols": abi.KsPodCols,
     "ks_quota_cols": abi.KsQuotaCols, "ks_quota_tree": abi.KsQuotaTree, "ks_result": abi.KsResult, "ks_node_state": abi.KsNodeState,
     "ks_stats": abi.KsStats, "ks_reservation_args": abi.KsReservationArgs,
-    "ks_reservation_cols": abi.KsReservationCols,
+    "ks_reservation_cols": abi.KsReservationCols, "ks_numa_args": abi.KsNumaArgs,
+    "ks_deviceshare_args": abi.KsDeviceShareArgs, "ks_device_cols": abi.KsDeviceCols,
+    "ks_cpu_topology": abi.KsCpuTopology, "ks_cpu_state_cols": abi.KsCpuStateCols,
 }
 
 

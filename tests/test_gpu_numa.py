@@ -1,4 +1,4 @@
-"""GPU parity for NodeNUMAResource (non-cpuset pods, topology policy None):
+"""GPU parity for NodeNUMAResource (SURVEY a21-a23 on topology-policy-None nodes; cpuset pods in test_gpu_cpuset.py):
 the golden tables through the HIP library, and whole-queue scheduling vs the oracle with
 amplified CPUs and cpuset-held CPUs on the nodes, alone and with Fit + LoadAware + Reservation."""
 import numpy as np
@@ -108,13 +108,15 @@ def test_schedule_numa_with_reservations(runtime, oracle_lib):
     assert (got["reservation"] >= 0).sum() > 100
 
 
-def test_cpu_bind_pods_rejected(runtime):
+def test_cpu_bind_pod_needs_policy(runtime):
+    """KS_POD_CPU_BIND without a bind policy in ks_pod_cols.cpu_bind is an invalid argument"""
     rng = np.random.Generator(np.random.PCG64(35))
     nodes = numa_nodes(64, rng)
     pods = synth.make_pods(4, rng)
     pods.flags[1] |= abi.KS_POD_CPU_BIND
+    pods.req_milli_cpu[1] = 4000
     ev = runtime.Evaluator(prof_with_numa(synth.koord_profile()).to_ks_config(), nodes)
     with pytest.raises(runtime.KsError) as ei:
         ev.schedule(pods)
-    assert ei.value.rc == abi.KS_EUNSUPPORTED
+    assert ei.value.rc == abi.KS_EINVAL
     ev.close()
