@@ -1213,6 +1213,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         if (!rsvc) row->pod_count += 1;
       }
     }
+    KS_STAMP(4);
     int32_t nom_row = -1;
     int64_t fitla_pref = -1;  // Fit + LoadAware total of a preferred (ordered) chosen node
     if (RSV && rsvc) {
@@ -1351,13 +1352,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         }
       }
     }
-    KS_STAMP(4);
+    KS_STAMP(5);
     }
   next_pod:
     if (j + 1 < np) lookahead(j + 1);
     KS_STAMP(1);
   }
-  KS_STAMP(5);
+  KS_STAMP(6);
   // ---- write back: results, touched rows, quota usage ----
   if (lane < processed) a.results[cursor0 + lane] = sres[lane];
   if (lane < nslots) {
@@ -1395,9 +1396,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     if (processed < np) atomicAdd(&a.counters[1], 1ull);
     atomicAdd(&a.counters[2], (unsigned long long)rescans);
     atomicAdd(&a.counters[3], (unsigned long long)misses);
-    atomicAdd(&a.counters[14], (unsigned long long)fast);  // ks_stats.diag[6]: monotone fast picks
+    atomicAdd(&a.counters[15], (unsigned long long)fast);  // ks_stats.diag[7]: monotone fast picks
 #ifdef KS_COMMIT_STAMPS
-    for (int i = 0; i < 6; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
+    for (int i = 0; i < 7; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
 #endif
   }
 #undef KS_STAMP
