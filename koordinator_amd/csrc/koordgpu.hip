@@ -1124,22 +1124,34 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         }
         if (lane < RF_N) raw[lane] = v;
       }
-      if (cpubind && (int32_t)src[RF_CPU_FREE] < cpu_need) {
+      // Every field this slot needs is read before the first LDS write: the compiler cannot prove the
+      // slot writes do not alias `src`, so each read after a write would cost a full LDS round trip.
+      const bool take = !t_prod_only || (pflags & KS_POD_PROD);  // (before the Reservation match below)
+      const int64_t f_cap = src[t_cap], f_req = src[t_req], f_pw = podw[t_pw];
+      const int64_t u_bits = src[RF_LA_BITS], u_allowed = src[RF_ALLOWED], u_pods = src[RF_POD_COUNT];
+      const int64_t u_acpu = src[RF_ALLOC_CPU], u_amem = src[RF_ALLOC_MEM], u_aeph = src[RF_ALLOC_EPH];
+      const uint64_t ncl = RSV ? (uint64_t)src[RF_RSV_CLS] : 0ull;
+      const int32_t u_rb = RSV ? (int32_t)src[RF_RSV_BEG] : 0, u_re = RSV ? (int32_t)src[RF_RSV_END] : 0;
+      const int64_t u_A = (FEAT & 2) ? src[RF_NUMA_A] : 0, u_off = (FEAT & 2) ? src[RF_NUMA_OFF] : 0;
+      const int64_t u_ratio = (FEAT & 2) ? src[RF_NUMA_RATIO] : 0;
+      const int32_t u_free = (FEAT & 2) ? (int32_t)src[RF_CPU_FREE] : 0;
+      if (cpubind && u_free < cpu_need) {
         // NodeNUMAResource Reserve -> Allocate: not enough CPUs; every plugin unreserves
         --nslots;
         if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0};
         goto next_pod;
       }
       if (lane == s) snode = node;
-      if (lane == 0) touched[node >> 6] |= 1ull << (node & 63);
-      const uint64_t ncl = (uint64_t)src[RF_RSV_CLS];
+      if (lane == 0) atomicOr(&touched[node >> 6], 1ull << (node & 63));
       rsvc = pcls >= 0 && pcls < 64 && ((ncl >> pcls) & 1ull);
       if (lane == 0) {
-        scls[s] = ncl;
-        snuma[4 * s] = src[RF_NUMA_A];
-        snuma[4 * s + 1] = src[RF_NUMA_OFF];
-        snuma[4 * s + 2] = src[RF_NUMA_RATIO];
-        snuma[4 * s + 3] = (int64_t)(int32_t)src[RF_CPU_FREE];
+        if (RSV) scls[s] = ncl;
+        if (FEAT & 2) {
+          snuma[4 * s] = u_A;
+          snuma[4 * s + 1] = u_off;
+          snuma[4 * s + 2] = u_ratio;
+          snuma[4 * s + 3] = (int64_t)u_free;
+        }
       }
       if (DEV && cfg.dev) {
         // the node's GPU totals / used / present flag into LDS (lane = word)
@@ -1154,7 +1166,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       }
       if (RSV && cfg.rsv) {
         // the node's reservations into LDS (lane = record word), unless too many or too wide
-        const int32_t rb = (int32_t)src[RF_RSV_BEG], cnt = (int32_t)src[RF_RSV_END] - rb;
+        const int32_t rb = u_rb, cnt = u_re - u_rb;
         int32_t mode = -1;
         if (cnt <= a.rcap) {
           constexpr int W = (int)(sizeof(RsvRec<RD>) / 8);
@@ -1181,9 +1193,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         }
       }
       // build the slot row with the pod already reserved on it (lane-parallel, one code path)
-      const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
-      const int64_t cap = src[t_cap],
-                    req = src[t_req] + (take ? podw[t_pw] : 0) + (lane == ST_NCPU ? src[RF_NUMA_OFF] : 0);
+      const bool take_here = take && !rsvc;
+      const int64_t cap = f_cap, req = f_req + (take_here ? f_pw : 0) + (lane == ST_NCPU ? u_off : 0);
       if (lane < ST_N) {
         Term t;
         t.c = cap;
@@ -1193,11 +1204,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         t.rcp = rcp100(cap);
         row->t[lane] = t;
       } else if (lane == kLaneCounts) {
-        row->la_bits = (uint32_t)src[RF_LA_BITS];
-        row->allowed = (int32_t)src[RF_ALLOWED];
-        row->pod_count = (int32_t)src[RF_POD_COUNT] + (rsvc ? 0 : 1);
-        row->fit_ws = (src[RF_ALLOC_CPU] != 0 ? cfg.fw_cpu : 0) + (src[RF_ALLOC_MEM] != 0 ? cfg.fw_mem : 0) +
-                      (src[RF_ALLOC_EPH] != 0 ? cfg.fw_eph : 0);
+        row->la_bits = (uint32_t)u_bits;
+        row->allowed = (int32_t)u_allowed;
+        row->pod_count = (int32_t)u_pods + (rsvc ? 0 : 1);
+        row->fit_ws = (u_acpu != 0 ? cfg.fw_cpu : 0) + (u_amem != 0 ? cfg.fw_mem : 0) + (u_aeph != 0 ? cfg.fw_eph : 0);
       }
     } else {
       if (cpubind && (int32_t)snuma[4 * s + 3] < cpu_need) {
@@ -1339,9 +1349,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
           const int64_t qreq = pqreq[j * KS_QUOTA_DIMS + lane];
           const bool np_ = (pflags & KS_POD_NONPREEMPTIBLE) != 0;
           if (QC) {
-            for (int32_t cur = qrow; cur >= 0; cur = qlds->parent[cur]) {
-              qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
-              if (np_) qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+            // LDS atomics: no read-back on the sequential path (the next pod's admission reads after them)
+            for (int32_t cur = qrow; cur >= 0;) {
+              const int32_t up = qlds->parent[cur];
+              atomicAdd((unsigned long long*)&qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane], (unsigned long long)qreq);
+              if (np_) atomicAdd((unsigned long long*)&qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane], (unsigned long long)qreq);
+              cur = up;
             }
           } else {
             for (int32_t cur = qrow; cur >= 0; cur = a.q.parent[cur]) {
