@@ -58,6 +58,7 @@ extern "C" {
 #define KS_MAX_GPUS 8     /* GPU minors per node (ks_device_cols); minor = slot index */
 #define KS_MAX_CPUS 256   /* logical CPUs per node topology (ks_cpu_topology); CPU ids 0..ncpus-1 */
 #define KS_CPU_WORDS 4    /* uint64 words of a CPU set (bit c = CPU c) */
+#define KS_MAX_NUMA 8     /* NUMA nodes per node (ks_numa_node_cols); the device evaluates up to 4 */
 
 /* ---- status codes ---- */
 #define KS_OK 0
@@ -103,6 +104,11 @@ extern "C" {
 #define KS_NUMA_TOPOLOGY_POLICY 0x4u /* NUMA topology policy != None (getNUMATopologyPolicy): unsupported         */
 #define KS_NUMA_ALLOC_LEAST 0x8u     /* label numa-allocate-strategy = LeastAllocated (GetNUMAAllocateStrategy, util.go:30-36) */
 #define KS_NUMA_ALLOC_MOST 0x10u     /* label numa-allocate-strategy = MostAllocated                                */
+#define KS_NUMA_POLICY_SHIFT 5       /* bits 5-6: NUMA topology policy (getNUMATopologyPolicy, util.go:52-58)          */
+#define KS_NUMA_POLICY_NONE 0u
+#define KS_NUMA_POLICY_BEST_EFFORT 1u
+#define KS_NUMA_POLICY_RESTRICTED 2u
+#define KS_NUMA_POLICY_SINGLE_NUMA_NODE 3u
 
 /* ---- pod cpuset request (ks_pod_cols.cpu_bind, with KS_POD_CPU_BIND) ---- */
 #define KS_CPU_BIND_FULL_PCPUS 1u       /* schedulingconfig.CPUBindPolicyFullPCPUs     */
@@ -130,6 +136,9 @@ extern "C" {
 #define KS_R_DEV_INSUFFICIENT 0x2000u   /* DeviceShare "Insufficient gpu devices" (device_allocator.go:453-456)  */
 #define KS_R_DEV_NO_GPU 0x4000u         /* DeviceShare: node has no (healthy) GPU (devicehandler_gpu.go:41-50)  */
 #define KS_R_NUMA_INVALID_TOPOLOGY 0x8000u /* ErrInvalidCPUTopology: cpu-bind pod on a node without a valid CPU topology (plugin.go:296-301) */
+#define KS_R_NUMA_AFFINITY 0x10000u    /* topology manager Admit: "node(s) NUMA Topology affinity error" (topologymanager/manager.go:64-66) */
+#define KS_R_NUMA_INSUFFICIENT 0x20000u /* NUMA Allocate: "Insufficient NUMA <resource>" (resource_manager.go:269-276) */
+#define KS_R_NUMA_MISSING 0x40000u     /* "node(s) missing NUMA resources" (topology_hint.go:33-36) */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -408,6 +417,21 @@ typedef struct ks_cpu_state_cols {
   const uint64_t *reserved;     /* kubelet reserved CPUs (TopologyOptions.ReservedCPUs); NULL = none */
 } ks_cpu_state_cols;
 
+/* NUMA node resources of the nodes with a NUMA topology policy (TopologyOptions.NUMANodeResources and
+ * NodeAllocation.allocatedResources, node_allocation.go:37-177), [node*KS_MAX_NUMA + k] for NUMA node k
+ * (ids 0..count-1).  The cpu amplification ratio of the node (ks_node_cols.numa_cpu_amplification)
+ * amplifies alloc_cpu and the cpuset part of used_cpu as amplifyNUMANodeResources /
+ * getAvailableNUMANodeResources do. */
+typedef struct ks_numa_node_cols {
+  const int32_t *count;         /* [node] NUMA nodes with resources (0 = none) */
+  const int64_t *alloc_cpu;     /* milli-CPU, before amplification */
+  const int64_t *alloc_memory;
+  const int64_t *used_cpu;      /* NULL = 0 */
+  const int64_t *used_memory;   /* NULL = 0 */
+  const uint8_t *used_present;  /* an allocatedResources entry exists for the NUMA node; NULL = used != 0 */
+  const int32_t *cpuset_cpus;   /* allocated cpuset CPUs on the NUMA node; NULL = 0 */
+} ks_numa_node_cols;
+
 typedef struct ks_result {
   int32_t node;    /* chosen node index, -1 if not scheduled */
   uint32_t status; /* KS_S_* */
@@ -469,6 +493,12 @@ int ks_read_devices(ks_ctx *ctx, int64_t *used_core, int64_t *used_memory, int64
  * a KS_POD_CPU_BIND pod allocates its CPUs with the CPU accumulator (takeCPUs, cpu_accumulator.go:86-232)
  * and adds them to the node's allocation (NodeAllocation.addPodAllocation, node_allocation.go:75-100). */
 int ks_load_cpu_state(ks_ctx *ctx, const ks_cpu_topology *topologies, int32_t ntopo, const ks_cpu_state_cols *state);
+/* NUMA node resources of the nodes with a NUMA topology policy (policy in ks_node_cols.numa_flags); call
+ * after ks_load_nodes.  Pods on such nodes go through the hint providers, the topology manager merge
+ * and the NUMA allocation; Reserve adds the allocation to used. */
+int ks_load_numa_nodes(ks_ctx *ctx, const ks_numa_node_cols *numa);
+/* used amounts after commits, [node*KS_MAX_NUMA + k]; NULL = skip */
+int ks_read_numa_nodes(ks_ctx *ctx, int64_t *used_cpu, int64_t *used_memory);
 /* CPU sets after commits, [node*KS_CPU_WORDS + w]; NULL = skip */
 int ks_read_cpu_state(ks_ctx *ctx, uint64_t *allocated, uint64_t *excl_pcpu, uint64_t *excl_numa);
 /* The CPUs allocated to each pod of the last ks_schedule / ks_schedule_staged call ([pod*KS_CPU_WORDS + w],

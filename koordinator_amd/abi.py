@@ -14,6 +14,7 @@ KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
 KS_MAX_CPUS = 256
 KS_CPU_WORDS = 4
+KS_MAX_NUMA = 8
 KS_RSV_DIMS = 3 + KS_MAX_SCALARS
 KS_RSV_CLASSES = 64
 
@@ -51,6 +52,11 @@ KS_NUMA_CPU_BIND_POLICY = 0x2
 KS_NUMA_TOPOLOGY_POLICY = 0x4
 KS_NUMA_ALLOC_LEAST = 0x8
 KS_NUMA_ALLOC_MOST = 0x10
+KS_NUMA_POLICY_SHIFT = 5
+KS_NUMA_POLICY_NONE = 0
+KS_NUMA_POLICY_BEST_EFFORT = 1
+KS_NUMA_POLICY_RESTRICTED = 2
+KS_NUMA_POLICY_SINGLE_NUMA_NODE = 3
 
 KS_CPU_BIND_FULL_PCPUS = 1
 KS_CPU_BIND_SPREAD_BY_PCPUS = 2
@@ -76,6 +82,9 @@ KS_R_NUMA_INVALID_RATIO = 0x1000
 KS_R_DEV_INSUFFICIENT = 0x2000
 KS_R_DEV_NO_GPU = 0x4000
 KS_R_NUMA_INVALID_TOPOLOGY = 0x8000
+KS_R_NUMA_AFFINITY = 0x10000
+KS_R_NUMA_INSUFFICIENT = 0x20000
+KS_R_NUMA_MISSING = 0x40000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -305,6 +314,11 @@ class KsCpuStateCols(C.Structure):
                 ("reserved", PU64)]
 
 
+class KsNumaNodeCols(C.Structure):
+    _fields_ = [("count", P32), ("alloc_cpu", P64), ("alloc_memory", P64), ("used_cpu", P64), ("used_memory", P64),
+                ("used_present", C.POINTER(C.c_uint8)), ("cpuset_cpus", P32)]
+
+
 class KsResult(C.Structure):
     _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64), ("reservation", C.c_int32),
                 ("gpu_minors", C.c_uint32)]
@@ -362,6 +376,8 @@ EXPORTED_SYMBOLS = [
     "ks_load_cpu_state",
     "ks_read_cpu_state",
     "ks_fetch_cpusets",
+    "ks_load_numa_nodes",
+    "ks_read_numa_nodes",
     "ks_load_reservations",
     "ks_read_reservations",
     "ks_refresh_quota_runtime",

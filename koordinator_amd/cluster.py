@@ -376,6 +376,41 @@ class CpuState:
         return c
 
 
+class NumaNodes:
+    """ks_numa_node_cols: per node the NUMA nodes of a node with a NUMA topology policy, [node][k] arrays
+    (NUMANodeResources cpu milli / memory, allocatedResources used cpu / memory + presence, cpuset CPUs)."""
+
+    def __init__(self, n: int):
+        self.n = int(n)
+        K = abi.KS_MAX_NUMA
+        self.count = np.zeros(self.n, np.int32)
+        for k in ("alloc_cpu", "alloc_memory", "used_cpu", "used_memory"):
+            setattr(self, k, np.zeros((self.n, K), np.int64))
+        self.used_present = np.zeros((self.n, K), np.uint8)
+        self.cpuset_cpus = np.zeros((self.n, K), np.int32)
+
+    def copy(self) -> "NumaNodes":
+        t = NumaNodes(self.n)
+        for k in ("count", "alloc_cpu", "alloc_memory", "used_cpu", "used_memory", "used_present", "cpuset_cpus"):
+            setattr(t, k, getattr(self, k).copy())
+        return t
+
+    def ks(self) -> abi.KsNumaNodeCols:
+        c = abi.KsNumaNodeCols()
+        self.count = np.ascontiguousarray(self.count, np.int32)
+        c.count = _p32(self.count)
+        for k in ("alloc_cpu", "alloc_memory", "used_cpu", "used_memory"):
+            arr = np.ascontiguousarray(getattr(self, k), np.int64)
+            setattr(self, k, arr)
+            setattr(c, k, _p64(arr))
+        self.used_present = np.ascontiguousarray(self.used_present, np.uint8)
+        c.used_present = self.used_present.ctypes.data_as(C.POINTER(C.c_uint8))
+        self.cpuset_cpus = np.ascontiguousarray(self.cpuset_cpus, np.int32)
+        c.cpuset_cpus = _p32(self.cpuset_cpus)
+        c._keep = self
+        return c
+
+
 class ReservationTable:
     """Available reservations (ks_reservation_cols): one row per ReservationInfo
     (pkg/scheduler/frameworkext/reservation_info.go:37-115); resources [dim][row] with dims

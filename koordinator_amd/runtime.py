@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import CpuState, DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
+from .cluster import CpuState, DeviceTable, NumaNodes, NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
     L.ks_load_cpu_state.argtypes = [vp, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
     L.ks_read_cpu_state.argtypes = [vp, abi.PU64, abi.PU64, abi.PU64]
     L.ks_fetch_cpusets.argtypes = [vp, abi.PU64, C.c_int32]
+    L.ks_load_numa_nodes.argtypes = [vp, C.POINTER(abi.KsNumaNodeCols)]
+    L.ks_read_numa_nodes.argtypes = [vp, abi.P64, abi.P64]
     L.ks_refresh_quota_runtime.argtypes = [vp, C.POINTER(abi.KsQuotaTree), C.c_int32, abi.P64, abi.PU32]
     L.ks_schedule.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
     L.ks_stage_pods.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32]
@@ -99,7 +101,7 @@ class Evaluator:
 
     def __init__(self, cfg: abi.KsConfig, nodes: Optional[NodeTable] = None, quotas: Optional[QuotaTable] = None,
                  reservations: Optional[ReservationTable] = None, devices: Optional[DeviceTable] = None,
-                 cpu_state: Optional[CpuState] = None):
+                 cpu_state: Optional[CpuState] = None, numa_nodes: Optional[NumaNodes] = None):
         self.L = lib()
         self.cfg = cfg
         h = C.c_void_p()
@@ -121,6 +123,8 @@ class Evaluator:
             self.load_devices(devices)
         if cpu_state is not None:
             self.load_cpu_state(cpu_state)
+        if numa_nodes is not None:
+            self.load_numa_nodes(numa_nodes)
 
     def _chk(self, rc: int):
         if rc != abi.KS_OK:
@@ -172,6 +176,18 @@ class Evaluator:
         cols = st.ks()
         topos = st.topo_array()
         self._chk(self.L.ks_load_cpu_state(self.h, topos, len(st.topologies), C.byref(cols)))
+
+    def load_numa_nodes(self, nn: NumaNodes):
+        """NUMA node resources of the nodes with a NUMA topology policy."""
+        cols = nn.ks()
+        self._chk(self.L.ks_load_numa_nodes(self.h, C.byref(cols)))
+
+    def read_numa_nodes(self):
+        """(used_cpu, used_memory), each [n][KS_MAX_NUMA]"""
+        K = abi.KS_MAX_NUMA
+        out = [np.zeros((max(self.n, 1), K), np.int64) for _ in range(2)]
+        self._chk(self.L.ks_read_numa_nodes(self.h, *[o.ctypes.data_as(abi.P64) for o in out]))
+        return tuple(o[: self.n] for o in out)
 
     def read_cpu_state(self):
         """(allocated, excl_pcpu, excl_numa), each [n][KS_CPU_WORDS] uint64"""

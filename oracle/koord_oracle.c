@@ -175,6 +175,13 @@ typedef struct ko_sched {
   uint8_t *cpu_resv;  /* [n][KO_MAX_CPUS] */
   uint64_t *cpusets;  /* [np][KS_CPU_WORDS] of the last ko_schedule */
   int32_t cpusets_cap;
+  /* NUMA topology policies: per node and NUMA node k ([n*KS_MAX_NUMA + k]) */
+  int numa_loaded;
+  int32_t *numa_count;
+  int64_t *numa_alloc;  /* [n][KS_MAX_NUMA][2]: NUMANodeResources cpu (milli, raw), memory */
+  int64_t *numa_used;   /* [n][KS_MAX_NUMA][2]: allocatedResources */
+  uint8_t *numa_present;
+  int32_t *numa_cs;     /* allocated cpuset CPUs per NUMA node */
 } ko_sched;
 
 /* pod view for one pod (values pulled out of ks_pod_cols) */
@@ -332,11 +339,19 @@ static uint32_t numa_filter_amplified(const ko_sched *s, const ko_pod *p, int64_
 /* NodeNUMAResource Filter on a topology-policy-None node (plugin.go:275-338): the amplified-CPU check,
  * then for a cpu-bind pod a valid CPU topology (:296-301).  Preferred bind policies run no trial Allocate
  * (:318-327 is for a required policy, which the evaluator refuses). */
+static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *score,
+                                 int64_t alloc[][2]);
+static int node_numa_policy(const ko_sched *s, int64_t n);
+
 static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   if (p->reqzero) return 0; /* PreFilter skip */
   uint32_t r = numa_filter_amplified(s, p, n, e);
   if (r) return r;
   if (p->bind && !(s->cpu_loaded && s->topo_of[n] >= 0)) return KS_R_NUMA_INVALID_TOPOLOGY;
+  if (node_numa_policy(s, n) != 0) {
+    int64_t alloc[KS_MAX_NUMA][2];
+    return numa_policy_eval(s, p, n, e, NULL, alloc);
+  }
   return 0;
 }
 
@@ -345,6 +360,10 @@ static int64_t numa_score(const ko_sched *s, const ko_pod *p, int64_t n, const k
   const ko_nodes *d = &s->nd;
   const ks_numa_args *a = &s->cfg.numa;
   if (p->reqzero) return 0;
+  if (node_numa_policy(s, n) != 0) {
+    int64_t sc = 0, alloc[KS_MAX_NUMA][2];
+    return numa_policy_eval(s, p, n, e, &sc, alloc) ? 0 : sc;
+  }
   int64_t req_cpu = e->req[0];
   double ratio = d->numa_ratio[n];
   int64_t pod_cpu = p->cpu;
@@ -367,6 +386,276 @@ static int64_t numa_score(const ko_sched *s, const ko_pod *p, int64_t n, const k
   }
   if (weight_sum == 0) return 0;
   return node_score / weight_sum;
+}
+
+/* ------------------------------------------------------------------ */
+/* NUMA topology policies (nodenumaresource + frameworkext/topologymanager)                      */
+/* ------------------------------------------------------------------ */
+
+static int node_numa_policy(const ko_sched *s, int64_t n) {
+  return (int)((s->nd.numa_flags[n] >> KS_NUMA_POLICY_SHIFT) & 3u);
+}
+
+typedef struct {
+  uint32_t mask;  /* NUMANodeAffinity, 0 = nil */
+  int preferred;
+  int64_t score;
+} ko_hint;
+
+/* resourceAllocationScorer.score (scoring.go:206-242) over cpu / memory with the plugin weights */
+static int64_t numa_res_score(const ko_sched *s, int most, const int64_t req[2], const int64_t alloc[2],
+                              const ko_pod *p) {
+  const int64_t w[2] = {s->cfg.numa.weight_cpu, s->cfg.numa.weight_memory};
+  const int64_t pod[2] = {p->cpu, p->mem};
+  int64_t ns = 0, ws = 0;
+  for (int r = 0; r < 2; r++) {
+    if (!w[r] || alloc[r] == 0) continue;
+    int64_t rq = req[r] + pod[r];
+    ns += (most ? ko_most_requested_score(rq, alloc[r]) : ko_least_requested_score(rq, alloc[r])) * w[r];
+    ws += w[r];
+  }
+  return ws ? ns / ws : 0;
+}
+
+/* per NUMA node: amplified NUMANodeResources (amplifyNUMANodeResources, util.go:60-80), allocated with
+ * the cpuset amplification adjustment and available (getAvailableNUMANodeResources, node_allocation.go:148-177) */
+static void numa_state(const ko_sched *s, int64_t n, int K, int64_t total[][2], int64_t used[][2], int present[],
+                       int64_t avail[][2]) {
+  const double ratio = s->nd.numa_ratio[n];
+  for (int k = 0; k < K; k++) {
+    const size_t o = (size_t)n * KS_MAX_NUMA + k;
+    total[k][0] = amplify(s->numa_alloc[o * 2], ratio);
+    total[k][1] = s->numa_alloc[o * 2 + 1];
+    present[k] = s->numa_present[o];
+    used[k][0] = used[k][1] = 0;
+    if (present[k]) {
+      used[k][0] = s->numa_used[o * 2];
+      used[k][1] = s->numa_used[o * 2 + 1];
+      if (ratio > 1) {
+        int64_t cs = (int64_t)s->numa_cs[o] * 1000;
+        used[k][0] = used[k][0] - cs + amplify(cs, ratio);
+      }
+      for (int r = 0; r < 2; r++)
+        if (used[k][r] < 0) used[k][r] = 0; /* SubtractWithNonNegativeResult(allocated, reusable) */
+    }
+    for (int r = 0; r < 2; r++) {
+      avail[k][r] = total[k][r] - used[k][r];
+      if (avail[k][r] < 0) avail[k][r] = 0;
+    }
+  }
+}
+
+/* bitmask.IterateBitMasks order: by size, then lexicographic over the NUMA ids */
+static int iterate_masks(int K, uint32_t *out) {
+  int m = 0;
+  for (int size = 1; size <= K; size++) {
+    int idx[KS_MAX_NUMA];
+    for (int i = 0; i < size; i++) idx[i] = i;
+    for (;;) {
+      uint32_t mask = 0;
+      for (int i = 0; i < size; i++) mask |= 1u << idx[i];
+      out[m++] = mask;
+      int i = size - 1;
+      while (i >= 0 && idx[i] == K - size + i) i--;
+      if (i < 0) break;
+      idx[i]++;
+      for (int k = i + 1; k < size; k++) idx[k] = idx[k - 1] + 1;
+    }
+  }
+  return m;
+}
+
+/* IsNarrowerThan (pkg/util/bitmask/bitmask.go:146-151) */
+static int narrower(uint32_t a, uint32_t b) {
+  int ca = __builtin_popcount(a), cb = __builtin_popcount(b);
+  if (ca == cb) return a < b;
+  return ca < cb;
+}
+
+/* Filter (FilterByNUMANode -> topology manager Admit) and Score for a pod on a node with a NUMA topology
+ * policy.  Hints: generateResourceHints (resource_manager.go:459-593, numaScorer = the NUMAScoringStrategy
+ * type with the ScoringStrategy weights, plugin.go:118-124); merge: filterProvidersHints / mergeFilteredHints
+ * (topologymanager/policy.go:96-187) with the resources in the order cpu, memory (Go iterates a map);
+ * policies policy_best_effort.go / policy_restricted.go / policy_single_numa_node.go; allocation:
+ * tryBestToDistributeEvenly (resource_manager.go:221-283, its sort compares totalAvailable by slice
+ * position as the Go code does).  Returns KS_R_* reasons; *score = the node score over the allocated NUMA
+ * nodes (calculateAllocatableAndRequested, scoring.go:116-163); alloc[k] = the pod's allocation. */
+static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *score,
+                                 int64_t alloc[][2]) {
+  const int K = s->numa_loaded ? s->numa_count[n] : 0;
+  const int pol = node_numa_policy(s, n);
+  if (score) *score = 0;
+  for (int k = 0; k < KS_MAX_NUMA; k++) alloc[k][0] = alloc[k][1] = 0;
+  if (K == 0) return KS_R_NUMA_MISSING;
+  int64_t total[KS_MAX_NUMA][2], used[KS_MAX_NUMA][2], avail[KS_MAX_NUMA][2];
+  int present[KS_MAX_NUMA];
+  numa_state(s, n, K, total, used, present, avail);
+  const int64_t req[2] = {p->cpu, p->mem};
+  const int want[2] = {p->cpu != 0, p->mem != 0};
+  /* generateResourceHints */
+  uint32_t masks[256];
+  const int nm = iterate_masks(K, masks);
+  ko_hint hints[2][256];
+  int nh[2] = {0, 0}, min_size[2] = {K, K};
+  uint32_t lack[2] = {0, 0};
+  for (int r = 0; r < 2; r++)
+    for (int k = 0; k < K; k++)
+      if (avail[k][r] == 0) lack[r] |= 1u << k;
+  const int numa_most = s->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED;
+  for (int m = 0; m < nm; m++) {
+    int64_t tsum[2] = {0, 0}, fsum[2] = {0, 0};
+    for (int k = 0; k < K; k++)
+      if ((masks[m] >> k) & 1u)
+        for (int r = 0; r < 2; r++) {
+          tsum[r] += total[k][r];
+          fsum[r] += avail[k][r];
+        }
+    int64_t rq[2] = {tsum[0] - fsum[0], tsum[1] - fsum[1]};
+    for (int r = 0; r < 2; r++)
+      if (rq[r] < 0) rq[r] = 0;
+    const int64_t sc = numa_res_score(s, numa_most, rq, tsum, p);
+    for (int r = 0; r < 2; r++) { /* memory first (memoryResourceNames), then cpu: independent lists */
+      if (!want[r]) continue;
+      if (tsum[r] < req[r]) continue;
+      if (masks[m] & lack[r]) continue;
+      int cnt = __builtin_popcount(masks[m]);
+      if (cnt < min_size[r]) min_size[r] = cnt;
+      if (fsum[r] < req[r]) continue;
+      hints[r][nh[r]++] = (ko_hint){masks[m], 0, sc};
+    }
+  }
+  for (int r = 0; r < 2; r++)
+    for (int i = 0; i < nh[r]; i++) hints[r][i].preferred = __builtin_popcount(hints[r][i].mask) == min_size[r];
+  /* filterProvidersHints: one list per requested NUMA resource (cpu, then memory); none -> any-numa */
+  ko_hint lists[2][256];
+  int nl = 0, ln[2];
+  for (int r = 0; r < 2; r++) {
+    if (!want[r]) continue;
+    if (nh[r] == 0) {
+      lists[nl][0] = (ko_hint){0, 0, 0}; /* no possible NUMA affinities */
+      ln[nl++] = 1;
+    } else {
+      memcpy(lists[nl], hints[r], sizeof(ko_hint) * nh[r]);
+      ln[nl++] = nh[r];
+    }
+  }
+  if (nl == 0) {
+    lists[0][0] = (ko_hint){0, 1, 0};
+    ln[0] = 1;
+    nl = 1;
+  }
+  if (pol == KS_NUMA_POLICY_SINGLE_NUMA_NODE) { /* filterSingleNumaHints */
+    for (int l = 0; l < nl; l++) {
+      int k = 0;
+      for (int i = 0; i < ln[l]; i++) {
+        const ko_hint h = lists[l][i];
+        if ((h.mask == 0 && h.preferred) || (h.mask != 0 && __builtin_popcount(h.mask) == 1 && h.preferred))
+          lists[l][k++] = h;
+      }
+      ln[l] = k;
+    }
+  }
+  /* mergeFilteredHints over the cartesian product (first list outermost) */
+  const uint32_t dflt = (K >= 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);
+  ko_hint best = {dflt, 0, 0};
+  int idx[2] = {0, 0};
+  int empty = 0;
+  for (int l = 0; l < nl; l++) empty |= ln[l] == 0;
+  while (!empty) {
+    uint32_t merged = dflt;
+    int pref = 1, have = 0;
+    uint32_t first = 0;
+    for (int l = 0; l < nl; l++) {
+      const ko_hint h = lists[l][idx[l]];
+      if (h.mask) {
+        if (!have) first = h.mask;
+        else if (h.mask != first) pref = 0;
+        have = 1;
+        merged &= h.mask;
+      }
+      if (!h.preferred) pref = 0;
+    }
+    if (merged) {
+      int64_t msc = 0;
+      for (int l = 0; l < nl; l++) {
+        const ko_hint h = lists[l][idx[l]];
+        if (h.mask && h.mask == merged && h.score > msc) msc = h.score;
+      }
+      if (pref && !best.preferred) {
+        best = (ko_hint){merged, pref, msc};
+      } else if (!pref && best.preferred) {
+        /* keep */
+      } else if (!narrower(merged, best.mask)) {
+        if (__builtin_popcount(merged) == __builtin_popcount(best.mask) && msc > best.score)
+          best = (ko_hint){merged, pref, msc};
+      } else {
+        best = (ko_hint){merged, pref, msc};
+      }
+    }
+    int l = nl - 1;
+    while (l >= 0 && ++idx[l] == ln[l]) idx[l--] = 0;
+    if (l < 0) break;
+  }
+  uint32_t affinity = best.mask;
+  int admit = 1;
+  if (pol == KS_NUMA_POLICY_SINGLE_NUMA_NODE) {
+    if (affinity == dflt) affinity = 0;
+    admit = best.preferred;
+  } else if (pol == KS_NUMA_POLICY_RESTRICTED) {
+    admit = best.preferred;
+  }
+  if (!admit) return KS_R_NUMA_AFFINITY;
+  /* NUMA plugin Allocate -> allocateResourcesByHint -> tryBestToDistributeEvenly */
+  if (affinity) {
+    int bits[KS_MAX_NUMA], nb = 0;
+    for (int k = 0; k < K; k++)
+      if ((affinity >> k) & 1u) bits[nb++] = k;
+    for (int r = 0; r < 2; r++) {
+      if (!want[r]) continue;
+      int order[KS_MAX_NUMA];
+      memcpy(order, bits, sizeof(int) * nb);
+      /* sort.Slice insertion sort with less(i, j) = totalAvailable[i] < totalAvailable[j] (positions) */
+      for (int i = 1; i < nb; i++)
+        for (int j = i; j > 0; j--) {
+          const int64_t aj = j < K ? avail[j][r] : 0, ai = (j - 1) < K ? avail[j - 1][r] : 0;
+          if (!(aj < ai)) break;
+          int t = order[j];
+          order[j] = order[j - 1];
+          order[j - 1] = t;
+        }
+      int64_t q = req[r];
+      for (int i = 0; i < nb; i++) {
+        const int64_t split = q / (nb - i);
+        const int64_t a = avail[order[i]][r];
+        const int64_t got = a > split ? split : a;
+        if (got != 0) {
+          alloc[order[i]][r] = got;
+          q -= got;
+        }
+      }
+      if (q != 0) return KS_R_NUMA_INSUFFICIENT;
+    }
+  }
+  if (score) {
+    int64_t treq[2] = {0, 0}, talloc[2] = {0, 0};
+    int any = 0;
+    for (int k = 0; k < K; k++) {
+      if (!alloc[k][0] && !alloc[k][1]) continue;
+      any = 1;
+      for (int r = 0; r < 2; r++) {
+        talloc[r] += total[k][r];
+        if (present[k]) treq[r] += used[k][r];
+      }
+    }
+    if (!any) { /* nodeInfo.Allocatable / Requested */
+      talloc[0] = s->nd.alloc_cpu[n];
+      talloc[1] = s->nd.alloc_mem[n];
+      treq[0] = e->req[0];
+      treq[1] = e->req[1];
+    }
+    *score = numa_res_score(s, s->cfg.numa.strategy == KS_MOST_ALLOCATED, treq, talloc, p);
+  }
+  return 0;
 }
 
 static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
@@ -1026,6 +1315,7 @@ void ko_destroy(ko_sched *s) {
   free(s->dv.total);
   free(s->dv.used);
   free(s->topos); free(s->topo_of); free(s->cpu_alloc); free(s->cpu_excl); free(s->cpu_resv); free(s->cpusets);
+  free(s->numa_count); free(s->numa_alloc); free(s->numa_used); free(s->numa_present); free(s->numa_cs);
   ko_rsv *rv = &s->rv;
   free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
   free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
@@ -1327,6 +1617,57 @@ static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod) {
   return 0;
 }
 
+/* NodeNUMAResource Reserve on a node with a NUMA policy: Allocate with the Filter's hint, then
+ * NodeAllocation.addPodAllocation adds the NUMANodeResources (node_allocation.go:86-99) */
+static void numa_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
+  if (!s->cfg.numa.enable || p->reqzero || !s->numa_loaded || node_numa_policy(s, n) == 0) return;
+  ko_eff e;
+  node_eff(&s->nd, n, &e);
+  int64_t alloc[KS_MAX_NUMA][2];
+  if (numa_policy_eval(s, p, n, &e, NULL, alloc) != 0) return;
+  for (int k = 0; k < s->numa_count[n]; k++) {
+    if (!alloc[k][0] && !alloc[k][1]) continue;
+    const size_t o = (size_t)n * KS_MAX_NUMA + k;
+    s->numa_used[o * 2] += alloc[k][0];
+    s->numa_used[o * 2 + 1] += alloc[k][1];
+    s->numa_present[o] = 1;
+  }
+}
+
+int ko_load_numa_nodes(ko_sched *s, const ks_numa_node_cols *c) {
+  size_t nn = (size_t)(s->n > 0 ? s->n : 1) * KS_MAX_NUMA;
+  free(s->numa_count); free(s->numa_alloc); free(s->numa_used); free(s->numa_present); free(s->numa_cs);
+  s->numa_count = (int32_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 4);
+  s->numa_alloc = (int64_t *)calloc(nn * 2, 8);
+  s->numa_used = (int64_t *)calloc(nn * 2, 8);
+  s->numa_present = (uint8_t *)calloc(nn, 1);
+  s->numa_cs = (int32_t *)calloc(nn, 4);
+  for (int64_t n = 0; n < s->n; n++) {
+    s->numa_count[n] = c->count[n];
+    for (int k = 0; k < KS_MAX_NUMA; k++) {
+      const size_t o = (size_t)n * KS_MAX_NUMA + k;
+      s->numa_alloc[o * 2] = colv64(c->alloc_cpu, o);
+      s->numa_alloc[o * 2 + 1] = colv64(c->alloc_memory, o);
+      s->numa_used[o * 2] = colv64(c->used_cpu, o);
+      s->numa_used[o * 2 + 1] = colv64(c->used_memory, o);
+      s->numa_present[o] = c->used_present ? c->used_present[o] != 0 : (s->numa_used[o * 2] || s->numa_used[o * 2 + 1]);
+      s->numa_cs[o] = c->cpuset_cpus ? c->cpuset_cpus[o] : 0;
+    }
+  }
+  s->numa_loaded = 1;
+  return 0;
+}
+
+int ko_read_numa_nodes(const ko_sched *s, int64_t *used_cpu, int64_t *used_memory) {
+  for (int64_t n = 0; n < s->n; n++)
+    for (int k = 0; k < KS_MAX_NUMA; k++) {
+      const size_t o = (size_t)n * KS_MAX_NUMA + k;
+      if (used_cpu) used_cpu[o] = s->numa_loaded ? s->numa_used[o * 2] : 0;
+      if (used_memory) used_memory[o] = s->numa_loaded ? s->numa_used[o * 2 + 1] : 0;
+    }
+  return 0;
+}
+
 /* one scheduling cycle per pod, in order (scheduleOne loop) */
 int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) {
   if (np > s->cpusets_cap) {
@@ -1373,6 +1714,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
       rsv_reserve(s, &p, s->nom[best_n]);
     }
     out[i].gpu_minors = dev_reserve(s, &p, best_n);
+    numa_reserve(s, &p, best_n);
     node_reserve(s, &p, best_n);
     quota_reserve(s, &p);
   }

@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 from koordinator_amd import abi
-from koordinator_amd.cluster import CpuState, DeviceTable, NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
+from koordinator_amd.cluster import CpuState, DeviceTable, NumaNodes, NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
@@ -46,6 +46,8 @@ def lib():
         L.ko_load_cpu_state.argtypes = [C.c_void_p, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
         L.ko_read_cpu_state.argtypes = [C.c_void_p, abi.PU64, abi.PU64, abi.PU64]
         L.ko_fetch_cpusets.argtypes = [C.c_void_p, abi.PU64, C.c_int32]
+        L.ko_load_numa_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNumaNodeCols)]
+        L.ko_read_numa_nodes.argtypes = [C.c_void_p, abi.P64, abi.P64]
         L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
         L.ko_eval_pod.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
         L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
@@ -116,7 +118,7 @@ class Oracle:
 
     def __init__(self, cfg: abi.KsConfig, nodes: NodeTable, quotas: QuotaTable | None = None, nthreads: int = 1,
                  reservations: ReservationTable | None = None, devices: DeviceTable | None = None,
-                 cpu_state: CpuState | None = None):
+                 cpu_state: CpuState | None = None, numa_nodes: NumaNodes | None = None):
         self.L = lib()
         self.cfg = cfg
         self.n = nodes.n
@@ -140,6 +142,9 @@ class Oracle:
             self._cs = cpu_state.ks()
             self._ct = cpu_state.topo_array()
             self.L.ko_load_cpu_state(self.h, self._ct, len(cpu_state.topologies), C.byref(self._cs))
+        if numa_nodes is not None:
+            self._nn = numa_nodes.ks()
+            self.L.ko_load_numa_nodes(self.h, C.byref(self._nn))
 
     def close(self):
         if self.h:
@@ -186,6 +191,12 @@ class Oracle:
         out = [np.zeros(G * max(self.n, 1), np.int64) for _ in range(3)]
         self.L.ko_read_devices(self.h, *[o.ctypes.data_as(abi.P64) for o in out])
         return tuple(o[: G * self.n].reshape(G, self.n) for o in out)
+
+    def read_numa_nodes(self):
+        K = abi.KS_MAX_NUMA
+        out = [np.zeros((max(self.n, 1), K), np.int64) for _ in range(2)]
+        self.L.ko_read_numa_nodes(self.h, *[o.ctypes.data_as(abi.P64) for o in out])
+        return tuple(o[: self.n] for o in out)
 
     def read_cpu_state(self):
         W = abi.KS_CPU_WORDS
