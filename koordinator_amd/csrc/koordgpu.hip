@@ -31,6 +31,7 @@
 #include "ks_rsv.h"
 #include "ks_dev.h"
 #include "ks_cpuset.h"
+#include "ks_numa.h"
 
 using namespace ks;
 
@@ -173,6 +174,7 @@ struct SweepArgs {
   const DevNodes* __restrict__ dn;
   const DevRsv* __restrict__ rv;
   const DevDev* __restrict__ dv;
+  const DevNuma* __restrict__ nv;
   unsigned long long* dev_M;  // [64] DeviceShare: (max raw << 32) | ~witness node per pod of the pass
   int32_t phase;              // 0: reduce dev_M only (DeviceShare), 1: chunk keys
   Cfg c;
@@ -214,9 +216,10 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     uint32_t best = 0, second = 0;
     for (int32_t p = p0; p < p1; ++p) {
       const PodRec pod = load_pod_uniform(a.pods + cursor + p);
-      const EvalOut o = eval_full<NSC, false, true, FEAT>(
+      EvalOut o = eval_full<NSC, false, true, FEAT>(
           a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
           [&]() { return dev_eval<false>(a.c, pod, DevGView{*a.dv, node}); });
+      numa_policy_fix<NSC, false, FEAT>(a.c, pod, r, o, [&]() { return NumaGView{*a.nv, node}; });
       if ((FEAT & 4) && a.phase == 0) {
         // DeviceShare normalization max over the feasible nodes, witness = lowest index holding it
         const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | (0xFFFFFFFFull - (uint64_t)node));
@@ -585,6 +588,7 @@ struct CommitArgs {
   const DevNodes* __restrict__ dn;
   const DevRsv* __restrict__ rv;
   const DevDev* __restrict__ dv;
+  const DevNuma* __restrict__ nv;
   const unsigned long long* __restrict__ dev_M;  // [64] DeviceShare normalization max + witness (sweep phase 0)
   Cfg c;
   const PodRec* __restrict__ pods;
@@ -606,6 +610,7 @@ struct CommitArgs {
   int32_t rcap;        // reservations cached in LDS per slot (0 = none)
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
   int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
+  int32_t numa_bytes;  // LDS bytes of the slot NUMA-node state (commit_layout)
 };
 
 struct QuotaRowsLds {
@@ -616,13 +621,13 @@ struct QuotaRowsLds {
 };
 
 struct CommitLayout {
-  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, quota, touched, total;
+  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, touched, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 
 __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0,
-                                                      size_t dev_bytes = 0) {
+                                                      size_t dev_bytes = 0, size_t numa_bytes = 0) {
   CommitLayout L;
   size_t o = 0;
   L.rows = o;
@@ -651,6 +656,8 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += align16(rsv_bytes);     // per slot: the node's reservations (RsvRec, rcap each)
   L.sdev = o;
   o += align16(dev_bytes);     // per slot: GPU totals / used [3][kGpus] + present flag
+  L.snp = o;
+  o += align16(numa_bytes);    // per slot: NUMA-node totals / used / offsets + policy, count, present (ks_numa.h)
   L.quota = o;
   if (qc) o += align16(sizeof(QuotaRowsLds));
   L.touched = o;
@@ -779,9 +786,10 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
     const DevNodes d = *a.dn;
     load_node<NSC>(cfg, d, node, node < a.n, r);
   }
-  const EvalOut o = eval_full<NSC, false, false, FEAT>(
+  EvalOut o = eval_full<NSC, false, false, FEAT>(
       cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
       [&]() { return dev_eval<false>(cfg, pod, DevGView{*a.dv, node}); });
+  numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaGView{*a.nv, node}; });
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
   return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
 }
@@ -791,7 +799,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   constexpr bool RSV = (FEAT & 1) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
-  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes);
+  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes, (size_t)a.numa_bytes);
   SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
   PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
   ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
@@ -813,6 +821,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   int64_t* sdev_tot = reinterpret_cast<int64_t*>(smem_raw + lay.sdev);
   int64_t* sdev_use = sdev_tot + kMaxBatch * DW;
   int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kMaxBatch * DW);
+  int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -1051,6 +1060,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
               return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
             },
             [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane * DW, sdev_use + lane * DW, sdev_pres[lane] != 0}); });
+        numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
         feas = o.reasons == 0;
       }
       if (DEV && cfg.dev) {
@@ -1152,6 +1162,18 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
           snuma[4 * s + 2] = u_ratio;
           snuma[4 * s + 3] = (int64_t)u_free;
         }
+      }
+      if ((FEAT & 8) && cfg.numa_pol) {
+        // the node's NUMA-node state into LDS (lane = word, NumaLView layout)
+        const DevNuma& nv = *a.nv;
+        int64_t v = 0;
+        if (lane < 2 * kNumaDev) v = gld(nv.total + (int64_t)lane * nv.npad + node);
+        else if (lane < 4 * kNumaDev) v = gld(nv.used + (int64_t)(lane - 2 * kNumaDev) * nv.npad + node);
+        else if (lane < 5 * kNumaDev) v = gld(nv.off + (int64_t)(lane - 4 * kNumaDev) * nv.npad + node);
+        else if (lane == 5 * kNumaDev)
+          v = (int64_t)((gld(nv.flags + node) >> KS_NUMA_POLICY_SHIFT) & 3u) | ((int64_t)gld(nv.count + node) << 8) |
+              ((int64_t)gld(nv.present + node) << 32);
+        if (lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = v;
       }
       if (DEV && cfg.dev) {
         // the node's GPU totals / used / present flag into LDS (lane = word)
@@ -1322,6 +1344,34 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         const int64_t nv = sdev_use[s * DW + lane] + add;
         sdev_use[s * DW + lane] = nv;
         gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
+      }
+    }
+    if ((FEAT & 8) && cfg.numa_pol) {
+      // NodeNUMAResource Reserve on a node with a NUMA policy: Allocate with the Filter's hint on the pre-pod
+      // NUMA state, then addPodAllocation adds it to allocatedResources (node_allocation.go:86-99)
+      const NumaLView nl{snp + s * kNumaSlotWords};
+      PodRec pod = spods[j];
+      pod.flags = pflags;
+      if (nl.policy() != 0 && !(pflags & kPodReqZero)) {
+        const NumaPolOut pr = numa_policy_eval(cfg, pod, nl, 0, 0, 0, 0);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < kNumaDev; ++k) bits |= (pr.alloc[0][k] != 0 || pr.alloc[1][k] != 0) ? (1u << k) : 0u;
+        const int rr = lane / kNumaDev, kk = lane % kNumaDev;
+        if (lane < 2 * kNumaDev) {
+          int64_t add = 0;
+#pragma unroll
+          for (int q = 0; q < 2 * kNumaDev; ++q) add = (q == lane) ? pr.alloc[q / kNumaDev][q % kNumaDev] : add;
+          if (add != 0) {
+            const int64_t nvv = snp[s * kNumaSlotWords + 2 * kNumaDev + lane] + add;
+            snp[s * kNumaSlotWords + 2 * kNumaDev + lane] = nvv;
+            gst(a.nv->used + ((int64_t)rr * kNumaDev + kk) * a.nv->npad + node, nvv);
+          }
+        } else if (lane == 2 * kNumaDev && bits) {
+          const int64_t meta = snp[s * kNumaSlotWords + 5 * kNumaDev] | ((int64_t)bits << 32);
+          snp[s * kNumaSlotWords + 5 * kNumaDev] = meta;
+          gst(a.nv->present + node, (uint32_t)(meta >> 32));
+        }
       }
     }
     if (cpubind) {
@@ -1556,7 +1606,7 @@ __global__ __launch_bounds__(512) void quota_runtime_kernel(QrtArgs a) {
 // ------------------------------------------------------------------------------------------
 
 template <int NSC>
-__global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, Cfg c, const PodRec* pod, int64_t n,
+__global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n,
                                   uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
                                   int32_t* draw) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1565,9 +1615,10 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   load_node<NSC>(c, d, i, 1, r);
   const PodRec p = *pod;
   RsvOut ro;
-  const EvalOut o = eval_full<NSC, true, false, 7>(
+  EvalOut o = eval_full<NSC, true, false, 7>(
       c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
       [&]() { return dev_eval<false>(c, p, DevGView{*dv, i}); }, &ro);
+  numa_policy_fix<NSC, true, 15>(c, p, r, o, [&]() { return NumaGView{*nv, i}; });
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
@@ -1824,6 +1875,13 @@ struct ks_ctx {
   int32_t* cpuset_n = nullptr;
   CpuSet* cpuset_out = nullptr;          // [pod_cap] CPUs allocated per pod of the last schedule
   int32_t cpuset_cap = 0;
+  // NUMA topology policies (ks_numa.h)
+  void* numa_blob = nullptr;
+  DevNuma nv{};
+  DevNuma* dnv = nullptr;    // device copy (always allocated: kernels take its address)
+  int64_t* numa_used_ckpt = nullptr;
+  uint32_t* numa_present_ckpt = nullptr;
+  int64_t numa_policy_nodes = 0;  // nodes with a NUMA topology policy
   // debug
   PodRec* dbg_pod = nullptr;
   // stats
@@ -1883,6 +1941,7 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.monotone = c.fit.strategy == KS_LEAST_ALLOCATED || !c.fit.enable_score;
   k.numa = c.numa.enable ? 1 : 0;
   k.numa_most = c.numa.strategy == KS_MOST_ALLOCATED;
+  k.numa_sc_most = c.numa.numa_scoring_strategy == KS_MOST_ALLOCATED;  // hint scores (NUMAScoringStrategy)
   k.nw_cpu = (int32_t)c.numa.weight_cpu;
   k.nw_mem = (int32_t)c.numa.weight_memory;
   k.numa_pw = c.numa.enable ? (int32_t)c.numa.plugin_weight : 0;
@@ -2045,6 +2104,8 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->dev_M; dev_free(p);
   dev_free(ctx->cpu_blob);
   p = ctx->cpuset_list; dev_free(p);
+  dev_free(ctx->numa_blob);
+  p = ctx->dnv; dev_free(p);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -2215,6 +2276,12 @@ static int upload_rowcols(ks_ctx* ctx) {
     if (dev_alloc(ctx, &p, sizeof(DevNodes)) != KS_OK) return KS_ENOMEM;
     ctx->dnodes = (DevNodes*)p;
   }
+  if (!ctx->dnv) {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, sizeof(DevNuma)) != KS_OK) return KS_ENOMEM;
+    HIPCHK(ctx, hipMemsetAsync(p, 0, sizeof(DevNuma), ctx->stream));
+    ctx->dnv = (DevNuma*)p;
+  }
   HIPCHK(ctx, hipMemcpyAsync(ctx->rowcols, h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->dnodes, &ctx->d, sizeof(DevNodes), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2233,6 +2300,7 @@ static int upload_prep_nodes(ks_ctx* ctx) {
 
 static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
 static int dev_install(ks_ctx* ctx, const ks_device_cols* dc);
+static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h);
 
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
@@ -2284,6 +2352,18 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
   if (ctx->cfg.reservation.enable && rsv_install(ctx, nullptr, 0) != KS_OK) return KS_EHIP;
   if (ctx->cfg.deviceshare.enable && dev_install(ctx, nullptr) != KS_OK) return KS_EHIP;
+  // NUMA topology policies: an empty NUMA-node table until ks_load_numa_nodes
+  ctx->numa_policy_nodes = 0;
+  for (int64_t i = 0; ctx->cfg.numa.enable && nodes->numa_flags && i < n; ++i)
+    ctx->numa_policy_nodes += ((nodes->numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u) != 0;
+  dev_free(ctx->numa_blob);
+  if (ctx->numa_policy_nodes > 0) {
+    if (ctx->cfg.reservation.enable)
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "NUMA topology policies together with the Reservation plugin are not supported");
+    if (numa_install(ctx, nullptr, nullptr, nullptr) != KS_OK) return KS_EHIP;
+    ctx->kc.numa_pol = 1;
+    ctx->kc.monotone = 0;  // a Reserve can move a node's best NUMA hint: keys are not monotone
+  }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -2640,6 +2720,101 @@ int ks_fetch_cpusets(ks_ctx* ctx, uint64_t* out, int32_t p) {
   }
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->cpuset_out, (size_t)p * sizeof(CpuSet), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+// NUMA node resources of the policy nodes; nc == nullptr installs an empty table (every policy node
+// then reports "missing NUMA resources", as the reference does without a NodeResourceTopology).
+static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h) {
+  const size_t np = (size_t)ctx->npad;
+  constexpr int K = kNumaDev;
+  const size_t o_cnt = 0, o_tot = align16(np * 4), o_used = o_tot + 2 * K * np * 8, o_off = o_used + 2 * K * np * 8,
+               o_pres = o_off + K * np * 8, o_uck = o_pres + align16(np * 4), o_pck = o_uck + 2 * K * np * 8,
+               bytes = o_pck + align16(np * 4);
+  std::vector<char> h(bytes, 0);
+  int32_t* cnt = (int32_t*)(h.data() + o_cnt);
+  int64_t* tot = (int64_t*)(h.data() + o_tot);
+  int64_t* used = (int64_t*)(h.data() + o_used);
+  int64_t* off = (int64_t*)(h.data() + o_off);
+  uint32_t* pres = (uint32_t*)(h.data() + o_pres);
+  for (int64_t i = 0; nc && i < ctx->n; ++i) {
+    const uint32_t pol = (flags_h[i] >> KS_NUMA_POLICY_SHIFT) & 3u;
+    const int32_t c = nc->count[i];
+    if (c < 0 || c > KS_MAX_NUMA) KS_FAIL(ctx, KS_EINVAL, "node %lld: NUMA node count %d", (long long)i, c);
+    if (pol == 0) continue;  // the policy-None path never reads NUMA-node resources
+    if (c > K) KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: %d NUMA nodes with a NUMA policy (the device evaluates up to %d)", (long long)i, c, K);
+    cnt[i] = c;
+    const double ratio = ratio_h ? ratio_h[i] : 0.0;
+    for (int k = 0; k < c; ++k) {
+      const size_t o = (size_t)i * KS_MAX_NUMA + k;
+      const int64_t ac = nc->alloc_cpu ? nc->alloc_cpu[o] : 0, am = nc->alloc_memory ? nc->alloc_memory[o] : 0;
+      const int64_t uc = nc->used_cpu ? nc->used_cpu[o] : 0, um = nc->used_memory ? nc->used_memory[o] : 0;
+      const int64_t cs = nc->cpuset_cpus ? (int64_t)nc->cpuset_cpus[o] * 1000 : 0;
+      const int64_t lim = (int64_t)1 << 50;
+      if (ac < 0 || am < 0 || uc < 0 || um < 0 || cs < 0 || ac > lim || am > lim || uc > lim || um > lim || cs > lim)
+        KS_FAIL(ctx, KS_EINVAL, "node %lld NUMA %d: quantity out of range", (long long)i, k);
+      // amplifyNUMANodeResources / extension.Amplify: int64(math.Ceil(float64(v) * ratio)) for ratio > 1
+      tot[(size_t)(0 * K + k) * np + i] = ratio > 1.0 ? (int64_t)std::ceil((double)ac * ratio) : ac;
+      tot[(size_t)(1 * K + k) * np + i] = am;
+      used[(size_t)(0 * K + k) * np + i] = uc;
+      used[(size_t)(1 * K + k) * np + i] = um;
+      off[(size_t)k * np + i] = ratio > 1.0 ? (int64_t)std::ceil((double)cs * ratio) - cs : 0;
+      const bool present = nc->used_present ? nc->used_present[o] != 0 : (uc != 0 || um != 0);
+      if (present) pres[i] |= 1u << k;
+    }
+  }
+  dev_free(ctx->numa_blob);
+  if (dev_alloc(ctx, &ctx->numa_blob, bytes) != KS_OK) return KS_ENOMEM;
+  char* b = (char*)ctx->numa_blob;
+  HIPCHK(ctx, hipMemcpyAsync(b, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+  DevNuma& v = ctx->nv;
+  v.count = (const int32_t*)(b + o_cnt);
+  v.total = (const int64_t*)(b + o_tot);
+  v.used = (int64_t*)(b + o_used);
+  v.off = (const int64_t*)(b + o_off);
+  v.present = (uint32_t*)(b + o_pres);
+  v.flags = ctx->d.numa_flags;
+  v.npad = ctx->npad;
+  ctx->numa_used_ckpt = (int64_t*)(b + o_uck);
+  ctx->numa_present_ckpt = (uint32_t*)(b + o_pck);
+  HIPCHK(ctx, hipMemcpyAsync(ctx->numa_used_ckpt, v.used, 2 * K * np * 8, hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->numa_present_ckpt, v.present, np * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->dnv, &v, sizeof(DevNuma), hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_load_numa_nodes(ks_ctx* ctx, const ks_numa_node_cols* nc) {
+  if (!ctx || !nc || !nc->count) return ctx ? (ctx->err = "ks_load_numa_nodes: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_load_numa_nodes before ks_load_nodes");
+  if (!ctx->cfg.numa.enable) KS_FAIL(ctx, KS_ESTATE, "ks_load_numa_nodes: the NodeNUMAResource plugin is not enabled");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t n = (size_t)ctx->n;
+  std::vector<uint32_t> flags(n ? n : 1);
+  std::vector<double> ratio(n ? n : 1);
+  if (n) {
+    HIPCHK(ctx, hipMemcpyAsync(flags.data(), ctx->d.numa_flags, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ratio.data(), ctx->d.numa_ratio, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return numa_install(ctx, nc, flags.data(), ratio.data());
+}
+
+int ks_read_numa_nodes(ks_ctx* ctx, int64_t* used_cpu, int64_t* used_memory) {
+  if (!ctx) return KS_EINVAL;
+  const size_t n = (size_t)ctx->n, np = (size_t)ctx->npad;
+  std::vector<int64_t> u(2 * kNumaDev * (np ? np : 1), 0);
+  std::vector<uint32_t> pr(np ? np : 1, 0);
+  if (ctx->numa_blob && n) {
+    HIPCHK(ctx, hipMemcpyAsync(u.data(), ctx->nv.used, u.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  int64_t* outs[2] = {used_cpu, used_memory};
+  for (int r = 0; r < 2; ++r)
+    if (outs[r])
+      for (size_t i = 0; i < n; ++i)
+        for (int k = 0; k < KS_MAX_NUMA; ++k)
+          outs[r][i * KS_MAX_NUMA + k] = k < kNumaDev ? u[((size_t)r * kNumaDev + k) * np + i] : 0;
   return KS_OK;
 }
 
@@ -3016,12 +3191,21 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
         KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
       // takeCPUs' FullPCPUs fallback can take a whole core past numCPUsNeeded when the request is not a
       // whole number of cores (cpu_accumulator.go:163-175); the count-only commit does not model that
+      if (ctx->numa_policy_nodes > 0)
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: cpuset pods on clusters with NUMA topology policies are not supported", i);
       if (pol == KS_CPU_BIND_FULL_PCPUS)
         for (int32_t cpc : ctx->cpu_cpc)
           if (cpc > 1 && (cpu / 1000) % cpc != 0)
             KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: FullPCPUs request of %lld CPUs is not a whole number of %d-thread cores", i,
                     (long long)(cpu / 1000), cpc);
     }
+  }
+  if (ctx->numa_policy_nodes > 0 && ctx->cfg.deviceshare.enable) {
+    const int64_t* g[3] = {pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio};
+    for (int q = 0; q < 3; ++q)
+      for (int32_t i = 0; g[q] && i < p; ++i)
+        if (g[q][i] != 0)
+          KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: GPU pods on clusters with NUMA topology policies (DeviceShare hints) are not supported", i);
   }
   if (pc->rsv_class) {
     for (int32_t i = 0; i < p; ++i)
@@ -3074,14 +3258,23 @@ static hipEvent_t take_event(ks_ctx* ctx, size_t i) {
   return ctx->ev_pool[i];
 }
 
+static size_t dev_cache_bytes(const ks_ctx* ctx);
+static size_t numa_cache_bytes(const ks_ctx* ctx) {
+  return ctx->kc.numa_pol ? (size_t)kMaxBatch * kNumaSlotWords * 8 : 0;
+}
+
 // Quota rows are cached in LDS for the pass when the table is small enough and the LDS image fits.
 static bool commit_qcache(const ks_ctx* ctx) {
   if (!(ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows)) return false;
-  return commit_layout(ctx->k, ctx->nchunks, true).total <= 160 * 1024;
+  return commit_layout(ctx->k, ctx->nchunks, true, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx)).total <= 160 * 1024;
 }
 
 // kernel variant: 0 = Fit/LoadAware/Quota, 1 = + Reservation, 3 = + Reservation + NodeNUMAResource
-static int kernel_feat(const ks_ctx* ctx) { return ctx->kc.dev ? 7 : (ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0)); }
+// + 8: NodeNUMAResource with NUMA topology policies (ks_numa.h)
+static int kernel_feat(const ks_ctx* ctx) {
+  const int f = ctx->kc.dev ? 7 : (ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0));
+  return f | (ctx->kc.numa_pol ? 8 : 0);
+}
 
 static size_t dev_cache_bytes(const ks_ctx* ctx) {
   return ctx->kc.dev ? (size_t)kMaxBatch * (2 * 3 * kGpus * 8 + 4) : 0;
@@ -3097,7 +3290,7 @@ static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
   *qcache = commit_qcache(ctx);
   if (!ctx->kc.rsv) return 0;
   auto fit = [&](bool qc) {
-    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx)).total + 64;
+    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx)).total + 64;
     const size_t avail = base < 160 * 1024 ? 160 * 1024 - base : 0;
     return (int32_t)std::min<size_t>(8, avail / rsv_cache_bytes(ctx, 1));
   };
@@ -3135,24 +3328,27 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.ppw = ppw;
   const int feat = kernel_feat(ctx);
   sa.dv = ctx->ddv;
+  sa.nv = ctx->dnv;
   sa.dev_M = ctx->dev_M;
   sa.phase = 1;
-  if (feat == 7) {
+  if (feat == 7 || feat == 15) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
     // each launch is timed on its own (the roofline is per sweep launch)
     (void)hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream);
     sa.phase = 0;
     rec(0);
-    hipLaunchKernelGGL((sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    hipLaunchKernelGGL(feat == 15 ? (sweep_kernel<NSC, 15>) : (sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
     rec(0);
     if (ctx->nranks > 1)
       (void)ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ctx->stream);
     sa.phase = 1;
     rec(0);
-    hipLaunchKernelGGL((sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    hipLaunchKernelGGL(feat == 15 ? (sweep_kernel<NSC, 15>) : (sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
   } else {
     rec(0);
-    if (feat == 3)
+    if (feat == 11)
+      hipLaunchKernelGGL((sweep_kernel<NSC, 11>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    else if (feat == 3)
       hipLaunchKernelGGL((sweep_kernel<NSC, 3>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
     else if (feat == 1)
       hipLaunchKernelGGL((sweep_kernel<NSC, 1>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
@@ -3242,7 +3438,10 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   ca.dev_M = ctx->dev_M;
   ca.cpuset_list = ctx->cpuset_list;
   ca.cpuset_n = ctx->cpuset_n;
-  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes).total;
+  ca.numa_bytes = (int32_t)numa_cache_bytes(ctx);
+  ca.nv = ctx->dnv;
+  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes,
+                                    (size_t)ca.numa_bytes).total;
   rec(2);
 #define KS_COMMIT(F)                                                                                          \
   do {                                                                                                        \
@@ -3251,7 +3450,9 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
     else                                                                                                      \
       hipLaunchKernelGGL((commit_kernel<NSC, false, F>), dim3(1), dim3(kCommitThreads), smem, ctx->stream, ca); \
   } while (0)
-  if (feat == 7) KS_COMMIT(7);
+  if (feat == 15) KS_COMMIT(15);
+  else if (feat == 11) KS_COMMIT(11);
+  else if (feat == 7) KS_COMMIT(7);
   else if (feat == 3) KS_COMMIT(3);
   else if (feat == 1) KS_COMMIT(1);
   else KS_COMMIT(0);
@@ -3268,7 +3469,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   {
     bool qcache = false;
     const int32_t rcap = commit_rcap(ctx, &qcache);
-    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx)).total;
+    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx),
+                                      numa_cache_bytes(ctx)).total;
     if (smem > 160 * 1024)
       KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
     hipError_t e = hipSuccess;
@@ -3278,7 +3480,9 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     const int feat = kernel_feat(ctx);
 #define KS_SETATTR(N)                                                                                                         \
   do {                                                                                                                        \
-    if (feat == 7) qcache ? setattr((const void*)commit_kernel<N, true, 7>) : setattr((const void*)commit_kernel<N, false, 7>); \
+    if (feat == 15) qcache ? setattr((const void*)commit_kernel<N, true, 15>) : setattr((const void*)commit_kernel<N, false, 15>); \
+    else if (feat == 11) qcache ? setattr((const void*)commit_kernel<N, true, 11>) : setattr((const void*)commit_kernel<N, false, 11>); \
+    else if (feat == 7) qcache ? setattr((const void*)commit_kernel<N, true, 7>) : setattr((const void*)commit_kernel<N, false, 7>); \
     else if (feat == 3) qcache ? setattr((const void*)commit_kernel<N, true, 3>) : setattr((const void*)commit_kernel<N, false, 3>); \
     else if (feat == 1) qcache ? setattr((const void*)commit_kernel<N, true, 1>) : setattr((const void*)commit_kernel<N, false, 1>); \
     else qcache ? setattr((const void*)commit_kernel<N, true, 0>) : setattr((const void*)commit_kernel<N, false, 0>); \
@@ -3425,6 +3629,10 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->dev_used_ckpt, ctx->dv.used, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->cpu_loaded)
     HIPCHK(ctx, hipMemcpyAsync(ctx->cpu_ckpt, ctx->cpu.allocated, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->numa_blob) {
+    HIPCHK(ctx, hipMemcpyAsync(ctx->numa_used_ckpt, ctx->nv.used, (size_t)2 * kNumaDev * ctx->npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->numa_present_ckpt, ctx->nv.present, (size_t)ctx->npad * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  }
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_allocd_ckpt, ctx->rv.allocd, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -3445,6 +3653,10 @@ int ks_restore(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->dv.used, ctx->dev_used_ckpt, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->cpu_loaded)
     HIPCHK(ctx, hipMemcpyAsync(ctx->cpu.allocated, ctx->cpu_ckpt, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
+  if (ctx->numa_blob) {
+    HIPCHK(ctx, hipMemcpyAsync(ctx->nv.used, ctx->numa_used_ckpt, (size_t)2 * kNumaDev * ctx->npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->nv.present, ctx->numa_present_ckpt, (size_t)ctx->npad * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  }
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -3474,9 +3686,9 @@ int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, in
   const int blocks = (int)((n + threads - 1) / threads);
   if (blocks > 0) {
     switch (ctx->nsc) {
-      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
-      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
-      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
+      case 0: hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
+      case 2: hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
+      default: hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(threads), 0, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc, ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw); break;
     }
     if (ctx->kc.dev)
       hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,

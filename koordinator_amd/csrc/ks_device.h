@@ -60,6 +60,8 @@ struct Cfg {
   int32_t rsv_F;     // key radix: key total = hi * rsv_F + (Fit + LoadAware + NUMA weighted total), see ks_rsv.h
   int32_t numa, numa_most, nw_cpu, nw_mem, numa_pw;  // NodeNUMAResource
   int32_t cpuset;    // CPU state loaded: cpu-bind pods are evaluated (ks_cpuset.h)
+  int32_t numa_pol;  // nodes with a NUMA topology policy exist (ks_numa.h)
+  int32_t numa_sc_most;  // NUMAScoringStrategy MostAllocated (hint scores)
   int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw;  // DeviceShare (GPU)
 };
 
@@ -368,6 +370,7 @@ struct EvalOut {
   int32_t numa;
   int32_t dev_raw;         // DeviceShare raw score (normalized in key_total)
   int32_t hi;              // Reservation ranking component (ks_rsv.h)
+  uint32_t numa_rs;        // NodeNUMAResource reasons of the policy-None checks (before the policy path)
 };
 
 // Filter + Score of one (pod, node).  DEBUG=false computes feasibility (reasons != 0) and the
@@ -416,6 +419,7 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   o.numa = 0;
   o.dev_raw = 0;
   o.hi = 0;
+  o.numa_rs = 0;
   int32_t total = 0;
   if (c.fit_score) {
     int32_t ns = 0, ws = r.fit_ws;
@@ -481,6 +485,7 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
   }
   if (bind && rs == 0 && r.cpu_free < 0) rs = KS_R_NUMA_INVALID_TOPOLOGY;
   o.reasons |= DEBUG ? rs : (rs ? KS_R_FIT_PODS : 0u);
+  o.numa_rs = rs;
   Term tc = r.t_ncpu;
   if (p.cpu == 0) term_take(tc, -r.numa_off, -r.numa_off * 100);  // a cpu-less pod scores the plain Requested
   int32_t ns = 0, ws = 0;

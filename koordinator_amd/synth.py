@@ -327,6 +327,33 @@ def cpuset_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4, exc
     return pods
 
 
+def make_numa_nodes(nodes: NodeTable, rng: np.random.Generator, policy_frac: float = 0.5, cores=None):
+    """NUMA topology policies on a fraction of the nodes (best-effort / restricted / single-numa-node in equal
+    parts), 1, 2 or 4 NUMA nodes splitting the node's CPUs and memory, and earlier pods' NUMA allocations
+    (allocatedResources) on some NUMA nodes.  Returns the NumaNodes table; policies go into numa_flags."""
+    from .cluster import NumaNodes
+    n = nodes.n
+    cores = np.asarray(cores if cores is not None else nodes.alloc_milli_cpu // 1000)
+    nn = NumaNodes(n)
+    pol = np.where(rng.random(n) < policy_frac, rng.integers(1, 4, n), 0).astype(np.uint32)
+    nodes.numa_flags[:] = (nodes.numa_flags & ~np.uint32(3 << abi.KS_NUMA_POLICY_SHIFT)) | (pol << abi.KS_NUMA_POLICY_SHIFT)
+    cnt = rng.choice(np.array([1, 2, 4]), n, p=[0.2, 0.6, 0.2])
+    for i in range(n):
+        if pol[i] == 0:
+            continue
+        k = int(cnt[i])
+        nn.count[i] = k
+        nn.alloc_cpu[i, :k] = int(cores[i]) * 1000 // k
+        nn.alloc_memory[i, :k] = int(nodes.alloc_memory[i]) // k
+        for j in range(k):
+            if rng.random() < 0.5:
+                f = rng.random() * 0.6
+                nn.used_cpu[i, j] = int(nn.alloc_cpu[i, j] * f) // 1000 * 1000
+                nn.used_memory[i, j] = int(nn.alloc_memory[i, j] * f) // MI * MI
+                nn.used_present[i, j] = 1
+    return nn
+
+
 def c1(seed: int = SEED, n_nodes: int = 500, n_pods: int = 1000, **kw) -> Workload:
     rng = np.random.Generator(np.random.PCG64(seed))
     nodes = make_nodes(n_nodes, rng)

@@ -17,5 +17,6 @@ int main(void) {
   O(ks_config, numa); O(ks_config, deviceshare); O(ks_numa_args, numa_scoring_strategy); O(ks_pod_cols, gpu_core);
   O(ks_pod_cols, cpu_bind); O(ks_cpu_topology, numa_node); O(ks_cpu_topology, socket); O(ks_cpu_state_cols, reserved);
   O(ks_node_cols, numa_flags); O(ks_result, gpu_minors);
+  P(ks_numa_node_cols); O(ks_numa_node_cols, used_present); O(ks_numa_node_cols, cpuset_cpus);
   return 0;
 }

@@ -50,3 +50,20 @@ def test_missing_numa_resources():
     o = Oracle(numa_profile(), nodes, numa_nodes=nn)
     reasons, _, _ = o.eval_pod(pod)
     assert reasons[1] == abi.KS_R_NUMA_MISSING
+
+
+def test_oracle_random_policy_cluster_runs():
+    from koordinator_amd import synth
+    from koordinator_amd.config import CPU, MEMORY, NodeNUMAResourceArgs
+
+    rng = np.random.Generator(np.random.PCG64(7))
+    nodes = synth.make_nodes(200, rng)
+    nn = synth.make_numa_nodes(nodes, rng)
+    pods = synth.make_pods(400, rng)
+    p = synth.koord_profile()
+    p.numa = NodeNUMAResourceArgs(resources={CPU: 1, MEMORY: 1})
+    o = Oracle(p.to_ks_config(), nodes, nthreads=4, numa_nodes=nn)
+    r = o.schedule(pods)
+    assert (r["status"] == 0).sum() > 300
+    used, _ = o.read_numa_nodes()
+    assert (used > nn.used_cpu).any()
