@@ -34,8 +34,11 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def build_workload(name: str, seed: int):
+def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
+
+    if n_pods:
+        return getattr(synth, name)(seed=seed, n_pods=n_pods)
 
     if name == "c2":
         return synth.c2(seed=seed)
@@ -46,7 +49,7 @@ def build_workload(name: str, seed: int):
     if name == "c4":
         return synth.c4(seed=seed)
     if name == "c5":
-        return synth.c5(seed=seed, n_pods=20_000)
+        return synth.c5(seed=seed)  # BASELINE configs[4]: 1M pods x 100k nodes
     raise SystemExit(f"unknown config {name}")
 
 
@@ -133,6 +136,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--pods", type=int, default=0, help="pods per step (default: the config's own count)")
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="do not bracket kernels with HIP events")
@@ -158,7 +162,7 @@ def main():
     from koordinator_amd import abi, runtime
 
     # replicas schedule their own cluster (seed + rank); shards split one shared cluster
-    w = build_workload(args.config, seed=20261015 + (0 if args.shard else rank))
+    w = build_workload(args.config, seed=20261015 + (0 if args.shard else rank), n_pods=args.pods)
     prof = w.profile
     prof.device = local_rank if world > 1 else 0
     prof.batch_pods = args.batch_pods
