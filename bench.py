@@ -105,6 +105,7 @@ def cpu_baseline(w, gpu_res, budget_s: float):
                   and np.array_equal(r["score"], gpu_res["score"][:n_sample])
                   and np.array_equal(r["reservation"], gpu_res["reservation"][:n_sample])
                   and np.array_equal(r["gpu_minors"], gpu_res["gpu_minors"][:n_sample])
+                  and np.array_equal(r["rdma_minors"], gpu_res["rdma_minors"][:n_sample])
                   and (cs is None or np.array_equal(cs, gpu_res["cpusets"][:n_sample])))
     cpu_model = ""
     try:
@@ -257,7 +258,7 @@ def main():
             "config": {"workload": f"{w.name}: {n_pods} pods x {n_nodes} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
                                    f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
                                    + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else "")
-                                   + (" + NodeNUMAResource(amplified CPUs, cpuset pods) + DeviceShare(GPU, 8x80GiB/node)" if w.devices is not None else ""),
+                                   + (" + NodeNUMAResource(amplified CPUs, cpuset pods) + DeviceShare(8 GPUs x 80GiB + 4 RDMA on 4 PCIe/2 NUMA per node, joint GPU+RDMA)" if w.devices is not None else ""),
                        "pods_per_step": n_pods, "nodes": n_nodes, "percentage_of_nodes_to_score": 100,
                        "parallelism": (f"node-shards{world}x{args.vshards}" if args.shard or args.vshards > 1
                                        else (f"replicas{world}" if world > 1 else "single-gpu")),
@@ -266,6 +267,7 @@ def main():
             "placed_per_step": int((res["status"] == 0).sum()),
             "into_reservations_per_step": int((res["reservation"] >= 0).sum()),
             "gpu_pods_placed_per_step": int((res["gpu_minors"] != 0).sum()),
+            "rdma_pods_placed_per_step": int((res["rdma_minors"] != 0).sum()),
             "cpuset_pods_placed_per_step": int(((res["status"] == 0) & ((w.pods.flags & abi.KS_POD_CPU_BIND) != 0)).sum()),
             "passes_per_step": agg["passes"] / args.steps,
             "cut_passes_per_step": agg["cut_passes"] / args.steps,

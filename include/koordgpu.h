@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 3
+#define KS_ABI_VERSION 4
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -56,6 +56,9 @@ extern "C" {
 #define KS_RSV_DIMS (3 + KS_MAX_SCALARS) /* reservation resources: cpu, memory, ephemeral-storage, scalar[k] */
 #define KS_RSV_CLASSES 64 /* pod match classes (ks_reservation_cols.owner_classes bits) */
 #define KS_MAX_GPUS 8     /* GPU minors per node (ks_device_cols); minor = slot index */
+#define KS_MAX_RDMA 8     /* RDMA minors per node (ks_device_cols); minor = slot index */
+#define KS_MAX_PCIE 8     /* PCIe switches per node (ks_device_cols.pcie_*) */
+#define KS_PCIE_NONE 0xFFu /* device without topology (DeviceInfo.Topology == nil) */
 #define KS_MAX_CPUS 256   /* logical CPUs per node topology (ks_cpu_topology); CPU ids 0..ncpus-1 */
 #define KS_CPU_WORDS 4    /* uint64 words of a CPU set (bit c = CPU c) */
 #define KS_MAX_NUMA 8     /* NUMA nodes per node (ks_numa_node_cols); the device evaluates up to 4 */
@@ -139,6 +142,10 @@ extern "C" {
 #define KS_R_NUMA_AFFINITY 0x10000u    /* topology manager Admit: "node(s) NUMA Topology affinity error" (topologymanager/manager.go:64-66) */
 #define KS_R_NUMA_INSUFFICIENT 0x20000u /* NUMA Allocate: "Insufficient NUMA <resource>" (resource_manager.go:269-276) */
 #define KS_R_NUMA_MISSING 0x40000u     /* "node(s) missing NUMA resources" (topology_hint.go:33-36) */
+#define KS_R_DEV_NO_RDMA 0x80000u      /* DeviceShare: "Insufficient rdma devices", no RDMA device on the node
+                                          (DefaultDeviceHandler, devicehandler_default.go:45-48) */
+#define KS_R_DEV_JOINT 0x100000u       /* DeviceShare joint allocation: "node(s) Joint-Allocate rules not met" or
+                                          "Device Joint-Allocate rules violation" (device_allocator.go:252,280) */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -233,8 +240,8 @@ typedef struct ks_numa_args {
 } ks_numa_args;
 
 /* DeviceShareArgs.ScoringStrategy (defaults v1beta2/defaults.go:187-207: LeastAllocated,
- * gpu-memory-ratio 1 (rdma / fpga weights do not apply to GPUs)).  GPU devices only: no
- * allocate hints, joint allocation, NUMA affinity, VFs or device-holding reservations. */
+ * gpu-memory-ratio 1, rdma 1).  GPU and RDMA devices with joint [gpu, rdma] allocation; no allocate
+ * hints, FPGAs, NUMA affinity, VFs or device-holding reservations. */
 typedef struct ks_deviceshare_args {
   int32_t enable;
   int32_t strategy; /* KS_LEAST_ALLOCATED | KS_MOST_ALLOCATED */
@@ -242,6 +249,7 @@ typedef struct ks_deviceshare_args {
   int64_t weight_gpu_memory;
   int64_t weight_gpu_memory_ratio;
   int64_t plugin_weight;
+  int64_t weight_rdma; /* koordinator.sh/rdma (default 1): scores RDMA minors and the RDMA part of scoreNode */
 } ks_deviceshare_args;
 
 typedef struct ks_config {
@@ -336,7 +344,17 @@ typedef struct ks_pod_cols {
    * (preferredCPUBindPolicy after the args default, preferredCPUExclusivePolicy); numCPUsNeeded =
    * req_milli_cpu / 1000 (a multiple of 1000).  NULL = none */
   const uint32_t *cpu_bind;
+  /* DeviceShare RDMA request koordinator.sh/rdma (DefaultDeviceHandler, devicehandler_default.go:44-93: a value
+   * > 100 and divisible by 100 asks for value/100 devices); NULL = none */
+  const int64_t *rdma;
+  /* DeviceShare joint allocation (apiext.DeviceJointAllocate, device_allocator.go:188-339): KS_JOINT_*; the
+   * only supported DeviceTypes list is [gpu, rdma]; NULL = none */
+  const uint8_t *joint;
 } ks_pod_cols;
+
+#define KS_JOINT_NONE 0u
+#define KS_JOINT_GPU_RDMA 1u           /* DeviceTypes [gpu, rdma], no RequiredScope (best effort) */
+#define KS_JOINT_GPU_RDMA_SAME_PCIE 2u /* DeviceTypes [gpu, rdma], RequiredScope SamePCIe */
 
 /* ElasticQuota table: QuotaInfo.CalculateInfo per quota (core/quota_info.go). */
 typedef struct ks_quota_cols {
@@ -394,6 +412,17 @@ typedef struct ks_device_cols {
   const int64_t *used_core[KS_MAX_GPUS];   /* NULL = 0 */
   const int64_t *used_memory[KS_MAX_GPUS];
   const int64_t *used_ratio[KS_MAX_GPUS];
+  /* RDMA minors: koordinator.sh/rdma total and used (a minor with total 0 is absent); NULL = 0 */
+  const int64_t *total_rdma[KS_MAX_RDMA];
+  const int64_t *used_rdma[KS_MAX_RDMA];
+  /* device topology (newNUMATopology, numa_topology.go:46-96): per node the PCIe switches are numbered
+   * 0..KS_MAX_PCIE-1 in ascending (socketID, nodeID, pcieID) order (the order newDeviceTopologyGuide sorts
+   * them into, numa_topology.go:141-151); gpu_pcie / rdma_pcie give each minor's switch (KS_PCIE_NONE: no
+   * topology), pcie_numa / pcie_socket each switch's NUMA node and socket.  NULL = no topology */
+  const uint8_t *gpu_pcie[KS_MAX_GPUS];
+  const uint8_t *rdma_pcie[KS_MAX_RDMA];
+  const uint8_t *pcie_numa[KS_MAX_PCIE];
+  const uint8_t *pcie_socket[KS_MAX_PCIE];
 } ks_device_cols;
 
 /* A node CPU topology (CPUTopology, nodenumaresource/cpu_topology.go:27-33, built from the
@@ -438,6 +467,8 @@ typedef struct ks_result {
   int64_t score;   /* total weighted score of the chosen node */
   int32_t reservation; /* reservation row the pod was assumed into (Reserve, plugin.go:532-570), -1 = none */
   uint32_t gpu_minors; /* DeviceShare Reserve: bit k = GPU minor k allocated (plugin.go:377-430) */
+  uint32_t rdma_minors; /* DeviceShare Reserve: bit k = RDMA minor k allocated */
+  int32_t _pad0;
 } ks_result;
 
 /* Mutable node state after commits (read back for parity). */
@@ -487,6 +518,8 @@ int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
 int ks_load_devices(ks_ctx *ctx, const ks_device_cols *dev, int64_t n);
 /* used amounts after commits, [k*n + node] for minor k; NULL = skip */
 int ks_read_devices(ks_ctx *ctx, int64_t *used_core, int64_t *used_memory, int64_t *used_ratio);
+/* RDMA used amounts after commits, [k*n + node] for minor k */
+int ks_read_devices_rdma(ks_ctx *ctx, int64_t *used_rdma);
 
 /* CPU topologies and per-node CPU allocation state for cpuset pods (NodeNUMAResource
  * resourceManager / NodeAllocation, resource_manager.go:58-401); call after ks_load_nodes.  Reserve of

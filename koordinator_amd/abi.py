@@ -8,10 +8,16 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 3
+KS_ABI_VERSION = 4
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
+KS_MAX_RDMA = 8
+KS_MAX_PCIE = 8
+KS_PCIE_NONE = 0xFF
+KS_JOINT_NONE = 0
+KS_JOINT_GPU_RDMA = 1
+KS_JOINT_GPU_RDMA_SAME_PCIE = 2
 KS_MAX_CPUS = 256
 KS_CPU_WORDS = 4
 KS_MAX_NUMA = 8
@@ -81,6 +87,8 @@ KS_R_NUMA_AMPLIFIED_CPU = 0x800
 KS_R_NUMA_INVALID_RATIO = 0x1000
 KS_R_DEV_INSUFFICIENT = 0x2000
 KS_R_DEV_NO_GPU = 0x4000
+KS_R_DEV_NO_RDMA = 0x80000
+KS_R_DEV_JOINT = 0x100000
 KS_R_NUMA_INVALID_TOPOLOGY = 0x8000
 KS_R_NUMA_AFFINITY = 0x10000
 KS_R_NUMA_INSUFFICIENT = 0x20000
@@ -155,7 +163,8 @@ class KsNumaArgs(C.Structure):
 
 class KsDeviceShareArgs(C.Structure):
     _fields_ = [("enable", C.c_int32), ("strategy", C.c_int32), ("weight_gpu_core", C.c_int64),
-                ("weight_gpu_memory", C.c_int64), ("weight_gpu_memory_ratio", C.c_int64), ("plugin_weight", C.c_int64)]
+                ("weight_gpu_memory", C.c_int64), ("weight_gpu_memory_ratio", C.c_int64), ("plugin_weight", C.c_int64),
+                ("weight_rdma", C.c_int64)]
 
 
 class KsConfig(C.Structure):
@@ -237,6 +246,8 @@ POD_COLS = [
     ("gpu_memory", P64),
     ("gpu_memory_ratio", P64),
     ("cpu_bind", PU32),
+    ("rdma", P64),
+    ("joint", C.POINTER(C.c_uint8)),
 ]
 
 
@@ -298,6 +309,12 @@ class KsDeviceCols(C.Structure):
         ("used_core", P64 * KS_MAX_GPUS),
         ("used_memory", P64 * KS_MAX_GPUS),
         ("used_ratio", P64 * KS_MAX_GPUS),
+        ("total_rdma", P64 * KS_MAX_RDMA),
+        ("used_rdma", P64 * KS_MAX_RDMA),
+        ("gpu_pcie", C.POINTER(C.c_uint8) * KS_MAX_GPUS),
+        ("rdma_pcie", C.POINTER(C.c_uint8) * KS_MAX_RDMA),
+        ("pcie_numa", C.POINTER(C.c_uint8) * KS_MAX_PCIE),
+        ("pcie_socket", C.POINTER(C.c_uint8) * KS_MAX_PCIE),
     ]
 
 
@@ -321,11 +338,11 @@ class KsNumaNodeCols(C.Structure):
 
 class KsResult(C.Structure):
     _fields_ = [("node", C.c_int32), ("status", C.c_uint32), ("score", C.c_int64), ("reservation", C.c_int32),
-                ("gpu_minors", C.c_uint32)]
+                ("gpu_minors", C.c_uint32), ("rdma_minors", C.c_uint32), ("_pad0", C.c_int32)]
 
 
 RESULT_DTYPE_FIELDS = [("node", "<i4"), ("status", "<u4"), ("score", "<i8"), ("reservation", "<i4"),
-                       ("gpu_minors", "<u4")]
+                       ("gpu_minors", "<u4"), ("rdma_minors", "<u4"), ("_pad0", "<i4")]
 
 
 NODE_STATE_COLS = [
@@ -373,6 +390,7 @@ EXPORTED_SYMBOLS = [
     "ks_load_quotas",
     "ks_load_devices",
     "ks_read_devices",
+    "ks_read_devices_rdma",
     "ks_load_cpu_state",
     "ks_read_cpu_state",
     "ks_fetch_cpusets",

@@ -34,10 +34,11 @@ POD_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral",
     "nonzero_milli_cpu", "nonzero_memory",
     "la_req_cpu", "la_lim_cpu", "la_dflt_cpu", "la_req_memory", "la_lim_memory", "la_dflt_memory",
-    "gpu_core", "gpu_memory", "gpu_memory_ratio",
+    "gpu_core", "gpu_memory", "gpu_memory_ratio", "rdma",
 ]
 POD_I32 = ["quota", "rsv_class"]
 POD_U32 = ["flags", "quota_mask", "cpu_bind"]
+POD_U8 = ["joint"]
 
 STATE_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral", "nonzero_milli_cpu", "nonzero_memory",
@@ -63,6 +64,7 @@ class _Table:
     I64: list = []
     I32: list = []
     U32: list = []
+    U8: list = []
     N_SCALAR_ARRAYS: tuple = ()
 
     def __init__(self, n: int):
@@ -73,9 +75,11 @@ class _Table:
             setattr(self, name, np.zeros(self.n, np.int32))
         for name in self.U32:
             setattr(self, name, np.zeros(self.n, np.uint32))
+        for name in self.U8:
+            setattr(self, name, np.zeros(self.n, np.uint8))
 
     def columns(self) -> Dict[str, np.ndarray]:
-        return {k: getattr(self, k) for k in self.I64 + self.I32 + self.U32}
+        return {k: getattr(self, k) for k in self.I64 + self.I32 + self.U32 + self.U8}
 
     def _fix(self):
         for name in self.I64:
@@ -90,6 +94,10 @@ class _Table:
             a = getattr(self, name)
             if a.dtype != np.uint32 or not a.flags.c_contiguous:
                 setattr(self, name, np.ascontiguousarray(a, np.uint32))
+        for name in self.U8:
+            a = getattr(self, name)
+            if a.dtype != np.uint8 or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, np.uint8))
 
 
 class NodeTable(_Table):
@@ -152,6 +160,7 @@ class PodTable(_Table):
     I64 = POD_I64
     I32 = POD_I32
     U32 = POD_U32
+    U8 = POD_U8
 
     def __init__(self, n: int):
         super().__init__(n)
@@ -181,6 +190,7 @@ class PodTable(_Table):
         c.flags = _pu32(self.flags)
         c.quota_mask = _pu32(self.quota_mask)
         c.cpu_bind = _pu32(self.cpu_bind)
+        c.joint = self.joint.ctypes.data_as(C.POINTER(C.c_uint8))
         for k in range(abi.KS_MAX_SCALARS):
             c.req_scalar[k] = _p64(self.req_scalar[k])
         for d in range(abi.KS_QUOTA_DIMS):
@@ -265,20 +275,32 @@ class QuotaTree:
         return c
 
 
+DEV_I64 = ("total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio")
+DEV_RDMA = ("total_rdma", "used_rdma")
+DEV_TOPO = (("gpu_pcie", abi.KS_MAX_GPUS), ("rdma_pcie", abi.KS_MAX_RDMA), ("pcie_numa", abi.KS_MAX_PCIE),
+            ("pcie_socket", abi.KS_MAX_PCIE))
+
+
 class DeviceTable:
-    """GPU devices per node (ks_device_cols): [minor][node] arrays of total / used gpu-core,
-    gpu-memory, gpu-memory-ratio (deviceshare nodeDeviceCache deviceTotal / deviceUsed)."""
+    """Devices per node (ks_device_cols): [minor][node] arrays of total / used gpu-core, gpu-memory,
+    gpu-memory-ratio and koordinator.sh/rdma (deviceshare nodeDeviceCache deviceTotal / deviceUsed), and the
+    device topology: each minor's PCIe switch (dense per node in (socket, NUMA node, pcieID) order,
+    KS_PCIE_NONE = no topology) and each switch's NUMA node and socket (newNUMATopology)."""
 
     def __init__(self, n: int):
         self.n = int(n)
         G = abi.KS_MAX_GPUS
         self.flags = np.zeros(self.n, np.uint32)
-        for name in ("total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio"):
+        for name in DEV_I64:
             setattr(self, name, np.zeros((G, self.n), np.int64))
+        for name in DEV_RDMA:
+            setattr(self, name, np.zeros((abi.KS_MAX_RDMA, self.n), np.int64))
+        for name, k in DEV_TOPO:
+            setattr(self, name, np.full((k, self.n), abi.KS_PCIE_NONE if name.endswith("pcie") else 0, np.uint8))
 
     def copy(self) -> "DeviceTable":
         t = DeviceTable(self.n)
-        for k in ("flags", "total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio"):
+        for k in ("flags",) + DEV_I64 + DEV_RDMA + tuple(x for x, _ in DEV_TOPO):
             setattr(t, k, getattr(self, k).copy())
         return t
 
@@ -286,12 +308,18 @@ class DeviceTable:
         c = abi.KsDeviceCols()
         self.flags = np.ascontiguousarray(self.flags, np.uint32)
         c.flags = _pu32(self.flags)
-        for name in ("total_core", "total_memory", "total_ratio", "used_core", "used_memory", "used_ratio"):
+        for name in DEV_I64 + DEV_RDMA:
             arr = np.ascontiguousarray(getattr(self, name), np.int64)
             setattr(self, name, arr)
             field = getattr(c, name)
-            for k in range(abi.KS_MAX_GPUS):
+            for k in range(arr.shape[0]):
                 field[k] = _p64(arr[k])
+        for name, kk in DEV_TOPO:
+            arr = np.ascontiguousarray(getattr(self, name), np.uint8)
+            setattr(self, name, arr)
+            field = getattr(c, name)
+            for k in range(kk):
+                field[k] = arr[k].ctypes.data_as(C.POINTER(C.c_uint8))
         c._keep = self
         return c
 

@@ -28,6 +28,8 @@ BATCH_MEMORY = "kubernetes.io/batch-memory"
 GPU_CORE = "koordinator.sh/gpu-core"
 GPU_MEMORY = "koordinator.sh/gpu-memory"
 GPU_MEMORY_RATIO = "koordinator.sh/gpu-memory-ratio"
+RDMA = "koordinator.sh/rdma"
+FPGA = "koordinator.sh/fpga"
 
 DEFAULT_NODE_METRIC_EXPIRATION_SECONDS = 180
 DEFAULT_RESOURCE_WEIGHTS = {CPU: 1, MEMORY: 1}
@@ -120,9 +122,9 @@ class NodeNUMAResourceArgs:
 @dataclass
 class DeviceShareArgs:
     """DeviceShareArgs.ScoringStrategy after v1beta2 defaults (defaults.go:187-207): LeastAllocated,
-    gpu-memory-ratio weight 1."""
+    gpu-memory-ratio, rdma and fpga weight 1."""
     strategy: str = "LeastAllocated"
-    resources: Dict[str, int] = field(default_factory=lambda: {GPU_MEMORY_RATIO: 1})
+    resources: Dict[str, int] = field(default_factory=lambda: {GPU_MEMORY_RATIO: 1, RDMA: 1, FPGA: 1})
 
 
 @dataclass
@@ -213,11 +215,12 @@ class SchedulerProfile:
             c.deviceshare.enable = 1
             c.deviceshare.strategy = abi.KS_MOST_ALLOCATED if d.strategy == "MostAllocated" else abi.KS_LEAST_ALLOCATED
             for name in d.resources:
-                if name not in (GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, "koordinator.sh/rdma", "koordinator.sh/fpga"):
+                if name not in (GPU_CORE, GPU_MEMORY, GPU_MEMORY_RATIO, RDMA, FPGA):
                     raise ValidationError(f"DeviceShare weight on {name} is not supported")
             c.deviceshare.weight_gpu_core = d.resources.get(GPU_CORE, 0)
             c.deviceshare.weight_gpu_memory = d.resources.get(GPU_MEMORY, 0)
             c.deviceshare.weight_gpu_memory_ratio = d.resources.get(GPU_MEMORY_RATIO, 0)
+            c.deviceshare.weight_rdma = d.resources.get(RDMA, 0)
             c.deviceshare.plugin_weight = self.deviceshare_weight
         if self.reservation_weight is not None:
             c.reservation.enable = 1

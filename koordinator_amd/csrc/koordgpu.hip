@@ -98,8 +98,9 @@ struct DevPodCols {
   int32_t *quota;
   int64_t *la_req_cpu, *la_lim_cpu, *la_dflt_cpu, *la_req_mem, *la_lim_mem, *la_dflt_mem;
   int32_t *rsv_class;
-  int64_t *gpu_core, *gpu_mem, *gpu_ratio;
+  int64_t *gpu_core, *gpu_mem, *gpu_ratio, *rdma;
   uint32_t* cpu_bind;
+  uint8_t* joint;
 };
 
 // estimatedUsedByResource (estimator/default_estimator.go:73-108)
@@ -161,7 +162,11 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   r.gpu_core = s.gpu_core[i];
   r.gpu_mem = s.gpu_mem[i];
   r.gpu_ratio = s.gpu_ratio[i];
-  if (r.gpu_core != 0 || r.gpu_mem != 0 || r.gpu_ratio != 0) r.flags |= kPodHasGpu;
+  if (r.gpu_core != 0 || r.gpu_mem != 0 || r.gpu_ratio != 0) r.flags |= kPodHasGpu | kPodGpuReq;
+  r.rdma = s.rdma ? s.rdma[i] : 0;
+  r.joint = s.joint ? s.joint[i] : 0u;
+  r._pad0 = 0;
+  if (r.rdma > 0) r.flags |= kPodHasGpu;
   r.cpu_bind = (r.flags & KS_POD_CPU_BIND) ? ((s.cpu_bind[i] & 0xFu) | ((uint32_t)(r.cpu / 1000) << 8)) : 0u;
   out[i] = r;
 }
@@ -817,10 +822,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   constexpr int RD = 3 + NSC;
   RsvRec<RD>* srec = reinterpret_cast<RsvRec<RD>*>(smem_raw + lay.srec);
   constexpr bool DEV = (FEAT & 4) != 0;
-  constexpr int DW = 3 * kGpus;  // int64 words of one slot's GPU totals (and of its used amounts)
+  constexpr int DW = kDevTW;   // int64 words of one slot's device totals + topology (ks_dev.h)
+  constexpr int DU = kDevQW;   // int64 words of its used amounts
   int64_t* sdev_tot = reinterpret_cast<int64_t*>(smem_raw + lay.sdev);
   int64_t* sdev_use = sdev_tot + kMaxBatch * DW;
-  int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kMaxBatch * DW);
+  int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kMaxBatch * DU);
   int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1025,7 +1031,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const uint32_t st = st_next;
     const Cands cj = cn;
     if (st) {
-      if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0};
+      if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0, 0, 0};
       goto next_pod;
     }
     {
@@ -1059,7 +1065,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
               if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
               return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
             },
-            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane * DW, sdev_use + lane * DW, sdev_pres[lane] != 0}); });
+            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane * DW, sdev_use + lane * DU, sdev_pres[lane] != 0}); });
         numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
         feas = o.reasons == 0;
       }
@@ -1103,7 +1109,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       KS_STAMP(3);
     }
     if (best == 0) {
-      if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0, -1, 0};
+      if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0, -1, 0, 0, 0};
       goto next_pod;
     }
     const int32_t node = (int32_t)gkey_node(best);
@@ -1148,7 +1154,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       if (cpubind && u_free < cpu_need) {
         // NodeNUMAResource Reserve -> Allocate: not enough CPUs; every plugin unreserves
         --nslots;
-        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0};
+        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0, 0, 0};
         goto next_pod;
       }
       if (lane == s) snode = node;
@@ -1176,15 +1182,15 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         if (lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = v;
       }
       if (DEV && cfg.dev) {
-        // the node's GPU totals / used / present flag into LDS (lane = word)
+        // the node's device totals + topology / used / present flag into LDS (lane = word)
         const DevDev& dv = *a.dv;
-        int64_t v = 0;
+        int64_t v = 0, w = 0;
         if (lane < DW) v = gld(dv.total + (int64_t)lane * dv.npad + node);
-        else if (lane < 2 * DW) v = gld(dv.used + (int64_t)(lane - DW) * dv.npad + node);
-        else if (lane == 2 * DW) v = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
+        else if (lane == DW) v = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
+        if (lane < DU) w = gld(dv.used + (int64_t)lane * dv.npad + node);
         if (lane < DW) sdev_tot[s * DW + lane] = v;
-        else if (lane < 2 * DW) sdev_use[s * DW + lane - DW] = v;
-        else if (lane == 2 * DW) sdev_pres[s] = (int32_t)v;
+        else if (lane == DW) sdev_pres[s] = (int32_t)v;
+        if (lane < DU) sdev_use[s * DU + lane] = w;
       }
       if (RSV && cfg.rsv) {
         // the node's reservations into LDS (lane = record word), unless too many or too wide
@@ -1233,7 +1239,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       }
     } else {
       if (cpubind && (int32_t)snuma[4 * s + 3] < cpu_need) {
-        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0};
+        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0, 0, 0};
         goto next_pod;
       }
       row = &rows[s];
@@ -1273,7 +1279,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
         fitla_pref = e2.total;
         if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
-          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DW, sdev_pres[s] != 0});
+          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DU, sdev_pres[s] != 0});
           fitla_pref += cfg.dev_pw * (Muse == 0 ? dd.raw : small_div(100 * dd.raw, Muse));
         }
       }
@@ -1330,19 +1336,24 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       const int64_t fitla = hi >= kRsvOrderBase ? fitla_pref : score - hi * cfg.rsv_F;
       score_out = fitla + (hi > 0 ? a.rv->w100 : 0);
     }
-    uint32_t gminors = 0;
+    uint32_t gminors = 0, rminors = 0;
     if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
       // DeviceShare Reserve: allocate the minors on the pre-pod GPU state, add the request per instance
       PodRec pod = spods[j];
       pod.flags = pflags;
       GpuReq g;
-      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DW, sdev_pres[s] != 0}, &g);
+      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DU, sdev_pres[s] != 0}, &g);
       gminors = __builtin_amdgcn_readfirstlane(dd.minors);
-      if (lane < DW && ((gminors >> (lane % kGpus)) & 1u)) {
+      rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
+      // used word `lane`: GPU (q, k) for lane < 3 * kGpus, RDMA j = lane - kDevRdmaW after
+      const bool is_gpu = lane < kDevRdmaW;
+      const int k = is_gpu ? lane % kGpus : lane - kDevRdmaW;
+      const uint32_t m = is_gpu ? gminors : rminors;
+      if (lane < DU && ((m >> k) & 1u)) {
         const int q = lane / kGpus;
-        const int64_t add = q == 0 ? (g.has_core ? g.core : 0) : (q == 1 ? g.mem : g.ratio);
-        const int64_t nv = sdev_use[s * DW + lane] + add;
-        sdev_use[s * DW + lane] = nv;
+        const int64_t add = !is_gpu ? g.rdma : (q == 0 ? g.core : (q == 1 ? g.mem : g.ratio));
+        const int64_t nv = sdev_use[s * DU + lane] + add;
+        sdev_use[s * DU + lane] = nv;
         gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
       }
     }
@@ -1389,7 +1400,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         a.cpuset_list[atomicAdd(a.cpuset_n, 1)] = make_int2(cursor0 + j, node);
       }
     }
-    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors};
+    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors, rminors, 0};
     {
       const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
       if (cfg.quota_enable && qrow >= 0) {
@@ -1951,6 +1962,7 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.dw_core = (int32_t)c.deviceshare.weight_gpu_core;
   k.dw_mem = (int32_t)c.deviceshare.weight_gpu_memory;
   k.dw_ratio = (int32_t)c.deviceshare.weight_gpu_memory_ratio;
+  k.dw_rdma = (int32_t)c.deviceshare.weight_rdma;
   k.dev_pw = c.deviceshare.enable ? (int32_t)c.deviceshare.plugin_weight : 0;
   if (k.dev) k.monotone = 0;  // a commit changes the pod's DeviceShare normalization max
   k.rsv = c.reservation.enable ? 1 : 0;
@@ -2010,6 +2022,7 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
     const ks_deviceshare_args& da = cfg->deviceshare;
     if (da.weight_gpu_core < 0 || da.weight_gpu_core > 100 || da.weight_gpu_memory < 0 || da.weight_gpu_memory > 100 ||
         da.weight_gpu_memory_ratio < 0 || da.weight_gpu_memory_ratio > 100 || da.plugin_weight < 0 ||
+        da.weight_rdma < 0 || da.weight_rdma > 100 ||
         da.plugin_weight > 1000 || (da.strategy != KS_LEAST_ALLOCATED && da.strategy != KS_MOST_ALLOCATED)) {
       g_create_error = "ks_create: DeviceShare args out of range";
       return KS_EINVAL;
@@ -2493,11 +2506,12 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
   return KS_OK;
 }
 
-// Upload the GPU device table ([3][kGpus][npad] totals / used + flags); dc == NULL: no device info.
+// Upload the device table (kDevTW words of totals + topology, kDevQW words of used, flags per node; ks_dev.h);
+// dc == NULL: no device info.
 static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
-  const size_t np = (size_t)ctx->npad, words = 3 * (size_t)kGpus * np;
-  const size_t o_flags = 0, o_total = (np * 4 + 15) / 16 * 16, o_used = o_total + words * 8, o_ck = o_used + words * 8,
-               bytes = o_ck + words * 8;
+  const size_t np = (size_t)ctx->npad, tw = (size_t)kDevTW * np, uw = (size_t)kDevQW * np;
+  const size_t o_flags = 0, o_total = (np * 4 + 15) / 16 * 16, o_used = o_total + tw * 8, o_ck = o_used + uw * 8,
+               bytes = o_ck + uw * 8;
   std::vector<char> h(bytes, 0);
   uint32_t* flags = (uint32_t*)(h.data() + o_flags);
   int64_t* total = (int64_t*)(h.data() + o_total);
@@ -2513,6 +2527,47 @@ static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
           total[((size_t)q * kGpus + k) * np + n] = cols[q] ? cols[q][n] : 0;
           used[((size_t)q * kGpus + k) * np + n] = cols[3 + q] ? cols[3 + q][n] : 0;
         }
+    }
+    for (int j = 0; j < kRdma; ++j) {
+      if (check_range64(ctx, dc->total_rdma[j], ctx->n, "rdma quantity") != KS_OK ||
+          check_range64(ctx, dc->used_rdma[j], ctx->n, "rdma quantity") != KS_OK)
+        return KS_EINVAL;
+      for (int64_t n = 0; n < ctx->n; ++n) {
+        total[((size_t)kDevRdmaW + j) * np + n] = dc->total_rdma[j] ? dc->total_rdma[j][n] : 0;
+        used[((size_t)kDevRdmaW + j) * np + n] = dc->used_rdma[j] ? dc->used_rdma[j][n] : 0;
+      }
+    }
+    // topology: 4-bit switch per minor, NUMA node / socket per switch; switches numbered in (socket, node) order
+    for (int64_t n = 0; n < ctx->n; ++n) {
+      uint64_t topo = 0, meta = 0;
+      uint32_t used_sw = 0;
+      auto sw = [&](const uint8_t* col, int k, int shift) -> int {
+        const uint32_t p = col ? col[n] : KS_PCIE_NONE;
+        if (p != KS_PCIE_NONE && p >= (uint32_t)kPcie) return -1;
+        topo |= (uint64_t)(p == KS_PCIE_NONE ? 0xFu : p) << (shift + 4 * k);
+        if (p != KS_PCIE_NONE) used_sw |= 1u << p;
+        return 0;
+      };
+      for (int k = 0; k < kGpus; ++k)
+        if (sw(dc->gpu_pcie[k], k, 0)) KS_FAIL(ctx, KS_EINVAL, "node %lld: gpu %d PCIe switch >= %d", (long long)n, k, kPcie);
+      for (int j = 0; j < kRdma; ++j)
+        if (sw(dc->rdma_pcie[j], j, 32)) KS_FAIL(ctx, KS_EINVAL, "node %lld: rdma %d PCIe switch >= %d", (long long)n, j, kPcie);
+      int last = -1;
+      for (int p = 0; p < kPcie; ++p) {
+        const uint32_t nu = dc->pcie_numa[p] ? dc->pcie_numa[p][n] : 0, so = dc->pcie_socket[p] ? dc->pcie_socket[p][n] : 0;
+        if (nu > 15 || so > 15) KS_FAIL(ctx, KS_EINVAL, "node %lld: PCIe switch %d NUMA node / socket > 15", (long long)n, p);
+        meta |= (uint64_t)(nu | (so << 4)) << (8 * p);
+        if (!((used_sw >> p) & 1u)) continue;
+        // the device walks switches in index order: it must be (socket, node) order (newDeviceTopologyGuide)
+        if (last >= 0) {
+          const uint32_t lnu = (uint32_t)(meta >> (8 * last)) & 0xFu, lso = (uint32_t)(meta >> (8 * last + 4)) & 0xFu;
+          if (so < lso || (so == lso && nu < lnu))
+            KS_FAIL(ctx, KS_EINVAL, "node %lld: PCIe switches not numbered in (socket, NUMA node) order", (long long)n);
+        }
+        last = p;
+      }
+      total[(size_t)kDevTopoW * np + n] = (int64_t)topo;
+      total[(size_t)kDevMetaW * np + n] = (int64_t)meta;
     }
     for (int64_t n = 0; n < ctx->n; ++n) flags[n] = dc->flags ? dc->flags[n] : 0;
   }
@@ -2545,17 +2600,33 @@ int ks_load_devices(ks_ctx* ctx, const ks_device_cols* dev, int64_t n) {
   return dev_install(ctx, dev);
 }
 
+static int read_dev_used(ks_ctx* ctx, std::vector<int64_t>& u) {
+  u.resize((size_t)kDevQW * (size_t)ctx->npad);
+  HIPCHK(ctx, hipMemcpyAsync(u.data(), ctx->dv.used, u.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
 int ks_read_devices(ks_ctx* ctx, int64_t* used_core, int64_t* used_memory, int64_t* used_ratio) {
   if (!ctx) return KS_EINVAL;
   if (!ctx->dev_blob) return KS_OK;
   const size_t np = (size_t)ctx->npad, n = (size_t)ctx->n;
-  std::vector<int64_t> u(3 * (size_t)kGpus * np);
-  HIPCHK(ctx, hipMemcpyAsync(u.data(), ctx->dv.used, u.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<int64_t> u;
+  if (read_dev_used(ctx, u) != KS_OK) return KS_EHIP;
   int64_t* outs[3] = {used_core, used_memory, used_ratio};
   for (int q = 0; q < 3; ++q)
     if (outs[q])
       for (int k = 0; k < kGpus; ++k) memcpy(outs[q] + (size_t)k * n, u.data() + ((size_t)q * kGpus + k) * np, n * 8);
+  return KS_OK;
+}
+
+int ks_read_devices_rdma(ks_ctx* ctx, int64_t* used_rdma) {
+  if (!ctx || !used_rdma) return KS_EINVAL;
+  if (!ctx->dev_blob) return KS_OK;
+  const size_t np = (size_t)ctx->npad, n = (size_t)ctx->n;
+  std::vector<int64_t> u;
+  if (read_dev_used(ctx, u) != KS_OK) return KS_EHIP;
+  for (int j = 0; j < kRdma; ++j) memcpy(used_rdma + (size_t)j * n, u.data() + ((size_t)kDevRdmaW + j) * np, n * 8);
   return KS_OK;
 }
 
@@ -3098,8 +3169,9 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   const size_t res = ((size_t)cap * sizeof(ks_result) + 255) / 256 * 256;
   const size_t col8 = ((size_t)cap * 8 + 255) / 256 * 256;
   const size_t col4 = ((size_t)cap * 4 + 255) / 256 * 256;
-  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 qreq[8] = 26 int64 cols; flags quota qmask rsv_class cpu_bind = 5 x32
-  const size_t bytes = rec + res + col8 * 26 + col4 * 5;
+  // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 rdma qreq[8] = 27 int64 cols; flags quota qmask rsv_class
+  // cpu_bind joint(u8) = 6 x32
+  const size_t bytes = rec + res + col8 * 27 + col4 * 6;
   if (dev_alloc(ctx, &ctx->pod_blob, bytes) != KS_OK) return KS_ENOMEM;
   char* b = (char*)ctx->pod_blob;
   ctx->pods = (PodRec*)b;
@@ -3109,7 +3181,7 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   DevPodCols& s = ctx->pstage;
   int64_t** c8[] = {&s.cpu, &s.mem, &s.eph, &s.nzcpu, &s.nzmem, &s.sc[0], &s.sc[1], &s.sc[2], &s.sc[3],
                     &s.la_req_cpu, &s.la_lim_cpu, &s.la_dflt_cpu, &s.la_req_mem, &s.la_lim_mem, &s.la_dflt_mem,
-                    &s.gpu_core, &s.gpu_mem, &s.gpu_ratio};
+                    &s.gpu_core, &s.gpu_mem, &s.gpu_ratio, &s.rdma};
   for (int64_t** f : c8) {
     *f = (int64_t*)b;
     b += col8;
@@ -3127,6 +3199,8 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   s.rsv_class = (int32_t*)b;
   b += col4;
   s.cpu_bind = (uint32_t*)b;
+  b += col4;
+  s.joint = (uint8_t*)b;
   ctx->pod_cap = cap;
   return KS_OK;
 }
@@ -3153,6 +3227,9 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
   HIPCHK(ctx, cp8(s.gpu_core, pc->gpu_core));
   HIPCHK(ctx, cp8(s.gpu_mem, pc->gpu_memory));
   HIPCHK(ctx, cp8(s.gpu_ratio, pc->gpu_memory_ratio));
+  HIPCHK(ctx, cp8(s.rdma, pc->rdma));
+  if (pc->joint) HIPCHK(ctx, hipMemcpyAsync(s.joint, pc->joint, (size_t)p, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(s.joint, 0, (size_t)p, ctx->stream));
   for (int d = 0; d < KS_QUOTA_DIMS; ++d) HIPCHK(ctx, cp8(ctx->pq.req[d], pc->quota_req[d]));
   if (pc->flags) HIPCHK(ctx, hipMemcpyAsync(s.flags, pc->flags, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.flags, 0, (size_t)p * 4, ctx->stream));
@@ -3174,7 +3251,7 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
 static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
   const int64_t* cols[] = {pc->req_milli_cpu, pc->req_memory, pc->req_ephemeral, pc->nonzero_milli_cpu,
                            pc->nonzero_memory, pc->la_req_cpu, pc->la_lim_cpu, pc->la_req_memory, pc->la_lim_memory,
-                           pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio};
+                           pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio, pc->rdma};
   for (const int64_t* c : cols)
     if (check_range64(ctx, c, p, "pod quantity") != KS_OK) return KS_EINVAL;
   for (int k = 0; k < KS_MAX_SCALARS; ++k)
@@ -3201,11 +3278,23 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
     }
   }
   if (ctx->numa_policy_nodes > 0 && ctx->cfg.deviceshare.enable) {
-    const int64_t* g[3] = {pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio};
-    for (int q = 0; q < 3; ++q)
+    const int64_t* g[4] = {pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio, pc->rdma};
+    for (int q = 0; q < 4; ++q)
       for (int32_t i = 0; g[q] && i < p; ++i)
         if (g[q][i] != 0)
-          KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: GPU pods on clusters with NUMA topology policies (DeviceShare hints) are not supported", i);
+          KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: device pods on clusters with NUMA topology policies (DeviceShare hints) are not supported", i);
+  }
+  if (pc->joint) {
+    for (int32_t i = 0; i < p; ++i) {
+      const uint8_t j = pc->joint[i];
+      if (j > KS_JOINT_GPU_RDMA_SAME_PCIE) KS_FAIL(ctx, KS_EINVAL, "pod %d: joint %u invalid", i, (unsigned)j);
+      const bool gpu = (pc->gpu_core && pc->gpu_core[i]) || (pc->gpu_memory && pc->gpu_memory[i]) ||
+                       (pc->gpu_memory_ratio && pc->gpu_memory_ratio[i]);
+      // jointAllocate without an RDMA request allocates an RDMA device with a nil request
+      // (device_allocator.go:308-330): not modelled
+      if (j && gpu && !(pc->rdma && pc->rdma[i] > 0))
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: joint [gpu, rdma] allocation without an rdma request", i);
+    }
   }
   if (pc->rsv_class) {
     for (int32_t i = 0; i < p; ++i)
@@ -3277,7 +3366,7 @@ static int kernel_feat(const ks_ctx* ctx) {
 }
 
 static size_t dev_cache_bytes(const ks_ctx* ctx) {
-  return ctx->kc.dev ? (size_t)kMaxBatch * (2 * 3 * kGpus * 8 + 4) : 0;
+  return ctx->kc.dev ? (size_t)kMaxBatch * ((kDevTW + kDevQW) * 8 + 4) : 0;
 }
 
 static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {
@@ -3589,7 +3678,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   }
   // algorithmic bytes of one full sweep launch: node columns read once per pod group + outputs
   int64_t b_node = 8 * 15 + 4 * 3 + (int64_t)ctx->nsc * 16 + (ctx->kc.rsv ? 8 : 0) + (ctx->kc.numa ? 16 : 0) +
-                   (ctx->kc.dev ? 4 + 2 * 3 * kGpus * 8 : 0);
+                   (ctx->kc.dev ? 4 + (kDevTW + kDevQW) * 8 : 0);
   const int64_t groups = (ctx->batch + ppw - 1) / ppw;
   ctx->stats.sweep_bytes = local_chunks * 64 * b_node * groups + (int64_t)ctx->batch * sizeof(PodRec) + local_chunks * 64 * 4;
   return KS_OK;
@@ -3626,7 +3715,7 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->quota_npused_ckpt, ctx->q.npused, tb, hipMemcpyDeviceToDevice, ctx->stream));
   }
   if (ctx->dev_blob)
-    HIPCHK(ctx, hipMemcpyAsync(ctx->dev_used_ckpt, ctx->dv.used, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dev_used_ckpt, ctx->dv.used, (size_t)kDevQW * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->cpu_loaded)
     HIPCHK(ctx, hipMemcpyAsync(ctx->cpu_ckpt, ctx->cpu.allocated, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->numa_blob) {
@@ -3650,7 +3739,7 @@ int ks_restore(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->q.npused, ctx->quota_npused_ckpt, tb, hipMemcpyDeviceToDevice, ctx->stream));
   }
   if (ctx->dev_blob)
-    HIPCHK(ctx, hipMemcpyAsync(ctx->dv.used, ctx->dev_used_ckpt, (size_t)3 * kGpus * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dv.used, ctx->dev_used_ckpt, (size_t)kDevQW * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->cpu_loaded)
     HIPCHK(ctx, hipMemcpyAsync(ctx->cpu.allocated, ctx->cpu_ckpt, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->numa_blob) {

@@ -1,18 +1,25 @@
-// ks_dev.h — DeviceShare (GPU) on the device (pkg/scheduler/plugins/deviceshare).
+// ks_dev.h — DeviceShare (GPU + RDMA, joint allocation) on the device (pkg/scheduler/plugins/deviceshare).
 //
-// Per (pod, node): GPUHandler.CalcDesiredRequestsAndCount after fillGPUTotalMem
-// (devicehandler_gpu.go:40-98: the request per instance and the instance count), the
-// defaultAllocateDevices feasibility (device_allocator.go:392-462: enough free minors satisfy
-// LessThanOrEqual(request, free)), and the node score scoreNode (scoring.go:228-253) over the summed
-// totals / free amounts.  Reserve picks the minors in sortDeviceResourcesByMinor order (score desc,
-// minor asc; device_resources.go:171-208) and adds the request to each (updateCacheUsed).
+// Per (pod, node): AutopilotAllocator.Prepare (GPUHandler.CalcDesiredRequestsAndCount after fillGPUTotalMem,
+// devicehandler_gpu.go:40-98; DefaultDeviceHandler for RDMA, devicehandler_default.go:44-93), the Allocate
+// feasibility (device_allocator.go:94-132: tryJointAllocate for [gpu, rdma] pods, then defaultAllocateDevices
+// per remaining type, :392-462), and the node score AutopilotAllocator.score (:507-530: scoreNode per requested
+// type, summed).  Reserve takes the minors the same Allocate picks and adds the request per instance to each
+// (updateCacheUsed).
 //
-// NormalizeScore is DefaultNormalizeScore(100) over the feasible nodes (scoring.go:95-97): a
-// cross-node max M.  The sweep runs twice when DeviceShare is on — phase 0 reduces, per pod, the
-// key (M << 32 | ~witness) where the witness is the lowest-index feasible node holding M; phase 1
-// scores with floor(100 * raw / M).  The commit kernel keeps M valid: the untouched nodes'
-// maximum is still M while the witness is untouched, the touched nodes are re-scored, and a pass
-// whose M would change is cut so the next pass re-sweeps from that pod.
+// Minors are bit masks.  defaultAllocateDevices' sort (sortDeviceResourcesByPreferredPCIe then
+// sortDeviceResourcesByMinor: preferred switch first, score desc, minor asc; device_resources.go:187-220) is
+// a repeated arg-max over the key (preferred << 12 | score << 4 | 15 - minor).  The topology walk of
+// allocateByTopology (:210-253) runs over at most KS_MAX_PCIE switches (numbered per node in (socket, NUMA
+// node, pcieID) order, so the stable sort of freeNodeDevicesInPCIe is "preferred first, then index order") and
+// the NUMA-node groups of freeNodeDevicesInNode (numa_topology.go:185-240: |preferred switches| desc, preferred
+// desc, node asc).
+//
+// NormalizeScore is DefaultNormalizeScore(100) over the feasible nodes (scoring.go:95-97): a cross-node max M.
+// The sweep runs twice when DeviceShare is on — phase 0 reduces, per pod, the key (M << 32 | ~witness) where
+// the witness is the lowest-index feasible node holding M; phase 1 scores with floor(100 * raw / M).  The
+// commit kernel keeps M valid: the untouched nodes' maximum is still M while the witness is untouched, the
+// touched nodes are re-scored, and a pass whose M would change is cut so the next pass re-sweeps from that pod.
 #pragma once
 
 #include "ks_device.h"
@@ -20,77 +27,98 @@
 namespace ks {
 
 constexpr int kGpus = KS_MAX_GPUS;
+constexpr int kRdma = KS_MAX_RDMA;
+constexpr int kPcie = KS_MAX_PCIE;
+// int64 words per node: totals [0, 3*kGpus) GPU (q * kGpus + k), [kDevRdmaW, +kRdma) RDMA, then the packed
+// topology (kDevTopoW: 4-bit switch of GPU k at bit 4k, of RDMA j at bit 32 + 4j, 0xF = none; kDevMetaW: NUMA
+// node of switch p at bit 8p, socket at bit 8p + 4).  Used amounts cover the quantity words only.
+constexpr int kDevRdmaW = 3 * kGpus;
+constexpr int kDevQW = 3 * kGpus + kRdma;  // quantity words (totals and used)
+constexpr int kDevTopoW = kDevQW;
+constexpr int kDevMetaW = kDevQW + 1;
+constexpr int kDevTW = kDevQW + 2;  // total-table words
 
 struct DevDev {
   const uint32_t* flags;  // [npad] KS_DEV_*
-  const int64_t* total;   // [3][kGpus][npad]  q = 0 core, 1 memory, 2 ratio
-  int64_t* used;          // [3][kGpus][npad]  mutable (Reserve)
+  const int64_t* total;   // [kDevTW][npad]
+  int64_t* used;          // [kDevQW][npad]  mutable (Reserve)
   int64_t npad;
 };
 
-// A GPU instance request for one node: per-instance (core, memory, ratio), count, core key present.
-struct GpuReq {
-  int64_t core, mem, ratio;
-  int32_t desired;
-  bool has_core;
-  bool no_gpu;  // no healthy GPU on the node (UnschedulableAndUnresolvable)
-};
-
-// views of one node's GPUs: HBM columns or the commit kernel's LDS copy (tot/use[q*kGpus+k])
+// views of one node's devices: HBM columns or the commit kernel's LDS copy (tot[kDevTW], use[kDevQW])
 struct DevGView {
   const DevDev& d;
   int64_t n;
   __device__ __forceinline__ bool present() const { return (gld(d.flags + n) & KS_DEV_PRESENT) != 0; }
-  __device__ __forceinline__ int64_t total(int q, int k) const { return gld(d.total + ((int64_t)q * kGpus + k) * d.npad + n); }
-  __device__ __forceinline__ int64_t used(int q, int k) const { return gld(d.used + ((int64_t)q * kGpus + k) * d.npad + n); }
+  __device__ __forceinline__ int64_t tot(int w) const { return gld(d.total + (int64_t)w * d.npad + n); }
+  __device__ __forceinline__ int64_t use(int w) const { return gld(d.used + (int64_t)w * d.npad + n); }
 };
 
 struct DevLView {
-  const int64_t* tot;  // [3*kGpus]
-  const int64_t* use;  // [3*kGpus]
+  const int64_t* t;  // [kDevTW]
+  const int64_t* u;  // [kDevQW]
   bool pres;
   __device__ __forceinline__ bool present() const { return pres; }
-  __device__ __forceinline__ int64_t total(int q, int k) const { return tot[q * kGpus + k]; }
-  __device__ __forceinline__ int64_t used(int q, int k) const { return use[q * kGpus + k]; }
+  __device__ __forceinline__ int64_t tot(int w) const { return t[w]; }
+  __device__ __forceinline__ int64_t use(int w) const { return u[w]; }
+};
+
+// The pod's request per instance and desired count per device type on one node.
+struct GpuReq {
+  int64_t core, mem, ratio;  // GPU per instance (core 0 without a gpu-core key)
+  int64_t rdma;              // RDMA per instance
+  int32_t desired, rdesired;
+  bool has_core;
 };
 
 template <typename V>
-__device__ __forceinline__ GpuReq gpu_request(const PodRec& p, const V& v) {
-  GpuReq g{0, 0, 0, 1, (p.flags & KS_POD_GPU_CORE) != 0, false};
-  int64_t total_mem = -1;
+__device__ __forceinline__ uint32_t dev_prepare(const PodRec& p, const V& v, GpuReq& g) {
+  g = GpuReq{0, 0, 0, 0, 1, 1, (p.flags & KS_POD_GPU_CORE) != 0};
+  if (p.flags & kPodGpuReq) {
+    int64_t total_mem = -1;
 #pragma unroll
-  for (int k = kGpus - 1; k >= 0; --k) {  // the first healthy minor (all GPUs of a node are the same model)
-    const int64_t tc = v.total(0, k), tm = v.total(1, k), tr = v.total(2, k);
-    if (tc || tm || tr) total_mem = tm;
+    for (int k = kGpus - 1; k >= 0; --k) {  // the first healthy minor (all GPUs of a node are the same model)
+      const int64_t tc = v.tot(k), tm = v.tot(kGpus + k), tr = v.tot(2 * kGpus + k);
+      if (tc || tm || tr) total_mem = tm;
+    }
+    if (total_mem < 0) return KS_R_DEV_NO_GPU;
+    int64_t core = p.gpu_core, mem = p.gpu_mem, ratio = p.gpu_ratio;
+    if (p.flags & KS_POD_GPU_MEMORY)
+      ratio = (int64_t)((double)mem / (double)total_mem * 100.0);  // memoryBytesToRatio
+    else
+      mem = ratio * total_mem / 100;  // memoryRatioToBytes
+    if (ratio > 100 && ratio % 100 == 0) {
+      g.desired = (int32_t)(ratio / 100);
+      core /= g.desired;
+      mem /= g.desired;
+      ratio /= g.desired;
+    }
+    g.core = g.has_core ? core : 0;
+    g.mem = mem;
+    g.ratio = ratio;
   }
-  if (total_mem < 0) {
-    g.no_gpu = true;
-    return g;
+  if (p.rdma > 0) {
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < kRdma; ++j) any |= v.tot(kDevRdmaW + j) != 0;
+    if (!any) return KS_R_DEV_NO_RDMA;
+    int64_t q = p.rdma;
+    if (q > 100 && q % 100 == 0) {
+      g.rdesired = (int32_t)(q / 100);
+      q /= g.rdesired;
+    }
+    g.rdma = q;
   }
-  int64_t core = p.gpu_core, mem = p.gpu_mem, ratio = p.gpu_ratio;
-  if (p.flags & KS_POD_GPU_MEMORY)
-    ratio = (int64_t)((double)mem / (double)total_mem * 100.0);  // memoryBytesToRatio
-  else
-    mem = ratio * total_mem / 100;  // memoryRatioToBytes
-  if (ratio > 100 && ratio % 100 == 0) {
-    g.desired = (int32_t)(ratio / 100);
-    core /= g.desired;
-    mem /= g.desired;
-    ratio /= g.desired;
-  }
-  g.core = core;
-  g.mem = mem;
-  g.ratio = ratio;
-  return g;
+  return 0u;
 }
 
-// one resource of the scorer: Least/MostAllocated of (requested, capacity) (scoring.go:278-308)
+// one resource of the scorer: Least/MostAllocated of (requested, capacity) (scoring.go:270-308)
 __device__ __forceinline__ int32_t dev_term(bool most, int64_t req, int64_t cap) {
   if (most) return pct_floor_i64(req > cap ? cap : req, cap);
   return req > cap ? 0 : pct_floor_i64(cap - req, cap);
 }
 
-// scoreDevice / scoreNode body: requested = total - free + pod (total >= free), allocatable = total
+// scoreDevice / scoreNode body for GPUs: requested = total - free + pod (total >= free), allocatable = total
 __device__ __forceinline__ int32_t dev_score3(const Cfg& c, const int64_t* tot, const int64_t* fre, const int64_t* pod) {
   const int32_t w[3] = {c.dw_core, c.dw_mem, c.dw_ratio};
   int32_t ns = 0, ws = 0;
@@ -104,63 +132,228 @@ __device__ __forceinline__ int32_t dev_score3(const Cfg& c, const int64_t* tot, 
   return ws ? small_div(ns, ws) : 0;
 }
 
+// the same for RDMA (one resource, koordinator.sh/rdma)
+__device__ __forceinline__ int32_t dev_score1(const Cfg& c, int64_t tot, int64_t fre, int64_t pod) {
+  if (c.dw_rdma == 0 || tot == 0) return 0;
+  const int64_t req = tot >= fre ? tot - fre + pod : tot;
+  return dev_term(c.dev_most != 0, req, tot);  // (s * w) / w
+}
+
 struct DevOut {
   uint32_t reasons;  // KS_R_DEV_*
-  int32_t raw;       // scoreNode (feasible only)
-  uint32_t minors;   // allocation (ALLOC only)
+  int32_t raw;       // AutopilotAllocator.score (feasible only)
+  uint32_t minors;   // GPU allocation (ALLOC only)
+  uint32_t rminors;  // RDMA allocation (ALLOC only)
 };
+
+// per-type state of one node for one pod: fitting minors, per-minor scores, switches
+struct DevType {
+  uint32_t fit;       // minors with non-zero free that satisfy the request per instance
+  int32_t sc[8];      // scoreDevice (only with scores)
+  uint32_t pcie[8];   // switch of each minor (0xF = none)
+};
+
+// defaultAllocateDevices over the fitting minors in `sub`: up to maxd minors in (preferred switch, score desc,
+// minor asc) order, at least `desired`; 0 = "Insufficient <type> devices"
+__device__ __forceinline__ uint32_t dev_take(const DevType& t, int nm, uint32_t sub, int desired, uint32_t pref) {
+  int maxd = desired;
+  const int npref = __builtin_popcount(pref);
+  maxd = npref > maxd ? npref : maxd;
+  desired = desired == 0 ? 1 : desired;
+  maxd = maxd < desired ? desired : maxd;
+  const uint32_t cand = t.fit & sub;
+  uint32_t mask = 0;
+  int got = 0;
+  for (int r = 0; r < maxd; ++r) {
+    int best = -1, bk = -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= nm) break;
+      const bool ok = ((cand >> k) & 1u) && !((mask >> k) & 1u);
+      const int key = ((t.pcie[k] < 8u && ((pref >> t.pcie[k]) & 1u)) ? (1 << 12) : 0) | (t.sc[k] << 4) | (15 - k);
+      best = (ok && key > bk) ? k : best;
+      bk = (ok && key > bk) ? key : bk;
+    }
+    if (best < 0) break;
+    mask |= 1u << best;
+    ++got;
+  }
+  return got >= desired ? mask : 0u;
+}
+
+__device__ __forceinline__ uint32_t dev_pcies_of(const DevType& t, int nm, uint32_t mask) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < nm && ((mask >> k) & 1u) && t.pcie[k] < 8u) p |= 1u << t.pcie[k];
+  return p;
+}
+
+__device__ __forceinline__ uint32_t dev_sub_of(const DevType& t, int nm, uint32_t pcies) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (k < nm && t.pcie[k] < 8u && ((pcies >> t.pcie[k]) & 1u)) s |= 1u << k;
+  return s;
+}
+
+// jointAllocate (device_allocator.go:286-339) restricted to the switches `sw` (all minors if sw == ~0)
+__device__ __forceinline__ bool dev_joint(const DevType& G, const DevType& R, const GpuReq& g, bool same, uint32_t sw,
+                                          uint32_t pref, uint32_t& om, uint32_t& orm) {
+  const uint32_t gs = sw == ~0u ? 0xFFu : dev_sub_of(G, kGpus, sw);
+  const uint32_t rs = sw == ~0u ? 0xFFu : dev_sub_of(R, kRdma, sw);
+  const uint32_t prim = dev_take(G, kGpus, gs, g.desired, pref);
+  if (!prim) return false;
+  const uint32_t pc = dev_pcies_of(G, kGpus, prim);
+  const uint32_t sec = dev_take(R, kRdma, rs, same ? __builtin_popcount(pc) : 1, pc);
+  if (!sec) return false;
+  om = prim;
+  orm = sec;
+  return true;
+}
+
+// tryJointAllocate -> allocateByTopology with DeviceTypes [gpu, rdma] (device_allocator.go:188-253)
+__device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType& R, const GpuReq& g, bool same,
+                                                uint64_t meta, uint32_t& om, uint32_t& orm) {
+  uint32_t exist = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    exist |= G.pcie[k] < 8u ? (1u << G.pcie[k]) : 0u;
+    exist |= R.pcie[k] < 8u ? (1u << R.pcie[k]) : 0u;
+  }
+  // per switch: preferred = a fitting RDMA instance on it (freeDevices[rdma] of the last joint type)
+  uint32_t swpref = 0;
+#pragma unroll
+  for (int p = 0; p < kPcie; ++p)
+    if (((exist >> p) & 1u) && (R.fit & dev_sub_of(R, kRdma, 1u << p))) swpref |= 1u << p;
+  // freeNodeDevicesInPCIe: preferred switches first (a switch without a fitting RDMA fails jointAllocate)
+  for (int p = 0; p < kPcie; ++p) {
+    if (!((swpref >> p) & 1u)) continue;
+    if (__builtin_popcount(G.fit & dev_sub_of(G, kGpus, 1u << p)) >= g.desired &&
+        dev_joint(G, R, g, same, 1u << p, 1u << p, om, orm))
+      return true;
+  }
+  // freeNodeDevicesInNode: one group per NUMA node, ordered by (|preferred switches| desc, preferred desc,
+  // node asc)
+  uint32_t gsw[kPcie], gkey[kPcie];
+  int ng = 0;
+  uint32_t seen = 0;
+  for (int p = 0; p < kPcie; ++p) {
+    if (!((exist >> p) & 1u)) continue;
+    const uint32_t node = (uint32_t)(meta >> (8 * p)) & 0xFu;
+    if ((seen >> node) & 1u) continue;
+    seen |= 1u << node;
+    uint32_t sw = 0;
+    for (int q = p; q < kPcie; ++q)
+      if (((exist >> q) & 1u) && ((uint32_t)(meta >> (8 * q)) & 0xFu) == node) sw |= 1u << q;
+    const bool pr = (R.fit & dev_sub_of(R, kRdma, sw)) != 0;
+    gsw[ng] = sw;
+    gkey[ng] = ((uint32_t)__builtin_popcount(sw & swpref) << 8) | (pr ? 16u : 0u) | (15u - node);
+    ++ng;
+  }
+  uint32_t done = 0;
+  for (int r = 0; r < ng; ++r) {
+    int bi = -1;
+    uint32_t bk = 0;
+    for (int i = 0; i < ng; ++i)
+      if (!((done >> i) & 1u) && (bi < 0 || gkey[i] > bk)) {
+        bi = i;
+        bk = gkey[i];
+      }
+    done |= 1u << bi;
+    const uint32_t sw = gsw[bi];
+    if (__builtin_popcount(G.fit & dev_sub_of(G, kGpus, sw)) >= g.desired &&
+        dev_joint(G, R, g, same, sw, sw & swpref, om, orm))
+      return true;
+  }
+  // the whole node, preferring every preferred switch
+  return dev_joint(G, R, g, same, ~0u, swpref, om, orm);
+}
 
 // DeviceShare Filter + Score (+ the allocation with ALLOC) of one (pod, node).
 template <bool ALLOC, typename V>
 __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const V& v, GpuReq* req_out = nullptr) {
-  DevOut o{0u, 0, 0u};
+  DevOut o{0u, 0, 0u, 0u};
   if (!v.present()) return o;  // no device info: Filter passes, Score 0
-  const GpuReq g = gpu_request(p, v);
+  GpuReq g;
+  o.reasons = dev_prepare(p, v, g);
   if (req_out) *req_out = g;
-  if (g.no_gpu) {
-    o.reasons = KS_R_DEV_NO_GPU;
-    return o;
-  }
-  const int64_t pod[3] = {g.has_core ? g.core : 0, g.mem, g.ratio};
-  int64_t tsum[3] = {0, 0, 0}, fsum[3] = {0, 0, 0};
-  int32_t nfit = 0;
-  int32_t sc[kGpus];
-  uint32_t fitmask = 0;
+  if (o.reasons) return o;
+  const bool has_gpu = (p.flags & kPodGpuReq) != 0, has_rdma = p.rdma > 0;
+  const bool joint = has_gpu && has_rdma && p.joint != KS_JOINT_NONE;
+  const bool scores = ALLOC || joint;
+  const uint64_t topo = (joint || ALLOC) ? (uint64_t)v.tot(kDevTopoW) : 0ull;
+  DevType G, R;
+  G.fit = R.fit = 0;
+  int32_t raw = 0;
+  if (has_gpu) {
+    const int64_t pod[3] = {g.core, g.mem, g.ratio};
+    int64_t tsum[3] = {0, 0, 0}, fsum[3] = {0, 0, 0};
 #pragma unroll
-  for (int k = 0; k < kGpus; ++k) {
-    const int64_t t[3] = {v.total(0, k), v.total(1, k), v.total(2, k)};
-    const int64_t f[3] = {t[0] - v.used(0, k), t[1] - v.used(1, k), t[2] - v.used(2, k)};
-    const bool exists = t[0] || t[1] || t[2];
-    const bool has_free = exists && (f[0] || f[1] || f[2]);
-    const bool fits = has_free && (!g.has_core || g.core <= f[0]) && g.mem <= f[1] && g.ratio <= f[2];
+    for (int k = 0; k < kGpus; ++k) {
+      const int64_t t[3] = {v.tot(k), v.tot(kGpus + k), v.tot(2 * kGpus + k)};
+      const int64_t u[3] = {v.use(k), v.use(kGpus + k), v.use(2 * kGpus + k)};
+      const int64_t f[3] = {t[0] > u[0] ? t[0] - u[0] : 0, t[1] > u[1] ? t[1] - u[1] : 0, t[2] > u[2] ? t[2] - u[2] : 0};
+      const bool exists = t[0] || t[1] || t[2];
+      const bool has_free = exists && (f[0] || f[1] || f[2]);
+      const bool fits = has_free && (!g.has_core || g.core <= f[0]) && g.mem <= f[1] && g.ratio <= f[2];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      tsum[q] += exists ? t[q] : 0;
-      fsum[q] += has_free ? f[q] : 0;
-    }
-    nfit += fits ? 1 : 0;
-    fitmask |= fits ? (1u << k) : 0u;
-    sc[k] = (ALLOC && fits) ? dev_score3(c, t, f, pod) : 0;
-  }
-  if (nfit < g.desired) {
-    o.reasons = KS_R_DEV_INSUFFICIENT;
-    return o;
-  }
-  o.raw = dev_score3(c, tsum, fsum, pod);
-  if (ALLOC) {
-    uint32_t mask = 0;
-    for (int got = 0; got < g.desired; ++got) {
-      int best = -1;
-      int32_t bs = -1;
-#pragma unroll
-      for (int k = 0; k < kGpus; ++k) {
-        const bool cand = ((fitmask >> k) & 1u) && !((mask >> k) & 1u) && sc[k] > bs;
-        best = cand ? k : best;
-        bs = cand ? sc[k] : bs;
+      for (int q = 0; q < 3; ++q) {
+        tsum[q] += exists ? t[q] : 0;
+        fsum[q] += exists ? f[q] : 0;
       }
-      mask |= 1u << best;
+      G.fit |= fits ? (1u << k) : 0u;
+      G.sc[k] = (scores && fits) ? dev_score3(c, t, f, pod) : 0;
+      G.pcie[k] = (uint32_t)(topo >> (4 * k)) & 0xFu;
     }
-    o.minors = mask;
+    raw += dev_score3(c, tsum, fsum, pod);
+  }
+  if (has_rdma) {
+    int64_t tsum = 0, fsum = 0;
+#pragma unroll
+    for (int j = 0; j < kRdma; ++j) {
+      const int64_t t = v.tot(kDevRdmaW + j), u = v.use(kDevRdmaW + j);
+      const int64_t f = t > u ? t - u : 0;
+      tsum += t;
+      fsum += f;
+      const bool fits = t != 0 && f != 0 && g.rdma <= f;
+      R.fit |= fits ? (1u << j) : 0u;
+      R.sc[j] = (scores && fits) ? dev_score1(c, t, f, g.rdma) : 0;
+      R.pcie[j] = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
+    }
+    raw += dev_score1(c, tsum, fsum, g.rdma);
+  }
+  uint32_t om = 0, orm = 0;
+  bool jdone = false;
+  if (joint) {
+    const bool same = p.joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
+    if (dev_by_topology(G, R, g, same, (uint64_t)v.tot(kDevMetaW), om, orm)) {
+      // validateJointAllocation (device_allocator.go:255-284)
+      if (same && dev_pcies_of(G, kGpus, om) != dev_pcies_of(R, kRdma, orm)) {
+        o.reasons = KS_R_DEV_JOINT;
+        return o;
+      }
+      jdone = true;
+    } else if (same) {
+      o.reasons = KS_R_DEV_JOINT;
+      return o;
+    }
+  }
+  if (!jdone) {
+    // allocateDevices per remaining type: feasibility is a count; the minors only with ALLOC
+    if ((has_gpu && __builtin_popcount(G.fit) < g.desired) || (has_rdma && __builtin_popcount(R.fit) < g.rdesired)) {
+      o.reasons = KS_R_DEV_INSUFFICIENT;
+      return o;
+    }
+    if (ALLOC) {
+      om = has_gpu ? dev_take(G, kGpus, 0xFFu, g.desired, 0u) : 0u;
+      orm = has_rdma ? dev_take(R, kRdma, 0xFFu, g.rdesired, 0u) : 0u;
+    }
+  }
+  o.raw = raw;
+  if (ALLOC) {
+    o.minors = om;
+    o.rminors = orm;
   }
   return o;
 }

@@ -35,8 +35,10 @@ constexpr int kMaxCand = 64;   // candidate chunks per pod
 constexpr uint32_t kPodAllZero = 0x100u;
 // internal pod flag: every request value is zero (quotav1.IsZero, NodeNUMAResource PreFilter skip)
 constexpr uint32_t kPodReqZero = 0x200u;
-// internal pod flag: the pod has a GPU request (DeviceShare preparePod: skip = false)
+// internal pod flag: the pod has a device request, GPU or RDMA (DeviceShare preparePod: skip = false)
 constexpr uint32_t kPodHasGpu = 0x400u;
+// internal pod flag: the pod has a GPU request
+constexpr uint32_t kPodGpuReq = 0x800u;
 
 // la_bits (prep_nodes_kernel output)
 constexpr uint32_t kLaZeroScore = 0x1u;     // Score returns 0 (no NodeMetric / expired)
@@ -62,7 +64,7 @@ struct Cfg {
   int32_t cpuset;    // CPU state loaded: cpu-bind pods are evaluated (ks_cpuset.h)
   int32_t numa_pol;  // nodes with a NUMA topology policy exist (ks_numa.h)
   int32_t numa_sc_most;  // NUMAScoringStrategy MostAllocated (hint scores)
-  int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw;  // DeviceShare (GPU)
+  int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw, dw_rdma;  // DeviceShare (GPU, RDMA)
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -106,8 +108,11 @@ struct __attribute__((aligned(16))) PodRec {
   int64_t h_cpu, h_mem;  // 100 x the Requested cpu / memory (NodeNUMAResource score)
   float f_cpu, f_mem;
   int64_t gpu_core, gpu_mem, gpu_ratio;  // DeviceShare: converted GPU request
+  int64_t rdma;                          // DeviceShare: koordinator.sh/rdma request
+  uint32_t joint;                        // DeviceShare: KS_JOINT_*
+  int32_t _pad0;
 };
-static_assert(sizeof(PodRec) == 272, "PodRec layout");
+static_assert(sizeof(PodRec) == 288, "PodRec layout");
 // PodRec int64 word indices read by the commit kernel's lane-parallel Reserve
 constexpr int kPodWordHCpu = (int)(offsetof(PodRec, h_cpu) / 8), kPodWordHMem = (int)(offsetof(PodRec, h_mem) / 8);
 static_assert(offsetof(PodRec, h_nzcpu) == 12 * 8 && offsetof(PodRec, h_sc) == 17 * 8, "PodRec word layout");

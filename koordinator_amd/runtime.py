@@ -61,6 +61,7 @@ def lib() -> C.CDLL:
     L.ks_read_reservations.argtypes = [vp, abi.P64, abi.P32]
     L.ks_load_devices.argtypes = [vp, C.POINTER(abi.KsDeviceCols), C.c_int64]
     L.ks_read_devices.argtypes = [vp, abi.P64, abi.P64, abi.P64]
+    L.ks_read_devices_rdma.argtypes = [vp, abi.P64]
     L.ks_load_cpu_state.argtypes = [vp, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
     L.ks_read_cpu_state.argtypes = [vp, abi.PU64, abi.PU64, abi.PU64]
     L.ks_fetch_cpusets.argtypes = [vp, abi.PU64, C.c_int32]
@@ -203,11 +204,14 @@ class Evaluator:
         return out[:p]
 
     def read_devices(self):
-        """(used_core, used_memory, used_ratio), each [KS_MAX_GPUS][n]"""
+        """(used_core, used_memory, used_ratio) [KS_MAX_GPUS][n], used_rdma [KS_MAX_RDMA][n]"""
         G = abi.KS_MAX_GPUS
         out = [np.zeros(G * max(self.n, 1), np.int64) for _ in range(3)]
         self._chk(self.L.ks_read_devices(self.h, *[o.ctypes.data_as(abi.P64) for o in out]))
-        return tuple(o[: G * self.n].reshape(G, self.n) for o in out)
+        R = abi.KS_MAX_RDMA
+        r = np.zeros(R * max(self.n, 1), np.int64)
+        self._chk(self.L.ks_read_devices_rdma(self.h, r.ctypes.data_as(abi.P64)))
+        return tuple(o[: G * self.n].reshape(G, self.n) for o in out) + (r[: R * self.n].reshape(R, self.n),)
 
     def read_reservations(self):
         """(allocated [r][KS_RSV_DIMS], assigned [r]) after commits"""
@@ -240,7 +244,8 @@ class Evaluator:
         self._chk(self.L.ks_schedule(self.h, C.byref(cols), pods.n, out.ctypes.data_as(C.POINTER(abi.KsResult))))
         out = out[: pods.n]
         return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy(),
-                "reservation": out["reservation"].copy(), "gpu_minors": out["gpu_minors"].copy()}
+                "reservation": out["reservation"].copy(), "gpu_minors": out["gpu_minors"].copy(),
+                "rdma_minors": out["rdma_minors"].copy()}
 
     def stage(self, pods: PodTable):
         cols = pods.ks()
@@ -255,7 +260,8 @@ class Evaluator:
         self._chk(self.L.ks_fetch_results(self.h, out.ctypes.data_as(C.POINTER(abi.KsResult)), self.np_staged))
         out = out[: self.np_staged]
         return {"node": out["node"].copy(), "status": out["status"].copy(), "score": out["score"].copy(),
-                "reservation": out["reservation"].copy(), "gpu_minors": out["gpu_minors"].copy()}
+                "reservation": out["reservation"].copy(), "gpu_minors": out["gpu_minors"].copy(),
+                "rdma_minors": out["rdma_minors"].copy()}
 
     def checkpoint(self):
         self._chk(self.L.ks_checkpoint(self.h))

@@ -7,11 +7,13 @@ would produce from a scheduler-cache snapshot plus NodeMetric objects:
 * C1  500 nodes, 1k pods, NodeResourcesFit + LoadAwareScheduling
 * C2  5k nodes, 10k pods, + ElasticQuota admission (32 leaf quotas under root,
       limits sized so roughly a tenth of the pods are rejected)
-* C3  5k nodes with 8 (or 4) 80 GiB GPUs each (make_devices) and cpu amplification ratios with
-      cpuset-held CPUs (NodeNUMAResource); 10k pods, 40 % requesting GPUs (whole devices 1/2/4, half a
-      GPU by ratio, or a gpu-memory amount); Fit + LoadAware + NodeNUMAResource + DeviceShare.  The
-      reference's C3 also has cpuset (LSR) pods and GPU+RDMA joint allocation, which this build
-      does not model
+* C3  5k nodes with 8 (or 4) 80 GiB GPUs and 4 RDMA devices on 4 PCIe switches / 2 NUMA nodes each
+      (make_devices, the device_allocator_test.go layout) and cpu amplification ratios with cpuset-held
+      CPUs (NodeNUMAResource); 10k pods, 40 % requesting GPUs (whole devices 1/2/4, half a GPU by ratio,
+      or a gpu-memory amount; half of the whole-GPU pods with rdma 1 and joint [gpu, rdma] allocation,
+      half of those SamePCIe), a few RDMA-only pods, and cpuset (LSR) pods; Fit + LoadAware +
+      NodeNUMAResource + DeviceShare.  Nodes carry no NUMA topology policy here (the reference's C3 has
+      SingleNUMANode nodes; DeviceShare NUMA hints are DESIGN.md §9)
 * C4  20k nodes with 50k reservations (make_reservations), 10k pods of which 60 % belong to one
       of 16 reservation owner classes, NodeResourcesFit + LoadAwareScheduling + Reservation (weight 5000)
 * C5  100k nodes, C1 pod distribution (the multi-GPU sharding config)
@@ -223,7 +225,7 @@ def reservation_pods(pods: PodTable, rng: np.random.Generator, n_classes: int = 
     return pods
 
 
-def make_devices(nodes: NodeTable, rng: np.random.Generator, gpu_frac: float = 0.9) -> "DeviceTable":
+def make_devices(nodes: NodeTable, rng: np.random.Generator, gpu_frac: float = 0.9, rdma: bool = False) -> "DeviceTable":
     """GPU devices (DeviceShare): 90 % of the nodes carry 8 (or 4) GPUs of 80 GiB (gpu-core 100,
     gpu-memory-ratio 100 each), some already partly used by running GPU pods; the rest have no
     device information.  A few nodes carry an unhealthy minor (zero totals)."""
@@ -243,7 +245,36 @@ def make_devices(nodes: NodeTable, rng: np.random.Generator, gpu_frac: float = 0
         d.used_core[k] = np.where(used, part, 0)
         d.used_ratio[k] = np.where(used, part, 0)
         d.used_memory[k] = np.where(used, part * 80 * GI // 100, 0)
+    if rdma:
+        # the layout of deviceshare/device_allocator_test.go:49-57: GPU k on PCIe switch k // 2, RDMA minor
+        # j = 1..4 on switch j - 1, switches 0-1 on socket 0 / NUMA node 0 and 2-3 on socket 1 / node 1;
+        # koordinator.sh/rdma 100 per RDMA device, some partly used
+        for k in range(abi.KS_MAX_GPUS):
+            d.gpu_pcie[k] = np.where(d.total_ratio[k] > 0, k // 2, abi.KS_PCIE_NONE)
+        for j in range(1, 5):
+            on = has & (rng.random(n) > 0.02)
+            d.total_rdma[j] = np.where(on, 100, 0)
+            d.used_rdma[j] = np.where(on & (rng.random(n) < 0.3), rng.choice(np.array([1, 50, 100], np.int64), n), 0)
+            d.rdma_pcie[j] = j - 1
+        for p in range(4):
+            d.pcie_numa[p] = p // 2
+            d.pcie_socket[p] = p // 2
     return d
+
+
+def rdma_pods(pods: PodTable, rng: np.random.Generator, joint_frac: float = 0.5, rdma_only: float = 0.03) -> PodTable:
+    """Half of the whole-GPU pods also ask for koordinator.sh/rdma 1 with joint [gpu, rdma] allocation (half of
+    those with RequiredScope SamePCIe, SURVEY C3's "GPU+RDMA joint SamePCIe" pods); a few pods ask for RDMA
+    only (1, 50 or 100 = one whole device)."""
+    p = pods.n
+    whole = (pods.gpu_core >= 100) & (pods.gpu_core % 100 == 0)
+    j = whole & (rng.random(p) < joint_frac)
+    same = rng.random(p) < 0.5
+    pods.rdma[:] = np.where(j, 1, 0)
+    pods.joint[:] = np.where(j, np.where(same, abi.KS_JOINT_GPU_RDMA_SAME_PCIE, abi.KS_JOINT_GPU_RDMA), 0)
+    only = (pods.gpu_core + pods.gpu_memory + pods.gpu_memory_ratio == 0) & (rng.random(p) < rdma_only)
+    pods.rdma[:] = np.where(only, rng.choice(np.array([1, 50, 100], np.int64), p), pods.rdma)
+    return pods
 
 
 def gpu_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4) -> PodTable:
@@ -379,12 +410,12 @@ def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, **kw) -> Wor
     nodes.numa_cpu_amplification[:] = ratio
     nodes.alloc_milli_cpu[amp] = np.ceil(nodes.alloc_milli_cpu[amp] * ratio[amp]).astype(np.int64)
     cpus = make_cpu_state(nodes, rng, cores=cores)
-    devs = make_devices(nodes, rng)
-    pods = gpu_pods(make_pods(n_pods, rng), rng)
+    devs = make_devices(nodes, rng, rdma=True)
+    pods = rdma_pods(gpu_pods(make_pods(n_pods, rng), rng), rng)
     pods = cpuset_pods(pods, rng, 0.4 / 0.6, exclude=pods.gpu_memory_ratio + pods.gpu_memory > 0)
     prof = koord_profile(**kw)
     prof.numa = NodeNUMAResourceArgs()
-    prof.deviceshare = DeviceShareArgs(resources={GPU_MEMORY_RATIO: 1})
+    prof.deviceshare = DeviceShareArgs()  # v1beta2 defaults: gpu-memory-ratio, rdma, fpga weight 1
     return Workload("C3", prof, nodes, pods, None, None, devs, cpus)
 
 

@@ -127,13 +127,33 @@ typedef struct {
 typedef struct ko_pool ko_pool;
 
 #define KO_GPUS KS_MAX_GPUS
-/* nodeDeviceCache: per node and GPU minor, deviceTotal / deviceUsed of (core, memory, ratio) */
+#define KO_RDMA KS_MAX_RDMA
+#define KO_PCIE KS_MAX_PCIE
+/* nodeDeviceCache: per node and GPU minor, deviceTotal / deviceUsed of (core, memory, ratio); per RDMA
+ * minor of koordinator.sh/rdma; the device topology (PCIe switch per minor, NUMA node / socket per switch) */
 typedef struct {
   int loaded;
   uint32_t *flags;
   int64_t *total; /* [n][KO_GPUS][3] */
   int64_t *used;  /* [n][KO_GPUS][3] */
+  int64_t *rtotal, *rused; /* [n][KO_RDMA] */
+  uint8_t *gpcie;  /* [n][KO_GPUS] */
+  uint8_t *rpcie;  /* [n][KO_RDMA] */
+  uint8_t *pnuma, *psock; /* [n][KO_PCIE] */
 } ko_dev;
+
+static void dev_free(ko_dev *d) {
+  free(d->flags);
+  free(d->total);
+  free(d->used);
+  free(d->rtotal);
+  free(d->rused);
+  free(d->gpcie);
+  free(d->rpcie);
+  free(d->pnuma);
+  free(d->psock);
+  memset(d, 0, sizeof(*d));
+}
 
 /* reservation cache: rows in caller order, CSR by node (rows of a node in table order) */
 typedef struct {
@@ -197,6 +217,8 @@ typedef struct {
   int reqzero;   /* quotav1.IsZero(PodRequestsAndLimits) (NodeNUMAResource PreFilter skip) */
   int64_t gpu[3]; /* converted GPU request: core, memory, ratio */
   int has_gpu;
+  int64_t rdma;  /* koordinator.sh/rdma request */
+  uint8_t joint; /* KS_JOINT_* */
   uint32_t keys; /* bit d: request dimension d is a key of the pod's requests (value != 0) */
   uint32_t bind;  /* cpu-bind pod (preFilterState.requestCPUBind): ks_pod_cols.cpu_bind, else 0 */
   int32_t needed; /* numCPUsNeeded */
@@ -238,6 +260,8 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
   p->gpu[1] = colv64(pc->gpu_memory, i);
   p->gpu[2] = colv64(pc->gpu_memory_ratio, i);
   p->has_gpu = p->gpu[0] != 0 || p->gpu[1] != 0 || p->gpu[2] != 0;
+  p->rdma = colv64(pc->rdma, i);
+  p->joint = pc->joint ? pc->joint[i] : 0;
   if (s->cfg.numa.enable && (p->flags & KS_POD_CPU_BIND) && pc->cpu_bind) {
     p->bind = pc->cpu_bind[i];
     p->needed = (int32_t)(p->cpu / 1000);
@@ -974,60 +998,113 @@ static void rsv_reserve(ko_sched *s, const ko_pod *p, int32_t r) {
 }
 
 /* ------------------------------------------------------------------ */
-/* DeviceShare (GPU)                                                   */
+/* DeviceShare (GPU + RDMA, joint allocation)                          */
 /* ------------------------------------------------------------------ */
+
+enum { KO_T_GPU = 0, KO_T_RDMA = 1, KO_NTYPES = 2 };
 
 static const int64_t *dev_total(const ko_sched *s, int64_t n, int k) { return s->dv.total + ((size_t)n * KO_GPUS + k) * 3; }
 static const int64_t *dev_used(const ko_sched *s, int64_t n, int k) { return s->dv.used + ((size_t)n * KO_GPUS + k) * 3; }
 
-/* a GPU instance: the request per instance and how many (GPUHandler.CalcDesiredRequestsAndCount
- * after fillGPUTotalMem); returns KS_R_DEV_NO_GPU when the node has no healthy GPU */
-typedef struct {
-  int64_t req[3]; /* core, memory, ratio */
-  int has_core;
-  int desired;
-} ko_gpureq;
-
-static uint32_t dev_prepare(const ko_sched *s, const ko_pod *p, int64_t n, ko_gpureq *g) {
-  int64_t total_mem = -1;
-  for (int k = 0; k < KO_GPUS; k++) {
-    const int64_t *t = dev_total(s, n, k);
-    if (t[0] || t[1] || t[2]) {
-      total_mem = t[1];
-      break;
+/* one minor of a device type as nodeDevice sees it: deviceTotal / deviceFree (= total - used, kept as
+ * an all-zero entry when fully used, resetDeviceFree device_cache.go:157-174); RDMA uses q = 0 only.
+ * Returns 0 for an absent minor (all-zero total). */
+static int dev_minor(const ko_sched *s, int64_t n, int type, int k, int64_t tot[3], int64_t fre[3]) {
+  tot[0] = tot[1] = tot[2] = fre[0] = fre[1] = fre[2] = 0;
+  if (type == KO_T_GPU) {
+    const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
+    for (int q = 0; q < 3; q++) {
+      tot[q] = t[q];
+      fre[q] = t[q] > u[q] ? t[q] - u[q] : 0;
     }
+  } else {
+    tot[0] = s->dv.rtotal[(size_t)n * KO_RDMA + k];
+    int64_t u = s->dv.rused[(size_t)n * KO_RDMA + k];
+    fre[0] = tot[0] > u ? tot[0] - u : 0;
   }
-  if (total_mem < 0) return KS_R_DEV_NO_GPU;
-  int64_t core = p->gpu[0], mem = p->gpu[1], ratio = p->gpu[2];
-  if (p->flags & KS_POD_GPU_MEMORY)
-    ratio = (int64_t)((double)mem / (double)total_mem * 100); /* memoryBytesToRatio */
-  else
-    mem = ratio * total_mem / 100; /* memoryRatioToBytes */
-  g->has_core = (p->flags & KS_POD_GPU_CORE) != 0;
-  g->desired = 1;
-  if (ratio > 100 && ratio % 100 == 0) {
-    g->desired = (int)(ratio / 100);
-    core /= g->desired;
-    mem /= g->desired;
-    ratio /= g->desired;
+  return tot[0] != 0 || tot[1] != 0 || tot[2] != 0;
+}
+static int dev_nminors(int type) { return type == KO_T_GPU ? KO_GPUS : KO_RDMA; }
+static int dev_pcie(const ko_sched *s, int64_t n, int type, int k) {
+  return type == KO_T_GPU ? s->dv.gpcie[(size_t)n * KO_GPUS + k] : s->dv.rpcie[(size_t)n * KO_RDMA + k];
+}
+
+/* AutopilotAllocator.Prepare -> calcRequestsAndCountByDeviceType (device_allocator.go:72-92, 160-186): the
+ * request per instance and the desired count per requested device type */
+typedef struct {
+  int has[KO_NTYPES];
+  int64_t req[KO_NTYPES][3]; /* GPU: core, memory, ratio; RDMA: rdma */
+  int has_core;
+  int desired[KO_NTYPES];
+} ko_devreq;
+
+/* GPUHandler.CalcDesiredRequestsAndCount after fillGPUTotalMem (devicehandler_gpu.go:40-98) and
+ * DefaultDeviceHandler for RDMA (devicehandler_default.go:44-93, no hints).  Returns KS_R_DEV_NO_GPU /
+ * KS_R_DEV_NO_RDMA (UnschedulableAndUnresolvable) for a node without such devices (GPU checked first). */
+static uint32_t dev_prepare(const ko_sched *s, const ko_pod *p, int64_t n, ko_devreq *g) {
+  memset(g, 0, sizeof(*g));
+  if (p->has_gpu) {
+    int64_t total_mem = -1;
+    for (int k = 0; k < KO_GPUS; k++) {
+      const int64_t *t = dev_total(s, n, k);
+      if (t[0] || t[1] || t[2]) {
+        total_mem = t[1];
+        break;
+      }
+    }
+    if (total_mem < 0) return KS_R_DEV_NO_GPU;
+    int64_t core = p->gpu[0], mem = p->gpu[1], ratio = p->gpu[2];
+    if (p->flags & KS_POD_GPU_MEMORY)
+      ratio = (int64_t)((double)mem / (double)total_mem * 100); /* memoryBytesToRatio */
+    else
+      mem = ratio * total_mem / 100; /* memoryRatioToBytes */
+    g->has_core = (p->flags & KS_POD_GPU_CORE) != 0;
+    int d = 1;
+    if (ratio > 100 && ratio % 100 == 0) {
+      d = (int)(ratio / 100);
+      core /= d;
+      mem /= d;
+      ratio /= d;
+    }
+    g->has[KO_T_GPU] = 1;
+    g->desired[KO_T_GPU] = d;
+    g->req[KO_T_GPU][0] = g->has_core ? core : 0;
+    g->req[KO_T_GPU][1] = mem;
+    g->req[KO_T_GPU][2] = ratio;
   }
-  g->req[0] = core;
-  g->req[1] = mem;
-  g->req[2] = ratio;
+  if (p->rdma > 0) {
+    int any = 0;
+    for (int k = 0; k < KO_RDMA; k++) {
+      int64_t t[3], f[3];
+      any |= dev_minor(s, n, KO_T_RDMA, k, t, f);
+    }
+    if (!any) return KS_R_DEV_NO_RDMA;
+    int64_t q = p->rdma;
+    int d = 1;
+    if (q > 100 && q % 100 == 0) {
+      d = (int)(q / 100);
+      q /= d;
+    }
+    g->has[KO_T_RDMA] = 1;
+    g->desired[KO_T_RDMA] = d;
+    g->req[KO_T_RDMA][0] = q;
+  }
   return 0;
 }
 
-static int64_t dev_weight(const ko_sched *s, int r) {
+static int64_t dev_weight(const ko_sched *s, int type, int r) {
   const ks_deviceshare_args *a = &s->cfg.deviceshare;
+  if (type == KO_T_RDMA) return r == 0 ? a->weight_rdma : 0;
   return r == 0 ? a->weight_gpu_core : r == 1 ? a->weight_gpu_memory : a->weight_gpu_memory_ratio;
 }
 
-/* resourceAllocationScorer over (requested, allocatable) pairs (scoring.go:254-308) */
-static int64_t dev_scorer(const ko_sched *s, const int64_t *total, const int64_t *free, const int64_t *podreq) {
+/* resourceAllocationScorer.scoreDevice / scoreNode body over (requested, allocatable) pairs
+ * (scoring.go:187-243, 254-308): requested = total - free + pod when total >= free */
+static int64_t dev_scorer(const ko_sched *s, int type, const int64_t *total, const int64_t *free, const int64_t *podreq) {
   int most = s->cfg.deviceshare.strategy == KS_MOST_ALLOCATED;
   int64_t node_score = 0, weight_sum = 0;
   for (int r = 0; r < 3; r++) {
-    int64_t w = dev_weight(s, r);
+    int64_t w = dev_weight(s, type, r);
     if (w == 0 || total[r] == 0) continue;
     int64_t req = total[r];
     if (total[r] >= free[r]) req = total[r] - free[r] + podreq[r];
@@ -1037,71 +1114,265 @@ static int64_t dev_scorer(const ko_sched *s, const int64_t *total, const int64_t
   return weight_sum ? node_score / weight_sum : 0;
 }
 
-/* defaultAllocateDevices: the free minors sorted by (scoreDevice desc, minor asc), the first `desired`
- * that satisfy LessThanOrEqual(request, free).  Returns the minor mask, 0 if fewer fit. */
-static uint32_t dev_allocate(const ko_sched *s, int64_t n, const ko_gpureq *g) {
-  int64_t sc[KO_GPUS];
-  int ok[KO_GPUS];
-  int64_t podreq[3] = {g->has_core ? g->req[0] : 0, g->req[1], g->req[2]};
-  for (int k = 0; k < KO_GPUS; k++) {
-    const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
-    int64_t free[3] = {t[0] - u[0], t[1] - u[1], t[2] - u[2]};
-    ok[k] = 0;
-    sc[k] = 0;
-    if (!(t[0] || t[1] || t[2])) continue;           /* no such minor */
-    if (!(free[0] || free[1] || free[2])) continue;  /* fully used: dropped from deviceFree */
-    int fits = (!g->has_core || g->req[0] <= free[0]) && g->req[1] <= free[1] && g->req[2] <= free[2];
-    ok[k] = fits;
-    sc[k] = dev_scorer(s, t, free, podreq);
+/* quotav1.LessThanOrEqual(requestPerInstance, free) over the request's keys */
+static int dev_fits(const ko_devreq *g, int type, const int64_t *fre) {
+  if (type == KO_T_RDMA) return g->req[type][0] <= fre[0];
+  return (!g->has_core || g->req[type][0] <= fre[0]) && g->req[type][1] <= fre[1] && g->req[type][2] <= fre[2];
+}
+
+/* nodeDevice.split: how many minors of `sub` satisfy the request per instance (device_cache.go:419-433) */
+static int dev_split(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub) {
+  int c = 0;
+  for (int k = 0; k < dev_nminors(type); k++) {
+    int64_t t[3], f[3];
+    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f)) continue;
+    c += dev_fits(g, type, f);
   }
+  return c;
+}
+
+typedef struct {
+  int minor, preferred;
+  int64_t score;
+  int64_t free[3];
+} ko_pair;
+
+/* sortDeviceResourcesByMinor comparator (device_resources.go:194-206) */
+static int pair_less(const ko_pair *a, const ko_pair *b) {
+  if (a->preferred != b->preferred) return a->preferred;
+  if (a->score != b->score) return a->score > b->score;
+  return a->minor < b->minor;
+}
+
+/* allocateDevices -> defaultAllocateDevices (device_allocator.go:360-462) over the minors `sub` of the
+ * (filtered) node device: scoreDevices, sortDeviceResourcesByPreferredPCIe (pcie in `pref`), the first
+ * maxDesiredCount = max(desired, |pref|) minors with non-zero free that satisfy the request.  Returns the
+ * allocated minors as a mask (0 = "Insufficient <type> devices"). */
+static uint32_t dev_alloc_type(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub, int desired,
+                               uint32_t pref) {
+  int maxd = desired, npref = __builtin_popcount(pref);
+  if (npref > maxd) maxd = npref;
+  if (desired == 0) desired = 1;
+  if (maxd < desired) maxd = desired;
+  ko_pair r[KO_GPUS > KO_RDMA ? KO_GPUS : KO_RDMA];
+  int m = 0;
+  for (int k = 0; k < dev_nminors(type); k++) {
+    int64_t t[3], f[3];
+    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f)) continue;
+    ko_pair *x = &r[m++];
+    x->minor = k;
+    x->score = dev_scorer(s, type, t, f, g->req[type]);
+    int pc = dev_pcie(s, n, type, k);
+    x->preferred = pc != KS_PCIE_NONE && ((pref >> pc) & 1u);
+    memcpy(x->free, f, sizeof(f));
+  }
+  for (int i = 1; i < m; i++) /* insertion sort (a total order: minors are unique) */
+    for (int j = i; j > 0 && pair_less(&r[j], &r[j - 1]); j--) {
+      ko_pair tmp = r[j];
+      r[j] = r[j - 1];
+      r[j - 1] = tmp;
+    }
   uint32_t mask = 0;
-  for (int got = 0; got < g->desired; got++) {
-    int best = -1;
-    for (int k = 0; k < KO_GPUS; k++)
-      if (ok[k] && !((mask >> k) & 1u) && (best < 0 || sc[k] > sc[best])) best = k;
-    if (best < 0) return 0;
-    mask |= 1u << best;
+  int got = 0;
+  for (int i = 0; i < m && got < maxd; i++) {
+    if (!r[i].free[0] && !r[i].free[1] && !r[i].free[2]) continue; /* zero resources */
+    if (!dev_fits(g, type, r[i].free)) continue;
+    mask |= 1u << r[i].minor;
+    got++;
   }
-  return mask;
+  return got < desired ? 0 : mask;
+}
+
+/* the PCIe switches of the allocated minors (newPreferredPCIes, device_allocator.go:494-505) */
+static uint32_t dev_pcies_of(const ko_sched *s, int64_t n, int type, uint32_t mask) {
+  uint32_t p = 0;
+  for (int k = 0; k < dev_nminors(type); k++) {
+    int pc = dev_pcie(s, n, type, k);
+    if (((mask >> k) & 1u) && pc != KS_PCIE_NONE) p |= 1u << pc;
+  }
+  return p;
+}
+
+/* jointAllocate (device_allocator.go:286-339) on the node device restricted to sub[]: the GPUs, then the
+ * RDMA devices preferring the GPUs' PCIe switches.  0 = failed. */
+static int dev_joint_alloc(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, const uint32_t sub[2],
+                           uint32_t pref, uint32_t out[2]) {
+  uint32_t prim = dev_alloc_type(s, n, g, KO_T_GPU, sub[KO_T_GPU], g->desired[KO_T_GPU], pref);
+  if (!prim) return 0;
+  uint32_t pcies = dev_pcies_of(s, n, KO_T_GPU, prim);
+  int desired = same_pcie ? __builtin_popcount(pcies) : 1;
+  uint32_t sec = dev_alloc_type(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], desired, pcies);
+  if (!sec) return 0;
+  out[KO_T_GPU] = prim;
+  out[KO_T_RDMA] = sec;
+  return 1;
+}
+
+/* the minors of each type whose PCIe switch is in `pcies` */
+static void dev_sub_of(const ko_sched *s, int64_t n, uint32_t pcies, uint32_t sub[2]) {
+  for (int t = 0; t < KO_NTYPES; t++) {
+    sub[t] = 0;
+    for (int k = 0; k < dev_nminors(t); k++) {
+      int pc = dev_pcie(s, n, t, k);
+      if (pc != KS_PCIE_NONE && ((pcies >> pc) & 1u)) sub[t] |= 1u << k;
+    }
+  }
+}
+
+/* tryJointAllocate -> allocateByTopology (device_allocator.go:188-253) with DeviceTypes [gpu, rdma]:
+ * per PCIe switch (newDeviceTopologyGuide / freeNodeDevicesInPCIe, numa_topology.go:109-175), per NUMA node
+ * (freeNodeDevicesInNode :185-240), then the whole node.  Returns 1 with out[] on success. */
+static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, uint32_t out[2]) {
+  const uint32_t all[2] = {(1u << KO_GPUS) - 1u, (1u << KO_RDMA) - 1u};
+  uint32_t exist = 0; /* switches that hold a device */
+  for (int t = 0; t < KO_NTYPES; t++)
+    for (int k = 0; k < dev_nminors(t); k++) {
+      int64_t tt[3], ff[3];
+      int pc = dev_pcie(s, n, t, k);
+      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff)) exist |= 1u << pc;
+    }
+  const uint8_t *pnuma = s->dv.pnuma + (size_t)n * KO_PCIE, *psock = s->dv.psock + (size_t)n * KO_PCIE;
+  /* pcieSwitches in (socket, node, pcie) order = index order; preferred: free rdma instances on the switch */
+  int sw[KO_PCIE], nsw = 0, swpref[KO_PCIE] = {0};
+  for (int pc = 0; pc < KO_PCIE; pc++) {
+    if (!((exist >> pc) & 1u)) continue;
+    uint32_t sub[2];
+    dev_sub_of(s, n, 1u << pc, sub);
+    swpref[pc] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA]) > 0;
+    sw[nsw++] = pc;
+  }
+  /* freeNodeDevicesInPCIe: sort.Slice by (preferred desc, socket, node); stable here (insertion sort for
+   * <= 12 elements in Go's sort) */
+  for (int i = 1; i < nsw; i++)
+    for (int j = i; j > 0; j--) {
+      int a = sw[j], b = sw[j - 1];
+      int less = swpref[a] != swpref[b] ? swpref[a] : (psock[a] != psock[b] ? psock[a] < psock[b] : pnuma[a] < pnuma[b]);
+      if (!less) break;
+      sw[j] = b;
+      sw[j - 1] = a;
+    }
+  for (int i = 0; i < nsw; i++) {
+    uint32_t sub[2];
+    dev_sub_of(s, n, 1u << sw[i], sub);
+    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU]) >= g->desired[KO_T_GPU] &&
+        dev_joint_alloc(s, n, g, same_pcie, sub, 1u << sw[i], out))
+      return 1;
+  }
+  /* groupedNodeDevices per NUMA node: preferredPCIes = the node's preferred switches */
+  int grp[KO_PCIE], ng = 0;
+  uint32_t gp[256] = {0}, gpref_pcies[256] = {0};
+  int gpref[256] = {0};
+  for (int pc = 0; pc < KO_PCIE; pc++) {
+    if (!((exist >> pc) & 1u)) continue;
+    int node = pnuma[pc];
+    if (!gp[node]) grp[ng++] = node;
+    gp[node] |= 1u << pc;
+    if (swpref[pc]) gpref_pcies[node] |= 1u << pc;
+  }
+  for (int i = 0; i < ng; i++) {
+    uint32_t sub[2];
+    dev_sub_of(s, n, gp[grp[i]], sub);
+    gpref[grp[i]] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA]) > 0;
+  }
+  for (int i = 1; i < ng; i++)
+    for (int j = i; j > 0; j--) {
+      int a = grp[j], b = grp[j - 1];
+      int pa = __builtin_popcount(gpref_pcies[a]), pb = __builtin_popcount(gpref_pcies[b]);
+      int less = pa != pb ? pa > pb : (gpref[a] != gpref[b] ? gpref[a] : a < b);
+      if (!less) break;
+      grp[j] = b;
+      grp[j - 1] = a;
+    }
+  uint32_t union_pref = 0;
+  for (int i = 0; i < ng; i++) {
+    uint32_t sub[2];
+    dev_sub_of(s, n, gp[grp[i]], sub);
+    union_pref |= gpref_pcies[grp[i]];
+    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU]) >= g->desired[KO_T_GPU] &&
+        dev_joint_alloc(s, n, g, same_pcie, sub, gpref_pcies[grp[i]], out))
+      return 1;
+  }
+  /* the whole node, preferring every preferred switch */
+  return dev_joint_alloc(s, n, g, same_pcie, all, union_pref, out);
+}
+
+/* AutopilotAllocator.Allocate (device_allocator.go:94-132) without hints, preemption or reservations:
+ * tryJointAllocate, then allocateDevices for the types joint allocation did not cover.  Returns the
+ * KS_R_DEV_* reason (0 = allocated, masks in out[]). */
+static uint32_t dev_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_devreq *g, uint32_t out[2]) {
+  const uint32_t all[2] = {(1u << KO_GPUS) - 1u, (1u << KO_RDMA) - 1u};
+  out[0] = out[1] = 0;
+  if (p->joint && g->has[KO_T_GPU]) {
+    const int same = p->joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
+    uint32_t j[2] = {0, 0};
+    if (dev_by_topology(s, n, g, same, j)) {
+      /* validateJointAllocation (:255-284): the RDMA switches must equal the GPU switches */
+      if (same && dev_pcies_of(s, n, KO_T_GPU, j[0]) != dev_pcies_of(s, n, KO_T_RDMA, j[1])) return KS_R_DEV_JOINT;
+      out[0] = j[0];
+      out[1] = j[1];
+    } else if (same) {
+      return KS_R_DEV_JOINT;
+    }
+  }
+  for (int t = 0; t < KO_NTYPES; t++) {
+    if (!g->has[t] || out[t]) continue;
+    out[t] = dev_alloc_type(s, n, g, t, all[t], g->desired[t], 0);
+    if (!out[t]) return KS_R_DEV_INSUFFICIENT;
+  }
+  return 0;
+}
+
+/* AutopilotAllocator.score (device_allocator.go:507-530): scoreNode per requested type, summed */
+static int64_t dev_node_score(const ko_sched *s, int64_t n, const ko_devreq *g) {
+  int64_t sum = 0;
+  for (int t = 0; t < KO_NTYPES; t++) {
+    if (!g->has[t]) continue;
+    int64_t total[3] = {0, 0, 0}, free[3] = {0, 0, 0};
+    for (int k = 0; k < dev_nminors(t); k++) {
+      int64_t tt[3], ff[3];
+      if (!dev_minor(s, n, t, k, tt, ff)) continue;
+      for (int q = 0; q < 3; q++) {
+        total[q] += tt[q];
+        free[q] += ff[q];
+      }
+    }
+    sum += dev_scorer(s, t, total, free, g->req[t]);
+  }
+  return sum;
 }
 
 /* DeviceShare Filter; *raw gets the node score (scoreNode) when feasible */
 static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *raw) {
   *raw = 0;
-  if (!s->cfg.deviceshare.enable || !p->has_gpu) return 0;
+  if (!s->cfg.deviceshare.enable || !(p->has_gpu || p->rdma > 0)) return 0;
   if (!s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return 0; /* no device info: pass, score 0 */
-  ko_gpureq g;
+  ko_devreq g;
   uint32_t r = dev_prepare(s, p, n, &g);
   if (r) return r;
-  if (!dev_allocate(s, n, &g)) return KS_R_DEV_INSUFFICIENT;
-  int64_t total[3] = {0, 0, 0}, free[3] = {0, 0, 0};
-  for (int k = 0; k < KO_GPUS; k++) {
-    const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
-    if (!(t[0] || t[1] || t[2])) continue;
-    int64_t f[3] = {t[0] - u[0], t[1] - u[1], t[2] - u[2]};
-    for (int q = 0; q < 3; q++) total[q] += t[q];
-    if (f[0] || f[1] || f[2])
-      for (int q = 0; q < 3; q++) free[q] += f[q];
-  }
-  int64_t podreq[3] = {g.has_core ? g.req[0] : 0, g.req[1], g.req[2]};
-  *raw = dev_scorer(s, total, free, podreq);
+  uint32_t m[2];
+  r = dev_allocate(s, p, n, &g, m);
+  if (r) return r;
+  *raw = dev_node_score(s, n, &g);
   return 0;
 }
 
-/* Reserve -> nodeDevice.updateCacheUsed: used += the allocation on each chosen minor */
-static uint32_t dev_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
-  if (!s->cfg.deviceshare.enable || !p->has_gpu || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return 0;
-  ko_gpureq g;
-  if (dev_prepare(s, p, n, &g)) return 0;
-  uint32_t mask = dev_allocate(s, n, &g);
+/* Reserve -> nodeDevice.updateCacheUsed: used += the request per instance on each allocated minor */
+static void dev_reserve(ko_sched *s, const ko_pod *p, int64_t n, uint32_t *gpu_minors, uint32_t *rdma_minors) {
+  *gpu_minors = *rdma_minors = 0;
+  if (!s->cfg.deviceshare.enable || !(p->has_gpu || p->rdma > 0) || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT))
+    return;
+  ko_devreq g;
+  uint32_t m[2];
+  if (dev_prepare(s, p, n, &g) || dev_allocate(s, p, n, &g, m)) return;
   for (int k = 0; k < KO_GPUS; k++) {
-    if (!((mask >> k) & 1u)) continue;
+    if (!((m[0] >> k) & 1u)) continue;
     int64_t *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
-    if (g.has_core) u[0] += g.req[0];
-    u[1] += g.req[1];
-    u[2] += g.req[2];
+    for (int q = 0; q < 3; q++) u[q] += g.req[KO_T_GPU][q];
   }
-  return mask;
+  for (int k = 0; k < KO_RDMA; k++)
+    if ((m[1] >> k) & 1u) s->dv.rused[(size_t)n * KO_RDMA + k] += g.req[KO_T_RDMA][0];
+  *gpu_minors = m[0];
+  *rdma_minors = m[1];
 }
 
 /* NodeInfo.AddPod (upstream) + podAssignCache.assign (pod_assign_cache.go:53) */
@@ -1311,9 +1582,7 @@ void ko_destroy(ko_sched *s) {
   free(s->rraw);
   free(s->rord);
   free(s->draw);
-  free(s->dv.flags);
-  free(s->dv.total);
-  free(s->dv.used);
+  dev_free(&s->dv);
   free(s->topos); free(s->topo_of); free(s->cpu_alloc); free(s->cpu_excl); free(s->cpu_resv); free(s->cpusets);
   free(s->numa_count); free(s->numa_alloc); free(s->numa_used); free(s->numa_present); free(s->numa_cs);
   ko_rsv *rv = &s->rv;
@@ -1439,14 +1708,28 @@ int ko_fetch_cpusets(const ko_sched *s, uint64_t *out, int32_t p) {
 
 int ko_load_devices(ko_sched *s, const ks_device_cols *dc) {
   size_t nn = (size_t)(s->n > 0 ? s->n : 1);
-  free(s->dv.flags);
-  free(s->dv.total);
-  free(s->dv.used);
+  dev_free(&s->dv);
   s->dv.flags = (uint32_t *)calloc(nn, 4);
   s->dv.total = (int64_t *)calloc(nn * KO_GPUS * 3, 8);
   s->dv.used = (int64_t *)calloc(nn * KO_GPUS * 3, 8);
+  s->dv.rtotal = (int64_t *)calloc(nn * KO_RDMA, 8);
+  s->dv.rused = (int64_t *)calloc(nn * KO_RDMA, 8);
+  s->dv.gpcie = (uint8_t *)calloc(nn * KO_GPUS, 1);
+  s->dv.rpcie = (uint8_t *)calloc(nn * KO_RDMA, 1);
+  s->dv.pnuma = (uint8_t *)calloc(nn * KO_PCIE, 1);
+  s->dv.psock = (uint8_t *)calloc(nn * KO_PCIE, 1);
   for (int64_t n = 0; n < s->n; n++) {
     s->dv.flags[n] = colvu32(dc->flags, n);
+    for (int k = 0; k < KO_RDMA; k++) {
+      s->dv.rtotal[(size_t)n * KO_RDMA + k] = colv64(dc->total_rdma[k], n);
+      s->dv.rused[(size_t)n * KO_RDMA + k] = colv64(dc->used_rdma[k], n);
+      s->dv.rpcie[(size_t)n * KO_RDMA + k] = dc->rdma_pcie[k] ? dc->rdma_pcie[k][n] : KS_PCIE_NONE;
+    }
+    for (int k = 0; k < KO_GPUS; k++) s->dv.gpcie[(size_t)n * KO_GPUS + k] = dc->gpu_pcie[k] ? dc->gpu_pcie[k][n] : KS_PCIE_NONE;
+    for (int k = 0; k < KO_PCIE; k++) {
+      s->dv.pnuma[(size_t)n * KO_PCIE + k] = dc->pcie_numa[k] ? dc->pcie_numa[k][n] : 0;
+      s->dv.psock[(size_t)n * KO_PCIE + k] = dc->pcie_socket[k] ? dc->pcie_socket[k][n] : 0;
+    }
     for (int k = 0; k < KO_GPUS; k++) {
       int64_t *t = s->dv.total + ((size_t)n * KO_GPUS + k) * 3, *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
       t[0] = colv64(dc->total_core[k], n);
@@ -1471,6 +1754,13 @@ int ko_read_devices(const ko_sched *s, int64_t *used_core, int64_t *used_memory,
       if (used_memory) used_memory[o] = u ? u[1] : 0;
       if (used_ratio) used_ratio[o] = u ? u[2] : 0;
     }
+  return 0;
+}
+
+/* RDMA used amounts, [k*n + node] per minor k */
+int ko_read_devices_rdma(const ko_sched *s, int64_t *used_rdma) {
+  for (int64_t n = 0; n < s->n; n++)
+    for (int k = 0; k < KO_RDMA; k++) used_rdma[(size_t)k * s->n + n] = s->dv.rused ? s->dv.rused[(size_t)n * KO_RDMA + k] : 0;
   return 0;
 }
 
@@ -1683,6 +1973,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     out[i].score = 0;
     out[i].reservation = -1;
     out[i].gpu_minors = 0;
+    out[i].rdma_minors = 0;
     out[i].status = quota_prefilter(s, &p);
     if (out[i].status) continue;
     sweep_arg a = {s, &p};
@@ -1713,7 +2004,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
       out[i].reservation = s->nom[best_n];
       rsv_reserve(s, &p, s->nom[best_n]);
     }
-    out[i].gpu_minors = dev_reserve(s, &p, best_n);
+    dev_reserve(s, &p, best_n, &out[i].gpu_minors, &out[i].rdma_minors);
     numa_reserve(s, &p, best_n);
     node_reserve(s, &p, best_n);
     quota_reserve(s, &p);

@@ -43,6 +43,7 @@ def lib():
         L.ko_read_reservations.argtypes = [C.c_void_p, abi.P64, abi.P32]
         L.ko_load_devices.argtypes = [C.c_void_p, C.POINTER(abi.KsDeviceCols)]
         L.ko_read_devices.argtypes = [C.c_void_p, abi.P64, abi.P64, abi.P64]
+        L.ko_read_devices_rdma.argtypes = [C.c_void_p, abi.P64]
         L.ko_load_cpu_state.argtypes = [C.c_void_p, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
         L.ko_read_cpu_state.argtypes = [C.c_void_p, abi.PU64, abi.PU64, abi.PU64]
         L.ko_fetch_cpusets.argtypes = [C.c_void_p, abi.PU64, C.c_int32]
@@ -163,7 +164,8 @@ class Oracle:
         self.L.ko_schedule(self.h, C.byref(cols), pods.n, out)
         arr = np.frombuffer(out, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS), count=pods.n)
         return {"node": arr["node"].copy(), "status": arr["status"].copy(), "score": arr["score"].copy(),
-                "reservation": arr["reservation"].copy(), "gpu_minors": arr["gpu_minors"].copy()}
+                "reservation": arr["reservation"].copy(), "gpu_minors": arr["gpu_minors"].copy(),
+                "rdma_minors": arr["rdma_minors"].copy()}
 
     def eval_pod(self, pod: PodTable):
         reasons = np.zeros(self.n, np.uint32)
@@ -190,7 +192,10 @@ class Oracle:
         G = abi.KS_MAX_GPUS
         out = [np.zeros(G * max(self.n, 1), np.int64) for _ in range(3)]
         self.L.ko_read_devices(self.h, *[o.ctypes.data_as(abi.P64) for o in out])
-        return tuple(o[: G * self.n].reshape(G, self.n) for o in out)
+        R = abi.KS_MAX_RDMA
+        r = np.zeros(R * max(self.n, 1), np.int64)
+        self.L.ko_read_devices_rdma(self.h, r.ctypes.data_as(abi.P64))
+        return tuple(o[: G * self.n].reshape(G, self.n) for o in out) + (r[: R * self.n].reshape(R, self.n),)
 
     def read_numa_nodes(self):
         K = abi.KS_MAX_NUMA

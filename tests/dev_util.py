@@ -55,3 +55,51 @@ def gpu_pod(core, ratio=0, memory=0):
 def dev_only(strategy="LeastAllocated"):
     return SchedulerProfile(fit=None, loadaware=None,
                             deviceshare=DeviceShareArgs(strategy=strategy, resources={GPU_MEMORY_RATIO: 1})).to_ks_config()
+
+
+J = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "deviceshare_joint.json")))
+
+
+def joint_devices(c, n=1):
+    """The TestAutopilotAllocator device CR of case c on n identical nodes (ks_device_cols incl. RDMA and
+    the PCIe / NUMA topology), with the case's assigned devices as used amounts."""
+    t = J["topologies"][c["topology"]]
+    gpu = J["gpu"]
+    d = DeviceTable(n)
+    d.flags[:] = abi.KS_DEV_PRESENT
+    for k in range(8):
+        d.total_core[k], d.total_memory[k], d.total_ratio[k] = gpu["core"], gpu["memory"], gpu["ratio"]
+        d.gpu_pcie[k] = t["gpu_pcie"][k]
+    for m, pc in zip(t["rdma_minors"], t["rdma_pcie"]):
+        d.total_rdma[m] = J["rdma_total"]
+        d.rdma_pcie[m] = pc
+    for p, (nu, so) in enumerate(zip(t["pcie_numa"], t["pcie_socket"])):
+        d.pcie_numa[p], d.pcie_socket[p] = nu, so
+    a = c.get("assigned") or {}
+    for k in a.get("gpu", []):
+        d.used_core[k], d.used_memory[k], d.used_ratio[k] = gpu["core"], gpu["memory"], gpu["ratio"]
+    for m, v in a.get("rdma", {}).items():
+        d.used_rdma[int(m)] = v
+    return d
+
+
+def joint_pod(gpus, rdma=1, joint=abi.KS_JOINT_GPU_RDMA):
+    p = gpu_pod(100 * gpus, 100 * gpus) if gpus else gpu_pod(0)
+    p.rdma[:] = rdma
+    p.joint[:] = joint if gpus else abi.KS_JOINT_NONE
+    return p
+
+
+def dev_default():
+    """DeviceShareArgs after the v1beta2 defaults: LeastAllocated over gpu-memory-ratio, rdma, fpga (weight 1)"""
+    return SchedulerProfile(fit=None, loadaware=None, deviceshare=DeviceShareArgs()).to_ks_config()
+
+
+def dev_zero_weights():
+    """allocator.scorer == nil in TestAutopilotAllocator: every device score is 0"""
+    return SchedulerProfile(fit=None, loadaware=None,
+                            deviceshare=DeviceShareArgs(resources={GPU_MEMORY_RATIO: 0})).to_ks_config()
+
+
+def minors(mask, k=8):
+    return [i for i in range(k) if (int(mask) >> i) & 1]

@@ -21,7 +21,7 @@ def test_allocate_minor(c):
     res = o.schedule(gpu_pod(c["pod"]["core"], c["pod"]["ratio"]))
     assert res["node"][0] == 0
     assert [k for k in range(abi.KS_MAX_GPUS) if (int(res["gpu_minors"][0]) >> k) & 1] == c["want_minors"]
-    uc, um, ur = o.read_devices()
+    uc, um, ur, _ = o.read_devices()
     k = c["want_minors"][0]
     before = alloc_devices(c)
     assert uc[k, 0] - before.used_core[k, 0] == 50 and ur[k, 0] - before.used_ratio[k, 0] == 50

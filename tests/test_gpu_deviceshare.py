@@ -53,7 +53,8 @@ def check(runtime, oracle_lib, p, nodes, pods, devs, rs=None, label=""):
     assert np.array_equal(got["gpu_minors"], want["gpu_minors"]), f"{label}: allocated minors differ"
     assert np.array_equal(got["reservation"], want["reservation"]), label
     assert_same_state(ev.read_nodes(), orc.read_nodes(), label)
-    for g, w, name in zip(ev.read_devices(), orc.read_devices(), ("core", "memory", "ratio")):
+    assert np.array_equal(got["rdma_minors"], want["rdma_minors"]), f"{label}: allocated RDMA minors differ"
+    for g, w, name in zip(ev.read_devices(), orc.read_devices(), ("core", "memory", "ratio", "rdma")):
         assert np.array_equal(g, w), f"{label}: device used {name} differs"
     st = ev.stats()
     ev.close()
