@@ -230,8 +230,9 @@ def main():
             local_nodes = n_nodes // (world if args.shard else 1)  # one rank sweeps its shard
             algo = local_nodes * b_node + 64 * 128 + ((local_nodes + 63) // 64) * 64 * 4
             if w.devices is not None:
-                # + NUMA amplification columns (16 B) and the GPU table (flags + 2 x 3 x 8 int64)
-                algo += local_nodes * (16 + 4 + 2 * 3 * 8 * 8)
+                # + NUMA amplification columns (16 B) and the device table (flags + 34 total / topology words +
+                # 32 used words, int64; ks_dev.h)
+                algo += local_nodes * (16 + 4 + (34 + 32) * 8)
             if w.reservations is not None:
                 # + the owner-class column and the reservation table (CSR offsets, classes, meta, order rank,
                 # allocatable/allocated x7, assigned, reserve-pod non-zero x2) read once
