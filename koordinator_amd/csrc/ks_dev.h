@@ -146,11 +146,13 @@ struct DevOut {
   uint32_t rminors;  // RDMA allocation (ALLOC only)
 };
 
-// per-type state of one node for one pod: fitting minors, per-minor scores, switches
+// per-type state of one node for one pod, packed to keep the sweep's register footprint small
 struct DevType {
-  uint32_t fit;       // minors with non-zero free that satisfy the request per instance
-  int32_t sc[8];      // scoreDevice (only with scores)
-  uint32_t pcie[8];   // switch of each minor (0xF = none)
+  uint32_t fit;  // minors with non-zero free that satisfy the request per instance
+  uint32_t pcw;  // 4-bit switch of each minor (0xF = none)
+  uint64_t sc;   // 8-bit scoreDevice of each minor (only with scores; <= 100)
+  __device__ __forceinline__ uint32_t pcie(int k) const { return (pcw >> (4 * k)) & 0xFu; }
+  __device__ __forceinline__ int score(int k) const { return (int)((sc >> (8 * k)) & 0xFFu); }
 };
 
 // defaultAllocateDevices over the fitting minors in `sub`: up to maxd minors in (preferred switch, score desc,
@@ -170,7 +172,8 @@ __device__ __forceinline__ uint32_t dev_take(const DevType& t, int nm, uint32_t 
     for (int k = 0; k < 8; ++k) {
       if (k >= nm) break;
       const bool ok = ((cand >> k) & 1u) && !((mask >> k) & 1u);
-      const int key = ((t.pcie[k] < 8u && ((pref >> t.pcie[k]) & 1u)) ? (1 << 12) : 0) | (t.sc[k] << 4) | (15 - k);
+      const uint32_t pc = t.pcie(k);
+      const int key = ((pc < 8u && ((pref >> pc) & 1u)) ? (1 << 12) : 0) | (t.score(k) << 4) | (15 - k);
       best = (ok && key > bk) ? k : best;
       bk = (ok && key > bk) ? key : bk;
     }
@@ -185,7 +188,7 @@ __device__ __forceinline__ uint32_t dev_pcies_of(const DevType& t, int nm, uint3
   uint32_t p = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k)
-    if (k < nm && ((mask >> k) & 1u) && t.pcie[k] < 8u) p |= 1u << t.pcie[k];
+    if (k < nm && ((mask >> k) & 1u) && t.pcie(k) < 8u) p |= 1u << t.pcie(k);
   return p;
 }
 
@@ -193,7 +196,7 @@ __device__ __forceinline__ uint32_t dev_sub_of(const DevType& t, int nm, uint32_
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k)
-    if (k < nm && t.pcie[k] < 8u && ((pcies >> t.pcie[k]) & 1u)) s |= 1u << k;
+    if (k < nm && t.pcie(k) < 8u && ((pcies >> t.pcie(k)) & 1u)) s |= 1u << k;
   return s;
 }
 
@@ -218,8 +221,8 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
   uint32_t exist = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    exist |= G.pcie[k] < 8u ? (1u << G.pcie[k]) : 0u;
-    exist |= R.pcie[k] < 8u ? (1u << R.pcie[k]) : 0u;
+    exist |= G.pcie(k) < 8u ? (1u << G.pcie(k)) : 0u;
+    exist |= R.pcie(k) < 8u ? (1u << R.pcie(k)) : 0u;
   }
   // per switch: preferred = a fitting RDMA instance on it (freeDevices[rdma] of the last joint type)
   uint32_t swpref = 0;
@@ -281,10 +284,18 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   if (o.reasons) return o;
   const bool has_gpu = (p.flags & kPodGpuReq) != 0, has_rdma = p.rdma > 0;
   const bool joint = has_gpu && has_rdma && p.joint != KS_JOINT_NONE;
-  const bool scores = ALLOC || joint;
-  const uint64_t topo = (joint || ALLOC) ? (uint64_t)v.tot(kDevTopoW) : 0ull;
+  const bool same = p.joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
+  // A best-effort joint pod asking for one RDMA device is feasible iff the per-type counts are: a joint
+  // success takes >= desired GPUs and one RDMA device, a joint failure falls back to allocateDevices.  Only
+  // the allocation itself (Reserve) needs the walk then.
+  const bool walk = joint && (ALLOC || same || g.rdesired > 1);
+  const bool scores = ALLOC || walk;
+  const uint64_t topo = (walk || ALLOC) ? (uint64_t)v.tot(kDevTopoW) : 0ull;
   DevType G, R;
   G.fit = R.fit = 0;
+  G.sc = R.sc = 0;
+  G.pcw = (uint32_t)topo;
+  R.pcw = (uint32_t)(topo >> 32);
   int32_t raw = 0;
   if (has_gpu) {
     const int64_t pod[3] = {g.core, g.mem, g.ratio};
@@ -303,8 +314,7 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
         fsum[q] += exists ? f[q] : 0;
       }
       G.fit |= fits ? (1u << k) : 0u;
-      G.sc[k] = (scores && fits) ? dev_score3(c, t, f, pod) : 0;
-      G.pcie[k] = (uint32_t)(topo >> (4 * k)) & 0xFu;
+      if (scores && fits) G.sc |= (uint64_t)dev_score3(c, t, f, pod) << (8 * k);
     }
     raw += dev_score3(c, tsum, fsum, pod);
   }
@@ -318,15 +328,13 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
       fsum += f;
       const bool fits = t != 0 && f != 0 && g.rdma <= f;
       R.fit |= fits ? (1u << j) : 0u;
-      R.sc[j] = (scores && fits) ? dev_score1(c, t, f, g.rdma) : 0;
-      R.pcie[j] = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
+      if (scores && fits) R.sc |= (uint64_t)dev_score1(c, t, f, g.rdma) << (8 * j);
     }
     raw += dev_score1(c, tsum, fsum, g.rdma);
   }
   uint32_t om = 0, orm = 0;
   bool jdone = false;
-  if (joint) {
-    const bool same = p.joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
+  if (walk) {
     if (dev_by_topology(G, R, g, same, (uint64_t)v.tot(kDevMetaW), om, orm)) {
       // validateJointAllocation (device_allocator.go:255-284)
       if (same && dev_pcies_of(G, kGpus, om) != dev_pcies_of(R, kRdma, orm)) {
