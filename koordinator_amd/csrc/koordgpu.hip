@@ -824,9 +824,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   constexpr bool DEV = (FEAT & 4) != 0;
   constexpr int DW = kDevTW;   // int64 words of one slot's device totals + topology (ks_dev.h)
   constexpr int DU = kDevQW;   // int64 words of its used amounts
+  // word-major [w][kDevLdsStride] (slot s at column s): the slot-parallel reads (lane = slot) are
+  // bank-conflict free, the lane = word row fills hit distinct bank pairs
   int64_t* sdev_tot = reinterpret_cast<int64_t*>(smem_raw + lay.sdev);
-  int64_t* sdev_use = sdev_tot + kMaxBatch * DW;
-  int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kMaxBatch * DU);
+  int64_t* sdev_use = sdev_tot + kDevLdsStride * DW;
+  int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kDevLdsStride * DU);
   int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -972,7 +974,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   uint32_t st_next = 0;
   Cands cn{};
   auto lookahead = [&](int32_t j) {
-    const uint64_t top = monotone ? readlane64(my_top, j) : 0ull;
+    // the fast path also holds for a pod without device requests when only DeviceShare's normalization
+    // max made the profile non-monotone (its DeviceShare score is 0 on every node)
+    const bool mono = monotone || (cfg.monotone_nd && !(__builtin_amdgcn_readlane(my_flags, j) & kPodHasGpu));
+    const uint64_t top = mono ? readlane64(my_top, j) : 0ull;
     const int32_t tn = top ? (int32_t)gkey_node(top) : 0;
     if (QC) {
       // every LDS read of the admission and of the fast check issued together (one latency)
@@ -1065,7 +1070,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
               if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
               return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
             },
-            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane * DW, sdev_use + lane * DU, sdev_pres[lane] != 0}); });
+            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}); });
         numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
         feas = o.reasons == 0;
       }
@@ -1188,9 +1193,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         if (lane < DW) v = gld(dv.total + (int64_t)lane * dv.npad + node);
         else if (lane == DW) v = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
         if (lane < DU) w = gld(dv.used + (int64_t)lane * dv.npad + node);
-        if (lane < DW) sdev_tot[s * DW + lane] = v;
+        if (lane < DW) sdev_tot[lane * kDevLdsStride + s] = v;
         else if (lane == DW) sdev_pres[s] = (int32_t)v;
-        if (lane < DU) sdev_use[s * DU + lane] = w;
+        if (lane < DU) sdev_use[lane * kDevLdsStride + s] = w;
       }
       if (RSV && cfg.rsv) {
         // the node's reservations into LDS (lane = record word), unless too many or too wide
@@ -1279,7 +1284,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
         fitla_pref = e2.total;
         if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
-          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DU, sdev_pres[s] != 0});
+          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0});
           fitla_pref += cfg.dev_pw * (Muse == 0 ? dd.raw : small_div(100 * dd.raw, Muse));
         }
       }
@@ -1342,7 +1347,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       PodRec pod = spods[j];
       pod.flags = pflags;
       GpuReq g;
-      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s * DW, sdev_use + s * DU, sdev_pres[s] != 0}, &g);
+      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g);
       gminors = __builtin_amdgcn_readfirstlane(dd.minors);
       rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
       // used word `lane`: GPU (q, k) for lane < 3 * kGpus, RDMA j = lane - kDevRdmaW after
@@ -1352,8 +1357,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       if (lane < DU && ((m >> k) & 1u)) {
         const int q = lane / kGpus;
         const int64_t add = !is_gpu ? g.rdma : (q == 0 ? g.core : (q == 1 ? g.mem : g.ratio));
-        const int64_t nv = sdev_use[s * DU + lane] + add;
-        sdev_use[s * DU + lane] = nv;
+        const int64_t nv = sdev_use[lane * kDevLdsStride + s] + add;
+        sdev_use[lane * kDevLdsStride + s] = nv;
         gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
       }
     }
@@ -1964,12 +1969,14 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.dw_ratio = (int32_t)c.deviceshare.weight_gpu_memory_ratio;
   k.dw_rdma = (int32_t)c.deviceshare.weight_rdma;
   k.dev_pw = c.deviceshare.enable ? (int32_t)c.deviceshare.plugin_weight : 0;
+  k.monotone_nd = k.monotone;
   if (k.dev) k.monotone = 0;  // a commit changes the pod's DeviceShare normalization max
   k.rsv = c.reservation.enable ? 1 : 0;
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
                              (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw) + 1);
   // a commit into a reservation can raise that node's Reservation score for later pods
   if (k.rsv) k.monotone = 0;
+  if (k.rsv) k.monotone_nd = 0;
   return k;
 }
 
@@ -2376,6 +2383,7 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
     if (numa_install(ctx, nullptr, nullptr, nullptr) != KS_OK) return KS_EHIP;
     ctx->kc.numa_pol = 1;
     ctx->kc.monotone = 0;  // a Reserve can move a node's best NUMA hint: keys are not monotone
+    ctx->kc.monotone_nd = 0;
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
@@ -3366,7 +3374,7 @@ static int kernel_feat(const ks_ctx* ctx) {
 }
 
 static size_t dev_cache_bytes(const ks_ctx* ctx) {
-  return ctx->kc.dev ? (size_t)kMaxBatch * ((kDevTW + kDevQW) * 8 + 4) : 0;
+  return ctx->kc.dev ? (size_t)kDevLdsStride * (kDevTW + kDevQW) * 8 + (size_t)kMaxBatch * 4 : 0;
 }
 
 static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {

@@ -45,7 +45,7 @@ struct DevDev {
   int64_t npad;
 };
 
-// views of one node's devices: HBM columns or the commit kernel's LDS copy (tot[kDevTW], use[kDevQW])
+// views of one node's devices: HBM columns or the commit kernel's LDS copy
 struct DevGView {
   const DevDev& d;
   int64_t n;
@@ -54,13 +54,16 @@ struct DevGView {
   __device__ __forceinline__ int64_t use(int w) const { return gld(d.used + (int64_t)w * d.npad + n); }
 };
 
+// LDS slot copies are word-major with this row stride (an odd multiple of 8 B: conflict-free lane = slot reads)
+constexpr int kDevLdsStride = kMaxBatch + 1;
+
 struct DevLView {
-  const int64_t* t;  // [kDevTW]
-  const int64_t* u;  // [kDevQW]
+  const int64_t* t;  // word w at t[w * kDevLdsStride]  (kDevTW words)
+  const int64_t* u;  // (kDevQW words)
   bool pres;
   __device__ __forceinline__ bool present() const { return pres; }
-  __device__ __forceinline__ int64_t tot(int w) const { return t[w]; }
-  __device__ __forceinline__ int64_t use(int w) const { return u[w]; }
+  __device__ __forceinline__ int64_t tot(int w) const { return t[w * kDevLdsStride]; }
+  __device__ __forceinline__ int64_t use(int w) const { return u[w * kDevLdsStride]; }
 };
 
 // The pod's request per instance and desired count per device type on one node.

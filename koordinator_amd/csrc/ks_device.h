@@ -65,6 +65,7 @@ struct Cfg {
   int32_t numa_pol;  // nodes with a NUMA topology policy exist (ks_numa.h)
   int32_t numa_sc_most;  // NUMAScoringStrategy MostAllocated (hint scores)
   int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw, dw_rdma;  // DeviceShare (GPU, RDMA)
+  int32_t monotone_nd;  // monotone for pods without device requests (DeviceShare skips them: no normalization max)
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
