@@ -224,9 +224,10 @@ def main():
         roofline = None
         if agg["sweep_launches"]:
             avg_s = agg["sweep_ms"] / agg["sweep_launches"] / 1000.0
-            # algorithmic bytes per sweep launch: every node column the enabled plugins read, once
-            # (B_node), + the pass's pod records + the chunk-maxima output
-            b_node = 8 * 15 + 4 * 3 + 16 * 2  # LA+Fit columns + batch-cpu/batch-memory scalar columns
+            # algorithmic bytes per sweep launch: SURVEY §8(d)'s B_node (LoadAware + Fit columns, each read
+            # once per pass: 106 B, +16 B with the prod-usage score term, +32 B for the batch-cpu / batch-memory
+            # scalar columns) x the nodes one launch sweeps, + the pass's pod records + the chunk-maxima output
+            b_node = 106 + (16 if prof.loadaware is not None and prof.loadaware.score_according_prod_usage else 0) + 32
             local_nodes = n_nodes // (world if args.shard else 1)  # one rank sweeps its shard
             algo = local_nodes * b_node + 64 * 128 + ((local_nodes + 63) // 64) * 64 * 4
             if w.devices is not None:
