@@ -580,6 +580,10 @@ int ks_eval_pod_debug(ks_ctx *ctx, const ks_pod_cols *pod, uint32_t *reasons, in
 int ks_read_nodes(ks_ctx *ctx, ks_node_state *out);
 int ks_read_quota_used(ks_ctx *ctx, int64_t *used /* q*KS_QUOTA_DIMS, row-major */);
 int ks_get_stats(const ks_ctx *ctx, ks_stats *out);
+/* Turn the per-kernel HIP-event bracketing (ks_config.profile) on or off for later calls: the events
+ * add dispatch gaps between the pass kernels, so throughput is timed with them off and the kernel split
+ * from separate profiled calls. */
+int ks_set_profile(ks_ctx *ctx, int32_t on);
 
 /* Node sharding over GPUs (one process per GPU).  The node table stays replicated
  * (every rank applies the same commits); shard s = rank * virtual_shards + v sweeps and selects

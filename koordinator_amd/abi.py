@@ -409,6 +409,7 @@ EXPORTED_SYMBOLS = [
     "ks_read_nodes",
     "ks_read_quota_used",
     "ks_get_stats",
+    "ks_set_profile",
     "ks_shard_unique_id",
     "ks_shard_init",
 ]

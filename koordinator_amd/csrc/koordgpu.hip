@@ -3874,3 +3874,9 @@ int ks_get_stats(const ks_ctx* ctx, ks_stats* out) {
   return KS_OK;
 }
 
+int ks_set_profile(ks_ctx* ctx, int32_t on) {
+  if (!ctx) return KS_EINVAL;
+  ctx->cfg.profile = on ? 1 : 0;
+  return KS_OK;
+}
+

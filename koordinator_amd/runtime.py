@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
     L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
     L.ks_read_quota_used.argtypes = [vp, abi.P64]
     L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
+    L.ks_set_profile.argtypes = [vp, C.c_int32]
     L.ks_shard_unique_id.argtypes = [C.POINTER(C.c_uint8)]
     L.ks_shard_init.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32]
     for name in abi.EXPORTED_SYMBOLS:
@@ -289,6 +290,9 @@ class Evaluator:
         used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)
         self._chk(self.L.ks_read_quota_used(self.h, used.ctypes.data_as(abi.P64)))
         return used[: self.nq * abi.KS_QUOTA_DIMS].reshape(self.nq, abi.KS_QUOTA_DIMS)
+
+    def set_profile(self, on: bool):
+        self._chk(self.L.ks_set_profile(self.h, 1 if on else 0))
 
     def stats(self) -> dict:
         s = abi.KsStats()
