@@ -182,6 +182,10 @@ struct SweepArgs {
   const DevNuma* __restrict__ nv;
   unsigned long long* dev_M;  // [64] DeviceShare: (max raw << 32) | ~witness node per pod of the pass
   int32_t phase;              // 0: reduce dev_M only (DeviceShare), 1: chunk keys
+  // DeviceShare without Reservation: phase 0 keeps each (pod, node)'s (feasible, Fit + LoadAware + NUMA
+  // total, DeviceShare raw) here and phase 1 only applies the normalization ([64][dstride]); NULL = re-evaluate
+  unsigned long long* dcache;
+  int64_t dstride;
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
@@ -212,6 +216,24 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
     const int64_t c = a.c0 + w / groups;
     const int32_t g = (int32_t)(w - c * groups);
     const int64_t node = c * 64 + lane;
+    if ((FEAT & 4) && a.phase == 1 && a.dcache) {
+      const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
+      uint32_t best = 0, second = 0;
+      for (int32_t p = p0; p < p1; ++p) {
+        const unsigned long long e = a.dcache[(size_t)p * a.dstride + node];
+        EvalOut o{};
+        o.total = (int32_t)(uint32_t)e;
+        o.dev_raw = (int32_t)((e >> 32) & 0xFFFFull);
+        const int32_t M = (int32_t)(a.dev_M[p] >> 32);
+        const uint32_t key = (e >> 63) ? (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane)) : 0u;
+        const uint32_t m1 = wave_max_u32(key);
+        const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
+        best = (lane == p) ? m1 : best;
+        second = (lane == p) ? m2 : second;
+      }
+      if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
+      continue;
+    }
     NodeReg<NSC> r;
     {
       const DevNodes d = *a.dn;
@@ -230,6 +252,10 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
         const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | (0xFFFFFFFFull - (uint64_t)node));
         const uint64_t m = wave_max_u64(mk);
         if (lane == 0 && m) atomicMax(a.dev_M + p, (unsigned long long)m);
+        if (a.dcache)
+          a.dcache[(size_t)p * a.dstride + node] =
+              (node < a.n && !o.reasons) ? ((1ull << 63) | ((unsigned long long)(uint32_t)o.dev_raw << 32) | (uint32_t)o.total)
+                                         : 0ull;
         continue;
       }
       const int32_t M = (FEAT & 4) ? (int32_t)(a.dev_M[p] >> 32) : 0;
@@ -1881,6 +1907,8 @@ struct ks_ctx {
   bool dev_loaded = false;
   int64_t* dev_used_ckpt = nullptr;
   unsigned long long* dev_M = nullptr;  // [64] per pass
+  unsigned long long* dcache = nullptr;  // [64][npad] DeviceShare phase-0 results (SweepArgs.dcache)
+  int64_t dcache_words = 0;
   // NodeNUMAResource cpusets (ks_cpuset.h)
   void* cpu_blob = nullptr;
   DevCpu cpu{};
@@ -2122,6 +2150,7 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->ddv; dev_free(p);
   dev_free(ctx->dev_blob);
   p = ctx->dev_M; dev_free(p);
+  p = ctx->dcache; dev_free(p);
   dev_free(ctx->cpu_blob);
   p = ctx->cpuset_list; dev_free(p);
   dev_free(ctx->numa_blob);
@@ -3427,6 +3456,8 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.dv = ctx->ddv;
   sa.nv = ctx->dnv;
   sa.dev_M = ctx->dev_M;
+  sa.dcache = (ctx->kc.dev && !ctx->kc.rsv && ctx->dcache_words >= (int64_t)kMaxBatch * ctx->npad) ? ctx->dcache : nullptr;
+  sa.dstride = ctx->npad;
   sa.phase = 1;
   if (feat == 7 || feat == 15) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
@@ -3593,6 +3624,15 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
     e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_smem);
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(select LDS %zu): %s", sel_smem, hipGetErrorString(e));
+    if (ctx->kc.dev && !ctx->kc.rsv && ctx->dcache_words < (int64_t)kMaxBatch * ctx->npad) {
+      void* q = ctx->dcache;
+      dev_free(q);
+      ctx->dcache = nullptr;
+      ctx->dcache_words = 0;
+      if (dev_alloc(ctx, &q, (size_t)kMaxBatch * ctx->npad * 8) != KS_OK) return KS_ENOMEM;
+      ctx->dcache = (unsigned long long*)q;
+      ctx->dcache_words = (int64_t)kMaxBatch * ctx->npad;
+    }
     const size_t gb = (size_t)ctx->nranks * ctx->vshards * cand_slot_layout(ctx->k).bytes;
     if (ctx->nranks * ctx->vshards > 1 && ctx->gather_bytes < gb) {
       void* g = ctx->gather;
