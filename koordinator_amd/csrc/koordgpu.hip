@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -34,6 +35,12 @@
 #include "ks_numa.h"
 
 using namespace ks;
+
+// Launch-shape overrides for tuning runs (tools/sweep_shape.sh); unset = the built-in heuristic.
+static int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::strtoll(v, nullptr, 10) : dflt;
+}
 
 // ------------------------------------------------------------------------------------------
 // prep kernels
@@ -3647,11 +3654,15 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   // pods per wave: aim for >= ~4096 waves per sweep
   const int64_t S = (int64_t)ctx->nranks * ctx->vshards;
   const int64_t local_chunks = ctx->nchunks * (ctx->rank + 1) * ctx->vshards / S - ctx->nchunks * ctx->rank * ctx->vshards / S;
+  static const int64_t env_waves = env_i64("KS_SWEEP_WAVES", 4096);
+  static const int64_t env_ppw = env_i64("KS_SWEEP_PPW", 0);
+  static const int64_t env_cap = env_i64("KS_SWEEP_BLOCK_CAP", 2048);
   int32_t ppw = 64;
-  while (ppw > 4 && local_chunks * (ctx->batch / ppw) < 4096) ppw >>= 1;
+  while (ppw > 4 && local_chunks * (ctx->batch / ppw) < env_waves) ppw >>= 1;
+  if (env_ppw > 0) ppw = (int32_t)env_ppw;
   if (ppw > ctx->batch) ppw = ctx->batch;
   const int64_t nwork = std::max<int64_t>(local_chunks, 1) * ((ctx->batch + ppw - 1) / ppw);
-  const int sweep_blocks = (int)((std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, 2048)) + 7) & ~7ll);  // % 8 == 0 (XCD swizzle)
+  const int sweep_blocks = (int)((std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, env_cap)) + 7) & ~7ll);  // % 8 == 0 (XCD swizzle)
   if (ctx->cfg.numa.enable && ctx->cpuset_cap < np) {
     // (pod, node) list + its count + the per-pod CPU sets of this call
     void* p = ctx->cpuset_list;
