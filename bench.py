@@ -77,6 +77,28 @@ def pmc_traffic(config: str, kernel: str):
     return round(b / n), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
 
 
+def pmc_valu(config: str, kernel: str):
+    """VALU-issue floor per launch of `kernel` (us) from the newest committed PMC summary for this
+    config (profiles/rNN_<config>_valu.json, tools/pmc_valu.sh + tools/valu.py: SQ_INSTS_VALU x 2 cycles
+    over 1024 SIMDs at 2.4 GHz); None when absent."""
+    import glob
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_{config}_valu.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    n = us = 0.0
+    for k, v in t.get("kernels", {}).items():
+        if kernel in k and "valu_issue_floor_us" in v:
+            n += v["launches"]
+            us += v["valu_issue_floor_us"] * v["launches"]
+    if not n:
+        return None, None
+    return us / n, os.path.relpath(files[-1], here)
+
+
 def cpu_baseline(w, gpu_res, budget_s: float):
     """Time the CPU oracle (port of the reference loop) on a bounded prefix of the workload."""
     from oracle.oracle import Oracle
@@ -262,6 +284,11 @@ def main():
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
                         "kernel": "sweep_kernel", "avg_launch_us": round(avg_s * 1e6, 3),
                         "algorithmic_bytes_per_launch": algo, "bytes_incl_pod_group_rereads": sweep_bytes}
+            floor_us, valu_src = pmc_valu(args.config, "sweep_kernel")
+            if floor_us is not None and world == 1:
+                # the sweep's instruction-issue bound next to the HBM one
+                roofline["valu_issue"] = {"floor_us": round(floor_us, 3),
+                                          "frac": round(floor_us / (avg_s * 1e6), 4), "source": valu_src}
         out = {
             "metric": "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k nodes",
             "value": round(value, 1),
