@@ -37,9 +37,18 @@
 using namespace ks;
 
 // Launch-shape overrides for tuning runs (tools/sweep_shape.sh); unset = the built-in heuristic.
-static int64_t env_i64(const char* name, int64_t dflt) {
+// A malformed or out-of-range value is reported on stderr and ignored (the default is used).
+static int64_t env_i64(const char* name, int64_t dflt, int64_t lo, int64_t hi) {
   const char* v = std::getenv(name);
-  return (v && *v) ? std::strtoll(v, nullptr, 10) : dflt;
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  const long long x = std::strtoll(v, &end, 10);
+  if (*end != '\0' || x < lo || x > hi) {
+    fprintf(stderr, "libkoordgpu: ignoring %s=%s (expected an integer in [%lld, %lld])\n", name, v, (long long)lo,
+            (long long)hi);
+    return dflt;
+  }
+  return (int64_t)x;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -220,8 +229,9 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const int32_t groups = (np + a.ppw - 1) / a.ppw;
   const int64_t nwork = (a.c1 - a.c0) * groups;
   for (int64_t w = wave; w < nwork; w += nwaves) {
-    const int64_t c = a.c0 + w / groups;
-    const int32_t g = (int32_t)(w - c * groups);
+    const int64_t lc = w / groups;  // chunk within this shard's range
+    const int64_t c = a.c0 + lc;
+    const int32_t g = (int32_t)(w - lc * groups);
     const int64_t node = c * 64 + lane;
     if ((FEAT & 4) && a.phase == 1 && a.dcache) {
       const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
@@ -3436,7 +3446,7 @@ static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
 }
 
 template <int NSC>
-static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
+static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
   auto rec = [&](int kind) {
     if (!evs) return;
     hipEvent_t e = take_event(ctx, *evn);
@@ -3466,29 +3476,39 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   sa.dcache = (ctx->kc.dev && !ctx->kc.rsv && ctx->dcache_words >= (int64_t)kMaxBatch * ctx->npad) ? ctx->dcache : nullptr;
   sa.dstride = ctx->npad;
   sa.phase = 1;
+  // One sweep launch per virtual shard (a rank's virtual shards are swept as separate chunk ranges, so the
+  // c0 > 0 decode of every non-first shard runs on one GPU too); timed together as one launch.
+  auto sweep = [&](auto kern) {
+    for (int32_t v = 0; v < ctx->vshards; ++v) {
+      const int32_t sh = ctx->rank * ctx->vshards + v;
+      sa.c0 = shard_lo(sh);
+      sa.c1 = shard_lo(sh + 1);
+      hipLaunchKernelGGL(kern, dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    }
+  };
   if (feat == 7 || feat == 15) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
     // each launch is timed on its own (the roofline is per sweep launch)
-    (void)hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream);
+    HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream));
     sa.phase = 0;
     rec(0);
-    hipLaunchKernelGGL(feat == 15 ? (sweep_kernel<NSC, 15>) : (sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    if (feat == 15) sweep(sweep_kernel<NSC, 15>);
+    else sweep(sweep_kernel<NSC, 7>);
     rec(0);
-    if (ctx->nranks > 1)
-      (void)ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ctx->stream);
+    if (ctx->nranks > 1) {
+      const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ctx->stream);
+      if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllReduce (DeviceShare max): %s", ncclGetErrorString(r));
+    }
     sa.phase = 1;
     rec(0);
-    hipLaunchKernelGGL(feat == 15 ? (sweep_kernel<NSC, 15>) : (sweep_kernel<NSC, 7>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    if (feat == 15) sweep(sweep_kernel<NSC, 15>);
+    else sweep(sweep_kernel<NSC, 7>);
   } else {
     rec(0);
-    if (feat == 11)
-      hipLaunchKernelGGL((sweep_kernel<NSC, 11>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
-    else if (feat == 3)
-      hipLaunchKernelGGL((sweep_kernel<NSC, 3>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
-    else if (feat == 1)
-      hipLaunchKernelGGL((sweep_kernel<NSC, 1>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
-    else
-      hipLaunchKernelGGL((sweep_kernel<NSC, 0>), dim3(sweep_blocks), dim3(256), 0, ctx->stream, sa);
+    if (feat == 11) sweep(sweep_kernel<NSC, 11>);
+    else if (feat == 3) sweep(sweep_kernel<NSC, 3>);
+    else if (feat == 1) sweep(sweep_kernel<NSC, 1>);
+    else sweep(sweep_kernel<NSC, 0>);
   }
   rec(0);
   SelectArgs se;
@@ -3527,7 +3547,9 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
     if (ctx->nranks > 1) {
       // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
       const size_t bytes = (size_t)ctx->vshards * L.bytes;
-      (void)ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, ctx->stream);
+      const ncclResult_t r =
+          ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, ctx->stream);
+      if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllGather (candidate slots): %s", ncclGetErrorString(r));
     }
     MergeArgs ma;
     ma.gather = ctx->gather;
@@ -3593,6 +3615,8 @@ static void launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<
   else KS_COMMIT(0);
 #undef KS_COMMIT
   rec(2);
+  HIPCHK(ctx, hipGetLastError());
+  return KS_OK;
 }
 
 static int schedule_staged_impl(ks_ctx* ctx) {
@@ -3654,9 +3678,9 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   // pods per wave: aim for >= ~4096 waves per sweep
   const int64_t S = (int64_t)ctx->nranks * ctx->vshards;
   const int64_t local_chunks = ctx->nchunks * (ctx->rank + 1) * ctx->vshards / S - ctx->nchunks * ctx->rank * ctx->vshards / S;
-  static const int64_t env_waves = env_i64("KS_SWEEP_WAVES", 4096);
-  static const int64_t env_ppw = env_i64("KS_SWEEP_PPW", 0);
-  static const int64_t env_cap = env_i64("KS_SWEEP_BLOCK_CAP", 2048);
+  static const int64_t env_waves = env_i64("KS_SWEEP_WAVES", 4096, 64, (int64_t)1 << 24);
+  static const int64_t env_ppw = env_i64("KS_SWEEP_PPW", 0, 1, kMaxBatch);
+  static const int64_t env_cap = env_i64("KS_SWEEP_BLOCK_CAP", 2048, 8, 65535 * 8);
   int32_t ppw = 64;
   while (ppw > 4 && local_chunks * (ctx->batch / ppw) < env_waves) ppw >>= 1;
   if (env_ppw > 0) ppw = (int32_t)env_ppw;
@@ -3692,11 +3716,13 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     const int32_t g = std::min<int32_t>((remaining + ctx->batch - 1) / ctx->batch, 256);
     for (int32_t i = 0; i < g; ++i) {
       auto* ev = ctx->cfg.profile ? &evs : nullptr;
+      int rc;
       switch (ctx->nsc) {
-        case 0: launch_pass<0>(ctx, ppw, sweep_blocks, ev, &evn); break;
-        case 2: launch_pass<2>(ctx, ppw, sweep_blocks, ev, &evn); break;
-        default: launch_pass<4>(ctx, ppw, sweep_blocks, ev, &evn); break;
+        case 0: rc = launch_pass<0>(ctx, ppw, sweep_blocks, ev, &evn); break;
+        case 2: rc = launch_pass<2>(ctx, ppw, sweep_blocks, ev, &evn); break;
+        default: rc = launch_pass<4>(ctx, ppw, sweep_blocks, ev, &evn); break;
       }
+      if (rc != KS_OK) return rc;
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(&host_cursor, ctx->cursor, 4, hipMemcpyDeviceToHost, ctx->stream));
