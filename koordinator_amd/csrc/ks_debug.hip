@@ -1,0 +1,51 @@
+// ks_debug.hip — ks_eval_pod_debug's per-node evaluation (every reason bit and per-plugin score of one pod on
+// every node, no Reserve), in its own translation unit.
+#include "ks_pass.h"
+#include "ks_debug.h"
+
+namespace ks {
+// ------------------------------------------------------------------------------------------
+// debug evaluation of one pod over every node (no Reserve)
+// ------------------------------------------------------------------------------------------
+
+template <int NSC>
+__global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n,
+                                  uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
+                                  int32_t* draw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  NodeReg<NSC> r;
+  load_node<NSC>(c, d, i, 1, r);
+  const PodRec p = *pod;
+  RsvOut ro;
+  EvalOut o = eval_full<NSC, true, false, 7>(
+      c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
+      [&]() { return dev_eval<false>(c, p, DevGView{*dv, i}); }, &ro);
+  numa_policy_fix<NSC, true, 15>(c, p, r, o, [&]() { return NumaGView{*nv, i}; });
+  reasons[i] = o.reasons;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
+  // Fit + LoadAware + NUMA part (the Reservation part is added by rsv_normalize_debug_kernel)
+  total[i] = o.reasons ? -1 : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw;
+  raw[i] = ro.raw;
+  hiord[i] = ro.hiord;
+  draw[i] = o.dev_raw;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
+}
+
+
+hipError_t launch_eval_debug(int nsc, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,
+                             const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
+                             int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw) {
+  if (nsc == 0)
+    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw);
+  else if (nsc == 2)
+    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw);
+  else
+    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw);
+  return hipGetLastError();
+}
+
+}  // namespace ks

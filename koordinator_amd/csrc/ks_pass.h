@@ -1,0 +1,1106 @@
+// ks_pass.h — the per-pass kernels that exist in one variant per plugin set (FEAT) and scalar-slot count
+// (NSC): the node sweep and the sequential commit.  Each FEAT is compiled in its own translation unit
+// (ks_variant.hip, -DKS_FEAT=F) so the variants build in parallel; koordgpu.hip launches them through
+// the plain host wrappers declared at the end of this header.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ks_device.h"
+#include "ks_rsv.h"
+#include "ks_dev.h"
+#include "ks_cpuset.h"
+#include "ks_numa.h"
+
+namespace ks {
+
+// global candidate key of a chunk-local key: (score + 1) << 32 | ~node
+__device__ __forceinline__ uint64_t local_gkey(uint32_t loc, int64_t chunk) {
+  if (loc == 0) return 0;
+  const int64_t node = chunk * 64 + (63 - (int64_t)(loc & 63u));
+  return ((uint64_t)(loc >> 6) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)node);
+}
+
+// ------------------------------------------------------------------------------------------
+// sweep: per (pod, 64-node chunk) best and runner-up
+// ------------------------------------------------------------------------------------------
+
+struct SweepArgs {
+  const DevNodes* __restrict__ dn;
+  const DevRsv* __restrict__ rv;
+  const DevDev* __restrict__ dv;
+  const DevNuma* __restrict__ nv;
+  unsigned long long* dev_M;  // [64] DeviceShare: (max raw << 32) | ~witness node per pod of the pass
+  int32_t phase;              // 0: reduce dev_M only (DeviceShare), 1: chunk keys
+  // DeviceShare without Reservation: phase 0 keeps each (pod, node)'s (feasible, Fit + LoadAware + NUMA
+  // total, DeviceShare raw) here and phase 1 only applies the normalization ([64][dstride]); NULL = re-evaluate
+  unsigned long long* dcache;
+  int64_t dstride;
+  Cfg c;
+  const PodRec* __restrict__ pods;
+  const int32_t* __restrict__ cursor;
+  uint2* __restrict__ out;  // [64 pods][nchunks]: {best, runner-up} local keys (pod-major: select reads a row)
+  int64_t n, nchunks;
+  int64_t c0, c1;  // this shard's chunk range
+  int32_t total_pods, batch, ppw;
+};
+
+// local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
+template <int NSC, int FEAT>
+__global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
+  const int lane = threadIdx.x & 63;
+  // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar).
+  // XCD-aware: blocks are dealt round-robin over the 8 XCDs, so block b works as virtual block
+  // (b % 8) * (grid / 8) + b / 8 — each XCD gets a contiguous run of work items, i.e. every pod
+  // group of a node chunk is swept on one XCD and the chunk's columns are fetched into one L2 only.
+  // The host launches a multiple of 8 blocks.
+  const uint32_t vblock = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int64_t wave = (int64_t)vblock * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor);
+  const int32_t groups = (np + a.ppw - 1) / a.ppw;
+  const int64_t nwork = (a.c1 - a.c0) * groups;
+  for (int64_t w = wave; w < nwork; w += nwaves) {
+    const int64_t lc = w / groups;  // chunk within this shard's range
+    const int64_t c = a.c0 + lc;
+    const int32_t g = (int32_t)(w - lc * groups);
+    const int64_t node = c * 64 + lane;
+    if ((FEAT & 4) && a.phase == 1 && a.dcache) {
+      const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
+      uint32_t best = 0, second = 0;
+      for (int32_t p = p0; p < p1; ++p) {
+        const unsigned long long e = a.dcache[(size_t)p * a.dstride + node];
+        EvalOut o{};
+        o.total = (int32_t)(uint32_t)e;
+        o.dev_raw = (int32_t)((e >> 32) & 0xFFFFull);
+        const int32_t M = (int32_t)(a.dev_M[p] >> 32);
+        const uint32_t key = (e >> 63) ? (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane)) : 0u;
+        const uint32_t m1 = wave_max_u32(key);
+        const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
+        best = (lane == p) ? m1 : best;
+        second = (lane == p) ? m2 : second;
+      }
+      if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
+      continue;
+    }
+    NodeReg<NSC> r;
+    {
+      const DevNodes d = *a.dn;
+      load_node<NSC>(a.c, d, node, node < a.n, r);
+    }
+    const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
+    uint32_t best = 0, second = 0;
+    for (int32_t p = p0; p < p1; ++p) {
+      const PodRec pod = load_pod_uniform(a.pods + cursor + p);
+      EvalOut o = eval_full<NSC, false, true, FEAT>(
+          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+          [&]() { return dev_eval<false>(a.c, pod, DevGView{*a.dv, node}); });
+      numa_policy_fix<NSC, false, FEAT>(a.c, pod, r, o, [&]() { return NumaGView{*a.nv, node}; });
+      if ((FEAT & 4) && a.phase == 0) {
+        // DeviceShare normalization max over the feasible nodes, witness = lowest index holding it
+        const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | (0xFFFFFFFFull - (uint64_t)node));
+        const uint64_t m = wave_max_u64(mk);
+        if (lane == 0 && m) atomicMax(a.dev_M + p, (unsigned long long)m);
+        if (a.dcache)
+          a.dcache[(size_t)p * a.dstride + node] =
+              (node < a.n && !o.reasons) ? ((1ull << 63) | ((unsigned long long)(uint32_t)o.dev_raw << 32) | (uint32_t)o.total)
+                                         : 0ull;
+        continue;
+      }
+      const int32_t M = (FEAT & 4) ? (int32_t)(a.dev_M[p] >> 32) : 0;
+      const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane));
+      const uint32_t m1 = wave_max_u32(key);
+      const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
+      best = (lane == p) ? m1 : best;
+      second = (lane == p) ? m2 : second;
+    }
+    if ((FEAT & 4) && a.phase == 0) continue;
+    if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
+  }
+}
+
+struct CandSlot {  // one shard's select output inside the gather buffer (byte offsets)
+  size_t chunk, t, count, total, top, bytes;
+};
+
+__host__ __device__ inline CandSlot cand_slot_layout(int32_t k) {
+  CandSlot L;
+  size_t o = 0;
+  L.chunk = o;
+  o += (size_t)kMaxBatch * k * 4;
+  L.t = o;
+  o += (size_t)kMaxBatch * k * 8;
+  L.count = o;
+  o += kMaxBatch * 4;
+  L.total = o;
+  o += kMaxBatch * 4;
+  L.top = o;
+  o += kMaxBatch * 8;
+  L.bytes = (o + 255) / 256 * 256;
+  return L;
+}
+
+// ------------------------------------------------------------------------------------------
+// commit: sequential exact selection + Reserve, one wave, pass state resident in LDS
+// ------------------------------------------------------------------------------------------
+//
+// Slot s (the s-th node touched in this pass) is an LDS row of score Terms + Filter headrooms,
+// updated in place by every Reserve.  Building a slot and Reserve are lane-parallel (lane t owns
+// term t).  For pod j the wave evaluates every slot at once (lane = slot; touched nodes exact)
+// and takes the best untouched node from the candidate lists (snapshot keys, exact for untouched
+// nodes).  Monotone profiles skip the slot evaluation whenever the pod's snapshot-best node is
+// still untouched (a commit can only lower keys).  Pod j+1's quota admission and candidate
+// resolution depend only on state pod j has finished changing, so they run right after pod j's
+// Reserve, and the row of pod j+1's best untouched candidate is put in flight from HBM then.
+
+constexpr int kQuotaLdsRows = 128;  // quota tables up to this size are cached in LDS for the pass
+constexpr int kCommitThreads = 256; // 4 waves load the pass; wave 0 alone runs the sequential loop
+
+// fields of a raw node row (lane f of a row load holds field f)
+enum RowField : int {
+  RF_REQ_CPU = 0, RF_REQ_MEM = 1, RF_REQ_EPH = 2, RF_NZ_CPU = 3, RF_NZ_MEM = 4, RF_REQ_SC = 5,  // 5..8
+  RF_TERM_CPU = 9, RF_TERM_MEM = 10, RF_PTERM_CPU = 11, RF_PTERM_MEM = 12, RF_POD_COUNT = 13,
+  RF_ALLOC_CPU = 14, RF_ALLOC_MEM = 15, RF_ALLOC_EPH = 16, RF_ALLOC_SC = 17,  // 17..20
+  RF_LA_ALLOC_CPU = 21, RF_LA_ALLOC_MEM = 22, RF_ALLOWED = 23, RF_LA_BITS = 24, RF_RSV_CLS = 25,
+  RF_RSV_BEG = 26, RF_RSV_END = 27,  // the node's reservation range [beg, end) in the CSR table
+  RF_NUMA_A = 28, RF_NUMA_OFF = 29,   // NodeNUMAResource cpuset milli-CPUs and amplification offset
+  RF_NUMA_RATIO = 30, RF_CPU_FREE = 31,  // cpu amplification ratio (f64 bits), available CPUs (i32, -1 = no topology)
+  RF_N = 32
+};
+
+// slot-row terms: score terms 0..10, then the Filter headrooms (Allocatable - Requested) stored as
+// Terms too (only .h is read), so building a row and Reserve are one lane-uniform code path
+enum SlotTerm : int {
+  ST_CPU = 0, ST_MEM = 1, ST_EPH = 2, ST_SC = 3, ST_LCPU = 7, ST_LMEM = 8, ST_PLCPU = 9, ST_PLMEM = 10,
+  ST_FREE_CPU = 11, ST_FREE_MEM = 12, ST_FREE_EPH = 13, ST_FREE_SC = 14,  // 14..17
+  ST_NCPU = 18, ST_NMEM = 19,  // NodeNUMAResource: Requested (+ amplified cpuset part) cpu / memory
+  ST_N = 20
+};
+
+struct __attribute__((aligned(16))) SlotRow {
+  Term t[ST_N];
+  uint32_t la_bits;
+  int32_t fit_ws, allowed, pod_count;
+};
+// 656 B = 41 x 16 B (an odd number of 16 B units): lane = slot ds_read_b128 is conflict-free
+static_assert(sizeof(SlotRow) == 656, "SlotRow layout");
+
+// Device column of each row field (built by the host at ks_load_nodes).
+struct RowCol {
+  const void* p;
+  int32_t width;
+  int32_t _pad;
+};
+
+struct CommitArgs {
+  const DevNodes* __restrict__ dn;
+  const DevRsv* __restrict__ rv;
+  const DevDev* __restrict__ dv;
+  const DevNuma* __restrict__ nv;
+  const unsigned long long* __restrict__ dev_M;  // [64] DeviceShare normalization max + witness (sweep phase 0)
+  Cfg c;
+  const PodRec* __restrict__ pods;
+  DevPodQuota pq;
+  DevQuotas q;
+  const RowCol* __restrict__ rowcols;  // [RF_N]
+  int32_t* cursor;
+  const uint32_t* __restrict__ cand_chunk;
+  const uint2* __restrict__ cand_t;
+  const uint64_t* __restrict__ cand_bound;
+  const uint64_t* __restrict__ cand_top;
+  const int32_t* __restrict__ cand_count;
+  ks_result* results;
+  unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot row misses [14] fast picks
+  int64_t n, nchunks;
+  int32_t total_pods, batch, k;
+  int2* cpuset_list;   // (pod, node) of every cpu-bind Reserve, in placement order (ks_cpuset.h)
+  int32_t* cpuset_n;
+  int32_t rcap;        // reservations cached in LDS per slot (0 = none)
+  int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
+  int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
+  int32_t numa_bytes;  // LDS bytes of the slot NUMA-node state (commit_layout)
+};
+
+struct QuotaRowsLds {
+  int32_t parent[kQuotaLdsRows];
+  uint32_t limit_mask[kQuotaLdsRows], min_mask[kQuotaLdsRows];
+  int64_t limit[kQuotaLdsRows * KS_QUOTA_DIMS], used[kQuotaLdsRows * KS_QUOTA_DIMS];
+  int64_t min[kQuotaLdsRows * KS_QUOTA_DIMS], npused[kQuotaLdsRows * KS_QUOTA_DIMS];
+};
+
+struct CommitLayout {
+  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, touched, total;
+};
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+
+__host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0,
+                                                      size_t dev_bytes = 0, size_t numa_bytes = 0) {
+  CommitLayout L;
+  size_t o = 0;
+  L.rows = o;
+  o += (size_t)kMaxBatch * sizeof(SlotRow);
+  L.pods = o;
+  o += (size_t)kMaxBatch * sizeof(PodRec);
+  L.res = o;
+  o += align16((size_t)kMaxBatch * sizeof(ks_result));
+  L.raw = o;
+  o += 32 * 8;  // one raw row being turned into a slot row
+  L.rawtop = o;
+  o += (size_t)kMaxBatch * 32 * 8;  // raw row of each pod's snapshot-best node, prefetched per pass
+  L.pqreq = o;
+  o += (size_t)kMaxBatch * KS_QUOTA_DIMS * 8;
+  L.cand_t = o;
+  o += (size_t)kMaxBatch * k * sizeof(uint2);
+  L.cand_chunk = o;
+  o += align16((size_t)kMaxBatch * k * 4);
+  L.scls = o;
+  o += (size_t)kMaxBatch * 8;  // per slot: owner classes of the node's matchable reservations
+  L.snuma = o;
+  o += (size_t)kMaxBatch * 32;  // per slot: NodeNUMAResource cpuset milli-CPUs, amplification offset, ratio, free CPUs
+  L.srcnt = o;
+  o += (size_t)kMaxBatch * 8;  // per slot: reservations cached (-1 = on the HBM table), CSR begin
+  L.srec = o;
+  o += align16(rsv_bytes);     // per slot: the node's reservations (RsvRec, rcap each)
+  L.sdev = o;
+  o += align16(dev_bytes);     // per slot: GPU totals / used [3][kGpus] + present flag
+  L.snp = o;
+  o += align16(numa_bytes);    // per slot: NUMA-node totals / used / offsets + policy, count, present (ks_numa.h)
+  L.quota = o;
+  if (qc) o += align16(sizeof(QuotaRowsLds));
+  L.touched = o;
+  o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
+  L.total = o;
+  return L;
+}
+
+// ElasticQuota PreFilter (plugin.go:210-255, plugin_helper.go:281-319); lane d checks dimension d.
+// The leaf's used/limit/mask reads are independent, so they are issued together.
+template <typename P32, typename PU32, typename P64>
+__device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU32 min_mask, P64 limit, P64 used,
+                                                P64 minv, P64 npused, bool check_parent, int32_t quota,
+                                                uint32_t flags, uint32_t pmask, int64_t req,
+                                                bool skip_leaf = false) {
+  const int lane = threadIdx.x & 63;
+  const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
+  const int ld = lane < KS_QUOTA_DIMS ? lane : 0;
+  const size_t o = (size_t)quota * KS_QUOTA_DIMS + ld;
+  if (!skip_leaf) {
+    const uint32_t lm = limit_mask[quota];
+    const int64_t u = used[o], l = limit[o];
+    const bool bad = in_pod && ((lm >> lane) & 1u) && (req + u > l);
+    if (__ballot(bad)) return KS_S_QUOTA;
+  }
+  if (flags & KS_POD_NONPREEMPTIBLE) {
+    const uint32_t mm = min_mask[quota];
+    const int64_t u = npused[o], m = minv[o];
+    const bool bad = in_pod && ((mm >> lane) & 1u) && (req + u > m);
+    if (__ballot(bad)) return KS_S_QUOTA_NONPREEMPTIBLE;
+  }
+  if (check_parent) {
+    for (int32_t cur = parent[quota]; cur >= 0; cur = parent[cur]) {
+      const size_t oc = (size_t)cur * KS_QUOTA_DIMS + ld;
+      const bool bad = in_pod && ((limit_mask[cur] >> lane) & 1u) && (req + used[oc] > limit[oc]);
+      if (__ballot(bad)) return KS_S_QUOTA | KS_S_QUOTA_PARENT;
+    }
+  }
+  return 0;
+}
+
+// One row field of node `node`, lane f loading field f (4-byte columns zero-extended).
+__device__ __forceinline__ int64_t load_field(const void* p, int32_t w, int64_t node) {
+  if (w == 8) return gld((const int64_t*)p + node);
+  return (int64_t)(uint64_t)gld((const uint32_t*)p + node);
+}
+
+// NodeReg of one slot row (lane-private LDS reads).
+template <int NSC>
+__device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
+  r.free_cpu = s.t[ST_FREE_CPU].h;
+  r.free_mem = s.t[ST_FREE_MEM].h;
+  r.free_eph = s.t[ST_FREE_EPH].h;
+  r.t_cpu = s.t[ST_CPU];
+  r.t_mem = s.t[ST_MEM];
+  r.t_eph = s.t[ST_EPH];
+#pragma unroll
+  for (int k = 0; k < NSC; ++k) {
+    r.free_sc[k] = s.t[ST_FREE_SC + k].h;
+    r.t_sc[k] = s.t[ST_SC + k];
+  }
+  r.t_lcpu = s.t[ST_LCPU];
+  r.t_lmem = s.t[ST_LMEM];
+  r.t_plcpu = s.t[ST_PLCPU];
+  r.t_plmem = s.t[ST_PLMEM];
+  r.t_ncpu = s.t[ST_NCPU];
+  r.t_nmem = s.t[ST_NMEM];
+  r.numa_A = 0;
+  r.numa_off = 0;
+  r.la_bits = s.la_bits;
+  r.fit_ws = s.fit_ws;
+  r.allowed = s.allowed;
+  r.pod_count = s.pod_count;
+  r.pods_full = (int64_t)s.pod_count + 1 > (int64_t)s.allowed;
+  r.valid = 1;
+  r.rsv_cls = 0;
+}
+
+// Untouched-candidate resolution of one pod (lane k = candidate k), against the current touched masks.
+struct Cands {
+  uint64_t u;      // exact best untouched key of the lane's chunk (0 = none / unknown)
+  uint64_t ub;     // upper bound when inexact (best and runner-up both touched)
+  uint32_t chunk;
+  bool exact, valid;
+  uint64_t umax;   // wave max of the exact u
+  bool fast;       // monotone profile and the pod's snapshot-best node is untouched
+};
+
+__device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const uint2* cand_t,
+                                               const unsigned long long* touched, int32_t j, int32_t K,
+                                               int32_t cnt) {
+  const int lane = threadIdx.x & 63;
+  Cands r;
+  r.valid = lane < cnt;
+  r.chunk = r.valid ? cand_chunk[j * K + lane] : 0u;
+  const uint2 t = r.valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
+  const uint64_t tm = r.valid ? touched[r.chunk] : 0ull;
+  r.u = local_gkey(t.x, r.chunk);
+  r.fast = false;
+  r.ub = 0;
+  r.exact = r.valid;
+  if (r.valid && ((tm >> (63 - (t.x & 63u))) & 1ull)) {  // chunk best touched
+    if (t.y == 0) {
+      r.u = 0;                                           // no other feasible node in the chunk
+    } else if (!((tm >> (63 - (t.y & 63u))) & 1ull)) {
+      r.u = local_gkey(t.y, r.chunk);                    // runner-up untouched: exact
+    } else {
+      r.exact = false;                                   // both touched: below the runner-up, unknown
+      r.ub = local_gkey(t.y, r.chunk);
+      r.u = 0;
+    }
+  }
+  r.umax = wave_max_u64(r.exact ? r.u : 0ull);
+  return r;
+}
+
+// Re-scan a candidate chunk's untouched nodes exactly for one pod (lane = node); touched nodes are
+// covered by the slot evaluation.
+template <int NSC, int FEAT>
+__device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const Cfg& cfg, const PodRec& pod,
+                                                     int64_t chunk, uint64_t touched_mask, int32_t M) {
+  const int lane = threadIdx.x & 63;
+  const int64_t node = chunk * 64 + lane;
+  NodeReg<NSC> r;
+  {
+    const DevNodes d = *a.dn;
+    load_node<NSC>(cfg, d, node, node < a.n, r);
+  }
+  EvalOut o = eval_full<NSC, false, false, FEAT>(
+      cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+      [&]() { return dev_eval<false>(cfg, pod, DevGView{*a.dv, node}); });
+  numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaGView{*a.nv, node}; });
+  const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
+  return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
+}
+
+template <int NSC, bool QC, int FEAT>
+__global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
+  constexpr bool RSV = (FEAT & 1) != 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int32_t K = a.k;
+  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes, (size_t)a.numa_bytes);
+  SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
+  PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
+  ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
+  int64_t* raw = reinterpret_cast<int64_t*>(smem_raw + lay.raw);
+  int64_t* rawtop = reinterpret_cast<int64_t*>(smem_raw + lay.rawtop);
+  int64_t* pqreq = reinterpret_cast<int64_t*>(smem_raw + lay.pqreq);
+  uint2* cand_t = reinterpret_cast<uint2*>(smem_raw + lay.cand_t);
+  uint32_t* cand_chunk = reinterpret_cast<uint32_t*>(smem_raw + lay.cand_chunk);
+  QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
+  unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
+  uint64_t* scls = reinterpret_cast<uint64_t*>(smem_raw + lay.scls);
+  int64_t* snuma = reinterpret_cast<int64_t*>(smem_raw + lay.snuma);
+  int32_t* srcnt = reinterpret_cast<int32_t*>(smem_raw + lay.srcnt);
+  int32_t* srbeg = srcnt + kMaxBatch;
+  constexpr int RD = 3 + NSC;
+  RsvRec<RD>* srec = reinterpret_cast<RsvRec<RD>*>(smem_raw + lay.srec);
+  constexpr bool DEV = (FEAT & 4) != 0;
+  constexpr int DW = kDevTW;   // int64 words of one slot's device totals + topology (ks_dev.h)
+  constexpr int DU = kDevQW;   // int64 words of its used amounts
+  // word-major [w][kDevLdsStride] (slot s at column s): the slot-parallel reads (lane = slot) are
+  // bank-conflict free, the lane = word row fills hit distinct bank pairs
+  int64_t* sdev_tot = reinterpret_cast<int64_t*>(smem_raw + lay.sdev);
+  int64_t* sdev_use = sdev_tot + kDevLdsStride * DW;
+  int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kDevLdsStride * DU);
+  int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor0 >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor0);
+#ifdef KS_COMMIT_STAMPS
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tlast = __builtin_amdgcn_s_memtime();
+#define KS_STAMP(i)                                    \
+  do {                                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - tlast;                               \
+    tlast = t_;                                        \
+  } while (0)
+#else
+#define KS_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
+  // ---- load the pass into LDS with all four waves (independent loads, one burst) ----
+  for (int32_t i = tid; i < np * K; i += kCommitThreads) {
+    cand_chunk[i] = a.cand_chunk[i];
+    cand_t[i] = a.cand_t[i];
+  }
+  for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += kCommitThreads) {
+    const int32_t p = i / KS_QUOTA_DIMS, dd = i - p * KS_QUOTA_DIMS;
+    pqreq[i] = a.pq.req[dd][cursor0 + p];
+  }
+  {
+    const int64_t* src = reinterpret_cast<const int64_t*>(a.pods + cursor0);
+    int64_t* dst = reinterpret_cast<int64_t*>(spods);
+    const int32_t words = np * (int32_t)(sizeof(PodRec) / 8);
+    for (int32_t i = tid; i < words; i += kCommitThreads) dst[i] = src[i];
+  }
+  for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
+  // raw row of every pod's snapshot-best node (the monotone fast path's winner): all loads in flight together
+  for (int32_t i = tid; i < np * RF_N; i += kCommitThreads) {
+    const int32_t p = i / RF_N, f = i - p * RF_N;
+    const uint64_t top = a.cand_top[p];
+    if (top) {
+      const RowCol rc = a.rowcols[f];
+      rawtop[p * 32 + f] = load_field(rc.p, rc.width, gkey_node(top));
+    }
+  }
+  if (QC) {
+    for (int32_t r = tid; r < a.q.q; r += kCommitThreads) {
+      qlds->parent[r] = a.q.parent[r];
+      qlds->limit_mask[r] = a.q.limit_mask[r];
+      qlds->min_mask[r] = a.q.min_mask[r];
+    }
+    for (int32_t i = tid; i < a.q.q * KS_QUOTA_DIMS; i += kCommitThreads) {
+      qlds->limit[i] = a.q.limit[i];
+      qlds->used[i] = a.q.used[i];
+      qlds->min[i] = a.q.min[i];
+      qlds->npused[i] = a.q.npused[i];
+    }
+  }
+  // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
+  int32_t my_cnt = 0, my_quota = -1;
+  uint32_t my_flags = 0, my_pmask = 0;
+  uint64_t my_bound = 0, my_top = 0, my_devM = 0;
+  if (tid < 64 && lane < np) {
+    my_cnt = a.cand_count[lane];
+    my_bound = a.cand_bound[lane];
+    my_top = a.cand_top[lane];
+    if (DEV) my_devM = a.dev_M[lane];
+    my_pmask = a.pq.mask[cursor0 + lane];
+    my_quota = a.pods[cursor0 + lane].quota;
+    my_flags = a.pods[cursor0 + lane].flags;
+  }
+  // lane f < RF_N: the column of row field f
+  const void* my_col = nullptr;
+  int32_t my_w = 8;
+  if (tid < RF_N) {
+    my_col = a.rowcols[lane].p;
+    my_w = a.rowcols[lane].width;
+  }
+  __syncthreads();
+  if (tid >= 64) return;  // waves 1-3 are done; wave 0 runs the sequential loop alone
+  KS_STAMP(0);
+  // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
+  // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
+  Cfg cfg = a.c;
+  {
+    int32_t* w = reinterpret_cast<int32_t*>(&cfg);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(Cfg) / 4); ++i) asm volatile("" : "+s"(w[i]));
+  }
+  int32_t Kc = K;
+  asm volatile("" : "+s"(Kc));
+
+  // ---- per-lane roles in slot construction and Reserve: lane t < ST_N owns slot term t ----
+  // capacity / requested raw fields, the PodRec words of its Reserve delta (x1, x100), and whether a
+  // zero capacity disables the term (score terms) or not (headrooms)
+  int32_t t_cap = 0, t_req = 0, t_pw = 0, t_pw100 = 0;
+  int32_t t_rdim = -1;  // reservation restore dimension of the lane's term: 0..6 Requested, 8/9 NonZero cpu/memory
+  bool t_prod_only = false, t_score = true;
+  switch (lane) {
+    case ST_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_NZ_CPU; t_pw = 3; t_pw100 = 12; t_rdim = 8; break;
+    case ST_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_NZ_MEM; t_pw = 4; t_pw100 = 13; t_rdim = 9; break;
+    case ST_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 14; t_rdim = 2; break;
+    case ST_SC + 0: case ST_SC + 1: case ST_SC + 2: case ST_SC + 3:
+      t_cap = RF_ALLOC_SC + (lane - ST_SC); t_req = RF_REQ_SC + (lane - ST_SC); t_pw = 7 + (lane - ST_SC); t_pw100 = 17 + (lane - ST_SC);
+      t_rdim = 3 + (lane - ST_SC); break;
+    case ST_LCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_TERM_CPU; t_pw = 5; t_pw100 = 15; break;
+    case ST_LMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_TERM_MEM; t_pw = 6; t_pw100 = 16; break;
+    case ST_PLCPU: t_cap = RF_LA_ALLOC_CPU; t_req = RF_PTERM_CPU; t_pw = 5; t_pw100 = 15; t_prod_only = true; break;
+    case ST_PLMEM: t_cap = RF_LA_ALLOC_MEM; t_req = RF_PTERM_MEM; t_pw = 6; t_pw100 = 16; t_prod_only = true; break;
+    case ST_FREE_CPU: t_cap = RF_ALLOC_CPU; t_req = RF_REQ_CPU; t_pw = 0; t_pw100 = 0; t_score = false; t_rdim = 0; break;
+    case ST_FREE_MEM: t_cap = RF_ALLOC_MEM; t_req = RF_REQ_MEM; t_pw = 1; t_pw100 = 1; t_score = false; t_rdim = 1; break;
+    case ST_FREE_EPH: t_cap = RF_ALLOC_EPH; t_req = RF_REQ_EPH; t_pw = 2; t_pw100 = 2; t_score = false; t_rdim = 2; break;
+    case ST_FREE_SC + 0: case ST_FREE_SC + 1: case ST_FREE_SC + 2: case ST_FREE_SC + 3:
+      t_cap = RF_ALLOC_SC + (lane - ST_FREE_SC); t_req = RF_REQ_SC + (lane - ST_FREE_SC);
+      t_pw = 7 + (lane - ST_FREE_SC); t_pw100 = t_pw; t_score = false; t_rdim = 3 + (lane - ST_FREE_SC); break;
+    case ST_NCPU: t_cap = RF_ALLOC_CPU; t_req = RF_REQ_CPU; t_pw = 0; t_pw100 = kPodWordHCpu; t_rdim = 0; break;
+    case ST_NMEM: t_cap = RF_ALLOC_MEM; t_req = RF_REQ_MEM; t_pw = 1; t_pw100 = kPodWordHMem; t_rdim = 1; break;
+    default: break;
+  }
+  constexpr int kLaneCounts = ST_N;  // lane: pod count / flags of the row
+  const bool monotone = cfg.monotone != 0;
+
+  int32_t snode = -1;  // lane s: node of slot s
+  int32_t nslots = 0;
+  int32_t processed = np;
+  uint32_t rescans = 0, misses = 0, fast = 0;
+  // speculative raw row of the next pod's best untouched candidate (lane f = field f)
+  int64_t spec_val = 0;
+  int32_t spec_node = -1;
+
+  auto admit = [&](int32_t j) -> uint32_t {
+    const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
+    if (!cfg.quota_enable || qrow < 0) return 0u;
+    const uint32_t flags = __builtin_amdgcn_readlane(my_flags, j);
+    const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
+    const int64_t req = pqreq[j * KS_QUOTA_DIMS + (lane & (KS_QUOTA_DIMS - 1))];
+    return QC ? quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
+                            qlds->npused, cfg.quota_parent, qrow, flags, pmask, req)
+              : quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
+                            cfg.quota_parent, qrow, flags, pmask, req);
+  };
+  uint32_t st_next = 0;
+  Cands cn{};
+  auto lookahead = [&](int32_t j) {
+    // the fast path also holds for a pod without device requests when only DeviceShare's normalization
+    // max made the profile non-monotone (its DeviceShare score is 0 on every node)
+    const bool mono = monotone || (cfg.monotone_nd && !(__builtin_amdgcn_readlane(my_flags, j) & kPodHasGpu));
+    const uint64_t top = mono ? readlane64(my_top, j) : 0ull;
+    const int32_t tn = top ? (int32_t)gkey_node(top) : 0;
+    if (QC) {
+      // every LDS read of the admission and of the fast check issued together (one latency)
+      const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
+      const bool has_q = cfg.quota_enable && qrow >= 0;
+      const int32_t qr = has_q ? qrow : 0;
+      const int ld = lane & (KS_QUOTA_DIMS - 1);
+      const size_t o = (size_t)qr * KS_QUOTA_DIMS + ld;
+      const int64_t req = pqreq[j * KS_QUOTA_DIMS + ld];
+      const uint32_t lm = qlds->limit_mask[qr];
+      const int64_t u = qlds->used[o], l = qlds->limit[o];
+      const uint64_t tw = touched[tn >> 6];
+      st_next = 0;
+      if (has_q) {
+        const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
+        const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
+        if (__ballot(in_pod && ((lm >> lane) & 1u) && (req + u > l))) {
+          st_next = KS_S_QUOTA;
+        } else {
+          const uint32_t flags = __builtin_amdgcn_readlane(my_flags, j);
+          st_next = quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
+                                qlds->npused, cfg.quota_parent, qrow, flags & KS_POD_NONPREEMPTIBLE, pmask, req,
+                                /*skip_leaf=*/true);
+        }
+      }
+      if (st_next) return;
+      if (top && !((tw >> (tn & 63)) & 1ull)) {
+        cn.fast = true;  // its row is in rawtop[j]
+        cn.umax = top;
+        return;
+      }
+    } else {
+      st_next = admit(j);
+      if (st_next) return;
+      if (top && !((touched[tn >> 6] >> (tn & 63)) & 1ull)) {
+        cn.fast = true;
+        cn.umax = top;
+        return;
+      }
+    }
+    cn = resolve_cands(cand_chunk, cand_t, touched, j, Kc, __builtin_amdgcn_readlane(my_cnt, j));
+#ifndef KS_NO_SPEC
+    if (cn.umax) {
+      const int32_t node = (int32_t)gkey_node(cn.umax);
+      if (node != spec_node) {
+        spec_node = node;
+        if (lane < RF_N) spec_val = load_field(my_col, my_w, node);
+      }
+    }
+#endif
+  };
+  lookahead(0);
+  KS_STAMP(1);
+
+  for (int32_t j = 0; j < np; ++j) {
+    const uint32_t st = st_next;
+    const Cands cj = cn;
+    if (st) {
+      if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0, 0, 0};
+      goto next_pod;
+    }
+    {
+    uint64_t best;
+    int32_t Muse = 0;  // DeviceShare normalization max used for this pod
+    if (cj.fast) {
+      best = cj.umax;  // the snapshot-best node is untouched: commits only lower keys, so it wins
+      ++fast;
+      KS_STAMP(2);
+    } else {
+      // pod j: LDS broadcast into VGPRs; flags scalar so the plugin branches stay wave-uniform
+      PodRec pod = spods[j];
+      pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
+      pod.rsv_class = __builtin_amdgcn_readfirstlane(pod.rsv_class);
+      // ---- every touched node exactly (lane = slot), untouched from the candidates ----
+      uint64_t key_mod = 0;
+      EvalOut o{};
+      bool feas = false;
+      if (lane < nslots) {
+        NodeReg<NSC> r;
+        slot_to_reg<NSC>(rows[lane], r);
+        r.rsv_cls = scls[lane];
+        r.numa_A = snuma[4 * lane];
+        r.numa_off = snuma[4 * lane + 1];
+        r.numa_ratio = __longlong_as_double(snuma[4 * lane + 2]);
+        r.cpu_free = (int32_t)snuma[4 * lane + 3];
+        o = eval_full<NSC, false, false, FEAT>(
+            cfg, pod, r,
+            [&](RsvDelta<NSC>& dl) {
+              const int32_t c = srcnt[lane];
+              if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
+              return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
+            },
+            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}); });
+        numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
+        feas = o.reasons == 0;
+      }
+      if (DEV && cfg.dev) {
+        // DeviceShare normalization: the untouched nodes' max is the sweep's M while its witness is
+        // untouched; the touched nodes are current.  If the pod's max changes, cut the pass here.
+        const uint64_t mk = readlane64(my_devM, j);
+        const int32_t Msw = (int32_t)(mk >> 32);
+        const int32_t Mt = (int32_t)wave_max_u32(feas ? (uint32_t)o.dev_raw + 1u : 0u) - 1;
+        if (mk == 0) {
+          Muse = Mt < 0 ? 0 : Mt;  // no untouched node is feasible: only the touched ones compete
+        } else {
+          const int64_t wn = (int64_t)(0xFFFFFFFFull - (mk & 0xFFFFFFFFull));
+          const bool wt = ((touched[wn >> 6] >> (wn & 63)) & 1ull) != 0;
+          if (wt ? (Mt != Msw) : (Mt > Msw)) {
+            processed = j;
+            break;
+          }
+          Muse = Msw;
+        }
+      }
+      if (feas) key_mod = gkey(key_total(cfg, o, Muse), snode);
+      best = umax64(cj.umax, wave_max_u64(key_mod));
+      KS_STAMP(2);
+      uint64_t need = __ballot(!cj.exact && cj.valid && cj.ub > best);
+      while (need) {
+        const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? cj.ub : 0ull);
+        const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && cj.ub == kmax)) - 1;
+        const int64_t c = (int64_t)(uint32_t)__shfl((int)cj.chunk, sel, 64);
+        const uint64_t v = rescan_untouched<NSC, FEAT>(a, cfg, pod, c, touched[c], Muse);
+        ++rescans;
+        best = umax64(best, v);
+        need &= ~(1ull << sel);
+        need &= __ballot(cj.ub > best);
+      }
+      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, j);
+      if (cnt == Kc && best < readlane64(my_bound, j)) {
+        processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep from j
+        break;
+      }
+      KS_STAMP(3);
+    }
+    if (best == 0) {
+      if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0, -1, 0, 0, 0};
+      goto next_pod;
+    }
+    const int32_t node = (int32_t)gkey_node(best);
+    const int64_t score = gkey_score(best);
+    const uint32_t pflags = __builtin_amdgcn_readlane(my_flags, j);
+    const int64_t* podw = reinterpret_cast<const int64_t*>(&spods[j]);
+    // ---- Reserve: NodeInfo.AddPod + podAssignCache.assign on the slot row (lane = term) ----
+    // a cpu-bind pod first needs numCPUsNeeded available CPUs on the node (resource_manager.go:333-335)
+    const bool cpubind = (FEAT & 2) && cfg.cpuset && (pflags & KS_POD_CPU_BIND);
+    const int32_t cpu_need = cpubind ? (int32_t)(__builtin_amdgcn_readfirstlane(spods[j].cpu_bind) >> 8) : 0;
+    int32_t s = __ffsll((long long)__ballot(snode == node)) - 1;
+    SlotRow* row;
+    // Reservation Reserve needs the node's pre-pod row: when the pod's class matches one of the
+    // node's reservations the row is built / kept without the pod, nominated on, then taken.
+    const int32_t pcls = (RSV && cfg.rsv) ? __builtin_amdgcn_readfirstlane(spods[j].rsv_class) : -1;
+    bool rsvc = false;
+    if (s < 0) {
+      s = nslots++;
+      row = &rows[s];
+      const int64_t* src = raw;
+      if (node == (int32_t)gkey_node(readlane64(my_top, j))) {
+        src = rawtop + j * 32;  // prefetched at pass start
+      } else {
+        int64_t v = spec_val;
+        if (node != spec_node) {
+          ++misses;
+          if (lane < RF_N) v = load_field(my_col, my_w, node);
+        }
+        if (lane < RF_N) raw[lane] = v;
+      }
+      // Every field this slot needs is read before the first LDS write: the compiler cannot prove the
+      // slot writes do not alias `src`, so each read after a write would cost a full LDS round trip.
+      const bool take = !t_prod_only || (pflags & KS_POD_PROD);  // (before the Reservation match below)
+      const int64_t f_cap = src[t_cap], f_req = src[t_req], f_pw = podw[t_pw];
+      const int64_t u_bits = src[RF_LA_BITS], u_allowed = src[RF_ALLOWED], u_pods = src[RF_POD_COUNT];
+      const int64_t u_acpu = src[RF_ALLOC_CPU], u_amem = src[RF_ALLOC_MEM], u_aeph = src[RF_ALLOC_EPH];
+      const uint64_t ncl = RSV ? (uint64_t)src[RF_RSV_CLS] : 0ull;
+      const int32_t u_rb = RSV ? (int32_t)src[RF_RSV_BEG] : 0, u_re = RSV ? (int32_t)src[RF_RSV_END] : 0;
+      const int64_t u_A = (FEAT & 2) ? src[RF_NUMA_A] : 0, u_off = (FEAT & 2) ? src[RF_NUMA_OFF] : 0;
+      const int64_t u_ratio = (FEAT & 2) ? src[RF_NUMA_RATIO] : 0;
+      const int32_t u_free = (FEAT & 2) ? (int32_t)src[RF_CPU_FREE] : 0;
+      if (cpubind && u_free < cpu_need) {
+        // NodeNUMAResource Reserve -> Allocate: not enough CPUs; every plugin unreserves
+        --nslots;
+        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0, 0, 0};
+        goto next_pod;
+      }
+      if (lane == s) snode = node;
+      if (lane == 0) atomicOr(&touched[node >> 6], 1ull << (node & 63));
+      rsvc = pcls >= 0 && pcls < 64 && ((ncl >> pcls) & 1ull);
+      if (lane == 0) {
+        if (RSV) scls[s] = ncl;
+        if (FEAT & 2) {
+          snuma[4 * s] = u_A;
+          snuma[4 * s + 1] = u_off;
+          snuma[4 * s + 2] = u_ratio;
+          snuma[4 * s + 3] = (int64_t)u_free;
+        }
+      }
+      if ((FEAT & 8) && cfg.numa_pol) {
+        // the node's NUMA-node state into LDS (lane = word, NumaLView layout)
+        const DevNuma& nv = *a.nv;
+        int64_t v = 0;
+        if (lane < 2 * kNumaDev) v = gld(nv.total + (int64_t)lane * nv.npad + node);
+        else if (lane < 4 * kNumaDev) v = gld(nv.used + (int64_t)(lane - 2 * kNumaDev) * nv.npad + node);
+        else if (lane < 5 * kNumaDev) v = gld(nv.off + (int64_t)(lane - 4 * kNumaDev) * nv.npad + node);
+        else if (lane == 5 * kNumaDev)
+          v = (int64_t)((gld(nv.flags + node) >> KS_NUMA_POLICY_SHIFT) & 3u) | ((int64_t)gld(nv.count + node) << 8) |
+              ((int64_t)gld(nv.present + node) << 32);
+        if (lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = v;
+      }
+      if (DEV && cfg.dev) {
+        // the node's device totals + topology / used / present flag into LDS (lane = word)
+        const DevDev& dv = *a.dv;
+        int64_t v = 0, w = 0;
+        if (lane < DW) v = gld(dv.total + (int64_t)lane * dv.npad + node);
+        else if (lane == DW) v = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
+        if (lane < DU) w = gld(dv.used + (int64_t)lane * dv.npad + node);
+        if (lane < DW) sdev_tot[lane * kDevLdsStride + s] = v;
+        else if (lane == DW) sdev_pres[s] = (int32_t)v;
+        if (lane < DU) sdev_use[lane * kDevLdsStride + s] = w;
+      }
+      if (RSV && cfg.rsv) {
+        // the node's reservations into LDS (lane = record word), unless too many or too wide
+        const int32_t rb = u_rb, cnt = u_re - u_rb;
+        int32_t mode = -1;
+        if (cnt <= a.rcap) {
+          constexpr int W = (int)(sizeof(RsvRec<RD>) / 8);
+          int64_t* dst = reinterpret_cast<int64_t*>(srec + s * a.rcap);
+          const DevRsv& rv = *a.rv;
+          for (int t = lane; t < cnt * W; t += 64) {
+            const int rr = t / W, w = t - rr * W;
+            const int64_t i = rb + rr;
+            int64_t v;
+            if (w == 0) v = (int64_t)gld(rv.cls + i);
+            else if (w == 1) v = (int64_t)(((uint64_t)(uint32_t)gld(rv.ohi + i) << 32) | gld(rv.meta + i));
+            else if (w == 2) v = (int64_t)(uint32_t)gld(rv.assigned + i);
+            else if (w < 3 + RD) v = gld(rv.alloc + (int64_t)(w - 3) * rv.nr + i);
+            else if (w < 3 + 2 * RD) v = gld(rv.allocd + (int64_t)(w - 3 - RD) * rv.nr + i);
+            else v = gld(rv.rnz + (int64_t)(w - 3 - 2 * RD) * rv.nr + i);
+            dst[t] = v;
+          }
+          const bool wide = __ballot(lane < cnt && rsv_ndims(srec[s * a.rcap + (lane < cnt ? lane : 0)].meta) > RD) != 0;
+          mode = wide ? -1 : cnt;
+        }
+        if (lane == 0) {
+          srcnt[s] = mode;
+          srbeg[s] = rb;
+        }
+      }
+      // build the slot row with the pod already reserved on it (lane-parallel, one code path)
+      const bool take_here = take && !rsvc;
+      const int64_t cap = f_cap, req = f_req + (take_here ? f_pw : 0) + (lane == ST_NCPU ? u_off : 0);
+      if (lane < ST_N) {
+        Term t;
+        t.c = cap;
+        t.h = cap - req + ((cap != 0 || !t_score) ? 0 : kNoCap);
+        t.h100 = cap != 0 ? (cap - req) * 100 : 0;
+        t.fh = i64_to_f32(t.h);
+        t.rcp = rcp100(cap);
+        row->t[lane] = t;
+      } else if (lane == kLaneCounts) {
+        row->la_bits = (uint32_t)u_bits;
+        row->allowed = (int32_t)u_allowed;
+        row->pod_count = (int32_t)u_pods + (rsvc ? 0 : 1);
+        row->fit_ws = (u_acpu != 0 ? cfg.fw_cpu : 0) + (u_amem != 0 ? cfg.fw_mem : 0) + (u_aeph != 0 ? cfg.fw_eph : 0);
+      }
+    } else {
+      if (cpubind && (int32_t)snuma[4 * s + 3] < cpu_need) {
+        if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0, 0, 0};
+        goto next_pod;
+      }
+      row = &rows[s];
+      rsvc = pcls >= 0 && pcls < 64 && ((scls[s] >> pcls) & 1ull);
+      const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
+      if (lane < ST_N) {
+        if (take) term_take(row->t[lane], podw[t_pw], podw[t_pw100]);
+      } else if (lane == kLaneCounts) {
+        if (!rsvc) row->pod_count += 1;
+      }
+    }
+    KS_STAMP(4);
+    int32_t nom_row = -1;
+    int64_t fitla_pref = -1;  // Fit + LoadAware total of a preferred (ordered) chosen node
+    if (RSV && rsvc) {
+      // NominateReservation on the pre-pod state, Reserve into it (AddAssignedPod), then the pod
+      PodRec pod = spods[j];
+      pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
+      pod.rsv_class = pcls;
+      NodeReg<NSC> nr;
+      slot_to_reg<NSC>(*row, nr);
+      nr.rsv_cls = scls[s];
+      nr.numa_A = snuma[4 * s];
+      nr.numa_off = snuma[4 * s + 1];
+      nr.numa_ratio = __longlong_as_double(snuma[4 * s + 2]);
+      nr.cpu_free = (int32_t)snuma[4 * s + 3];
+      RsvDelta<NSC> dl;
+      const int32_t mode = srcnt[s];
+      const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s]};
+      RsvOut ro;
+      if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl);
+      else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl);
+      const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);  // view index
+      if (ro.hi >= kRsvOrderBase) {
+        rsv_apply<NSC>(nr, dl, 1);
+        EvalOut e2 = eval_pod_node<NSC, false>(cfg, pod, nr);
+        if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
+        fitla_pref = e2.total;
+        if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
+          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0});
+          fitla_pref += cfg.dev_pw * (Muse == 0 ? dd.raw : small_div(100 * dd.raw, Muse));
+        }
+      }
+      int64_t dd = 0;
+      if (nom >= 0) {
+        RsvReserve rr;
+        int64_t gi;
+        if (mode >= 0) {
+          rr = rsv_reserve_delta(lv, pod, nom);
+          gi = lv.csr(nom);
+        } else {
+          const RsvG<true> gv(*a.rv, node);
+          rr = rsv_reserve_delta(gv, pod, nom);
+          gi = gv.csr(nom);
+        }
+        RsvRec<RD>* rec = srec + s * a.rcap + nom;
+#pragma unroll
+        for (int d = 0; d < kRsvDims; ++d) {
+          dd = (t_rdim == d) ? rr.dreq[d] : dd;
+          if (lane == d && rr.add[d] != 0) {
+            // the HBM table stays current for the next pass; the LDS copy for this one
+            atomicAdd((unsigned long long*)(a.rv->allocd + (int64_t)d * a.rv->nr + gi), (unsigned long long)rr.add[d]);
+            if (mode >= 0 && d < RD) rec->allocd[d] += rr.add[d];
+          }
+        }
+        dd = (t_rdim == 8) ? rr.dnz[0] : (t_rdim == 9) ? rr.dnz[1] : dd;
+        if (lane == 0) {
+          atomicAdd(a.rv->assigned + gi, 1);
+          if (mode >= 0) rec->assigned += 1;
+        }
+        if (mode < 0) __threadfence();
+        if (rr.now_ineligible) {
+          const uint64_t ncl = mode >= 0 ? rsv_node_classes(lv) : rsv_node_classes(RsvG<true>(*a.rv, node));
+          if (lane == 0) {
+            scls[s] = ncl;
+            atomicExch((unsigned long long*)(a.rv->ncls + node), (unsigned long long)ncl);
+          }
+        }
+        nom_row = a.rv->rowid[gi];
+      }
+      const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+      if (lane < ST_N) {
+        const int64_t v = (take ? podw[t_pw] : 0) + dd;
+        const int64_t v100 = (take ? podw[t_pw100] : 0) + dd * 100;
+        if (take || dd != 0) term_take(row->t[lane], v, v100);
+      } else if (lane == kLaneCounts) {
+        row->pod_count += 1;
+      }
+    }
+    int64_t score_out = score;
+    if (RSV && cfg.rsv) {
+      // the chosen node holds the maximum normalized Reservation score: 100 if hi > 0, else 0
+      const int64_t hi = score / cfg.rsv_F;
+      const int64_t fitla = hi >= kRsvOrderBase ? fitla_pref : score - hi * cfg.rsv_F;
+      score_out = fitla + (hi > 0 ? a.rv->w100 : 0);
+    }
+    uint32_t gminors = 0, rminors = 0;
+    if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
+      // DeviceShare Reserve: allocate the minors on the pre-pod GPU state, add the request per instance
+      PodRec pod = spods[j];
+      pod.flags = pflags;
+      GpuReq g;
+      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g);
+      gminors = __builtin_amdgcn_readfirstlane(dd.minors);
+      rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
+      // used word `lane`: GPU (q, k) for lane < 3 * kGpus, RDMA j = lane - kDevRdmaW after
+      const bool is_gpu = lane < kDevRdmaW;
+      const int k = is_gpu ? lane % kGpus : lane - kDevRdmaW;
+      const uint32_t m = is_gpu ? gminors : rminors;
+      if (lane < DU && ((m >> k) & 1u)) {
+        const int q = lane / kGpus;
+        const int64_t add = !is_gpu ? g.rdma : (q == 0 ? g.core : (q == 1 ? g.mem : g.ratio));
+        const int64_t nv = sdev_use[lane * kDevLdsStride + s] + add;
+        sdev_use[lane * kDevLdsStride + s] = nv;
+        gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
+      }
+    }
+    if ((FEAT & 8) && cfg.numa_pol) {
+      // NodeNUMAResource Reserve on a node with a NUMA policy: Allocate with the Filter's hint on the pre-pod
+      // NUMA state, then addPodAllocation adds it to allocatedResources (node_allocation.go:86-99)
+      const NumaLView nl{snp + s * kNumaSlotWords};
+      PodRec pod = spods[j];
+      pod.flags = pflags;
+      if (nl.policy() != 0 && !(pflags & kPodReqZero)) {
+        const NumaPolOut pr = numa_policy_eval(cfg, pod, nl, 0, 0, 0, 0);
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < kNumaDev; ++k) bits |= (pr.alloc[0][k] != 0 || pr.alloc[1][k] != 0) ? (1u << k) : 0u;
+        const int rr = lane / kNumaDev, kk = lane % kNumaDev;
+        if (lane < 2 * kNumaDev) {
+          int64_t add = 0;
+#pragma unroll
+          for (int q = 0; q < 2 * kNumaDev; ++q) add = (q == lane) ? pr.alloc[q / kNumaDev][q % kNumaDev] : add;
+          if (add != 0) {
+            const int64_t nvv = snp[s * kNumaSlotWords + 2 * kNumaDev + lane] + add;
+            snp[s * kNumaSlotWords + 2 * kNumaDev + lane] = nvv;
+            gst(a.nv->used + ((int64_t)rr * kNumaDev + kk) * a.nv->npad + node, nvv);
+          }
+        } else if (lane == 2 * kNumaDev && bits) {
+          const int64_t meta = snp[s * kNumaSlotWords + 5 * kNumaDev] | ((int64_t)bits << 32);
+          snp[s * kNumaSlotWords + 5 * kNumaDev] = meta;
+          gst(a.nv->present + node, (uint32_t)(meta >> 32));
+        }
+      }
+    }
+    if (cpubind) {
+      // NodeAllocation.addPodAllocation of numCPUsNeeded CPUs: the cpuset millicores A grow, the
+      // amplification offset Amplify(A) - A is re-derived (the CPU ids are chosen by cpuset_kernel)
+      const int64_t A0 = snuma[4 * s], off0 = snuma[4 * s + 1];
+      const double ratio = __longlong_as_double(snuma[4 * s + 2]);
+      const int64_t A1 = A0 + (int64_t)cpu_need * 1000;
+      const int64_t off1 = ratio > 1.0 ? (int64_t)::ceil((double)A1 * ratio) - A1 : 0;
+      if (lane == ST_NCPU) term_take(row->t[ST_NCPU], off1 - off0, (off1 - off0) * 100);
+      if (lane == 0) {
+        snuma[4 * s] = A1;
+        snuma[4 * s + 1] = off1;
+        snuma[4 * s + 3] -= cpu_need;
+        a.cpuset_list[atomicAdd(a.cpuset_n, 1)] = make_int2(cursor0 + j, node);
+      }
+    }
+    if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors, rminors, 0};
+    {
+      const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
+      if (cfg.quota_enable && qrow >= 0) {
+        const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
+        if (lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u)) {
+          // updatePodUsedNoLock -> updateGroupDeltaUsedNoLock (group_quota_manager.go:620-655)
+          const int64_t qreq = pqreq[j * KS_QUOTA_DIMS + lane];
+          const bool np_ = (pflags & KS_POD_NONPREEMPTIBLE) != 0;
+          if (QC) {
+            // LDS atomics: no read-back on the sequential path (the next pod's admission reads after them)
+            for (int32_t cur = qrow; cur >= 0;) {
+              const int32_t up = qlds->parent[cur];
+              atomicAdd((unsigned long long*)&qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane], (unsigned long long)qreq);
+              if (np_) atomicAdd((unsigned long long*)&qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane], (unsigned long long)qreq);
+              cur = up;
+            }
+          } else {
+            for (int32_t cur = qrow; cur >= 0; cur = a.q.parent[cur]) {
+              a.q.used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+              if (np_) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+            }
+          }
+        }
+      }
+    }
+    KS_STAMP(5);
+    }
+  next_pod:
+    if (j + 1 < np) lookahead(j + 1);
+    KS_STAMP(1);
+  }
+  KS_STAMP(6);
+  // ---- write back: results, touched rows, quota usage ----
+  if (lane < processed) a.results[cursor0 + lane] = sres[lane];
+  if (lane < nslots) {
+    const DevNodes d = *a.dn;
+    const SlotRow& r = rows[lane];
+    const int64_t node = snode;
+    gst(d.req_cpu + node, r.t[ST_FREE_CPU].c - r.t[ST_FREE_CPU].h);
+    gst(d.req_mem + node, r.t[ST_FREE_MEM].c - r.t[ST_FREE_MEM].h);
+    gst(d.req_eph + node, r.t[ST_FREE_EPH].c - r.t[ST_FREE_EPH].h);
+    gst(d.nz_cpu + node, term_requested(r.t[ST_CPU]));
+    gst(d.nz_mem + node, term_requested(r.t[ST_MEM]));
+#pragma unroll
+    for (int k = 0; k < KS_MAX_SCALARS; ++k) gst(d.req_sc[k] + node, r.t[ST_FREE_SC + k].c - r.t[ST_FREE_SC + k].h);
+    gst(d.pod_count + node, r.pod_count);
+    gst(d.la_term_cpu + node, term_requested(r.t[ST_LCPU]));
+    gst(d.la_term_mem + node, term_requested(r.t[ST_LMEM]));
+    gst(d.la_pterm_cpu + node, term_requested(r.t[ST_PLCPU]));
+    gst(d.la_pterm_mem + node, term_requested(r.t[ST_PLMEM]));
+    if ((FEAT & 2) && cfg.cpuset) {
+      gst(d.numa_amilli + node, snuma[4 * lane]);
+      gst(d.numa_off + node, snuma[4 * lane + 1]);
+      gst(d.numa_cpus + node, (int32_t)(snuma[4 * lane] / 1000));
+      gst(d.cpu_free + node, (int32_t)snuma[4 * lane + 3]);
+    }
+  }
+  if (QC) {
+    for (int32_t i = lane; i < a.q.q * KS_QUOTA_DIMS; i += 64) {
+      a.q.used[i] = qlds->used[i];
+      a.q.npused[i] = qlds->npused[i];
+    }
+  }
+  if (lane == 0) {
+    *a.cursor = cursor0 + processed;
+    atomicAdd(&a.counters[0], 1ull);
+    if (processed < np) atomicAdd(&a.counters[1], 1ull);
+    atomicAdd(&a.counters[2], (unsigned long long)rescans);
+    atomicAdd(&a.counters[3], (unsigned long long)misses);
+    atomicAdd(&a.counters[15], (unsigned long long)fast);  // ks_stats.diag[7]: monotone fast picks
+#ifdef KS_COMMIT_STAMPS
+    for (int i = 0; i < 7; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
+#endif
+  }
+#undef KS_STAMP
+}
+
+// ---- host launch wrappers (one set per (FEAT, NSC) translation unit of ks_variant.hip) ----
+struct PassLaunch {
+  hipError_t (*sweep)(int blocks, hipStream_t s, const SweepArgs& a);
+  hipError_t (*commit)(bool qc, size_t smem, hipStream_t s, const CommitArgs& a);
+  hipError_t (*commit_attr)(bool qc, size_t smem);
+};
+#define KS_DECLARE_VARIANT(F) PassLaunch pass_launch_f##F##_n0(); PassLaunch pass_launch_f##F##_n2(); PassLaunch pass_launch_f##F##_n4();
+KS_DECLARE_VARIANT(0)
+KS_DECLARE_VARIANT(1)
+KS_DECLARE_VARIANT(3)
+KS_DECLARE_VARIANT(7)
+KS_DECLARE_VARIANT(11)
+KS_DECLARE_VARIANT(15)
+#undef KS_DECLARE_VARIANT
+
+}  // namespace ks

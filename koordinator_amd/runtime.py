@@ -30,8 +30,10 @@ class KsError(RuntimeError):
 
 
 def build(force: bool = False) -> str:
-    """Compile libkoordgpu.so for gfx950 in-tree (hipcc)."""
-    args = ["make", "-s", "-C", CSRC]
+    """Compile libkoordgpu.so for gfx950 in-tree (hipcc; the kernel variants are separate objects, built in
+    parallel)."""
+    jobs = max(1, min(16, os.cpu_count() or 1))
+    args = ["make", "-s", f"-j{jobs}", "-C", CSRC]
     if force:
         args.append("-B")
     subprocess.check_call(args)
