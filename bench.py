@@ -1,25 +1,28 @@
 #!/usr/bin/env python3
 """bench.py — koord-scheduler sweep on MI355X: pods scheduled/sec + node-evals/sec.
 
-Default workload (N=1): BASELINE.json configs[1] = "C2": 10k pods onto a 5k-node
-synthetic cluster with NodeResourcesFit + LoadAwareScheduling + ElasticQuota
-admission, percentageOfNodesToScore=100, lowest-index tie-break.  One "step" =
-schedule the whole 10k-pod queue, one pod at a time semantically (sweep ->
-select -> commit passes on the device), starting from the same snapshot
-(``ks_restore`` of a device-side checkpoint, included in the timed region).
-Inputs are staged in HBM before the timed region.
+Headline (``value``): BASELINE.json configs[1] = "C2": 10k pods onto a 5k-node synthetic cluster with
+NodeResourcesFit + LoadAwareScheduling + ElasticQuota admission, percentageOfNodesToScore=100, lowest-index
+tie-break.  One "step" = schedule the whole 10k-pod queue, one pod at a time semantically: restore the
+snapshot (``ks_restore`` of a device-side checkpoint), the pods' PreFilter / EstimatePod work
+(``prep_pods_kernel``), then the sweep -> select -> commit passes.  The raw pod columns are staged in HBM
+before the timed region (host -> HBM copies are not timed; everything computed from them is).
 
-Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU, each
-rank schedules its own C2 replica (seed + rank): replicas only, weak scaling —
-the 5k-node C2 cluster does not warrant node sharding.
+The metric names 5k AND 100k nodes, so the same line carries ``c5``: configs[4] (1M pods x 100k nodes,
+Fit + LoadAware) timed the same way — on one GPU at N=1, node-sharded over the N ranks at N>1 (strong
+scaling: every rank sweeps its node range, one RCCL allgather of per-shard candidates per pass).
 
-rank 0 prints ONE JSON line.  The timed steps run with the library's per-kernel HIP
-events off (they add a dispatch gap between the pass kernels, ~19 % at C2); the same
-number of steps is then re-run with the events on (``profiled_steps``) for the
-kernel split.  Extra fields: ``roofline`` for the sweep (scoring) kernel from those
-per-launch HIP events, ``cpu_baseline`` from the CPU
-oracle (oracle/koord_oracle.c, the reference's 16-worker Parallelizer shape)
-on the same workload, and ``parity`` = GPU placements == oracle placements.
+Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU.  ``value`` at N>1 is N
+independent C2 replicas (seed + rank; weak scaling: the 5k-node cluster does not warrant node sharding,
+DESIGN.md §6); the ``c5`` record is the sharded 100k-node cluster.
+
+rank 0 prints ONE JSON line.  Timed steps run with the library's per-kernel HIP events off (they add a
+dispatch gap between the pass kernels); the same number of steps is then re-run with the events on
+(``profiled_steps``) for the kernel split, ``roofline`` (the sweep kernel, HBM bound) and
+``roofline.commit`` (the sequential commit kernel).  ``cpu_baseline``: the CPU oracle (oracle/koord_oracle.c,
+the reference's 16-worker Parallelizer shape) on a bounded sample of the same workload at 16 threads, with
+1 and all-usable-host-core runs next to it (``by_threads``); ``parity`` = GPU results == oracle results on
+that sample.
 """
 from __future__ import annotations
 
@@ -35,38 +38,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GPU_CLOCK_GHZ = 2.4    # MI355X peak engine clock (MI355X_MICROARCH.md): commit cycles/pod are quoted at it
+METRIC = "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k nodes"
 
 
 def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
 
-    if n_pods:
-        return getattr(synth, name)(seed=seed, n_pods=n_pods)
+    if name not in ("c1", "c2", "c3", "c4", "c5"):
+        raise SystemExit(f"unknown config {name}")
+    fn = getattr(synth, name)
+    return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
-    if name == "c2":
-        return synth.c2(seed=seed)
-    if name == "c1":
-        return synth.c1(seed=seed)
-    if name == "c3":
-        return synth.c3(seed=seed)
-    if name == "c4":
-        return synth.c4(seed=seed)
-    if name == "c5":
-        return synth.c5(seed=seed)  # BASELINE configs[4]: 1M pods x 100k nodes
-    raise SystemExit(f"unknown config {name}")
+
+def newest_profile(pattern: str):
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
 def pmc_traffic(config: str, kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary for this config
     (profiles/rNN_<config>_traffic.json, written by tools/pmc_traffic.sh + tools/traffic.py from
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command); None when absent."""
-    import glob
-
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", f"r*_{config}_traffic.json")))
-    if not files:
+    t, src = newest_profile(f"r*_{config}_traffic.json")
+    if t is None:
         return None, None
-    with open(files[-1]) as f:
-        t = json.load(f)
     n = b = 0
     for k, v in t.get("kernels", {}).items():
         if kernel in k:
@@ -74,21 +75,16 @@ def pmc_traffic(config: str, kernel: str):
             b += v["hbm_bytes_per_launch"] * v["launches"]
     if not n:
         return None, None
-    return round(b / n), os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    return round(b / n), src
 
 
 def pmc_valu(config: str, kernel: str):
-    """VALU-issue floor per launch of `kernel` (us) from the newest committed PMC summary for this
-    config (profiles/rNN_<config>_valu.json, tools/pmc_valu.sh + tools/valu.py: SQ_INSTS_VALU x 2 cycles
+    """VALU-issue floor per launch of `kernel` (us) from the newest committed PMC summary for this config
+    (profiles/rNN_<config>_valu.json, tools/pmc_valu.sh + tools/valu.py: SQ_INSTS_VALU x 2 cycles
     over 1024 SIMDs at 2.4 GHz); None when absent."""
-    import glob
-
-    here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_{config}_valu.json")))
-    if not files:
+    t, src = newest_profile(f"r*_{config}_valu.json")
+    if t is None:
         return None, None
-    with open(files[-1]) as f:
-        t = json.load(f)
     n = us = 0.0
     for k, v in t.get("kernels", {}).items():
         if kernel in k and "valu_issue_floor_us" in v:
@@ -96,64 +92,251 @@ def pmc_valu(config: str, kernel: str):
             us += v["valu_issue_floor_us"] * v["launches"]
     if not n:
         return None, None
-    return us / n, os.path.relpath(files[-1], here)
+    return us / n, src
 
 
-def cpu_baseline(w, gpu_res, budget_s: float):
-    """Time the CPU oracle (port of the reference loop) on a bounded prefix of the workload."""
-    from oracle.oracle import Oracle
-
-    threads = int(os.environ.get("KS_CPU_THREADS", "16"))
-    threads = max(1, min(threads, os.cpu_count() or 1))
-    # estimate the prefix that fits the budget from a short probe
-    probe = min(w.pods.n, 500)
-    rs = w.reservations
-    dv = w.devices
-    o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None,
-               cpu_state=w.cpus.copy() if w.cpus is not None else None)
-    t = time.perf_counter()
-    r_probe = o.schedule(w.pods.rows(range(probe)))
-    dt = time.perf_counter() - t
-    o.close()
-    n_sample = w.pods.n if dt * w.pods.n / probe <= budget_s else max(probe, int(budget_s * probe / dt))
-    o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None,
-               cpu_state=w.cpus.copy() if w.cpus is not None else None)
-    t = time.perf_counter()
-    r = o.schedule(w.pods.rows(range(n_sample)))
-    dt = time.perf_counter() - t
-    cs = o.fetch_cpusets(n_sample) if w.cpus is not None else None
-    o.close()
-    parity = bool(np.array_equal(r["node"], gpu_res["node"][:n_sample])
-                  and np.array_equal(r["status"], gpu_res["status"][:n_sample])
-                  and np.array_equal(r["score"], gpu_res["score"][:n_sample])
-                  and np.array_equal(r["reservation"], gpu_res["reservation"][:n_sample])
-                  and np.array_equal(r["gpu_minors"], gpu_res["gpu_minors"][:n_sample])
-                  and np.array_equal(r["rdma_minors"], gpu_res["rdma_minors"][:n_sample])
-                  and (cs is None or np.array_equal(cs, gpu_res["cpusets"][:n_sample])))
-    cpu_model = ""
+def host_cpus():
+    """(CPU model, CPUs this process may run on): the affinity mask, capped by a cgroup-v2 cpu.max quota."""
+    model = ""
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
+                    model = line.split(":", 1)[1].strip()
                     break
     except OSError:
         pass
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return model, n
+
+
+def time_oracle(w, threads: int, n_pods: int):
+    from oracle.oracle import Oracle
+
+    rs, dv, cs = w.reservations, w.devices, w.cpus
+    o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
+               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None,
+               cpu_state=cs.copy() if cs is not None else None)
+    try:
+        t = time.perf_counter()
+        r = o.schedule(w.pods.rows(range(n_pods)))
+        dt = time.perf_counter() - t
+        if cs is not None:
+            r["cpusets"] = o.fetch_cpusets(n_pods)
+    finally:
+        o.close()
+    return r, dt
+
+
+def sample_size(w, threads: int, budget_s: float) -> int:
+    """Pods of a bounded prefix sized from a short probe so the timed oracle run takes about budget_s."""
+    probe = min(w.pods.n, 300)
+    _, dt = time_oracle(w, threads, probe)
+    if dt * w.pods.n / probe <= budget_s:
+        return w.pods.n
+    return max(probe, int(budget_s * probe / max(dt, 1e-9)))
+
+
+def cpu_baseline(w, gpu_res, budget_s: float, extra_budget_s: float):
+    """The CPU oracle (port of the reference loop) on bounded prefixes of the workload: 16 threads (the
+    reference Parallelizer's default, the headline baseline) plus 1 thread and every usable host core."""
+    model, ncpu = host_cpus()
+    n16 = sample_size(w, 16, budget_s)
+    r, dt = time_oracle(w, 16, n16)
+    keys = ("node", "status", "score", "reservation", "gpu_minors", "rdma_minors")
+    parity = all(np.array_equal(r[k], gpu_res[k][:n16]) for k in keys)
+    if "cpusets" in r:
+        parity = parity and np.array_equal(r["cpusets"], gpu_res["cpusets"][:n16])
+    by_threads = {"16": {"pods_per_s": round(n16 / dt, 1), "sample_pods": n16}}
+    for th in sorted({1, ncpu} - {16}):
+        if extra_budget_s <= 0:
+            break
+        n = sample_size(w, th, extra_budget_s)
+        _, d = time_oracle(w, th, n)
+        by_threads[str(th)] = {"pods_per_s": round(n / d, 1), "sample_pods": n}
     return {
-        "value": round(n_sample / dt, 1),
+        "value": round(n16 / dt, 1),
         "unit": "pods/s",
-        "cores": threads,
+        "cores": 16,
         "kind": "port",
-        "sample": f"first {n_sample} of {w.pods.n} pods of {w.name} ({w.nodes.n} nodes), same inputs as the GPU run; "
+        "sample": f"first {n16} of {w.pods.n} pods of {w.name} ({w.nodes.n} nodes), same inputs as the GPU run; "
                   f"CPU restatement with the reference Parallelizer shape (16 workers, chunk=min(sqrt(n),n/16+1)); "
                   f"omits Go map/Quantity/lister overheads, so it is a faster-than-reference baseline",
-        "node_evals_per_s": round(n_sample * w.nodes.n / dt, 1),
-        "host_cpu": cpu_model,
+        "node_evals_per_s": round(n16 * w.nodes.n / dt, 1),
+        "by_threads": by_threads,
+        "host_cpu": model,
+        "host_usable_cpus": ncpu,
         "host_nproc": os.cpu_count(),
-        "parity_with_gpu_on_sample": parity,
+        "parity_with_gpu_on_sample": bool(parity),
     }
+
+
+def sweep_algo_bytes(w, prof, local_nodes: int) -> int:
+    """Algorithmic bytes per sweep launch: SURVEY §8(d)'s B_node (LoadAware + Fit columns, each read once
+    per pass: 106 B, +16 B with the prod-usage score term, +32 B for the batch-cpu / batch-memory scalar
+    columns) x the nodes one launch sweeps, + the pass's pod records + the chunk-maxima output."""
+    b_node = 106 + (16 if prof.loadaware is not None and prof.loadaware.score_according_prod_usage else 0) + 32
+    algo = local_nodes * b_node + 64 * 128 + ((local_nodes + 63) // 64) * 64 * 4
+    if w.devices is not None:
+        # + NUMA amplification columns (16 B) and the device table (flags + 34 total / topology words +
+        # 32 used words, int64; ks_dev.h)
+        algo += local_nodes * (16 + 4 + (34 + 32) * 8)
+    if w.reservations is not None:
+        # + the owner-class column and the reservation table (CSR offsets, classes, meta, order rank,
+        # allocatable/allocated x7, assigned, reserve-pod non-zero x2) read once
+        algo += local_nodes * (8 + 4) + w.reservations.r * (8 + 4 + 4 + 7 * 8 * 2 + 4 + 16)
+    return algo
+
+
+def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: bool, steps: int, warmup: int,
+               cfg_key: str, profile: bool):
+    """Time `steps` scheduling steps of workload w on this rank (max over ranks); then the same steps with
+    the per-kernel events on for the split.  Returns (record fields, gpu results)."""
+    from koordinator_amd import abi, runtime
+
+    prof = w.profile
+    prof.device = local_rank if world > 1 else 0
+    prof.batch_pods = args.batch_pods
+    prof.candidates = args.candidates
+    cfg = prof.to_ks_config()
+    cfg.profile = 0
+    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices, w.cpus)
+    try:
+        nshards = 1
+        if shard and world > 1:
+            box = [runtime.shard_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            ev.shard(world, rank, box[0], args.vshards)
+            nshards = world
+        elif args.vshards > 1:
+            ev.shard(1, 0, None, args.vshards)
+        ev.stage(w.pods)
+        ev.checkpoint()
+
+        def sync():
+            if dist is not None:
+                import torch
+
+                torch.cuda.synchronize()
+                dist.barrier()
+
+        ev.set_profile(False)
+        for _ in range(warmup):
+            ev.restore()
+            ev.schedule_staged()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ev.restore()
+            ev.schedule_staged()
+        sync()
+        elapsed = time.perf_counter() - t0
+        st_last = ev.stats()
+        agg = {"sweep_ms": 0.0, "select_ms": 0.0, "commit_ms": 0.0, "sweep_launches": 0, "passes": 0,
+               "cut_passes": 0, "rescans": 0}
+        prof_elapsed = 0.0
+        sweep_bytes = 0
+        if profile:
+            ev.set_profile(True)
+            for _ in range(steps):
+                ev.restore()
+                tp = time.perf_counter()
+                ev.schedule_staged()
+                prof_elapsed += time.perf_counter() - tp
+                st = ev.stats()
+                for k in agg:
+                    agg[k] += st[k]
+                sweep_bytes = st["sweep_bytes"]
+            ev.set_profile(False)
+        else:
+            for k in ("passes", "cut_passes", "rescans"):
+                agg[k] = st_last[k] * steps
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        res = ev.fetch()
+        if w.cpus is not None:
+            res["cpusets"] = ev.fetch_cpusets(w.pods.n)
+    finally:
+        ev.close()
+
+    n_pods, n_nodes = w.pods.n, w.nodes.n
+    units = n_pods * steps * (1 if shard else world)  # replicas each schedule their own queue
+    value = units / elapsed
+    rec = {
+        "value": round(value, 1),
+        "unit": "pods/s",
+        "ms_per_step": round(elapsed * 1000.0 / steps, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "node_evals_per_s": round(value * n_nodes, 1),
+        "pods_per_step": n_pods,
+        "nodes": n_nodes,
+        "placed_per_step": int((res["status"] == 0).sum()),
+        "into_reservations_per_step": int((res["reservation"] >= 0).sum()),
+        "gpu_pods_placed_per_step": int((res["gpu_minors"] != 0).sum()),
+        "rdma_pods_placed_per_step": int((res["rdma_minors"] != 0).sum()),
+        "cpuset_pods_placed_per_step": int(((res["status"] == 0) & ((w.pods.flags & abi.KS_POD_CPU_BIND) != 0)).sum()),
+        "profiled_steps": steps if profile else 0,
+        "ms_per_profiled_step": round(prof_elapsed * 1000.0 / steps, 3) if profile else None,
+        "passes_per_step": agg["passes"] / steps,
+        "cut_passes_per_step": agg["cut_passes"] / steps,
+        "rescans_per_step": agg["rescans"] / steps,
+        "kernel_ms_per_step": {"sweep": round(agg["sweep_ms"] / steps, 3), "select": round(agg["select_ms"] / steps, 3),
+                               "commit": round(agg["commit_ms"] / steps, 3)},
+        "roofline": None,
+    }
+    if profile and agg["sweep_launches"]:
+        avg_s = agg["sweep_ms"] / agg["sweep_launches"] / 1000.0
+        local_nodes = n_nodes // nshards  # one rank sweeps its shard
+        algo = sweep_algo_bytes(w, prof, local_nodes)
+        achieved = algo / avg_s / 1e9
+        traffic, traffic_src = pmc_traffic(cfg_key, "sweep_kernel")
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
+                "kernel": "sweep_kernel", "avg_launch_us": round(avg_s * 1e6, 3),
+                "algorithmic_bytes_per_launch": algo, "bytes_incl_pod_group_rereads": sweep_bytes}
+        floor_us, valu_src = pmc_valu(cfg_key, "sweep_kernel")
+        if floor_us is not None and world == 1:
+            # the sweep's instruction-issue bound next to the HBM one (DESIGN.md §4)
+            roof["valu_issue"] = {"floor_us": round(floor_us, 3), "frac": round(floor_us / (avg_s * 1e6), 4),
+                                  "source": valu_src}
+        # the sequential commit kernel (one launch per pass): SURVEY §8(d) counts its traffic as P x B_node
+        passes = max(agg["passes"], 1)
+        commit_s = agg["commit_ms"] / 1000.0
+        pods_per_launch = n_pods * steps / passes
+        c_algo = int(round(pods_per_launch * 138))
+        c_traffic, c_src = pmc_traffic(cfg_key, "commit_kernel")
+        step_kernels = agg["sweep_ms"] + agg["select_ms"] + agg["commit_ms"]
+        roof["commit"] = {
+            "kernel": "commit_kernel", "bound": "latency (one wave walks the pass's pods in queue order)",
+            "avg_launch_us": round(commit_s / passes * 1e6, 3), "pods_per_launch": round(pods_per_launch, 2),
+            "cycles_per_pod": round(commit_s * GPU_CLOCK_GHZ * 1e9 / (n_pods * steps), 1),
+            "share_of_kernel_time": round(agg["commit_ms"] / step_kernels, 4) if step_kernels else None,
+            "algorithmic_bytes_per_launch": c_algo, "traffic": c_traffic, "traffic_source": c_src,
+            "traffic_over_algorithmic": round(c_traffic / c_algo, 2) if c_traffic else None,
+            "achieved_gbs": round(c_algo / (commit_s / passes) / 1e9, 3),
+        }
+        rec["roofline"] = roof
+    return rec, res
+
+
+def workload_desc(w):
+    return (f"{w.name}: {w.pods.n} pods x {w.nodes.n} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
+            f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
+            + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else "")
+            + (" + NodeNUMAResource(amplified CPUs, cpuset pods, NUMA topology policies) + DeviceShare(8 GPUs x 80GiB + 4 RDMA on"
+               " 4 PCIe/2 NUMA per node, joint GPU+RDMA)" if w.devices is not None else ""))
 
 
 def main():
@@ -167,11 +350,15 @@ def main():
     ap.add_argument("--candidates", type=int, default=0)
     ap.add_argument("--no-profile", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0, help="16-thread oracle sample (per config)")
+    ap.add_argument("--cpu-extra-budget-s", type=float, default=6.0, help="1-thread / all-core oracle samples")
     ap.add_argument("--shard", action="store_true",
-                    help="shard the nodes over the ranks (RCCL allgather of per-shard candidates, SURVEY §8e); "
-                         "default for --gpus N is N independent replicas")
+                    help="shard the main config's nodes over the ranks (default for --gpus N: N independent replicas)")
     ap.add_argument("--vshards", type=int, default=1, help="virtual shards per GPU (exercises the merge on one GPU)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the 100k-node c5 record")
+    ap.add_argument("--c5-pods", type=int, default=1_000_000)
+    ap.add_argument("--c5-steps", type=int, default=1)
+    ap.add_argument("--c5-warmup", type=int, default=1)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,154 +372,57 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from koordinator_amd import abi, runtime
-
     # replicas schedule their own cluster (seed + rank); shards split one shared cluster
     w = build_workload(args.config, seed=20261015 + (0 if args.shard else rank), n_pods=args.pods)
-    prof = w.profile
-    prof.device = local_rank if world > 1 else 0
-    prof.batch_pods = args.batch_pods
-    prof.candidates = args.candidates
-    cfg = prof.to_ks_config()
-    cfg.profile = 0
-    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices, w.cpus)
-    if args.shard or args.vshards > 1:
-        uid = None
-        if world > 1:
-            box = [runtime.shard_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(box, src=0)
-            uid = box[0]
-        ev.shard(world if args.shard else 1, rank if args.shard else 0, uid, args.vshards)
-    ev.stage(w.pods)
-    ev.checkpoint()
-
-    def sync():
-        if dist is not None:
-            import torch
-
-            torch.cuda.synchronize()
-            dist.barrier()
-
-    # the timed steps run without the per-kernel HIP events (they add a dispatch gap between the pass
-    # kernels); the kernel split and the roofline come from the same number of profiled steps afterwards
-    ev.set_profile(False)
-    for _ in range(args.warmup):
-        ev.restore()
-        ev.schedule_staged()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ev.restore()
-        ev.schedule_staged()
-    sync()
-    elapsed = time.perf_counter() - t0
-    st_last = ev.stats()
-    agg = {"sweep_ms": 0.0, "select_ms": 0.0, "commit_ms": 0.0, "sweep_launches": 0, "passes": 0, "cut_passes": 0,
-           "rescans": 0}
-    sweep_bytes = 0
-    prof_elapsed = 0.0
-    if not args.no_profile:
-        ev.set_profile(True)
-        for _ in range(args.steps):
-            ev.restore()
-            tp = time.perf_counter()
-            ev.schedule_staged()
-            prof_elapsed += time.perf_counter() - tp
-            st = ev.stats()
-            for k in agg:
-                agg[k] += st[k]
-            sweep_bytes = st["sweep_bytes"]
-    else:
-        for k in ("passes", "cut_passes", "rescans"):
-            agg[k] = st_last[k] * args.steps
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    res = ev.fetch()
-    if w.cpus is not None:
-        res["cpusets"] = ev.fetch_cpusets(w.pods.n)
-
-    n_pods, n_nodes = w.pods.n, w.nodes.n
-    total_pods = n_pods * args.steps * (1 if args.shard else world)
-    value = total_pods / elapsed
-    ms_per_step = elapsed * 1000.0 / args.steps
+    rec, res = run_config(w, args, dist, world, rank, local_rank, args.shard, args.steps, args.warmup, args.config,
+                          not args.no_profile)
     out = None
     if rank == 0:
-        roofline = None
-        if agg["sweep_launches"]:
-            avg_s = agg["sweep_ms"] / agg["sweep_launches"] / 1000.0
-            # algorithmic bytes per sweep launch: SURVEY §8(d)'s B_node (LoadAware + Fit columns, each read
-            # once per pass: 106 B, +16 B with the prod-usage score term, +32 B for the batch-cpu / batch-memory
-            # scalar columns) x the nodes one launch sweeps, + the pass's pod records + the chunk-maxima output
-            b_node = 106 + (16 if prof.loadaware is not None and prof.loadaware.score_according_prod_usage else 0) + 32
-            local_nodes = n_nodes // (world if args.shard else 1)  # one rank sweeps its shard
-            algo = local_nodes * b_node + 64 * 128 + ((local_nodes + 63) // 64) * 64 * 4
-            if w.devices is not None:
-                # + NUMA amplification columns (16 B) and the device table (flags + 34 total / topology words +
-                # 32 used words, int64; ks_dev.h)
-                algo += local_nodes * (16 + 4 + (34 + 32) * 8)
-            if w.reservations is not None:
-                # + the owner-class column and the reservation table (CSR offsets, classes, meta, order rank,
-                # allocatable/allocated x7, assigned, reserve-pod non-zero x2) read once
-                algo += local_nodes * (8 + 4) + w.reservations.r * (8 + 4 + 4 + 7 * 8 * 2 + 4 + 16)
-            achieved = algo / avg_s / 1e9
-            traffic, traffic_src = pmc_traffic(args.config, "sweep_kernel")
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
-                        "kernel": "sweep_kernel", "avg_launch_us": round(avg_s * 1e6, 3),
-                        "algorithmic_bytes_per_launch": algo, "bytes_incl_pod_group_rereads": sweep_bytes}
-            floor_us, valu_src = pmc_valu(args.config, "sweep_kernel")
-            if floor_us is not None and world == 1:
-                # the sweep's instruction-issue bound next to the HBM one
-                roofline["valu_issue"] = {"floor_us": round(floor_us, 3),
-                                          "frac": round(floor_us / (avg_s * 1e6), 4), "source": valu_src}
         out = {
-            "metric": "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k nodes",
-            "value": round(value, 1),
+            "metric": METRIC,
+            "value": rec["value"],
             "unit": "pods/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step": rec["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong" if args.shard else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
-            "config": {"workload": f"{w.name}: {n_pods} pods x {n_nodes} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
-                                   f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
-                                   + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else "")
-                                   + (" + NodeNUMAResource(amplified CPUs, cpuset pods) + DeviceShare(8 GPUs x 80GiB + 4 RDMA on 4 PCIe/2 NUMA per node, joint GPU+RDMA)" if w.devices is not None else ""),
-                       "pods_per_step": n_pods, "nodes": n_nodes, "percentage_of_nodes_to_score": 100,
+            "config": {"workload": workload_desc(w), "pods_per_step": w.pods.n, "nodes": w.nodes.n,
+                       "percentage_of_nodes_to_score": 100,
                        "parallelism": (f"node-shards{world}x{args.vshards}" if args.shard or args.vshards > 1
                                        else (f"replicas{world}" if world > 1 else "single-gpu")),
-                       "batch_pods": cfg.batch_pods or 64, "candidates": cfg.candidates or 32},
-            "node_evals_per_s": round(value * n_nodes, 1),
-            "placed_per_step": int((res["status"] == 0).sum()),
-            "into_reservations_per_step": int((res["reservation"] >= 0).sum()),
-            "gpu_pods_placed_per_step": int((res["gpu_minors"] != 0).sum()),
-            "rdma_pods_placed_per_step": int((res["rdma_minors"] != 0).sum()),
-            "cpuset_pods_placed_per_step": int(((res["status"] == 0) & ((w.pods.flags & abi.KS_POD_CPU_BIND) != 0)).sum()),
-            "profiled_steps": 0 if args.no_profile else args.steps,
-            "ms_per_profiled_step": round(prof_elapsed * 1000.0 / args.steps, 3) if not args.no_profile else None,
-            "passes_per_step": agg["passes"] / args.steps,
-            "cut_passes_per_step": agg["cut_passes"] / args.steps,
-            "rescans_per_step": agg["rescans"] / args.steps,
-            "kernel_ms_per_step": {"sweep": round(agg["sweep_ms"] / args.steps, 3),
-                                   "select": round(agg["select_ms"] / args.steps, 3),
-                                   "commit": round(agg["commit_ms"] / args.steps, 3)},
-            "roofline": roofline,
-            "cpu_baseline": None,
+                       "batch_pods": args.batch_pods or 64, "candidates": args.candidates or 32,
+                       "timed_region": "restore snapshot + PreFilter/EstimatePod (prep_pods_kernel) + sweep/select/commit "
+                                       "passes; raw pod columns staged in HBM beforehand"},
         }
+        out.update({k: v for k, v in rec.items() if k not in ("value", "unit", "ms_per_step", "steps", "warmup")})
+        out["cpu_baseline"] = None
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(w, res, args.cpu_budget_s)
+            cb = cpu_baseline(w, res, args.cpu_budget_s, args.cpu_extra_budget_s)
             out["cpu_baseline"] = cb
             out["parity"] = cb["parity_with_gpu_on_sample"]
-            out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 2)
-    ev.close()
+            out["speedup_vs_cpu_baseline"] = round(rec["value"] / cb["value"], 2)
+    del w, res
+
+    if not args.no_c5 and args.config != "c5":
+        # the metric's 100k-node configuration: one GPU at N=1, node-sharded over the ranks at N>1
+        w5 = build_workload("c5", seed=20261015, n_pods=args.c5_pods)
+        r5, res5 = run_config(w5, args, dist, world, rank, local_rank, True, args.c5_steps, args.c5_warmup, "c5",
+                              not args.no_profile)
+        if rank == 0:
+            r5["workload"] = workload_desc(w5)
+            r5["scaling"] = "strong"
+            r5["parallelism"] = f"node-shards{world}" if world > 1 else "single-gpu"
+            if world == 1 and not args.no_cpu_baseline:
+                cb5 = cpu_baseline(w5, res5, args.cpu_budget_s, args.cpu_extra_budget_s)
+                r5["cpu_baseline"] = cb5
+                r5["parity"] = cb5["parity_with_gpu_on_sample"]
+                r5["speedup_vs_cpu_baseline"] = round(r5["value"] / cb5["value"], 2)
+            out["c5"] = r5
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -561,7 +561,10 @@ int ks_refresh_quota_runtime(ks_ctx *ctx, const ks_quota_tree *tree, int32_t q, 
 int ks_schedule(ks_ctx *ctx, const ks_pod_cols *pods, int32_t p, ks_result *out);
 
 /* Device-resident variant: stage pods once (host buffers copied to HBM), then
- * schedule the staged batch; results stay in HBM until ks_fetch_results. */
+ * schedule the staged batch; results stay in HBM until ks_fetch_results.  Every
+ * ks_schedule_staged call starts from the staged columns (the pods' PreFilter work — request
+ * vectors, EstimatePod, flags — runs on the device as part of the call), so a staged queue can be
+ * scheduled repeatedly (e.g. after ks_restore). */
 int ks_stage_pods(ks_ctx *ctx, const ks_pod_cols *pods, int32_t p);
 int ks_schedule_staged(ks_ctx *ctx);
 int ks_fetch_results(ks_ctx *ctx, ks_result *out, int32_t p);

@@ -757,6 +757,15 @@ struct Col {
 
 }  // namespace
 
+struct PodStage {
+  void* blob = nullptr;
+  int32_t cap = 0;
+  PodRec* recs = nullptr;       // [cap] built by prep_pods_kernel
+  ks_result* results = nullptr; // [cap]
+  DevPodCols cols{};            // the caller's columns in HBM
+  DevPodQuota pq{};             // quota request columns (read by the commit kernel)
+};
+
 struct ks_ctx {
   ks_config cfg{};
   Cfg kc{};
@@ -777,12 +786,9 @@ struct ks_ctx {
   int64_t* quota_used_ckpt = nullptr;
   int64_t* quota_npused_ckpt = nullptr;
   // pods
-  int32_t np = 0, pod_cap = 0;
-  PodRec* pods = nullptr;
-  DevPodQuota pq{};
-  void* pod_blob = nullptr;
-  DevPodCols pstage{};
-  ks_result* results = nullptr;
+  int32_t np = 0;
+  PodStage st{};   // staged pods of ks_stage_pods / ks_schedule
+  PodStage est{};  // single-pod evaluation (ks_eval_pod_debug)
   // pass scratch
   uint2* sweep_out = nullptr;
   uint32_t* cand_chunk = nullptr;
@@ -837,8 +843,6 @@ struct ks_ctx {
   int64_t* numa_used_ckpt = nullptr;
   uint32_t* numa_present_ckpt = nullptr;
   int64_t numa_policy_nodes = 0;  // nodes with a NUMA topology policy
-  // debug
-  PodRec* dbg_pod = nullptr;
   // stats
   ks_stats stats{};
   std::vector<hipEvent_t> ev_pool;
@@ -1022,8 +1026,6 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->cursor = (int32_t*)p;
   if (dev_alloc(ctx, &p, 256) != KS_OK) goto fail;
   ctx->counters = (unsigned long long*)p;
-  if (dev_alloc(ctx, &p, sizeof(PodRec)) != KS_OK) goto fail;
-  ctx->dbg_pod = (PodRec*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
   ctx->dev_M = (unsigned long long*)p;
   *out = ctx;
@@ -1041,7 +1043,8 @@ void ks_destroy(ks_ctx* ctx) {
   dev_free(ctx->ckpt_blob);
   dev_free(ctx->quota_blob);
   void* p;
-  p = ctx->pod_blob; dev_free(p);
+  dev_free(ctx->st.blob);
+  dev_free(ctx->est.blob);
   p = ctx->sweep_out; dev_free(p);
   p = ctx->cand_chunk; dev_free(p);
   p = ctx->cand_t; dev_free(p);
@@ -1053,7 +1056,6 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->cand_count; dev_free(p);
   p = ctx->cursor; dev_free(p);
   p = ctx->counters; dev_free(p);
-  p = ctx->dbg_pod; dev_free(p);
   p = ctx->rowcols; dev_free(p);
   p = ctx->dnodes; dev_free(p);
   p = ctx->drv; dev_free(p);
@@ -2109,9 +2111,14 @@ int ks_refresh_quota_runtime(ks_ctx* ctx, const ks_quota_tree* t, int32_t nq, in
   return KS_OK;
 }
 
-static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
-  if (p <= ctx->pod_cap && ctx->pod_blob) return KS_OK;
-  dev_free(ctx->pod_blob);
+// Pod staging area: the raw pod columns as the caller gave them (HBM) and the PodRec / result arrays built from
+// them.  The schedule's own stage (ctx->st) is rebuilt into PodRec by prep_pods_kernel at the start of every
+// ks_schedule_staged (PreFilter / EstimatePod work is part of the scheduling call); single-pod evaluation has its
+// own stage (ctx->est) so it never disturbs staged pods.
+static int ensure_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
+  if (p <= st.cap && st.blob) return KS_OK;
+  dev_free(st.blob);
+  st.cap = 0;
   const int32_t cap = std::max<int32_t>(p, 64);
   const size_t rec = (size_t)cap * sizeof(PodRec);
   const size_t res = ((size_t)cap * sizeof(ks_result) + 255) / 256 * 256;
@@ -2120,13 +2127,13 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
   // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 rdma qreq[8] = 27 int64 cols; flags quota qmask rsv_class
   // cpu_bind joint(u8) = 6 x32
   const size_t bytes = rec + res + col8 * 27 + col4 * 6;
-  if (dev_alloc(ctx, &ctx->pod_blob, bytes) != KS_OK) return KS_ENOMEM;
-  char* b = (char*)ctx->pod_blob;
-  ctx->pods = (PodRec*)b;
+  if (dev_alloc(ctx, &st.blob, bytes) != KS_OK) return KS_ENOMEM;
+  char* b = (char*)st.blob;
+  st.recs = (PodRec*)b;
   b += rec;
-  ctx->results = (ks_result*)b;
+  st.results = (ks_result*)b;
   b += res;
-  DevPodCols& s = ctx->pstage;
+  DevPodCols& s = st.cols;
   int64_t** c8[] = {&s.cpu, &s.mem, &s.eph, &s.nzcpu, &s.nzmem, &s.sc[0], &s.sc[1], &s.sc[2], &s.sc[3],
                     &s.la_req_cpu, &s.la_lim_cpu, &s.la_dflt_cpu, &s.la_req_mem, &s.la_lim_mem, &s.la_dflt_mem,
                     &s.gpu_core, &s.gpu_mem, &s.gpu_ratio, &s.rdma};
@@ -2135,27 +2142,27 @@ static int ensure_pod_capacity(ks_ctx* ctx, int32_t p) {
     b += col8;
   }
   for (int d = 0; d < KS_QUOTA_DIMS; ++d) {
-    ctx->pq.req[d] = (int64_t*)b;
+    st.pq.req[d] = (int64_t*)b;
     b += col8;
   }
   s.flags = (uint32_t*)b;
   b += col4;
   s.quota = (int32_t*)b;
   b += col4;
-  ctx->pq.mask = (uint32_t*)b;
+  st.pq.mask = (uint32_t*)b;
   b += col4;
   s.rsv_class = (int32_t*)b;
   b += col4;
   s.cpu_bind = (uint32_t*)b;
   b += col4;
   s.joint = (uint8_t*)b;
-  ctx->pod_cap = cap;
+  st.cap = cap;
   return KS_OK;
 }
 
-static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* dst) {
-  // copy host columns into the staging area, then build PodRec on device
-  DevPodCols& s = ctx->pstage;
+// host columns -> the stage's HBM columns (async on the ctx stream)
+static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t p) {
+  DevPodCols& s = st.cols;
   auto cp8 = [&](int64_t* d, const int64_t* h) -> hipError_t {
     if (h) return hipMemcpyAsync(d, h, (size_t)p * 8, hipMemcpyHostToDevice, ctx->stream);
     return hipMemsetAsync(d, 0, (size_t)p * 8, ctx->stream);
@@ -2178,20 +2185,26 @@ static int stage_pods_to(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p, PodRec* 
   HIPCHK(ctx, cp8(s.rdma, pc->rdma));
   if (pc->joint) HIPCHK(ctx, hipMemcpyAsync(s.joint, pc->joint, (size_t)p, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.joint, 0, (size_t)p, ctx->stream));
-  for (int d = 0; d < KS_QUOTA_DIMS; ++d) HIPCHK(ctx, cp8(ctx->pq.req[d], pc->quota_req[d]));
+  for (int d = 0; d < KS_QUOTA_DIMS; ++d) HIPCHK(ctx, cp8(st.pq.req[d], pc->quota_req[d]));
   if (pc->flags) HIPCHK(ctx, hipMemcpyAsync(s.flags, pc->flags, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.flags, 0, (size_t)p * 4, ctx->stream));
   if (pc->quota) HIPCHK(ctx, hipMemcpyAsync(s.quota, pc->quota, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.quota, 0xFF, (size_t)p * 4, ctx->stream));
-  if (pc->quota_mask) HIPCHK(ctx, hipMemcpyAsync(ctx->pq.mask, pc->quota_mask, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
-  else HIPCHK(ctx, hipMemsetAsync(ctx->pq.mask, 0, (size_t)p * 4, ctx->stream));
+  if (pc->quota_mask) HIPCHK(ctx, hipMemcpyAsync(st.pq.mask, pc->quota_mask, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
+  else HIPCHK(ctx, hipMemsetAsync(st.pq.mask, 0, (size_t)p * 4, ctx->stream));
   if (pc->rsv_class) HIPCHK(ctx, hipMemcpyAsync(s.rsv_class, pc->rsv_class, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.rsv_class, 0xFF, (size_t)p * 4, ctx->stream));
   if (pc->cpu_bind) HIPCHK(ctx, hipMemcpyAsync(s.cpu_bind, pc->cpu_bind, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.cpu_bind, 0, (size_t)p * 4, ctx->stream));
+  return KS_OK;
+}
+
+// PreFilter / EstimatePod: the stage's columns -> PodRec (prep_pods_kernel)
+static int prep_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
+  if (p <= 0) return KS_OK;
   const int threads = 256;
-  hipLaunchKernelGGL(prep_pods_kernel, dim3((p + threads - 1) / threads), dim3(threads), 0, ctx->stream, s, dst, p,
-                     ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory);
+  hipLaunchKernelGGL(prep_pods_kernel, dim3((p + threads - 1) / threads), dim3(threads), 0, ctx->stream, st.cols,
+                     st.recs, p, ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory);
   HIPCHK(ctx, hipGetLastError());
   return KS_OK;
 }
@@ -2279,8 +2292,8 @@ int ks_stage_pods(ks_ctx* ctx, const ks_pod_cols* pods, int32_t p) {
     KS_FAIL(ctx, KS_ESTATE, "ElasticQuota enabled but ks_load_quotas not called");
   if (int rc = validate_pods(ctx, pods, p); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  if (ensure_pod_capacity(ctx, p) != KS_OK) return KS_ENOMEM;
-  if (p > 0 && stage_pods_to(ctx, pods, p, ctx->pods) != KS_OK) return KS_EHIP;
+  if (ensure_stage(ctx, ctx->st, p) != KS_OK) return KS_ENOMEM;
+  if (p > 0 && stage_cols(ctx, ctx->st, pods, p) != KS_OK) return KS_EHIP;
   ctx->np = p;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
@@ -2367,7 +2380,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   sa.dn = ctx->dnodes;
   sa.rv = ctx->drv;
   sa.c = ctx->kc;
-  sa.pods = ctx->pods;
+  sa.pods = ctx->st.recs;
   sa.cursor = ctx->cursor;
   sa.out = ctx->sweep_out;
   sa.n = ctx->n;
@@ -2476,8 +2489,8 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   ca.dn = ctx->dnodes;
   ca.rv = ctx->drv;
   ca.c = ctx->kc;
-  ca.pods = ctx->pods;
-  ca.pq = ctx->pq;
+  ca.pods = ctx->st.recs;
+  ca.pq = ctx->st.pq;
   ca.q = ctx->q;
   ca.cursor = ctx->cursor;
   ca.cand_chunk = ctx->cand_chunk;
@@ -2485,7 +2498,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   ca.cand_bound = ctx->cand_bound;
   ca.cand_top = ctx->cand_top;
   ca.cand_count = ctx->cand_count;
-  ca.results = ctx->results;
+  ca.results = ctx->st.results;
   ca.counters = ctx->counters;
   ca.n = ctx->n;
   ca.nchunks = ctx->nchunks;
@@ -2582,6 +2595,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 256, ctx->stream));
   HIPCHK(ctx, hipEventRecord(t0, ctx->stream));
+  // PreFilter / EstimatePod for the staged queue (the pods' request vectors, estimates, flags)
+  if (prep_stage(ctx, ctx->st, np) != KS_OK) return KS_EHIP;
   std::vector<std::pair<int, size_t>> evs;
   size_t evn = 2;
   int32_t host_cursor = 0;
@@ -2607,7 +2622,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   if (ctx->cpu_loaded && ctx->n > 0) {
     // the CPU ids of the pass's cpu-bind Reserves (ks_cpuset.h), per node in placement order
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
-                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const PodRec*)ctx->pods,
+                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const PodRec*)ctx->st.recs,
                        ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
                        (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
     HIPCHK(ctx, hipGetLastError());
@@ -2652,7 +2667,7 @@ int ks_schedule_staged(ks_ctx* ctx) {
 int ks_fetch_results(ks_ctx* ctx, ks_result* out, int32_t p) {
   if (!ctx || !out || p < 0 || p > ctx->np) return ctx ? (ctx->err = "ks_fetch_results: bad args", KS_EINVAL) : KS_EINVAL;
   if (p == 0) return KS_OK;
-  HIPCHK(ctx, hipMemcpyAsync(out, ctx->results, (size_t)p * sizeof(ks_result), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(out, ctx->st.results, (size_t)p * sizeof(ks_result), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -2719,8 +2734,8 @@ int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, in
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_eval_pod_debug before ks_load_nodes");
   if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  if (ensure_pod_capacity(ctx, 1) != KS_OK) return KS_ENOMEM;
-  if (stage_pods_to(ctx, pod, 1, ctx->dbg_pod) != KS_OK) return KS_EHIP;
+  if (ensure_stage(ctx, ctx->est, 1) != KS_OK) return KS_ENOMEM;
+  if (stage_cols(ctx, ctx->est, pod, 1) != KS_OK || prep_stage(ctx, ctx->est, 1) != KS_OK) return KS_EHIP;
   const int64_t n = ctx->n;
   void* buf = nullptr;
   const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4) + 64;
@@ -2735,7 +2750,7 @@ int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, in
   const int blocks = (int)((n + threads - 1) / threads);
   if (blocks > 0) {
     HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
-                                  ctx->dbg_pod, n, dr, ds, dt, draw, dhi, ddraw));
+                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw));
     if (ctx->kc.dev)
       hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,
                          ctx->cfg.deviceshare.plugin_weight);
