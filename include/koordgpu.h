@@ -146,6 +146,8 @@ extern "C" {
                                           (DefaultDeviceHandler, devicehandler_default.go:45-48) */
 #define KS_R_DEV_JOINT 0x100000u       /* DeviceShare joint allocation: "node(s) Joint-Allocate rules not met" or
                                           "Device Joint-Allocate rules violation" (device_allocator.go:252,280) */
+#define KS_R_NUMA_CPUSET 0x200000u     /* NUMA Allocate of a cpu-bind pod on a NUMA-policy node: "not enough cpus available
+                                          to satisfy request" (allocateCPUSet, resource_manager.go:333-335,366-368) */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u

@@ -61,6 +61,7 @@
 #define DEFAULT_MILLI_CPU 100                 /* schedutil.DefaultMilliCPURequest */
 #define DEFAULT_MEMORY (200LL * 1024 * 1024)  /* schedutil.DefaultMemoryRequest */
 #define MOST_PREFERRED_SCORE 1000             /* reservation/scoring.go:39 */
+#define KO_ALLOW_ALL 0xFFFFFFFFu              /* DeviceShare NUMA restriction: none (no topology-manager affinity) */
 
 /* ------------------------------------------------------------------ */
 /* scorers                                                             */
@@ -363,31 +364,46 @@ static uint32_t numa_filter_amplified(const ko_sched *s, const ko_pod *p, int64_
 /* NodeNUMAResource Filter on a topology-policy-None node (plugin.go:275-338): the amplified-CPU check,
  * then for a cpu-bind pod a valid CPU topology (:296-301).  Preferred bind policies run no trial Allocate
  * (:318-327 is for a required policy, which the evaluator refuses). */
+/* the NUMA policy path's result for one (pod, node) */
+typedef struct ko_numa_out {
+  uint32_t affinity;              /* merged NUMANodeAffinity stored for the node (0 = nil) */
+  int64_t alloc[KS_MAX_NUMA][2];  /* NUMA plugin Allocate: cpu (milli), memory per NUMA node */
+  int32_t cpus[KS_MAX_NUMA];      /* cpu-bind pod: CPUs allocateCPUSet takes in each allocated NUMA node */
+} ko_numa_out;
 static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *score,
-                                 int64_t alloc[][2]);
+                                 ko_numa_out *out);
 static int node_numa_policy(const ko_sched *s, int64_t n);
 
-static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+/* the policy path of one (pod, node), computed once per evaluation (Filter, Score and DeviceShare's affinity) */
+typedef struct {
+  int on;            /* NodeNUMAResource enabled, pod not skipped, node with a NUMA topology policy */
+  uint32_t reasons;  /* KS_R_* of the policy path (FilterByNUMANode) */
+  int64_t score;
+  ko_numa_out *out;
+} ko_npol;
+
+static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c) {
   if (p->reqzero) return 0; /* PreFilter skip */
   uint32_t r = numa_filter_amplified(s, p, n, e);
   if (r) return r;
   if (p->bind && !(s->cpu_loaded && s->topo_of[n] >= 0)) return KS_R_NUMA_INVALID_TOPOLOGY;
-  if (node_numa_policy(s, n) != 0) {
-    int64_t alloc[KS_MAX_NUMA][2];
-    return numa_policy_eval(s, p, n, e, NULL, alloc);
-  }
-  return 0;
+  return c->on ? c->reasons : 0;
+}
+
+/* DeviceShare's NUMA affinity on node n: the topology manager stores it when Admit admits (manager.go:69), i.e.
+ * after the amplified-CPU and CPU-topology checks passed */
+static uint32_t npol_allow(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c) {
+  if (!c->on || !c->out->affinity) return KO_ALLOW_ALL;
+  if (numa_filter_amplified(s, p, n, e) || (p->bind && !(s->cpu_loaded && s->topo_of[n] >= 0))) return KO_ALLOW_ALL;
+  return c->out->affinity;
 }
 
 /* scoreWithAmplifiedCPUs (scoring.go:98-114) -> resourceAllocationScorer.score (:206-221) */
-static int64_t numa_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+static int64_t numa_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c) {
   const ko_nodes *d = &s->nd;
   const ks_numa_args *a = &s->cfg.numa;
   if (p->reqzero) return 0;
-  if (node_numa_policy(s, n) != 0) {
-    int64_t sc = 0, alloc[KS_MAX_NUMA][2];
-    return numa_policy_eval(s, p, n, e, &sc, alloc) ? 0 : sc;
-  }
+  if (c->on) return c->reasons ? 0 : c->score;
   int64_t req_cpu = e->req[0];
   double ratio = d->numa_ratio[n];
   int64_t pod_cpu = p->cpu;
@@ -496,78 +512,34 @@ static int narrower(uint32_t a, uint32_t b) {
   return ca < cb;
 }
 
-/* Filter (FilterByNUMANode -> topology manager Admit) and Score for a pod on a node with a NUMA topology
- * policy.  Hints: generateResourceHints (resource_manager.go:459-593, numaScorer = the NUMAScoringStrategy
- * type with the ScoringStrategy weights, plugin.go:118-124); merge: filterProvidersHints / mergeFilteredHints
- * (topologymanager/policy.go:96-187) with the resources in the order cpu, memory (Go iterates a map);
- * policies policy_best_effort.go / policy_restricted.go / policy_single_numa_node.go; allocation:
- * tryBestToDistributeEvenly (resource_manager.go:221-283, its sort compares totalAvailable by slice
- * position as the Go code does).  Returns KS_R_* reasons; *score = the node score over the allocated NUMA
- * nodes (calculateAllocatableAndRequested, scoring.go:116-163); alloc[k] = the pod's allocation. */
-static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *score,
-                                 int64_t alloc[][2]) {
-  const int K = s->numa_loaded ? s->numa_count[n] : 0;
-  const int pol = node_numa_policy(s, n);
-  if (score) *score = 0;
-  for (int k = 0; k < KS_MAX_NUMA; k++) alloc[k][0] = alloc[k][1] = 0;
-  if (K == 0) return KS_R_NUMA_MISSING;
-  int64_t total[KS_MAX_NUMA][2], used[KS_MAX_NUMA][2], avail[KS_MAX_NUMA][2];
-  int present[KS_MAX_NUMA];
-  numa_state(s, n, K, total, used, present, avail);
-  const int64_t req[2] = {p->cpu, p->mem};
-  const int want[2] = {p->cpu != 0, p->mem != 0};
-  /* generateResourceHints */
-  uint32_t masks[256];
-  const int nm = iterate_masks(K, masks);
-  ko_hint hints[2][256];
-  int nh[2] = {0, 0}, min_size[2] = {K, K};
-  uint32_t lack[2] = {0, 0};
-  for (int r = 0; r < 2; r++)
-    for (int k = 0; k < K; k++)
-      if (avail[k][r] == 0) lack[r] |= 1u << k;
-  const int numa_most = s->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED;
-  for (int m = 0; m < nm; m++) {
-    int64_t tsum[2] = {0, 0}, fsum[2] = {0, 0};
-    for (int k = 0; k < K; k++)
-      if ((masks[m] >> k) & 1u)
-        for (int r = 0; r < 2; r++) {
-          tsum[r] += total[k][r];
-          fsum[r] += avail[k][r];
-        }
-    int64_t rq[2] = {tsum[0] - fsum[0], tsum[1] - fsum[1]};
-    for (int r = 0; r < 2; r++)
-      if (rq[r] < 0) rq[r] = 0;
-    const int64_t sc = numa_res_score(s, numa_most, rq, tsum, p);
-    for (int r = 0; r < 2; r++) { /* memory first (memoryResourceNames), then cpu: independent lists */
-      if (!want[r]) continue;
-      if (tsum[r] < req[r]) continue;
-      if (masks[m] & lack[r]) continue;
-      int cnt = __builtin_popcount(masks[m]);
-      if (cnt < min_size[r]) min_size[r] = cnt;
-      if (fsum[r] < req[r]) continue;
-      hints[r][nh[r]++] = (ko_hint){masks[m], 0, sc};
-    }
-  }
-  for (int r = 0; r < 2; r++)
-    for (int i = 0; i < nh[r]; i++) hints[r][i].preferred = __builtin_popcount(hints[r][i].mask) == min_size[r];
-  /* filterProvidersHints: one list per requested NUMA resource (cpu, then memory); none -> any-numa */
-  ko_hint lists[2][256];
-  int nl = 0, ln[2];
-  for (int r = 0; r < 2; r++) {
-    if (!want[r]) continue;
-    if (nh[r] == 0) {
-      lists[nl][0] = (ko_hint){0, 0, 0}; /* no possible NUMA affinities */
-      ln[nl++] = 1;
-    } else {
-      memcpy(lists[nl], hints[r], sizeof(ko_hint) * nh[r]);
-      ln[nl++] = nh[r];
-    }
-  }
-  if (nl == 0) {
-    lists[0][0] = (ko_hint){0, 1, 0};
-    ln[0] = 1;
-    nl = 1;
-  }
+typedef struct {
+  int lists;
+  int nh;
+  uint32_t mask[16];
+  int pref[16];
+} ko_devhints;
+static void dev_hints(const ko_sched *s, const ko_pod *p, int64_t n, ko_devhints *h);
+static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *raw, uint32_t allow);
+
+
+/* CPUs of NUMA node k available to cpuset pods: topology CPUs of the node minus allocated minus reserved */
+static int numa_free_cpus(const ko_sched *s, int64_t n, int k) {
+  if (!s->cpu_loaded || s->topo_of[n] < 0) return 0;
+  const ko_topo *t = &s->topos[s->topo_of[n]];
+  const uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
+  int c = 0;
+  for (int i = 0; i < t->ncpus; i++) c += t->node[i] == k && !al[i] && !rs[i];
+  return c;
+}
+
+/* The topology manager's Merge over the providers' hint lists after filterProvidersHints: the policy's
+ * filter (filterSingleNumaHints, policy_single_numa_node.go:47-63), mergeFilteredHints over the cartesian product,
+ * first list outermost (policy.go:129-226), the single-numa-node default -> nil rewrite (:71-74) and the policy's
+ * canAdmitPodResult (best-effort: always, restricted / single-numa-node: preferred).  lists[l][0..ln[l]) are
+ * modified (filtered).  Returns admit; *affinity = the merged NUMANodeAffinity (0 = nil), *preferred. */
+#define KO_MAX_LISTS 8
+static int ko_merge_hints(int pol, int K, int nl, int *ln, ko_hint lists[][256], uint32_t *affinity_out,
+                          int *preferred_out) {
   if (pol == KS_NUMA_POLICY_SINGLE_NUMA_NODE) { /* filterSingleNumaHints */
     for (int l = 0; l < nl; l++) {
       int k = 0;
@@ -582,7 +554,7 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
   /* mergeFilteredHints over the cartesian product (first list outermost) */
   const uint32_t dflt = (K >= 32) ? 0xFFFFFFFFu : ((1u << K) - 1u);
   ko_hint best = {dflt, 0, 0};
-  int idx[2] = {0, 0};
+  int idx[KO_MAX_LISTS] = {0};
   int empty = 0;
   for (int l = 0; l < nl; l++) empty |= ln[l] == 0;
   while (!empty) {
@@ -628,7 +600,132 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
   } else if (pol == KS_NUMA_POLICY_RESTRICTED) {
     admit = best.preferred;
   }
+  *affinity_out = affinity;
+  if (preferred_out) *preferred_out = best.preferred;
+  return admit;
+}
+
+/* test entry: the merge over explicit lists (tests/golden/topology_merge.json) */
+int ko_topology_merge(int policy, int K, int nlists, const int *lens, const uint32_t *masks, const int *prefs,
+                      const int64_t *scores, uint32_t *affinity, int *preferred) {
+  static __thread ko_hint lists[KO_MAX_LISTS][256];
+  int ln[KO_MAX_LISTS];
+  if (nlists > KO_MAX_LISTS) return -1;
+  int o = 0;
+  for (int l = 0; l < nlists; l++) {
+    ln[l] = lens[l];
+    for (int i = 0; i < lens[l]; i++, o++) lists[l][i] = (ko_hint){masks[o], prefs[o], scores[o]};
+  }
+  return ko_merge_hints(policy, K, nlists, ln, lists, affinity, preferred);
+}
+
+/* Filter (FilterByNUMANode -> topology manager Admit) and Score for a pod on a node with a NUMA topology
+ * policy.  Hint providers in the order NodeNUMAResource, DeviceShare (the reference registers them in plugin
+ * construction order, which Go's registry map leaves random).  NodeNUMAResource hints: generateResourceHints
+ * (resource_manager.go:459-593, numaScorer = the NUMAScoringStrategy type with the ScoringStrategy weights,
+ * plugin.go:118-124; a cpu-bind pod's cpu request amplified, getResourceOptions plugin.go:495-506), one list
+ * per requested resource in the order cpu, memory (Go iterates a map); DeviceShare hints: dev_hints.  Merge:
+ * filterProvidersHints / mergeFilteredHints over the cartesian product, first list outermost
+ * (topologymanager/policy.go:96-226) with policy_best_effort.go / policy_restricted.go /
+ * policy_single_numa_node.go.  Then allocateResources (manager.go:101-111) in provider order: the NUMA plugin's
+ * Allocate -> resourceManager.Allocate (resource_manager.go:169-188): allocateResourcesByHint ->
+ * tryBestToDistributeEvenly (:221-283, its sort compares totalAvailable by slice position as the Go code does;
+ * a cpu-bind pod distributes its original request in whole CPUs, splitQuantity :285-300) and for a cpu-bind pod
+ * allocateCPUSet (:314-401: per allocated NUMA node min(available CPUs there, the node's whole CPUs)); then
+ * DeviceShare's Allocate restricted to the affinity (topology_hint.go:57-106).  Returns KS_R_* reasons; *score =
+ * the node score (plugin Score scoring.go:55-96 -> calculateAllocatableAndRequested :116-163). */
+static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *score,
+                                 ko_numa_out *out) {
+  const int K = s->numa_loaded ? s->numa_count[n] : 0;
+  const int pol = node_numa_policy(s, n);
+  if (score) *score = 0;
+  memset(out, 0, sizeof(*out));
+  if (K == 0) return KS_R_NUMA_MISSING;
+  int64_t total[KS_MAX_NUMA][2], used[KS_MAX_NUMA][2], avail[KS_MAX_NUMA][2];
+  int present[KS_MAX_NUMA];
+  numa_state(s, n, K, total, used, present, avail);
+  const double ratio = s->nd.numa_ratio[n];
+  const int bind = p->bind != 0;
+  /* options.requests: a cpu-bind pod's cpu amplified (hints, score); originalRequests for the allocation */
+  const int64_t req[2] = {bind ? amplify(p->cpu, ratio) : p->cpu, p->mem};
+  const int64_t oreq[2] = {p->cpu, p->mem};
+  const int want[2] = {p->cpu != 0, p->mem != 0};
+  ko_pod pa = *p;
+  pa.cpu = req[0];
+  /* generateResourceHints */
+  uint32_t masks[256];
+  const int nm = iterate_masks(K, masks);
+  ko_hint hints[2][256];
+  int nh[2] = {0, 0}, min_size[2] = {K, K};
+  uint32_t lack[2] = {0, 0};
+  for (int r = 0; r < 2; r++)
+    for (int k = 0; k < K; k++)
+      if (avail[k][r] == 0) lack[r] |= 1u << k;
+  const int numa_most = s->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED;
+  for (int m = 0; m < nm; m++) {
+    int64_t tsum[2] = {0, 0}, fsum[2] = {0, 0};
+    for (int k = 0; k < K; k++)
+      if ((masks[m] >> k) & 1u)
+        for (int r = 0; r < 2; r++) {
+          tsum[r] += total[k][r];
+          fsum[r] += avail[k][r];
+        }
+    int64_t rq[2] = {tsum[0] - fsum[0], tsum[1] - fsum[1]};
+    for (int r = 0; r < 2; r++)
+      if (rq[r] < 0) rq[r] = 0;
+    const int64_t sc = numa_res_score(s, numa_most, rq, tsum, &pa);
+    for (int r = 0; r < 2; r++) { /* memory first (memoryResourceNames), then cpu: independent lists */
+      if (!want[r]) continue;
+      if (tsum[r] < req[r]) continue;
+      if (masks[m] & lack[r]) continue;
+      int cnt = __builtin_popcount(masks[m]);
+      if (cnt < min_size[r]) min_size[r] = cnt;
+      if (fsum[r] < req[r]) continue;
+      hints[r][nh[r]++] = (ko_hint){masks[m], 0, sc};
+    }
+  }
+  for (int r = 0; r < 2; r++)
+    for (int i = 0; i < nh[r]; i++) hints[r][i].preferred = __builtin_popcount(hints[r][i].mask) == min_size[r];
+  /* filterProvidersHints: NodeNUMAResource's lists (cpu, then memory; no resource -> any-numa), then
+   * DeviceShare's identical lists */
+  ko_hint lists[KO_MAX_LISTS][256];
+  int nl = 0, ln[KO_MAX_LISTS];
+  int numa_lists = 0;
+  for (int r = 0; r < 2; r++) {
+    if (!want[r]) continue;
+    if (nh[r] == 0) {
+      lists[nl][0] = (ko_hint){0, 0, 0}; /* no possible NUMA affinities */
+      ln[nl++] = 1;
+    } else {
+      memcpy(lists[nl], hints[r], sizeof(ko_hint) * nh[r]);
+      ln[nl++] = nh[r];
+    }
+    numa_lists++;
+  }
+  if (numa_lists == 0) { /* the NUMA provider returns no hints: a preferred any-numa hint */
+    lists[nl][0] = (ko_hint){0, 1, 0};
+    ln[nl++] = 1;
+  }
+  ko_devhints dh;
+  dev_hints(s, p, n, &dh);
+  if (dh.lists == 0) {
+    lists[nl][0] = (ko_hint){0, 1, 0};
+    ln[nl++] = 1;
+  } else {
+    for (int l = 0; l < dh.lists; l++) {
+      if (dh.nh == 0) {
+        lists[nl][0] = (ko_hint){0, 0, 0};
+        ln[nl++] = 1;
+      } else {
+        for (int i = 0; i < dh.nh; i++) lists[nl][i] = (ko_hint){dh.mask[i], dh.pref[i], 0};
+        ln[nl++] = dh.nh;
+      }
+    }
+  }
+  uint32_t affinity = 0;
+  const int admit = ko_merge_hints(pol, K, nl, ln, lists, &affinity, NULL);
   if (!admit) return KS_R_NUMA_AFFINITY;
+  out->affinity = affinity;
   /* NUMA plugin Allocate -> allocateResourcesByHint -> tryBestToDistributeEvenly */
   if (affinity) {
     int bits[KS_MAX_NUMA], nb = 0;
@@ -647,24 +744,51 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
           order[j] = order[j - 1];
           order[j - 1] = t;
         }
-      int64_t q = req[r];
+      int64_t q = oreq[r];
       for (int i = 0; i < nb; i++) {
-        const int64_t split = q / (nb - i);
+        /* splitQuantity: cpu of a cpu-bind pod in whole CPUs (Quantity.Value() rounds up), else milli / bytes */
+        const int64_t split = (r == 0 && bind) ? ((q + 999) / 1000) / (nb - i) * 1000 : q / (nb - i);
         const int64_t a = avail[order[i]][r];
         const int64_t got = a > split ? split : a;
         if (got != 0) {
-          alloc[order[i]][r] = got;
+          out->alloc[order[i]][r] = got;
           q -= got;
         }
       }
       if (q != 0) return KS_R_NUMA_INSUFFICIENT;
     }
   }
+  if (bind) {
+    /* allocateCPUSet: too few available CPUs on the node, or the allocated NUMA nodes' CPUs do not add up */
+    int free_total = 0, free_k[KS_MAX_NUMA];
+    for (int k = 0; k < K; k++) free_k[k] = numa_free_cpus(s, n, k);
+    if (s->cpu_loaded && s->topo_of[n] >= 0) { /* GetAvailableCPUs over the whole node */
+      const ko_topo *t = &s->topos[s->topo_of[n]];
+      const uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
+      for (int i = 0; i < t->ncpus; i++) free_total += !al[i] && !rs[i];
+    }
+    if (free_total < p->needed) return KS_R_NUMA_CPUSET;
+    int any = 0, taken = 0;
+    for (int k = 0; k < K; k++) {
+      if (!out->alloc[k][0] && !out->alloc[k][1]) continue;
+      any = 1;
+      const int want_k = (int)(out->alloc[k][0] / 1000);
+      out->cpus[k] = free_k[k] < want_k ? free_k[k] : want_k;
+      taken += out->cpus[k];
+    }
+    if (any && taken != p->needed) return KS_R_NUMA_CPUSET;
+  }
+  /* DeviceShare's Allocate with the affinity */
+  {
+    int64_t draw = 0;
+    const uint32_t dr = dev_eval(s, p, n, &draw, affinity ? affinity : KO_ALLOW_ALL);
+    if (dr) return dr;
+  }
   if (score) {
     int64_t treq[2] = {0, 0}, talloc[2] = {0, 0};
     int any = 0;
     for (int k = 0; k < K; k++) {
-      if (!alloc[k][0] && !alloc[k][1]) continue;
+      if (!out->alloc[k][0] && !out->alloc[k][1]) continue;
       any = 1;
       for (int r = 0; r < 2; r++) {
         talloc[r] += total[k][r];
@@ -677,17 +801,29 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
       treq[0] = e->req[0];
       treq[1] = e->req[1];
     }
-    *score = numa_res_score(s, s->cfg.numa.strategy == KS_MOST_ALLOCATED, treq, talloc, p);
+    /* a cpu-bind pod: requested cpu = the node's allocated cpuset CPUs, amplified */
+    if (bind) treq[0] = amplify((int64_t)s->nd.numa_cpus[n] * 1000, ratio);
+    *score = numa_res_score(s, s->cfg.numa.strategy == KS_MOST_ALLOCATED, treq, talloc, &pa);
   }
   return 0;
 }
 
-static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+static uint32_t filter_node(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c) {
   uint32_t r = 0;
   if (s->cfg.fit.enable_filter) r |= fit_filter(s, p, n, e);
   if (s->cfg.loadaware.enable_filter) r |= la_filter(s, p, n);
-  if (s->cfg.numa.enable) r |= numa_filter(s, p, n, e);
+  if (s->cfg.numa.enable) r |= numa_filter(s, p, n, e, c);
   return r;
+}
+
+static void numa_policy_ctx(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, ko_npol *c,
+                            ko_numa_out *out) {
+  c->on = s->cfg.numa.enable && !p->reqzero && node_numa_policy(s, n) != 0;
+  c->reasons = 0;
+  c->score = 0;
+  c->out = out;
+  memset(out, 0, sizeof(*out));
+  if (c->on) c->reasons = numa_policy_eval(s, p, n, e, &c->score, out);
 }
 
 /* ------------------------------------------------------------------ */
@@ -744,11 +880,11 @@ static int64_t la_score(const ko_sched *s, const ko_pod *p, int64_t n) {
   return node_score / weight_sum;
 }
 
-static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, int64_t *fit_out,
-                           int64_t *la_out, int64_t *numa_out) {
+static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c,
+                           int64_t *fit_out, int64_t *la_out, int64_t *numa_out) {
   int64_t t = 0, fs = 0, ls = 0, ns = 0;
   if (s->cfg.numa.enable) {
-    ns = numa_score(s, p, n, e);
+    ns = numa_score(s, p, n, e, c);
     t += ns * s->cfg.numa.plugin_weight;
   }
   if (numa_out) *numa_out = ns;
@@ -1009,8 +1145,20 @@ static const int64_t *dev_used(const ko_sched *s, int64_t n, int k) { return s->
 /* one minor of a device type as nodeDevice sees it: deviceTotal / deviceFree (= total - used, kept as
  * an all-zero entry when fully used, resetDeviceFree device_cache.go:157-174); RDMA uses q = 0 only.
  * Returns 0 for an absent minor (all-zero total). */
-static int dev_minor(const ko_sched *s, int64_t n, int type, int k, int64_t tot[3], int64_t fre[3]) {
+static int dev_pcie(const ko_sched *s, int64_t n, int type, int k);
+
+/* Minor k of `type` belongs to the node device the allocator sees: with a NUMA affinity (topology manager
+ * store, deviceshare/plugin.go:292-303) filterNodeDevice keeps only devices whose topology NUMA node is in the
+ * affinity (device_allocator.go:134-158); allow = bit per NUMA node id, KO_ALLOW_ALL = no affinity. */
+static int dev_allowed(const ko_sched *s, int64_t n, int type, int k, uint32_t allow) {
+  if (allow == KO_ALLOW_ALL) return 1;
+  const int pc = dev_pcie(s, n, type, k);
+  return pc != KS_PCIE_NONE && ((allow >> s->dv.pnuma[(size_t)n * KO_PCIE + pc]) & 1u);
+}
+
+static int dev_minor(const ko_sched *s, int64_t n, int type, int k, int64_t tot[3], int64_t fre[3], uint32_t allow) {
   tot[0] = tot[1] = tot[2] = fre[0] = fre[1] = fre[2] = 0;
+  if (!dev_allowed(s, n, type, k, allow)) return 0;
   if (type == KO_T_GPU) {
     const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
     for (int q = 0; q < 3; q++) {
@@ -1076,7 +1224,7 @@ static uint32_t dev_prepare(const ko_sched *s, const ko_pod *p, int64_t n, ko_de
     int any = 0;
     for (int k = 0; k < KO_RDMA; k++) {
       int64_t t[3], f[3];
-      any |= dev_minor(s, n, KO_T_RDMA, k, t, f);
+      any |= dev_minor(s, n, KO_T_RDMA, k, t, f, KO_ALLOW_ALL);
     }
     if (!any) return KS_R_DEV_NO_RDMA;
     int64_t q = p->rdma;
@@ -1121,11 +1269,11 @@ static int dev_fits(const ko_devreq *g, int type, const int64_t *fre) {
 }
 
 /* nodeDevice.split: how many minors of `sub` satisfy the request per instance (device_cache.go:419-433) */
-static int dev_split(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub) {
+static int dev_split(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub, uint32_t allow) {
   int c = 0;
   for (int k = 0; k < dev_nminors(type); k++) {
     int64_t t[3], f[3];
-    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f)) continue;
+    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f, allow)) continue;
     c += dev_fits(g, type, f);
   }
   return c;
@@ -1149,7 +1297,7 @@ static int pair_less(const ko_pair *a, const ko_pair *b) {
  * maxDesiredCount = max(desired, |pref|) minors with non-zero free that satisfy the request.  Returns the
  * allocated minors as a mask (0 = "Insufficient <type> devices"). */
 static uint32_t dev_alloc_type(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub, int desired,
-                               uint32_t pref) {
+                               uint32_t pref, uint32_t allow) {
   int maxd = desired, npref = __builtin_popcount(pref);
   if (npref > maxd) maxd = npref;
   if (desired == 0) desired = 1;
@@ -1158,7 +1306,7 @@ static uint32_t dev_alloc_type(const ko_sched *s, int64_t n, const ko_devreq *g,
   int m = 0;
   for (int k = 0; k < dev_nminors(type); k++) {
     int64_t t[3], f[3];
-    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f)) continue;
+    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f, allow)) continue;
     ko_pair *x = &r[m++];
     x->minor = k;
     x->score = dev_scorer(s, type, t, f, g->req[type]);
@@ -1196,12 +1344,12 @@ static uint32_t dev_pcies_of(const ko_sched *s, int64_t n, int type, uint32_t ma
 /* jointAllocate (device_allocator.go:286-339) on the node device restricted to sub[]: the GPUs, then the
  * RDMA devices preferring the GPUs' PCIe switches.  0 = failed. */
 static int dev_joint_alloc(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, const uint32_t sub[2],
-                           uint32_t pref, uint32_t out[2]) {
-  uint32_t prim = dev_alloc_type(s, n, g, KO_T_GPU, sub[KO_T_GPU], g->desired[KO_T_GPU], pref);
+                           uint32_t pref, uint32_t out[2], uint32_t allow) {
+  uint32_t prim = dev_alloc_type(s, n, g, KO_T_GPU, sub[KO_T_GPU], g->desired[KO_T_GPU], pref, allow);
   if (!prim) return 0;
   uint32_t pcies = dev_pcies_of(s, n, KO_T_GPU, prim);
   int desired = same_pcie ? __builtin_popcount(pcies) : 1;
-  uint32_t sec = dev_alloc_type(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], desired, pcies);
+  uint32_t sec = dev_alloc_type(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], desired, pcies, allow);
   if (!sec) return 0;
   out[KO_T_GPU] = prim;
   out[KO_T_RDMA] = sec;
@@ -1222,14 +1370,15 @@ static void dev_sub_of(const ko_sched *s, int64_t n, uint32_t pcies, uint32_t su
 /* tryJointAllocate -> allocateByTopology (device_allocator.go:188-253) with DeviceTypes [gpu, rdma]:
  * per PCIe switch (newDeviceTopologyGuide / freeNodeDevicesInPCIe, numa_topology.go:109-175), per NUMA node
  * (freeNodeDevicesInNode :185-240), then the whole node.  Returns 1 with out[] on success. */
-static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, uint32_t out[2]) {
+static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, uint32_t out[2],
+                           uint32_t allow) {
   const uint32_t all[2] = {(1u << KO_GPUS) - 1u, (1u << KO_RDMA) - 1u};
   uint32_t exist = 0; /* switches that hold a device */
   for (int t = 0; t < KO_NTYPES; t++)
     for (int k = 0; k < dev_nminors(t); k++) {
       int64_t tt[3], ff[3];
       int pc = dev_pcie(s, n, t, k);
-      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff)) exist |= 1u << pc;
+      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff, allow)) exist |= 1u << pc;
     }
   const uint8_t *pnuma = s->dv.pnuma + (size_t)n * KO_PCIE, *psock = s->dv.psock + (size_t)n * KO_PCIE;
   /* pcieSwitches in (socket, node, pcie) order = index order; preferred: free rdma instances on the switch */
@@ -1238,7 +1387,7 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
     if (!((exist >> pc) & 1u)) continue;
     uint32_t sub[2];
     dev_sub_of(s, n, 1u << pc, sub);
-    swpref[pc] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA]) > 0;
+    swpref[pc] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
     sw[nsw++] = pc;
   }
   /* freeNodeDevicesInPCIe: sort.Slice by (preferred desc, socket, node); stable here (insertion sort for
@@ -1254,8 +1403,8 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
   for (int i = 0; i < nsw; i++) {
     uint32_t sub[2];
     dev_sub_of(s, n, 1u << sw[i], sub);
-    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU]) >= g->desired[KO_T_GPU] &&
-        dev_joint_alloc(s, n, g, same_pcie, sub, 1u << sw[i], out))
+    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU], allow) >= g->desired[KO_T_GPU] &&
+        dev_joint_alloc(s, n, g, same_pcie, sub, 1u << sw[i], out, allow))
       return 1;
   }
   /* groupedNodeDevices per NUMA node: preferredPCIes = the node's preferred switches */
@@ -1272,7 +1421,7 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
   for (int i = 0; i < ng; i++) {
     uint32_t sub[2];
     dev_sub_of(s, n, gp[grp[i]], sub);
-    gpref[grp[i]] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA]) > 0;
+    gpref[grp[i]] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
   }
   for (int i = 1; i < ng; i++)
     for (int j = i; j > 0; j--) {
@@ -1288,24 +1437,25 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
     uint32_t sub[2];
     dev_sub_of(s, n, gp[grp[i]], sub);
     union_pref |= gpref_pcies[grp[i]];
-    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU]) >= g->desired[KO_T_GPU] &&
-        dev_joint_alloc(s, n, g, same_pcie, sub, gpref_pcies[grp[i]], out))
+    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU], allow) >= g->desired[KO_T_GPU] &&
+        dev_joint_alloc(s, n, g, same_pcie, sub, gpref_pcies[grp[i]], out, allow))
       return 1;
   }
   /* the whole node, preferring every preferred switch */
-  return dev_joint_alloc(s, n, g, same_pcie, all, union_pref, out);
+  return dev_joint_alloc(s, n, g, same_pcie, all, union_pref, out, allow);
 }
 
 /* AutopilotAllocator.Allocate (device_allocator.go:94-132) without hints, preemption or reservations:
  * tryJointAllocate, then allocateDevices for the types joint allocation did not cover.  Returns the
  * KS_R_DEV_* reason (0 = allocated, masks in out[]). */
-static uint32_t dev_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_devreq *g, uint32_t out[2]) {
+static uint32_t dev_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_devreq *g, uint32_t out[2],
+                             uint32_t allow) {
   const uint32_t all[2] = {(1u << KO_GPUS) - 1u, (1u << KO_RDMA) - 1u};
   out[0] = out[1] = 0;
   if (p->joint && g->has[KO_T_GPU]) {
     const int same = p->joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
     uint32_t j[2] = {0, 0};
-    if (dev_by_topology(s, n, g, same, j)) {
+    if (dev_by_topology(s, n, g, same, j, allow)) {
       /* validateJointAllocation (:255-284): the RDMA switches must equal the GPU switches */
       if (same && dev_pcies_of(s, n, KO_T_GPU, j[0]) != dev_pcies_of(s, n, KO_T_RDMA, j[1])) return KS_R_DEV_JOINT;
       out[0] = j[0];
@@ -1316,21 +1466,21 @@ static uint32_t dev_allocate(const ko_sched *s, const ko_pod *p, int64_t n, cons
   }
   for (int t = 0; t < KO_NTYPES; t++) {
     if (!g->has[t] || out[t]) continue;
-    out[t] = dev_alloc_type(s, n, g, t, all[t], g->desired[t], 0);
+    out[t] = dev_alloc_type(s, n, g, t, all[t], g->desired[t], 0, allow);
     if (!out[t]) return KS_R_DEV_INSUFFICIENT;
   }
   return 0;
 }
 
 /* AutopilotAllocator.score (device_allocator.go:507-530): scoreNode per requested type, summed */
-static int64_t dev_node_score(const ko_sched *s, int64_t n, const ko_devreq *g) {
+static int64_t dev_node_score(const ko_sched *s, int64_t n, const ko_devreq *g, uint32_t allow) {
   int64_t sum = 0;
   for (int t = 0; t < KO_NTYPES; t++) {
     if (!g->has[t]) continue;
     int64_t total[3] = {0, 0, 0}, free[3] = {0, 0, 0};
     for (int k = 0; k < dev_nminors(t); k++) {
       int64_t tt[3], ff[3];
-      if (!dev_minor(s, n, t, k, tt, ff)) continue;
+      if (!dev_minor(s, n, t, k, tt, ff, allow)) continue;
       for (int q = 0; q < 3; q++) {
         total[q] += tt[q];
         free[q] += ff[q];
@@ -1341,8 +1491,9 @@ static int64_t dev_node_score(const ko_sched *s, int64_t n, const ko_devreq *g) 
   return sum;
 }
 
-/* DeviceShare Filter; *raw gets the node score (scoreNode) when feasible */
-static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *raw) {
+/* DeviceShare Filter; *raw gets the node score (scoreNode) when feasible.  allow: the node's NUMA affinity from
+ * the topology manager (KO_ALLOW_ALL without one). */
+static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *raw, uint32_t allow) {
   *raw = 0;
   if (!s->cfg.deviceshare.enable || !(p->has_gpu || p->rdma > 0)) return 0;
   if (!s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return 0; /* no device info: pass, score 0 */
@@ -1350,20 +1501,21 @@ static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t 
   uint32_t r = dev_prepare(s, p, n, &g);
   if (r) return r;
   uint32_t m[2];
-  r = dev_allocate(s, p, n, &g, m);
+  r = dev_allocate(s, p, n, &g, m, allow);
   if (r) return r;
-  *raw = dev_node_score(s, n, &g);
+  *raw = dev_node_score(s, n, &g, allow);
   return 0;
 }
 
 /* Reserve -> nodeDevice.updateCacheUsed: used += the request per instance on each allocated minor */
-static void dev_reserve(ko_sched *s, const ko_pod *p, int64_t n, uint32_t *gpu_minors, uint32_t *rdma_minors) {
+static void dev_reserve(ko_sched *s, const ko_pod *p, int64_t n, uint32_t *gpu_minors, uint32_t *rdma_minors,
+                        uint32_t allow) {
   *gpu_minors = *rdma_minors = 0;
   if (!s->cfg.deviceshare.enable || !(p->has_gpu || p->rdma > 0) || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT))
     return;
   ko_devreq g;
   uint32_t m[2];
-  if (dev_prepare(s, p, n, &g) || dev_allocate(s, p, n, &g, m)) return;
+  if (dev_prepare(s, p, n, &g) || dev_allocate(s, p, n, &g, m, allow)) return;
   for (int k = 0; k < KO_GPUS; k++) {
     if (!((m[0] >> k) & 1u)) continue;
     int64_t *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
@@ -1373,6 +1525,61 @@ static void dev_reserve(ko_sched *s, const ko_pod *p, int64_t n, uint32_t *gpu_m
     if ((m[1] >> k) & 1u) s->dv.rused[(size_t)n * KO_RDMA + k] += g.req[KO_T_RDMA][0];
   *gpu_minors = m[0];
   *rdma_minors = m[1];
+}
+
+/* DeviceShare as a topology-manager hint provider: GetPodTopologyHints -> generateTopologyHints
+ * (deviceshare/topology_hint.go:33-55, 108-210).  Per mask over the device topology's NUMA nodes
+ * (IterateBitMasks order): Prepare, the device count of the mask's NUMA nodes (calcTotalDevicesByNUMA
+ * :212-227) against each type's desired count, minAffinitySize, then a trial Allocate restricted to the
+ * mask; every allocating mask is a hint (score 0) of each resource name of the request, preferred when its
+ * size is minAffinitySize.  lists = number of resource names (identical lists); 0 = no preference (the
+ * provider returns nil or an empty map: skip pod, no device info, Prepare failing or no mask with enough
+ * devices -> one preferred any-numa hint in filterProvidersHints). */
+static void dev_hints(const ko_sched *s, const ko_pod *p, int64_t n, ko_devhints *h) {
+  memset(h, 0, sizeof(*h));
+  if (!s->cfg.deviceshare.enable || !(p->has_gpu || p->rdma > 0)) return;
+  if (!s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return;
+  const uint8_t *pnuma = s->dv.pnuma + (size_t)n * KO_PCIE;
+  uint32_t ids = 0; /* numaTopology.nodes: NUMA nodes of the switches holding a device with a topology */
+  for (int t = 0; t < KO_NTYPES; t++)
+    for (int k = 0; k < dev_nminors(t); k++) {
+      int64_t tt[3], ff[3];
+      const int pc = dev_pcie(s, n, t, k);
+      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff, KO_ALLOW_ALL)) ids |= 1u << pnuma[pc];
+    }
+  ko_devreq g;
+  if (dev_prepare(s, p, n, &g)) return;
+  int idl[16], nid = 0;
+  for (int i = 0; i < 16; i++)
+    if ((ids >> i) & 1u) idl[nid++] = i;
+  uint32_t pos[256];
+  const int nm = iterate_masks(nid, pos); /* masks over positions in the sorted id list */
+  int minaff = -1;
+  for (int m = 0; m < nm; m++) {
+    uint32_t mask = 0;
+    for (int i = 0; i < nid; i++)
+      if ((pos[m] >> i) & 1u) mask |= 1u << idl[i];
+    int cnt[KO_NTYPES] = {0, 0};
+    for (int t = 0; t < KO_NTYPES; t++)
+      for (int k = 0; k < dev_nminors(t); k++) {
+        int64_t tt[3], ff[3];
+        const int pc = dev_pcie(s, n, t, k);
+        if (pc != KS_PCIE_NONE && ((mask >> pnuma[pc]) & 1u) && dev_minor(s, n, t, k, tt, ff, KO_ALLOW_ALL)) cnt[t]++;
+      }
+    int enough = 1;
+    for (int t = 0; t < KO_NTYPES; t++)
+      if (g.has[t] && cnt[t] < g.desired[t]) enough = 0;
+    if (!enough) continue;
+    if (minaff < 0) minaff = nid;
+    if (__builtin_popcount(mask) < minaff) minaff = __builtin_popcount(mask);
+    uint32_t out[2];
+    if (dev_allocate(s, p, n, &g, out, mask) == 0) h->mask[h->nh++] = mask;
+  }
+  if (minaff < 0) return;
+  /* quotav1.ResourceNames(requestsPerInstance): gpu-core (requested, or the multi-device split), gpu-memory,
+   * gpu-memory-ratio; koordinator.sh/rdma */
+  h->lists = (g.has[KO_T_GPU] ? ((g.has_core || g.desired[KO_T_GPU] > 1) ? 3 : 2) : 0) + (g.has[KO_T_RDMA] ? 1 : 0);
+  for (int i = 0; i < h->nh; i++) h->pref[i] = __builtin_popcount(h->mask[i]) == minaff;
 }
 
 /* NodeInfo.AddPod (upstream) + podAssignCache.assign (pod_assign_cache.go:53) */
@@ -1804,7 +2011,11 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_
   int64_t draw = 0;
   /* a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
    * NodeNames, plugin.go:235-246) before any Filter plugin runs */
-  if (r != KS_R_RSV_AFFINITY) r |= filter_node(s, p, n, &st.e) | dev_eval(s, p, n, &draw);
+  ko_numa_out no;
+  ko_npol npc;
+  numa_policy_ctx(s, p, n, &st.e, &npc, &no);
+  if (r != KS_R_RSV_AFFINITY)
+    r |= filter_node(s, p, n, &st.e, &npc) | dev_eval(s, p, n, &draw, npol_allow(s, p, n, &st.e, &npc));
   s->draw[n] = r ? 0 : draw;
   s->nom[n] = -1;
   s->rraw[n] = 0;
@@ -1813,7 +2024,7 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_
     s->total[n] = -1;
     return r;
   }
-  s->total[n] = total_score(s, p, n, &st.e, fit_out, la_out, numa_out);
+  s->total[n] = total_score(s, p, n, &st.e, &npc, fit_out, la_out, numa_out);
   if (s->cfg.reservation.enable) {
     int32_t nom = rsv_nominate(s, p, n, &st, &s->rord[n]);
     s->nom[n] = nom;
@@ -1873,18 +2084,19 @@ static void rsv_normalize(ko_sched *s, int64_t *norm) {
 }
 
 /* NodeNUMAResource Reserve for a cpu-bind pod (plugin.go:376-429): resourceManager.Allocate ->
- * allocateCPUSet (resource_manager.go:314-380: available = CPUs - allocated - reserved, too few -> error;
- * takeCPUs) then Update -> NodeAllocation.addPodAllocation (node_allocation.go:75-100). */
-static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod) {
+ * allocateCPUSet (resource_manager.go:314-401: available = CPUs - allocated - reserved, too few -> error;
+ * with a NUMA allocation takeCPUs per allocated NUMA node over its available CPUs, else over the whole node)
+ * then Update -> NodeAllocation.addPodAllocation (node_allocation.go:75-100). */
+static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod, const ko_npol *c) {
   if (!s->cpu_loaded || s->topo_of[n] < 0) return -1;
   const ko_topo *t = &s->topos[s->topo_of[n]];
   uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
   int8_t *ex = s->cpu_excl + (size_t)n * KO_MAX_CPUS;
-  uint8_t avail[KO_MAX_CPUS], res[KO_MAX_CPUS];
+  uint8_t avail[KO_MAX_CPUS], res[KO_MAX_CPUS], part[KO_MAX_CPUS], sub[KO_MAX_CPUS];
   int navail = 0;
-  for (int c = 0; c < t->ncpus; c++) {
-    avail[c] = !al[c] && !rs[c];
-    navail += avail[c];
+  for (int i = 0; i < t->ncpus; i++) {
+    avail[i] = !al[i] && !rs[i];
+    navail += avail[i];
   }
   if (navail < p->needed) return -1;
   uint32_t nf = s->nd.numa_flags[n];
@@ -1893,15 +2105,35 @@ static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod) {
                  : (s->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED ? KO_NUMA_MOST : KO_NUMA_LEAST);
   int excl_policy = (int)((p->bind >> KS_CPU_EXCL_SHIFT) & 3u);
   int bind = (p->bind & KS_CPU_BIND_POLICY_MASK) == KS_CPU_BIND_FULL_PCPUS ? KO_BIND_FULL_PCPUS : KO_BIND_SPREAD_BY_PCPUS;
-  if (ko_take_cpus(t, 1, avail, NULL, ex, p->needed, bind, excl_policy, strategy, res) != 0) return -1;
+  int numa_alloc = 0;
+  if (c && c->on && c->out->affinity)
+    for (int k = 0; k < KS_MAX_NUMA; k++) numa_alloc |= c->out->alloc[k][0] != 0 || c->out->alloc[k][1] != 0;
+  if (numa_alloc) {
+    /* per allocated NUMA node (NUMANodeResources in node order), against the allocation before this pod */
+    memset(res, 0, sizeof(res));
+    int taken = 0;
+    for (int k = 0; k < KS_MAX_NUMA; k++) {
+      if (!c->out->alloc[k][0] && !c->out->alloc[k][1]) continue;
+      for (int i = 0; i < t->ncpus; i++) sub[i] = avail[i] && t->node[i] == k;
+      if (ko_take_cpus(t, 1, sub, NULL, ex, c->out->cpus[k], bind, excl_policy, strategy, part) != 0) return -1;
+      for (int i = 0; i < t->ncpus; i++) {
+        res[i] |= part[i];
+        taken += part[i];
+      }
+    }
+    if (taken != p->needed) return -1;
+  } else if (ko_take_cpus(t, 1, avail, NULL, ex, p->needed, bind, excl_policy, strategy, res) != 0) {
+    return -1;
+  }
   uint64_t *o = s->cpusets + (size_t)pod * KS_CPU_WORDS;
   int taken = 0;
-  for (int c = 0; c < t->ncpus; c++) {
-    if (!res[c]) continue;
-    al[c] = 1;
-    ex[c] = (int8_t)excl_policy;
-    o[c >> 6] |= 1ull << (c & 63);
+  for (int i = 0; i < t->ncpus; i++) {
+    if (!res[i]) continue;
+    al[i] = 1;
+    ex[i] = (int8_t)excl_policy;
+    o[i >> 6] |= 1ull << (i & 63);
     taken++;
+    if (s->numa_loaded && t->node[i] >= 0 && t->node[i] < KS_MAX_NUMA) s->numa_cs[(size_t)n * KS_MAX_NUMA + t->node[i]]++;
   }
   s->nd.numa_cpus[n] += taken;
   return 0;
@@ -1909,17 +2141,14 @@ static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod) {
 
 /* NodeNUMAResource Reserve on a node with a NUMA policy: Allocate with the Filter's hint, then
  * NodeAllocation.addPodAllocation adds the NUMANodeResources (node_allocation.go:86-99) */
-static void numa_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
-  if (!s->cfg.numa.enable || p->reqzero || !s->numa_loaded || node_numa_policy(s, n) == 0) return;
-  ko_eff e;
-  node_eff(&s->nd, n, &e);
-  int64_t alloc[KS_MAX_NUMA][2];
-  if (numa_policy_eval(s, p, n, &e, NULL, alloc) != 0) return;
+static void numa_reserve(ko_sched *s, const ko_pod *p, int64_t n, const ko_npol *c) {
+  if (!c->on || c->reasons || !s->numa_loaded) return;
   for (int k = 0; k < s->numa_count[n]; k++) {
-    if (!alloc[k][0] && !alloc[k][1]) continue;
+    const int64_t *a = c->out->alloc[k];
+    if (!a[0] && !a[1]) continue;
     const size_t o = (size_t)n * KS_MAX_NUMA + k;
-    s->numa_used[o * 2] += alloc[k][0];
-    s->numa_used[o * 2 + 1] += alloc[k][1];
+    s->numa_used[o * 2] += a[0];
+    s->numa_used[o * 2 + 1] += a[1];
     s->numa_present[o] = 1;
   }
 }
@@ -1994,7 +2223,16 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     }
     out[i].node = (int32_t)best_n;
     out[i].score = best;
-    if (p.bind && cpu_reserve(s, &p, best_n, i) != 0) {
+    /* the chosen node's NUMA policy path on the pre-Reserve state (the Filter's affinity and allocation) */
+    ko_eff e0;
+    ko_rstate st0;
+    rsv_restore(s, &p, best_n, &st0);
+    e0 = st0.e;
+    ko_numa_out no;
+    ko_npol npc;
+    numa_policy_ctx(s, &p, best_n, &e0, &npc, &no);
+    const uint32_t allow = npol_allow(s, &p, best_n, &e0, &npc);
+    if (p.bind && cpu_reserve(s, &p, best_n, i, &npc) != 0) {
       /* NodeNUMAResource Reserve -> Allocate failed: every Reserve plugin unreserves */
       out[i].status = KS_S_RESERVE_FAILED;
       out[i].score = 0;
@@ -2004,8 +2242,8 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
       out[i].reservation = s->nom[best_n];
       rsv_reserve(s, &p, s->nom[best_n]);
     }
-    dev_reserve(s, &p, best_n, &out[i].gpu_minors, &out[i].rdma_minors);
-    numa_reserve(s, &p, best_n);
+    dev_reserve(s, &p, best_n, &out[i].gpu_minors, &out[i].rdma_minors, allow);
+    numa_reserve(s, &p, best_n, &npc);
     node_reserve(s, &p, best_n);
     quota_reserve(s, &p);
   }
@@ -2037,6 +2275,21 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
   }
   free(norm);
   free(dnorm);
+  return 0;
+}
+
+/* test entry: DeviceShare's topology hints for pod 0 of pc on node n (tests/golden/deviceshare_hints.json) */
+int ko_dev_hints(ko_sched *s, const ks_pod_cols *pc, int64_t n, int *lists, int *nh, uint32_t *masks, int *prefs) {
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  ko_devhints h;
+  dev_hints(s, &p, n, &h);
+  *lists = h.lists;
+  *nh = h.nh;
+  for (int i = 0; i < h.nh; i++) {
+    masks[i] = h.mask[i];
+    prefs[i] = h.pref[i];
+  }
   return 0;
 }
 

@@ -65,6 +65,11 @@ def lib():
         L.ko_spread_order.restype = C.c_int
         L.ko_spread_order.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.ko_topo_finish.argtypes = [C.c_void_p]
+        L.ko_topology_merge.restype = C.c_int
+        L.ko_topology_merge.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+        L.ko_dev_hints.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int64, C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int), C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -112,6 +117,25 @@ def spread_order(t: KoTopo, strategy: str = "Most"):
     out = np.zeros(KO_MAX_CPUS, np.int32)
     k = lib().ko_spread_order(C.byref(t), STRATEGY[strategy], out.ctypes.data)
     return [int(x) for x in out[:k]]
+
+
+POLICY = {"best-effort": abi.KS_NUMA_POLICY_BEST_EFFORT, "restricted": abi.KS_NUMA_POLICY_RESTRICTED,
+          "single-numa-node": abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE}
+
+
+def topology_merge(policy: str, numa_nodes: int, lists):
+    """The topology manager's Merge (koord_oracle.c ko_merge_hints) over hint lists after
+    filterProvidersHints; a hint is (mask, preferred, score), mask 0 = nil.  Returns (admit, mask, preferred)."""
+    lens = np.array([len(l) for l in lists] or [0], np.int32)
+    flat = [h for l in lists for h in l] or [(0, 0, 0)]
+    masks = np.array([h[0] for h in flat], np.uint32)
+    prefs = np.array([int(h[1]) for h in flat], np.int32)
+    scores = np.array([h[2] for h in flat], np.int64)
+    aff = C.c_uint32()
+    pref = C.c_int()
+    admit = lib().ko_topology_merge(POLICY[policy], numa_nodes, len(lists), lens.ctypes.data, masks.ctypes.data,
+                                    prefs.ctypes.data, scores.ctypes.data, C.byref(aff), C.byref(pref))
+    return admit, aff.value, bool(pref.value)
 
 
 class Oracle:
@@ -175,6 +199,16 @@ class Oracle:
         self.L.ko_eval_pod(self.h, C.byref(cols), reasons.ctypes.data_as(abi.PU32),
                            scores.ctypes.data_as(abi.P64), total.ctypes.data_as(abi.P64))
         return reasons, scores.reshape(self.n, abi.KS_NUM_SCORE_PLUGINS), total
+
+    def dev_hints(self, pod: PodTable, node: int):
+        """DeviceShare's topology hints for pod 0 on `node`: (lists, [(mask, preferred)]); lists 0 = none."""
+        cols = pod.ks()
+        lists, nh = C.c_int(), C.c_int()
+        masks = np.zeros(16, np.uint32)
+        prefs = np.zeros(16, np.int32)
+        self.L.ko_dev_hints(self.h, C.byref(cols), node, C.byref(lists), C.byref(nh), masks.ctypes.data,
+                            prefs.ctypes.data)
+        return lists.value, [(int(masks[i]), bool(prefs[i])) for i in range(nh.value)]
 
     def read_nodes(self) -> NodeState:
         st = NodeState(self.n)
