@@ -120,10 +120,8 @@ def host_cpus():
 def time_oracle(w, threads: int, n_pods: int):
     from oracle.oracle import Oracle
 
-    rs, dv, cs = w.reservations, w.devices, w.cpus
-    o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy() if w.quotas is not None else None, nthreads=threads,
-               reservations=rs.copy() if rs is not None else None, devices=dv.copy() if dv is not None else None,
-               cpu_state=cs.copy() if cs is not None else None)
+    cs = w.cpus
+    o = Oracle(w.cfg, w.nodes.copy(), nthreads=threads, **w.tables())
     try:
         t = time.perf_counter()
         r = o.schedule(w.pods.rows(range(n_pods)))
@@ -207,7 +205,7 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
     prof.candidates = args.candidates
     cfg = prof.to_ks_config()
     cfg.profile = 0
-    ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices, w.cpus)
+    ev = runtime.Evaluator(cfg, w.nodes, **w.tables(copy=False))
     try:
         nshards = 1
         if shard and world > 1:

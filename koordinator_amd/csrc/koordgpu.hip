@@ -651,8 +651,8 @@ __global__ __launch_bounds__(1024) void rsv_normalize_debug_kernel(int64_t n, co
 constexpr int kCpusetStage = 1024;
 
 __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* list, const int32_t* count_p,
-                                                     const PodRec* pods, CpuSet* out, const uint32_t* numa_flags,
-                                                     int32_t default_most, int64_t n) {
+                                                     const uint32_t* split, const PodRec* pods, CpuSet* out,
+                                                     const uint32_t* numa_flags, int32_t default_most, int64_t n) {
   __shared__ int2 stage[kCpusetStage];
   const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t count = *count_p;
@@ -669,27 +669,54 @@ __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* lis
       const CpuTopo& t = cpu.topo[tid];
       const uint32_t cb = pods[pod].cpu_bind;
       const uint32_t nf = numa_flags[node];
-      CpuAcc a;
-      a.t = &t;
       const CpuSet alloc = cpu.allocated[node], xp = cpu.excl_pcpu[node], xn = cpu.excl_numa[node];
-      a.al = cs_andnot(cs_andnot(t.all, alloc), cpu.reserved[node]);
-      a.res = cs_zero();
-      a.exc_cores = cs_zero();
-      a.exc_nodes = 0;
+      const CpuSet avail = cs_andnot(cs_andnot(t.all, alloc), cpu.reserved[node]);
+      CpuSet exc_cores = cs_zero();
+      uint64_t exc_nodes = 0;
       for (int w = 0; w < kCpuW; ++w) {
-        for (uint64_t b = xp.w[w]; b; b &= b - 1) cs_add(a.exc_cores, t.core_of[w * 64 + __builtin_ctzll(b)]);
-        for (uint64_t b = xn.w[w]; b; b &= b - 1) a.exc_nodes |= 1ull << t.node_of[w * 64 + __builtin_ctzll(b)];
+        for (uint64_t b = xp.w[w]; b; b &= b - 1) cs_add(exc_cores, t.core_of[w * 64 + __builtin_ctzll(b)]);
+        for (uint64_t b = xn.w[w]; b; b &= b - 1) exc_nodes |= 1ull << t.node_of[w * 64 + __builtin_ctzll(b)];
       }
-      a.excl = (int32_t)((cb >> KS_CPU_EXCL_SHIFT) & 3u);
-      a.most = (nf & KS_NUMA_ALLOC_MOST) ? true : ((nf & KS_NUMA_ALLOC_LEAST) ? false : default_most != 0);
-      a.needed = (int32_t)(cb >> 8);
-      if (!take_cpus(a, (int)(cb & KS_CPU_BIND_POLICY_MASK), keys)) a.res = cs_zero();  // unreachable (count checked)
-      cpu.allocated[node] = cs_or(alloc, a.res);
-      if (a.excl == KS_CPU_EXCL_PCPU_LEVEL) cpu.excl_pcpu[node] = cs_or(xp, a.res);
-      if (a.excl == KS_CPU_EXCL_NUMA_NODE_LEVEL) cpu.excl_numa[node] = cs_or(xn, a.res);
-      out[pod] = a.res;
+      const int32_t excl = (int32_t)((cb >> KS_CPU_EXCL_SHIFT) & 3u);
+      const bool most = (nf & KS_NUMA_ALLOC_MOST) ? true : ((nf & KS_NUMA_ALLOC_LEAST) ? false : default_most != 0);
+      // allocateCPUSet (resource_manager.go:314-401): with a NUMA allocation one takeCPUs per allocated NUMA node over
+      // its available CPUs, each against the allocation before this pod; else one over the whole node
+      const uint32_t sp = split[pod];
+      CpuSet res = cs_zero();
+      for (int k = 0; k < (sp ? kNumaDev : 1); ++k) {
+        const int32_t need = sp ? (int32_t)((sp >> (8 * k)) & 0xFFu) : (int32_t)(cb >> 8);
+        if (sp && need == 0) continue;
+        CpuAcc a;
+        a.t = &t;
+        a.al = sp ? cs_and(avail, t.node_mask[k]) : avail;
+        a.res = cs_zero();
+        a.exc_cores = exc_cores;
+        a.exc_nodes = exc_nodes;
+        a.excl = excl;
+        a.most = most;
+        a.needed = need;
+        if (take_cpus(a, (int)(cb & KS_CPU_BIND_POLICY_MASK), keys)) res = cs_or(res, a.res);  // (count checked)
+      }
+      cpu.allocated[node] = cs_or(alloc, res);
+      if (excl == KS_CPU_EXCL_PCPU_LEVEL) cpu.excl_pcpu[node] = cs_or(xp, res);
+      if (excl == KS_CPU_EXCL_NUMA_NODE_LEVEL) cpu.excl_numa[node] = cs_or(xn, res);
+      out[pod] = res;
     }
     __syncthreads();
+  }
+}
+
+// CPUs of each NUMA node available to cpuset pods (topology CPUs of the node - allocated - reserved), for the NUMA
+// policy path's allocateCPUSet check; NUMA node k = the topology's k-th NUMA id (ids are 0..n-1, ks_load_cpu_state).
+__global__ void numa_free_kernel(DevCpu cpu, DevNuma nv, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t tid = cpu.topo_id[i];
+  for (int k = 0; k < kNumaDev; ++k) {
+    int32_t f = 0;
+    if (tid >= 0 && k < cpu.topo[tid].nnodes)
+      f = cs_count(cs_andnot(cs_andnot(cpu.topo[tid].node_mask[k], cpu.allocated[i]), cpu.reserved[i]));
+    nv.free[(int64_t)k * nv.npad + i] = f;
   }
 }
 
@@ -840,9 +867,12 @@ struct ks_ctx {
   void* numa_blob = nullptr;
   DevNuma nv{};
   DevNuma* dnv = nullptr;    // device copy (always allocated: kernels take its address)
-  int64_t* numa_used_ckpt = nullptr;
-  uint32_t* numa_present_ckpt = nullptr;
+  char* numa_ckpt = nullptr;       // checkpoint copy of the mutable NUMA block (numa_mut_bytes)
   int64_t numa_policy_nodes = 0;  // nodes with a NUMA topology policy
+  std::vector<int8_t> h_numa_k;    // per node: NUMA node count of a policy node (0 = no policy / none)
+  std::vector<uint16_t> h_dev_ids; // per node: NUMA ids of the device topology (DeviceShare hints)
+  std::vector<int8_t> h_cpu_nn;    // per node: NUMA nodes of its CPU topology (0 = none, -1 = ids not 0..n-1)
+  uint32_t* cpuset_split = nullptr;  // [cpuset_cap] per pod (CommitArgs.cpuset_split)
   // stats
   ks_stats stats{};
   std::vector<hipEvent_t> ev_pool;
@@ -1263,6 +1293,8 @@ static int upload_prep_nodes(ks_ctx* ctx) {
 static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
 static int dev_install(ks_ctx* ctx, const ks_device_cols* dc);
 static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h);
+static int check_dev_numa(ks_ctx* ctx);
+static int numa_refresh_free(ks_ctx* ctx);
 
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
@@ -1521,6 +1553,23 @@ static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
     }
     for (int64_t n = 0; n < ctx->n; ++n) flags[n] = dc->flags ? dc->flags[n] : 0;
   }
+  // NUMA nodes of the device topology per node, as dev_hints (ks_numa.h) derives them
+  ctx->h_dev_ids.assign((size_t)ctx->n, 0);
+  for (int64_t n = 0; dc && n < ctx->n; ++n) {
+    const uint64_t topo = (uint64_t)total[(size_t)kDevTopoW * np + n], meta = (uint64_t)total[(size_t)kDevMetaW * np + n];
+    uint32_t ids = 0;
+    for (int k = 0; k < kGpus; ++k) {
+      const uint32_t pc = (uint32_t)(topo >> (4 * k)) & 0xFu;
+      bool ex = false;
+      for (int q = 0; q < 3; ++q) ex |= total[((size_t)q * kGpus + k) * np + n] != 0;
+      if (ex && pc < 8u) ids |= 1u << ((uint32_t)(meta >> (8 * pc)) & 0xFu);
+    }
+    for (int j = 0; j < kRdma; ++j) {
+      const uint32_t pc = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
+      if (total[((size_t)kDevRdmaW + j) * np + n] != 0 && pc < 8u) ids |= 1u << ((uint32_t)(meta >> (8 * pc)) & 0xFu);
+    }
+    ctx->h_dev_ids[(size_t)n] = (uint16_t)ids;
+  }
   dev_free(ctx->dev_blob);
   if (dev_alloc(ctx, &ctx->dev_blob, bytes) != KS_OK) return KS_ENOMEM;
   HIPCHK(ctx, hipMemcpyAsync(ctx->dev_blob, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -1538,7 +1587,7 @@ static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
   HIPCHK(ctx, hipMemcpyAsync(ctx->ddv, &ctx->dv, sizeof(DevDev), hipMemcpyHostToDevice, ctx->stream));
   ctx->dev_loaded = dc != nullptr;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  return KS_OK;
+  return check_dev_numa(ctx);
 }
 
 int ks_load_devices(ks_ctx* ctx, const ks_device_cols* dev, int64_t n) {
@@ -1652,9 +1701,13 @@ int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, 
   const int64_t n = ctx->n, np = ctx->npad;
   std::vector<CpuTopo> tt((size_t)std::max(ntopo, 1));
   std::vector<int32_t> cpc;
+  std::vector<int8_t> dense((size_t)std::max(ntopo, 1), 1);
   for (int32_t i = 0; i < ntopo; ++i) {
     if (int rc = build_cpu_topo(ctx, topos[i], i, tt[i]); rc != KS_OK) return rc;
     cpc.push_back(tt[i].cpc);
+    int32_t mx = 0;
+    for (int c = 0; c < topos[i].ncpus; ++c) mx = std::max(mx, topos[i].numa_node[c]);
+    dense[(size_t)i] = mx + 1 == tt[i].nnodes;  // NUMA ids 0..nnodes-1: topology index == NUMA id
   }
   std::vector<int32_t> tid((size_t)np, -1), freec((size_t)np, -1), ncpu((size_t)np, 0);
   std::vector<CpuSet> al((size_t)np, cs_zero()), xp((size_t)np, cs_zero()), xn((size_t)np, cs_zero()), rs((size_t)np, cs_zero());
@@ -1716,6 +1769,11 @@ int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, 
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->cpu_cpc = cpc;
   ctx->cpu_loaded = true;
+  ctx->h_cpu_nn.assign((size_t)n, 0);
+  for (int64_t i = 0; i < n; ++i)
+    if (const int32_t ti = tid[(size_t)i]; ti >= 0) ctx->h_cpu_nn[(size_t)i] = dense[(size_t)ti] ? (int8_t)tt[(size_t)ti].nnodes : (int8_t)-1;
+  if (int rc = numa_refresh_free(ctx); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
 
@@ -1744,20 +1802,71 @@ int ks_fetch_cpusets(ks_ctx* ctx, uint64_t* out, int32_t p) {
   return KS_OK;
 }
 
+// NUMA nodes' available CPUs from the CPU state (numa_free_kernel); zero without a loaded CPU state
+static int numa_refresh_free(ks_ctx* ctx) {
+  if (!ctx->numa_blob) return KS_OK;
+  const size_t np = (size_t)ctx->npad;
+  if (!ctx->cpu_loaded) {
+    HIPCHK(ctx, hipMemsetAsync(ctx->nv.free, 0, (size_t)kNumaDev * np * 4, ctx->stream));
+    return KS_OK;
+  }
+  // the per-NUMA cpuset takes index the topology's NUMA nodes by NUMA id, and a cpu-bind pod admitted with a nil
+  // affinity (single NUMA node) takes from NUMA node 0: the CPU topology's NUMA ids are 0..m-1 with m <= the count
+  for (int64_t i = 0; i < ctx->n && i < (int64_t)ctx->h_numa_k.size() && i < (int64_t)ctx->h_cpu_nn.size(); ++i) {
+    const int k = ctx->h_numa_k[(size_t)i], m = ctx->h_cpu_nn[(size_t)i];
+    if (k > 0 && m != 0 && (m < 0 || m > k))
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: NUMA-policy node whose CPU topology NUMA ids are not 0..m-1 with m <= %d",
+              (long long)i, k);
+  }
+  if (ctx->n > 0)
+    hipLaunchKernelGGL(numa_free_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu, ctx->nv,
+                       ctx->n);
+  HIPCHK(ctx, hipGetLastError());
+  // a load re-bases the checkpoint (as the CPU state's own checkpoint is re-based by ks_load_cpu_state)
+  char* ck_free = ctx->numa_ckpt + ((char*)ctx->nv.free - (char*)ctx->nv.used);
+  HIPCHK(ctx, hipMemcpyAsync(ck_free, ctx->nv.free, (size_t)kNumaDev * np * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  return KS_OK;
+}
+
+// DeviceShare as a hint provider on NUMA-policy nodes: its hint masks range over the device topology's NUMA nodes,
+// which must be NUMA nodes of the node (ids < its NUMA count), at most kDevHintIds of them, on nodes with at most
+// kDevHintIds NUMA nodes (this bounds the merge's cartesian product, ks_numa.h).
+static int check_dev_numa(ks_ctx* ctx) {
+  if (!ctx->cfg.deviceshare.enable || ctx->h_numa_k.empty() || ctx->h_dev_ids.empty()) return KS_OK;
+  for (int64_t i = 0; i < ctx->n; ++i) {
+    const int k = ctx->h_numa_k[(size_t)i];
+    const uint32_t ids = ctx->h_dev_ids[(size_t)i];
+    if (k == 0 || ids == 0) continue;
+    if (k > kDevHintIds || __builtin_popcount(ids) > kDevHintIds || (ids >> k) != 0)
+      KS_FAIL(ctx, KS_EUNSUPPORTED,
+              "node %lld: DeviceShare NUMA hints need the devices on at most %d NUMA nodes of a node with at most %d "
+              "(%d NUMA nodes, device NUMA ids 0x%x)", (long long)i, kDevHintIds, kDevHintIds, k, ids);
+  }
+  return KS_OK;
+}
+
 // NUMA node resources of the policy nodes; nc == nullptr installs an empty table (every policy node
 // then reports "missing NUMA resources", as the reference does without a NodeResourceTopology).
+// Layout: count | total | mutable {used, off, cs, free, present} | checkpoint copy of the mutable block.
+static size_t numa_mut_bytes(size_t np) {
+  constexpr int K = kNumaDev;
+  return 2 * K * np * 8 + K * np * 8 + 2 * K * np * 4 + align16(np * 4);
+}
+
 static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h) {
   const size_t np = (size_t)ctx->npad;
   constexpr int K = kNumaDev;
   const size_t o_cnt = 0, o_tot = align16(np * 4), o_used = o_tot + 2 * K * np * 8, o_off = o_used + 2 * K * np * 8,
-               o_pres = o_off + K * np * 8, o_uck = o_pres + align16(np * 4), o_pck = o_uck + 2 * K * np * 8,
-               bytes = o_pck + align16(np * 4);
+               o_cs = o_off + K * np * 8, o_free = o_cs + K * np * 4, o_pres = o_free + K * np * 4,
+               o_ck = o_pres + align16(np * 4), bytes = o_ck + numa_mut_bytes(np);
   std::vector<char> h(bytes, 0);
   int32_t* cnt = (int32_t*)(h.data() + o_cnt);
   int64_t* tot = (int64_t*)(h.data() + o_tot);
   int64_t* used = (int64_t*)(h.data() + o_used);
   int64_t* off = (int64_t*)(h.data() + o_off);
+  int32_t* csv = (int32_t*)(h.data() + o_cs);
   uint32_t* pres = (uint32_t*)(h.data() + o_pres);
+  ctx->h_numa_k.assign((size_t)ctx->n, 0);
   for (int64_t i = 0; nc && i < ctx->n; ++i) {
     const uint32_t pol = (flags_h[i] >> KS_NUMA_POLICY_SHIFT) & 3u;
     const int32_t c = nc->count[i];
@@ -1765,12 +1874,14 @@ static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t
     if (pol == 0) continue;  // the policy-None path never reads NUMA-node resources
     if (c > K) KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: %d NUMA nodes with a NUMA policy (the device evaluates up to %d)", (long long)i, c, K);
     cnt[i] = c;
+    ctx->h_numa_k[(size_t)i] = (int8_t)c;
     const double ratio = ratio_h ? ratio_h[i] : 0.0;
     for (int k = 0; k < c; ++k) {
       const size_t o = (size_t)i * KS_MAX_NUMA + k;
       const int64_t ac = nc->alloc_cpu ? nc->alloc_cpu[o] : 0, am = nc->alloc_memory ? nc->alloc_memory[o] : 0;
       const int64_t uc = nc->used_cpu ? nc->used_cpu[o] : 0, um = nc->used_memory ? nc->used_memory[o] : 0;
-      const int64_t cs = nc->cpuset_cpus ? (int64_t)nc->cpuset_cpus[o] * 1000 : 0;
+      const int32_t cpus = nc->cpuset_cpus ? nc->cpuset_cpus[o] : 0;
+      const int64_t cs = (int64_t)cpus * 1000;
       const int64_t lim = (int64_t)1 << 50;
       if (ac < 0 || am < 0 || uc < 0 || um < 0 || cs < 0 || ac > lim || am > lim || uc > lim || um > lim || cs > lim)
         KS_FAIL(ctx, KS_EINVAL, "node %lld NUMA %d: quantity out of range", (long long)i, k);
@@ -1780,6 +1891,7 @@ static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t
       used[(size_t)(0 * K + k) * np + i] = uc;
       used[(size_t)(1 * K + k) * np + i] = um;
       off[(size_t)k * np + i] = ratio > 1.0 ? (int64_t)std::ceil((double)cs * ratio) - cs : 0;
+      csv[(size_t)k * np + i] = cpus;
       const bool present = nc->used_present ? nc->used_present[o] != 0 : (uc != 0 || um != 0);
       if (present) pres[i] |= 1u << k;
     }
@@ -1792,17 +1904,18 @@ static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t
   v.count = (const int32_t*)(b + o_cnt);
   v.total = (const int64_t*)(b + o_tot);
   v.used = (int64_t*)(b + o_used);
-  v.off = (const int64_t*)(b + o_off);
+  v.off = (int64_t*)(b + o_off);
+  v.cs = (int32_t*)(b + o_cs);
+  v.free = (int32_t*)(b + o_free);
   v.present = (uint32_t*)(b + o_pres);
   v.flags = ctx->d.numa_flags;
   v.npad = ctx->npad;
-  ctx->numa_used_ckpt = (int64_t*)(b + o_uck);
-  ctx->numa_present_ckpt = (uint32_t*)(b + o_pck);
-  HIPCHK(ctx, hipMemcpyAsync(ctx->numa_used_ckpt, v.used, 2 * K * np * 8, hipMemcpyDeviceToDevice, ctx->stream));
-  HIPCHK(ctx, hipMemcpyAsync(ctx->numa_present_ckpt, v.present, np * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  ctx->numa_ckpt = b + o_ck;
   HIPCHK(ctx, hipMemcpyAsync(ctx->dnv, &v, sizeof(DevNuma), hipMemcpyHostToDevice, ctx->stream));
+  if (int rc = numa_refresh_free(ctx); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->numa_ckpt, v.used, numa_mut_bytes(np), hipMemcpyDeviceToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  return KS_OK;
+  return check_dev_numa(ctx);
 }
 
 int ks_load_numa_nodes(ks_ctx* ctx, const ks_numa_node_cols* nc) {
@@ -2227,23 +2340,14 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
         KS_FAIL(ctx, KS_EINVAL, "pod %d: cpu_bind 0x%x invalid", i, cb);
       if (cpu <= 0 || cpu % 1000 != 0 || cpu / 1000 > KS_MAX_CPUS)
         KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
-      // takeCPUs' FullPCPUs fallback can take a whole core past numCPUsNeeded when the request is not a
-      // whole number of cores (cpu_accumulator.go:163-175); the count-only commit does not model that
-      if (ctx->numa_policy_nodes > 0)
-        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: cpuset pods on clusters with NUMA topology policies are not supported", i);
+      // a FullPCPUs request that is not a whole number of cores fails the Filter's SMT alignment check per node
+      // (plugin.go:300-310); the count-only commit does not carry per-node cores, so such pods are refused
       if (pol == KS_CPU_BIND_FULL_PCPUS)
         for (int32_t cpc : ctx->cpu_cpc)
           if (cpc > 1 && (cpu / 1000) % cpc != 0)
             KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: FullPCPUs request of %lld CPUs is not a whole number of %d-thread cores", i,
                     (long long)(cpu / 1000), cpc);
     }
-  }
-  if (ctx->numa_policy_nodes > 0 && ctx->cfg.deviceshare.enable) {
-    const int64_t* g[4] = {pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio, pc->rdma};
-    for (int q = 0; q < 4; ++q)
-      for (int32_t i = 0; g[q] && i < p; ++i)
-        if (g[q][i] != 0)
-          KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: device pods on clusters with NUMA topology policies (DeviceShare hints) are not supported", i);
   }
   if (pc->joint) {
     for (int32_t i = 0; i < p; ++i) {
@@ -2514,6 +2618,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   ca.dev_M = ctx->dev_M;
   ca.cpuset_list = ctx->cpuset_list;
   ca.cpuset_n = ctx->cpuset_n;
+  ca.cpuset_split = ctx->cpuset_split;
   ca.numa_bytes = (int32_t)numa_cache_bytes(ctx);
   ca.nv = ctx->dnv;
   const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes,
@@ -2581,10 +2686,11 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     dev_free(p);
     ctx->cpuset_list = nullptr;
     const int32_t cap = std::max<int32_t>(np, 64);
-    if (dev_alloc(ctx, &p, (size_t)cap * 8 + 16 + (size_t)cap * sizeof(CpuSet)) != KS_OK) return KS_ENOMEM;
+    if (dev_alloc(ctx, &p, (size_t)cap * 8 + 16 + (size_t)cap * sizeof(CpuSet) + (size_t)cap * 4) != KS_OK) return KS_ENOMEM;
     ctx->cpuset_list = (int2*)p;
     ctx->cpuset_n = (int32_t*)((char*)p + (size_t)cap * 8);
     ctx->cpuset_out = (CpuSet*)((char*)p + (size_t)cap * 8 + 16);
+    ctx->cpuset_split = (uint32_t*)((char*)p + (size_t)cap * 8 + 16 + (size_t)cap * sizeof(CpuSet));
     ctx->cpuset_cap = cap;
   }
   hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
@@ -2622,8 +2728,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   if (ctx->cpu_loaded && ctx->n > 0) {
     // the CPU ids of the pass's cpu-bind Reserves (ks_cpuset.h), per node in placement order
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
-                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const PodRec*)ctx->st.recs,
-                       ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
+                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
+                       (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
                        (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
     HIPCHK(ctx, hipGetLastError());
   }
@@ -2693,10 +2799,8 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->dev_used_ckpt, ctx->dv.used, (size_t)kDevQW * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->cpu_loaded)
     HIPCHK(ctx, hipMemcpyAsync(ctx->cpu_ckpt, ctx->cpu.allocated, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
-  if (ctx->numa_blob) {
-    HIPCHK(ctx, hipMemcpyAsync(ctx->numa_used_ckpt, ctx->nv.used, (size_t)2 * kNumaDev * ctx->npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->numa_present_ckpt, ctx->nv.present, (size_t)ctx->npad * 4, hipMemcpyDeviceToDevice, ctx->stream));
-  }
+  if (ctx->numa_blob)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->numa_ckpt, ctx->nv.used, numa_mut_bytes((size_t)ctx->npad), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_allocd_ckpt, ctx->rv.allocd, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
@@ -2717,10 +2821,8 @@ int ks_restore(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->dv.used, ctx->dev_used_ckpt, (size_t)kDevQW * ctx->dv.npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->cpu_loaded)
     HIPCHK(ctx, hipMemcpyAsync(ctx->cpu.allocated, ctx->cpu_ckpt, (size_t)3 * ctx->cpu.npad * sizeof(CpuSet), hipMemcpyDeviceToDevice, ctx->stream));
-  if (ctx->numa_blob) {
-    HIPCHK(ctx, hipMemcpyAsync(ctx->nv.used, ctx->numa_used_ckpt, (size_t)2 * kNumaDev * ctx->npad * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->nv.present, ctx->numa_present_ckpt, (size_t)ctx->npad * 4, hipMemcpyDeviceToDevice, ctx->stream));
-  }
+  if (ctx->numa_blob)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->nv.used, ctx->numa_ckpt, numa_mut_bytes((size_t)ctx->npad), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));

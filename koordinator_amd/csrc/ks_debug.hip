@@ -18,10 +18,9 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   load_node<NSC>(c, d, i, 1, r);
   const PodRec p = *pod;
   RsvOut ro;
-  EvalOut o = eval_full<NSC, true, false, 7>(
+  EvalOut o = eval_full<NSC, true, false, 15>(
       c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
-      [&]() { return dev_eval<false>(c, p, DevGView{*dv, i}); }, &ro);
-  numa_policy_fix<NSC, true, 15>(c, p, r, o, [&]() { return NumaGView{*nv, i}; });
+      [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;

@@ -276,9 +276,29 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
   return dev_joint(G, R, g, same, ~0u, swpref, om, orm);
 }
 
-// DeviceShare Filter + Score (+ the allocation with ALLOC) of one (pod, node).
+// The minors of each type on the NUMA nodes of `allow` (a bit per NUMA node id; ~0u = every minor): with a
+// topology-manager affinity, filterNodeDevice keeps only devices with a topology on an allowed NUMA node
+// (device_allocator.go:134-158).
+template <typename V>
+__device__ __forceinline__ void dev_allowed(const V& v, uint32_t allow, uint32_t& gin, uint32_t& rin) {
+  gin = 0xFFu;
+  rin = 0xFFu;
+  if (allow == ~0u) return;
+  const uint64_t topo = (uint64_t)v.tot(kDevTopoW), meta = (uint64_t)v.tot(kDevMetaW);
+  gin = rin = 0u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t pg = (uint32_t)(topo >> (4 * k)) & 0xFu, pr = (uint32_t)(topo >> (32 + 4 * k)) & 0xFu;
+    gin |= (pg < 8u && ((allow >> ((uint32_t)(meta >> (8 * pg)) & 0xFu)) & 1u)) ? (1u << k) : 0u;
+    rin |= (pr < 8u && ((allow >> ((uint32_t)(meta >> (8 * pr)) & 0xFu)) & 1u)) ? (1u << k) : 0u;
+  }
+}
+
+// DeviceShare Filter + Score (+ the allocation with ALLOC) of one (pod, node); allow restricts the devices to a
+// NUMA affinity (dev_allowed).
 template <bool ALLOC, typename V>
-__device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const V& v, GpuReq* req_out = nullptr) {
+__device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const V& v, GpuReq* req_out = nullptr,
+                                           uint32_t allow = ~0u) {
   DevOut o{0u, 0, 0u, 0u};
   if (!v.present()) return o;  // no device info: Filter passes, Score 0
   GpuReq g;
@@ -293,6 +313,8 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   // the allocation itself (Reserve) needs the walk then.
   const bool walk = joint && (ALLOC || same || g.rdesired > 1);
   const bool scores = ALLOC || walk;
+  uint32_t gin, rin;
+  dev_allowed(v, allow, gin, rin);
   const uint64_t topo = (walk || ALLOC) ? (uint64_t)v.tot(kDevTopoW) : 0ull;
   DevType G, R;
   G.fit = R.fit = 0;
@@ -308,7 +330,7 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
       const int64_t t[3] = {v.tot(k), v.tot(kGpus + k), v.tot(2 * kGpus + k)};
       const int64_t u[3] = {v.use(k), v.use(kGpus + k), v.use(2 * kGpus + k)};
       const int64_t f[3] = {t[0] > u[0] ? t[0] - u[0] : 0, t[1] > u[1] ? t[1] - u[1] : 0, t[2] > u[2] ? t[2] - u[2] : 0};
-      const bool exists = t[0] || t[1] || t[2];
+      const bool exists = (t[0] || t[1] || t[2]) && ((gin >> k) & 1u);
       const bool has_free = exists && (f[0] || f[1] || f[2]);
       const bool fits = has_free && (!g.has_core || g.core <= f[0]) && g.mem <= f[1] && g.ratio <= f[2];
 #pragma unroll
@@ -325,7 +347,8 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
     int64_t tsum = 0, fsum = 0;
 #pragma unroll
     for (int j = 0; j < kRdma; ++j) {
-      const int64_t t = v.tot(kDevRdmaW + j), u = v.use(kDevRdmaW + j);
+      const bool in = ((rin >> j) & 1u) != 0;
+      const int64_t t = in ? v.tot(kDevRdmaW + j) : 0, u = in ? v.use(kDevRdmaW + j) : 0;
       const int64_t f = t > u ? t - u : 0;
       tsum += t;
       fsum += f;

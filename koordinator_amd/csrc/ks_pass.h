@@ -96,8 +96,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       const PodRec pod = load_pod_uniform(a.pods + cursor + p);
       EvalOut o = eval_full<NSC, false, true, FEAT>(
           a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
-          [&]() { return dev_eval<false>(a.c, pod, DevGView{*a.dv, node}); });
-      numa_policy_fix<NSC, false, FEAT>(a.c, pod, r, o, [&]() { return NumaGView{*a.nv, node}; });
+          [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
       if ((FEAT & 4) && a.phase == 0) {
         // DeviceShare normalization max over the feasible nodes, witness = lowest index holding it
         const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | (0xFFFFFFFFull - (uint64_t)node));
@@ -217,6 +216,7 @@ struct CommitArgs {
   int32_t total_pods, batch, k;
   int2* cpuset_list;   // (pod, node) of every cpu-bind Reserve, in placement order (ks_cpuset.h)
   int32_t* cpuset_n;
+  uint32_t* cpuset_split;  // [pod] CPUs per NUMA node of a cpu-bind Reserve on a NUMA-policy node (0 = whole node)
   int32_t rcap;        // reservations cached in LDS per slot (0 = none)
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
   int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
@@ -398,8 +398,7 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
   }
   EvalOut o = eval_full<NSC, false, false, FEAT>(
       cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
-      [&]() { return dev_eval<false>(cfg, pod, DevGView{*a.dv, node}); });
-  numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaGView{*a.nv, node}; });
+      [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
   return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
 }
@@ -675,8 +674,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
               if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
               return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
             },
-            [&]() { return dev_eval<false>(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}); });
-        numa_policy_fix<NSC, false, FEAT>(cfg, pod, r, o, [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
+            [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
+            [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
         feas = o.reasons == 0;
       }
       if (DEV && cfg.dev) {
@@ -783,10 +782,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         // the node's NUMA-node state into LDS (lane = word, NumaLView layout)
         const DevNuma& nv = *a.nv;
         int64_t v = 0;
-        if (lane < 2 * kNumaDev) v = gld(nv.total + (int64_t)lane * nv.npad + node);
-        else if (lane < 4 * kNumaDev) v = gld(nv.used + (int64_t)(lane - 2 * kNumaDev) * nv.npad + node);
-        else if (lane < 5 * kNumaDev) v = gld(nv.off + (int64_t)(lane - 4 * kNumaDev) * nv.npad + node);
-        else if (lane == 5 * kNumaDev)
+        if (lane < kNumaWUsed) v = gld(nv.total + (int64_t)lane * nv.npad + node);
+        else if (lane < kNumaWOff) v = gld(nv.used + (int64_t)(lane - kNumaWUsed) * nv.npad + node);
+        else if (lane < kNumaWCpu) v = gld(nv.off + (int64_t)(lane - kNumaWOff) * nv.npad + node);
+        else if (lane < kNumaWMeta)
+          v = ((int64_t)gld(nv.cs + (int64_t)(lane - kNumaWCpu) * nv.npad + node) << 32) |
+              (int64_t)(uint32_t)gld(nv.free + (int64_t)(lane - kNumaWCpu) * nv.npad + node);
+        else if (lane == kNumaWMeta)
           v = (int64_t)((gld(nv.flags + node) >> KS_NUMA_POLICY_SHIFT) & 3u) | ((int64_t)gld(nv.count + node) << 8) |
               ((int64_t)gld(nv.present + node) << 32);
         if (lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = v;
@@ -947,12 +949,39 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       score_out = fitla + (hi > 0 ? a.rv->w100 : 0);
     }
     uint32_t gminors = 0, rminors = 0;
+    // NodeNUMAResource Reserve on a node with a NUMA policy: Allocate with the Filter's hint on the pre-pod state
+    // (the topology manager's stored affinity also restricts DeviceShare's Reserve)
+    NumaPolOut npr;
+    npr.admitted = false;
+    npr.affinity = 0;
+    bool npol = false;
+    if ((FEAT & 8) && cfg.numa_pol && !(pflags & kPodReqZero)) {
+      const NumaLView nl{snp + s * kNumaSlotWords};
+      if (nl.policy() != 0) {
+        PodRec pod = spods[j];
+        pod.flags = pflags;
+        NumaNodeCtx nc;
+        nc.plain_req_cpu = nc.plain_req_mem = nc.plain_alloc_cpu = nc.plain_alloc_mem = 0;  // (score only)
+        nc.cs_milli = snuma[4 * s];
+        nc.cs_off = snuma[4 * s + 1];
+        nc.ratio = __longlong_as_double(snuma[4 * s + 2]);
+        nc.cpu_free = (int32_t)snuma[4 * s + 3];
+        if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
+          const DevLView dvl{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0};
+          npr = numa_policy_eval(cfg, pod, nl, nc, &dvl);
+        } else {
+          npr = numa_policy_eval(cfg, pod, nl, nc, (const DevLView*)nullptr);
+        }
+        npol = true;
+      }
+    }
+    const uint32_t dev_allow = (npol && npr.admitted && npr.affinity) ? npr.affinity : ~0u;
     if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
       // DeviceShare Reserve: allocate the minors on the pre-pod GPU state, add the request per instance
       PodRec pod = spods[j];
       pod.flags = pflags;
       GpuReq g;
-      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g);
+      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g, dev_allow);
       gminors = __builtin_amdgcn_readfirstlane(dd.minors);
       rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
       // used word `lane`: GPU (q, k) for lane < 3 * kGpus, RDMA j = lane - kDevRdmaW after
@@ -967,31 +996,57 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
       }
     }
-    if ((FEAT & 8) && cfg.numa_pol) {
-      // NodeNUMAResource Reserve on a node with a NUMA policy: Allocate with the Filter's hint on the pre-pod
-      // NUMA state, then addPodAllocation adds it to allocatedResources (node_allocation.go:86-99)
-      const NumaLView nl{snp + s * kNumaSlotWords};
-      PodRec pod = spods[j];
-      pod.flags = pflags;
-      if (nl.policy() != 0 && !(pflags & kPodReqZero)) {
-        const NumaPolOut pr = numa_policy_eval(cfg, pod, nl, 0, 0, 0, 0);
-        uint32_t bits = 0;
+    uint32_t cpu_split = 0;  // cpu-bind pod: CPUs per NUMA node (8 bits each), 0 = takeCPUs over the whole node
+    if (npol && npr.reasons == 0) {
+      // addPodAllocation: the NUMANodeResources to allocatedResources (node_allocation.go:86-99); a cpu-bind pod's
+      // CPUs to the NUMA nodes' cpuset counts (and their amplification offsets) and available CPUs
+      int64_t* w = snp + s * kNumaSlotWords;
+      uint32_t bits = 0;
 #pragma unroll
-        for (int k = 0; k < kNumaDev; ++k) bits |= (pr.alloc[0][k] != 0 || pr.alloc[1][k] != 0) ? (1u << k) : 0u;
-        const int rr = lane / kNumaDev, kk = lane % kNumaDev;
-        if (lane < 2 * kNumaDev) {
-          int64_t add = 0;
+      for (int k = 0; k < kNumaDev; ++k) bits |= (npr.alloc[0][k] != 0 || npr.alloc[1][k] != 0) ? (1u << k) : 0u;
+      int32_t cpus[kNumaDev];
 #pragma unroll
-          for (int q = 0; q < 2 * kNumaDev; ++q) add = (q == lane) ? pr.alloc[q / kNumaDev][q % kNumaDev] : add;
-          if (add != 0) {
-            const int64_t nvv = snp[s * kNumaSlotWords + 2 * kNumaDev + lane] + add;
-            snp[s * kNumaSlotWords + 2 * kNumaDev + lane] = nvv;
-            gst(a.nv->used + ((int64_t)rr * kNumaDev + kk) * a.nv->npad + node, nvv);
-          }
-        } else if (lane == 2 * kNumaDev && bits) {
-          const int64_t meta = snp[s * kNumaSlotWords + 5 * kNumaDev] | ((int64_t)bits << 32);
-          snp[s * kNumaSlotWords + 5 * kNumaDev] = meta;
-          gst(a.nv->present + node, (uint32_t)(meta >> 32));
+      for (int k = 0; k < kNumaDev; ++k) cpus[k] = 0;
+      if (cpubind) {
+        if (bits) {
+#pragma unroll
+          for (int k = 0; k < kNumaDev; ++k) cpus[k] = npr.cpus[k];
+        } else {
+          cpus[0] = cpu_need;  // no NUMA allocation: admitted with a nil affinity, i.e. one NUMA node (count 1)
+        }
+#pragma unroll
+        for (int k = 0; k < kNumaDev; ++k) cpu_split |= bits ? ((uint32_t)cpus[k] << (8 * k)) : 0u;
+      }
+      const int rr = lane / kNumaDev, kk = lane % kNumaDev;
+      const double ratio = __longlong_as_double(snuma[4 * s + 2]);
+      if (lane < 2 * kNumaDev) {
+        int64_t add = 0;
+#pragma unroll
+        for (int q = 0; q < 2 * kNumaDev; ++q) add = (q == lane) ? npr.alloc[q / kNumaDev][q % kNumaDev] : add;
+        if (add != 0) {
+          const int64_t nvv = w[kNumaWUsed + lane] + add;
+          w[kNumaWUsed + lane] = nvv;
+          gst(a.nv->used + ((int64_t)rr * kNumaDev + kk) * a.nv->npad + node, nvv);
+        }
+      } else if (lane == 2 * kNumaDev && bits) {
+        const int64_t meta = w[kNumaWMeta] | ((int64_t)bits << 32);
+        w[kNumaWMeta] = meta;
+        gst(a.nv->present + node, (uint32_t)(meta >> 32));
+      } else if (lane >= 3 * kNumaDev && lane < 4 * kNumaDev) {
+        const int k = lane - 3 * kNumaDev;
+        int32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < kNumaDev; ++q) c = (q == k) ? cpus[q] : c;
+        if (c != 0) {
+          const int64_t cw = w[kNumaWCpu + k];
+          const int32_t cs1 = (int32_t)(cw >> 32) + c, fr1 = (int32_t)(uint32_t)cw - c;
+          const int64_t m = (int64_t)cs1 * 1000;
+          const int64_t off1 = ratio > 1.0 ? (int64_t)::ceil((double)m * ratio) - m : 0;
+          w[kNumaWCpu + k] = ((int64_t)cs1 << 32) | (int64_t)(uint32_t)fr1;
+          w[kNumaWOff + k] = off1;
+          gst(a.nv->cs + (int64_t)k * a.nv->npad + node, cs1);
+          gst(a.nv->free + (int64_t)k * a.nv->npad + node, fr1);
+          gst(a.nv->off + (int64_t)k * a.nv->npad + node, off1);
         }
       }
     }
@@ -1008,6 +1063,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         snuma[4 * s + 1] = off1;
         snuma[4 * s + 3] -= cpu_need;
         a.cpuset_list[atomicAdd(a.cpuset_n, 1)] = make_int2(cursor0 + j, node);
+        a.cpuset_split[cursor0 + j] = cpu_split;
       }
     }
     if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors, rminors, 0};

@@ -26,6 +26,7 @@
 #pragma once
 
 #include "ks_device.h"
+#include "ks_numa.h"
 
 namespace ks {
 
@@ -285,22 +286,46 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
 // r must be the base row; with UNDO it is returned unchanged (the sweep reuses it across pods).
 // rsv(dl) runs rsv_eval on the node's reservation view; it is called only when the pod's class
 // matches one of them.
-// FEAT: bit 0 Reservation, bit 1 NodeNUMAResource, bit 2 DeviceShare compiled in (the Cfg flags
-// switch them at run time).  dev() returns the node's DevOut (ks_dev.h).  The key total is
-// key_total(c, o, M) with M the pod's DeviceShare normalization max.
-template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G>
-__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& dev,
-                                             RsvOut* info = nullptr) {
-  constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0, DEV = (FEAT & 4) != 0;
+// FEAT: bit 0 Reservation, bit 1 NodeNUMAResource, bit 2 DeviceShare, bit 3 NUMA topology policies compiled in
+// (the Cfg flags switch them at run time).  devv() / numav() return the node's device view (ks_dev.h) and NUMA
+// view (ks_numa.h).  Filter order as in the profile: Fit, LoadAware, NodeNUMAResource (on a node with a NUMA
+// topology policy its topology-manager Admit, whose affinity then restricts DeviceShare), DeviceShare,
+// Reservation.  The key total is key_total(c, o, M) with M the pod's DeviceShare normalization max.
+template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, typename H>
+__device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& devv,
+                                             H&& numav, RsvOut* info = nullptr) {
+  constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0, DEV = (FEAT & 4) != 0, POL = (FEAT & 8) != 0;
+  const bool dev_pod = DEV && c.dev && (p.flags & kPodHasGpu);
+  // NodeNUMAResource (policy None part, then the topology-manager path on a policy node); returns DeviceShare's
+  // NUMA restriction
+  auto numa = [&](EvalOut& o) __attribute__((always_inline)) -> uint32_t {
+    if (!(NUMA && c.numa)) return ~0u;
+    numa_eval<NSC, DEBUG>(c, p, r, o);
+    if (!(POL && c.numa_pol) || (p.flags & kPodReqZero)) return ~0u;
+    const auto nv = numav();
+    if (nv.policy() == 0) return ~0u;
+    using DVT = decltype(devv());
+    NumaPolOut pr;
+    if (dev_pod) {
+      const DVT dv = devv();
+      pr = numa_policy_eval(c, p, nv, numa_node_ctx<NSC>(r), &dv);
+    } else {
+      pr = numa_policy_eval(c, p, nv, numa_node_ctx<NSC>(r), (const DVT*)nullptr);
+    }
+    numa_policy_apply<DEBUG>(c, p, o, o.numa_rs, pr);
+    return (o.numa_rs == 0 && pr.admitted && pr.affinity) ? pr.affinity : ~0u;
+  };
+  auto dev = [&](EvalOut& o, uint32_t allow) __attribute__((always_inline)) {
+    if (!dev_pod) return;
+    const DevOut d = dev_eval<false>(c, p, devv(), nullptr, allow);
+    o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
+    o.dev_raw = d.raw;
+  };
   if (!RSV || !c.rsv || (p.rsv_class < 0 && !(p.flags & KS_POD_RSV_AFFINITY))) {
     if (info) *info = RsvOut{0u, 0, 0, 0, -1};
     EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
-    if (NUMA && c.numa) numa_eval<NSC, DEBUG>(c, p, r, o);
-    if (DEV && c.dev && (p.flags & kPodHasGpu)) {
-      const auto d = dev();
-      o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
-      o.dev_raw = d.raw;
-    }
+    const uint32_t allow = numa(o);
+    dev(o, allow);
     return o;
   }
   const bool slow = p.rsv_class >= 0 && p.rsv_class < 64 && ((r.rsv_cls >> p.rsv_class) & 1ull);
@@ -311,13 +336,9 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
     rsv_apply<NSC>(r, dl, 1);
   }
   EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
-  if (NUMA && c.numa) numa_eval<NSC, DEBUG>(c, p, r, o);
+  const uint32_t allow = numa(o);
   if (UNDO && slow) rsv_apply<NSC>(r, dl, -1);
-  if (DEV && c.dev && (p.flags & kPodHasGpu)) {
-    const auto d = dev();
-    o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
-    o.dev_raw = d.raw;
-  }
+  dev(o, allow);
   // a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
   // NodeNames, plugin.go:235-246) before any Filter plugin runs
   o.reasons = ro.reasons == KS_R_RSV_AFFINITY ? ro.reasons : (o.reasons | ro.reasons);

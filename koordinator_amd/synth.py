@@ -12,8 +12,9 @@ would produce from a scheduler-cache snapshot plus NodeMetric objects:
       CPUs (NodeNUMAResource); 10k pods, 40 % requesting GPUs (whole devices 1/2/4, half a GPU by ratio,
       or a gpu-memory amount; half of the whole-GPU pods with rdma 1 and joint [gpu, rdma] allocation,
       half of those SamePCIe), a few RDMA-only pods, and cpuset (LSR) pods; Fit + LoadAware +
-      NodeNUMAResource + DeviceShare.  Nodes carry no NUMA topology policy here (the reference's C3 has
-      SingleNUMANode nodes; DeviceShare NUMA hints are DESIGN.md §9)
+      NodeNUMAResource + DeviceShare.  Half of the nodes carry the SingleNUMANode topology policy with two
+      NUMA nodes (policy_numa_nodes): NodeNUMAResource and DeviceShare are both hint providers there, and
+      cpuset pods take their CPUs per allocated NUMA node
 * C4  20k nodes with 50k reservations (make_reservations), 10k pods of which 60 % belong to one
       of 16 reservation owner classes, NodeResourcesFit + LoadAwareScheduling + Reservation (weight 5000)
 * C5  100k nodes, C1 pod distribution (the multi-GPU sharding config)
@@ -66,10 +67,21 @@ class Workload:
     reservations: Optional[ReservationTable] = None
     devices: Optional["DeviceTable"] = None
     cpus: Optional[CpuState] = None
+    numa_nodes: Optional["NumaNodes"] = None
 
     @property
     def cfg(self) -> abi.KsConfig:
         return self.profile.to_ks_config()
+
+    def tables(self, copy: bool = True) -> dict:
+        """The non-node tables as the keyword arguments of runtime.Evaluator / the oracle (copies by default:
+        both consume and mutate what they are given)."""
+        out = {}
+        for k, v in (("quotas", self.quotas), ("reservations", self.reservations), ("devices", self.devices),
+                     ("cpu_state", self.cpus), ("numa_nodes", self.numa_nodes)):
+            if v is not None:
+                out[k] = v.copy() if copy else v
+        return out
 
 
 def koord_profile(with_quota: bool = False, batch_pods: int = 0, candidates: int = 0,
@@ -294,24 +306,29 @@ def gpu_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4) -> Pod
 
 # node CPU topologies by core count: (sockets, NUMA nodes per socket, cores per NUMA node, threads per core)
 CPU_TOPOLOGIES = {32: (2, 1, 8, 2), 48: (2, 1, 12, 2), 64: (2, 2, 8, 2), 96: (2, 2, 12, 2)}
+# the two-NUMA-node layout of the same core counts (one NUMA node per socket), for nodes with a NUMA policy
+CPU_TOPOLOGIES_2NUMA = {32: (2, 1, 8, 2), 48: (2, 1, 12, 2), 64: (2, 1, 16, 2), 96: (2, 1, 24, 2)}
 
 
 def make_cpu_state(nodes: NodeTable, rng: np.random.Generator, cores=None, no_topology: float = 0.05,
-                   max_alloc: float = 0.3, label_frac: float = 0.2) -> CpuState:
+                   max_alloc: float = 0.3, label_frac: float = 0.2, two_numa=None) -> CpuState:
     """NodeResourceTopology-derived CPU state: a regular topology per node (by its core count), a
     fragmented set of already-allocated CPUs (exclusive policy None / PCPULevel / NUMANodeLevel), kubelet
     reserved CPUs 0-1 on a third of the nodes, and numa-allocate-strategy labels on some nodes.  Node
-    Requested cpu and numa_cpuset_cpus are raised to include the allocated cpusets."""
+    Requested cpu and numa_cpuset_cpus are raised to include the allocated cpusets.  Nodes in two_numa
+    (a mask) get the one-NUMA-node-per-socket layout."""
     n = nodes.n
     cores = np.asarray(cores if cores is not None else nodes.alloc_milli_cpu // 1000)
     keys = sorted(CPU_TOPOLOGIES)
-    st = CpuState(n, [regular_topology(*CPU_TOPOLOGIES[k]) for k in keys])
+    st = CpuState(n, [regular_topology(*CPU_TOPOLOGIES[k]) for k in keys] +
+                  [regular_topology(*CPU_TOPOLOGIES_2NUMA[k]) for k in keys])
+    two = np.zeros(n, bool) if two_numa is None else np.asarray(two_numa, bool)
     W = abi.KS_CPU_WORDS
     for i in range(n):
         c = int(cores[i])
         if c not in CPU_TOPOLOGIES or rng.random() < no_topology:
             continue
-        st.topology[i] = keys.index(c)
+        st.topology[i] = keys.index(c) + (len(keys) if two[i] else 0)
         resv = [0, 1] if rng.random() < 0.33 else []
         free = np.array([x for x in range(c) if x not in resv])
         k = int(rng.integers(0, int(max_alloc * c) + 1))
@@ -385,6 +402,38 @@ def make_numa_nodes(nodes: NodeTable, rng: np.random.Generator, policy_frac: flo
     return nn
 
 
+def policy_numa_nodes(nodes: NodeTable, cpus: CpuState, policy_mask, rng: np.random.Generator, cores,
+                      policy: int = abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE) -> "NumaNodes":
+    """NodeResourceTopology zones of the policy nodes, consistent with their CPU state: two NUMA nodes (the
+    one-NUMA-node-per-socket CPU topology) splitting cpu and memory, the allocated cpuset CPUs counted per NUMA
+    node (cpuset_cpus, and in allocatedResources cpu), plus earlier non-cpuset pods' NUMA allocations."""
+    from .cluster import NumaNodes
+    n = nodes.n
+    nn = NumaNodes(n)
+    pol = np.where(policy_mask, policy, 0).astype(np.uint32)
+    nodes.numa_flags[:] = (nodes.numa_flags & ~np.uint32(3 << abi.KS_NUMA_POLICY_SHIFT)) | (pol << abi.KS_NUMA_POLICY_SHIFT)
+    W = abi.KS_CPU_WORDS
+    for i in np.flatnonzero(policy_mask):
+        c = int(cores[i])
+        nn.count[i] = 2
+        nn.alloc_cpu[i, :2] = c * 1000 // 2
+        nn.alloc_memory[i, :2] = int(nodes.alloc_memory[i]) // 2
+        if cpus.topology[i] >= 0:
+            bits = np.unpackbits(cpus.allocated[i].view(np.uint8), bitorder="little")[: W * 64]
+            held = np.flatnonzero(bits)
+            for k in range(2):
+                nn.cpuset_cpus[i, k] = int(np.count_nonzero(held // (c // 2) == k))
+        for k in range(2):
+            extra = 0
+            if rng.random() < 0.5:
+                f = rng.random() * 0.4
+                extra = int(nn.alloc_cpu[i, k] * f) // 1000 * 1000
+                nn.used_memory[i, k] = int(nn.alloc_memory[i, k] * f) // MI * MI
+            nn.used_cpu[i, k] = int(nn.cpuset_cpus[i, k]) * 1000 + extra
+            nn.used_present[i, k] = 1 if (nn.used_cpu[i, k] or nn.used_memory[i, k]) else 0
+    return nn
+
+
 def c1(seed: int = SEED, n_nodes: int = 500, n_pods: int = 1000, **kw) -> Workload:
     rng = np.random.Generator(np.random.PCG64(seed))
     nodes = make_nodes(n_nodes, rng)
@@ -400,7 +449,8 @@ def c2(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, n_quotas: int
     return Workload("C2", koord_profile(with_quota=True, **kw), nodes, pods, quotas)
 
 
-def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, **kw) -> Workload:
+def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, policy_frac: float = 0.5,
+       policy: int = abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE, **kw) -> Workload:
     from .config import GPU_MEMORY_RATIO, DeviceShareArgs, NodeNUMAResourceArgs
     rng = np.random.Generator(np.random.PCG64(seed))
     nodes = make_nodes(n_nodes, rng)
@@ -409,14 +459,16 @@ def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, **kw) -> Wor
     cores = nodes.alloc_milli_cpu // 1000
     nodes.numa_cpu_amplification[:] = ratio
     nodes.alloc_milli_cpu[amp] = np.ceil(nodes.alloc_milli_cpu[amp] * ratio[amp]).astype(np.int64)
-    cpus = make_cpu_state(nodes, rng, cores=cores)
+    pmask = rng.random(n_nodes) < policy_frac
+    cpus = make_cpu_state(nodes, rng, cores=cores, two_numa=pmask)
     devs = make_devices(nodes, rng, rdma=True)
+    numa = policy_numa_nodes(nodes, cpus, pmask, rng, cores, policy) if policy_frac > 0 else None
     pods = rdma_pods(gpu_pods(make_pods(n_pods, rng), rng), rng)
     pods = cpuset_pods(pods, rng, 0.4 / 0.6, exclude=pods.gpu_memory_ratio + pods.gpu_memory > 0)
     prof = koord_profile(**kw)
     prof.numa = NodeNUMAResourceArgs()
     prof.deviceshare = DeviceShareArgs()  # v1beta2 defaults: gpu-memory-ratio, rdma, fpga weight 1
-    return Workload("C3", prof, nodes, pods, None, None, devs, cpus)
+    return Workload("C3", prof, nodes, pods, None, None, devs, cpus, numa)
 
 
 def c4(seed: int = SEED, n_nodes: int = 20_000, n_reservations: int = 50_000, n_pods: int = 10_000, **kw) -> Workload:

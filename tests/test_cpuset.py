@@ -67,7 +67,7 @@ def test_cpu_bind_request_amplified():
 
 def test_c3_small_oracle_runs():
     w = synth.c3(n_nodes=200, n_pods=300)
-    o = Oracle(w.cfg, w.nodes.copy(), devices=w.devices.copy(), cpu_state=w.cpus.copy())
+    o = Oracle(w.cfg, w.nodes.copy(), **w.tables())
     r = o.schedule(w.pods)
     bind = (w.pods.flags & abi.KS_POD_CPU_BIND) != 0
     cs = o.fetch_cpusets(w.pods.n)

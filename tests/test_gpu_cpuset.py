@@ -41,11 +41,12 @@ def test_golden_cpusets(runtime, case):
 
 def run_pair(runtime, oracle_lib, w, label, devices=True):
     cfg = w.cfg
-    dv = w.devices.copy() if (devices and w.devices is not None) else None
-    ev = runtime.Evaluator(cfg, w.nodes.copy(), devices=dv, cpu_state=w.cpus.copy())
+    tabs = w.tables()
+    if not devices:
+        tabs.pop("devices", None)
+    ev = runtime.Evaluator(cfg, w.nodes.copy(), **tabs)
     got = ev.schedule(w.pods)
-    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), nthreads=8, devices=w.devices.copy() if dv is not None else None,
-                            cpu_state=w.cpus.copy())
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), nthreads=8, **{k: v.copy() for k, v in tabs.items()})
     want = orc.schedule(w.pods)
     assert_same_results(got, want, label)
     assert np.array_equal(got["gpu_minors"], want["gpu_minors"]), label
@@ -94,7 +95,7 @@ def test_schedule_cpuset_c3_prefix(runtime, oracle_lib):
 
 def test_cpuset_checkpoint_restore(runtime):
     w = synth.c3(seed=45, n_nodes=200, n_pods=500)
-    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), devices=w.devices.copy(), cpu_state=w.cpus.copy())
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
     ev.stage(w.pods)
     ev.checkpoint()
     outs = []
@@ -111,8 +112,8 @@ def test_cpuset_checkpoint_restore(runtime):
 
 def test_eval_debug_cpu_bind(runtime, oracle_lib):
     w = synth.c3(seed=46, n_nodes=300, n_pods=60)
-    ev = runtime.Evaluator(w.cfg, w.nodes, devices=w.devices, cpu_state=w.cpus)
-    orc = oracle_lib.Oracle(w.cfg, w.nodes, devices=w.devices, cpu_state=w.cpus)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), **w.tables())
     seen = 0
     for i in range(w.pods.n):
         one = w.pods.rows([i])

@@ -80,9 +80,9 @@ def c3_small(seed, n=500, p=700):
 
 def check(runtime, oracle_lib, w, label, cfg=None):
     cfg = cfg or w.cfg
-    ev = runtime.Evaluator(cfg, w.nodes.copy(), None, None, w.devices.copy(), w.cpus.copy())
+    ev = runtime.Evaluator(cfg, w.nodes.copy(), **w.tables())
     got = ev.schedule(w.pods)
-    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), nthreads=8, devices=w.devices.copy(), cpu_state=w.cpus.copy())
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), nthreads=8, **w.tables())
     want = orc.schedule(w.pods)
     assert_same_results(got, want, label)
     for k in ("gpu_minors", "rdma_minors"):
@@ -99,8 +99,8 @@ def check(runtime, oracle_lib, w, label, cfg=None):
 def test_eval_debug_joint_pods(runtime, oracle_lib):
     w = c3_small(51, n=300, p=400)
     idx = np.nonzero((w.pods.rdma > 0))[0][:40]
-    ev = runtime.Evaluator(w.cfg, w.nodes, None, None, w.devices, w.cpus)
-    orc = oracle_lib.Oracle(w.cfg, w.nodes, devices=w.devices, cpu_state=w.cpus)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), **w.tables())
     for i in idx:
         one = w.pods.rows([i])
         r_g, s_g, t_g = ev.eval_pod(one)
