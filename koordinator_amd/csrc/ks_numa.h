@@ -21,7 +21,8 @@
 //   * the node score over the allocated NUMA nodes (calculateAllocatableAndRequested, scoring.go:116-163; a
 //     cpu-bind pod's requested cpu is the node's amplified cpuset CPUs).
 // Up to kNumaDev NUMA nodes per node (15 masks); DeviceShare hints over at most 2 device NUMA nodes on nodes
-// with at most 2 NUMA nodes (ks_load_* refuses more), so the product is at most 3 x 3 x 3^4 = 729 permutations.
+// with at most 2 NUMA nodes (ks_load_* refuses more); its identical per-resource lists merge as one list, so the
+// product is at most 15 x 15 permutations (3 x 3 x 3 with device hints).
 // The oracle (oracle/koord_oracle.c numa_policy_eval, ko_merge_hints, dev_hints) restates the same code with
 // per-NUMA arrays and explicit hint lists; its merge is pinned by the reference's policy_test.go tables.
 #pragma once
@@ -92,6 +93,9 @@ struct NumaPolOut {
   int32_t cpus[kNumaDev];      // cpu-bind pod: CPUs allocateCPUSet takes per allocated NUMA node
   uint32_t affinity;           // merged NUMANodeAffinity (0 = nil)
   bool admitted;               // Admit stored the affinity (DeviceShare's Filter / Score / Reserve read it)
+  bool dev_done;               // reached DeviceShare's Allocate under the affinity (allow = affinity, or all if nil)
+  bool dev_hit;                // ... and dev is its result (a hint's trial allocation, or computed without DEFER_DEV)
+  DevOut dev;
 };
 
 // resourceAllocationScorer.score over cpu / memory with the plugin weights (scoring.go:206-242)
@@ -111,53 +115,51 @@ __device__ __forceinline__ int32_t numa_res_score(const Cfg& c, bool most, int64
   return ws ? small_div(ns, ws) : 0;
 }
 
-// IterateBitMasks order for K NUMA nodes: size 1..K, lexicographic index lists (bitmask.go:206-222)
-__device__ __forceinline__ int numa_masks(int K, uint32_t* m) {
-  int n = 0;
-  for (int size = 1; size <= K; ++size) {
-    for (int i0 = 0; i0 < K; ++i0) {
-      if (size == 1) { m[n++] = 1u << i0; continue; }
-      for (int i1 = i0 + 1; i1 < K; ++i1) {
-        if (size == 2) { m[n++] = (1u << i0) | (1u << i1); continue; }
-        for (int i2 = i1 + 1; i2 < K; ++i2) {
-          if (size == 3) { m[n++] = (1u << i0) | (1u << i1) | (1u << i2); continue; }
-          for (int i3 = i2 + 1; i3 < K; ++i3) m[n++] = (1u << i0) | (1u << i1) | (1u << i2) | (1u << i3);
-        }
-      }
-    }
-  }
-  return n;
+// IterateBitMasks order (bitmask.go:206-222) for K <= 4 NUMA nodes: size 1..K, lexicographic index lists; mask i
+// in bits [4i, 4i + 4) of the table
+__device__ __forceinline__ uint64_t numa_mask_table(int K) {
+  return K <= 1 ? 0x1ull : (K == 2 ? 0x321ull : (K == 3 ? 0x7653421ull : 0xFEDB7CA69538421ull));
 }
+__device__ __forceinline__ uint32_t numa_mask_at(uint64_t tab, int i) { return (uint32_t)(tab >> (4 * i)) & 0xFu; }
 
 __device__ __forceinline__ bool numa_narrower(uint32_t a, uint32_t b) {
   const int ca = __builtin_popcount(a), cb = __builtin_popcount(b);
   return ca == cb ? a < b : ca < cb;
 }
 
-// DeviceShare's topology hints on one node (generateTopologyHints): the hint masks (NUMA-id bit masks, IterateBitMasks
-// order over the device topology's NUMA nodes), which of them allocate (ok bits), minAffinitySize, and the number
-// of identical resource lists (0 = the provider expresses no preference).
+// DeviceShare's topology hints on one node (generateTopologyHints): hint positions 0: {id0}, 1: {id1}, 2: {id0, id1}
+// over the device topology's (at most kDevHintIds) NUMA ids, which of them were tried / allocate, minAffinitySize,
+// the number of identical resource lists (0 = the provider expresses no preference), and each tried position's
+// trial allocation (reused when the merged affinity is that position's mask).
 struct DevHints {
   int lists;
-  int nm;
-  uint32_t masks[3];
-  uint32_t ok;
+  int npos;
+  int id0, id1;
+  uint32_t tried, ok;
   int minaff;
+  uint32_t r0, r1, r2;  // trial allocation reasons / raw score per tried position
+  int32_t s0, s1, s2;
 };
+
+__device__ __forceinline__ uint32_t dev_hint_mask(const DevHints& h, int i) {
+  const uint32_t pos = (uint32_t)i + 1u;
+  return ((pos & 1u) ? (1u << h.id0) : 0u) | ((pos & 2u) ? (1u << h.id1) : 0u);
+}
 
 template <typename V>
 __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, const V& v) {
   DevHints h;
   h.lists = 0;
-  h.nm = 0;
-  h.ok = 0;
+  h.npos = 0;
+  h.id0 = h.id1 = 0;
+  h.tried = h.ok = 0;
   h.minaff = -1;
+  h.r0 = h.r1 = h.r2 = 0u;
+  h.s0 = h.s1 = h.s2 = 0;
   if (!v.present()) return h;
   const uint64_t topo = (uint64_t)v.tot(kDevTopoW), meta = (uint64_t)v.tot(kDevMetaW);
   // numaTopology.nodes: NUMA nodes of the switches holding a device with a topology
-  uint32_t ids = 0, gin[2] = {0u, 0u}, rin[2] = {0u, 0u};
-  int idl[kDevHintIds];
-  int nid = 0;
+  uint32_t ids = 0;
 #pragma unroll
   for (int k = 0; k < kGpus; ++k) {
     const uint32_t pc = (uint32_t)(topo >> (4 * k)) & 0xFu;
@@ -169,40 +171,45 @@ __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, con
     const uint32_t pc = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
     if (v.tot(kDevRdmaW + j) != 0 && pc < 8u) ids |= 1u << ((uint32_t)(meta >> (8 * pc)) & 0xFu);
   }
-  for (uint32_t b = ids; b && nid < kDevHintIds; b &= b - 1) idl[nid++] = __builtin_ctz(b);
+  const int nid = __builtin_popcount(ids) < kDevHintIds ? __builtin_popcount(ids) : kDevHintIds;  // ks_load_* checks <= 2
+  const uint32_t rest = ids & (ids - 1u);
+  h.id0 = ids ? __builtin_ctz(ids) : 0;
+  h.id1 = rest ? __builtin_ctz(rest) : 0;
   GpuReq g;
   if (dev_prepare(p, v, g)) return h;  // every mask returns before minAffinitySize is set: no preference
-  // minors of each type per position of the id list (existing, with a topology)
+  // minors of each type on id0 / id1 (existing, with a topology)
+  uint32_t gin0 = 0, gin1 = 0, rin0 = 0, rin1 = 0;
 #pragma unroll
   for (int k = 0; k < kGpus; ++k) {
     const uint32_t pc = (uint32_t)(topo >> (4 * k)) & 0xFu;
-    const bool ex = v.tot(k) != 0 || v.tot(kGpus + k) != 0 || v.tot(2 * kGpus + k) != 0;
-    const uint32_t id = (uint32_t)(meta >> (8 * (pc & 7u))) & 0xFu;
-    for (int i = 0; i < nid; ++i) gin[i] |= (ex && pc < 8u && (int)id == idl[i]) ? (1u << k) : 0u;
+    const bool ex = pc < 8u && (v.tot(k) != 0 || v.tot(kGpus + k) != 0 || v.tot(2 * kGpus + k) != 0);
+    const int id = (int)((uint32_t)(meta >> (8 * (pc & 7u))) & 0xFu);
+    gin0 |= (ex && nid >= 1 && id == h.id0) ? (1u << k) : 0u;
+    gin1 |= (ex && nid >= 2 && id == h.id1) ? (1u << k) : 0u;
   }
 #pragma unroll
   for (int j = 0; j < kRdma; ++j) {
     const uint32_t pc = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
-    const uint32_t id = (uint32_t)(meta >> (8 * (pc & 7u))) & 0xFu;
-    for (int i = 0; i < nid; ++i) rin[i] |= (v.tot(kDevRdmaW + j) != 0 && pc < 8u && (int)id == idl[i]) ? (1u << j) : 0u;
+    const bool ex = pc < 8u && v.tot(kDevRdmaW + j) != 0;
+    const int id = (int)((uint32_t)(meta >> (8 * (pc & 7u))) & 0xFu);
+    rin0 |= (ex && nid >= 1 && id == h.id0) ? (1u << j) : 0u;
+    rin1 |= (ex && nid >= 2 && id == h.id1) ? (1u << j) : 0u;
   }
   const bool has_gpu = (p.flags & kPodGpuReq) != 0, has_rdma = p.rdma > 0;
-  // masks over positions: {0}, {1}, {0, 1} (IterateBitMasks over the sorted id list)
-  const uint32_t pos[3] = {1u, 2u, 3u};
-  const int npos = nid == 0 ? 0 : (nid == 1 ? 1 : 3);
-  for (int i = 0; i < npos; ++i) {
-    uint32_t mask = 0, gm = 0, rm = 0;
-    for (int q = 0; q < nid; ++q)
-      if ((pos[i] >> q) & 1u) {
-        mask |= 1u << idl[q];
-        gm |= gin[q];
-        rm |= rin[q];
-      }
-    h.masks[h.nm++] = mask;
+  h.npos = nid == 0 ? 0 : (nid == 1 ? 1 : 3);
+  for (int i = 0; i < h.npos; ++i) {  // not unrolled: one inlined copy of dev_eval
+    const uint32_t pos = (uint32_t)i + 1u;
+    const uint32_t gm = ((pos & 1u) ? gin0 : 0u) | ((pos & 2u) ? gin1 : 0u);
+    const uint32_t rm = ((pos & 1u) ? rin0 : 0u) | ((pos & 2u) ? rin1 : 0u);
     if ((has_gpu && __builtin_popcount(gm) < g.desired) || (has_rdma && __builtin_popcount(rm) < g.rdesired)) continue;
-    const int cnt = __builtin_popcount(pos[i]);
+    const int cnt = __builtin_popcount(pos);
     h.minaff = h.minaff < 0 ? (cnt < nid ? cnt : nid) : (cnt < h.minaff ? cnt : h.minaff);
-    if (dev_eval<false>(c, p, v, nullptr, mask).reasons == 0) h.ok |= 1u << i;
+    const DevOut d = dev_eval<false>(c, p, v, nullptr, dev_hint_mask(h, i));
+    h.tried |= 1u << i;
+    if (d.reasons == 0) h.ok |= 1u << i;
+    if (i == 0) { h.r0 = d.reasons; h.s0 = d.raw; }
+    else if (i == 1) { h.r1 = d.reasons; h.s1 = d.raw; }
+    else { h.r2 = d.reasons; h.s2 = d.raw; }
   }
   if (h.minaff >= 0)
     h.lists = (has_gpu ? ((g.has_core || g.desired > 1) ? 3 : 2) : 0) + (has_rdma ? 1 : 0);
@@ -210,8 +217,13 @@ __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, con
 }
 
 // Filter (FilterByNUMANode -> Admit -> allocateResources) and Score of one (pod, node) with a NUMA policy.
-// dv: the node's device view when DeviceShare is a hint provider for this pod, else nullptr.
-template <typename V, typename DV>
+// dv: the node's device view when DeviceShare is a hint provider for this pod, else nullptr.  DEFER_DEV leaves
+// DeviceShare's Allocate under the affinity to the caller (eval_full's DeviceShare Filter runs it with the same
+// restriction; one inlined copy of dev_eval less), which then owns the score rule "a DeviceShare failure there
+// returns before the NUMA score".
+// Register-resident: hint sets are bit sets over mask indices, per-mask hint scores are packed bytes, the merge is
+// three nested bit-set walks; no dynamically indexed local arrays (those would live in scratch memory).
+template <bool DEFER_DEV = false, typename V, typename DV>
 __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRec& p, const V& v, const NumaNodeCtx& nc,
                                                        const DV* dv) {
   NumaPolOut o;
@@ -219,6 +231,8 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
   o.score = 0;
   o.affinity = 0;
   o.admitted = false;
+  o.dev_done = o.dev_hit = false;
+  o.dev = DevOut{0u, 0, 0u, 0u};
 #pragma unroll
   for (int k = 0; k < kNumaDev; ++k) {
     o.alloc[0][k] = o.alloc[1][k] = 0;
@@ -229,18 +243,27 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
     o.reasons = KS_R_NUMA_MISSING;
     return o;
   }
+  // DeviceShare's hints first: its trial allocations are the register-heaviest part, nothing else is live yet
+  DevHints dh;
+  dh.lists = 0;
+  dh.npos = 0;
+  dh.tried = dh.ok = 0;
+  dh.minaff = -1;
+  if (dv) dh = dev_hints(c, p, *dv);
   const int pol = v.policy();
   const uint32_t pres = v.present();
   const bool bind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
-  int64_t tot[2][kNumaDev], use[2][kNumaDev], av[2][kNumaDev];
+  // used (with the cpuset amplification) is re-read for the score; total and available stay live
+  auto used_of = [&](int r, int k) -> int64_t {
+    return (k < K && ((pres >> k) & 1u)) ? v.used(r, k) + (r == 0 ? v.off(k) : 0) : 0;
+  };
+  int64_t tot[2][kNumaDev], av[2][kNumaDev];
 #pragma unroll
   for (int k = 0; k < kNumaDev; ++k) {
-    const bool in = k < K, pr = in && ((pres >> k) & 1u);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      tot[r][k] = in ? v.total(r, k) : 0;
-      use[r][k] = pr ? v.used(r, k) + (r == 0 ? v.off(k) : 0) : 0;
-      const int64_t a = tot[r][k] - use[r][k];
+      tot[r][k] = k < K ? v.total(r, k) : 0;
+      const int64_t a = tot[r][k] - used_of(r, k);
       av[r][k] = a < 0 ? 0 : a;
     }
   }
@@ -248,171 +271,131 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
   const int64_t req_cpu = (bind && nc.ratio > 1.0) ? (int64_t)::ceil((double)p.cpu * nc.ratio) : p.cpu;
   const int64_t req[2] = {req_cpu, p.mem};
   const bool want[2] = {p.cpu != 0, p.mem != 0};
-  uint32_t masks[kNumaMasks];
-  const int nm = numa_masks(K, masks);
+  const uint64_t tab = numa_mask_table(K);
+  const int nm = (1 << K) - 1;
   uint32_t lack[2] = {0u, 0u};
 #pragma unroll
   for (int k = 0; k < kNumaDev; ++k)
 #pragma unroll
     for (int r = 0; r < 2; ++r)
       if (k < K && av[r][k] == 0) lack[r] |= 1u << k;
-  // NodeNUMAResource hints: bit i of hset[r] = mask i is a hint of resource r; one score per mask
+  // NodeNUMAResource hints: bit i of hset[r] = mask i is a hint of resource r; one score per mask (byte i)
   uint32_t hset[2] = {0u, 0u};
   int min_size[2] = {K, K};
-  int32_t hsc[kNumaMasks];
+  uint64_t hsc_lo = 0, hsc_hi = 0;
   const bool nmost = c.numa_sc_most != 0;
   for (int i = 0; i < nm; ++i) {
+    const uint32_t mk = numa_mask_at(tab, i);
     int64_t ts[2] = {0, 0}, fs[2] = {0, 0};
 #pragma unroll
     for (int k = 0; k < kNumaDev; ++k)
-      if ((masks[i] >> k) & 1u)
+      if ((mk >> k) & 1u)
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           ts[r] += tot[r][k];
           fs[r] += av[r][k];
         }
-    hsc[i] = numa_res_score(c, nmost, ts[0] - fs[0], ts[1] - fs[1], ts[0], ts[1], req[0], req[1]);
-    const int cnt = __builtin_popcount(masks[i]);
+    const uint64_t sc = (uint64_t)(uint32_t)numa_res_score(c, nmost, ts[0] - fs[0], ts[1] - fs[1], ts[0], ts[1], req[0], req[1]);
+    if (i < 8) hsc_lo |= sc << (8 * i);
+    else hsc_hi |= sc << (8 * (i - 8));
+    const int cnt = __builtin_popcount(mk);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      if (!want[r] || ts[r] < req[r] || (masks[i] & lack[r])) continue;
+      if (!want[r] || ts[r] < req[r] || (mk & lack[r])) continue;
       min_size[r] = cnt < min_size[r] ? cnt : min_size[r];
       if (fs[r] >= req[r]) hset[r] |= 1u << i;
     }
   }
-  auto pref_of = [&](int r, int i) { return __builtin_popcount(masks[i]) == min_size[r]; };
+  auto hscore = [&](int i) -> int32_t {
+    return (int32_t)(((i < 8 ? (hsc_lo >> (8 * i)) : (hsc_hi >> (8 * (i - 8))))) & 0xFFu);
+  };
   const bool single = pol == KS_NUMA_POLICY_SINGLE_NUMA_NODE;
-  // DeviceShare's hints
-  DevHints dh;
-  dh.lists = 0;
-  dh.nm = 0;
-  dh.ok = 0;
-  if (dv) dh = dev_hints(c, p, *dv);
-  // the lists after filterProvidersHints (and filterSingleNumaHints): a list is a bit set of entries; entry 15 is
-  // the list's nil entry.  lkind: 0 / 1 = NodeNUMAResource cpu / memory, 2 = DeviceShare
-  constexpr int kNil = 15, kMaxLists = 2 + 4;
-  uint32_t bits[kMaxLists];
-  int lkind[kMaxLists];
-  bool nilpref[kMaxLists];
-  int nl = 0;
-  bool any_numa = false;
+  // The lists after filterProvidersHints (and filterSingleNumaHints), as bit sets of entries; bit kNil is the
+  // list's nil entry.  A list holding only a preferred nil entry (a provider / resource without preference) is a
+  // no-op in mergePermutation, so it stands for "no list".  Lists, outermost first: NodeNUMAResource cpu, memory,
+  // then DeviceShare.  DeviceShare returns one identical list per requested device resource; the merge over L
+  // identical lists equals the merge over one of them (checked exhaustively for K <= 2, the only case with device
+  // hints: tools/merge_collapse_check.c), so one list is walked.
+  constexpr int kNil = 15;
+  uint32_t lb[2];
+  bool lnp[2];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
-    if (!want[r]) continue;
-    any_numa = true;
-    lkind[nl] = r;
-    if (hset[r] == 0) {
-      bits[nl] = 1u << kNil;  // {nil, false}: "no possible NUMA affinities"
-      nilpref[nl] = false;
+    lnp[r] = !want[r];
+    if (!want[r]) {
+      lb[r] = 1u << kNil;  // no hints for this resource (the provider returns none when neither is requested)
+    } else if (hset[r] == 0) {
+      lb[r] = single ? 0u : (1u << kNil);  // {nil, false}: "no possible NUMA affinities"
     } else {
       uint32_t s = hset[r];
       if (single) {
         uint32_t f = 0;
-        for (int i = 0; i < nm; ++i)
-          if (((s >> i) & 1u) && __builtin_popcount(masks[i]) == 1 && pref_of(r, i)) f |= 1u << i;
+        for (int i = 0; i < nm; ++i) {
+          const uint32_t mk = numa_mask_at(tab, i);
+          if (((s >> i) & 1u) && __builtin_popcount(mk) == 1 && __builtin_popcount(mk) == min_size[r]) f |= 1u << i;
+        }
         s = f;
       }
-      bits[nl] = s;
-      nilpref[nl] = false;
+      lb[r] = s;
     }
-    ++nl;
   }
-  if (!any_numa) {  // the NUMA provider returns no hints: one preferred any-numa hint
-    lkind[nl] = 0;
-    bits[nl] = 1u << kNil;
-    nilpref[nl] = true;
-    ++nl;
-  }
-  uint32_t dbits = 0;  // DeviceShare entries (positions of dh.masks), after the single-numa-node filter
+  uint32_t db = 1u << kNil;
+  bool dnp = true;
   if (dh.lists) {
-    for (int i = 0; i < dh.nm; ++i) {
-      if (!((dh.ok >> i) & 1u)) continue;
-      const bool pr = __builtin_popcount(dh.masks[i]) == dh.minaff;
-      if (!single || (__builtin_popcount(dh.masks[i]) == 1 && pr)) dbits |= 1u << i;
+    dnp = false;
+    if (dh.ok == 0) {
+      db = single ? 0u : (1u << kNil);  // no allocating mask: {nil, false}
+    } else {
+      db = 0;
+      for (int i = 0; i < dh.npos; ++i) {
+        if (!((dh.ok >> i) & 1u)) continue;
+        const int pc = __builtin_popcount(dev_hint_mask(dh, i));
+        if (!single || (pc == 1 && pc == dh.minaff)) db |= 1u << i;
+      }
     }
-    const bool none = dh.ok == 0;  // no allocating mask: {nil, false} per list (dropped by single-numa-node)
-    for (int l = 0; l < dh.lists; ++l) {
-      lkind[nl] = 2;
-      bits[nl] = none ? (single ? 0u : (1u << kNil)) : dbits;
-      nilpref[nl] = false;
-      ++nl;
-    }
-  } else {
-    lkind[nl] = 2;
-    bits[nl] = 1u << kNil;
-    nilpref[nl] = true;
-    ++nl;
   }
-  if (single)
-    for (int l = 0; l < nl; ++l)
-      if (bits[l] == (1u << kNil) && !nilpref[l]) bits[l] = 0;
-  // mergeFilteredHints over the cartesian product, first list outermost
+  // mergeFilteredHints over the cartesian product, first list outermost (policy.go:129-226)
   const uint32_t dflt = (1u << K) - 1u;
   uint32_t best_mask = dflt;
   bool best_pref = false;
   int32_t best_score = 0;
-  bool empty = false;
-  for (int l = 0; l < nl; ++l) empty |= bits[l] == 0;
-  if (!empty) {
-    uint32_t rest[kMaxLists];
-    int cur[kMaxLists];
-    for (int l = 0; l < nl; ++l) {
-      cur[l] = __builtin_ctz(bits[l]);
-      rest[l] = bits[l] & (bits[l] - 1);
-    }
-    for (;;) {
-      // mergePermutation
-      uint32_t merged = dflt, first = 0;
-      bool pref = true, have = false;
-      for (int l = 0; l < nl; ++l) {
-        const int e = cur[l];
-        uint32_t m = 0;
-        bool hp;
-        if (e == kNil) {
-          hp = nilpref[l];
-        } else if (lkind[l] < 2) {
-          m = masks[e];
-          hp = pref_of(lkind[l], e);
-        } else {
-          m = dh.masks[e];
-          hp = __builtin_popcount(m) == dh.minaff;
-        }
-        if (m) {
-          if (!have) first = m;
-          else if (m != first) pref = false;
-          have = true;
-          merged &= m;
-        }
-        if (!hp) pref = false;
-      }
-      if (merged != 0) {
-        int32_t msc = 0;
-        for (int l = 0; l < nl; ++l) {
-          const int e = cur[l];
-          if (e != kNil && lkind[l] < 2 && masks[e] == merged && hsc[e] > msc) msc = hsc[e];
-        }
-        if (pref && !best_pref) {
-          best_mask = merged; best_pref = true; best_score = msc;
-        } else if (!pref && best_pref) {
-        } else if (!numa_narrower(merged, best_mask)) {
-          if (__builtin_popcount(merged) == __builtin_popcount(best_mask) && msc > best_score) {
+  if (lb[0] && lb[1] && db) {
+    for (uint32_t b0 = lb[0]; b0; b0 &= b0 - 1u) {
+      const int e0 = __builtin_ctz(b0);
+      const uint32_t m0 = e0 == kNil ? 0u : numa_mask_at(tab, e0);
+      const bool h0 = e0 == kNil ? lnp[0] : __builtin_popcount(m0) == min_size[0];
+      const int32_t s0 = e0 == kNil ? 0 : hscore(e0);
+      for (uint32_t b1 = lb[1]; b1; b1 &= b1 - 1u) {
+        const int e1 = __builtin_ctz(b1);
+        const uint32_t m1 = e1 == kNil ? 0u : numa_mask_at(tab, e1);
+        const bool h1 = e1 == kNil ? lnp[1] : __builtin_popcount(m1) == min_size[1];
+        const int32_t s1 = e1 == kNil ? 0 : hscore(e1);
+        for (uint32_t b2 = db; b2; b2 &= b2 - 1u) {
+          const int e2 = __builtin_ctz(b2);
+          const uint32_t m2 = e2 == kNil ? 0u : dev_hint_mask(dh, e2);
+          const bool h2 = e2 == kNil ? dnp : __builtin_popcount(m2) == dh.minaff;
+          // mergePermutation
+          uint32_t merged = dflt, first = 0;
+          bool pref = h0 && h1 && h2, have = false;
+          if (m0) { first = m0; have = true; merged &= m0; }
+          if (m1) { if (have && m1 != first) pref = false; if (!have) first = m1; have = true; merged &= m1; }
+          if (m2) { if (have && m2 != first) pref = false; have = true; merged &= m2; }
+          if (merged == 0) continue;
+          int32_t msc = 0;
+          if (m0 == merged && s0 > msc) msc = s0;
+          if (m1 == merged && s1 > msc) msc = s1;
+          if (pref && !best_pref) {
+            best_mask = merged; best_pref = true; best_score = msc;
+          } else if (!pref && best_pref) {
+          } else if (!numa_narrower(merged, best_mask)) {
+            if (__builtin_popcount(merged) == __builtin_popcount(best_mask) && msc > best_score) {
+              best_mask = merged; best_pref = pref; best_score = msc;
+            }
+          } else {
             best_mask = merged; best_pref = pref; best_score = msc;
           }
-        } else {
-          best_mask = merged; best_pref = pref; best_score = msc;
         }
       }
-      int l = nl - 1;
-      for (; l >= 0; --l) {
-        if (rest[l]) {
-          cur[l] = __builtin_ctz(rest[l]);
-          rest[l] &= rest[l] - 1;
-          break;
-        }
-        cur[l] = __builtin_ctz(bits[l]);
-        rest[l] = bits[l] & (bits[l] - 1);
-      }
-      if (l < 0) break;
     }
   }
   uint32_t affinity = best_mask;
@@ -429,34 +412,52 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
   }
   o.admitted = true;
   o.affinity = affinity;
-  // the NUMA plugin's Allocate
+  // the NUMA plugin's Allocate (tryBestToDistributeEvenly)
   if (affinity) {
-    int bitsk[kNumaDev], nb = 0;
+    const int nb = __builtin_popcount(affinity);
+    int ord0[kNumaDev];  // the affinity's NUMA ids ascending
+    {
+      uint32_t b = affinity;
 #pragma unroll
-    for (int k = 0; k < kNumaDev; ++k)
-      if ((affinity >> k) & 1u) bitsk[nb++] = k;
+      for (int i = 0; i < kNumaDev; ++i) {
+        ord0[i] = b ? __builtin_ctz(b) : 0;
+        b &= b - 1u;
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       if (!want[r]) continue;
       int ord[kNumaDev];
 #pragma unroll
-      for (int i = 0; i < kNumaDev; ++i) ord[i] = i < nb ? bitsk[i] : 0;
-      // sort.Slice insertion sort with less(i, j) comparing totalAvailable by slice position
-      for (int i = 1; i < nb; ++i)
+      for (int i = 0; i < kNumaDev; ++i) ord[i] = ord0[i];
+      // sort.Slice insertion sort with less(i, j) comparing totalAvailable by slice position (fixed per position)
+#pragma unroll
+      for (int i = 1; i < kNumaDev; ++i) {
+        bool go = i < nb;
+#pragma unroll
         for (int j = i; j > 0; --j) {
           const int64_t aj = j < K ? av[r][j] : 0, ai = (j - 1) < K ? av[r][j - 1] : 0;
-          if (!(aj < ai)) break;
-          const int t = ord[j];
-          ord[j] = ord[j - 1];
-          ord[j - 1] = t;
+          go = go && aj < ai;
+          if (go) {
+            const int t = ord[j];
+            ord[j] = ord[j - 1];
+            ord[j - 1] = t;
+          }
         }
+      }
       int64_t q = r == 0 ? p.cpu : p.mem;  // originalRequests
-      for (int i = 0; i < nb; ++i) {
+#pragma unroll
+      for (int i = 0; i < kNumaDev; ++i) {
+        if (i >= nb) break;
         // splitQuantity: a cpu-bind pod's cpu in whole CPUs (Quantity.Value() rounds up)
         const int64_t split = (r == 0 && bind) ? ((q + 999) / 1000) / (nb - i) * 1000 : q / (nb - i);
-        const int64_t a = av[r][ord[i]];
+        int64_t a = 0;
+#pragma unroll
+        for (int k = 0; k < kNumaDev; ++k) a = ord[i] == k ? av[r][k] : a;
         const int64_t got = a > split ? split : a;
-        o.alloc[r][ord[i]] = got;
+#pragma unroll
+        for (int k = 0; k < kNumaDev; ++k)
+          if (ord[i] == k) o.alloc[r][k] = got;
         q -= got;
       }
       if (q != 0) {
@@ -490,11 +491,25 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
       }
     }
   }
-  // DeviceShare's Allocate with the affinity
+  // DeviceShare's Allocate with the affinity (a hint's trial allocation when it had the same restriction)
   if (dv) {
-    const uint32_t dr = dev_eval<false>(c, p, *dv, nullptr, affinity ? affinity : ~0u).reasons;
-    if (dr) {
-      o.reasons = dr;
+    o.dev_done = true;
+    bool hit = false;
+    DevOut d = DevOut{0u, 0, 0u, 0u};
+    if (affinity) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (((dh.tried >> i) & 1u) && dev_hint_mask(dh, i) == affinity) {
+          d.reasons = i == 0 ? dh.r0 : (i == 1 ? dh.r1 : dh.r2);
+          d.raw = i == 0 ? dh.s0 : (i == 1 ? dh.s1 : dh.s2);
+          hit = true;
+        }
+    }
+    o.dev_hit = hit;
+    if (!hit && !DEFER_DEV) d = dev_eval<false>(c, p, *dv, nullptr, affinity ? affinity : ~0u);
+    o.dev = d;
+    if (d.reasons) {
+      o.reasons = d.reasons;
       return o;
     }
   }
@@ -505,7 +520,7 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       tal[r] += tot[r][k];
-      trq[r] += use[r][k];
+      trq[r] += used_of(r, k);
     }
   }
   if (!any_alloc) {

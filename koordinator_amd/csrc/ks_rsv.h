@@ -298,28 +298,42 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
   const bool dev_pod = DEV && c.dev && (p.flags & kPodHasGpu);
   // NodeNUMAResource (policy None part, then the topology-manager path on a policy node); returns DeviceShare's
   // NUMA restriction
+  // (without DEBUG a node some earlier Filter already rejected skips the expensive paths: its key is 0)
+  bool dev_pol = false;  // the policy path reached DeviceShare's Allocate under the same restriction as dev()
+  bool dev_pre = false;  // ... and dpre is its result
+  DevOut dpre = DevOut{0u, 0, 0u, 0u};
   auto numa = [&](EvalOut& o) __attribute__((always_inline)) -> uint32_t {
     if (!(NUMA && c.numa)) return ~0u;
     numa_eval<NSC, DEBUG>(c, p, r, o);
     if (!(POL && c.numa_pol) || (p.flags & kPodReqZero)) return ~0u;
+    if (!DEBUG && o.reasons) return ~0u;
     const auto nv = numav();
     if (nv.policy() == 0) return ~0u;
     using DVT = decltype(devv());
     NumaPolOut pr;
     if (dev_pod) {
       const DVT dv = devv();
-      pr = numa_policy_eval(c, p, nv, numa_node_ctx<NSC>(r), &dv);
+      pr = numa_policy_eval<!DEBUG>(c, p, nv, numa_node_ctx<NSC>(r), &dv);
     } else {
-      pr = numa_policy_eval(c, p, nv, numa_node_ctx<NSC>(r), (const DVT*)nullptr);
+      pr = numa_policy_eval<!DEBUG>(c, p, nv, numa_node_ctx<NSC>(r), (const DVT*)nullptr);
     }
     numa_policy_apply<DEBUG>(c, p, o, o.numa_rs, pr);
-    return (o.numa_rs == 0 && pr.admitted && pr.affinity) ? pr.affinity : ~0u;
+    const uint32_t allow = (o.numa_rs == 0 && pr.admitted && pr.affinity) ? pr.affinity : ~0u;
+    dev_pol = pr.dev_done && allow == (pr.affinity ? pr.affinity : ~0u);
+    dev_pre = dev_pol && pr.dev_hit;
+    dpre = pr.dev;
+    return allow;
   };
   auto dev = [&](EvalOut& o, uint32_t allow) __attribute__((always_inline)) {
     if (!dev_pod) return;
-    const DevOut d = dev_eval<false>(c, p, devv(), nullptr, allow);
+    if (!DEBUG && o.reasons) return;
+    const DevOut d = dev_pre ? dpre : dev_eval<false>(c, p, devv(), nullptr, allow);
     o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
     o.dev_raw = d.raw;
+    if (!DEBUG && dev_pol && d.reasons) {  // the deferred policy-path failure: no NUMA score (numa_policy_eval)
+      o.total -= o.numa * c.numa_pw;
+      o.numa = 0;
+    }
   };
   if (!RSV || !c.rsv || (p.rsv_class < 0 && !(p.flags & KS_POD_RSV_AFFINITY))) {
     if (info) *info = RsvOut{0u, 0, 0, 0, -1};
