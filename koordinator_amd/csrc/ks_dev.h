@@ -392,4 +392,79 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   return o;
 }
 
+// DeviceShare's Filter under several NUMA restrictions (generateTopologyHints' trial allocations): the per-minor
+// fits and scores do not depend on the restriction, so they are computed once; under a restriction the fit sets
+// are masked to its minors and dev_eval's feasibility logic runs on them.  dev_fits_ok(f, gin, rin) ==
+// (dev_eval<false>(c, p, v, nullptr, allow).reasons == 0) for dev_allowed(v, allow) = (gin, rin).
+struct DevFits {
+  DevType G, R;
+  GpuReq g;
+  uint64_t meta;
+  bool walk, same, has_gpu, has_rdma;
+};
+
+template <typename V>
+__device__ __forceinline__ DevFits dev_fits(const Cfg& c, const PodRec& p, const V& v, const GpuReq& g) {
+  DevFits f;
+  f.g = g;
+  f.has_gpu = (p.flags & kPodGpuReq) != 0;
+  f.has_rdma = p.rdma > 0;
+  const bool joint = f.has_gpu && f.has_rdma && p.joint != KS_JOINT_NONE;
+  f.same = p.joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
+  f.walk = joint && (f.same || g.rdesired > 1);
+  const uint64_t topo = (uint64_t)v.tot(kDevTopoW);
+  f.meta = (uint64_t)v.tot(kDevMetaW);
+  f.G.fit = f.R.fit = 0;
+  f.G.sc = f.R.sc = 0;
+  f.G.pcw = (uint32_t)topo;
+  f.R.pcw = (uint32_t)(topo >> 32);
+  if (f.has_gpu) {
+    const int64_t pod[3] = {g.core, g.mem, g.ratio};
+#pragma unroll
+    for (int k = 0; k < kGpus; ++k) {
+      const int64_t t[3] = {v.tot(k), v.tot(kGpus + k), v.tot(2 * kGpus + k)};
+      const int64_t u[3] = {v.use(k), v.use(kGpus + k), v.use(2 * kGpus + k)};
+      const int64_t fr[3] = {t[0] > u[0] ? t[0] - u[0] : 0, t[1] > u[1] ? t[1] - u[1] : 0, t[2] > u[2] ? t[2] - u[2] : 0};
+      const bool exists = t[0] || t[1] || t[2];
+      const bool fits = exists && (fr[0] || fr[1] || fr[2]) && (!g.has_core || g.core <= fr[0]) && g.mem <= fr[1] &&
+                        g.ratio <= fr[2];
+      f.G.fit |= fits ? (1u << k) : 0u;
+      if (f.walk && fits) f.G.sc |= (uint64_t)dev_score3(c, t, fr, pod) << (8 * k);
+    }
+  }
+  if (f.has_rdma) {
+#pragma unroll
+    for (int j = 0; j < kRdma; ++j) {
+      const int64_t t = v.tot(kDevRdmaW + j), u = v.use(kDevRdmaW + j);
+      const int64_t fr = t > u ? t - u : 0;
+      const bool fits = t != 0 && fr != 0 && g.rdma <= fr;
+      f.R.fit |= fits ? (1u << j) : 0u;
+      if (f.walk && fits) f.R.sc |= (uint64_t)dev_score1(c, t, fr, g.rdma) << (8 * j);
+    }
+  }
+  return f;
+}
+
+__device__ __forceinline__ uint64_t dev_byte_mask(uint32_t bits) {
+  uint64_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m |= ((bits >> k) & 1u) ? (0xFFull << (8 * k)) : 0ull;
+  return m;
+}
+
+__device__ __forceinline__ bool dev_fits_ok(const DevFits& f, uint32_t gin, uint32_t rin) {
+  DevType G = f.G, R = f.R;
+  G.fit &= gin;
+  R.fit &= rin;
+  G.sc &= dev_byte_mask(G.fit);
+  R.sc &= dev_byte_mask(R.fit);
+  if (f.walk) {
+    uint32_t om = 0, orm = 0;
+    if (dev_by_topology(G, R, f.g, f.same, f.meta, om, orm))
+      return !(f.same && dev_pcies_of(G, kGpus, om) != dev_pcies_of(R, kRdma, orm));
+    if (f.same) return false;
+  }
+  return !((f.has_gpu && __builtin_popcount(G.fit) < f.g.desired) || (f.has_rdma && __builtin_popcount(R.fit) < f.g.rdesired));
+}
+
 }  // namespace ks

@@ -128,17 +128,14 @@ __device__ __forceinline__ bool numa_narrower(uint32_t a, uint32_t b) {
 }
 
 // DeviceShare's topology hints on one node (generateTopologyHints): hint positions 0: {id0}, 1: {id1}, 2: {id0, id1}
-// over the device topology's (at most kDevHintIds) NUMA ids, which of them were tried / allocate, minAffinitySize,
-// the number of identical resource lists (0 = the provider expresses no preference), and each tried position's
-// trial allocation (reused when the merged affinity is that position's mask).
+// over the device topology's (at most kDevHintIds) NUMA ids, which of them allocate, minAffinitySize and the
+// number of identical resource lists (0 = the provider expresses no preference).
 struct DevHints {
   int lists;
   int npos;
   int id0, id1;
-  uint32_t tried, ok;
+  uint32_t ok;
   int minaff;
-  uint32_t r0, r1, r2;  // trial allocation reasons / raw score per tried position
-  int32_t s0, s1, s2;
 };
 
 __device__ __forceinline__ uint32_t dev_hint_mask(const DevHints& h, int i) {
@@ -152,10 +149,8 @@ __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, con
   h.lists = 0;
   h.npos = 0;
   h.id0 = h.id1 = 0;
-  h.tried = h.ok = 0;
+  h.ok = 0;
   h.minaff = -1;
-  h.r0 = h.r1 = h.r2 = 0u;
-  h.s0 = h.s1 = h.s2 = 0;
   if (!v.present()) return h;
   const uint64_t topo = (uint64_t)v.tot(kDevTopoW), meta = (uint64_t)v.tot(kDevMetaW);
   // numaTopology.nodes: NUMA nodes of the switches holding a device with a topology
@@ -197,19 +192,16 @@ __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, con
   }
   const bool has_gpu = (p.flags & kPodGpuReq) != 0, has_rdma = p.rdma > 0;
   h.npos = nid == 0 ? 0 : (nid == 1 ? 1 : 3);
-  for (int i = 0; i < h.npos; ++i) {  // not unrolled: one inlined copy of dev_eval
+  const DevFits fits = dev_fits(c, p, v, g);  // the trial allocations share the unrestricted per-minor fits
+  for (int i = 0; i < h.npos; ++i) {
     const uint32_t pos = (uint32_t)i + 1u;
     const uint32_t gm = ((pos & 1u) ? gin0 : 0u) | ((pos & 2u) ? gin1 : 0u);
     const uint32_t rm = ((pos & 1u) ? rin0 : 0u) | ((pos & 2u) ? rin1 : 0u);
     if ((has_gpu && __builtin_popcount(gm) < g.desired) || (has_rdma && __builtin_popcount(rm) < g.rdesired)) continue;
     const int cnt = __builtin_popcount(pos);
     h.minaff = h.minaff < 0 ? (cnt < nid ? cnt : nid) : (cnt < h.minaff ? cnt : h.minaff);
-    const DevOut d = dev_eval<false>(c, p, v, nullptr, dev_hint_mask(h, i));
-    h.tried |= 1u << i;
-    if (d.reasons == 0) h.ok |= 1u << i;
-    if (i == 0) { h.r0 = d.reasons; h.s0 = d.raw; }
-    else if (i == 1) { h.r1 = d.reasons; h.s1 = d.raw; }
-    else { h.r2 = d.reasons; h.s2 = d.raw; }
+    // the restriction to dev_hint_mask(h, i) keeps exactly the minors in gm / rm (dev_allowed)
+    if (dev_fits_ok(fits, gm, rm)) h.ok |= 1u << i;
   }
   if (h.minaff >= 0)
     h.lists = (has_gpu ? ((g.has_core || g.desired > 1) ? 3 : 2) : 0) + (has_rdma ? 1 : 0);
@@ -247,7 +239,7 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
   DevHints dh;
   dh.lists = 0;
   dh.npos = 0;
-  dh.tried = dh.ok = 0;
+  dh.ok = 0;
   dh.minaff = -1;
   if (dv) dh = dev_hints(c, p, *dv);
   const int pol = v.policy();
@@ -491,26 +483,16 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
       }
     }
   }
-  // DeviceShare's Allocate with the affinity (a hint's trial allocation when it had the same restriction)
+  // DeviceShare's Allocate with the affinity (with DEFER_DEV the caller's DeviceShare Filter, same restriction)
   if (dv) {
     o.dev_done = true;
-    bool hit = false;
-    DevOut d = DevOut{0u, 0, 0u, 0u};
-    if (affinity) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (((dh.tried >> i) & 1u) && dev_hint_mask(dh, i) == affinity) {
-          d.reasons = i == 0 ? dh.r0 : (i == 1 ? dh.r1 : dh.r2);
-          d.raw = i == 0 ? dh.s0 : (i == 1 ? dh.s1 : dh.s2);
-          hit = true;
-        }
-    }
-    o.dev_hit = hit;
-    if (!hit && !DEFER_DEV) d = dev_eval<false>(c, p, *dv, nullptr, affinity ? affinity : ~0u);
-    o.dev = d;
-    if (d.reasons) {
-      o.reasons = d.reasons;
-      return o;
+    if (!DEFER_DEV) {
+      o.dev = dev_eval<false>(c, p, *dv, nullptr, affinity ? affinity : ~0u);
+      o.dev_hit = true;
+      if (o.dev.reasons) {
+        o.reasons = o.dev.reasons;
+        return o;
+      }
     }
   }
   int64_t trq[2] = {0, 0}, tal[2] = {0, 0};

@@ -968,7 +968,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         nc.cpu_free = (int32_t)snuma[4 * s + 3];
         if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
           const DevLView dvl{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0};
-          npr = numa_policy_eval(cfg, pod, nl, nc, &dvl);
+          npr = numa_policy_eval<true>(cfg, pod, nl, nc, &dvl);  // the Filter passed on this state: DeviceShare follows
         } else {
           npr = numa_policy_eval(cfg, pod, nl, nc, (const DevLView*)nullptr);
         }
