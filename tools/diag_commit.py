@@ -8,7 +8,7 @@ which = sys.argv[1] if len(sys.argv) > 1 else "c2"
 w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4}[which]()
 cfg = w.cfg
 cfg.profile = 1
-ev = runtime.Evaluator(cfg, w.nodes, w.quotas, w.reservations, w.devices, w.cpus)
+ev = runtime.Evaluator(cfg, w.nodes, **w.tables(copy=False))
 ev.stage(w.pods)
 ev.checkpoint()
 for i in range(3):
