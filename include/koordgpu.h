@@ -25,7 +25,8 @@
  *                      followed by Reserve (framework_extender.go:457; load_aware.go:260;
  *                      elasticquota/plugin.go:323), for a batch of pods in queue order,
  *                      with exact one-pod-at-a-time semantics.
- *   ks_eval_pod_debug  one pod's Filter + Score over every node without Reserve
+ *   ks_eval_pod        one pod's Filter + Score over every node without Reserve
+ *   ks_assume          Reserve of one pod on the node the framework chose; ks_unreserve its Unreserve
  *                      (framework_extender.go:204 RunFilterPluginsWithNominatedPods,
  *                      :237 RunScorePlugins) — the parity/debug entry point.
  *
@@ -575,12 +576,43 @@ int ks_fetch_results(ks_ctx *ctx, ks_result *out, int32_t p);
 int ks_checkpoint(ks_ctx *ctx);
 int ks_restore(ks_ctx *ctx);
 
-/* Evaluate pod 0 of `pod` against every node without Reserve.
+/* ---- per-pod framework mode (INTEGRATION.md "per-pod drop-in"): the Go framework keeps its own
+ * scheduleOne and calls the plugins' PreFilter/Filter/Score through ks_eval_pod, selects the node, then reports
+ * Reserve (ks_assume) and, when Reserve of another plugin, Permit or Bind fails, Unreserve (ks_unreserve). ---- */
+
+/* Evaluate pod 0 of `pod` against every node without Reserve (PreFilter + Filter + Score +
+ * NormalizeScore of every enabled plugin; upstream findNodesThatPassFilters + prioritizeNodes).
  * reasons[n] gets KS_R_* bits (0 = feasible); scores[n*KS_NUM_SCORE_PLUGINS+k]
  * the un-weighted plugin-k score (0 for infeasible nodes); total[n] the weighted
- * sum (-1 for infeasible). Any output pointer may be NULL. */
+ * sum (-1 for infeasible). Any output pointer may be NULL.  Writes only into the caller's buffers; its
+ * device scratch lives with the context (no per-call allocation). */
+int ks_eval_pod(ks_ctx *ctx, const ks_pod_cols *pod, uint32_t *reasons, int64_t *scores, int64_t *total);
+/* the same entry under its round-1 name */
 int ks_eval_pod_debug(ks_ctx *ctx, const ks_pod_cols *pod, uint32_t *reasons, int64_t *scores,
                       int64_t *total);
+
+/* Reserve of pod 0 of `pod` on `node`, which the framework chose: every enabled plugin's Reserve
+ * (load_aware.go:260; elasticquota/plugin.go:323-335; reservation/plugin.go:532-570 with NominateReservation on
+ * the node; deviceshare/plugin.go:377-430; nodenumaresource/plugin.go:375-419) plus the scheduler cache's
+ * AssumePod (NodeInfo.AddPod).  No Filter and no quota admission run.  out: status KS_S_SCHEDULED or
+ * KS_S_RESERVE_FAILED (NodeNUMAResource could not allocate the cpuset; nothing changed), the reservation row
+ * and the GPU / RDMA minors; score is 0.  cpuset (optional): the pod's CPUs [KS_CPU_WORDS]; numa_alloc
+ * (optional): its NUMA-node allocation [KS_MAX_NUMA][2] (cpu milli, memory) on a NUMA-policy node.  Keep them
+ * for ks_unreserve. */
+int ks_assume(ks_ctx *ctx, const ks_pod_cols *pod, int32_t node, ks_result *out, uint64_t *cpuset,
+              int64_t *numa_alloc);
+
+/* Unreserve of every plugin (load_aware.go:265; elasticquota/plugin.go:339; reservation/plugin.go:572;
+ * deviceshare/plugin.go:432; nodenumaresource/plugin.go:421 -> NodeAllocation.release node_allocation.go:105-131)
+ * plus the cache's ForgetPod, for pod 0 of `pod` placed as `r` says (a ks_assume or ks_schedule result with
+ * status KS_S_SCHEDULED) with the CPUs `cpuset` and NUMA allocation `numa_alloc` it got (either may be NULL
+ * when the pod has none). */
+int ks_unreserve(ks_ctx *ctx, const ks_pod_cols *pod, const ks_result *r, const uint64_t *cpuset,
+                 const int64_t *numa_alloc);
+
+/* The NUMA-node allocation [p][KS_MAX_NUMA][2] of the last ks_schedule* call's first p pods (zeros off
+ * NUMA-policy nodes). */
+int ks_fetch_numa_alloc(ks_ctx *ctx, int64_t *out, int32_t p);
 
 int ks_read_nodes(ks_ctx *ctx, ks_node_state *out);
 int ks_read_quota_used(ks_ctx *ctx, int64_t *used /* q*KS_QUOTA_DIMS, row-major */);

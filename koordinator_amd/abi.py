@@ -406,6 +406,10 @@ EXPORTED_SYMBOLS = [
     "ks_checkpoint",
     "ks_restore",
     "ks_eval_pod_debug",
+    "ks_eval_pod",
+    "ks_assume",
+    "ks_unreserve",
+    "ks_fetch_numa_alloc",
     "ks_read_nodes",
     "ks_read_quota_used",
     "ks_get_stats",

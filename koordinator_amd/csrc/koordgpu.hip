@@ -815,7 +815,14 @@ struct ks_ctx {
   // pods
   int32_t np = 0;
   PodStage st{};   // staged pods of ks_stage_pods / ks_schedule
-  PodStage est{};  // single-pod evaluation (ks_eval_pod_debug)
+  PodStage est{};  // single-pod evaluation (ks_eval_pod)
+  PodStage ast{};  // per-pod framework mode (ks_assume / ks_unreserve)
+  int64_t* numa_alloc = nullptr;  // [cpuset_cap][2][kNumaDev] NUMA-policy allocation per pod of the last call
+  void* evbuf = nullptr;          // ks_eval_pod scratch, kept across calls
+  size_t evbuf_bytes = 0;
+  void* ures = nullptr;           // ks_unreserve scratch: node index, the pod's cpuset and NUMA allocation
+  void* rdscratch = nullptr;      // ks_read_nodes: the NodeInfo view of the reservation-restored columns
+  std::vector<int32_t> h_rsv_gi;  // caller reservation row -> CSR position
   // pass scratch
   uint2* sweep_out = nullptr;
   uint32_t* cand_chunk = nullptr;
@@ -1075,6 +1082,10 @@ void ks_destroy(ks_ctx* ctx) {
   void* p;
   dev_free(ctx->st.blob);
   dev_free(ctx->est.blob);
+  dev_free(ctx->ast.blob);
+  dev_free(ctx->evbuf);
+  dev_free(ctx->ures);
+  dev_free(ctx->rdscratch);
   p = ctx->sweep_out; dev_free(p);
   p = ctx->cand_chunk; dev_free(p);
   p = ctx->cand_t; dev_free(p);
@@ -1426,9 +1437,11 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
   int32_t* rowid = (int32_t*)(h.data() + o_row);
   for (int32_t i = 0; i < nr; ++i) beg[rc->node[perm[i]] + 1]++;
   for (int64_t n = 0; n < ctx->npad; ++n) beg[n + 1] += beg[n];
+  ctx->h_rsv_gi.assign((size_t)nr, -1);
   for (int32_t i = 0; i < nr; ++i) {
     const int32_t r = perm[i];
     rowid[i] = r;
+    ctx->h_rsv_gi[(size_t)r] = i;
     cls[i] = rc->owner_classes[r];
     const uint32_t flags = rc->flags ? rc->flags[r] & 0xfu : 0u;
     const uint32_t pol = rc->policy ? std::min<uint32_t>(rc->policy[r], 0xfu) : 0u;
@@ -2470,6 +2483,77 @@ static PassLaunch pass_launcher(int feat, int nsc) {
 #undef KS_PICK
 }
 
+// The commit kernel's arguments for the pods of stage st (cursor ctx->cursor, `total` pods, `batch` per pass).
+static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t batch, bool* qcache, size_t* smem) {
+  CommitArgs ca;
+  ca.dn = ctx->dnodes;
+  ca.rv = ctx->drv;
+  ca.c = ctx->kc;
+  ca.pods = st.recs;
+  ca.pq = st.pq;
+  ca.q = ctx->q;
+  ca.cursor = ctx->cursor;
+  ca.cand_chunk = ctx->cand_chunk;
+  ca.cand_t = ctx->cand_t;
+  ca.cand_bound = ctx->cand_bound;
+  ca.cand_top = ctx->cand_top;
+  ca.cand_count = ctx->cand_count;
+  ca.results = st.results;
+  ca.counters = ctx->counters;
+  ca.n = ctx->n;
+  ca.nchunks = ctx->nchunks;
+  ca.total_pods = total;
+  ca.batch = batch;
+  ca.k = ctx->k;
+  ca.rowcols = ctx->rowcols;
+  ca.rcap = commit_rcap(ctx, qcache);
+  ca.rsv_bytes = (int32_t)rsv_cache_bytes(ctx, ca.rcap);
+  ca.dev_bytes = (int32_t)dev_cache_bytes(ctx);
+  ca.dv = ctx->ddv;
+  ca.dev_M = ctx->dev_M;
+  ca.cpuset_list = ctx->cpuset_list;
+  ca.cpuset_n = ctx->cpuset_n;
+  ca.cpuset_split = ctx->cpuset_split;
+  ca.numa_alloc = ctx->numa_alloc;
+  ca.force = 0;
+  ca.numa_bytes = (int32_t)numa_cache_bytes(ctx);
+  ca.nv = ctx->dnv;
+  *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes).total;
+  return ca;
+}
+
+// the commit kernel's LDS size for this context: checked against the CU's 160 KB and set on the variant
+static int commit_attr_set(ks_ctx* ctx) {
+  bool qcache = false;
+  const int32_t rcap = commit_rcap(ctx, &qcache);
+  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx),
+                                    numa_cache_bytes(ctx)).total;
+  if (smem > 160 * 1024)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
+  hipError_t e = pass_launcher(kernel_feat(ctx), ctx->nsc).commit_attr(qcache, smem);
+  if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
+  return KS_OK;
+}
+
+// (pod, node) list + count + per-pod CPU sets / NUMA split / NUMA allocation of one call, for np pods
+static int ensure_cpuset_bufs(ks_ctx* ctx, int32_t np) {
+  if (!ctx->cfg.numa.enable || ctx->cpuset_cap >= np) return KS_OK;
+  void* p = ctx->cpuset_list;
+  dev_free(p);
+  ctx->cpuset_list = nullptr;
+  const int32_t cap = std::max<int32_t>(np, 64);
+  const size_t o_n = (size_t)cap * 8, o_out = o_n + 16, o_split = o_out + (size_t)cap * sizeof(CpuSet),
+               o_alloc = align16(o_split + (size_t)cap * 4), bytes = o_alloc + (size_t)cap * 2 * kNumaDev * 8;
+  if (dev_alloc(ctx, &p, bytes) != KS_OK) return KS_ENOMEM;
+  ctx->cpuset_list = (int2*)p;
+  ctx->cpuset_n = (int32_t*)((char*)p + o_n);
+  ctx->cpuset_out = (CpuSet*)((char*)p + o_out);
+  ctx->cpuset_split = (uint32_t*)((char*)p + o_split);
+  ctx->numa_alloc = (int64_t*)((char*)p + o_alloc);
+  ctx->cpuset_cap = cap;
+  return KS_OK;
+}
+
 template <int NSC>
 static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
   auto rec = [&](int kind) {
@@ -2589,40 +2673,9 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
     hipLaunchKernelGGL(merge_kernel, dim3(ctx->batch), dim3(64), 0, ctx->stream, ma);
   }
   rec(1);
-  CommitArgs ca;
-  ca.dn = ctx->dnodes;
-  ca.rv = ctx->drv;
-  ca.c = ctx->kc;
-  ca.pods = ctx->st.recs;
-  ca.pq = ctx->st.pq;
-  ca.q = ctx->q;
-  ca.cursor = ctx->cursor;
-  ca.cand_chunk = ctx->cand_chunk;
-  ca.cand_t = ctx->cand_t;
-  ca.cand_bound = ctx->cand_bound;
-  ca.cand_top = ctx->cand_top;
-  ca.cand_count = ctx->cand_count;
-  ca.results = ctx->st.results;
-  ca.counters = ctx->counters;
-  ca.n = ctx->n;
-  ca.nchunks = ctx->nchunks;
-  ca.total_pods = ctx->np;
-  ca.batch = ctx->batch;
-  ca.k = ctx->k;
-  ca.rowcols = ctx->rowcols;
   bool qcache = false;
-  ca.rcap = commit_rcap(ctx, &qcache);
-  ca.rsv_bytes = (int32_t)rsv_cache_bytes(ctx, ca.rcap);
-  ca.dev_bytes = (int32_t)dev_cache_bytes(ctx);
-  ca.dv = ctx->ddv;
-  ca.dev_M = ctx->dev_M;
-  ca.cpuset_list = ctx->cpuset_list;
-  ca.cpuset_n = ctx->cpuset_n;
-  ca.cpuset_split = ctx->cpuset_split;
-  ca.numa_bytes = (int32_t)numa_cache_bytes(ctx);
-  ca.nv = ctx->dnv;
-  const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes,
-                                    (size_t)ca.numa_bytes).total;
+  size_t smem = 0;
+  const CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, ctx->batch, &qcache, &smem);
   rec(2);
   HIPCHK(ctx, pl.commit(qcache, smem, ctx->stream, ca));
   rec(2);
@@ -2636,14 +2689,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   const int32_t np = ctx->np;
   if (np == 0) return KS_OK;
   {
-    bool qcache = false;
-    const int32_t rcap = commit_rcap(ctx, &qcache);
-    const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx),
-                                      numa_cache_bytes(ctx)).total;
-    if (smem > 160 * 1024)
-      KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
-    hipError_t e = pass_launcher(kernel_feat(ctx), ctx->nsc).commit_attr(qcache, smem);
-    if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
+    if (int rc = commit_attr_set(ctx); rc != KS_OK) return rc;
+    hipError_t e = hipSuccess;
     const size_t sel_smem = (size_t)ctx->nchunks * sizeof(uint2) + kSelHistBins * 4;
     if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
     e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_smem);
@@ -2680,23 +2727,12 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   if (ppw > ctx->batch) ppw = ctx->batch;
   const int64_t nwork = std::max<int64_t>(local_chunks, 1) * ((ctx->batch + ppw - 1) / ppw);
   const int sweep_blocks = (int)((std::max<int64_t>(1, std::min<int64_t>((nwork + 3) / 4, env_cap)) + 7) & ~7ll);  // % 8 == 0 (XCD swizzle)
-  if (ctx->cfg.numa.enable && ctx->cpuset_cap < np) {
-    // (pod, node) list + its count + the per-pod CPU sets of this call
-    void* p = ctx->cpuset_list;
-    dev_free(p);
-    ctx->cpuset_list = nullptr;
-    const int32_t cap = std::max<int32_t>(np, 64);
-    if (dev_alloc(ctx, &p, (size_t)cap * 8 + 16 + (size_t)cap * sizeof(CpuSet) + (size_t)cap * 4) != KS_OK) return KS_ENOMEM;
-    ctx->cpuset_list = (int2*)p;
-    ctx->cpuset_n = (int32_t*)((char*)p + (size_t)cap * 8);
-    ctx->cpuset_out = (CpuSet*)((char*)p + (size_t)cap * 8 + 16);
-    ctx->cpuset_split = (uint32_t*)((char*)p + (size_t)cap * 8 + 16 + (size_t)cap * sizeof(CpuSet));
-    ctx->cpuset_cap = cap;
-  }
+  if (ensure_cpuset_bufs(ctx, np) != KS_OK) return KS_ENOMEM;
   hipEvent_t t0 = take_event(ctx, 0), t1 = take_event(ctx, 1);
   if (ctx->cpuset_list) {
     HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_out, 0, (size_t)np * sizeof(CpuSet), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->numa_alloc, 0, (size_t)np * 2 * kNumaDev * 8, ctx->stream));
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 256, ctx->stream));
@@ -2831,17 +2867,23 @@ int ks_restore(ks_ctx* ctx) {
   return KS_OK;
 }
 
-int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t* scores, int64_t* total) {
-  if (!ctx || !pod) return ctx ? (ctx->err = "ks_eval_pod_debug: bad args", KS_EINVAL) : KS_EINVAL;
-  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_eval_pod_debug before ks_load_nodes");
+int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t* scores, int64_t* total) {
+  if (!ctx || !pod) return ctx ? (ctx->err = "ks_eval_pod: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_eval_pod before ks_load_nodes");
   if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ensure_stage(ctx, ctx->est, 1) != KS_OK) return KS_ENOMEM;
   if (stage_cols(ctx, ctx->est, pod, 1) != KS_OK || prep_stage(ctx, ctx->est, 1) != KS_OK) return KS_EHIP;
   const int64_t n = ctx->n;
-  void* buf = nullptr;
+  // the per-node outputs in a scratch buffer that lives with the context (grown, never freed per call)
   const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4) + 64;
-  if (dev_alloc(ctx, &buf, bytes) != KS_OK) return KS_ENOMEM;
+  if (ctx->evbuf_bytes < bytes) {
+    dev_free(ctx->evbuf);
+    ctx->evbuf_bytes = 0;
+    if (dev_alloc(ctx, &ctx->evbuf, bytes) != KS_OK) return KS_ENOMEM;
+    ctx->evbuf_bytes = bytes;
+  }
+  void* buf = ctx->evbuf;
   uint32_t* dr = (uint32_t*)buf;
   int64_t* ds = (int64_t*)((char*)buf + ((size_t)n * 4 + 15) / 16 * 16);
   int64_t* dt = ds + (size_t)n * KS_NUM_SCORE_PLUGINS;
@@ -2860,13 +2902,266 @@ int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, in
       hipLaunchKernelGGL(rsv_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, draw, dhi, ds, dt,
                          ctx->cfg.reservation.plugin_weight);
   }
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess && reasons && n) e = hipMemcpyAsync(reasons, dr, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess && scores && n) e = hipMemcpyAsync(scores, ds, (size_t)n * 8 * KS_NUM_SCORE_PLUGINS, hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess && total && n) e = hipMemcpyAsync(total, dt, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  (void)hipFree(buf);
-  if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "ks_eval_pod_debug: %s", hipGetErrorString(e));
+  HIPCHK(ctx, hipGetLastError());
+  if (reasons && n) HIPCHK(ctx, hipMemcpyAsync(reasons, dr, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (scores && n) HIPCHK(ctx, hipMemcpyAsync(scores, ds, (size_t)n * 8 * KS_NUM_SCORE_PLUGINS, hipMemcpyDeviceToHost, ctx->stream));
+  if (total && n) HIPCHK(ctx, hipMemcpyAsync(total, dt, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_eval_pod_debug(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t* scores, int64_t* total) {
+  return ks_eval_pod(ctx, pod, reasons, scores, total);
+}
+
+// Unreserve of every plugin + the scheduler cache's ForgetPod for one pod (ks_unreserve; one thread, a few dozen
+// read-modify-writes on the node's, the quota chain's, the reservation's and the devices' rows).
+struct UnreserveArgs {
+  DevNodes d;
+  DevRsv rv;
+  DevDev dv;
+  DevNuma nv;
+  DevCpu cpu;
+  DevQuotas q;
+  DevPodQuota pq;
+  const PodRec* pod;
+  Cfg c;
+  int32_t node, gi;        // node; the reservation's CSR position (-1 = none)
+  uint32_t gmin, rmin;     // DeviceShare minors of the allocation
+  const uint64_t* cpuset;  // [KS_CPU_WORDS] the pod's CPUs
+  const int64_t* nalloc;   // [2][kNumaDev] its NUMA-node allocation (cpu milli, memory)
+  int32_t quota, dev, cpu_loaded, numa_pol, ratio_amp;
+};
+
+__global__ void unreserve_kernel(UnreserveArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const PodRec p = a.pod[0];
+  const int64_t n = a.node;
+  DevNodes& d = a.d;
+  // ElasticQuota UnreservePod (group_quota_manager.go updatePodUsedNoLock with the pod removed)
+  if (a.quota && p.quota >= 0) {
+    const uint32_t mask = a.pq.mask[0];
+    for (int32_t cur = p.quota; cur >= 0; cur = a.q.parent[cur])
+      for (int dd = 0; dd < KS_QUOTA_DIMS; ++dd) {
+        if (!((mask >> dd) & 1u)) continue;
+        a.q.used[(size_t)cur * KS_QUOTA_DIMS + dd] -= a.pq.req[dd][0];
+        if (p.flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + dd] -= a.pq.req[dd][0];
+      }
+  }
+  // ForgetPod (NodeInfo.RemovePod) + podAssignCache.unAssign (load_aware.go:265)
+  d.req_cpu[n] -= p.cpu;
+  d.req_mem[n] -= p.mem;
+  d.req_eph[n] -= p.eph;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) d.req_sc[k][n] -= p.sc[k];
+  d.nz_cpu[n] -= p.nzcpu;
+  d.nz_mem[n] -= p.nzmem;
+  d.pod_count[n] -= 1;
+  d.la_term_cpu[n] -= p.est_cpu;
+  d.la_term_mem[n] -= p.est_mem;
+  if (p.flags & KS_POD_PROD) {
+    d.la_pterm_cpu[n] -= p.est_cpu;
+    d.la_pterm_mem[n] -= p.est_mem;
+  }
+  // reservationCache.forgetPod: Allocated -= Mask(requests, ResourceNames); the pod leaves the assigned set
+  if (a.gi >= 0) {
+    const uint32_t keys = rsv_keys(a.rv.meta[a.gi]);
+    for (int dd = 0; dd < kRsvDims; ++dd)
+      if ((keys >> dd) & 1u) a.rv.allocd[(int64_t)dd * a.rv.nr + a.gi] -= pod_dim(p, dd);
+    a.rv.assigned[a.gi] -= 1;
+  }
+  // DeviceShare: nodeDevice.updateCacheUsed(allocation, pod, false)
+  if (a.dev && (a.gmin | a.rmin)) {
+    GpuReq g;
+    if (dev_prepare(p, DevGView{a.dv, n}, g) == 0) {
+      for (int k = 0; k < kGpus; ++k) {
+        if (!((a.gmin >> k) & 1u)) continue;
+        a.dv.used[(int64_t)(0 * kGpus + k) * a.dv.npad + n] -= g.core;
+        a.dv.used[(int64_t)(1 * kGpus + k) * a.dv.npad + n] -= g.mem;
+        a.dv.used[(int64_t)(2 * kGpus + k) * a.dv.npad + n] -= g.ratio;
+      }
+      for (int j = 0; j < kRdma; ++j)
+        if ((a.rmin >> j) & 1u) a.dv.used[(int64_t)(kDevRdmaW + j) * a.dv.npad + n] -= g.rdma;
+    }
+  }
+  // NodeAllocation.release (node_allocation.go:105-131): the CPUs (reference count 1 -> removed) and the
+  // NUMA-node resources (SubtractWithNonNegativeResult; the entries stay)
+  if (a.cpu_loaded && a.cpuset) {
+    CpuSet cs;
+    int32_t cnt = 0;
+    for (int w = 0; w < kCpuW; ++w) cs.w[w] = a.cpuset[w] & a.cpu.allocated[n].w[w];
+    for (int w = 0; w < kCpuW; ++w) cnt += __builtin_popcountll(cs.w[w]);
+    if (cnt) {
+      a.cpu.allocated[n] = cs_andnot(a.cpu.allocated[n], cs);
+      a.cpu.excl_pcpu[n] = cs_andnot(a.cpu.excl_pcpu[n], cs);
+      a.cpu.excl_numa[n] = cs_andnot(a.cpu.excl_numa[n], cs);
+      const int32_t cpus = d.numa_cpus[n] - cnt;
+      d.numa_cpus[n] = cpus;
+      const int64_t A = (int64_t)cpus * 1000;
+      const double ratio = d.numa_ratio[n];
+      d.numa_amilli[n] = A;
+      d.numa_off[n] = (a.ratio_amp && ratio > 1.0) ? (int64_t)::ceil((double)A * ratio) - A : 0;
+      if (d.cpu_free[n] >= 0) d.cpu_free[n] += cnt;
+      const int32_t tid = a.cpu.topo_id[n];
+      if (a.numa_pol && tid >= 0 && a.nv.count[n] > 0) {
+        const CpuTopo& t = a.cpu.topo[tid];
+        for (int k = 0; k < kNumaDev && k < a.nv.count[n]; ++k) {
+          const int32_t ck = cs_count(cs_and(cs, t.node_mask[k]));
+          if (!ck) continue;
+          const int64_t o = (int64_t)k * a.nv.npad + n;
+          const int32_t c1 = a.nv.cs[o] - ck;
+          a.nv.cs[o] = c1;
+          a.nv.free[o] += ck;
+          const int64_t m = (int64_t)c1 * 1000;
+          a.nv.off[o] = ratio > 1.0 ? (int64_t)::ceil((double)m * ratio) - m : 0;
+        }
+      }
+    }
+  }
+  if (a.numa_pol && a.nalloc && a.nv.count[n] > 0) {
+    for (int k = 0; k < kNumaDev && k < a.nv.count[n]; ++k)
+      for (int r = 0; r < 2; ++r) {
+        const int64_t o = ((int64_t)r * kNumaDev + k) * a.nv.npad + n;
+        const int64_t v = a.nv.used[o] - a.nalloc[r * kNumaDev + k];
+        a.nv.used[o] = v < 0 ? 0 : v;
+      }
+  }
+}
+
+// ---- per-pod framework mode: the framework runs Filter/Score through ks_eval_pod, picks the node, and
+// reports its Reserve / Unreserve here ----
+
+int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out, uint64_t* cpuset, int64_t* numa_alloc) {
+  if (!ctx || !pod || !out) return ctx ? (ctx->err = "ks_assume: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_assume before ks_load_nodes");
+  if (node < 0 || node >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_assume: node %d out of range", node);
+  if (ctx->cfg.quota.enable && pod->quota && !ctx->quota_blob) KS_FAIL(ctx, KS_ESTATE, "ks_assume: quotas not loaded");
+  if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (int rc = commit_attr_set(ctx); rc != KS_OK) return rc;
+  if (ensure_stage(ctx, ctx->ast, 1) != KS_OK || ensure_cpuset_bufs(ctx, 1) != KS_OK) return KS_ENOMEM;
+  if (stage_cols(ctx, ctx->ast, pod, 1) != KS_OK || prep_stage(ctx, ctx->ast, 1) != KS_OK) return KS_EHIP;
+  // one pass of one pod whose only candidate is `node` (an untouched node's snapshot key is taken as is): the
+  // commit kernel's Reserve path of every plugin runs on it; force skips the quota admission
+  struct {
+    uint32_t chunk;
+    uint2 t;
+    int32_t count;
+    uint64_t bound, top;
+  } h{(uint32_t)(node >> 6), make_uint2((1u << 6) | (uint32_t)(63 - (node & 63)), 0u), 1, 0ull, 0ull};
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cand_chunk, &h.chunk, 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cand_t, &h.t, 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cand_count, &h.count, 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cand_bound, &h.bound, 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cand_top, &h.top, 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream));
+  if (ctx->cpuset_list) {
+    HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_out, 0, sizeof(CpuSet), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->numa_alloc, 0, 2 * kNumaDev * 8, ctx->stream));
+  }
+  bool qcache = false;
+  size_t smem = 0;
+  CommitArgs ca = commit_args(ctx, ctx->ast, 1, 1, &qcache, &smem);
+  ca.force = 1;
+  HIPCHK(ctx, pass_launcher(kernel_feat(ctx), ctx->nsc).commit(qcache, smem, ctx->stream, ca));
+  if (ctx->cpu_loaded && ctx->n > 0) {
+    hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
+                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
+                       (const PodRec*)ctx->ast.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
+                       (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+    HIPCHK(ctx, hipGetLastError());
+  }
+  HIPCHK(ctx, hipMemcpyAsync(out, ctx->ast.results, sizeof(ks_result), hipMemcpyDeviceToHost, ctx->stream));
+  int64_t na[2 * kNumaDev] = {0};
+  if (cpuset) {
+    if (ctx->cpuset_list) HIPCHK(ctx, hipMemcpyAsync(cpuset, ctx->cpuset_out, sizeof(CpuSet), hipMemcpyDeviceToHost, ctx->stream));
+    else memset(cpuset, 0, sizeof(CpuSet));
+  }
+  if (numa_alloc && ctx->cpuset_list)
+    HIPCHK(ctx, hipMemcpyAsync(na, ctx->numa_alloc, sizeof(na), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (numa_alloc) {
+    memset(numa_alloc, 0, sizeof(int64_t) * KS_MAX_NUMA * 2);
+    for (int k = 0; k < kNumaDev; ++k)
+      for (int r = 0; r < 2; ++r) numa_alloc[k * 2 + r] = na[r * kNumaDev + k];
+  }
+  if (out->node != node && out->status == KS_S_SCHEDULED)
+    KS_FAIL(ctx, KS_EHIP, "ks_assume: placed on node %d instead of %d", out->node, node);
+  return KS_OK;
+}
+
+int ks_unreserve(ks_ctx* ctx, const ks_pod_cols* pod, const ks_result* r, const uint64_t* cpuset, const int64_t* numa_alloc) {
+  if (!ctx || !pod || !r) return ctx ? (ctx->err = "ks_unreserve: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_unreserve before ks_load_nodes");
+  if (r->status != KS_S_SCHEDULED || r->node < 0 || r->node >= ctx->n)
+    KS_FAIL(ctx, KS_EINVAL, "ks_unreserve: the result is not a placement (status %u, node %d)", r->status, r->node);
+  if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
+  int32_t gi = -1;
+  if (r->reservation >= 0) {
+    if (!ctx->cfg.reservation.enable || (size_t)r->reservation >= ctx->h_rsv_gi.size())
+      KS_FAIL(ctx, KS_EINVAL, "ks_unreserve: reservation row %d unknown", r->reservation);
+    gi = ctx->h_rsv_gi[(size_t)r->reservation];
+  }
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ensure_stage(ctx, ctx->ast, 1) != KS_OK) return KS_ENOMEM;
+  if (!ctx->ures && dev_alloc(ctx, &ctx->ures, 16 + sizeof(CpuSet) + 2 * kNumaDev * 8) != KS_OK) return KS_ENOMEM;
+  if (stage_cols(ctx, ctx->ast, pod, 1) != KS_OK || prep_stage(ctx, ctx->ast, 1) != KS_OK) return KS_EHIP;
+  char* u = (char*)ctx->ures;
+  int32_t* d_idx = (int32_t*)u;
+  uint64_t* d_cs = (uint64_t*)(u + 16);
+  int64_t* d_na = (int64_t*)(u + 16 + sizeof(CpuSet));
+  const int32_t node = r->node;
+  HIPCHK(ctx, hipMemcpyAsync(d_idx, &node, 4, hipMemcpyHostToDevice, ctx->stream));
+  if (cpuset) HIPCHK(ctx, hipMemcpyAsync(d_cs, cpuset, sizeof(CpuSet), hipMemcpyHostToDevice, ctx->stream));
+  int64_t na[2 * kNumaDev] = {0};
+  if (numa_alloc)
+    for (int k = 0; k < kNumaDev; ++k)
+      for (int q = 0; q < 2; ++q) na[q * kNumaDev + k] = numa_alloc[k * 2 + q];
+  HIPCHK(ctx, hipMemcpyAsync(d_na, na, sizeof(na), hipMemcpyHostToDevice, ctx->stream));
+  // the node's reservation base restore follows the reservation's state: out before, back in after
+  const bool rb = gi >= 0 && ctx->rsv_based;
+  if (rb && rsv_launch_base(ctx, d_idx, 1, -1, 0) != KS_OK) return KS_EHIP;
+  UnreserveArgs ua;
+  ua.d = ctx->d;
+  ua.rv = ctx->rv;
+  ua.dv = ctx->dv;
+  ua.nv = ctx->nv;
+  ua.cpu = ctx->cpu;
+  ua.q = ctx->q;
+  ua.pq = ctx->ast.pq;
+  ua.pod = ctx->ast.recs;
+  ua.c = ctx->kc;
+  ua.node = node;
+  ua.gi = gi;
+  ua.gmin = r->gpu_minors;
+  ua.rmin = r->rdma_minors;
+  ua.cpuset = cpuset ? d_cs : nullptr;
+  ua.nalloc = numa_alloc ? d_na : nullptr;
+  ua.quota = ctx->kc.quota_enable && ctx->quota_blob;
+  ua.dev = ctx->kc.dev && ctx->dev_loaded;
+  ua.cpu_loaded = ctx->cpu_loaded;
+  ua.numa_pol = ctx->kc.numa_pol && ctx->numa_blob;
+  ua.ratio_amp = ctx->cfg.numa.enable;
+  hipLaunchKernelGGL(unreserve_kernel, dim3(1), dim3(64), 0, ctx->stream, ua);
+  HIPCHK(ctx, hipGetLastError());
+  if (rb && rsv_launch_base(ctx, d_idx, 1, +1, 1) != KS_OK) return KS_EHIP;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+int ks_fetch_numa_alloc(ks_ctx* ctx, int64_t* out, int32_t p) {
+  if (!ctx || (p > 0 && !out) || p < 0) return ctx ? (ctx->err = "ks_fetch_numa_alloc: bad args", KS_EINVAL) : KS_EINVAL;
+  if (p > ctx->np) KS_FAIL(ctx, KS_EINVAL, "ks_fetch_numa_alloc: %d pods requested, %d scheduled", p, ctx->np);
+  if (p == 0) return KS_OK;
+  memset(out, 0, (size_t)p * KS_MAX_NUMA * 2 * 8);
+  if (!ctx->numa_alloc || ctx->cpuset_cap < p) return KS_OK;
+  std::vector<int64_t> h((size_t)p * 2 * kNumaDev);
+  HIPCHK(ctx, hipMemcpyAsync(h.data(), ctx->numa_alloc, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  for (int32_t i = 0; i < p; ++i)
+    for (int k = 0; k < kNumaDev; ++k)
+      for (int q = 0; q < 2; ++q) out[((size_t)i * KS_MAX_NUMA + k) * 2 + q] = h[((size_t)i * 2 + q) * kNumaDev + k];
   return KS_OK;
 }
 
@@ -2878,20 +3173,37 @@ int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
     if (!h || !n) return hipSuccess;
     return hipMemcpyAsync(h, d, n * w, hipMemcpyDeviceToHost, ctx->stream);
   };
-  // the columns hold the reservation base restore: report the reference's NodeInfo
-  if (ctx->rsv_based && rsv_launch_base(ctx, nullptr, ctx->n, -1, 0) != KS_OK) return KS_EHIP;
-  HIPCHK(ctx, cp(o->req_milli_cpu, ctx->d.req_cpu, 8));
-  HIPCHK(ctx, cp(o->req_memory, ctx->d.req_mem, 8));
-  HIPCHK(ctx, cp(o->req_ephemeral, ctx->d.req_eph, 8));
-  HIPCHK(ctx, cp(o->pod_count, ctx->d.pod_count, 4));
-  HIPCHK(ctx, cp(o->nonzero_milli_cpu, ctx->d.nz_cpu, 8));
-  HIPCHK(ctx, cp(o->nonzero_memory, ctx->d.nz_mem, 8));
-  for (int k = 0; k < KS_MAX_SCALARS; ++k) HIPCHK(ctx, cp(o->req_scalar[k], ctx->d.req_sc[k], 8));
-  HIPCHK(ctx, cp(o->la_term_milli_cpu, ctx->d.la_term_cpu, 8));
-  HIPCHK(ctx, cp(o->la_term_memory, ctx->d.la_term_mem, 8));
-  HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, ctx->d.la_pterm_cpu, 8));
-  HIPCHK(ctx, cp(o->la_prod_term_memory, ctx->d.la_pterm_mem, 8));
-  if (ctx->rsv_based && rsv_launch_base(ctx, nullptr, ctx->n, +1, 0) != KS_OK) return KS_EHIP;
+  // the columns hold the reservation base restore: the reference's NodeInfo is computed into a scratch copy of
+  // the restored columns (the live columns are never touched)
+  DevNodes v = ctx->d;
+  if (ctx->rsv_based && n) {
+    const size_t bytes = n * 8 * (5 + KS_MAX_SCALARS);
+    if (!ctx->rdscratch && dev_alloc(ctx, &ctx->rdscratch, (size_t)ctx->npad * 8 * (5 + KS_MAX_SCALARS)) != KS_OK)
+      return KS_ENOMEM;
+    (void)bytes;
+    int64_t* sc = (int64_t*)ctx->rdscratch;
+    int64_t** cols[5 + KS_MAX_SCALARS] = {&v.req_cpu, &v.req_mem, &v.req_eph, &v.nz_cpu, &v.nz_mem};
+    for (int k = 0; k < KS_MAX_SCALARS; ++k) cols[5 + k] = &v.req_sc[k];
+    for (int c = 0; c < 5 + KS_MAX_SCALARS; ++c) {
+      int64_t* dst = sc + (size_t)c * ctx->npad;
+      HIPCHK(ctx, hipMemcpyAsync(dst, *cols[c], n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+      *cols[c] = dst;
+    }
+    hipLaunchKernelGGL(rsv_base_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, v, ctx->rv,
+                       (const int32_t*)nullptr, (int64_t)n, (int64_t)-1, 0);
+    HIPCHK(ctx, hipGetLastError());
+  }
+  HIPCHK(ctx, cp(o->req_milli_cpu, v.req_cpu, 8));
+  HIPCHK(ctx, cp(o->req_memory, v.req_mem, 8));
+  HIPCHK(ctx, cp(o->req_ephemeral, v.req_eph, 8));
+  HIPCHK(ctx, cp(o->pod_count, v.pod_count, 4));
+  HIPCHK(ctx, cp(o->nonzero_milli_cpu, v.nz_cpu, 8));
+  HIPCHK(ctx, cp(o->nonzero_memory, v.nz_mem, 8));
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) HIPCHK(ctx, cp(o->req_scalar[k], v.req_sc[k], 8));
+  HIPCHK(ctx, cp(o->la_term_milli_cpu, v.la_term_cpu, 8));
+  HIPCHK(ctx, cp(o->la_term_memory, v.la_term_mem, 8));
+  HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, v.la_pterm_cpu, 8));
+  HIPCHK(ctx, cp(o->la_prod_term_memory, v.la_pterm_mem, 8));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }

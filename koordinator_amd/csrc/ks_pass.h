@@ -217,6 +217,8 @@ struct CommitArgs {
   int2* cpuset_list;   // (pod, node) of every cpu-bind Reserve, in placement order (ks_cpuset.h)
   int32_t* cpuset_n;
   uint32_t* cpuset_split;  // [pod] CPUs per NUMA node of a cpu-bind Reserve on a NUMA-policy node (0 = whole node)
+  int64_t* numa_alloc;     // [pod][2][kNumaDev] NUMA-policy Reserve: the pod's NUMANodeResources (cpu milli, memory)
+  int32_t force;           // ks_assume: the framework chose the node; no quota admission (Reserve only)
   int32_t rcap;        // reservations cached in LDS per slot (0 = none)
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
   int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
@@ -595,7 +597,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       const int64_t u = qlds->used[o], l = qlds->limit[o];
       const uint64_t tw = touched[tn >> 6];
       st_next = 0;
-      if (has_q) {
+      if (has_q && !a.force) {
         const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
         const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
         if (__ballot(in_pod && ((lm >> lane) & 1u) && (req + u > l))) {
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         return;
       }
     } else {
-      st_next = admit(j);
+      st_next = a.force ? 0u : admit(j);
       if (st_next) return;
       if (top && !((touched[tn >> 6] >> (tn & 63)) & 1ull)) {
         cn.fast = true;
@@ -995,6 +997,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         sdev_use[lane * kDevLdsStride + s] = nv;
         gst(a.dv->used + (int64_t)lane * a.dv->npad + node, nv);  // the HBM table for the next pass
       }
+    }
+    if ((FEAT & 8) && a.numa_alloc && lane < 2 * kNumaDev) {
+      int64_t v = 0;
+#pragma unroll
+      for (int q = 0; q < 2 * kNumaDev; ++q) v = (q == lane) ? npr.alloc[q / kNumaDev][q % kNumaDev] : v;
+      a.numa_alloc[(int64_t)(cursor0 + j) * 2 * kNumaDev + lane] = (npol && npr.reasons == 0) ? v : 0;
     }
     uint32_t cpu_split = 0;  // cpu-bind pod: CPUs per NUMA node (8 bits each), 0 = takeCPUs over the whole node
     if (npol && npr.reasons == 0) {

@@ -77,6 +77,10 @@ def lib() -> C.CDLL:
     L.ks_checkpoint.argtypes = [vp]
     L.ks_restore.argtypes = [vp]
     L.ks_eval_pod_debug.argtypes = [vp, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
+    L.ks_eval_pod.argtypes = [vp, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
+    L.ks_assume.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult), abi.PU64, abi.P64]
+    L.ks_unreserve.argtypes = [vp, C.POINTER(abi.KsPodCols), C.POINTER(abi.KsResult), abi.PU64, abi.P64]
+    L.ks_fetch_numa_alloc.argtypes = [vp, abi.P64, C.c_int32]
     L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
     L.ks_read_quota_used.argtypes = [vp, abi.P64]
     L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
@@ -277,10 +281,43 @@ class Evaluator:
         scores = np.zeros(max(self.n, 1) * abi.KS_NUM_SCORE_PLUGINS, np.int64)
         total = np.zeros(max(self.n, 1), np.int64)
         cols = pod.ks()
-        self._chk(self.L.ks_eval_pod_debug(self.h, C.byref(cols), reasons.ctypes.data_as(abi.PU32),
-                                           scores.ctypes.data_as(abi.P64), total.ctypes.data_as(abi.P64)))
+        self._chk(self.L.ks_eval_pod(self.h, C.byref(cols), reasons.ctypes.data_as(abi.PU32),
+                                     scores.ctypes.data_as(abi.P64), total.ctypes.data_as(abi.P64)))
         n = self.n
         return reasons[:n], scores[: n * abi.KS_NUM_SCORE_PLUGINS].reshape(n, abi.KS_NUM_SCORE_PLUGINS), total[:n]
+
+    def assume(self, pod: PodTable, node: int):
+        """Reserve of pod 0 on `node` (the framework's choice): (result record, cpuset words, NUMA allocation
+        [KS_MAX_NUMA][2])."""
+        r = np.zeros(1, RESULT_DTYPE)
+        cs = np.zeros(abi.KS_CPU_WORDS, np.uint64)
+        na = np.zeros((abi.KS_MAX_NUMA, 2), np.int64)
+        cols = pod.ks()
+        self._chk(self.L.ks_assume(self.h, C.byref(cols), int(node), r.ctypes.data_as(C.POINTER(abi.KsResult)),
+                                   cs.ctypes.data_as(abi.PU64), na.ctypes.data_as(abi.P64)))
+        return r, cs, na
+
+    def unreserve(self, pod: PodTable, r, cpuset=None, numa_alloc=None):
+        """Unreserve of pod 0 placed as the result record r says (a 1-element RESULT_DTYPE array)."""
+        r = np.ascontiguousarray(r, RESULT_DTYPE).reshape(1)
+        cols = pod.ks()
+        cs = None if cpuset is None else np.ascontiguousarray(cpuset, np.uint64)
+        na = None if numa_alloc is None else np.ascontiguousarray(numa_alloc, np.int64)
+        self._chk(self.L.ks_unreserve(self.h, C.byref(cols), r.ctypes.data_as(C.POINTER(abi.KsResult)),
+                                      cs.ctypes.data_as(abi.PU64) if cs is not None else None,
+                                      na.ctypes.data_as(abi.P64) if na is not None else None))
+
+    def fetch_numa_alloc(self, p: int) -> np.ndarray:
+        out = np.zeros((max(p, 1), abi.KS_MAX_NUMA, 2), np.int64)
+        self._chk(self.L.ks_fetch_numa_alloc(self.h, out.ctypes.data_as(abi.P64), p))
+        return out[:p]
+
+    def schedule_raw(self, pods: PodTable) -> np.ndarray:
+        """ks_schedule's result records (RESULT_DTYPE), for ks_unreserve"""
+        out = np.zeros(max(pods.n, 1), RESULT_DTYPE)
+        cols = pods.ks()
+        self._chk(self.L.ks_schedule(self.h, C.byref(cols), pods.n, out.ctypes.data_as(C.POINTER(abi.KsResult))))
+        return out[: pods.n]
 
     def read_nodes(self) -> NodeState:
         st = NodeState(self.n)

@@ -2250,6 +2250,137 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
   return 0;
 }
 
+/* The framework chose `node` for pod 0 of pc (per-pod mode): every plugin's Reserve there, as ko_schedule runs it
+ * at its chosen node -- the NUMA policy path's allocation on the pre-Reserve state, NodeNUMAResource's cpuset,
+ * the Reservation nomination (NominateReservation on the node, plugin.go:544-557), DeviceShare, NodeInfo.AddPod +
+ * the LoadAware assign cache, ElasticQuota ReservePod.  No Filter and no quota admission.  numa_alloc (optional):
+ * [KS_MAX_NUMA][2] the NUMA plugin's allocation (cpu milli, memory). */
+int ko_assume(ko_sched *s, const ks_pod_cols *pc, int32_t node, ks_result *out, int64_t *numa_alloc) {
+  if (node < 0 || node >= s->n) return -1;
+  if (s->cpusets_cap < 1) {
+    free(s->cpusets);
+    s->cpusets = (uint64_t *)calloc(KS_CPU_WORDS, 8);
+    s->cpusets_cap = 1;
+  }
+  memset(s->cpusets, 0, KS_CPU_WORDS * 8);
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  const int64_t n = node;
+  memset(out, 0, sizeof(*out));
+  out->node = node;
+  out->reservation = -1;
+  out->status = KS_S_SCHEDULED;
+  ko_rstate st0;
+  rsv_restore(s, &p, n, &st0);
+  ko_eff e0 = st0.e;
+  ko_numa_out no;
+  ko_npol npc;
+  numa_policy_ctx(s, &p, n, &e0, &npc, &no);
+  if (numa_alloc) {
+    memset(numa_alloc, 0, sizeof(int64_t) * KS_MAX_NUMA * 2);
+    if (npc.on && !npc.reasons) memcpy(numa_alloc, no.alloc, sizeof(no.alloc));
+  }
+  const uint32_t allow = npol_allow(s, &p, n, &e0, &npc);
+  if (p.bind && cpu_reserve(s, &p, n, 0, &npc) != 0) {
+    out->status = KS_S_RESERVE_FAILED;
+    if (numa_alloc) memset(numa_alloc, 0, sizeof(int64_t) * KS_MAX_NUMA * 2);
+    return 0;
+  }
+  int32_t nom = -1;
+  if (s->cfg.reservation.enable) {
+    int64_t ord = 0;
+    nom = rsv_nominate(s, &p, n, &st0, &ord);
+  }
+  if (nom >= 0) {
+    out->reservation = nom;
+    rsv_reserve(s, &p, nom);
+  }
+  dev_reserve(s, &p, n, &out->gpu_minors, &out->rdma_minors, allow);
+  numa_reserve(s, &p, n, &npc);
+  node_reserve(s, &p, n);
+  quota_reserve(s, &p);
+  return 0;
+}
+
+/* Unreserve of every plugin (load_aware.go:265, elasticquota/plugin.go:339, reservation/plugin.go:572,
+ * deviceshare/plugin.go:432, nodenumaresource/plugin.go:421 -> NodeAllocation.release node_allocation.go:105-131)
+ * plus the scheduler cache's ForgetPod (NodeInfo.RemovePod), for pod 0 of pc placed on r->node with the
+ * allocation it got: r (reservation, minors), cpuset (KS_CPU_WORDS words, may be NULL), numa_alloc
+ * ([KS_MAX_NUMA][2], may be NULL). */
+int ko_unreserve(ko_sched *s, const ks_pod_cols *pc, const ks_result *r, const uint64_t *cpuset,
+                 const int64_t *numa_alloc) {
+  const int64_t n = r->node;
+  if (n < 0 || n >= s->n) return -1;
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  /* ElasticQuota UnreservePod */
+  if (s->cfg.quota.enable && p.quota >= 0)
+    for (int32_t cur = p.quota; cur >= 0; cur = s->q[cur].parent)
+      for (int d = 0; d < KS_QUOTA_DIMS; d++) {
+        if (!((p.qmask >> d) & 1u)) continue;
+        s->q[cur].used[d] -= p.qreq[d];
+        if (p.flags & KS_POD_NONPREEMPTIBLE) s->q[cur].npused[d] -= p.qreq[d];
+      }
+  /* ForgetPod + podAssignCache.unAssign */
+  ko_nodes *d = &s->nd;
+  d->req_cpu[n] -= p.cpu;
+  d->req_mem[n] -= p.mem;
+  d->req_eph[n] -= p.eph;
+  for (int k = 0; k < KS_MAX_SCALARS; k++) d->req_sc[k][n] -= p.sc[k];
+  d->nz_cpu[n] -= p.nzcpu;
+  d->nz_mem[n] -= p.nzmem;
+  d->pod_count[n] -= 1;
+  d->la_term_cpu[n] -= p.est_cpu;
+  d->la_term_mem[n] -= p.est_mem;
+  if (p.flags & KS_POD_PROD) {
+    d->la_pterm_cpu[n] -= p.est_cpu;
+    d->la_pterm_mem[n] -= p.est_mem;
+  }
+  /* reservationCache.forgetPod: Allocated -= Mask(req, names), the pod leaves the assigned set */
+  if (r->reservation >= 0 && s->cfg.reservation.enable) {
+    ko_rsv *rv = &s->rv;
+    const int32_t i = r->reservation;
+    for (int dd = 0; dd < KO_D; dd++)
+      if ((rv->keys[i] >> dd) & 1u) rv->allocd[(size_t)i * KO_D + dd] -= pod_dim(&p, dd);
+    rv->assigned[i] -= 1;
+  }
+  /* DeviceShare: nodeDevice.updateCacheUsed(allocation, pod, false) */
+  if ((r->gpu_minors || r->rdma_minors) && s->dv.loaded) {
+    ko_devreq g;
+    if (dev_prepare(s, &p, n, &g) == 0) {
+      for (int k = 0; k < KO_GPUS; k++) {
+        if (!((r->gpu_minors >> k) & 1u)) continue;
+        int64_t *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
+        for (int q = 0; q < 3; q++) u[q] -= g.req[KO_T_GPU][q];
+      }
+      for (int k = 0; k < KO_RDMA; k++)
+        if ((r->rdma_minors >> k) & 1u) s->dv.rused[(size_t)n * KO_RDMA + k] -= g.req[KO_T_RDMA][0];
+    }
+  }
+  /* NodeAllocation.release: the CPUs (refcount 1 -> removed) and the NUMA-node resources
+   * (SubtractWithNonNegativeResult; the entries stay) */
+  if (cpuset && s->cpu_loaded && s->topo_of[n] >= 0) {
+    const ko_topo *t = &s->topos[s->topo_of[n]];
+    for (int c = 0; c < t->ncpus; c++) {
+      if (!((cpuset[c >> 6] >> (c & 63)) & 1ull)) continue;
+      const size_t o = (size_t)n * KO_MAX_CPUS + c;
+      if (!s->cpu_alloc[o]) continue;
+      s->cpu_alloc[o] = 0;
+      s->cpu_excl[o] = -1;
+      d->numa_cpus[n] -= 1;
+      if (s->numa_loaded && t->node[c] >= 0 && t->node[c] < KS_MAX_NUMA) s->numa_cs[(size_t)n * KS_MAX_NUMA + t->node[c]]--;
+    }
+  }
+  if (numa_alloc && s->numa_loaded)
+    for (int k = 0; k < s->numa_count[n]; k++)
+      for (int q = 0; q < 2; q++) {
+        int64_t *u = s->numa_used + ((size_t)n * KS_MAX_NUMA + k) * 2 + q;
+        *u -= numa_alloc[k * 2 + q];
+        if (*u < 0) *u = 0;
+      }
+  return 0;
+}
+
 int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *scores, int64_t *total) {
   ko_pod p;
   load_pod(s, pc, 0, &p);

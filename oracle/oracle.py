@@ -51,6 +51,8 @@ def lib():
         L.ko_read_numa_nodes.argtypes = [C.c_void_p, abi.P64, abi.P64]
         L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
         L.ko_eval_pod.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), abi.PU32, abi.P64, abi.P64]
+        L.ko_assume.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult), abi.P64]
+        L.ko_unreserve.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.POINTER(abi.KsResult), abi.PU64, abi.P64]
         L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
         L.ko_read_quota_used.argtypes = [C.c_void_p, abi.P64]
         L.ko_least_requested_score.restype = C.c_int64
@@ -190,6 +192,32 @@ class Oracle:
         return {"node": arr["node"].copy(), "status": arr["status"].copy(), "score": arr["score"].copy(),
                 "reservation": arr["reservation"].copy(), "gpu_minors": arr["gpu_minors"].copy(),
                 "rdma_minors": arr["rdma_minors"].copy()}
+
+    def schedule_raw(self, pods: PodTable) -> np.ndarray:
+        out = (abi.KsResult * max(pods.n, 1))()
+        cols = pods.ks()
+        self.L.ko_schedule(self.h, C.byref(cols), pods.n, out)
+        return np.frombuffer(out, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS), count=pods.n).copy()
+
+    def assume(self, pod: PodTable, node: int):
+        """ko_assume: (result record, cpuset words, NUMA allocation [KS_MAX_NUMA][2])"""
+        r = (abi.KsResult * 1)()
+        na = np.zeros((abi.KS_MAX_NUMA, 2), np.int64)
+        cols = pod.ks()
+        if self.L.ko_assume(self.h, C.byref(cols), int(node), r, na.ctypes.data_as(abi.P64)) != 0:
+            raise ValueError("ko_assume failed")
+        rec = np.frombuffer(r, dtype=np.dtype(abi.RESULT_DTYPE_FIELDS), count=1).copy()
+        return rec, self.fetch_cpusets(1)[0].copy(), na
+
+    def unreserve(self, pod: PodTable, r, cpuset=None, numa_alloc=None):
+        rec = np.ascontiguousarray(r, np.dtype(abi.RESULT_DTYPE_FIELDS)).reshape(1)
+        cols = pod.ks()
+        cs = None if cpuset is None else np.ascontiguousarray(cpuset, np.uint64)
+        na = None if numa_alloc is None else np.ascontiguousarray(numa_alloc, np.int64)
+        if self.L.ko_unreserve(self.h, C.byref(cols), rec.ctypes.data_as(C.POINTER(abi.KsResult)),
+                               cs.ctypes.data_as(abi.PU64) if cs is not None else None,
+                               na.ctypes.data_as(abi.P64) if na is not None else None) != 0:
+            raise ValueError("ko_unreserve failed")
 
     def eval_pod(self, pod: PodTable):
         reasons = np.zeros(self.n, np.uint32)
