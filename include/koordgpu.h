@@ -516,6 +516,24 @@ int ks_load_nodes(ks_ctx *ctx, const ks_node_cols *nodes, int64_t n);
 int ks_update_nodes(ks_ctx *ctx, const int32_t *idx, const ks_node_cols *rows, int64_t m);
 int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
 
+/* ---- informer deltas for the other tables (f1): rows replaced in place on the device, the rest of each table
+ * untouched; idx / rows are distinct.  A batch of deltas is applied at a ks_schedule boundary (the snapshot
+ * semantics); ks_checkpoint after them if the bench restores. ---- */
+/* deviceshare nodeDeviceCache.updateNodeDevice (device_cache.go:489-527): rows[i] is node idx[i]'s devices */
+int ks_update_devices(ks_ctx *ctx, const int32_t *idx, const ks_device_cols *rows, int64_t m);
+/* NodeResourceTopology / NodeAllocation changes (nodenumaresource topology_eventhandler.go, resource_manager.go
+ * Update / Release): node idx[i]'s CPU state from row i, topology indices into the table of the last
+ * ks_load_cpu_state */
+int ks_update_cpu_state(ks_ctx *ctx, const int32_t *idx, const ks_cpu_state_cols *rows, int64_t m);
+/* GroupQuotaManager OnQuotaUpdate / pod events (elasticquota/core/group_quota_manager.go:736-870): quota idx[i]'s
+ * limit, min, used, non-preemptible used and masks from row i (the parents stay; a tree change is ks_load_quotas) */
+int ks_update_quotas(ks_ctx *ctx, const int32_t *idx, const ks_quota_cols *rows, int32_t m);
+/* reservation cache updates of loaded reservations (reservation/cache.go:104-216): the allocated amounts
+ * (allocated[d][i], d < KS_RSV_DIMS as in ks_reservation_cols) and assigned-pod counts of the caller rows rows[i]; the
+ * nodes' reservation restore and owner classes follow.  Adding or removing a reservation is ks_load_reservations. */
+int ks_update_reservation_usage(ks_ctx *ctx, const int32_t *rows, const int64_t *const *allocated,
+                                const int32_t *assigned, int32_t m);
+
 /* GPU devices of the loaded nodes (deviceshare nodeDeviceCache, device_cache.go:44-160); call after
  * ks_load_nodes.  Reserve (plugin.go:377-430 -> updateCacheUsed) adds each allocation to used. */
 int ks_load_devices(ks_ctx *ctx, const ks_device_cols *dev, int64_t n);

@@ -410,6 +410,10 @@ EXPORTED_SYMBOLS = [
     "ks_assume",
     "ks_unreserve",
     "ks_fetch_numa_alloc",
+    "ks_update_devices",
+    "ks_update_cpu_state",
+    "ks_update_quotas",
+    "ks_update_reservation_usage",
     "ks_read_nodes",
     "ks_read_quota_used",
     "ks_get_stats",

@@ -879,6 +879,11 @@ struct ks_ctx {
   std::vector<int8_t> h_numa_k;    // per node: NUMA node count of a policy node (0 = no policy / none)
   std::vector<uint16_t> h_dev_ids; // per node: NUMA ids of the device topology (DeviceShare hints)
   std::vector<int8_t> h_cpu_nn;    // per node: NUMA nodes of its CPU topology (0 = none, -1 = ids not 0..n-1)
+  std::vector<CpuTopo> h_topos;    // the loaded CPU topologies (ks_update_cpu_state refers to them)
+  std::vector<int8_t> h_topo_dense;
+  std::vector<int32_t> h_rsv_node; // CSR position -> node
+  void* dscratch = nullptr;        // delta uploads (ks_update_*): indices + row words
+  size_t dscratch_bytes = 0;
   uint32_t* cpuset_split = nullptr;  // [cpuset_cap] per pod (CommitArgs.cpuset_split)
   // stats
   ks_stats stats{};
@@ -1086,6 +1091,7 @@ void ks_destroy(ks_ctx* ctx) {
   dev_free(ctx->evbuf);
   dev_free(ctx->ures);
   dev_free(ctx->rdscratch);
+  dev_free(ctx->dscratch);
   p = ctx->sweep_out; dev_free(p);
   p = ctx->cand_chunk; dev_free(p);
   p = ctx->cand_t; dev_free(p);
@@ -1438,10 +1444,12 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
   for (int32_t i = 0; i < nr; ++i) beg[rc->node[perm[i]] + 1]++;
   for (int64_t n = 0; n < ctx->npad; ++n) beg[n + 1] += beg[n];
   ctx->h_rsv_gi.assign((size_t)nr, -1);
+  ctx->h_rsv_node.assign((size_t)nr, -1);
   for (int32_t i = 0; i < nr; ++i) {
     const int32_t r = perm[i];
     rowid[i] = r;
     ctx->h_rsv_gi[(size_t)r] = i;
+    ctx->h_rsv_node[(size_t)i] = rc->node[r];
     cls[i] = rc->owner_classes[r];
     const uint32_t flags = rc->flags ? rc->flags[r] & 0xfu : 0u;
     const uint32_t pol = rc->policy ? std::min<uint32_t>(rc->policy[r], 0xfu) : 0u;
@@ -1503,37 +1511,33 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
 
 // Upload the device table (kDevTW words of totals + topology, kDevQW words of used, flags per node; ks_dev.h);
 // dc == NULL: no device info.
-static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
-  const size_t np = (size_t)ctx->npad, tw = (size_t)kDevTW * np, uw = (size_t)kDevQW * np;
-  const size_t o_flags = 0, o_total = (np * 4 + 15) / 16 * 16, o_used = o_total + tw * 8, o_ck = o_used + uw * 8,
-               bytes = o_ck + uw * 8;
-  std::vector<char> h(bytes, 0);
-  uint32_t* flags = (uint32_t*)(h.data() + o_flags);
-  int64_t* total = (int64_t*)(h.data() + o_total);
-  int64_t* used = (int64_t*)(h.data() + o_used);
+// The device table words of `rows` rows of dc: flags[r], total[w * np + r], used[w * np + r] and the NUMA ids of
+// the device topology (dev_hints) per row; np = the column stride.
+static int dev_encode(ks_ctx* ctx, const ks_device_cols* dc, int64_t rows, size_t np, uint32_t* flags, int64_t* total,
+                      int64_t* used, uint16_t* ids_out) {
   if (dc) {
     for (int k = 0; k < kGpus; ++k) {
       const int64_t* cols[6] = {dc->total_core[k], dc->total_memory[k], dc->total_ratio[k],
                                 dc->used_core[k], dc->used_memory[k], dc->used_ratio[k]};
       for (int c = 0; c < 6; ++c)
-        if (check_range64(ctx, cols[c], ctx->n, "device quantity") != KS_OK) return KS_EINVAL;
-      for (int64_t n = 0; n < ctx->n; ++n)
+        if (check_range64(ctx, cols[c], rows, "device quantity") != KS_OK) return KS_EINVAL;
+      for (int64_t n = 0; n < rows; ++n)
         for (int q = 0; q < 3; ++q) {
           total[((size_t)q * kGpus + k) * np + n] = cols[q] ? cols[q][n] : 0;
           used[((size_t)q * kGpus + k) * np + n] = cols[3 + q] ? cols[3 + q][n] : 0;
         }
     }
     for (int j = 0; j < kRdma; ++j) {
-      if (check_range64(ctx, dc->total_rdma[j], ctx->n, "rdma quantity") != KS_OK ||
-          check_range64(ctx, dc->used_rdma[j], ctx->n, "rdma quantity") != KS_OK)
+      if (check_range64(ctx, dc->total_rdma[j], rows, "rdma quantity") != KS_OK ||
+          check_range64(ctx, dc->used_rdma[j], rows, "rdma quantity") != KS_OK)
         return KS_EINVAL;
-      for (int64_t n = 0; n < ctx->n; ++n) {
+      for (int64_t n = 0; n < rows; ++n) {
         total[((size_t)kDevRdmaW + j) * np + n] = dc->total_rdma[j] ? dc->total_rdma[j][n] : 0;
         used[((size_t)kDevRdmaW + j) * np + n] = dc->used_rdma[j] ? dc->used_rdma[j][n] : 0;
       }
     }
     // topology: 4-bit switch per minor, NUMA node / socket per switch; switches numbered in (socket, node) order
-    for (int64_t n = 0; n < ctx->n; ++n) {
+    for (int64_t n = 0; n < rows; ++n) {
       uint64_t topo = 0, meta = 0;
       uint32_t used_sw = 0;
       auto sw = [&](const uint8_t* col, int k, int shift) -> int {
@@ -1564,11 +1568,11 @@ static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
       total[(size_t)kDevTopoW * np + n] = (int64_t)topo;
       total[(size_t)kDevMetaW * np + n] = (int64_t)meta;
     }
-    for (int64_t n = 0; n < ctx->n; ++n) flags[n] = dc->flags ? dc->flags[n] : 0;
+    for (int64_t n = 0; n < rows; ++n) flags[n] = dc->flags ? dc->flags[n] : 0;
   }
   // NUMA nodes of the device topology per node, as dev_hints (ks_numa.h) derives them
-  ctx->h_dev_ids.assign((size_t)ctx->n, 0);
-  for (int64_t n = 0; dc && n < ctx->n; ++n) {
+  for (int64_t n = 0; n < rows; ++n) ids_out[n] = 0;
+  for (int64_t n = 0; dc && n < rows; ++n) {
     const uint64_t topo = (uint64_t)total[(size_t)kDevTopoW * np + n], meta = (uint64_t)total[(size_t)kDevMetaW * np + n];
     uint32_t ids = 0;
     for (int k = 0; k < kGpus; ++k) {
@@ -1581,8 +1585,21 @@ static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
       const uint32_t pc = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
       if (total[((size_t)kDevRdmaW + j) * np + n] != 0 && pc < 8u) ids |= 1u << ((uint32_t)(meta >> (8 * pc)) & 0xFu);
     }
-    ctx->h_dev_ids[(size_t)n] = (uint16_t)ids;
+    ids_out[n] = (uint16_t)ids;
   }
+  return KS_OK;
+}
+
+static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
+  const size_t np = (size_t)ctx->npad, tw = (size_t)kDevTW * np, uw = (size_t)kDevQW * np;
+  const size_t o_flags = 0, o_total = (np * 4 + 15) / 16 * 16, o_used = o_total + tw * 8, o_ck = o_used + uw * 8,
+               bytes = o_ck + uw * 8;
+  std::vector<char> h(bytes, 0);
+  uint32_t* flags = (uint32_t*)(h.data() + o_flags);
+  int64_t* total = (int64_t*)(h.data() + o_total);
+  int64_t* used = (int64_t*)(h.data() + o_used);
+  ctx->h_dev_ids.assign((size_t)ctx->n, 0);
+  if (int rc = dev_encode(ctx, dc, ctx->n, np, flags, total, used, ctx->h_dev_ids.data()); rc != KS_OK) return rc;
   dev_free(ctx->dev_blob);
   if (dev_alloc(ctx, &ctx->dev_blob, bytes) != KS_OK) return KS_ENOMEM;
   HIPCHK(ctx, hipMemcpyAsync(ctx->dev_blob, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -1705,6 +1722,38 @@ static int build_cpu_topo(ks_ctx* ctx, const ks_cpu_topology& in, int32_t ti, Cp
   return KS_OK;
 }
 
+// One node's CPU state from row i of st (validated against topology table tt): topology index, CPU sets, the
+// CPUs available to cpuset pods and |allocated| (the cpuset millicores of filterAmplifiedCPUs / 1000).
+static int cpu_encode_row(ks_ctx* ctx, const ks_cpu_state_cols* st, int64_t i, int64_t node, int32_t ntopo,
+                          const std::vector<CpuTopo>& tt, int32_t& tid, CpuSet& al, CpuSet& xp, CpuSet& xn, CpuSet& rs,
+                          int32_t& freec, int32_t& ncpu) {
+  const int32_t ti = st->topology[i];
+  if (ti < -1 || ti >= ntopo) KS_FAIL(ctx, KS_EINVAL, "node %lld: cpu topology %d out of range", (long long)node, ti);
+  auto rd = [&](const uint64_t* p) {
+    CpuSet c = cs_zero();
+    if (p) memcpy(c.w, p + i * kCpuW, sizeof(c.w));
+    return c;
+  };
+  al = rd(st->allocated);
+  xp = rd(st->excl_pcpu);
+  xn = rd(st->excl_numa);
+  rs = rd(st->reserved);
+  tid = ti;
+  freec = -1;
+  if (ti >= 0) {
+    const CpuSet& all = tt[ti].all;
+    if (cs_count(cs_andnot(cs_or(cs_or(al, xp), cs_or(xn, rs)), all)) != 0)
+      KS_FAIL(ctx, KS_EINVAL, "node %lld: CPU set outside its topology", (long long)node);
+    if (cs_count(cs_andnot(cs_or(xp, xn), al)) != 0 || cs_count(cs_and(xp, xn)) != 0)
+      KS_FAIL(ctx, KS_EINVAL, "node %lld: exclusive CPU sets must be disjoint subsets of allocated", (long long)node);
+    freec = cs_count(cs_andnot(all, cs_or(al, rs)));
+  } else if (cs_count(al) != 0) {
+    KS_FAIL(ctx, KS_EINVAL, "node %lld: allocated CPUs without a topology", (long long)node);
+  }
+  ncpu = cs_count(al);
+  return KS_OK;
+}
+
 int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, const ks_cpu_state_cols* st) {
   if (!ctx || ntopo < 0 || (ntopo > 0 && !topos) || !st || !st->topology || !st->allocated)
     return ctx ? (ctx->err = "ks_load_cpu_state: bad args", KS_EINVAL) : KS_EINVAL;
@@ -1724,31 +1773,9 @@ int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, 
   }
   std::vector<int32_t> tid((size_t)np, -1), freec((size_t)np, -1), ncpu((size_t)np, 0);
   std::vector<CpuSet> al((size_t)np, cs_zero()), xp((size_t)np, cs_zero()), xn((size_t)np, cs_zero()), rs((size_t)np, cs_zero());
-  for (int64_t i = 0; i < n; ++i) {
-    const int32_t ti = st->topology[i];
-    if (ti < -1 || ti >= ntopo) KS_FAIL(ctx, KS_EINVAL, "node %lld: cpu topology %d out of range", (long long)i, ti);
-    auto rd = [&](const uint64_t* p) {
-      CpuSet c = cs_zero();
-      if (p) memcpy(c.w, p + i * kCpuW, sizeof(c.w));
-      return c;
-    };
-    al[i] = rd(st->allocated);
-    xp[i] = rd(st->excl_pcpu);
-    xn[i] = rd(st->excl_numa);
-    rs[i] = rd(st->reserved);
-    tid[i] = ti;
-    if (ti >= 0) {
-      const CpuSet& all = tt[ti].all;
-      if (cs_count(cs_andnot(cs_or(cs_or(al[i], xp[i]), cs_or(xn[i], rs[i])), all)) != 0)
-        KS_FAIL(ctx, KS_EINVAL, "node %lld: CPU set outside its topology", (long long)i);
-      if (cs_count(cs_andnot(cs_or(xp[i], xn[i]), al[i])) != 0 || cs_count(cs_and(xp[i], xn[i])) != 0)
-        KS_FAIL(ctx, KS_EINVAL, "node %lld: exclusive CPU sets must be disjoint subsets of allocated", (long long)i);
-      freec[i] = cs_count(cs_andnot(all, cs_or(al[i], rs[i])));
-    } else if (cs_count(al[i]) != 0) {
-      KS_FAIL(ctx, KS_EINVAL, "node %lld: allocated CPUs without a topology", (long long)i);
-    }
-    ncpu[i] = cs_count(al[i]);  // the cpuset millicores of filterAmplifiedCPUs are |allocated| x 1000
-  }
+  for (int64_t i = 0; i < n; ++i)
+    if (int rc = cpu_encode_row(ctx, st, i, i, ntopo, tt, tid[i], al[i], xp[i], xn[i], rs[i], freec[i], ncpu[i]); rc != KS_OK)
+      return rc;
   dev_free(ctx->cpu_blob);
   ctx->cpu_loaded = false;
   const size_t tb = align16(tt.size() * sizeof(CpuTopo)), ib = align16((size_t)np * 4), sb = (size_t)np * sizeof(CpuSet);
@@ -1782,6 +1809,8 @@ int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, 
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   ctx->cpu_cpc = cpc;
   ctx->cpu_loaded = true;
+  ctx->h_topos = tt;
+  ctx->h_topo_dense = dense;
   ctx->h_cpu_nn.assign((size_t)n, 0);
   for (int64_t i = 0; i < n; ++i)
     if (const int32_t ti = tid[(size_t)i]; ti >= 0) ctx->h_cpu_nn[(size_t)i] = dense[(size_t)ti] ? (int8_t)tt[(size_t)ti].nnodes : (int8_t)-1;
@@ -2865,6 +2894,194 @@ int ks_restore(ks_ctx* ctx) {
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
+}
+
+// ---- informer deltas (f1): rows of the device, CPU-state, quota and reservation-usage tables replaced in place
+// (the node rows have ks_update_nodes); a delta re-bases nothing else, so ks_checkpoint after a batch of them ----
+
+// dst[idx[i] * rs + w * cs] = src[w * m + i] for the m rows and W words (elem = 4 or 8 bytes)
+template <typename T>
+__global__ void scatter_words_kernel(T* dst, int64_t rs, int64_t cs, int32_t W, const int32_t* idx, const T* src, int64_t m) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= m * W) return;
+  const int64_t w = t / m, i = t - w * m;
+  dst[(int64_t)idx[i] * rs + w * cs] = src[t];
+}
+
+static int scatter_words(ks_ctx* ctx, void* dst, size_t elem, int64_t rs, int64_t cs, int32_t W,
+                         const std::vector<int32_t>& idx, const void* src) {
+  const int64_t m = (int64_t)idx.size();
+  if (m == 0 || W == 0) return KS_OK;
+  const size_t need = align16((size_t)m * 4) + (size_t)m * W * elem;
+  if (ctx->dscratch_bytes < need) {
+    dev_free(ctx->dscratch);
+    ctx->dscratch_bytes = 0;
+    if (dev_alloc(ctx, &ctx->dscratch, need) != KS_OK) return KS_ENOMEM;
+    ctx->dscratch_bytes = need;
+  }
+  char* b = (char*)ctx->dscratch;
+  HIPCHK(ctx, hipMemcpyAsync(b, idx.data(), (size_t)m * 4, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(b + align16((size_t)m * 4), src, (size_t)m * W * elem, hipMemcpyHostToDevice, ctx->stream));
+  const unsigned blocks = (unsigned)((m * W + 255) / 256);
+  if (elem == 8)
+    hipLaunchKernelGGL(scatter_words_kernel<int64_t>, dim3(blocks), dim3(256), 0, ctx->stream, (int64_t*)dst, rs, cs, W,
+                       (const int32_t*)b, (const int64_t*)(b + align16((size_t)m * 4)), m);
+  else
+    hipLaunchKernelGGL(scatter_words_kernel<int32_t>, dim3(blocks), dim3(256), 0, ctx->stream, (int32_t*)dst, rs, cs, W,
+                       (const int32_t*)b, (const int32_t*)(b + align16((size_t)m * 4)), m);
+  HIPCHK(ctx, hipGetLastError());
+  // the scratch is reused by the next call: let this one finish reading it
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+static int check_idx(ks_ctx* ctx, const int32_t* idx, int64_t m, int64_t lim, const char* what, std::vector<int32_t>& out) {
+  out.assign(idx, idx + m);
+  std::vector<int32_t> sorted(out);
+  std::sort(sorted.begin(), sorted.end());
+  for (int64_t i = 0; i < m; ++i) {
+    if (sorted[i] < 0 || sorted[i] >= lim) KS_FAIL(ctx, KS_EINVAL, "%s: index %d out of range", what, sorted[i]);
+    if (i && sorted[i] == sorted[i - 1]) KS_FAIL(ctx, KS_EINVAL, "%s: index %d repeated", what, sorted[i]);
+  }
+  return KS_OK;
+}
+
+// deviceshare nodeDeviceCache.updateNodeDevice (device_cache.go:489-527): the device rows of m nodes
+int ks_update_devices(ks_ctx* ctx, const int32_t* idx, const ks_device_cols* rows, int64_t m) {
+  if (!ctx || !rows || m < 0 || (m > 0 && !idx)) return ctx ? (ctx->err = "ks_update_devices: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->dev_blob || !ctx->cfg.deviceshare.enable) KS_FAIL(ctx, KS_ESTATE, "ks_update_devices without a device table");
+  std::vector<int32_t> ix;
+  if (int rc = check_idx(ctx, idx, m, ctx->n, "ks_update_devices", ix); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  std::vector<uint32_t> flags((size_t)m, 0);
+  std::vector<int64_t> total((size_t)kDevTW * m, 0), used((size_t)kDevQW * m, 0);
+  std::vector<uint16_t> ids((size_t)m, 0);
+  if (int rc = dev_encode(ctx, rows, m, (size_t)m, flags.data(), total.data(), used.data(), ids.data()); rc != KS_OK) return rc;
+  const int64_t np = ctx->npad;
+  if (scatter_words(ctx, (void*)ctx->dv.flags, 4, 1, np, 1, ix, flags.data()) != KS_OK ||
+      scatter_words(ctx, (void*)ctx->dv.total, 8, 1, np, kDevTW, ix, total.data()) != KS_OK ||
+      scatter_words(ctx, (void*)ctx->dv.used, 8, 1, np, kDevQW, ix, used.data()) != KS_OK)
+    return KS_EHIP;
+  for (int64_t i = 0; i < m; ++i) ctx->h_dev_ids[(size_t)ix[i]] = ids[(size_t)i];
+  ctx->dev_loaded = true;
+  return check_dev_numa(ctx);
+}
+
+// nodenumaresource NodeResourceTopology / pod events (topology_eventhandler.go, resource_manager.go Update /
+// Release): the CPU state of m nodes, against the loaded topology table
+int ks_update_cpu_state(ks_ctx* ctx, const int32_t* idx, const ks_cpu_state_cols* rows, int64_t m) {
+  if (!ctx || !rows || m < 0 || (m > 0 && (!idx || !rows->topology || !rows->allocated)))
+    return ctx ? (ctx->err = "ks_update_cpu_state: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->cpu_loaded) KS_FAIL(ctx, KS_ESTATE, "ks_update_cpu_state before ks_load_cpu_state");
+  std::vector<int32_t> ix;
+  if (int rc = check_idx(ctx, idx, m, ctx->n, "ks_update_cpu_state", ix); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int32_t ntopo = (int32_t)ctx->cpu_cpc.size();
+  std::vector<int32_t> tid((size_t)m), freec((size_t)m), ncpu((size_t)m);
+  std::vector<CpuSet> sets((size_t)4 * m);
+  for (int64_t i = 0; i < m; ++i) {
+    if (int rc = cpu_encode_row(ctx, rows, i, ix[(size_t)i], ntopo, ctx->h_topos, tid[(size_t)i], sets[(size_t)i],
+                                sets[(size_t)m + i], sets[(size_t)2 * m + i], sets[(size_t)3 * m + i], freec[(size_t)i],
+                                ncpu[(size_t)i]);
+        rc != KS_OK)
+      return rc;
+    const int32_t k = (size_t)ix[(size_t)i] < ctx->h_numa_k.size() ? ctx->h_numa_k[(size_t)ix[(size_t)i]] : 0;
+    const int32_t nn = tid[(size_t)i] >= 0 ? (ctx->h_topo_dense[(size_t)tid[(size_t)i]] ? ctx->h_topos[(size_t)tid[(size_t)i]].nnodes : -1) : 0;
+    if (k > 0 && nn != 0 && (nn < 0 || nn > k))
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "node %d: NUMA-policy node whose CPU topology NUMA ids are not 0..m-1 with m <= %d", ix[(size_t)i], k);
+    ctx->h_cpu_nn[(size_t)ix[(size_t)i]] = (int8_t)nn;
+  }
+  // CpuSet rows: 4 tables of [npad] CpuSet, kCpuW u64 words each, row-major
+  std::vector<int64_t> words((size_t)kCpuW * m);
+  CpuSet* tables[4] = {ctx->cpu.allocated, ctx->cpu.excl_pcpu, ctx->cpu.excl_numa, const_cast<CpuSet*>(ctx->cpu.reserved)};
+  for (int q = 0; q < 4; ++q) {
+    for (int64_t i = 0; i < m; ++i)
+      for (int w = 0; w < kCpuW; ++w) words[(size_t)w * m + i] = (int64_t)sets[(size_t)q * m + i].w[w];
+    if (scatter_words(ctx, tables[q], 8, kCpuW, 1, kCpuW, ix, words.data()) != KS_OK) return KS_EHIP;
+  }
+  if (scatter_words(ctx, (void*)ctx->cpu.topo_id, 4, 1, 0, 1, ix, tid.data()) != KS_OK ||
+      scatter_words(ctx, ctx->d.cpu_free, 4, 1, 0, 1, ix, freec.data()) != KS_OK ||
+      scatter_words(ctx, ctx->d.numa_cpus, 4, 1, 0, 1, ix, ncpu.data()) != KS_OK)
+    return KS_EHIP;
+  if (upload_prep_nodes(ctx) != KS_OK || numa_refresh_free(ctx) != KS_OK) return KS_EHIP;  // cpuset millicores, offsets
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+// elasticquota GroupQuotaManager.OnQuotaUpdate / OnPodAdd-Update-Delete (group_quota_manager.go:736-870): the
+// limit / min / used / non-preemptible used / masks of m quotas (the tree, i.e. the parents, is fixed: a parent
+// change is a ks_load_quotas)
+int ks_update_quotas(ks_ctx* ctx, const int32_t* idx, const ks_quota_cols* rows, int32_t m) {
+  if (!ctx || !rows || m < 0 || (m > 0 && !idx)) return ctx ? (ctx->err = "ks_update_quotas: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->quota_blob) KS_FAIL(ctx, KS_ESTATE, "ks_update_quotas before ks_load_quotas");
+  std::vector<int32_t> ix;
+  if (int rc = check_idx(ctx, idx, m, ctx->q.q, "ks_update_quotas", ix); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  std::vector<int32_t> lm((size_t)m), mm((size_t)m);
+  std::vector<int64_t> t[4];
+  for (auto& v : t) v.assign((size_t)KS_QUOTA_DIMS * m, 0);
+  const int64_t* const* src[4] = {rows->limit, rows->used, rows->min, rows->nonpreemptible_used};
+  for (int32_t i = 0; i < m; ++i) {
+    lm[(size_t)i] = (int32_t)(rows->limit_mask ? rows->limit_mask[i] : 0);
+    mm[(size_t)i] = (int32_t)(rows->min_mask ? rows->min_mask[i] : 0);
+    for (int q = 0; q < 4; ++q)
+      for (int d = 0; d < KS_QUOTA_DIMS; ++d) t[q][(size_t)d * m + i] = src[q][d] ? src[q][d][i] : 0;
+  }
+  int64_t* dst[4] = {ctx->q.limit, ctx->q.used, ctx->q.min, ctx->q.npused};
+  if (scatter_words(ctx, ctx->q.limit_mask, 4, 1, 0, 1, ix, lm.data()) != KS_OK ||
+      scatter_words(ctx, ctx->q.min_mask, 4, 1, 0, 1, ix, mm.data()) != KS_OK)
+    return KS_EHIP;
+  for (int q = 0; q < 4; ++q)
+    if (scatter_words(ctx, dst[q], 8, KS_QUOTA_DIMS, 1, KS_QUOTA_DIMS, ix, t[q].data()) != KS_OK) return KS_EHIP;
+  return KS_OK;
+}
+
+// reservation cache updates of reservations already loaded (reservation/cache.go:104-216 updateReservation:
+// Allocated and the assigned pods change as pods bind / terminate): allocated [kRsvDims][m] and assigned [m] of
+// m caller rows; the nodes' reservation base restore follows.  A reservation added or removed is a
+// ks_load_reservations.
+int ks_update_reservation_usage(ks_ctx* ctx, const int32_t* rows, const int64_t* const* allocated, const int32_t* assigned,
+                                int32_t m) {
+  if (!ctx || m < 0 || (m > 0 && (!rows || !allocated || !assigned)))
+    return ctx ? (ctx->err = "ks_update_reservation_usage: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->rsv_blob) KS_FAIL(ctx, KS_ESTATE, "ks_update_reservation_usage before ks_load_reservations");
+  std::vector<int32_t> ix;
+  if (int rc = check_idx(ctx, rows, m, (int64_t)ctx->h_rsv_gi.size(), "ks_update_reservation_usage", ix); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  std::vector<int32_t> gi((size_t)m), nodes;
+  for (int32_t i = 0; i < m; ++i) {
+    gi[(size_t)i] = ctx->h_rsv_gi[(size_t)ix[(size_t)i]];
+    nodes.push_back(ctx->h_rsv_node[(size_t)gi[(size_t)i]]);
+    for (int d = 0; d < kRsvDims; ++d)
+      if (allocated[d] && (allocated[d][i] < 0 || allocated[d][i] >= ((int64_t)1 << 56)))
+        KS_FAIL(ctx, KS_EINVAL, "reservation row %d: allocated out of range", ix[(size_t)i]);
+    if (assigned[i] < 0) KS_FAIL(ctx, KS_EINVAL, "reservation row %d: assigned < 0", ix[(size_t)i]);
+  }
+  std::sort(nodes.begin(), nodes.end());
+  nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+  std::vector<int64_t> al((size_t)kRsvDims * m, 0);
+  for (int d = 0; d < kRsvDims; ++d)
+    for (int32_t i = 0; i < m; ++i) al[(size_t)d * m + i] = allocated[d] ? allocated[d][i] : 0;
+  // the affected nodes' base restore out, the usage in, the restore (and the nodes' owner classes) back
+  int32_t* dn = nullptr;
+  {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, nodes.size() * 4 + 16) != KS_OK) return KS_ENOMEM;
+    dn = (int32_t*)p;
+  }
+  auto done = [&](int rc) {
+    void* p = dn;
+    (void)hipStreamSynchronize(ctx->stream);
+    dev_free(p);
+    return rc;
+  };
+  HIPCHK(ctx, hipMemcpyAsync(dn, nodes.data(), nodes.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  if (ctx->rsv_based && rsv_launch_base(ctx, dn, (int64_t)nodes.size(), -1, 0) != KS_OK) return done(KS_EHIP);
+  if (scatter_words(ctx, ctx->rv.allocd, 8, 1, ctx->rv.nr, kRsvDims, gi, al.data()) != KS_OK ||
+      scatter_words(ctx, ctx->rv.assigned, 4, 1, 0, 1, gi, assigned) != KS_OK)
+    return done(KS_EHIP);
+  if (ctx->rsv_based && rsv_launch_base(ctx, dn, (int64_t)nodes.size(), +1, 1) != KS_OK) return done(KS_EHIP);
+  return done(KS_OK);
 }
 
 int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t* scores, int64_t* total) {

@@ -81,6 +81,10 @@ def lib() -> C.CDLL:
     L.ks_assume.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult), abi.PU64, abi.P64]
     L.ks_unreserve.argtypes = [vp, C.POINTER(abi.KsPodCols), C.POINTER(abi.KsResult), abi.PU64, abi.P64]
     L.ks_fetch_numa_alloc.argtypes = [vp, abi.P64, C.c_int32]
+    L.ks_update_devices.argtypes = [vp, abi.P32, C.POINTER(abi.KsDeviceCols), C.c_int64]
+    L.ks_update_cpu_state.argtypes = [vp, abi.P32, C.POINTER(abi.KsCpuStateCols), C.c_int64]
+    L.ks_update_quotas.argtypes = [vp, abi.P32, C.POINTER(abi.KsQuotaCols), C.c_int32]
+    L.ks_update_reservation_usage.argtypes = [vp, abi.P32, C.POINTER(abi.P64), abi.P32, C.c_int32]
     L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
     L.ks_read_quota_used.argtypes = [vp, abi.P64]
     L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
@@ -306,6 +310,33 @@ class Evaluator:
         self._chk(self.L.ks_unreserve(self.h, C.byref(cols), r.ctypes.data_as(C.POINTER(abi.KsResult)),
                                       cs.ctypes.data_as(abi.PU64) if cs is not None else None,
                                       na.ctypes.data_as(abi.P64) if na is not None else None))
+
+    def update_devices(self, idx, rows: DeviceTable):
+        """informer delta: node idx[i]'s devices from row i of rows"""
+        idx = np.ascontiguousarray(idx, np.int32)
+        cols = rows.ks()
+        self._chk(self.L.ks_update_devices(self.h, idx.ctypes.data_as(abi.P32), C.byref(cols), rows.n))
+
+    def update_cpu_state(self, idx, rows: CpuState):
+        """informer delta: node idx[i]'s CPU state from row i (topology indices into the loaded table)"""
+        idx = np.ascontiguousarray(idx, np.int32)
+        cols = rows.ks()
+        self._chk(self.L.ks_update_cpu_state(self.h, idx.ctypes.data_as(abi.P32), C.byref(cols), rows.n))
+
+    def update_quotas(self, idx, rows: QuotaTable):
+        """informer delta: quota idx[i]'s limits / usage from row i"""
+        idx = np.ascontiguousarray(idx, np.int32)
+        cols = rows.ks()
+        self._chk(self.L.ks_update_quotas(self.h, idx.ctypes.data_as(abi.P32), C.byref(cols), rows.q))
+
+    def update_reservation_usage(self, rows, allocated, assigned):
+        """informer delta: allocated [KS_RSV_DIMS][m] and assigned [m] of reservation rows `rows`"""
+        rows = np.ascontiguousarray(rows, np.int32)
+        allocated = np.ascontiguousarray(allocated, np.int64)
+        assigned = np.ascontiguousarray(assigned, np.int32)
+        ptrs = (abi.P64 * abi.KS_RSV_DIMS)(*[allocated[d].ctypes.data_as(abi.P64) for d in range(abi.KS_RSV_DIMS)])
+        self._chk(self.L.ks_update_reservation_usage(self.h, rows.ctypes.data_as(abi.P32), ptrs,
+                                                     assigned.ctypes.data_as(abi.P32), len(rows)))
 
     def fetch_numa_alloc(self, p: int) -> np.ndarray:
         out = np.zeros((max(p, 1), abi.KS_MAX_NUMA, 2), np.int64)

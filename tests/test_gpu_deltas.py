@@ -1,0 +1,116 @@
+"""GPU: the informer-delta entry points (ks_update_devices / _cpu_state / _quotas / _reservation_usage) leave
+the context exactly as a full reload of the changed tables would -- same placements, scores, minors, CPUs and
+state after scheduling a queue -- on C3 (devices, CPU state, SingleNUMANode nodes), C2 (quotas) and C4
+(reservation usage)."""
+import numpy as np
+import pytest
+
+from assume_util import assert_states_equal, state
+from koordinator_amd import abi, synth
+from koordinator_amd.cluster import CpuState, DeviceTable, QuotaTable
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def runtime():
+    from koordinator_amd import runtime as rt
+
+    rt.lib()
+    return rt
+
+
+def dev_rows(t: DeviceTable, idx) -> DeviceTable:
+    r = DeviceTable(len(idx))
+    r.flags = t.flags[idx].copy()
+    for k in vars(t):
+        v = getattr(t, k)
+        if isinstance(v, np.ndarray) and v.ndim == 2:
+            setattr(r, k, v[:, idx].copy())
+    return r
+
+
+def cpu_rows(t: CpuState, idx) -> CpuState:
+    r = CpuState(len(idx), t.topologies)
+    for k in ("topology", "allocated", "excl_pcpu", "excl_numa", "reserved"):
+        setattr(r, k, getattr(t, k)[idx].copy())
+    return r
+
+
+def quota_rows(t: QuotaTable, idx) -> QuotaTable:
+    r = QuotaTable(len(idx))
+    for k in ("parent", "limit_mask", "min_mask"):
+        setattr(r, k, getattr(t, k)[idx].copy())
+    for k in ("limit", "used", "min", "nonpreemptible_used"):
+        setattr(r, k, getattr(t, k)[:, idx].copy())
+    return r
+
+
+def check_same(runtime, a, b, w, label):
+    ra, rb = a.schedule(w.pods), b.schedule(w.pods)
+    for k in ("node", "status", "score", "reservation", "gpu_minors", "rdma_minors"):
+        assert np.array_equal(ra[k], rb[k]), f"{label}: {k}"
+    if w.cpus is not None:
+        assert np.array_equal(a.fetch_cpusets(w.pods.n), b.fetch_cpusets(w.pods.n)), label
+    assert_states_equal(state(a, w), state(b, w), label)
+
+
+def test_update_devices_and_cpu_state(runtime):
+    w = synth.c3(seed=91, n_nodes=400, n_pods=500)
+    w2 = synth.c3(seed=91, n_nodes=400, n_pods=500)  # same nodes; devices / CPU state re-drawn below
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(400, 60, replace=False)).astype(np.int32)
+    # new device usage and CPU allocations for the chosen nodes (a later snapshot of the same machines)
+    dv = w.devices.copy()
+    for k in range(abi.KS_MAX_GPUS):
+        dv.used_core[k, idx] = np.where(dv.total_core[k, idx] > 0, rng.choice([0, 25, 50, 100], idx.size), 0)
+        dv.used_ratio[k, idx] = dv.used_core[k, idx]
+        dv.used_memory[k, idx] = dv.used_core[k, idx] * dv.total_memory[k, idx] // 100
+    cs = w.cpus.copy()
+    for i in idx:
+        if cs.topology[i] >= 0:
+            cs.allocated[i] = 0
+            cs.excl_pcpu[i] = 0
+            cs.excl_numa[i] = 0
+    a = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    a.update_devices(idx, dev_rows(dv, idx))
+    a.update_cpu_state(idx, cpu_rows(cs, idx))
+    w2.devices, w2.cpus = dv, cs
+    # the node table's cpuset counts follow the CPU state (numa_cpuset_cpus), as the host would resend them
+    nodes = w.nodes.copy()
+    b = runtime.Evaluator(w.cfg, nodes, **w2.tables())
+    w.devices, w.cpus = dv, cs
+    check_same(runtime, a, b, w, "devices + cpu")
+    a.close()
+    b.close()
+
+
+def test_update_quotas(runtime):
+    w = synth.c2(n_nodes=500, n_pods=800, n_quotas=16)
+    q2 = w.quotas.copy()
+    idx = np.array([1, 4, 7, 11], np.int32)
+    q2.limit[:, idx] = q2.limit[:, idx] // 2
+    q2.used[:, idx] = q2.used[:, idx] + 1000
+    a = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    a.update_quotas(idx, quota_rows(q2, idx))
+    w.quotas = q2
+    b = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    check_same(runtime, a, b, w, "quotas")
+    a.close()
+    b.close()
+
+
+def test_update_reservation_usage(runtime):
+    w = synth.c4(n_nodes=800, n_reservations=2000, n_pods=600)
+    rs2 = w.reservations.copy()
+    rng = np.random.default_rng(9)
+    rows = np.sort(rng.choice(2000, 150, replace=False)).astype(np.int32)
+    rs2.allocated[:, rows] = rs2.allocatable[:, rows] * rng.integers(0, 3, rows.size) // 4
+    rs2.assigned[rows] = rng.integers(0, 3, rows.size)
+    a = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    a.update_reservation_usage(rows, rs2.allocated[:, rows], rs2.assigned[rows])
+    w.reservations = rs2
+    b = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    check_same(runtime, a, b, w, "reservation usage")
+    a.close()
+    b.close()
