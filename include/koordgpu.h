@@ -96,15 +96,15 @@ extern "C" {
 #define KS_POD_RSV_AFFINITY 0x10u    /* GetRequiredReservationAffinity != nil (reservation/transformer.go:51, stateData.hasAffinity) */
 #define KS_POD_CPU_BIND 0x20u        /* NodeNUMAResource preFilterState.requestCPUBind (nodenumaresource/plugin.go:236-262):
                                         a preferred FullPCPUs / SpreadByPCPUs policy of an LSE/LSR prod pod with a whole-CPU
-                                        request; policy and exclusive policy in ks_pod_cols.cpu_bind.  A required bind
-                                        policy (resourceSpec.requiredCPUBindPolicy) is not supported (KS_EUNSUPPORTED) */
+                                        request; policy and exclusive policy in ks_pod_cols.cpu_bind, KS_CPU_BIND_REQUIRED
+                                        when the policy is resourceSpec.requiredCPUBindPolicy */
 #define KS_POD_GPU_CORE 0x40u        /* DeviceShare: the converted GPU request has a gpu-core key (deviceshare/utils.go:96-146) */
 #define KS_POD_GPU_MEMORY 0x80u      /* DeviceShare: gpu-memory given (ratio derived per node, devicehandler_gpu.go:71-89);
                                         otherwise gpu-memory-ratio given (memory derived) */
 
 /* ---- per-node NodeNUMAResource flags (ks_node_cols.numa_flags) ---- */
 #define KS_NUMA_INVALID_RATIO 0x1u   /* GetNodeResourceAmplificationRatio returned an error (plugin.go:348-351)   */
-#define KS_NUMA_CPU_BIND_POLICY 0x2u /* node CPU bind policy label != None (GetNodeCPUBindPolicy): unsupported   */
+#define KS_NUMA_CPU_BIND_POLICY 0x2u /* a node CPU bind policy the caller cannot encode in bits 7-8: unsupported    */
 #define KS_NUMA_TOPOLOGY_POLICY 0x4u /* NUMA topology policy != None (getNUMATopologyPolicy): unsupported         */
 #define KS_NUMA_ALLOC_LEAST 0x8u     /* label numa-allocate-strategy = LeastAllocated (GetNUMAAllocateStrategy, util.go:30-36) */
 #define KS_NUMA_ALLOC_MOST 0x10u     /* label numa-allocate-strategy = MostAllocated                                */
@@ -113,11 +113,20 @@ extern "C" {
 #define KS_NUMA_POLICY_BEST_EFFORT 1u
 #define KS_NUMA_POLICY_RESTRICTED 2u
 #define KS_NUMA_POLICY_SINGLE_NUMA_NODE 3u
+#define KS_NUMA_CPU_BIND_SHIFT 7     /* bits 7-8: node CPU bind policy, extension.GetNodeCPUBindPolicy (apis/extension/
+                                        numa_aware.go:314-325: the node-cpu-bind-policy label, or a static kubelet CPU
+                                        manager with full-pcpus-only = FullPCPUsOnly).  Not combined with a NUMA policy. */
+#define KS_NODE_CPU_BIND_NONE 0u
+#define KS_NODE_CPU_BIND_FULL_PCPUS_ONLY 1u
+#define KS_NODE_CPU_BIND_SPREAD_BY_PCPUS 2u
 
 /* ---- pod cpuset request (ks_pod_cols.cpu_bind, with KS_POD_CPU_BIND) ---- */
 #define KS_CPU_BIND_FULL_PCPUS 1u       /* schedulingconfig.CPUBindPolicyFullPCPUs     */
 #define KS_CPU_BIND_SPREAD_BY_PCPUS 2u  /* schedulingconfig.CPUBindPolicySpreadByPCPUs */
 #define KS_CPU_BIND_POLICY_MASK 0x3u
+#define KS_CPU_BIND_REQUIRED 0x10u      /* the policy is required (resourceSpec.requiredCPUBindPolicy, PreFilter
+                                           plugin.go:245-250): Filter checks it on every node (plugin.go:303-327) and
+                                           allocateCPUSet keeps only CPUs that satisfy it (resource_manager.go:322-330) */
 #define KS_CPU_EXCL_SHIFT 2             /* bits 2-3: preferredCPUExclusivePolicy */
 #define KS_CPU_EXCL_NONE 0u
 #define KS_CPU_EXCL_PCPU_LEVEL 1u
@@ -148,7 +157,15 @@ extern "C" {
 #define KS_R_DEV_JOINT 0x100000u       /* DeviceShare joint allocation: "node(s) Joint-Allocate rules not met" or
                                           "Device Joint-Allocate rules violation" (device_allocator.go:252,280) */
 #define KS_R_NUMA_CPUSET 0x200000u     /* NUMA Allocate of a cpu-bind pod on a NUMA-policy node: "not enough cpus available
-                                          to satisfy request" (allocateCPUSet, resource_manager.go:333-335,366-368) */
+                                          to satisfy request" (allocateCPUSet, resource_manager.go:333-335,366-368); on a
+                                          node without NUMA policy the trial Allocate of a required CPU bind policy
+                                          (plugin.go:318-327) */
+#define KS_R_NUMA_INVALID_CPUS 0x400000u  /* ErrInvalidRequestedCPUs: a node CPU bind policy and a request that is not
+                                             whole CPUs (requestCPUBind, util.go:105-122) */
+#define KS_R_NUMA_BIND_CONFLICT 0x800000u /* ErrCPUBindPolicyConflict: the pod's required policy differs from the
+                                             node's (plugin.go:310-312) */
+#define KS_R_NUMA_SMT 0x1000000u          /* ErrSMTAlignmentError: required FullPCPUs and numCPUsNeeded not a multiple
+                                             of the node's CPUsPerCore (plugin.go:314-317) */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u

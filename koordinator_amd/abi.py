@@ -63,10 +63,15 @@ KS_NUMA_POLICY_NONE = 0
 KS_NUMA_POLICY_BEST_EFFORT = 1
 KS_NUMA_POLICY_RESTRICTED = 2
 KS_NUMA_POLICY_SINGLE_NUMA_NODE = 3
+KS_NUMA_CPU_BIND_SHIFT = 7
+KS_NODE_CPU_BIND_NONE = 0
+KS_NODE_CPU_BIND_FULL_PCPUS_ONLY = 1
+KS_NODE_CPU_BIND_SPREAD_BY_PCPUS = 2
 
 KS_CPU_BIND_FULL_PCPUS = 1
 KS_CPU_BIND_SPREAD_BY_PCPUS = 2
 KS_CPU_BIND_POLICY_MASK = 0x3
+KS_CPU_BIND_REQUIRED = 0x10
 KS_CPU_EXCL_SHIFT = 2
 KS_CPU_EXCL_NONE = 0
 KS_CPU_EXCL_PCPU_LEVEL = 1
@@ -93,6 +98,10 @@ KS_R_NUMA_INVALID_TOPOLOGY = 0x8000
 KS_R_NUMA_AFFINITY = 0x10000
 KS_R_NUMA_INSUFFICIENT = 0x20000
 KS_R_NUMA_MISSING = 0x40000
+KS_R_NUMA_CPUSET = 0x200000
+KS_R_NUMA_INVALID_CPUS = 0x400000
+KS_R_NUMA_BIND_CONFLICT = 0x800000
+KS_R_NUMA_SMT = 0x1000000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1

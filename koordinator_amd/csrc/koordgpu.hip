@@ -180,7 +180,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   r.joint = s.joint ? s.joint[i] : 0u;
   r._pad0 = 0;
   if (r.rdma > 0) r.flags |= kPodHasGpu;
-  r.cpu_bind = (r.flags & KS_POD_CPU_BIND) ? ((s.cpu_bind[i] & 0xFu) | ((uint32_t)(r.cpu / 1000) << 8)) : 0u;
+  r.cpu_bind = (r.flags & KS_POD_CPU_BIND) ? ((s.cpu_bind[i] & 0x1Fu) | ((uint32_t)(r.cpu / 1000) << 8)) : 0u;
   out[i] = r;
 }
 
@@ -652,11 +652,13 @@ constexpr int kCpusetStage = 1024;
 
 __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* list, const int32_t* count_p,
                                                      const uint32_t* split, const PodRec* pods, CpuSet* out,
-                                                     const uint32_t* numa_flags, int32_t default_most, int64_t n) {
+                                                     const uint32_t* numa_flags, uint32_t* cores, int32_t default_most,
+                                                     int64_t n) {
   __shared__ int2 stage[kCpusetStage];
   const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t count = *count_p;
   uint64_t keys[KS_MAX_CPUS];
+  bool any = false;
   for (int32_t base = 0; base < count; base += kCpusetStage) {
     const int32_t m = min(kCpusetStage, count - base);
     for (int32_t i = threadIdx.x; i < m; i += blockDim.x) stage[i] = list[base + i];
@@ -667,10 +669,17 @@ __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* lis
       const int32_t tid = cpu.topo_id[node];
       if (tid < 0) continue;  // unreachable: the Filter rejects nodes without a topology
       const CpuTopo& t = cpu.topo[tid];
-      const uint32_t cb = pods[pod].cpu_bind;
-      const uint32_t nf = numa_flags[node];
+      const uint32_t nf = numa_flags[node], label = (nf >> KS_NUMA_CPU_BIND_SHIFT) & 3u;
+      // getCPUBindPolicy (util.go:85-103): the pod's required policy, else the node's (required), else the pod's
+      // preferred one; a pod that is cpu-bind only through the node's policy has no exclusive policy
+      uint32_t cb = pods[pod].cpu_bind;
+      if (cb == 0) cb = label | KS_CPU_BIND_REQUIRED | ((uint32_t)(pods[pod].cpu / 1000) << 8);
+      else if (label && !(cb & KS_CPU_BIND_REQUIRED)) cb = (cb & ~KS_CPU_BIND_POLICY_MASK) | label | KS_CPU_BIND_REQUIRED;
+      const int pol = (int)(cb & KS_CPU_BIND_POLICY_MASK);
+      any = true;
       const CpuSet alloc = cpu.allocated[node], xp = cpu.excl_pcpu[node], xn = cpu.excl_numa[node];
-      const CpuSet avail = cs_andnot(cs_andnot(t.all, alloc), cpu.reserved[node]);
+      CpuSet avail = cs_andnot(cs_andnot(t.all, alloc), cpu.reserved[node]);
+      if (cb & KS_CPU_BIND_REQUIRED) avail = filter_required(t, avail, pol);  // (resource_manager.go:322-330)
       CpuSet exc_cores = cs_zero();
       uint64_t exc_nodes = 0;
       for (int w = 0; w < kCpuW; ++w) {
@@ -695,7 +704,7 @@ __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* lis
         a.excl = excl;
         a.most = most;
         a.needed = need;
-        if (take_cpus(a, (int)(cb & KS_CPU_BIND_POLICY_MASK), keys)) res = cs_or(res, a.res);  // (count checked)
+        if (take_cpus(a, pol, keys)) res = cs_or(res, a.res);  // (count checked)
       }
       cpu.allocated[node] = cs_or(alloc, res);
       if (excl == KS_CPU_EXCL_PCPU_LEVEL) cpu.excl_pcpu[node] = cs_or(xp, res);
@@ -704,6 +713,28 @@ __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* lis
     }
     __syncthreads();
   }
+  if (any && node < n) {
+    const CpuTopo& t = cpu.topo[cpu.topo_id[node]];
+    cores[node] = cores_word(t, cs_andnot(cs_andnot(t.all, cpu.allocated[node]), cpu.reserved[node]),
+                             (numa_flags[node] >> KS_NUMA_CPU_BIND_SHIFT) & 3u);
+  }
+}
+
+// CoresWord of every node (idx = NULL) or of idx[0..count): the node's CPU bind label, and its core counts when the
+// CPU state is loaded and the node has a topology.
+__global__ void cores_kernel(DevCpu cpu, int32_t loaded, const uint32_t* numa_flags, uint32_t* cores, const int32_t* idx,
+                             int64_t count) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  const int64_t i = idx ? idx[t] : t;
+  const uint32_t label = (numa_flags[i] >> KS_NUMA_CPU_BIND_SHIFT) & 3u;
+  const int32_t tid = loaded ? cpu.topo_id[i] : -1;
+  if (tid < 0) {
+    cores[i] = label << kCoresLabelShift;
+    return;
+  }
+  const CpuTopo& tp = cpu.topo[tid];
+  cores[i] = cores_word(tp, cs_andnot(cs_andnot(tp.all, cpu.allocated[i]), cpu.reserved[i]), label);
 }
 
 // CPUs of each NUMA node available to cpuset pods (topology CPUs of the node - allocated - reserved), for the NUMA
@@ -876,6 +907,8 @@ struct ks_ctx {
   DevNuma* dnv = nullptr;    // device copy (always allocated: kernels take its address)
   char* numa_ckpt = nullptr;       // checkpoint copy of the mutable NUMA block (numa_mut_bytes)
   int64_t numa_policy_nodes = 0;  // nodes with a NUMA topology policy
+  bool cpu_bind_labels = false;   // a node CPU bind policy was loaded (sticky)
+  bool cpu_bind_required = false; // a pod with a required CPU bind policy was staged (sticky)
   std::vector<int8_t> h_numa_k;    // per node: NUMA node count of a policy node (0 = no policy / none)
   std::vector<uint16_t> h_dev_ids; // per node: NUMA ids of the device topology (DeviceShare hints)
   std::vector<int8_t> h_cpu_nn;    // per node: NUMA nodes of its CPU topology (0 = none, -1 = ids not 0..n-1)
@@ -1141,6 +1174,7 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.pod_count, 4, true);
   add(&d.numa_cpus, 4, true);
   add(&d.cpu_free, 4, true);
+  add(&d.cpu_cores, 4, true);
   // read-only columns
   add(&d.alloc_cpu, 8, false);
   add(&d.alloc_mem, 8, false);
@@ -1184,6 +1218,7 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->pod_count);
   v.push_back(c->numa_cpuset_cpus);
   v.push_back(nullptr);  // cpu_free: ks_load_cpu_state (-1 = no CPU topology)
+  v.push_back(nullptr);  // cpu_cores: cores_refresh
   v.push_back(c->alloc_milli_cpu);
   v.push_back(c->alloc_memory);
   v.push_back(c->alloc_ephemeral);
@@ -1232,8 +1267,16 @@ static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
   }
   if (ctx->cfg.numa.enable) {
     for (int64_t i = 0; c->numa_flags && i < n; ++i)
-      if (c->numa_flags[i] & (KS_NUMA_CPU_BIND_POLICY | KS_NUMA_TOPOLOGY_POLICY))
-        KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: NodeNUMAResource CPU-bind / NUMA topology policies are not supported", (long long)i);
+    {
+      const uint32_t f = c->numa_flags[i], label = (f >> KS_NUMA_CPU_BIND_SHIFT) & 3u;
+      if (f & (KS_NUMA_CPU_BIND_POLICY | KS_NUMA_TOPOLOGY_POLICY))
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: numa_flags 0x%x: encode the CPU bind / NUMA topology policy in its bits", (long long)i, f);
+      if (label == 3u || (f >> (KS_NUMA_CPU_BIND_SHIFT + 2)))
+        KS_FAIL(ctx, KS_EINVAL, "node %lld: numa_flags 0x%x invalid", (long long)i, f);
+      // the required policy on a NUMA-policy node runs through FilterByNUMANode's per-NUMA allocation: not modelled
+      if (label && ((f >> KS_NUMA_POLICY_SHIFT) & 3u))
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: a node CPU bind policy together with a NUMA topology policy is not supported", (long long)i);
+    }
     for (int64_t i = 0; c->numa_cpuset_cpus && i < n; ++i)
       if (c->numa_cpuset_cpus[i] < 0 || c->numa_cpuset_cpus[i] > (1 << 20))
         KS_FAIL(ctx, KS_EINVAL, "node %lld: numa_cpuset_cpus out of range", (long long)i);
@@ -1307,6 +1350,23 @@ static int upload_prep_nodes(ks_ctx* ctx) {
   return KS_OK;
 }
 
+// CoresWord of every node (ks_device.h) after a load or delta of the node rows or the CPU state; the schedule
+// passes keep it current themselves (cpuset_kernel), as does ks_unreserve.
+static int cores_refresh(ks_ctx* ctx) {
+  if (!ctx->cfg.numa.enable || ctx->n == 0) return KS_OK;
+  hipLaunchKernelGGL(cores_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
+                     (int32_t)ctx->cpu_loaded, (const uint32_t*)ctx->d.numa_flags, ctx->d.cpu_cores, (const int32_t*)nullptr,
+                     ctx->n);
+  HIPCHK(ctx, hipGetLastError());
+  return KS_OK;
+}
+
+// Cfg.cores: the per-node core counts take part in the Filter once a node CPU bind policy or a required pod policy
+// has been seen; the passes then choose CPU ids after every commit (cpuset_kernel) so that the counts stay exact.
+static void cores_mode(ks_ctx* ctx) {
+  ctx->kc.cores = (ctx->cfg.numa.enable && (ctx->cpu_bind_labels || ctx->cpu_bind_required)) ? 1 : 0;
+}
+
 static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
 static int dev_install(ks_ctx* ctx, const ks_device_cols* dc);
 static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h);
@@ -1365,8 +1425,13 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (ctx->cfg.deviceshare.enable && dev_install(ctx, nullptr) != KS_OK) return KS_EHIP;
   // NUMA topology policies: an empty NUMA-node table until ks_load_numa_nodes
   ctx->numa_policy_nodes = 0;
-  for (int64_t i = 0; ctx->cfg.numa.enable && nodes->numa_flags && i < n; ++i)
+  ctx->cpu_bind_labels = false;
+  for (int64_t i = 0; ctx->cfg.numa.enable && nodes->numa_flags && i < n; ++i) {
     ctx->numa_policy_nodes += ((nodes->numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u) != 0;
+    ctx->cpu_bind_labels |= ((nodes->numa_flags[i] >> KS_NUMA_CPU_BIND_SHIFT) & 3u) != 0;
+  }
+  cores_mode(ctx);
+  if (cores_refresh(ctx) != KS_OK) return KS_EHIP;
   dev_free(ctx->numa_blob);
   if (ctx->numa_policy_nodes > 0) {
     if (ctx->cfg.reservation.enable)
@@ -1815,6 +1880,7 @@ int ks_load_cpu_state(ks_ctx* ctx, const ks_cpu_topology* topos, int32_t ntopo, 
   for (int64_t i = 0; i < n; ++i)
     if (const int32_t ti = tid[(size_t)i]; ti >= 0) ctx->h_cpu_nn[(size_t)i] = dense[(size_t)ti] ? (int8_t)tt[(size_t)ti].nnodes : (int8_t)-1;
   if (int rc = numa_refresh_free(ctx); rc != KS_OK) return rc;
+  if (int rc = cores_refresh(ctx); rc != KS_OK) return rc;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -2076,6 +2142,10 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
   // the replaced rows are the reference's NodeInfo: add the reservation base restore again
   if (ctx->rsv_based && rsv_launch_base(ctx, (const int32_t*)((char*)dbuf + idx_off), m, +1, 0) != KS_OK) return KS_EHIP;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
+  for (int64_t i = 0; ctx->cfg.numa.enable && rows->numa_flags && i < m; ++i)
+    ctx->cpu_bind_labels |= ((rows->numa_flags[i] >> KS_NUMA_CPU_BIND_SHIFT) & 3u) != 0;
+  cores_mode(ctx);
+  if (rows->numa_flags && cores_refresh(ctx) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   (void)hipFree(dbuf);
   return KS_OK;
@@ -2378,18 +2448,25 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
       if (!pc->cpu_bind) KS_FAIL(ctx, KS_EINVAL, "pod %d: KS_POD_CPU_BIND without ks_pod_cols.cpu_bind", i);
       const uint32_t cb = pc->cpu_bind[i], pol = cb & KS_CPU_BIND_POLICY_MASK, ex = (cb >> KS_CPU_EXCL_SHIFT) & 3u;
       const int64_t cpu = pc->req_milli_cpu ? pc->req_milli_cpu[i] : 0;
-      if ((pol != KS_CPU_BIND_FULL_PCPUS && pol != KS_CPU_BIND_SPREAD_BY_PCPUS) || ex > KS_CPU_EXCL_NUMA_NODE_LEVEL || (cb >> 4))
+      if ((pol != KS_CPU_BIND_FULL_PCPUS && pol != KS_CPU_BIND_SPREAD_BY_PCPUS) || ex > KS_CPU_EXCL_NUMA_NODE_LEVEL || (cb >> 5))
         KS_FAIL(ctx, KS_EINVAL, "pod %d: cpu_bind 0x%x invalid", i, cb);
+      const bool req = (cb & KS_CPU_BIND_REQUIRED) != 0;
+      // a required policy on a NUMA-policy node runs through FilterByNUMANode's per-NUMA allocation: not modelled
+      if (req && ctx->numa_policy_nodes > 0)
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: a required CPU bind policy together with NUMA topology policies is not supported", i);
+      ctx->cpu_bind_required |= req;
       if (cpu <= 0 || cpu % 1000 != 0 || cpu / 1000 > KS_MAX_CPUS)
         KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
-      // a FullPCPUs request that is not a whole number of cores fails the Filter's SMT alignment check per node
-      // (plugin.go:300-310); the count-only commit does not carry per-node cores, so such pods are refused
-      if (pol == KS_CPU_BIND_FULL_PCPUS)
+      // a preferred FullPCPUs request that is not a whole number of cores takes split cores in takeCPUs'
+      // fallbacks, which the device accumulator does not model: refused (a required one fails the Filter's SMT
+      // alignment check per node, plugin.go:314-317)
+      if (pol == KS_CPU_BIND_FULL_PCPUS && !req)
         for (int32_t cpc : ctx->cpu_cpc)
           if (cpc > 1 && (cpu / 1000) % cpc != 0)
             KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: FullPCPUs request of %lld CPUs is not a whole number of %d-thread cores", i,
                     (long long)(cpu / 1000), cpc);
     }
+    cores_mode(ctx);
   }
   if (pc->joint) {
     for (int32_t i = 0; i < p; ++i) {
@@ -2708,6 +2785,14 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   rec(2);
   HIPCHK(ctx, pl.commit(qcache, smem, ctx->stream, ca));
   rec(2);
+  if (ctx->kc.cores && ctx->cpu_loaded) {
+    // the pass's CPU ids now, so that the next sweep sees exact per-node core counts (Cfg.cores)
+    hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
+                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
+                       (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
+                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+    HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
+  }
   return KS_OK;
 }
 
@@ -2795,7 +2880,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
                        (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
                        (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
-                       (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
     HIPCHK(ctx, hipGetLastError());
   }
   HIPCHK(ctx, hipEventRecord(t1, ctx->stream));
@@ -3003,7 +3088,8 @@ int ks_update_cpu_state(ks_ctx* ctx, const int32_t* idx, const ks_cpu_state_cols
       scatter_words(ctx, ctx->d.cpu_free, 4, 1, 0, 1, ix, freec.data()) != KS_OK ||
       scatter_words(ctx, ctx->d.numa_cpus, 4, 1, 0, 1, ix, ncpu.data()) != KS_OK)
     return KS_EHIP;
-  if (upload_prep_nodes(ctx) != KS_OK || numa_refresh_free(ctx) != KS_OK) return KS_EHIP;  // cpuset millicores, offsets
+  if (upload_prep_nodes(ctx) != KS_OK || numa_refresh_free(ctx) != KS_OK || cores_refresh(ctx) != KS_OK)
+    return KS_EHIP;  // cpuset millicores, offsets, per-NUMA free CPUs, core counts
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -3219,6 +3305,11 @@ __global__ void unreserve_kernel(UnreserveArgs a) {
       d.numa_off[n] = (a.ratio_amp && ratio > 1.0) ? (int64_t)::ceil((double)A * ratio) - A : 0;
       if (d.cpu_free[n] >= 0) d.cpu_free[n] += cnt;
       const int32_t tid = a.cpu.topo_id[n];
+      if (tid >= 0) {
+        const CpuTopo& tp = a.cpu.topo[tid];
+        d.cpu_cores[n] = cores_word(tp, cs_andnot(cs_andnot(tp.all, a.cpu.allocated[n]), a.cpu.reserved[n]),
+                                    (d.numa_flags[n] >> KS_NUMA_CPU_BIND_SHIFT) & 3u);
+      }
       if (a.numa_pol && tid >= 0 && a.nv.count[n] > 0) {
         const CpuTopo& t = a.cpu.topo[tid];
         for (int k = 0; k < kNumaDev && k < a.nv.count[n]; ++k) {
@@ -3286,7 +3377,7 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
                        (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
                        (const PodRec*)ctx->ast.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
-                       (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
     HIPCHK(ctx, hipGetLastError());
   }
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->ast.results, sizeof(ks_result), hipMemcpyDeviceToHost, ctx->stream));

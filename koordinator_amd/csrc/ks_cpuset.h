@@ -413,4 +413,35 @@ __device__ inline bool take_cpus(CpuAcc& a, int bind, uint64_t* keys) {
   return take_free_cpus(a, false, keys);
 }
 
+// filterCPUsByRequiredCPUBindPolicy (resource_manager.go:595-627): FullPCPUs keeps the cores whose CPUs are all in
+// `avail` (CPUsPerCore of them), SpreadByPCPUs the lowest CPU of `avail` in every core.
+__device__ inline CpuSet filter_required(const CpuTopo& t, const CpuSet& avail, int policy) {
+  CpuSet r = cs_zero();
+  for (int k = 0; k < t.ncores; ++k) {
+    const CpuSet m = cs_and(avail, t.core_mask[k]);
+    const int c = cs_count(m);
+    if (policy == KS_CPU_BIND_FULL_PCPUS) {
+      if (c == t.cpc) r = cs_or(r, m);
+    } else if (c > 0) {
+      for (int w = 0; w < kCpuW; ++w)
+        if (m.w[w]) {
+          r.w[w] |= m.w[w] & (~m.w[w] + 1ull);
+          break;
+        }
+    }
+  }
+  return r;
+}
+
+// CoresWord (ks_device.h) of a node whose available CPUs are `avail`.
+__device__ inline uint32_t cores_word(const CpuTopo& t, const CpuSet& avail, uint32_t label) {
+  uint32_t full = 0, any = 0;
+  for (int k = 0; k < t.ncores; ++k) {
+    const int c = cs_count(cs_and(avail, t.core_mask[k]));
+    full += c == t.cpc ? 1u : 0u;
+    any += c > 0 ? 1u : 0u;
+  }
+  return full | (any << kCoresAnyShift) | ((uint32_t)min(t.cpc, 31) << kCoresCpcShift) | (label << kCoresLabelShift);
+}
+
 }  // namespace ks

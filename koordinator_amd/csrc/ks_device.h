@@ -66,6 +66,7 @@ struct Cfg {
   int32_t numa_sc_most;  // NUMAScoringStrategy MostAllocated (hint scores)
   int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw, dw_rdma;  // DeviceShare (GPU, RDMA)
   int32_t monotone_nd;  // monotone for pods without device requests (DeviceShare skips them: no normalization max)
+  int32_t cores;        // node CPU bind policies or required pod policies: the per-node core counts are read
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -89,7 +90,20 @@ struct DevNodes {
   int64_t *numa_amilli;     // derived: cpuset CPUs x 1000
   int64_t *numa_off;        // derived: Amplify(cpuset milli, ratio) - cpuset milli (ratio > 1), else 0
   int32_t *cpu_free;        // available CPUs for cpuset pods (ks_cpuset.h), -1 = no valid CPU topology
+  uint32_t *cpu_cores;      // derived: CoresWord (fully available / partly available cores, CPUsPerCore, CPU bind label)
 };
+
+// Per-node word of the required CPU bind policies (Cfg.cores): the cores whose CPUs are all available
+// (filterCPUsByRequiredCPUBindPolicy FullPCPUs keeps exactly these), the cores with any available CPU
+// (SpreadByPCPUs keeps one CPU of each), CPUsPerCore, and the node's CPU bind policy (KS_NODE_CPU_BIND_*).
+// Bit 26 is the commit kernel's per-slot "cores changed in this pass" flag.
+constexpr uint32_t kCoresCount = 0x1FFu;
+constexpr int kCoresAnyShift = 9, kCoresCpcShift = 18, kCoresLabelShift = 24;
+constexpr uint32_t kCoresDirty = 1u << 26;
+__device__ __forceinline__ uint32_t cores_full(uint32_t w) { return w & kCoresCount; }
+__device__ __forceinline__ uint32_t cores_any(uint32_t w) { return (w >> kCoresAnyShift) & kCoresCount; }
+__device__ __forceinline__ uint32_t cores_cpc(uint32_t w) { return (w >> kCoresCpcShift) & 31u; }
+__device__ __forceinline__ uint32_t cores_label(uint32_t w) { return (w >> kCoresLabelShift) & 3u; }
 
 // Per-pod record read by the sweep with scalar loads (AoS, 192 B).  The x100 and f32 copies feed
 // the exact score terms (see term_least below).
@@ -251,6 +265,7 @@ struct __attribute__((aligned(16))) NodeReg {
   int64_t numa_A, numa_off;                    // cpuset milli-CPUs, Amplify(A) - A
   double numa_ratio;                           // cpu amplification ratio (amplifies a cpu-bind pod's request)
   int32_t cpu_free;                            // available CPUs for cpuset pods, -1 = no valid CPU topology
+  uint32_t cpu_cores;                          // CoresWord (Cfg.cores), else 0
   uint32_t la_bits;
   int32_t fit_ws;                              // Σ weights of cpu/mem/eph terms with capacity != 0
   int32_t pods_full;
@@ -310,6 +325,7 @@ __device__ __forceinline__ void make_node(const Cfg& c, NodeReg<NSC>& r, int val
   r.numa_off = numa_off;
   r.numa_ratio = numa_ratio;
   r.cpu_free = cpu_free;
+  r.cpu_cores = 0;
   term_set(r.t_ncpu, alloc_cpu, req_cpu + numa_off);
   term_set(r.t_nmem, alloc_mem, req_mem);
 }
@@ -340,6 +356,7 @@ __device__ __forceinline__ void load_node(const Cfg& c, const DevNodes& d, int64
                  gld(d.la_pterm_cpu + n), gld(d.la_pterm_mem + n), gld(d.la_bits + n), gld(d.allowed_pods + n),
                  gld(d.pod_count + n), na, no, nr, cf);
   if (c.rsv && valid) r.rsv_cls = gld(d.rsv_cls + n);
+  if (c.cores) r.cpu_cores = gld(d.cpu_cores + n);
 }
 
 // Reserve: NodeInfo.AddPod (upstream framework/types.go) + podAssignCache.assign
@@ -471,7 +488,14 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
 template <int NSC, bool DEBUG>
 __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const NodeReg<NSC>& r, EvalOut& o) {
   if (p.flags & kPodReqZero) return;  // PreFilter skip
-  const bool bind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
+  bool bind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
+  uint32_t rs = 0;
+  // requestCPUBind (util.go:105-122): a node CPU bind policy makes a whole-CPU pod cpu-bind
+  const uint32_t label = c.cores ? cores_label(r.cpu_cores) : 0u;
+  if (label && !bind && p.cpu > 0) {
+    if (p.cpu % 1000 != 0) rs = KS_R_NUMA_INVALID_CPUS;
+    else bind = true;
+  }
   int64_t pc = p.cpu, pc100 = p.h_cpu;
   float pcf = p.f_cpu;
   if (bind && (r.la_bits & kNumaAmp)) {
@@ -479,8 +503,7 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
     pc100 = pc * 100;
     pcf = i64_to_f32(pc);
   }
-  uint32_t rs = 0;
-  if (p.cpu != 0) {
+  if (rs == 0 && p.cpu != 0) {
     if (r.la_bits & kNumaInvalid) {
       rs = KS_R_NUMA_INVALID_RATIO;
     } else if (r.la_bits & kNumaAmp) {
@@ -490,6 +513,24 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
     }
   }
   if (bind && rs == 0 && r.cpu_free < 0) rs = KS_R_NUMA_INVALID_TOPOLOGY;
+  if (c.cores && bind && rs == 0) {
+    // the Filter's required policy: the node's, else the pod's required one (plugin.go:303-312); FullPCPUs needs
+    // whole cores (:314-317); the trial Allocate keeps the cores the policy allows (resource_manager.go:322-335)
+    const bool preq = (p.flags & KS_POD_CPU_BIND) && (p.cpu_bind & KS_CPU_BIND_REQUIRED);
+    const uint32_t ppol = p.cpu_bind & KS_CPU_BIND_POLICY_MASK;
+    const uint32_t req = label ? label : (preq ? ppol : 0u);
+    if (preq && ppol != req) {
+      rs = KS_R_NUMA_BIND_CONFLICT;
+    } else if (req) {
+      const int32_t need = (int32_t)(p.cpu / 1000), cpc = max((int32_t)cores_cpc(r.cpu_cores), 1);
+      if (req == KS_CPU_BIND_FULL_PCPUS) {
+        if (need % cpc != 0) rs = KS_R_NUMA_SMT;
+        else if ((int32_t)cores_full(r.cpu_cores) * cpc < need) rs = KS_R_NUMA_CPUSET;
+      } else if ((int32_t)cores_any(r.cpu_cores) < need) {
+        rs = KS_R_NUMA_CPUSET;
+      }
+    }
+  }
   o.reasons |= DEBUG ? rs : (rs ? KS_R_FIT_PODS : 0u);
   o.numa_rs = rs;
   Term tc = r.t_ncpu;

@@ -346,6 +346,7 @@ __device__ __forceinline__ void slot_to_reg(const SlotRow& s, NodeReg<NSC>& r) {
   r.pods_full = (int64_t)s.pod_count + 1 > (int64_t)s.allowed;
   r.valid = 1;
   r.rsv_cls = 0;
+  r.cpu_cores = 0;
 }
 
 // Untouched-candidate resolution of one pod (lane k = candidate k), against the current touched masks.
@@ -661,6 +662,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       uint64_t key_mod = 0;
       EvalOut o{};
       bool feas = false;
+      bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
       if (lane < nslots) {
         NodeReg<NSC> r;
         slot_to_reg<NSC>(rows[lane], r);
@@ -669,6 +671,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         r.numa_off = snuma[4 * lane + 1];
         r.numa_ratio = __longlong_as_double(snuma[4 * lane + 2]);
         r.cpu_free = (int32_t)snuma[4 * lane + 3];
+        uint32_t cw = 0;
+        if ((FEAT & 2) && cfg.cores) {
+          // a cpu-bind Reserve on the slot in this pass moved its core counts (the CPU ids come after the pass):
+          // evaluate optimistically and cut the pass if that decides the pod
+          cw = (uint32_t)((uint64_t)snuma[4 * lane + 3] >> 32);
+          r.cpu_cores = (cw & kCoresDirty) ? (cw | kCoresCount | (kCoresCount << kCoresAnyShift)) : cw;
+        }
         o = eval_full<NSC, false, false, FEAT>(
             cfg, pod, r,
             [&](RsvDelta<NSC>& dl) {
@@ -679,6 +688,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
             [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
             [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
         feas = o.reasons == 0;
+        if ((FEAT & 2) && cfg.cores && (cw & kCoresDirty) && feas)
+          unk = ((pod.flags & KS_POD_CPU_BIND) && (pod.cpu_bind & KS_CPU_BIND_REQUIRED)) ||
+                (cores_label(cw) != 0 && pod.cpu > 0);
+      }
+      if ((FEAT & 2) && DEV && cfg.dev && cfg.cores && __ballot(unk)) {
+        processed = j;  // DeviceShare's normalization max over the feasible nodes would depend on it
+        break;
       }
       if (DEV && cfg.dev) {
         // DeviceShare normalization: the untouched nodes' max is the sweep's M while its witness is
@@ -717,6 +733,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep from j
         break;
       }
+      if ((FEAT & 2) && cfg.cores && __ballot(unk && key_mod == best)) {
+        processed = j;  // the winner's feasibility depends on core counts the next pass will have exact
+        break;
+      }
       KS_STAMP(3);
     }
     if (best == 0) {
@@ -729,9 +749,19 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const int64_t* podw = reinterpret_cast<const int64_t*>(&spods[j]);
     // ---- Reserve: NodeInfo.AddPod + podAssignCache.assign on the slot row (lane = term) ----
     // a cpu-bind pod first needs numCPUsNeeded available CPUs on the node (resource_manager.go:333-335)
-    const bool cpubind = (FEAT & 2) && cfg.cpuset && (pflags & KS_POD_CPU_BIND);
-    const int32_t cpu_need = cpubind ? (int32_t)(__builtin_amdgcn_readfirstlane(spods[j].cpu_bind) >> 8) : 0;
+    bool cpubind = (FEAT & 2) && cfg.cpuset && (pflags & KS_POD_CPU_BIND);
+    int32_t cpu_need = cpubind ? (int32_t)(__builtin_amdgcn_readfirstlane(spods[j].cpu_bind) >> 8) : 0;
     int32_t s = __ffsll((long long)__ballot(snode == node)) - 1;
+    uint32_t ncw = 0;  // Cfg.cores: the node's CoresWord
+    if ((FEAT & 2) && cfg.cores) {
+      ncw = __builtin_amdgcn_readfirstlane(s >= 0 ? (uint32_t)((uint64_t)snuma[4 * s + 3] >> 32) : gld(a.dn->cpu_cores + node));
+      // a whole-CPU pod is cpu-bind on a node with a CPU bind policy (requestCPUBind, util.go:105-122)
+      const int64_t pcpu = podw[0];  // PodRec.cpu
+      if (!cpubind && cfg.cpuset && cores_label(ncw) != 0 && pcpu > 0) {
+        cpubind = true;
+        cpu_need = __builtin_amdgcn_readfirstlane((int32_t)(pcpu / 1000));
+      }
+    }
     SlotRow* row;
     // Reservation Reserve needs the node's pre-pod row: when the pod's class matches one of the
     // node's reservations the row is built / kept without the pod, nominated on, then taken.
@@ -777,7 +807,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
           snuma[4 * s] = u_A;
           snuma[4 * s + 1] = u_off;
           snuma[4 * s + 2] = u_ratio;
-          snuma[4 * s + 3] = (int64_t)u_free;
+          snuma[4 * s + 3] = cfg.cores ? (int64_t)(((uint64_t)(ncw & ~kCoresDirty) << 32) | (uint32_t)u_free)
+                                       : (int64_t)u_free;
         }
       }
       if ((FEAT & 8) && cfg.numa_pol) {
@@ -880,6 +911,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       nr.numa_off = snuma[4 * s + 1];
       nr.numa_ratio = __longlong_as_double(snuma[4 * s + 2]);
       nr.cpu_free = (int32_t)snuma[4 * s + 3];
+      if ((FEAT & 2) && cfg.cores) nr.cpu_cores = (uint32_t)((uint64_t)snuma[4 * s + 3] >> 32);  // (score: the label)
       RsvDelta<NSC> dl;
       const int32_t mode = srcnt[s];
       const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s]};
@@ -1070,6 +1102,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         snuma[4 * s] = A1;
         snuma[4 * s + 1] = off1;
         snuma[4 * s + 3] -= cpu_need;
+        if (cfg.cores) snuma[4 * s + 3] |= (int64_t)((uint64_t)kCoresDirty << 32);
         a.cpuset_list[atomicAdd(a.cpuset_n, 1)] = make_int2(cursor0 + j, node);
         a.cpuset_split[cursor0 + j] = cpu_split;
       }

@@ -375,6 +375,29 @@ def cpuset_pods(pods: PodTable, rng: np.random.Generator, frac: float = 0.4, exc
     return pods
 
 
+def cpu_bind_policies(nodes: NodeTable, pods: PodTable, rng: np.random.Generator, label_frac: float = 0.4,
+                      required_frac: float = 0.4, whole_frac: float = 0.5, odd_frac: float = 0.1) -> None:
+    """Node CPU bind policies (the node-cpu-bind-policy label, FullPCPUsOnly / SpreadByPCPUs in equal parts) on
+    label_frac of the nodes; a required bind policy on required_frac of the cpuset pods (some required FullPCPUs
+    requests an odd number of CPUs: the SMT alignment check); whole-CPU requests for whole_frac of the other pods
+    (cpu-bind on a labelled node, requestCPUBind util.go:105-122; the rest fail ErrInvalidRequestedCPUs there)."""
+    n, p = nodes.n, pods.n
+    lab = np.where(rng.random(n) < label_frac, rng.integers(1, 3, n), 0).astype(np.uint32)
+    nodes.numa_flags[:] = (nodes.numa_flags & ~np.uint32(3 << abi.KS_NUMA_CPU_BIND_SHIFT)) | (lab << abi.KS_NUMA_CPU_BIND_SHIFT)
+    bind = (pods.flags & abi.KS_POD_CPU_BIND) != 0
+    req = bind & (rng.random(p) < required_frac)
+    pods.cpu_bind[:] = np.where(req, pods.cpu_bind | abi.KS_CPU_BIND_REQUIRED, pods.cpu_bind).astype(np.uint32)
+    odd = req & ((pods.cpu_bind & abi.KS_CPU_BIND_POLICY_MASK) == abi.KS_CPU_BIND_FULL_PCPUS) & (rng.random(p) < odd_frac)
+    for col in ("req_milli_cpu", "nonzero_milli_cpu", "la_req_cpu"):
+        v = getattr(pods, col)
+        v[:] = np.where(odd, v + 1000, v)
+    whole = ~bind & (pods.req_milli_cpu > 0) & (rng.random(p) < whole_frac)
+    cpu = np.clip((pods.req_milli_cpu + 999) // 1000, 1, 24) * 1000
+    for col in ("req_milli_cpu", "nonzero_milli_cpu"):
+        v = getattr(pods, col)
+        v[:] = np.where(whole, cpu, v)
+
+
 def make_numa_nodes(nodes: NodeTable, rng: np.random.Generator, policy_frac: float = 0.5, cores=None):
     """NUMA topology policies on a fraction of the nodes (best-effort / restricted / single-numa-node in equal
     parts), 1, 2 or 4 NUMA nodes splitting the node's CPUs and memory, and earlier pods' NUMA allocations
@@ -469,6 +492,17 @@ def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, policy_frac:
     prof.numa = NodeNUMAResourceArgs()
     prof.deviceshare = DeviceShareArgs()  # v1beta2 defaults: gpu-memory-ratio, rdma, fpga weight 1
     return Workload("C3", prof, nodes, pods, None, None, devs, cpus, numa)
+
+
+def c3_bind(seed: int = SEED, n_nodes: int = 2000, n_pods: int = 4000, label_frac: float = 0.4,
+            required_frac: float = 0.4, **kw) -> Workload:
+    """C3 without NUMA topology policies, with node CPU bind policies and required pod bind policies
+    (cpu_bind_policies)"""
+    w = c3(seed=seed, n_nodes=n_nodes, n_pods=n_pods, policy_frac=0.0, **kw)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    cpu_bind_policies(w.nodes, w.pods, rng, label_frac, required_frac)
+    w.name = "C3-bind"
+    return w
 
 
 def c4(seed: int = SEED, n_nodes: int = 20_000, n_reservations: int = 50_000, n_pods: int = 10_000, **kw) -> Workload:

@@ -221,8 +221,11 @@ typedef struct {
   int64_t rdma;  /* koordinator.sh/rdma request */
   uint8_t joint; /* KS_JOINT_* */
   uint32_t keys; /* bit d: request dimension d is a key of the pod's requests (value != 0) */
-  uint32_t bind;  /* cpu-bind pod (preFilterState.requestCPUBind): ks_pod_cols.cpu_bind, else 0 */
+  uint32_t bind;  /* cpu-bind pod (preFilterState.requestCPUBind): ks_pod_cols.cpu_bind, else 0; per node (node_pod)
+                     the allocation's policy (getCPUBindPolicy) with KS_CPU_BIND_REQUIRED when it is required */
   int32_t needed; /* numCPUsNeeded */
+  uint32_t bind_rs;  /* per node: ErrInvalidRequestedCPUs of requestCPUBind (util.go:115-118) */
+  int bind_conflict; /* per node: ErrCPUBindPolicyConflict (plugin.go:310-312) */
 } ko_pod;
 
 /* NodeInfo values the Fit plugin reads, after the Reservation restore */
@@ -343,6 +346,32 @@ static int64_t amplify(int64_t origin, double ratio) {
   return (int64_t)ceil((double)origin * ratio);
 }
 
+/* The pod as NodeNUMAResource sees it on node n with a node CPU bind policy (bits KS_NUMA_CPU_BIND_SHIFT):
+ * requestCPUBind (util.go:105-122) makes a whole-CPU pod cpu-bind there, a fractional one fails
+ * ErrInvalidRequestedCPUs; the Filter's required policy is the node's (plugin.go:303-309), a different required
+ * policy of the pod conflicts (:310-312); getCPUBindPolicy (util.go:85-103) allocates with the pod's required
+ * policy, else the node's, both required.  The exclusive policy stays the pod's preferred one (plugin.go:520).
+ * Returns p itself on a node without a CPU bind policy. */
+static const ko_pod *node_pod(const ko_sched *s, const ko_pod *p, int64_t n, ko_pod *pn) {
+  const uint32_t L = s->cfg.numa.enable ? (s->nd.numa_flags[n] >> KS_NUMA_CPU_BIND_SHIFT) & 3u : 0u;
+  if (!L || p->reqzero) return p;
+  *pn = *p;
+  if (p->bind) {
+    if ((p->bind & KS_CPU_BIND_REQUIRED) && (p->bind & KS_CPU_BIND_POLICY_MASK) != L)
+      pn->bind_conflict = 1;
+    else
+      pn->bind = L | (p->bind & (3u << KS_CPU_EXCL_SHIFT)) | KS_CPU_BIND_REQUIRED;
+  } else if (p->cpu > 0) {
+    if (p->cpu % 1000 != 0) {
+      pn->bind_rs = KS_R_NUMA_INVALID_CPUS;
+    } else {
+      pn->bind = L | KS_CPU_BIND_REQUIRED;
+      pn->needed = (int32_t)(p->cpu / 1000);
+    }
+  }
+  return pn;
+}
+
 /* filterAmplifiedCPUs (plugin.go:340-373) on the (restored) NodeInfo; a cpu-bind pod's request is amplified */
 static uint32_t numa_filter_amplified(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
   const ko_nodes *d = &s->nd;
@@ -382,11 +411,23 @@ typedef struct {
   ko_numa_out *out;
 } ko_npol;
 
+static int cpu_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_npol *c, uint8_t *res);
+
 static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c) {
   if (p->reqzero) return 0; /* PreFilter skip */
+  if (p->bind_rs) return p->bind_rs;
   uint32_t r = numa_filter_amplified(s, p, n, e);
   if (r) return r;
   if (p->bind && !(s->cpu_loaded && s->topo_of[n] >= 0)) return KS_R_NUMA_INVALID_TOPOLOGY;
+  if (p->bind && p->bind_conflict) return KS_R_NUMA_BIND_CONFLICT;
+  if (p->bind && (p->bind & KS_CPU_BIND_REQUIRED)) {
+    /* required FullPCPUs: whole cores (:314-317); on a node without NUMA policy a trial Allocate (:318-327) */
+    const ko_topo *t = &s->topos[s->topo_of[n]];
+    const int cpc = t->num_cores > 0 ? t->ncpus / t->num_cores : 1;
+    if ((p->bind & KS_CPU_BIND_POLICY_MASK) == KS_CPU_BIND_FULL_PCPUS && p->needed % cpc != 0) return KS_R_NUMA_SMT;
+    uint8_t res[KO_MAX_CPUS];
+    if (!c->on && cpu_allocate(s, p, n, NULL, res) != 0) return KS_R_NUMA_CPUSET;
+  }
   return c->on ? c->reasons : 0;
 }
 
@@ -2003,8 +2044,10 @@ typedef struct {
 
 /* BeforePreFilter restore + Filter for one node; the Reservation PreScore per-node part
  * (nomination, node order) for feasible ones.  Returns the KS_R_* bits. */
-static uint32_t eval_node(ko_sched *s, const ko_pod *p, int64_t n, int64_t *fit_out, int64_t *la_out,
+static uint32_t eval_node(ko_sched *s, const ko_pod *p0, int64_t n, int64_t *fit_out, int64_t *la_out,
                           int64_t *numa_out) {
+  ko_pod pn;
+  const ko_pod *p = node_pod(s, p0, n, &pn);
   ko_rstate st;
   rsv_restore(s, p, n, &st);
   uint32_t r = rsv_filter(s, p, n, &st);
@@ -2087,30 +2130,68 @@ static void rsv_normalize(ko_sched *s, int64_t *norm) {
  * allocateCPUSet (resource_manager.go:314-401: available = CPUs - allocated - reserved, too few -> error;
  * with a NUMA allocation takeCPUs per allocated NUMA node over its available CPUs, else over the whole node)
  * then Update -> NodeAllocation.addPodAllocation (node_allocation.go:75-100). */
-static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod, const ko_npol *c) {
+/* filterCPUsByRequiredCPUBindPolicy (resource_manager.go:595-627): FullPCPUs keeps the cores whose CPUs are all
+ * available (CPUsPerCore of them), SpreadByPCPUs the lowest available CPU of every core */
+static void filter_required(const ko_topo *t, int policy, uint8_t *avail) {
+  const int cpc = t->num_cores > 0 ? t->ncpus / t->num_cores : 1;
+  uint8_t keep[KO_MAX_CPUS];
+  memset(keep, 0, sizeof(keep));
+  for (int i = 0; i < t->ncpus; i++) {
+    if (!avail[i]) continue;
+    int first = 1, cnt = 0;
+    for (int j = 0; j < t->ncpus; j++) {
+      if (!avail[j] || t->core[j] != t->core[i]) continue;
+      cnt++;
+      if (j < i) first = 0;
+    }
+    keep[i] = policy == KS_CPU_BIND_FULL_PCPUS ? cnt == cpc : first;
+  }
+  memcpy(avail, keep, (size_t)t->ncpus);
+}
+
+/* satisfiedRequiredCPUBindPolicy (resource_manager.go:629-650): determineFullPCPUs / determineSpreadByPCPUs */
+static int satisfied_required(const ko_topo *t, int policy, const uint8_t *res) {
+  const int cpc = t->num_cores > 0 ? t->ncpus / t->num_cores : 1;
+  int ncpu = 0, ncore = 0;
+  for (int i = 0; i < t->ncpus; i++) {
+    if (!res[i]) continue;
+    ncpu++;
+    int first = 1;
+    for (int j = 0; j < i; j++)
+      if (res[j] && t->core[j] == t->core[i]) first = 0;
+    ncore += first;
+  }
+  return policy == KS_CPU_BIND_FULL_PCPUS ? ncore * cpc == ncpu : ncore == ncpu;
+}
+
+/* resourceManager.Allocate's allocateCPUSet (resource_manager.go:314-401) on node n's current CPU state: available =
+ * CPUs - allocated - reserved, narrowed by a required bind policy; too few -> error; with a NUMA allocation takeCPUs
+ * per allocated NUMA node over its available CPUs, else over the whole node; a required policy must be satisfied.
+ * res = the CPUs taken.  Returns 0 or -1. */
+static int cpu_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_npol *c, uint8_t *res) {
   if (!s->cpu_loaded || s->topo_of[n] < 0) return -1;
   const ko_topo *t = &s->topos[s->topo_of[n]];
-  uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
-  int8_t *ex = s->cpu_excl + (size_t)n * KO_MAX_CPUS;
-  uint8_t avail[KO_MAX_CPUS], res[KO_MAX_CPUS], part[KO_MAX_CPUS], sub[KO_MAX_CPUS];
+  const uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
+  const int8_t *ex = s->cpu_excl + (size_t)n * KO_MAX_CPUS;
+  uint8_t avail[KO_MAX_CPUS], part[KO_MAX_CPUS], sub[KO_MAX_CPUS];
+  const int policy = (int)(p->bind & KS_CPU_BIND_POLICY_MASK), required = (p->bind & KS_CPU_BIND_REQUIRED) != 0;
+  for (int i = 0; i < t->ncpus; i++) avail[i] = !al[i] && !rs[i];
+  if (required) filter_required(t, policy, avail);
   int navail = 0;
-  for (int i = 0; i < t->ncpus; i++) {
-    avail[i] = !al[i] && !rs[i];
-    navail += avail[i];
-  }
+  for (int i = 0; i < t->ncpus; i++) navail += avail[i];
   if (navail < p->needed) return -1;
   uint32_t nf = s->nd.numa_flags[n];
   int strategy = (nf & KS_NUMA_ALLOC_MOST) ? KO_NUMA_MOST
                  : (nf & KS_NUMA_ALLOC_LEAST) ? KO_NUMA_LEAST
                  : (s->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED ? KO_NUMA_MOST : KO_NUMA_LEAST);
   int excl_policy = (int)((p->bind >> KS_CPU_EXCL_SHIFT) & 3u);
-  int bind = (p->bind & KS_CPU_BIND_POLICY_MASK) == KS_CPU_BIND_FULL_PCPUS ? KO_BIND_FULL_PCPUS : KO_BIND_SPREAD_BY_PCPUS;
+  int bind = policy == KS_CPU_BIND_FULL_PCPUS ? KO_BIND_FULL_PCPUS : KO_BIND_SPREAD_BY_PCPUS;
   int numa_alloc = 0;
   if (c && c->on && c->out->affinity)
     for (int k = 0; k < KS_MAX_NUMA; k++) numa_alloc |= c->out->alloc[k][0] != 0 || c->out->alloc[k][1] != 0;
   if (numa_alloc) {
     /* per allocated NUMA node (NUMANodeResources in node order), against the allocation before this pod */
-    memset(res, 0, sizeof(res));
+    memset(res, 0, KO_MAX_CPUS);
     int taken = 0;
     for (int k = 0; k < KS_MAX_NUMA; k++) {
       if (!c->out->alloc[k][0] && !c->out->alloc[k][1]) continue;
@@ -2125,6 +2206,19 @@ static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod, con
   } else if (ko_take_cpus(t, 1, avail, NULL, ex, p->needed, bind, excl_policy, strategy, res) != 0) {
     return -1;
   }
+  if (required && !satisfied_required(t, policy, res)) return -1;
+  return 0;
+}
+
+/* NodeNUMAResource Reserve for a cpu-bind pod (plugin.go:376-429): Allocate, then Update ->
+ * NodeAllocation.addPodAllocation (node_allocation.go:75-100) */
+static int cpu_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t pod, const ko_npol *c) {
+  uint8_t res[KO_MAX_CPUS];
+  if (cpu_allocate(s, p, n, c, res) != 0) return -1;
+  const ko_topo *t = &s->topos[s->topo_of[n]];
+  uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS;
+  int8_t *ex = s->cpu_excl + (size_t)n * KO_MAX_CPUS;
+  const int excl_policy = (int)((p->bind >> KS_CPU_EXCL_SHIFT) & 3u);
   uint64_t *o = s->cpusets + (size_t)pod * KS_CPU_WORDS;
   int taken = 0;
   for (int i = 0; i < t->ncpus; i++) {
@@ -2230,9 +2324,11 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     e0 = st0.e;
     ko_numa_out no;
     ko_npol npc;
-    numa_policy_ctx(s, &p, best_n, &e0, &npc, &no);
-    const uint32_t allow = npol_allow(s, &p, best_n, &e0, &npc);
-    if (p.bind && cpu_reserve(s, &p, best_n, i, &npc) != 0) {
+    ko_pod pn;
+    const ko_pod *pb = node_pod(s, &p, best_n, &pn);
+    numa_policy_ctx(s, pb, best_n, &e0, &npc, &no);
+    const uint32_t allow = npol_allow(s, pb, best_n, &e0, &npc);
+    if (pb->bind && cpu_reserve(s, pb, best_n, i, &npc) != 0) {
       /* NodeNUMAResource Reserve -> Allocate failed: every Reserve plugin unreserves */
       out[i].status = KS_S_RESERVE_FAILED;
       out[i].score = 0;
@@ -2275,13 +2371,15 @@ int ko_assume(ko_sched *s, const ks_pod_cols *pc, int32_t node, ks_result *out, 
   ko_eff e0 = st0.e;
   ko_numa_out no;
   ko_npol npc;
-  numa_policy_ctx(s, &p, n, &e0, &npc, &no);
+  ko_pod pn;
+  const ko_pod *pb = node_pod(s, &p, n, &pn);
+  numa_policy_ctx(s, pb, n, &e0, &npc, &no);
   if (numa_alloc) {
     memset(numa_alloc, 0, sizeof(int64_t) * KS_MAX_NUMA * 2);
     if (npc.on && !npc.reasons) memcpy(numa_alloc, no.alloc, sizeof(no.alloc));
   }
-  const uint32_t allow = npol_allow(s, &p, n, &e0, &npc);
-  if (p.bind && cpu_reserve(s, &p, n, 0, &npc) != 0) {
+  const uint32_t allow = npol_allow(s, pb, n, &e0, &npc);
+  if (pb->bind && cpu_reserve(s, pb, n, 0, &npc) != 0) {
     out->status = KS_S_RESERVE_FAILED;
     if (numa_alloc) memset(numa_alloc, 0, sizeof(int64_t) * KS_MAX_NUMA * 2);
     return 0;

@@ -61,3 +61,80 @@ def supported_on_device(case):
     """maxRefCount 1, and FullPCPUs requests in whole cores (the evaluator refuses the rest)"""
     cpc = case["topo"][3]
     return case["max_ref"] == 1 and not (case["bind"] == "FullPCPUs" and case["needed"] % cpc)
+
+
+def bind_policy_cluster(topo, allocated=(), label=0, cpu_milli=4000, bind=None, required=False, excl=0,
+                        strategy="Least"):
+    """One node with CPU topology `topo` (buildCPUTopologyForTest), `allocated` CPUs, node CPU bind policy
+    `label` (KS_NODE_CPU_BIND_*), and one pod requesting cpu_milli: cpu-bind with policy `bind` (required or
+    preferred) or, for bind=None, a plain pod (cpu-bind only through the node's policy)."""
+    import numpy as np
+
+    from koordinator_amd import abi
+    from koordinator_amd.cluster import CpuState, NodeTable, PodTable, cpu_mask, cpu_topology
+    from koordinator_amd.config import CPU, MEMORY, NodeNUMAResourceArgs, SchedulerProfile
+
+    core, node, sock = build_topology(*topo)
+    ncpu = len(core)
+    st = CpuState(1, [cpu_topology(core, node, sock)])
+    st.topology[0] = 0
+    st.allocated[0] = cpu_mask(list(allocated))
+    nodes = NodeTable(1)
+    nodes.alloc_milli_cpu[:] = ncpu * 1000
+    nodes.alloc_memory[:] = 1 << 40
+    nodes.req_milli_cpu[:] = len(allocated) * 1000
+    nodes.nonzero_milli_cpu[:] = len(allocated) * 1000
+    nodes.allowed_pods[:] = 110
+    nodes.numa_cpuset_cpus[:] = len(allocated)
+    nodes.numa_flags[:] = ((abi.KS_NUMA_ALLOC_MOST if strategy == "Most" else abi.KS_NUMA_ALLOC_LEAST) |
+                           (label << abi.KS_NUMA_CPU_BIND_SHIFT))
+    pod = PodTable(1)
+    pod.req_milli_cpu[:] = cpu_milli
+    pod.nonzero_milli_cpu[:] = cpu_milli
+    pod.req_memory[:] = 1 << 30
+    pod.nonzero_memory[:] = 1 << 30
+    pod.flags[:] = abi.KS_POD_PROD
+    if bind is not None:
+        pod.flags[:] |= abi.KS_POD_CPU_BIND
+        pod.cpu_bind[:] = bind | (excl << abi.KS_CPU_EXCL_SHIFT) | (abi.KS_CPU_BIND_REQUIRED if required else 0)
+    cfg = SchedulerProfile(loadaware=None, numa=NodeNUMAResourceArgs(resources={CPU: 1, MEMORY: 1})).to_ks_config()
+    return cfg, nodes, st, pod
+
+
+# Filter of NodeNUMAResource with node CPU bind policies and required pod policies: the reference's
+# TestPlugin_Filter cases (nodenumaresource/plugin_test.go:592-760) on buildCPUTopologyForTest(2, 1, 4, 2), no
+# allocation.  (name, label, bind, required, cpu milli, expected reason bits)
+def filter_cases():
+    from koordinator_amd import abi
+    F, S = abi.KS_CPU_BIND_FULL_PCPUS, abi.KS_CPU_BIND_SPREAD_BY_PCPUS
+    LF, LS = abi.KS_NODE_CPU_BIND_FULL_PCPUS_ONLY, abi.KS_NODE_CPU_BIND_SPREAD_BY_PCPUS
+    return [
+        ("node FullPCPUsOnly, preferred FullPCPUs 5: SMTAlignmentError", LF, F, False, 5000, abi.KS_R_NUMA_SMT),
+        ("LS pod on node FullPCPUsOnly, 5 CPUs: SMTAlignmentError", LF, None, False, 5000, abi.KS_R_NUMA_SMT),
+        ("LS pod on node FullPCPUsOnly, 5200m: InvalidRequestedCPUs", LF, None, False, 5200, abi.KS_R_NUMA_INVALID_CPUS),
+        ("node FullPCPUsOnly, preferred FullPCPUs 4", LF, F, False, 4000, 0),
+        ("required FullPCPUs 5: SMTAlignmentError", 0, F, True, 5000, abi.KS_R_NUMA_SMT),
+        ("required FullPCPUs 4", 0, F, True, 4000, 0),
+        ("node FullPCPUsOnly, preferred SpreadByPCPUs 4", LF, S, False, 4000, 0),
+        ("node SpreadByPCPUs, required FullPCPUs: CPUBindPolicyConflict", LS, F, True, 4000, abi.KS_R_NUMA_BIND_CONFLICT),
+        ("node FullPCPUsOnly, required FullPCPUs 4", LF, F, True, 4000, 0),
+        ("kubelet FullPCPUsOnly, required SpreadByPCPUs: CPUBindPolicyConflict", LF, S, True, 4000,
+         abi.KS_R_NUMA_BIND_CONFLICT),
+        ("required FullPCPUs 4 with no NUMA topology policy", 0, F, True, 4000, 0),
+    ]
+
+
+# allocateCPUSet with a required policy: TestResourceManagerAllocate (resource_manager_test.go:95-330) on
+# buildCPUTopologyForTest(2, 1, 26, 2), NUMALeastAllocated, 4 CPUs.  (name, bind, allocated, want cpus or None)
+def allocate_cases():
+    from koordinator_amd import abi
+    F, S = abi.KS_CPU_BIND_FULL_PCPUS, abi.KS_CPU_BIND_SPREAD_BY_PCPUS
+    holes = [1, 3, 5] + list(range(7, 104))
+    return [
+        ("required FullPCPUs", F, [], [0, 1, 2, 3]),
+        ("required FullPCPUs and allocated", F, list(range(4, 104)), [0, 1, 2, 3]),
+        ("required FullPCPUs and allocated: no whole core", F, holes, None),
+        ("required SpreadByPCPUs", S, [], [0, 2, 4, 6]),
+        ("required SpreadByPCPUs and allocated", S, holes, [0, 2, 4, 6]),
+        ("required SpreadByPCPUs and allocated: two cores", S, list(range(4, 104)), None),
+    ]
