@@ -244,9 +244,10 @@ typedef struct ks_reservation_args {
 } ks_reservation_args;
 
 /* NodeNUMAResourceArgs.ScoringStrategy (pkg/scheduler/apis/config/types.go; defaults
- * v1beta2/defaults.go:107-136: LeastAllocated, cpu 1, memory 1).  Nodes with a CPU-bind or NUMA
- * topology policy are not supported; cpuset pods (KS_POD_CPU_BIND) are, on nodes whose CPU
- * topology and allocation state were given to ks_load_cpu_state. */
+ * v1beta2/defaults.go:107-136: LeastAllocated, cpu 1, memory 1).  Node CPU bind policies
+ * (numa_flags bits 7-8), NUMA topology policies (bits 5-6, with ks_load_numa_nodes) and cpuset pods
+ * (KS_POD_CPU_BIND, preferred or KS_CPU_BIND_REQUIRED) are supported on nodes whose CPU topology and
+ * allocation state were given to ks_load_cpu_state; a CPU bind policy together with a NUMA policy is not. */
 typedef struct ks_numa_args {
   int32_t enable;
   int32_t strategy; /* KS_LEAST_ALLOCATED | KS_MOST_ALLOCATED */
