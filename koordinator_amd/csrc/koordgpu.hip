@@ -29,6 +29,7 @@
 #include <rccl/rccl.h>
 
 #include "ks_pass.h"
+#include "ks_mono.h"
 #include "ks_debug.h"
 
 using namespace ks;
@@ -101,6 +102,11 @@ __global__ void prep_nodes_kernel(DevNodes d, int64_t n, int32_t filter_expired)
   d.numa_off[i] = amp ? (int64_t)::ceil((double)A * ratio) - A : 0;
   if (amp) bits |= kNumaAmp;
   if (d.numa_flags[i] & KS_NUMA_INVALID_RATIO) bits |= kNumaInvalid;
+  // a score-term capacity outside the f64 path's range (ks_device.h term_least): the node scores in int64
+  bool big = d.alloc_cpu[i] >= kBigCap || d.alloc_mem[i] >= kBigCap || d.alloc_eph[i] >= kBigCap ||
+             d.la_alloc_cpu[i] >= kBigCap || d.la_alloc_mem[i] >= kBigCap;
+  for (int k = 0; k < KS_MAX_SCALARS; ++k) big |= d.alloc_sc[k][i] >= kBigCap;
+  if (big) bits |= kNodeBigCap;
   d.la_bits[i] = bits;
 }
 
@@ -147,20 +153,22 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   if (r.cpu == 0 && r.mem == 0 && r.eph == 0 && !(fl & KS_POD_SCALAR_KEYS)) fl |= kPodAllZero;
   r.flags = fl;
   r.quota = s.quota[i];
-  r.h_nzcpu = r.nzcpu * 100;
-  r.h_nzmem = r.nzmem * 100;
-  r.h_eph = r.eph * 100;
-  r.h_est_cpu = r.est_cpu * 100;
-  r.h_est_mem = r.est_mem * 100;
-  r.f_nzcpu = i64_to_f32(r.nzcpu);
-  r.f_nzmem = i64_to_f32(r.nzmem);
-  r.f_eph = i64_to_f32(r.eph);
-  r.f_est_cpu = i64_to_f32(r.est_cpu);
-  r.f_est_mem = i64_to_f32(r.est_mem);
+  // 100 x the score-term requests as f64 (exact below kBigReq; a larger request sends the pod's terms to the
+  // int64 path, ks_device.h term_least)
+  r.h_nzcpu = (double)r.nzcpu * 100.0;
+  r.h_nzmem = (double)r.nzmem * 100.0;
+  r.h_eph = (double)r.eph * 100.0;
+  r.h_est_cpu = (double)r.est_cpu * 100.0;
+  r.h_est_mem = (double)r.est_mem * 100.0;
+  bool big = false;
   for (int k = 0; k < KS_MAX_SCALARS; ++k) {
-    r.h_sc[k] = r.sc[k] * 100;
-    r.f_sc[k] = i64_to_f32(r.sc[k]);
+    r.h_sc[k] = (double)r.sc[k] * 100.0;
+    big |= r.sc[k] >= kBigReq || r.sc[k] < 0;
   }
+  const int64_t tw[7] = {r.cpu, r.mem, r.eph, r.nzcpu, r.nzmem, r.est_cpu, r.est_mem};
+  for (int k = 0; k < 7; ++k) big |= tw[k] >= kBigReq || tw[k] < 0;
+  if (big) fl |= kPodBigReq;
+  r.flags = fl;
   r.rsv_class = s.rsv_class[i];
   uint32_t keys = 0;
   const int64_t dims[3] = {r.cpu, r.mem, r.eph};
@@ -168,10 +176,8 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   for (int k = 0; k < KS_MAX_SCALARS; ++k) keys |= r.sc[k] != 0 ? (1u << (3 + k)) : 0u;
   r.rsv_keys = keys;
   if (keys == 0) r.flags |= kPodReqZero;
-  r.h_cpu = r.cpu * 100;
-  r.h_mem = r.mem * 100;
-  r.f_cpu = i64_to_f32(r.cpu);
-  r.f_mem = i64_to_f32(r.mem);
+  r.h_cpu = (double)r.cpu * 100.0;
+  r.h_mem = (double)r.mem * 100.0;
   r.gpu_core = s.gpu_core[i];
   r.gpu_mem = s.gpu_mem[i];
   r.gpu_ratio = s.gpu_ratio[i];
@@ -2628,6 +2634,16 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   return ca;
 }
 
+// The monotone commit kernel (ks_mono.h) runs the passes of a plugin set without Reservation, NodeNUMAResource or
+// DeviceShare whose keys commits can only lower (Fit LeastAllocated + LoadAware [+ ElasticQuota]) when its LDS
+// fits; KS_COMMIT_GENERAL=1 keeps the general kernel (A/B).  ks_assume always uses the general kernel.
+static bool mono_commit(const ks_ctx* ctx, bool qcache, size_t* smem) {
+  static const bool general = env_i64("KS_COMMIT_GENERAL", 0, 0, 1) != 0;
+  if (general || kernel_feat(ctx) != 0 || !ctx->kc.monotone || ctx->kc.fit_most) return false;
+  *smem = mono_layout(ctx->k, ctx->nchunks, qcache).total;
+  return *smem <= 160 * 1024;
+}
+
 // the commit kernel's LDS size for this context: checked against the CU's 160 KB and set on the variant
 static int commit_attr_set(ks_ctx* ctx) {
   bool qcache = false;
@@ -2638,6 +2654,11 @@ static int commit_attr_set(ks_ctx* ctx) {
     KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
   hipError_t e = pass_launcher(kernel_feat(ctx), ctx->nsc).commit_attr(qcache, smem);
   if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(commit LDS %zu): %s", smem, hipGetErrorString(e));
+  size_t msmem = 0;
+  if (mono_commit(ctx, qcache, &msmem)) {
+    e = pass_launcher(0, ctx->nsc).commit_mono_attr(qcache, msmem);
+    if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(mono commit LDS %zu): %s", msmem, hipGetErrorString(e));
+  }
   return KS_OK;
 }
 
@@ -2782,8 +2803,11 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   bool qcache = false;
   size_t smem = 0;
   const CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, ctx->batch, &qcache, &smem);
+  size_t msmem = 0;
+  const bool mono = mono_commit(ctx, qcache, &msmem);
   rec(2);
-  HIPCHK(ctx, pl.commit(qcache, smem, ctx->stream, ca));
+  if (mono) HIPCHK(ctx, pl.commit_mono(qcache, msmem, ctx->stream, ca));
+  else HIPCHK(ctx, pl.commit(qcache, smem, ctx->stream, ca));
   rec(2);
   if (ctx->kc.cores && ctx->cpu_loaded) {
     // the pass's CPU ids now, so that the next sweep sees exact per-node core counts (Cfg.cores)

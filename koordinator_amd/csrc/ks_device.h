@@ -13,10 +13,11 @@
 //   LoadAware Score          load_aware.go:269-397
 //
 // Integer division note: every score divides by a per-node capacity.  A 64-bit
-// divide is ~40 VALU ops on CDNA; instead q = floor(d*100/cap) is estimated in
-// f32 with a per-node reciprocal (relative error < 2^-20, so |q_est - q| <= 1)
-// and corrected exactly with one int64 multiply-subtract.  Results are bit-exact
-// with Go's int64 arithmetic for every 0 <= d <= cap < 2^56.
+// divide is ~40 VALU ops on CDNA; the score terms instead compute
+// q = floor(100*d/cap) as one f64 fma, trunc(fma(100*d, 1/cap, 2^-44)), exact for
+// cap < 2^43 and 100*|d| < 2^53 (see term_least); other nodes / pods take the
+// int64 path (f32 estimate corrected by one int64 multiply-subtract, exact for
+// 0 <= d <= cap < 2^56).  Results are bit-exact with Go's int64 arithmetic.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -39,6 +40,8 @@ constexpr uint32_t kPodReqZero = 0x200u;
 constexpr uint32_t kPodHasGpu = 0x400u;
 // internal pod flag: the pod has a GPU request
 constexpr uint32_t kPodGpuReq = 0x800u;
+// internal pod flag: a score-term request >= kBigReq: the pod's terms take the int64 path
+constexpr uint32_t kPodBigReq = 0x1000u;
 
 // la_bits (prep_nodes_kernel output)
 constexpr uint32_t kLaZeroScore = 0x1u;     // Score returns 0 (no NodeMetric / expired)
@@ -46,6 +49,7 @@ constexpr uint32_t kLaFailNonProd = 0x2u;   // Filter fails for non-prod (or no 
 constexpr uint32_t kLaFailProd = 0x4u;      // Filter fails for prod pods when prod thresholds exist
 constexpr int kLaReasonNonProdShift = 8;    // KS_R_LA_* reason bits for the non-prod case
 constexpr int kLaReasonProdShift = 20;      // KS_R_LA_* reason bits for the prod case
+constexpr uint32_t kNodeBigCap = 0x8u;      // a score-term capacity >= kBigCap: the node's terms take the int64 path
 constexpr uint32_t kNumaAmp = 1u << 30;     // NodeNUMAResource: cpu amplification ratio > 1
 constexpr uint32_t kNumaInvalid = 1u << 31; // NodeNUMAResource: invalid amplification annotation
 
@@ -112,22 +116,20 @@ struct __attribute__((aligned(16))) PodRec {
   int64_t sc[KS_MAX_SCALARS];                              // words 7..10
   uint32_t flags;                                          // word 11 (lo)
   int32_t quota;                                           // word 11 (hi)
-  // 100 x the score-term requests (nzcpu, nzmem, eph, est_cpu, est_mem, sc[k])
-  int64_t h_nzcpu, h_nzmem, h_eph, h_est_cpu, h_est_mem;   // words 12..16
-  int64_t h_sc[KS_MAX_SCALARS];                            // words 17..20
-  float f_nzcpu, f_nzmem, f_eph, f_est_cpu, f_est_mem;     // f32 of the same requests
-  float f_sc[KS_MAX_SCALARS];
+  // 100 x the score-term requests (nzcpu, nzmem, eph, est_cpu, est_mem, sc[k]) as f64 (exact: kPodBigReq otherwise)
+  double h_nzcpu, h_nzmem, h_eph, h_est_cpu, h_est_mem;    // words 12..16
+  double h_sc[KS_MAX_SCALARS];                             // words 17..20
   int32_t rsv_class;  // reservation match class (-1 = none)
   uint32_t rsv_keys;  // bit d: request dimension d is non-zero (a key of the pod's requests)
   uint32_t cpu_bind;  // KS_POD_CPU_BIND pods: KS_CPU_BIND_* | exclusive << KS_CPU_EXCL_SHIFT | numCPUsNeeded << 8
-  int64_t h_cpu, h_mem;  // 100 x the Requested cpu / memory (NodeNUMAResource score)
-  float f_cpu, f_mem;
+  int32_t _pad1;
+  double h_cpu, h_mem;  // 100 x the Requested cpu / memory (NodeNUMAResource score)
   int64_t gpu_core, gpu_mem, gpu_ratio;  // DeviceShare: converted GPU request
   int64_t rdma;                          // DeviceShare: koordinator.sh/rdma request
   uint32_t joint;                        // DeviceShare: KS_JOINT_*
   int32_t _pad0;
 };
-static_assert(sizeof(PodRec) == 288, "PodRec layout");
+static_assert(sizeof(PodRec) == 240, "PodRec layout");
 // PodRec int64 word indices read by the commit kernel's lane-parallel Reserve
 constexpr int kPodWordHCpu = (int)(offsetof(PodRec, h_cpu) / 8), kPodWordHMem = (int)(offsetof(PodRec, h_mem) / 8);
 static_assert(offsetof(PodRec, h_nzcpu) == 12 * 8 && offsetof(PodRec, h_sc) == 17 * 8, "PodRec word layout");
@@ -181,13 +183,12 @@ struct DevQuotas {
   int64_t *limit, *used, *min, *npused;  // [q][KS_QUOTA_DIMS]
 };
 
-// One score term's node side: capacity c, headroom h = c - requested_on_node, and the derived
-// 100*h, f32(h), 100/c used by term_least / term_most.  For c == 0 the headroom is offset by
-// -2^62 so the term scores 0 without a branch (leastRequestedScore's capacity == 0 case) while
-// the requested value stays recoverable (term_requested).
+// One score term's node side: capacity c and headroom h = c - requested_on_node (offset by -2^62 when
+// c == 0, so the int64 path scores 0 without a branch while the requested value stays recoverable,
+// term_requested), and for the f64 path hd = 100*h and r = 1/c (both 0 when c == 0).
 struct Term {
-  int64_t c, h, h100;
-  float fh, rcp;
+  int64_t c, h;
+  double hd, r;
 };
 
 __device__ __forceinline__ float i64_to_f32(int64_t v) {
@@ -204,52 +205,54 @@ __device__ __forceinline__ int32_t pct_floor_i64(int64_t num, int64_t cap) {
   return q;
 }
 
-__device__ __forceinline__ float rcp100(int64_t cap) {
-  // ~100 / cap in f32 (v_rcp_f32, 1 ulp); cap == 0 never reaches a divide (guarded by callers).
-  return cap > 0 ? 100.0f * __builtin_amdgcn_rcpf(i64_to_f32(cap)) : 0.0f;
-}
-
 constexpr int64_t kNoCap = -((int64_t)1 << 62);
+// f64 score path limits (term_least): capacities below kBigCap, requests below kBigReq
+constexpr int64_t kBigCap = (int64_t)1 << 43;
+constexpr int64_t kBigReq = (int64_t)1 << 46;
+constexpr double kScoreBias = 0x1p-44;
 
 __device__ __forceinline__ void term_set(Term& t, int64_t cap, int64_t requested) {
   t.c = cap;
   t.h = cap - requested + (cap != 0 ? 0 : kNoCap);
-  t.h100 = cap != 0 ? (cap - requested) * 100 : 0;
-  t.fh = i64_to_f32(t.h);
-  t.rcp = rcp100(cap);
+  t.hd = cap != 0 ? (double)(cap - requested) * 100.0 : 0.0;
+  t.r = cap != 0 ? 1.0 / (double)cap : 0.0;
 }
 
 __device__ __forceinline__ int64_t term_requested(const Term& t) { return t.c - t.h + (t.c != 0 ? 0 : kNoCap); }
 
-// Reserve: the node's requested grows by r (x100 and f32 copies kept in step).
-__device__ __forceinline__ void term_take(Term& t, int64_t r, int64_t r100) {
+// Reserve: the node's requested grows by r (rd = 100 r as f64).
+__device__ __forceinline__ void term_take(Term& t, int64_t r, double rd) {
   t.h -= r;
-  t.h100 -= r100;
-  t.fh = i64_to_f32(t.h);
+  t.hd -= rd;
 }
 
 // leastRequestedScore(requested = c - h + p, c) (load_aware.go:388-397, least_allocated.go:45-54):
-// 0 if c == 0 or requested > c, else floor((h - p) * 100 / c).  The quotient is estimated in f32
-// (|error| < 1e-4 for 0 <= h - p <= c < 2^56, so the truncated estimate is within one of the
-// floor) and corrected exactly with r = 100(h - p) - q c in int64.  Branch-free.
-__device__ __forceinline__ int32_t term_least(const Term& t, int64_t p, int64_t p100, float fp) {
-  int32_t q = (int32_t)((t.fh - fp) * t.rcp);
-  const int64_t r = t.h100 - (p100 + (int64_t)q * t.c);
-  q += (r >= t.c) ? 1 : 0;
-  q -= (r < 0) ? 1 : 0;
-  return (t.h >= p) ? q : 0;
+// 0 if c == 0 or requested > c, else floor(100 (h - p) / c).
+// f64 path: x = fma(100 (h - p), r, B) with r = fl(1/c), B = 2^-44, then trunc(max(x, 0)).  100(h-p) is an
+// exact f64 integer (100|h|, 100 p < 2^53).  For 0 <= h - p <= c the exact quotient x* lies in [0, 100] and
+// |x - (x* + B)| <= |100(h-p)| |r - 1/c| + ulp(x)/2 <= 100 * 2^-53 + 2^-47 < 2^-45, so an integral x*
+// truncates to itself (x >= x* + B - 2^-45 > x*), and a non-integral one is at least 1/c > 2^-43 below the
+// next integer (c < 2^43), which B + 2^-45 < 2^-43 cannot cross.  For h < p, x* <= -100/c and x < 1, so the
+// result is 0.  tests/test_score_f64.py replays the formula on the boundary cases with exact rational
+// arithmetic.
+__device__ __forceinline__ int32_t term_least(const Term& t, double pd) {
+  return (int32_t)fmax(fma(t.hd - pd, t.r, kScoreBias), 0.0);
+}
+__device__ __forceinline__ int32_t term_least_i64(const Term& t, int64_t p) {
+  return t.h >= p ? pct_floor_i64(t.h - p, t.c) : 0;
 }
 
 // mostRequestedScore(requested, c) (most_allocated.go:50-62): requested clamped to c, then
-// floor(requested * 100 / c); requested = c - (h - p).
-__device__ __forceinline__ int32_t term_most(const Term& t, int64_t p, int64_t p100, float fp) {
-  const bool over = p > t.h;  // requested > capacity: clamp -> 100
-  const int64_t d100 = t.c * 100 - (t.h100 - p100);
-  int32_t q = (int32_t)((i64_to_f32(t.c) - (t.fh - fp)) * t.rcp);
-  const int64_t r = d100 - (int64_t)q * t.c;
-  q += (r >= t.c) ? 1 : 0;
-  q -= (r < 0) ? 1 : 0;
-  return t.c == 0 ? 0 : (over ? 100 : q);
+// floor(requested * 100 / c); requested = c - (h - p).  f64 path: y = fma(100 (p - h), r, 100 + B), exact by
+// the same argument (y* = 100 requested / c >= 0), clamped to 100 for requested > c; 0 when c == 0.
+__device__ __forceinline__ int32_t term_most(const Term& t, double pd) {
+  const int32_t q = (int32_t)fmin(fma(pd - t.hd, t.r, 100.0 + kScoreBias), 100.0);
+  return t.r != 0.0 ? q : 0;
+}
+__device__ __forceinline__ int32_t term_most_i64(const Term& t, int64_t p) {
+  if (t.c == 0) return 0;
+  if (p > t.h) return 100;
+  return pct_floor_i64(t.c - (t.h - p), t.c);
 }
 
 // One node in registers, with node-only precomputation done once per load.
@@ -444,35 +447,54 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   o.hi = 0;
   o.numa_rs = 0;
   int32_t total = 0;
-  if (c.fit_score) {
+  // the score terms: the f64 path everywhere, then the int64 path for the lanes it does not cover
+  // (a divergent branch the wave skips when no lane needs it)
+  const bool exact64 = (r.la_bits & kNodeBigCap) || (p.flags & kPodBigReq);
+  auto fit_score = [&](auto least, auto most) -> int32_t {
     int32_t ns = 0, ws = r.fit_ws;
-    auto term = [&](int32_t w, const Term& t, int64_t pr, int64_t pr100, float fpr) {
+    auto term = [&](int32_t w, const Term& t, int64_t pr, double prd) {
       if (w != 0) {
-        const int32_t s = c.fit_most ? term_most(t, pr, pr100, fpr) : term_least(t, pr, pr100, fpr);
+        const int32_t s = c.fit_most ? most(t, pr, prd) : least(t, pr, prd);
         ns += (w == 1) ? s : s * w;
       }
     };
-    term(c.fw_cpu, r.t_cpu, p.nzcpu, p.h_nzcpu, p.f_nzcpu);
-    term(c.fw_mem, r.t_mem, p.nzmem, p.h_nzmem, p.f_nzmem);
-    term(c.fw_eph, r.t_eph, p.eph, p.h_eph, p.f_eph);
+    term(c.fw_cpu, r.t_cpu, p.nzcpu, p.h_nzcpu);
+    term(c.fw_mem, r.t_mem, p.nzmem, p.h_nzmem);
+    term(c.fw_eph, r.t_eph, p.eph, p.h_eph);
 #pragma unroll
     for (int k = 0; k < NSC; ++k) {
       if (p.sc[k] != 0 && c.fw_sc[k] != 0) {  // scalar skipped when the pod does not request it
-        term(c.fw_sc[k], r.t_sc[k], p.sc[k], p.h_sc[k], p.f_sc[k]);
+        term(c.fw_sc[k], r.t_sc[k], p.sc[k], p.h_sc[k]);
         ws += r.t_sc[k].c != 0 ? c.fw_sc[k] : 0;
       }
     }
-    o.fit = ws > 0 ? small_div(ns, ws > 0 ? ws : 1) : 0;
+    return ws > 0 ? small_div(ns, ws > 0 ? ws : 1) : 0;
+  };
+  const bool prod = (p.flags & KS_POD_PROD) && c.la_prod_usage;
+  const Term& tc = prod ? r.t_plcpu : r.t_lcpu;
+  const Term& tm = prod ? r.t_plmem : r.t_lmem;
+  auto la_score = [&](auto least) -> int32_t {
+    int32_t ns = 0;
+    if (c.lw_cpu) ns += least(tc, p.est_cpu, p.h_est_cpu) * c.lw_cpu;
+    if (c.lw_mem) ns += least(tm, p.est_mem, p.h_est_mem) * c.lw_mem;
+    return small_div(ns, c.lw_cpu + c.lw_mem);
+  };
+  auto least_f = [](const Term& t, int64_t, double pd) { return term_least(t, pd); };
+  auto most_f = [](const Term& t, int64_t, double pd) { return term_most(t, pd); };
+  auto least_i = [](const Term& t, int64_t pv, double) { return term_least_i64(t, pv); };
+  auto most_i = [](const Term& t, int64_t pv, double) { return term_most_i64(t, pv); };
+  int32_t fit = 0, la = 0;
+  if (c.fit_score) fit = fit_score(least_f, most_f);
+  if (c.la_score) la = la_score(least_f);
+  if (exact64) {
+    if (c.fit_score) fit = fit_score(least_i, most_i);
+    if (c.la_score) la = la_score(least_i);
+  }
+  if (c.fit_score) {
+    o.fit = fit;
     total += o.fit * c.fit_pw;
   }
   if (c.la_score) {
-    const bool prod = (p.flags & KS_POD_PROD) && c.la_prod_usage;
-    const Term& tc = prod ? r.t_plcpu : r.t_lcpu;
-    const Term& tm = prod ? r.t_plmem : r.t_lmem;
-    int32_t ns = 0;
-    if (c.lw_cpu) ns += term_least(tc, p.est_cpu, p.h_est_cpu, p.f_est_cpu) * c.lw_cpu;
-    if (c.lw_mem) ns += term_least(tm, p.est_mem, p.h_est_mem, p.f_est_mem) * c.lw_mem;
-    const int32_t la = small_div(ns, c.lw_cpu + c.lw_mem);
     o.la = (r.la_bits & kLaZeroScore) ? 0 : la;
     total += o.la * c.la_pw;
   }
@@ -496,12 +518,11 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
     if (p.cpu % 1000 != 0) rs = KS_R_NUMA_INVALID_CPUS;
     else bind = true;
   }
-  int64_t pc = p.cpu, pc100 = p.h_cpu;
-  float pcf = p.f_cpu;
+  int64_t pc = p.cpu;
+  double pcd = p.h_cpu;
   if (bind && (r.la_bits & kNumaAmp)) {
     pc = (int64_t)::ceil((double)p.cpu * r.numa_ratio);  // extension.Amplify
-    pc100 = pc * 100;
-    pcf = i64_to_f32(pc);
+    pcd = (double)(pc * 100);
   }
   if (rs == 0 && p.cpu != 0) {
     if (r.la_bits & kNumaInvalid) {
@@ -534,16 +555,19 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
   o.reasons |= DEBUG ? rs : (rs ? KS_R_FIT_PODS : 0u);
   o.numa_rs = rs;
   Term tc = r.t_ncpu;
-  if (p.cpu == 0) term_take(tc, -r.numa_off, -r.numa_off * 100);  // a cpu-less pod scores the plain Requested
+  if (p.cpu == 0) term_take(tc, -r.numa_off, (double)(-r.numa_off * 100));  // a cpu-less pod scores the plain Requested
   int32_t ns = 0, ws = 0;
-  if (c.nw_cpu && tc.c != 0) {
-    ns += (c.numa_most ? term_most(tc, pc, pc100, pcf) : term_least(tc, pc, pc100, pcf)) * c.nw_cpu;
-    ws += c.nw_cpu;
-  }
-  if (c.nw_mem && r.t_nmem.c != 0) {
-    ns += (c.numa_most ? term_most(r.t_nmem, p.mem, p.h_mem, p.f_mem) : term_least(r.t_nmem, p.mem, p.h_mem, p.f_mem)) *
-          c.nw_mem;
-    ws += c.nw_mem;
+  if (c.nw_cpu && tc.c != 0) ws += c.nw_cpu;
+  if (c.nw_mem && r.t_nmem.c != 0) ws += c.nw_mem;
+  const bool exact64 = (r.la_bits & kNodeBigCap) || (p.flags & kPodBigReq) || pc >= kBigReq;
+  if (c.nw_cpu && tc.c != 0) ns += (c.numa_most ? term_most(tc, pcd) : term_least(tc, pcd)) * c.nw_cpu;
+  if (c.nw_mem && r.t_nmem.c != 0)
+    ns += (c.numa_most ? term_most(r.t_nmem, p.h_mem) : term_least(r.t_nmem, p.h_mem)) * c.nw_mem;
+  if (exact64) {
+    ns = 0;
+    if (c.nw_cpu && tc.c != 0) ns += (c.numa_most ? term_most_i64(tc, pc) : term_least_i64(tc, pc)) * c.nw_cpu;
+    if (c.nw_mem && r.t_nmem.c != 0)
+      ns += (c.numa_most ? term_most_i64(r.t_nmem, p.mem) : term_least_i64(r.t_nmem, p.mem)) * c.nw_mem;
   }
   o.numa = ws > 0 ? small_div(ns, ws) : 0;
   o.total += o.numa * c.numa_pw;

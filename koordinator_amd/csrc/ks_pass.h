@@ -456,6 +456,18 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   do {              \
   } while (0)
 #endif
+#ifdef KS_COMMIT_CAT
+  // diagnostic build: whole-iteration cycles per pod category (0 quota-rejected, 1 fast, 2 slow onto a new slot,
+  // 3 slow onto a touched slot, 4 unschedulable) in diag[0..4]; counts of categories 2 and 3 in diag[5..6]
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t tcat = __builtin_amdgcn_s_memtime();
+  int32_t cat = 0;
+#define KS_CAT(c) cat = (c)
+#else
+#define KS_CAT(c) \
+  do {            \
+  } while (0)
+#endif
 
   // ---- load the pass into LDS with all four waves (independent loads, one burst) ----
   for (int32_t i = tid; i < np * K; i += kCommitThreads) {
@@ -532,6 +544,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   // ---- per-lane roles in slot construction and Reserve: lane t < ST_N owns slot term t ----
   // capacity / requested raw fields, the PodRec words of its Reserve delta (x1, x100), and whether a
   // zero capacity disables the term (score terms) or not (headrooms)
+  // (t_pw100: the PodRec word of 100 x the request as f64; headroom lanes only use .h, so theirs is a dummy)
   int32_t t_cap = 0, t_req = 0, t_pw = 0, t_pw100 = 0;
   int32_t t_rdim = -1;  // reservation restore dimension of the lane's term: 0..6 Requested, 8/9 NonZero cpu/memory
   bool t_prod_only = false, t_score = true;
@@ -638,10 +651,14 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   };
   lookahead(0);
   KS_STAMP(1);
+#ifdef KS_COMMIT_CAT
+  tcat = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int32_t j = 0; j < np; ++j) {
     const uint32_t st = st_next;
     const Cands cj = cn;
+    KS_CAT(0);
     if (st) {
       if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0, 0, 0};
       goto next_pod;
@@ -652,6 +669,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     if (cj.fast) {
       best = cj.umax;  // the snapshot-best node is untouched: commits only lower keys, so it wins
       ++fast;
+      KS_CAT(1);
       KS_STAMP(2);
     } else {
       // pod j: LDS broadcast into VGPRs; flags scalar so the plugin branches stay wave-uniform
@@ -740,6 +758,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       KS_STAMP(3);
     }
     if (best == 0) {
+      KS_CAT(4);
       if (lane == 0) sres[j] = ks_result{-1, KS_S_UNSCHEDULABLE, 0, -1, 0, 0, 0};
       goto next_pod;
     }
@@ -768,6 +787,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const int32_t pcls = (RSV && cfg.rsv) ? __builtin_amdgcn_readfirstlane(spods[j].rsv_class) : -1;
     bool rsvc = false;
     if (s < 0) {
+      if (!cj.fast) KS_CAT(2);
       s = nslots++;
       row = &rows[s];
       const int64_t* src = raw;
@@ -872,9 +892,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         Term t;
         t.c = cap;
         t.h = cap - req + ((cap != 0 || !t_score) ? 0 : kNoCap);
-        t.h100 = cap != 0 ? (cap - req) * 100 : 0;
-        t.fh = i64_to_f32(t.h);
-        t.rcp = rcp100(cap);
+        t.hd = cap != 0 ? (double)(cap - req) * 100.0 : 0.0;
+        t.r = cap != 0 ? 1.0 / (double)cap : 0.0;
         row->t[lane] = t;
       } else if (lane == kLaneCounts) {
         row->la_bits = (uint32_t)u_bits;
@@ -883,6 +902,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         row->fit_ws = (u_acpu != 0 ? cfg.fw_cpu : 0) + (u_amem != 0 ? cfg.fw_mem : 0) + (u_aeph != 0 ? cfg.fw_eph : 0);
       }
     } else {
+      KS_CAT(3);
       if (cpubind && (int32_t)snuma[4 * s + 3] < cpu_need) {
         if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0, 0, 0};
         goto next_pod;
@@ -891,7 +911,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       rsvc = pcls >= 0 && pcls < 64 && ((scls[s] >> pcls) & 1ull);
       const bool take = !rsvc && (!t_prod_only || (pflags & KS_POD_PROD));
       if (lane < ST_N) {
-        if (take) term_take(row->t[lane], podw[t_pw], podw[t_pw100]);
+        if (take) term_take(row->t[lane], podw[t_pw], __longlong_as_double(podw[t_pw100]));
       } else if (lane == kLaneCounts) {
         if (!rsvc) row->pod_count += 1;
       }
@@ -969,7 +989,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       const bool take = !t_prod_only || (pflags & KS_POD_PROD);
       if (lane < ST_N) {
         const int64_t v = (take ? podw[t_pw] : 0) + dd;
-        const int64_t v100 = (take ? podw[t_pw100] : 0) + dd * 100;
+        const double v100 = (take ? __longlong_as_double(podw[t_pw100]) : 0.0) + (double)dd * 100.0;
         if (take || dd != 0) term_take(row->t[lane], v, v100);
       } else if (lane == kLaneCounts) {
         row->pod_count += 1;
@@ -1097,7 +1117,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       const double ratio = __longlong_as_double(snuma[4 * s + 2]);
       const int64_t A1 = A0 + (int64_t)cpu_need * 1000;
       const int64_t off1 = ratio > 1.0 ? (int64_t)::ceil((double)A1 * ratio) - A1 : 0;
-      if (lane == ST_NCPU) term_take(row->t[ST_NCPU], off1 - off0, (off1 - off0) * 100);
+      if (lane == ST_NCPU) term_take(row->t[ST_NCPU], off1 - off0, (double)(off1 - off0) * 100.0);
       if (lane == 0) {
         snuma[4 * s] = A1;
         snuma[4 * s + 1] = off1;
@@ -1138,6 +1158,15 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   next_pod:
     if (j + 1 < np) lookahead(j + 1);
     KS_STAMP(1);
+#ifdef KS_COMMIT_CAT
+    {
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();
+      ph[cat] += t_ - tcat;
+      tcat = t_;
+      if (cat == 2) ph[5] += 1;
+      if (cat == 3) ph[6] += 1;
+    }
+#endif
   }
   KS_STAMP(6);
   // ---- write back: results, touched rows, quota usage ----
@@ -1178,11 +1207,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     atomicAdd(&a.counters[2], (unsigned long long)rescans);
     atomicAdd(&a.counters[3], (unsigned long long)misses);
     atomicAdd(&a.counters[15], (unsigned long long)fast);  // ks_stats.diag[7]: monotone fast picks
-#ifdef KS_COMMIT_STAMPS
+#if defined(KS_COMMIT_STAMPS) || defined(KS_COMMIT_CAT)
     for (int i = 0; i < 7; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
 #endif
   }
 #undef KS_STAMP
+#undef KS_CAT
 }
 
 // ---- host launch wrappers (one set per (FEAT, NSC) translation unit of ks_variant.hip) ----
@@ -1190,6 +1220,9 @@ struct PassLaunch {
   hipError_t (*sweep)(int blocks, hipStream_t s, const SweepArgs& a);
   hipError_t (*commit)(bool qc, size_t smem, hipStream_t s, const CommitArgs& a);
   hipError_t (*commit_attr)(bool qc, size_t smem);
+  // FEAT 0 only (else null): the monotone commit kernel (ks_mono.h)
+  hipError_t (*commit_mono)(bool qc, size_t smem, hipStream_t s, const CommitArgs& a);
+  hipError_t (*commit_mono_attr)(bool qc, size_t smem);
 };
 #define KS_DECLARE_VARIANT(F) PassLaunch pass_launch_f##F##_n0(); PassLaunch pass_launch_f##F##_n2(); PassLaunch pass_launch_f##F##_n4();
 KS_DECLARE_VARIANT(0)

@@ -268,16 +268,16 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
   r.free_cpu -= sign * dl.dreq[0];
   r.free_mem -= sign * dl.dreq[1];
   r.free_eph -= sign * dl.dreq[2];
-  term_take(r.t_eph, sign * dl.dreq[2], sign * dl.dreq[2] * 100);
+  term_take(r.t_eph, sign * dl.dreq[2], (double)(sign * dl.dreq[2]) * 100.0);
 #pragma unroll
   for (int k = 0; k < NSC; ++k) {
     r.free_sc[k] -= sign * dl.dreq[3 + k];
-    term_take(r.t_sc[k], sign * dl.dreq[3 + k], sign * dl.dreq[3 + k] * 100);
+    term_take(r.t_sc[k], sign * dl.dreq[3 + k], (double)(sign * dl.dreq[3 + k]) * 100.0);
   }
-  term_take(r.t_cpu, sign * dl.dnz[0], sign * dl.dnz[0] * 100);
-  term_take(r.t_mem, sign * dl.dnz[1], sign * dl.dnz[1] * 100);
-  term_take(r.t_ncpu, sign * dl.dreq[0], sign * dl.dreq[0] * 100);
-  term_take(r.t_nmem, sign * dl.dreq[1], sign * dl.dreq[1] * 100);
+  term_take(r.t_cpu, sign * dl.dnz[0], (double)(sign * dl.dnz[0]) * 100.0);
+  term_take(r.t_mem, sign * dl.dnz[1], (double)(sign * dl.dnz[1]) * 100.0);
+  term_take(r.t_ncpu, sign * dl.dreq[0], (double)(sign * dl.dreq[0]) * 100.0);
+  term_take(r.t_nmem, sign * dl.dreq[1], (double)(sign * dl.dreq[1]) * 100.0);
   r.pod_count -= (int32_t)sign * dl.nm;
   r.pods_full = ((int64_t)r.pod_count + 1 > (int64_t)r.allowed) || !r.valid;
 }

@@ -1,6 +1,7 @@
 // ks_variant.hip — one plugin-set (FEAT = KS_FEAT) x scalar-slot (NSC = KS_NSC) variant of the pass kernels (ks_pass.h) and its host launch
 // wrappers.  The Makefile compiles this file once per (FEAT, NSC) so the variants build in parallel.
 #include "ks_pass.h"
+#include "ks_mono.h"
 
 #if !defined(KS_FEAT) || !defined(KS_NSC)
 #error "compile with -DKS_FEAT=<feature bits> -DKS_NSC=<0|2|4>"
@@ -32,8 +33,28 @@ hipError_t commit_attr(bool qc, size_t smem) {
   return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
 }
 
+#if KS_FEAT == 0
+// the monotone Fit + LoadAware [+ ElasticQuota] commit (ks_mono.h)
+hipError_t commit_mono(bool qc, size_t smem, hipStream_t s, const CommitArgs& a) {
+  if (qc) hipLaunchKernelGGL((commit_mono_kernel<NSC, true>), dim3(1), dim3(kCommitThreads), smem, s, a);
+  else hipLaunchKernelGGL((commit_mono_kernel<NSC, false>), dim3(1), dim3(kCommitThreads), smem, s, a);
+  return hipGetLastError();
+}
+
+hipError_t commit_mono_attr(bool qc, size_t smem) {
+  const void* fn = qc ? (const void*)commit_mono_kernel<NSC, true> : (const void*)commit_mono_kernel<NSC, false>;
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+}
+#endif
+
 }  // namespace
 
-PassLaunch KS_CAT(KS_CAT(KS_CAT(pass_launch_f, KS_FEAT), _n), KS_NSC)() { return PassLaunch{sweep, commit, commit_attr}; }
+PassLaunch KS_CAT(KS_CAT(KS_CAT(pass_launch_f, KS_FEAT), _n), KS_NSC)() {
+#if KS_FEAT == 0
+  return PassLaunch{sweep, commit, commit_attr, commit_mono, commit_mono_attr};
+#else
+  return PassLaunch{sweep, commit, commit_attr, nullptr, nullptr};
+#endif
+}
 
 }  // namespace ks
