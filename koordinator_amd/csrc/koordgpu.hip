@@ -209,13 +209,23 @@ struct SelectArgs {
 };
 
 
-// One wave per pod: the pod's row of chunk keys is staged in LDS once (coalesced), then the K-th
-// largest chunk score is found from an LDS histogram (binary search over the LDS copy when the
-// score range exceeds the histogram).
+// One workgroup of four waves per pod.  The pod's row of chunk keys is staged in LDS once: every thread
+// issues up to kSelUnroll independent loads before the first wait, so at C5 (1,563 chunks) the row arrives
+// in about one HBM round trip instead of one per 64 chunks (one wave walking the row was latency-bound:
+// 18.8 us per launch).  All four waves build an LDS histogram of the chunk scores; wave 0 finds the K-th
+// largest score from it (binary search over the LDS copy when the score range exceeds the histogram) and
+// writes the candidate list in chunk order.
 constexpr int kSelHistBins = 1024;
-__global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
+constexpr int kSelThreads = 256;
+constexpr int kSelUnroll = 8;
+constexpr size_t kSelScratch = 128;  // cross-wave partials after the histogram
+__host__ __device__ inline size_t select_smem(int64_t nc) { return (size_t)nc * sizeof(uint2) + kSelHistBins * 4 + kSelScratch; }
+
+__global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint2 srow[];  // [nchunks]
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
@@ -224,38 +234,66 @@ __global__ __launch_bounds__(64) void select_kernel(SelectArgs a) {
   const int32_t K = a.k;
   const int64_t nc = a.c1 - a.c0;  // LDS row index e <-> chunk c0 + e
   const uint2* in = a.in + (size_t)p * a.nchunks + a.c0;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(srow + nc);
+  uint64_t* xw = reinterpret_cast<uint64_t*>(hist + kSelHistBins);  // [0..3] top, [4..7] cnt | hmax << 32, [8] t | need_eq << 32
   int32_t cnt = 0;
   uint32_t hmax = 0;
   uint64_t top = 0;
-  for (int64_t e = lane; e < nc; e += 64) {
-    const uint2 loc = in[e];
-    srow[e] = loc;
-    const uint32_t h = loc.x >> 6;
-    cnt += h != 0;
-    hmax = h > hmax ? h : hmax;
-    top = umax64(top, local_gkey(loc.x, a.c0 + e));
+  for (int i = tid; i < kSelHistBins; i += kSelThreads) hist[i] = 0u;
+  for (int64_t e0 = tid; e0 < nc; e0 += (int64_t)kSelThreads * kSelUnroll) {
+    uint2 v[kSelUnroll];
+#pragma unroll
+    for (int u = 0; u < kSelUnroll; ++u) {
+      const int64_t e = e0 + (int64_t)u * kSelThreads;
+      v[u] = e < nc ? in[e] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < kSelUnroll; ++u) {
+      const int64_t e = e0 + (int64_t)u * kSelThreads;
+      if (e < nc) {
+        srow[e] = v[u];
+        const uint32_t h = v[u].x >> 6;
+        cnt += h != 0;
+        hmax = h > hmax ? h : hmax;
+        top = umax64(top, local_gkey(v[u].x, a.c0 + e));
+      }
+    }
   }
-  __syncthreads();
   cnt = wave_sum_i32(cnt);
   hmax = wave_max_u32(hmax);
   top = wave_max_u64(top);
+  if (lane == 0) {
+    xw[wv] = top;
+    xw[4 + wv] = (uint64_t)(uint32_t)cnt | ((uint64_t)hmax << 32);
+  }
+  __syncthreads();
+  cnt = 0;
+  hmax = 0;
+  top = 0;
+#pragma unroll
+  for (int w = 0; w < kSelThreads / 64; ++w) {
+    top = umax64(top, xw[w]);
+    cnt += (int32_t)(uint32_t)xw[4 + w];
+    const uint32_t hm = (uint32_t)(xw[4 + w] >> 32);
+    hmax = hm > hmax ? hm : hmax;
+  }
   uint32_t t = 1;  // admit h >= t
   int32_t need_eq = 0x7fffffff;
   const bool exhaustive = cnt <= K;
+  const bool use_hist = !exhaustive && hmax < kSelHistBins;
+  if (use_hist) {
+    // histogram of chunk scores (LDS atomics from all four waves)
+    for (int64_t e = tid; e < nc; e += kSelThreads) {
+      const uint32_t h = srow[e].x >> 6;
+      if (h) atomicAdd(&hist[h], 1u);
+    }
+    __syncthreads();
+  }
+  if (wv != 0) return;  // waves 1-3 are done
   if (!exhaustive) {
-    if (hmax < kSelHistBins) {
-      // histogram of chunk scores (LDS atomics), then the largest t with count(h >= t) >= K by a
-      // suffix scan over the bins (lane l owns bins [l*B, l*B+B))
-      uint32_t* hist = reinterpret_cast<uint32_t*>(srow + nc);
+    if (use_hist) {
+      // the largest t with count(h >= t) >= K by a suffix scan over the bins (lane l owns bins [l*B, l*B+B))
       constexpr int B = kSelHistBins / 64;
-#pragma unroll
-      for (int i = 0; i < B; ++i) hist[lane * B + i] = 0u;
-      __syncthreads();
-      for (int64_t e = lane; e < nc; e += 64) {
-        const uint32_t h = srow[e].x >> 6;
-        if (h) atomicAdd(&hist[h], 1u);
-      }
-      __syncthreads();
       uint32_t mine[B];
       uint32_t part = 0;
 #pragma unroll
@@ -2635,11 +2673,16 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
 }
 
 // The monotone commit kernel (ks_mono.h) runs the passes of a plugin set without Reservation, NodeNUMAResource or
-// DeviceShare whose keys commits can only lower (Fit LeastAllocated + LoadAware [+ ElasticQuota]) when its LDS
-// fits; KS_COMMIT_GENERAL=1 keeps the general kernel (A/B).  ks_assume always uses the general kernel.
+// DeviceShare whose keys commits can only lower (Fit LeastAllocated + LoadAware) when its LDS fits.  With
+// ElasticQuota the general kernel runs instead: its admission look-ahead for pod j + 1 overlaps pod j's Reserve,
+// and that measured faster than the mono kernel's prebuilt rows at C2 (MI355X, commit 20.6 vs 21.4 ms/step;
+// C5 without quota: mono 275.6 vs general 281.3 ms per 200k pods, profiles/r02_commit_ab.txt).
+// KS_COMMIT_GENERAL=1 keeps the general kernel, =2 forces the mono kernel with quota too (A/B).  ks_assume always
+// uses the general kernel.
 static bool mono_commit(const ks_ctx* ctx, bool qcache, size_t* smem) {
-  static const bool general = env_i64("KS_COMMIT_GENERAL", 0, 0, 1) != 0;
-  if (general || kernel_feat(ctx) != 0 || !ctx->kc.monotone || ctx->kc.fit_most) return false;
+  static const int64_t mode = env_i64("KS_COMMIT_GENERAL", 0, 0, 2);
+  if (mode == 1 || kernel_feat(ctx) != 0 || !ctx->kc.monotone || ctx->kc.fit_most) return false;
+  if (mode == 0 && ctx->kc.quota_enable) return false;
   *smem = mono_layout(ctx->k, ctx->nchunks, qcache).total;
   return *smem <= 160 * 1024;
 }
@@ -2774,8 +2817,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
       se.cand_count = (int32_t*)(b + L.count);
       se.cand_total = (int32_t*)(b + L.total);
     }
-    hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(64),
-                       (size_t)(se.c1 - se.c0) * sizeof(uint2) + kSelHistBins * 4, ctx->stream, se);
+    hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(kSelThreads), select_smem(se.c1 - se.c0), ctx->stream, se);
   }
   if (S > 1) {
     if (ctx->nranks > 1) {
@@ -2829,7 +2871,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   {
     if (int rc = commit_attr_set(ctx); rc != KS_OK) return rc;
     hipError_t e = hipSuccess;
-    const size_t sel_smem = (size_t)ctx->nchunks * sizeof(uint2) + kSelHistBins * 4;
+    const size_t sel_smem = select_smem(ctx->nchunks);
     if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
     e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_smem);
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(select LDS %zu): %s", sel_smem, hipGetErrorString(e));

@@ -283,12 +283,15 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
     const int32_t p = i / kRoles, role = i - p * kRoles;
     if (top_node[p] >= 0) mono_build(cfg, rows[p], rawtop + p * 32, role, mono_role(role));
   }
+  // and the previous pod with the same top node (my_prev; -1: none), which bounds a run of fast pods
+  int32_t my_prev = -1;
   if (tid < 64) {
     const int32_t tn = top_node[lane];
     int32_t own = -1;
     for (int32_t q = 0; q < np; ++q) {
       const int32_t v = __builtin_amdgcn_readlane(tn, q);
       own = (own < 0 && v == tn) ? q : own;
+      my_prev = (q < lane && v == tn) ? q : my_prev;
     }
     top_owner[lane] = own;
   }
@@ -346,6 +349,56 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
 
   for (int32_t j = 0; j < np; ++j) {
     KS_MCAT(0);
+    if (!QC && !cfg.quota_enable) {
+      // ---- a run of fast pods, committed together ----
+      // Pods j, j+1, .. whose snapshot-best (top) nodes are untouched and distinct from each other's are all
+      // fast one after the other: each commit touches only its own top, so the next pod's top is still
+      // untouched and still wins.  Lane p tests pod p; the run ends at the first pod that fails (it takes the
+      // per-pod path below).  Their slots, touched bits, results and Reserves are independent of each other.
+      bool ok = false;
+      if (lane >= j && lane < np && my_top != 0ull && my_prev < j)
+        ok = !((touched[my_tn >> 6] >> (my_tn & 63)) & 1ull);
+      const uint64_t bad = ~__ballot(ok) & (~0ull << j);
+      const int32_t end = min(np, bad ? (int32_t)__ffsll((long long)bad) - 1 : 64);
+      const int32_t R = end - j;
+      if (R > 1) {
+        const bool in_run = lane >= j && lane < end;
+        if (in_run) {
+          atomicOr(&touched[my_tn >> 6], 1ull << (my_tn & 63));
+          sres[lane] = ks_result{my_tn, KS_S_SCHEDULED, gkey_score(my_top), -1, 0, 0, 0};
+        }
+        // slot nslots + k <- pod j + k (its top node and that node's prebuilt row)
+        const int32_t src = lane - nslots + j;
+        const int32_t tn_s = __shfl(my_tn, src & 63, 64), own_s = __shfl(my_own, src & 63, 64);
+        if (lane >= nslots && lane < nslots + R) {
+          snode = tn_s;
+          srow = own_s;
+        }
+        // Reserve: (pod, role) items, one per lane
+        // (the shuffles run with every lane active; only the store is predicated)
+        for (int32_t i0 = 0; i0 < R * kRoles; i0 += 64) {
+          const int32_t i = i0 + lane;
+          const int32_t k = min(i / kRoles, R - 1), role = i - k * kRoles;
+          const int32_t pj = j + k;
+          const int32_t ri = __shfl(my_own, pj, 64);
+          const uint32_t pf = (uint32_t)__shfl((int32_t)my_flags, pj, 64);
+          if (i < R * kRoles)
+            mono_reserve(rows[ri], reinterpret_cast<const int64_t*>(&spods[pj]), (pf & KS_POD_PROD) != 0, role,
+                         mono_role(role));
+        }
+        nslots += R;
+        fast += (uint32_t)R;
+        j = end - 1;
+#ifdef KS_COMMIT_CAT
+        {
+          const uint64_t t_ = __builtin_amdgcn_s_memtime();
+          ph[1] += t_ - tcat;
+          tcat = t_;
+        }
+#endif
+        continue;
+      }
+    }
     // ---- ElasticQuota admission (lane d = dimension d) and the fast check, their LDS reads issued together ----
     const uint64_t top = readlane64(my_top, j);
     const int32_t tn = top ? (int32_t)gkey_node(top) : 0;

@@ -1,8 +1,9 @@
 """GPU parity under forced launch shapes and commit-kernel choices.
 
 The sweep's grid-stride loop over (chunk, pod group) items must give the same candidates for any
-pods-per-wave and block count, and both commit kernels (the monotone one, ks_mono.h, and the general one,
-KS_COMMIT_GENERAL=1) must commit the same placements.  The overrides are read once per process, so each
+pods-per-wave and block count, and both commit kernels (the monotone one, ks_mono.h, the default for Fit +
+LoadAware without ElasticQuota; the general one, the default with ElasticQuota; KS_COMMIT_GENERAL=1 forces the
+general one, =2 the monotone one with ElasticQuota too) must commit the same placements.  The overrides are read once per process, so each
 shape runs in a child process: C2-shaped (ElasticQuota), C4-shaped (Reservation) and C3-shaped
 (DeviceShare with hints, cpuset pods, NUMA-policy nodes: the phase-1 DeviceShare cache has its own
 pods-per-wave output mapping) clusters, checked bit-exact against the CPU oracle.
@@ -25,6 +26,7 @@ from oracle.oracle import Oracle
 
 which = os.environ["SHAPE_WORKLOADS"].split(",")
 make = {"c2": lambda: synth.c2(n_nodes=900, n_pods=384),
+        "c1": lambda: synth.c1(n_pods=384),
         "c4": lambda: synth.c4(n_nodes=700, n_reservations=1500, n_pods=256),
         "c3": lambda: synth.c3(n_nodes=400, n_pods=320)}
 for name in which:
@@ -67,8 +69,17 @@ def test_sweep_shape_invariant_deviceshare(ppw, cap):
 
 @pytest.mark.parametrize("ppw", [0, 3])
 def test_general_commit_kernel_matches(ppw):
-    # the monotone plugin set (C2) through the general commit kernel instead of ks_mono.h
+    # the monotone plugin set without quota (C1, ks_mono.h by default) through the general commit kernel
     extra = {"KS_COMMIT_GENERAL": "1"}
+    if ppw:
+        extra["KS_SWEEP_PPW"] = str(ppw)
+    _run(extra, ["c1"])
+
+
+@pytest.mark.parametrize("ppw", [0, 3])
+def test_mono_commit_kernel_with_quota_matches(ppw):
+    # the monotone plugin set with ElasticQuota (C2, the general kernel by default) through ks_mono.h
+    extra = {"KS_COMMIT_GENERAL": "2"}
     if ppw:
         extra["KS_SWEEP_PPW"] = str(ppw)
     _run(extra, ["c2"])

@@ -26,3 +26,7 @@ if [ -f koordinator_amd/libkoordgpu_cat.so ]; then
     cat $OUT/cat_$C.txt
   done
 fi
+if [ -f koordinator_amd/libkoordgpu_cat.so ] && [ -n "$ITER_C3" ]; then
+  timeout -k 10 200 python -u tools/diag_commit.py c3 --cat > $OUT/cat_c3.txt 2>&1 || { echo "cat c3 failed"; tail -20 $OUT/cat_c3.txt; exit 1; }
+  cat $OUT/cat_c3.txt
+fi
