@@ -314,10 +314,14 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         commit_s = agg["commit_ms"] / 1000.0
         pods_per_launch = n_pods * steps / passes
         c_algo = int(round(pods_per_launch * 138))
-        c_traffic, c_src = pmc_traffic(cfg_key, "commit_kernel")
+        # Fit + LoadAware without ElasticQuota / Reservation / NUMA / DeviceShare: the monotone commit kernel
+        # (ks_mono.h, fast-pod runs); otherwise the general one (koordgpu.hip mono_commit)
+        mono = all(x is None for x in (w.quotas, w.reservations, w.devices, w.cpus, w.numa_nodes))
+        c_kernel = "commit_mono_kernel" if mono else "commit_kernel"
+        c_traffic, c_src = pmc_traffic(cfg_key, c_kernel)
         step_kernels = agg["sweep_ms"] + agg["select_ms"] + agg["commit_ms"]
         roof["commit"] = {
-            "kernel": "commit_kernel", "bound": "latency (one wave walks the pass's pods in queue order)",
+            "kernel": c_kernel, "bound": "latency (one wave walks the pass's pods in queue order)",
             "avg_launch_us": round(commit_s / passes * 1e6, 3), "pods_per_launch": round(pods_per_launch, 2),
             "cycles_per_pod": round(commit_s * GPU_CLOCK_GHZ * 1e9 / (n_pods * steps), 1),
             "share_of_kernel_time": round(agg["commit_ms"] / step_kernels, 4) if step_kernels else None,
