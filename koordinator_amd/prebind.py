@@ -1,0 +1,149 @@
+"""PreBind write-back: the annotations koord-scheduler's PreBind writes, materialised from what
+ks_schedule / ks_assume return (ks_result.node / reservation / gpu_minors / rdma_minors, ks_fetch_cpusets,
+ks_fetch_numa_alloc).  The Go shim writes the same strings with the reference's own helpers; this module is the
+host-side mirror the tests and the Python callers use.
+
+* NodeNUMAResource PreBind (``nodenumaresource/plugin.go:439-478``): ``scheduling.koordinator.sh/resource-status``
+  = ``json.Marshal(ResourceStatus)`` (``apis/extension/numa_aware.go:71-82``, ``SetResourceStatus`` :232-248):
+  ``cpuset`` (Linux CPU list, omitted when empty) and ``numaNodeResources`` (per allocated NUMA node, omitted when
+  none).
+* DeviceShare PreBind (``deviceshare/plugin.go:490-503``): ``scheduling.koordinator.sh/device-allocated`` =
+  ``json.Marshal(DeviceAllocations)`` (``apis/extension/device_share.go:151-165``), one entry per allocated minor
+  holding the per-instance request (``devicehandler_gpu.go:56-63``: gpu-core and gpu-memory-ratio DecimalSI,
+  gpu-memory BinarySI; ``devicehandler_default.go:58``: rdma DecimalSI).
+* Reservation PreBind: ``scheduling.koordinator.sh/reservation-allocated`` = ``{"name": .., "uid": ..}``.
+
+Go's ``encoding/json`` sorts map keys and writes no spaces; Kubernetes ``resource.Quantity`` marshals as its
+canonical string (``Quantity.String``), restated in ``quantity_string``.
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+ANNOTATION_RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
+ANNOTATION_DEVICE_ALLOCATED = "scheduling.koordinator.sh/device-allocated"
+ANNOTATION_RESERVATION_ALLOCATED = "scheduling.koordinator.sh/reservation-allocated"
+
+RESOURCE_GPU_CORE = "koordinator.sh/gpu-core"
+RESOURCE_GPU_MEMORY = "koordinator.sh/gpu-memory"
+RESOURCE_GPU_MEMORY_RATIO = "koordinator.sh/gpu-memory-ratio"
+RESOURCE_RDMA = "koordinator.sh/rdma"
+
+_DEC_SUFFIX = {-3: "m", 0: "", 3: "k", 6: "M", 9: "G", 12: "T", 15: "P", 18: "E"}
+_BIN_SUFFIX = ["", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"]
+
+
+def quantity_string(value: int, fmt: str = "DecimalSI", milli: bool = False) -> str:
+    """Canonical ``resource.Quantity`` string of an integer amount (``value`` in units, or in thousandths with
+    ``milli``), as ``Quantity.String`` / ``CanonicalizeBytes`` print it (k8s.io/apimachinery
+    pkg/api/resource/quantity.go): DecimalSI picks the largest power-of-1000 exponent (from m up to E) that leaves
+    an integral mantissa; BinarySI uses the largest power of 1024 that divides the value exactly, and prints as
+    DecimalSI when |value| < 1024 or the value is not a whole number of units."""
+    v = int(value)
+    if fmt == "BinarySI" and not (milli and v % 1000):
+        units = v // 1000 if milli else v
+        if abs(units) >= 1024:
+            e = 0
+            while e < len(_BIN_SUFFIX) - 1 and units % 1024 == 0 and units != 0:
+                units //= 1024
+                e += 1
+            return f"{units}{_BIN_SUFFIX[e]}"
+    if fmt not in ("DecimalSI", "BinarySI"):
+        raise ValueError(f"unsupported quantity format {fmt!r}")
+    # DecimalSI: mantissa * 10^exp with exp a multiple of 3, as large as keeps the mantissa integral
+    mant, exp = (v, -3) if milli else (v, 0)
+    if mant == 0:
+        return "0"
+    while exp < 18 and mant % 1000 == 0:
+        mant //= 1000
+        exp += 3
+    return f"{mant}{_DEC_SUFFIX[exp]}"
+
+
+def cpuset_string(cpus: Iterable[int]) -> str:
+    """``cpuset.CPUSet.String``: sorted CPU ids as a Linux list, runs of consecutive ids as ``a-b``."""
+    ids = sorted(set(int(c) for c in cpus))
+    out: List[str] = []
+    i = 0
+    while i < len(ids):
+        j = i
+        while j + 1 < len(ids) and ids[j + 1] == ids[j] + 1:
+            j += 1
+        out.append(str(ids[i]) if i == j else f"{ids[i]}-{ids[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def _marshal(obj) -> str:
+    return json.dumps(obj, separators=(",", ":"), sort_keys=True)
+
+
+def resource_status(cpus: Sequence[int] = (), numa_nodes: Sequence[Tuple[int, int, int]] = ()) -> str:
+    """resource-status annotation.  ``cpus``: the pod's CPU ids (``ks_fetch_cpusets``); ``numa_nodes``: per
+    allocated NUMA node ``(node, cpu_milli, memory_bytes)`` (``ks_fetch_numa_alloc``; zero amounts are left out of
+    the resource list, a node with neither is skipped).  Field order is the struct's (cpuset, numaNodeResources)."""
+    st: Dict[str, object] = {}
+    cs = cpuset_string(cpus)
+    if cs:
+        st["cpuset"] = cs
+    res = []
+    for node, cpu_milli, mem in numa_nodes:
+        rl = {}
+        if cpu_milli:
+            rl["cpu"] = quantity_string(cpu_milli, "DecimalSI", milli=True)
+        if mem:
+            rl["memory"] = quantity_string(mem, "BinarySI")
+        if rl:
+            res.append({"node": int(node), "resources": dict(sorted(rl.items()))})
+    if res:
+        st["numaNodeResources"] = res
+    # struct fields keep declaration order (json.Marshal of a struct); only the maps inside are sorted
+    return json.dumps(st, separators=(",", ":"))
+
+
+def _minors(mask: int) -> List[int]:
+    return [k for k in range(32) if (int(mask) >> k) & 1]
+
+
+def device_allocated(gpu_minors: int = 0, gpu_core: Optional[int] = None, gpu_memory: int = 0,
+                     gpu_memory_ratio: int = 0, rdma_minors: int = 0, rdma: int = 0) -> str:
+    """device-allocated annotation from the ``ks_result`` minor masks and the pod's per-instance request
+    (``devicehandler_gpu.go:56-63`` / ``devicehandler_default.go:58``: the request divided by the desired device
+    count; ``gpu_core`` None when the pod asked for no gpu-core).  Minors ascend within a type, as
+    ``sortDeviceResourcesByMinor`` leaves them; the type keys and resource names sort as Go's map marshalling
+    does."""
+    alloc: Dict[str, list] = {}
+    if gpu_minors:
+        rl = {RESOURCE_GPU_MEMORY: quantity_string(gpu_memory, "BinarySI"),
+              RESOURCE_GPU_MEMORY_RATIO: quantity_string(gpu_memory_ratio, "DecimalSI")}
+        if gpu_core is not None:
+            rl[RESOURCE_GPU_CORE] = quantity_string(gpu_core, "DecimalSI")
+        alloc["gpu"] = [{"minor": m, "resources": rl} for m in _minors(gpu_minors)]
+    if rdma_minors:
+        alloc["rdma"] = [{"minor": m, "resources": {RESOURCE_RDMA: quantity_string(rdma, "DecimalSI")}}
+                         for m in _minors(rdma_minors)]
+    return _marshal(alloc)
+
+
+def reservation_allocated(name: str, uid: str) -> str:
+    """reservation-allocated annotation (``apiext.ReservationAllocated``: name, uid in declaration order)."""
+    return json.dumps({"name": name, "uid": uid}, separators=(",", ":"))
+
+
+def prebind_annotations(result, cpus: Sequence[int] = (), numa_nodes: Sequence[Tuple[int, int, int]] = (),
+                        gpu_request: Optional[Tuple[Optional[int], int, int]] = None, rdma_request: int = 0,
+                        reservation: Optional[Tuple[str, str]] = None) -> Dict[str, str]:
+    """Every PreBind annotation of one scheduled pod: ``result`` is its ``ks_result`` row (a mapping or numpy
+    record with ``gpu_minors`` / ``rdma_minors``); ``gpu_request`` = (core or None, memory bytes, ratio) per
+    instance; ``reservation`` = (name, uid) of ``result.reservation``'s row when it is >= 0."""
+    out: Dict[str, str] = {}
+    if len(cpus) or len(numa_nodes):
+        out[ANNOTATION_RESOURCE_STATUS] = resource_status(cpus, numa_nodes)
+    gm, rm = int(result["gpu_minors"]), int(result["rdma_minors"])
+    if gm or rm:
+        core, mem, ratio = gpu_request if gpu_request is not None else (None, 0, 0)
+        out[ANNOTATION_DEVICE_ALLOCATED] = device_allocated(gm, core, mem, ratio, rm, rdma_request)
+    if reservation is not None:
+        out[ANNOTATION_RESERVATION_ALLOCATED] = reservation_allocated(*reservation)
+    return out
