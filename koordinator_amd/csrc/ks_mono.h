@@ -233,10 +233,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
 #endif
 
   // ---- prologue: the pass into LDS (all four waves, independent loads in one burst) ----
-  for (int32_t i = tid; i < np * K; i += kCommitThreads) {
-    cand_chunk[i] = a.cand_chunk[i];
-    cand_t[i] = a.cand_t[i];
-  }
+  lds_copy(cand_chunk, a.cand_chunk, np * K, tid);
+  lds_copy(cand_t, a.cand_t, np * K, tid);
   for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += kCommitThreads) {
     const int32_t p = i / KS_QUOTA_DIMS, dd = i - p * KS_QUOTA_DIMS;
     pqreq[i] = a.pq.req[dd][cursor0 + p];
@@ -245,7 +243,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
     const int64_t* src = reinterpret_cast<const int64_t*>(a.pods + cursor0);
     int64_t* dst = reinterpret_cast<int64_t*>(spods);
     const int32_t words = np * (int32_t)(sizeof(PodRec) / 8);
-    for (int32_t i = tid; i < words; i += kCommitThreads) dst[i] = src[i];
+    lds_copy(dst, src, words, tid);
   }
   for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
   if (QC) {
@@ -263,14 +261,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
   }
   // raw rows of every pod's top node (a node shared by several pods is loaded once per pod: no dependency on
   // the owner computation, which runs while these loads are in flight)
-  for (int32_t i = tid; i < np * RF_N; i += kCommitThreads) {
-    const int32_t p = i / RF_N, f = i - p * RF_N;
-    const uint64_t t = a.cand_top[p];
-    if (t) {
-      const RowCol rc = a.rowcols[f];
-      rawtop[p * 32 + f] = load_field(rc.p, rc.width, gkey_node(t));
-    }
-  }
+  lds_rawtop(rawtop, a.cand_top, a.rowcols, np, tid);
   if (tid < kMaxBatch) {
     const uint64_t t = tid < np ? a.cand_top[tid] : 0ull;
     top_node[tid] = t ? (int32_t)gkey_node(t) : -1;

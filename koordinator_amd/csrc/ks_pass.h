@@ -406,6 +406,58 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
   return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
 }
 
+// Prologue copies into LDS with every load of a thread issued before its first LDS store (kPro loads in flight per
+// thread), so a pass's candidate lists, pod records and top-node raw rows arrive in a few HBM round trips rather
+// than one per 256 elements.
+constexpr int kPro = 8;
+template <typename T>
+__device__ __forceinline__ void lds_copy(T* dst, const T* src, int32_t n, int tid) {
+  for (int32_t i0 = tid; i0 < n; i0 += kCommitThreads * kPro) {
+    T v[kPro];
+#pragma unroll
+    for (int u = 0; u < kPro; ++u) {
+      const int32_t i = i0 + u * kCommitThreads;
+      if (i < n) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kPro; ++u) {
+      const int32_t i = i0 + u * kCommitThreads;
+      if (i < n) dst[i] = v[u];
+    }
+  }
+}
+
+// rawtop[p * 32 + f] = raw row field f of pod p's snapshot-best node (pods without a feasible node: untouched)
+__device__ __forceinline__ void lds_rawtop(int64_t* rawtop, const uint64_t* cand_top, const RowCol* rowcols, int32_t np,
+                                           int tid) {
+  const int32_t n = np * RF_N;
+  for (int32_t i0 = tid; i0 < n; i0 += kCommitThreads * kPro) {
+    uint64_t t[kPro];
+    RowCol rc[kPro];
+#pragma unroll
+    for (int u = 0; u < kPro; ++u) {
+      const int32_t i = i0 + u * kCommitThreads;
+      t[u] = 0;
+      if (i < n) {
+        const int32_t p = i / RF_N, f = i - p * RF_N;
+        t[u] = cand_top[p];
+        rc[u] = rowcols[f];
+      }
+    }
+    int64_t v[kPro];
+#pragma unroll
+    for (int u = 0; u < kPro; ++u) v[u] = t[u] ? load_field(rc[u].p, rc[u].width, gkey_node(t[u])) : 0;
+#pragma unroll
+    for (int u = 0; u < kPro; ++u) {
+      const int32_t i = i0 + u * kCommitThreads;
+      if (i < n && t[u]) {
+        const int32_t p = i / RF_N, f = i - p * RF_N;
+        rawtop[p * 32 + f] = v[u];
+      }
+    }
+  }
+}
+
 template <int NSC, bool QC, int FEAT>
 __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   constexpr bool RSV = (FEAT & 1) != 0;
@@ -470,10 +522,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
 #endif
 
   // ---- load the pass into LDS with all four waves (independent loads, one burst) ----
-  for (int32_t i = tid; i < np * K; i += kCommitThreads) {
-    cand_chunk[i] = a.cand_chunk[i];
-    cand_t[i] = a.cand_t[i];
-  }
+  lds_copy(cand_chunk, a.cand_chunk, np * K, tid);
+  lds_copy(cand_t, a.cand_t, np * K, tid);
   for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += kCommitThreads) {
     const int32_t p = i / KS_QUOTA_DIMS, dd = i - p * KS_QUOTA_DIMS;
     pqreq[i] = a.pq.req[dd][cursor0 + p];
@@ -482,18 +532,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     const int64_t* src = reinterpret_cast<const int64_t*>(a.pods + cursor0);
     int64_t* dst = reinterpret_cast<int64_t*>(spods);
     const int32_t words = np * (int32_t)(sizeof(PodRec) / 8);
-    for (int32_t i = tid; i < words; i += kCommitThreads) dst[i] = src[i];
+    lds_copy(dst, src, words, tid);
   }
   for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
   // raw row of every pod's snapshot-best node (the monotone fast path's winner): all loads in flight together
-  for (int32_t i = tid; i < np * RF_N; i += kCommitThreads) {
-    const int32_t p = i / RF_N, f = i - p * RF_N;
-    const uint64_t top = a.cand_top[p];
-    if (top) {
-      const RowCol rc = a.rowcols[f];
-      rawtop[p * 32 + f] = load_field(rc.p, rc.width, gkey_node(top));
-    }
-  }
+  lds_rawtop(rawtop, a.cand_top, a.rowcols, np, tid);
   if (QC) {
     for (int32_t r = tid; r < a.q.q; r += kCommitThreads) {
       qlds->parent[r] = a.q.parent[r];
