@@ -237,8 +237,8 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         sync()
         elapsed = time.perf_counter() - t0
         st_last = ev.stats()
-        agg = {"sweep_ms": 0.0, "select_ms": 0.0, "commit_ms": 0.0, "sweep_launches": 0, "passes": 0,
-               "cut_passes": 0, "rescans": 0}
+        agg = {"sweep_ms": 0.0, "select_ms": 0.0, "commit_ms": 0.0, "fixup_ms": 0.0, "sweep_launches": 0, "passes": 0,
+               "cut_passes": 0, "rescans": 0, "bubble_passes": 0}
         prof_elapsed = 0.0
         sweep_bytes = 0
         if profile:
@@ -254,7 +254,7 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
                 sweep_bytes = st["sweep_bytes"]
             ev.set_profile(False)
         else:
-            for k in ("passes", "cut_passes", "rescans"):
+            for k in ("passes", "cut_passes", "rescans", "bubble_passes"):
                 agg[k] = st_last[k] * steps
         if dist is not None:
             import torch
@@ -290,8 +290,13 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         "passes_per_step": agg["passes"] / steps,
         "cut_passes_per_step": agg["cut_passes"] / steps,
         "rescans_per_step": agg["rescans"] / steps,
+        # pipelined passes: each pass's sweep runs on a second stream while the previous pass
+        # commits, so the kernel times below overlap and add up to more than ms_per_step
+        "pipelined": bool(st_last["pipelined"]),
+        "bubble_passes_per_step": agg["bubble_passes"] / steps,
         "kernel_ms_per_step": {"sweep": round(agg["sweep_ms"] / steps, 3), "select": round(agg["select_ms"] / steps, 3),
-                               "commit": round(agg["commit_ms"] / steps, 3)},
+                               "commit": round(agg["commit_ms"] / steps, 3),
+                               "dirty_resweep": round(agg["fixup_ms"] / steps, 3)},
         "roofline": None,
     }
     if profile and agg["sweep_launches"]:

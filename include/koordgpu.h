@@ -519,6 +519,9 @@ typedef struct ks_stats {
   int64_t sweep_bytes;     /* algorithmic bytes one sweep launch reads/writes */
   int64_t slot_misses;     /* commits whose node row was not prefetched (one extra HBM round trip) */
   int64_t diag[8];         /* diagnostic build only (KS_COMMIT_STAMPS): commit-phase cycle sums */
+  int64_t bubble_passes;   /* pipelined passes whose commit did nothing (the pass before was cut) */
+  double fixup_ms;         /* summed HIP-event time of the pipelined dirty-chunk re-sweeps */
+  int64_t pipelined;       /* 1 = the last call overlapped each pass's sweep with the previous commit */
 } ks_stats;
 
 typedef struct ks_ctx ks_ctx;
@@ -657,6 +660,11 @@ int ks_get_stats(const ks_ctx *ctx, ks_stats *out);
  * add dispatch gaps between the pass kernels, so throughput is timed with them off and the kernel split
  * from separate profiled calls. */
 int ks_set_profile(ks_ctx *ctx, int32_t on);
+/* Pipelined passes: each pass's sweep runs on a second stream while the previous pass
+ * commits, then the chunks that commit wrote are re-swept, so results are identical either way.
+ * mode 0 = off, 1 = automatic (clusters of at least 32,768 nodes; env KS_PIPE_MIN_NODES), 2 = always
+ * (plugin sets without DeviceShare / NodeNUMAResource only). */
+int ks_set_pipeline(ks_ctx *ctx, int32_t mode);
 
 /* Node sharding over GPUs (one process per GPU).  The node table stays replicated
  * (every rank applies the same commits); shard s = rank * virtual_shards + v sweeps and selects

@@ -386,6 +386,9 @@ class KsStats(C.Structure):
         ("sweep_bytes", C.c_int64),
         ("slot_misses", C.c_int64),
         ("diag", C.c_int64 * 8),
+        ("bubble_passes", C.c_int64),
+        ("fixup_ms", C.c_double),
+        ("pipelined", C.c_int64),
     ]
 
 
@@ -427,6 +430,7 @@ EXPORTED_SYMBOLS = [
     "ks_read_quota_used",
     "ks_get_stats",
     "ks_set_profile",
+    "ks_set_pipeline",
     "ks_shard_unique_id",
     "ks_shard_init",
 ]

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -201,11 +202,17 @@ struct SelectArgs {
   uint2* cand_t;                 // [64][K] {best, runner-up} local keys
   uint64_t* cand_bound;          // [64]
   uint64_t* cand_top;            // [64] the pod's snapshot-best key over every chunk
+  uint64_t* cand_second;         // [64] the pod's second-best key (its best node other than the top's)
   int32_t* cand_count;           // [64]
   int32_t* cand_total;           // [64] feasible chunks in this range (before the top-K cut)
   int64_t nchunks;               // row stride of the sweep output
   int64_t c0, c1;                // chunk range selected over
   int32_t total_pods, batch, k;
+  // Pipelined passes: block 0 writes the first pod of the NEXT pass's speculative sweep.  *cursor is
+  // this pass's first pod, *real_cursor where the previous commit left the queue: this pass commits iff they are
+  // equal, and then the next pass starts after its pods; otherwise (a bubble) the next pass starts at the cursor.
+  int32_t* next_base;            // NULL = not pipelined
+  const int32_t* real_cursor;
 };
 
 
@@ -227,6 +234,10 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   const int lane = tid & 63;
   const int wv = tid >> 6;
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (a.next_base && blockIdx.x == 0 && tid == 0) {
+    const int32_t rc = *a.real_cursor;
+    *a.next_base = (cursor == rc && cursor < a.total_pods) ? cursor + min(a.batch, a.total_pods - cursor) : rc;
+  }
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
   const int32_t p = blockIdx.x;
@@ -344,13 +355,16 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
       need_eq = K - gt;
     }
   }
-  // every h > t, plus the first need_eq entries (chunk order) with h == t
+  // every h > t, plus the first need_eq entries (chunk order) with h == t; on the way, the second-best key over
+  // every chunk (the top's chunk contributes its runner-up): the commit prefetches that node's row too
   int32_t base = 0, eq_taken = 0;
-  uint64_t bound = 0;
+  uint64_t bound = 0, second = 0;
+  const int64_t etop = top ? gkey_node(top) / 64 - a.c0 : -1;
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   for (int64_t e0 = 0; e0 < nc; e0 += 64) {
     const int64_t e = e0 + lane;
     const uint2 loc = e < nc ? srow[e] : make_uint2(0u, 0u);
+    second = umax64(second, local_gkey(e == etop ? loc.y : loc.x, a.c0 + e));
     const uint32_t h = loc.x >> 6;
     const bool is_gt = h > t;
     const bool is_eq = (h == t) && h != 0;
@@ -369,11 +383,13 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
     eq_taken += __popcll(beq);
   }
   bound = wave_max_u64(bound);  // only one lane holds a non-zero bound
+  second = wave_max_u64(second);
   if (lane == 0) {
     a.cand_count[p] = base;
     a.cand_total[p] = cnt;
     a.cand_bound[p] = exhaustive ? 0ull : bound;
     a.cand_top[p] = top;
+    a.cand_second[p] = second;
   }
 }
 
@@ -395,6 +411,7 @@ struct MergeArgs {
   uint2* cand_t;
   uint64_t* cand_bound;
   uint64_t* cand_top;
+  uint64_t* cand_second;
   int32_t* cand_count;
   int32_t nslots, total_pods, batch, k;
 };
@@ -460,7 +477,8 @@ __global__ __launch_bounds__(64) void merge_kernel(MergeArgs a) {
     need_eq = K - count_ge(t_thr, true);
   }
   int32_t base = 0, eq_taken = 0;
-  uint64_t bound = 0;
+  uint64_t bound = 0, second = 0;
+  const int64_t ctop = top ? gkey_node(top) / 64 : -1;  // the second-best key over the union (as select_kernel)
   const uint64_t lanemask_lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
   for (int32_t s = 0; s < a.nslots; ++s) {
     const int32_t cnt = reinterpret_cast<const int32_t*>(a.gather + (size_t)s * L.bytes + L.count)[p];
@@ -469,6 +487,7 @@ __global__ __launch_bounds__(64) void merge_kernel(MergeArgs a) {
       uint32_t c = 0;
       uint2 t = make_uint2(0u, 0u);
       if (i < cnt) entry(s, i, c, t);
+      if (i < cnt) second = umax64(second, local_gkey((int64_t)c == ctop ? t.y : t.x, c));
       const uint32_t h = t.x >> 6;
       const bool is_gt = h > t_thr;
       const bool is_eq = (h == t_thr) && h != 0;
@@ -488,10 +507,12 @@ __global__ __launch_bounds__(64) void merge_kernel(MergeArgs a) {
     }
   }
   bound = wave_max_u64(bound);
+  second = wave_max_u64(second);
   if (lane == 0) {
     a.cand_count[p] = base;
     a.cand_bound[p] = exhaustive ? 0ull : bound;
     a.cand_top[p] = top;
+    a.cand_second[p] = second;
   }
 }
 
@@ -859,6 +880,8 @@ struct Col {
 
 }  // namespace
 
+constexpr int kPipeEvents = 4;  // ring of cross-stream events of the pipelined passes
+
 struct PodStage {
   void* blob = nullptr;
   int32_t cap = 0;
@@ -904,6 +927,7 @@ struct ks_ctx {
   uint2* cand_t = nullptr;
   uint64_t* cand_bound = nullptr;
   uint64_t* cand_top = nullptr;
+  uint64_t* cand_second = nullptr;
   int32_t* cand_total = nullptr;
   // node sharding: shard s = rank * vshards + v owns chunks [s*nchunks/S, (s+1)*nchunks/S)
   int32_t nranks = 1, rank = 0, vshards = 1;
@@ -962,6 +986,14 @@ struct ks_ctx {
   void* dscratch = nullptr;        // delta uploads (ks_update_*): indices + row words
   size_t dscratch_bytes = 0;
   uint32_t* cpuset_split = nullptr;  // [cpuset_cap] per pod (CommitArgs.cpuset_split)
+  // pipelined passes: sweep + select on sstream while the commit runs on stream
+  hipStream_t sstream = nullptr;   // shared by the process's contexts on this device (ensure_pipe), never destroyed
+  hipStream_t cstream = nullptr;   // the pipelined commits: the CU the sweep stream leaves out (or `stream`)
+  int32_t* pipe = nullptr;          // [0..1] speculative first pod per pass parity, [4..68] commit carry list
+  hipEvent_t pev_sel[kPipeEvents] = {};
+  hipEvent_t pev_com[kPipeEvents] = {};
+  int64_t pipe_k = 0;               // pass index within the current ks_schedule* call
+  int32_t pipe_mode = -1;           // ks_set_pipeline (-1: KS_PIPE, default automatic)
   // stats
   ks_stats stats{};
   std::vector<hipEvent_t> ev_pool;
@@ -1137,6 +1169,8 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->cand_bound = (uint64_t*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_top = (uint64_t*)p;
+  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  ctx->cand_second = (uint64_t*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_total = (int32_t*)p;
   if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
@@ -1158,6 +1192,8 @@ fail:
 void ks_destroy(ks_ctx* ctx) {
   if (!ctx) return;
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->sstream) (void)hipStreamSynchronize(ctx->sstream);
+  if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
   dev_free(ctx->node_blob);
   dev_free(ctx->ckpt_blob);
   dev_free(ctx->quota_blob);
@@ -1174,6 +1210,7 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->cand_t; dev_free(p);
   p = ctx->cand_bound; dev_free(p);
   p = ctx->cand_top; dev_free(p);
+  p = ctx->cand_second; dev_free(p);
   p = ctx->cand_total; dev_free(p);
   p = ctx->gather; dev_free(p);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
@@ -1192,6 +1229,11 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->cpuset_list; dev_free(p);
   dev_free(ctx->numa_blob);
   p = ctx->dnv; dev_free(p);
+  p = ctx->pipe; dev_free(p);
+  for (int i = 0; i < kPipeEvents; ++i) {
+    if (ctx->pev_sel[i]) (void)hipEventDestroy(ctx->pev_sel[i]);
+    if (ctx->pev_com[i]) (void)hipEventDestroy(ctx->pev_com[i]);
+  }
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -2581,9 +2623,11 @@ static size_t numa_cache_bytes(const ks_ctx* ctx) {
 }
 
 // Quota rows are cached in LDS for the pass when the table is small enough and the LDS image fits.
+static int kernel_feat(const ks_ctx* ctx);
+
 static bool commit_qcache(const ks_ctx* ctx) {
   if (!(ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows)) return false;
-  return commit_layout(ctx->k, ctx->nchunks, true, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx)).total <= 160 * 1024;
+  return commit_layout(ctx->k, ctx->nchunks, true, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total <= 160 * 1024;
 }
 
 // kernel variant: 0 = Fit/LoadAware/Quota, 1 = + Reservation, 3 = + Reservation + NodeNUMAResource
@@ -2607,7 +2651,7 @@ static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
   *qcache = commit_qcache(ctx);
   if (!ctx->kc.rsv) return 0;
   auto fit = [&](bool qc) {
-    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx)).total + 64;
+    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total + 64;
     const size_t avail = base < 160 * 1024 ? 160 * 1024 - base : 0;
     return (int32_t)std::min<size_t>(8, avail / rsv_cache_bytes(ctx, 1));
   };
@@ -2647,6 +2691,7 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.cand_t = ctx->cand_t;
   ca.cand_bound = ctx->cand_bound;
   ca.cand_top = ctx->cand_top;
+  ca.cand_second = ctx->cand_second;
   ca.cand_count = ctx->cand_count;
   ca.results = st.results;
   ca.counters = ctx->counters;
@@ -2668,7 +2713,10 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.force = 0;
   ca.numa_bytes = (int32_t)numa_cache_bytes(ctx);
   ca.nv = ctx->dnv;
-  *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes).total;
+  ca.pipe_base = nullptr;
+  ca.carry = nullptr;
+  *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
+                        ctx->q.q, kernel_feat(ctx) == 0).total;
   return ca;
 }
 
@@ -2683,7 +2731,7 @@ static bool mono_commit(const ks_ctx* ctx, bool qcache, size_t* smem) {
   static const int64_t mode = env_i64("KS_COMMIT_GENERAL", 0, 0, 2);
   if (mode == 1 || kernel_feat(ctx) != 0 || !ctx->kc.monotone || ctx->kc.fit_most) return false;
   if (mode == 0 && ctx->kc.quota_enable) return false;
-  *smem = mono_layout(ctx->k, ctx->nchunks, qcache).total;
+  *smem = mono_layout(ctx->k, ctx->nchunks, qcache, ctx->q.q).total;
   return *smem <= 160 * 1024;
 }
 
@@ -2692,7 +2740,7 @@ static int commit_attr_set(ks_ctx* ctx) {
   bool qcache = false;
   const int32_t rcap = commit_rcap(ctx, &qcache);
   const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx),
-                                    numa_cache_bytes(ctx)).total;
+                                    numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total;
   if (smem > 160 * 1024)
     KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
   hipError_t e = pass_launcher(kernel_feat(ctx), ctx->nsc).commit_attr(qcache, smem);
@@ -2724,12 +2772,97 @@ static int ensure_cpuset_bufs(ks_ctx* ctx, int32_t np) {
   return KS_OK;
 }
 
+constexpr int kPipeWords = 4 + 1 + kMaxBatch;  // ks_ctx.pipe: bases [0..1], carry list at [4]
+
+// Pipelined passes are used for plugin sets whose sweep output depends on nothing but the node rows
+// (and reservations) a commit writes: no DeviceShare (its normalization max spans every node) and no
+// NodeNUMAResource (core counts are refreshed by cpuset_kernel).  KS_PIPE=0 turns them off (A/B).
+// The re-sweep, the select and two cross-stream hops then sit between consecutive commits instead of the sweep, so it
+// pays only when the sweep is long: clusters of at least KS_PIPE_MIN_NODES nodes (default 32,768; C5's 100k, not
+// C2's 5k: measured on MI355X, profiles/r03_pipe_ab.txt).
+static bool pipelined(const ks_ctx* ctx) {
+  static const int64_t env_pipe = env_i64("KS_PIPE", 1, 0, 2);
+  static const int64_t env_min = env_i64("KS_PIPE_MIN_NODES", 32768, 0, (int64_t)1 << 40);
+  const int64_t mode = ctx->pipe_mode >= 0 ? ctx->pipe_mode : env_pipe;
+  const int feat = kernel_feat(ctx);
+  if (mode == 0 || !(feat == 0 || feat == 1) || ctx->kc.dev || ctx->kc.cores) return false;
+  return mode == 2 || ctx->n >= env_min;
+}
+
+// The sweep stream (one CU left out of its mask by default, so the one-workgroup commit always finds a CU while a
+// sweep fills the rest; KS_PIPE_CUMASK=0: no mask), the pipe words and the event ring.
+static int ensure_pipe(ks_ctx* ctx) {
+  if (!ctx->pipe) {
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, kPipeWords * 4) != KS_OK) return KS_ENOMEM;
+    ctx->pipe = (int32_t*)p;
+  }
+  if (!ctx->sstream) {
+    // One sweep stream and one commit stream per device for the whole process, shared by every context: a
+    // CU-masked stream owns a hardware queue of its own, and creating them per context exhausts the process's
+    // queues (stream creation then stalls).  Sharing only orders the passes of different contexts; each context's
+    // own events order its passes.  The commit stream runs on the one CU the sweep stream leaves out, so the
+    // one-workgroup commit never shares a CU (and its SIMDs' issue slots) with sweep waves.
+    struct Pair {
+      hipStream_t s = nullptr, c = nullptr;
+    };
+    static std::mutex mu;
+    static std::vector<Pair> per_dev;
+    std::lock_guard<std::mutex> lock(mu);
+    if (per_dev.size() <= (size_t)ctx->device) per_dev.resize((size_t)ctx->device + 1);
+    Pair& st = per_dev[(size_t)ctx->device];
+    if (!st.s) {
+      static const int64_t env_mask = env_i64("KS_PIPE_CUMASK", 1, 0, 1);
+      int ncu = 0;
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+      bool masked = false;
+      if (env_mask && ncu > 8) {
+        std::vector<uint32_t> smask((size_t)(ncu + 31) / 32, 0u), cmask((size_t)(ncu + 31) / 32, 0u);
+        for (int c = 1; c < ncu; ++c) smask[(size_t)c / 32] |= 1u << (c % 32);
+        cmask[0] = 1u;
+        hipStream_t a = nullptr, b = nullptr;
+        if (hipExtStreamCreateWithCUMask(&a, (uint32_t)smask.size(), smask.data()) == hipSuccess) {
+          if (hipExtStreamCreateWithCUMask(&b, (uint32_t)cmask.size(), cmask.data()) == hipSuccess) {
+            st.s = a;
+            st.c = b;
+            masked = true;
+          } else {
+            (void)hipStreamDestroy(a);
+          }
+        }
+      }
+      if (!masked) HIPCHK(ctx, hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
+    }
+    ctx->sstream = st.s;
+    ctx->cstream = st.c ? st.c : ctx->stream;
+  }
+  for (int i = 0; i < kPipeEvents; ++i) {
+    if (!ctx->pev_sel[i]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->pev_sel[i], hipEventDisableTiming));
+    if (!ctx->pev_com[i]) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->pev_com[i], hipEventDisableTiming));
+  }
+  return KS_OK;
+}
+
+// Launch shape of the dirty-chunk re-sweep of a pipelined pass; pipe == nullptr: not pipelined.
+struct PipeShape {
+  int32_t fix_ppw;
+  int fix_blocks;
+};
+
 template <int NSC>
-static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
-  auto rec = [&](int kind) {
+static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeShape* pipe,
+                       std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
+  // Pipelined: the sweep and the select run on sstream; the sweep of pass k runs while commit k-1 does
+  // (for the pods after commit k-1's, speculatively), then the chunks commit k-1 wrote are re-swept, so the select
+  // and commit k see exactly what a sweep after commit k-1 gives.  Otherwise everything runs on ctx->stream.
+  hipStream_t ss = pipe ? ctx->sstream : ctx->stream;
+  const int64_t k = ctx->pipe_k;
+  int32_t* base = pipe ? ctx->pipe + (k & 1) : ctx->cursor;  // the first pod this pass sweeps
+  int32_t* carry = ctx->pipe + 4;
+  auto rec = [&](int kind, hipStream_t s) {
     if (!evs) return;
     hipEvent_t e = take_event(ctx, *evn);
-    (void)hipEventRecord(e, ctx->stream);
+    (void)hipEventRecord(e, s);
     evs->push_back({kind, (*evn)++});
   };
   const int32_t S = ctx->nranks * ctx->vshards;
@@ -2739,7 +2872,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   sa.rv = ctx->drv;
   sa.c = ctx->kc;
   sa.pods = ctx->st.recs;
-  sa.cursor = ctx->cursor;
+  sa.cursor = base;
   sa.out = ctx->sweep_out;
   sa.n = ctx->n;
   sa.nchunks = ctx->nchunks;
@@ -2748,6 +2881,8 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   sa.total_pods = ctx->np;
   sa.batch = ctx->batch;
   sa.ppw = ppw;
+  sa.fix = nullptr;
+  sa.fix_cursor = nullptr;
   const int feat = kernel_feat(ctx);
   sa.dv = ctx->ddv;
   sa.nv = ctx->dnv;
@@ -2759,53 +2894,68 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
   // c0 > 0 decode of every non-first shard runs on one GPU too); timed together as one launch.
   const PassLaunch pl = pass_launcher(feat, NSC);
   hipError_t le = hipSuccess;
-  auto sweep = [&]() {
+  auto sweep = [&](int blocks) {
     for (int32_t v = 0; v < ctx->vshards && le == hipSuccess; ++v) {
       const int32_t sh = ctx->rank * ctx->vshards + v;
       sa.c0 = shard_lo(sh);
       sa.c1 = shard_lo(sh + 1);
-      le = pl.sweep(sweep_blocks, ctx->stream, sa);
+      le = pl.sweep(blocks, ss, sa);
     }
   };
   if (feat == 7 || feat == 15) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
     // each launch is timed on its own (the roofline is per sweep launch)
-    HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ss));
     sa.phase = 0;
-    rec(0);
-    sweep();
-    rec(0);
+    rec(0, ss);
+    sweep(sweep_blocks);
+    rec(0, ss);
     if (ctx->nranks > 1) {
-      const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ctx->stream);
+      const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ss);
       if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllReduce (DeviceShare max): %s", ncclGetErrorString(r));
     }
     sa.phase = 1;
-    rec(0);
-    sweep();
+    rec(0, ss);
+    sweep(sweep_blocks);
   } else {
-    rec(0);
-    sweep();
+    rec(0, ss);
+    sweep(sweep_blocks);
   }
   HIPCHK(ctx, le);
-  rec(0);
+  rec(0, ss);
+  if (pipe) {
+    // after commit k-1: its rows' chunks again, for the same pods (nothing when the sweep's pods are not where
+    // commit k-1 left the cursor: commit k is then a bubble)
+    if (k > 0) HIPCHK(ctx, hipStreamWaitEvent(ss, ctx->pev_com[(k - 1) % kPipeEvents], 0));
+    sa.fix = carry;
+    sa.fix_cursor = ctx->cursor;
+    sa.ppw = pipe->fix_ppw;
+    rec(3, ss);
+    sweep(pipe->fix_blocks);
+    HIPCHK(ctx, le);
+    rec(3, ss);
+  }
   SelectArgs se;
   se.in = ctx->sweep_out;
-  se.cursor = ctx->cursor;
+  se.cursor = base;
   se.nchunks = ctx->nchunks;
   se.total_pods = ctx->np;
   se.batch = ctx->batch;
   se.k = ctx->k;
+  se.real_cursor = ctx->cursor;
   const CandSlot L = cand_slot_layout(ctx->k);
-  rec(1);
+  rec(1, ss);
   for (int32_t v = 0; v < ctx->vshards; ++v) {
     const int32_t sh = ctx->rank * ctx->vshards + v;
     se.c0 = shard_lo(sh);
     se.c1 = shard_lo(sh + 1);
+    se.next_base = (pipe && v == 0) ? ctx->pipe + ((k + 1) & 1) : nullptr;
     if (S == 1) {
       se.cand_chunk = ctx->cand_chunk;
       se.cand_t = ctx->cand_t;
       se.cand_bound = ctx->cand_bound;
       se.cand_top = ctx->cand_top;
+      se.cand_second = ctx->cand_second;
       se.cand_count = ctx->cand_count;
       se.cand_total = ctx->cand_total;
     } else {
@@ -2814,43 +2964,56 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, std::vector<s
       se.cand_t = (uint2*)(b + L.t);
       se.cand_bound = ctx->cand_bound;  // recomputed by the merge
       se.cand_top = (uint64_t*)(b + L.top);
+      se.cand_second = ctx->cand_second;  // recomputed by the merge
       se.cand_count = (int32_t*)(b + L.count);
       se.cand_total = (int32_t*)(b + L.total);
     }
-    hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(kSelThreads), select_smem(se.c1 - se.c0), ctx->stream, se);
+    hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(kSelThreads), select_smem(se.c1 - se.c0), ss, se);
   }
   if (S > 1) {
     if (ctx->nranks > 1) {
       // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
       const size_t bytes = (size_t)ctx->vshards * L.bytes;
       const ncclResult_t r =
-          ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, ctx->stream);
+          ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, ss);
       if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllGather (candidate slots): %s", ncclGetErrorString(r));
     }
     MergeArgs ma;
     ma.gather = ctx->gather;
-    ma.cursor = ctx->cursor;
+    ma.cursor = base;
     ma.cand_chunk = ctx->cand_chunk;
     ma.cand_t = ctx->cand_t;
     ma.cand_bound = ctx->cand_bound;
     ma.cand_top = ctx->cand_top;
+    ma.cand_second = ctx->cand_second;
     ma.cand_count = ctx->cand_count;
     ma.nslots = S;
     ma.total_pods = ctx->np;
     ma.batch = ctx->batch;
     ma.k = ctx->k;
-    hipLaunchKernelGGL(merge_kernel, dim3(ctx->batch), dim3(64), 0, ctx->stream, ma);
+    hipLaunchKernelGGL(merge_kernel, dim3(ctx->batch), dim3(64), 0, ss, ma);
   }
-  rec(1);
+  rec(1, ss);
+  hipStream_t cs = pipe ? ctx->cstream : ctx->stream;
+  if (pipe) {
+    HIPCHK(ctx, hipEventRecord(ctx->pev_sel[k % kPipeEvents], ss));
+    HIPCHK(ctx, hipStreamWaitEvent(cs, ctx->pev_sel[k % kPipeEvents], 0));
+  }
   bool qcache = false;
   size_t smem = 0;
-  const CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, ctx->batch, &qcache, &smem);
+  CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, ctx->batch, &qcache, &smem);
+  if (pipe) {
+    ca.pipe_base = base;
+    ca.carry = carry;
+  }
   size_t msmem = 0;
   const bool mono = mono_commit(ctx, qcache, &msmem);
-  rec(2);
-  if (mono) HIPCHK(ctx, pl.commit_mono(qcache, msmem, ctx->stream, ca));
-  else HIPCHK(ctx, pl.commit(qcache, smem, ctx->stream, ca));
-  rec(2);
+  rec(2, cs);
+  if (mono) HIPCHK(ctx, pl.commit_mono(qcache, msmem, cs, ca));
+  else HIPCHK(ctx, pl.commit(qcache, smem, cs, ca));
+  rec(2, cs);
+  if (pipe) HIPCHK(ctx, hipEventRecord(ctx->pev_com[k % kPipeEvents], cs));
+  ctx->pipe_k = k + 1;
   if (ctx->kc.cores && ctx->cpu_loaded) {
     // the pass's CPU ids now, so that the next sweep sees exact per-node core counts (Cfg.cores)
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
@@ -2916,9 +3079,29 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->counters, 0, 256, ctx->stream));
+  // pipelined passes: pass 0 sweeps from pod 0, no commit has written rows yet
+  PipeShape pshape{};
+  const PipeShape* pipe = nullptr;
+  if (pipelined(ctx)) {
+    if (ensure_pipe(ctx) != KS_OK) return KS_EHIP;
+    static const int64_t env_fix_ppw = env_i64("KS_PIPE_FIX_PPW", 2, 1, kMaxBatch);
+    pshape.fix_ppw = (int32_t)std::min<int64_t>(env_fix_ppw, ctx->batch);
+    const int64_t fwork = (int64_t)kMaxBatch * ((ctx->batch + pshape.fix_ppw - 1) / pshape.fix_ppw);
+    pshape.fix_blocks = (int)((std::max<int64_t>(1, (fwork + 3) / 4) + 7) & ~7ll);
+    pipe = &pshape;
+    HIPCHK(ctx, hipMemsetAsync(ctx->pipe, 0, kPipeWords * 4, ctx->stream));
+    ctx->pipe_k = 0;
+  }
   HIPCHK(ctx, hipEventRecord(t0, ctx->stream));
   // PreFilter / EstimatePod for the staged queue (the pods' request vectors, estimates, flags)
   if (prep_stage(ctx, ctx->st, np) != KS_OK) return KS_EHIP;
+  hipStream_t cs = pipe ? ctx->cstream : ctx->stream;  // where the commits (and the cursor read-back) run
+  if (pipe) {
+    // the sweep and commit streams start after everything before them on the context's stream
+    HIPCHK(ctx, hipEventRecord(ctx->pev_com[kPipeEvents - 1], ctx->stream));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->sstream, ctx->pev_com[kPipeEvents - 1], 0));
+    if (cs != ctx->stream) HIPCHK(ctx, hipStreamWaitEvent(cs, ctx->pev_com[kPipeEvents - 1], 0));
+  }
   std::vector<std::pair<int, size_t>> evs;
   size_t evn = 2;
   int32_t host_cursor = 0;
@@ -2930,16 +3113,21 @@ static int schedule_staged_impl(ks_ctx* ctx) {
       auto* ev = ctx->cfg.profile ? &evs : nullptr;
       int rc;
       switch (ctx->nsc) {
-        case 0: rc = launch_pass<0>(ctx, ppw, sweep_blocks, ev, &evn); break;
-        case 2: rc = launch_pass<2>(ctx, ppw, sweep_blocks, ev, &evn); break;
-        default: rc = launch_pass<4>(ctx, ppw, sweep_blocks, ev, &evn); break;
+        case 0: rc = launch_pass<0>(ctx, ppw, sweep_blocks, pipe, ev, &evn); break;
+        case 2: rc = launch_pass<2>(ctx, ppw, sweep_blocks, pipe, ev, &evn); break;
+        default: rc = launch_pass<4>(ctx, ppw, sweep_blocks, pipe, ev, &evn); break;
       }
       if (rc != KS_OK) return rc;
     }
     HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipMemcpyAsync(&host_cursor, ctx->cursor, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(&host_cursor, ctx->cursor, 4, hipMemcpyDeviceToHost, cs));
+    HIPCHK(ctx, hipStreamSynchronize(cs));
     if (++rounds > 1000000) KS_FAIL(ctx, KS_EHIP, "schedule made no progress");
+  }
+  if (cs != ctx->stream) {
+    // everything after the passes runs on the context's stream again
+    HIPCHK(ctx, hipEventRecord(ctx->pev_com[0], cs));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->pev_com[0], 0));
   }
   if (ctx->cpu_loaded && ctx->n > 0) {
     // the CPU ids of the pass's cpu-bind Reserves (ks_cpuset.h), per node in placement order
@@ -2960,6 +3148,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   ctx->stats.cut_passes = (int64_t)cnt[1];
   ctx->stats.rescans = (int64_t)cnt[2];
   ctx->stats.slot_misses = (int64_t)cnt[3];
+  ctx->stats.bubble_passes = (int64_t)cnt[4];
+  ctx->stats.pipelined = pipe ? 1 : 0;
   for (int i = 0; i < 8; ++i) ctx->stats.diag[i] = (int64_t)cnt[8 + i];
   for (size_t i = 0; i + 1 < evs.size(); i += 2) {
     float e = 0;
@@ -2969,6 +3159,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
       ctx->stats.sweep_launches += 1;
     } else if (evs[i].first == 1) {
       ctx->stats.select_ms += e;
+    } else if (evs[i].first == 3) {
+      ctx->stats.fixup_ms += e;
     } else {
       ctx->stats.commit_ms += e;
     }
@@ -3427,6 +3619,7 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
   HIPCHK(ctx, hipMemcpyAsync(ctx->cand_count, &h.count, 4, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->cand_bound, &h.bound, 8, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->cand_top, &h.top, 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->cand_second, &h.top, 8, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream));
   if (ctx->cpuset_list) {
@@ -3629,6 +3822,13 @@ int ks_get_stats(const ks_ctx* ctx, ks_stats* out) {
 int ks_set_profile(ks_ctx* ctx, int32_t on) {
   if (!ctx) return KS_EINVAL;
   ctx->cfg.profile = on ? 1 : 0;
+  return KS_OK;
+}
+
+int ks_set_pipeline(ks_ctx* ctx, int32_t mode) {
+  if (!ctx) return KS_EINVAL;
+  if (mode < 0 || mode > 2) KS_FAIL(ctx, KS_EINVAL, "ks_set_pipeline: mode %d (0 off, 1 automatic, 2 always)", mode);
+  ctx->pipe_mode = mode;
   return KS_OK;
 }
 

@@ -136,7 +136,7 @@ struct MonoLayout {
   size_t rows, pods, res, pqreq, cand_t, cand_chunk, tops, raw1, quota, touched, total;
 };
 
-__host__ __device__ inline MonoLayout mono_layout(int32_t k, int64_t nchunks, bool qc) {
+__host__ __device__ inline MonoLayout mono_layout(int32_t k, int64_t nchunks, bool qc, int32_t qrows = kQuotaLdsRows) {
   MonoLayout L;
   size_t o = 0;
   L.rows = o;
@@ -156,7 +156,7 @@ __host__ __device__ inline MonoLayout mono_layout(int32_t k, int64_t nchunks, bo
   L.raw1 = o;
   o += 32 * 8;  // one raw row being turned into a slot row
   L.quota = o;
-  if (qc) o += align16(sizeof(QuotaRowsLds));
+  if (qc) o += align16(quota_lds_bytes(qrows));
   L.touched = o;
   o += (size_t)nchunks * 8;
   L.total = o;
@@ -183,7 +183,7 @@ template <int NSC, bool QC>
 __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
-  const MonoLayout lay = mono_layout(K, a.nchunks, QC);
+  const MonoLayout lay = mono_layout(K, a.nchunks, QC, a.q.q);
   MonoRow* rows = reinterpret_cast<MonoRow*>(smem_raw + lay.rows);
   PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
   ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
@@ -193,7 +193,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
   int32_t* top_node = reinterpret_cast<int32_t*>(smem_raw + lay.tops);
   int32_t* top_owner = top_node + kMaxBatch;
   int64_t* raw1 = reinterpret_cast<int64_t*>(smem_raw + lay.raw1);
-  QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
+  QuotaRowsLds qview = quota_lds(smem_raw + lay.quota, a.q.q);
+  QuotaRowsLds* qlds = &qview;
   unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
   // prologue staging of the top nodes' raw rows ([64][32] words) in the dynamic-row half of `rows`
   int64_t* rawtop = reinterpret_cast<int64_t*>(rows + kMaxBatch);
@@ -202,6 +203,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor0 >= a.total_pods) return;
+  if (pipe_bubble(a, cursor0)) return;
   const int32_t np = min(a.batch, a.total_pods - cursor0);
   const Cfg cfg = a.c;
 #if defined(KS_COMMIT_SEG) && !defined(KS_COMMIT_CAT)
@@ -564,6 +566,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
       a.q.npused[i] = qlds->npused[i];
     }
   }
+  pipe_carry(a, nslots, snode);
   if (lane == 0) {
     *a.cursor = cursor0 + processed;
     atomicAdd(&a.counters[0], 1ull);

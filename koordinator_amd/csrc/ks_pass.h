@@ -43,6 +43,12 @@ struct SweepArgs {
   int64_t n, nchunks;
   int64_t c0, c1;  // this shard's chunk range
   int32_t total_pods, batch, ppw;
+  // Pipelined passes: the re-sweep of the chunks the previous commit wrote.  fix = that commit's
+  // node list ([0] count, [1..64] nodes); only chunks of those nodes inside [c0, c1) are swept, and nothing
+  // when the pass's speculative first pod (*cursor) is not where the real cursor (*fix_cursor) stands.
+  // NULL = a full sweep.
+  const int32_t* fix;
+  const int32_t* fix_cursor;
 };
 
 // local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
@@ -61,10 +67,16 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
   const int32_t groups = (np + a.ppw - 1) / a.ppw;
-  const int64_t nwork = (a.c1 - a.c0) * groups;
+  int64_t nitems = a.c1 - a.c0;
+  if (a.fix) {
+    if (__builtin_amdgcn_readfirstlane(*a.fix_cursor) != cursor) return;  // the next commit will not use it
+    nitems = min(__builtin_amdgcn_readfirstlane(a.fix[0]), kMaxBatch);
+  }
+  const int64_t nwork = nitems * groups;
   for (int64_t w = wave; w < nwork; w += nwaves) {
-    const int64_t lc = w / groups;  // chunk within this shard's range
-    const int64_t c = a.c0 + lc;
+    const int64_t lc = w / groups;  // chunk within this shard's range (or entry of the fix list)
+    const int64_t c = a.fix ? (int64_t)(__builtin_amdgcn_readfirstlane(a.fix[1 + lc]) >> 6) : a.c0 + lc;
+    if (a.fix && (c < a.c0 || c >= a.c1)) continue;  // another shard's chunk
     const int32_t g = (int32_t)(w - lc * groups);
     const int64_t node = c * 64 + lane;
     if ((FEAT & 4) && a.phase == 1 && a.dcache) {
@@ -209,6 +221,7 @@ struct CommitArgs {
   const uint2* __restrict__ cand_t;
   const uint64_t* __restrict__ cand_bound;
   const uint64_t* __restrict__ cand_top;
+  const uint64_t* __restrict__ cand_second;  // [64] each pod's second-best key (select_kernel)
   const int32_t* __restrict__ cand_count;
   ks_result* results;
   unsigned long long* counters;  // [0] passes [1] cut passes [2] rescans [3] new-slot row misses [14] fast picks
@@ -223,23 +236,68 @@ struct CommitArgs {
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
   int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
   int32_t numa_bytes;  // LDS bytes of the slot NUMA-node state (commit_layout)
+  // Pipelined passes: the first pod the pass's sweep was run for; the pass is a no-op (a bubble) when
+  // the real cursor is elsewhere (the previous pass was cut).  NULL = not pipelined.
+  const int32_t* pipe_base;
+  // [0] count, [1..64] nodes whose rows this pass wrote back (the next pass re-sweeps their chunks); NULL = not kept
+  int32_t* carry;
 };
 
+// Pipelined pass prologue: a pass whose sweep ran for other pods than the ones at the cursor does nothing (its
+// successor's sweep starts at the cursor).  Returns true when the calling kernel must return.
+__device__ __forceinline__ bool pipe_bubble(const CommitArgs& a, int32_t cursor0) {
+  if (!a.pipe_base || __builtin_amdgcn_readfirstlane(*a.pipe_base) == cursor0) return false;
+  if (threadIdx.x == 0) {
+    a.carry[0] = 0;
+    atomicAdd(&a.counters[4], 1ull);
+  }
+  return true;
+}
+
+// Pipelined pass epilogue: the nodes of the pass's slots (lane s holds slot s's node)
+__device__ __forceinline__ void pipe_carry(const CommitArgs& a, int32_t nslots, int32_t snode) {
+  if (!a.carry) return;
+  const int lane = threadIdx.x & 63;
+  if (lane < nslots) a.carry[1 + lane] = snode;
+  if (lane == 0) a.carry[0] = nslots;
+}
+
+// The pass's quota rows in LDS, sized by the loaded table (q <= kQuotaLdsRows rows): a view of pointers into the
+// commit kernel's dynamic LDS (quota_lds).
 struct QuotaRowsLds {
-  int32_t parent[kQuotaLdsRows];
-  uint32_t limit_mask[kQuotaLdsRows], min_mask[kQuotaLdsRows];
-  int64_t limit[kQuotaLdsRows * KS_QUOTA_DIMS], used[kQuotaLdsRows * KS_QUOTA_DIMS];
-  int64_t min[kQuotaLdsRows * KS_QUOTA_DIMS], npused[kQuotaLdsRows * KS_QUOTA_DIMS];
+  int32_t* parent;
+  uint32_t *limit_mask, *min_mask;
+  int64_t *limit, *used, *min, *npused;
 };
+
+__host__ __device__ inline size_t quota_lds_bytes(int32_t q) {
+  const size_t r = (size_t)(q > 0 ? q : 1);
+  return (r * 12 + 15) / 16 * 16 + r * KS_QUOTA_DIMS * 32;
+}
+
+__device__ __forceinline__ QuotaRowsLds quota_lds(unsigned char* p, int32_t q) {
+  const size_t r = (size_t)(q > 0 ? q : 1);
+  QuotaRowsLds v;
+  v.parent = reinterpret_cast<int32_t*>(p);
+  v.limit_mask = reinterpret_cast<uint32_t*>(p + r * 4);
+  v.min_mask = reinterpret_cast<uint32_t*>(p + r * 8);
+  int64_t* w = reinterpret_cast<int64_t*>(p + (r * 12 + 15) / 16 * 16);
+  v.limit = w;
+  v.used = w + r * KS_QUOTA_DIMS;
+  v.min = w + 2 * r * KS_QUOTA_DIMS;
+  v.npused = w + 3 * r * KS_QUOTA_DIMS;
+  return v;
+}
 
 struct CommitLayout {
-  size_t rows, pods, res, raw, rawtop, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, touched, total;
+  size_t rows, pods, res, raw, rawtop, rawrun, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, touched, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 
 __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0,
-                                                      size_t dev_bytes = 0, size_t numa_bytes = 0) {
+                                                      size_t dev_bytes = 0, size_t numa_bytes = 0,
+                                                      int32_t qrows = kQuotaLdsRows, bool run = false) {
   CommitLayout L;
   size_t o = 0;
   L.rows = o;
@@ -252,6 +310,10 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += 32 * 8;  // one raw row being turned into a slot row
   L.rawtop = o;
   o += (size_t)kMaxBatch * 32 * 8;  // raw row of each pod's snapshot-best node, prefetched per pass
+  L.rawrun = o;
+  // raw row of each pod's second-best node (its likely winner once the top is taken); Fit + LoadAware
+  // [+ ElasticQuota] only (FEAT 0: the other plugin sets need the LDS for their slot state)
+  if (run) o += (size_t)kMaxBatch * 32 * 8;
   L.pqreq = o;
   o += (size_t)kMaxBatch * KS_QUOTA_DIMS * 8;
   L.cand_t = o;
@@ -271,7 +333,7 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   L.snp = o;
   o += align16(numa_bytes);    // per slot: NUMA-node totals / used / offsets + policy, count, present (ks_numa.h)
   L.quota = o;
-  if (qc) o += align16(sizeof(QuotaRowsLds));
+  if (qc) o += align16(quota_lds_bytes(qrows));
   L.touched = o;
   o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
   L.total = o;
@@ -463,7 +525,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   constexpr bool RSV = (FEAT & 1) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
-  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes, (size_t)a.numa_bytes);
+  const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes, (size_t)a.numa_bytes, a.q.q,
+                                         FEAT == 0);
   SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
   PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
   ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
@@ -472,8 +535,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   int64_t* pqreq = reinterpret_cast<int64_t*>(smem_raw + lay.pqreq);
   uint2* cand_t = reinterpret_cast<uint2*>(smem_raw + lay.cand_t);
   uint32_t* cand_chunk = reinterpret_cast<uint32_t*>(smem_raw + lay.cand_chunk);
-  QuotaRowsLds* qlds = reinterpret_cast<QuotaRowsLds*>(smem_raw + lay.quota);
+  QuotaRowsLds qview = quota_lds(smem_raw + lay.quota, a.q.q);
+  QuotaRowsLds* qlds = &qview;
   unsigned long long* touched = reinterpret_cast<unsigned long long*>(smem_raw + lay.touched);
+  int64_t* rawrun = reinterpret_cast<int64_t*>(smem_raw + lay.rawrun);
   uint64_t* scls = reinterpret_cast<uint64_t*>(smem_raw + lay.scls);
   int64_t* snuma = reinterpret_cast<int64_t*>(smem_raw + lay.snuma);
   int32_t* srcnt = reinterpret_cast<int32_t*>(smem_raw + lay.srcnt);
@@ -493,6 +558,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor0 >= a.total_pods) return;
+  if (pipe_bubble(a, cursor0)) return;
   const int32_t np = min(a.batch, a.total_pods - cursor0);
 #ifdef KS_COMMIT_STAMPS
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -535,8 +601,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     lds_copy(dst, src, words, tid);
   }
   for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
-  // raw row of every pod's snapshot-best node (the monotone fast path's winner): all loads in flight together
+  // raw rows of every pod's snapshot-best node (the monotone fast path's winner) and second-best node (the usual
+  // winner of a pod whose top an earlier pod took): all loads in flight together
   lds_rawtop(rawtop, a.cand_top, a.rowcols, np, tid);
+  if (FEAT == 0) lds_rawtop(rawrun, a.cand_second, a.rowcols, np, tid);
   if (QC) {
     for (int32_t r = tid; r < a.q.q; r += kCommitThreads) {
       qlds->parent[r] = a.q.parent[r];
@@ -553,11 +621,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
   int32_t my_cnt = 0, my_quota = -1;
   uint32_t my_flags = 0, my_pmask = 0;
-  uint64_t my_bound = 0, my_top = 0, my_devM = 0;
+  uint64_t my_bound = 0, my_top = 0, my_devM = 0, my_second = 0;
   if (tid < 64 && lane < np) {
     my_cnt = a.cand_count[lane];
     my_bound = a.cand_bound[lane];
     my_top = a.cand_top[lane];
+    if (FEAT == 0) my_second = a.cand_second[lane];
     if (DEV) my_devM = a.dev_M[lane];
     my_pmask = a.pq.mask[cursor0 + lane];
     my_quota = a.pods[cursor0 + lane].quota;
@@ -685,7 +754,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
 #ifndef KS_NO_SPEC
     if (cn.umax) {
       const int32_t node = (int32_t)gkey_node(cn.umax);
-      if (node != spec_node) {
+      // (the top's and the second-best node's rows are in LDS already)
+      if (node != spec_node && node != (int32_t)gkey_node(readlane64(my_top, j)) &&
+          node != (int32_t)gkey_node(readlane64(my_second, j))) {
         spec_node = node;
         if (lane < RF_N) spec_val = load_field(my_col, my_w, node);
       }
@@ -836,6 +907,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       const int64_t* src = raw;
       if (node == (int32_t)gkey_node(readlane64(my_top, j))) {
         src = rawtop + j * 32;  // prefetched at pass start
+      } else if (node == (int32_t)gkey_node(readlane64(my_second, j))) {
+        src = rawrun + j * 32;  // prefetched at pass start
       } else {
         int64_t v = spec_val;
         if (node != spec_node) {
@@ -1243,6 +1316,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       a.q.npused[i] = qlds->npused[i];
     }
   }
+  pipe_carry(a, nslots, snode);
   if (lane == 0) {
     *a.cursor = cursor0 + processed;
     atomicAdd(&a.counters[0], 1ull);

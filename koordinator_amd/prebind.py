@@ -12,6 +12,8 @@ host-side mirror the tests and the Python callers use.
   holding the per-instance request (``devicehandler_gpu.go:56-63``: gpu-core and gpu-memory-ratio DecimalSI,
   gpu-memory BinarySI; ``devicehandler_default.go:58``: rdma DecimalSI).
 * Reservation PreBind: ``scheduling.koordinator.sh/reservation-allocated`` = ``{"name": .., "uid": ..}``.
+* NodeNUMAResource PreBind of a cpu-bind pod also writes ``scheduling.koordinator.sh/resource-spec`` back when the
+  pod did not state the policy the scheduler enforced (``appendResourceSpecIfMissed``, ``plugin.go:552-578``).
 
 Go's ``encoding/json`` sorts map keys and writes no spaces; Kubernetes ``resource.Quantity`` marshals as its
 canonical string (``Quantity.String``), restated in ``quantity_string``.
@@ -24,6 +26,13 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 ANNOTATION_RESOURCE_STATUS = "scheduling.koordinator.sh/resource-status"
 ANNOTATION_DEVICE_ALLOCATED = "scheduling.koordinator.sh/device-allocated"
 ANNOTATION_RESERVATION_ALLOCATED = "scheduling.koordinator.sh/reservation-allocated"
+ANNOTATION_RESOURCE_SPEC = "scheduling.koordinator.sh/resource-spec"
+
+CPU_BIND_POLICY_DEFAULT = "Default"
+CPU_BIND_POLICY_FULL_PCPUS = "FullPCPUs"
+CPU_BIND_POLICY_SPREAD_BY_PCPUS = "SpreadByPCPUs"
+NODE_CPU_BIND_POLICY_FULL_PCPUS_ONLY = "FullPCPUsOnly"
+NODE_CPU_BIND_POLICY_SPREAD_BY_PCPUS = "SpreadByPCPUs"
 
 RESOURCE_GPU_CORE = "koordinator.sh/gpu-core"
 RESOURCE_GPU_MEMORY = "koordinator.sh/gpu-memory"
@@ -131,13 +140,68 @@ def reservation_allocated(name: str, uid: str) -> str:
     return json.dumps({"name": name, "uid": uid}, separators=(",", ":"))
 
 
+def cpu_bind_policy(state_required: str, state_preferred: str, node_policy: str = "") -> Tuple[str, bool]:
+    """``getCPUBindPolicy`` (``nodenumaresource/util.go:85-103``): the pod's required policy wins; otherwise the
+    node's CPU bind policy label (``FullPCPUsOnly`` / ``SpreadByPCPUs``; a static kubelet CPU manager with
+    ``full-pcpus-only`` is the caller's ``FullPCPUsOnly``) makes the policy required; otherwise the PreFilter's
+    preferred policy (the plugin default already filled in for ``Default``), not required."""
+    if state_required:
+        return state_required, True
+    if node_policy == NODE_CPU_BIND_POLICY_SPREAD_BY_PCPUS:
+        return CPU_BIND_POLICY_SPREAD_BY_PCPUS, True
+    if node_policy == NODE_CPU_BIND_POLICY_FULL_PCPUS_ONLY:
+        return CPU_BIND_POLICY_FULL_PCPUS, True
+    return state_preferred, False
+
+
+def resource_spec_json(spec: Dict[str, str]) -> str:
+    """``json.Marshal(ResourceSpec)`` (``apis/extension/numa_aware.go:60-68``): the struct's field order, empty
+    fields omitted."""
+    out = {}
+    for k in ("requiredCPUBindPolicy", "preferredCPUBindPolicy", "preferredCPUExclusivePolicy"):
+        if spec.get(k):
+            out[k] = spec[k]
+    return json.dumps(out, separators=(",", ":"))
+
+
+def resource_spec_writeback(existing: Optional[Dict[str, str]], state_required: str, state_preferred: str,
+                            node_policy: str = "") -> Optional[Dict[str, str]]:
+    """``appendResourceSpecIfMissed`` (``nodenumaresource/plugin.go:552-578``), run by PreBind for every pod that
+    requests CPU binding on the chosen node (``requestCPUBind``).  ``existing`` is the pod's own resource-spec
+    annotation (parsed; None when absent); ``state_required`` / ``state_preferred`` are the PreFilter state's
+    policies (``plugin.go:238-261``: ``Default`` replaced by the plugin's DefaultCPUBindPolicy).  Returns the spec
+    to write back, or None when the reference leaves the annotation alone."""
+    policy, required = cpu_bind_policy(state_required, state_preferred, node_policy)
+    spec = dict(existing or {})
+    write = False
+    if required and spec.get("requiredCPUBindPolicy", "") in ("", CPU_BIND_POLICY_DEFAULT):
+        spec["requiredCPUBindPolicy"] = policy
+        write = True
+    if spec.get("preferredCPUBindPolicy", "") == CPU_BIND_POLICY_DEFAULT:
+        spec["preferredCPUBindPolicy"] = policy
+        write = True
+    if not spec.get("requiredCPUBindPolicy") and not spec.get("preferredCPUBindPolicy") and policy:
+        spec["preferredCPUBindPolicy"] = policy
+        write = True
+    return spec if write else None
+
+
 def prebind_annotations(result, cpus: Sequence[int] = (), numa_nodes: Sequence[Tuple[int, int, int]] = (),
                         gpu_request: Optional[Tuple[Optional[int], int, int]] = None, rdma_request: int = 0,
-                        reservation: Optional[Tuple[str, str]] = None) -> Dict[str, str]:
+                        reservation: Optional[Tuple[str, str]] = None,
+                        cpu_bind: Optional[Tuple[Optional[Dict[str, str]], str, str, str]] = None) -> Dict[str, str]:
     """Every PreBind annotation of one scheduled pod: ``result`` is its ``ks_result`` row (a mapping or numpy
     record with ``gpu_minors`` / ``rdma_minors``); ``gpu_request`` = (core or None, memory bytes, ratio) per
-    instance; ``reservation`` = (name, uid) of ``result.reservation``'s row when it is >= 0."""
+    instance; ``reservation`` = (name, uid) of ``result.reservation``'s row when it is >= 0; ``cpu_bind`` =
+    (the pod's resource-spec annotation parsed or None, PreFilter required policy, PreFilter preferred policy, the
+    chosen node's CPU bind policy) for a pod that requests CPU binding there (``requestCPUBind``, which a cpuset in
+    ``cpus`` implies) — NodeNUMAResource PreBind then also writes the resource-spec annotation back when
+    ``appendResourceSpecIfMissed`` does (``plugin.go:460-464``)."""
     out: Dict[str, str] = {}
+    if cpu_bind is not None:
+        spec = resource_spec_writeback(*cpu_bind)
+        if spec is not None:
+            out[ANNOTATION_RESOURCE_SPEC] = resource_spec_json(spec)
     if len(cpus) or len(numa_nodes):
         out[ANNOTATION_RESOURCE_STATUS] = resource_status(cpus, numa_nodes)
     gm, rm = int(result["gpu_minors"]), int(result["rdma_minors"])

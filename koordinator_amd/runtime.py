@@ -89,6 +89,7 @@ def lib() -> C.CDLL:
     L.ks_read_quota_used.argtypes = [vp, abi.P64]
     L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
     L.ks_set_profile.argtypes = [vp, C.c_int32]
+    L.ks_set_pipeline.argtypes = [vp, C.c_int32]
     L.ks_shard_unique_id.argtypes = [C.POINTER(C.c_uint8)]
     L.ks_shard_init.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32]
     for name in abi.EXPORTED_SYMBOLS:
@@ -363,6 +364,11 @@ class Evaluator:
 
     def set_profile(self, on: bool):
         self._chk(self.L.ks_set_profile(self.h, 1 if on else 0))
+
+    def set_pipeline(self, mode: int):
+        """0 off, 1 automatic (large clusters), 2 always: overlap each pass's sweep with the previous commit
+        (results are identical either way)."""
+        self._chk(self.L.ks_set_pipeline(self.h, int(mode)))
 
     def stats(self) -> dict:
         s = abi.KsStats()

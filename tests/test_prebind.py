@@ -3,6 +3,7 @@ expect, and Kubernetes Quantity / CPUSet string forms.  CPU only."""
 import json
 
 import numpy as np
+import pytest
 
 from koordinator_amd import prebind as pb
 
@@ -71,3 +72,47 @@ def test_prebind_annotations_from_result_rows():
         "rdma": [{"minor": 1, "resources": {"koordinator.sh/rdma": "1"}}]}
     assert ann[pb.ANNOTATION_RESERVATION_ALLOCATED] == '{"name":"r-1","uid":"uid-1"}'
     assert pb.ANNOTATION_RESOURCE_STATUS not in ann
+
+
+# Test_appendResourceSpecIfMissed (nodenumaresource/plugin_test.go:1537-1645): (pod resource-spec, node CPU bind
+# policy label, PreFilter state (required, preferred)) -> the pod's resource-spec afterwards
+APPEND_RESOURCE_SPEC_CASES = [
+    ("declared preferred cpu bind policy", {"preferredCPUBindPolicy": "SpreadByPCPUs"}, "", ("", "SpreadByPCPUs"),
+     {"preferredCPUBindPolicy": "SpreadByPCPUs"}),
+    ("declared default preferred cpu bind policy", {"preferredCPUBindPolicy": "Default"}, "", ("", "SpreadByPCPUs"),
+     {"preferredCPUBindPolicy": "SpreadByPCPUs"}),
+    ("declared required cpu bind policy", {"requiredCPUBindPolicy": "SpreadByPCPUs"}, "",
+     ("SpreadByPCPUs", "SpreadByPCPUs"), {"requiredCPUBindPolicy": "SpreadByPCPUs"}),
+    ("declared required and default preferred", {"requiredCPUBindPolicy": "SpreadByPCPUs", "preferredCPUBindPolicy": "Default"},
+     "", ("SpreadByPCPUs", "SpreadByPCPUs"),
+     {"requiredCPUBindPolicy": "SpreadByPCPUs", "preferredCPUBindPolicy": "SpreadByPCPUs"}),
+    ("declared required, default preferred and exclusive policy",
+     {"requiredCPUBindPolicy": "SpreadByPCPUs", "preferredCPUBindPolicy": "Default", "preferredCPUExclusivePolicy": "PCPULevel"},
+     "", ("SpreadByPCPUs", "SpreadByPCPUs"),
+     {"requiredCPUBindPolicy": "SpreadByPCPUs", "preferredCPUBindPolicy": "SpreadByPCPUs",
+      "preferredCPUExclusivePolicy": "PCPULevel"}),
+    ("LS Pod assigned on node with FullPCPUsOnly", None, "FullPCPUsOnly", ("", ""), {"requiredCPUBindPolicy": "FullPCPUs"}),
+]
+
+
+@pytest.mark.parametrize("name,spec,node_policy,state,want", APPEND_RESOURCE_SPEC_CASES, ids=[c[0] for c in APPEND_RESOURCE_SPEC_CASES])
+def test_append_resource_spec_if_missed(name, spec, node_policy, state, want):
+    got = pb.resource_spec_writeback(spec, state[0], state[1], node_policy)
+    final = got if got is not None else (spec or {})
+    assert final == want
+
+
+def test_prebind_writes_resource_spec_for_defaulted_preferred_policy():
+    # TestPlugin_PreBindWithCPUBindPolicyNone (plugin_test.go:1328-1381): a pod without a resource-spec whose
+    # PreFilter state carries the default FullPCPUs preferred policy gets {"preferredCPUBindPolicy":"FullPCPUs"}
+    # next to its resource-status {"cpuset":"0-3"}
+    r = {"gpu_minors": 0, "rdma_minors": 0}
+    out = pb.prebind_annotations(r, cpus=[0, 1, 2, 3], cpu_bind=(None, "", "FullPCPUs", ""))
+    assert out[pb.ANNOTATION_RESOURCE_SPEC] == '{"preferredCPUBindPolicy":"FullPCPUs"}'
+    assert out[pb.ANNOTATION_RESOURCE_STATUS] == '{"cpuset":"0-3"}'
+    # a pod that already states the policy: no write-back (only the status)
+    out = pb.prebind_annotations(r, cpus=[0, 1], cpu_bind=({"requiredCPUBindPolicy": "FullPCPUs"}, "FullPCPUs", "FullPCPUs", ""))
+    assert pb.ANNOTATION_RESOURCE_SPEC not in out
+    # a node label overrides the preferred policy and makes it required
+    out = pb.prebind_annotations(r, cpus=[0, 1], cpu_bind=(None, "", "FullPCPUs", "SpreadByPCPUs"))
+    assert out[pb.ANNOTATION_RESOURCE_SPEC] == '{"requiredCPUBindPolicy":"SpreadByPCPUs"}'
