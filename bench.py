@@ -11,6 +11,8 @@ before the timed region (host -> HBM copies are not timed; everything computed f
 The metric names 5k AND 100k nodes, so the same line carries ``c5``: configs[4] (1M pods x 100k nodes,
 Fit + LoadAware) timed the same way — on one GPU at N=1, node-sharded over the N ranks at N>1 (strong
 scaling: every rank sweeps its node range, one RCCL allgather of per-shard candidates per pass).
+At N=1 it also carries ``c3`` (configs[2]: NUMA + DeviceShare joint allocation, 5k nodes) and ``c4`` (configs[3]:
+20k nodes with 50k Reservations), each with its own CPU baseline, sample parity and roofline.
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU.  ``value`` at N>1 is N
 independent C2 replicas (seed + rank; weak scaling: the 5k-node cluster does not warrant node sharding,
@@ -366,6 +368,9 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
     ap.add_argument("--c5-steps", type=int, default=1)
     ap.add_argument("--c5-warmup", type=int, default=1)
+    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 sub-records")
+    ap.add_argument("--sub-steps", type=int, default=3)
+    ap.add_argument("--sub-warmup", type=int, default=1)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -430,6 +435,22 @@ def main():
                 r5["parity"] = cb5["parity_with_gpu_on_sample"]
                 r5["speedup_vs_cpu_baseline"] = round(r5["value"] / cb5["value"], 2)
             out["c5"] = r5
+    if not args.no_sub and world == 1 and args.config == "c2":
+        # SURVEY's C3 (NUMA + DeviceShare) and C4 (Reservation) workloads, each timed like the headline with its own
+        # CPU baseline, sample parity and commit roofline (single GPU: neither is node-sharded)
+        for sub in ("c3", "c4"):
+            ws = build_workload(sub, seed=20261015)
+            rs, ress = run_config(ws, args, None, 1, 0, 0, False, args.sub_steps, args.sub_warmup, sub,
+                                  not args.no_profile)
+            rs["workload"] = workload_desc(ws)
+            rs["parallelism"] = "single-gpu"
+            if not args.no_cpu_baseline:
+                cbs = cpu_baseline(ws, ress, args.cpu_budget_s, args.cpu_extra_budget_s)
+                rs["cpu_baseline"] = cbs
+                rs["parity"] = cbs["parity_with_gpu_on_sample"]
+                rs["speedup_vs_cpu_baseline"] = round(rs["value"] / cbs["value"], 2)
+            out[sub] = rs
+            del ws, ress
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -540,7 +540,8 @@ int ks_load_quotas(ks_ctx *ctx, const ks_quota_cols *quotas, int32_t q);
 /* ---- informer deltas for the other tables (f1): rows replaced in place on the device, the rest of each table
  * untouched; idx / rows are distinct.  A batch of deltas is applied at a ks_schedule boundary (the snapshot
  * semantics); ks_checkpoint after them if the bench restores. ---- */
-/* deviceshare nodeDeviceCache.updateNodeDevice (device_cache.go:489-527): rows[i] is node idx[i]'s devices */
+/* deviceshare nodeDeviceCache.updateNodeDevice (device_cache.go:489-527): rows[i] is node idx[i]'s devices;
+ * KS_ESTATE for a node that holds a ks_assume'd device pod (see ks_assume) */
 int ks_update_devices(ks_ctx *ctx, const int32_t *idx, const ks_device_cols *rows, int64_t m);
 /* NodeResourceTopology / NodeAllocation changes (nodenumaresource topology_eventhandler.go, resource_manager.go
  * Update / Release): node idx[i]'s CPU state from row i, topology indices into the table of the last
@@ -637,7 +638,10 @@ int ks_eval_pod_debug(ks_ctx *ctx, const ks_pod_cols *pod, uint32_t *reasons, in
  * KS_S_RESERVE_FAILED (NodeNUMAResource could not allocate the cpuset; nothing changed), the reservation row
  * and the GPU / RDMA minors; score is 0.  cpuset (optional): the pod's CPUs [KS_CPU_WORDS]; numa_alloc
  * (optional): its NUMA-node allocation [KS_MAX_NUMA][2] (cpu milli, memory) on a NUMA-policy node.  Keep them
- * for ks_unreserve. */
+ * for ks_unreserve.  The assume reuses the batch's cpuset / NUMA buffers: ks_fetch_cpusets and ks_fetch_numa_alloc
+ * return KS_ESTATE until the next ks_schedule*.  A node holding an assumed device pod refuses ks_update_devices
+ * (KS_ESTATE) until the pod is ks_unreserve'd, because Unreserve derives the per-instance request from the node's
+ * device totals (devicehandler_gpu.go:40-98), which must be the ones Reserve saw. */
 int ks_assume(ks_ctx *ctx, const ks_pod_cols *pod, int32_t node, ks_result *out, uint64_t *cpuset,
               int64_t *numa_alloc);
 

@@ -976,7 +976,13 @@ struct ks_ctx {
   char* numa_ckpt = nullptr;       // checkpoint copy of the mutable NUMA block (numa_mut_bytes)
   int64_t numa_policy_nodes = 0;  // nodes with a NUMA topology policy
   bool cpu_bind_labels = false;   // a node CPU bind policy was loaded (sticky)
-  bool cpu_bind_required = false; // a pod with a required CPU bind policy was staged (sticky)
+  bool cpu_bind_required = false;    // the current operation's pods include a required CPU bind policy
+  bool val_bind_required = false;    // ... set by the last successful validate_pods
+  bool staged_bind_required = false; // ... of the staged batch (ks_stage_pods)
+  bool cpusets_clobbered = false;    // ks_assume reused the batch's cpuset / NUMA buffers since the last schedule
+  // nodes with device pods placed by ks_assume and not yet ks_unreserve'd: their Unreserve re-derives the
+  // per-instance request from the node's device totals, so ks_update_devices must not change those meanwhile
+  std::vector<int32_t> h_dev_assumed, h_dev_assumed_ckpt;
   std::vector<int8_t> h_numa_k;    // per node: NUMA node count of a policy node (0 = no policy / none)
   std::vector<uint16_t> h_dev_ids; // per node: NUMA ids of the device topology (DeviceShare hints)
   std::vector<int8_t> h_cpu_nn;    // per node: NUMA nodes of its CPU topology (0 = none, -1 = ids not 0..n-1)
@@ -1464,6 +1470,7 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (int rc = validate_nodes(ctx, nodes, n); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->h_dev_assumed.clear();
   dev_free(ctx->node_blob);
   dev_free(ctx->ckpt_blob);
   void* p = ctx->sweep_out;
@@ -1777,6 +1784,7 @@ int ks_load_devices(ks_ctx* ctx, const ks_device_cols* dev, int64_t n) {
   if (n != ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_load_devices: %lld rows for %lld nodes", (long long)n, (long long)ctx->n);
   if (!ctx->cfg.deviceshare.enable) KS_FAIL(ctx, KS_ESTATE, "ks_load_devices: the DeviceShare plugin is not enabled");
   HIPCHK(ctx, hipSetDevice(ctx->device));
+  ctx->h_dev_assumed.clear();  // a full reload carries its own usage
   return dev_install(ctx, dev);
 }
 
@@ -1986,6 +1994,7 @@ int ks_read_cpu_state(ks_ctx* ctx, uint64_t* allocated, uint64_t* excl_pcpu, uin
 int ks_fetch_cpusets(ks_ctx* ctx, uint64_t* out, int32_t p) {
   if (!ctx || (p > 0 && !out) || p < 0) return ctx ? (ctx->err = "ks_fetch_cpusets: bad args", KS_EINVAL) : KS_EINVAL;
   if (p > ctx->np) KS_FAIL(ctx, KS_EINVAL, "ks_fetch_cpusets: %d pods requested, %d scheduled", p, ctx->np);
+  if (p > 0 && ctx->cpusets_clobbered) KS_FAIL(ctx, KS_ESTATE, "ks_fetch_cpusets: a ks_assume since the last schedule overwrote them");
   if (p == 0) return KS_OK;
   if (!ctx->cpuset_out || ctx->cpuset_cap < p) {
     memset(out, 0, (size_t)p * sizeof(CpuSet));
@@ -2528,6 +2537,7 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
     if (check_range64(ctx, c, p, "pod quantity") != KS_OK) return KS_EINVAL;
   for (int k = 0; k < KS_MAX_SCALARS; ++k)
     if (check_range64(ctx, pc->req_scalar[k], p, "pod scalar") != KS_OK) return KS_EINVAL;
+  bool any_req = false;
   if (ctx->cfg.numa.enable && pc->flags) {
     for (int32_t i = 0; i < p; ++i) {
       if (!(pc->flags[i] & KS_POD_CPU_BIND)) continue;
@@ -2540,7 +2550,7 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
       // a required policy on a NUMA-policy node runs through FilterByNUMANode's per-NUMA allocation: not modelled
       if (req && ctx->numa_policy_nodes > 0)
         KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: a required CPU bind policy together with NUMA topology policies is not supported", i);
-      ctx->cpu_bind_required |= req;
+      any_req |= req;
       if (cpu <= 0 || cpu % 1000 != 0 || cpu / 1000 > KS_MAX_CPUS)
         KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
       // a preferred FullPCPUs request that is not a whole number of cores takes split cores in takeCPUs'
@@ -2552,7 +2562,6 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
             KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: FullPCPUs request of %lld CPUs is not a whole number of %d-thread cores", i,
                     (long long)(cpu / 1000), cpc);
     }
-    cores_mode(ctx);
   }
   if (pc->joint) {
     for (int32_t i = 0; i < p; ++i) {
@@ -2591,7 +2600,16 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
     ctx->nsc = need <= 2 ? 2 : 4;
     ctx->kc.nsc = ctx->nsc;
   }
+  // only a batch (or pod) that passed every check decides the core-count mode, and only for its own operation
+  // (bind_mode): a rejected or probed pod leaves later schedules as they were
+  ctx->val_bind_required = any_req;
   return KS_OK;
+}
+
+// Cfg.cores for the operation about to run: node CPU bind labels, or a required policy among its pods
+static void bind_mode(ks_ctx* ctx, bool required) {
+  ctx->cpu_bind_required = required;
+  cores_mode(ctx);
 }
 
 int ks_stage_pods(ks_ctx* ctx, const ks_pod_cols* pods, int32_t p) {
@@ -2604,6 +2622,7 @@ int ks_stage_pods(ks_ctx* ctx, const ks_pod_cols* pods, int32_t p) {
   if (ensure_stage(ctx, ctx->st, p) != KS_OK) return KS_ENOMEM;
   if (p > 0 && stage_cols(ctx, ctx->st, pods, p) != KS_OK) return KS_EHIP;
   ctx->np = p;
+  ctx->staged_bind_required = ctx->val_bind_required;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -3028,6 +3047,8 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
 static int schedule_staged_impl(ks_ctx* ctx) {
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "schedule before ks_load_nodes");
   HIPCHK(ctx, hipSetDevice(ctx->device));
+  bind_mode(ctx, ctx->staged_bind_required);
+  ctx->cpusets_clobbered = false;
   ctx->stats = ks_stats{};
   const int32_t np = ctx->np;
   if (np == 0) return KS_OK;
@@ -3214,6 +3235,7 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->h_dev_assumed_ckpt = ctx->h_dev_assumed;
   return KS_OK;
 }
 
@@ -3235,6 +3257,7 @@ int ks_restore(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
   }
+  ctx->h_dev_assumed = ctx->h_dev_assumed_ckpt;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -3295,6 +3318,10 @@ int ks_update_devices(ks_ctx* ctx, const int32_t* idx, const ks_device_cols* row
   if (!ctx->dev_blob || !ctx->cfg.deviceshare.enable) KS_FAIL(ctx, KS_ESTATE, "ks_update_devices without a device table");
   std::vector<int32_t> ix;
   if (int rc = check_idx(ctx, idx, m, ctx->n, "ks_update_devices", ix); rc != KS_OK) return rc;
+  for (int32_t i : ix)
+    if ((size_t)i < ctx->h_dev_assumed.size() && ctx->h_dev_assumed[(size_t)i] > 0)
+      KS_FAIL(ctx, KS_ESTATE, "ks_update_devices: node %d holds %d assumed device pod(s); ks_unreserve them first (their "
+              "Unreserve subtracts the request derived from the current device totals)", i, ctx->h_dev_assumed[(size_t)i]);
   HIPCHK(ctx, hipSetDevice(ctx->device));
   std::vector<uint32_t> flags((size_t)m, 0);
   std::vector<int64_t> total((size_t)kDevTW * m, 0), used((size_t)kDevQW * m, 0);
@@ -3432,6 +3459,7 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
   if (!ctx || !pod) return ctx ? (ctx->err = "ks_eval_pod: bad args", KS_EINVAL) : KS_EINVAL;
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_eval_pod before ks_load_nodes");
   if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
+  bind_mode(ctx, ctx->val_bind_required);
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ensure_stage(ctx, ctx->est, 1) != KS_OK) return KS_ENOMEM;
   if (stage_cols(ctx, ctx->est, pod, 1) != KS_OK || prep_stage(ctx, ctx->est, 1) != KS_OK) return KS_EHIP;
@@ -3602,6 +3630,7 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
   if (node < 0 || node >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_assume: node %d out of range", node);
   if (ctx->cfg.quota.enable && pod->quota && !ctx->quota_blob) KS_FAIL(ctx, KS_ESTATE, "ks_assume: quotas not loaded");
   if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
+  bind_mode(ctx, ctx->val_bind_required);
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (int rc = commit_attr_set(ctx); rc != KS_OK) return rc;
   if (ensure_stage(ctx, ctx->ast, 1) != KS_OK || ensure_cpuset_bufs(ctx, 1) != KS_OK) return KS_ENOMEM;
@@ -3652,6 +3681,13 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
     memset(numa_alloc, 0, sizeof(int64_t) * KS_MAX_NUMA * 2);
     for (int k = 0; k < kNumaDev; ++k)
       for (int r = 0; r < 2; ++r) numa_alloc[k * 2 + r] = na[r * kNumaDev + k];
+  }
+  // the assume wrote pod 0's slots of the batch's cpuset and NUMA-allocation buffers: the last ks_schedule*'s
+  // CPU sets are gone, so ks_fetch_cpusets / ks_fetch_numa_alloc refuse until the next schedule
+  ctx->cpusets_clobbered = true;
+  if (out->status == KS_S_SCHEDULED && (out->gpu_minors | out->rdma_minors)) {
+    if (ctx->h_dev_assumed.size() < (size_t)ctx->n) ctx->h_dev_assumed.resize((size_t)ctx->n, 0);
+    ++ctx->h_dev_assumed[(size_t)node];
   }
   if (out->node != node && out->status == KS_S_SCHEDULED)
     KS_FAIL(ctx, KS_EHIP, "ks_assume: placed on node %d instead of %d", out->node, node);
@@ -3714,12 +3750,15 @@ int ks_unreserve(ks_ctx* ctx, const ks_pod_cols* pod, const ks_result* r, const 
   HIPCHK(ctx, hipGetLastError());
   if (rb && rsv_launch_base(ctx, d_idx, 1, +1, 1) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if ((r->gpu_minors | r->rdma_minors) && (size_t)node < ctx->h_dev_assumed.size() && ctx->h_dev_assumed[(size_t)node] > 0)
+    --ctx->h_dev_assumed[(size_t)node];
   return KS_OK;
 }
 
 int ks_fetch_numa_alloc(ks_ctx* ctx, int64_t* out, int32_t p) {
   if (!ctx || (p > 0 && !out) || p < 0) return ctx ? (ctx->err = "ks_fetch_numa_alloc: bad args", KS_EINVAL) : KS_EINVAL;
   if (p > ctx->np) KS_FAIL(ctx, KS_EINVAL, "ks_fetch_numa_alloc: %d pods requested, %d scheduled", p, ctx->np);
+  if (p > 0 && ctx->cpusets_clobbered) KS_FAIL(ctx, KS_ESTATE, "ks_fetch_numa_alloc: a ks_assume since the last schedule overwrote it");
   if (p == 0) return KS_OK;
   memset(out, 0, (size_t)p * KS_MAX_NUMA * 2 * 8);
   if (!ctx->numa_alloc || ctx->cpuset_cap < p) return KS_OK;

@@ -116,22 +116,43 @@ def _minors(mask: int) -> List[int]:
 
 
 def device_allocated(gpu_minors: int = 0, gpu_core: Optional[int] = None, gpu_memory: int = 0,
-                     gpu_memory_ratio: int = 0, rdma_minors: int = 0, rdma: int = 0) -> str:
+                     gpu_memory_ratio: int = 0, rdma_minors: int = 0, rdma: int = 0, *,
+                     gpu_memory_format: str = "BinarySI", gpu_order: Optional[Sequence[int]] = None,
+                     rdma_order: Optional[Sequence[int]] = None) -> str:
     """device-allocated annotation from the ``ks_result`` minor masks and the pod's per-instance request
-    (``devicehandler_gpu.go:56-63`` / ``devicehandler_default.go:58``: the request divided by the desired device
-    count; ``gpu_core`` None when the pod asked for no gpu-core).  Minors ascend within a type, as
-    ``sortDeviceResourcesByMinor`` leaves them; the type keys and resource names sort as Go's map marshalling
-    does."""
+    (``CalcDesiredRequestsAndCount``, ``devicehandler_gpu.go:40-64`` / ``devicehandler_default.go:58``).
+
+    * Several GPUs (memory ratio > 100 and a multiple of 100): the per-instance list is rebuilt with all three
+      names, so gpu-core is present (``gpuCore.Value()/desiredCount``, 0 when the pod asked for none), gpu-memory
+      BinarySI and the ratio DecimalSI.
+    * One GPU: the pod's own request list after ``fillGPUTotalMem``: gpu-core only when the pod asked for it
+      (``gpu_core`` None otherwise), gpu-memory in the pod's own Quantity format when the pod gave bytes
+      (``gpu_memory_format``; BinarySI when it was derived from the ratio by ``memoryRatioToBytes``).
+    * Entries follow the allocation order, ``sortDeviceResourcesByMinor`` (``device_allocator.go:415-433``:
+      preferred first, then device score descending, then minor).  ``gpu_order`` / ``rdma_order`` give it when the
+      caller has it; without them minors ascend, which is the reference's order whenever the allocated devices
+      scored alike (e.g. all free) and otherwise differs only in the order of the list's entries.
+    """
+    def ordered(mask: int, order: Optional[Sequence[int]]) -> List[int]:
+        ms = _minors(mask)
+        if order is None:
+            return ms
+        o = [int(m) for m in order]
+        if sorted(o) != ms:
+            raise ValueError(f"allocation order {o} does not list the minors of mask {mask:#x}")
+        return o
+
     alloc: Dict[str, list] = {}
     if gpu_minors:
-        rl = {RESOURCE_GPU_MEMORY: quantity_string(gpu_memory, "BinarySI"),
+        multi = bin(int(gpu_minors)).count("1") > 1  # one instance per minor: desiredCount > 1
+        rl = {RESOURCE_GPU_MEMORY: quantity_string(gpu_memory, "BinarySI" if multi else gpu_memory_format),
               RESOURCE_GPU_MEMORY_RATIO: quantity_string(gpu_memory_ratio, "DecimalSI")}
-        if gpu_core is not None:
-            rl[RESOURCE_GPU_CORE] = quantity_string(gpu_core, "DecimalSI")
-        alloc["gpu"] = [{"minor": m, "resources": rl} for m in _minors(gpu_minors)]
+        if gpu_core is not None or multi:
+            rl[RESOURCE_GPU_CORE] = quantity_string(gpu_core or 0, "DecimalSI")
+        alloc["gpu"] = [{"minor": m, "resources": rl} for m in ordered(gpu_minors, gpu_order)]
     if rdma_minors:
         alloc["rdma"] = [{"minor": m, "resources": {RESOURCE_RDMA: quantity_string(rdma, "DecimalSI")}}
-                         for m in _minors(rdma_minors)]
+                         for m in ordered(rdma_minors, rdma_order)]
     return _marshal(alloc)
 
 

@@ -95,3 +95,33 @@ def test_read_nodes_leaves_state_alone(runtime, oracle_lib):
         assert np.array_equal(ra[k], rb[k]), k
     a.close()
     b.close()
+
+
+def test_assume_guards(runtime):
+    """ks_assume overwrites the batch's cpuset / NUMA buffers (ks_fetch_cpusets refuses until the next schedule),
+    and a node holding an assumed device pod refuses ks_update_devices until the pod is unreserved: its Unreserve
+    re-derives the per-instance request from the node's device totals."""
+    from test_gpu_deltas import dev_rows
+
+    w = workloads()[1]  # C3: devices + cpusets
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    ev.schedule(w.pods.rows(range(20)))
+    ev.fetch_cpusets(20)
+    gpu = [i for i in range(20, 200) if w.pods.gpu_core[i] > 0 or w.pods.gpu_memory_ratio[i] > 0]
+    pod = w.pods.rows([gpu[0]])
+    _, _, tot = ev.eval_pod(pod)
+    node = pick(tot)
+    assert node >= 0
+    r, cs, na = ev.assume(pod, node)
+    assert r[0]["status"] == abi.KS_S_SCHEDULED and r[0]["gpu_minors"] != 0
+    with pytest.raises(runtime.KsError):
+        ev.fetch_cpusets(20)
+    idx = np.array([node], np.int32)
+    with pytest.raises(runtime.KsError):
+        ev.update_devices(idx, dev_rows(w.devices, idx))
+    ev.update_devices(np.array([(node + 1) % w.nodes.n], np.int32), dev_rows(w.devices, np.array([(node + 1) % w.nodes.n])))
+    ev.unreserve(pod, r, cs, na)
+    ev.update_devices(idx, dev_rows(w.devices, idx))
+    ev.schedule(w.pods.rows(range(20, 40)))
+    ev.fetch_cpusets(20)
+    ev.close()

@@ -1,7 +1,7 @@
 """GPU: the informer-delta entry points (ks_update_devices / _cpu_state / _quotas / _reservation_usage) leave
-the context exactly as a full reload of the changed tables would -- same placements, scores, minors, CPUs and
+the context exactly as the CPU oracle loaded with the merged tables -- same placements, scores, minors, CPUs and
 state after scheduling a queue -- on C3 (devices, CPU state, SingleNUMANode nodes), C2 (quotas) and C4
-(reservation usage)."""
+(reservation usage).  The HIP context gets the old tables plus the delta; the oracle gets the new tables whole."""
 import numpy as np
 import pytest
 
@@ -10,6 +10,10 @@ from koordinator_amd import abi, synth
 from koordinator_amd.cluster import CpuState, DeviceTable, QuotaTable
 
 pytestmark = pytest.mark.gpu
+
+
+def oracle_on(oracle_lib, w, nodes=None):
+    return oracle_lib.Oracle(w.cfg, (nodes if nodes is not None else w.nodes).copy(), nthreads=8, **w.tables())
 
 
 @pytest.fixture(scope="module")
@@ -47,6 +51,7 @@ def quota_rows(t: QuotaTable, idx) -> QuotaTable:
 
 
 def check_same(runtime, a, b, w, label):
+    """a: the HIP context after the deltas; b: the oracle on the merged tables."""
     ra, rb = a.schedule(w.pods), b.schedule(w.pods)
     for k in ("node", "status", "score", "reservation", "gpu_minors", "rdma_minors"):
         assert np.array_equal(ra[k], rb[k]), f"{label}: {k}"
@@ -55,7 +60,7 @@ def check_same(runtime, a, b, w, label):
     assert_states_equal(state(a, w), state(b, w), label)
 
 
-def test_update_devices_and_cpu_state(runtime):
+def test_update_devices_and_cpu_state(runtime, oracle_lib):
     w = synth.c3(seed=91, n_nodes=400, n_pods=500)
     w2 = synth.c3(seed=91, n_nodes=400, n_pods=500)  # same nodes; devices / CPU state re-drawn below
     rng = np.random.default_rng(5)
@@ -77,15 +82,14 @@ def test_update_devices_and_cpu_state(runtime):
     a.update_cpu_state(idx, cpu_rows(cs, idx))
     w2.devices, w2.cpus = dv, cs
     # the node table's cpuset counts follow the CPU state (numa_cpuset_cpus), as the host would resend them
-    nodes = w.nodes.copy()
-    b = runtime.Evaluator(w.cfg, nodes, **w2.tables())
+    b = oracle_on(oracle_lib, w2, w.nodes)
     w.devices, w.cpus = dv, cs
     check_same(runtime, a, b, w, "devices + cpu")
     a.close()
     b.close()
 
 
-def test_update_quotas(runtime):
+def test_update_quotas(runtime, oracle_lib):
     w = synth.c2(n_nodes=500, n_pods=800, n_quotas=16)
     q2 = w.quotas.copy()
     idx = np.array([1, 4, 7, 11], np.int32)
@@ -94,13 +98,13 @@ def test_update_quotas(runtime):
     a = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
     a.update_quotas(idx, quota_rows(q2, idx))
     w.quotas = q2
-    b = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    b = oracle_on(oracle_lib, w)
     check_same(runtime, a, b, w, "quotas")
     a.close()
     b.close()
 
 
-def test_update_reservation_usage(runtime):
+def test_update_reservation_usage(runtime, oracle_lib):
     w = synth.c4(n_nodes=800, n_reservations=2000, n_pods=600)
     rs2 = w.reservations.copy()
     rng = np.random.default_rng(9)
@@ -110,7 +114,7 @@ def test_update_reservation_usage(runtime):
     a = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
     a.update_reservation_usage(rows, rs2.allocated[:, rows], rs2.assigned[rows])
     w.reservations = rs2
-    b = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    b = oracle_on(oracle_lib, w)
     check_same(runtime, a, b, w, "reservation usage")
     a.close()
     b.close()

@@ -79,6 +79,22 @@ def test_c2_quota_schedule_matches_oracle(runtime, oracle_lib):
     assert 0 < rejected.sum() < len(rejected)
 
 
+def test_c2_full_queue_matches_oracle(runtime, oracle_lib):
+    """The headline workload exactly as bench.py runs it: all 10k pods of C2 onto its 5k nodes with the 32 quotas."""
+    w = synth.c2()
+    cfg = w.profile.to_ks_config()
+    ev = runtime.Evaluator(cfg, w.nodes.copy(), w.quotas.copy())
+    got = ev.schedule(w.pods)
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), w.quotas.copy(), nthreads=16)
+    want = orc.schedule(w.pods)
+    assert_same_results(got, want, "C2-10k")
+    assert_same_state(ev.read_nodes(), orc.read_nodes(), "C2-10k")
+    assert np.array_equal(ev.read_quota_used(), orc.read_quota_used()), "C2-10k: quota used differs"
+    assert (got["status"] == 0).sum() > 8000
+    ev.close()
+    orc.close()
+
+
 @pytest.mark.parametrize("batch,cand", [(1, 1), (7, 2), (64, 1), (64, 64), (33, 5)])
 def test_batch_and_candidate_sizes(runtime, oracle_lib, batch, cand):
     rng = np.random.Generator(np.random.PCG64(100 + batch * 3 + cand))

@@ -220,7 +220,7 @@ def test_virtual_shards_match(runtime, oracle_lib):
 
 
 def test_c4_sample_matches_oracle(runtime, oracle_lib):
-    """The C4 benchmark cluster (20k nodes, 50k reservations) on its first 1500 pods."""
-    w = synth.c4(n_pods=1500)
+    """The C4 benchmark cluster (20k nodes, 50k reservations) on its first 5000 pods."""
+    w = synth.c4(n_pods=5000)
     got, st = check(runtime, oracle_lib, w.profile, w.nodes, w.reservations, w.pods, "c4")
     print("c4 sample stats", {k: st[k] for k in ("passes", "cut_passes", "rescans", "total_ms")})

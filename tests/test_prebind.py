@@ -19,6 +19,24 @@ def test_device_allocated_matches_reference_prebind_case():
     assert pb.device_allocated(gpu_minors=0b11, gpu_core=100, gpu_memory=16 * GI, gpu_memory_ratio=100) == want
 
 
+def test_device_allocated_multi_gpu_core_order_and_format():
+    # devicehandler_gpu.go:55-63: a multi-GPU request rebuilds the per-instance list with gpu-core even when the
+    # pod asked for none (0); a single GPU keeps the pod's own list (no gpu-core) and the pod's gpu-memory format
+    multi = json.loads(pb.device_allocated(gpu_minors=0b110, gpu_core=None, gpu_memory=8 * GI, gpu_memory_ratio=100))
+    assert [a["minor"] for a in multi["gpu"]] == [1, 2]
+    assert multi["gpu"][0]["resources"] == {"koordinator.sh/gpu-core": "0", "koordinator.sh/gpu-memory": "8Gi",
+                                            "koordinator.sh/gpu-memory-ratio": "100"}
+    one = json.loads(pb.device_allocated(gpu_minors=0b1000, gpu_core=None, gpu_memory=8_000_000_000,
+                                         gpu_memory_ratio=9, gpu_memory_format="DecimalSI"))
+    assert one["gpu"][0]["resources"] == {"koordinator.sh/gpu-memory": "8G", "koordinator.sh/gpu-memory-ratio": "9"}
+    # sortDeviceResourcesByMinor's order (score desc, then minor) when the caller has it
+    o = json.loads(pb.device_allocated(gpu_minors=0b1011, gpu_core=50, gpu_memory=4 * GI, gpu_memory_ratio=50,
+                                       gpu_order=[3, 0, 1], rdma_minors=0b101, rdma=100, rdma_order=[2, 0]))
+    assert [a["minor"] for a in o["gpu"]] == [3, 0, 1] and [a["minor"] for a in o["rdma"]] == [2, 0]
+    with pytest.raises(ValueError):
+        pb.device_allocated(gpu_minors=0b11, gpu_core=1, gpu_memory=GI, gpu_memory_ratio=1, gpu_order=[0, 2])
+
+
 def test_resource_status_matches_reference_prebind_case():
     # nodenumaresource/plugin_test.go:1281-1326: allocation CPUSet {0,1,2,3} -> ResourceStatus{CPUSet: "0-3"}
     got = pb.resource_status(cpus=[0, 1, 2, 3])
