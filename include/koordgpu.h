@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 4
+#define KS_ABI_VERSION 5
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -183,7 +183,8 @@ extern "C" {
 #define KS_SCORE_RESERVATION 2 /* after DefaultNormalizeScore (reservation/scoring.go:126-131) */
 #define KS_SCORE_NUMA 3        /* NodeNUMAResource scoreWithAmplifiedCPUs (nodenumaresource/scoring.go:98-114) */
 #define KS_SCORE_DEVICESHARE 4 /* after DefaultNormalizeScore (deviceshare/scoring.go:95-97) */
-#define KS_NUM_SCORE_PLUGINS 5
+#define KS_SCORE_BALANCED 5    /* upstream NodeResourcesBalancedAllocation (balanced_allocation.go, v1.24) */
+#define KS_NUM_SCORE_PLUGINS 6
 
 /* ---- per-node DeviceShare flags (ks_device_cols.flags) ---- */
 #define KS_DEV_PRESENT 0x1u /* nodeDeviceCache.getNodeDevice != nil (deviceshare/plugin.go:286-289) */
@@ -273,6 +274,20 @@ typedef struct ks_deviceshare_args {
   int64_t weight_rdma; /* koordinator.sh/rdma (default 1): scores RDMA minors and the RDMA part of scoreNode */
 } ks_deviceshare_args;
 
+/* Upstream NodeResourcesBalancedAllocation (kube-scheduler v1.24.15 noderesources/balanced_allocation.go, enabled with
+ * weight 1 by the v1beta2 default profile): score = int64((1 - std) * 100) over the fractions
+ * (Requested + pod request) / Allocatable, each capped at 1, of the listed resources with Allocatable != 0; std is
+ * |f_cpu - f_memory| / 2 for two fractions and 0 for fewer (balancedResourceScorer, useRequested = true).  The
+ * resource set is cpu and/or memory (NodeResourcesBalancedAllocationArgs.Resources; the v1beta2 default is both);
+ * other resources are refused.  Pod overhead is not modelled (the host folds it into the request vector). */
+#define KS_BAL_CPU 0x1
+#define KS_BAL_MEMORY 0x2
+typedef struct ks_balanced_args {
+  int32_t enable;
+  int32_t resources; /* KS_BAL_* bits */
+  int64_t plugin_weight;
+} ks_balanced_args;
+
 typedef struct ks_config {
   int32_t abi_version; /* = KS_ABI_VERSION */
   int32_t device;      /* HIP device ordinal */
@@ -286,6 +301,7 @@ typedef struct ks_config {
   ks_reservation_args reservation;
   ks_numa_args numa;
   ks_deviceshare_args deviceshare;
+  ks_balanced_args balanced; /* ABI 5 */
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -521,7 +537,8 @@ typedef struct ks_stats {
   int64_t diag[8];         /* diagnostic build only (KS_COMMIT_STAMPS): commit-phase cycle sums */
   int64_t bubble_passes;   /* pipelined passes whose commit did nothing (the pass before was cut) */
   double fixup_ms;         /* summed HIP-event time of the pipelined dirty-chunk re-sweeps */
-  int64_t pipelined;       /* 1 = the last call overlapped each pass's sweep with the previous commit */
+  int64_t pipelined;       /* 1 = the last call overlapped each pass's sweep with the previous commit; 2 = its
+                              select too, the lists patched after the commit (monotone plugin sets) */
 } ks_stats;
 
 typedef struct ks_ctx ks_ctx;

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 4
+KS_ABI_VERSION = 5
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
@@ -115,7 +115,10 @@ KS_SCORE_LOADAWARE = 1
 KS_SCORE_RESERVATION = 2
 KS_SCORE_NUMA = 3
 KS_SCORE_DEVICESHARE = 4
-KS_NUM_SCORE_PLUGINS = 5
+KS_SCORE_BALANCED = 5
+KS_NUM_SCORE_PLUGINS = 6
+KS_BAL_CPU = 0x1
+KS_BAL_MEMORY = 0x2
 
 KS_RSV_UNSCHEDULABLE = 0x1
 KS_RSV_ALLOCATE_ONCE = 0x2
@@ -176,6 +179,10 @@ class KsDeviceShareArgs(C.Structure):
                 ("weight_rdma", C.c_int64)]
 
 
+class KsBalancedArgs(C.Structure):
+    _fields_ = [("enable", C.c_int32), ("resources", C.c_int32), ("plugin_weight", C.c_int64)]
+
+
 class KsConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -190,6 +197,7 @@ class KsConfig(C.Structure):
         ("reservation", KsReservationArgs),
         ("numa", KsNumaArgs),
         ("deviceshare", KsDeviceShareArgs),
+        ("balanced", KsBalancedArgs),
     ]
 
 

@@ -128,6 +128,13 @@ class DeviceShareArgs:
 
 
 @dataclass
+class NodeResourcesBalancedAllocationArgs:
+    """Upstream NodeResourcesBalancedAllocationArgs (kube-scheduler v1.24 config/v1beta2 defaults: cpu and memory,
+    weight 1; the weights do not enter balancedResourceScorer, only the resource set does)."""
+    resources: Dict[str, int] = field(default_factory=lambda: {CPU: 1, MEMORY: 1})
+
+
+@dataclass
 class ElasticQuotaArgs:
     enable_runtime_quota: bool = True
     enable_check_parent_quota: bool = False
@@ -147,6 +154,8 @@ class SchedulerProfile:
     numa_weight: int = 1
     deviceshare: Optional[DeviceShareArgs] = None
     deviceshare_weight: int = 1
+    balanced: Optional[NodeResourcesBalancedAllocationArgs] = None  # upstream default plugin; None = disabled
+    balanced_weight: int = 1
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -222,6 +231,16 @@ class SchedulerProfile:
             c.deviceshare.weight_gpu_memory_ratio = d.resources.get(GPU_MEMORY_RATIO, 0)
             c.deviceshare.weight_rdma = d.resources.get(RDMA, 0)
             c.deviceshare.plugin_weight = self.deviceshare_weight
+        if self.balanced is not None:
+            c.balanced.enable = 1
+            for name in self.balanced.resources:
+                if name == CPU:
+                    c.balanced.resources |= abi.KS_BAL_CPU
+                elif name == MEMORY:
+                    c.balanced.resources |= abi.KS_BAL_MEMORY
+                else:
+                    raise ValidationError(f"NodeResourcesBalancedAllocation on {name} is not supported (cpu/memory only)")
+            c.balanced.plugin_weight = self.balanced_weight
         if self.reservation_weight is not None:
             c.reservation.enable = 1
             c.reservation.plugin_weight = int(self.reservation_weight)

@@ -996,6 +996,7 @@ struct ks_ctx {
   hipStream_t sstream = nullptr;   // shared by the process's contexts on this device (ensure_pipe), never destroyed
   hipStream_t cstream = nullptr;   // the pipelined commits: the CU the sweep stream leaves out (or `stream`)
   int32_t* pipe = nullptr;          // [0..1] speculative first pod per pass parity, [4..68] commit carry list
+  unsigned long long* pipe_top = nullptr;  // patched passes: [2][64] each pod's top after the list re-evaluation
   hipEvent_t pev_sel[kPipeEvents] = {};
   hipEvent_t pev_com[kPipeEvents] = {};
   int64_t pipe_k = 0;               // pass index within the current ks_schedule* call
@@ -1072,8 +1073,17 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.monotone_nd = k.monotone;
   if (k.dev) k.monotone = 0;  // a commit changes the pod's DeviceShare normalization max
   k.rsv = c.reservation.enable ? 1 : 0;
+  // upstream NodeResourcesBalancedAllocation: a commit can move a node's fractions closer together, i.e. raise its
+  // score, so keys are not monotone with it
+  k.bal = c.balanced.enable ? (c.balanced.resources & (KS_BAL_CPU | KS_BAL_MEMORY)) : 0;
+  k.bal_pw = c.balanced.enable ? (int32_t)c.balanced.plugin_weight : 0;
+  if (k.bal) {
+    k.monotone = 0;
+    k.monotone_nd = 0;
+  }
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
-                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw) + 1);
+                             (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw +
+                             k.bal_pw) + 1);
   // a commit into a reservation can raise that node's Reservation score for later pods
   if (k.rsv) k.monotone = 0;
   if (k.rsv) k.monotone_nd = 0;
@@ -1135,11 +1145,23 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
       return KS_EINVAL;
     }
   }
+  if (cfg->balanced.enable) {
+    const ks_balanced_args& ba = cfg->balanced;
+    if (ba.plugin_weight < 0 || ba.plugin_weight > 1000) {
+      g_create_error = "ks_create: NodeResourcesBalancedAllocation plugin weight out of range";
+      return KS_EINVAL;
+    }
+    if (ba.resources == 0 || (ba.resources & ~(KS_BAL_CPU | KS_BAL_MEMORY)) != 0) {
+      g_create_error = "ks_create: NodeResourcesBalancedAllocation resources other than cpu / memory are not supported";
+      return KS_EUNSUPPORTED;
+    }
+  }
   if (cfg->reservation.enable) {
     const int64_t fitla = 100 * ((cfg->fit.enable_score ? cfg->fit.plugin_weight : 0) +
                                  (cfg->loadaware.enable_score ? cfg->loadaware.plugin_weight : 0) +
                                  (cfg->numa.enable ? cfg->numa.plugin_weight : 0) +
-                                 (cfg->deviceshare.enable ? cfg->deviceshare.plugin_weight : 0));
+                                 (cfg->deviceshare.enable ? cfg->deviceshare.plugin_weight : 0) +
+                                 (cfg->balanced.enable ? cfg->balanced.plugin_weight : 0));
     if (cfg->reservation.plugin_weight <= fitla || cfg->reservation.plugin_weight > ((int64_t)1 << 40) ||
         (fitla + 1) * (kRsvOrderBase + 1) >= (1 << 26)) {
       g_create_error = "ks_create: Reservation plugin weight must exceed 100 x (Fit + LoadAware weights) (ks_rsv.h ranking)";
@@ -1166,20 +1188,21 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
     return KS_EHIP;
   }
   void* p = nullptr;
-  size_t cand_bytes = (size_t)kMaxBatch * kMaxCand;
+  // two sets of candidate lists (CandSet): pipelined passes select pass k+1 while pass k commits
+  size_t cand_bytes = (size_t)2 * kMaxBatch * kMaxCand;
   if (dev_alloc(ctx, &p, cand_bytes * 4) != KS_OK) goto fail;
   ctx->cand_chunk = (uint32_t*)p;
   if (dev_alloc(ctx, &p, cand_bytes * 8) != KS_OK) goto fail;
   ctx->cand_t = (uint2*)p;
-  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, 2 * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_bound = (uint64_t*)p;
-  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, 2 * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_top = (uint64_t*)p;
-  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, 2 * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_second = (uint64_t*)p;
-  if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, 2 * kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_total = (int32_t*)p;
-  if (dev_alloc(ctx, &p, kMaxBatch * 4) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, 2 * kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_count = (int32_t*)p;
   if (dev_alloc(ctx, &p, 64) != KS_OK) goto fail;
   ctx->cursor = (int32_t*)p;
@@ -1236,6 +1259,7 @@ void ks_destroy(ks_ctx* ctx) {
   dev_free(ctx->numa_blob);
   p = ctx->dnv; dev_free(p);
   p = ctx->pipe; dev_free(p);
+  p = ctx->pipe_top; dev_free(p);
   for (int i = 0; i < kPipeEvents; ++i) {
     if (ctx->pev_sel[i]) (void)hipEventDestroy(ctx->pev_sel[i]);
     if (ctx->pev_com[i]) (void)hipEventDestroy(ctx->pev_com[i]);
@@ -1510,7 +1534,8 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->d.cpu_free, 0xFF, (size_t)ctx->npad * 4, ctx->stream));  // no CPU topology yet
   ctx->cpu_loaded = false;
-  if (dev_alloc(ctx, &p, (size_t)ctx->nchunks * 64 * 8) != KS_OK) return KS_ENOMEM;
+  // two sweep outputs: patched pipelined passes sweep pass k+1 while pass k's re-sweep still reads pass k's
+  if (dev_alloc(ctx, &p, (size_t)2 * ctx->nchunks * 64 * 8) != KS_OK) return KS_ENOMEM;
   ctx->sweep_out = (uint2*)p;
   if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
@@ -2697,6 +2722,19 @@ static PassLaunch pass_launcher(int feat, int nsc) {
 }
 
 // The commit kernel's arguments for the pods of stage st (cursor ctx->cursor, `total` pods, `batch` per pass).
+// Candidate-list set i (0 or 1) of the context's double buffer; set 0 unless passes are pipelined.
+struct CandSet {
+  uint32_t* chunk;
+  uint2* t;
+  uint64_t *bound, *top, *second;
+  int32_t *count, *total;
+};
+static CandSet cand_set(const ks_ctx* ctx, int i) {
+  const size_t e = (size_t)i * kMaxBatch * kMaxCand, r = (size_t)i * kMaxBatch;
+  return CandSet{ctx->cand_chunk + e, ctx->cand_t + e, ctx->cand_bound + r, ctx->cand_top + r, ctx->cand_second + r,
+                 ctx->cand_count + r, ctx->cand_total + r};
+}
+
 static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t batch, bool* qcache, size_t* smem) {
   CommitArgs ca;
   ca.dn = ctx->dnodes;
@@ -2734,6 +2772,9 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.nv = ctx->dnv;
   ca.pipe_base = nullptr;
   ca.carry = nullptr;
+  ca.pipe_follow = nullptr;
+  ca.pipe_after = nullptr;
+  ca.top_reset = nullptr;
   *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
                         ctx->q.q, kernel_feat(ctx) == 0).total;
   return ca;
@@ -2815,6 +2856,8 @@ static int ensure_pipe(ks_ctx* ctx) {
     void* p = nullptr;
     if (dev_alloc(ctx, &p, kPipeWords * 4) != KS_OK) return KS_ENOMEM;
     ctx->pipe = (int32_t*)p;
+    if (dev_alloc(ctx, &p, 2 * kMaxBatch * 8) != KS_OK) return KS_ENOMEM;
+    ctx->pipe_top = (unsigned long long*)p;
   }
   if (!ctx->sstream) {
     // One sweep stream and one commit stream per device for the whole process, shared by every context: a
@@ -2837,8 +2880,11 @@ static int ensure_pipe(ks_ctx* ctx) {
       bool masked = false;
       if (env_mask && ncu > 8) {
         std::vector<uint32_t> smask((size_t)(ncu + 31) / 32, 0u), cmask((size_t)(ncu + 31) / 32, 0u);
-        for (int c = 1; c < ncu; ++c) smask[(size_t)c / 32] |= 1u << (c % 32);
-        cmask[0] = 1u;
+        // the commit stream's CUs: the one-workgroup commit and, for patched passes, the re-sweep and list patch
+        // that run between two commits
+        static const int64_t env_ccus = env_i64("KS_PIPE_COMMIT_CUS", 16, 1, 128);
+        const int rc = (int)std::min<int64_t>(env_ccus, ncu / 2);
+        for (int c = 0; c < ncu; ++c) (c < rc ? cmask : smask)[(size_t)c / 32] |= 1u << (c % 32);
         hipStream_t a = nullptr, b = nullptr;
         if (hipExtStreamCreateWithCUMask(&a, (uint32_t)smask.size(), smask.data()) == hipSuccess) {
           if (hipExtStreamCreateWithCUMask(&b, (uint32_t)cmask.size(), cmask.data()) == hipSuccess) {
@@ -2866,6 +2912,8 @@ static int ensure_pipe(ks_ctx* ctx) {
 struct PipeShape {
   int32_t fix_ppw;
   int fix_blocks;
+  int list_blocks;  // patched: one wave per (pod, list entry)
+  bool patch;  // monotone plugin sets: select before the previous commit ends, re-evaluate the listed chunks after
 };
 
 template <int NSC>
@@ -2874,8 +2922,17 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   // Pipelined: the sweep and the select run on sstream; the sweep of pass k runs while commit k-1 does
   // (for the pods after commit k-1's, speculatively), then the chunks commit k-1 wrote are re-swept, so the select
   // and commit k see exactly what a sweep after commit k-1 gives.  Otherwise everything runs on ctx->stream.
+  // Patched (monotone plugin sets on one shard): sweep k and select k run on sstream as soon as commit k-2 is done
+  // (concurrently with commit k-1), into the sweep output and list set of parity k & 1; after commit k-1 the fix
+  // stream re-evaluates the listed chunks it wrote in place (sweep_kernel's list mode), and commit k runs on them.
   hipStream_t ss = pipe ? ctx->sstream : ctx->stream;
   const int64_t k = ctx->pipe_k;
+  const int32_t S = ctx->nranks * ctx->vshards;
+  const bool patch = pipe && pipe->patch;
+  // the re-sweep (and patch): patched passes run it on the commit stream, between commit k-1 and commit k
+  hipStream_t fs = patch ? ctx->cstream : ss;
+  const CandSet cset = cand_set(ctx, patch ? (int)(k & 1) : 0);
+  uint2* sout = ctx->sweep_out + (patch ? (size_t)(k & 1) * kMaxBatch * ctx->nchunks : 0);
   int32_t* base = pipe ? ctx->pipe + (k & 1) : ctx->cursor;  // the first pod this pass sweeps
   int32_t* carry = ctx->pipe + 4;
   auto rec = [&](int kind, hipStream_t s) {
@@ -2884,7 +2941,6 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     (void)hipEventRecord(e, s);
     evs->push_back({kind, (*evn)++});
   };
-  const int32_t S = ctx->nranks * ctx->vshards;
   auto shard_lo = [&](int32_t sh) { return ctx->nchunks * sh / S; };
   SweepArgs sa;
   sa.dn = ctx->dnodes;
@@ -2892,7 +2948,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   sa.c = ctx->kc;
   sa.pods = ctx->st.recs;
   sa.cursor = base;
-  sa.out = ctx->sweep_out;
+  sa.out = sout;
   sa.n = ctx->n;
   sa.nchunks = ctx->nchunks;
   sa.c0 = shard_lo(ctx->rank * ctx->vshards);
@@ -2902,6 +2958,12 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   sa.ppw = ppw;
   sa.fix = nullptr;
   sa.fix_cursor = nullptr;
+  sa.list_t = nullptr;
+  sa.list_chunk = nullptr;
+  sa.list_count = nullptr;
+  sa.list_bound = nullptr;
+  sa.list_top = nullptr;
+  sa.list_k = 0;
   const int feat = kernel_feat(ctx);
   sa.dv = ctx->ddv;
   sa.nv = ctx->dnv;
@@ -2913,21 +2975,23 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   // c0 > 0 decode of every non-first shard runs on one GPU too); timed together as one launch.
   const PassLaunch pl = pass_launcher(feat, NSC);
   hipError_t le = hipSuccess;
-  auto sweep = [&](int blocks) {
+  auto sweep = [&](int blocks, hipStream_t st) {
     for (int32_t v = 0; v < ctx->vshards && le == hipSuccess; ++v) {
       const int32_t sh = ctx->rank * ctx->vshards + v;
       sa.c0 = shard_lo(sh);
       sa.c1 = shard_lo(sh + 1);
-      le = pl.sweep(blocks, ss, sa);
+      le = pl.sweep(blocks, st, sa);
     }
   };
+  // patched: commit k-2 wrote this pass's first pod and its rows are final
+  if (patch && k >= 2) HIPCHK(ctx, hipStreamWaitEvent(ss, ctx->pev_com[(k - 2) % kPipeEvents], 0));
   if (feat == 7 || feat == 15) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
     // each launch is timed on its own (the roofline is per sweep launch)
     HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ss));
     sa.phase = 0;
     rec(0, ss);
-    sweep(sweep_blocks);
+    sweep(sweep_blocks, ss);
     rec(0, ss);
     if (ctx->nranks > 1) {
       const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ss);
@@ -2935,27 +2999,48 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     }
     sa.phase = 1;
     rec(0, ss);
-    sweep(sweep_blocks);
+    sweep(sweep_blocks, ss);
   } else {
     rec(0, ss);
-    sweep(sweep_blocks);
+    sweep(sweep_blocks, ss);
   }
   HIPCHK(ctx, le);
   rec(0, ss);
-  if (pipe) {
+  auto fix = [&]() -> int {
     // after commit k-1: its rows' chunks again, for the same pods (nothing when the sweep's pods are not where
     // commit k-1 left the cursor: commit k is then a bubble)
-    if (k > 0) HIPCHK(ctx, hipStreamWaitEvent(ss, ctx->pev_com[(k - 1) % kPipeEvents], 0));
+    if (patch) {
+      // the select must have read the stale keys before the re-sweep overwrites them (commit k-1 is ahead of
+      // the re-sweep on the same stream)
+      HIPCHK(ctx, hipEventRecord(ctx->pev_sel[k % kPipeEvents], ss));
+      HIPCHK(ctx, hipStreamWaitEvent(fs, ctx->pev_sel[k % kPipeEvents], 0));
+    } else if (k > 0) {
+      HIPCHK(ctx, hipStreamWaitEvent(fs, ctx->pev_com[(k - 1) % kPipeEvents], 0));
+    }
     sa.fix = carry;
     sa.fix_cursor = ctx->cursor;
     sa.ppw = pipe->fix_ppw;
-    rec(3, ss);
-    sweep(pipe->fix_blocks);
+    rec(3, fs);
+    if (patch) {
+      // the listed chunks commit k-1 wrote, re-evaluated in place; the pods' tops rebuilt (ks_pass.h)
+      sa.list_t = cset.t;
+      sa.list_chunk = cset.chunk;
+      sa.list_count = cset.count;
+      sa.list_bound = cset.bound;
+      sa.list_top = ctx->pipe_top + (size_t)(k & 1) * kMaxBatch;
+      sa.list_k = ctx->k;
+      sweep(pipe->list_blocks, fs);
+    } else {
+      sweep(pipe->fix_blocks, fs);
+    }
     HIPCHK(ctx, le);
-    rec(3, ss);
-  }
+    rec(3, fs);
+    return KS_OK;
+  };
+  if (pipe && !patch)
+    if (int rc = fix(); rc != KS_OK) return rc;
   SelectArgs se;
-  se.in = ctx->sweep_out;
+  se.in = sout;
   se.cursor = base;
   se.nchunks = ctx->nchunks;
   se.total_pods = ctx->np;
@@ -2968,15 +3053,15 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     const int32_t sh = ctx->rank * ctx->vshards + v;
     se.c0 = shard_lo(sh);
     se.c1 = shard_lo(sh + 1);
-    se.next_base = (pipe && v == 0) ? ctx->pipe + ((k + 1) & 1) : nullptr;
+    se.next_base = (pipe && !patch && v == 0) ? ctx->pipe + ((k + 1) & 1) : nullptr;
     if (S == 1) {
-      se.cand_chunk = ctx->cand_chunk;
-      se.cand_t = ctx->cand_t;
-      se.cand_bound = ctx->cand_bound;
-      se.cand_top = ctx->cand_top;
-      se.cand_second = ctx->cand_second;
-      se.cand_count = ctx->cand_count;
-      se.cand_total = ctx->cand_total;
+      se.cand_chunk = cset.chunk;
+      se.cand_t = cset.t;
+      se.cand_bound = cset.bound;
+      se.cand_top = cset.top;
+      se.cand_second = cset.second;
+      se.cand_count = cset.count;
+      se.cand_total = cset.total;
     } else {
       unsigned char* b = ctx->gather + (size_t)sh * L.bytes;
       se.cand_chunk = (uint32_t*)(b + L.chunk);
@@ -3013,8 +3098,12 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     hipLaunchKernelGGL(merge_kernel, dim3(ctx->batch), dim3(64), 0, ss, ma);
   }
   rec(1, ss);
+  if (patch)
+    if (int rc = fix(); rc != KS_OK) return rc;
   hipStream_t cs = pipe ? ctx->cstream : ctx->stream;
-  if (pipe) {
+  if (patch) {
+    // the re-sweep and the patch ran on cs
+  } else if (pipe) {
     HIPCHK(ctx, hipEventRecord(ctx->pev_sel[k % kPipeEvents], ss));
     HIPCHK(ctx, hipStreamWaitEvent(cs, ctx->pev_sel[k % kPipeEvents], 0));
   }
@@ -3024,6 +3113,18 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   if (pipe) {
     ca.pipe_base = base;
     ca.carry = carry;
+  }
+  ca.cand_chunk = cset.chunk;
+  ca.cand_t = cset.t;
+  ca.cand_bound = cset.bound;
+  ca.cand_top = cset.top;
+  ca.cand_second = cset.second;
+  ca.cand_count = cset.count;
+  if (patch) {
+    ca.pipe_follow = ctx->pipe + ((k + 1) & 1);
+    ca.pipe_after = base;
+    ca.cand_top = (const uint64_t*)(ctx->pipe_top + (size_t)(k & 1) * kMaxBatch);  // rebuilt by the list re-evaluation
+    ca.top_reset = ctx->pipe_top + (size_t)(k & 1) * kMaxBatch;
   }
   size_t msmem = 0;
   const bool mono = mono_commit(ctx, qcache, &msmem);
@@ -3105,12 +3206,21 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   const PipeShape* pipe = nullptr;
   if (pipelined(ctx)) {
     if (ensure_pipe(ctx) != KS_OK) return KS_EHIP;
-    static const int64_t env_fix_ppw = env_i64("KS_PIPE_FIX_PPW", 2, 1, kMaxBatch);
-    pshape.fix_ppw = (int32_t)std::min<int64_t>(env_fix_ppw, ctx->batch);
+    static const int64_t env_patch = env_i64("KS_PIPE_PATCH", 1, 0, 1);
+    pshape.patch = env_patch != 0 && S == 1 && ctx->kc.monotone;
+    // the re-sweep runs on the commit stream's few CUs when patched: more pods per wave, fewer waves
+    static const int64_t env_fix_ppw = env_i64("KS_PIPE_FIX_PPW", 0, 1, kMaxBatch);
+    pshape.fix_ppw = (int32_t)std::min<int64_t>(env_fix_ppw > 0 ? env_fix_ppw : (pshape.patch ? 16 : 2), ctx->batch);
     const int64_t fwork = (int64_t)kMaxBatch * ((ctx->batch + pshape.fix_ppw - 1) / pshape.fix_ppw);
     pshape.fix_blocks = (int)((std::max<int64_t>(1, (fwork + 3) / 4) + 7) & ~7ll);
+    pshape.list_blocks = (int)((((int64_t)ctx->batch * ctx->k + 3) / 4 + 7) & ~7ll);
     pipe = &pshape;
     HIPCHK(ctx, hipMemsetAsync(ctx->pipe, 0, kPipeWords * 4, ctx->stream));
+    // patched: pass 1's sweep starts before commit 0 has decided anything, behind pass 0's pods
+    if (pshape.patch) {
+      HIPCHK(ctx, hipMemsetD32Async((hipDeviceptr_t)(ctx->pipe + 1), std::min(ctx->batch, np), 1, ctx->stream));
+      HIPCHK(ctx, hipMemsetAsync(ctx->pipe_top, 0, 2 * kMaxBatch * 8, ctx->stream));
+    }
     ctx->pipe_k = 0;
   }
   HIPCHK(ctx, hipEventRecord(t0, ctx->stream));
@@ -3170,7 +3280,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   ctx->stats.rescans = (int64_t)cnt[2];
   ctx->stats.slot_misses = (int64_t)cnt[3];
   ctx->stats.bubble_passes = (int64_t)cnt[4];
-  ctx->stats.pipelined = pipe ? 1 : 0;
+  ctx->stats.pipelined = pipe ? (pipe->patch ? 2 : 1) : 0;
   for (int i = 0; i < 8; ++i) ctx->stats.diag[i] = (int64_t)cnt[8 + i];
   for (size_t i = 0; i + 1 < evs.size(); i += 2) {
     float e = 0;

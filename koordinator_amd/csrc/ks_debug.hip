@@ -26,8 +26,11 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
-  // Fit + LoadAware + NUMA part (the Reservation part is added by rsv_normalize_debug_kernel)
-  total[i] = o.reasons ? -1 : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_BALANCED] = o.reasons ? 0 : o.bal;
+  // Fit + LoadAware + NUMA + BalancedAllocation part (the Reservation part is added by rsv_normalize_debug_kernel)
+  total[i] = o.reasons ? -1
+                       : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw +
+                             (int64_t)o.bal * c.bal_pw;
   raw[i] = ro.raw;
   hiord[i] = ro.hiord;
   draw[i] = o.dev_raw;

@@ -71,6 +71,7 @@ struct Cfg {
   int32_t dev, dev_most, dw_core, dw_mem, dw_ratio, dev_pw, dw_rdma;  // DeviceShare (GPU, RDMA)
   int32_t monotone_nd;  // monotone for pods without device requests (DeviceShare skips them: no normalization max)
   int32_t cores;        // node CPU bind policies or required pod policies: the per-node core counts are read
+  int32_t bal, bal_pw;  // upstream NodeResourcesBalancedAllocation: KS_BAL_* resources (0 = off), plugin weight
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -396,8 +397,31 @@ struct EvalOut {
   int32_t numa;
   int32_t dev_raw;         // DeviceShare raw score (normalized in key_total)
   int32_t hi;              // Reservation ranking component (ks_rsv.h)
+  int32_t bal;             // NodeResourcesBalancedAllocation score
   uint32_t numa_rs;        // NodeNUMAResource reasons of the policy-None checks (before the policy path)
 };
+
+// Upstream NodeResourcesBalancedAllocation (kube-scheduler v1.24 noderesources/balanced_allocation.go,
+// balancedResourceScorer with useRequested = true): fraction = float64(Requested + pod request) / float64(Allocatable)
+// for each listed resource with Allocatable != 0, capped at 1; std = |f0 - f1| / 2 for two fractions, 0 for fewer;
+// score = int64((1 - std) * 100).  Plain f64 operations in Go's order (-ffp-contract=off: no fused multiply-add).
+__device__ __forceinline__ int32_t balanced_score(int32_t res, int64_t acpu, int64_t rcpu, int64_t amem, int64_t rmem) {
+  double f0 = 0.0, f1 = 0.0;
+  int n = 0;
+  if ((res & KS_BAL_CPU) && acpu != 0) {
+    const double x = (double)rcpu / (double)acpu;
+    f0 = x > 1.0 ? 1.0 : x;
+    n = 1;
+  }
+  if ((res & KS_BAL_MEMORY) && amem != 0) {
+    const double x = (double)rmem / (double)amem;
+    if (n == 0) f0 = x > 1.0 ? 1.0 : x;
+    else f1 = x > 1.0 ? 1.0 : x;
+    ++n;
+  }
+  const double sd = n == 2 ? fabs((f0 - f1) / 2.0) : 0.0;
+  return (int32_t)((1.0 - sd) * 100.0);
+}
 
 // Filter + Score of one (pod, node).  DEBUG=false computes feasibility (reasons != 0) and the
 // total without branches on node data; DEBUG=true also fills every reason bit and the
@@ -446,6 +470,7 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   o.dev_raw = 0;
   o.hi = 0;
   o.numa_rs = 0;
+  o.bal = 0;
   int32_t total = 0;
   // the score terms: the f64 path everywhere, then the int64 path for the lanes it does not cover
   // (a divergent branch the wave skips when no lane needs it)
@@ -497,6 +522,11 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   if (c.la_score) {
     o.la = (r.la_bits & kLaZeroScore) ? 0 : la;
     total += o.la * c.la_pw;
+  }
+  if (c.bal) {
+    // Requested + pod = Allocatable - (Allocatable - Requested) + pod request
+    o.bal = balanced_score(c.bal, r.t_cpu.c, r.t_cpu.c - r.free_cpu + p.cpu, r.t_mem.c, r.t_mem.c - r.free_mem + p.mem);
+    total += o.bal * c.bal_pw;
   }
   o.total = total;
   return o;

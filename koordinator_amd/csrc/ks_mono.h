@@ -202,7 +202,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
-  if (cursor0 >= a.total_pods) return;
+  if (cursor0 >= a.total_pods) {
+    if (threadIdx.x == 0) pipe_next(a, cursor0);  // the queue is done: so are the speculative sweeps after it
+    return;
+  }
   if (pipe_bubble(a, cursor0)) return;
   const int32_t np = min(a.batch, a.total_pods - cursor0);
   const Cfg cfg = a.c;
@@ -450,8 +453,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
           need &= ~(1ull << sel);
           need &= __ballot(cj.ub > best);
         }
-        const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, j);
-        if (cnt == Kc && best < readlane64(my_bound, j)) {
+        if (best < readlane64(my_bound, j)) {
           processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep from j
           break;
         }
@@ -567,8 +569,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
     }
   }
   pipe_carry(a, nslots, snode);
+  if (a.top_reset) a.top_reset[lane] = 0ull;
   if (lane == 0) {
     *a.cursor = cursor0 + processed;
+    pipe_next(a, cursor0 + processed);
     atomicAdd(&a.counters[0], 1ull);
     if (processed < np) atomicAdd(&a.counters[1], 1ull);
     atomicAdd(&a.counters[2], (unsigned long long)rescans);

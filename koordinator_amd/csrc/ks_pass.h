@@ -49,6 +49,16 @@ struct SweepArgs {
   // NULL = a full sweep.
   const int32_t* fix;
   const int32_t* fix_cursor;
+  // Patched pipelined passes: instead of whole chunks, re-evaluate each pod's listed chunks that the
+  // previous commit wrote (the fix list's chunks), in place in the pass's candidate lists (select_kernel ran on the
+  // speculative sweep), and rebuild each pod's top into list_top (atomic max, zeroed by the commit that read it).
+  // NULL = off.
+  uint2* list_t;
+  const uint32_t* list_chunk;
+  const int32_t* list_count;
+  const uint64_t* list_bound;
+  unsigned long long* list_top;
+  int32_t list_k;
 };
 
 // local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
@@ -66,6 +76,45 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
+  if (a.list_t) {
+    // one wave per (pod, list entry): a monotone commit only lowered the keys of the nodes it wrote, so an entry
+    // whose chunk it did not write keeps its keys, a written one takes fresh keys, and a chunk outside the list
+    // stays below the bound.  The pod's top is the largest listed key when that is at least the bound (else 0:
+    // the best node may lie outside the list, and the commit's resolution then cuts the pass there).
+    if (__builtin_amdgcn_readfirstlane(*a.fix_cursor) != cursor) return;  // a bubble pass
+    const int32_t m = min(__builtin_amdgcn_readfirstlane(a.fix[0]), kMaxBatch);
+    const int32_t dch = lane < m ? (a.fix[1 + lane] >> 6) : -1;  // lane i: the chunk of written node i
+    const int32_t K = a.list_k;
+    for (int64_t w = wave; w < (int64_t)np * K; w += nwaves) {
+      const int32_t p = (int32_t)(w / K), e = (int32_t)(w - (int64_t)p * K);
+      if (e >= __builtin_amdgcn_readfirstlane(a.list_count[p])) continue;
+      const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(a.list_chunk[p * K + e]);
+      uint2 t;
+      if (__ballot(dch == (int32_t)c)) {
+        const int64_t node = c * 64 + lane;
+        NodeReg<NSC> r;
+        {
+          const DevNodes d = *a.dn;
+          load_node<NSC>(a.c, d, node, node < a.n, r);
+        }
+        const PodRec pod = load_pod_uniform(a.pods + cursor + p);
+        EvalOut o = eval_full<NSC, false, true, FEAT>(
+            a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+            [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
+        const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, 0) + 1) << 6) | (uint32_t)(63 - lane));
+        t.x = wave_max_u32(key);
+        t.y = wave_max_u32(key == t.x ? 0u : key);
+        if (lane == 0) a.list_t[p * K + e] = t;
+      } else {
+        const uint2 v = a.list_t[p * K + e];
+        t.x = __builtin_amdgcn_readfirstlane(v.x);
+      }
+      const uint64_t b = a.list_bound[p];
+      const uint64_t g = t.x ? local_gkey(t.x, c) : 0ull;
+      if (lane == 0 && g && (b == 0ull || g >= b)) atomicMax(a.list_top + p, (unsigned long long)g);
+    }
+    return;
+  }
   const int32_t groups = (np + a.ppw - 1) / a.ppw;
   int64_t nitems = a.c1 - a.c0;
   if (a.fix) {
@@ -241,7 +290,22 @@ struct CommitArgs {
   const int32_t* pipe_base;
   // [0] count, [1..64] nodes whose rows this pass wrote back (the next pass re-sweeps their chunks); NULL = not kept
   int32_t* carry;
+  // Patched pipelined passes: the commit of pass k decides where pass k+2's speculative sweep starts,
+  // from pass k+1's start (pipe_follow) and the cursor it leaves, into pipe_after (pass k's own start word, read by
+  // nobody after this commit's prologue).  NULL = the select / patch kernels write it.
+  const int32_t* pipe_follow;
+  int32_t* pipe_after;
+  // patched passes: cand_top is the list re-evaluation's atomic max, which the commit zeroes after reading
+  unsigned long long* top_reset;
 };
+
+// The first pod of the pass after next: pass k+1 commits iff it was swept for the pods at the cursor this commit
+// leaves (rc), and then the pass after it starts behind its pods; otherwise pass k+1 is a bubble and k+2 starts at rc.
+__device__ __forceinline__ void pipe_next(const CommitArgs& a, int32_t rc) {
+  if (!a.pipe_after) return;
+  const int32_t b1 = *a.pipe_follow;
+  *a.pipe_after = (b1 == rc && b1 < a.total_pods) ? b1 + min(a.batch, a.total_pods - b1) : rc;
+}
 
 // Pipelined pass prologue: a pass whose sweep ran for other pods than the ones at the cursor does nothing (its
 // successor's sweep starts at the cursor).  Returns true when the calling kernel must return.
@@ -250,6 +314,7 @@ __device__ __forceinline__ bool pipe_bubble(const CommitArgs& a, int32_t cursor0
   if (threadIdx.x == 0) {
     a.carry[0] = 0;
     atomicAdd(&a.counters[4], 1ull);
+    pipe_next(a, cursor0);
   }
   return true;
 }
@@ -429,6 +494,7 @@ __device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const
   r.valid = lane < cnt;
   r.chunk = r.valid ? cand_chunk[j * K + lane] : 0u;
   const uint2 t = r.valid ? cand_t[j * K + lane] : make_uint2(0u, 0u);
+  r.valid = r.valid && t.x != 0u;  // a patched list's chunk whose nodes all became infeasible
   const uint64_t tm = r.valid ? touched[r.chunk] : 0ull;
   r.u = local_gkey(t.x, r.chunk);
   r.fast = false;
@@ -557,7 +623,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
-  if (cursor0 >= a.total_pods) return;
+  if (cursor0 >= a.total_pods) {
+    if (threadIdx.x == 0) pipe_next(a, cursor0);  // the queue is done: so are the speculative sweeps after it
+    return;
+  }
   if (pipe_bubble(a, cursor0)) return;
   const int32_t np = min(a.batch, a.total_pods - cursor0);
 #ifdef KS_COMMIT_STAMPS
@@ -860,8 +929,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         need &= ~(1ull << sel);
         need &= __ballot(cj.ub > best);
       }
-      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, j);
-      if (cnt == Kc && best < readlane64(my_bound, j)) {
+      if (best < readlane64(my_bound, j)) {
         processed = j;  // an untouched chunk outside the list may hold a better node: re-sweep from j
         break;
       }
@@ -1317,8 +1385,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     }
   }
   pipe_carry(a, nslots, snode);
+  if (a.top_reset) a.top_reset[lane] = 0ull;
   if (lane == 0) {
     *a.cursor = cursor0 + processed;
+    pipe_next(a, cursor0 + processed);
     atomicAdd(&a.counters[0], 1ull);
     if (processed < np) atomicAdd(&a.counters[1], 1ull);
     atomicAdd(&a.counters[2], (unsigned long long)rescans);

@@ -921,9 +921,30 @@ static int64_t la_score(const ko_sched *s, const ko_pod *p, int64_t n) {
   return node_score / weight_sum;
 }
 
+/* Upstream NodeResourcesBalancedAllocation (kube-scheduler v1.24.15 noderesources/balanced_allocation.go, not on
+ * disk: parity unpinned), balancedResourceScorer with useRequested = true: for cpu and memory (the v1beta2 default
+ * resource list) with Allocatable != 0, fraction = float64(Requested + pod request) / float64(Allocatable), capped
+ * at 1; two fractions give std = |f0 - f1| / 2, fewer give 0; score = int64((1 - std) * MaxNodeScore). */
+static int64_t balanced_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e) {
+  const ko_nodes *d = &s->nd;
+  double f[2];
+  int k = 0;
+  if ((s->cfg.balanced.resources & KS_BAL_CPU) && d->alloc_cpu[n] != 0) {
+    double x = (double)(e->req[0] + p->cpu) / (double)d->alloc_cpu[n];
+    f[k++] = x > 1 ? 1 : x;
+  }
+  if ((s->cfg.balanced.resources & KS_BAL_MEMORY) && d->alloc_mem[n] != 0) {
+    double x = (double)(e->req[1] + p->mem) / (double)d->alloc_mem[n];
+    f[k++] = x > 1 ? 1 : x;
+  }
+  double sd = 0;
+  if (k == 2) sd = fabs((f[0] - f[1]) / 2);
+  return (int64_t)((1 - sd) * 100);
+}
+
 static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c,
-                           int64_t *fit_out, int64_t *la_out, int64_t *numa_out) {
-  int64_t t = 0, fs = 0, ls = 0, ns = 0;
+                           int64_t *fit_out, int64_t *la_out, int64_t *numa_out, int64_t *bal_out) {
+  int64_t t = 0, fs = 0, ls = 0, ns = 0, bs = 0;
   if (s->cfg.numa.enable) {
     ns = numa_score(s, p, n, e, c);
     t += ns * s->cfg.numa.plugin_weight;
@@ -937,8 +958,13 @@ static int64_t total_score(const ko_sched *s, const ko_pod *p, int64_t n, const 
     ls = la_score(s, p, n);
     t += ls * s->cfg.loadaware.plugin_weight;
   }
+  if (s->cfg.balanced.enable) {
+    bs = balanced_score(s, p, n, e);
+    t += bs * s->cfg.balanced.plugin_weight;
+  }
   if (fit_out) *fit_out = fs;
   if (la_out) *la_out = ls;
+  if (bal_out) *bal_out = bs;
   return t;
 }
 
@@ -2045,7 +2071,7 @@ typedef struct {
 /* BeforePreFilter restore + Filter for one node; the Reservation PreScore per-node part
  * (nomination, node order) for feasible ones.  Returns the KS_R_* bits. */
 static uint32_t eval_node(ko_sched *s, const ko_pod *p0, int64_t n, int64_t *fit_out, int64_t *la_out,
-                          int64_t *numa_out) {
+                          int64_t *numa_out, int64_t *bal_out) {
   ko_pod pn;
   const ko_pod *p = node_pod(s, p0, n, &pn);
   ko_rstate st;
@@ -2067,7 +2093,7 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p0, int64_t n, int64_t *fit
     s->total[n] = -1;
     return r;
   }
-  s->total[n] = total_score(s, p, n, &st.e, &npc, fit_out, la_out, numa_out);
+  s->total[n] = total_score(s, p, n, &st.e, &npc, fit_out, la_out, numa_out, bal_out);
   if (s->cfg.reservation.enable) {
     int32_t nom = rsv_nominate(s, p, n, &st, &s->rord[n]);
     s->nom[n] = nom;
@@ -2078,7 +2104,7 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p0, int64_t n, int64_t *fit
 
 static void filter_piece(void *v, int64_t lo, int64_t hi) {
   sweep_arg *a = (sweep_arg *)v;
-  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = eval_node(a->s, a->p, n, NULL, NULL, NULL) == 0;
+  for (int64_t n = lo; n < hi; n++) a->s->feasible[n] = eval_node(a->s, a->p, n, NULL, NULL, NULL, NULL) == 0;
 }
 
 /* Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and
@@ -2483,14 +2509,15 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
   ko_pod p;
   load_pod(s, pc, 0, &p);
   for (int64_t n = 0; n < s->n; n++) {
-    int64_t fs = 0, ls = 0, ns = 0;
-    uint32_t r = eval_node(s, &p, n, &fs, &ls, &ns);
+    int64_t fs = 0, ls = 0, ns = 0, bs = 0;
+    uint32_t r = eval_node(s, &p, n, &fs, &ls, &ns, &bs);
     if (reasons) reasons[n] = r;
     if (scores) {
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = r ? 0 : fs;
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = r ? 0 : ls;
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
       scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = r ? 0 : ns;
+      scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_BALANCED] = r ? 0 : bs;
     }
   }
   int64_t *norm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);

@@ -6,6 +6,7 @@ import numpy as np
 from koordinator_amd import abi, synth
 from koordinator_amd.cluster import NodeTable, PodTable, QuotaTable
 from koordinator_amd.config import (BATCH_CPU, BATCH_MEMORY, CPU, EPHEMERAL, MEMORY, ElasticQuotaArgs,
+                                    NodeResourcesBalancedAllocationArgs,
                                     LoadAwareSchedulingArgs, NodeResourcesFitArgs, SchedulerProfile)
 
 
@@ -66,7 +67,8 @@ def stress_pods(p: int, rng: np.random.Generator, n_quotas: int = 0) -> PodTable
 
 def profile(strategy: str = "LeastAllocated", quota: bool = False, prod_usage: bool = False,
             batch_pods: int = 0, candidates: int = 0, fit_weight: int = 1, la_weight: int = 1,
-            eph_weight: int = 0, check_parent: bool = False, filter_expired: bool = True) -> SchedulerProfile:
+            eph_weight: int = 0, check_parent: bool = False, filter_expired: bool = True,
+            balanced: int = 0) -> SchedulerProfile:
     res = {CPU: 1, MEMORY: 1, BATCH_CPU: 1, BATCH_MEMORY: 1}
     if eph_weight:
         res[EPHEMERAL] = eph_weight
@@ -74,7 +76,9 @@ def profile(strategy: str = "LeastAllocated", quota: bool = False, prod_usage: b
     return SchedulerProfile(fit=NodeResourcesFitArgs(strategy=strategy, resources=res), fit_weight=fit_weight,
                             loadaware=la, loadaware_weight=la_weight,
                             quota=ElasticQuotaArgs(enable_check_parent_quota=check_parent) if quota else None,
-                            batch_pods=batch_pods, candidates=candidates)
+                            batch_pods=batch_pods, candidates=candidates,
+                            balanced=NodeResourcesBalancedAllocationArgs() if balanced else None,
+                            balanced_weight=balanced or 1)
 
 
 def nested_quotas(pods: PodTable, rng: np.random.Generator, n_leaf: int) -> QuotaTable:
