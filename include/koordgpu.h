@@ -604,6 +604,14 @@ int ks_fetch_cpusets(ks_ctx *ctx, uint64_t *out, int32_t p);
  * and Reserve (plugin.go:532-570 -> cache.go:171-192 -> reservation_info.go:379-388).
  * Node columns stay the reference's NodeInfo (reserve pods included); call after ks_load_nodes. */
 int ks_load_reservations(ks_ctx *ctx, const ks_reservation_cols *rsv, int32_t r);
+/* Reservation informer events between cycles (reservationCache updateReservation / deleteReservation,
+ * reservation/cache.go:104-216).  ks_add_reservations appends r rows; they get the caller rows *first_row ..
+ * *first_row + r - 1 (ks_result.reservation, ks_read_reservations, ks_update_reservation_usage use them).
+ * ks_delete_reservations removes caller rows; their numbers are not reused and read back as zeros.  Both keep the
+ * Allocated / assigned state of the other rows (commits included) and re-derive the node columns' reservation
+ * base restore; ks_checkpoint again afterwards if the caller restores. */
+int ks_add_reservations(ks_ctx *ctx, const ks_reservation_cols *rsv, int32_t r, int32_t *first_row);
+int ks_delete_reservations(ks_ctx *ctx, const int32_t *rows, int32_t m);
 /* Allocated (r*KS_RSV_DIMS, row-major) and len(AssignedPods) after commits; NULL = skip. */
 int ks_read_reservations(ks_ctx *ctx, int64_t *allocated, int32_t *assigned);
 

@@ -434,6 +434,8 @@ EXPORTED_SYMBOLS = [
     "ks_update_cpu_state",
     "ks_update_quotas",
     "ks_update_reservation_usage",
+    "ks_add_reservations",
+    "ks_delete_reservations",
     "ks_read_nodes",
     "ks_read_quota_used",
     "ks_get_stats",

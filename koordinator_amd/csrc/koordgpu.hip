@@ -948,8 +948,19 @@ struct ks_ctx {
   int64_t* rsv_allocd_ckpt = nullptr;
   int32_t* rsv_assigned_ckpt = nullptr;
   int32_t rsv_ndist = 0;     // distinct order labels
-  int32_t rsv_nrows = 0;     // caller rows
+  int32_t rsv_nrows = 0;     // caller rows (deleted ones included)
+  int32_t rsv_live = 0;      // rows of the device table (the caller rows not deleted)
   std::vector<int32_t> rsv_perm;  // CSR position -> caller row
+  // host mirror of the caller rows, for ks_add_reservations / ks_delete_reservations (allocated / assigned are
+  // refreshed from the device before each change)
+  struct RsvMirror {
+    std::vector<int32_t> node, assigned;
+    std::vector<uint64_t> cls;
+    std::vector<uint32_t> flags, policy, key_mask;
+    std::vector<int64_t> order, rnz_cpu, rnz_mem;
+    std::vector<int64_t> alloc[kRsvDims], allocd[kRsvDims];
+    std::vector<uint8_t> live;
+  } rmir;
   // DeviceShare GPUs (ks_dev.h)
   void* dev_blob = nullptr;
   DevDev dv{};
@@ -1483,7 +1494,8 @@ static void cores_mode(ks_ctx* ctx) {
   ctx->kc.cores = (ctx->cfg.numa.enable && (ctx->cpu_bind_labels || ctx->cpu_bind_required)) ? 1 : 0;
 }
 
-static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr);
+static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, const int32_t* caller = nullptr,
+                       int32_t ncaller = -1);
 static int dev_install(ks_ctx* ctx, const ks_device_cols* dc);
 static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h);
 static int check_dev_numa(ks_ctx* ctx);
@@ -1502,6 +1514,8 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   ctx->sweep_out = nullptr;
   ctx->rsv_based = false;  // fresh columns (a loaded reservation table is dropped: reload it)
   ctx->rsv_nrows = 0;
+  ctx->rsv_live = 0;
+  ctx->rmir = ks_ctx::RsvMirror{};
   ctx->n = n;
   ctx->nchunks = (n + 63) / 64;
   if (ctx->nchunks == 0) ctx->nchunks = 1;
@@ -1572,8 +1586,12 @@ static int rsv_launch_base(ks_ctx* ctx, const int32_t* didx, int64_t count, int6
 }
 
 // Upload the reservation table (CSR by node), add its base restore to the node columns.
-static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
+// rc holds the device table's rows; caller[r] is row r's caller row (NULL: r itself) of ncaller caller rows.
+static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, const int32_t* caller,
+                       int32_t ncaller) {
   constexpr int D = kRsvDims;
+  if (ncaller < 0) ncaller = nr;
+  auto crow = [&](int32_t r) { return caller ? caller[r] : r; };
   if (nr > 0 && (!rc || !rc->node || !rc->owner_classes || !rc->key_mask))
     KS_FAIL(ctx, KS_EINVAL, "ks_reservation_cols: node, owner_classes and key_mask are required");
   for (int32_t r = 0; r < nr; ++r) {
@@ -1626,12 +1644,12 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
   int32_t* rowid = (int32_t*)(h.data() + o_row);
   for (int32_t i = 0; i < nr; ++i) beg[rc->node[perm[i]] + 1]++;
   for (int64_t n = 0; n < ctx->npad; ++n) beg[n + 1] += beg[n];
-  ctx->h_rsv_gi.assign((size_t)nr, -1);
+  ctx->h_rsv_gi.assign((size_t)ncaller, -1);
   ctx->h_rsv_node.assign((size_t)nr, -1);
   for (int32_t i = 0; i < nr; ++i) {
     const int32_t r = perm[i];
-    rowid[i] = r;
-    ctx->h_rsv_gi[(size_t)r] = i;
+    rowid[i] = crow(r);
+    ctx->h_rsv_gi[(size_t)crow(r)] = i;
     ctx->h_rsv_node[(size_t)i] = rc->node[r];
     cls[i] = rc->owner_classes[r];
     const uint32_t flags = rc->flags ? rc->flags[r] & 0xfu : 0u;
@@ -1677,7 +1695,9 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
   ctx->rsv_allocd_ckpt = (int64_t*)(b + o_ck_allocd);
   ctx->rsv_assigned_ckpt = (int32_t*)(b + o_ck_asg);
   ctx->rsv_ndist = (int32_t)ndist;
-  ctx->rsv_nrows = nr;
+  ctx->rsv_nrows = ncaller;
+  ctx->rsv_live = nr;
+  for (int32_t i = 0; i < nr; ++i) perm[i] = crow(perm[i]);
   ctx->rsv_perm = perm;
   if (!ctx->drv) {
     void* p = nullptr;
@@ -2180,17 +2200,135 @@ int ks_read_numa_nodes(ks_ctx* ctx, int64_t* used_cpu, int64_t* used_memory) {
   return KS_OK;
 }
 
+// rows of rc appended to the host mirror (NULL columns as rsv_install reads them; the reserve pod's NonZeroRequested
+// resolved the same way)
+static void rsv_mirror_append(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr) {
+  auto& M = ctx->rmir;
+  for (int32_t r = 0; r < nr; ++r) {
+    M.node.push_back(rc->node[r]);
+    M.cls.push_back(rc->owner_classes[r]);
+    M.flags.push_back(rc->flags ? rc->flags[r] : 0u);
+    M.policy.push_back(rc->policy ? rc->policy[r] : 0u);
+    M.key_mask.push_back(rc->key_mask[r]);
+    M.order.push_back(rc->order ? rc->order[r] : 0);
+    M.assigned.push_back(rc->assigned ? rc->assigned[r] : 0);
+    for (int d = 0; d < kRsvDims; ++d) {
+      M.alloc[d].push_back(rc->allocatable[d] ? rc->allocatable[d][r] : 0);
+      M.allocd[d].push_back(rc->allocated[d] ? rc->allocated[d][r] : 0);
+    }
+    const uint32_t keys = rc->key_mask[r];
+    M.rnz_cpu.push_back(rc->reserve_nonzero_milli_cpu ? rc->reserve_nonzero_milli_cpu[r]
+                                                      : ((keys & 1u) ? M.alloc[0].back() : kDefaultMilliCPU));
+    M.rnz_mem.push_back(rc->reserve_nonzero_memory ? rc->reserve_nonzero_memory[r]
+                                                   : ((keys & 2u) ? M.alloc[1].back() : kDefaultMemory));
+    M.live.push_back(1);
+  }
+}
+
 int ks_load_reservations(ks_ctx* ctx, const ks_reservation_cols* rsv, int32_t r) {
   if (!ctx || r < 0 || (r > 0 && !rsv)) return ctx ? (ctx->err = "ks_load_reservations: bad args", KS_EINVAL) : KS_EINVAL;
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_load_reservations before ks_load_nodes");
   if (!ctx->cfg.reservation.enable) KS_FAIL(ctx, KS_ESTATE, "ks_load_reservations: the Reservation plugin is not enabled");
   HIPCHK(ctx, hipSetDevice(ctx->device));
-  return rsv_install(ctx, rsv, r);
+  if (int rc = rsv_install(ctx, rsv, r); rc != KS_OK) return rc;
+  ctx->rmir = ks_ctx::RsvMirror{};
+  rsv_mirror_append(ctx, rsv, r);
+  return KS_OK;
+}
+
+// Reservation informer events between scheduling cycles (reservationCache.updateReservation /
+// deleteReservation, reservation/cache.go:104-216): rows are added to or removed from the host mirror, the
+// device's Allocated / assigned counts are read back into it, and the table is re-installed (the node
+// columns' base restore follows, rsv_install).  Caller row numbers stay stable: added rows get the next numbers,
+// deleted rows leave gaps.
+static int rsv_reinstall(ks_ctx* ctx) {
+  auto& M = ctx->rmir;
+  const int32_t total = (int32_t)M.node.size();
+  if (ctx->rsv_blob && ctx->rsv_live > 0) {
+    // the device's Allocated / assigned (commits since the last install) into the mirror
+    const size_t m = (size_t)ctx->rv.nr;
+    std::vector<int64_t> ad(kRsvDims * m);
+    std::vector<int32_t> as(m);
+    HIPCHK(ctx, hipMemcpyAsync(ad.data(), ctx->rv.allocd, ad.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(as.data(), ctx->rv.assigned, m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int32_t i = 0; i < ctx->rsv_live; ++i) {
+      const int32_t r = ctx->rsv_perm[(size_t)i];
+      for (int d = 0; d < kRsvDims; ++d) M.allocd[d][(size_t)r] = ad[(size_t)d * m + i];
+      M.assigned[(size_t)r] = as[(size_t)i];
+    }
+  }
+  std::vector<int32_t> caller;
+  for (int32_t r = 0; r < total; ++r)
+    if (M.live[(size_t)r]) caller.push_back(r);
+  const int32_t nl = (int32_t)caller.size();
+  auto pick64 = [&](const std::vector<int64_t>& v) {
+    std::vector<int64_t> o((size_t)nl);
+    for (int32_t i = 0; i < nl; ++i) o[(size_t)i] = v[(size_t)caller[(size_t)i]];
+    return o;
+  };
+  auto pick32 = [&](const auto& v) {
+    std::vector<typename std::decay_t<decltype(v)>::value_type> o((size_t)nl);
+    for (int32_t i = 0; i < nl; ++i) o[(size_t)i] = v[(size_t)caller[(size_t)i]];
+    return o;
+  };
+  auto node = pick32(M.node), assigned = pick32(M.assigned);
+  auto cls = pick32(M.cls);
+  auto flags = pick32(M.flags), policy = pick32(M.policy), key_mask = pick32(M.key_mask);
+  auto order = pick64(M.order), rnzc = pick64(M.rnz_cpu), rnzm = pick64(M.rnz_mem);
+  std::vector<int64_t> alloc[kRsvDims], allocd[kRsvDims];
+  ks_reservation_cols rc{};
+  rc.node = node.data();
+  rc.owner_classes = cls.data();
+  rc.flags = flags.data();
+  rc.policy = policy.data();
+  rc.order = order.data();
+  rc.key_mask = key_mask.data();
+  rc.assigned = assigned.data();
+  rc.reserve_nonzero_milli_cpu = rnzc.data();
+  rc.reserve_nonzero_memory = rnzm.data();
+  for (int d = 0; d < kRsvDims; ++d) {
+    alloc[d] = pick64(M.alloc[d]);
+    allocd[d] = pick64(M.allocd[d]);
+    rc.allocatable[d] = alloc[d].data();
+    rc.allocated[d] = allocd[d].data();
+  }
+  return rsv_install(ctx, &rc, nl, caller.data(), total);
+}
+
+int ks_add_reservations(ks_ctx* ctx, const ks_reservation_cols* rsv, int32_t r, int32_t* first_row) {
+  if (!ctx || r < 0 || (r > 0 && !rsv)) return ctx ? (ctx->err = "ks_add_reservations: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_add_reservations before ks_load_nodes");
+  if (!ctx->cfg.reservation.enable) KS_FAIL(ctx, KS_ESTATE, "ks_add_reservations: the Reservation plugin is not enabled");
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const int32_t first = (int32_t)ctx->rmir.node.size();
+  if (first_row) *first_row = first;
+  if (r == 0) return KS_OK;
+  const ks_ctx::RsvMirror saved = ctx->rmir;
+  rsv_mirror_append(ctx, rsv, r);
+  if (int rc = rsv_reinstall(ctx); rc != KS_OK) {
+    ctx->rmir = saved;  // the previous table stays installed when validation refused the new rows
+    return rc;
+  }
+  return KS_OK;
+}
+
+int ks_delete_reservations(ks_ctx* ctx, const int32_t* rows, int32_t m) {
+  if (!ctx || m < 0 || (m > 0 && !rows)) return ctx ? (ctx->err = "ks_delete_reservations: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->cfg.reservation.enable) KS_FAIL(ctx, KS_ESTATE, "ks_delete_reservations: the Reservation plugin is not enabled");
+  auto& M = ctx->rmir;
+  for (int32_t i = 0; i < m; ++i)
+    if (rows[i] < 0 || (size_t)rows[i] >= M.live.size() || !M.live[(size_t)rows[i]])
+      KS_FAIL(ctx, KS_EINVAL, "ks_delete_reservations: row %d is not a loaded reservation", rows[i]);
+  if (m == 0) return KS_OK;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  for (int32_t i = 0; i < m; ++i) M.live[(size_t)rows[i]] = 0;
+  return rsv_reinstall(ctx);
 }
 
 int ks_read_reservations(ks_ctx* ctx, int64_t* allocated, int32_t* assigned) {
   if (!ctx) return KS_EINVAL;
-  const int32_t nr = ctx->rsv_nrows;
+  const int32_t nr = ctx->rsv_live;
   if (nr == 0 || !ctx->rsv_blob) return KS_OK;
   const size_t m = (size_t)ctx->rv.nr;
   std::vector<int64_t> ad(kRsvDims * m);
@@ -2882,7 +3020,7 @@ static int ensure_pipe(ks_ctx* ctx) {
         std::vector<uint32_t> smask((size_t)(ncu + 31) / 32, 0u), cmask((size_t)(ncu + 31) / 32, 0u);
         // the commit stream's CUs: the one-workgroup commit and, for patched passes, the re-sweep and list patch
         // that run between two commits
-        static const int64_t env_ccus = env_i64("KS_PIPE_COMMIT_CUS", 16, 1, 128);
+        static const int64_t env_ccus = env_i64("KS_PIPE_COMMIT_CUS", 32, 1, 128);
         const int rc = (int)std::min<int64_t>(env_ccus, ncu / 2);
         for (int c = 0; c < ncu; ++c) (c < rc ? cmask : smask)[(size_t)c / 32] |= 1u << (c % 32);
         hipStream_t a = nullptr, b = nullptr;
@@ -3532,6 +3670,7 @@ int ks_update_reservation_usage(ks_ctx* ctx, const int32_t* rows, const int64_t*
   std::vector<int32_t> gi((size_t)m), nodes;
   for (int32_t i = 0; i < m; ++i) {
     gi[(size_t)i] = ctx->h_rsv_gi[(size_t)ix[(size_t)i]];
+    if (gi[(size_t)i] < 0) KS_FAIL(ctx, KS_EINVAL, "ks_update_reservation_usage: row %d was deleted", ix[(size_t)i]);
     nodes.push_back(ctx->h_rsv_node[(size_t)gi[(size_t)i]]);
     for (int d = 0; d < kRsvDims; ++d)
       if (allocated[d] && (allocated[d][i] < 0 || allocated[d][i] >= ((int64_t)1 << 56)))
@@ -3815,6 +3954,7 @@ int ks_unreserve(ks_ctx* ctx, const ks_pod_cols* pod, const ks_result* r, const 
     if (!ctx->cfg.reservation.enable || (size_t)r->reservation >= ctx->h_rsv_gi.size())
       KS_FAIL(ctx, KS_EINVAL, "ks_unreserve: reservation row %d unknown", r->reservation);
     gi = ctx->h_rsv_gi[(size_t)r->reservation];
+    if (gi < 0) KS_FAIL(ctx, KS_EINVAL, "ks_unreserve: reservation row %d was deleted", r->reservation);
   }
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ensure_stage(ctx, ctx->ast, 1) != KS_OK) return KS_ENOMEM;

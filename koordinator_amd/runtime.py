@@ -85,6 +85,8 @@ def lib() -> C.CDLL:
     L.ks_update_cpu_state.argtypes = [vp, abi.P32, C.POINTER(abi.KsCpuStateCols), C.c_int64]
     L.ks_update_quotas.argtypes = [vp, abi.P32, C.POINTER(abi.KsQuotaCols), C.c_int32]
     L.ks_update_reservation_usage.argtypes = [vp, abi.P32, C.POINTER(abi.P64), abi.P32, C.c_int32]
+    L.ks_add_reservations.argtypes = [vp, C.POINTER(abi.KsReservationCols), C.c_int32, abi.P32]
+    L.ks_delete_reservations.argtypes = [vp, abi.P32, C.c_int32]
     L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
     L.ks_read_quota_used.argtypes = [vp, abi.P64]
     L.ks_get_stats.argtypes = [vp, C.POINTER(abi.KsStats)]
@@ -179,6 +181,19 @@ class Evaluator:
         cols = rs.ks()
         self._chk(self.L.ks_load_reservations(self.h, C.byref(cols), rs.r))
         self.nr = rs.r
+
+    def add_reservations(self, rs: ReservationTable) -> int:
+        """informer add: rs's rows become caller rows first .. first + rs.r - 1; returns first"""
+        cols = rs.ks()
+        first = np.zeros(1, np.int32)
+        self._chk(self.L.ks_add_reservations(self.h, C.byref(cols), rs.r, first.ctypes.data_as(abi.P32)))
+        self.nr = int(first[0]) + rs.r
+        return int(first[0])
+
+    def delete_reservations(self, rows):
+        """informer delete of caller rows (their numbers are not reused)"""
+        rows = np.ascontiguousarray(rows, np.int32)
+        self._chk(self.L.ks_delete_reservations(self.h, rows.ctypes.data_as(abi.P32), rows.size))
 
     def load_devices(self, dev: DeviceTable):
         cols = dev.ks()

@@ -195,6 +195,7 @@ typedef struct ko_sched {
   int8_t *cpu_excl;   /* [n][KO_MAX_CPUS]: KO_EXCL_* of an allocated CPU, -1 = free */
   uint8_t *cpu_resv;  /* [n][KO_MAX_CPUS] */
   uint64_t *cpusets;  /* [np][KS_CPU_WORDS] of the last ko_schedule */
+  int64_t *numa_allocs; /* [np][KS_MAX_NUMA][2] of the last ko_schedule: each pod's NUMA-node allocation */
   int32_t cpusets_cap;
   /* NUMA topology policies: per node and NUMA node k ([n*KS_MAX_NUMA + k]) */
   int numa_loaded;
@@ -1858,6 +1859,7 @@ void ko_destroy(ko_sched *s) {
   free(s->draw);
   dev_free(&s->dv);
   free(s->topos); free(s->topo_of); free(s->cpu_alloc); free(s->cpu_excl); free(s->cpu_resv); free(s->cpusets);
+  free(s->numa_allocs);
   free(s->numa_count); free(s->numa_alloc); free(s->numa_used); free(s->numa_present); free(s->numa_cs);
   ko_rsv *rv = &s->rv;
   free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
@@ -1977,6 +1979,14 @@ int ko_read_cpu_state(const ko_sched *s, uint64_t *allocated, uint64_t *excl_pcp
 int ko_fetch_cpusets(const ko_sched *s, uint64_t *out, int32_t p) {
   if (p > s->cpusets_cap) return -1;
   if (p > 0) memcpy(out, s->cpusets, (size_t)p * KS_CPU_WORDS * 8);
+  return 0;
+}
+
+/* each pod's NUMA-node allocation [p][KS_MAX_NUMA][2] (cpu milli, memory) of the last ko_schedule: what
+ * NodeNUMAResource's Reserve recorded in the cycle state for PreBind (zeros off NUMA-policy nodes) */
+int ko_fetch_numa_alloc(const ko_sched *s, int64_t *out, int32_t p) {
+  if (p > s->cpusets_cap || (p > 0 && !s->numa_allocs)) return -1;
+  if (p > 0) memcpy(out, s->numa_allocs, (size_t)p * KS_MAX_NUMA * 2 * 8);
   return 0;
 }
 
@@ -2309,12 +2319,17 @@ int ko_read_numa_nodes(const ko_sched *s, int64_t *used_cpu, int64_t *used_memor
 
 /* one scheduling cycle per pod, in order (scheduleOne loop) */
 int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) {
-  if (np > s->cpusets_cap) {
+  if (np > s->cpusets_cap || !s->numa_allocs) {
     free(s->cpusets);
-    s->cpusets = (uint64_t *)calloc((size_t)np * KS_CPU_WORDS, 8);
-    s->cpusets_cap = np;
+    free(s->numa_allocs);
+    s->cpusets = (uint64_t *)calloc((size_t)(np > 0 ? np : 1) * KS_CPU_WORDS, 8);
+    s->numa_allocs = (int64_t *)calloc((size_t)(np > 0 ? np : 1) * KS_MAX_NUMA * 2, 8);
+    s->cpusets_cap = np > 0 ? np : 1;
   }
-  if (np > 0) memset(s->cpusets, 0, (size_t)np * KS_CPU_WORDS * 8);
+  if (np > 0) {
+    memset(s->cpusets, 0, (size_t)np * KS_CPU_WORDS * 8);
+    memset(s->numa_allocs, 0, (size_t)np * KS_MAX_NUMA * 2 * 8);
+  }
   for (int32_t i = 0; i < np; i++) {
     ko_pod p;
     load_pod(s, pc, i, &p);
@@ -2366,6 +2381,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     }
     dev_reserve(s, &p, best_n, &out[i].gpu_minors, &out[i].rdma_minors, allow);
     numa_reserve(s, &p, best_n, &npc);
+    if (npc.on && !npc.reasons) memcpy(s->numa_allocs + (size_t)i * KS_MAX_NUMA * 2, no.alloc, sizeof(no.alloc));
     node_reserve(s, &p, best_n);
     quota_reserve(s, &p);
   }

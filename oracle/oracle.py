@@ -47,6 +47,7 @@ def lib():
         L.ko_load_cpu_state.argtypes = [C.c_void_p, C.POINTER(abi.KsCpuTopology), C.c_int32, C.POINTER(abi.KsCpuStateCols)]
         L.ko_read_cpu_state.argtypes = [C.c_void_p, abi.PU64, abi.PU64, abi.PU64]
         L.ko_fetch_cpusets.argtypes = [C.c_void_p, abi.PU64, C.c_int32]
+        L.ko_fetch_numa_alloc.argtypes = [C.c_void_p, abi.P64, C.c_int32]
         L.ko_load_numa_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNumaNodeCols)]
         L.ko_read_numa_nodes.argtypes = [C.c_void_p, abi.P64, abi.P64]
         L.ko_schedule.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.POINTER(abi.KsResult)]
@@ -277,6 +278,15 @@ class Oracle:
         out = np.zeros((max(p, 1), abi.KS_CPU_WORDS), np.uint64)
         if self.L.ko_fetch_cpusets(self.h, out.ctypes.data_as(abi.PU64), p) != 0:
             raise ValueError("no cpusets for that many pods")
+        return out[:p]
+
+    def fetch_numa_alloc(self, p: int) -> np.ndarray:
+        """each pod's NUMA-node allocation [p][KS_MAX_NUMA][2] (cpu milli, memory) of the last schedule"""
+        if not self.h:
+            raise ValueError("oracle closed")
+        out = np.zeros((max(p, 1), abi.KS_MAX_NUMA, 2), np.int64)
+        if self.L.ko_fetch_numa_alloc(self.h, out.ctypes.data_as(abi.P64), p) != 0:
+            raise ValueError("no NUMA allocations for that many pods")
         return out[:p]
 
     def read_quota_used(self) -> np.ndarray:

@@ -118,3 +118,65 @@ def test_update_reservation_usage(runtime, oracle_lib):
     check_same(runtime, a, b, w, "reservation usage")
     a.close()
     b.close()
+
+
+def rsv_rows(t, idx):
+    from koordinator_amd.cluster import ReservationTable
+
+    idx = np.asarray(idx)
+    r = ReservationTable(idx.size)
+    for k in ("node", "owner_classes", "flags", "policy", "order", "key_mask", "assigned"):
+        setattr(r, k, getattr(t, k)[idx].copy())
+    for k in ("allocatable", "allocated"):
+        setattr(r, k, getattr(t, k)[:, idx].copy())
+    return r
+
+
+def test_add_delete_reservations(runtime, oracle_lib):
+    """ks_add_reservations / ks_delete_reservations between two scheduled queues: the second queue's results and
+    the final state equal the oracle loaded from scratch with the state after the first queue (node columns,
+    reservation Allocated / assigned) and the merged reservation set."""
+    w = synth.c4(n_nodes=800, n_reservations=2400, n_pods=700)
+    rs = w.reservations
+    first, later = np.arange(1800), np.arange(1800, 2400)
+    rng = np.random.default_rng(12)
+    dead = np.sort(rng.choice(1800, 150, replace=False))
+    q1, q2 = w.pods.rows(range(250)), w.pods.rows(range(250, 700))
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), reservations=rsv_rows(rs, first))
+    orc1 = oracle_lib.Oracle(w.cfg, w.nodes.copy(), nthreads=8, reservations=rsv_rows(rs, first))
+    g1, o1 = ev.schedule(q1), orc1.schedule(q1)
+    assert np.array_equal(g1["reservation"], o1["reservation"]) and np.array_equal(g1["node"], o1["node"])
+    # the oracle's state after queue 1 as a fresh snapshot
+    st = orc1.read_nodes()
+    nodes2 = w.nodes.copy()
+    for k, v in st.as_dict().items():
+        setattr(nodes2, k, v.copy())
+    allocd, assigned = orc1.read_reservations()
+    orc1.close()
+    rs1 = rsv_rows(rs, first)
+    rs1.allocated = np.ascontiguousarray(allocd.T, np.int64)
+    rs1.assigned = assigned.copy()
+    # the deltas on the GPU context
+    assert ev.add_reservations(rsv_rows(rs, later)) == 1800
+    ev.delete_reservations(dead)
+    live = np.setdiff1d(np.arange(2400), dead)  # caller rows of the merged table, in the oracle's row order
+    merged = rsv_rows(rs, np.arange(2400))
+    merged.allocated[:, :1800] = rs1.allocated
+    merged.assigned[:1800] = rs1.assigned
+    merged = rsv_rows(merged, live)
+    orc2 = oracle_lib.Oracle(w.cfg, nodes2, nthreads=8, reservations=merged)
+    g2, o2 = ev.schedule(q2), orc2.schedule(q2)
+    for k in ("node", "status", "score"):
+        assert np.array_equal(g2[k], o2[k]), k
+    want_rsv = np.where(o2["reservation"] >= 0, live[np.maximum(o2["reservation"], 0)], -1)
+    assert np.array_equal(g2["reservation"], want_rsv)
+    assert (g2["reservation"] >= 1800).any(), "no pod went into an added reservation"
+    assert not np.isin(g2["reservation"], dead).any()
+    assert_states_equal({k: v for k, v in ev.read_nodes().as_dict().items()},
+                        {k: v for k, v in orc2.read_nodes().as_dict().items()}, "nodes after deltas")
+    ga, gs = ev.read_reservations()
+    oa, os_ = orc2.read_reservations()
+    assert np.array_equal(ga[live], oa) and np.array_equal(gs[live], os_)
+    assert not ga[dead].any() and not gs[dead].any()
+    ev.close()
+    orc2.close()
