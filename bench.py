@@ -294,7 +294,7 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         "rescans_per_step": agg["rescans"] / steps,
         # pipelined passes: each pass's sweep runs on a second stream while the previous pass
         # commits, so the kernel times below overlap and add up to more than ms_per_step
-        "pipelined": bool(st_last["pipelined"]),
+        "pipelined": int(st_last["pipelined"]),  # 0 off, 1 re-swept, 2 patched lists
         "bubble_passes_per_step": agg["bubble_passes"] / steps,
         "kernel_ms_per_step": {"sweep": round(agg["sweep_ms"] / steps, 3), "select": round(agg["select_ms"] / steps, 3),
                                "commit": round(agg["commit_ms"] / steps, 3),

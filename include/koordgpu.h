@@ -591,6 +591,11 @@ int ks_load_cpu_state(ks_ctx *ctx, const ks_cpu_topology *topologies, int32_t nt
  * and the NUMA allocation; Reserve adds the allocation to used. */
 int ks_load_numa_nodes(ks_ctx *ctx, const ks_numa_node_cols *numa);
 /* used amounts after commits, [node*KS_MAX_NUMA + k]; NULL = skip */
+/* informer delta for the NUMA-node table (NodeResourceTopology / NodeAllocation changes, topology_eventhandler.go,
+ * node_allocation.go): row i of rows ([i*KS_MAX_NUMA + k]) replaces node idx[i]'s NUMA-node resources, allocated
+ * resources and cpuset CPUs; the available CPUs per NUMA node follow from the loaded CPU state.  KS_ESTATE when no
+ * NUMA-node table is loaded; ks_checkpoint again afterwards if the caller restores. */
+int ks_update_numa_nodes(ks_ctx *ctx, const int32_t *idx, const ks_numa_node_cols *rows, int64_t m);
 int ks_read_numa_nodes(ks_ctx *ctx, int64_t *used_cpu, int64_t *used_memory);
 /* CPU sets after commits, [node*KS_CPU_WORDS + w]; NULL = skip */
 int ks_read_cpu_state(ks_ctx *ctx, uint64_t *allocated, uint64_t *excl_pcpu, uint64_t *excl_numa);

@@ -435,6 +435,7 @@ EXPORTED_SYMBOLS = [
     "ks_update_quotas",
     "ks_update_reservation_usage",
     "ks_add_reservations",
+    "ks_update_numa_nodes",
     "ks_delete_reservations",
     "ks_read_nodes",
     "ks_read_quota_used",

@@ -2101,6 +2101,46 @@ static size_t numa_mut_bytes(size_t np) {
   return 2 * K * np * 8 + K * np * 8 + 2 * K * np * 4 + align16(np * 4);
 }
 
+// One node's NUMA-node table words (ks_numa.h layout): row r of nc describes node `node` (numa_flags f, cpu
+// amplification ratio).  Only NUMA-policy nodes carry resources; the policy-None path never reads them.
+struct NumaRow {
+  int32_t cnt = 0;
+  uint32_t pres = 0;
+  int64_t tot[2 * kNumaDev] = {}, used[2 * kNumaDev] = {}, off[kNumaDev] = {};
+  int32_t cs[kNumaDev] = {};
+};
+static int numa_encode(ks_ctx* ctx, const ks_numa_node_cols* nc, int64_t r, int64_t node, uint32_t f, double ratio,
+                       NumaRow& w) {
+  constexpr int K = kNumaDev;
+  w = NumaRow{};
+  const uint32_t pol = (f >> KS_NUMA_POLICY_SHIFT) & 3u;
+  const int32_t c = nc->count[r];
+  if (c < 0 || c > KS_MAX_NUMA) KS_FAIL(ctx, KS_EINVAL, "node %lld: NUMA node count %d", (long long)node, c);
+  if (pol == 0) return KS_OK;
+  if (c > K) KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: %d NUMA nodes with a NUMA policy (the device evaluates up to %d)", (long long)node, c, K);
+  w.cnt = c;
+  for (int k = 0; k < c; ++k) {
+    const size_t o = (size_t)r * KS_MAX_NUMA + k;
+    const int64_t ac = nc->alloc_cpu ? nc->alloc_cpu[o] : 0, am = nc->alloc_memory ? nc->alloc_memory[o] : 0;
+    const int64_t uc = nc->used_cpu ? nc->used_cpu[o] : 0, um = nc->used_memory ? nc->used_memory[o] : 0;
+    const int32_t cpus = nc->cpuset_cpus ? nc->cpuset_cpus[o] : 0;
+    const int64_t cs = (int64_t)cpus * 1000;
+    const int64_t lim = (int64_t)1 << 50;
+    if (ac < 0 || am < 0 || uc < 0 || um < 0 || cs < 0 || ac > lim || am > lim || uc > lim || um > lim || cs > lim)
+      KS_FAIL(ctx, KS_EINVAL, "node %lld NUMA %d: quantity out of range", (long long)node, k);
+    // amplifyNUMANodeResources / extension.Amplify: int64(math.Ceil(float64(v) * ratio)) for ratio > 1
+    w.tot[0 * K + k] = ratio > 1.0 ? (int64_t)std::ceil((double)ac * ratio) : ac;
+    w.tot[1 * K + k] = am;
+    w.used[0 * K + k] = uc;
+    w.used[1 * K + k] = um;
+    w.off[k] = ratio > 1.0 ? (int64_t)std::ceil((double)cs * ratio) - cs : 0;
+    w.cs[k] = cpus;
+    const bool present = nc->used_present ? nc->used_present[o] != 0 : (uc != 0 || um != 0);
+    if (present) w.pres |= 1u << k;
+  }
+  return KS_OK;
+}
+
 static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t* flags_h, const double* ratio_h) {
   const size_t np = (size_t)ctx->npad;
   constexpr int K = kNumaDev;
@@ -2116,32 +2156,18 @@ static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t
   uint32_t* pres = (uint32_t*)(h.data() + o_pres);
   ctx->h_numa_k.assign((size_t)ctx->n, 0);
   for (int64_t i = 0; nc && i < ctx->n; ++i) {
-    const uint32_t pol = (flags_h[i] >> KS_NUMA_POLICY_SHIFT) & 3u;
-    const int32_t c = nc->count[i];
-    if (c < 0 || c > KS_MAX_NUMA) KS_FAIL(ctx, KS_EINVAL, "node %lld: NUMA node count %d", (long long)i, c);
-    if (pol == 0) continue;  // the policy-None path never reads NUMA-node resources
-    if (c > K) KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: %d NUMA nodes with a NUMA policy (the device evaluates up to %d)", (long long)i, c, K);
-    cnt[i] = c;
-    ctx->h_numa_k[(size_t)i] = (int8_t)c;
-    const double ratio = ratio_h ? ratio_h[i] : 0.0;
-    for (int k = 0; k < c; ++k) {
-      const size_t o = (size_t)i * KS_MAX_NUMA + k;
-      const int64_t ac = nc->alloc_cpu ? nc->alloc_cpu[o] : 0, am = nc->alloc_memory ? nc->alloc_memory[o] : 0;
-      const int64_t uc = nc->used_cpu ? nc->used_cpu[o] : 0, um = nc->used_memory ? nc->used_memory[o] : 0;
-      const int32_t cpus = nc->cpuset_cpus ? nc->cpuset_cpus[o] : 0;
-      const int64_t cs = (int64_t)cpus * 1000;
-      const int64_t lim = (int64_t)1 << 50;
-      if (ac < 0 || am < 0 || uc < 0 || um < 0 || cs < 0 || ac > lim || am > lim || uc > lim || um > lim || cs > lim)
-        KS_FAIL(ctx, KS_EINVAL, "node %lld NUMA %d: quantity out of range", (long long)i, k);
-      // amplifyNUMANodeResources / extension.Amplify: int64(math.Ceil(float64(v) * ratio)) for ratio > 1
-      tot[(size_t)(0 * K + k) * np + i] = ratio > 1.0 ? (int64_t)std::ceil((double)ac * ratio) : ac;
-      tot[(size_t)(1 * K + k) * np + i] = am;
-      used[(size_t)(0 * K + k) * np + i] = uc;
-      used[(size_t)(1 * K + k) * np + i] = um;
-      off[(size_t)k * np + i] = ratio > 1.0 ? (int64_t)std::ceil((double)cs * ratio) - cs : 0;
-      csv[(size_t)k * np + i] = cpus;
-      const bool present = nc->used_present ? nc->used_present[o] != 0 : (uc != 0 || um != 0);
-      if (present) pres[i] |= 1u << k;
+    NumaRow w;
+    if (int rc = numa_encode(ctx, nc, i, i, flags_h[i], ratio_h ? ratio_h[i] : 0.0, w); rc != KS_OK) return rc;
+    cnt[i] = w.cnt;
+    ctx->h_numa_k[(size_t)i] = (int8_t)w.cnt;
+    pres[i] = w.pres;
+    for (int k = 0; k < K; ++k) {
+      for (int q = 0; q < 2; ++q) {
+        tot[(size_t)(q * K + k) * np + i] = w.tot[q * K + k];
+        used[(size_t)(q * K + k) * np + i] = w.used[q * K + k];
+      }
+      off[(size_t)k * np + i] = w.off[k];
+      csv[(size_t)k * np + i] = w.cs[k];
     }
   }
   dev_free(ctx->numa_blob);
@@ -2180,6 +2206,62 @@ int ks_load_numa_nodes(ks_ctx* ctx, const ks_numa_node_cols* nc) {
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   }
   return numa_install(ctx, nc, flags.data(), ratio.data());
+}
+
+// NodeResourceTopology / NodeAllocation changes of m nodes (topology_eventhandler.go, node_allocation.go): row i
+// of rows ([i * KS_MAX_NUMA + k]) replaces node idx[i]'s NUMA-node resources, allocated resources and cpuset CPUs;
+// the available CPUs per NUMA node follow from the CPU state (numa_refresh_free).
+static int scatter_words(ks_ctx* ctx, void* dst, size_t elem, int64_t rs, int64_t cs, int32_t W,
+                         const std::vector<int32_t>& idx, const void* src);
+static int check_idx(ks_ctx* ctx, const int32_t* idx, int64_t m, int64_t lim, const char* what, std::vector<int32_t>& out);
+
+int ks_update_numa_nodes(ks_ctx* ctx, const int32_t* idx, const ks_numa_node_cols* rows, int64_t m) {
+  if (!ctx || !rows || m < 0 || (m > 0 && (!idx || !rows->count)))
+    return ctx ? (ctx->err = "ks_update_numa_nodes: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->numa_blob) KS_FAIL(ctx, KS_ESTATE, "ks_update_numa_nodes: no NUMA-node table (no node has a NUMA policy)");
+  std::vector<int32_t> ix;
+  if (int rc = check_idx(ctx, idx, m, ctx->n, "ks_update_numa_nodes", ix); rc != KS_OK) return rc;
+  if (m == 0) return KS_OK;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  const size_t n = (size_t)ctx->n;
+  std::vector<uint32_t> flags(n);
+  std::vector<double> ratio(n);
+  HIPCHK(ctx, hipMemcpyAsync(flags.data(), ctx->d.numa_flags, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(ratio.data(), ctx->d.numa_ratio, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  constexpr int K = kNumaDev;
+  std::vector<int32_t> cnt((size_t)m), cs((size_t)m * K);
+  std::vector<uint32_t> pres((size_t)m);
+  std::vector<int64_t> tot((size_t)m * 2 * K), used((size_t)m * 2 * K), off((size_t)m * K);
+  for (int64_t i = 0; i < m; ++i) {
+    const int32_t node = ix[(size_t)i];
+    NumaRow w;
+    if (int rc = numa_encode(ctx, rows, i, node, flags[(size_t)node], ratio[(size_t)node], w); rc != KS_OK) return rc;
+    cnt[(size_t)i] = w.cnt;
+    pres[(size_t)i] = w.pres;
+    // word-major [w][m] (scatter_words)
+    for (int q = 0; q < 2 * K; ++q) {
+      tot[(size_t)q * m + i] = w.tot[q];
+      used[(size_t)q * m + i] = w.used[q];
+    }
+    for (int q = 0; q < K; ++q) {
+      off[(size_t)q * m + i] = w.off[q];
+      cs[(size_t)q * m + i] = w.cs[q];
+    }
+  }
+  const int64_t np = ctx->npad;
+  DevNuma& v = ctx->nv;
+  if (scatter_words(ctx, (void*)v.count, 4, 1, np, 1, ix, cnt.data()) != KS_OK ||
+      scatter_words(ctx, (void*)v.present, 4, 1, np, 1, ix, pres.data()) != KS_OK ||
+      scatter_words(ctx, (void*)v.total, 8, 1, np, 2 * K, ix, tot.data()) != KS_OK ||
+      scatter_words(ctx, (void*)v.used, 8, 1, np, 2 * K, ix, used.data()) != KS_OK ||
+      scatter_words(ctx, (void*)v.off, 8, 1, np, K, ix, off.data()) != KS_OK ||
+      scatter_words(ctx, (void*)v.cs, 4, 1, np, K, ix, cs.data()) != KS_OK)
+    return KS_EHIP;
+  for (int64_t i = 0; i < m; ++i) ctx->h_numa_k[(size_t)ix[(size_t)i]] = (int8_t)cnt[(size_t)i];
+  if (int rc = numa_refresh_free(ctx); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return check_dev_numa(ctx);
 }
 
 int ks_read_numa_nodes(ks_ctx* ctx, int64_t* used_cpu, int64_t* used_memory) {
@@ -2987,6 +3069,15 @@ static bool pipelined(const ks_ctx* ctx) {
   return mode == 2 || ctx->n >= env_min;
 }
 
+// The pipelined passes' two streams per device, shared by the process's contexts and never destroyed: destroying
+// the CU-masked streams and creating new ones for a later context hung that context's teardown on MI355X
+// (gpurun_out/r03c).
+struct PipeStreams {
+  hipStream_t s = nullptr, c = nullptr;
+};
+static std::mutex g_pipe_mu;
+static std::vector<PipeStreams> g_pipe;
+
 // The sweep stream (one CU left out of its mask by default, so the one-workgroup commit always finds a CU while a
 // sweep fills the rest; KS_PIPE_CUMASK=0: no mask), the pipe words and the event ring.
 static int ensure_pipe(ks_ctx* ctx) {
@@ -3003,14 +3094,9 @@ static int ensure_pipe(ks_ctx* ctx) {
     // queues (stream creation then stalls).  Sharing only orders the passes of different contexts; each context's
     // own events order its passes.  The commit stream runs on the one CU the sweep stream leaves out, so the
     // one-workgroup commit never shares a CU (and its SIMDs' issue slots) with sweep waves.
-    struct Pair {
-      hipStream_t s = nullptr, c = nullptr;
-    };
-    static std::mutex mu;
-    static std::vector<Pair> per_dev;
-    std::lock_guard<std::mutex> lock(mu);
-    if (per_dev.size() <= (size_t)ctx->device) per_dev.resize((size_t)ctx->device + 1);
-    Pair& st = per_dev[(size_t)ctx->device];
+    std::lock_guard<std::mutex> lock(g_pipe_mu);
+    if (g_pipe.size() <= (size_t)ctx->device) g_pipe.resize((size_t)ctx->device + 1);
+    PipeStreams& st = g_pipe[(size_t)ctx->device];
     if (!st.s) {
       static const int64_t env_mask = env_i64("KS_PIPE_CUMASK", 1, 0, 1);
       int ncu = 0;

@@ -73,48 +73,57 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
   const uint32_t vblock = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   const int64_t wave = (int64_t)vblock * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
-  if (cursor >= a.total_pods) return;
-  const int32_t np = min(a.batch, a.total_pods - cursor);
   if (a.list_t) {
     // one wave per (pod, list entry): a monotone commit only lowered the keys of the nodes it wrote, so an entry
     // whose chunk it did not write keeps its keys, a written one takes fresh keys, and a chunk outside the list
     // stays below the bound.  The pod's top is the largest listed key when that is at least the bound (else 0:
     // the best node may lie outside the list, and the commit's resolution then cuts the pass there).
-    if (__builtin_amdgcn_readfirstlane(*a.fix_cursor) != cursor) return;  // a bubble pass
-    const int32_t m = min(__builtin_amdgcn_readfirstlane(a.fix[0]), kMaxBatch);
-    const int32_t dch = lane < m ? (a.fix[1 + lane] >> 6) : -1;  // lane i: the chunk of written node i
+    // A written chunk whose best and runner-up nodes were both left alone keeps them: their keys are exact, and
+    // every other node's key was at most the runner-up's when swept (a half-written row included) and has only
+    // dropped since.  Most waves have nothing to re-evaluate, so every input load is issued before the first use
+    // (one HBM round trip instead of one per dependent read); the host launches >= kMaxBatch * K waves.
     const int32_t K = a.list_k;
-    for (int64_t w = wave; w < (int64_t)np * K; w += nwaves) {
-      const int32_t p = (int32_t)(w / K), e = (int32_t)(w - (int64_t)p * K);
-      if (e >= __builtin_amdgcn_readfirstlane(a.list_count[p])) continue;
-      const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(a.list_chunk[p * K + e]);
-      uint2 t;
-      if (__ballot(dch == (int32_t)c)) {
-        const int64_t node = c * 64 + lane;
-        NodeReg<NSC> r;
-        {
-          const DevNodes d = *a.dn;
-          load_node<NSC>(a.c, d, node, node < a.n, r);
-        }
-        const PodRec pod = load_pod_uniform(a.pods + cursor + p);
-        EvalOut o = eval_full<NSC, false, true, FEAT>(
-            a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
-            [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
-        const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, 0) + 1) << 6) | (uint32_t)(63 - lane));
-        t.x = wave_max_u32(key);
-        t.y = wave_max_u32(key == t.x ? 0u : key);
-        if (lane == 0) a.list_t[p * K + e] = t;
-      } else {
-        const uint2 v = a.list_t[p * K + e];
-        t.x = __builtin_amdgcn_readfirstlane(v.x);
+    if (wave >= (int64_t)kMaxBatch * K) return;
+    const int32_t p = (int32_t)(wave / K), e = (int32_t)(wave - (int64_t)p * K);
+    const int32_t c_raw = *a.cursor, fc_raw = *a.fix_cursor, m_raw = a.fix[0];
+    const int32_t wn_raw = a.fix[1 + lane];                 // the list has kMaxBatch node words
+    const int32_t cnt_raw = a.list_count[p];
+    const uint32_t ch_raw = a.list_chunk[p * K + e];
+    const uint2 v = a.list_t[p * K + e];
+    const uint64_t b = a.list_bound[p];
+    const int32_t cursor = __builtin_amdgcn_readfirstlane(c_raw);
+    if (cursor >= a.total_pods || __builtin_amdgcn_readfirstlane(fc_raw) != cursor) return;  // done / a bubble
+    const int32_t np = min(a.batch, a.total_pods - cursor);
+    if (p >= np || e >= __builtin_amdgcn_readfirstlane(cnt_raw)) return;
+    const int32_t m = min(__builtin_amdgcn_readfirstlane(m_raw), kMaxBatch);
+    const int32_t wn = lane < m ? wn_raw : -1;  // lane i: written node i
+    const int64_t c = (int64_t)__builtin_amdgcn_readfirstlane(ch_raw);
+    uint2 t = make_uint2(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y));
+    const int32_t nb = (int32_t)(c * 64 + 63 - (int64_t)(t.x & 63u));
+    const int32_t nr = t.y ? (int32_t)(c * 64 + 63 - (int64_t)(t.y & 63u)) : -2;
+    if (__ballot(wn >= 0 && (wn == nb || wn == nr))) {
+      const int64_t node = c * 64 + lane;
+      NodeReg<NSC> r;
+      {
+        const DevNodes d = *a.dn;
+        load_node<NSC>(a.c, d, node, node < a.n, r);
       }
-      const uint64_t b = a.list_bound[p];
-      const uint64_t g = t.x ? local_gkey(t.x, c) : 0ull;
-      if (lane == 0 && g && (b == 0ull || g >= b)) atomicMax(a.list_top + p, (unsigned long long)g);
+      const PodRec pod = load_pod_uniform(a.pods + cursor + p);
+      EvalOut o = eval_full<NSC, false, true, FEAT>(
+          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+          [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
+      const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, 0) + 1) << 6) | (uint32_t)(63 - lane));
+      t.x = wave_max_u32(key);
+      t.y = wave_max_u32(key == t.x ? 0u : key);
+      if (lane == 0) a.list_t[p * K + e] = t;
     }
+    const uint64_t g = t.x ? local_gkey(t.x, c) : 0ull;
+    if (lane == 0 && g && (b == 0ull || g >= b)) atomicMax(a.list_top + p, (unsigned long long)g);
     return;
   }
+  const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor);
   const int32_t groups = (np + a.ppw - 1) / a.ppw;
   int64_t nitems = a.c1 - a.c0;
   if (a.fix) {

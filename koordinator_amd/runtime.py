@@ -85,6 +85,7 @@ def lib() -> C.CDLL:
     L.ks_update_cpu_state.argtypes = [vp, abi.P32, C.POINTER(abi.KsCpuStateCols), C.c_int64]
     L.ks_update_quotas.argtypes = [vp, abi.P32, C.POINTER(abi.KsQuotaCols), C.c_int32]
     L.ks_update_reservation_usage.argtypes = [vp, abi.P32, C.POINTER(abi.P64), abi.P32, C.c_int32]
+    L.ks_update_numa_nodes.argtypes = [vp, abi.P32, C.POINTER(abi.KsNumaNodeCols), C.c_int64]
     L.ks_add_reservations.argtypes = [vp, C.POINTER(abi.KsReservationCols), C.c_int32, abi.P32]
     L.ks_delete_reservations.argtypes = [vp, abi.P32, C.c_int32]
     L.ks_read_nodes.argtypes = [vp, C.POINTER(abi.KsNodeState)]
@@ -189,6 +190,12 @@ class Evaluator:
         self._chk(self.L.ks_add_reservations(self.h, C.byref(cols), rs.r, first.ctypes.data_as(abi.P32)))
         self.nr = int(first[0]) + rs.r
         return int(first[0])
+
+    def update_numa_nodes(self, idx, rows):
+        """informer delta: node idx[i]'s NUMA-node table from row i of rows (a NumaNodeTable of len(idx) nodes)"""
+        idx = np.ascontiguousarray(idx, np.int32)
+        cols = rows.ks()
+        self._chk(self.L.ks_update_numa_nodes(self.h, idx.ctypes.data_as(abi.P32), C.byref(cols), idx.size))
 
     def delete_reservations(self, rows):
         """informer delete of caller rows (their numbers are not reused)"""

@@ -180,3 +180,34 @@ def test_add_delete_reservations(runtime, oracle_lib):
     assert not ga[dead].any() and not gs[dead].any()
     ev.close()
     orc2.close()
+
+
+def numa_rows(t, idx):
+    from koordinator_amd.cluster import NumaNodes
+
+    r = NumaNodes(len(idx))
+    for k in ("count", "alloc_cpu", "alloc_memory", "used_cpu", "used_memory", "used_present", "cpuset_cpus"):
+        setattr(r, k, getattr(t, k)[idx].copy())
+    return r
+
+
+def test_update_numa_nodes(runtime, oracle_lib):
+    """ks_update_numa_nodes (NodeAllocation allocatedResources changed on some NUMA-policy nodes) == the oracle
+    loaded with the merged NUMA-node table"""
+    w = synth.c3(seed=93, n_nodes=400, n_pods=500)
+    pol = np.nonzero(((w.nodes.numa_flags >> abi.KS_NUMA_POLICY_SHIFT) & 3) != 0)[0]
+    rng = np.random.default_rng(14)
+    idx = np.sort(rng.choice(pol, 60, replace=False)).astype(np.int32)
+    nn = w.numa_nodes.copy()
+    for i in idx:
+        for k in range(nn.count[i]):
+            nn.used_cpu[i, k] = nn.alloc_cpu[i, k] * rng.integers(0, 4) // 8
+            nn.used_memory[i, k] = nn.alloc_memory[i, k] * rng.integers(0, 4) // 8
+            nn.used_present[i, k] = 1 if (nn.used_cpu[i, k] or nn.used_memory[i, k] or rng.random() < 0.3) else 0
+    a = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    a.update_numa_nodes(idx, numa_rows(nn, idx))
+    w.numa_nodes = nn
+    b = oracle_on(oracle_lib, w)
+    check_same(runtime, a, b, w, "numa nodes")
+    a.close()
+    b.close()
