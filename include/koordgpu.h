@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 5
+#define KS_ABI_VERSION 6
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -166,6 +166,9 @@ extern "C" {
                                              node's (plugin.go:310-312) */
 #define KS_R_NUMA_SMT 0x1000000u          /* ErrSMTAlignmentError: required FullPCPUs and numCPUsNeeded not a multiple
                                              of the node's CPUsPerCore (plugin.go:314-317) */
+#define KS_R_TAINT 0x2000000u             /* upstream TaintToleration Filter: "node(s) had untolerated taint" (a NoSchedule /
+                                             NoExecute taint no toleration of the pod tolerates) */
+#define KS_R_NODE_AFFINITY 0x4000000u     /* upstream NodeAffinity Filter: "node(s) didn't match Pod's node affinity/selector" */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -184,7 +187,9 @@ extern "C" {
 #define KS_SCORE_NUMA 3        /* NodeNUMAResource scoreWithAmplifiedCPUs (nodenumaresource/scoring.go:98-114) */
 #define KS_SCORE_DEVICESHARE 4 /* after DefaultNormalizeScore (deviceshare/scoring.go:95-97) */
 #define KS_SCORE_BALANCED 5    /* upstream NodeResourcesBalancedAllocation (balanced_allocation.go, v1.24) */
-#define KS_NUM_SCORE_PLUGINS 6
+#define KS_SCORE_TAINT 6       /* upstream TaintToleration after DefaultNormalizeScore(100, reverse) (v1.24) */
+#define KS_SCORE_NODE_AFFINITY 7 /* upstream NodeAffinity after DefaultNormalizeScore(100) (v1.24) */
+#define KS_NUM_SCORE_PLUGINS 8
 
 /* ---- per-node DeviceShare flags (ks_device_cols.flags) ---- */
 #define KS_DEV_PRESENT 0x1u /* nodeDeviceCache.getNodeDevice != nil (deviceshare/plugin.go:286-289) */
@@ -288,6 +293,29 @@ typedef struct ks_balanced_args {
   int64_t plugin_weight;
 } ks_balanced_args;
 
+/* Upstream TaintToleration and NodeAffinity (kube-scheduler v1.24.15 plugins/tainttoleration, plugins/nodeaffinity;
+ * both enabled with weight 1 by the v1beta2 default profile).  The label and taint matching runs on the host once per
+ * distinct taint / label requirement and reaches the device as bit masks over two per-context dictionaries
+ * (INTEGRATION.md "Taints and node affinity"):
+ *   taint dictionary   <= 64 distinct node taints (key, value, effect); ks_node_cols.taints_hard / taints_soft carry
+ *                      the node's NoSchedule|NoExecute / PreferNoSchedule taints, ks_pod_cols.tolerated the taints
+ *                      some toleration of the pod tolerates (Toleration.ToleratesTaint);
+ *   label dictionary   <= 63 distinct node selector requirements (key, operator, values) of the pending pods
+ *                      (nodeSelector entries become key In [value]); ks_node_cols.labels bit i = requirement i
+ *                      matches the node's labels (or metadata.name for matchFields); bit 63 (KS_LABEL_NEVER) is
+ *                      never set on a node and stands for an empty NodeSelectorTerm, which matches nothing.
+ * TaintToleration Filter: no NoSchedule/NoExecute taint untolerated; Score: the number of PreferNoSchedule taints
+ * untolerated, DefaultNormalizeScore(100, reverse = true) over the feasible nodes.  NodeAffinity Filter: the pod's
+ * required terms (nodeSelector requirements ANDed into every term) -- one term whose requirement bits are all set on
+ * the node; Score: sum of the weights of the preferred terms whose bits are all set, DefaultNormalizeScore(100). */
+#define KS_AFFINITY_TERMS 4
+#define KS_LABEL_NEVER (1ull << 63)
+typedef struct ks_static_plugin_args {
+  int32_t enable_filter;
+  int32_t enable_score;
+  int64_t plugin_weight;
+} ks_static_plugin_args;
+
 typedef struct ks_config {
   int32_t abi_version; /* = KS_ABI_VERSION */
   int32_t device;      /* HIP device ordinal */
@@ -302,6 +330,8 @@ typedef struct ks_config {
   ks_numa_args numa;
   ks_deviceshare_args deviceshare;
   ks_balanced_args balanced; /* ABI 5 */
+  ks_static_plugin_args taint;    /* ABI 6: upstream TaintToleration */
+  ks_static_plugin_args affinity; /* ABI 6: upstream NodeAffinity */
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -343,6 +373,11 @@ typedef struct ks_node_cols {
   const double *numa_cpu_amplification; /* node annotation cpu amplification ratio; NULL / <= 1 = none */
   const int32_t *numa_cpuset_cpus;      /* CPUs allocated to cpuset pods: GetAvailableCPUs' allocated.Size() */
   const uint32_t *numa_flags;           /* KS_NUMA_* */
+  /* TaintToleration / NodeAffinity (ABI 6; NULL = 0): bits over the context's taint / label dictionaries, see
+   * ks_static_plugin_args.  Static per node: changed only through ks_load_nodes / ks_update_nodes. */
+  const uint64_t *taints_hard;  /* taints with effect NoSchedule or NoExecute */
+  const uint64_t *taints_soft;  /* taints with effect PreferNoSchedule */
+  const uint64_t *labels;       /* node selector requirements the node matches (bit 63 must be 0) */
 } ks_node_cols;
 
 /* Pending pods, queue order, structure-of-arrays. */
@@ -387,6 +422,12 @@ typedef struct ks_pod_cols {
   /* DeviceShare joint allocation (apiext.DeviceJointAllocate, device_allocator.go:188-339): KS_JOINT_*; the
    * only supported DeviceTypes list is [gpu, rdma]; NULL = none */
   const uint8_t *joint;
+  /* TaintToleration / NodeAffinity (ABI 6; NULL = none): see ks_static_plugin_args */
+  const uint64_t *tolerated;                              /* dictionary taints some toleration tolerates */
+  const int32_t *affinity_required_n;                     /* required terms (0 = no nodeSelector / required affinity) */
+  const uint64_t *affinity_required[KS_AFFINITY_TERMS];   /* term t: the requirement bits it needs */
+  const uint64_t *affinity_preferred[KS_AFFINITY_TERMS];  /* preferred term t: the requirement bits it needs */
+  const int32_t *affinity_weight[KS_AFFINITY_TERMS];      /* preferred term t's weight, 1..100 (0 = unused) */
 } ks_pod_cols;
 
 #define KS_JOINT_NONE 0u

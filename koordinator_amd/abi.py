@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 5
+KS_ABI_VERSION = 6
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
@@ -102,6 +102,8 @@ KS_R_NUMA_CPUSET = 0x200000
 KS_R_NUMA_INVALID_CPUS = 0x400000
 KS_R_NUMA_BIND_CONFLICT = 0x800000
 KS_R_NUMA_SMT = 0x1000000
+KS_R_TAINT = 0x2000000
+KS_R_NODE_AFFINITY = 0x4000000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -116,7 +118,11 @@ KS_SCORE_RESERVATION = 2
 KS_SCORE_NUMA = 3
 KS_SCORE_DEVICESHARE = 4
 KS_SCORE_BALANCED = 5
-KS_NUM_SCORE_PLUGINS = 6
+KS_SCORE_TAINT = 6
+KS_SCORE_NODE_AFFINITY = 7
+KS_NUM_SCORE_PLUGINS = 8
+KS_AFFINITY_TERMS = 4
+KS_LABEL_NEVER = 1 << 63
 KS_BAL_CPU = 0x1
 KS_BAL_MEMORY = 0x2
 
@@ -183,6 +189,10 @@ class KsBalancedArgs(C.Structure):
     _fields_ = [("enable", C.c_int32), ("resources", C.c_int32), ("plugin_weight", C.c_int64)]
 
 
+class KsStaticPluginArgs(C.Structure):
+    _fields_ = [("enable_filter", C.c_int32), ("enable_score", C.c_int32), ("plugin_weight", C.c_int64)]
+
+
 class KsConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -198,6 +208,8 @@ class KsConfig(C.Structure):
         ("numa", KsNumaArgs),
         ("deviceshare", KsDeviceShareArgs),
         ("balanced", KsBalancedArgs),
+        ("taint", KsStaticPluginArgs),
+        ("affinity", KsStaticPluginArgs),
     ]
 
 
@@ -234,6 +246,9 @@ NODE_COLS = [
     ("numa_cpu_amplification", C.POINTER(C.c_double)),
     ("numa_cpuset_cpus", P32),
     ("numa_flags", PU32),
+    ("taints_hard", C.POINTER(C.c_uint64)),
+    ("taints_soft", C.POINTER(C.c_uint64)),
+    ("labels", C.POINTER(C.c_uint64)),
 ]
 
 
@@ -265,6 +280,11 @@ POD_COLS = [
     ("cpu_bind", PU32),
     ("rdma", P64),
     ("joint", C.POINTER(C.c_uint8)),
+    ("tolerated", C.POINTER(C.c_uint64)),
+    ("affinity_required_n", P32),
+    ("affinity_required", C.POINTER(C.c_uint64) * KS_AFFINITY_TERMS),
+    ("affinity_preferred", C.POINTER(C.c_uint64) * KS_AFFINITY_TERMS),
+    ("affinity_weight", P32 * KS_AFFINITY_TERMS),
 ]
 
 

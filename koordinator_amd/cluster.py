@@ -29,6 +29,8 @@ NODE_I64 = [
 NODE_I32 = ["allowed_pods", "pod_count", "la_thr_cpu", "la_thr_memory", "la_prod_thr_cpu", "la_prod_thr_memory",
             "numa_cpuset_cpus"]
 NODE_U32 = ["la_flags", "numa_flags"]
+# TaintToleration / NodeAffinity dictionary bits (static_plugins.compile_cluster)
+NODE_U64 = ["taints_hard", "taints_soft", "labels"]
 
 POD_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral",
@@ -36,9 +38,10 @@ POD_I64 = [
     "la_req_cpu", "la_lim_cpu", "la_dflt_cpu", "la_req_memory", "la_lim_memory", "la_dflt_memory",
     "gpu_core", "gpu_memory", "gpu_memory_ratio", "rdma",
 ]
-POD_I32 = ["quota", "rsv_class"]
+POD_I32 = ["quota", "rsv_class", "affinity_required_n"]
 POD_U32 = ["flags", "quota_mask", "cpu_bind"]
 POD_U8 = ["joint"]
+POD_U64 = ["tolerated"]
 
 STATE_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral", "nonzero_milli_cpu", "nonzero_memory",
@@ -65,6 +68,7 @@ class _Table:
     I32: list = []
     U32: list = []
     U8: list = []
+    U64: list = []
     N_SCALAR_ARRAYS: tuple = ()
 
     def __init__(self, n: int):
@@ -77,9 +81,11 @@ class _Table:
             setattr(self, name, np.zeros(self.n, np.uint32))
         for name in self.U8:
             setattr(self, name, np.zeros(self.n, np.uint8))
+        for name in self.U64:
+            setattr(self, name, np.zeros(self.n, np.uint64))
 
     def columns(self) -> Dict[str, np.ndarray]:
-        return {k: getattr(self, k) for k in self.I64 + self.I32 + self.U32 + self.U8}
+        return {k: getattr(self, k) for k in self.I64 + self.I32 + self.U32 + self.U8 + self.U64}
 
     def _fix(self):
         for name in self.I64:
@@ -98,12 +104,17 @@ class _Table:
             a = getattr(self, name)
             if a.dtype != np.uint8 or not a.flags.c_contiguous:
                 setattr(self, name, np.ascontiguousarray(a, np.uint8))
+        for name in self.U64:
+            a = getattr(self, name)
+            if a.dtype != np.uint64 or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, np.uint64))
 
 
 class NodeTable(_Table):
     I64 = NODE_I64
     I32 = NODE_I32
     U32 = NODE_U32
+    U64 = NODE_U64
 
     def __init__(self, n: int):
         super().__init__(n)
@@ -147,6 +158,8 @@ class NodeTable(_Table):
             setattr(c, name, _p32(getattr(self, name)))
         c.la_flags = _pu32(self.la_flags)
         c.numa_flags = _pu32(self.numa_flags)
+        for name in NODE_U64:
+            setattr(c, name, getattr(self, name).ctypes.data_as(C.POINTER(C.c_uint64)))
         self.numa_cpu_amplification = np.ascontiguousarray(self.numa_cpu_amplification, np.float64)
         c.numa_cpu_amplification = self.numa_cpu_amplification.ctypes.data_as(C.POINTER(C.c_double))
         for k in range(abi.KS_MAX_SCALARS):
@@ -161,6 +174,7 @@ class PodTable(_Table):
     I32 = POD_I32
     U32 = POD_U32
     U8 = POD_U8
+    U64 = POD_U64
 
     def __init__(self, n: int):
         super().__init__(n)
@@ -168,6 +182,10 @@ class PodTable(_Table):
         self.rsv_class[:] = -1
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.quota_req = np.zeros((abi.KS_QUOTA_DIMS, self.n), np.int64)
+        # NodeAffinity terms over the label dictionary (static_plugins.compile_cluster)
+        self.affinity_required = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.uint64)
+        self.affinity_preferred = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.uint64)
+        self.affinity_weight = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.int32)
 
     def rows(self, idx) -> "PodTable":
         idx = np.asarray(idx)
@@ -176,6 +194,8 @@ class PodTable(_Table):
             setattr(t, k, np.ascontiguousarray(v[idx]))
         t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
         t.quota_req = np.ascontiguousarray(self.quota_req[:, idx])
+        for k in ("affinity_required", "affinity_preferred", "affinity_weight"):
+            setattr(t, k, np.ascontiguousarray(getattr(self, k)[:, idx]))
         return t
 
     def ks(self) -> abi.KsPodCols:
@@ -195,6 +215,15 @@ class PodTable(_Table):
             c.req_scalar[k] = _p64(self.req_scalar[k])
         for d in range(abi.KS_QUOTA_DIMS):
             c.quota_req[d] = _p64(self.quota_req[d])
+        c.tolerated = self.tolerated.ctypes.data_as(C.POINTER(C.c_uint64))
+        c.affinity_required_n = _p32(self.affinity_required_n)
+        self.affinity_required = np.ascontiguousarray(self.affinity_required, np.uint64)
+        self.affinity_preferred = np.ascontiguousarray(self.affinity_preferred, np.uint64)
+        self.affinity_weight = np.ascontiguousarray(self.affinity_weight, np.int32)
+        for t in range(abi.KS_AFFINITY_TERMS):
+            c.affinity_required[t] = self.affinity_required[t].ctypes.data_as(C.POINTER(C.c_uint64))
+            c.affinity_preferred[t] = self.affinity_preferred[t].ctypes.data_as(C.POINTER(C.c_uint64))
+            c.affinity_weight[t] = _p32(self.affinity_weight[t])
         c._keep = self
         return c
 

@@ -156,6 +156,12 @@ class SchedulerProfile:
     deviceshare_weight: int = 1
     balanced: Optional[NodeResourcesBalancedAllocationArgs] = None  # upstream default plugin; None = disabled
     balanced_weight: int = 1
+    # upstream TaintToleration / NodeAffinity (v1beta2 default profile: both on, weight 1); the host compiles taints,
+    # tolerations, node labels and node selectors into dictionary bits (static_plugins.compile_cluster)
+    taint_toleration: bool = False
+    taint_toleration_weight: int = 1
+    node_affinity: bool = False
+    node_affinity_weight: int = 1
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -241,6 +247,14 @@ class SchedulerProfile:
                 else:
                     raise ValidationError(f"NodeResourcesBalancedAllocation on {name} is not supported (cpu/memory only)")
             c.balanced.plugin_weight = self.balanced_weight
+        if self.taint_toleration:
+            c.taint.enable_filter = 1
+            c.taint.enable_score = 1 if self.taint_toleration_weight else 0
+            c.taint.plugin_weight = self.taint_toleration_weight
+        if self.node_affinity:
+            c.affinity.enable_filter = 1
+            c.affinity.enable_score = 1 if self.node_affinity_weight else 0
+            c.affinity.plugin_weight = self.node_affinity_weight
         if self.reservation_weight is not None:
             c.reservation.enable = 1
             c.reservation.plugin_weight = int(self.reservation_weight)

@@ -121,6 +121,7 @@ struct DevPodCols {
   int64_t *gpu_core, *gpu_mem, *gpu_ratio, *rdma;
   uint32_t* cpu_bind;
   uint8_t* joint;
+  uint8_t* stat_dyn;  // per pod: 1 = a TaintToleration / NodeAffinity raw score can differ between nodes (host-built)
 };
 
 // estimatedUsedByResource (estimator/default_estimator.go:73-108)
@@ -187,6 +188,8 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   r.joint = s.joint ? s.joint[i] : 0u;
   r._pad0 = 0;
   if (r.rdma > 0) r.flags |= kPodHasGpu;
+  // a normalized score that can differ between nodes: DeviceShare (device requests), TaintToleration / NodeAffinity
+  if ((r.flags & kPodHasGpu) || s.stat_dyn[i]) r.flags |= kPodNormDyn;
   r.cpu_bind = (r.flags & KS_POD_CPU_BIND) ? ((s.cpu_bind[i] & 0x1Fu) | ((uint32_t)(r.cpu / 1000) << 8)) : 0u;
   out[i] = r;
 }
@@ -669,6 +672,29 @@ __global__ __launch_bounds__(1024) void dev_normalize_debug_kernel(int64_t n, co
   }
 }
 
+// TaintToleration (reverse) / NodeAffinity NormalizeScore = DefaultNormalizeScore(100, reverse) over the feasible
+// nodes for the debug path (one block); slot = KS_SCORE_TAINT or KS_SCORE_NODE_AFFINITY
+__global__ __launch_bounds__(1024) void stat_normalize_debug_kernel(int64_t n, const uint32_t* reasons,
+                                                                    const int32_t* raw, int64_t* scores,
+                                                                    int64_t* total, int64_t w, int32_t slot,
+                                                                    int32_t reverse) {
+  __shared__ int32_t s_max;
+  if (threadIdx.x == 0) s_max = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
+    if (!reasons[i]) atomicMax(&s_max, raw[i]);
+  __syncthreads();
+  const int64_t mx = s_max;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    if (reasons[i]) continue;
+    int64_t sc;
+    if (mx == 0) sc = reverse ? 100 : raw[i];
+    else sc = reverse ? 100 - 100 * (int64_t)raw[i] / mx : 100 * (int64_t)raw[i] / mx;
+    scores[i * KS_NUM_SCORE_PLUGINS + slot] = sc;
+    total[i] += sc * w;
+  }
+}
+
 // Reservation PreScore preferred node (scoring.go:87-96), Score (:103-122) and DefaultNormalizeScore
 // (normalize_score.go:24-52) over the feasible nodes for the debug path (one block).
 __global__ __launch_bounds__(1024) void rsv_normalize_debug_kernel(int64_t n, const uint32_t* reasons,
@@ -886,9 +912,12 @@ struct PodStage {
   void* blob = nullptr;
   int32_t cap = 0;
   PodRec* recs = nullptr;       // [cap] built by prep_pods_kernel
+  PodStat* stat = nullptr;      // [cap] TaintToleration / NodeAffinity inputs (host-built at staging)
   ks_result* results = nullptr; // [cap]
   DevPodCols cols{};            // the caller's columns in HBM
   DevPodQuota pq{};             // quota request columns (read by the commit kernel)
+  std::vector<PodStat> h_stat;  // host staging of stat (kept until the async copy has run: the stream syncs
+  std::vector<uint8_t> h_dyn;   // before the next stage_cols)
 };
 
 struct ks_ctx {
@@ -967,7 +996,8 @@ struct ks_ctx {
   DevDev* ddv = nullptr;
   bool dev_loaded = false;
   int64_t* dev_used_ckpt = nullptr;
-  unsigned long long* dev_M = nullptr;  // [64] per pass
+  unsigned long long* dev_M = nullptr;  // [3][64] per pass: normalization maxima (ks_pass.h SweepArgs.dev_M)
+  uint64_t soft_union = 0;  // TaintToleration: OR of every node's PreferNoSchedule taint bits (kPodNormDyn at staging)
   unsigned long long* dcache = nullptr;  // [64][npad] DeviceShare phase-0 results (SweepArgs.dcache)
   int64_t dcache_words = 0;
   // NodeNUMAResource cpusets (ks_cpuset.h)
@@ -1092,9 +1122,20 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
     k.monotone = 0;
     k.monotone_nd = 0;
   }
+  // upstream TaintToleration / NodeAffinity: static per (pod, node), but normalized over the feasible nodes, so a
+  // commit that makes the max-holding node infeasible changes the pod's scores elsewhere (monotone_nd covers the
+  // pods whose raw scores are 0 everywhere, kPodNormDyn)
+  k.taint = c.taint.enable_filter ? 1 : 0;
+  k.taint |= c.taint.enable_score ? 2 : 0;
+  k.taint_pw = c.taint.enable_score ? (int32_t)c.taint.plugin_weight : 0;
+  k.aff = c.affinity.enable_filter ? 1 : 0;
+  k.aff |= c.affinity.enable_score ? 2 : 0;
+  k.aff_pw = c.affinity.enable_score ? (int32_t)c.affinity.plugin_weight : 0;
+  k.stat = (k.taint | k.aff) ? 1 : 0;
+  if ((k.taint | k.aff) & 2) k.monotone = 0;
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
                              (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw +
-                             k.bal_pw) + 1);
+                             k.bal_pw + k.taint_pw + k.aff_pw) + 1);
   // a commit into a reservation can raise that node's Reservation score for later pods
   if (k.rsv) k.monotone = 0;
   if (k.rsv) k.monotone_nd = 0;
@@ -1167,12 +1208,20 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
       return KS_EUNSUPPORTED;
     }
   }
+  for (const ks_static_plugin_args* sp : {&cfg->taint, &cfg->affinity}) {
+    if (sp->enable_score && (sp->plugin_weight < 0 || sp->plugin_weight > 1000)) {
+      g_create_error = "ks_create: TaintToleration / NodeAffinity plugin weight out of range";
+      return KS_EINVAL;
+    }
+  }
   if (cfg->reservation.enable) {
     const int64_t fitla = 100 * ((cfg->fit.enable_score ? cfg->fit.plugin_weight : 0) +
                                  (cfg->loadaware.enable_score ? cfg->loadaware.plugin_weight : 0) +
                                  (cfg->numa.enable ? cfg->numa.plugin_weight : 0) +
                                  (cfg->deviceshare.enable ? cfg->deviceshare.plugin_weight : 0) +
-                                 (cfg->balanced.enable ? cfg->balanced.plugin_weight : 0));
+                                 (cfg->balanced.enable ? cfg->balanced.plugin_weight : 0) +
+                                 (cfg->taint.enable_score ? cfg->taint.plugin_weight : 0) +
+                                 (cfg->affinity.enable_score ? cfg->affinity.plugin_weight : 0));
     if (cfg->reservation.plugin_weight <= fitla || cfg->reservation.plugin_weight > ((int64_t)1 << 40) ||
         (fitla + 1) * (kRsvOrderBase + 1) >= (1 << 26)) {
       g_create_error = "ks_create: Reservation plugin weight must exceed 100 x (Fit + LoadAware weights) (ks_rsv.h ranking)";
@@ -1219,7 +1268,7 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->cursor = (int32_t*)p;
   if (dev_alloc(ctx, &p, 256) != KS_OK) goto fail;
   ctx->counters = (unsigned long long*)p;
-  if (dev_alloc(ctx, &p, kMaxBatch * 8) != KS_OK) goto fail;
+  if (dev_alloc(ctx, &p, kNormRows * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->dev_M = (unsigned long long*)p;
   *out = ctx;
   return KS_OK;
@@ -1324,6 +1373,9 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.la_bits, 4, false);
   add(&d.numa_ratio, 8, false);
   add(&d.numa_flags, 4, false);
+  add(&d.taints_hard, 8, false);
+  add(&d.taints_soft, 8, false);
+  add(&d.labels, 8, false);
 }
 
 // host source pointers in the same order as build_col_table (NULL = zeros)
@@ -1367,6 +1419,9 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(nullptr);  // la_bits: derived on device
   v.push_back(c->numa_cpu_amplification);
   v.push_back(c->numa_flags);
+  v.push_back(c->taints_hard);
+  v.push_back(c->taints_soft);
+  v.push_back(c->labels);
   return v;
 }
 
@@ -1382,6 +1437,8 @@ static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
   if (!c->alloc_milli_cpu || !c->alloc_memory || !c->allowed_pods || !c->req_milli_cpu || !c->req_memory ||
       !c->pod_count || !c->nonzero_milli_cpu || !c->nonzero_memory || !c->la_flags)
     KS_FAIL(ctx, KS_EINVAL, "ks_node_cols: required column missing");
+  for (int64_t i = 0; c->labels && i < n; ++i)
+    if (c->labels[i] & KS_LABEL_NEVER) KS_FAIL(ctx, KS_EINVAL, "node %lld: labels bit 63 (KS_LABEL_NEVER) set", (long long)i);
   const int64_t* cols64[] = {c->alloc_milli_cpu, c->alloc_memory, c->alloc_ephemeral, c->req_milli_cpu, c->req_memory,
                              c->req_ephemeral, c->nonzero_milli_cpu, c->nonzero_memory, c->la_alloc_milli_cpu,
                              c->la_alloc_memory, c->la_term_milli_cpu, c->la_term_memory, c->la_prod_term_milli_cpu,
@@ -1529,6 +1586,8 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   }
   ctx->nsc = nsc <= 0 ? 0 : (nsc <= 2 ? 2 : 4);
   ctx->kc = make_cfg(ctx->cfg, ctx->nsc);
+  ctx->soft_union = 0;
+  for (int64_t i = 0; nodes->taints_soft && i < n; ++i) ctx->soft_union |= nodes->taints_soft[i];
   build_col_table(ctx);
   size_t total = 0, mut = 0;
   for (const Col& c : ctx->cols) {
@@ -2484,6 +2543,8 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
   for (int64_t i = 0; ctx->cfg.numa.enable && rows->numa_flags && i < m; ++i)
     ctx->cpu_bind_labels |= ((rows->numa_flags[i] >> KS_NUMA_CPU_BIND_SHIFT) & 3u) != 0;
+  // (the union only grows: a stale bit only withholds the fast path from a pod)
+  for (int64_t i = 0; rows->taints_soft && i < m; ++i) ctx->soft_union |= rows->taints_soft[i];
   cores_mode(ctx);
   if (rows->numa_flags && cores_refresh(ctx) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2691,11 +2752,14 @@ static int ensure_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
   const size_t col4 = ((size_t)cap * 4 + 255) / 256 * 256;
   // stage: cpu mem eph nzcpu nzmem sc[4] la x6 gpu x3 rdma qreq[8] = 27 int64 cols; flags quota qmask rsv_class
   // cpu_bind joint(u8) = 6 x32
-  const size_t bytes = rec + res + col8 * 27 + col4 * 6;
+  const size_t pst = (size_t)cap * sizeof(PodStat);
+  const size_t bytes = rec + pst + res + col8 * 27 + col4 * 7;
   if (dev_alloc(ctx, &st.blob, bytes) != KS_OK) return KS_ENOMEM;
   char* b = (char*)st.blob;
   st.recs = (PodRec*)b;
   b += rec;
+  st.stat = (PodStat*)b;
+  b += pst;
   st.results = (ks_result*)b;
   b += res;
   DevPodCols& s = st.cols;
@@ -2719,6 +2783,8 @@ static int ensure_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
   s.rsv_class = (int32_t*)b;
   b += col4;
   s.cpu_bind = (uint32_t*)b;
+  b += col4;
+  s.stat_dyn = (uint8_t*)b;
   b += col4;
   s.joint = (uint8_t*)b;
   st.cap = cap;
@@ -2761,6 +2827,34 @@ static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t 
   else HIPCHK(ctx, hipMemsetAsync(s.rsv_class, 0xFF, (size_t)p * 4, ctx->stream));
   if (pc->cpu_bind) HIPCHK(ctx, hipMemcpyAsync(s.cpu_bind, pc->cpu_bind, (size_t)p * 4, hipMemcpyHostToDevice, ctx->stream));
   else HIPCHK(ctx, hipMemsetAsync(s.cpu_bind, 0, (size_t)p * 4, ctx->stream));
+  // TaintToleration / NodeAffinity: the pods' PodStat records and normalization flags, built here from the columns
+  // (a pod whose raw scores are 0 on every node normalizes the same under every max: not kPodNormDyn)
+  if (ctx->kc.stat) {
+    std::vector<PodStat>& hs = st.h_stat;
+    std::vector<uint8_t>& hd = st.h_dyn;
+    hs.assign((size_t)p, PodStat{});
+    hd.assign((size_t)p, 0);
+    for (int32_t i = 0; i < p; ++i) {
+      PodStat& r = hs[(size_t)i];
+      r.tol = pc->tolerated ? pc->tolerated[i] : 0;
+      r.nreq = pc->affinity_required_n ? pc->affinity_required_n[i] : 0;
+      bool dyn = (ctx->kc.taint & 2) && (ctx->soft_union & ~r.tol) != 0;
+      for (int t = 0; t < KS_AFFINITY_TERMS; ++t) {
+        r.req[t] = pc->affinity_required[t] ? pc->affinity_required[t][i] : 0;
+        r.pref[t] = pc->affinity_preferred[t] ? pc->affinity_preferred[t][i] : 0;
+        r.w[t] = pc->affinity_weight[t] ? pc->affinity_weight[t][i] : 0;
+        dyn |= (ctx->kc.aff & 2) && r.w[t] != 0;
+      }
+      hd[(size_t)i] = dyn ? 1 : 0;
+    }
+    if (p > 0) {
+      HIPCHK(ctx, hipMemcpyAsync(st.stat, hs.data(), (size_t)p * sizeof(PodStat), hipMemcpyHostToDevice, ctx->stream));
+      HIPCHK(ctx, hipMemcpyAsync(s.stat_dyn, hd.data(), (size_t)p, hipMemcpyHostToDevice, ctx->stream));
+      HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // pageable sources
+    }
+  } else {
+    HIPCHK(ctx, hipMemsetAsync(s.stat_dyn, 0, (size_t)p, ctx->stream));
+  }
   return KS_OK;
 }
 
@@ -2775,6 +2869,14 @@ static int prep_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
 }
 
 static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
+  for (int32_t i = 0; pc->affinity_required_n && i < p; ++i)
+    if (pc->affinity_required_n[i] < 0 || pc->affinity_required_n[i] > KS_AFFINITY_TERMS)
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: %d required node affinity terms (the device evaluates up to %d)", i,
+              pc->affinity_required_n[i], KS_AFFINITY_TERMS);
+  for (int t = 0; t < KS_AFFINITY_TERMS; ++t)
+    for (int32_t i = 0; pc->affinity_weight[t] && i < p; ++i)
+      if (pc->affinity_weight[t][i] < 0 || pc->affinity_weight[t][i] > 100)
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: preferred node affinity weight %d outside [0, 100]", i, pc->affinity_weight[t][i]);
   const int64_t* cols[] = {pc->req_milli_cpu, pc->req_memory, pc->req_ephemeral, pc->nonzero_milli_cpu,
                            pc->nonzero_memory, pc->la_req_cpu, pc->la_lim_cpu, pc->la_req_memory, pc->la_lim_memory,
                            pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio, pc->rdma};
@@ -2896,13 +2998,17 @@ static bool commit_qcache(const ks_ctx* ctx) {
 
 // kernel variant: 0 = Fit/LoadAware/Quota, 1 = + Reservation, 3 = + Reservation + NodeNUMAResource
 // + 8: NodeNUMAResource with NUMA topology policies (ks_numa.h)
+// (TaintToleration / NodeAffinity are normalized like DeviceShare: they run in the DeviceShare variants)
 static int kernel_feat(const ks_ctx* ctx) {
-  const int f = ctx->kc.dev ? 7 : (ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0));
+  const int f = (ctx->kc.dev || ctx->kc.stat) ? 7 : (ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0));
   return f | (ctx->kc.numa_pol ? 8 : 0);
 }
 
+// the slot device region of the commit kernel: GPU state (DeviceShare), then the TaintToleration / NodeAffinity words
+// (3 x u64 per slot, the region's last kMaxBatch * 24 B)
 static size_t dev_cache_bytes(const ks_ctx* ctx) {
-  return ctx->kc.dev ? (size_t)kDevLdsStride * (kDevTW + kDevQW) * 8 + (size_t)kMaxBatch * 4 : 0;
+  return (ctx->kc.dev ? (size_t)kDevLdsStride * (kDevTW + kDevQW) * 8 + (size_t)kMaxBatch * 4 : 0) +
+         (ctx->kc.stat ? (size_t)kMaxBatch * 24 : 0);
 }
 
 static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {
@@ -2961,6 +3067,7 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.rv = ctx->drv;
   ca.c = ctx->kc;
   ca.pods = st.recs;
+  ca.pstat = st.stat;
   ca.pq = st.pq;
   ca.q = ctx->q;
   ca.cursor = ctx->cursor;
@@ -3192,7 +3299,9 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   sa.dv = ctx->ddv;
   sa.nv = ctx->dnv;
   sa.dev_M = ctx->dev_M;
-  sa.dcache = (ctx->kc.dev && !ctx->kc.rsv && ctx->dcache_words >= (int64_t)kMaxBatch * ctx->npad) ? ctx->dcache : nullptr;
+  sa.dcache = (ctx->kc.dev && !ctx->kc.rsv && !ctx->kc.stat && ctx->dcache_words >= (int64_t)kMaxBatch * ctx->npad)
+                  ? ctx->dcache : nullptr;
+  sa.pstat = ctx->st.stat;
   sa.dstride = ctx->npad;
   sa.phase = 1;
   // One sweep launch per virtual shard (a rank's virtual shards are swept as separate chunk ranges, so the
@@ -3212,14 +3321,14 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   if (feat == 7 || feat == 15) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
     // each launch is timed on its own (the roofline is per sweep launch)
-    HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ss));
+    HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kNormRows * kMaxBatch * 8, ss));
     sa.phase = 0;
     rec(0, ss);
     sweep(sweep_blocks, ss);
     rec(0, ss);
     if (ctx->nranks > 1) {
-      const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kMaxBatch, ncclUint64, ncclMax, ctx->comm, ss);
-      if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllReduce (DeviceShare max): %s", ncclGetErrorString(r));
+      const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kNormRows * kMaxBatch, ncclUint64, ncclMax, ctx->comm, ss);
+      if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllReduce (normalization maxima): %s", ncclGetErrorString(r));
     }
     sa.phase = 1;
     rec(0, ss);
@@ -3384,7 +3493,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     if (sel_smem > 160 * 1024) KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the select kernel's LDS (%lld nodes)", (long long)ctx->n);
     e = hipFuncSetAttribute((const void*)select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_smem);
     if (e != hipSuccess) KS_FAIL(ctx, KS_EHIP, "hipFuncSetAttribute(select LDS %zu): %s", sel_smem, hipGetErrorString(e));
-    if (ctx->kc.dev && !ctx->kc.rsv && ctx->dcache_words < (int64_t)kMaxBatch * ctx->npad) {
+    if (ctx->kc.dev && !ctx->kc.rsv && !ctx->kc.stat && ctx->dcache_words < (int64_t)kMaxBatch * ctx->npad) {
       void* q = ctx->dcache;
       dev_free(q);
       ctx->dcache = nullptr;
@@ -3800,7 +3909,7 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
   if (stage_cols(ctx, ctx->est, pod, 1) != KS_OK || prep_stage(ctx, ctx->est, 1) != KS_OK) return KS_EHIP;
   const int64_t n = ctx->n;
   // the per-node outputs in a scratch buffer that lives with the context (grown, never freed per call)
-  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4) + 64;
+  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4 + 8) + 64;
   if (ctx->evbuf_bytes < bytes) {
     dev_free(ctx->evbuf);
     ctx->evbuf_bytes = 0;
@@ -3814,14 +3923,22 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
   int32_t* draw = (int32_t*)(dt + n);
   int32_t* dhi = draw + n;
   int32_t* ddraw = dhi + n;
+  int32_t* dtraw = ddraw + n;
+  int32_t* daraw = dtraw + n;
   const int threads = 256;
   const int blocks = (int)((n + threads - 1) / threads);
   if (blocks > 0) {
     HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
-                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw));
+                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw));
     if (ctx->kc.dev)
       hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,
                          ctx->cfg.deviceshare.plugin_weight);
+    if (ctx->kc.taint & 2)
+      hipLaunchKernelGGL(stat_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, dtraw, ds, dt,
+                         ctx->cfg.taint.plugin_weight, KS_SCORE_TAINT, 1);
+    if (ctx->kc.aff & 2)
+      hipLaunchKernelGGL(stat_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, daraw, ds, dt,
+                         ctx->cfg.affinity.plugin_weight, KS_SCORE_NODE_AFFINITY, 0);
     if (ctx->kc.rsv)
       hipLaunchKernelGGL(rsv_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, draw, dhi, ds, dt,
                          ctx->cfg.reservation.plugin_weight);
@@ -3985,7 +4102,7 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
   HIPCHK(ctx, hipMemcpyAsync(ctx->cand_top, &h.top, 8, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemcpyAsync(ctx->cand_second, &h.top, 8, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipMemsetAsync(ctx->cursor, 0, 4, ctx->stream));
-  HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kMaxBatch * 8, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kNormRows * kMaxBatch * 8, ctx->stream));
   if (ctx->cpuset_list) {
     HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_out, 0, sizeof(CpuSet), ctx->stream));

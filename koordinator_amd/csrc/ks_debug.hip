@@ -11,7 +11,7 @@ namespace ks {
 template <int NSC>
 __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n,
                                   uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
-                                  int32_t* draw) {
+                                  int32_t* draw, const PodStat* pstat, int32_t* traw, int32_t* araw) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   NodeReg<NSC> r;
@@ -21,6 +21,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   EvalOut o = eval_full<NSC, true, false, 15>(
       c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
       [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
+  if (c.stat) stat_eval(c, *pstat, d.taints_hard[i], d.taints_soft[i], d.labels[i], o);
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
@@ -34,19 +35,24 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   raw[i] = ro.raw;
   hiord[i] = ro.hiord;
   draw[i] = o.dev_raw;
+  traw[i] = o.traw;
+  araw[i] = o.araw;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TAINT] = 0;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = 0;
 }
 
 
 hipError_t launch_eval_debug(int nsc, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,
                              const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
-                             int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw) {
+                             int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw,
+                             const PodStat* pstat, int32_t* traw, int32_t* araw) {
   if (nsc == 0)
-    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw);
+    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw);
   else if (nsc == 2)
-    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw);
+    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw);
   else
-    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw);
+    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw);
   return hipGetLastError();
 }
 

@@ -42,6 +42,9 @@ constexpr uint32_t kPodHasGpu = 0x400u;
 constexpr uint32_t kPodGpuReq = 0x800u;
 // internal pod flag: a score-term request >= kBigReq: the pod's terms take the int64 path
 constexpr uint32_t kPodBigReq = 0x1000u;
+// internal pod flag: a normalized score (DeviceShare, TaintToleration, NodeAffinity) can differ between nodes for the
+// pod, so a commit may change its normalization max (the monotone fast path does not hold for it)
+constexpr uint32_t kPodNormDyn = 0x2000u;
 
 // la_bits (prep_nodes_kernel output)
 constexpr uint32_t kLaZeroScore = 0x1u;     // Score returns 0 (no NodeMetric / expired)
@@ -72,6 +75,9 @@ struct Cfg {
   int32_t monotone_nd;  // monotone for pods without device requests (DeviceShare skips them: no normalization max)
   int32_t cores;        // node CPU bind policies or required pod policies: the per-node core counts are read
   int32_t bal, bal_pw;  // upstream NodeResourcesBalancedAllocation: KS_BAL_* resources (0 = off), plugin weight
+  int32_t taint, taint_pw;  // upstream TaintToleration: bit 0 Filter, bit 1 Score; plugin weight
+  int32_t aff, aff_pw;      // upstream NodeAffinity: bit 0 Filter, bit 1 Score; plugin weight
+  int32_t stat;             // taint | aff: the dictionary-bit plugins are on (kernel variant FEAT & 4, PodStat read)
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -96,6 +102,7 @@ struct DevNodes {
   int64_t *numa_off;        // derived: Amplify(cpuset milli, ratio) - cpuset milli (ratio > 1), else 0
   int32_t *cpu_free;        // available CPUs for cpuset pods (ks_cpuset.h), -1 = no valid CPU topology
   uint32_t *cpu_cores;      // derived: CoresWord (fully available / partly available cores, CPUsPerCore, CPU bind label)
+  uint64_t *taints_hard, *taints_soft, *labels;  // TaintToleration / NodeAffinity dictionary bits (static per node)
 };
 
 // Per-node word of the required CPU bind policies (Cfg.cores): the cores whose CPUs are all available
@@ -399,7 +406,65 @@ struct EvalOut {
   int32_t hi;              // Reservation ranking component (ks_rsv.h)
   int32_t bal;             // NodeResourcesBalancedAllocation score
   uint32_t numa_rs;        // NodeNUMAResource reasons of the policy-None checks (before the policy path)
+  int32_t traw, araw;      // TaintToleration / NodeAffinity raw scores (normalized in key_total)
 };
+
+// TaintToleration / NodeAffinity inputs of one pod over the context's dictionaries (ks_static_plugin_args), built by
+// the host at staging; read wave-uniform (scalar loads) by the kernels of the FEAT & 4 variants.
+struct __attribute__((aligned(16))) PodStat {
+  uint64_t tol;                       // dictionary taints some toleration tolerates
+  uint64_t req[KS_AFFINITY_TERMS];    // required terms (nodeSelector folded in); KS_LABEL_NEVER = an empty term
+  uint64_t pref[KS_AFFINITY_TERMS];   // preferred terms
+  int32_t w[KS_AFFINITY_TERMS];       // preferred weights (0 = unused)
+  int32_t nreq;                       // required terms (0 = no required node affinity / selector)
+  int32_t _pad;
+};
+static_assert(sizeof(PodStat) == 96, "PodStat layout");
+
+__device__ __forceinline__ PodStat load_stat_uniform(const PodStat* p) {
+  PodStat r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) int64_t* ConstWords;
+  const ConstWords src = (ConstWords)p;
+  int64_t* dst = reinterpret_cast<int64_t*>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(PodStat) / 8); ++i) dst[i] = src[i];
+#else
+  r = *p;
+#endif
+  return r;
+}
+
+// Upstream TaintToleration and NodeAffinity (kube-scheduler v1.24.15, plugins/tainttoleration/taint_toleration.go and
+// plugins/nodeaffinity/node_affinity.go; not on disk: parity unpinned, restated in oracle/static_plugins_ref.py) on
+// the node's dictionary words: Filter -- an untolerated NoSchedule / NoExecute taint (FindMatchingUntoleratedTaint),
+// no required term whose requirement bits the node has (RequiredNodeAffinity.Match); Score raw values -- untolerated
+// PreferNoSchedule taints (countIntolerableTaintsPreferNoSchedule) and the weights of the matching preferred terms.
+// Every node is evaluated the same way whatever other Filters said (reasons are OR-ed).
+__device__ __forceinline__ void stat_eval(const Cfg& c, const PodStat& s, uint64_t hard, uint64_t soft, uint64_t labels,
+                                          EvalOut& o) {
+  if ((c.taint & 1) && (hard & ~s.tol)) o.reasons |= KS_R_TAINT;
+  if ((c.aff & 1) && s.nreq > 0) {
+    bool ok = false;
+#pragma unroll
+    for (int t = 0; t < KS_AFFINITY_TERMS; ++t) ok |= t < s.nreq && (labels & s.req[t]) == s.req[t];
+    if (!ok) o.reasons |= KS_R_NODE_AFFINITY;
+  }
+  o.traw = (c.taint & 2) ? __builtin_popcountll(soft & ~s.tol) : 0;
+  int32_t a = 0;
+  if (c.aff & 2) {
+#pragma unroll
+    for (int t = 0; t < KS_AFFINITY_TERMS; ++t) a += (s.w[t] != 0 && (labels & s.pref[t]) == s.pref[t]) ? s.w[t] : 0;
+  }
+  o.araw = a;
+}
+
+// Normalization maxima of one pod: DeviceShare, TaintToleration, NodeAffinity (DefaultNormalizeScore over the feasible
+// nodes, normalize_score.go:24-52)
+struct NormM {
+  int32_t dev, taint, aff;
+};
+constexpr int kNormRows = 3;  // rows of the per-pass maxima table (SweepArgs.dev_M)
 
 // Upstream NodeResourcesBalancedAllocation (kube-scheduler v1.24 noderesources/balanced_allocation.go,
 // balancedResourceScorer with useRequested = true): fraction = float64(Requested + pod request) / float64(Allocatable)
@@ -468,6 +533,8 @@ __device__ __forceinline__ EvalOut eval_pod_node(const Cfg& c, const PodRec& p, 
   o.la = 0;
   o.numa = 0;
   o.dev_raw = 0;
+  o.traw = 0;
+  o.araw = 0;
   o.hi = 0;
   o.numa_rs = 0;
   o.bal = 0;

@@ -30,8 +30,11 @@ struct SweepArgs {
   const DevRsv* __restrict__ rv;
   const DevDev* __restrict__ dv;
   const DevNuma* __restrict__ nv;
-  unsigned long long* dev_M;  // [64] DeviceShare: (max raw << 32) | ~witness node per pod of the pass
-  int32_t phase;              // 0: reduce dev_M only (DeviceShare), 1: chunk keys
+  // [3][64] normalization maxima per pod of the pass: (max raw << 32) | ~witness node of DeviceShare, TaintToleration,
+  // NodeAffinity (kNormPlugins rows)
+  unsigned long long* dev_M;
+  int32_t phase;              // 0: reduce dev_M only (normalized plugins), 1: chunk keys
+  const PodStat* __restrict__ pstat;  // TaintToleration / NodeAffinity per pod (Cfg.stat), queue order
   // DeviceShare without Reservation: phase 0 keeps each (pod, node)'s (feasible, Fit + LoadAware + NUMA
   // total, DeviceShare raw) here and phase 1 only applies the normalization ([64][dstride]); NULL = re-evaluate
   unsigned long long* dcache;
@@ -112,7 +115,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       EvalOut o = eval_full<NSC, false, true, FEAT>(
           a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
           [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
-      const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, 0) + 1) << 6) | (uint32_t)(63 - lane));
+      const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, NormM{0, 0, 0}) + 1) << 6) | (uint32_t)(63 - lane));
       t.x = wave_max_u32(key);
       t.y = wave_max_u32(key == t.x ? 0u : key);
       if (lane == 0) a.list_t[p * K + e] = t;
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
         EvalOut o{};
         o.total = (int32_t)(uint32_t)e;
         o.dev_raw = (int32_t)((e >> 32) & 0xFFFFull);
-        const int32_t M = (int32_t)(a.dev_M[p] >> 32);
+        const NormM M{(int32_t)(a.dev_M[p] >> 32), 0, 0};  // (no dcache with the dictionary-bit plugins)
         const uint32_t key = (e >> 63) ? (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane)) : 0u;
         const uint32_t m1 = wave_max_u32(key);
         const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
@@ -156,9 +159,15 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       continue;
     }
     NodeReg<NSC> r;
+    uint64_t st_hard = 0, st_soft = 0, st_lab = 0;  // TaintToleration / NodeAffinity words (FEAT & 4 variants)
     {
       const DevNodes d = *a.dn;
       load_node<NSC>(a.c, d, node, node < a.n, r);
+      if ((FEAT & 4) && a.c.stat && node < a.n) {
+        st_hard = gld(d.taints_hard + node);
+        st_soft = gld(d.taints_soft + node);
+        st_lab = gld(d.labels + node);
+      }
     }
     const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
     uint32_t best = 0, second = 0;
@@ -167,18 +176,33 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       EvalOut o = eval_full<NSC, false, true, FEAT>(
           a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
           [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
+      if ((FEAT & 4) && a.c.stat) stat_eval(a.c, load_stat_uniform(a.pstat + cursor + p), st_hard, st_soft, st_lab, o);
       if ((FEAT & 4) && a.phase == 0) {
-        // DeviceShare normalization max over the feasible nodes, witness = lowest index holding it
-        const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | (0xFFFFFFFFull - (uint64_t)node));
+        // normalization maxima over the feasible nodes, witness = lowest index holding each
+        const uint64_t wit = 0xFFFFFFFFull - (uint64_t)node;
+        const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | wit);
         const uint64_t m = wave_max_u64(mk);
         if (lane == 0 && m) atomicMax(a.dev_M + p, (unsigned long long)m);
+        if (a.c.stat) {
+          const uint64_t mt = wave_max_u64(o.reasons ? 0ull : (((uint64_t)(uint32_t)o.traw << 32) | wit));
+          const uint64_t ma = wave_max_u64(o.reasons ? 0ull : (((uint64_t)(uint32_t)o.araw << 32) | wit));
+          if (lane == 0 && mt) atomicMax(a.dev_M + kMaxBatch + p, (unsigned long long)mt);
+          if (lane == 0 && ma) atomicMax(a.dev_M + 2 * kMaxBatch + p, (unsigned long long)ma);
+        }
         if (a.dcache)
           a.dcache[(size_t)p * a.dstride + node] =
               (node < a.n && !o.reasons) ? ((1ull << 63) | ((unsigned long long)(uint32_t)o.dev_raw << 32) | (uint32_t)o.total)
                                          : 0ull;
         continue;
       }
-      const int32_t M = (FEAT & 4) ? (int32_t)(a.dev_M[p] >> 32) : 0;
+      NormM M{0, 0, 0};
+      if (FEAT & 4) {
+        M.dev = (int32_t)(a.dev_M[p] >> 32);
+        if (a.c.stat) {
+          M.taint = (int32_t)(a.dev_M[kMaxBatch + p] >> 32);
+          M.aff = (int32_t)(a.dev_M[2 * kMaxBatch + p] >> 32);
+        }
+      }
       const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane));
       const uint32_t m1 = wave_max_u32(key);
       const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
@@ -268,7 +292,8 @@ struct CommitArgs {
   const DevRsv* __restrict__ rv;
   const DevDev* __restrict__ dv;
   const DevNuma* __restrict__ nv;
-  const unsigned long long* __restrict__ dev_M;  // [64] DeviceShare normalization max + witness (sweep phase 0)
+  const unsigned long long* __restrict__ dev_M;  // [3][64] normalization maxima + witnesses (sweep phase 0)
+  const PodStat* __restrict__ pstat;             // TaintToleration / NodeAffinity per pod (Cfg.stat), queue order
   Cfg c;
   const PodRec* __restrict__ pods;
   DevPodQuota pq;
@@ -528,17 +553,25 @@ __device__ __forceinline__ Cands resolve_cands(const uint32_t* cand_chunk, const
 // covered by the slot evaluation.
 template <int NSC, int FEAT>
 __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const Cfg& cfg, const PodRec& pod,
-                                                     int64_t chunk, uint64_t touched_mask, int32_t M) {
+                                                     int64_t chunk, uint64_t touched_mask, const NormM& M,
+                                                     const PodStat* ps) {
   const int lane = threadIdx.x & 63;
   const int64_t node = chunk * 64 + lane;
   NodeReg<NSC> r;
+  uint64_t sh = 0, ss = 0, sl = 0;
   {
     const DevNodes d = *a.dn;
     load_node<NSC>(cfg, d, node, node < a.n, r);
+    if ((FEAT & 4) && cfg.stat && node < a.n) {
+      sh = gld(d.taints_hard + node);
+      ss = gld(d.taints_soft + node);
+      sl = gld(d.labels + node);
+    }
   }
   EvalOut o = eval_full<NSC, false, false, FEAT>(
       cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
       [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
+  if ((FEAT & 4) && cfg.stat) stat_eval(cfg, *ps, sh, ss, sl, o);
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
   return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
 }
@@ -629,6 +662,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   int64_t* sdev_use = sdev_tot + kDevLdsStride * DW;
   int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kDevLdsStride * DU);
   int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
+  // per slot: the node's TaintToleration / NodeAffinity words (hard, soft, labels): the last kMaxBatch * 24 B of the
+  // slot device region (dev_cache_bytes)
+  uint64_t* sstat = reinterpret_cast<uint64_t*>(smem_raw + lay.sdev + a.dev_bytes - (size_t)kMaxBatch * 24);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -699,13 +735,17 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
   int32_t my_cnt = 0, my_quota = -1;
   uint32_t my_flags = 0, my_pmask = 0;
-  uint64_t my_bound = 0, my_top = 0, my_devM = 0, my_second = 0;
+  uint64_t my_bound = 0, my_top = 0, my_devM = 0, my_second = 0, my_tM = 0, my_aM = 0;
   if (tid < 64 && lane < np) {
     my_cnt = a.cand_count[lane];
     my_bound = a.cand_bound[lane];
     my_top = a.cand_top[lane];
     if (FEAT == 0) my_second = a.cand_second[lane];
     if (DEV) my_devM = a.dev_M[lane];
+    if (DEV && a.c.stat) {
+      my_tM = a.dev_M[kMaxBatch + lane];
+      my_aM = a.dev_M[2 * kMaxBatch + lane];
+    }
     my_pmask = a.pq.mask[cursor0 + lane];
     my_quota = a.pods[cursor0 + lane].quota;
     my_flags = a.pods[cursor0 + lane].flags;
@@ -786,7 +826,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   auto lookahead = [&](int32_t j) {
     // the fast path also holds for a pod without device requests when only DeviceShare's normalization
     // max made the profile non-monotone (its DeviceShare score is 0 on every node)
-    const bool mono = monotone || (cfg.monotone_nd && !(__builtin_amdgcn_readlane(my_flags, j) & kPodHasGpu));
+    const bool mono = monotone || (cfg.monotone_nd && !(__builtin_amdgcn_readlane(my_flags, j) & kPodNormDyn));
     const uint64_t top = mono ? readlane64(my_top, j) : 0ull;
     const int32_t tn = top ? (int32_t)gkey_node(top) : 0;
     if (QC) {
@@ -857,7 +897,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     }
     {
     uint64_t best;
-    int32_t Muse = 0;  // DeviceShare normalization max used for this pod
+    NormM Muse{0, 0, 0};  // normalization maxima used for this pod
+    PodStat pst{};        // TaintToleration / NodeAffinity inputs (Cfg.stat)
+    if (DEV && cfg.stat) pst = load_stat_uniform(a.pstat + cursor0 + j);
     if (cj.fast) {
       best = cj.umax;  // the snapshot-best node is untouched: commits only lower keys, so it wins
       ++fast;
@@ -897,31 +939,36 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
             },
             [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
             [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
+        if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[3 * lane], sstat[3 * lane + 1], sstat[3 * lane + 2], o);
         feas = o.reasons == 0;
         if ((FEAT & 2) && cfg.cores && (cw & kCoresDirty) && feas)
           unk = ((pod.flags & KS_POD_CPU_BIND) && (pod.cpu_bind & KS_CPU_BIND_REQUIRED)) ||
                 (cores_label(cw) != 0 && pod.cpu > 0);
       }
-      if ((FEAT & 2) && DEV && cfg.dev && cfg.cores && __ballot(unk)) {
-        processed = j;  // DeviceShare's normalization max over the feasible nodes would depend on it
+      if ((FEAT & 2) && DEV && (cfg.dev || cfg.stat) && cfg.cores && __ballot(unk)) {
+        processed = j;  // a normalization max over the feasible nodes would depend on it
         break;
       }
-      if (DEV && cfg.dev) {
-        // DeviceShare normalization: the untouched nodes' max is the sweep's M while its witness is
-        // untouched; the touched nodes are current.  If the pod's max changes, cut the pass here.
-        const uint64_t mk = readlane64(my_devM, j);
-        const int32_t Msw = (int32_t)(mk >> 32);
-        const int32_t Mt = (int32_t)wave_max_u32(feas ? (uint32_t)o.dev_raw + 1u : 0u) - 1;
-        if (mk == 0) {
-          Muse = Mt < 0 ? 0 : Mt;  // no untouched node is feasible: only the touched ones compete
-        } else {
+      if (DEV && (cfg.dev || cfg.stat) && (pod.flags & kPodNormDyn)) {
+        // Normalization (DeviceShare, TaintToleration, NodeAffinity): the untouched nodes' max is the sweep's M
+        // while its witness is untouched; the touched nodes are current.  If a pod's max changes, cut the pass
+        // here.  (A pod without kPodNormDyn has raw 0 everywhere: every M normalizes it the same.)
+        bool cut = false;
+        auto norm1 = [&](uint64_t mk, int32_t raw) -> int32_t {
+          const int32_t Msw = (int32_t)(mk >> 32);
+          const int32_t Mt = (int32_t)wave_max_u32(feas ? (uint32_t)raw + 1u : 0u) - 1;
+          if (mk == 0) return Mt < 0 ? 0 : Mt;  // no untouched node is feasible: only the touched ones compete
           const int64_t wn = (int64_t)(0xFFFFFFFFull - (mk & 0xFFFFFFFFull));
           const bool wt = ((touched[wn >> 6] >> (wn & 63)) & 1ull) != 0;
-          if (wt ? (Mt != Msw) : (Mt > Msw)) {
-            processed = j;
-            break;
-          }
-          Muse = Msw;
+          if (wt ? (Mt != Msw) : (Mt > Msw)) cut = true;
+          return Msw;
+        };
+        if (cfg.dev) Muse.dev = norm1(readlane64(my_devM, j), o.dev_raw);
+        if (cfg.taint & 2) Muse.taint = norm1(readlane64(my_tM, j), o.traw);
+        if (cfg.aff & 2) Muse.aff = norm1(readlane64(my_aM, j), o.araw);
+        if (cut) {
+          processed = j;
+          break;
         }
       }
       if (feas) key_mod = gkey(key_total(cfg, o, Muse), snode);
@@ -932,7 +979,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         const uint64_t kmax = wave_max_u64(((need >> lane) & 1ull) ? cj.ub : 0ull);
         const int sel = __ffsll((long long)__ballot(((need >> lane) & 1ull) && cj.ub == kmax)) - 1;
         const int64_t c = (int64_t)(uint32_t)__shfl((int)cj.chunk, sel, 64);
-        const uint64_t v = rescan_untouched<NSC, FEAT>(a, cfg, pod, c, touched[c], Muse);
+        const uint64_t v = rescan_untouched<NSC, FEAT>(a, cfg, pod, c, touched[c], Muse, &pst);
         ++rescans;
         best = umax64(best, v);
         need &= ~(1ull << sel);
@@ -1039,6 +1086,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
               ((int64_t)gld(nv.present + node) << 32);
         if (lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = v;
       }
+      if (DEV && cfg.stat) {
+        const DevNodes d = *a.dn;
+        const uint64_t* col = lane == 0 ? d.taints_hard : (lane == 1 ? d.taints_soft : d.labels);
+        if (lane < 3) sstat[3 * s + lane] = gld(col + node);
+      }
       if (DEV && cfg.dev) {
         // the node's device totals + topology / used / present flag into LDS (lane = word)
         const DevDev& dv = *a.dv;
@@ -1136,11 +1188,12 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         rsv_apply<NSC>(nr, dl, 1);
         EvalOut e2 = eval_pod_node<NSC, false>(cfg, pod, nr);
         if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
-        fitla_pref = e2.total;
         if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
           const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0});
-          fitla_pref += cfg.dev_pw * (Muse == 0 ? dd.raw : small_div(100 * dd.raw, Muse));
+          e2.dev_raw = dd.raw;
         }
+        if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[3 * s], sstat[3 * s + 1], sstat[3 * s + 2], e2);
+        fitla_pref = e2.total + norm_terms(cfg, e2, Muse);
       }
       int64_t dd = 0;
       if (nom >= 0) {

@@ -290,7 +290,7 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
 // (the Cfg flags switch them at run time).  devv() / numav() return the node's device view (ks_dev.h) and NUMA
 // view (ks_numa.h).  Filter order as in the profile: Fit, LoadAware, NodeNUMAResource (on a node with a NUMA
 // topology policy its topology-manager Admit, whose affinity then restricts DeviceShare), DeviceShare,
-// Reservation.  The key total is key_total(c, o, M) with M the pod's DeviceShare normalization max.
+// Reservation.  The key total is key_total(c, o, M) with M the pod's normalization maxima (NormM).
 template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, typename H>
 __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& devv,
                                              H&& numav, RsvOut* info = nullptr) {
@@ -361,13 +361,21 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
   return o;
 }
 
-// Key total of a feasible node: Fit + LoadAware + NUMA + DeviceShare normalized with the pod's max M,
+// Key total of a feasible node: Fit + LoadAware + NUMA + the normalized plugins with the pod's maxima M,
 // then the Reservation ranking.  The preferred node is the lowest INDEX among equal order labels,
 // whatever its other scores: ordered nodes rank by hi alone (ties to the lower index through the
 // key's node bits).
-__device__ __forceinline__ int32_t key_total(const Cfg& c, const EvalOut& o, int32_t M) {
-  int32_t t = o.total;
-  if (c.dev) t += c.dev_pw * (M == 0 ? o.dev_raw : small_div(100 * o.dev_raw, M));
+__device__ __forceinline__ int32_t norm_terms(const Cfg& c, const EvalOut& o, const NormM& M) {
+  int32_t t = 0;
+  if (c.dev) t += c.dev_pw * (M.dev == 0 ? o.dev_raw : small_div(100 * o.dev_raw, M.dev));
+  // TaintToleration: DefaultNormalizeScore(100, reverse = true); NodeAffinity: DefaultNormalizeScore(100)
+  if (c.taint & 2) t += c.taint_pw * (M.taint == 0 ? 100 : 100 - small_div(100 * o.traw, M.taint));
+  if (c.aff & 2) t += c.aff_pw * (M.aff == 0 ? o.araw : small_div(100 * o.araw, M.aff));
+  return t;
+}
+
+__device__ __forceinline__ int32_t key_total(const Cfg& c, const EvalOut& o, const NormM& M) {
+  int32_t t = o.total + norm_terms(c, o, M);
   if (c.rsv) t = o.hi >= kRsvOrderBase ? o.hi * c.rsv_F : t + o.hi * c.rsv_F;
   return t;
 }

@@ -521,3 +521,92 @@ def c5(seed: int = SEED, n_nodes: int = 100_000, n_pods: int = 1_000_000, **kw) 
     nodes = make_nodes(n_nodes, rng)
     pods = make_pods(n_pods, rng)
     return Workload("C5", koord_profile(**kw), nodes, pods, None)
+
+
+def static_specs(n_nodes: int, n_pods: int, rng: np.random.Generator):
+    """Node labels / taints and pod tolerations / node selectors / node affinity for the upstream TaintToleration and
+    NodeAffinity plugins (static_plugins): 4 zones, 3 instance types, integer rack labels (Gt / Lt), GPU labels;
+    NoSchedule / NoExecute / PreferNoSchedule taints on part of the nodes; pods with Equal / Exists / wildcard
+    tolerations, nodeSelectors, required terms (In, NotIn, Gt, matchFields) and weighted preferred terms."""
+    from .static_plugins import (NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, FIELD_NAME, NodeSpec,
+                                 PodAffinitySpec, Requirement, Taint, Term, Toleration)
+    zones = ["zone-a", "zone-b", "zone-c", "zone-d"]
+    types = ["m.large", "m.xlarge", "c.2xlarge"]
+    nodes = []
+    for i in range(n_nodes):
+        lab = {"topology.kubernetes.io/zone": zones[rng.integers(0, 4)],
+               "node.kubernetes.io/instance-type": types[rng.integers(0, 3)],
+               "rack": str(int(rng.integers(0, 20)))}
+        if rng.random() < 0.1:
+            lab["accelerator"] = "mi355x"
+        taints = []
+        u = rng.random()
+        if u < 0.08:
+            taints.append(Taint("dedicated", "infra", NO_SCHEDULE))
+        elif u < 0.12:
+            taints.append(Taint("maintenance", "", NO_EXECUTE))
+        if rng.random() < 0.25:
+            taints.append(Taint("spot", "true", PREFER_NO_SCHEDULE))
+        if rng.random() < 0.15:
+            taints.append(Taint("noisy", "", PREFER_NO_SCHEDULE))
+        nodes.append(NodeSpec(f"node-{i}", lab, taints))
+    pods = []
+    for i in range(n_pods):
+        tol = []
+        if rng.random() < 0.3:
+            tol.append(Toleration("dedicated", "Equal", "infra", NO_SCHEDULE))
+        if rng.random() < 0.05:
+            tol.append(Toleration("", "Exists"))  # tolerates everything
+        if rng.random() < 0.4:
+            tol.append(Toleration("spot", "Equal", "true", rng.choice(["", PREFER_NO_SCHEDULE])))
+        if rng.random() < 0.1:
+            tol.append(Toleration("noisy", "Exists", "", PREFER_NO_SCHEDULE))
+        sel = {}
+        if rng.random() < 0.15:
+            sel["topology.kubernetes.io/zone"] = zones[rng.integers(0, 4)]
+        req = None
+        u = rng.random()
+        if u < 0.15:
+            z = tuple(sorted(rng.choice(zones, 2, replace=False)))
+            req = [Term([Requirement("topology.kubernetes.io/zone", "In", z)]),
+                   Term([Requirement("rack", "Gt", (str(int(rng.integers(8, 16))),))])]
+        elif u < 0.2:
+            req = [Term([Requirement("node.kubernetes.io/instance-type", "NotIn", (types[rng.integers(0, 3)],)),
+                         Requirement("accelerator", "DoesNotExist")])]
+        elif u < 0.21:
+            req = [Term([Requirement(FIELD_NAME, "NotIn", (f"node-{int(rng.integers(0, n_nodes))}",), field=True)])]
+        pref = []
+        if rng.random() < 0.4:
+            pref.append((int(rng.integers(1, 101)), Term([Requirement("topology.kubernetes.io/zone", "In",
+                                                                      (zones[rng.integers(0, 4)],))])))
+            if rng.random() < 0.5:
+                pref.append((int(rng.integers(1, 101)), Term([Requirement("rack", "Lt", ("5",))])))
+            if rng.random() < 0.3:
+                pref.append((int(rng.integers(1, 101)), Term([Requirement("accelerator", "Exists")])))
+        pods.append(PodAffinitySpec(tol, sel, req, pref))
+    return nodes, pods
+
+
+def with_static_plugins(w: Workload, seed: int = SEED + 7, weight_taint: int = 1, weight_affinity: int = 1) -> Workload:
+    """The workload with upstream TaintToleration and NodeAffinity switched on and random specs compiled in."""
+    from .static_plugins import compile_cluster
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nspec, pspec = static_specs(w.nodes.n, w.pods.n, rng)
+    compile_cluster(nspec, pspec, w.nodes, w.pods)
+    w.profile.taint_toleration = True
+    w.profile.taint_toleration_weight = weight_taint
+    w.profile.node_affinity = True
+    w.profile.node_affinity_weight = weight_affinity
+    w.specs = (nspec, pspec)
+    return w
+
+
+def c2_default(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, **kw) -> Workload:
+    """C2 under the v1beta2 default profile's upstream plugins as well: NodeResourcesBalancedAllocation,
+    TaintToleration and NodeAffinity (weight 1 each) next to Fit + LoadAware + ElasticQuota."""
+    from .config import NodeResourcesBalancedAllocationArgs
+    w = c2(seed=seed, n_nodes=n_nodes, n_pods=n_pods, **kw)
+    w.profile.balanced = NodeResourcesBalancedAllocationArgs()
+    w = with_static_plugins(w)
+    w.name = "C2-default"
+    return w

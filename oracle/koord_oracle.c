@@ -117,6 +117,7 @@ typedef struct {
   double *numa_ratio;
   int32_t *numa_cpus;
   uint32_t *numa_flags;
+  uint64_t *taints_hard, *taints_soft, *labels; /* TaintToleration / NodeAffinity dictionary bits (ks_config.taint) */
 } ko_nodes;
 
 typedef struct {
@@ -186,6 +187,8 @@ typedef struct ko_sched {
   int64_t *rord;    /* per node: findMostPreferredReservationByOrder over matched (0 = none) */
   ko_dev dv;
   int64_t *draw;    /* per node: DeviceShare raw score */
+  int64_t *traw;    /* per node: TaintToleration raw score (untolerated PreferNoSchedule taints) */
+  int64_t *araw;    /* per node: NodeAffinity raw score (sum of the matching preferred terms' weights) */
   /* NodeNUMAResource cpusets: topologies, per node topology / allocated / exclusive policy / reserved */
   int cpu_loaded;
   int32_t ntopo;
@@ -227,6 +230,10 @@ typedef struct {
   int32_t needed; /* numCPUsNeeded */
   uint32_t bind_rs;  /* per node: ErrInvalidRequestedCPUs of requestCPUBind (util.go:115-118) */
   int bind_conflict; /* per node: ErrCPUBindPolicyConflict (plugin.go:310-312) */
+  uint64_t tol;      /* TaintToleration: dictionary taints some toleration tolerates */
+  int32_t nreq;      /* NodeAffinity: required terms (0 = none) */
+  uint64_t req[KS_AFFINITY_TERMS], pref[KS_AFFINITY_TERMS];
+  int32_t w[KS_AFFINITY_TERMS];
 } ko_pod;
 
 /* NodeInfo values the Fit plugin reads, after the Reservation restore */
@@ -271,6 +278,41 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
     p->bind = pc->cpu_bind[i];
     p->needed = (int32_t)(p->cpu / 1000);
   }
+  p->tol = pc->tolerated ? pc->tolerated[i] : 0;
+  p->nreq = pc->affinity_required_n ? pc->affinity_required_n[i] : 0;
+  for (int t = 0; t < KS_AFFINITY_TERMS; t++) {
+    p->req[t] = pc->affinity_required[t] ? pc->affinity_required[t][i] : 0;
+    p->pref[t] = pc->affinity_preferred[t] ? pc->affinity_preferred[t][i] : 0;
+    p->w[t] = pc->affinity_weight[t] ? pc->affinity_weight[t][i] : 0;
+  }
+}
+
+/* Upstream TaintToleration (kube-scheduler v1.24.15 plugins/tainttoleration/taint_toleration.go, not on disk: parity
+ * unpinned) and NodeAffinity (plugins/nodeaffinity/node_affinity.go) over the dictionary bits the host compiled
+ * (koordinator_amd/static_plugins.py; restated on raw taints / labels by oracle/static_plugins_ref.py):
+ * TaintToleration Filter: FindMatchingUntoleratedTaint over the NoSchedule / NoExecute taints; NodeAffinity Filter:
+ * RequiredNodeAffinity.Match (nodeSelector ANDed into each required term, OR over the terms).  Returns KS_R_* bits. */
+static uint32_t static_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
+  uint32_t r = 0;
+  if (s->cfg.taint.enable_filter && (s->nd.taints_hard[n] & ~p->tol)) r |= KS_R_TAINT;
+  if (s->cfg.affinity.enable_filter && p->nreq > 0) {
+    int ok = 0;
+    for (int t = 0; t < p->nreq && t < KS_AFFINITY_TERMS; t++)
+      if ((s->nd.labels[n] & p->req[t]) == p->req[t]) ok = 1;
+    if (!ok) r |= KS_R_NODE_AFFINITY;
+  }
+  return r;
+}
+
+/* TaintToleration Score: countIntolerableTaintsPreferNoSchedule; NodeAffinity Score: the weights of the matching
+ * preferred terms (weight 0 terms are dropped by NewPreferredSchedulingTerms) */
+static void static_raw(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *traw, int64_t *araw) {
+  *traw = 0;
+  *araw = 0;
+  if (s->cfg.taint.enable_score) *traw = __builtin_popcountll(s->nd.taints_soft[n] & ~p->tol);
+  if (s->cfg.affinity.enable_score)
+    for (int t = 0; t < KS_AFFINITY_TERMS; t++)
+      if (p->w[t] != 0 && (s->nd.labels[n] & p->pref[t]) == p->pref[t]) *araw += p->w[t];
 }
 
 static int64_t pod_dim(const ko_pod *p, int d) { return d == 0 ? p->cpu : d == 1 ? p->mem : d == 2 ? p->eph : p->sc[d - 3]; }
@@ -1809,6 +1851,9 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   b += nn * 4;
   TAKE32(numa_cpus);
   s->nd.numa_ratio = (double *)calloc(nn, 8);
+  s->nd.taints_hard = (uint64_t *)calloc(nn, 8);
+  s->nd.taints_soft = (uint64_t *)calloc(nn, 8);
+  s->nd.labels = (uint64_t *)calloc(nn, 8);
 #undef TAKE64
 #undef TAKE32
 #define CP64(dst, src) do { if (src) memcpy(s->nd.dst, src, (size_t)n * 8); } while (0)
@@ -1831,6 +1876,9 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   CP32(numa_cpus, nc->numa_cpuset_cpus);
   CP32(numa_flags, (const int32_t *)nc->numa_flags);
   if (nc->numa_cpu_amplification) memcpy(s->nd.numa_ratio, nc->numa_cpu_amplification, (size_t)n * 8);
+  if (nc->taints_hard) memcpy(s->nd.taints_hard, nc->taints_hard, (size_t)n * 8);
+  if (nc->taints_soft) memcpy(s->nd.taints_soft, nc->taints_soft, (size_t)n * 8);
+  if (nc->labels) memcpy(s->nd.labels, nc->labels, (size_t)n * 8);
 #undef CP64
 #undef CP32
   s->feasible = (uint8_t *)calloc(nn, 1);
@@ -1839,6 +1887,8 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   s->rraw = (int64_t *)calloc(nn, 8);
   s->rord = (int64_t *)calloc(nn, 8);
   s->draw = (int64_t *)calloc(nn, 8);
+  s->traw = (int64_t *)calloc(nn, 8);
+  s->araw = (int64_t *)calloc(nn, 8);
   s->rv.beg = (int32_t *)calloc(nn + 1, 4);
   s->nthreads = nthreads < 1 ? 1 : nthreads;
   s->pool = pool_create(s->nthreads);
@@ -1850,6 +1900,11 @@ void ko_destroy(ko_sched *s) {
   pool_destroy(s->pool);
   free(s->blob);
   free(s->nd.numa_ratio);
+  free(s->nd.taints_hard);
+  free(s->nd.taints_soft);
+  free(s->nd.labels);
+  free(s->traw);
+  free(s->araw);
   free(s->q);
   free(s->feasible);
   free(s->total);
@@ -2094,8 +2149,10 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p0, int64_t n, int64_t *fit
   ko_npol npc;
   numa_policy_ctx(s, p, n, &st.e, &npc, &no);
   if (r != KS_R_RSV_AFFINITY)
-    r |= filter_node(s, p, n, &st.e, &npc) | dev_eval(s, p, n, &draw, npol_allow(s, p, n, &st.e, &npc));
+    r |= static_filter(s, p, n) | filter_node(s, p, n, &st.e, &npc) |
+         dev_eval(s, p, n, &draw, npol_allow(s, p, n, &st.e, &npc));
   s->draw[n] = r ? 0 : draw;
+  static_raw(s, p, n, &s->traw[n], &s->araw[n]);
   s->nom[n] = -1;
   s->rraw[n] = 0;
   s->rord[n] = 0;
@@ -2134,6 +2191,35 @@ static void dev_normalize(ko_sched *s, int64_t *norm) {
     int64_t sc = mx == 0 ? s->draw[n] : MAX_NODE_SCORE * s->draw[n] / mx;
     if (norm) norm[n] = sc;
     s->total[n] += sc * s->cfg.deviceshare.plugin_weight;
+  }
+}
+
+/* TaintToleration NormalizeScore = DefaultNormalizeScore(100, reverse = true), NodeAffinity NormalizeScore =
+ * DefaultNormalizeScore(100, false) (upstream plugins/helper/normalize_score.go, in-tree copy
+ * frameworkext/normalize_score.go:24-52), over the feasible nodes, weighted into total[] */
+static void static_normalize(ko_sched *s, int64_t *tnorm, int64_t *anorm) {
+  for (int pl = 0; pl < 2; pl++) {
+    const ks_static_plugin_args *a = pl == 0 ? &s->cfg.taint : &s->cfg.affinity;
+    if (!a->enable_score) continue;
+    const int64_t *raw = pl == 0 ? s->traw : s->araw;
+    int64_t *norm = pl == 0 ? tnorm : anorm;
+    int64_t mx = 0;
+    for (int64_t n = 0; n < s->n; n++)
+      if (s->total[n] >= 0 && raw[n] > mx) mx = raw[n];
+    for (int64_t n = 0; n < s->n; n++) {
+      if (s->total[n] < 0) {
+        if (norm) norm[n] = 0;
+        continue;
+      }
+      int64_t sc;
+      if (mx == 0) sc = pl == 0 ? MAX_NODE_SCORE : raw[n];
+      else {
+        sc = MAX_NODE_SCORE * raw[n] / mx;
+        if (pl == 0) sc = MAX_NODE_SCORE - sc;
+      }
+      if (norm) norm[n] = sc;
+      s->total[n] += sc * a->plugin_weight;
+    }
   }
 }
 
@@ -2343,6 +2429,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     sweep_arg a = {s, &p};
     pool_until(s->pool, s->n, filter_piece, &a);
     dev_normalize(s, NULL);
+    static_normalize(s, NULL, NULL);
     rsv_normalize(s, NULL);
     /* prioritizeNodes sum + selectHost: max score, lowest index on ties */
     int64_t best = -1, best_n = -1;
@@ -2538,15 +2625,22 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
   }
   int64_t *norm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
   int64_t *dnorm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
+  int64_t *tnorm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
+  int64_t *anorm = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
   dev_normalize(s, dnorm);
+  static_normalize(s, tnorm, anorm);
   rsv_normalize(s, norm);
   for (int64_t n = 0; n < s->n; n++) {
     if (scores && s->cfg.reservation.enable) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = norm[n];
     if (scores) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = s->cfg.deviceshare.enable ? dnorm[n] : 0;
+    if (scores) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_TAINT] = s->cfg.taint.enable_score ? tnorm[n] : 0;
+    if (scores) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = s->cfg.affinity.enable_score ? anorm[n] : 0;
     if (total) total[n] = s->total[n];
   }
   free(norm);
   free(dnorm);
+  free(tnorm);
+  free(anorm);
   return 0;
 }
 

@@ -1,0 +1,131 @@
+"""Upstream TaintToleration and NodeAffinity (kube-scheduler v1.24.15 plugins/tainttoleration, plugins/nodeaffinity;
+not on disk, so parity is unpinned against reference fixtures).  CPU only:
+  * hand-worked matching cases (Toleration.ToleratesTaint, labels.Requirement.Matches, empty terms);
+  * the host compiler (koordinator_amd/static_plugins.py: dictionaries + bit masks) with the C oracle's bit-mask
+    evaluation against oracle/static_plugins_ref.py, which restates both plugins on the taint / label objects --
+    per-node Filter verdicts and normalized scores, alone and next to NodeResourcesFit (normalization over the
+    nodes the other Filters leave);
+  * refusals the device dictionaries imply."""
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, synth
+from koordinator_amd.cluster import NodeTable, PodTable
+from koordinator_amd.config import SchedulerProfile
+from koordinator_amd.static_plugins import (FIELD_NAME, NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, NodeSpec,
+                                            PodAffinitySpec, Requirement, StaticPluginError, Taint, Term, Toleration,
+                                            compile_cluster, requirement_matches)
+from oracle import static_plugins_ref as ref
+from oracle.oracle import Oracle
+
+
+def test_toleration_cases():
+    t_ns = Taint("dedicated", "infra", NO_SCHEDULE)
+    t_pns = Taint("dedicated", "infra", PREFER_NO_SCHEDULE)
+    assert Toleration("", "Exists").tolerates(t_ns) and Toleration("", "Exists").tolerates(t_pns)
+    assert Toleration("dedicated", "Exists", "", NO_SCHEDULE).tolerates(t_ns)
+    assert not Toleration("dedicated", "Exists", "", NO_SCHEDULE).tolerates(t_pns)  # effect mismatch
+    assert Toleration("dedicated", "Equal", "infra").tolerates(t_pns)                # empty effect: every effect
+    assert Toleration("dedicated", "", "infra").tolerates(t_ns)                       # "" operator = Equal
+    assert not Toleration("dedicated", "Equal", "db").tolerates(t_ns)
+    assert not Toleration("other", "Exists").tolerates(t_ns)
+    assert not Toleration("dedicated", "Bogus", "infra").tolerates(t_ns)
+
+
+def test_requirement_cases():
+    n = NodeSpec("n1", {"zone": "a", "rack": "12", "bad": "x1"})
+    assert requirement_matches(Requirement("zone", "In", ("a", "b")), n)
+    assert not requirement_matches(Requirement("zone", "In", ("b",)), n)
+    assert requirement_matches(Requirement("missing", "NotIn", ("a",)), n)  # NotIn holds when the key is absent
+    assert not requirement_matches(Requirement("zone", "NotIn", ("a",)), n)
+    assert requirement_matches(Requirement("zone", "Exists"), n)
+    assert requirement_matches(Requirement("missing", "DoesNotExist"), n)
+    assert requirement_matches(Requirement("rack", "Gt", ("11",)), n)
+    assert not requirement_matches(Requirement("rack", "Gt", ("12",)), n)
+    assert requirement_matches(Requirement("rack", "Lt", ("13",)), n)
+    assert not requirement_matches(Requirement("bad", "Gt", ("0",)), n)      # label not an integer
+    assert not requirement_matches(Requirement("missing", "Lt", ("5",)), n)  # Gt / Lt need the key
+    assert requirement_matches(Requirement(FIELD_NAME, "In", ("n1",), field=True), n)
+    assert requirement_matches(Requirement(FIELD_NAME, "NotIn", ("n2",), field=True), n)
+
+
+def _profile(fit=False):
+    p = SchedulerProfile(fit=None, loadaware=None, taint_toleration=True, node_affinity=True,
+                         taint_toleration_weight=2, node_affinity_weight=3)
+    if fit:
+        p = SchedulerProfile(loadaware=None, taint_toleration=True, node_affinity=True,
+                             taint_toleration_weight=2, node_affinity_weight=3)
+    return p
+
+
+def _compare(w, fit: bool, pods=range(60)):
+    nspec, pspec = w.specs
+    cfg = _profile(fit).to_ks_config()
+    orc = Oracle(cfg, w.nodes.copy())
+    base = None
+    if fit:
+        bcfg = SchedulerProfile(loadaware=None).to_ks_config()
+        base = Oracle(bcfg, w.nodes.copy())
+    for i in pods:
+        one = w.pods.rows([i])
+        r, s, t = orc.eval_pod(one)
+        other = [True] * len(nspec)
+        if base is not None:
+            rb, sb, tb = base.eval_pod(one)
+            other = list(rb == 0)
+        feas, ts, as_ = ref.evaluate(pspec[i], nspec, other)
+        assert list(r == 0) == feas, f"pod {i}: feasibility"
+        for n in range(len(nspec)):
+            if r[n] & ~np.uint32(abi.KS_R_TAINT | abi.KS_R_NODE_AFFINITY) == 0 and base is None:
+                assert bool(r[n] & abi.KS_R_TAINT) == (not ref.taint_filter(pspec[i], nspec[n]))
+                assert bool(r[n] & abi.KS_R_NODE_AFFINITY) == (not ref.affinity_filter(pspec[i], nspec[n]))
+        assert list(s[:, abi.KS_SCORE_TAINT]) == ts, f"pod {i}: TaintToleration scores"
+        assert list(s[:, abi.KS_SCORE_NODE_AFFINITY]) == as_, f"pod {i}: NodeAffinity scores"
+        if base is None:
+            want_t = [2 * a + 3 * b if f else -1 for a, b, f in zip(ts, as_, feas)]
+            assert list(t) == want_t, f"pod {i}: totals"
+    orc.close()
+    if base is not None:
+        base.close()
+
+
+@pytest.mark.parametrize("fit", [False, True])
+def test_oracle_against_restatement(fit):
+    w = synth.with_static_plugins(synth.c1(n_nodes=300, n_pods=120), seed=11)
+    _compare(w, fit)
+
+
+def test_empty_terms_and_selector():
+    nodes = [NodeSpec("a", {"zone": "z1"}), NodeSpec("b", {"zone": "z2"}, [Taint("t", "", PREFER_NO_SCHEDULE)])]
+    pods = [PodAffinitySpec(required=[]),                                   # no terms: nothing matches
+            PodAffinitySpec(required=[Term([])]),                           # an empty term matches nothing
+            PodAffinitySpec(node_selector={"zone": "z2"}),
+            PodAffinitySpec(node_selector={"zone": "z2"}, required=[Term([Requirement("zone", "In", ("z1",))])]),
+            PodAffinitySpec(preferred=[(10, Term([])), (5, Term([Requirement("zone", "In", ("z1",))]))])]
+    nt = synth.make_nodes(2, np.random.Generator(np.random.PCG64(1)))
+    pt = synth.make_pods(len(pods), np.random.Generator(np.random.PCG64(2)))
+    compile_cluster(nodes, pods, nt, pt)
+    orc = Oracle(_profile().to_ks_config(), nt)
+    want_feas = [[False, False], [False, False], [False, True], [False, False], [True, True]]
+    for i in range(len(pods)):
+        r, s, t = orc.eval_pod(pt.rows([i]))
+        assert list(r == 0) == want_feas[i], i
+        feas, ts, as_ = ref.evaluate(pods[i], nodes, [True, True])
+        assert feas == want_feas[i]
+        assert list(s[:, abi.KS_SCORE_TAINT]) == ts and list(s[:, abi.KS_SCORE_NODE_AFFINITY]) == as_
+    # pod 4: affinity raw 5 / 0 -> 100 / 0; taint raw 0 / 1 -> reverse 100 / 0
+    r, s, t = orc.eval_pod(pt.rows([4]))
+    assert list(s[:, abi.KS_SCORE_NODE_AFFINITY]) == [100, 0] and list(s[:, abi.KS_SCORE_TAINT]) == [100, 0]
+    orc.close()
+
+
+def test_refusals():
+    nodes = [NodeSpec(f"n{i}", {}, [Taint(f"k{i}", "", NO_EXECUTE)]) for i in range(65)]
+    with pytest.raises(StaticPluginError):
+        compile_cluster(nodes, [], NodeTable(65), PodTable(0))
+    pods = [PodAffinitySpec(required=[Term([Requirement("z", "In", (str(i),))]) for i in range(5)])]
+    with pytest.raises(StaticPluginError):
+        compile_cluster([NodeSpec("a")], pods, NodeTable(1), PodTable(1))
+    with pytest.raises(StaticPluginError):
+        compile_cluster([NodeSpec("a")], [PodAffinitySpec(required=[Term([Requirement("z", "Gt", ("x",))])])],
+                        NodeTable(1), PodTable(1))
