@@ -169,6 +169,7 @@ extern "C" {
 #define KS_R_TAINT 0x2000000u             /* upstream TaintToleration Filter: "node(s) had untolerated taint" (a NoSchedule /
                                              NoExecute taint no toleration of the pod tolerates) */
 #define KS_R_NODE_AFFINITY 0x4000000u     /* upstream NodeAffinity Filter: "node(s) didn't match Pod's node affinity/selector" */
+#define KS_R_NODE_PORTS 0x8000000u        /* upstream NodePorts Filter: "node(s) didn't have free ports for the requested pod ports" */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -332,6 +333,7 @@ typedef struct ks_config {
   ks_balanced_args balanced; /* ABI 5 */
   ks_static_plugin_args taint;    /* ABI 6: upstream TaintToleration */
   ks_static_plugin_args affinity; /* ABI 6: upstream NodeAffinity */
+  ks_static_plugin_args nodeports; /* ABI 6: upstream NodePorts (Filter only: enable_score / plugin_weight unused) */
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -378,6 +380,9 @@ typedef struct ks_node_cols {
   const uint64_t *taints_hard;  /* taints with effect NoSchedule or NoExecute */
   const uint64_t *taints_soft;  /* taints with effect PreferNoSchedule */
   const uint64_t *labels;       /* node selector requirements the node matches (bit 63 must be 0) */
+  /* NodePorts (ABI 6; NULL = 0): host-port dictionary bits in use on the node (NodeInfo.UsedPorts); every Reserve
+   * adds the pod's bits while ks_config.nodeports is on (read back with ks_read_nodes) */
+  const uint64_t *host_ports;
 } ks_node_cols;
 
 /* Pending pods, queue order, structure-of-arrays. */
@@ -428,6 +433,11 @@ typedef struct ks_pod_cols {
   const uint64_t *affinity_required[KS_AFFINITY_TERMS];   /* term t: the requirement bits it needs */
   const uint64_t *affinity_preferred[KS_AFFINITY_TERMS];  /* preferred term t: the requirement bits it needs */
   const int32_t *affinity_weight[KS_AFFINITY_TERMS];      /* preferred term t's weight, 1..100 (0 = unused) */
+  /* NodePorts (ABI 6; NULL = none): the pod's host ports as dictionary bits (the entries it uses) and the entries
+   * any of them conflicts with (HostPortInfo.CheckConflict: same protocol and port, equal host IPs or either
+   * 0.0.0.0) */
+  const uint64_t *host_ports;
+  const uint64_t *host_ports_conflict;
 } ks_pod_cols;
 
 #define KS_JOINT_NONE 0u
@@ -562,6 +572,7 @@ typedef struct ks_node_state {
   int64_t *la_term_memory;
   int64_t *la_prod_term_milli_cpu;
   int64_t *la_prod_term_memory;
+  uint64_t *host_ports;  /* ABI 6: NodePorts dictionary bits in use (NULL = skip) */
 } ks_node_state;
 
 typedef struct ks_stats {

@@ -104,6 +104,7 @@ KS_R_NUMA_BIND_CONFLICT = 0x800000
 KS_R_NUMA_SMT = 0x1000000
 KS_R_TAINT = 0x2000000
 KS_R_NODE_AFFINITY = 0x4000000
+KS_R_NODE_PORTS = 0x8000000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -210,6 +211,7 @@ class KsConfig(C.Structure):
         ("balanced", KsBalancedArgs),
         ("taint", KsStaticPluginArgs),
         ("affinity", KsStaticPluginArgs),
+        ("nodeports", KsStaticPluginArgs),
     ]
 
 
@@ -249,6 +251,7 @@ NODE_COLS = [
     ("taints_hard", C.POINTER(C.c_uint64)),
     ("taints_soft", C.POINTER(C.c_uint64)),
     ("labels", C.POINTER(C.c_uint64)),
+    ("host_ports", C.POINTER(C.c_uint64)),
 ]
 
 
@@ -285,6 +288,8 @@ POD_COLS = [
     ("affinity_required", C.POINTER(C.c_uint64) * KS_AFFINITY_TERMS),
     ("affinity_preferred", C.POINTER(C.c_uint64) * KS_AFFINITY_TERMS),
     ("affinity_weight", P32 * KS_AFFINITY_TERMS),
+    ("host_ports", C.POINTER(C.c_uint64)),
+    ("host_ports_conflict", C.POINTER(C.c_uint64)),
 ]
 
 
@@ -394,6 +399,7 @@ NODE_STATE_COLS = [
     ("la_term_memory", P64),
     ("la_prod_term_milli_cpu", P64),
     ("la_prod_term_memory", P64),
+    ("host_ports", C.POINTER(C.c_uint64)),
 ]
 
 

@@ -30,7 +30,7 @@ NODE_I32 = ["allowed_pods", "pod_count", "la_thr_cpu", "la_thr_memory", "la_prod
             "numa_cpuset_cpus"]
 NODE_U32 = ["la_flags", "numa_flags"]
 # TaintToleration / NodeAffinity dictionary bits (static_plugins.compile_cluster)
-NODE_U64 = ["taints_hard", "taints_soft", "labels"]
+NODE_U64 = ["taints_hard", "taints_soft", "labels", "host_ports"]
 
 POD_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral",
@@ -41,7 +41,7 @@ POD_I64 = [
 POD_I32 = ["quota", "rsv_class", "affinity_required_n"]
 POD_U32 = ["flags", "quota_mask", "cpu_bind"]
 POD_U8 = ["joint"]
-POD_U64 = ["tolerated"]
+POD_U64 = ["tolerated", "host_ports", "host_ports_conflict"]
 
 STATE_I64 = [
     "req_milli_cpu", "req_memory", "req_ephemeral", "nonzero_milli_cpu", "nonzero_memory",
@@ -198,7 +198,7 @@ class PodTable(_Table):
             setattr(t, k, np.ascontiguousarray(getattr(self, k)[:, idx]))
         return t
 
-    def ks(self) -> abi.KsPodCols:
+    def ks(self) -> abi.KsPodCols:  # noqa: C901
         self._fix()
         self.req_scalar = np.ascontiguousarray(self.req_scalar, np.int64)
         self.quota_req = np.ascontiguousarray(self.quota_req, np.int64)
@@ -215,7 +215,8 @@ class PodTable(_Table):
             c.req_scalar[k] = _p64(self.req_scalar[k])
         for d in range(abi.KS_QUOTA_DIMS):
             c.quota_req[d] = _p64(self.quota_req[d])
-        c.tolerated = self.tolerated.ctypes.data_as(C.POINTER(C.c_uint64))
+        for name in POD_U64:
+            setattr(c, name, getattr(self, name).ctypes.data_as(C.POINTER(C.c_uint64)))
         c.affinity_required_n = _p32(self.affinity_required_n)
         self.affinity_required = np.ascontiguousarray(self.affinity_required, np.uint64)
         self.affinity_preferred = np.ascontiguousarray(self.affinity_preferred, np.uint64)
@@ -522,12 +523,14 @@ class NodeState:
             setattr(self, name, np.zeros(n, np.int64))
         self.pod_count = np.zeros(n, np.int32)
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, n), np.int64)
+        self.host_ports = np.zeros(n, np.uint64)
 
     def ks(self) -> abi.KsNodeState:
         s = abi.KsNodeState()
         for name in STATE_I64:
             setattr(s, name, _p64(getattr(self, name)))
         s.pod_count = _p32(self.pod_count)
+        s.host_ports = self.host_ports.ctypes.data_as(C.POINTER(C.c_uint64))
         for k in range(abi.KS_MAX_SCALARS):
             s.req_scalar[k] = _p64(self.req_scalar[k])
         s._keep = self
@@ -537,6 +540,7 @@ class NodeState:
         d = {k: getattr(self, k) for k in STATE_I64}
         d["pod_count"] = self.pod_count
         d["req_scalar"] = self.req_scalar
+        d["host_ports"] = self.host_ports
         return d
 
 

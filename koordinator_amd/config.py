@@ -162,6 +162,7 @@ class SchedulerProfile:
     taint_toleration_weight: int = 1
     node_affinity: bool = False
     node_affinity_weight: int = 1
+    node_ports: bool = False  # upstream NodePorts (Filter only); host ports as dictionary bits (static_plugins)
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -255,6 +256,8 @@ class SchedulerProfile:
             c.affinity.enable_filter = 1
             c.affinity.enable_score = 1 if self.node_affinity_weight else 0
             c.affinity.plugin_weight = self.node_affinity_weight
+        if self.node_ports:
+            c.nodeports.enable_filter = 1
         if self.reservation_weight is not None:
             c.reservation.enable = 1
             c.reservation.plugin_weight = int(self.reservation_weight)

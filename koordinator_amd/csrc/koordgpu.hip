@@ -1131,7 +1131,8 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.aff = c.affinity.enable_filter ? 1 : 0;
   k.aff |= c.affinity.enable_score ? 2 : 0;
   k.aff_pw = c.affinity.enable_score ? (int32_t)c.affinity.plugin_weight : 0;
-  k.stat = (k.taint | k.aff) ? 1 : 0;
+  k.ports = c.nodeports.enable_filter ? 1 : 0;
+  k.stat = (k.taint | k.aff | k.ports) ? 1 : 0;
   if ((k.taint | k.aff) & 2) k.monotone = 0;
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
                              (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw +
@@ -1351,6 +1352,7 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.numa_cpus, 4, true);
   add(&d.cpu_free, 4, true);
   add(&d.cpu_cores, 4, true);
+  add(&d.host_ports, 8, true);
   // read-only columns
   add(&d.alloc_cpu, 8, false);
   add(&d.alloc_mem, 8, false);
@@ -1398,6 +1400,7 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->numa_cpuset_cpus);
   v.push_back(nullptr);  // cpu_free: ks_load_cpu_state (-1 = no CPU topology)
   v.push_back(nullptr);  // cpu_cores: cores_refresh
+  v.push_back(c->host_ports);
   v.push_back(c->alloc_milli_cpu);
   v.push_back(c->alloc_memory);
   v.push_back(c->alloc_ephemeral);
@@ -2845,6 +2848,8 @@ static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t 
         r.w[t] = pc->affinity_weight[t] ? pc->affinity_weight[t][i] : 0;
         dyn |= (ctx->kc.aff & 2) && r.w[t] != 0;
       }
+      r.pwant = pc->host_ports ? pc->host_ports[i] : 0;
+      r.pconf = pc->host_ports_conflict ? pc->host_ports_conflict[i] : 0;
       hd[(size_t)i] = dyn ? 1 : 0;
     }
     if (p > 0) {
@@ -3005,10 +3010,10 @@ static int kernel_feat(const ks_ctx* ctx) {
 }
 
 // the slot device region of the commit kernel: GPU state (DeviceShare), then the TaintToleration / NodeAffinity words
-// (3 x u64 per slot, the region's last kMaxBatch * 24 B)
+// and NodePorts words (4 x u64 per slot, the region's last kMaxBatch * 32 B)
 static size_t dev_cache_bytes(const ks_ctx* ctx) {
   return (ctx->kc.dev ? (size_t)kDevLdsStride * (kDevTW + kDevQW) * 8 + (size_t)kMaxBatch * 4 : 0) +
-         (ctx->kc.stat ? (size_t)kMaxBatch * 24 : 0);
+         (ctx->kc.stat ? (size_t)kMaxBatch * 32 : 0);
 }
 
 static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {
@@ -3966,6 +3971,7 @@ struct UnreserveArgs {
   DevQuotas q;
   DevPodQuota pq;
   const PodRec* pod;
+  const PodStat* pstat;    // NodePorts: the pod's host ports (Cfg.ports)
   Cfg c;
   int32_t node, gi;        // node; the reservation's CSR position (-1 = none)
   uint32_t gmin, rmin;     // DeviceShare minors of the allocation
@@ -4003,6 +4009,8 @@ __global__ void unreserve_kernel(UnreserveArgs a) {
     d.la_pterm_cpu[n] -= p.est_cpu;
     d.la_pterm_mem[n] -= p.est_mem;
   }
+  // NodeInfo.RemovePod: the pod's host ports (a used entry conflicts with itself, so no other pod holds it)
+  if (a.c.ports & 1) d.host_ports[n] &= ~a.pstat[0].pwant;
   // reservationCache.forgetPod: Allocated -= Mask(requests, ResourceNames); the pod leaves the assigned set
   if (a.gi >= 0) {
     const uint32_t keys = rsv_keys(a.rv.meta[a.gi]);
@@ -4187,6 +4195,7 @@ int ks_unreserve(ks_ctx* ctx, const ks_pod_cols* pod, const ks_result* r, const 
   ua.q = ctx->q;
   ua.pq = ctx->ast.pq;
   ua.pod = ctx->ast.recs;
+  ua.pstat = ctx->ast.stat;
   ua.c = ctx->kc;
   ua.node = node;
   ua.gi = gi;
@@ -4263,6 +4272,7 @@ int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
   HIPCHK(ctx, cp(o->la_term_memory, v.la_term_mem, 8));
   HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, v.la_pterm_cpu, 8));
   HIPCHK(ctx, cp(o->la_prod_term_memory, v.la_pterm_mem, 8));
+  HIPCHK(ctx, cp(o->host_ports, v.host_ports, 8));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }

@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   EvalOut o = eval_full<NSC, true, false, 15>(
       c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
       [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
-  if (c.stat) stat_eval(c, *pstat, d.taints_hard[i], d.taints_soft[i], d.labels[i], o);
+  if (c.stat) stat_eval(c, *pstat, d.taints_hard[i], d.taints_soft[i], d.labels[i], d.host_ports[i], o);
   reasons[i] = o.reasons;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;

@@ -77,7 +77,8 @@ struct Cfg {
   int32_t bal, bal_pw;  // upstream NodeResourcesBalancedAllocation: KS_BAL_* resources (0 = off), plugin weight
   int32_t taint, taint_pw;  // upstream TaintToleration: bit 0 Filter, bit 1 Score; plugin weight
   int32_t aff, aff_pw;      // upstream NodeAffinity: bit 0 Filter, bit 1 Score; plugin weight
-  int32_t stat;             // taint | aff: the dictionary-bit plugins are on (kernel variant FEAT & 4, PodStat read)
+  int32_t ports;            // upstream NodePorts Filter (bit 0)
+  int32_t stat;             // taint | aff | ports: the dictionary-bit plugins are on (kernel variant FEAT & 4, PodStat)
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).
@@ -103,6 +104,7 @@ struct DevNodes {
   int32_t *cpu_free;        // available CPUs for cpuset pods (ks_cpuset.h), -1 = no valid CPU topology
   uint32_t *cpu_cores;      // derived: CoresWord (fully available / partly available cores, CPUsPerCore, CPU bind label)
   uint64_t *taints_hard, *taints_soft, *labels;  // TaintToleration / NodeAffinity dictionary bits (static per node)
+  uint64_t *host_ports;                          // NodePorts dictionary bits in use (mutable: every Reserve adds)
 };
 
 // Per-node word of the required CPU bind policies (Cfg.cores): the cores whose CPUs are all available
@@ -418,8 +420,9 @@ struct __attribute__((aligned(16))) PodStat {
   int32_t w[KS_AFFINITY_TERMS];       // preferred weights (0 = unused)
   int32_t nreq;                       // required terms (0 = no required node affinity / selector)
   int32_t _pad;
+  uint64_t pwant, pconf;              // NodePorts: the pod's host-port bits, the bits any of them conflicts with
 };
-static_assert(sizeof(PodStat) == 96, "PodStat layout");
+static_assert(sizeof(PodStat) == 112, "PodStat layout");
 
 __device__ __forceinline__ PodStat load_stat_uniform(const PodStat* p) {
   PodStat r;
@@ -442,8 +445,10 @@ __device__ __forceinline__ PodStat load_stat_uniform(const PodStat* p) {
 // PreferNoSchedule taints (countIntolerableTaintsPreferNoSchedule) and the weights of the matching preferred terms.
 // Every node is evaluated the same way whatever other Filters said (reasons are OR-ed).
 __device__ __forceinline__ void stat_eval(const Cfg& c, const PodStat& s, uint64_t hard, uint64_t soft, uint64_t labels,
-                                          EvalOut& o) {
+                                          uint64_t ports, EvalOut& o) {
   if ((c.taint & 1) && (hard & ~s.tol)) o.reasons |= KS_R_TAINT;
+  // upstream NodePorts Filter (plugins/nodeports/node_ports.go fitsPorts: UsedPorts.CheckConflict per wanted port)
+  if ((c.ports & 1) && (ports & s.pconf)) o.reasons |= KS_R_NODE_PORTS;
   if ((c.aff & 1) && s.nreq > 0) {
     bool ok = false;
 #pragma unroll

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       continue;
     }
     NodeReg<NSC> r;
-    uint64_t st_hard = 0, st_soft = 0, st_lab = 0;  // TaintToleration / NodeAffinity words (FEAT & 4 variants)
+    uint64_t st_hard = 0, st_soft = 0, st_lab = 0, st_port = 0;  // dictionary-bit plugin words (FEAT & 4 variants)
     {
       const DevNodes d = *a.dn;
       load_node<NSC>(a.c, d, node, node < a.n, r);
@@ -167,6 +167,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
         st_hard = gld(d.taints_hard + node);
         st_soft = gld(d.taints_soft + node);
         st_lab = gld(d.labels + node);
+        st_port = gld(d.host_ports + node);
       }
     }
     const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
       EvalOut o = eval_full<NSC, false, true, FEAT>(
           a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
           [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
-      if ((FEAT & 4) && a.c.stat) stat_eval(a.c, load_stat_uniform(a.pstat + cursor + p), st_hard, st_soft, st_lab, o);
+      if ((FEAT & 4) && a.c.stat) stat_eval(a.c, load_stat_uniform(a.pstat + cursor + p), st_hard, st_soft, st_lab, st_port, o);
       if ((FEAT & 4) && a.phase == 0) {
         // normalization maxima over the feasible nodes, witness = lowest index holding each
         const uint64_t wit = 0xFFFFFFFFull - (uint64_t)node;
@@ -558,7 +559,7 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
   const int lane = threadIdx.x & 63;
   const int64_t node = chunk * 64 + lane;
   NodeReg<NSC> r;
-  uint64_t sh = 0, ss = 0, sl = 0;
+  uint64_t sh = 0, ss = 0, sl = 0, sp = 0;
   {
     const DevNodes d = *a.dn;
     load_node<NSC>(cfg, d, node, node < a.n, r);
@@ -566,12 +567,13 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
       sh = gld(d.taints_hard + node);
       ss = gld(d.taints_soft + node);
       sl = gld(d.labels + node);
+      sp = gld(d.host_ports + node);
     }
   }
   EvalOut o = eval_full<NSC, false, false, FEAT>(
       cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
       [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
-  if ((FEAT & 4) && cfg.stat) stat_eval(cfg, *ps, sh, ss, sl, o);
+  if ((FEAT & 4) && cfg.stat) stat_eval(cfg, *ps, sh, ss, sl, sp, o);
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
   return wave_max_u64(skip ? 0ull : gkey(key_total(cfg, o, M), node));
 }
@@ -662,9 +664,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   int64_t* sdev_use = sdev_tot + kDevLdsStride * DW;
   int32_t* sdev_pres = reinterpret_cast<int32_t*>(sdev_use + kDevLdsStride * DU);
   int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
-  // per slot: the node's TaintToleration / NodeAffinity words (hard, soft, labels): the last kMaxBatch * 24 B of the
-  // slot device region (dev_cache_bytes)
-  uint64_t* sstat = reinterpret_cast<uint64_t*>(smem_raw + lay.sdev + a.dev_bytes - (size_t)kMaxBatch * 24);
+  // per slot: the node's dictionary-bit plugin words (taints hard, soft, labels, host ports -- the last one updated
+  // by every Reserve of the pass): the last kMaxBatch * 32 B of the slot device region (dev_cache_bytes)
+  uint64_t* sstat = reinterpret_cast<uint64_t*>(smem_raw + lay.sdev + a.dev_bytes - (size_t)kMaxBatch * 32);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -939,7 +941,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
             },
             [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
             [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
-        if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[3 * lane], sstat[3 * lane + 1], sstat[3 * lane + 2], o);
+        if (DEV && cfg.stat)
+          stat_eval(cfg, pst, sstat[4 * lane], sstat[4 * lane + 1], sstat[4 * lane + 2], sstat[4 * lane + 3], o);
         feas = o.reasons == 0;
         if ((FEAT & 2) && cfg.cores && (cw & kCoresDirty) && feas)
           unk = ((pod.flags & KS_POD_CPU_BIND) && (pod.cpu_bind & KS_CPU_BIND_REQUIRED)) ||
@@ -1088,8 +1091,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       }
       if (DEV && cfg.stat) {
         const DevNodes d = *a.dn;
-        const uint64_t* col = lane == 0 ? d.taints_hard : (lane == 1 ? d.taints_soft : d.labels);
-        if (lane < 3) sstat[3 * s + lane] = gld(col + node);
+        const uint64_t* col = lane == 0 ? d.taints_hard : (lane == 1 ? d.taints_soft : (lane == 2 ? d.labels : d.host_ports));
+        if (lane < 4) sstat[4 * s + lane] = gld(col + node);
       }
       if (DEV && cfg.dev) {
         // the node's device totals + topology / used / present flag into LDS (lane = word)
@@ -1192,7 +1195,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
           const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0});
           e2.dev_raw = dd.raw;
         }
-        if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[3 * s], sstat[3 * s + 1], sstat[3 * s + 2], e2);
+        if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[4 * s], sstat[4 * s + 1], sstat[4 * s + 2], sstat[4 * s + 3], e2);
         fitla_pref = e2.total + norm_terms(cfg, e2, Muse);
       }
       int64_t dd = 0;
@@ -1373,6 +1376,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
         a.cpuset_split[cursor0 + j] = cpu_split;
       }
     }
+    // NodePorts: NodeInfo.AddPod adds the pod's host ports (written back with the slot)
+    if (DEV && (cfg.ports & 1) && lane == 0) sstat[4 * s + 3] |= pst.pwant;
     if (lane == 0) sres[j] = ks_result{node, KS_S_SCHEDULED, score_out, nom_row, gminors, rminors, 0};
     {
       const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
@@ -1433,6 +1438,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     gst(d.la_term_mem + node, term_requested(r.t[ST_LMEM]));
     gst(d.la_pterm_cpu + node, term_requested(r.t[ST_PLCPU]));
     gst(d.la_pterm_mem + node, term_requested(r.t[ST_PLMEM]));
+    if (DEV && (cfg.ports & 1)) gst(d.host_ports + node, sstat[4 * lane + 3]);
     if ((FEAT & 2) && cfg.cpuset) {
       gst(d.numa_amilli + node, snuma[4 * lane]);
       gst(d.numa_off + node, snuma[4 * lane + 1]);

@@ -81,12 +81,32 @@ class Term:
     requirements: List[Requirement] = field(default_factory=list)
 
 
+@dataclass(frozen=True)
+class HostPort:
+    """A container port with a host port (framework.HostPortInfo entry); sanitized like HostPortInfo.sanitize:
+    empty host IP -> 0.0.0.0, empty protocol -> TCP."""
+    port: int
+    protocol: str = "TCP"
+    host_ip: str = "0.0.0.0"
+
+    def sanitized(self) -> "HostPort":
+        return HostPort(self.port, self.protocol or "TCP", self.host_ip or "0.0.0.0")
+
+    def conflicts(self, other: "HostPort") -> bool:
+        """HostPortInfo.CheckConflict for one used entry: same protocol and port, and equal IPs or either 0.0.0.0"""
+        a, b = self.sanitized(), other.sanitized()
+        if a.port <= 0 or b.port <= 0 or a.protocol != b.protocol or a.port != b.port:
+            return False
+        return a.host_ip == b.host_ip or a.host_ip == "0.0.0.0" or b.host_ip == "0.0.0.0"
+
+
 @dataclass
 class PodAffinitySpec:
     tolerations: List[Toleration] = field(default_factory=list)
     node_selector: Dict[str, str] = field(default_factory=dict)
     required: Optional[List[Term]] = None             # requiredDuringSchedulingIgnoredDuringExecution terms
     preferred: List[Tuple[int, Term]] = field(default_factory=list)  # (weight, preference)
+    host_ports: List[HostPort] = field(default_factory=list)          # NodePorts: the containers' host ports
 
 
 @dataclass
@@ -94,6 +114,7 @@ class NodeSpec:
     name: str
     labels: Dict[str, str] = field(default_factory=dict)
     taints: List[Taint] = field(default_factory=list)
+    used_ports: List[HostPort] = field(default_factory=list)         # NodeInfo.UsedPorts of the running pods
 
 
 def _parse_int(v: str) -> Optional[int]:
@@ -156,6 +177,7 @@ def _term_reqs(pod: PodAffinitySpec, term: Optional[Term]) -> List[Requirement]:
 class Dictionaries:
     taints: List[Taint]
     requirements: List[Requirement]
+    ports: List[HostPort] = field(default_factory=list)
 
 
 def build_dictionaries(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec]) -> Dictionaries:
@@ -181,7 +203,14 @@ def build_dictionaries(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec
                 reqs.setdefault(r, len(reqs))
     if len(reqs) > 63:
         raise StaticPluginError(f"{len(reqs)} distinct node selector requirements (the device dictionary holds 63)")
-    return Dictionaries(list(taints), list(reqs))
+    ports: Dict[HostPort, int] = {}
+    for hp in [h for nd in nodes for h in nd.used_ports] + [h for p in pods for h in p.host_ports]:
+        hp = hp.sanitized()
+        if hp.port > 0:
+            ports.setdefault(hp, len(ports))
+    if len(ports) > 64:
+        raise StaticPluginError(f"{len(ports)} distinct host ports (the device dictionary holds 64)")
+    return Dictionaries(list(taints), list(reqs), list(ports))
 
 
 def _mask(reqs: List[Requirement], index: Dict[Requirement, int]) -> int:
@@ -218,6 +247,16 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
     node_table.taints_hard = hard
     node_table.taints_soft = soft
     node_table.labels = labels
+    pindex = {hp: i for i, hp in enumerate(d.ports)}
+    used = np.zeros(len(nodes), np.uint64)
+    for i, nd in enumerate(nodes):
+        m = 0
+        for hp in nd.used_ports:
+            hp = hp.sanitized()
+            if hp.port > 0:
+                m |= 1 << pindex[hp]
+        used[i] = m
+    node_table.host_ports = used
     T = abi.KS_AFFINITY_TERMS
     tol = np.zeros(len(pods), np.uint64)
     nreq = np.zeros(len(pods), np.int32)
@@ -254,6 +293,21 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
                 raise StaticPluginError(f"pod {i}: preferred weight {w} outside [1, 100]")
             pref[k, i] = _mask(list(t.requirements), rindex) if t.requirements else never
             wt[k, i] = w
+    want = np.zeros(len(pods), np.uint64)
+    conf = np.zeros(len(pods), np.uint64)
+    for i, p in enumerate(pods):
+        w = c = 0
+        for hp in p.host_ports:
+            hp = hp.sanitized()
+            if hp.port <= 0:
+                continue
+            w |= 1 << pindex[hp]
+            for k, q in enumerate(d.ports):
+                if hp.conflicts(q):
+                    c |= 1 << k
+        want[i], conf[i] = w, c
+    pod_table.host_ports = want
+    pod_table.host_ports_conflict = conf
     pod_table.tolerated = tol
     pod_table.affinity_required_n = nreq
     pod_table.affinity_required = req

@@ -528,7 +528,7 @@ def static_specs(n_nodes: int, n_pods: int, rng: np.random.Generator):
     NodeAffinity plugins (static_plugins): 4 zones, 3 instance types, integer rack labels (Gt / Lt), GPU labels;
     NoSchedule / NoExecute / PreferNoSchedule taints on part of the nodes; pods with Equal / Exists / wildcard
     tolerations, nodeSelectors, required terms (In, NotIn, Gt, matchFields) and weighted preferred terms."""
-    from .static_plugins import (NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, FIELD_NAME, NodeSpec,
+    from .static_plugins import (NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, FIELD_NAME, HostPort, NodeSpec,
                                  PodAffinitySpec, Requirement, Taint, Term, Toleration)
     zones = ["zone-a", "zone-b", "zone-c", "zone-d"]
     types = ["m.large", "m.xlarge", "c.2xlarge"]
@@ -549,7 +549,12 @@ def static_specs(n_nodes: int, n_pods: int, rng: np.random.Generator):
             taints.append(Taint("spot", "true", PREFER_NO_SCHEDULE))
         if rng.random() < 0.15:
             taints.append(Taint("noisy", "", PREFER_NO_SCHEDULE))
-        nodes.append(NodeSpec(f"node-{i}", lab, taints))
+        used = []
+        if rng.random() < 0.2:
+            used.append(HostPort(80, "TCP", rng.choice(["0.0.0.0", "10.0.0.1", "10.0.0.2"])))
+        if rng.random() < 0.1:
+            used.append(HostPort(443))
+        nodes.append(NodeSpec(f"node-{i}", lab, taints, used))
     pods = []
     for i in range(n_pods):
         tol = []
@@ -583,12 +588,21 @@ def static_specs(n_nodes: int, n_pods: int, rng: np.random.Generator):
                 pref.append((int(rng.integers(1, 101)), Term([Requirement("rack", "Lt", ("5",))])))
             if rng.random() < 0.3:
                 pref.append((int(rng.integers(1, 101)), Term([Requirement("accelerator", "Exists")])))
-        pods.append(PodAffinitySpec(tol, sel, req, pref))
+        ports = []
+        u = rng.random()
+        if u < 0.1:
+            ports.append(HostPort(80, "", ""))  # sanitized to TCP on 0.0.0.0
+        elif u < 0.15:
+            ports.append(HostPort(80, "TCP", rng.choice(["10.0.0.1", "10.0.0.3"])))
+        elif u < 0.18:
+            ports += [HostPort(443), HostPort(9100, "UDP")]
+        pods.append(PodAffinitySpec(tol, sel, req, pref, ports))
     return nodes, pods
 
 
 def with_static_plugins(w: Workload, seed: int = SEED + 7, weight_taint: int = 1, weight_affinity: int = 1) -> Workload:
-    """The workload with upstream TaintToleration and NodeAffinity switched on and random specs compiled in."""
+    """The workload with upstream TaintToleration, NodeAffinity and NodePorts switched on and random specs compiled
+    in."""
     from .static_plugins import compile_cluster
     rng = np.random.Generator(np.random.PCG64(seed))
     nspec, pspec = static_specs(w.nodes.n, w.pods.n, rng)
@@ -597,13 +611,14 @@ def with_static_plugins(w: Workload, seed: int = SEED + 7, weight_taint: int = 1
     w.profile.taint_toleration_weight = weight_taint
     w.profile.node_affinity = True
     w.profile.node_affinity_weight = weight_affinity
+    w.profile.node_ports = True
     w.specs = (nspec, pspec)
     return w
 
 
 def c2_default(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, **kw) -> Workload:
     """C2 under the v1beta2 default profile's upstream plugins as well: NodeResourcesBalancedAllocation,
-    TaintToleration and NodeAffinity (weight 1 each) next to Fit + LoadAware + ElasticQuota."""
+    TaintToleration and NodeAffinity (weight 1 each) and NodePorts next to Fit + LoadAware + ElasticQuota."""
     from .config import NodeResourcesBalancedAllocationArgs
     w = c2(seed=seed, n_nodes=n_nodes, n_pods=n_pods, **kw)
     w.profile.balanced = NodeResourcesBalancedAllocationArgs()

@@ -118,6 +118,7 @@ typedef struct {
   int32_t *numa_cpus;
   uint32_t *numa_flags;
   uint64_t *taints_hard, *taints_soft, *labels; /* TaintToleration / NodeAffinity dictionary bits (ks_config.taint) */
+  uint64_t *host_ports;                          /* NodePorts: NodeInfo.UsedPorts as host-port dictionary bits */
 } ko_nodes;
 
 typedef struct {
@@ -234,6 +235,7 @@ typedef struct {
   int32_t nreq;      /* NodeAffinity: required terms (0 = none) */
   uint64_t req[KS_AFFINITY_TERMS], pref[KS_AFFINITY_TERMS];
   int32_t w[KS_AFFINITY_TERMS];
+  uint64_t pwant, pconf; /* NodePorts: the pod's host-port bits, the bits any of them conflicts with */
 } ko_pod;
 
 /* NodeInfo values the Fit plugin reads, after the Reservation restore */
@@ -285,6 +287,8 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
     p->pref[t] = pc->affinity_preferred[t] ? pc->affinity_preferred[t][i] : 0;
     p->w[t] = pc->affinity_weight[t] ? pc->affinity_weight[t][i] : 0;
   }
+  p->pwant = pc->host_ports ? pc->host_ports[i] : 0;
+  p->pconf = pc->host_ports_conflict ? pc->host_ports_conflict[i] : 0;
 }
 
 /* Upstream TaintToleration (kube-scheduler v1.24.15 plugins/tainttoleration/taint_toleration.go, not on disk: parity
@@ -295,6 +299,8 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
 static uint32_t static_filter(const ko_sched *s, const ko_pod *p, int64_t n) {
   uint32_t r = 0;
   if (s->cfg.taint.enable_filter && (s->nd.taints_hard[n] & ~p->tol)) r |= KS_R_TAINT;
+  /* upstream NodePorts Filter (plugins/nodeports/node_ports.go fitsPorts): a wanted port conflicts with a used one */
+  if (s->cfg.nodeports.enable_filter && (s->nd.host_ports[n] & p->pconf)) r |= KS_R_NODE_PORTS;
   if (s->cfg.affinity.enable_filter && p->nreq > 0) {
     int ok = 0;
     for (int t = 0; t < p->nreq && t < KS_AFFINITY_TERMS; t++)
@@ -1702,6 +1708,7 @@ static void node_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
   d->nz_cpu[n] += p->nzcpu;
   d->nz_mem[n] += p->nzmem;
   d->pod_count[n] += 1;
+  if (s->cfg.nodeports.enable_filter) d->host_ports[n] |= p->pwant; /* NodeInfo.AddPod: UsedPorts */
   /* the freshly assigned pod has no PodMetric, so estimatedAssignedPodUsed counts
    * its estimate (load_aware.go:350-355) in every later Score on this node. */
   d->la_term_cpu[n] += p->est_cpu;
@@ -1854,6 +1861,7 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   s->nd.taints_hard = (uint64_t *)calloc(nn, 8);
   s->nd.taints_soft = (uint64_t *)calloc(nn, 8);
   s->nd.labels = (uint64_t *)calloc(nn, 8);
+  s->nd.host_ports = (uint64_t *)calloc(nn, 8);
 #undef TAKE64
 #undef TAKE32
 #define CP64(dst, src) do { if (src) memcpy(s->nd.dst, src, (size_t)n * 8); } while (0)
@@ -1879,6 +1887,7 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   if (nc->taints_hard) memcpy(s->nd.taints_hard, nc->taints_hard, (size_t)n * 8);
   if (nc->taints_soft) memcpy(s->nd.taints_soft, nc->taints_soft, (size_t)n * 8);
   if (nc->labels) memcpy(s->nd.labels, nc->labels, (size_t)n * 8);
+  if (nc->host_ports) memcpy(s->nd.host_ports, nc->host_ports, (size_t)n * 8);
 #undef CP64
 #undef CP32
   s->feasible = (uint8_t *)calloc(nn, 1);
@@ -1903,6 +1912,7 @@ void ko_destroy(ko_sched *s) {
   free(s->nd.taints_hard);
   free(s->nd.taints_soft);
   free(s->nd.labels);
+  free(s->nd.host_ports);
   free(s->traw);
   free(s->araw);
   free(s->q);
@@ -2557,6 +2567,7 @@ int ko_unreserve(ko_sched *s, const ks_pod_cols *pc, const ks_result *r, const u
   d->nz_cpu[n] -= p.nzcpu;
   d->nz_mem[n] -= p.nzmem;
   d->pod_count[n] -= 1;
+  if (s->cfg.nodeports.enable_filter) d->host_ports[n] &= ~p.pwant;
   d->la_term_cpu[n] -= p.est_cpu;
   d->la_term_mem[n] -= p.est_mem;
   if (p.flags & KS_POD_PROD) {
@@ -2673,6 +2684,7 @@ int ko_read_nodes(const ko_sched *s, ks_node_state *o) {
   if (o->la_term_memory) memcpy(o->la_term_memory, s->nd.la_term_mem, b8);
   if (o->la_prod_term_milli_cpu) memcpy(o->la_prod_term_milli_cpu, s->nd.la_pterm_cpu, b8);
   if (o->la_prod_term_memory) memcpy(o->la_prod_term_memory, s->nd.la_pterm_mem, b8);
+  if (o->host_ports) memcpy(o->host_ports, s->nd.host_ports, b8);
   return 0;
 }
 

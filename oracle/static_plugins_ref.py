@@ -11,6 +11,9 @@ Restated from its published source:
     PreScore -- getAllTolerationPreferNoSchedule: tolerations with an empty effect or PreferNoSchedule
     Score    -- countIntolerableTaintsPreferNoSchedule: PreferNoSchedule taints none of those tolerates
     NormalizeScore -- helper.DefaultNormalizeScore(framework.MaxNodeScore, true, scores)
+  plugins/nodeports/node_ports.go
+    Filter   -- fitsPorts: HostPortInfo.CheckConflict(ip, protocol, port) for every wanted port (same protocol and
+                port, and equal host IPs or either 0.0.0.0; ports <= 0 never conflict)
   plugins/nodeaffinity/node_affinity.go
     Filter   -- nodeaffinity.GetRequiredNodeAffinity(pod).Match(node): pod.Spec.NodeSelector AND (OR over the
                 required NodeSelectorTerms; a term with no requirements matches nothing)
@@ -67,11 +70,17 @@ def default_normalize(scores: Sequence[int], reverse: bool) -> List[int]:
     return out
 
 
+def ports_filter(pod: PodAffinitySpec, node: NodeSpec) -> bool:
+    """upstream plugins/nodeports/node_ports.go fitsPorts: no wanted port conflicts with NodeInfo.UsedPorts"""
+    return not any(w.conflicts(u) for w in pod.host_ports for u in node.used_ports)
+
+
 def evaluate(pod: PodAffinitySpec, nodes: Sequence[NodeSpec], feasible_other: Sequence[bool]) -> Tuple[
         List[bool], List[int], List[int]]:
     """Per node: feasible (the other plugins' verdict AND both Filters) and the two normalized scores
     (0 on infeasible nodes)."""
-    feas = [bool(f) and taint_filter(pod, n) and affinity_filter(pod, n) for f, n in zip(feasible_other, nodes)]
+    feas = [bool(f) and taint_filter(pod, n) and affinity_filter(pod, n) and ports_filter(pod, n)
+            for f, n in zip(feasible_other, nodes)]
     idx = [i for i, f in enumerate(feas) if f]
     tn = default_normalize([taint_raw(pod, nodes[i]) for i in idx], True)
     an = default_normalize([affinity_raw(pod, nodes[i]) for i in idx], False)

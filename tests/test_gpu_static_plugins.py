@@ -93,3 +93,34 @@ def test_schedule_with_numa_and_devices(runtime, oracle_lib):
 def test_virtual_shards(runtime, oracle_lib):
     w = synth.with_static_plugins(synth.c1(n_nodes=900, n_pods=600), seed=26)
     run(runtime, oracle_lib, w, "static-vshards", vshards=3)
+
+
+def test_assume_unreserve_ports(runtime, oracle_lib):
+    # per-pod mode: ks_assume adds the pod's host ports to the node (as the oracle's Reserve does), ks_unreserve
+    # removes them again
+    w = synth.with_static_plugins(synth.c1(n_nodes=64, n_pods=200), seed=27)
+    cfg = w.cfg
+    ev = runtime.Evaluator(cfg, w.nodes.copy())
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy())
+    before = ev.read_nodes().host_ports.copy()
+    ports = [i for i in range(w.pods.n) if w.pods.host_ports[i]]
+    assert ports
+    done = []
+    for i in ports[:6]:
+        one = w.pods.rows([i])
+        r_g, s_g, t_g = ev.eval_pod(one)
+        r_o, s_o, t_o = orc.eval_pod(one)
+        assert np.array_equal(r_g, r_o) and np.array_equal(t_g, t_o), f"pod {i}"
+        if not (t_g >= 0).any():
+            continue
+        node = int(np.argmax(t_g))
+        res, cs, na = ev.assume(one, node)
+        orc.assume(one, node)
+        assert_same_state(ev.read_nodes(), orc.read_nodes(), f"assume {i}")
+        assert int(ev.read_nodes().host_ports[node]) & int(w.pods.host_ports[i])
+        done.append((one, res, cs, na))
+    for one, res, cs, na in reversed(done):
+        ev.unreserve(one, res, cs, na)
+    assert np.array_equal(ev.read_nodes().host_ports, before)
+    ev.close()
+    orc.close()

@@ -51,10 +51,10 @@ def test_requirement_cases():
 
 def _profile(fit=False):
     p = SchedulerProfile(fit=None, loadaware=None, taint_toleration=True, node_affinity=True,
-                         taint_toleration_weight=2, node_affinity_weight=3)
+                         taint_toleration_weight=2, node_affinity_weight=3, node_ports=True)
     if fit:
         p = SchedulerProfile(loadaware=None, taint_toleration=True, node_affinity=True,
-                             taint_toleration_weight=2, node_affinity_weight=3)
+                             taint_toleration_weight=2, node_affinity_weight=3, node_ports=True)
     return p
 
 
@@ -76,9 +76,10 @@ def _compare(w, fit: bool, pods=range(60)):
         feas, ts, as_ = ref.evaluate(pspec[i], nspec, other)
         assert list(r == 0) == feas, f"pod {i}: feasibility"
         for n in range(len(nspec)):
-            if r[n] & ~np.uint32(abi.KS_R_TAINT | abi.KS_R_NODE_AFFINITY) == 0 and base is None:
+            if base is None:
                 assert bool(r[n] & abi.KS_R_TAINT) == (not ref.taint_filter(pspec[i], nspec[n]))
                 assert bool(r[n] & abi.KS_R_NODE_AFFINITY) == (not ref.affinity_filter(pspec[i], nspec[n]))
+                assert bool(r[n] & abi.KS_R_NODE_PORTS) == (not ref.ports_filter(pspec[i], nspec[n]))
         assert list(s[:, abi.KS_SCORE_TAINT]) == ts, f"pod {i}: TaintToleration scores"
         assert list(s[:, abi.KS_SCORE_NODE_AFFINITY]) == as_, f"pod {i}: NodeAffinity scores"
         if base is None:
@@ -116,6 +117,32 @@ def test_empty_terms_and_selector():
     # pod 4: affinity raw 5 / 0 -> 100 / 0; taint raw 0 / 1 -> reverse 100 / 0
     r, s, t = orc.eval_pod(pt.rows([4]))
     assert list(s[:, abi.KS_SCORE_NODE_AFFINITY]) == [100, 0] and list(s[:, abi.KS_SCORE_TAINT]) == [100, 0]
+    orc.close()
+
+
+def test_host_port_cases():
+    from koordinator_amd.static_plugins import HostPort
+    any80 = HostPort(80, "", "")
+    assert any80.conflicts(HostPort(80, "TCP", "10.0.0.1")) and HostPort(80, "TCP", "10.0.0.1").conflicts(any80)
+    assert not HostPort(80, "TCP", "10.0.0.1").conflicts(HostPort(80, "TCP", "10.0.0.2"))
+    assert not HostPort(80, "UDP").conflicts(HostPort(80, "TCP"))
+    assert not HostPort(0).conflicts(HostPort(0))  # no host port: never a conflict
+    nodes = [NodeSpec("a", used_ports=[HostPort(80, "TCP", "10.0.0.1")]), NodeSpec("b")]
+    pods = [PodAffinitySpec(host_ports=[HostPort(80, "TCP", "10.0.0.2")]), PodAffinitySpec(host_ports=[any80])]
+    nt = synth.make_nodes(2, np.random.Generator(np.random.PCG64(1)))
+    pt = synth.make_pods(2, np.random.Generator(np.random.PCG64(2)))
+    compile_cluster(nodes, pods, nt, pt)
+    cfg = SchedulerProfile(fit=None, loadaware=None, node_ports=True).to_ks_config()
+    orc = Oracle(cfg, nt)
+    r, _, _ = orc.eval_pod(pt.rows([0]))
+    assert list(r) == [0, 0]
+    r, _, _ = orc.eval_pod(pt.rows([1]))
+    assert list(r) == [abi.KS_R_NODE_PORTS, 0]
+    # schedule both: pod 0 takes 10.0.0.2:80 on node a (lowest index on a tie), pod 1 (0.0.0.0:80) then fits b only
+    res = orc.schedule(pt)
+    assert list(res["node"]) == [0, 1]
+    st = orc.read_nodes()
+    assert int(st.host_ports[0]) == int(nt.host_ports[0]) | int(pt.host_ports[0])
     orc.close()
 
 
