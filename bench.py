@@ -11,8 +11,10 @@ before the timed region (host -> HBM copies are not timed; everything computed f
 The metric names 5k AND 100k nodes, so the same line carries ``c5``: configs[4] (1M pods x 100k nodes,
 Fit + LoadAware) timed the same way — on one GPU at N=1, node-sharded over the N ranks at N>1 (strong
 scaling: every rank sweeps its node range, one RCCL allgather of per-shard candidates per pass).
-At N=1 it also carries ``c3`` (configs[2]: NUMA + DeviceShare joint allocation, 5k nodes) and ``c4`` (configs[3]:
-20k nodes with 50k Reservations), each with its own CPU baseline, sample parity and roofline.
+At N=1 it also carries ``c3`` (configs[2]: NUMA + DeviceShare joint allocation, 5k nodes), ``c4`` (configs[3]:
+20k nodes with 50k Reservations) and ``c2d`` (C2 with the v1beta2 default profile's upstream plugins on as well:
+NodeResourcesBalancedAllocation, TaintToleration, NodeAffinity, NodePorts), each with its own CPU baseline, sample
+parity and roofline.
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU.  ``value`` at N>1 is N
 independent C2 replicas (seed + rank; weak scaling: the 5k-node cluster does not warrant node sharding,
@@ -47,9 +49,9 @@ METRIC = "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k no
 def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
 
-    if name not in ("c1", "c2", "c3", "c4", "c5"):
+    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d"):
         raise SystemExit(f"unknown config {name}")
-    fn = getattr(synth, name)
+    fn = synth.c2_default if name == "c2d" else getattr(synth, name)
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
 
@@ -188,6 +190,9 @@ def sweep_algo_bytes(w, prof, local_nodes: int) -> int:
         # + NUMA amplification columns (16 B) and the device table (flags + 34 total / topology words +
         # 32 used words, int64; ks_dev.h)
         algo += local_nodes * (16 + 4 + (34 + 32) * 8)
+    if prof.taint_toleration or prof.node_affinity or prof.node_ports:
+        # + the TaintToleration / NodeAffinity / NodePorts dictionary words (4 x u64) and the pods' PodStat records
+        algo += local_nodes * 32 + 64 * 112
     if w.reservations is not None:
         # + the owner-class column and the reservation table (CSR offsets, classes, meta, order rank,
         # allocatable/allocated x7, assigned, reserve-pod non-zero x2) read once
@@ -345,7 +350,9 @@ def workload_desc(w):
             f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
             + (f" + Reservation(weight 5000, {w.reservations.r} reservations)" if w.reservations is not None else "")
             + (" + NodeNUMAResource(amplified CPUs, cpuset pods, NUMA topology policies) + DeviceShare(8 GPUs x 80GiB + 4 RDMA on"
-               " 4 PCIe/2 NUMA per node, joint GPU+RDMA)" if w.devices is not None else ""))
+               " 4 PCIe/2 NUMA per node, joint GPU+RDMA)" if w.devices is not None else "")
+            + (" + upstream NodeResourcesBalancedAllocation + TaintToleration + NodeAffinity + NodePorts (v1beta2 default"
+               " plugins)" if w.profile.balanced is not None and w.profile.taint_toleration else ""))
 
 
 def main():
@@ -368,7 +375,7 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
     ap.add_argument("--c5-steps", type=int, default=1)
     ap.add_argument("--c5-warmup", type=int, default=1)
-    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 sub-records")
+    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d sub-records")
     ap.add_argument("--sub-steps", type=int, default=3)
     ap.add_argument("--sub-warmup", type=int, default=1)
     args = ap.parse_args()
@@ -438,7 +445,9 @@ def main():
     if not args.no_sub and world == 1 and args.config == "c2":
         # SURVEY's C3 (NUMA + DeviceShare) and C4 (Reservation) workloads, each timed like the headline with its own
         # CPU baseline, sample parity and commit roofline (single GPU: neither is node-sharded)
-        for sub in ("c3", "c4"):
+        # c2d: C2 under the v1beta2 default profile's upstream plugins as well (BalancedAllocation, TaintToleration,
+        # NodeAffinity, NodePorts)
+        for sub in ("c3", "c4", "c2d"):
             ws = build_workload(sub, seed=20261015)
             rs, ress = run_config(ws, args, None, 1, 0, 0, False, args.sub_steps, args.sub_warmup, sub,
                                   not args.no_profile)

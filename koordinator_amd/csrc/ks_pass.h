@@ -65,8 +65,13 @@ struct SweepArgs {
 };
 
 // local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
+// Fit + LoadAware (FEAT 0, C2 / C5): 4 waves per SIMD (<= 128 VGPRs; the kernel is latency-bound, more waves in
+// flight hide the HBM round trips), the other variants as many as their registers allow.
+#ifndef KS_SWEEP_WAVES
+#define KS_SWEEP_WAVES 4  // (profiles/r03_sweep_w4_ab.txt: C5 sweep 51.1 -> 43.1 us per launch)
+#endif
 template <int NSC, int FEAT>
-__global__ __launch_bounds__(256) void sweep_kernel(SweepArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEAT == 0 ? KS_SWEEP_WAVES : 1))) void sweep_kernel(SweepArgs a) {
   const int lane = threadIdx.x & 63;
   // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar).
   // XCD-aware: blocks are dealt round-robin over the 8 XCDs, so block b works as virtual block

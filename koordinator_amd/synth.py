@@ -579,7 +579,7 @@ def static_specs(n_nodes: int, n_pods: int, rng: np.random.Generator):
             req = [Term([Requirement("node.kubernetes.io/instance-type", "NotIn", (types[rng.integers(0, 3)],)),
                          Requirement("accelerator", "DoesNotExist")])]
         elif u < 0.21:
-            req = [Term([Requirement(FIELD_NAME, "NotIn", (f"node-{int(rng.integers(0, n_nodes))}",), field=True)])]
+            req = [Term([Requirement(FIELD_NAME, "NotIn", (f"node-{int(rng.integers(0, min(n_nodes, 8)))}",), field=True)])]
         pref = []
         if rng.random() < 0.4:
             pref.append((int(rng.integers(1, 101)), Term([Requirement("topology.kubernetes.io/zone", "In",
