@@ -360,7 +360,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d"])
     ap.add_argument("--pods", type=int, default=0, help="pods per step (default: the config's own count)")
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)

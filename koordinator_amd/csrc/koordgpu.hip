@@ -3010,11 +3010,23 @@ static int kernel_feat(const ks_ctx* ctx) {
 }
 
 // the slot device region of the commit kernel: GPU state (DeviceShare), then the TaintToleration / NodeAffinity words
-// and NodePorts words (4 x u64 per slot, the region's last kMaxBatch * 32 B)
-static size_t dev_cache_bytes(const ks_ctx* ctx) {
+// and NodePorts words (4 x u64 per slot, the region's last kMaxBatch * 32 B) after the pass's PodStat records and the
+// normalization maxima table (ks_pass.h commit_kernel)
+static size_t dev_cache_bytes_with(const ks_ctx* ctx, bool stat_lds) {
   return (ctx->kc.dev ? (size_t)kDevLdsStride * (kDevTW + kDevQW) * 8 + (size_t)kMaxBatch * 4 : 0) +
-         (ctx->kc.stat ? (size_t)kMaxBatch * 32 : 0);
+         ((ctx->kc.dev || ctx->kc.stat) ? (size_t)kNormRows * kMaxBatch * 8 : 0) +
+         (ctx->kc.stat ? (size_t)kMaxBatch * 32 : 0) + (stat_lds ? (size_t)kMaxBatch * sizeof(PodStat) : 0);
 }
+
+// The pass's PodStat records go to LDS when the commit image still fits with them (before the quota-row and
+// reservation caches are sized); otherwise the commit reads them from HBM (CommitArgs.stat_lds)
+static bool commit_stat_lds(const ks_ctx* ctx) {
+  if (!ctx->kc.stat) return false;
+  return commit_layout(ctx->k, ctx->nchunks, false, 0, dev_cache_bytes_with(ctx, true), numa_cache_bytes(ctx), ctx->q.q,
+                       kernel_feat(ctx) == 0).total + 64 <= 160 * 1024;
+}
+
+static size_t dev_cache_bytes(const ks_ctx* ctx) { return dev_cache_bytes_with(ctx, commit_stat_lds(ctx)); }
 
 static size_t rsv_cache_bytes(const ks_ctx* ctx, int32_t rcap) {
   return (size_t)kMaxBatch * rcap * 8 * (size_t)(3 + 2 * (3 + ctx->nsc) + 2);  // sizeof(RsvRec<3+nsc>)
@@ -3093,6 +3105,7 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.rcap = commit_rcap(ctx, qcache);
   ca.rsv_bytes = (int32_t)rsv_cache_bytes(ctx, ca.rcap);
   ca.dev_bytes = (int32_t)dev_cache_bytes(ctx);
+  ca.stat_lds = commit_stat_lds(ctx) ? 1 : 0;
   ca.dv = ctx->ddv;
   ca.dev_M = ctx->dev_M;
   ca.cpuset_list = ctx->cpuset_list;

@@ -180,7 +180,8 @@ __device__ __forceinline__ uint64_t mono_rescan(const DevNodes* dnp, const Cfg& 
 }
 
 template <int NSC, bool QC>
-__global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs a) {
+__global__ __launch_bounds__(commit_threads(0)) void commit_mono_kernel(CommitArgs a) {
+  constexpr int NT = commit_threads(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
   const MonoLayout lay = mono_layout(K, a.nchunks, QC, a.q.q);
@@ -238,9 +239,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
 #endif
 
   // ---- prologue: the pass into LDS (all four waves, independent loads in one burst) ----
-  lds_copy(cand_chunk, a.cand_chunk, np * K, tid);
-  lds_copy(cand_t, a.cand_t, np * K, tid);
-  for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += kCommitThreads) {
+  lds_copy<NT>(cand_chunk, a.cand_chunk, np * K, tid);
+  lds_copy<NT>(cand_t, a.cand_t, np * K, tid);
+  for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += NT) {
     const int32_t p = i / KS_QUOTA_DIMS, dd = i - p * KS_QUOTA_DIMS;
     pqreq[i] = a.pq.req[dd][cursor0 + p];
   }
@@ -248,16 +249,16 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
     const int64_t* src = reinterpret_cast<const int64_t*>(a.pods + cursor0);
     int64_t* dst = reinterpret_cast<int64_t*>(spods);
     const int32_t words = np * (int32_t)(sizeof(PodRec) / 8);
-    lds_copy(dst, src, words, tid);
+    lds_copy<NT>(dst, src, words, tid);
   }
-  for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
+  for (int64_t c = tid; c < a.nchunks; c += NT) touched[c] = 0ull;
   if (QC) {
-    for (int32_t r = tid; r < a.q.q; r += kCommitThreads) {
+    for (int32_t r = tid; r < a.q.q; r += NT) {
       qlds->parent[r] = a.q.parent[r];
       qlds->limit_mask[r] = a.q.limit_mask[r];
       qlds->min_mask[r] = a.q.min_mask[r];
     }
-    for (int32_t i = tid; i < a.q.q * KS_QUOTA_DIMS; i += kCommitThreads) {
+    for (int32_t i = tid; i < a.q.q * KS_QUOTA_DIMS; i += NT) {
       qlds->limit[i] = a.q.limit[i];
       qlds->used[i] = a.q.used[i];
       qlds->min[i] = a.q.min[i];
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
   }
   // raw rows of every pod's top node (a node shared by several pods is loaded once per pod: no dependency on
   // the owner computation, which runs while these loads are in flight)
-  lds_rawtop(rawtop, a.cand_top, a.rowcols, np, tid);
+  lds_rawtop<NT>(rawtop, a.cand_top, a.rowcols, np, tid);
   if (tid < kMaxBatch) {
     const uint64_t t = tid < np ? a.cand_top[tid] : 0ull;
     top_node[tid] = t ? (int32_t)gkey_node(t) : -1;
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
   constexpr int kRoles = MT_N + MF_N + 1;
   // every top row (role per thread); wave 0 also finds each pod's owner: the first pod of the pass with the same
   // top node, whose row the slot of that node uses
-  for (int32_t i = tid; i < np * kRoles; i += kCommitThreads) {
+  for (int32_t i = tid; i < np * kRoles; i += NT) {
     const int32_t p = i / kRoles, role = i - p * kRoles;
     if (top_node[p] >= 0) mono_build(cfg, rows[p], rawtop + p * 32, role, mono_role(role));
   }
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_mono_kernel(CommitArgs 
     reinterpret_cast<int32_t*>(top_node + 2 * kMaxBatch)[lane] = a.rowcols[lane].width;
   }
   __syncthreads();
-  if (tid >= 64) return;  // waves 1-3 are done; wave 0 runs the sequential loop alone
+  if (tid >= 64) return;  // the other waves are done; wave 0 runs the sequential loop alone
   int32_t my_cnt = 0, my_quota = -1, my_tn = -1, my_own = 0;
   uint32_t my_flags = 0, my_pmask = 0;
   uint64_t my_bound = 0, my_top = 0;

@@ -255,7 +255,14 @@ __host__ __device__ inline CandSlot cand_slot_layout(int32_t k) {
 // Reserve, and the row of pod j+1's best untouched candidate is put in flight from HBM then.
 
 constexpr int kQuotaLdsRows = 128;  // quota tables up to this size are cached in LDS for the pass
-constexpr int kCommitThreads = 256; // 4 waves load the pass; wave 0 alone runs the sequential loop
+// Threads of a commit workgroup: its waves load the pass into LDS together, then wave 0 alone runs the sequential
+// loop.  The Fit + LoadAware [+ ElasticQuota] kernels fit 2 waves per SIMD (<= 256 VGPRs), so they load with 8 waves;
+// the other variants use every register of a SIMD (1 wave each).
+constexpr int kCommitThreads = 256;
+#ifndef KS_COMMIT_THREADS0
+#define KS_COMMIT_THREADS0 512
+#endif
+__host__ __device__ constexpr int commit_threads(int feat) { return feat == 0 ? KS_COMMIT_THREADS0 : 256; }
 
 // fields of a raw node row (lane f of a row load holds field f)
 enum RowField : int {
@@ -325,6 +332,7 @@ struct CommitArgs {
   int32_t rsv_bytes;   // LDS bytes of the slot reservation cache (commit_layout)
   int32_t dev_bytes;   // LDS bytes of the slot GPU state (commit_layout)
   int32_t numa_bytes;  // LDS bytes of the slot NUMA-node state (commit_layout)
+  int32_t stat_lds;    // the pass's PodStat records are staged in LDS (else read from pstat in HBM)
   // Pipelined passes: the first pod the pass's sweep was run for; the pass is a no-op (a bubble) when
   // the real cursor is elsewhere (the previous pass was cut).  NULL = not pipelined.
   const int32_t* pipe_base;
@@ -587,33 +595,34 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
 // thread), so a pass's candidate lists, pod records and top-node raw rows arrive in a few HBM round trips rather
 // than one per 256 elements.
 constexpr int kPro = 8;
-template <typename T>
+template <int NT = kCommitThreads, typename T>
 __device__ __forceinline__ void lds_copy(T* dst, const T* src, int32_t n, int tid) {
-  for (int32_t i0 = tid; i0 < n; i0 += kCommitThreads * kPro) {
+  for (int32_t i0 = tid; i0 < n; i0 += NT * kPro) {
     T v[kPro];
 #pragma unroll
     for (int u = 0; u < kPro; ++u) {
-      const int32_t i = i0 + u * kCommitThreads;
+      const int32_t i = i0 + u * NT;
       if (i < n) v[u] = src[i];
     }
 #pragma unroll
     for (int u = 0; u < kPro; ++u) {
-      const int32_t i = i0 + u * kCommitThreads;
+      const int32_t i = i0 + u * NT;
       if (i < n) dst[i] = v[u];
     }
   }
 }
 
 // rawtop[p * 32 + f] = raw row field f of pod p's snapshot-best node (pods without a feasible node: untouched)
+template <int NT = kCommitThreads>
 __device__ __forceinline__ void lds_rawtop(int64_t* rawtop, const uint64_t* cand_top, const RowCol* rowcols, int32_t np,
                                            int tid) {
   const int32_t n = np * RF_N;
-  for (int32_t i0 = tid; i0 < n; i0 += kCommitThreads * kPro) {
+  for (int32_t i0 = tid; i0 < n; i0 += NT * kPro) {
     uint64_t t[kPro];
     RowCol rc[kPro];
 #pragma unroll
     for (int u = 0; u < kPro; ++u) {
-      const int32_t i = i0 + u * kCommitThreads;
+      const int32_t i = i0 + u * NT;
       t[u] = 0;
       if (i < n) {
         const int32_t p = i / RF_N, f = i - p * RF_N;
@@ -626,7 +635,7 @@ __device__ __forceinline__ void lds_rawtop(int64_t* rawtop, const uint64_t* cand
     for (int u = 0; u < kPro; ++u) v[u] = t[u] ? load_field(rc[u].p, rc[u].width, gkey_node(t[u])) : 0;
 #pragma unroll
     for (int u = 0; u < kPro; ++u) {
-      const int32_t i = i0 + u * kCommitThreads;
+      const int32_t i = i0 + u * NT;
       if (i < n && t[u]) {
         const int32_t p = i / RF_N, f = i - p * RF_N;
         rawtop[p * 32 + f] = v[u];
@@ -636,7 +645,8 @@ __device__ __forceinline__ void lds_rawtop(int64_t* rawtop, const uint64_t* cand
 }
 
 template <int NSC, bool QC, int FEAT>
-__global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
+__global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs a) {
+  constexpr int NT = commit_threads(FEAT);
   constexpr bool RSV = (FEAT & 1) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
@@ -671,7 +681,15 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   int64_t* snp = reinterpret_cast<int64_t*>(smem_raw + lay.snp);  // [slot][kNumaSlotWords]
   // per slot: the node's dictionary-bit plugin words (taints hard, soft, labels, host ports -- the last one updated
   // by every Reserve of the pass): the last kMaxBatch * 32 B of the slot device region (dev_cache_bytes)
-  uint64_t* sstat = reinterpret_cast<uint64_t*>(smem_raw + lay.sdev + a.dev_bytes - (size_t)kMaxBatch * 32);
+  // and before them the pass's PodStat records (Cfg.stat), and before those the normalization maxima table
+  // ([kNormRows][kMaxBatch], DeviceShare variants): dev_cache_bytes
+  // (the PodStat records only with CommitArgs.stat_lds)
+  unsigned char* const sdev_end = smem_raw + lay.sdev + a.dev_bytes;
+  uint64_t* sstat = reinterpret_cast<uint64_t*>(sdev_end - (size_t)kMaxBatch * 32);
+  unsigned char* sp = a.c.stat ? reinterpret_cast<unsigned char*>(sstat) : sdev_end;
+  PodStat* spstat = reinterpret_cast<PodStat*>(sp - (size_t)kMaxBatch * sizeof(PodStat));
+  if (a.stat_lds) sp = reinterpret_cast<unsigned char*>(spstat);
+  uint64_t* snorm = reinterpret_cast<uint64_t*>(sp - (size_t)kNormRows * kMaxBatch * 8);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -709,30 +727,38 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
 #endif
 
   // ---- load the pass into LDS with all four waves (independent loads, one burst) ----
-  lds_copy(cand_chunk, a.cand_chunk, np * K, tid);
-  lds_copy(cand_t, a.cand_t, np * K, tid);
-  for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += kCommitThreads) {
+  lds_copy<NT>(cand_chunk, a.cand_chunk, np * K, tid);
+  lds_copy<NT>(cand_t, a.cand_t, np * K, tid);
+  for (int32_t i = tid; i < np * KS_QUOTA_DIMS; i += NT) {
     const int32_t p = i / KS_QUOTA_DIMS, dd = i - p * KS_QUOTA_DIMS;
     pqreq[i] = a.pq.req[dd][cursor0 + p];
+  }
+  if (DEV) {
+    // the normalization maxima and the PodStat records in LDS (read per pod, not held in registers: these variants
+    // are register-bound)
+    lds_copy<NT>(snorm, reinterpret_cast<const uint64_t*>(a.dev_M), kNormRows * kMaxBatch, tid);
+    if (a.stat_lds)
+      lds_copy<NT>(reinterpret_cast<int64_t*>(spstat), reinterpret_cast<const int64_t*>(a.pstat + cursor0),
+                   np * (int32_t)(sizeof(PodStat) / 8), tid);
   }
   {
     const int64_t* src = reinterpret_cast<const int64_t*>(a.pods + cursor0);
     int64_t* dst = reinterpret_cast<int64_t*>(spods);
     const int32_t words = np * (int32_t)(sizeof(PodRec) / 8);
-    lds_copy(dst, src, words, tid);
+    lds_copy<NT>(dst, src, words, tid);
   }
-  for (int64_t c = tid; c < a.nchunks; c += kCommitThreads) touched[c] = 0ull;
+  for (int64_t c = tid; c < a.nchunks; c += NT) touched[c] = 0ull;
   // raw rows of every pod's snapshot-best node (the monotone fast path's winner) and second-best node (the usual
   // winner of a pod whose top an earlier pod took): all loads in flight together
-  lds_rawtop(rawtop, a.cand_top, a.rowcols, np, tid);
-  if (FEAT == 0) lds_rawtop(rawrun, a.cand_second, a.rowcols, np, tid);
+  lds_rawtop<NT>(rawtop, a.cand_top, a.rowcols, np, tid);
+  if (FEAT == 0) lds_rawtop<NT>(rawrun, a.cand_second, a.rowcols, np, tid);
   if (QC) {
-    for (int32_t r = tid; r < a.q.q; r += kCommitThreads) {
+    for (int32_t r = tid; r < a.q.q; r += NT) {
       qlds->parent[r] = a.q.parent[r];
       qlds->limit_mask[r] = a.q.limit_mask[r];
       qlds->min_mask[r] = a.q.min_mask[r];
     }
-    for (int32_t i = tid; i < a.q.q * KS_QUOTA_DIMS; i += kCommitThreads) {
+    for (int32_t i = tid; i < a.q.q * KS_QUOTA_DIMS; i += NT) {
       qlds->limit[i] = a.q.limit[i];
       qlds->used[i] = a.q.used[i];
       qlds->min[i] = a.q.min[i];
@@ -742,17 +768,13 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
   // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
   int32_t my_cnt = 0, my_quota = -1;
   uint32_t my_flags = 0, my_pmask = 0;
-  uint64_t my_bound = 0, my_top = 0, my_devM = 0, my_second = 0, my_tM = 0, my_aM = 0;
+  uint64_t my_bound = 0, my_top = 0, my_second = 0;
   if (tid < 64 && lane < np) {
     my_cnt = a.cand_count[lane];
     my_bound = a.cand_bound[lane];
     my_top = a.cand_top[lane];
     if (FEAT == 0) my_second = a.cand_second[lane];
-    if (DEV) my_devM = a.dev_M[lane];
-    if (DEV && a.c.stat) {
-      my_tM = a.dev_M[kMaxBatch + lane];
-      my_aM = a.dev_M[2 * kMaxBatch + lane];
-    }
+
     my_pmask = a.pq.mask[cursor0 + lane];
     my_quota = a.pods[cursor0 + lane].quota;
     my_flags = a.pods[cursor0 + lane].flags;
@@ -765,7 +787,7 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     my_w = a.rowcols[lane].width;
   }
   __syncthreads();
-  if (tid >= 64) return;  // waves 1-3 are done; wave 0 runs the sequential loop alone
+  if (tid >= 64) return;  // the other waves are done; wave 0 runs the sequential loop alone
   KS_STAMP(0);
   // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
   // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
@@ -905,8 +927,8 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
     {
     uint64_t best;
     NormM Muse{0, 0, 0};  // normalization maxima used for this pod
-    PodStat pst{};        // TaintToleration / NodeAffinity inputs (Cfg.stat)
-    if (DEV && cfg.stat) pst = load_stat_uniform(a.pstat + cursor0 + j);
+    // TaintToleration / NodeAffinity / NodePorts inputs (Cfg.stat), in LDS when they fit
+    const PodStat& pst = a.stat_lds ? spstat[j] : a.pstat[cursor0 + j];
     if (cj.fast) {
       best = cj.umax;  // the snapshot-best node is untouched: commits only lower keys, so it wins
       ++fast;
@@ -923,6 +945,10 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
       if (lane < nslots) {
+        // the dictionary-bit plugins first: three words out, their temporaries dead before eval_full's peak
+        EvalOut so{};
+        if (DEV && cfg.stat)
+          stat_eval(cfg, pst, sstat[4 * lane], sstat[4 * lane + 1], sstat[4 * lane + 2], sstat[4 * lane + 3], so);
         NodeReg<NSC> r;
         slot_to_reg<NSC>(rows[lane], r);
         r.rsv_cls = scls[lane];
@@ -946,8 +972,11 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
             },
             [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
             [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
-        if (DEV && cfg.stat)
-          stat_eval(cfg, pst, sstat[4 * lane], sstat[4 * lane + 1], sstat[4 * lane + 2], sstat[4 * lane + 3], o);
+        if (DEV && cfg.stat) {
+          o.reasons |= so.reasons;
+          o.traw = so.traw;
+          o.araw = so.araw;
+        }
         feas = o.reasons == 0;
         if ((FEAT & 2) && cfg.cores && (cw & kCoresDirty) && feas)
           unk = ((pod.flags & KS_POD_CPU_BIND) && (pod.cpu_bind & KS_CPU_BIND_REQUIRED)) ||
@@ -971,9 +1000,9 @@ __global__ __launch_bounds__(kCommitThreads) void commit_kernel(CommitArgs a) {
           if (wt ? (Mt != Msw) : (Mt > Msw)) cut = true;
           return Msw;
         };
-        if (cfg.dev) Muse.dev = norm1(readlane64(my_devM, j), o.dev_raw);
-        if (cfg.taint & 2) Muse.taint = norm1(readlane64(my_tM, j), o.traw);
-        if (cfg.aff & 2) Muse.aff = norm1(readlane64(my_aM, j), o.araw);
+        if (cfg.dev) Muse.dev = norm1(snorm[j], o.dev_raw);
+        if (cfg.taint & 2) Muse.taint = norm1(snorm[kMaxBatch + j], o.traw);
+        if (cfg.aff & 2) Muse.aff = norm1(snorm[2 * kMaxBatch + j], o.araw);
         if (cut) {
           processed = j;
           break;

@@ -23,8 +23,8 @@ hipError_t sweep(int blocks, hipStream_t s, const SweepArgs& a) {
 }
 
 hipError_t commit(bool qc, size_t smem, hipStream_t s, const CommitArgs& a) {
-  if (qc) hipLaunchKernelGGL((commit_kernel<NSC, true, F>), dim3(1), dim3(kCommitThreads), smem, s, a);
-  else hipLaunchKernelGGL((commit_kernel<NSC, false, F>), dim3(1), dim3(kCommitThreads), smem, s, a);
+  if (qc) hipLaunchKernelGGL((commit_kernel<NSC, true, F>), dim3(1), dim3(commit_threads(F)), smem, s, a);
+  else hipLaunchKernelGGL((commit_kernel<NSC, false, F>), dim3(1), dim3(commit_threads(F)), smem, s, a);
   return hipGetLastError();
 }
 
@@ -36,8 +36,8 @@ hipError_t commit_attr(bool qc, size_t smem) {
 #if KS_FEAT == 0
 // the monotone Fit + LoadAware [+ ElasticQuota] commit (ks_mono.h)
 hipError_t commit_mono(bool qc, size_t smem, hipStream_t s, const CommitArgs& a) {
-  if (qc) hipLaunchKernelGGL((commit_mono_kernel<NSC, true>), dim3(1), dim3(kCommitThreads), smem, s, a);
-  else hipLaunchKernelGGL((commit_mono_kernel<NSC, false>), dim3(1), dim3(kCommitThreads), smem, s, a);
+  if (qc) hipLaunchKernelGGL((commit_mono_kernel<NSC, true>), dim3(1), dim3(commit_threads(0)), smem, s, a);
+  else hipLaunchKernelGGL((commit_mono_kernel<NSC, false>), dim3(1), dim3(commit_threads(0)), smem, s, a);
   return hipGetLastError();
 }
 
