@@ -402,8 +402,11 @@ __device__ __forceinline__ QuotaRowsLds quota_lds(unsigned char* p, int32_t q) {
   return v;
 }
 
+constexpr size_t kHelpBytes = (size_t)kMaxBatch * 8 + 16 + 16;
+
 struct CommitLayout {
-  size_t rows, pods, res, raw, rawtop, rawrun, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, touched, total;
+  size_t rows, pods, res, raw, rawtop, rawrun, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, help,
+      touched, total;
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
@@ -447,6 +450,8 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   o += align16(numa_bytes);    // per slot: NUMA-node totals / used / offsets + policy, count, present (ks_numa.h)
   L.quota = o;
   if (qc) o += align16(quota_lds_bytes(qrows));
+  L.help = o;
+  o += kHelpBytes;  // slot-row hand-off to the builder wave (FEAT 0): descriptors, issued count, done flag, ready mask
   L.touched = o;
   o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
   L.total = o;
@@ -690,6 +695,18 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   PodStat* spstat = reinterpret_cast<PodStat*>(sp - (size_t)kMaxBatch * sizeof(PodStat));
   if (a.stat_lds) sp = reinterpret_cast<unsigned char*>(spstat);
   uint64_t* snorm = reinterpret_cast<uint64_t*>(sp - (size_t)kNormRows * kMaxBatch * 8);
+  // Fit + LoadAware [+ ElasticQuota] (FEAT 0): wave 1 builds the slot rows of new slots whose node row was
+  // prefetched (the pod's top or second-best node) while wave 0 goes on with the next pods; wave 0 waits for a
+  // row only where it reads one (a later pod's slot evaluation, a Reserve onto the slot, the write-back).
+#ifdef KS_NO_HELP
+  constexpr bool HELP = false;  // (A/B builds)
+#else
+  constexpr bool HELP = FEAT == 0;
+#endif
+  int2* hdesc = reinterpret_cast<int2*>(smem_raw + lay.help);  // [issue order] {node, slot | pod << 8 | second << 16}
+  int32_t* hpend = reinterpret_cast<int32_t*>(smem_raw + lay.help + (size_t)kMaxBatch * 8);  // descriptors issued
+  int32_t* hdone = hpend + 1;                                                                // wave 0 is done
+  unsigned long long* hready = reinterpret_cast<unsigned long long*>(smem_raw + lay.help + (size_t)kMaxBatch * 8 + 16);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -786,8 +803,13 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     my_col = a.rowcols[lane].p;
     my_w = a.rowcols[lane].width;
   }
+  if (HELP && tid == 0) {
+    *hpend = 0;
+    *hdone = 0;
+    *hready = 0ull;
+  }
   __syncthreads();
-  if (tid >= 64) return;  // the other waves are done; wave 0 runs the sequential loop alone
+  if (tid >= (HELP ? 128 : 64)) return;  // the other waves are done; wave 0 runs the sequential loop alone
   KS_STAMP(0);
   // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
   // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
@@ -830,6 +852,63 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   }
   constexpr int kLaneCounts = ST_N;  // lane: pod count / flags of the row
   const bool monotone = cfg.monotone != 0;
+
+  if (HELP && tid >= 64) {
+    // ---- wave 1: the slot-row builder (runs until wave 0 is done and every descriptor is built) ----
+    int32_t next = 0;
+    for (;;) {
+      const int32_t pend =
+          __builtin_amdgcn_readfirstlane(__hip_atomic_load(hpend, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (next < pend) {
+        const int2 d = hdesc[next];
+        const int32_t w = __builtin_amdgcn_readfirstlane(d.y);
+        const int32_t s = w & 0xFF, jj = (w >> 8) & 0xFF;
+        const int64_t* src = (((w >> 16) & 1) ? rawrun : rawtop) + jj * 32;
+        const int64_t* podw = reinterpret_cast<const int64_t*>(&spods[jj]);
+        const uint32_t pflags = __builtin_amdgcn_readfirstlane(spods[jj].flags);
+        const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+        const int64_t f_cap = src[t_cap], f_req = src[t_req], f_pw = podw[t_pw];
+        const int64_t u_bits = src[RF_LA_BITS], u_allowed = src[RF_ALLOWED], u_pods = src[RF_POD_COUNT];
+        const int64_t u_acpu = src[RF_ALLOC_CPU], u_amem = src[RF_ALLOC_MEM], u_aeph = src[RF_ALLOC_EPH];
+        SlotRow* row = &rows[s];
+        const int64_t cap = f_cap, req = f_req + (take ? f_pw : 0);
+        if (lane < ST_N) {
+          Term t;
+          t.c = cap;
+          t.h = cap - req + ((cap != 0 || !t_score) ? 0 : kNoCap);
+          t.hd = cap != 0 ? (double)(cap - req) * 100.0 : 0.0;
+          t.r = cap != 0 ? 1.0 / (double)cap : 0.0;
+          row->t[lane] = t;
+        } else if (lane == kLaneCounts) {
+          row->la_bits = (uint32_t)u_bits;
+          row->allowed = (int32_t)u_allowed;
+          row->pod_count = (int32_t)u_pods + 1;
+          row->fit_ws = (u_acpu != 0 ? cfg.fw_cpu : 0) + (u_amem != 0 ? cfg.fw_mem : 0) + (u_aeph != 0 ? cfg.fw_eph : 0);
+        }
+        if (lane == 0)
+          __hip_atomic_fetch_or(hready, 1ull << s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ++next;
+        continue;
+      }
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) &&
+          next >= __builtin_amdgcn_readfirstlane(__hip_atomic_load(hpend, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)))
+        break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return;
+  }
+  int32_t hn = 0;        // descriptors issued to wave 1
+  uint64_t hown = 0;     // slots whose rows wave 0 built itself
+  // wave 0: every row of `need` is built (wave 1's ready mask or its own)
+  auto wait_rows = [&](uint64_t need) {
+    if (!HELP || (hown & need) == need) return;
+    for (;;) {
+      const uint64_t r =
+          readlane64(__hip_atomic_load(hready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP), 0) | hown;
+      if ((r & need) == need) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
 
   int32_t snode = -1;  // lane s: node of slot s
   int32_t nslots = 0;
@@ -944,6 +1023,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       EvalOut o{};
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
+      wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
       if (lane < nslots) {
         // the dictionary-bit plugins first: three words out, their temporaries dead before eval_full's peak
         EvalOut so{};
@@ -1078,6 +1158,18 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         }
         if (lane < RF_N) raw[lane] = v;
       }
+      if (HELP && src != raw) {
+        // the row comes from a prefetched node row: wave 1 builds it
+        if (lane == s) snode = node;
+        if (lane == 0) {
+          atomicOr(&touched[node >> 6], 1ull << (node & 63));
+          hdesc[hn] = make_int2(node, s | (j << 8) | (src == rawtop + j * 32 ? 0 : (1 << 16)));
+          __hip_atomic_store(hpend, hn + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        ++hn;
+        goto row_done;
+      }
+      if (HELP) hown |= 1ull << s;
       // Every field this slot needs is read before the first LDS write: the compiler cannot prove the
       // slot writes do not alias `src`, so each read after a write would cost a full LDS round trip.
       const bool take = !t_prod_only || (pflags & KS_POD_PROD);  // (before the Reservation match below)
@@ -1185,6 +1277,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       }
     } else {
       KS_CAT(3);
+      wait_rows(1ull << s);
       if (cpubind && (int32_t)snuma[4 * s + 3] < cpu_need) {
         if (lane == 0) sres[j] = ks_result{node, KS_S_RESERVE_FAILED, 0, -1, 0, 0, 0};
         goto next_pod;
@@ -1198,6 +1291,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         if (!rsvc) row->pod_count += 1;
       }
     }
+  row_done:
     KS_STAMP(4);
     int32_t nom_row = -1;
     int64_t fitla_pref = -1;  // Fit + LoadAware total of a preferred (ordered) chosen node
@@ -1454,6 +1548,10 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 #endif
   }
   KS_STAMP(6);
+  if (HELP) {
+    if (lane == 0) __hip_atomic_store(hdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
+  }
   // ---- write back: results, touched rows, quota usage ----
   if (lane < processed) a.results[cursor0 + lane] = sres[lane];
   if (lane < nslots) {
