@@ -65,13 +65,15 @@ struct SweepArgs {
 };
 
 // local key: ((total+1) << 6) | (63 - lane); 0 = no feasible node.  Max = best score, lowest lane.
-// Fit + LoadAware (FEAT 0, C2 / C5): 4 waves per SIMD (<= 128 VGPRs; the kernel is latency-bound, more waves in
-// flight hide the HBM round trips), the other variants as many as their registers allow.
+// Fit + LoadAware (FEAT 0, C2 / C5) with up to two scalar slots: 4 waves per SIMD (<= 128 VGPRs; the kernel is
+// latency-bound, more waves in flight hide the HBM round trips), the other variants as many as their registers allow
+// (NSC 4 would spill inside the node loop at 128).
 #ifndef KS_SWEEP_WAVES
 #define KS_SWEEP_WAVES 4  // (profiles/r03_sweep_w4_ab.txt: C5 sweep 51.1 -> 43.1 us per launch)
 #endif
 template <int NSC, int FEAT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEAT == 0 ? KS_SWEEP_WAVES : 1))) void sweep_kernel(SweepArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((FEAT == 0 && NSC <= 2) ? KS_SWEEP_WAVES : 1)))
+void sweep_kernel(SweepArgs a) {
   const int lane = threadIdx.x & 63;
   // wave-uniform work indices (readfirstlane: the compiler keeps the pod loop and its records scalar).
   // XCD-aware: blocks are dealt round-robin over the 8 XCDs, so block b works as virtual block
@@ -140,7 +142,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEAT == 0 ?
   }
   const int64_t nwork = nitems * groups;
   for (int64_t w = wave; w < nwork; w += nwaves) {
-    const int64_t lc = w / groups;  // chunk within this shard's range (or entry of the fix list)
+    // (32-bit, with the divisor opaque per item: a hoisted reciprocal would be one more value live across the loop)
+    int32_t gdiv = groups;
+    asm volatile("" : "+s"(gdiv));
+    const int64_t lc = (int64_t)((uint32_t)w / (uint32_t)gdiv);  // chunk within this shard's range (or fix-list entry)
     const int64_t c = a.fix ? (int64_t)(__builtin_amdgcn_readfirstlane(a.fix[1 + lc]) >> 6) : a.c0 + lc;
     if (a.fix && (c < a.c0 || c >= a.c1)) continue;  // another shard's chunk
     const int32_t g = (int32_t)(w - lc * groups);
@@ -216,7 +221,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FEAT == 0 ?
       second = (lane == p) ? m2 : second;
     }
     if ((FEAT & 4) && a.phase == 0) continue;
-    if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
+    if (lane >= p0 && lane < p1) {
+      // (the lane's row offset is recomputed per work item: hoisted out of the loop it is a 64-bit value live across
+      // it, which at 4 waves per SIMD the compiler spills to scratch -- one scratch write per wave, in HBM traffic)
+      int32_t ln = lane;
+      asm volatile("" : "+v"(ln));
+      a.out[(size_t)ln * a.nchunks + c] = make_uint2(best, second);
+    }
   }
 }
 
