@@ -156,3 +156,27 @@ def test_refusals():
     with pytest.raises(StaticPluginError):
         compile_cluster([NodeSpec("a")], [PodAffinitySpec(required=[Term([Requirement("z", "Gt", ("x",))])])],
                         NodeTable(1), PodTable(1))
+
+
+def test_schedule_against_restatement():
+    # whole queues, one pod at a time: the C oracle (bit masks, ko_schedule) against a sequential loop over the
+    # restatement on raw objects -- Filter, normalized Scores, selectHost (max total, lowest index), and NodePorts'
+    # Reserve (the placed pod's host ports join the node's UsedPorts) -- with only these plugins enabled
+    import copy
+    w = synth.with_static_plugins(synth.c1(n_nodes=40, n_pods=160), seed=13)
+    nspec, pspec = copy.deepcopy(w.specs[0]), w.specs[1]
+    cfg = _profile().to_ks_config()  # taint x2, affinity x3, ports
+    orc = Oracle(cfg, w.nodes.copy())
+    got = orc.schedule(w.pods)
+    orc.close()
+    for i, p in enumerate(pspec):
+        feas, ts, as_ = ref.evaluate(p, nspec, [True] * len(nspec))
+        totals = [2 * a + 3 * b if f else -1 for a, b, f in zip(ts, as_, feas)]
+        best = max(totals)
+        want = totals.index(best) if best >= 0 else -1
+        assert int(got["node"][i]) == want, f"pod {i}"
+        if want >= 0:
+            assert int(got["score"][i]) == best
+            nspec[want].used_ports = list(nspec[want].used_ports) + [h.sanitized() for h in p.host_ports if h.port > 0]
+        else:
+            assert int(got["status"][i]) == abi.KS_S_UNSCHEDULABLE
