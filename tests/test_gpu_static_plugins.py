@@ -124,3 +124,55 @@ def test_assume_unreserve_ports(runtime, oracle_lib):
     assert np.array_equal(ev.read_nodes().host_ports, before)
     ev.close()
     orc.close()
+
+
+def test_node_deltas(runtime, oracle_lib):
+    # informer deltas: nodes gain / lose taints, labels and used host ports (ks_update_nodes with the recompiled
+    # dictionary words, the dictionaries kept) between two queues; the second queue must match the oracle loaded
+    # with the merged table (post-queue state + the changed rows)
+    from koordinator_amd.static_plugins import PREFER_NO_SCHEDULE, build_dictionaries, compile_cluster
+    w = synth.with_static_plugins(synth.c1(n_nodes=400, n_pods=900), seed=28)
+    nspec, pspec = w.specs
+    d0 = build_dictionaries(nspec, pspec)
+    cfg = w.cfg
+    ev = runtime.Evaluator(cfg, w.nodes.copy())
+    first = w.pods.rows(range(0, 450))
+    second = w.pods.rows(range(450, 900))
+    ev.schedule(first)
+    orc0 = oracle_lib.Oracle(cfg, w.nodes.copy())
+    orc0.schedule(first)
+    st = orc0.read_nodes()
+    orc0.close()
+    soft = [t for t in d0.taints if t.effect == PREFER_NO_SCHEDULE]
+    assert soft and d0.ports
+    rng = np.random.Generator(np.random.PCG64(29))
+    idx = np.sort(rng.choice(w.nodes.n, 60, replace=False))
+    for i in idx:
+        nd = nspec[i]
+        nd.taints = [] if nd.taints else [soft[0]]
+        nd.labels = dict(nd.labels)
+        z = nd.labels.get("topology.kubernetes.io/zone")
+        nd.labels["topology.kubernetes.io/zone"] = "zone-b" if z == "zone-a" else "zone-a"
+        nd.used_ports = [] if nd.used_ports else [d0.ports[0]]
+    tmpn = w.nodes.copy()
+    pods2 = w.pods.rows(range(w.pods.n))
+    compile_cluster(nspec, pspec, tmpn, pods2, dicts=d0)
+    assert np.array_equal(pods2.tolerated, w.pods.tolerated)  # same dictionaries: the staged pods stay valid
+    merged = w.nodes.copy()
+    for k, v in st.as_dict().items():  # the post-queue node state
+        if k == "req_scalar":
+            merged.req_scalar[:] = v
+        else:
+            setattr(merged, k, np.asarray(v).astype(getattr(merged, k).dtype))
+    for k in ("taints_hard", "taints_soft", "labels", "host_ports"):
+        col = getattr(merged, k).copy()
+        col[idx] = getattr(tmpn, k)[idx]
+        setattr(merged, k, col)
+    ev.update_nodes(idx, merged.rows(idx))
+    got = ev.schedule(second)
+    orc = oracle_lib.Oracle(cfg, merged.copy())
+    want = orc.schedule(second)
+    assert_same_results(got, want, "static-deltas")
+    assert_same_state(ev.read_nodes(), orc.read_nodes(), "static-deltas")
+    ev.close()
+    orc.close()
