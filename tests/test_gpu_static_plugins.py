@@ -45,6 +45,7 @@ def test_eval_pod(runtime, oracle_lib):
     cfg = w.cfg
     ev = runtime.Evaluator(cfg, w.nodes)
     orc = oracle_lib.Oracle(cfg, w.nodes)
+    seen = 0
     for i in range(w.pods.n):
         one = w.pods.rows([i])
         r_g, s_g, t_g = ev.eval_pod(one)
@@ -52,7 +53,10 @@ def test_eval_pod(runtime, oracle_lib):
         assert np.array_equal(r_g, r_o), f"pod {i}: reasons"
         assert np.array_equal(s_g, s_o), f"pod {i}: scores"
         assert np.array_equal(t_g, t_o), f"pod {i}: totals"
-    assert (r_o & abi.KS_R_TAINT).any() or True
+        seen |= int(np.bitwise_or.reduce(r_g))
+    # every Filter of the three plugins rejected some (pod, node)
+    for bit in (abi.KS_R_TAINT, abi.KS_R_NODE_AFFINITY, abi.KS_R_NODE_PORTS):
+        assert seen & bit, hex(bit)
     ev.close()
     orc.close()
 
