@@ -763,6 +763,14 @@ int ks_set_pipeline(ks_ctx *ctx, int32_t mode);
  * (exercises the merge on one GPU). */
 int ks_shard_unique_id(uint8_t *out /* KS_SHARD_ID_BYTES */);
 int ks_shard_init(ks_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *unique_id, int32_t virtual_shards);
+/* Test transport for the nranks > 1 path without RCCL: ctxs[0..nranks) (contexts of this process, each loaded with the
+ * same node table, batch and candidate count) become ranks 0..nranks-1 of one sharded group whose candidate allgather
+ * and normalization-max all-reduce are device copies between the contexts' buffers, ordered by host barriers and HIP
+ * events.  Every rank's ks_schedule* must then be called concurrently, each from its own host thread (a rank waits at
+ * most 120 s for its peers, then fails with KS_EHIP).  Everything else -- rank chunk ranges, the rank-offset gather
+ * slots, merge_kernel, the replicated commits -- is the RCCL path's code.  ks_shard_init or ks_destroy leaves the
+ * group. */
+int ks_shard_init_loopback(ks_ctx *const *ctxs, int32_t nranks, int32_t virtual_shards);
 
 #ifdef __cplusplus
 }

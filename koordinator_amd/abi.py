@@ -470,5 +470,6 @@ EXPORTED_SYMBOLS = [
     "ks_set_pipeline",
     "ks_shard_unique_id",
     "ks_shard_init",
+    "ks_shard_init_loopback",
 ]
 KS_SHARD_ID_BYTES = 128

@@ -19,7 +19,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -920,6 +922,23 @@ struct PodStage {
   std::vector<uint8_t> h_dyn;   // before the next stage_cols)
 };
 
+// Test transport for nranks > 1 without RCCL (ks_shard_init_loopback): the ranks are contexts of one process, each
+// driven by its own host thread.  An exchange is two host barriers and device copies: every rank records an event
+// behind its block, waits at the first barrier until every rank has, then pulls the peers' blocks into its own buffer
+// behind their events and records a second event; past the second barrier it waits for the peers' second events, so
+// no rank overwrites its block (the next pass's select) before every peer has copied it.  Each wait is enqueued after
+// the record it waits on (the barriers order them), so the streams cannot deadlock.
+struct LoopGroup {
+  int32_t n = 0;
+  std::vector<ks_ctx*> ranks;  // rank r's context (nullptr once destroyed)
+  std::mutex mu;
+  std::condition_variable cv;
+  int32_t arrived = 0;
+  int64_t gen = 0;
+  bool broken = false;  // a rank failed or timed out: every later barrier fails at once
+  int32_t refs = 0;
+};
+
 struct ks_ctx {
   ks_config cfg{};
   Cfg kc{};
@@ -961,6 +980,10 @@ struct ks_ctx {
   // node sharding: shard s = rank * vshards + v owns chunks [s*nchunks/S, (s+1)*nchunks/S)
   int32_t nranks = 1, rank = 0, vshards = 1;
   ncclComm_t comm = nullptr;
+  struct LoopGroup* loop = nullptr;  // test transport (ks_shard_init_loopback) in place of comm
+  hipEvent_t lev[2][2] = {};         // loopback: [parity][0 = block ready, 1 = peers' blocks pulled]
+  int64_t loop_seq = 0;              // loopback exchanges so far (every rank makes the same sequence)
+  unsigned long long* loop_scratch = nullptr;  // loopback all-reduce: the peers' blocks [nranks][kNormRows * kMaxBatch]
   unsigned char* gather = nullptr;  // [nranks * vshards] CandSlot blocks
   size_t gather_bytes = 0;
   int32_t* cand_count = nullptr;
@@ -1071,6 +1094,31 @@ static int dev_alloc(ks_ctx* ctx, void** p, size_t bytes) {
 static void dev_free(void*& p) {
   if (p) (void)hipFree(p);
   p = nullptr;
+}
+
+// Leave the loopback group (ks_shard_init_loopback): the group is freed with its last member.
+static void loop_leave(ks_ctx* ctx) {
+  if (ctx->loop) {
+    LoopGroup* g = ctx->loop;
+    bool last = false;
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      if ((size_t)ctx->rank < g->ranks.size() && g->ranks[(size_t)ctx->rank] == ctx) g->ranks[(size_t)ctx->rank] = nullptr;
+      g->broken = true;  // a group with a missing rank cannot exchange any more
+      g->cv.notify_all();
+      last = --g->refs == 0;
+    }
+    if (last) delete g;
+    ctx->loop = nullptr;
+  }
+  for (auto& pr : ctx->lev)
+    for (hipEvent_t& e : pr) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+  void* p = ctx->loop_scratch;
+  dev_free(p);
+  ctx->loop_scratch = nullptr;
 }
 
 static Cfg make_cfg(const ks_config& c, int nsc) {
@@ -1304,6 +1352,7 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->cand_total; dev_free(p);
   p = ctx->gather; dev_free(p);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  loop_leave(ctx);
   p = ctx->cand_count; dev_free(p);
   p = ctx->cursor; dev_free(p);
   p = ctx->counters; dev_free(p);
@@ -3257,6 +3306,103 @@ static int ensure_pipe(ks_ctx* ctx) {
   return KS_OK;
 }
 
+// ---- the candidate exchange between ranks: RCCL (ks_shard_init), or the loopback test transport ----
+
+static bool loop_barrier(LoopGroup* g) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  if (g->broken) return false;
+  const int64_t my = g->gen;
+  if (++g->arrived == g->n) {
+    g->arrived = 0;
+    ++g->gen;
+    g->cv.notify_all();
+    return true;
+  }
+  const bool ok = g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->gen != my || g->broken; });
+  if (!ok || g->broken) {
+    g->broken = true;
+    g->cv.notify_all();
+    return false;
+  }
+  return true;
+}
+
+static void loop_break(LoopGroup* g) {
+  std::lock_guard<std::mutex> lk(g->mu);
+  g->broken = true;
+  g->cv.notify_all();
+}
+
+// The loopback exchange's two phases around `pull` (the device copies of the peers' blocks, on stream s).
+template <typename Pull>
+static int loop_exchange(ks_ctx* ctx, hipStream_t s, Pull pull) {
+  LoopGroup* g = ctx->loop;
+  const int par = (int)(ctx->loop_seq++ & 1);
+  auto fail = [&](const char* what) {
+    loop_break(g);
+    KS_FAIL(ctx, KS_EHIP, "loopback exchange: %s", what);
+  };
+  if (hipEventRecord(ctx->lev[par][0], s) != hipSuccess) return fail("hipEventRecord");
+  if (!loop_barrier(g)) return fail("a peer rank failed or timed out");
+  for (int32_t p = 0; p < g->n; ++p) {
+    if (p == ctx->rank) continue;
+    ks_ctx* peer = g->ranks[(size_t)p];
+    if (!peer) return fail("a peer rank was destroyed");
+    if (hipStreamWaitEvent(s, peer->lev[par][0], 0) != hipSuccess) return fail("hipStreamWaitEvent");
+    if (pull(peer, p) != hipSuccess) return fail("device copy of a peer's block");
+  }
+  if (hipEventRecord(ctx->lev[par][1], s) != hipSuccess) return fail("hipEventRecord");
+  if (!loop_barrier(g)) return fail("a peer rank failed or timed out");
+  for (int32_t p = 0; p < g->n; ++p) {
+    if (p == ctx->rank) continue;
+    ks_ctx* peer = g->ranks[(size_t)p];
+    if (!peer) return fail("a peer rank was destroyed");
+    if (hipStreamWaitEvent(s, peer->lev[par][1], 0) != hipSuccess) return fail("hipStreamWaitEvent");
+  }
+  return KS_OK;
+}
+
+// In-place allgather of the ranks' candidate-slot blocks: rank r's `bytes` at gather + r * bytes.
+static int exchange_allgather(ks_ctx* ctx, size_t bytes, hipStream_t s) {
+  if (ctx->loop)
+    return loop_exchange(ctx, s, [&](ks_ctx* peer, int32_t p) {
+      return hipMemcpyAsync(ctx->gather + (size_t)p * bytes, peer->gather + (size_t)p * bytes, bytes,
+                            hipMemcpyDeviceToDevice, s);
+    });
+  const ncclResult_t r = ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, s);
+  if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllGather (candidate slots): %s", ncclGetErrorString(r));
+  return KS_OK;
+}
+
+__global__ void max_reduce_kernel(unsigned long long* buf, const unsigned long long* peers, int32_t nranks, int32_t rank,
+                                   int32_t count) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  unsigned long long m = buf[i];
+  for (int32_t p = 0; p < nranks; ++p)
+    if (p != rank) m = max(m, peers[(size_t)p * count + i]);
+  buf[i] = m;
+}
+
+// In-place max all-reduce of the pass's normalization maxima (count u64 words at buf = ctx->dev_M).
+static int exchange_allreduce_max(ks_ctx* ctx, unsigned long long* buf, int32_t count, hipStream_t s) {
+  if (ctx->loop) {
+    if (int rc = loop_exchange(ctx, s, [&](ks_ctx* peer, int32_t p) {
+          return hipMemcpyAsync(ctx->loop_scratch + (size_t)p * count, peer->dev_M, (size_t)count * 8,
+                                hipMemcpyDeviceToDevice, s);
+        });
+        rc != KS_OK)
+      return rc;
+    hipLaunchKernelGGL(max_reduce_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, buf,
+                       (const unsigned long long*)ctx->loop_scratch, ctx->nranks, ctx->rank, count);
+    HIPCHK(ctx, hipGetLastError());
+    return KS_OK;
+  }
+  const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclUint64, ncclMax, ctx->comm, s);
+  if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllReduce (normalization maxima): %s", ncclGetErrorString(r));
+  return KS_OK;
+}
+
 // Launch shape of the dirty-chunk re-sweep of a pipelined pass; pipe == nullptr: not pipelined.
 struct PipeShape {
   int32_t fix_ppw;
@@ -3344,10 +3490,8 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     rec(0, ss);
     sweep(sweep_blocks, ss);
     rec(0, ss);
-    if (ctx->nranks > 1) {
-      const ncclResult_t r = ncclAllReduce(ctx->dev_M, ctx->dev_M, kNormRows * kMaxBatch, ncclUint64, ncclMax, ctx->comm, ss);
-      if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllReduce (normalization maxima): %s", ncclGetErrorString(r));
-    }
+    if (ctx->nranks > 1)
+      if (int rc = exchange_allreduce_max(ctx, ctx->dev_M, kNormRows * kMaxBatch, ss); rc != KS_OK) return rc;
     sa.phase = 1;
     rec(0, ss);
     sweep(sweep_blocks, ss);
@@ -3380,7 +3524,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
       sa.list_bound = cset.bound;
       sa.list_top = ctx->pipe_top + (size_t)(k & 1) * kMaxBatch;
       sa.list_k = ctx->k;
-      sweep(pipe->list_blocks, fs);
+      le = pl.sweep(pipe->list_blocks, fs, sa);  // once: the (merged) lists span every shard's chunks
     } else {
       sweep(pipe->fix_blocks, fs);
     }
@@ -3417,31 +3561,26 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
       unsigned char* b = ctx->gather + (size_t)sh * L.bytes;
       se.cand_chunk = (uint32_t*)(b + L.chunk);
       se.cand_t = (uint2*)(b + L.t);
-      se.cand_bound = ctx->cand_bound;  // recomputed by the merge
+      se.cand_bound = cset.bound;  // scratch: recomputed by the merge
       se.cand_top = (uint64_t*)(b + L.top);
-      se.cand_second = ctx->cand_second;  // recomputed by the merge
+      se.cand_second = cset.second;  // scratch: recomputed by the merge
       se.cand_count = (int32_t*)(b + L.count);
       se.cand_total = (int32_t*)(b + L.total);
     }
     hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(kSelThreads), select_smem(se.c1 - se.c0), ss, se);
   }
   if (S > 1) {
-    if (ctx->nranks > 1) {
-      // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
-      const size_t bytes = (size_t)ctx->vshards * L.bytes;
-      const ncclResult_t r =
-          ncclAllGather(ctx->gather + (size_t)ctx->rank * bytes, ctx->gather, bytes, ncclUint8, ctx->comm, ss);
-      if (r != ncclSuccess) KS_FAIL(ctx, KS_EHIP, "ncclAllGather (candidate slots): %s", ncclGetErrorString(r));
-    }
+    if (ctx->nranks > 1)  // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
+      if (int rc = exchange_allgather(ctx, (size_t)ctx->vshards * L.bytes, ss); rc != KS_OK) return rc;
     MergeArgs ma;
     ma.gather = ctx->gather;
     ma.cursor = base;
-    ma.cand_chunk = ctx->cand_chunk;
-    ma.cand_t = ctx->cand_t;
-    ma.cand_bound = ctx->cand_bound;
-    ma.cand_top = ctx->cand_top;
-    ma.cand_second = ctx->cand_second;
-    ma.cand_count = ctx->cand_count;
+    ma.cand_chunk = cset.chunk;
+    ma.cand_t = cset.t;
+    ma.cand_bound = cset.bound;
+    ma.cand_top = cset.top;
+    ma.cand_second = cset.second;
+    ma.cand_count = cset.count;
     ma.nslots = S;
     ma.total_pods = ctx->np;
     ma.batch = ctx->batch;
@@ -3558,7 +3697,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   if (pipelined(ctx)) {
     if (ensure_pipe(ctx) != KS_OK) return KS_EHIP;
     static const int64_t env_patch = env_i64("KS_PIPE_PATCH", 1, 0, 1);
-    pshape.patch = env_patch != 0 && S == 1 && ctx->kc.monotone;
+    pshape.patch = env_patch != 0 && ctx->kc.monotone;
     // the re-sweep runs on the commit stream's few CUs when patched: more pods per wave, fewer waves
     static const int64_t env_fix_ppw = env_i64("KS_PIPE_FIX_PPW", 0, 1, kMaxBatch);
     pshape.fix_ppw = (int32_t)std::min<int64_t>(env_fix_ppw > 0 ? env_fix_ppw : (pshape.patch ? 16 : 2), ctx->batch);
@@ -4316,6 +4455,7 @@ int ks_shard_init(ks_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* uniq
     (void)ncclCommDestroy(ctx->comm);
     ctx->comm = nullptr;
   }
+  loop_leave(ctx);
   if (nranks > 1) {
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof(id));
@@ -4325,6 +4465,44 @@ int ks_shard_init(ks_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* uniq
   ctx->nranks = nranks;
   ctx->rank = rank;
   ctx->vshards = virtual_shards;
+  return KS_OK;
+}
+
+int ks_shard_init_loopback(ks_ctx* const* ctxs, int32_t nranks, int32_t virtual_shards) {
+  if (!ctxs || nranks < 2 || nranks > 64 || virtual_shards < 1 || nranks * virtual_shards > 1024) return KS_EINVAL;
+  for (int32_t r = 0; r < nranks; ++r) {
+    if (!ctxs[r]) return KS_EINVAL;
+    for (int32_t q = 0; q < r; ++q)
+      if (ctxs[q] == ctxs[r]) KS_FAIL(ctxs[r], KS_EINVAL, "ks_shard_init_loopback: a context is given twice");
+    if (ctxs[r]->n != ctxs[0]->n || ctxs[r]->k != ctxs[0]->k || ctxs[r]->batch != ctxs[0]->batch)
+      KS_FAIL(ctxs[r], KS_EINVAL, "ks_shard_init_loopback: the ranks must load the same node count, batch and candidates");
+  }
+  LoopGroup* g = new LoopGroup();
+  g->n = nranks;
+  g->ranks.assign(ctxs, ctxs + nranks);
+  for (int32_t r = 0; r < nranks; ++r) {
+    ks_ctx* ctx = ctxs[r];
+    auto undo = [&](int rc) {
+      loop_break(g);
+      if (g->refs == 0) delete g;
+      return rc;
+    };
+    if (int rc = ks_shard_init(ctx, 1, 0, nullptr, 1); rc != KS_OK) return undo(rc);
+    void* p = nullptr;
+    if (dev_alloc(ctx, &p, (size_t)nranks * kNormRows * kMaxBatch * 8) != KS_OK) return undo(KS_ENOMEM);
+    ctx->loop_scratch = (unsigned long long*)p;
+    for (auto& pr : ctx->lev)
+      for (hipEvent_t& e : pr)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+          ctx->err = "ks_shard_init_loopback: hipEventCreate failed";
+          return undo(KS_EHIP);
+        }
+    ctx->loop = g;
+    ++g->refs;
+    ctx->nranks = nranks;
+    ctx->rank = r;
+    ctx->vshards = virtual_shards;
+  }
   return KS_OK;
 }
 

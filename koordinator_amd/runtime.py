@@ -95,6 +95,7 @@ def lib() -> C.CDLL:
     L.ks_set_pipeline.argtypes = [vp, C.c_int32]
     L.ks_shard_unique_id.argtypes = [C.POINTER(C.c_uint8)]
     L.ks_shard_init.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32]
+    L.ks_shard_init_loopback.argtypes = [C.POINTER(vp), C.c_int32, C.c_int32]
     for name in abi.EXPORTED_SYMBOLS:
         if name not in ("ks_destroy", "ks_last_error"):
             getattr(L, name).restype = C.c_int
@@ -110,6 +111,43 @@ def shard_unique_id() -> bytes:
     if rc != abi.KS_OK:
         raise KsError(rc, "ncclGetUniqueId failed")
     return bytes(buf)
+
+
+def shard_loopback(evaluators, virtual_shards: int = 1):
+    """Test transport (ks_shard_init_loopback): the evaluators (same node table, batch and candidates) become ranks
+    0..n-1 of one node-sharded group whose candidate exchange is device copies between them instead of RCCL.  Each
+    rank's schedule* must then run concurrently on its own thread (run_ranks)."""
+    L = lib()
+    hs = (C.c_void_p * len(evaluators))(*[ev.h.value for ev in evaluators])
+    rc = L.ks_shard_init_loopback(hs, len(evaluators), virtual_shards)
+    if rc != abi.KS_OK:
+        msgs = [L.ks_last_error(ev.h).decode() for ev in evaluators]
+        raise KsError(rc, "ks_shard_init_loopback: " + "; ".join(m for m in msgs if m))
+
+
+def run_ranks(fn, evaluators):
+    """fn(evaluator) on every rank concurrently, one host thread each (ctypes releases the GIL inside the library);
+    returns the per-rank results and re-raises the first rank's exception."""
+    import threading
+
+    out = [None] * len(evaluators)
+    err = [None] * len(evaluators)
+
+    def body(i):
+        try:
+            out[i] = fn(evaluators[i])
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            err[i] = e
+
+    ts = [threading.Thread(target=body, args=(i,)) for i in range(len(evaluators))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return out
 
 
 class Evaluator:
