@@ -16,9 +16,11 @@ At N=1 it also carries ``c3`` (configs[2]: NUMA + DeviceShare joint allocation, 
 NodeResourcesBalancedAllocation, TaintToleration, NodeAffinity, NodePorts), each with its own CPU baseline, sample
 parity and roofline.
 
-Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU.  ``value`` at N>1 is N
-independent C2 replicas (seed + rank; weak scaling: the 5k-node cluster does not warrant node sharding,
-DESIGN.md §6); the ``c5`` record is the sharded 100k-node cluster.
+Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU.  ``value`` at N>1 is C2 node-sharded
+over the N ranks (strong scaling: one cluster, one queue, every rank sweeps its node range and the per-shard
+candidates are exchanged by one RCCL allgather per pass); the ``c5`` record is the sharded 100k-node
+cluster.  ``c2_replicas`` keeps the old replica line: N independent C2 clusters (seed + rank, weak scaling), which
+the single-leader reference has no analogue of.  ``--replicas`` makes the replicas ``value`` again.
 
 rank 0 prints ONE JSON line.  Timed steps run with the library's per-kernel HIP events off (they add a
 dispatch gap between the pass kernels); the same number of steps is then re-run with the events on
@@ -55,19 +57,33 @@ def build_workload(name: str, seed: int, n_pods: int = 0):
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
 
+def lib_sha256() -> str:
+    import hashlib
+
+    from koordinator_amd import runtime
+
+    with open(runtime.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def newest_profile(pattern: str):
+    """The newest committed profile summary matching `pattern` that was measured with the library this process
+    loaded (its lib_sha256 stamp, tools/traffic.py / valu.py); summaries of another build are skipped, so a number
+    in the bench line always comes from this build."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        return json.load(f), os.path.relpath(files[-1], ROOT)
+    want = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("lib_sha256") == want:
+            return t, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def pmc_traffic(config: str, kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary for this config
-    (profiles/rNN_<config>_traffic.json, written by tools/pmc_traffic.sh + tools/traffic.py from
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary for this config measured with this
+    library (profiles/rNN_<config>_traffic.json, written by tools/pmc_traffic.sh + tools/traffic.py from
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command); None when absent."""
     t, src = newest_profile(f"r*_{config}_traffic.json")
     if t is None:
@@ -83,8 +99,8 @@ def pmc_traffic(config: str, kernel: str):
 
 
 def pmc_valu(config: str, kernel: str):
-    """VALU-issue floor per launch of `kernel` (us) from the newest committed PMC summary for this config
-    (profiles/rNN_<config>_valu.json, tools/pmc_valu.sh + tools/valu.py: SQ_INSTS_VALU x 2 cycles
+    """VALU-issue floor per launch of `kernel` (us) from the newest committed PMC summary for this config measured
+    with this library (profiles/rNN_<config>_valu.json, tools/pmc_valu.sh + tools/valu.py: SQ_INSTS_VALU x 2 cycles
     over 1024 SIMDs at 2.4 GHz); None when absent."""
     t, src = newest_profile(f"r*_{config}_valu.json")
     if t is None:
@@ -368,8 +384,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0, help="16-thread oracle sample (per config)")
     ap.add_argument("--cpu-extra-budget-s", type=float, default=6.0, help="1-thread / all-core oracle samples")
-    ap.add_argument("--shard", action="store_true",
-                    help="shard the main config's nodes over the ranks (default for --gpus N: N independent replicas)")
+    ap.add_argument("--replicas", action="store_true",
+                    help="at N>1: N independent replicas of the main config as `value` (default: node-sharded)")
+    ap.add_argument("--shard", action="store_true", help="(default at N>1; kept for old command lines)")
     ap.add_argument("--vshards", type=int, default=1, help="virtual shards per GPU (exercises the merge on one GPU)")
     ap.add_argument("--no-c5", action="store_true", help="skip the 100k-node c5 record")
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
@@ -384,6 +401,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    args.shard = world > 1 and not args.replicas
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -426,6 +444,16 @@ def main():
             out["parity"] = cb["parity_with_gpu_on_sample"]
             out["speedup_vs_cpu_baseline"] = round(rec["value"] / cb["value"], 2)
     del w, res
+
+    if world > 1 and args.shard and not args.no_sub:
+        # the replica line: N independent clusters of the main config (seed + rank), weak scaling
+        wr = build_workload(args.config, seed=20261015 + rank, n_pods=args.pods)
+        rr, _ = run_config(wr, args, dist, world, rank, local_rank, False, args.steps, args.warmup, args.config, False)
+        if rank == 0:
+            rr["scaling"] = "weak"
+            rr["parallelism"] = f"replicas{world}"
+            out["c2_replicas" if args.config == "c2" else f"{args.config}_replicas"] = rr
+        del wr
 
     if not args.no_c5 and args.config != "c5":
         # the metric's 100k-node configuration: one GPU at N=1, node-sharded over the ranks at N>1

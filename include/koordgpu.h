@@ -595,6 +595,14 @@ typedef struct ks_stats {
 
 typedef struct ks_ctx ks_ctx;
 
+/* The layout this library was compiled with, for a binding to refuse a library built from another header (a stale
+ * .so whose score-matrix width or struct sizes differ writes past the caller's buffers): out[0] = KS_ABI_VERSION,
+ * out[1] = KS_NUM_SCORE_PLUGINS, then sizeof ks_config, ks_node_cols, ks_pod_cols, ks_quota_cols, ks_quota_tree,
+ * ks_reservation_cols, ks_device_cols, ks_cpu_topology, ks_cpu_state_cols, ks_numa_node_cols, ks_result,
+ * ks_node_state, ks_stats (KS_ABI_LAYOUT_WORDS words; n < that fills the first n).  Returns KS_ABI_LAYOUT_WORDS. */
+#define KS_ABI_LAYOUT_WORDS 15
+int ks_abi_layout(int64_t *out, int32_t n);
+
 /* Returns KS_OK and *out on success.  On failure *out is NULL and
  * ks_last_error(NULL) describes the problem. */
 int ks_create(const ks_config *cfg, ks_ctx **out);

@@ -428,6 +428,7 @@ class KsStats(C.Structure):
 
 # every symbol include/koordgpu.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
+    "ks_abi_layout",
     "ks_create",
     "ks_destroy",
     "ks_last_error",
@@ -473,3 +474,4 @@ EXPORTED_SYMBOLS = [
     "ks_shard_init_loopback",
 ]
 KS_SHARD_ID_BYTES = 128
+KS_ABI_LAYOUT_WORDS = 15

@@ -1195,6 +1195,16 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
 
 const char* ks_last_error(const ks_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
+int ks_abi_layout(int64_t* out, int32_t n) {
+  const int64_t v[KS_ABI_LAYOUT_WORDS] = {
+      KS_ABI_VERSION, KS_NUM_SCORE_PLUGINS, sizeof(ks_config), sizeof(ks_node_cols), sizeof(ks_pod_cols),
+      sizeof(ks_quota_cols), sizeof(ks_quota_tree), sizeof(ks_reservation_cols), sizeof(ks_device_cols),
+      sizeof(ks_cpu_topology), sizeof(ks_cpu_state_cols), sizeof(ks_numa_node_cols), sizeof(ks_result),
+      sizeof(ks_node_state), sizeof(ks_stats)};
+  for (int32_t i = 0; out && i < n && i < KS_ABI_LAYOUT_WORDS; ++i) out[i] = v[i];
+  return KS_ABI_LAYOUT_WORDS;
+}
+
 int ks_create(const ks_config* cfg, ks_ctx** out) {
   if (out) *out = nullptr;
   if (!cfg || !out) {
@@ -1329,9 +1339,18 @@ fail:
 
 void ks_destroy(ks_ctx* ctx) {
   if (!ctx) return;
+  // This context's work only: its own stream, and on the process-wide pipeline streams (shared with other contexts,
+  // ensure_pipe) the last records of its own events -- each pipelined pass ends its sweep-stream work with a
+  // pev_sel record and its commit-stream work with a pev_com record.  Synchronizing the shared streams instead would
+  // also wait for every other context's in-flight passes.
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->sstream) (void)hipStreamSynchronize(ctx->sstream);
-  if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
+  for (int i = 0; i < kPipeEvents; ++i) {
+    if (ctx->pev_sel[i]) (void)hipEventSynchronize(ctx->pev_sel[i]);
+    if (ctx->pev_com[i]) (void)hipEventSynchronize(ctx->pev_com[i]);
+  }
+  for (auto& pr : ctx->lev)
+    for (hipEvent_t e : pr)
+      if (e) (void)hipEventSynchronize(e);
   dev_free(ctx->node_blob);
   dev_free(ctx->ckpt_blob);
   dev_free(ctx->quota_blob);
@@ -3243,17 +3262,19 @@ static bool pipelined(const ks_ctx* ctx) {
   return mode == 2 || ctx->n >= env_min;
 }
 
-// The pipelined passes' two streams per device, shared by the process's contexts and never destroyed: destroying
-// the CU-masked streams and creating new ones for a later context hung that context's teardown on MI355X
-// (gpurun_out/r03c).
+// The pipelined passes' two streams per device, shared by the process's contexts for the life of the process
+// (DESIGN §5a "Streams"): each CU-masked stream owns a hardware queue of its own (a queue carries one CU mask), and
+// the process has GPU_MAX_HW_QUEUES = 4 of them, so per-context masked streams would run out as soon as two contexts
+// pipeline (two scheduler profiles, the loopback ranks).  ks_destroy waits only for its own context's events on them.
 struct PipeStreams {
   hipStream_t s = nullptr, c = nullptr;
 };
 static std::mutex g_pipe_mu;
 static std::vector<PipeStreams> g_pipe;
 
-// The sweep stream (one CU left out of its mask by default, so the one-workgroup commit always finds a CU while a
-// sweep fills the rest; KS_PIPE_CUMASK=0: no mask), the pipe words and the event ring.
+// The sweep stream (CU-masked to all but KS_PIPE_COMMIT_CUS = 32 CUs, which the commit stream gets: the one-workgroup
+// commit and the patched passes' list re-evaluation never share a CU with sweep waves; KS_PIPE_CUMASK=0: no masks), the
+// pipe words and the event ring.
 static int ensure_pipe(ks_ctx* ctx) {
   if (!ctx->pipe) {
     void* p = nullptr;
@@ -3265,9 +3286,9 @@ static int ensure_pipe(ks_ctx* ctx) {
   if (!ctx->sstream) {
     // One sweep stream and one commit stream per device for the whole process, shared by every context: a
     // CU-masked stream owns a hardware queue of its own, and creating them per context exhausts the process's
-    // queues (stream creation then stalls).  Sharing only orders the passes of different contexts; each context's
-    // own events order its passes.  The commit stream runs on the one CU the sweep stream leaves out, so the
-    // one-workgroup commit never shares a CU (and its SIMDs' issue slots) with sweep waves.
+    // queues.  Sharing only orders the passes of different contexts; each context's own events order its passes.
+    // The commit stream runs on the KS_PIPE_COMMIT_CUS CUs the sweep stream leaves out, so the one-workgroup commit
+    // never shares a CU (and its SIMDs' issue slots) with sweep waves.
     std::lock_guard<std::mutex> lock(g_pipe_mu);
     if (g_pipe.size() <= (size_t)ctx->device) g_pipe.resize((size_t)ctx->device + 1);
     PipeStreams& st = g_pipe[(size_t)ctx->device];

@@ -96,11 +96,32 @@ def lib() -> C.CDLL:
     L.ks_shard_unique_id.argtypes = [C.POINTER(C.c_uint8)]
     L.ks_shard_init.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32]
     L.ks_shard_init_loopback.argtypes = [C.POINTER(vp), C.c_int32, C.c_int32]
+    L.ks_abi_layout.argtypes = [abi.P64, C.c_int32]
     for name in abi.EXPORTED_SYMBOLS:
         if name not in ("ks_destroy", "ks_last_error"):
             getattr(L, name).restype = C.c_int
+    check_layout(L)
     _lib = L
     return L
+
+
+def expected_layout() -> list:
+    """ks_abi_layout's words as this binding's ctypes mirrors of include/koordgpu.h lay them out"""
+    return [abi.KS_ABI_VERSION, abi.KS_NUM_SCORE_PLUGINS] + [C.sizeof(t) for t in (
+        abi.KsConfig, abi.KsNodeCols, abi.KsPodCols, abi.KsQuotaCols, abi.KsQuotaTree, abi.KsReservationCols,
+        abi.KsDeviceCols, abi.KsCpuTopology, abi.KsCpuStateCols, abi.KsNumaNodeCols, abi.KsResult, abi.KsNodeState,
+        abi.KsStats)]
+
+
+def check_layout(L) -> None:
+    """Refuse a library compiled from another header than this binding mirrors (a stale libkoordgpu.so would write
+    score rows or results past the buffers this module allocates)."""
+    want = expected_layout()
+    got = (C.c_int64 * len(want))()
+    n = L.ks_abi_layout(got, len(want))
+    if n != len(want) or list(got) != want:
+        raise ImportError(f"{LIB_PATH} was built from another include/koordgpu.h (library layout {list(got)[:n]}, "
+                          f"binding {want}); rebuild it with koordinator_amd.runtime.build()")
 
 
 def shard_unique_id() -> bytes:

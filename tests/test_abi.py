@@ -85,3 +85,27 @@ def test_abi_version_checked():
     cfg = abi.KsConfig(abi_version=999)
     assert L.ks_create(C.byref(cfg), C.byref(h)) == abi.KS_EINVAL
     assert b"ABI" in L.ks_last_error(None)
+
+
+def test_library_layout_matches_binding():
+    """The library reports the layout it was compiled with; the binding refuses a library from another header (the
+    round-3 eval-pod abort: a score matrix written with another row width overruns the caller's buffer)."""
+    if not os.path.exists(LIB):
+        pytest.skip("libkoordgpu.so not built")
+    from koordinator_amd import runtime
+
+    L = runtime.lib()
+    want = runtime.expected_layout()
+    got = (C.c_int64 * len(want))()
+    assert L.ks_abi_layout(got, len(want)) == abi.KS_ABI_LAYOUT_WORDS == len(want)
+    assert list(got) == want
+
+    class Fake:
+        def ks_abi_layout(self, out, n):
+            for i in range(n):
+                out[i] = want[i]
+            out[1] = 5  # a library built when KS_NUM_SCORE_PLUGINS was 5
+            return n
+
+    with pytest.raises(ImportError):
+        runtime.check_layout(Fake())

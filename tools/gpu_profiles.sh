@@ -1,26 +1,40 @@
 #!/bin/bash
-# rocprofv3 kernel stats for the default bench line (C2), the PMC HBM traffic / VALU-issue passes for C2 and C5
-# (C5's sweep measured unpipelined, KS_PIPE=0: the same kernel without the list re-evaluation launches), and last
-# the C5 kernel trace (200k pods, patched pipeline) with its overlap summary (tools/trace_overlap.py).  Output
-# under gpurun_out/$1, copied into profiles/ by hand.
-# A pipelined process under rocprofv3 may segfault at exit after writing its output (the process-lifetime
-# CU-masked streams, koordgpu.hip ensure_pipe): the trace step is the last GPU step, and its output is kept only
-# when the trace file was written.
+# Profile evidence of the bench line's records, all from the library in this tree (each summary is stamped with its
+# sha256, which bench.py checks): per config (c2, c3, c4, c2d) the rocprofv3 kernel statistics of the bench command and
+# the PMC HBM traffic (FETCH_SIZE / WRITE_SIZE passes) and VALU-issue summaries; for c5 the PMC passes on a 200k-pod
+# queue (sweep measured unpipelined, KS_PIPE=0: the same kernel without the list re-evaluation launches) and last the
+# pipelined kernel trace with its overlap summary (tools/trace_overlap.py).
+# Output: gpurun_out/$1/<cfg>_{kernel_stats.csv,traffic.json,valu.json}, c5_overlap.json; tools/keep_profiles.sh copies
+# them into profiles/ under a round tag.
 set -o pipefail
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- python3 bench.py --no-c5 --no-sub --no-cpu-baseline > $OUT/prof_c2.json 2> $OUT/prof_c2.err || { echo "rocprof c2 failed"; tail -30 $OUT/prof_c2.err; exit 1; }
-find $OUT/prof_c2 -type f ! -name '*kernel_stats.csv' -delete
-echo prof c2 done
-BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_traffic.sh c2 $(basename $OUT)/traffic_c2 || exit 1
-BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_valu.sh c2 $(basename $OUT)/valu_c2 10.8 || exit 1
-KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_traffic.sh c5 $(basename $OUT)/traffic_c5 || exit 1
-KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_valu.sh c5 $(basename $OUT)/valu_c5 40.3 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --no-c5 --no-cpu-baseline --pods 200000 --steps 2 --warmup 1 > $OUT/prof_c5.json 2> $OUT/prof_c5.err
-rc=$?
-TR=$(find $OUT/prof_c5 -name '*kernel_trace.csv' | head -1)
-[ -n "$TR" ] && python3 tools/trace_overlap.py $TR > $OUT/c5_overlap.json
-find $OUT -type f ! -name '*kernel_stats.csv' ! -name '*.json' ! -name '*.err' -delete
-echo "prof c5 trace rc=$rc"
+for CFG in ${CONFIGS:-c2 c3 c4 c2d}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$CFG -o run -- python3 bench.py --config $CFG --no-c5 --no-sub --no-cpu-baseline > $OUT/prof_$CFG.json 2> $OUT/prof_$CFG.err || { echo "rocprof $CFG failed"; tail -30 $OUT/prof_$CFG.err; exit 1; }
+  S=$(find $OUT/prof_$CFG -name '*kernel_stats.csv' | head -1)
+  [ -n "$S" ] && cp $S $OUT/${CFG}_kernel_stats.csv
+  rm -rf $OUT/prof_$CFG
+  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_traffic.sh $CFG $(basename $OUT)/traffic_$CFG > /dev/null || exit 1
+  cp $OUT/traffic_$CFG/traffic.json $OUT/${CFG}_traffic.json
+  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_valu.sh $CFG $(basename $OUT)/valu_$CFG > /dev/null || exit 1
+  cp $OUT/valu_$CFG/valu.json $OUT/${CFG}_valu.json
+  rm -rf $OUT/traffic_$CFG $OUT/valu_$CFG
+  echo "profiles $CFG done"
+done
+if [ "${C5:-1}" = 1 ]; then
+  KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_traffic.sh c5 $(basename $OUT)/traffic_c5 > /dev/null || exit 1
+  cp $OUT/traffic_c5/traffic.json $OUT/c5_traffic.json
+  KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_valu.sh c5 $(basename $OUT)/valu_c5 > /dev/null || exit 1
+  cp $OUT/valu_c5/valu.json $OUT/c5_valu.json
+  rm -rf $OUT/traffic_c5 $OUT/valu_c5
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --no-c5 --no-cpu-baseline --pods 200000 --steps 2 --warmup 1 > $OUT/prof_c5.json 2> $OUT/prof_c5.err
+  rc=$?
+  S=$(find $OUT/prof_c5 -name '*kernel_stats.csv' | head -1)
+  [ -n "$S" ] && cp $S $OUT/c5_kernel_stats.csv
+  TR=$(find $OUT/prof_c5 -name '*kernel_trace.csv' | head -1)
+  [ -n "$TR" ] && python3 tools/trace_overlap.py $TR > $OUT/c5_overlap.json
+  rm -rf $OUT/prof_c5
+  echo "profiles c5 done (trace rc=$rc)"
+fi
 exit 0

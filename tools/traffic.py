@@ -4,6 +4,7 @@ gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) reports half the
 coalesced read, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Usage: traffic.py OUT_DIR CONFIG
 """
 import csv
+import hashlib
 import glob
 import json
 import os
@@ -25,6 +26,13 @@ def per_dispatch(root, counter):
     return vals, names
 
 
+def lib_sha256():
+    """sha256 of the libkoordgpu.so the profiled bench loaded (bench.py refuses summaries of another build)"""
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "koordinator_amd", "libkoordgpu.so")
+    with open(p, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def main():
     root, cfg = sys.argv[1], sys.argv[2]
     fetch, names = per_dispatch(root, "FETCH_SIZE")
@@ -38,7 +46,7 @@ def main():
         k = wnames[d].split("(")[0]
         by_kernel[k]["launches_w"] += 1
         by_kernel[k]["write_kib"] += v
-    out = {"config": cfg, "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
+    out = {"config": cfg, "lib_sha256": lib_sha256(), "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
            f"bench.py --config {cfg} --steps 1 --warmup 0; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch", "kernels": {}}
     for k, a in sorted(by_kernel.items()):
         if not a["launches"] or not a["launches_w"]:

@@ -7,6 +7,7 @@ launch time can be compared with its VALU-issue floor.  Usage: valu.py OUT_DIR C
 (LAUNCH_US: the un-instrumented average launch time of the sweep from bench.py, for the fraction).
 """
 import csv
+import hashlib
 import glob
 import json
 import os
@@ -16,6 +17,13 @@ from collections import defaultdict
 SIMDS = 256 * 4
 CYC_PER_VALU = 2.0
 CLOCK_HZ = 2.4e9
+
+
+def lib_sha256():
+    """sha256 of the libkoordgpu.so the profiled bench loaded (bench.py refuses summaries of another build)"""
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "koordinator_amd", "libkoordgpu.so")
+    with open(p, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 
 
 def main():
@@ -36,7 +44,7 @@ def main():
         launches[k] += 1
         for c, v in cs.items():
             by_kernel[k][c] += v
-    out = {"config": cfg, "method": f"rocprofv3 --pmc (one pass) of bench.py --config {cfg}; per-launch averages; "
+    out = {"config": cfg, "lib_sha256": lib_sha256(), "method": f"rocprofv3 --pmc (one pass) of bench.py --config {cfg}; per-launch averages; "
            f"VALU floor = SQ_INSTS_VALU x {CYC_PER_VALU} cyc / ({SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz)", "kernels": {}}
     for k, cs in sorted(by_kernel.items()):
         n = launches[k]
