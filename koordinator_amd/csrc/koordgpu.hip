@@ -3069,12 +3069,19 @@ static bool commit_qcache(const ks_ctx* ctx) {
   return commit_layout(ctx->k, ctx->nchunks, true, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total <= 160 * 1024;
 }
 
-// kernel variant: 0 = Fit/LoadAware/Quota, 1 = + Reservation, 3 = + Reservation + NodeNUMAResource
-// + 8: NodeNUMAResource with NUMA topology policies (ks_numa.h)
-// (TaintToleration / NodeAffinity are normalized like DeviceShare: they run in the DeviceShare variants)
+// Kernel variant (FEAT bits, ks_pass.h): 1 Reservation, 2 NodeNUMAResource, 4 the normalized plugins (DeviceShare,
+// TaintToleration / NodeAffinity / NodePorts), 8 NUMA topology policies (with 2).  A context runs the smallest built
+// variant whose bits cover the plugins it enables: a bit that is compiled in but unused still costs registers -- the
+// variants with Reservation and the normalized plugins together spill 180-320 B/lane in the commit kernel, those
+// without Reservation (4, 6, 14) none (hipcc -Rpass-analysis=kernel-resource-usage).
+constexpr int kBuiltFeats[] = {0, 1, 3, 4, 6, 7, 11, 14, 15};  // ascending (koordinator_amd/csrc/Makefile FEATS)
+
 static int kernel_feat(const ks_ctx* ctx) {
-  const int f = (ctx->kc.dev || ctx->kc.stat) ? 7 : (ctx->kc.numa ? 3 : (ctx->kc.rsv ? 1 : 0));
-  return f | (ctx->kc.numa_pol ? 8 : 0);
+  const int need = (ctx->kc.rsv ? 1 : 0) | (ctx->kc.numa ? 2 : 0) | ((ctx->kc.dev || ctx->kc.stat) ? 4 : 0) |
+                   (ctx->kc.numa_pol ? 10 : 0);
+  for (int f : kBuiltFeats)
+    if ((f & need) == need) return f;
+  return 15;
 }
 
 // the slot device region of the commit kernel: GPU state (DeviceShare), then the TaintToleration / NodeAffinity words
@@ -3123,8 +3130,11 @@ static PassLaunch pass_launcher(int feat, int nsc) {
 #define KS_PICK(F) return nsc == 0 ? pass_launch_f##F##_n0() : (nsc == 2 ? pass_launch_f##F##_n2() : pass_launch_f##F##_n4())
   switch (feat) {
     case 15: KS_PICK(15);
+    case 14: KS_PICK(14);
     case 11: KS_PICK(11);
     case 7: KS_PICK(7);
+    case 6: KS_PICK(6);
+    case 4: KS_PICK(4);
     case 3: KS_PICK(3);
     case 1: KS_PICK(1);
     default: KS_PICK(0);
@@ -3503,7 +3513,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   };
   // patched: commit k-2 wrote this pass's first pod and its rows are final
   if (patch && k >= 2) HIPCHK(ctx, hipStreamWaitEvent(ss, ctx->pev_com[(k - 2) % kPipeEvents], 0));
-  if (feat == 7 || feat == 15) {
+  if (feat & 4) {
     // DeviceShare: phase 0 reduces the per-pod normalization max, (RCCL max over the ranks), phase 1 keys;
     // each launch is timed on its own (the roofline is per sweep launch)
     HIPCHK(ctx, hipMemsetAsync(ctx->dev_M, 0, kNormRows * kMaxBatch * 8, ss));

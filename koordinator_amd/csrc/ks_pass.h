@@ -1626,8 +1626,11 @@ struct PassLaunch {
 KS_DECLARE_VARIANT(0)
 KS_DECLARE_VARIANT(1)
 KS_DECLARE_VARIANT(3)
+KS_DECLARE_VARIANT(4)
+KS_DECLARE_VARIANT(6)
 KS_DECLARE_VARIANT(7)
 KS_DECLARE_VARIANT(11)
+KS_DECLARE_VARIANT(14)
 KS_DECLARE_VARIANT(15)
 #undef KS_DECLARE_VARIANT
 
