@@ -593,14 +593,61 @@ typedef struct ks_stats {
                               select too, the lists patched after the commit (monotone plugin sets) */
 } ks_stats;
 
+/* ---- preemption: the ElasticQuota PostFilter ----
+ * NodeInfo.Pods of every node, the victims pool of the dry runs (one row per running pod; rows of a node in any
+ * order).  The host resolves each pod's quota (getPodAssociateQuotaName, elasticquota/plugin_helper.go:41-61) to a
+ * quota row of ks_load_quotas and its PodDisruptionBudget (filterPodsWithPDBViolation's namespace + selector match,
+ * preempt.go:222-265; pods listed in the PDB's DisruptedPods get -1) to an index of ks_load_node_pods' pdb_allowed. */
+#define KS_NPOD_NONPREEMPTIBLE 0x1u /* extension.IsPodNonPreemptible: never a victim (preempt.go:284-287) */
+#define KS_NPOD_IN_QUOTA 0x2u       /* quotaInfo.IsPodExist (the pod is in its quota's PodCache): the dry run's
+                                       quota used follows its removal / re-add (elasticquota/plugin.go:263-301) */
+#define KS_NPOD_TERMINATING 0x4u    /* DeletionTimestamp != nil (PodEligibleToPreemptOthers, preempt.go:80-90) */
+typedef struct ks_node_pod_cols {
+  const int32_t *node;         /* node row (NodeInfo) */
+  const int32_t *priority;     /* corev1helpers.PodPriority */
+  const int64_t *start_time;   /* util.GetPodStartTime, any monotone unit (e.g. unix ns) */
+  const uint32_t *flags;       /* KS_NPOD_*; NULL = KS_NPOD_IN_QUOTA */
+  const int32_t *quota;        /* quota row, -1 = none (never a victim: the preemptor has a quota) */
+  const int32_t *pdb;          /* PodDisruptionBudget index, -1 = none; NULL = none */
+  /* the pod's part of NodeInfo.Requested (upstream computePodResourceRequest), removed / re-added by the dry run */
+  const int64_t *req_milli_cpu;
+  const int64_t *req_memory;
+  const int64_t *req_ephemeral;
+  const int64_t *req_scalar[KS_MAX_SCALARS]; /* NULL = 0 */
+  const int64_t *quota_req[KS_QUOTA_DIMS];   /* core.PodRequestsAndLimits requests per quota dimension; NULL = 0 */
+} ks_node_pod_cols;
+
+/* ks_preempt result (upstream preemption.Evaluator.Preempt, k8s v1.24 framework/preemption/preemption.go, driven by the
+ * ElasticQuota plugin's SelectVictimsOnNode / PodEligibleToPreemptOthers / GetOffsetAndNumCandidates) */
+#define KS_P_NOMINATED 0    /* Success: PostFilterResult.NominatedNodeName = node; delete the victims */
+#define KS_P_NOT_ELIGIBLE 1 /* Unschedulable: PodEligibleToPreemptOthers refused (PreemptNever, or a terminating
+                               lower-priority pod of the same quota on the nominated node) */
+#define KS_P_NO_CANDIDATE 2 /* Unschedulable: no node where preemption helps (FitError) */
+#define KS_P_ERROR 3        /* Error: no candidate and some node's dry run failed with an error (KS_PN_ERROR) */
+typedef struct ks_preempt_result {
+  int32_t node;               /* nominated node row, -1 = none */
+  uint32_t status;            /* KS_P_* */
+  int32_t num_victims;        /* len(Victims.Pods) of the chosen node */
+  int32_t num_pdb_violations; /* Victims.NumPDBViolations */
+  int32_t candidates;         /* nodes whose dry run found victims (len(candidates)) */
+  int32_t potential_nodes;    /* nodesWherePreemptionMightHelp */
+} ks_preempt_result;
+/* per-node dry-run outcome (ks_preempt node_status) */
+#define KS_PN_CANDIDATE 0   /* victims found: a candidate */
+#define KS_PN_UNRESOLVABLE 1 /* the node's filter status was UnschedulableAndUnresolvable: not a potential node */
+#define KS_PN_NO_VICTIMS 2  /* "No victims found on node" (UnschedulableAndUnresolvable) */
+#define KS_PN_FILTER 3      /* the filters fail with every potential victim removed */
+#define KS_PN_ERROR 4       /* Error: a victim removed twice (reprievePod's quota branch after a failed fit, preempt.go:192-199
+                               after :180-186) or every potential victim reprieved ("expected at least one victim pod") */
+
 typedef struct ks_ctx ks_ctx;
 
 /* The layout this library was compiled with, for a binding to refuse a library built from another header (a stale
  * .so whose score-matrix width or struct sizes differ writes past the caller's buffers): out[0] = KS_ABI_VERSION,
  * out[1] = KS_NUM_SCORE_PLUGINS, then sizeof ks_config, ks_node_cols, ks_pod_cols, ks_quota_cols, ks_quota_tree,
  * ks_reservation_cols, ks_device_cols, ks_cpu_topology, ks_cpu_state_cols, ks_numa_node_cols, ks_result,
- * ks_node_state, ks_stats (KS_ABI_LAYOUT_WORDS words; n < that fills the first n).  Returns KS_ABI_LAYOUT_WORDS. */
-#define KS_ABI_LAYOUT_WORDS 15
+ * ks_node_state, ks_stats, ks_node_pod_cols, ks_preempt_result (KS_ABI_LAYOUT_WORDS words; n < that fills the first n).  Returns KS_ABI_LAYOUT_WORDS. */
+#define KS_ABI_LAYOUT_WORDS 17
 int ks_abi_layout(int64_t *out, int32_t n);
 
 /* Returns KS_OK and *out on success.  On failure *out is NULL and
@@ -769,6 +816,27 @@ int ks_set_pipeline(ks_ctx *ctx, int32_t mode);
  * findNodesThatPassFilters + prioritizeNodes).  ks_shard_unique_id is called on rank 0 and the
  * bytes broadcast by the host; virtual_shards > 1 splits one GPU's range into several shards
  * (exercises the merge on one GPU). */
+/* ---- preemption (ElasticQuota PostFilter, pkg/scheduler/plugins/elasticquota/plugin.go:302-321, preempt.go) ---- */
+/* NodeInfo.Pods of every loaded node (replaces the table; m rows) and the PodDisruptionBudgets' DisruptionsAllowed
+ * (npdb entries).  Call after ks_load_nodes; refresh at a ks_schedule boundary from the informer's pod events
+ * (including the pods ks_schedule placed). */
+int ks_load_node_pods(ks_ctx *ctx, const ks_node_pod_cols *pods, int64_t m, const int32_t *pdb_allowed, int32_t npdb);
+/* PostFilter of pod 0 of `pod` (priority `priority`, flags KS_PREEMPT_*, nominated node row or -1) after a failed
+ * scheduling cycle: unresolvable[n] != 0 for the nodes whose filter status was UnschedulableAndUnresolvable (NULL =
+ * none, e.g. an ElasticQuota PreFilter rejection, which gives every node Unschedulable).  Every node's dry run
+ * (SelectVictimsOnNode: the same-quota lower-priority preemptible pods removed, the Filter plugins, the PDB split, the
+ * reprieve loop with the quota check) runs on the device; the candidate is chosen as pickOneNodeForPreemption does,
+ * remaining ties to the lowest node row.  victims[0..min(cap, num_victims)) get the chosen node's victims as rows of
+ * the ks_load_node_pods table, in Victims.Pods order; node_status[n] (optional) the KS_PN_* of every node.  Nothing
+ * is changed: the caller deletes the victims (prepareCandidate) and refreshes the tables.  Supported with Fit,
+ * LoadAware, ElasticQuota (required; the pod needs a quota row), BalancedAllocation, TaintToleration and NodeAffinity;
+ * Reservation, NodeNUMAResource, DeviceShare and NodePorts (filters that read other pods of the node) give
+ * KS_EUNSUPPORTED. */
+#define KS_PREEMPT_NEVER 0x1u /* pod.Spec.PreemptionPolicy == Never */
+int ks_preempt(ks_ctx *ctx, const ks_pod_cols *pod, int32_t priority, uint32_t flags, int32_t nominated_node,
+               const uint8_t *unresolvable, ks_preempt_result *out, int32_t *victims, int32_t victims_cap,
+               uint8_t *node_status);
+
 int ks_shard_unique_id(uint8_t *out /* KS_SHARD_ID_BYTES */);
 int ks_shard_init(ks_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *unique_id, int32_t virtual_shards);
 /* Test transport for the nranks > 1 path without RCCL: ctxs[0..nranks) (contexts of this process, each loaded with the

@@ -472,6 +472,50 @@ EXPORTED_SYMBOLS = [
     "ks_shard_unique_id",
     "ks_shard_init",
     "ks_shard_init_loopback",
+    "ks_load_node_pods",
+    "ks_preempt",
 ]
 KS_SHARD_ID_BYTES = 128
-KS_ABI_LAYOUT_WORDS = 15
+
+# ---- preemption (ElasticQuota PostFilter) ----
+KS_NPOD_NONPREEMPTIBLE = 0x1
+KS_NPOD_IN_QUOTA = 0x2
+KS_NPOD_TERMINATING = 0x4
+KS_P_NOMINATED = 0
+KS_P_NOT_ELIGIBLE = 1
+KS_P_NO_CANDIDATE = 2
+KS_P_ERROR = 3
+KS_PN_CANDIDATE = 0
+KS_PN_UNRESOLVABLE = 1
+KS_PN_NO_VICTIMS = 2
+KS_PN_FILTER = 3
+KS_PN_ERROR = 4
+KS_PREEMPT_NEVER = 0x1
+
+
+class KsNodePodCols(C.Structure):
+    _fields_ = [
+        ("node", P32),
+        ("priority", P32),
+        ("start_time", P64),
+        ("flags", PU32),
+        ("quota", P32),
+        ("pdb", P32),
+        ("req_milli_cpu", P64),
+        ("req_memory", P64),
+        ("req_ephemeral", P64),
+        ("req_scalar", P64 * KS_MAX_SCALARS),
+        ("quota_req", P64 * KS_QUOTA_DIMS),
+    ]
+
+
+class KsPreemptResult(C.Structure):
+    _fields_ = [
+        ("node", C.c_int32),
+        ("status", C.c_uint32),
+        ("num_victims", C.c_int32),
+        ("num_pdb_violations", C.c_int32),
+        ("candidates", C.c_int32),
+        ("potential_nodes", C.c_int32),
+    ]
+KS_ABI_LAYOUT_WORDS = 17

@@ -514,6 +514,63 @@ class ReservationTable:
         return c
 
 
+class NodePodTable:
+    """NodeInfo.Pods of every node for the preemption dry runs (ks_node_pod_cols): one row per running pod with its
+    node, priority, start time, KS_NPOD_* flags, quota row, PodDisruptionBudget index, its part of NodeInfo.Requested
+    ([dim][row]: cpu, memory, ephemeral-storage, scalar[k]) and its quota request (PodRequestsAndLimits,
+    [dim][row]); plus the PodDisruptionBudgets' DisruptionsAllowed."""
+
+    def __init__(self, m: int, npdb: int = 0):
+        self.m = int(m)
+        self.node = np.zeros(self.m, np.int32)
+        self.priority = np.zeros(self.m, np.int32)
+        self.start_time = np.zeros(self.m, np.int64)
+        self.flags = np.full(self.m, abi.KS_NPOD_IN_QUOTA, np.uint32)
+        self.quota = np.full(self.m, -1, np.int32)
+        self.pdb = np.full(self.m, -1, np.int32)
+        self.req = np.zeros((abi.KS_RSV_DIMS, self.m), np.int64)
+        self.quota_req = np.zeros((abi.KS_QUOTA_DIMS, self.m), np.int64)
+        self.pdb_allowed = np.zeros(int(npdb), np.int32)
+
+    def copy(self) -> "NodePodTable":
+        t = NodePodTable(self.m, len(self.pdb_allowed))
+        for k in ("node", "priority", "start_time", "flags", "quota", "pdb", "req", "quota_req", "pdb_allowed"):
+            setattr(t, k, getattr(self, k).copy())
+        return t
+
+    def rows(self, idx) -> "NodePodTable":
+        idx = np.asarray(idx)
+        t = NodePodTable(len(idx), len(self.pdb_allowed))
+        for k in ("node", "priority", "start_time", "flags", "quota", "pdb"):
+            setattr(t, k, getattr(self, k)[idx].copy())
+        t.req = self.req[:, idx].copy()
+        t.quota_req = self.quota_req[:, idx].copy()
+        t.pdb_allowed = self.pdb_allowed.copy()
+        return t
+
+    def ks(self) -> abi.KsNodePodCols:
+        c = abi.KsNodePodCols()
+        for name, dt in (("node", np.int32), ("priority", np.int32), ("start_time", np.int64), ("flags", np.uint32),
+                         ("quota", np.int32), ("pdb", np.int32), ("req", np.int64), ("quota_req", np.int64),
+                         ("pdb_allowed", np.int32)):
+            setattr(self, name, np.ascontiguousarray(getattr(self, name), dt))
+        c.node = _p32(self.node)
+        c.priority = _p32(self.priority)
+        c.start_time = _p64(self.start_time)
+        c.flags = _pu32(self.flags)
+        c.quota = _p32(self.quota)
+        c.pdb = _p32(self.pdb)
+        c.req_milli_cpu = _p64(self.req[0])
+        c.req_memory = _p64(self.req[1])
+        c.req_ephemeral = _p64(self.req[2])
+        for k in range(abi.KS_MAX_SCALARS):
+            c.req_scalar[k] = _p64(self.req[3 + k])
+        for d in range(abi.KS_QUOTA_DIMS):
+            c.quota_req[d] = _p64(self.quota_req[d])
+        c._keep = self
+        return c
+
+
 class NodeState:
     """Host buffers for ks_read_nodes / ko_read_nodes."""
 

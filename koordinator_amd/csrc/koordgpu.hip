@@ -34,6 +34,7 @@
 #include "ks_pass.h"
 #include "ks_mono.h"
 #include "ks_debug.h"
+#include "ks_preempt.h"
 
 using namespace ks;
 
@@ -1065,6 +1066,15 @@ struct ks_ctx {
   hipEvent_t pev_com[kPipeEvents] = {};
   int64_t pipe_k = 0;               // pass index within the current ks_schedule* call
   int32_t pipe_mode = -1;           // ks_set_pipeline (-1: KS_PIPE, default automatic)
+  // preemption (ks_load_node_pods / ks_preempt, ks_preempt.h)
+  void* npod_blob = nullptr;       // the node-pod table (positions sorted per node) + per-call scratch
+  DevNodePods npt{};
+  int32_t npod_slots = 0;          // positions per lane of the dry run (max pods on a node / 64, rounded up)
+  PreemptCand* pre_cand = nullptr; // [n]
+  int32_t* pre_vrank = nullptr;    // [m]
+  uint8_t* pre_status = nullptr;   // [n]
+  PreemptOut* pre_out = nullptr;
+  int32_t* pre_victims = nullptr;  // [kPreemptMaxPods]
   // stats
   ks_stats stats{};
   std::vector<hipEvent_t> ev_pool;
@@ -1200,7 +1210,7 @@ int ks_abi_layout(int64_t* out, int32_t n) {
       KS_ABI_VERSION, KS_NUM_SCORE_PLUGINS, sizeof(ks_config), sizeof(ks_node_cols), sizeof(ks_pod_cols),
       sizeof(ks_quota_cols), sizeof(ks_quota_tree), sizeof(ks_reservation_cols), sizeof(ks_device_cols),
       sizeof(ks_cpu_topology), sizeof(ks_cpu_state_cols), sizeof(ks_numa_node_cols), sizeof(ks_result),
-      sizeof(ks_node_state), sizeof(ks_stats)};
+      sizeof(ks_node_state), sizeof(ks_stats), sizeof(ks_node_pod_cols), sizeof(ks_preempt_result)};
   for (int32_t i = 0; out && i < n && i < KS_ABI_LAYOUT_WORDS; ++i) out[i] = v[i];
   return KS_ABI_LAYOUT_WORDS;
 }
@@ -1389,6 +1399,7 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->dnv; dev_free(p);
   p = ctx->pipe; dev_free(p);
   p = ctx->pipe_top; dev_free(p);
+  dev_free(ctx->npod_blob);
   for (int i = 0; i < kPipeEvents; ++i) {
     if (ctx->pev_sel[i]) (void)hipEventDestroy(ctx->pev_sel[i]);
     if (ctx->pev_com[i]) (void)hipEventDestroy(ctx->pev_com[i]);
@@ -4465,6 +4476,188 @@ int ks_read_quota_used(ks_ctx* ctx, int64_t* used) {
   if (!ctx->quota_blob || ctx->q.q == 0) return KS_OK;
   HIPCHK(ctx, hipMemcpyAsync(used, ctx->q.used, (size_t)ctx->q.q * KS_QUOTA_DIMS * 8, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+// ---- preemption: the ElasticQuota PostFilter (ks_preempt.h) ----
+
+int ks_load_node_pods(ks_ctx* ctx, const ks_node_pod_cols* pc, int64_t m, const int32_t* pdb_allowed, int32_t npdb) {
+  if (!ctx || !pc || m < 0 || npdb < 0 || (m > 0 && !pc->node) || (npdb > 0 && !pdb_allowed))
+    return ctx ? (ctx->err = "ks_load_node_pods: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_load_node_pods before ks_load_nodes");
+  if (m >= ((int64_t)1 << 31)) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: too many pods");
+  const int64_t n = ctx->n;
+  std::vector<int64_t> beg((size_t)n + 1, 0);
+  for (int64_t i = 0; i < m; ++i) {
+    const int32_t nd = pc->node[i];
+    if (nd < 0 || nd >= n) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: pod %lld on node %d outside [0, %lld)", (long long)i, nd, (long long)n);
+    const int32_t q = pc->pdb ? pc->pdb[i] : -1;
+    if (q < -1 || q >= npdb) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: pod %lld: PDB index %d outside [-1, %d)", (long long)i, q, npdb);
+    ++beg[(size_t)nd + 1];
+  }
+  int32_t maxc = 0;
+  for (int64_t v = 0; v < n; ++v) {
+    maxc = std::max<int32_t>(maxc, (int32_t)beg[(size_t)v + 1]);
+    beg[(size_t)v + 1] += beg[(size_t)v];
+  }
+  if (maxc > kPreemptMaxPods)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_load_node_pods: a node holds %d pods (the dry run holds up to %d)", maxc, kPreemptMaxPods);
+  for (int32_t i = 0; i < npdb; ++i)
+    if (pdb_allowed[i] < -(1 << 30) || pdb_allowed[i] > (1 << 30)) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: DisruptionsAllowed out of range");
+  const int64_t* reqc[kRsvDims] = {pc->req_milli_cpu, pc->req_memory, pc->req_ephemeral, pc->req_scalar[0],
+                                   pc->req_scalar[1], pc->req_scalar[2], pc->req_scalar[3]};
+  for (int dd = 0; dd < kRsvDims; ++dd)
+    if (int rc = check_range64(ctx, reqc[dd], m, "node pod request"); rc != KS_OK) return rc;
+  for (int dd = 0; dd < KS_QUOTA_DIMS; ++dd)
+    if (int rc = check_range64(ctx, pc->quota_req[dd], m, "node pod quota request"); rc != KS_OK) return rc;
+  // positions: per node, util.MoreImportantPod order (priority desc, start time asc), equal pairs in caller order
+  std::vector<int32_t> order((size_t)m);
+  for (int64_t i = 0; i < m; ++i) order[(size_t)i] = (int32_t)i;
+  auto prio = [&](int32_t i) { return pc->priority ? pc->priority[i] : 0; };
+  auto start = [&](int32_t i) { return pc->start_time ? pc->start_time[i] : (int64_t)0; };
+  std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+    if (pc->node[x] != pc->node[y]) return pc->node[x] < pc->node[y];
+    if (prio(x) != prio(y)) return prio(x) > prio(y);
+    if (start(x) != start(y)) return start(x) < start(y);
+    return x < y;
+  });
+  const size_t mm = (size_t)std::max<int64_t>(m, 1), nn = (size_t)n + 1;
+  // one blob: beg, then the position columns, the PDB budgets and the per-call scratch
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off = align16(off + bytes); return o; };
+  const size_t o_beg = take(nn * 8), o_prio = take(mm * 4), o_start = take(mm * 8), o_flags = take(mm * 4),
+               o_quota = take(mm * 4), o_pdb = take(mm * 4), o_row = take(mm * 4), o_req = take(mm * 8 * kRsvDims),
+               o_qreq = take(mm * 8 * KS_QUOTA_DIMS), o_pdba = take((size_t)std::max(npdb, 1) * 4),
+               o_cand = take(nn * sizeof(PreemptCand)), o_vrank = take(mm * 4), o_status = take(nn),
+               o_out = take(sizeof(PreemptOut)), o_vic = take((size_t)kPreemptMaxPods * 4);
+  std::vector<unsigned char> h(off, 0);
+  auto put = [&](size_t o, size_t i, const void* v, size_t w) { memcpy(h.data() + o + i * w, v, w); };
+  memcpy(h.data() + o_beg, beg.data(), nn * 8);
+  for (size_t pos = 0; pos < (size_t)m; ++pos) {
+    const int32_t i = order[pos];
+    const int32_t pr = prio(i);
+    const int64_t st = start(i);
+    const uint32_t fl = pc->flags ? pc->flags[i] : KS_NPOD_IN_QUOTA;
+    const int32_t q = pc->quota ? pc->quota[i] : -1, pd = pc->pdb ? pc->pdb[i] : -1;
+    put(o_prio, pos, &pr, 4);
+    put(o_start, pos, &st, 8);
+    put(o_flags, pos, &fl, 4);
+    put(o_quota, pos, &q, 4);
+    put(o_pdb, pos, &pd, 4);
+    put(o_row, pos, &i, 4);
+    for (int dd = 0; dd < kRsvDims; ++dd) {
+      const int64_t v = reqc[dd] ? reqc[dd][i] : 0;
+      put(o_req, (size_t)dd * mm + pos, &v, 8);
+    }
+    for (int dd = 0; dd < KS_QUOTA_DIMS; ++dd) {
+      const int64_t v = pc->quota_req[dd] ? pc->quota_req[dd][i] : 0;
+      put(o_qreq, (size_t)dd * mm + pos, &v, 8);
+    }
+  }
+  if (npdb) memcpy(h.data() + o_pdba, pdb_allowed, (size_t)npdb * 4);
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  dev_free(ctx->npod_blob);
+  if (dev_alloc(ctx, &ctx->npod_blob, off) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemcpyAsync(ctx->npod_blob, h.data(), off, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  unsigned char* b = (unsigned char*)ctx->npod_blob;
+  DevNodePods& t = ctx->npt;
+  t.beg = (const int64_t*)(b + o_beg);
+  t.prio = (const int32_t*)(b + o_prio);
+  t.start = (const int64_t*)(b + o_start);
+  t.flags = (const uint32_t*)(b + o_flags);
+  t.quota = (const int32_t*)(b + o_quota);
+  t.pdb = (const int32_t*)(b + o_pdb);
+  t.row = (const int32_t*)(b + o_row);
+  t.req = (const int64_t*)(b + o_req);
+  t.qreq = (const int64_t*)(b + o_qreq);
+  t.pdb_allowed = (const int32_t*)(b + o_pdba);
+  t.m = (int64_t)mm;
+  t.npdb = npdb;
+  ctx->pre_cand = (PreemptCand*)(b + o_cand);
+  ctx->pre_vrank = (int32_t*)(b + o_vrank);
+  ctx->pre_status = (uint8_t*)(b + o_status);
+  ctx->pre_out = (PreemptOut*)(b + o_out);
+  ctx->pre_victims = (int32_t*)(b + o_vic);
+  ctx->npod_slots = maxc <= 64 ? 1 : (maxc <= 128 ? 2 : 4);
+  return KS_OK;
+}
+
+int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t flags, int32_t nominated,
+               const uint8_t* unresolvable, ks_preempt_result* out, int32_t* victims, int32_t victims_cap,
+               uint8_t* node_status) {
+  if (!ctx || !pod || !out || victims_cap < 0 || (victims_cap > 0 && !victims))
+    return ctx ? (ctx->err = "ks_preempt: bad args", KS_EINVAL) : KS_EINVAL;
+  if (!ctx->npod_blob) KS_FAIL(ctx, KS_ESTATE, "ks_preempt before ks_load_node_pods");
+  if (!ctx->cfg.quota.enable || !ctx->quota_blob || ctx->q.q == 0)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_preempt: the ElasticQuota PostFilter needs ElasticQuota and a loaded quota table");
+  if (ctx->kc.rsv || ctx->kc.numa || ctx->kc.dev || (ctx->kc.ports & 1))
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_preempt: Reservation / NodeNUMAResource / DeviceShare / NodePorts filters read the "
+                                  "node's other pods (their PreFilter extensions are not modelled)");
+  const int32_t q = pod->quota ? pod->quota[0] : -1;
+  if (q < 0 || q >= ctx->q.q)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_preempt: the pod has no quota row (the reference's cloned PostFilterState has no "
+                                  "QuotaInfo then)");
+  if (nominated < -1 || nominated >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_preempt: nominated node %d out of range", nominated);
+  if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  if (ensure_stage(ctx, ctx->est, 1) != KS_OK) return KS_ENOMEM;
+  if (stage_cols(ctx, ctx->est, pod, 1) != KS_OK || prep_stage(ctx, ctx->est, 1) != KS_OK) return KS_EHIP;
+  const int64_t n = ctx->n;
+  uint8_t* dunres = nullptr;
+  if (unresolvable && n > 0) {
+    // the caller's per-node statuses, staged through the ks_eval_pod scratch
+    if (ctx->evbuf_bytes < (size_t)n) {
+      dev_free(ctx->evbuf);
+      ctx->evbuf_bytes = 0;
+      if (dev_alloc(ctx, &ctx->evbuf, (size_t)n) != KS_OK) return KS_ENOMEM;
+      ctx->evbuf_bytes = (size_t)n;
+    }
+    dunres = (uint8_t*)ctx->evbuf;
+    HIPCHK(ctx, hipMemcpyAsync(dunres, unresolvable, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+  }
+  PreemptArgs a;
+  a.dn = ctx->dnodes;
+  a.t = ctx->npt;
+  a.q = ctx->q;
+  a.pq = ctx->est.pq;
+  a.c = ctx->kc;
+  a.pod = ctx->est.recs;
+  a.pst = ctx->est.stat;
+  a.prio = priority;
+  a.pflags = flags;
+  a.nominated = nominated;
+  a.unresolvable = dunres;
+  a.n = n;
+  a.cand = ctx->pre_cand;
+  a.vrank = ctx->pre_vrank;
+  a.status = ctx->pre_status;
+  a.out = ctx->pre_out;
+  a.victims = ctx->pre_victims;
+  HIPCHK(ctx, hipMemsetAsync(ctx->pre_vrank, 0xFF, (size_t)ctx->npt.m * 4, ctx->stream));
+  if (n > 0) {
+    const dim3 grid((unsigned)((n + 3) / 4)), block(256);
+    if (ctx->npod_slots == 1) hipLaunchKernelGGL(preempt_dry_run_kernel<1>, grid, block, 0, ctx->stream, a);
+    else if (ctx->npod_slots == 2) hipLaunchKernelGGL(preempt_dry_run_kernel<2>, grid, block, 0, ctx->stream, a);
+    else hipLaunchKernelGGL(preempt_dry_run_kernel<4>, grid, block, 0, ctx->stream, a);
+  }
+  hipLaunchKernelGGL(preempt_select_kernel, dim3(1), dim3(kPreemptSelThreads), 0, ctx->stream, a);
+  HIPCHK(ctx, hipGetLastError());
+  PreemptOut o{};
+  HIPCHK(ctx, hipMemcpyAsync(&o, ctx->pre_out, sizeof(o), hipMemcpyDeviceToHost, ctx->stream));
+  if (node_status && n > 0) HIPCHK(ctx, hipMemcpyAsync(node_status, ctx->pre_status, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const int32_t nv = std::min(o.nvict, victims_cap);
+  if (nv > 0) {
+    HIPCHK(ctx, hipMemcpyAsync(victims, ctx->pre_victims, (size_t)nv * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  out->node = o.node;
+  out->status = o.status;
+  out->num_victims = o.nvict;
+  out->num_pdb_violations = o.nviol;
+  out->candidates = o.candidates;
+  out->potential_nodes = o.potential;
   return KS_OK;
 }
 

@@ -14,7 +14,8 @@ from typing import Optional
 import numpy as np
 
 from . import abi
-from .cluster import CpuState, DeviceTable, NumaNodes, NodeState, NodeTable, PodTable, QuotaTable, QuotaTree, ReservationTable
+from .cluster import (CpuState, DeviceTable, NodePodTable, NumaNodes, NodeState, NodeTable, PodTable, QuotaTable,
+                      QuotaTree, ReservationTable)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KS_LIB_PATH") or os.path.join(HERE, "libkoordgpu.so")
@@ -97,6 +98,9 @@ def lib() -> C.CDLL:
     L.ks_shard_init.argtypes = [vp, C.c_int32, C.c_int32, C.POINTER(C.c_uint8), C.c_int32]
     L.ks_shard_init_loopback.argtypes = [C.POINTER(vp), C.c_int32, C.c_int32]
     L.ks_abi_layout.argtypes = [abi.P64, C.c_int32]
+    L.ks_load_node_pods.argtypes = [vp, C.POINTER(abi.KsNodePodCols), C.c_int64, abi.P32, C.c_int32]
+    L.ks_preempt.argtypes = [vp, C.POINTER(abi.KsPodCols), C.c_int32, C.c_uint32, C.c_int32, C.POINTER(C.c_uint8),
+                             C.POINTER(abi.KsPreemptResult), abi.P32, C.c_int32, C.POINTER(C.c_uint8)]
     for name in abi.EXPORTED_SYMBOLS:
         if name not in ("ks_destroy", "ks_last_error"):
             getattr(L, name).restype = C.c_int
@@ -110,7 +114,7 @@ def expected_layout() -> list:
     return [abi.KS_ABI_VERSION, abi.KS_NUM_SCORE_PLUGINS] + [C.sizeof(t) for t in (
         abi.KsConfig, abi.KsNodeCols, abi.KsPodCols, abi.KsQuotaCols, abi.KsQuotaTree, abi.KsReservationCols,
         abi.KsDeviceCols, abi.KsCpuTopology, abi.KsCpuStateCols, abi.KsNumaNodeCols, abi.KsResult, abi.KsNodeState,
-        abi.KsStats)]
+        abi.KsStats, abi.KsNodePodCols, abi.KsPreemptResult)]
 
 
 def check_layout(L) -> None:
@@ -431,6 +435,34 @@ class Evaluator:
         cols = pods.ks()
         self._chk(self.L.ks_schedule(self.h, C.byref(cols), pods.n, out.ctypes.data_as(C.POINTER(abi.KsResult))))
         return out[: pods.n]
+
+    def load_node_pods(self, t: NodePodTable):
+        """NodeInfo.Pods of every node + the PDBs' DisruptionsAllowed, the victims pool of preempt()"""
+        cols = t.ks()
+        self._chk(self.L.ks_load_node_pods(self.h, C.byref(cols), t.m, t.pdb_allowed.ctypes.data_as(abi.P32),
+                                           len(t.pdb_allowed)))
+        self.npods = t.m
+
+    def preempt(self, pod: PodTable, priority: int, flags: int = 0, nominated_node: int = -1, unresolvable=None,
+                node_status: bool = False) -> dict:
+        """ElasticQuota PostFilter of pod 0 (ks_preempt): {status, node, victims (node-pod table rows, Victims.Pods
+        order), num_pdb_violations, candidates, potential_nodes[, node_status]}"""
+        out = abi.KsPreemptResult()
+        cap = max(getattr(self, "npods", 0), 1)
+        vic = np.zeros(cap, np.int32)
+        ns = np.zeros(max(self.n, 1), np.uint8) if node_status else None
+        ur = None if unresolvable is None else np.ascontiguousarray(unresolvable, np.uint8)
+        cols = pod.ks()
+        self._chk(self.L.ks_preempt(self.h, C.byref(cols), int(priority), int(flags), int(nominated_node),
+                                    ur.ctypes.data_as(C.POINTER(C.c_uint8)) if ur is not None else None, C.byref(out),
+                                    vic.ctypes.data_as(abi.P32), cap,
+                                    ns.ctypes.data_as(C.POINTER(C.c_uint8)) if ns is not None else None))
+        r = {"status": out.status, "node": out.node, "victims": vic[: out.num_victims].copy(),
+             "num_pdb_violations": out.num_pdb_violations, "candidates": out.candidates,
+             "potential_nodes": out.potential_nodes}
+        if ns is not None:
+            r["node_status"] = ns[: self.n].copy()
+        return r
 
     def read_nodes(self) -> NodeState:
         st = NodeState(self.n)

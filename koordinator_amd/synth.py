@@ -625,3 +625,94 @@ def c2_default(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, **kw)
     w = with_static_plugins(w)
     w.name = "C2-default"
     return w
+
+
+# ---- preemption (ks_preempt) ----
+
+PRIORITIES = np.array([0, 100, 1000, 3000, 5000, 8000], np.int32)
+
+
+def make_node_pods(nodes: NodeTable, rng: np.random.Generator, n_quotas: int, per_node=(4, 40), n_pdb: int = 12,
+                   pdb_frac: float = 0.15, nonpreemptible_frac: float = 0.08, terminating_frac: float = 0.02,
+                   out_of_quota_frac: float = 0.03):
+    """Running pods on every node (make_pods' request distribution), with priorities, distinct start times, quotas,
+    PDBs and flags.  The nodes' NodeInfo columns (Requested, NonZeroRequested, pod count) are set to the sums over their
+    pods, so the table is the NodeInfo.Pods the columns were built from.  Returns (NodePodTable, per-quota used [dim][q])
+    -- the quotas' used of their in-quota pods (QuotaInfo.CalculateInfo.Used)."""
+    from .cluster import NodePodTable
+
+    counts = rng.integers(per_node[0], per_node[1] + 1, nodes.n)
+    counts = np.minimum(counts, nodes.allowed_pods - 1)
+    m = int(counts.sum())
+    src = make_pods(m, rng, n_quotas)
+    t = NodePodTable(m, n_pdb)
+    t.node[:] = np.repeat(np.arange(nodes.n, dtype=np.int32), counts)
+    t.priority[:] = rng.choice(PRIORITIES, m)
+    t.start_time[:] = rng.permutation(m).astype(np.int64) * 1_000_000 + 1_700_000_000_000_000_000
+    fl = np.full(m, abi.KS_NPOD_IN_QUOTA, np.uint32)
+    fl[rng.random(m) < nonpreemptible_frac] |= abi.KS_NPOD_NONPREEMPTIBLE
+    fl[rng.random(m) < terminating_frac] |= abi.KS_NPOD_TERMINATING
+    fl[rng.random(m) < out_of_quota_frac] &= ~np.uint32(abi.KS_NPOD_IN_QUOTA)
+    t.flags[:] = fl
+    t.quota[:] = src.quota if n_quotas else -1
+    t.pdb[:] = np.where(rng.random(m) < pdb_frac, rng.integers(0, max(n_pdb, 1), m), -1) if n_pdb else -1
+    t.pdb_allowed[:] = rng.integers(0, 4, n_pdb)
+    t.req[0] = src.req_milli_cpu
+    t.req[1] = src.req_memory
+    t.req[2] = 0
+    t.req[3 + SLOT_BATCH_CPU] = src.req_scalar[SLOT_BATCH_CPU]
+    t.req[3 + SLOT_BATCH_MEMORY] = src.req_scalar[SLOT_BATCH_MEMORY]
+    t.quota_req[:] = src.quota_req
+    # NodeInfo = the sum over the node's pods
+    nodes.req_milli_cpu[:] = np.bincount(t.node, weights=t.req[0], minlength=nodes.n).astype(np.int64)
+    nodes.req_memory[:] = np.bincount(t.node, weights=t.req[1], minlength=nodes.n).astype(np.int64)
+    nodes.req_ephemeral[:] = 0
+    for k in (SLOT_BATCH_CPU, SLOT_BATCH_MEMORY):
+        nodes.req_scalar[k] = np.bincount(t.node, weights=t.req[3 + k], minlength=nodes.n).astype(np.int64)
+    nodes.nonzero_milli_cpu[:] = np.bincount(t.node, weights=src.nonzero_milli_cpu, minlength=nodes.n).astype(np.int64)
+    nodes.nonzero_memory[:] = np.bincount(t.node, weights=src.nonzero_memory, minlength=nodes.n).astype(np.int64)
+    nodes.pod_count[:] = counts.astype(np.int32)
+    used = np.zeros((abi.KS_QUOTA_DIMS, max(n_quotas, 1)), np.int64)
+    inq = ((t.flags & abi.KS_NPOD_IN_QUOTA) != 0) & (t.quota >= 0)
+    for d in range(abi.KS_QUOTA_DIMS):
+        used[d] = np.bincount(t.quota[inq], weights=t.quota_req[d][inq].astype(np.float64),
+                              minlength=max(n_quotas, 1)).astype(np.int64)
+    return t, used[:, :n_quotas]
+
+
+@dataclass
+class PreemptWorkload:
+    name: str
+    profile: SchedulerProfile
+    nodes: NodeTable
+    quotas: QuotaTable
+    node_pods: "NodePodTable"
+    preemptors: PodTable
+    priority: np.ndarray  # [preemptors.n]
+
+    @property
+    def cfg(self) -> abi.KsConfig:
+        return self.profile.to_ks_config()
+
+
+def c2_preempt(seed: int = SEED, n_nodes: int = 5000, n_preemptors: int = 64, n_quotas: int = 32, per_node=(4, 40),
+               headroom=(0.97, 1.03), tight_nodes: float = 0.6, **kw) -> PreemptWorkload:
+    """C2's cluster and profile (Fit + LoadAware + ElasticQuota) with NodeInfo.Pods on every node and quotas at their
+    runtime limits, so a new pod is rejected by the quota PreFilter (and every node's status is Unschedulable) or
+    finds no room: the ElasticQuota PostFilter then looks for same-quota lower-priority victims on every node."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nodes = make_nodes(n_nodes, rng)
+    t, used = make_node_pods(nodes, rng, n_quotas, per_node=per_node)
+    # a share of the nodes filled up (Requested close to Allocatable): preemption must free room there
+    tight = rng.random(n_nodes) < tight_nodes
+    nodes.alloc_milli_cpu[tight] = np.maximum(nodes.req_milli_cpu[tight] + rng.integers(0, 4000, int(tight.sum())) // 250 * 250,
+                                              1000)
+    q = QuotaTable(n_quotas)
+    q.limit_mask[:] = (1 << QDIM_CPU) | (1 << QDIM_MEMORY) | (1 << QDIM_BATCH_CPU) | (1 << QDIM_BATCH_MEMORY)
+    q.used[:] = used
+    q.limit[:] = (used * rng.uniform(headroom[0], headroom[1], (abi.KS_QUOTA_DIMS, n_quotas))).astype(np.int64)
+    q.min_mask[:] = q.limit_mask
+    q.min[:] = q.limit // 2
+    pre = make_pods(n_preemptors, rng, n_quotas)
+    prio = rng.choice(np.array([1000, 3000, 5000, 9000], np.int32), n_preemptors)
+    return PreemptWorkload("C2-preempt", koord_profile(with_quota=True, **kw), nodes, q, t, pre, prio)

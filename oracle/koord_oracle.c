@@ -208,6 +208,7 @@ typedef struct ko_sched {
   int64_t *numa_used;   /* [n][KS_MAX_NUMA][2]: allocatedResources */
   uint8_t *numa_present;
   int32_t *numa_cs;     /* allocated cpuset CPUs per NUMA node */
+  struct ko_npods *npods; /* NodeInfo.Pods of every node (ko_load_node_pods), the preemption victims pool */
 } ko_sched;
 
 /* pod view for one pod (values pulled out of ks_pod_cols) */
@@ -1904,6 +1905,8 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   return s;
 }
 
+static void npods_free(ko_sched *s);
+
 void ko_destroy(ko_sched *s) {
   if (!s) return;
   pool_destroy(s->pool);
@@ -1929,6 +1932,7 @@ void ko_destroy(ko_sched *s) {
   ko_rsv *rv = &s->rv;
   free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
   free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
+  npods_free(s);
   free(s);
 }
 
@@ -2691,5 +2695,334 @@ int ko_read_nodes(const ko_sched *s, ks_node_state *o) {
 int ko_read_quota_used(const ko_sched *s, int64_t *used) {
   for (int32_t i = 0; i < s->nq; i++)
     for (int d = 0; d < KS_QUOTA_DIMS; d++) used[(size_t)i * KS_QUOTA_DIMS + d] = s->q[i].used[d];
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* Preemption: the ElasticQuota PostFilter              */
+/* ------------------------------------------------------------------ */
+/*
+ * pkg/scheduler/plugins/elasticquota/plugin.go:302-321 (PostFilter -> preemption.Evaluator.Preempt with the plugin
+ * as the Interface), preempt.go (GetOffsetAndNumCandidates :42-44, PodEligibleToPreemptOthers :60-97,
+ * SelectVictimsOnNode :113-217, filterPodsWithPDBViolation :223-265, canPreempt :283-294), the PreFilter extensions
+ * AddPod / RemovePod plugin.go:263-301 on the PostFilterState snapshot of PreFilter (plugin_helper.go:250-259;
+ * PostFilterState.Clone plugin.go:65-72), and upstream kube-scheduler v1.24.15 framework/preemption/preemption.go
+ * (Preempt, findCandidates, nodesWherePreemptionMightHelp, DryRunPreemption, SelectCandidate,
+ * pickOneNodeForPreemption) + util.MoreImportantPod / GetEarliestPodStartTime -- upstream is not on disk, so that
+ * part is parity unpinned (restated from the v1.24 source as published).  Restated object by object: each node's dry
+ * run works on a copy of its NodeInfo (the pod list, Requested, the pod count) and of the PostFilterState, removes and
+ * re-adds pods one at a time (NodeInfo.RemovePod fails for a pod that is not on the node), and sorts the potential
+ * victims with a comparison sort.  Where the reference leaves an order unspecified -- sort.Slice over equal
+ * (priority, start time), the candidates map in pickOneNodeForPreemption -- the table order / the lowest node row
+ * decides.
+ */
+typedef struct ko_npods {
+  int64_t m;
+  int32_t *node, *prio, *quota, *pdb;
+  int64_t *start;
+  uint32_t *flags;
+  int64_t *req;  /* [m][KO_D] */
+  int64_t *qreq; /* [m][KS_QUOTA_DIMS] */
+  int64_t *beg;  /* [n + 1] CSR of the rows of each node in table order (NodeInfo.Pods order) */
+  int32_t *rows;
+  int32_t npdb;
+  int32_t *pdb_allowed;
+} ko_npods;
+
+static void npods_free(ko_sched *s) {
+  ko_npods *t = s->npods;
+  if (!t) return;
+  free(t->node); free(t->prio); free(t->quota); free(t->pdb); free(t->start); free(t->flags); free(t->req);
+  free(t->qreq); free(t->beg); free(t->rows); free(t->pdb_allowed);
+  free(t);
+  s->npods = NULL;
+}
+
+int ko_load_node_pods(ko_sched *s, const ks_node_pod_cols *pc, int64_t m, const int32_t *pdb_allowed, int32_t npdb) {
+  npods_free(s);
+  ko_npods *t = calloc(1, sizeof(*t));
+  size_t mm = (size_t)(m > 0 ? m : 1);
+  t->m = m;
+  t->node = malloc(mm * 4); t->prio = malloc(mm * 4); t->quota = malloc(mm * 4); t->pdb = malloc(mm * 4);
+  t->start = malloc(mm * 8); t->flags = malloc(mm * 4);
+  t->req = malloc(mm * KO_D * 8); t->qreq = malloc(mm * KS_QUOTA_DIMS * 8);
+  t->beg = calloc((size_t)s->n + 1, 8); t->rows = malloc(mm * 4);
+  t->npdb = npdb;
+  t->pdb_allowed = malloc((size_t)(npdb > 0 ? npdb : 1) * 4);
+  for (int32_t i = 0; i < npdb; i++) t->pdb_allowed[i] = pdb_allowed[i];
+  for (int64_t i = 0; i < m; i++) {
+    t->node[i] = pc->node[i];
+    if (t->node[i] < 0 || t->node[i] >= s->n) { npods_free(s); s->npods = NULL; free(t); return -1; }
+    t->prio[i] = pc->priority ? pc->priority[i] : 0;
+    t->quota[i] = pc->quota ? pc->quota[i] : -1;
+    t->pdb[i] = pc->pdb ? pc->pdb[i] : -1;
+    t->start[i] = pc->start_time ? pc->start_time[i] : 0;
+    t->flags[i] = pc->flags ? pc->flags[i] : KS_NPOD_IN_QUOTA;
+    int64_t *r = t->req + i * KO_D;
+    r[0] = colv64(pc->req_milli_cpu, i);
+    r[1] = colv64(pc->req_memory, i);
+    r[2] = colv64(pc->req_ephemeral, i);
+    for (int k = 0; k < KS_MAX_SCALARS; k++) r[3 + k] = colv64(pc->req_scalar[k], i);
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) t->qreq[i * KS_QUOTA_DIMS + d] = colv64(pc->quota_req[d], i);
+    t->beg[t->node[i] + 1]++;
+  }
+  for (int64_t n = 0; n < s->n; n++) t->beg[n + 1] += t->beg[n];
+  int64_t *fill = malloc(((size_t)s->n + 1) * 8);
+  memcpy(fill, t->beg, ((size_t)s->n + 1) * 8);
+  for (int64_t i = 0; i < m; i++) t->rows[fill[t->node[i]]++] = (int32_t)i;
+  free(fill);
+  s->npods = t;
+  return 0;
+}
+
+/* framework.NodeInfo of one node, as the dry run mutates its copy: the pods and what the Filter plugins read */
+typedef struct {
+  int32_t *rows; /* NodeInfo.Pods (table rows) */
+  int32_t n;
+  ko_eff e;      /* Requested, pod count */
+} ko_ninfo;
+
+/* ElasticQuota PostFilterState (plugin.go:57-63) */
+typedef struct {
+  int32_t quota;
+  int64_t used[KS_QUOTA_DIMS];
+} ko_pfstate;
+
+/* NodeInfo.RemovePod + RunPreFilterExtensionRemovePod (ElasticQuota RemovePod, plugin.go:283-299):
+ * -1 when the pod is not on the node */
+static int dry_remove(const ko_npods *t, ko_ninfo *ni, ko_pfstate *st, int32_t row) {
+  int32_t at = -1;
+  for (int32_t i = 0; i < ni->n; i++)
+    if (ni->rows[i] == row) at = i;
+  if (at < 0) return -1;
+  memmove(ni->rows + at, ni->rows + at + 1, (size_t)(ni->n - at - 1) * 4);
+  ni->n--;
+  for (int d = 0; d < KO_D; d++) ni->e.req[d] -= t->req[(size_t)row * KO_D + d];
+  ni->e.pods--;
+  if (t->flags[row] & KS_NPOD_IN_QUOTA) /* quotav1.SubtractWithNonNegativeResult */
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) {
+      const int64_t v = st->used[d] - t->qreq[(size_t)row * KS_QUOTA_DIMS + d];
+      st->used[d] = v > 0 ? v : 0;
+    }
+  return 0;
+}
+
+/* NodeInfo.AddPodInfo + RunPreFilterExtensionAddPod (ElasticQuota AddPod, plugin.go:263-279) */
+static void dry_add(const ko_npods *t, ko_ninfo *ni, ko_pfstate *st, int32_t row) {
+  ni->rows[ni->n++] = row;
+  for (int d = 0; d < KO_D; d++) ni->e.req[d] += t->req[(size_t)row * KO_D + d];
+  ni->e.pods++;
+  if (t->flags[row] & KS_NPOD_IN_QUOTA)
+    for (int d = 0; d < KS_QUOTA_DIMS; d++) st->used[d] += t->qreq[(size_t)row * KS_QUOTA_DIMS + d];
+}
+
+/* RunFilterPluginsWithNominatedPods (no nominated pods) on the dry run's NodeInfo */
+static int dry_fits(const ko_sched *s, const ko_pod *p, int64_t n, const ko_ninfo *ni) {
+  return (static_filter(s, p, n) | filter_node(s, p, n, &ni->e, NULL)) == 0;
+}
+
+/* util.MoreImportantPod (priority desc, then the earlier start time); equal pairs keep table order */
+static const ko_npods *g_sort_t;
+static int more_important_cmp(const void *a, const void *b) {
+  const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+  const ko_npods *t = g_sort_t;
+  if (t->prio[x] != t->prio[y]) return t->prio[x] > t->prio[y] ? -1 : 1;
+  if (t->start[x] != t->start[y]) return t->start[x] < t->start[y] ? -1 : 1;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+typedef struct {
+  int status;    /* KS_PN_* */
+  int32_t nv;    /* len(victims) */
+  int32_t nviol; /* numViolatingVictim */
+  int32_t *victims;
+} ko_dry;
+
+/* SelectVictimsOnNode (preempt.go:113-217) on a copy of node n's NodeInfo and of the PostFilterState */
+static void select_victims_on_node(const ko_sched *s, const ko_pod *p, int32_t prio, int64_t n, ko_dry *out) {
+  const ko_npods *t = s->npods;
+  const int64_t b = t->beg[n], cnt = t->beg[n + 1] - b;
+  ko_ninfo ni;
+  ni.rows = malloc((size_t)(cnt > 0 ? cnt : 1) * 4);
+  ni.n = (int32_t)cnt;
+  for (int64_t i = 0; i < cnt; i++) ni.rows[i] = t->rows[b + i];
+  node_eff(&s->nd, n, &ni.e);
+  ko_pfstate st; /* PostFilterState.Clone of PreFilter's snapshot: quotaInfo.GetUsed(), getQuotaInfoUsedLimit */
+  st.quota = p->quota;
+  for (int d = 0; d < KS_QUOTA_DIMS; d++) st.used[d] = s->q[p->quota].used[d];
+  const ko_quota *lim = &s->q[p->quota];
+  int32_t *pot = malloc((size_t)(cnt > 0 ? cnt : 1) * 4);
+  int32_t npot = 0;
+  out->nv = 0;
+  out->nviol = 0;
+  out->victims = malloc((size_t)(cnt > 0 ? cnt : 1) * 4);
+  /* remove every lower-priority pod this pod may preempt (canPreempt, preempt.go:283-294), in NodeInfo.Pods order */
+  for (int64_t i = 0; i < cnt; i++) {
+    const int32_t r = t->rows[b + i];
+    if ((t->flags[r] & KS_NPOD_NONPREEMPTIBLE) || !(prio > t->prio[r]) || t->quota[r] != p->quota) continue;
+    pot[npot++] = r;
+    if (dry_remove(t, &ni, &st, r) != 0) { out->status = KS_PN_ERROR; goto done; }
+  }
+  if (npot == 0) { out->status = KS_PN_NO_VICTIMS; goto done; }
+  if (!dry_fits(s, p, n, &ni)) { out->status = KS_PN_FILTER; goto done; }
+  g_sort_t = t;
+  qsort(pot, (size_t)npot, 4, more_important_cmp);
+  /* filterPodsWithPDBViolation: one budget copy per dry run, decremented in the sorted order */
+  int32_t *allowed = malloc((size_t)(t->npdb > 0 ? t->npdb : 1) * 4);
+  for (int32_t i = 0; i < t->npdb; i++) allowed[i] = t->pdb_allowed[i];
+  uint8_t *viol = calloc((size_t)npot, 1);
+  for (int32_t i = 0; i < npot; i++) {
+    const int32_t q = t->pdb[pot[i]];
+    if (q < 0 || q >= t->npdb) continue;
+    allowed[q]--;
+    if (allowed[q] < 0) viol[i] = 1;
+  }
+  free(allowed);
+  out->status = KS_PN_CANDIDATE;
+  /* reprievePod, the PDB-violating victims first, then the others; both in the sorted order */
+  for (int pass = 0; pass < 2 && out->status == KS_PN_CANDIDATE; pass++) {
+    for (int32_t i = 0; i < npot; i++) {
+      if (viol[i] != (pass == 0)) continue;
+      const int32_t r = pot[i];
+      dry_add(t, &ni, &st, r);
+      const int fits = dry_fits(s, p, n, &ni);
+      if (!fits) {
+        if (dry_remove(t, &ni, &st, r) != 0) { out->status = KS_PN_ERROR; break; }
+        out->victims[out->nv++] = r;
+      }
+      int exceed = 0; /* quotav1.LessThanOrEqual(Mask(Add(used, podReq), names(podReq)), usedLimit) */
+      for (int d = 0; d < KS_QUOTA_DIMS; d++)
+        if (((lim->limit_mask >> d) & 1u) && ((p->qmask >> d) & 1u) && st.used[d] + p->qreq[d] > lim->limit[d]) exceed = 1;
+      if (exceed) {
+        if (dry_remove(t, &ni, &st, r) != 0) { out->status = KS_PN_ERROR; break; }
+        out->victims[out->nv++] = r;
+      }
+      if (pass == 0 && !fits) out->nviol++;
+    }
+  }
+  free(viol);
+  /* DryRunPreemption: success with no victim is an error ("expected at least one victim pod on node") */
+  if (out->status == KS_PN_CANDIDATE && out->nv == 0) out->status = KS_PN_ERROR;
+done:
+  free(pot);
+  free(ni.rows);
+}
+
+/* util.GetEarliestPodStartTime: the earliest start among the victims of the highest priority seen (Pods[0] first) */
+static int64_t earliest_start(const ko_npods *t, const ko_dry *d) {
+  int64_t e = t->start[d->victims[0]];
+  int32_t mp = t->prio[d->victims[0]];
+  for (int32_t i = 0; i < d->nv; i++) {
+    const int32_t r = d->victims[i];
+    if (t->prio[r] == mp) {
+      if (t->start[r] < e) e = t->start[r];
+    } else if (t->prio[r] > mp) {
+      mp = t->prio[r];
+      e = t->start[r];
+    }
+  }
+  return e;
+}
+
+/* pickOneNodeForPreemption over the candidates in node-row order (the reference iterates a map) */
+static int64_t pick_one_node(const ko_sched *s, const ko_dry *dry, const int64_t *cand, int64_t nc) {
+  const ko_npods *t = s->npods;
+  int64_t *a = calloc((size_t)nc, 8), *b = calloc((size_t)nc, 8);
+  int64_t na = 0, nb = 0;
+  int64_t minv = INT64_MAX;
+  for (int64_t i = 0; i < nc; i++) { /* minimum number of PDB violations */
+    const int64_t v = dry[cand[i]].nviol;
+    if (v < minv) { minv = v; na = 0; }
+    if (v == minv) a[na++] = cand[i];
+  }
+  int64_t res = a[0];
+  if (na == 1) goto out;
+  minv = INT64_MAX; /* minimum highest victim priority (Pods[0]) */
+  for (int64_t i = 0; i < na; i++) {
+    const int64_t v = t->prio[dry[a[i]].victims[0]];
+    if (v < minv) { minv = v; nb = 0; }
+    if (v == minv) b[nb++] = a[i];
+  }
+  res = b[0];
+  if (nb == 1) goto out;
+  minv = INT64_MAX; /* minimum sum of priorities (each + MaxInt32 + 1) */
+  na = 0;
+  for (int64_t i = 0; i < nb; i++) {
+    int64_t sum = 0;
+    for (int32_t k = 0; k < dry[b[i]].nv; k++) sum += (int64_t)t->prio[dry[b[i]].victims[k]] + 2147483648LL;
+    if (sum < minv) { minv = sum; na = 0; }
+    if (sum == minv) a[na++] = b[i];
+  }
+  res = a[0];
+  if (na == 1) goto out;
+  minv = INT64_MAX; /* minimum number of victims */
+  nb = 0;
+  for (int64_t i = 0; i < na; i++) {
+    const int64_t v = dry[a[i]].nv;
+    if (v < minv) { minv = v; nb = 0; }
+    if (v == minv) b[nb++] = a[i];
+  }
+  res = b[0];
+  if (nb == 1) goto out;
+  { /* the latest earliest start time of the highest-priority victims (strictly later replaces) */
+    int64_t latest = earliest_start(t, &dry[b[0]]);
+    for (int64_t i = 1; i < nb; i++) {
+      const int64_t e = earliest_start(t, &dry[b[i]]);
+      if (e > latest) { latest = e; res = b[i]; }
+    }
+  }
+out:
+  free(a);
+  free(b);
+  return res;
+}
+
+int ko_preempt(ko_sched *s, const ks_pod_cols *pc, int32_t prio, uint32_t pflags, int32_t nominated,
+               const uint8_t *unresolvable, ks_preempt_result *out, int32_t *victims, int32_t cap, uint8_t *node_status) {
+  if (!s->npods || !s->cfg.quota.enable) return -1;
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  if (p.quota < 0 || p.quota >= s->nq) return -1;
+  const ko_npods *t = s->npods;
+  memset(out, 0, sizeof(*out));
+  out->node = -1;
+  for (int64_t n = 0; node_status && n < s->n; n++) node_status[n] = KS_PN_UNRESOLVABLE;
+  /* PodEligibleToPreemptOthers */
+  if (pflags & KS_PREEMPT_NEVER) { out->status = KS_P_NOT_ELIGIBLE; return 0; }
+  if (nominated >= 0 && nominated < s->n && !(unresolvable && unresolvable[nominated])) {
+    for (int64_t i = t->beg[nominated]; i < t->beg[nominated + 1]; i++) {
+      const int32_t r = t->rows[i];
+      if ((t->flags[r] & KS_NPOD_TERMINATING) && t->quota[r] == p.quota && t->prio[r] < prio) {
+        out->status = KS_P_NOT_ELIGIBLE;
+        return 0;
+      }
+    }
+  }
+  /* findCandidates: nodesWherePreemptionMightHelp, then every potential node's dry run (offset 0, all nodes) */
+  ko_dry *dry = calloc((size_t)(s->n > 0 ? s->n : 1), sizeof(ko_dry));
+  int64_t *cand = malloc((size_t)(s->n > 0 ? s->n : 1) * 8);
+  int64_t nc = 0, errs = 0;
+  for (int64_t n = 0; n < s->n; n++) {
+    if (unresolvable && unresolvable[n]) { dry[n].status = KS_PN_UNRESOLVABLE; continue; }
+    out->potential_nodes++;
+    select_victims_on_node(s, &p, prio, n, &dry[n]);
+    if (dry[n].status == KS_PN_CANDIDATE) cand[nc++] = n;
+    if (dry[n].status == KS_PN_ERROR) errs++;
+    if (node_status) node_status[n] = (uint8_t)dry[n].status;
+  }
+  out->candidates = (int32_t)nc;
+  if (nc == 0) {
+    out->status = errs ? KS_P_ERROR : KS_P_NO_CANDIDATE;
+  } else {
+    const int64_t best = nc == 1 ? cand[0] : pick_one_node(s, dry, cand, nc);
+    out->status = KS_P_NOMINATED;
+    out->node = (int32_t)best;
+    out->num_victims = dry[best].nv;
+    out->num_pdb_violations = dry[best].nviol;
+    for (int32_t k = 0; k < dry[best].nv && k < cap; k++) victims[k] = dry[best].victims[k];
+  }
+  for (int64_t n = 0; n < s->n; n++) free(dry[n].victims);
+  free(dry);
+  free(cand);
   return 0;
 }

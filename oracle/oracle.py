@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 from koordinator_amd import abi
-from koordinator_amd.cluster import CpuState, DeviceTable, NumaNodes, NodeState, NodeTable, PodTable, QuotaTable, ReservationTable
+from koordinator_amd.cluster import (CpuState, DeviceTable, NodePodTable, NumaNodes, NodeState, NodeTable, PodTable,
+                                     QuotaTable, ReservationTable)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libkoord_oracle.so")
@@ -56,6 +57,10 @@ def lib():
         L.ko_unreserve.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.POINTER(abi.KsResult), abi.PU64, abi.P64]
         L.ko_read_nodes.argtypes = [C.c_void_p, C.POINTER(abi.KsNodeState)]
         L.ko_read_quota_used.argtypes = [C.c_void_p, abi.P64]
+        L.ko_load_node_pods.argtypes = [C.c_void_p, C.POINTER(abi.KsNodePodCols), C.c_int64, abi.P32, C.c_int32]
+        L.ko_preempt.argtypes = [C.c_void_p, C.POINTER(abi.KsPodCols), C.c_int32, C.c_uint32, C.c_int32,
+                                 C.POINTER(C.c_uint8), C.POINTER(abi.KsPreemptResult), abi.P32, C.c_int32,
+                                 C.POINTER(C.c_uint8)]
         L.ko_least_requested_score.restype = C.c_int64
         L.ko_least_requested_score.argtypes = [C.c_int64, C.c_int64]
         L.ko_most_requested_score.restype = C.c_int64
@@ -288,6 +293,33 @@ class Oracle:
         if self.L.ko_fetch_numa_alloc(self.h, out.ctypes.data_as(abi.P64), p) != 0:
             raise ValueError("no NUMA allocations for that many pods")
         return out[:p]
+
+    def load_node_pods(self, t: NodePodTable):
+        cols = t.ks()
+        if self.L.ko_load_node_pods(self.h, C.byref(cols), t.m, t.pdb_allowed.ctypes.data_as(abi.P32),
+                                    len(t.pdb_allowed)) != 0:
+            raise ValueError("ko_load_node_pods: a row references a node outside the table")
+        self.npods = t.m
+
+    def preempt(self, pod: PodTable, priority: int, flags: int = 0, nominated_node: int = -1, unresolvable=None,
+                node_status: bool = False) -> dict:
+        out = abi.KsPreemptResult()
+        cap = max(getattr(self, "npods", 0), 1)
+        vic = np.zeros(cap, np.int32)
+        ns = np.zeros(max(self.n, 1), np.uint8) if node_status else None
+        ur = None if unresolvable is None else np.ascontiguousarray(unresolvable, np.uint8)
+        cols = pod.ks()
+        if self.L.ko_preempt(self.h, C.byref(cols), int(priority), int(flags), int(nominated_node),
+                             ur.ctypes.data_as(C.POINTER(C.c_uint8)) if ur is not None else None, C.byref(out),
+                             vic.ctypes.data_as(abi.P32), cap,
+                             ns.ctypes.data_as(C.POINTER(C.c_uint8)) if ns is not None else None) != 0:
+            raise ValueError("ko_preempt: no node-pod table, ElasticQuota off or the pod has no quota")
+        r = {"status": out.status, "node": out.node, "victims": vic[: out.num_victims].copy(),
+             "num_pdb_violations": out.num_pdb_violations, "candidates": out.candidates,
+             "potential_nodes": out.potential_nodes}
+        if ns is not None:
+            r["node_status"] = ns[: self.n].copy()
+        return r
 
     def read_quota_used(self) -> np.ndarray:
         used = np.zeros(max(self.nq, 1) * abi.KS_QUOTA_DIMS, np.int64)

@@ -18,5 +18,7 @@ int main(void) {
   O(ks_pod_cols, cpu_bind); O(ks_cpu_topology, numa_node); O(ks_cpu_topology, socket); O(ks_cpu_state_cols, reserved);
   O(ks_node_cols, numa_flags); O(ks_result, gpu_minors);
   P(ks_numa_node_cols); O(ks_numa_node_cols, used_present); O(ks_numa_node_cols, cpuset_cpus);
+  P(ks_node_pod_cols); O(ks_node_pod_cols, req_scalar); O(ks_node_pod_cols, quota_req); P(ks_preempt_result);
+  O(ks_preempt_result, potential_nodes);
   return 0;
 }

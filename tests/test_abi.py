@@ -28,7 +28,8 @@ STRUCTS = {
     "ks_reservation_cols": abi.KsReservationCols, "ks_numa_args": abi.KsNumaArgs,
     "ks_deviceshare_args": abi.KsDeviceShareArgs, "ks_device_cols": abi.KsDeviceCols,
     "ks_cpu_topology": abi.KsCpuTopology, "ks_cpu_state_cols": abi.KsCpuStateCols,
-    "ks_numa_node_cols": abi.KsNumaNodeCols,
+    "ks_numa_node_cols": abi.KsNumaNodeCols, "ks_node_pod_cols": abi.KsNodePodCols,
+    "ks_preempt_result": abi.KsPreemptResult,
 }
 
 

@@ -1,0 +1,107 @@
+"""GPU parity of the ElasticQuota PostFilter (ks_preempt, koordinator_amd/csrc/ks_preempt.h) against the CPU oracle
+(ko_preempt, a literal restatement of preempt.go's SelectVictimsOnNode and upstream's candidate selection, pinned by
+tests/test_preempt.py): status, nominated node, victims in order, PDB violations, candidate and potential-node counts
+and every node's dry-run outcome must be identical."""
+import numpy as np
+import pytest
+
+import test_preempt as hand
+from helpers import profile
+from koordinator_amd import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def runtime():
+    from koordinator_amd import runtime as rt
+
+    rt.lib()
+    return rt
+
+
+KEYS = ("status", "node", "num_pdb_violations", "candidates", "potential_nodes")
+
+
+def compare(runtime, oracle_lib, cfg, nodes, quotas, t, pods, prios, label, **kw):
+    ev = runtime.Evaluator(cfg, nodes.copy(), quotas.copy())
+    orc = oracle_lib.Oracle(cfg, nodes.copy(), quotas.copy())
+    try:
+        ev.load_node_pods(t)
+        orc.load_node_pods(t)
+        outs = []
+        for i in range(pods.n):
+            extra = {k: (v[i] if isinstance(v, list) else v) for k, v in kw.items()}
+            g = ev.preempt(pods.rows([i]), int(prios[i]), node_status=True, **extra)
+            w = orc.preempt(pods.rows([i]), int(prios[i]), node_status=True, **extra)
+            for k in KEYS:
+                assert g[k] == w[k], f"{label} pod {i}: {k} {g[k]} (GPU) vs {w[k]} (oracle)"
+            assert np.array_equal(g["victims"], w["victims"]), f"{label} pod {i}: victims {g['victims']} vs {w['victims']}"
+            assert np.array_equal(g["node_status"], w["node_status"]), f"{label} pod {i}: node statuses differ"
+            outs.append(g)
+        return outs
+    finally:
+        ev.close()
+        orc.close()
+
+
+def test_hand_cases_through_hip(runtime, oracle_lib):
+    cfg = profile(quota=True).to_ks_config()
+    cases = [(hand.BASE, 1500, 1 << 40), (hand.BASE, 500, 1 << 40), (hand.BASE, 500, 2000), (hand.BASE, 1500, 2000),
+             (hand.BASE, 2500, 1 << 40)]
+    for specs, cpu, lim in cases:
+        nodes = hand.cluster(1)
+        t = hand.running(nodes, specs)
+        p = hand.preemptor(cpu)
+        compare(runtime, oracle_lib, cfg, nodes, hand.quotas(t, limit_cpu=lim), t, p, [1000], f"hand {cpu}/{lim}")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_c2_shaped_cluster(runtime, oracle_lib, seed):
+    w = synth.c2_preempt(seed=seed, n_nodes=2000, n_preemptors=24)
+    outs = compare(runtime, oracle_lib, w.cfg, w.nodes, w.quotas, w.node_pods, w.preemptors, w.priority, f"c2p{seed}")
+    st = [o["status"] for o in outs]
+    assert st.count(abi.KS_P_NOMINATED) >= 8, st  # the workload exercises real preemptions
+    assert sum(len(o["victims"]) for o in outs) > 0
+
+
+def test_unresolvable_masks_and_nominated_nodes(runtime, oracle_lib):
+    w = synth.c2_preempt(seed=7, n_nodes=1500, n_preemptors=16)
+    rng = np.random.Generator(np.random.PCG64(7))
+    masks = [(rng.random(w.nodes.n) < f).astype(np.uint8) for f in np.linspace(0.0, 0.97, w.preemptors.n)]
+    nominated = [int(x) for x in rng.integers(-1, w.nodes.n, w.preemptors.n)]
+    compare(runtime, oracle_lib, w.cfg, w.nodes, w.quotas, w.node_pods, w.preemptors, w.priority, "masks",
+            unresolvable=masks, nominated_node=nominated)
+
+
+@pytest.mark.parametrize("per_node,allowed", [((60, 120), 130), ((150, 250), 256)])
+def test_large_nodes(runtime, oracle_lib, per_node, allowed):
+    # 2 and 4 positions per lane of the dry run (nodes with up to 128 / 256 pods)
+    rng = np.random.Generator(np.random.PCG64(per_node[1]))
+    nodes = synth.make_nodes(300, rng)
+    nodes.allowed_pods[:] = allowed
+    t, used = synth.make_node_pods(nodes, rng, 8, per_node=per_node, n_pdb=6, pdb_frac=0.4)
+    nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 3000, nodes.n), 1000)
+    q = synth.QuotaTable(8)
+    q.limit_mask[:] = 0xF
+    q.used[:] = used
+    q.limit[:] = (used * 1.01).astype(np.int64)
+    pods = synth.make_pods(12, rng, 8)
+    prio = rng.choice(np.array([1000, 5000, 9000], np.int32), 12)
+    compare(runtime, oracle_lib, profile(quota=True).to_ks_config(), nodes, q, t, pods, prio, f"large{per_node}")
+
+
+def test_pdb_heavy(runtime, oracle_lib):
+    rng = np.random.Generator(np.random.PCG64(31))
+    nodes = synth.make_nodes(800, rng)
+    t, used = synth.make_node_pods(nodes, rng, 4, per_node=(10, 50), n_pdb=5, pdb_frac=0.8)
+    t.pdb_allowed[:] = [0, 1, 2, 0, 5]
+    nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 2000, nodes.n), 1000)
+    q = synth.QuotaTable(4)
+    q.limit_mask[:] = 0xF
+    q.used[:] = used
+    q.limit[:] = used * 2
+    pods = synth.make_pods(16, rng, 4)
+    prio = np.full(16, 9000, np.int32)
+    outs = compare(runtime, oracle_lib, profile(quota=True).to_ks_config(), nodes, q, t, pods, prio, "pdb")
+    assert any(o["num_pdb_violations"] > 0 for o in outs)
