@@ -361,6 +361,88 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
     return rec, res
 
 
+def run_preempt(args, steps: int, warmup: int, profile: bool, cpu: bool):
+    """The ElasticQuota PostFilter (f4) on C2's cluster with NodeInfo.Pods on every node (synth.c2_preempt: 5k nodes,
+    ~110k running pods, quotas at their limits): one step = the PostFilter of every preemptor in turn (ks_preempt:
+    every node's dry run on the device + the candidate selection; nothing is deleted, so steps repeat exactly)."""
+    from koordinator_amd import runtime
+    from koordinator_amd.cluster import PodTable  # noqa: F401
+
+    w = __import__("koordinator_amd.synth", fromlist=["c2_preempt"]).c2_preempt(n_nodes=5000, n_preemptors=args.preempt_pods)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), w.quotas.copy())
+    pods = [w.preemptors.rows([i]) for i in range(w.preemptors.n)]
+    res = []
+    try:
+        ev.load_node_pods(w.node_pods)
+        ev.set_profile(False)
+        for _ in range(warmup):
+            for i, p in enumerate(pods):
+                ev.preempt(p, int(w.priority[i]))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = [ev.preempt(p, int(w.priority[i])) for i, p in enumerate(pods)]
+        elapsed = time.perf_counter() - t0
+        dry_ms = sel_ms = 0.0
+        algo = 0
+        if profile:
+            ev.set_profile(True)
+            for i, p in enumerate(pods):
+                ev.preempt(p, int(w.priority[i]))
+                st = ev.stats()
+                dry_ms += st["sweep_ms"]
+                sel_ms += st["select_ms"]
+                algo = st["sweep_bytes"]
+            ev.set_profile(False)
+    finally:
+        ev.close()
+    calls = steps * len(pods)
+    rec = {"value": round(calls / elapsed, 1), "unit": "preemptions/s", "ms_per_step": round(elapsed * 1000 / steps, 3),
+           "steps": steps, "warmup": warmup, "preemptors_per_step": len(pods), "nodes": w.nodes.n,
+           "running_pods": w.node_pods.m, "node_dry_runs_per_s": round(calls * w.nodes.n / elapsed, 1),
+           "us_per_preemption": round(elapsed * 1e6 / calls, 2),
+           "nominated_per_step": sum(1 for r in res if r["status"] == 0),
+           "victims_per_step": int(sum(len(r["victims"]) for r in res)),
+           "workload": f"C2-preempt: {w.nodes.n} nodes, {w.node_pods.m} running pods (NodeInfo.Pods), 32 quotas at their "
+                       f"limits, {len(pods)} preemptors; ElasticQuota PostFilter (SelectVictimsOnNode on every node, "
+                       f"pickOneNodeForPreemption) with Fit + LoadAware filters; timed per call (host staging + 2 kernels "
+                       f"+ read-back)",
+           "roofline": None}
+    if profile and dry_ms:
+        avg = dry_ms / len(pods) / 1000.0
+        achieved = algo / avg / 1e9
+        rec["roofline"] = {"bound": "hbm", "kernel": "preempt_dry_run_kernel", "achieved": round(achieved, 2),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                           "avg_launch_us": round(avg * 1e6, 3), "algorithmic_bytes_per_launch": algo,
+                           "select_us": round(sel_ms / len(pods) * 1000, 3),
+                           "traffic": pmc_traffic("preempt", "preempt_dry_run_kernel")[0]}
+    if cpu:
+        from oracle.oracle import Oracle
+
+        model, ncpu = host_cpus()
+        o = Oracle(w.cfg, w.nodes.copy(), w.quotas.copy(), nthreads=16)
+        try:
+            o.load_node_pods(w.node_pods)
+            t0 = time.perf_counter()
+            k = 0
+            want = []
+            while k < len(pods) and (k < 4 or time.perf_counter() - t0 < args.cpu_budget_s):
+                want.append(o.preempt(pods[k], int(w.priority[k])))
+                k += 1
+            dt = time.perf_counter() - t0
+        finally:
+            o.close()
+        keys = ("status", "node", "num_pdb_violations", "candidates", "potential_nodes")
+        parity = all(all(res[i][kk] == want[i][kk] for kk in keys) and np.array_equal(res[i]["victims"], want[i]["victims"])
+                     for i in range(k))
+        rec["cpu_baseline"] = {"value": round(k / dt, 1), "unit": "preemptions/s", "cores": 16, "kind": "port",
+                               "sample": f"first {k} of {len(pods)} preemptors, same cluster; the CPU restatement of "
+                                         f"DryRunPreemption on the Parallelizer (16 workers)",
+                               "host_cpu": model, "host_usable_cpus": ncpu}
+        rec["parity"] = bool(parity)
+        rec["speedup_vs_cpu_baseline"] = round(rec["value"] / rec["cpu_baseline"]["value"], 2)
+    return rec
+
+
 def workload_desc(w):
     return (f"{w.name}: {w.pods.n} pods x {w.nodes.n} nodes, NodeResourcesFit(LeastAllocated cpu/mem/batch-cpu/batch-mem)"
             f" + LoadAwareScheduling(defaults)" + (" + ElasticQuota(32 leaf quotas)" if w.quotas is not None else "")
@@ -395,6 +477,8 @@ def main():
     ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d sub-records")
     ap.add_argument("--sub-steps", type=int, default=3)
     ap.add_argument("--sub-warmup", type=int, default=1)
+    ap.add_argument("--no-preempt", action="store_true", help="skip the preempt (ElasticQuota PostFilter) record")
+    ap.add_argument("--preempt-pods", type=int, default=128)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -488,6 +572,8 @@ def main():
                 rs["speedup_vs_cpu_baseline"] = round(rs["value"] / cbs["value"], 2)
             out[sub] = rs
             del ws, ress
+    if not args.no_sub and not args.no_preempt and world == 1 and args.config == "c2":
+        out["preempt"] = run_preempt(args, args.sub_steps, args.sub_warmup, not args.no_profile, not args.no_cpu_baseline)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -831,7 +831,8 @@ int ks_load_node_pods(ks_ctx *ctx, const ks_node_pod_cols *pods, int64_t m, cons
  * is changed: the caller deletes the victims (prepareCandidate) and refreshes the tables.  Supported with Fit,
  * LoadAware, ElasticQuota (required; the pod needs a quota row), BalancedAllocation, TaintToleration and NodeAffinity;
  * Reservation, NodeNUMAResource, DeviceShare and NodePorts (filters that read other pods of the node) give
- * KS_EUNSUPPORTED. */
+ * KS_EUNSUPPORTED.  ks_get_stats afterwards: sweep_bytes = the dry-run launch's algorithmic bytes and, with
+ * ks_set_profile on, sweep_ms / select_ms / total_ms = the dry-run kernel, the selection kernel, both. */
 #define KS_PREEMPT_NEVER 0x1u /* pod.Spec.PreemptionPolicy == Never */
 int ks_preempt(ks_ctx *ctx, const ks_pod_cols *pod, int32_t priority, uint32_t flags, int32_t nominated_node,
                const uint8_t *unresolvable, ks_preempt_result *out, int32_t *victims, int32_t victims_cap,

@@ -4635,14 +4635,21 @@ int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t f
   a.out = ctx->pre_out;
   a.victims = ctx->pre_victims;
   HIPCHK(ctx, hipMemsetAsync(ctx->pre_vrank, 0xFF, (size_t)ctx->npt.m * 4, ctx->stream));
+  // with ks_set_profile on: the dry-run kernel in stats.sweep_ms, the selection in stats.select_ms
+  const bool prof = ctx->cfg.profile != 0;
+  hipEvent_t e0 = prof ? take_event(ctx, 0) : nullptr, e1 = prof ? take_event(ctx, 1) : nullptr,
+             e2 = prof ? take_event(ctx, 2) : nullptr;
+  if (prof) HIPCHK(ctx, hipEventRecord(e0, ctx->stream));
   if (n > 0) {
     const dim3 grid((unsigned)((n + 3) / 4)), block(256);
     if (ctx->npod_slots == 1) hipLaunchKernelGGL(preempt_dry_run_kernel<1>, grid, block, 0, ctx->stream, a);
     else if (ctx->npod_slots == 2) hipLaunchKernelGGL(preempt_dry_run_kernel<2>, grid, block, 0, ctx->stream, a);
     else hipLaunchKernelGGL(preempt_dry_run_kernel<4>, grid, block, 0, ctx->stream, a);
   }
+  if (prof) HIPCHK(ctx, hipEventRecord(e1, ctx->stream));
   hipLaunchKernelGGL(preempt_select_kernel, dim3(1), dim3(kPreemptSelThreads), 0, ctx->stream, a);
   HIPCHK(ctx, hipGetLastError());
+  if (prof) HIPCHK(ctx, hipEventRecord(e2, ctx->stream));
   PreemptOut o{};
   HIPCHK(ctx, hipMemcpyAsync(&o, ctx->pre_out, sizeof(o), hipMemcpyDeviceToHost, ctx->stream));
   if (node_status && n > 0) HIPCHK(ctx, hipMemcpyAsync(node_status, ctx->pre_status, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
@@ -4652,6 +4659,21 @@ int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t f
     HIPCHK(ctx, hipMemcpyAsync(victims, ctx->pre_victims, (size_t)nv * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   }
+  ctx->stats = ks_stats{};
+  if (prof) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ctx->stats.sweep_ms = ms;
+    ctx->stats.sweep_launches = n > 0 ? 1 : 0;
+    (void)hipEventElapsedTime(&ms, e1, e2);
+    ctx->stats.select_ms = ms;
+    (void)hipEventElapsedTime(&ms, e0, e2);
+    ctx->stats.total_ms = ms;
+  }
+  // algorithmic bytes of the dry-run launch: every node's pod positions (priority, start, flags, quota, PDB, 7 request
+  // and 8 quota-request words: 148 B) and node words (allocatable + requested x 7, pod count, allowed, LoadAware bits;
+  // the taint / label words with the dictionary plugins) once, the per-node outcome written
+  ctx->stats.sweep_bytes = ctx->npt.m * 148 + n * (int64_t)(7 * 16 + 12 + (ctx->kc.stat ? 16 : 0) + sizeof(PreemptCand) + 1);
   out->node = o.node;
   out->status = o.status;
   out->num_victims = o.nvict;

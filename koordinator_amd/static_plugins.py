@@ -213,10 +213,19 @@ def build_dictionaries(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec
     return Dictionaries(list(taints), list(reqs), list(ports))
 
 
+def _lookup(index: Dict, item, what: str) -> int:
+    """The dictionary bit of `item`; an item the prebuilt dictionaries do not hold (the informer path keeps them across
+    cycles) means they must be rebuilt, which the shim handles like every other StaticPluginError (reference path)."""
+    k = index.get(item)
+    if k is None:
+        raise StaticPluginError(f"{what} {item} not in dictionary: rebuild the dictionaries")
+    return k
+
+
 def _mask(reqs: List[Requirement], index: Dict[Requirement, int]) -> int:
     m = 0
     for r in reqs:
-        m |= 1 << index[r]
+        m |= 1 << _lookup(index, r, "node selector requirement")
     return m
 
 
@@ -225,6 +234,13 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
     """Fill node_table.{taints_hard, taints_soft, labels} and pod_table.{tolerated, affinity_*} from the specs."""
     if len(nodes) != node_table.n or len(pods) != pod_table.n:
         raise ValueError("spec / table length mismatch")
+    if dicts is not None:
+        # the pods' requirements are validated here too (build_dictionaries does it for new dictionaries)
+        for p in pods:
+            for rl in ([_term_reqs(p, t) for t in p.required] if p.required is not None else
+                       ([_term_reqs(p, None)] if p.node_selector else [])) + [list(t.requirements) for w, t in p.preferred if w != 0]:
+                for r in rl:
+                    validate_requirement(r)
     d = dicts or build_dictionaries(nodes, pods)
     tindex = {t: i for i, t in enumerate(d.taints)}
     rindex = {r: i for i, r in enumerate(d.requirements)}
@@ -234,7 +250,7 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
     for i, nd in enumerate(nodes):
         h = s = 0
         for t in nd.taints:
-            b = 1 << tindex[t]
+            b = 1 << _lookup(tindex, t, "taint")
             if t.effect == PREFER_NO_SCHEDULE:
                 s |= b
             else:
@@ -254,7 +270,7 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
         for hp in nd.used_ports:
             hp = hp.sanitized()
             if hp.port > 0:
-                m |= 1 << pindex[hp]
+                m |= 1 << _lookup(pindex, hp, "host port")
         used[i] = m
     node_table.host_ports = used
     T = abi.KS_AFFINITY_TERMS
@@ -301,7 +317,7 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
             hp = hp.sanitized()
             if hp.port <= 0:
                 continue
-            w |= 1 << pindex[hp]
+            w |= 1 << _lookup(pindex, hp, "host port")
             for k, q in enumerate(d.ports):
                 if hp.conflicts(q):
                     c |= 1 << k

@@ -2822,10 +2822,9 @@ static int dry_fits(const ko_sched *s, const ko_pod *p, int64_t n, const ko_ninf
 }
 
 /* util.MoreImportantPod (priority desc, then the earlier start time); equal pairs keep table order */
-static const ko_npods *g_sort_t;
-static int more_important_cmp(const void *a, const void *b) {
+static int more_important_cmp(const void *a, const void *b, void *arg) {
   const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
-  const ko_npods *t = g_sort_t;
+  const ko_npods *t = (const ko_npods *)arg;
   if (t->prio[x] != t->prio[y]) return t->prio[x] > t->prio[y] ? -1 : 1;
   if (t->start[x] != t->start[y]) return t->start[x] < t->start[y] ? -1 : 1;
   return x < y ? -1 : (x > y ? 1 : 0);
@@ -2865,8 +2864,7 @@ static void select_victims_on_node(const ko_sched *s, const ko_pod *p, int32_t p
   }
   if (npot == 0) { out->status = KS_PN_NO_VICTIMS; goto done; }
   if (!dry_fits(s, p, n, &ni)) { out->status = KS_PN_FILTER; goto done; }
-  g_sort_t = t;
-  qsort(pot, (size_t)npot, 4, more_important_cmp);
+  qsort_r(pot, (size_t)npot, 4, more_important_cmp, (void *)t);
   /* filterPodsWithPDBViolation: one budget copy per dry run, decremented in the sorted order */
   int32_t *allowed = malloc((size_t)(t->npdb > 0 ? t->npdb : 1) * 4);
   for (int32_t i = 0; i < t->npdb; i++) allowed[i] = t->pdb_allowed[i];
@@ -2977,6 +2975,25 @@ out:
   return res;
 }
 
+typedef struct {
+  const ko_sched *s;
+  const ko_pod *p;
+  int32_t prio;
+  const uint8_t *unresolvable;
+  ko_dry *dry;
+} ko_dry_arg;
+
+static void dry_piece(void *v, int64_t lo, int64_t hi) {
+  const ko_dry_arg *a = (const ko_dry_arg *)v;
+  for (int64_t n = lo; n < hi; n++) {
+    if (a->unresolvable && a->unresolvable[n]) {
+      a->dry[n].status = KS_PN_UNRESOLVABLE;
+      continue;
+    }
+    select_victims_on_node(a->s, a->p, a->prio, n, &a->dry[n]);
+  }
+}
+
 int ko_preempt(ko_sched *s, const ks_pod_cols *pc, int32_t prio, uint32_t pflags, int32_t nominated,
                const uint8_t *unresolvable, ks_preempt_result *out, int32_t *victims, int32_t cap, uint8_t *node_status) {
   if (!s->npods || !s->cfg.quota.enable) return -1;
@@ -2998,14 +3015,16 @@ int ko_preempt(ko_sched *s, const ks_pod_cols *pc, int32_t prio, uint32_t pflags
       }
     }
   }
-  /* findCandidates: nodesWherePreemptionMightHelp, then every potential node's dry run (offset 0, all nodes) */
+  /* findCandidates: nodesWherePreemptionMightHelp, then every potential node's dry run (offset 0, all nodes) on the
+   * Parallelizer (DryRunPreemption -> fh.Parallelizer().Until; every dry run works on its own copies) */
   ko_dry *dry = calloc((size_t)(s->n > 0 ? s->n : 1), sizeof(ko_dry));
   int64_t *cand = malloc((size_t)(s->n > 0 ? s->n : 1) * 8);
   int64_t nc = 0, errs = 0;
+  ko_dry_arg da = {s, &p, prio, unresolvable, dry};
+  pool_until(s->pool, s->n, dry_piece, &da);
   for (int64_t n = 0; n < s->n; n++) {
-    if (unresolvable && unresolvable[n]) { dry[n].status = KS_PN_UNRESOLVABLE; continue; }
+    if (dry[n].status == KS_PN_UNRESOLVABLE) continue;
     out->potential_nodes++;
-    select_victims_on_node(s, &p, prio, n, &dry[n]);
     if (dry[n].status == KS_PN_CANDIDATE) cand[nc++] = n;
     if (dry[n].status == KS_PN_ERROR) errs++;
     if (node_status) node_status[n] = (uint8_t)dry[n].status;

@@ -23,28 +23,92 @@ DefaultNormalizeScore is also the reference's frameworkext/normalize_score.go:24
 """
 from __future__ import annotations
 
+import re
 from typing import List, Sequence, Tuple
 
-from koordinator_amd.static_plugins import (NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, NodeSpec, PodAffinitySpec,
-                                            Requirement, requirement_matches)
+# Only the plain data records (taints, tolerations, requirements, host ports as the host's informer would decode them)
+# come from the product module; every matching rule below is restated here, so a bug in the product's host compiler
+# (koordinator_amd/static_plugins.py: Toleration.tolerates, requirement_matches, HostPort.conflicts) shows up as a
+# parity failure instead of being shared by both sides.
+from koordinator_amd.static_plugins import NodeSpec, PodAffinitySpec, Requirement
+
+NO_SCHEDULE, PREFER_NO_SCHEDULE, NO_EXECUTE = "NoSchedule", "PreferNoSchedule", "NoExecute"
+BIND_ALL = "0.0.0.0"  # framework.DefaultBindAllHostIP
+
+
+def tolerates_taint(tol, taint) -> bool:
+    """k8s.io/api/core/v1 Toleration.ToleratesTaint"""
+    if len(tol.effect) > 0 and tol.effect != taint.effect:
+        return False
+    if len(tol.key) > 0 and tol.key != taint.key:
+        return False
+    op = tol.operator
+    if op == "" or op == "Equal":  # an empty operator means Equal
+        return tol.value == taint.value
+    if op == "Exists":
+        return True
+    return False
+
+
+_GO_INT = re.compile(r"[+-]?[0-9]+")
+
+
+def parse_int64(v: str):
+    """strconv.ParseInt(v, 10, 64): optional sign and decimal digits only, within int64; None on error"""
+    if _GO_INT.fullmatch(v) is None:
+        return None
+    x = int(v)
+    return x if -(1 << 63) <= x <= (1 << 63) - 1 else None
+
+
+def label_requirement_matches(r: Requirement, labels) -> bool:
+    """k8s.io/apimachinery/pkg/labels Requirement.Matches"""
+    has = r.key in labels
+    if r.operator == "In":
+        return has and labels[r.key] in r.values
+    if r.operator == "NotIn":
+        return (not has) or labels[r.key] not in r.values
+    if r.operator == "Exists":
+        return has
+    if r.operator == "DoesNotExist":
+        return not has
+    if r.operator in ("Gt", "Lt"):
+        if not has:
+            return False
+        lv = parse_int64(labels[r.key])
+        if lv is None or len(r.values) != 1:
+            return False
+        rv = parse_int64(r.values[0])
+        if rv is None:
+            return False
+        return (r.operator == "Gt" and lv > rv) or (r.operator == "Lt" and lv < rv)
+    return False
+
+
+def node_requirement_matches(r: Requirement, node: NodeSpec) -> bool:
+    """nodeaffinity's NodeSelectorTerm: matchExpressions against the node's labels, matchFields (metadata.name, In /
+    NotIn) against its fields"""
+    if r.field:
+        return label_requirement_matches(r, {"metadata.name": node.name})
+    return label_requirement_matches(r, node.labels)
 
 
 def taint_filter(pod: PodAffinitySpec, node: NodeSpec) -> bool:
     for t in node.taints:
         if t.effect not in (NO_SCHEDULE, NO_EXECUTE):
             continue
-        if not any(x.tolerates(t) for x in pod.tolerations):
+        if not any(tolerates_taint(x, t) for x in pod.tolerations):
             return False
     return True
 
 
 def taint_raw(pod: PodAffinitySpec, node: NodeSpec) -> int:
     tols = [x for x in pod.tolerations if x.effect in ("", PREFER_NO_SCHEDULE)]
-    return sum(1 for t in node.taints if t.effect == PREFER_NO_SCHEDULE and not any(x.tolerates(t) for x in tols))
+    return sum(1 for t in node.taints if t.effect == PREFER_NO_SCHEDULE and not any(tolerates_taint(x, t) for x in tols))
 
 
 def _term_match(reqs: List[Requirement], node: NodeSpec) -> bool:
-    return bool(reqs) and all(requirement_matches(r, node) for r in reqs)
+    return bool(reqs) and all(node_requirement_matches(r, node) for r in reqs)
 
 
 def affinity_filter(pod: PodAffinitySpec, node: NodeSpec) -> bool:
@@ -70,9 +134,32 @@ def default_normalize(scores: Sequence[int], reverse: bool) -> List[int]:
     return out
 
 
+def host_port_info(used) -> dict:
+    """framework.HostPortInfo built with Add(ip, protocol, port): sanitized (empty IP -> 0.0.0.0, empty protocol ->
+    TCP), ports <= 0 skipped; {ip: {(protocol, port)}}"""
+    h = {}
+    for u in used:
+        if u.port <= 0:
+            continue
+        h.setdefault(u.host_ip or BIND_ALL, set()).add((u.protocol or "TCP", u.port))
+    return h
+
+
+def check_conflict(h: dict, ip: str, protocol: str, port: int) -> bool:
+    """framework.HostPortInfo.CheckConflict"""
+    if port <= 0:
+        return False
+    ip, protocol = ip or BIND_ALL, protocol or "TCP"
+    pp = (protocol, port)
+    if ip == BIND_ALL:
+        return any(pp in m for m in h.values())
+    return any(pp in h.get(k, ()) for k in (BIND_ALL, ip))
+
+
 def ports_filter(pod: PodAffinitySpec, node: NodeSpec) -> bool:
     """upstream plugins/nodeports/node_ports.go fitsPorts: no wanted port conflicts with NodeInfo.UsedPorts"""
-    return not any(w.conflicts(u) for w in pod.host_ports for u in node.used_ports)
+    h = host_port_info(node.used_ports)
+    return not any(check_conflict(h, w.host_ip, w.protocol, w.port) for w in pod.host_ports)
 
 
 def evaluate(pod: PodAffinitySpec, nodes: Sequence[NodeSpec], feasible_other: Sequence[bool]) -> Tuple[

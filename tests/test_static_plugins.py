@@ -180,3 +180,58 @@ def test_schedule_against_restatement():
             nspec[want].used_ports = list(nspec[want].used_ports) + [h.sanitized() for h in p.host_ports if h.port > 0]
         else:
             assert int(got["status"][i]) == abi.KS_S_UNSCHEDULABLE
+
+
+def test_prebuilt_dictionaries_refuse_unknown_items():
+    """The informer path keeps the dictionaries across cycles: a requirement, host port or taint that arrives later is
+    refused with StaticPluginError (the shim falls back to the reference path and rebuilds), never a bare KeyError;
+    the new pods' requirements are validated on that path too."""
+    from koordinator_amd.static_plugins import HostPort, build_dictionaries
+
+    nodes = [NodeSpec("a", {"zone": "z1"}, [Taint("t", "", NO_SCHEDULE)], used_ports=[HostPort(80)])]
+    pods = [PodAffinitySpec(node_selector={"zone": "z1"}, host_ports=[HostPort(80)])]
+    d = build_dictionaries(nodes, pods)
+    compile_cluster(nodes, pods, NodeTable(1), PodTable(1), dicts=d)  # the same items: fine
+    later = [PodAffinitySpec(node_selector={"zone": "z2"})]
+    with pytest.raises(StaticPluginError):
+        compile_cluster(nodes, later, NodeTable(1), PodTable(1), dicts=d)
+    with pytest.raises(StaticPluginError):
+        compile_cluster(nodes, [PodAffinitySpec(host_ports=[HostPort(8080)])], NodeTable(1), PodTable(1), dicts=d)
+    tainted = [NodeSpec("a", {"zone": "z1"}, [Taint("new", "", NO_EXECUTE)])]
+    with pytest.raises(StaticPluginError):
+        compile_cluster(tainted, pods, NodeTable(1), PodTable(1), dicts=d)
+    bad = [PodAffinitySpec(required=[Term([Requirement("zone", "Gt", ("x",))])])]
+    with pytest.raises(StaticPluginError):
+        compile_cluster(nodes, bad, NodeTable(1), PodTable(1), dicts=d)
+
+
+def test_matching_rules_against_independent_restatement():
+    """The host compiler's matching rules (Toleration.tolerates, requirement_matches, HostPort.conflicts) against
+    oracle/static_plugins_ref.py's own restatement of ToleratesTaint, labels.Requirement.Matches and
+    HostPortInfo.CheckConflict on random objects (including Gt / Lt on non-numeric and signed values)."""
+    from koordinator_amd.static_plugins import HostPort
+
+    rng = np.random.Generator(np.random.PCG64(77))
+    vals = ["", "a", "b", "10", "-3", "+7", "007", "1_000", " 5", "x1"]
+    keys = ["k", "zone", "n"]
+    for _ in range(3000):
+        labels = {k: str(rng.choice(vals)) for k in keys if rng.random() < 0.6}
+        node = NodeSpec(str(rng.choice(["n1", "n2"])), labels)
+        op = str(rng.choice(["In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"]))
+        if op in ("Exists", "DoesNotExist"):
+            r = Requirement(str(rng.choice(keys)), op, ())
+        elif op in ("Gt", "Lt"):
+            r = Requirement(str(rng.choice(keys)), op, (str(rng.choice(["5", "-1", "0", "12"])),))
+        elif rng.random() < 0.2:
+            r = Requirement(FIELD_NAME, op, (str(rng.choice(["n1", "n2"])),), field=True)
+        else:
+            r = Requirement(str(rng.choice(keys)), op, tuple(sorted({str(v) for v in rng.choice(vals, 2)})))
+        assert requirement_matches(r, node) == ref.node_requirement_matches(r, node), (r, labels)
+        t = Taint(str(rng.choice(["", "k"])), str(rng.choice(["", "v"])),
+                  str(rng.choice([NO_SCHEDULE, NO_EXECUTE, PREFER_NO_SCHEDULE])))
+        tol = Toleration(str(rng.choice(["", "k", "x"])), str(rng.choice(["", "Equal", "Exists", "Bogus"])),
+                         str(rng.choice(["", "v"])), str(rng.choice(["", NO_SCHEDULE, PREFER_NO_SCHEDULE])))
+        assert tol.tolerates(t) == ref.tolerates_taint(tol, t), (tol, t)
+        a = HostPort(int(rng.choice([0, 80, 81])), str(rng.choice(["", "TCP", "UDP"])), str(rng.choice(["", "0.0.0.0", "10.0.0.1", "10.0.0.2"])))
+        b = HostPort(int(rng.choice([0, 80, 81])), str(rng.choice(["", "TCP", "UDP"])), str(rng.choice(["", "0.0.0.0", "10.0.0.1", "10.0.0.2"])))
+        assert a.conflicts(b) == ref.check_conflict(ref.host_port_info([b]), a.host_ip, a.protocol, a.port), (a, b)
