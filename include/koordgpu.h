@@ -99,6 +99,10 @@ extern "C" {
                                         request; policy and exclusive policy in ks_pod_cols.cpu_bind, KS_CPU_BIND_REQUIRED
                                         when the policy is resourceSpec.requiredCPUBindPolicy */
 #define KS_POD_GPU_CORE 0x40u        /* DeviceShare: the converted GPU request has a gpu-core key (deviceshare/utils.go:96-146) */
+#define KS_POD_UNMODELLED 0x100u     /* set by the shim for a pod with anything the library does not model: FPGA requests,
+                                        DeviceShare allocate hints (VF selectors, RequestsAsCount, exclusive policies), a
+                                        reserve pod as the scheduling subject; every pod entry point refuses it with
+                                        KS_EUNSUPPORTED (the pod keeps the reference path) */
 #define KS_POD_GPU_MEMORY 0x80u      /* DeviceShare: gpu-memory given (ratio derived per node, devicehandler_gpu.go:71-89);
                                         otherwise gpu-memory-ratio given (memory derived) */
 
@@ -116,6 +120,8 @@ extern "C" {
 #define KS_NUMA_CPU_BIND_SHIFT 7     /* bits 7-8: node CPU bind policy, extension.GetNodeCPUBindPolicy (apis/extension/
                                         numa_aware.go:314-325: the node-cpu-bind-policy label, or a static kubelet CPU
                                         manager with full-pcpus-only = FullPCPUsOnly).  Not combined with a NUMA policy. */
+#define KS_NUMA_MAX_REF_COUNT 0x200u /* the node shares CPUs (NodeAllocation maxRefCount > 1, node_allocation.go:133-149):
+                                        refused with KS_EUNSUPPORTED */
 #define KS_NODE_CPU_BIND_NONE 0u
 #define KS_NODE_CPU_BIND_FULL_PCPUS_ONLY 1u
 #define KS_NODE_CPU_BIND_SPREAD_BY_PCPUS 2u
@@ -194,6 +200,8 @@ extern "C" {
 
 /* ---- per-node DeviceShare flags (ks_device_cols.flags) ---- */
 #define KS_DEV_PRESENT 0x1u /* nodeDeviceCache.getNodeDevice != nil (deviceshare/plugin.go:286-289) */
+#define KS_DEV_UNMODELLED 0x2u /* the node has preemptible device capacity (device_cache.go:314) or device-holding
+                                  reservations (deviceshare/reservation.go): ks_load_devices / ks_update_devices refuse it */
 
 /* ---- reservation flags (ks_reservation_cols.flags) ---- */
 #define KS_RSV_UNSCHEDULABLE 0x1u /* ReservationInfo.IsUnschedulable (transformer.go:113)              */

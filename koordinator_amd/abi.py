@@ -16,6 +16,9 @@ KS_MAX_RDMA = 8
 KS_MAX_PCIE = 8
 KS_PCIE_NONE = 0xFF
 KS_JOINT_NONE = 0
+KS_POD_UNMODELLED = 0x100
+KS_DEV_UNMODELLED = 0x2
+KS_NUMA_MAX_REF_COUNT = 0x200
 KS_JOINT_GPU_RDMA = 1
 KS_JOINT_GPU_RDMA_SAME_PCIE = 2
 KS_MAX_CPUS = 256

@@ -921,7 +921,13 @@ struct PodStage {
   DevPodQuota pq{};             // quota request columns (read by the commit kernel)
   std::vector<PodStat> h_stat;  // host staging of stat (kept until the async copy has run: the stream syncs
   std::vector<uint8_t> h_dyn;   // before the next stage_cols)
+  // small batches (ks_eval_pod, ks_assume, ks_preempt, short queues): the column region [cols.cpu, end) packed on the
+  // host in its device layout and sent with one copy instead of ~35 (each a HIP API round trip)
+  void* h_pack = nullptr;       // pinned, kPackPods pods
+  size_t pack_bytes = 0;
+  size_t col8 = 0, col4 = 0;    // device column strides of this stage
 };
+constexpr int32_t kPackPods = 64;
 
 // Test transport for nranks > 1 without RCCL (ks_shard_init_loopback): the ranks are contexts of one process, each
 // driven by its own host thread.  An exchange is two host barriers and device copies: every rank records an event
@@ -1368,6 +1374,8 @@ void ks_destroy(ks_ctx* ctx) {
   dev_free(ctx->st.blob);
   dev_free(ctx->est.blob);
   dev_free(ctx->ast.blob);
+  for (PodStage* ps : {&ctx->st, &ctx->est, &ctx->ast})
+    if (ps->h_pack) (void)hipHostFree(ps->h_pack);
   dev_free(ctx->evbuf);
   dev_free(ctx->ures);
   dev_free(ctx->rdscratch);
@@ -1535,6 +1543,8 @@ static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
     for (int64_t i = 0; c->numa_flags && i < n; ++i)
     {
       const uint32_t f = c->numa_flags[i], label = (f >> KS_NUMA_CPU_BIND_SHIFT) & 3u;
+      if (f & KS_NUMA_MAX_REF_COUNT)
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: CPU sharing with maxRefCount > 1 (node_allocation.go:133-149) is not modelled", (long long)i);
       if (f & (KS_NUMA_CPU_BIND_POLICY | KS_NUMA_TOPOLOGY_POLICY))
         KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: numa_flags 0x%x: encode the CPU bind / NUMA topology policy in its bits", (long long)i, f);
       if (label == 3u || (f >> (KS_NUMA_CPU_BIND_SHIFT + 2)))
@@ -1912,7 +1922,13 @@ static int dev_encode(ks_ctx* ctx, const ks_device_cols* dc, int64_t rows, size_
       total[(size_t)kDevTopoW * np + n] = (int64_t)topo;
       total[(size_t)kDevMetaW * np + n] = (int64_t)meta;
     }
-    for (int64_t n = 0; n < rows; ++n) flags[n] = dc->flags ? dc->flags[n] : 0;
+    for (int64_t n = 0; n < rows; ++n) {
+      flags[n] = dc->flags ? dc->flags[n] : 0;
+      if (flags[n] & KS_DEV_UNMODELLED)
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "node row %lld: preemptible device capacity or device-holding reservations "
+                                      "(device_cache.go:314, deviceshare/reservation.go) are not modelled", (long long)n);
+      if (flags[n] & ~(uint32_t)KS_DEV_PRESENT) KS_FAIL(ctx, KS_EINVAL, "node row %lld: device flags 0x%x", (long long)n, flags[n]);
+    }
   }
   // NUMA nodes of the device topology per node, as dev_hints (ks_numa.h) derives them
   for (int64_t n = 0; n < rows; ++n) ids_out[n] = 0;
@@ -2844,6 +2860,8 @@ static int ensure_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
   b += pst;
   st.results = (ks_result*)b;
   b += res;
+  st.col8 = col8;
+  st.col4 = col4;
   DevPodCols& s = st.cols;
   int64_t** c8[] = {&s.cpu, &s.mem, &s.eph, &s.nzcpu, &s.nzmem, &s.sc[0], &s.sc[1], &s.sc[2], &s.sc[3],
                     &s.la_req_cpu, &s.la_lim_cpu, &s.la_dflt_cpu, &s.la_req_mem, &s.la_lim_mem, &s.la_dflt_mem,
@@ -2874,8 +2892,49 @@ static int ensure_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
 }
 
 // host columns -> the stage's HBM columns (async on the ctx stream)
+// The column region of stage st for p <= kPackPods pods, packed on the host in the device layout (ensure_stage: 27
+// int64 columns, then 7 x 32-bit ones, each st.col8 / st.col4 bytes apart) and copied once.
+static int stage_cols_packed(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t p) {
+  const size_t bytes = st.col8 * 27 + st.col4 * 7;
+  if (!st.h_pack || st.pack_bytes < bytes) {
+    if (st.h_pack) (void)hipHostFree(st.h_pack);
+    st.h_pack = nullptr;
+    st.pack_bytes = 0;
+    HIPCHK(ctx, hipHostMalloc(&st.h_pack, bytes, hipHostMallocDefault));
+    st.pack_bytes = bytes;
+  }
+  // the previous call's copy out of the pinned buffer must be done before it is rewritten
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  unsigned char* h = (unsigned char*)st.h_pack;
+  const int64_t* c8[27] = {pc->req_milli_cpu, pc->req_memory, pc->req_ephemeral, pc->nonzero_milli_cpu, pc->nonzero_memory,
+                           pc->req_scalar[0], pc->req_scalar[1], pc->req_scalar[2], pc->req_scalar[3], pc->la_req_cpu,
+                           pc->la_lim_cpu, pc->la_dflt_cpu, pc->la_req_memory, pc->la_lim_memory, pc->la_dflt_memory,
+                           pc->gpu_core, pc->gpu_memory, pc->gpu_memory_ratio, pc->rdma};
+  for (int d = 0; d < KS_QUOTA_DIMS; ++d) c8[19 + d] = pc->quota_req[d];
+  for (int c = 0; c < 27; ++c) {
+    unsigned char* dst = h + (size_t)c * st.col8;
+    if (c8[c]) memcpy(dst, c8[c], (size_t)p * 8);
+    else memset(dst, 0, (size_t)p * 8);
+  }
+  unsigned char* b4 = h + st.col8 * 27;
+  // flags, quota, quota mask, reservation class, cpu_bind, stat_dyn (u8), joint (u8)
+  const void* c4[5] = {pc->flags, pc->quota, pc->quota_mask, pc->rsv_class, pc->cpu_bind};
+  const int fill4[5] = {0, 0xFF, 0, 0xFF, 0};
+  for (int c = 0; c < 5; ++c) {
+    unsigned char* dst = b4 + (size_t)c * st.col4;
+    if (c4[c]) memcpy(dst, c4[c], (size_t)p * 4);
+    else memset(dst, fill4[c], (size_t)p * 4);
+  }
+  memset(b4 + 5 * st.col4, 0, (size_t)p);  // stat_dyn: stage_cols fills it with the PodStat records
+  if (pc->joint) memcpy(b4 + 6 * st.col4, pc->joint, (size_t)p);
+  else memset(b4 + 6 * st.col4, 0, (size_t)p);
+  HIPCHK(ctx, hipMemcpyAsync(st.cols.cpu, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return KS_OK;
+}
+
 static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t p) {
   DevPodCols& s = st.cols;
+  if (p <= kPackPods && st.col8 && !ctx->kc.stat) return stage_cols_packed(ctx, st, pc, p);
   auto cp8 = [&](int64_t* d, const int64_t* h) -> hipError_t {
     if (h) return hipMemcpyAsync(d, h, (size_t)p * 8, hipMemcpyHostToDevice, ctx->stream);
     return hipMemsetAsync(d, 0, (size_t)p * 8, ctx->stream);
@@ -2953,6 +3012,10 @@ static int prep_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
 }
 
 static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
+  for (int32_t i = 0; pc->flags && i < p; ++i)
+    if (pc->flags[i] & KS_POD_UNMODELLED)
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: requests the library does not model (FPGA, DeviceShare allocate hints, "
+                                    "a reserve pod as the scheduling subject)", i);
   for (int32_t i = 0; pc->affinity_required_n && i < p; ++i)
     if (pc->affinity_required_n[i] < 0 || pc->affinity_required_n[i] > KS_AFFINITY_TERMS)
       KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: %d required node affinity terms (the device evaluates up to %d)", i,
@@ -4634,7 +4697,6 @@ int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t f
   a.status = ctx->pre_status;
   a.out = ctx->pre_out;
   a.victims = ctx->pre_victims;
-  HIPCHK(ctx, hipMemsetAsync(ctx->pre_vrank, 0xFF, (size_t)ctx->npt.m * 4, ctx->stream));
   // with ks_set_profile on: the dry-run kernel in stats.sweep_ms, the selection in stats.select_ms
   const bool prof = ctx->cfg.profile != 0;
   hipEvent_t e0 = prof ? take_event(ctx, 0) : nullptr, e1 = prof ? take_event(ctx, 1) : nullptr,
@@ -4650,15 +4712,22 @@ int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t f
   hipLaunchKernelGGL(preempt_select_kernel, dim3(1), dim3(kPreemptSelThreads), 0, ctx->stream, a);
   HIPCHK(ctx, hipGetLastError());
   if (prof) HIPCHK(ctx, hipEventRecord(e2, ctx->stream));
-  PreemptOut o{};
-  HIPCHK(ctx, hipMemcpyAsync(&o, ctx->pre_out, sizeof(o), hipMemcpyDeviceToHost, ctx->stream));
+  // the result and the victims (adjacent in the blob) in one read-back
+  struct {
+    PreemptOut o;
+    unsigned char pad[16 - sizeof(PreemptOut) % 16];
+    int32_t v[kPreemptMaxPods];
+  } rb;
+  static_assert(sizeof(PreemptOut) % 16 != 0, "PreemptOut padding");
+  const size_t rbytes = (size_t)((const unsigned char*)ctx->pre_victims - (const unsigned char*)ctx->pre_out) +
+                        (size_t)kPreemptMaxPods * 4;
+  if (rbytes != sizeof(rb)) KS_FAIL(ctx, KS_EHIP, "ks_preempt: read-back layout");
+  HIPCHK(ctx, hipMemcpyAsync(&rb, ctx->pre_out, rbytes, hipMemcpyDeviceToHost, ctx->stream));
   if (node_status && n > 0) HIPCHK(ctx, hipMemcpyAsync(node_status, ctx->pre_status, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const PreemptOut o = rb.o;
   const int32_t nv = std::min(o.nvict, victims_cap);
-  if (nv > 0) {
-    HIPCHK(ctx, hipMemcpyAsync(victims, ctx->pre_victims, (size_t)nv * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-  }
+  if (nv > 0) memcpy(victims, rb.v, (size_t)nv * 4);
   ctx->stats = ks_stats{};
   if (prof) {
     float ms = 0;

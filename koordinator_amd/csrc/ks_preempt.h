@@ -78,7 +78,7 @@ struct PreemptArgs {
   const uint8_t* unresolvable;  // [n] or null
   int64_t n;
   PreemptCand* cand;  // [n]
-  int32_t* vrank;     // [m]: the position's index in its node's victims, -1 (memset by the host)
+  int32_t* vrank;     // [m]: the position's index in its node's victims, -1 (written by the dry run)
   uint8_t* status;    // [n] KS_PN_*
   PreemptOut* out;
   int32_t* victims;   // [kPreemptMaxPods]: the chosen node's victims as caller rows
@@ -108,13 +108,14 @@ __global__ __launch_bounds__(256) void preempt_dry_run_kernel(PreemptArgs a) {
       a.status[n] = (uint8_t)out.status;
     }
   };
+  const int64_t b = a.t.beg[n], cnt = a.t.beg[n + 1] - b;
+  for (int64_t i = lane; i < cnt; i += 64) a.vrank[b + i] = -1;  // (the victims' ranks are written after these)
   if (a.unresolvable && a.unresolvable[n]) {  // nodesWherePreemptionMightHelp
     finish();
     return;
   }
   const PodRec p = load_pod_uniform(a.pod);
   const int32_t Q = p.quota;
-  const int64_t b = a.t.beg[n], cnt = a.t.beg[n + 1] - b;
   // ---- the node's pods, canPreempt (preempt.go:283-294) ----
   bool canp[S], inq[S];
   int32_t pdbv[S], prv[S];

@@ -452,7 +452,7 @@ class Evaluator:
         vic = np.zeros(cap, np.int32)
         ns = np.zeros(max(self.n, 1), np.uint8) if node_status else None
         ur = None if unresolvable is None else np.ascontiguousarray(unresolvable, np.uint8)
-        cols = pod.ks()
+        cols = pod if isinstance(pod, abi.KsPodCols) else pod.ks()  # (a prebuilt pointer struct: no per-call rebuild)
         self._chk(self.L.ks_preempt(self.h, C.byref(cols), int(priority), int(flags), int(nominated_node),
                                     ur.ctypes.data_as(C.POINTER(C.c_uint8)) if ur is not None else None, C.byref(out),
                                     vic.ctypes.data_as(abi.P32), cap,

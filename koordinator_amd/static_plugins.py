@@ -307,6 +307,9 @@ def compile_cluster(nodes: Sequence[NodeSpec], pods: Sequence[PodAffinitySpec], 
         for k, (w, t) in enumerate(prefs):
             if not 1 <= w <= 100:
                 raise StaticPluginError(f"pod {i}: preferred weight {w} outside [1, 100]")
+            # upstream component-helpers nodeaffinity.NewPreferredSchedulingTerms (k8s v1.24.15, not on disk) skips a term
+            # with weight 0 or an empty preference (isEmptyNodeSelectorTerm: no matchExpressions and no matchFields);
+            # an empty term compiled to KS_LABEL_NEVER never matches, so it adds 0 like a skipped one
             pref[k, i] = _mask(list(t.requirements), rindex) if t.requirements else never
             wt[k, i] = w
     want = np.zeros(len(pods), np.uint64)

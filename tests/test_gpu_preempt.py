@@ -94,8 +94,10 @@ def test_large_nodes(runtime, oracle_lib, per_node, allowed):
 def test_pdb_heavy(runtime, oracle_lib):
     rng = np.random.Generator(np.random.PCG64(31))
     nodes = synth.make_nodes(800, rng)
-    t, used = synth.make_node_pods(nodes, rng, 4, per_node=(10, 50), n_pdb=5, pdb_frac=0.8)
-    t.pdb_allowed[:] = [0, 1, 2, 0, 5]
+    # every running pod in an exhausted budget: every victim violates (the budgets shared by several victims of a
+    # node, decremented in the sorted order, are covered by test_large_nodes)
+    t, used = synth.make_node_pods(nodes, rng, 4, per_node=(10, 50), n_pdb=5, pdb_frac=1.0)
+    t.pdb_allowed[:] = 0
     nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 2000, nodes.n), 1000)
     q = synth.QuotaTable(4)
     q.limit_mask[:] = 0xF
