@@ -1201,6 +1201,10 @@ static Cfg make_cfg(const ks_config& c, int nsc) {
   k.rsv_F = (int32_t)(100 * ((c.fit.enable_score ? c.fit.plugin_weight : 0) +
                              (c.loadaware.enable_score ? c.loadaware.plugin_weight : 0) + k.numa_pw + k.dev_pw +
                              k.bal_pw + k.taint_pw + k.aff_pw) + 1);
+  // a pod that matches no reservation sees every node through the base restore only (ks_rsv.h): a commit there lowers
+  // the node's key unless it lowers the restored Requested (a reservation whose remainder shrank to zero), which the
+  // commit kernel detects per pass
+  k.monotone_rsv = (k.rsv && !k.dev && !k.stat && !k.numa && !k.bal) ? k.monotone_nd : 0;
   // a commit into a reservation can raise that node's Reservation score for later pods
   if (k.rsv) k.monotone = 0;
   if (k.rsv) k.monotone_nd = 0;

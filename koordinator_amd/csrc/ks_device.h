@@ -79,6 +79,9 @@ struct Cfg {
   int32_t aff, aff_pw;      // upstream NodeAffinity: bit 0 Filter, bit 1 Score; plugin weight
   int32_t ports;            // upstream NodePorts Filter (bit 0)
   int32_t stat;             // taint | aff | ports: the dictionary-bit plugins are on (kernel variant FEAT & 4, PodStat)
+  // Reservation with an otherwise monotone plugin set: monotone for the pods that match no reservation (class -1)
+  // while no commit of the pass lowered a node's restored Requested (ks_pass.h commit_kernel)
+  int32_t monotone_rsv;
 };
 
 // Device node columns (SoA, length npad = nchunks*64, zero padded).

@@ -794,7 +794,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     }
   }
   // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
-  int32_t my_cnt = 0, my_quota = -1;
+  int32_t my_cnt = 0, my_quota = -1, my_cls = -1;
   uint32_t my_flags = 0, my_pmask = 0;
   uint64_t my_bound = 0, my_top = 0, my_second = 0;
   if (tid < 64 && lane < np) {
@@ -806,6 +806,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     my_pmask = a.pq.mask[cursor0 + lane];
     my_quota = a.pods[cursor0 + lane].quota;
     my_flags = a.pods[cursor0 + lane].flags;
+    if (RSV) my_cls = a.pods[cursor0 + lane].rsv_class;
   }
   // lane f < RF_N: the column of row field f
   const void* my_col = nullptr;
@@ -942,10 +943,15 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   };
   uint32_t st_next = 0;
   Cands cn{};
+  // Reservation: set once a commit of this pass lowered a node's restored Requested (the class -1 fast path is off then)
+  bool rsv_raised = false;
   auto lookahead = [&](int32_t j) {
     // the fast path also holds for a pod without device requests when only DeviceShare's normalization
-    // max made the profile non-monotone (its DeviceShare score is 0 on every node)
-    const bool mono = monotone || (cfg.monotone_nd && !(__builtin_amdgcn_readlane(my_flags, j) & kPodNormDyn));
+    // max made the profile non-monotone (its DeviceShare score is 0 on every node), and, with Reservation, for a pod
+    // that matches no reservation: it sees every node through the base restore, whose Requested a commit only raises
+    // (NodeInfo.AddPod) unless the commit shrank a reservation's remainder by more than the pod adds -- rsv_raised
+    const bool mono = monotone || (cfg.monotone_nd && !(__builtin_amdgcn_readlane(my_flags, j) & kPodNormDyn)) ||
+                      (RSV && cfg.monotone_rsv && !rsv_raised && __builtin_amdgcn_readlane(my_cls, j) < 0);
     const uint64_t top = mono ? readlane64(my_top, j) : 0ull;
     const int32_t tn = top ? (int32_t)gkey_node(top) : 0;
     if (QC) {
@@ -1375,13 +1381,16 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         nom_row = a.rv->rowid[gi];
       }
       const bool take = !t_prod_only || (pflags & KS_POD_PROD);
+      int64_t v = 0;
       if (lane < ST_N) {
-        const int64_t v = (take ? podw[t_pw] : 0) + dd;
+        v = (take ? podw[t_pw] : 0) + dd;
         const double v100 = (take ? __longlong_as_double(podw[t_pw100]) : 0.0) + (double)dd * 100.0;
         if (take || dd != 0) term_take(row->t[lane], v, v100);
       } else if (lane == kLaneCounts) {
         row->pod_count += 1;
       }
+      // a restored Requested went down: this node's key may rise for the pods of class -1 (no fast path for them)
+      if (__ballot(lane < ST_N && v < 0)) rsv_raised = true;
     }
     int64_t score_out = score;
     if (RSV && cfg.rsv) {

@@ -224,3 +224,34 @@ def test_c4_sample_matches_oracle(runtime, oracle_lib):
     w = synth.c4(n_pods=5000)
     got, st = check(runtime, oracle_lib, w.profile, w.nodes, w.reservations, w.pods, "c4")
     print("c4 sample stats", {k: st[k] for k in ("passes", "cut_passes", "rescans", "total_ms")})
+
+
+def test_unmatched_pods_fast_path_and_raised_nodes(runtime, oracle_lib):
+    """Pods of class -1 (no reservation matches them) take the monotone fast path in the Reservation kernels; a commit
+    that lowers a node's restored Requested turns it off for the rest of the pass.  Here it happens on purpose: cpu-only
+    reservations with one assigned pod and 500m left, filled by 500m / 1 MiB pods of their class -- the remainder's
+    default non-zero memory (200 MiB) leaves the restore while the pod adds 1 MiB, so the node's NonZeroRequested memory
+    drops and its Fit score rises for the class -1 pods after it."""
+    rng = np.random.Generator(np.random.PCG64(404))
+    n, r, p = 400, 600, 900
+    nodes = synth.make_nodes(n, rng)
+    rs = ReservationTable(r)
+    rs.node[:] = rng.integers(0, n, r)
+    rs.owner_classes[:] = np.uint64(1) << rng.integers(0, 4, r).astype(np.uint64)
+    rs.key_mask[:] = 0b1
+    rs.allocatable[0] = 1000
+    rs.allocated[0] = 500
+    rs.assigned[:] = 1
+    nodes.req_milli_cpu[:] += np.bincount(rs.node, weights=np.full(r, 1500.0), minlength=n).astype(np.int64)
+    nodes.nonzero_milli_cpu[:] += np.bincount(rs.node, weights=np.full(r, 1500.0), minlength=n).astype(np.int64)
+    nodes.nonzero_memory[:] += np.bincount(rs.node, weights=np.full(r, float(2 * synth.DEFAULT_MEMORY_NZ)), minlength=n).astype(np.int64)
+    nodes.pod_count[:] += np.bincount(rs.node, weights=np.full(r, 2.0), minlength=n).astype(np.int32)
+    pods = synth.make_pods(p, rng)
+    matched = rng.random(p) < 0.4
+    pods.rsv_class[:] = np.where(matched, rng.integers(0, 4, p), -1)
+    pods.req_milli_cpu[matched] = 500
+    pods.nonzero_milli_cpu[matched] = 500
+    pods.req_memory[matched] = synth.MI
+    pods.nonzero_memory[matched] = synth.MI
+    got, st = check(runtime, oracle_lib, prof(), nodes, rs, pods, "class -1 fast path")
+    assert st["diag"][7] > 0, "no class -1 pod took the fast path"
