@@ -261,7 +261,7 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         elapsed = time.perf_counter() - t0
         st_last = ev.stats()
         agg = {"sweep_ms": 0.0, "select_ms": 0.0, "commit_ms": 0.0, "fixup_ms": 0.0, "sweep_launches": 0, "passes": 0,
-               "cut_passes": 0, "rescans": 0, "bubble_passes": 0}
+               "cut_passes": 0, "rescans": 0, "bubble_passes": 0, "pre_reserves": 0}
         prof_elapsed = 0.0
         sweep_bytes = 0
         if profile:
@@ -277,7 +277,7 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
                 sweep_bytes = st["sweep_bytes"]
             ev.set_profile(False)
         else:
-            for k in ("passes", "cut_passes", "rescans", "bubble_passes"):
+            for k in ("passes", "cut_passes", "rescans", "bubble_passes", "pre_reserves"):
                 agg[k] = st_last[k] * steps
         if dist is not None:
             import torch
@@ -317,6 +317,8 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         # commits, so the kernel times below overlap and add up to more than ms_per_step
         "pipelined": int(st_last["pipelined"]),  # 0 off, 1 re-swept, 2 patched lists
         "bubble_passes_per_step": agg["bubble_passes"] / steps,
+        # NUMA / device Reserves computed ahead of the commit (reserve_pre_kernel)
+        "pre_reserves_per_step": agg["pre_reserves"] / steps,
         "kernel_ms_per_step": {"sweep": round(agg["sweep_ms"] / steps, 3), "select": round(agg["select_ms"] / steps, 3),
                                "commit": round(agg["commit_ms"] / steps, 3),
                                "dirty_resweep": round(agg["fixup_ms"] / steps, 3)},

@@ -599,6 +599,8 @@ typedef struct ks_stats {
   double fixup_ms;         /* summed HIP-event time of the pipelined dirty-chunk re-sweeps */
   int64_t pipelined;       /* 1 = the last call overlapped each pass's sweep with the previous commit; 2 = its
                               select too, the lists patched after the commit (monotone plugin sets) */
+  int64_t pre_reserves;    /* Reserves whose NodeNUMAResource / DeviceShare allocation was computed ahead of the commit
+                              (the pod's node ranked in its snapshot top) */
 } ks_stats;
 
 /* ---- preemption: the ElasticQuota PostFilter ----

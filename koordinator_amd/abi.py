@@ -426,6 +426,7 @@ class KsStats(C.Structure):
         ("bubble_passes", C.c_int64),
         ("fixup_ms", C.c_double),
         ("pipelined", C.c_int64),
+        ("pre_reserves", C.c_int64),
     ]
 
 

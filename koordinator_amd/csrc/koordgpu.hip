@@ -983,6 +983,7 @@ struct ks_ctx {
   uint64_t* cand_bound = nullptr;
   uint64_t* cand_top = nullptr;
   uint64_t* cand_second = nullptr;
+  PreRsv* pre_rsv = nullptr;       // [kMaxBatch][kPreRsvM] reserve_pre_kernel's records (NUMA / device variants)
   int32_t* cand_total = nullptr;
   // node sharding: shard s = rank * vshards + v owns chunks [s*nchunks/S, (s+1)*nchunks/S)
   int32_t nranks = 1, rank = 0, vshards = 1;
@@ -1339,6 +1340,8 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->cand_top = (uint64_t*)p;
   if (dev_alloc(ctx, &p, 2 * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->cand_second = (uint64_t*)p;
+  if (dev_alloc(ctx, &p, (size_t)kMaxBatch * kPreRsvM * sizeof(PreRsv)) != KS_OK) goto fail;
+  ctx->pre_rsv = (PreRsv*)p;
   if (dev_alloc(ctx, &p, 2 * kMaxBatch * 4) != KS_OK) goto fail;
   ctx->cand_total = (int32_t*)p;
   if (dev_alloc(ctx, &p, 2 * kMaxBatch * 4) != KS_OK) goto fail;
@@ -3276,6 +3279,7 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.pipe_follow = nullptr;
   ca.pipe_after = nullptr;
   ca.top_reset = nullptr;
+  ca.pre_rsv = nullptr;
   *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
                         ctx->q.q, kernel_feat(ctx) == 0).total;
   return ca;
@@ -3294,6 +3298,13 @@ static bool mono_commit(const ks_ctx* ctx, bool qcache, size_t* smem) {
   if (mode == 0 && ctx->kc.quota_enable) return false;
   *smem = mono_layout(ctx->k, ctx->nchunks, qcache, ctx->q.q).total;
   return *smem <= 160 * 1024;
+}
+
+// Reserve's NodeNUMAResource / DeviceShare allocations ahead of the commit (reserve_pre_kernel): on for
+// the variants that have them when the profile enables either plugin; KS_PRE_RSV=0 turns it off (A/B).
+static bool pre_reserve(const ks_ctx* ctx) {
+  static const int64_t env_pre = env_i64("KS_PRE_RSV", 1, 0, 1);
+  return env_pre != 0 && (ctx->kc.numa_pol || ctx->kc.dev);
 }
 
 // the commit kernel's LDS size for this context: checked against the CU's 160 KB and set on the variant
@@ -3727,7 +3738,9 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   }
   size_t msmem = 0;
   const bool mono = mono_commit(ctx, qcache, &msmem);
+  if (!mono && !pipe && pl.reserve_pre && pre_reserve(ctx)) ca.pre_rsv = ctx->pre_rsv;
   rec(2, cs);
+  if (ca.pre_rsv) HIPCHK(ctx, pl.reserve_pre(ctx->batch, cs, ca));  // (timed with the commit)
   if (mono) HIPCHK(ctx, pl.commit_mono(qcache, msmem, cs, ca));
   else HIPCHK(ctx, pl.commit(qcache, smem, cs, ca));
   rec(2, cs);
@@ -3879,6 +3892,7 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   ctx->stats.rescans = (int64_t)cnt[2];
   ctx->stats.slot_misses = (int64_t)cnt[3];
   ctx->stats.bubble_passes = (int64_t)cnt[4];
+  ctx->stats.pre_reserves = (int64_t)cnt[5];
   ctx->stats.pipelined = pipe ? (pipe->patch ? 2 : 1) : 0;
   for (int i = 0; i < 8; ++i) ctx->stats.diag[i] = (int64_t)cnt[8 + i];
   for (size_t i = 0; i + 1 < evs.size(); i += 2) {

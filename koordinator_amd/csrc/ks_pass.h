@@ -356,7 +356,25 @@ struct CommitArgs {
   int32_t* pipe_after;
   // patched passes: cand_top is the list re-evaluation's atomic max, which the commit zeroes after reading
   unsigned long long* top_reset;
+  // NodeNUMAResource / DeviceShare variants: Reserve's allocations on each pod's snapshot-best nodes, computed before
+  // the commit by reserve_pre_kernel ([64][kPreRsvM]); NULL = the commit computes every Reserve itself
+  const struct PreRsv* pre_rsv;
 };
+
+// One pod's NodeNUMAResource + DeviceShare Reserve on one node of its snapshot ranking, computed on the snapshot state
+// (what the commit's Reserve computes on the slot state of a node no earlier pod of the pass touched).
+constexpr int kPreRsvM = 16;  // ranks per pod (C3: the winner is within the snapshot top-16 for 97.7% of pods)
+struct __attribute__((aligned(16))) PreRsv {
+  int32_t node;     // -1 = none
+  uint32_t flags;   // bit 0: the node has a NUMA policy (npr valid), bit 1: npr.admitted
+  uint32_t reasons, affinity;
+  int64_t alloc[2][kNumaDev];
+  int32_t cpus[kNumaDev];
+  uint32_t gminors, rminors;
+  int32_t _pad[2];
+  int64_t g_core, g_mem, g_ratio, g_rdma;  // GpuReq per instance
+};
+static_assert(sizeof(PreRsv) == 144, "PreRsv layout");
 
 // The first pod of the pass after next: pass k+1 commits iff it was swept for the pods at the cursor this commit
 // leaves (rc), and then the pass after it starts behind its pods; otherwise pass k+1 is a bubble and k+2 starts at rc.
@@ -925,7 +943,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   int32_t snode = -1;  // lane s: node of slot s
   int32_t nslots = 0;
   int32_t processed = np;
-  uint32_t rescans = 0, misses = 0, fast = 0;
+  uint32_t rescans = 0, misses = 0, fast = 0, prehits = 0;
   // speculative raw row of the next pod's best untouched candidate (lane f = field f)
   int64_t spec_val = 0;
   int32_t spec_node = -1;
@@ -1158,8 +1176,10 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     // node's reservations the row is built / kept without the pod, nominated on, then taken.
     const int32_t pcls = (RSV && cfg.rsv) ? __builtin_amdgcn_readfirstlane(spods[j].rsv_class) : -1;
     bool rsvc = false;
+    bool fresh = false;  // the slot is created by this pod: its state is the snapshot's
     if (s < 0) {
       if (!cj.fast) KS_CAT(2);
+      fresh = true;
       s = nslots++;
       row = &rows[s];
       const int64_t* src = raw;
@@ -1406,7 +1426,36 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     npr.admitted = false;
     npr.affinity = 0;
     bool npol = false;
-    if ((FEAT & 8) && cfg.numa_pol && !(pflags & kPodReqZero)) {
+    const bool want_npol = (FEAT & 8) && cfg.numa_pol && !(pflags & kPodReqZero);
+    const bool want_dev = DEV && cfg.dev && (pflags & kPodHasGpu);
+    // a slot created by this pod holds the snapshot state: reserve_pre_kernel's allocation for the node, if it ranked
+    const PreRsv* pre = nullptr;
+    if ((FEAT & 12) && a.pre_rsv && fresh && (want_npol || want_dev)) {
+      const int32_t pn = lane < kPreRsvM ? a.pre_rsv[j * kPreRsvM + lane].node : -1;
+      const uint64_t hit = __ballot(pn == node);
+      if (hit) pre = a.pre_rsv + j * kPreRsvM + (__ffsll((long long)hit) - 1);
+    }
+    GpuReq g;
+    if (pre) {
+      const uint32_t pf = pre->flags;
+      npol = (pf & 1u) != 0;
+      npr.admitted = (pf & 2u) != 0;
+      npr.reasons = pre->reasons;
+      npr.affinity = pre->affinity;
+#pragma unroll
+      for (int k = 0; k < kNumaDev; ++k) {
+        npr.alloc[0][k] = pre->alloc[0][k];
+        npr.alloc[1][k] = pre->alloc[1][k];
+        npr.cpus[k] = pre->cpus[k];
+      }
+      gminors = pre->gminors;
+      rminors = pre->rminors;
+      g.core = pre->g_core;
+      g.mem = pre->g_mem;
+      g.ratio = pre->g_ratio;
+      g.rdma = pre->g_rdma;
+      ++prehits;
+    } else if (want_npol) {
       const NumaLView nl{snp + s * kNumaSlotWords};
       if (nl.policy() != 0) {
         PodRec pod = spods[j];
@@ -1427,14 +1476,15 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       }
     }
     const uint32_t dev_allow = (npol && npr.admitted && npr.affinity) ? npr.affinity : ~0u;
-    if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
+    if (want_dev) {
       // DeviceShare Reserve: allocate the minors on the pre-pod GPU state, add the request per instance
-      PodRec pod = spods[j];
-      pod.flags = pflags;
-      GpuReq g;
-      const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g, dev_allow);
-      gminors = __builtin_amdgcn_readfirstlane(dd.minors);
-      rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
+      if (!pre) {
+        PodRec pod = spods[j];
+        pod.flags = pflags;
+        const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g, dev_allow);
+        gminors = __builtin_amdgcn_readfirstlane(dd.minors);
+        rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
+      }
       // used word `lane`: GPU (q, k) for lane < 3 * kGpus, RDMA j = lane - kDevRdmaW after
       const bool is_gpu = lane < kDevRdmaW;
       const int k = is_gpu ? lane % kGpus : lane - kDevRdmaW;
@@ -1614,6 +1664,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     atomicAdd(&a.counters[2], (unsigned long long)rescans);
     atomicAdd(&a.counters[3], (unsigned long long)misses);
     atomicAdd(&a.counters[15], (unsigned long long)fast);  // ks_stats.diag[7]: monotone fast picks
+    if (FEAT & 12) atomicAdd(&a.counters[5], (unsigned long long)prehits);
 #if defined(KS_COMMIT_STAMPS) || defined(KS_COMMIT_CAT)
     for (int i = 0; i < 7; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
 #endif
@@ -1623,6 +1674,109 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 }
 
 // ---- host launch wrappers (one set per (FEAT, NSC) translation unit of ks_variant.hip) ----
+// Reserve ahead of the commit (NodeNUMAResource / DeviceShare variants): one workgroup per pod of the pass ranks the
+// pod's candidate-list keys (each listed chunk's best and runner-up, the snapshot-best nodes of SelectArgs) and computes,
+// for the kPreRsvM highest, what the commit's Reserve computes for a node no earlier pod of the pass touched --
+// numa_policy_eval<ALLOC> (NodeNUMAResource Reserve -> Allocate with the Filter's hint) and dev_eval<ALLOC>
+// (DeviceShare Reserve) -- on the snapshot state, all ranks in parallel.  It runs on the commit's stream right before
+// the commit, so the state it reads is the state the commit loads into a new slot; the commit takes the record when
+// the pod lands on one of these nodes as a new slot and computes the Reserve itself otherwise.
+template <int FEAT>
+__global__ __launch_bounds__(64) void reserve_pre_kernel(CommitArgs a) {
+  constexpr bool DEV = (FEAT & 4) != 0;
+  __shared__ int32_t sel[kPreRsvM];
+  const int lane = threadIdx.x;
+  const int32_t j = blockIdx.x;
+  const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
+  if (cursor0 >= a.total_pods) return;
+  const int32_t np = min(a.batch, a.total_pods - cursor0);
+  if (j >= np) return;
+  const Cfg& cfg = a.c;
+  const int32_t K = a.k, cnt = min(a.cand_count[j], K);
+  // lane i: list entry i (K <= kMaxCand = 64)
+  uint64_t kb = 0, kr = 0;
+  if (lane < cnt) {
+    const uint32_t ch = a.cand_chunk[j * K + lane];
+    const uint2 t = a.cand_t[j * K + lane];
+    kb = local_gkey(t.x, ch);
+    kr = local_gkey(t.y, ch);
+  }
+  int32_t rb = 0, rr = 0;  // ranks: keys are distinct (the node is in the low word)
+  for (int l = 0; l < 64; ++l) {
+    const uint64_t ob = readlane64(kb, l), orr = readlane64(kr, l);
+    rb += (ob > kb) + (orr > kb);
+    rr += (ob > kr) + (orr > kr);
+  }
+  if (lane < kPreRsvM) sel[lane] = -1;
+  __syncthreads();
+  if (kb && rb < kPreRsvM) sel[rb] = (int32_t)gkey_node(kb);
+  if (kr && rr < kPreRsvM) sel[rr] = (int32_t)gkey_node(kr);
+  __syncthreads();
+  if (lane >= kPreRsvM) return;
+  PreRsv o;
+  o.node = sel[lane];
+  o.flags = 0;
+  o.reasons = 0;
+  o.affinity = 0;
+#pragma unroll
+  for (int k = 0; k < kNumaDev; ++k) {
+    o.alloc[0][k] = o.alloc[1][k] = 0;
+    o.cpus[k] = 0;
+  }
+  o.gminors = o.rminors = 0;
+  o._pad[0] = o._pad[1] = 0;
+  o.g_core = o.g_mem = o.g_ratio = o.g_rdma = 0;
+  if (o.node >= 0) {
+    const int64_t node = o.node;
+    const PodRec pod = a.pods[cursor0 + j];
+    const uint32_t pflags = pod.flags;
+    NumaPolOut npr;
+    npr.admitted = false;
+    npr.affinity = 0;
+    npr.reasons = 0;
+    bool npol = false;
+    const DevGView dvg{*a.dv, node};
+    if ((FEAT & 8) && cfg.numa_pol && !(pflags & kPodReqZero)) {
+      const NumaGView nv{*a.nv, node};
+      if (nv.policy() != 0) {
+        // the commit's slot copy of the node's cpuset state (RF_NUMA_* row fields)
+        NumaNodeCtx nc;
+        nc.plain_req_cpu = nc.plain_req_mem = nc.plain_alloc_cpu = nc.plain_alloc_mem = 0;
+        nc.cs_milli = load_field(a.rowcols[RF_NUMA_A].p, a.rowcols[RF_NUMA_A].width, node);
+        nc.cs_off = load_field(a.rowcols[RF_NUMA_OFF].p, a.rowcols[RF_NUMA_OFF].width, node);
+        nc.ratio = __longlong_as_double(load_field(a.rowcols[RF_NUMA_RATIO].p, a.rowcols[RF_NUMA_RATIO].width, node));
+        nc.cpu_free = (int32_t)load_field(a.rowcols[RF_CPU_FREE].p, a.rowcols[RF_CPU_FREE].width, node);
+        if (DEV && cfg.dev && (pflags & kPodHasGpu)) npr = numa_policy_eval<true>(cfg, pod, nv, nc, &dvg);
+        else npr = numa_policy_eval(cfg, pod, nv, nc, (const DevGView*)nullptr);
+        npol = true;
+      }
+    }
+    if (npol) {
+      o.flags = 1u | (npr.admitted ? 2u : 0u);
+      o.reasons = npr.reasons;
+      o.affinity = npr.affinity;
+#pragma unroll
+      for (int k = 0; k < kNumaDev; ++k) {
+        o.alloc[0][k] = npr.alloc[0][k];
+        o.alloc[1][k] = npr.alloc[1][k];
+        o.cpus[k] = npr.cpus[k];
+      }
+    }
+    if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
+      const uint32_t dev_allow = (npol && npr.admitted && npr.affinity) ? npr.affinity : ~0u;
+      GpuReq g;
+      const DevOut dd = dev_eval<true>(cfg, pod, dvg, &g, dev_allow);
+      o.gminors = dd.minors;
+      o.rminors = dd.rminors;
+      o.g_core = g.core;
+      o.g_mem = g.mem;
+      o.g_ratio = g.ratio;
+      o.g_rdma = g.rdma;
+    }
+  }
+  const_cast<PreRsv*>(a.pre_rsv)[j * kPreRsvM + lane] = o;
+}
+
 struct PassLaunch {
   hipError_t (*sweep)(int blocks, hipStream_t s, const SweepArgs& a);
   hipError_t (*commit)(bool qc, size_t smem, hipStream_t s, const CommitArgs& a);
@@ -1630,6 +1784,8 @@ struct PassLaunch {
   // FEAT 0 only (else null): the monotone commit kernel (ks_mono.h)
   hipError_t (*commit_mono)(bool qc, size_t smem, hipStream_t s, const CommitArgs& a);
   hipError_t (*commit_mono_attr)(bool qc, size_t smem);
+  // NodeNUMAResource / DeviceShare variants only (else null): reserve_pre_kernel, one workgroup per pod of the pass
+  hipError_t (*reserve_pre)(int blocks, hipStream_t s, const CommitArgs& a);
 };
 #define KS_DECLARE_VARIANT(F) PassLaunch pass_launch_f##F##_n0(); PassLaunch pass_launch_f##F##_n2(); PassLaunch pass_launch_f##F##_n4();
 KS_DECLARE_VARIANT(0)
