@@ -3301,10 +3301,10 @@ static bool mono_commit(const ks_ctx* ctx, bool qcache, size_t* smem) {
 }
 
 // Reserve's NodeNUMAResource / DeviceShare allocations ahead of the commit (reserve_pre_kernel): on for
-// the variants that have them when the profile enables either plugin; KS_PRE_RSV=0 turns it off (A/B).
+// the NUMA topology policy variants when policy nodes are loaded; KS_PRE_RSV=0 turns it off (A/B).
 static bool pre_reserve(const ks_ctx* ctx) {
   static const int64_t env_pre = env_i64("KS_PRE_RSV", 1, 0, 1);
-  return env_pre != 0 && (ctx->kc.numa_pol || ctx->kc.dev);
+  return env_pre != 0 && ctx->kc.numa_pol;
 }
 
 // the commit kernel's LDS size for this context: checked against the CU's 160 KB and set on the variant

@@ -356,8 +356,8 @@ struct CommitArgs {
   int32_t* pipe_after;
   // patched passes: cand_top is the list re-evaluation's atomic max, which the commit zeroes after reading
   unsigned long long* top_reset;
-  // NodeNUMAResource / DeviceShare variants: Reserve's allocations on each pod's snapshot-best nodes, computed before
-  // the commit by reserve_pre_kernel ([64][kPreRsvM]); NULL = the commit computes every Reserve itself
+  // NUMA topology policy variants: Reserve's NodeNUMAResource / DeviceShare allocations on each pod's snapshot-best
+  // nodes, computed before the commit by reserve_pre_kernel ([64][kPreRsvM]); NULL = the commit computes every Reserve
   const struct PreRsv* pre_rsv;
 };
 
@@ -960,6 +960,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
                             cfg.quota_parent, qrow, flags, pmask, req);
   };
   uint32_t st_next = 0;
+  int32_t par_next = -1;  // QC: the quota parent of the pod the look-ahead ran for (read with its admission)
   Cands cn{};
   // Reservation: set once a commit of this pass lowered a node's restored Requested (the class -1 fast path is off then)
   bool rsv_raised = false;
@@ -982,18 +983,26 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       const int64_t req = pqreq[j * KS_QUOTA_DIMS + ld];
       const uint32_t lm = qlds->limit_mask[qr];
       const int64_t u = qlds->used[o], l = qlds->limit[o];
+      // the leaf's min check (non-preemptible pods) and its parent, in the same batch of reads
+      const uint32_t mm = qlds->min_mask[qr];
+      const int64_t nu = qlds->npused[o], mn = qlds->min[o];
+      const int32_t par = qlds->parent[qr];
       const uint64_t tw = touched[tn >> 6];
       st_next = 0;
+      par_next = par;
       if (has_q && !a.force) {
+        // quota_admit's three checks in its order: the leaf's limits, the leaf's min for a non-preemptible pod, the
+        // ancestors' limits
         const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
         const bool in_pod = lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u);
+        const uint32_t flags = __builtin_amdgcn_readlane(my_flags, j);
         if (__ballot(in_pod && ((lm >> lane) & 1u) && (req + u > l))) {
           st_next = KS_S_QUOTA;
-        } else {
-          const uint32_t flags = __builtin_amdgcn_readlane(my_flags, j);
+        } else if ((flags & KS_POD_NONPREEMPTIBLE) && __ballot(in_pod && ((mm >> lane) & 1u) && (req + nu > mn))) {
+          st_next = KS_S_QUOTA_NONPREEMPTIBLE;
+        } else if (cfg.quota_parent && par >= 0) {
           st_next = quota_admit(qlds->parent, qlds->limit_mask, qlds->min_mask, qlds->limit, qlds->used, qlds->min,
-                                qlds->npused, cfg.quota_parent, qrow, flags & KS_POD_NONPREEMPTIBLE, pmask, req,
-                                /*skip_leaf=*/true);
+                                qlds->npused, true, qrow, 0u, pmask, req, /*skip_leaf=*/true);
         }
       }
       if (st_next) return;
@@ -1033,6 +1042,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   for (int32_t j = 0; j < np; ++j) {
     const uint32_t st = st_next;
     const Cands cj = cn;
+    const int32_t qpar = par_next;
     KS_CAT(0);
     if (st) {
       if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0, 0, 0};
@@ -1398,7 +1408,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
             atomicExch((unsigned long long*)(a.rv->ncls + node), (unsigned long long)ncl);
           }
         }
-        nom_row = a.rv->rowid[gi];
+        nom_row = (int32_t)gi;  // CSR position: the caller's row is looked up at the write-back (off the sequential path)
       }
       const bool take = !t_prod_only || (pflags & KS_POD_PROD);
       int64_t v = 0;
@@ -1430,7 +1440,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     const bool want_dev = DEV && cfg.dev && (pflags & kPodHasGpu);
     // a slot created by this pod holds the snapshot state: reserve_pre_kernel's allocation for the node, if it ranked
     const PreRsv* pre = nullptr;
-    if ((FEAT & 12) && a.pre_rsv && fresh && (want_npol || want_dev)) {
+    if ((FEAT & 8) && a.pre_rsv && fresh && (want_npol || want_dev)) {
       const int32_t pn = lane < kPreRsvM ? a.pre_rsv[j * kPreRsvM + lane].node : -1;
       const uint64_t hit = __ballot(pn == node);
       if (hit) pre = a.pre_rsv + j * kPreRsvM + (__ffsll((long long)hit) - 1);
@@ -1588,7 +1598,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           if (QC) {
             // LDS atomics: no read-back on the sequential path (the next pod's admission reads after them)
             for (int32_t cur = qrow; cur >= 0;) {
-              const int32_t up = qlds->parent[cur];
+              const int32_t up = cur == qrow ? qpar : qlds->parent[cur];  // (the leaf's parent: read by the look-ahead)
               atomicAdd((unsigned long long*)&qlds->used[(size_t)cur * KS_QUOTA_DIMS + lane], (unsigned long long)qreq);
               if (np_) atomicAdd((unsigned long long*)&qlds->npused[(size_t)cur * KS_QUOTA_DIMS + lane], (unsigned long long)qreq);
               cur = up;
@@ -1623,7 +1633,11 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
   }
   // ---- write back: results, touched rows, quota usage ----
-  if (lane < processed) a.results[cursor0 + lane] = sres[lane];
+  if (lane < processed) {
+    ks_result r = sres[lane];
+    if (RSV && r.reservation >= 0) r.reservation = a.rv->rowid[r.reservation];
+    a.results[cursor0 + lane] = r;
+  }
   if (lane < nslots) {
     const DevNodes d = *a.dn;
     const SlotRow& r = rows[lane];
@@ -1664,7 +1678,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     atomicAdd(&a.counters[2], (unsigned long long)rescans);
     atomicAdd(&a.counters[3], (unsigned long long)misses);
     atomicAdd(&a.counters[15], (unsigned long long)fast);  // ks_stats.diag[7]: monotone fast picks
-    if (FEAT & 12) atomicAdd(&a.counters[5], (unsigned long long)prehits);
+    if (FEAT & 8) atomicAdd(&a.counters[5], (unsigned long long)prehits);
 #if defined(KS_COMMIT_STAMPS) || defined(KS_COMMIT_CAT)
     for (int i = 0; i < 7; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
 #endif
@@ -1674,7 +1688,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 }
 
 // ---- host launch wrappers (one set per (FEAT, NSC) translation unit of ks_variant.hip) ----
-// Reserve ahead of the commit (NodeNUMAResource / DeviceShare variants): one workgroup per pod of the pass ranks the
+// Reserve ahead of the commit (NUMA topology policy variants, FEAT bit 8; in the DeviceShare-only variants the extra
+// registers of the commit's look-up cost more than the device Reserve it saves): one workgroup per pod of the pass ranks the
 // pod's candidate-list keys (each listed chunk's best and runner-up, the snapshot-best nodes of SelectArgs) and computes,
 // for the kPreRsvM highest, what the commit's Reserve computes for a node no earlier pod of the pass touched --
 // numa_policy_eval<ALLOC> (NodeNUMAResource Reserve -> Allocate with the Filter's hint) and dev_eval<ALLOC>
@@ -1784,7 +1799,7 @@ struct PassLaunch {
   // FEAT 0 only (else null): the monotone commit kernel (ks_mono.h)
   hipError_t (*commit_mono)(bool qc, size_t smem, hipStream_t s, const CommitArgs& a);
   hipError_t (*commit_mono_attr)(bool qc, size_t smem);
-  // NodeNUMAResource / DeviceShare variants only (else null): reserve_pre_kernel, one workgroup per pod of the pass
+  // NUMA topology policy variants only (else null): reserve_pre_kernel, one workgroup per pod of the pass
   hipError_t (*reserve_pre)(int blocks, hipStream_t s, const CommitArgs& a);
 };
 #define KS_DECLARE_VARIANT(F) PassLaunch pass_launch_f##F##_n0(); PassLaunch pass_launch_f##F##_n2(); PassLaunch pass_launch_f##F##_n4();

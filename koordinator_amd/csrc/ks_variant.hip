@@ -47,7 +47,7 @@ hipError_t commit_mono_attr(bool qc, size_t smem) {
 }
 #endif
 
-#if (KS_FEAT & 12) != 0
+#if (KS_FEAT & 8) != 0
 hipError_t reserve_pre(int blocks, hipStream_t s, const CommitArgs& a) {
   hipLaunchKernelGGL((reserve_pre_kernel<F>), dim3(blocks), dim3(64), 0, s, a);
   return hipGetLastError();
@@ -59,7 +59,7 @@ hipError_t reserve_pre(int blocks, hipStream_t s, const CommitArgs& a) {
 PassLaunch KS_CAT(KS_CAT(KS_CAT(pass_launch_f, KS_FEAT), _n), KS_NSC)() {
 #if KS_FEAT == 0
   return PassLaunch{sweep, commit, commit_attr, commit_mono, commit_mono_attr, nullptr};
-#elif (KS_FEAT & 12) != 0
+#elif (KS_FEAT & 8) != 0
   return PassLaunch{sweep, commit, commit_attr, nullptr, nullptr, reserve_pre};
 #else
   return PassLaunch{sweep, commit, commit_attr, nullptr, nullptr, nullptr};
