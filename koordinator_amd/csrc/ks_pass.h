@@ -748,6 +748,9 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 #ifdef KS_COMMIT_STAMPS
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tlast = __builtin_amdgcn_s_memtime();
+#ifdef KS_SLOT_SPLIT
+  uint64_t split[4] = {0, 0, 0, 0}, split_sink = 0;
+#endif
 #define KS_STAMP(i)                                    \
   do {                                                 \
     const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
@@ -1069,6 +1072,48 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
       wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
+#ifdef KS_SLOT_SPLIT
+      // diagnostic build (with KS_COMMIT_STAMPS): the slot evaluation's parts timed separately, each run once more on
+      // the same slots ahead of the real evaluation; cycles in diag[0] Fit / LoadAware / NUMA policy None,
+      // diag[1] the NUMA policy path (with DeviceShare's hints), diag[2] DeviceShare's Filter / Score
+      if (lane < nslots) {
+        NodeReg<NSC> r;
+        slot_to_reg<NSC>(rows[lane], r);
+        r.numa_A = snuma[4 * lane];
+        r.numa_off = snuma[4 * lane + 1];
+        r.numa_ratio = __longlong_as_double(snuma[4 * lane + 2]);
+        r.cpu_free = (int32_t)snuma[4 * lane + 3];
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
+        EvalOut e = eval_pod_node<NSC, false>(cfg, pod, r);
+        if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, r, e);
+        split_sink ^= (uint64_t)e.total ^ e.reasons;
+        uint64_t t1 = __builtin_amdgcn_s_memtime();
+        split[0] += t1 - t0;
+        const DevLView dvl{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+        if ((FEAT & 8) && cfg.numa_pol && !(pod.flags & kPodReqZero)) {
+          const NumaLView nl{snp + lane * kNumaSlotWords};
+          if (nl.policy() != 0) {
+            const NumaPolOut pr = (DEV && cfg.dev && (pod.flags & kPodHasGpu))
+                                      ? numa_policy_eval<true>(cfg, pod, nl, numa_node_ctx<NSC>(r), &dvl)
+                                      : numa_policy_eval(cfg, pod, nl, numa_node_ctx<NSC>(r), (const DevLView*)nullptr);
+            split_sink ^= (uint64_t)pr.score ^ pr.affinity ^ pr.reasons;
+          }
+        }
+        uint64_t t2 = __builtin_amdgcn_s_memtime();
+        split[1] += t2 - t1;
+        if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
+          const DevOut d = dev_eval<false>(cfg, pod, dvl, nullptr, ~0u);
+          split_sink ^= (uint64_t)d.raw ^ d.reasons;
+        }
+        uint64_t t3 = __builtin_amdgcn_s_memtime();
+        split[2] += t3 - t2;
+        if ((FEAT & 8) && DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
+          const DevHints dh = dev_hints(cfg, pod, dvl);
+          split_sink ^= (uint64_t)dh.ok ^ dh.minaff ^ dh.lists;
+        }
+        split[3] += __builtin_amdgcn_s_memtime() - t3;
+      }
+#endif
       if (lane < nslots) {
         // the dictionary-bit plugins first: three words out, their temporaries dead before eval_full's peak
         EvalOut so{};
@@ -1680,6 +1725,14 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     atomicAdd(&a.counters[15], (unsigned long long)fast);  // ks_stats.diag[7]: monotone fast picks
     if (FEAT & 8) atomicAdd(&a.counters[5], (unsigned long long)prehits);
 #if defined(KS_COMMIT_STAMPS) || defined(KS_COMMIT_CAT)
+#ifdef KS_SLOT_SPLIT
+    // (the slowest lane of each part: the wave's time; the sink keeps the timed evaluations)
+    ph[0] = split[0] + (split_sink == 0x5eedull ? 1 : 0);
+    ph[1] = split[1];
+    ph[2] = split[2];
+    ph[3] = split[3];
+    ph[4] = ph[5] = ph[6] = 0;
+#endif
     for (int i = 0; i < 7; ++i) atomicAdd(&a.counters[8 + i], (unsigned long long)ph[i]);
 #endif
   }

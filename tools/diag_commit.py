@@ -1,14 +1,17 @@
 """Diagnostic: per-phase cycle split of the commit kernel (libkoordgpu_diag.so, -DKS_COMMIT_STAMPS) or, with
 --cat, per-pod-category cycles (libkoordgpu_cat.so, -DKS_COMMIT_CAT); both built by tools/build_diag.sh.
 --seg: the fast pods' iteration split (libkoordgpu_seg.so, -DKS_COMMIT_SEG; monotone commit kernel only).
-usage: python tools/diag_commit.py [c2|c3|c4|c5] [--cat|--seg]"""
+--split: the slot evaluation's parts timed separately (libkoordgpu_split.so, -DKS_COMMIT_STAMPS -DKS_SLOT_SPLIT).
+usage: python tools/diag_commit.py [c2|c3|c4|c5] [--cat|--seg|--split]"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CAT = "--cat" in sys.argv
 SEG = "--seg" in sys.argv
-sys.argv = [a for a in sys.argv if a not in ("--cat", "--seg")]
+SPLIT = "--split" in sys.argv
+sys.argv = [a for a in sys.argv if a not in ("--cat", "--seg", "--split")]
 os.environ.setdefault("KS_LIB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "koordinator_amd",
-                                                  "libkoordgpu_seg.so" if SEG else ("libkoordgpu_cat.so" if CAT else "libkoordgpu_diag.so")))
+                                                  "libkoordgpu_seg.so" if SEG else ("libkoordgpu_cat.so" if CAT else (
+                                                      "libkoordgpu_split.so" if SPLIT else "libkoordgpu_diag.so"))))
 from koordinator_amd import runtime, synth
 which = sys.argv[1] if len(sys.argv) > 1 else "c2"
 w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4, "c5": lambda: synth.c5(n_pods=100_000)}[which]()
@@ -19,6 +22,12 @@ ev.stage(w.pods)
 ev.checkpoint()
 for i in range(3):
     ev.restore(); ev.schedule_staged(); st = ev.stats()
+if SPLIT:
+    d = st["diag"]
+    print(w.name, {k: st[k] for k in ("passes", "commit_ms")})
+    for nm, v in zip(("Fit+LoadAware+NUMA none", "NUMA policy path", "DeviceShare Filter/Score", "(DeviceShare hints alone)"), d[:4]):
+        print(f"{nm:26s} {v:14d} cycles {v / w.pods.n:10.1f} cyc/pod (slowest lane, re-run ahead of the slot evaluation)")
+    sys.exit(0)
 if SEG:
     d = st["diag"]
     nf = max(d[7], 1)
