@@ -964,10 +964,15 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   };
   uint32_t st_next = 0;
   int32_t par_next = -1;  // QC: the quota parent of the pod the look-ahead ran for (read with its admission)
+  // NUMA-policy variants: the node ids of the look-ahead pod's reserve_pre_kernel records (lane < kPreRsvM) and, with
+  // Cfg.cores, the core word of its best untouched candidate; both loads in flight across the pod's slot evaluation
+  int32_t pre_nodes = -1, cw_node = -1;
+  uint32_t cw_next = 0;
   Cands cn{};
   // Reservation: set once a commit of this pass lowered a node's restored Requested (the class -1 fast path is off then)
   bool rsv_raised = false;
   auto lookahead = [&](int32_t j) {
+    if ((FEAT & 8) && a.pre_rsv) pre_nodes = lane < kPreRsvM ? a.pre_rsv[j * kPreRsvM + lane].node : -1;
     // the fast path also holds for a pod without device requests when only DeviceShare's normalization
     // max made the profile non-monotone (its DeviceShare score is 0 on every node), and, with Reservation, for a pod
     // that matches no reservation: it sees every node through the base restore, whose Requested a commit only raises
@@ -1024,6 +1029,10 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       }
     }
     cn = resolve_cands(cand_chunk, cand_t, touched, j, Kc, __builtin_amdgcn_readlane(my_cnt, j));
+    if ((FEAT & 2) && cfg.cores && cn.umax) {
+      cw_node = (int32_t)gkey_node(cn.umax);
+      cw_next = gld(a.dn->cpu_cores + cw_node);
+    }
 #ifndef KS_NO_SPEC
     if (cn.umax) {
       const int32_t node = (int32_t)gkey_node(cn.umax);
@@ -1218,7 +1227,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     int32_t s = __ffsll((long long)__ballot(snode == node)) - 1;
     uint32_t ncw = 0;  // Cfg.cores: the node's CoresWord
     if ((FEAT & 2) && cfg.cores) {
-      ncw = __builtin_amdgcn_readfirstlane(s >= 0 ? (uint32_t)((uint64_t)snuma[4 * s + 3] >> 32) : gld(a.dn->cpu_cores + node));
+      ncw = __builtin_amdgcn_readfirstlane(s >= 0 ? (uint32_t)((uint64_t)snuma[4 * s + 3] >> 32)
+                                                  : (node == cw_node ? cw_next : gld(a.dn->cpu_cores + node)));
       // a whole-CPU pod is cpu-bind on a node with a CPU bind policy (requestCPUBind, util.go:105-122)
       const int64_t pcpu = podw[0];  // PodRec.cpu
       if (!cpubind && cfg.cpuset && cores_label(ncw) != 0 && pcpu > 0) {
@@ -1237,6 +1247,31 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       fresh = true;
       s = nslots++;
       row = &rows[s];
+      // the node's NUMA-node, dictionary and device words: loads issued before the raw row's, one HBM round trip
+      int64_t ld_numa = 0, ld_stat = 0, ld_dtot = 0, ld_duse = 0;
+      if ((FEAT & 8) && cfg.numa_pol) {
+        const DevNuma& nv = *a.nv;
+        if (lane < kNumaWUsed) ld_numa = gld(nv.total + (int64_t)lane * nv.npad + node);
+        else if (lane < kNumaWOff) ld_numa = gld(nv.used + (int64_t)(lane - kNumaWUsed) * nv.npad + node);
+        else if (lane < kNumaWCpu) ld_numa = gld(nv.off + (int64_t)(lane - kNumaWOff) * nv.npad + node);
+        else if (lane < kNumaWMeta)
+          ld_numa = ((int64_t)gld(nv.cs + (int64_t)(lane - kNumaWCpu) * nv.npad + node) << 32) |
+                    (int64_t)(uint32_t)gld(nv.free + (int64_t)(lane - kNumaWCpu) * nv.npad + node);
+        else if (lane == kNumaWMeta)
+          ld_numa = (int64_t)((gld(nv.flags + node) >> KS_NUMA_POLICY_SHIFT) & 3u) |
+                    ((int64_t)gld(nv.count + node) << 8) | ((int64_t)gld(nv.present + node) << 32);
+      }
+      if (DEV && cfg.stat && lane < 4) {
+        const DevNodes d = *a.dn;
+        const uint64_t* col = lane == 0 ? d.taints_hard : (lane == 1 ? d.taints_soft : (lane == 2 ? d.labels : d.host_ports));
+        ld_stat = (int64_t)gld(col + node);
+      }
+      if (DEV && cfg.dev) {
+        const DevDev& dv = *a.dv;
+        if (lane < DW) ld_dtot = gld(dv.total + (int64_t)lane * dv.npad + node);
+        else if (lane == DW) ld_dtot = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
+        if (lane < DU) ld_duse = gld(dv.used + (int64_t)lane * dv.npad + node);
+      }
       const int64_t* src = raw;
       if (node == (int32_t)gkey_node(readlane64(my_top, j))) {
         src = rawtop + j * 32;  // prefetched at pass start
@@ -1292,36 +1327,14 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
                                        : (int64_t)u_free;
         }
       }
-      if ((FEAT & 8) && cfg.numa_pol) {
-        // the node's NUMA-node state into LDS (lane = word, NumaLView layout)
-        const DevNuma& nv = *a.nv;
-        int64_t v = 0;
-        if (lane < kNumaWUsed) v = gld(nv.total + (int64_t)lane * nv.npad + node);
-        else if (lane < kNumaWOff) v = gld(nv.used + (int64_t)(lane - kNumaWUsed) * nv.npad + node);
-        else if (lane < kNumaWCpu) v = gld(nv.off + (int64_t)(lane - kNumaWOff) * nv.npad + node);
-        else if (lane < kNumaWMeta)
-          v = ((int64_t)gld(nv.cs + (int64_t)(lane - kNumaWCpu) * nv.npad + node) << 32) |
-              (int64_t)(uint32_t)gld(nv.free + (int64_t)(lane - kNumaWCpu) * nv.npad + node);
-        else if (lane == kNumaWMeta)
-          v = (int64_t)((gld(nv.flags + node) >> KS_NUMA_POLICY_SHIFT) & 3u) | ((int64_t)gld(nv.count + node) << 8) |
-              ((int64_t)gld(nv.present + node) << 32);
-        if (lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = v;
-      }
-      if (DEV && cfg.stat) {
-        const DevNodes d = *a.dn;
-        const uint64_t* col = lane == 0 ? d.taints_hard : (lane == 1 ? d.taints_soft : (lane == 2 ? d.labels : d.host_ports));
-        if (lane < 4) sstat[4 * s + lane] = gld(col + node);
-      }
+      // the slot's NUMA-node state (lane = word, NumaLView layout), dictionary words and device totals + topology /
+      // used / present flag into LDS (loaded above)
+      if ((FEAT & 8) && cfg.numa_pol && lane < kNumaSlotWords) snp[s * kNumaSlotWords + lane] = ld_numa;
+      if (DEV && cfg.stat && lane < 4) sstat[4 * s + lane] = (uint64_t)ld_stat;
       if (DEV && cfg.dev) {
-        // the node's device totals + topology / used / present flag into LDS (lane = word)
-        const DevDev& dv = *a.dv;
-        int64_t v = 0, w = 0;
-        if (lane < DW) v = gld(dv.total + (int64_t)lane * dv.npad + node);
-        else if (lane == DW) v = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
-        if (lane < DU) w = gld(dv.used + (int64_t)lane * dv.npad + node);
-        if (lane < DW) sdev_tot[lane * kDevLdsStride + s] = v;
-        else if (lane == DW) sdev_pres[s] = (int32_t)v;
-        if (lane < DU) sdev_use[lane * kDevLdsStride + s] = w;
+        if (lane < DW) sdev_tot[lane * kDevLdsStride + s] = ld_dtot;
+        else if (lane == DW) sdev_pres[s] = (int32_t)ld_dtot;
+        if (lane < DU) sdev_use[lane * kDevLdsStride + s] = ld_duse;
       }
       if (RSV && cfg.rsv) {
         // the node's reservations into LDS (lane = record word), unless too many or too wide
@@ -1486,8 +1499,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     // a slot created by this pod holds the snapshot state: reserve_pre_kernel's allocation for the node, if it ranked
     const PreRsv* pre = nullptr;
     if ((FEAT & 8) && a.pre_rsv && fresh && (want_npol || want_dev)) {
-      const int32_t pn = lane < kPreRsvM ? a.pre_rsv[j * kPreRsvM + lane].node : -1;
-      const uint64_t hit = __ballot(pn == node);
+      const uint64_t hit = __ballot(pre_nodes == node);  // (read by the look-ahead)
       if (hit) pre = a.pre_rsv + j * kPreRsvM + (__ffsll((long long)hit) - 1);
     }
     GpuReq g;
