@@ -482,7 +482,13 @@ def main():
     ap.add_argument("--sub-warmup", type=int, default=1)
     ap.add_argument("--no-preempt", action="store_true", help="skip the preempt (ElasticQuota PostFilter) record")
     ap.add_argument("--preempt-pods", type=int, default=128)
+    ap.add_argument("--preempt-only", action="store_true",
+                    help="print only the preempt record (profiling runs of the PostFilter kernels, tools/pmc_traffic.sh)")
     args = ap.parse_args()
+    if args.preempt_only:
+        rec = run_preempt(args, args.steps, args.warmup, not args.no_profile, not args.no_cpu_baseline)
+        print(json.dumps({"preempt": rec}), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -4,7 +4,8 @@
 # the PMC HBM traffic (FETCH_SIZE / WRITE_SIZE passes) and VALU-issue summaries; for c5 the PMC passes on a 200k-pod
 # queue (sweep measured unpipelined, KS_PIPE=0: the same kernel without the list re-evaluation launches) and last the
 # pipelined kernel trace with its overlap summary (tools/trace_overlap.py).
-# Output: gpurun_out/$1/<cfg>_{kernel_stats.csv,traffic.json,valu.json}, c5_overlap.json; tools/keep_profiles.sh copies
+# Output: gpurun_out/$1/<cfg>_{kernel_stats.csv,traffic.json,valu.json}, preempt_{kernel_stats.csv,traffic.json},
+# c5_overlap.json; tools/keep_profiles.sh copies
 # them into profiles/ under a round tag.
 set -o pipefail
 OUT=gpurun_out/${1:-prof}
@@ -22,6 +23,17 @@ for CFG in ${CONFIGS:-c2 c3 c4 c2d}; do
   rm -rf $OUT/traffic_$CFG $OUT/valu_$CFG
   echo "profiles $CFG done"
 done
+if [ "${PREEMPT:-1}" = 1 ]; then
+  # the PostFilter kernels (bench.py --preempt-only): kernel statistics and PMC HBM traffic
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_preempt -o run -- python3 bench.py --preempt-only --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof_preempt.json 2> $OUT/prof_preempt.err || { echo "rocprof preempt failed"; tail -30 $OUT/prof_preempt.err; exit 1; }
+  S=$(find $OUT/prof_preempt -name '*kernel_stats.csv' | head -1)
+  [ -n "$S" ] && cp $S $OUT/preempt_kernel_stats.csv
+  rm -rf $OUT/prof_preempt
+  bash tools/pmc_traffic.sh preempt $(basename $OUT)/traffic_preempt > /dev/null || exit 1
+  cp $OUT/traffic_preempt/traffic.json $OUT/preempt_traffic.json
+  rm -rf $OUT/traffic_preempt
+  echo "profiles preempt done"
+fi
 if [ "${C5:-1}" = 1 ]; then
   KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_traffic.sh c5 $(basename $OUT)/traffic_c5 > /dev/null || exit 1
   cp $OUT/traffic_c5/traffic.json $OUT/c5_traffic.json
