@@ -3054,14 +3054,9 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
       any_req |= req;
       if (cpu <= 0 || cpu % 1000 != 0 || cpu / 1000 > KS_MAX_CPUS)
         KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
-      // a preferred FullPCPUs request that is not a whole number of cores takes split cores in takeCPUs'
-      // fallbacks, which the device accumulator does not model: refused (a required one fails the Filter's SMT
-      // alignment check per node, plugin.go:314-317)
-      if (pol == KS_CPU_BIND_FULL_PCPUS && !req)
-        for (int32_t cpc : ctx->cpu_cpc)
-          if (cpc > 1 && (cpu / 1000) % cpc != 0)
-            KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: FullPCPUs request of %lld CPUs is not a whole number of %d-thread cores", i,
-                    (long long)(cpu / 1000), cpc);
+      // (a preferred FullPCPUs request that is not a whole number of cores takes a split core in takeCPUs'
+      // freeCoresInNode / freeCoresInSocket prefixes or the fallbacks, as ks_cpuset.h does; a required one fails the
+      // Filter's SMT alignment check per node, plugin.go:314-317)
     }
   }
   if (pc->joint) {

@@ -58,9 +58,8 @@ def golden_cluster(case):
 
 
 def supported_on_device(case):
-    """maxRefCount 1, and FullPCPUs requests in whole cores (the evaluator refuses the rest)"""
-    cpc = case["topo"][3]
-    return case["max_ref"] == 1 and not (case["bind"] == "FullPCPUs" and case["needed"] % cpc)
+    """maxRefCount 1 (the evaluator refuses CPU sharing)"""
+    return case["max_ref"] == 1
 
 
 def bind_policy_cluster(topo, allocated=(), label=0, cpu_milli=4000, bind=None, required=False, excl=0,

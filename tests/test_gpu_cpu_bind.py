@@ -28,12 +28,8 @@ def test_reference_filter_cases(runtime, case):
     _, label, bind, required, cpu, want = case
     cfg, nodes, st, pod = bind_policy_cluster((2, 1, 4, 2), label=label, cpu_milli=cpu, bind=bind, required=required)
     ev = runtime.Evaluator(cfg, nodes, cpu_state=st)
-    if bind == abi.KS_CPU_BIND_FULL_PCPUS and not required and cpu % 2000:
-        # a preferred FullPCPUs request in split cores: refused by the evaluator (koordgpu.h)
-        with pytest.raises(runtime.KsError):
-            ev.eval_pod(pod)
-    else:
-        assert int(ev.eval_pod(pod)[0][0]) == want
+    # (preferred FullPCPUs requests in split cores included)
+    assert int(ev.eval_pod(pod)[0][0]) == want
     ev.close()
 
 

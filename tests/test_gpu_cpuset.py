@@ -128,12 +128,46 @@ def test_eval_debug_cpu_bind(runtime, oracle_lib):
     orc.close()
 
 
-def test_full_pcpus_partial_core_refused(runtime):
-    case = dict(G["cases"][0])
-    case["needed"] = 3  # 3 CPUs on 2-thread cores with FullPCPUs
-    cfg, nodes, st, pod = golden_cluster(case)
-    ev = runtime.Evaluator(cfg, nodes, cpu_state=st)
-    with pytest.raises(runtime.KsError) as ei:
-        ev.schedule(pod)
-    assert ei.value.rc == abi.KS_EUNSUPPORTED
-    ev.close()
+@pytest.mark.parametrize("seed", range(4))
+def test_full_pcpus_split_cores(runtime, oracle_lib, seed):
+    """A preferred FullPCPUs request that is not a whole number of cores (takeCPUs takes a core's first CPUs in
+    freeCoresInNode / freeCoresInSocket prefixes, whole cores then single cores in the fallback, then spread CPUs):
+    the HIP accumulator against the oracle's restatement on the golden tables' topologies with random allocations,
+    exclusive policies and strategies.  (The reference's tables hold no such request: parity against the oracle
+    only.)"""
+    rng = np.random.default_rng(100 + seed)
+    n_checked = 0
+    for case in G["cases"]:
+        if case["max_ref"] != 1 or case["topo"][3] < 2:
+            continue
+        core_count = case["topo"][0] * case["topo"][1] * case["topo"][2]
+        ncpu = core_count * case["topo"][3]
+        c = dict(case)
+        c["allocated"] = sorted(rng.choice(ncpu, int(rng.integers(0, ncpu // 2)), replace=False).tolist())
+        c["allocated_excl"] = str(rng.choice(["None", "PCPULevel", "NUMANodeLevel"]))
+        free = ncpu - len(c["allocated"])
+        c["needed"] = int(rng.integers(1, max(2, free)))
+        if c["needed"] % case["topo"][3] == 0:
+            c["needed"] = max(1, c["needed"] - 1)
+        c["bind"] = "FullPCPUs"
+        c["excl"] = str(rng.choice(["None", "PCPULevel", "NUMANodeLevel"]))
+        c["strategy"] = str(rng.choice(["Most", "Least"]))
+        cfg, nodes, st, pod = golden_cluster(c)
+        ev = runtime.Evaluator(cfg, nodes.copy(), cpu_state=st.copy() if hasattr(st, "copy") else st)
+        got = ev.schedule(pod)
+        cs_g = mask_cpus(ev.fetch_cpusets(1)[0])
+        state_g = ev.read_cpu_state()
+        ev.close()
+        cfg, nodes, st, pod = golden_cluster(c)
+        orc = oracle_lib.Oracle(cfg, nodes, cpu_state=st)
+        want = orc.schedule(pod)
+        cs_o = mask_cpus(orc.fetch_cpusets(1)[0])
+        state_o = orc.read_cpu_state()
+        orc.close()
+        label = f"{case['name']} needed {c['needed']} excl {c['excl']}/{c['allocated_excl']} {c['strategy']}"
+        assert got["status"][0] == want["status"][0] and got["node"][0] == want["node"][0], label
+        assert cs_g == cs_o, f"{label}: {cs_g} (GPU) vs {cs_o} (oracle)"
+        for a, b in zip(state_g, state_o):
+            assert np.array_equal(a, b), label
+        n_checked += int(want["status"][0] == abi.KS_S_SCHEDULED)
+    assert n_checked > 10
