@@ -107,3 +107,28 @@ def test_pdb_heavy(runtime, oracle_lib):
     prio = np.full(16, 9000, np.int32)
     outs = compare(runtime, oracle_lib, profile(quota=True).to_ks_config(), nodes, q, t, pods, prio, "pdb")
     assert any(o["num_pdb_violations"] > 0 for o in outs)
+
+
+def test_edge_inputs(runtime, oracle_lib):
+    """No running pod anywhere; every node unresolvable; one running pod that is not preemptible; a node holding
+    the dry run's maximum of 256 pods."""
+    w = synth.c2_preempt(seed=11, n_nodes=300, n_preemptors=4)
+    empty = w.node_pods.rows(np.arange(0))
+    compare(runtime, oracle_lib, w.cfg, w.nodes, w.quotas, empty, w.preemptors, w.priority, "no running pods")
+    compare(runtime, oracle_lib, w.cfg, w.nodes, w.quotas, w.node_pods, w.preemptors, w.priority, "all unresolvable",
+            unresolvable=np.ones(w.nodes.n, np.uint8))
+    one = w.node_pods.rows(np.arange(1))
+    one.flags[:] |= abi.KS_NPOD_NONPREEMPTIBLE
+    compare(runtime, oracle_lib, w.cfg, w.nodes, w.quotas, one, w.preemptors, w.priority, "one non-preemptible pod")
+    rng = np.random.Generator(np.random.PCG64(12))
+    nodes = synth.make_nodes(40, rng)
+    nodes.allowed_pods[:] = 300
+    t, used = synth.make_node_pods(nodes, rng, 8, per_node=(256, 256), n_pdb=4, pdb_frac=0.3)
+    nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 2000, nodes.n), 1000)
+    q = synth.QuotaTable(8)
+    q.limit_mask[:] = 0xF
+    q.used[:] = used
+    q.limit[:] = (used * 1.02).astype(np.int64)
+    pods = synth.make_pods(6, rng, 8)
+    compare(runtime, oracle_lib, profile(quota=True).to_ks_config(), nodes, q, t, pods,
+            np.full(6, 9000, np.int32), "256 pods per node")
