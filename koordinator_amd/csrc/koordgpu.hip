@@ -3366,6 +3366,19 @@ struct PipeStreams {
 static std::mutex g_pipe_mu;
 static std::vector<PipeStreams> g_pipe;
 
+// At process exit the shared streams are released before the HIP runtime's own teardown (atexit handlers run in
+// reverse order of registration, and the runtime registers its handlers before the first stream exists): left to the
+// runtime's teardown, the CU-masked streams crashed a rocprofv3 --kernel-trace run in __cxa_finalize after its output
+// was written.  By then no context may still be using them.
+static void release_pipe_streams() {
+  std::lock_guard<std::mutex> lock(g_pipe_mu);
+  for (PipeStreams& st : g_pipe) {
+    if (st.c) (void)hipStreamDestroy(st.c);
+    if (st.s) (void)hipStreamDestroy(st.s);
+    st.s = st.c = nullptr;
+  }
+}
+
 // The sweep stream (CU-masked to all but KS_PIPE_COMMIT_CUS = 32 CUs, which the commit stream gets: the one-workgroup
 // commit and the patched passes' list re-evaluation never share a CU with sweep waves; KS_PIPE_CUMASK=0: no masks), the
 // pipe words and the event ring.
@@ -3384,6 +3397,8 @@ static int ensure_pipe(ks_ctx* ctx) {
     // The commit stream runs on the KS_PIPE_COMMIT_CUS CUs the sweep stream leaves out, so the one-workgroup commit
     // never shares a CU (and its SIMDs' issue slots) with sweep waves.
     std::lock_guard<std::mutex> lock(g_pipe_mu);
+    static const bool at_exit = std::atexit(release_pipe_streams) == 0;
+    (void)at_exit;
     if (g_pipe.size() <= (size_t)ctx->device) g_pipe.resize((size_t)ctx->device + 1);
     PipeStreams& st = g_pipe[(size_t)ctx->device];
     if (!st.s) {
