@@ -2,7 +2,7 @@
 --cat, per-pod-category cycles (libkoordgpu_cat.so, -DKS_COMMIT_CAT); both built by tools/build_diag.sh.
 --seg: the fast pods' iteration split (libkoordgpu_seg.so, -DKS_COMMIT_SEG; monotone commit kernel only).
 --split: the slot evaluation's parts timed separately (libkoordgpu_split.so, -DKS_COMMIT_STAMPS -DKS_SLOT_SPLIT).
-usage: python tools/diag_commit.py [c2|c3|c4|c5] [--cat|--seg|--split]"""
+usage: python tools/diag_commit.py [c2|c3|c4|c5|c2d] [--cat|--seg|--split]"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CAT = "--cat" in sys.argv
@@ -14,7 +14,8 @@ os.environ.setdefault("KS_LIB_PATH", os.path.join(os.path.dirname(os.path.dirnam
                                                       "libkoordgpu_split.so" if SPLIT else "libkoordgpu_diag.so"))))
 from koordinator_amd import runtime, synth
 which = sys.argv[1] if len(sys.argv) > 1 else "c2"
-w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4, "c5": lambda: synth.c5(n_pods=100_000)}[which]()
+w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4, "c2d": synth.c2_default,
+     "c5": lambda: synth.c5(n_pods=100_000)}[which]()
 cfg = w.cfg
 cfg.profile = 1
 ev = runtime.Evaluator(cfg, w.nodes, **w.tables(copy=False))
