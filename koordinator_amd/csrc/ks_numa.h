@@ -215,9 +215,16 @@ __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, con
 // returns before the NUMA score".
 // Register-resident: hint sets are bit sets over mask indices, per-mask hint scores are packed bytes, the merge is
 // three nested bit-set walks; no dynamically indexed local arrays (those would live in scratch memory).
-template <bool DEFER_DEV = false, typename V, typename DV>
+// dhf: DeviceShare's hints from elsewhere (the commit kernel's hint wave, ks_pass.h), fetched after the NodeNUMAResource
+// hints instead of computed first; NoDevHints = compute them here.
+struct NoDevHints {};
+template <typename T> struct LateDevHints { static constexpr bool value = true; };
+template <> struct LateDevHints<NoDevHints> { static constexpr bool value = false; };
+
+template <bool DEFER_DEV = false, typename V, typename DV, typename DHF = NoDevHints>
 __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRec& p, const V& v, const NumaNodeCtx& nc,
-                                                       const DV* dv) {
+                                                       const DV* dv, DHF dhf = DHF{}) {
+  constexpr bool LATE = LateDevHints<DHF>::value;
   NumaPolOut o;
   o.reasons = 0;
   o.score = 0;
@@ -241,7 +248,7 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
   dh.npos = 0;
   dh.ok = 0;
   dh.minaff = -1;
-  if (dv) dh = dev_hints(c, p, *dv);
+  if (!LATE && dv) dh = dev_hints(c, p, *dv);
   const int pol = v.policy();
   const uint32_t pres = v.present();
   const bool bind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
@@ -330,6 +337,9 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
       }
       lb[r] = s;
     }
+  }
+  if constexpr (LATE) {
+    if (dv) dh = dhf();
   }
   uint32_t db = 1u << kNil;
   bool dnp = true;

@@ -431,7 +431,10 @@ __device__ __forceinline__ QuotaRowsLds quota_lds(unsigned char* p, int32_t q) {
   return v;
 }
 
-constexpr size_t kHelpBytes = (size_t)kMaxBatch * 8 + 16 + 16;
+// FEAT 0: the builder wave's descriptors, counts and ready mask; NUMA-policy + DeviceShare variants: the hint wave's
+// per-slot DevHints and its request words
+constexpr size_t kHelpBytes = (size_t)kMaxBatch * 24 + 64;
+static_assert(sizeof(DevHints) == 24 && kHelpBytes >= (size_t)kMaxBatch * 8 + 32, "help region");
 
 struct CommitLayout {
   size_t rows, pods, res, raw, rawtop, rawrun, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, help,
@@ -736,6 +739,12 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   int32_t* hpend = reinterpret_cast<int32_t*>(smem_raw + lay.help + (size_t)kMaxBatch * 8);  // descriptors issued
   int32_t* hdone = hpend + 1;                                                                // wave 0 is done
   unsigned long long* hready = reinterpret_cast<unsigned long long*>(smem_raw + lay.help + (size_t)kMaxBatch * 8 + 16);
+  // NUMA topology policies + DeviceShare: wave 1 computes DeviceShare's topology hints of every touched slot for the
+  // pod wave 0 is evaluating (lane = slot, the same dev_hints on the same LDS state), while wave 0 runs the other
+  // plugins and the NodeNUMAResource hints; wave 0 takes them at the merge (numa_policy_eval's dhf)
+  constexpr bool HINTW = (FEAT & 12) == 12;
+  DevHints* shint = reinterpret_cast<DevHints*>(smem_raw + lay.help);                      // [slot]
+  int32_t* hw = reinterpret_cast<int32_t*>(smem_raw + lay.help + (size_t)kMaxBatch * 24);  // seq, pod, n, done, quit
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -841,8 +850,9 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     *hdone = 0;
     *hready = 0ull;
   }
+  if (HINTW && tid < 5) hw[tid] = 0;
   __syncthreads();
-  if (tid >= (HELP ? 128 : 64)) return;  // the other waves are done; wave 0 runs the sequential loop alone
+  if (tid >= ((HELP || HINTW) ? 128 : 64)) return;  // the other waves are done; wave 0 runs the sequential loop
   KS_STAMP(0);
   // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
   // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
@@ -930,6 +940,33 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     }
     return;
   }
+  if (HINTW && tid >= 64) {
+    // ---- wave 1: the hint wave (serves wave 0's requests in order until told to quit; an idle ~0.1 s, far
+    // beyond any pass, also ends it: wave 0's wait is bounded the same way and then computes the hints itself) ----
+    int32_t last = 0;
+    uint32_t idle = 0;
+    for (;;) {
+      const int32_t sq = __builtin_amdgcn_readfirstlane(__hip_atomic_load(hw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (sq != last) {
+        const int32_t jj = __builtin_amdgcn_readfirstlane(hw[1]), ns = __builtin_amdgcn_readfirstlane(hw[2]);
+        if (lane < ns) {
+          PodRec pod = spods[jj];
+          pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
+          pod.rsv_class = __builtin_amdgcn_readfirstlane(pod.rsv_class);
+          shint[lane] = dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
+        }
+        if (lane == 0) __hip_atomic_store(hw + 3, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        last = sq;
+        idle = 0;
+        continue;
+      }
+      if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 4, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))) break;
+      if (++idle > (1u << 22)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return;
+  }
+  int32_t hseq = 0;      // hint-wave requests issued
   int32_t hn = 0;        // descriptors issued to wave 1
   uint64_t hown = 0;     // slots whose rows wave 0 built itself
   // wave 0: every row of `need` is built (wave 1's ready mask or its own)
@@ -1081,6 +1118,28 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
       wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
+      const bool use_hw = HINTW && cfg.dev && cfg.numa_pol && (pod.flags & kPodHasGpu) && !(pod.flags & kPodReqZero) &&
+                          nslots > 0;
+      if (use_hw) {
+        ++hseq;
+        if (lane == 0) {
+          hw[1] = j;
+          hw[2] = nslots;
+          __hip_atomic_store(hw, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      // the slot's DeviceShare hints: the hint wave's (use_hw), else computed here
+      auto dhf = [&]() -> DevHints {
+        if (use_hw) {
+          for (uint32_t it = 0; it <= (1u << 22); ++it) {
+            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                hseq)
+              return shint[lane];
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        return dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
+      };
 #ifdef KS_SLOT_SPLIT
       // diagnostic build (with KS_COMMIT_STAMPS): the slot evaluation's parts timed separately, each run once more on
       // the same slots ahead of the real evaluation; cycles in diag[0] Fit / LoadAware / NUMA policy None,
@@ -1150,7 +1209,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
               return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
             },
             [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
-            [&]() { return NumaLView{snp + lane * kNumaSlotWords}; });
+            [&]() { return NumaLView{snp + lane * kNumaSlotWords}; }, nullptr, dhf);
         if (DEV && cfg.stat) {
           o.reasons |= so.reasons;
           o.traw = so.traw;
@@ -1685,6 +1744,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 #endif
   }
   KS_STAMP(6);
+  if (HINTW && lane == 0) __hip_atomic_store(hw + 4, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (HELP) {
     if (lane == 0) __hip_atomic_store(hdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));

@@ -291,9 +291,9 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
 // view (ks_numa.h).  Filter order as in the profile: Fit, LoadAware, NodeNUMAResource (on a node with a NUMA
 // topology policy its topology-manager Admit, whose affinity then restricts DeviceShare), DeviceShare,
 // Reservation.  The key total is key_total(c, o, M) with M the pod's normalization maxima (NormM).
-template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, typename H>
+template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, typename H, typename DHF = NoDevHints>
 __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& devv,
-                                             H&& numav, RsvOut* info = nullptr) {
+                                             H&& numav, RsvOut* info = nullptr, DHF dhf = DHF{}) {
   constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0, DEV = (FEAT & 4) != 0, POL = (FEAT & 8) != 0;
   const bool dev_pod = DEV && c.dev && (p.flags & kPodHasGpu);
   // NodeNUMAResource (policy None part, then the topology-manager path on a policy node); returns DeviceShare's
@@ -313,7 +313,7 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
     NumaPolOut pr;
     if (dev_pod) {
       const DVT dv = devv();
-      pr = numa_policy_eval<!DEBUG>(c, p, nv, numa_node_ctx<NSC>(r), &dv);
+      pr = numa_policy_eval<!DEBUG>(c, p, nv, numa_node_ctx<NSC>(r), &dv, dhf);
     } else {
       pr = numa_policy_eval<!DEBUG>(c, p, nv, numa_node_ctx<NSC>(r), (const DVT*)nullptr);
     }
