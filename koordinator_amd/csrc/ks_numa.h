@@ -143,17 +143,10 @@ __device__ __forceinline__ uint32_t dev_hint_mask(const DevHints& h, int i) {
   return ((pos & 1u) ? (1u << h.id0) : 0u) | ((pos & 2u) ? (1u << h.id1) : 0u);
 }
 
+// numaTopology.nodes of a node's devices: the NUMA ids (a bit each) of the switches holding a device with a topology
 template <typename V>
-__device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, const V& v) {
-  DevHints h;
-  h.lists = 0;
-  h.npos = 0;
-  h.id0 = h.id1 = 0;
-  h.ok = 0;
-  h.minaff = -1;
-  if (!v.present()) return h;
+__device__ __forceinline__ uint32_t dev_topo_ids(const V& v) {
   const uint64_t topo = (uint64_t)v.tot(kDevTopoW), meta = (uint64_t)v.tot(kDevMetaW);
-  // numaTopology.nodes: NUMA nodes of the switches holding a device with a topology
   uint32_t ids = 0;
 #pragma unroll
   for (int k = 0; k < kGpus; ++k) {
@@ -166,6 +159,20 @@ __device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, con
     const uint32_t pc = (uint32_t)(topo >> (32 + 4 * j)) & 0xFu;
     if (v.tot(kDevRdmaW + j) != 0 && pc < 8u) ids |= 1u << ((uint32_t)(meta >> (8 * pc)) & 0xFu);
   }
+  return ids;
+}
+
+template <typename V>
+__device__ __forceinline__ DevHints dev_hints(const Cfg& c, const PodRec& p, const V& v) {
+  DevHints h;
+  h.lists = 0;
+  h.npos = 0;
+  h.id0 = h.id1 = 0;
+  h.ok = 0;
+  h.minaff = -1;
+  if (!v.present()) return h;
+  const uint64_t topo = (uint64_t)v.tot(kDevTopoW), meta = (uint64_t)v.tot(kDevMetaW);
+  const uint32_t ids = dev_topo_ids(v);
   const int nid = __builtin_popcount(ids) < kDevHintIds ? __builtin_popcount(ids) : kDevHintIds;  // ks_load_* checks <= 2
   const uint32_t rest = ids & (ids - 1u);
   h.id0 = ids ? __builtin_ctz(ids) : 0;

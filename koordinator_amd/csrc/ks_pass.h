@@ -431,10 +431,19 @@ __device__ __forceinline__ QuotaRowsLds quota_lds(unsigned char* p, int32_t q) {
   return v;
 }
 
-// FEAT 0: the builder wave's descriptors, counts and ready mask; NUMA-policy + DeviceShare variants: the hint wave's
-// per-slot DevHints and its request words
-constexpr size_t kHelpBytes = (size_t)kMaxBatch * 24 + 64;
-static_assert(sizeof(DevHints) == 24 && kHelpBytes >= (size_t)kMaxBatch * 8 + 32, "help region");
+// FEAT 0: the builder wave's descriptors, counts and ready mask
+constexpr size_t kHelpBytes = (size_t)kMaxBatch * 8 + 16 + 16;
+// NUMA policies + DeviceShare (the commit's LDS holds both slot caches): the helper waves' per-slot DevHints, four
+// DeviceShare Filter / Score variants per slot (DevVar) and the request words
+struct DevVar {
+  uint32_t sel;  // bit 31: valid; GPU minors allowed in bits 0-7, RDMA minors in bits 8-15 (dev_allowed)
+  uint32_t reasons;
+  int32_t raw;
+  uint32_t _pad;
+};
+constexpr int kDevVars = 4;
+constexpr size_t kHelpHintBytes = (size_t)kMaxBatch * (24 + kDevVars * 16) + 64;
+static_assert(sizeof(DevHints) == 24 && sizeof(DevVar) == 16, "help region");
 
 struct CommitLayout {
   size_t rows, pods, res, raw, rawtop, rawrun, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, help,
@@ -483,7 +492,9 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   L.quota = o;
   if (qc) o += align16(quota_lds_bytes(qrows));
   L.help = o;
-  o += kHelpBytes;  // slot-row hand-off to the builder wave (FEAT 0): descriptors, issued count, done flag, ready mask
+  // slot-row hand-off to the builder wave (FEAT 0): descriptors, issued count, done flag, ready mask; with both the
+  // device and the NUMA slot caches, the helper waves' hints and DeviceShare variants
+  o += (dev_bytes && numa_bytes) ? kHelpHintBytes : kHelpBytes;
   L.touched = o;
   o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
   L.total = o;
@@ -742,9 +753,14 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   // NUMA topology policies + DeviceShare: wave 1 computes DeviceShare's topology hints of every touched slot for the
   // pod wave 0 is evaluating (lane = slot, the same dev_hints on the same LDS state), while wave 0 runs the other
   // plugins and the NodeNUMAResource hints; wave 0 takes them at the merge (numa_policy_eval's dhf)
+  // (waves 2 and 3 compute DeviceShare's Filter / Score of every touched slot under the restrictions an affinity can
+  // give: the device NUMA ids one by one, both, none -- wave 0 takes the one matching its merged affinity)
   constexpr bool HINTW = (FEAT & 12) == 12;
-  DevHints* shint = reinterpret_cast<DevHints*>(smem_raw + lay.help);                      // [slot]
-  int32_t* hw = reinterpret_cast<int32_t*>(smem_raw + lay.help + (size_t)kMaxBatch * 24);  // seq, pod, n, done, quit
+  const bool hintw = HINTW && a.dev_bytes != 0 && a.numa_bytes != 0;  // (the layout holds the helper region)
+  DevHints* shint = reinterpret_cast<DevHints*>(smem_raw + lay.help);                                // [slot]
+  DevVar* sdv = reinterpret_cast<DevVar*>(smem_raw + lay.help + (size_t)kMaxBatch * 24);             // [k][slot]
+  // seq, pod, n, done (wave 1), quit, done (wave 2), done (wave 3)
+  int32_t* hw = reinterpret_cast<int32_t*>(smem_raw + lay.help + (size_t)kMaxBatch * (24 + kDevVars * 16));
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
@@ -850,9 +866,9 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     *hdone = 0;
     *hready = 0ull;
   }
-  if (HINTW && tid < 5) hw[tid] = 0;
+  if (hintw && tid < 7) hw[tid] = 0;
   __syncthreads();
-  if (tid >= ((HELP || HINTW) ? 128 : 64)) return;  // the other waves are done; wave 0 runs the sequential loop
+  if (tid >= (HELP ? 128 : (hintw ? 256 : 64))) return;  // the other waves are done; wave 0 runs the sequential loop
   KS_STAMP(0);
   // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
   // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
@@ -940,7 +956,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     }
     return;
   }
-  if (HINTW && tid >= 64) {
+  if (hintw && tid >= 64) {
+    const int wv = tid >> 6;  // 1: hints, 2 / 3: DeviceShare variants 0-1 / 2-3
     // ---- wave 1: the hint wave (serves wave 0's requests in order until told to quit; an idle ~0.1 s, far
     // beyond any pass, also ends it: wave 0's wait is bounded the same way and then computes the hints itself) ----
     int32_t last = 0;
@@ -953,9 +970,33 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           PodRec pod = spods[jj];
           pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
           pod.rsv_class = __builtin_amdgcn_readfirstlane(pod.rsv_class);
-          shint[lane] = dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
+          const DevLView v{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+          if (wv == 1) {
+            shint[lane] = dev_hints(cfg, pod, v);
+          } else {
+            const uint32_t ids = v.present() ? dev_topo_ids(v) : 0u;
+            const uint32_t rest = ids & (ids - 1u);
+            const uint32_t m0 = ids ? (1u << __builtin_ctz(ids)) : 0u, m1 = rest ? (1u << __builtin_ctz(rest)) : 0u;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int k = 2 * (wv - 2) + q;
+              // the restrictions: {id0}, {id1}, {id0, id1} (with two ids), none
+              const uint32_t allow = k == 0 ? m0 : (k == 1 ? m1 : (k == 2 ? (m1 ? (m0 | m1) : 0u) : ~0u));
+              DevVar dv{0u, 0u, 0, 0u};
+              if (allow) {
+                uint32_t gin, rin;
+                dev_allowed(v, allow, gin, rin);
+                const DevOut d = dev_eval<false>(cfg, pod, v, nullptr, allow);
+                dv.sel = (1u << 31) | (gin & 0xFFu) | ((rin & 0xFFu) << 8);
+                dv.reasons = d.reasons;
+                dv.raw = d.raw;
+              }
+              sdv[k * kMaxBatch + lane] = dv;
+            }
+          }
         }
-        if (lane == 0) __hip_atomic_store(hw + 3, sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0)
+          __hip_atomic_store(hw + (wv == 1 ? 3 : (wv == 2 ? 5 : 6)), sq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         last = sq;
         idle = 0;
         continue;
@@ -1118,7 +1159,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
       wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
-      const bool use_hw = HINTW && cfg.dev && cfg.numa_pol && (pod.flags & kPodHasGpu) && !(pod.flags & kPodReqZero) &&
+      const bool use_hw = hintw && cfg.dev && cfg.numa_pol && (pod.flags & kPodHasGpu) && !(pod.flags & kPodReqZero) &&
                           nslots > 0;
       if (use_hw) {
         ++hseq;
@@ -1139,6 +1180,33 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           }
         }
         return dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
+      };
+      // the slot's DeviceShare Filter / Score under `allow`: a helper wave's variant with the same allowed minors (the
+      // result depends on the restriction only through them), else computed here
+      auto dff = [&](uint32_t allow) -> DevOut {
+        const DevLView v{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+        if (use_hw) {
+          uint32_t gin, rin;
+          dev_allowed(v, allow, gin, rin);
+          const uint32_t want = (1u << 31) | (gin & 0xFFu) | ((rin & 0xFFu) << 8);
+          bool ready = false;
+          for (uint32_t it = 0; it <= (1u << 22); ++it) {
+            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 5, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == hseq &&
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == hseq) {
+              ready = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (ready) {
+#pragma unroll
+            for (int k = 0; k < kDevVars; ++k) {
+              const DevVar dv = sdv[k * kMaxBatch + lane];
+              if (dv.sel == want) return DevOut{dv.reasons, dv.raw, 0u, 0u};
+            }
+          }
+        }
+        return dev_eval<false>(cfg, pod, v, nullptr, allow);
       };
 #ifdef KS_SLOT_SPLIT
       // diagnostic build (with KS_COMMIT_STAMPS): the slot evaluation's parts timed separately, each run once more on
@@ -1209,7 +1277,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
               return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
             },
             [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
-            [&]() { return NumaLView{snp + lane * kNumaSlotWords}; }, nullptr, dhf);
+            [&]() { return NumaLView{snp + lane * kNumaSlotWords}; }, nullptr, dhf, dff);
         if (DEV && cfg.stat) {
           o.reasons |= so.reasons;
           o.traw = so.traw;
@@ -1744,7 +1812,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 #endif
   }
   KS_STAMP(6);
-  if (HINTW && lane == 0) __hip_atomic_store(hw + 4, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (hintw && lane == 0) __hip_atomic_store(hw + 4, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (HELP) {
     if (lane == 0) __hip_atomic_store(hdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));

@@ -291,9 +291,12 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
 // view (ks_numa.h).  Filter order as in the profile: Fit, LoadAware, NodeNUMAResource (on a node with a NUMA
 // topology policy its topology-manager Admit, whose affinity then restricts DeviceShare), DeviceShare,
 // Reservation.  The key total is key_total(c, o, M) with M the pod's normalization maxima (NormM).
-template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, typename H, typename DHF = NoDevHints>
+// dhf / dff: DeviceShare's topology hints and its Filter / Score under a NUMA restriction from elsewhere (the commit
+// kernel's helper waves, ks_pass.h); NoDevHints = computed here.
+template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, typename H, typename DHF = NoDevHints,
+          typename DFF = NoDevHints>
 __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& devv,
-                                             H&& numav, RsvOut* info = nullptr, DHF dhf = DHF{}) {
+                                             H&& numav, RsvOut* info = nullptr, DHF dhf = DHF{}, DFF dff = DFF{}) {
   constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0, DEV = (FEAT & 4) != 0, POL = (FEAT & 8) != 0;
   const bool dev_pod = DEV && c.dev && (p.flags & kPodHasGpu);
   // NodeNUMAResource (policy None part, then the topology-manager path on a policy node); returns DeviceShare's
@@ -327,7 +330,13 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
   auto dev = [&](EvalOut& o, uint32_t allow) __attribute__((always_inline)) {
     if (!dev_pod) return;
     if (!DEBUG && o.reasons) return;
-    const DevOut d = dev_pre ? dpre : dev_eval<false>(c, p, devv(), nullptr, allow);
+    DevOut d;
+    if (dev_pre) {
+      d = dpre;
+    } else {
+      if constexpr (LateDevHints<DFF>::value) d = dff(allow);
+      else d = dev_eval<false>(c, p, devv(), nullptr, allow);
+    }
     o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
     o.dev_raw = d.raw;
     if (!DEBUG && dev_pol && d.reasons) {  // the deferred policy-path failure: no NUMA score (numa_policy_eval)
