@@ -3133,6 +3133,9 @@ static hipEvent_t take_event(ks_ctx* ctx, size_t i) {
 }
 
 static size_t dev_cache_bytes(const ks_ctx* ctx);
+static int kernel_feat(const ks_ctx* ctx);
+// the context's commit variant runs the helper waves (NUMA policies + DeviceShare compiled in, ks_pass.h)
+static bool commit_hint_variant(const ks_ctx* ctx) { return (kernel_feat(ctx) & 12) == 12; }
 static size_t numa_cache_bytes(const ks_ctx* ctx) {
   return ctx->kc.numa_pol ? (size_t)kMaxBatch * kNumaSlotWords * 8 : 0;
 }
@@ -3142,7 +3145,8 @@ static int kernel_feat(const ks_ctx* ctx);
 
 static bool commit_qcache(const ks_ctx* ctx) {
   if (!(ctx->kc.quota_enable && ctx->q.q > 0 && ctx->q.q <= kQuotaLdsRows)) return false;
-  return commit_layout(ctx->k, ctx->nchunks, true, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total <= 160 * 1024;
+  return commit_layout(ctx->k, ctx->nchunks, true, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0,
+                       commit_hint_variant(ctx)).total <= 160 * 1024;
 }
 
 // Kernel variant (FEAT bits, ks_pass.h): 1 Reservation, 2 NodeNUMAResource, 4 the normalized plugins (DeviceShare,
@@ -3174,7 +3178,7 @@ static size_t dev_cache_bytes_with(const ks_ctx* ctx, bool stat_lds) {
 static bool commit_stat_lds(const ks_ctx* ctx) {
   if (!ctx->kc.stat) return false;
   return commit_layout(ctx->k, ctx->nchunks, false, 0, dev_cache_bytes_with(ctx, true), numa_cache_bytes(ctx), ctx->q.q,
-                       kernel_feat(ctx) == 0).total + 64 <= 160 * 1024;
+                       kernel_feat(ctx) == 0, commit_hint_variant(ctx)).total + 64 <= 160 * 1024;
 }
 
 static size_t dev_cache_bytes(const ks_ctx* ctx) { return dev_cache_bytes_with(ctx, commit_stat_lds(ctx)); }
@@ -3189,7 +3193,8 @@ static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
   *qcache = commit_qcache(ctx);
   if (!ctx->kc.rsv) return 0;
   auto fit = [&](bool qc) {
-    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total + 64;
+    const size_t base = commit_layout(ctx->k, ctx->nchunks, qc, 0, dev_cache_bytes(ctx), numa_cache_bytes(ctx), ctx->q.q,
+                                      kernel_feat(ctx) == 0, commit_hint_variant(ctx)).total + 64;
     const size_t avail = base < 160 * 1024 ? 160 * 1024 - base : 0;
     return (int32_t)std::min<size_t>(8, avail / rsv_cache_bytes(ctx, 1));
   };
@@ -3276,7 +3281,7 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.top_reset = nullptr;
   ca.pre_rsv = nullptr;
   *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
-                        ctx->q.q, kernel_feat(ctx) == 0).total;
+                        ctx->q.q, kernel_feat(ctx) == 0, commit_hint_variant(ctx)).total;
   return ca;
 }
 
@@ -3307,7 +3312,7 @@ static int commit_attr_set(ks_ctx* ctx) {
   bool qcache = false;
   const int32_t rcap = commit_rcap(ctx, &qcache);
   const size_t smem = commit_layout(ctx->k, ctx->nchunks, qcache, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx),
-                                    numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0).total;
+                                    numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0, commit_hint_variant(ctx)).total;
   if (smem > 160 * 1024)
     KS_FAIL(ctx, KS_EUNSUPPORTED, "too many nodes for the commit kernel's LDS (%lld nodes, %zu B)", (long long)ctx->n, smem);
   hipError_t e = pass_launcher(kernel_feat(ctx), ctx->nsc).commit_attr(qcache, smem);

@@ -448,13 +448,16 @@ static_assert(sizeof(DevHints) == 24 && sizeof(DevVar) == 16, "help region");
 struct CommitLayout {
   size_t rows, pods, res, raw, rawtop, rawrun, pqreq, cand_t, cand_chunk, scls, snuma, srcnt, srec, sdev, snp, quota, help,
       touched, total;
+  bool hint;  // the helper waves' region is in the layout (the commit kernel runs them)
 };
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 
+// hint_ok: the variant runs the helper waves (NUMA policies + DeviceShare compiled in, (FEAT & 12) == 12)
 __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks, bool qc, size_t rsv_bytes = 0,
                                                       size_t dev_bytes = 0, size_t numa_bytes = 0,
-                                                      int32_t qrows = kQuotaLdsRows, bool run = false) {
+                                                      int32_t qrows = kQuotaLdsRows, bool run = false,
+                                                      bool hint_ok = false) {
   CommitLayout L;
   size_t o = 0;
   L.rows = o;
@@ -493,8 +496,9 @@ __host__ __device__ inline CommitLayout commit_layout(int32_t k, int64_t nchunks
   if (qc) o += align16(quota_lds_bytes(qrows));
   L.help = o;
   // slot-row hand-off to the builder wave (FEAT 0): descriptors, issued count, done flag, ready mask; with both the
-  // device and the NUMA slot caches, the helper waves' hints and DeviceShare variants
-  o += (dev_bytes && numa_bytes) ? kHelpHintBytes : kHelpBytes;
+  // device and the NUMA slot caches, the helper waves' hints and DeviceShare variants when they still fit the CU's LDS
+  L.hint = hint_ok && dev_bytes && numa_bytes && o + kHelpHintBytes + (size_t)nchunks * 8 <= (size_t)160 * 1024;
+  o += L.hint ? kHelpHintBytes : kHelpBytes;
   L.touched = o;
   o += (size_t)nchunks * 8;  // u64 per chunk: lanes touched in this pass
   L.total = o;
@@ -699,7 +703,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int32_t K = a.k;
   const CommitLayout lay = commit_layout(K, a.nchunks, QC, (size_t)a.rsv_bytes, (size_t)a.dev_bytes, (size_t)a.numa_bytes, a.q.q,
-                                         FEAT == 0);
+                                         FEAT == 0, (FEAT & 12) == 12);
   SlotRow* rows = reinterpret_cast<SlotRow*>(smem_raw + lay.rows);
   PodRec* spods = reinterpret_cast<PodRec*>(smem_raw + lay.pods);
   ks_result* sres = reinterpret_cast<ks_result*>(smem_raw + lay.res);
@@ -756,7 +760,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   // (waves 2 and 3 compute DeviceShare's Filter / Score of every touched slot under the restrictions an affinity can
   // give: the device NUMA ids one by one, both, none -- wave 0 takes the one matching its merged affinity)
   constexpr bool HINTW = (FEAT & 12) == 12;
-  const bool hintw = HINTW && a.dev_bytes != 0 && a.numa_bytes != 0;  // (the layout holds the helper region)
+  const bool hintw = HINTW && lay.hint;  // (the layout holds the helper region)
   DevHints* shint = reinterpret_cast<DevHints*>(smem_raw + lay.help);                                // [slot]
   DevVar* sdv = reinterpret_cast<DevVar*>(smem_raw + lay.help + (size_t)kMaxBatch * 24);             // [k][slot]
   // seq, pod, n, done (wave 1), quit, done (wave 2), done (wave 3)
@@ -1159,55 +1163,18 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
       wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
-      const bool use_hw = hintw && cfg.dev && cfg.numa_pol && (pod.flags & kPodHasGpu) && !(pod.flags & kPodReqZero) &&
-                          nslots > 0;
-      if (use_hw) {
-        ++hseq;
-        if (lane == 0) {
-          hw[1] = j;
-          hw[2] = nslots;
-          __hip_atomic_store(hw, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      bool use_hw = false;
+      if constexpr (HINTW) {
+        use_hw = hintw && cfg.dev && cfg.numa_pol && (pod.flags & kPodHasGpu) && !(pod.flags & kPodReqZero) && nslots > 0;
+        if (use_hw) {
+          ++hseq;
+          if (lane == 0) {
+            hw[1] = j;
+            hw[2] = nslots;
+            __hip_atomic_store(hw, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
         }
       }
-      // the slot's DeviceShare hints: the hint wave's (use_hw), else computed here
-      auto dhf = [&]() -> DevHints {
-        if (use_hw) {
-          for (uint32_t it = 0; it <= (1u << 22); ++it) {
-            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
-                hseq)
-              return shint[lane];
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        return dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
-      };
-      // the slot's DeviceShare Filter / Score under `allow`: a helper wave's variant with the same allowed minors (the
-      // result depends on the restriction only through them), else computed here
-      auto dff = [&](uint32_t allow) -> DevOut {
-        const DevLView v{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
-        if (use_hw) {
-          uint32_t gin, rin;
-          dev_allowed(v, allow, gin, rin);
-          const uint32_t want = (1u << 31) | (gin & 0xFFu) | ((rin & 0xFFu) << 8);
-          bool ready = false;
-          for (uint32_t it = 0; it <= (1u << 22); ++it) {
-            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 5, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == hseq &&
-                __builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == hseq) {
-              ready = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          if (ready) {
-#pragma unroll
-            for (int k = 0; k < kDevVars; ++k) {
-              const DevVar dv = sdv[k * kMaxBatch + lane];
-              if (dv.sel == want) return DevOut{dv.reasons, dv.raw, 0u, 0u};
-            }
-          }
-        }
-        return dev_eval<false>(cfg, pod, v, nullptr, allow);
-      };
 #ifdef KS_SLOT_SPLIT
       // diagnostic build (with KS_COMMIT_STAMPS): the slot evaluation's parts timed separately, each run once more on
       // the same slots ahead of the real evaluation; cycles in diag[0] Fit / LoadAware / NUMA policy None,
@@ -1269,15 +1236,57 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           cw = (uint32_t)((uint64_t)snuma[4 * lane + 3] >> 32);
           r.cpu_cores = (cw & kCoresDirty) ? (cw | kCoresCount | (kCoresCount << kCoresAnyShift)) : cw;
         }
-        o = eval_full<NSC, false, false, FEAT>(
-            cfg, pod, r,
-            [&](RsvDelta<NSC>& dl) {
-              const int32_t c = srcnt[lane];
-              if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
-              return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
-            },
-            [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; },
-            [&]() { return NumaLView{snp + lane * kNumaSlotWords}; }, nullptr, dhf, dff);
+        auto rsvf = [&](RsvDelta<NSC>& dl) {
+          const int32_t c = srcnt[lane];
+          if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
+          return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
+        };
+        auto devf = [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; };
+        auto numaf = [&]() { return NumaLView{snp + lane * kNumaSlotWords}; };
+        if constexpr (HINTW) {
+          // the slot's DeviceShare hints: the hint wave's (use_hw), else computed here
+          auto dhf = [&]() -> DevHints {
+            if (use_hw) {
+              for (uint32_t it = 0; it <= (1u << 22); ++it) {
+                if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+                    hseq)
+                  return shint[lane];
+                __builtin_amdgcn_s_sleep(1);
+              }
+            }
+            return dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
+          };
+          // the slot's DeviceShare Filter / Score under `allow`: a helper wave's variant with the same allowed minors (the
+          // result depends on the restriction only through them), else computed here
+          auto dff = [&](uint32_t allow) -> DevOut {
+            const DevLView v{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+            if (use_hw) {
+              uint32_t gin, rin;
+              dev_allowed(v, allow, gin, rin);
+              const uint32_t want = (1u << 31) | (gin & 0xFFu) | ((rin & 0xFFu) << 8);
+              bool ready = false;
+              for (uint32_t it = 0; it <= (1u << 22); ++it) {
+                if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 5, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == hseq &&
+                    __builtin_amdgcn_readfirstlane(__hip_atomic_load(hw + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == hseq) {
+                  ready = true;
+                  break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+              if (ready) {
+    #pragma unroll
+                for (int k = 0; k < kDevVars; ++k) {
+                  const DevVar dv = sdv[k * kMaxBatch + lane];
+                  if (dv.sel == want) return DevOut{dv.reasons, dv.raw, 0u, 0u};
+                }
+              }
+            }
+            return dev_eval<false>(cfg, pod, v, nullptr, allow);
+          };
+          o = eval_full<NSC, false, false, FEAT>(cfg, pod, r, rsvf, devf, numaf, nullptr, dhf, dff);
+        } else {
+          o = eval_full<NSC, false, false, FEAT>(cfg, pod, r, rsvf, devf, numaf);
+        }
         if (DEV && cfg.stat) {
           o.reasons |= so.reasons;
           o.traw = so.traw;
