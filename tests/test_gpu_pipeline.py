@@ -147,3 +147,20 @@ def test_c5_prefix_automatic_mode(runtime, oracle_lib):
     assert_same_results(got, orc.schedule(w.pods), "C5 prefix")
     assert_same_state(state, orc.read_nodes(), "C5 prefix")
     orc.close()
+
+
+def test_c5_16k_pods_automatic_mode(runtime, oracle_lib):
+    """100k nodes, 16,384 pods (256 pipelined passes with patched candidate lists, each pass's speculative sweep
+    checked against the commit it overlapped): bit-exact placements and node state against the oracle (16 threads,
+    ~10 s)."""
+    w = synth.c5(n_pods=16_384, seed=77)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy())
+    got = ev.schedule(w.pods)
+    st = ev.stats()
+    state = ev.read_nodes()
+    ev.close()
+    assert st["pipelined"] == 2 and st["passes"] >= 256
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), nthreads=16)
+    assert_same_results(got, orc.schedule(w.pods), "C5 16k")
+    assert_same_state(state, orc.read_nodes(), "C5 16k")
+    orc.close()
