@@ -184,6 +184,7 @@ def cpu_baseline(w, gpu_res, budget_s: float, extra_budget_s: float):
         "unit": "pods/s",
         "cores": 16,
         "kind": "port",
+        "sample_short": f"first {n16} of {w.pods.n} pods, same inputs; C restatement, 16-worker Parallelizer",
         "sample": f"first {n16} of {w.pods.n} pods of {w.name} ({w.nodes.n} nodes), same inputs as the GPU run; "
                   f"CPU restatement with the reference Parallelizer shape (16 workers, chunk=min(sqrt(n),n/16+1)); "
                   f"omits Go map/Quantity/lister overheads, so it is a faster-than-reference baseline",
@@ -325,42 +326,53 @@ def run_config(w, args, dist, world: int, rank: int, local_rank: int, shard: boo
         "roofline": None,
     }
     if profile and agg["sweep_launches"]:
-        avg_s = agg["sweep_ms"] / agg["sweep_launches"] / 1000.0
-        local_nodes = n_nodes // nshards  # one rank sweeps its shard
-        algo = sweep_algo_bytes(w, prof, local_nodes)
-        achieved = algo / avg_s / 1e9
-        traffic, traffic_src = pmc_traffic(cfg_key, "sweep_kernel")
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "sweep_kernel", "avg_launch_us": round(avg_s * 1e6, 3),
-                "algorithmic_bytes_per_launch": algo, "bytes_incl_pod_group_rereads": sweep_bytes}
-        floor_us, valu_src = pmc_valu(cfg_key, "sweep_kernel")
-        if floor_us is not None and world == 1:
-            # the sweep's instruction-issue bound next to the HBM one
-            roof["valu_issue"] = {"floor_us": round(floor_us, 3), "frac": round(floor_us / (avg_s * 1e6), 4),
-                                  "source": valu_src}
-        # the sequential commit kernel (one launch per pass): SURVEY §8(d) counts its traffic as P x B_node
-        passes = max(agg["passes"], 1)
-        commit_s = agg["commit_ms"] / 1000.0
-        pods_per_launch = n_pods * steps / passes
-        c_algo = int(round(pods_per_launch * 138))
-        # Fit + LoadAware without ElasticQuota / Reservation / NUMA / DeviceShare: the monotone commit kernel
-        # (ks_mono.h, fast-pod runs); otherwise the general one (koordgpu.hip mono_commit)
-        mono = all(x is None for x in (w.quotas, w.reservations, w.devices, w.cpus, w.numa_nodes))
-        c_kernel = "commit_mono_kernel" if mono else "commit_kernel"
-        c_traffic, c_src = pmc_traffic(cfg_key, c_kernel)
-        step_kernels = agg["sweep_ms"] + agg["select_ms"] + agg["commit_ms"]
-        roof["commit"] = {
-            "kernel": c_kernel, "bound": "latency (one wave walks the pass's pods in queue order)",
-            "avg_launch_us": round(commit_s / passes * 1e6, 3), "pods_per_launch": round(pods_per_launch, 2),
-            "cycles_per_pod": round(commit_s * GPU_CLOCK_GHZ * 1e9 / (n_pods * steps), 1),
-            "share_of_kernel_time": round(agg["commit_ms"] / step_kernels, 4) if step_kernels else None,
-            "algorithmic_bytes_per_launch": c_algo, "traffic": c_traffic, "traffic_source": c_src,
-            "traffic_over_algorithmic": round(c_traffic / c_algo, 2) if c_traffic else None,
-            "achieved_gbs": round(c_algo / (commit_s / passes) / 1e9, 3),
-        }
-        rec["roofline"] = roof
+        rec["roofline"] = pass_roofline(w, prof, cfg_key, agg, steps, n_pods, n_nodes // nshards, sweep_bytes,
+                                        args.candidates or 32, world)
     return rec, res
+
+
+def pass_roofline(w, prof, cfg_key: str, agg: dict, steps: int, n_pods: int, local_nodes: int, sweep_bytes: int,
+                  cands: int, world: int) -> dict:
+    """achieved = B_pass_total / t_kernels over one scheduling pass (a batch of <= 64 pods):
+    B_pass_total = the sweep's algorithmic bytes (N x B_node + the pass's pod records + the chunk maxima) + the
+    select's candidate lists (P x K x 16 B) + the commit's P x B_node (138 B: SURVEY's 106 B + the two batch scalar
+    columns); t_kernels = (sweep + select + commit kernel time) / passes, from per-kernel HIP events of the profiled
+    steps.  The same figure reproduces from rocprofv3's kernel statistics (profiles/rNN_<config>_kernel_stats.csv):
+    B_pass_total / (avg sweep x sweep launches/pass + avg select + avg commit).  `sweep_*` is the sweep kernel alone,
+    `commit_*` the sequential commit (the kernel that bounds the step)."""
+    passes = max(agg["passes"], 1)
+    sweep_s = agg["sweep_ms"] / agg["sweep_launches"] / 1000.0
+    sweep_algo = sweep_algo_bytes(w, prof, local_nodes)
+    pods_per_pass = n_pods * steps / passes
+    commit_algo = int(round(pods_per_pass * 138))
+    select_algo = int(round(pods_per_pass * cands * 16))
+    launches_per_pass = agg["sweep_launches"] / passes  # two-phase sweeps (DeviceShare, normalizing plugins): 2
+    b_pass = int(round(sweep_algo * launches_per_pass)) + select_algo + commit_algo
+    # (+ the pipelined passes' list re-evaluation, a sweep_kernel launch in list mode on the commit stream)
+    t_pass = (agg["sweep_ms"] + agg["select_ms"] + agg["commit_ms"] + agg["fixup_ms"]) / 1000.0 / passes
+    achieved = b_pass / t_pass / 1e9
+    mono = all(x is None for x in (w.quotas, w.reservations, w.devices, w.cpus, w.numa_nodes))
+    c_kernel = "commit_mono_kernel" if mono else "commit_kernel"
+    tr_sweep, src = pmc_traffic(cfg_key, "sweep_kernel")
+    tr_sel, _ = pmc_traffic(cfg_key, "select_kernel")
+    tr_com, _ = pmc_traffic(cfg_key, c_kernel)
+    traffic = (int(round(tr_sweep * launches_per_pass)) + tr_sel + tr_com
+               if None not in (tr_sweep, tr_sel, tr_com) else None)
+    commit_s = agg["commit_ms"] / 1000.0 / passes
+    roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 7), "traffic": traffic,
+            "kernel": "pass (sweep+select+commit)", "bytes_per_pass": b_pass, "us_per_pass": round(t_pass * 1e6, 2),
+            "sweep_frac": round(sweep_algo / sweep_s / 1e9 / HBM_PEAK_GBS, 5), "sweep_us": round(sweep_s * 1e6, 2),
+            "sweep_bytes": sweep_algo, "sweep_traffic": tr_sweep,
+            "commit_us": round(commit_s * 1e6, 2), "commit_kernel": c_kernel,
+            "commit_share": round(agg["commit_ms"] / (agg["sweep_ms"] + agg["select_ms"] + agg["commit_ms"]), 4),
+            "commit_cycles_per_pod": round(agg["commit_ms"] / 1000.0 * GPU_CLOCK_GHZ * 1e9 / (n_pods * steps), 1),
+            "commit_traffic": tr_com, "traffic_source": src}
+    floor_us, _ = pmc_valu(cfg_key, "sweep_kernel")
+    if floor_us is not None and world == 1:
+        # the sweep's instruction-issue bound next to the HBM one (DESIGN.md §4)
+        roof["sweep_valu_issue_frac"] = round(floor_us / (sweep_s * 1e6), 4)
+    return roof
 
 
 def run_preempt(args, steps: int, warmup: int, profile: bool, cpu: bool):
@@ -475,13 +487,15 @@ def main():
     ap.add_argument("--vshards", type=int, default=1, help="virtual shards per GPU (exercises the merge on one GPU)")
     ap.add_argument("--no-c5", action="store_true", help="skip the 100k-node c5 record")
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
-    ap.add_argument("--c5-steps", type=int, default=1)
+    ap.add_argument("--c5-steps", type=int, default=3)
     ap.add_argument("--c5-warmup", type=int, default=1)
     ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d sub-records")
     ap.add_argument("--sub-steps", type=int, default=3)
     ap.add_argument("--sub-warmup", type=int, default=1)
     ap.add_argument("--no-preempt", action="store_true", help="skip the preempt (ElasticQuota PostFilter) record")
     ap.add_argument("--preempt-pods", type=int, default=128)
+    ap.add_argument("--detail", default="", help="also write every record in full (kernel split, per-thread CPU "
+                    "baselines, roofline parts) to this JSON file; the printed line is the compact form")
     ap.add_argument("--preempt-only", action="store_true",
                     help="print only the preempt record (profiling runs of the PostFilter kernels, tools/pmc_traffic.sh)")
     args = ap.parse_args()
@@ -587,7 +601,54 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     if out is not None:
-        print(json.dumps(out), flush=True)
+        if args.detail:
+            with open(args.detail, "w") as f:
+                json.dump(out, f, indent=1)
+        print(json.dumps(compact_line(out), separators=(",", ":")), flush=True)
+
+
+SUB_KEYS = ("value", "unit", "ms_per_step", "steps", "warmup", "nodes", "pods_per_step", "node_evals_per_s", "scaling",
+            "parallelism", "passes_per_step", "pipelined", "parity", "speedup_vs_cpu_baseline", "preemptors_per_step",
+            "us_per_preemption")
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "sweep_frac", "commit_us", "commit_share", "kernel",
+             "avg_launch_us")
+
+
+def compact_roof(r):
+    return {k: r[k] for k in ROOF_KEYS if k in r} if r else None
+
+
+def compact_cpu(cb):
+    if not cb:
+        return cb
+    return {"value": cb["value"], "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+            "sample": cb.get("sample_short", cb.get("sample", ""))[:90]}
+
+
+def compact_line(out: dict) -> dict:
+    """The printed line: the contract's keys, a flat roofline (SURVEY §8(d) pass figure + the sweep / commit parts), a
+    short cpu_baseline, one short record per sub-workload, and c5 (the metric's 100k-node half) LAST, so a reader
+    holding only the line's tail (the driver keeps ~2 KB) still sees its value, roofline, CPU baseline and parity."""
+    head = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: out[k] for k in head}
+    cfg = dict(out["config"])
+    cfg["workload"] = cfg["workload"][:160]
+    line["config"] = cfg
+    line["roofline"] = compact_roof(out.get("roofline"))
+    line["cpu_baseline"] = compact_cpu(out.get("cpu_baseline"))
+    for k in ("parity", "speedup_vs_cpu_baseline", "node_evals_per_s", "passes_per_step", "pipelined"):
+        if k in out:
+            line[k] = out[k]
+    subs = [k for k in out if isinstance(out[k], dict) and k not in head + ("config", "roofline", "cpu_baseline",
+                                                                                 "kernel_ms_per_step", "c5")]
+    for k in subs + (["c5"] if "c5" in out else []):
+        r = out[k]
+        c = {kk: r[kk] for kk in SUB_KEYS if kk in r}
+        c["roofline"] = compact_roof(r.get("roofline"))
+        c["cpu_baseline"] = compact_cpu(r.get("cpu_baseline"))
+        line[k] = c
+    return line
 
 
 if __name__ == "__main__":

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 6
+#define KS_ABI_VERSION 7
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -607,7 +607,11 @@ typedef struct ks_stats {
  * NodeInfo.Pods of every node, the victims pool of the dry runs (one row per running pod; rows of a node in any
  * order).  The host resolves each pod's quota (getPodAssociateQuotaName, elasticquota/plugin_helper.go:41-61) to a
  * quota row of ks_load_quotas and its PodDisruptionBudget (filterPodsWithPDBViolation's namespace + selector match,
- * preempt.go:222-265; pods listed in the PDB's DisruptedPods get -1) to an index of ks_load_node_pods' pdb_allowed. */
+ * preempt.go:222-265) to indices of ks_load_node_pods' pdb_allowed: every PDB whose namespace and selector match and whose
+ * DisruptedPods does not list the pod, in any order (`pdb`, then `pdb_more[k]`; -1 = none; an index listed twice for
+ * one pod is KS_EINVAL).  The shim keeps the reference PostFilter when some pod matches more than 1 + KS_NPOD_MORE_PDBS
+ * budgets. */
+#define KS_NPOD_MORE_PDBS 3
 #define KS_NPOD_NONPREEMPTIBLE 0x1u /* extension.IsPodNonPreemptible: never a victim (preempt.go:284-287) */
 #define KS_NPOD_IN_QUOTA 0x2u       /* quotaInfo.IsPodExist (the pod is in its quota's PodCache): the dry run's
                                        quota used follows its removal / re-add (elasticquota/plugin.go:263-301) */
@@ -625,6 +629,7 @@ typedef struct ks_node_pod_cols {
   const int64_t *req_ephemeral;
   const int64_t *req_scalar[KS_MAX_SCALARS]; /* NULL = 0 */
   const int64_t *quota_req[KS_QUOTA_DIMS];   /* core.PodRequestsAndLimits requests per quota dimension; NULL = 0 */
+  const int32_t *pdb_more[KS_NPOD_MORE_PDBS]; /* further matching PDB indices of the pod, -1 = none; NULL = none */
 } ks_node_pod_cols;
 
 /* ks_preempt result (upstream preemption.Evaluator.Preempt, k8s v1.24 framework/preemption/preemption.go, driven by the
@@ -849,6 +854,11 @@ int ks_preempt(ks_ctx *ctx, const ks_pod_cols *pod, int32_t priority, uint32_t f
                uint8_t *node_status);
 
 int ks_shard_unique_id(uint8_t *out /* KS_SHARD_ID_BYTES */);
+/* Node sharding over nranks processes (one per GPU): this rank sweeps its chunk range as virtual_shards
+ * shards; the per-shard candidates are exchanged by one ncclAllGather per pass and the normalization maxima by one
+ * ncclAllReduce(max), on an RCCL communicator made from rank 0's ks_shard_unique_id.  nranks == 1 with a unique id
+ * makes a one-rank communicator, so the RCCL exchange calls run on a single GPU (with virtual_shards > 1); nranks == 1
+ * without one shards virtually with no exchange. */
 int ks_shard_init(ks_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t *unique_id, int32_t virtual_shards);
 /* Test transport for the nranks > 1 path without RCCL: ctxs[0..nranks) (contexts of this process, each loaded with the
  * same node table, batch and candidate count) become ranks 0..nranks-1 of one sharded group whose candidate allgather

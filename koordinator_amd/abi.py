@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 6
+KS_ABI_VERSION = 7
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
@@ -495,6 +495,7 @@ KS_PN_NO_VICTIMS = 2
 KS_PN_FILTER = 3
 KS_PN_ERROR = 4
 KS_PREEMPT_NEVER = 0x1
+KS_NPOD_MORE_PDBS = 3
 
 
 class KsNodePodCols(C.Structure):
@@ -510,6 +511,7 @@ class KsNodePodCols(C.Structure):
         ("req_ephemeral", P64),
         ("req_scalar", P64 * KS_MAX_SCALARS),
         ("quota_req", P64 * KS_QUOTA_DIMS),
+        ("pdb_more", P32 * KS_NPOD_MORE_PDBS),
     ]
 
 

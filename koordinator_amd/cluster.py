@@ -528,13 +528,15 @@ class NodePodTable:
         self.flags = np.full(self.m, abi.KS_NPOD_IN_QUOTA, np.uint32)
         self.quota = np.full(self.m, -1, np.int32)
         self.pdb = np.full(self.m, -1, np.int32)
+        # further PodDisruptionBudgets the pod matches ([k][row], -1 = none; ks_node_pod_cols.pdb_more)
+        self.pdb_more = np.full((abi.KS_NPOD_MORE_PDBS, self.m), -1, np.int32)
         self.req = np.zeros((abi.KS_RSV_DIMS, self.m), np.int64)
         self.quota_req = np.zeros((abi.KS_QUOTA_DIMS, self.m), np.int64)
         self.pdb_allowed = np.zeros(int(npdb), np.int32)
 
     def copy(self) -> "NodePodTable":
         t = NodePodTable(self.m, len(self.pdb_allowed))
-        for k in ("node", "priority", "start_time", "flags", "quota", "pdb", "req", "quota_req", "pdb_allowed"):
+        for k in ("node", "priority", "start_time", "flags", "quota", "pdb", "pdb_more", "req", "quota_req", "pdb_allowed"):
             setattr(t, k, getattr(self, k).copy())
         return t
 
@@ -545,14 +547,15 @@ class NodePodTable:
             setattr(t, k, getattr(self, k)[idx].copy())
         t.req = self.req[:, idx].copy()
         t.quota_req = self.quota_req[:, idx].copy()
+        t.pdb_more = self.pdb_more[:, idx].copy()
         t.pdb_allowed = self.pdb_allowed.copy()
         return t
 
     def ks(self) -> abi.KsNodePodCols:
         c = abi.KsNodePodCols()
         for name, dt in (("node", np.int32), ("priority", np.int32), ("start_time", np.int64), ("flags", np.uint32),
-                         ("quota", np.int32), ("pdb", np.int32), ("req", np.int64), ("quota_req", np.int64),
-                         ("pdb_allowed", np.int32)):
+                         ("quota", np.int32), ("pdb", np.int32), ("pdb_more", np.int32), ("req", np.int64),
+                         ("quota_req", np.int64), ("pdb_allowed", np.int32)):
             setattr(self, name, np.ascontiguousarray(getattr(self, name), dt))
         c.node = _p32(self.node)
         c.priority = _p32(self.priority)
@@ -567,6 +570,8 @@ class NodePodTable:
             c.req_scalar[k] = _p64(self.req[3 + k])
         for d in range(abi.KS_QUOTA_DIMS):
             c.quota_req[d] = _p64(self.quota_req[d])
+        for k in range(abi.KS_NPOD_MORE_PDBS):
+            c.pdb_more[k] = _p32(self.pdb_more[k])
         c._keep = self
         return c
 

@@ -1672,6 +1672,15 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   ctx->rsv_nrows = 0;
   ctx->rsv_live = 0;
   ctx->rmir = ks_ctx::RsvMirror{};
+  // the node-pod table (ks_load_node_pods) is indexed by the old node rows and its per-call scratch is sized to the
+  // old node count: drop it, so ks_preempt returns KS_ESTATE until it is reloaded for these nodes
+  dev_free(ctx->npod_blob);
+  ctx->npt = DevNodePods{};
+  ctx->pre_cand = nullptr;
+  ctx->pre_vrank = nullptr;
+  ctx->pre_status = nullptr;
+  ctx->pre_out = nullptr;
+  ctx->pre_victims = nullptr;
   ctx->n = n;
   ctx->nchunks = (n + 63) / 64;
   if (ctx->nchunks == 0) ctx->nchunks = 1;
@@ -3625,7 +3634,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     rec(0, ss);
     sweep(sweep_blocks, ss);
     rec(0, ss);
-    if (ctx->nranks > 1)
+    if (ctx->comm || ctx->loop)
       if (int rc = exchange_allreduce_max(ctx, ctx->dev_M, kNormRows * kMaxBatch, ss); rc != KS_OK) return rc;
     sa.phase = 1;
     rec(0, ss);
@@ -3705,7 +3714,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(kSelThreads), select_smem(se.c1 - se.c0), ss, se);
   }
   if (S > 1) {
-    if (ctx->nranks > 1)  // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
+    if (ctx->comm || ctx->loop)  // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
       if (int rc = exchange_allgather(ctx, (size_t)ctx->vshards * L.bytes, ss); rc != KS_OK) return rc;
     MergeArgs ma;
     ma.gather = ctx->gather;
@@ -4587,8 +4596,14 @@ int ks_load_node_pods(ks_ctx* ctx, const ks_node_pod_cols* pc, int64_t m, const 
   for (int64_t i = 0; i < m; ++i) {
     const int32_t nd = pc->node[i];
     if (nd < 0 || nd >= n) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: pod %lld on node %d outside [0, %lld)", (long long)i, nd, (long long)n);
-    const int32_t q = pc->pdb ? pc->pdb[i] : -1;
-    if (q < -1 || q >= npdb) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: pod %lld: PDB index %d outside [-1, %d)", (long long)i, q, npdb);
+    int32_t qs[kPreemptPdbs];
+    for (int k = 0; k < kPreemptPdbs; ++k) {
+      const int32_t* col = k == 0 ? pc->pdb : pc->pdb_more[k - 1];
+      const int32_t q = qs[k] = col ? col[i] : -1;
+      if (q < -1 || q >= npdb) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: pod %lld: PDB index %d outside [-1, %d)", (long long)i, q, npdb);
+      for (int k2 = 0; k2 < k; ++k2)
+        if (q >= 0 && qs[k2] == q) KS_FAIL(ctx, KS_EINVAL, "ks_load_node_pods: pod %lld lists PDB %d twice", (long long)i, q);
+    }
     ++beg[(size_t)nd + 1];
   }
   int32_t maxc = 0;
@@ -4622,7 +4637,7 @@ int ks_load_node_pods(ks_ctx* ctx, const ks_node_pod_cols* pc, int64_t m, const 
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off = align16(off + bytes); return o; };
   const size_t o_beg = take(nn * 8), o_prio = take(mm * 4), o_start = take(mm * 8), o_flags = take(mm * 4),
-               o_quota = take(mm * 4), o_pdb = take(mm * 4), o_row = take(mm * 4), o_req = take(mm * 8 * kRsvDims),
+               o_quota = take(mm * 4), o_pdb = take(mm * 4 * kPreemptPdbs), o_row = take(mm * 4), o_req = take(mm * 8 * kRsvDims),
                o_qreq = take(mm * 8 * KS_QUOTA_DIMS), o_pdba = take((size_t)std::max(npdb, 1) * 4),
                o_cand = take(nn * sizeof(PreemptCand)), o_vrank = take(mm * 4), o_status = take(nn),
                o_out = take(sizeof(PreemptOut)), o_vic = take((size_t)kPreemptMaxPods * 4);
@@ -4634,12 +4649,16 @@ int ks_load_node_pods(ks_ctx* ctx, const ks_node_pod_cols* pc, int64_t m, const 
     const int32_t pr = prio(i);
     const int64_t st = start(i);
     const uint32_t fl = pc->flags ? pc->flags[i] : KS_NPOD_IN_QUOTA;
-    const int32_t q = pc->quota ? pc->quota[i] : -1, pd = pc->pdb ? pc->pdb[i] : -1;
+    const int32_t q = pc->quota ? pc->quota[i] : -1;
     put(o_prio, pos, &pr, 4);
     put(o_start, pos, &st, 8);
     put(o_flags, pos, &fl, 4);
     put(o_quota, pos, &q, 4);
-    put(o_pdb, pos, &pd, 4);
+    for (int k = 0; k < kPreemptPdbs; ++k) {  // [k][m]
+      const int32_t* col = k == 0 ? pc->pdb : pc->pdb_more[k - 1];
+      const int32_t pd = col ? col[i] : -1;
+      put(o_pdb, (size_t)k * mm + pos, &pd, 4);
+    }
     put(o_row, pos, &i, 4);
     for (int dd = 0; dd < kRsvDims; ++dd) {
       const int64_t v = reqc[dd] ? reqc[dd][i] : 0;
@@ -4772,10 +4791,10 @@ int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t f
     (void)hipEventElapsedTime(&ms, e0, e2);
     ctx->stats.total_ms = ms;
   }
-  // algorithmic bytes of the dry-run launch: every node's pod positions (priority, start, flags, quota, PDB, 7 request
-  // and 8 quota-request words: 148 B) and node words (allocatable + requested x 7, pod count, allowed, LoadAware bits;
+  // algorithmic bytes of the dry-run launch: every node's pod positions (priority, start, flags, quota, 4 PDB, 7 request
+  // and 8 quota-request words: 160 B) and node words (allocatable + requested x 7, pod count, allowed, LoadAware bits;
   // the taint / label words with the dictionary plugins) once, the per-node outcome written
-  ctx->stats.sweep_bytes = ctx->npt.m * 148 + n * (int64_t)(7 * 16 + 12 + (ctx->kc.stat ? 16 : 0) + sizeof(PreemptCand) + 1);
+  ctx->stats.sweep_bytes = ctx->npt.m * 160 + n * (int64_t)(7 * 16 + 12 + (ctx->kc.stat ? 16 : 0) + sizeof(PreemptCand) + 1);
   out->node = o.node;
   out->status = o.status;
   out->num_victims = o.nvict;
@@ -4804,7 +4823,9 @@ int ks_shard_init(ks_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* uniq
     ctx->comm = nullptr;
   }
   loop_leave(ctx);
-  if (nranks > 1) {
+  if (nranks > 1 || unique_id) {
+    // (nranks == 1 with an id: a one-rank communicator, so the RCCL exchange calls run on one GPU -- the test of the
+    // production transport that needs no second GPU)
     ncclUniqueId id;
     memcpy(&id, unique_id, sizeof(id));
     const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);

@@ -11,8 +11,8 @@
 //                           potential victim is a wave sum (NodeInfo.Requested and the pod count go down, the quota used
 //                           goes down clamped at 0 -- SubtractWithNonNegativeResult of non-negative amounts, so the
 //                           order does not matter); the Filter plugins run once on that; the PDB split
-//                           (filterPodsWithPDBViolation :223-265) counts, per lane, the earlier potential victims of the
-//                           same budget with shuffles; the reprieve loop (:172-216) is wave-uniform over the victims in
+//                           (filterPodsWithPDBViolation :223-265) ranks, per budget, its members among the potential
+//                           victims with ballots (a pod may match several budgets); the reprieve loop (:172-216) is wave-uniform over the victims in
 //                           order, each step reading the pod's 15 request words from the lane that holds it.
 //   preempt_select_kernel   one workgroup: PodEligibleToPreemptOthers (:60-97) on the nominated node, the candidate
 //                           counts, the lexicographic minimum of pickOneNodeForPreemption's keys (fewest PDB violations,
@@ -34,6 +34,7 @@ __device__ __forceinline__ int64_t pre_sum_i64(int64_t v) {
 __device__ __forceinline__ int64_t pre_lane_i64(int64_t v, int l) { return (int64_t)readlane64((uint64_t)v, l); }
 
 constexpr int kPreemptMaxSlots = 4;               // positions per lane
+constexpr int kPreemptPdbs = 1 + KS_NPOD_MORE_PDBS;  // PodDisruptionBudgets one pod may match
 constexpr int kPreemptMaxPods = 64 * kPreemptMaxSlots;  // pods per node the dry run holds
 
 // NodeInfo.Pods of every node, positions in (node, MoreImportantPod, caller row) order (ks_load_node_pods)
@@ -43,7 +44,7 @@ struct DevNodePods {
   const int64_t* start;
   const uint32_t* flags;
   const int32_t* quota;
-  const int32_t* pdb;
+  const int32_t* pdb;   // [kPreemptPdbs][m], -1 = none
   const int32_t* row;   // caller row
   const int64_t* req;   // [kRsvDims][m]: cpu, memory, ephemeral, scalar[k] (NodeInfo.Requested share)
   const int64_t* qreq;  // [KS_QUOTA_DIMS][m]
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(256) void preempt_dry_run_kernel(PreemptArgs a) {
   const int32_t Q = p.quota;
   // ---- the node's pods, canPreempt (preempt.go:283-294) ----
   bool canp[S], inq[S];
-  int32_t pdbv[S], prv[S];
+  int32_t pdbv[S][kPreemptPdbs], prv[S];
   int64_t stv[S], rq[S][kRsvDims], qq[S][KS_QUOTA_DIMS];
 #pragma unroll
   for (int s = 0; s < S; ++s) {
@@ -128,7 +129,8 @@ __global__ __launch_bounds__(256) void preempt_dry_run_kernel(PreemptArgs a) {
     const uint32_t f = ok ? gld(a.t.flags + pos) : KS_NPOD_NONPREEMPTIBLE;
     prv[s] = ok ? gld(a.t.prio + pos) : 0;
     stv[s] = ok ? gld(a.t.start + pos) : 0;
-    pdbv[s] = ok ? gld(a.t.pdb + pos) : -1;
+#pragma unroll
+    for (int k = 0; k < kPreemptPdbs; ++k) pdbv[s][k] = ok ? gld(a.t.pdb + (int64_t)k * a.t.m + pos) : -1;
     const int32_t vq = ok ? gld(a.t.quota + pos) : -1;
     canp[s] = ok && !(f & KS_NPOD_NONPREEMPTIBLE) && a.prio > prv[s] && vq == Q;
     inq[s] = (f & KS_NPOD_IN_QUOTA) != 0;
@@ -198,30 +200,41 @@ __global__ __launch_bounds__(256) void preempt_dry_run_kernel(PreemptArgs a) {
     finish();
     return;
   }
-  // ---- filterPodsWithPDBViolation: a budget is decremented by each potential victim in the sorted order ----
-  uint64_t vm[S];
+  // ---- filterPodsWithPDBViolation (preempt.go:222-265): each potential victim, in the sorted order, decrements every
+  // budget it matches; it violates when one of them goes below 0.  Wave-uniform over the distinct budgets the node's
+  // potential victims match: one ballot per (slot, list entry) gives a budget's members, and a member's rank among
+  // them (the decrements before its own) is the popcount of the members at earlier positions. ----
+  uint64_t vm[S], pend[S][kPreemptPdbs];
   bool viol[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) viol[s] = false;
-  bool any_pdb = false;
+  for (int s = 0; s < S; ++s) {
+    viol[s] = false;
 #pragma unroll
-  for (int s = 0; s < S; ++s) any_pdb |= __ballot(canp[s] && pdbv[s] >= 0 && pdbv[s] < a.t.npdb) != 0;
-  if (any_pdb) {
-    int32_t before[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) before[s] = 0;
-#pragma unroll
-    for (int s2 = 0; s2 < S; ++s2) {
-      for (int k = 0; k < 64; ++k) {
-        if (!((pm[s2] >> k) & 1ull)) continue;
-        const int32_t v = __shfl(pdbv[s2], k, 64);
-#pragma unroll
-        for (int s = 0; s < S; ++s) before[s] += (v == pdbv[s] && (s2 < s || (s2 == s && k < lane))) ? 1 : 0;
-      }
-    }
+    for (int k = 0; k < kPreemptPdbs; ++k) pend[s][k] = __ballot(canp[s] && pdbv[s][k] >= 0 && pdbv[s][k] < a.t.npdb);
+  }
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (;;) {
+    int32_t j = -1;  // the next budget (wave-uniform)
 #pragma unroll
     for (int s = 0; s < S; ++s)
-      viol[s] = canp[s] && pdbv[s] >= 0 && pdbv[s] < a.t.npdb && before[s] + 1 > gld(a.t.pdb_allowed + pdbv[s]);
+#pragma unroll
+      for (int k = 0; k < kPreemptPdbs; ++k)
+        if (j < 0 && pend[s][k]) j = __builtin_amdgcn_readlane(pdbv[s][k], (int)__builtin_ctzll(pend[s][k]));
+    if (j < 0) break;
+    const int32_t allowed = gld(a.t.pdb_allowed + j);
+    int32_t before = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      uint64_t mem = 0;
+#pragma unroll
+      for (int k = 0; k < kPreemptPdbs; ++k) {
+        const uint64_t mk = __ballot(canp[s] && pdbv[s][k] == j);
+        mem |= mk;
+        pend[s][k] &= ~mk;
+      }
+      if (((mem >> lane) & 1ull) && before + __popcll(mem & lt_mask) + 1 > allowed) viol[s] = true;
+      before += __popcll(mem);
+    }
   }
 #pragma unroll
   for (int s = 0; s < S; ++s) vm[s] = __ballot(viol[s]);

@@ -634,7 +634,7 @@ PRIORITIES = np.array([0, 100, 1000, 3000, 5000, 8000], np.int32)
 
 def make_node_pods(nodes: NodeTable, rng: np.random.Generator, n_quotas: int, per_node=(4, 40), n_pdb: int = 12,
                    pdb_frac: float = 0.15, nonpreemptible_frac: float = 0.08, terminating_frac: float = 0.02,
-                   out_of_quota_frac: float = 0.03):
+                   out_of_quota_frac: float = 0.03, multi_pdb_frac: float = 0.0):
     """Running pods on every node (make_pods' request distribution), with priorities, distinct start times, quotas,
     PDBs and flags.  The nodes' NodeInfo columns (Requested, NonZeroRequested, pod count) are set to the sums over their
     pods, so the table is the NodeInfo.Pods the columns were built from.  Returns (NodePodTable, per-quota used [dim][q])
@@ -657,6 +657,12 @@ def make_node_pods(nodes: NodeTable, rng: np.random.Generator, n_quotas: int, pe
     t.quota[:] = src.quota if n_quotas else -1
     t.pdb[:] = np.where(rng.random(m) < pdb_frac, rng.integers(0, max(n_pdb, 1), m), -1) if n_pdb else -1
     t.pdb_allowed[:] = rng.integers(0, 4, n_pdb)
+    if multi_pdb_frac > 0 and n_pdb > 1:
+        # pods matching several budgets (filterPodsWithPDBViolation decrements each): up to 1 + KS_NPOD_MORE_PDBS distinct
+        for i in np.nonzero((t.pdb >= 0) & (rng.random(m) < multi_pdb_frac))[0]:
+            k = int(rng.integers(1, min(n_pdb, 1 + abi.KS_NPOD_MORE_PDBS)))
+            extra = rng.permutation(np.setdiff1d(np.arange(n_pdb), [t.pdb[i]]))[:k]
+            t.pdb_more[:k, i] = extra
     t.req[0] = src.req_milli_cpu
     t.req[1] = src.req_memory
     t.req[2] = 0

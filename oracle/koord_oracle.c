@@ -2716,9 +2716,11 @@ int ko_read_quota_used(const ko_sched *s, int64_t *used) {
  * (priority, start time), the candidates map in pickOneNodeForPreemption -- the table order / the lowest node row
  * decides.
  */
+#define KO_PDBS (1 + KS_NPOD_MORE_PDBS)
 typedef struct ko_npods {
   int64_t m;
-  int32_t *node, *prio, *quota, *pdb;
+  int32_t *node, *prio, *quota;
+  int32_t *pdb;  /* [m][KO_PDBS]: every PDB the pod matches (-1 = none) */
   int64_t *start;
   uint32_t *flags;
   int64_t *req;  /* [m][KO_D] */
@@ -2743,7 +2745,7 @@ int ko_load_node_pods(ko_sched *s, const ks_node_pod_cols *pc, int64_t m, const 
   ko_npods *t = calloc(1, sizeof(*t));
   size_t mm = (size_t)(m > 0 ? m : 1);
   t->m = m;
-  t->node = malloc(mm * 4); t->prio = malloc(mm * 4); t->quota = malloc(mm * 4); t->pdb = malloc(mm * 4);
+  t->node = malloc(mm * 4); t->prio = malloc(mm * 4); t->quota = malloc(mm * 4); t->pdb = malloc(mm * 4 * KO_PDBS);
   t->start = malloc(mm * 8); t->flags = malloc(mm * 4);
   t->req = malloc(mm * KO_D * 8); t->qreq = malloc(mm * KS_QUOTA_DIMS * 8);
   t->beg = calloc((size_t)s->n + 1, 8); t->rows = malloc(mm * 4);
@@ -2755,7 +2757,10 @@ int ko_load_node_pods(ko_sched *s, const ks_node_pod_cols *pc, int64_t m, const 
     if (t->node[i] < 0 || t->node[i] >= s->n) { npods_free(s); s->npods = NULL; free(t); return -1; }
     t->prio[i] = pc->priority ? pc->priority[i] : 0;
     t->quota[i] = pc->quota ? pc->quota[i] : -1;
-    t->pdb[i] = pc->pdb ? pc->pdb[i] : -1;
+    for (int k = 0; k < KO_PDBS; k++) {
+      const int32_t *col = k == 0 ? pc->pdb : pc->pdb_more[k - 1];
+      t->pdb[i * KO_PDBS + k] = col ? col[i] : -1;
+    }
     t->start[i] = pc->start_time ? pc->start_time[i] : 0;
     t->flags[i] = pc->flags ? pc->flags[i] : KS_NPOD_IN_QUOTA;
     int64_t *r = t->req + i * KO_D;
@@ -2870,10 +2875,12 @@ static void select_victims_on_node(const ko_sched *s, const ko_pod *p, int32_t p
   for (int32_t i = 0; i < t->npdb; i++) allowed[i] = t->pdb_allowed[i];
   uint8_t *viol = calloc((size_t)npot, 1);
   for (int32_t i = 0; i < npot; i++) {
-    const int32_t q = t->pdb[pot[i]];
-    if (q < 0 || q >= t->npdb) continue;
-    allowed[q]--;
-    if (allowed[q] < 0) viol[i] = 1;
+    for (int k = 0; k < KO_PDBS; k++) { /* every matching PDB (preempt.go:232-257) */
+      const int32_t q = t->pdb[(size_t)pot[i] * KO_PDBS + k];
+      if (q < 0 || q >= t->npdb) continue;
+      allowed[q]--;
+      if (allowed[q] < 0) viol[i] = 1;
+    }
   }
   free(allowed);
   out->status = KS_PN_CANDIDATE;

@@ -132,3 +132,51 @@ def test_edge_inputs(runtime, oracle_lib):
     pods = synth.make_pods(6, rng, 8)
     compare(runtime, oracle_lib, profile(quota=True).to_ks_config(), nodes, q, t, pods,
             np.full(6, 9000, np.int32), "256 pods per node")
+
+
+def test_overlapping_budgets(runtime, oracle_lib):
+    """Pods matching 2-4 PodDisruptionBudgets (filterPodsWithPDBViolation decrements every matching budget, preempt.go
+    :232-257): the hand-worked case, then random nodes of 10-250 pods with tight budgets."""
+    cfg = profile(quota=True).to_ks_config()
+    nodes = hand.cluster(1)
+    specs = [(0, 100, 1, 1000, 0, abi.KS_NPOD_IN_QUOTA, 0), (0, 100, 2, 1000, 0, abi.KS_NPOD_IN_QUOTA, 0),
+             hand.BASE[2], hand.BASE[3]]
+    t = hand.running(nodes, specs, npdb=2, allowed=[1, 0])
+    t.pdb_more[0, 1] = 1
+    outs = compare(runtime, oracle_lib, cfg, nodes, hand.quotas(t), t, hand.preemptor(1500), [1000], "two budgets")
+    assert list(outs[0]["victims"]) == [1, 0] and outs[0]["num_pdb_violations"] == 1
+    for seed, per_node in ((41, (10, 60)), (42, (100, 250))):
+        rng = np.random.Generator(np.random.PCG64(seed))
+        nodes = synth.make_nodes(400, rng)
+        nodes.allowed_pods[:] = 256
+        t, used = synth.make_node_pods(nodes, rng, 4, per_node=per_node, n_pdb=9, pdb_frac=0.7, multi_pdb_frac=0.5)
+        t.pdb_allowed[:] = rng.integers(0, 6, 9)
+        assert (t.pdb_more[2] >= 0).any()
+        nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 2000, nodes.n), 1000)
+        q = synth.QuotaTable(4)
+        q.limit_mask[:] = 0xF
+        q.used[:] = used
+        q.limit[:] = used * 2
+        pods = synth.make_pods(10, rng, 4)
+        outs = compare(runtime, oracle_lib, cfg, nodes, q, t, pods, np.full(10, 9000, np.int32), f"multi-pdb {seed}")
+        assert any(o["num_pdb_violations"] > 0 for o in outs)
+
+
+def test_reloaded_nodes_drop_the_node_pod_table(runtime):
+    """ks_load_nodes invalidates the node-pod table (its rows and scratch belong to the old nodes): ks_preempt refuses
+    with KS_ESTATE until ks_load_node_pods runs again, then works at the new node count."""
+    w = synth.c2_preempt(seed=5, n_nodes=200, n_preemptors=2)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), w.quotas.copy())
+    try:
+        ev.load_node_pods(w.node_pods)
+        ev.preempt(w.preemptors.rows([0]), int(w.priority[0]))
+        big = synth.c2_preempt(seed=6, n_nodes=900, n_preemptors=2)
+        ev.load_nodes(big.nodes.copy())
+        with pytest.raises(runtime.KsError) as e:
+            ev.preempt(big.preemptors.rows([0]), int(big.priority[0]))
+        assert e.value.rc == abi.KS_ESTATE
+        ev.load_node_pods(big.node_pods)
+        r = ev.preempt(big.preemptors.rows([0]), int(big.priority[0]), node_status=True)
+        assert len(r["node_status"]) == 900
+    finally:
+        ev.close()

@@ -141,6 +141,27 @@ def test_pdb_budget_shared_in_sorted_order():
     assert list(r["victims"]) == [1]
 
 
+def test_pod_matching_two_budgets():
+    # filterPodsWithPDBViolation (preempt.go:232-257) loops over every PDB: each match decrements that budget, and the pod
+    # violates if any goes below 0.  Budget 0 allows 1 (p0, p1), budget 1 allows 0 (p1 only).
+    nodes = cluster(1)
+    specs = [(0, 100, 1, 1000, 0, abi.KS_NPOD_IN_QUOTA, 0), (0, 100, 2, 1000, 0, abi.KS_NPOD_IN_QUOTA, 0), BASE[2], BASE[3]]
+    t = running(nodes, specs, npdb=2, allowed=[1, 0])
+    t.pdb_more[0, 1] = 1
+    # sorted p0 (start 1), p1: budget 0 -> 0 after p0, -1 after p1; budget 1 -> -1 after p1.  Only p1 violates.  At 1500m
+    # p1 is reprieved first and does not fit (1000m free): a victim with a violation; then p0 likewise.
+    r = run(nodes, t, quotas(t), preemptor(1500), 1000)
+    assert list(r["victims"]) == [1, 0] and r["num_pdb_violations"] == 1
+    # p1 in budget 0's DisruptedPods (the shim drops budget 0 for it) but matching budget 1 (allowed 0): still violating
+    t.pdb[1], t.pdb_more[0, 1] = 1, -1
+    r = run(nodes, t, quotas(t), preemptor(1500), 1000)
+    assert list(r["victims"]) == [1, 0] and r["num_pdb_violations"] == 1
+    # budget 1 allows 1: nobody violates; sorted order p0 then p1, both victims, no violation
+    t.pdb_allowed[1] = 1
+    r = run(nodes, t, quotas(t), preemptor(1500), 1000)
+    assert list(r["victims"]) == [0, 1] and r["num_pdb_violations"] == 0
+
+
 def test_non_preemptible_and_other_quota_are_not_victims():
     nodes = cluster(1)
     specs = [(0, 100, 1, 1000, 0, abi.KS_NPOD_IN_QUOTA | abi.KS_NPOD_NONPREEMPTIBLE), (0, 100, 2, 1000, 1),

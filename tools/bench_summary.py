@@ -1,9 +1,12 @@
-"""One line per record of a bench.py JSON line: pods/s, ms per step, kernel split (tools/*.sh summaries)."""
+"""One line per record of a bench.py JSON line: pods/s, ms per step, parity, the §8(d) pass roofline fraction, the
+commit kernel's time per pass, the CPU baseline."""
 import json
 import sys
 
 d = json.load(open(sys.argv[1]))
-recs = [("main", d)] + [(k, d[k]) for k in ("c5", "c3", "c4", "c2d", "preempt", "c2_replicas") if isinstance(d.get(k), dict)]
+recs = [("main", d)] + [(k, v) for k, v in d.items() if isinstance(v, dict) and "value" in v]
 for name, r in recs:
-    print(name, r["value"], r.get("ms_per_step"), r.get("parity"), r.get("kernel_ms_per_step"),
-          (r.get("cpu_baseline") or {}).get("value"))
+    roof = r.get("roofline") or {}
+    print(name, r["value"], r.get("ms_per_step"), "parity", r.get("parity"), "frac", roof.get("frac"),
+          "sweep_frac", roof.get("sweep_frac"), "commit_us", roof.get("commit_us"),
+          "cpu", (r.get("cpu_baseline") or {}).get("value"))

@@ -9,10 +9,6 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 1; }
 tail -3 $OUT/smoke.log
-timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
-python3 -c "
-import json; d=json.load(open('$OUT/bench.json'))
-print('c2', d['value'], d['parity'], d['kernel_ms_per_step'], 'cpu', d['cpu_baseline']['value'])
-for c in ('c5', 'c3', 'c4'):
-    r=d[c]; print(c, r['value'], r['ms_per_step'], r['parity'], r['kernel_ms_per_step'], 'cpu', r['cpu_baseline']['value'])"
+timeout -k 10 900 python -u bench.py --detail $OUT/bench_detail.json > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+python3 tools/bench_summary.py $OUT/bench.json
 if [ "${PROFILES:-0}" = 1 ]; then bash tools/gpu_profiles.sh $(basename $OUT)/prof || exit 1; fi
