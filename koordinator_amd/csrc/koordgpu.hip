@@ -222,7 +222,9 @@ struct SelectArgs {
 };
 
 
-// One workgroup of four waves per pod.  The pod's row of chunk keys is staged in LDS once: every thread
+// One workgroup of four waves per pod.  The pod's column of chunk keys (the sweep output is chunk-major: its
+// coalesced side is the sweep's stores, and the 16 pods sharing a 128 B line are 16 workgroups of this launch, served by
+// L2) is staged in LDS once as a row: every thread
 // issues up to kSelUnroll independent loads before the first wait, so at C5 (1,563 chunks) the row arrives
 // in about one HBM round trip instead of one per 64 chunks (one wave walking the row was latency-bound:
 // 18.8 us per launch).  All four waves build an LDS histogram of the chunk scores; wave 0 finds the K-th
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   if (p >= np) return;
   const int32_t K = a.k;
   const int64_t nc = a.c1 - a.c0;  // LDS row index e <-> chunk c0 + e
-  const uint2* in = a.in + (size_t)p * a.nchunks + a.c0;
+  const uint2* in = a.in + (size_t)a.c0 * kMaxBatch + p;  // chunk-major sweep output: the pod's column, stride 64
   uint32_t* hist = reinterpret_cast<uint32_t*>(srow + nc);
   uint64_t* xw = reinterpret_cast<uint64_t*>(hist + kSelHistBins);  // [0..3] top, [4..7] cnt | hmax << 32, [8] t | need_eq << 32
   int32_t cnt = 0;
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
 #pragma unroll
     for (int u = 0; u < kSelUnroll; ++u) {
       const int64_t e = e0 + (int64_t)u * kSelThreads;
-      v[u] = e < nc ? in[e] : make_uint2(0u, 0u);
+      v[u] = e < nc ? in[(size_t)e * kMaxBatch] : make_uint2(0u, 0u);
     }
 #pragma unroll
     for (int u = 0; u < kSelUnroll; ++u) {

