@@ -1735,8 +1735,6 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (cores_refresh(ctx) != KS_OK) return KS_EHIP;
   dev_free(ctx->numa_blob);
   if (ctx->numa_policy_nodes > 0) {
-    if (ctx->cfg.reservation.enable)
-      KS_FAIL(ctx, KS_EUNSUPPORTED, "NUMA topology policies together with the Reservation plugin are not supported");
     if (numa_install(ctx, nullptr, nullptr, nullptr) != KS_OK) return KS_EHIP;
     ctx->kc.numa_pol = 1;
     ctx->kc.monotone = 0;  // a Reserve can move a node's best NUMA hint: keys are not monotone

@@ -6,6 +6,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ks_device.h"
 #include "ks_rsv.h"
 #include "ks_dev.h"
@@ -143,94 +145,102 @@ void sweep_kernel(SweepArgs a) {
     nitems = min(__builtin_amdgcn_readfirstlane(a.fix[0]), kMaxBatch);
   }
   const int64_t nwork = nitems * groups;
-  for (int64_t w = wave; w < nwork; w += nwaves) {
-    // (32-bit, with the divisor opaque per item: a hoisted reciprocal would be one more value live across the loop)
-    int32_t gdiv = groups;
-    asm volatile("" : "+s"(gdiv));
-    const int64_t lc = (int64_t)((uint32_t)w / (uint32_t)gdiv);  // chunk within this shard's range (or fix-list entry)
-    const int64_t c = a.fix ? (int64_t)(__builtin_amdgcn_readfirstlane(a.fix[1 + lc]) >> 6) : a.c0 + lc;
-    if (a.fix && (c < a.c0 || c >= a.c1)) continue;  // another shard's chunk
-    const int32_t g = (int32_t)(w - lc * groups);
-    const int64_t node = c * 64 + lane;
-    if ((FEAT & 4) && a.phase == 1 && a.dcache) {
+  // The work loop, instantiated separately for the full sweep and the re-sweep of a commit's chunks (FIX): a run-time
+  // flag tested inside the loop was kept in a VGPR across it and spilled to scratch at 4 waves per SIMD (one scratch
+  // write per wave, written back to HBM at the kernel's end: most of the launch's write traffic).
+  auto items = [&](auto fixc) __attribute__((always_inline)) {
+    constexpr bool FIX = decltype(fixc)::value;
+    for (int64_t w = wave; w < nwork; w += nwaves) {
+      // (32-bit, with the divisor opaque per item: a hoisted reciprocal would be one more value live across the loop)
+      int32_t gdiv = groups;
+      asm volatile("" : "+s"(gdiv));
+      const int64_t lc = (int64_t)((uint32_t)w / (uint32_t)gdiv);  // chunk within this shard's range (or fix-list entry)
+      const int64_t c = FIX ? (int64_t)(__builtin_amdgcn_readfirstlane(a.fix[1 + lc]) >> 6) : a.c0 + lc;
+      if (FIX && (c < a.c0 || c >= a.c1)) continue;  // another shard's chunk
+      const int32_t g = (int32_t)(w - lc * groups);
+      const int64_t node = c * 64 + lane;
+      if ((FEAT & 4) && a.phase == 1 && a.dcache) {
+        const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
+        uint32_t best = 0, second = 0;
+        for (int32_t p = p0; p < p1; ++p) {
+          const unsigned long long e = a.dcache[(size_t)p * a.dstride + node];
+          EvalOut o{};
+          o.total = (int32_t)(uint32_t)e;
+          o.dev_raw = (int32_t)((e >> 32) & 0xFFFFull);
+          const NormM M{(int32_t)(a.dev_M[p] >> 32), 0, 0};  // (no dcache with the dictionary-bit plugins)
+          const uint32_t key = (e >> 63) ? (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane)) : 0u;
+          const uint32_t m1 = wave_max_u32(key);
+          const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
+          best = (lane == p) ? m1 : best;
+          second = (lane == p) ? m2 : second;
+        }
+        if (lane >= p0 && lane < p1) a.out[(size_t)c * kMaxBatch + lane] = make_uint2(best, second);
+        continue;
+      }
+      NodeReg<NSC> r;
+      uint64_t st_hard = 0, st_soft = 0, st_lab = 0, st_port = 0;  // dictionary-bit plugin words (FEAT & 4 variants)
+      {
+        const DevNodes d = *a.dn;
+        load_node<NSC>(a.c, d, node, node < a.n, r);
+        if ((FEAT & 4) && a.c.stat && node < a.n) {
+          st_hard = gld(d.taints_hard + node);
+          st_soft = gld(d.taints_soft + node);
+          st_lab = gld(d.labels + node);
+          st_port = gld(d.host_ports + node);
+        }
+      }
       const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
       uint32_t best = 0, second = 0;
       for (int32_t p = p0; p < p1; ++p) {
-        const unsigned long long e = a.dcache[(size_t)p * a.dstride + node];
-        EvalOut o{};
-        o.total = (int32_t)(uint32_t)e;
-        o.dev_raw = (int32_t)((e >> 32) & 0xFFFFull);
-        const NormM M{(int32_t)(a.dev_M[p] >> 32), 0, 0};  // (no dcache with the dictionary-bit plugins)
-        const uint32_t key = (e >> 63) ? (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane)) : 0u;
+        const PodRec pod = load_pod_uniform(a.pods + cursor + p);
+        EvalOut o = eval_full<NSC, false, true, FEAT>(
+            a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+            [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
+        if ((FEAT & 4) && a.c.stat) stat_eval(a.c, load_stat_uniform(a.pstat + cursor + p), st_hard, st_soft, st_lab, st_port, o);
+        if ((FEAT & 4) && a.phase == 0) {
+          // normalization maxima over the feasible nodes, witness = lowest index holding each
+          const uint64_t wit = 0xFFFFFFFFull - (uint64_t)node;
+          const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | wit);
+          const uint64_t m = wave_max_u64(mk);
+          if (lane == 0 && m) atomicMax(a.dev_M + p, (unsigned long long)m);
+          if (a.c.stat) {
+            const uint64_t mt = wave_max_u64(o.reasons ? 0ull : (((uint64_t)(uint32_t)o.traw << 32) | wit));
+            const uint64_t ma = wave_max_u64(o.reasons ? 0ull : (((uint64_t)(uint32_t)o.araw << 32) | wit));
+            if (lane == 0 && mt) atomicMax(a.dev_M + kMaxBatch + p, (unsigned long long)mt);
+            if (lane == 0 && ma) atomicMax(a.dev_M + 2 * kMaxBatch + p, (unsigned long long)ma);
+          }
+          if (a.dcache)
+            a.dcache[(size_t)p * a.dstride + node] =
+                (node < a.n && !o.reasons) ? ((1ull << 63) | ((unsigned long long)(uint32_t)o.dev_raw << 32) | (uint32_t)o.total)
+                                           : 0ull;
+          continue;
+        }
+        NormM M{0, 0, 0};
+        if (FEAT & 4) {
+          M.dev = (int32_t)(a.dev_M[p] >> 32);
+          if (a.c.stat) {
+            M.taint = (int32_t)(a.dev_M[kMaxBatch + p] >> 32);
+            M.aff = (int32_t)(a.dev_M[2 * kMaxBatch + p] >> 32);
+          }
+        }
+        const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane));
         const uint32_t m1 = wave_max_u32(key);
         const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
         best = (lane == p) ? m1 : best;
         second = (lane == p) ? m2 : second;
       }
-      if (lane >= p0 && lane < p1) a.out[(size_t)c * kMaxBatch + lane] = make_uint2(best, second);
-      continue;
-    }
-    NodeReg<NSC> r;
-    uint64_t st_hard = 0, st_soft = 0, st_lab = 0, st_port = 0;  // dictionary-bit plugin words (FEAT & 4 variants)
-    {
-      const DevNodes d = *a.dn;
-      load_node<NSC>(a.c, d, node, node < a.n, r);
-      if ((FEAT & 4) && a.c.stat && node < a.n) {
-        st_hard = gld(d.taints_hard + node);
-        st_soft = gld(d.taints_soft + node);
-        st_lab = gld(d.labels + node);
-        st_port = gld(d.host_ports + node);
+      if ((FEAT & 4) && a.phase == 0) continue;
+      if (lane >= p0 && lane < p1) {
+        // (the lane's offset is rematerialised per work item: hoisted out of the loop it is one more value live across
+        // it, which at 4 waves per SIMD the compiler spills to scratch -- one scratch write per wave, in HBM traffic)
+        int32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        a.out[(size_t)c * kMaxBatch + ln] = make_uint2(best, second);
       }
     }
-    const int32_t p0 = g * a.ppw, p1 = min(np, p0 + a.ppw);
-    uint32_t best = 0, second = 0;
-    for (int32_t p = p0; p < p1; ++p) {
-      const PodRec pod = load_pod_uniform(a.pods + cursor + p);
-      EvalOut o = eval_full<NSC, false, true, FEAT>(
-          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
-          [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
-      if ((FEAT & 4) && a.c.stat) stat_eval(a.c, load_stat_uniform(a.pstat + cursor + p), st_hard, st_soft, st_lab, st_port, o);
-      if ((FEAT & 4) && a.phase == 0) {
-        // normalization maxima over the feasible nodes, witness = lowest index holding each
-        const uint64_t wit = 0xFFFFFFFFull - (uint64_t)node;
-        const uint64_t mk = o.reasons ? 0ull : (((uint64_t)(uint32_t)o.dev_raw << 32) | wit);
-        const uint64_t m = wave_max_u64(mk);
-        if (lane == 0 && m) atomicMax(a.dev_M + p, (unsigned long long)m);
-        if (a.c.stat) {
-          const uint64_t mt = wave_max_u64(o.reasons ? 0ull : (((uint64_t)(uint32_t)o.traw << 32) | wit));
-          const uint64_t ma = wave_max_u64(o.reasons ? 0ull : (((uint64_t)(uint32_t)o.araw << 32) | wit));
-          if (lane == 0 && mt) atomicMax(a.dev_M + kMaxBatch + p, (unsigned long long)mt);
-          if (lane == 0 && ma) atomicMax(a.dev_M + 2 * kMaxBatch + p, (unsigned long long)ma);
-        }
-        if (a.dcache)
-          a.dcache[(size_t)p * a.dstride + node] =
-              (node < a.n && !o.reasons) ? ((1ull << 63) | ((unsigned long long)(uint32_t)o.dev_raw << 32) | (uint32_t)o.total)
-                                         : 0ull;
-        continue;
-      }
-      NormM M{0, 0, 0};
-      if (FEAT & 4) {
-        M.dev = (int32_t)(a.dev_M[p] >> 32);
-        if (a.c.stat) {
-          M.taint = (int32_t)(a.dev_M[kMaxBatch + p] >> 32);
-          M.aff = (int32_t)(a.dev_M[2 * kMaxBatch + p] >> 32);
-        }
-      }
-      const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, M) + 1) << 6) | (uint32_t)(63 - lane));
-      const uint32_t m1 = wave_max_u32(key);
-      const uint32_t m2 = wave_max_u32(key == m1 ? 0u : key);
-      best = (lane == p) ? m1 : best;
-      second = (lane == p) ? m2 : second;
-    }
-    if ((FEAT & 4) && a.phase == 0) continue;
-    if (lane >= p0 && lane < p1) {
-      // (the lane's offset is rematerialised per work item: hoisted out of the loop it is one more value live across
-      // it, which at 4 waves per SIMD the compiler spills to scratch -- one scratch write per wave, in HBM traffic)
-      int32_t ln = lane;
-      asm volatile("" : "+v"(ln));
-      a.out[(size_t)c * kMaxBatch + ln] = make_uint2(best, second);
-    }
-  }
+  };
+  if (a.fix) items(std::true_type{});
+  else items(std::false_type{});
 }
 
 struct CandSlot {  // one shard's select output inside the gather buffer (byte offsets)
@@ -1559,13 +1569,17 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl);
       const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);  // view index
       if (ro.hi >= kRsvOrderBase) {
-        rsv_apply<NSC>(nr, dl, 1);
-        EvalOut e2 = eval_pod_node<NSC, false>(cfg, pod, nr);
-        if ((FEAT & 2) && cfg.numa) numa_eval<NSC, false>(cfg, pod, nr, e2);
-        if (DEV && cfg.dev && (pod.flags & kPodHasGpu)) {
-          const DevOut dd = dev_eval<false>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0});
-          e2.dev_raw = dd.raw;
-        }
+        // the whole Filter / Score of the slot with this restore (eval_full: on a node with a NUMA topology policy the
+        // score over the allocated NUMA nodes and DeviceShare under the admitted affinity, not the policy-None parts)
+        NodeReg<NSC> n2 = nr;
+        EvalOut e2 = eval_full<NSC, false, false, FEAT>(
+            cfg, pod, n2,
+            [&](RsvDelta<NSC>& d2) {
+              d2 = dl;
+              return ro;
+            },
+            [&]() { return DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}; },
+            [&]() { return NumaLView{snp + s * kNumaSlotWords}; });
         if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[4 * s], sstat[4 * s + 1], sstat[4 * s + 2], sstat[4 * s + 3], e2);
         fitla_pref = e2.total + norm_terms(cfg, e2, Muse);
       }

@@ -494,6 +494,24 @@ def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, policy_frac:
     return Workload("C3", prof, nodes, pods, None, None, devs, cpus, numa)
 
 
+def c3_rsv(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, rsv_per_node: float = 2.5,
+           policy_frac: float = 0.5, policy: int = abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE, **kw) -> Workload:
+    """The shipped koord-scheduler profile's plugin set (config/manager/scheduler-config.yaml:58-96: Reservation +
+    NodeNUMAResource + DeviceShare next to Fit + LoadAware): C3's nodes (NUMA topology policies, cpuset pods, GPU /
+    RDMA devices) with C4's reservations (~2.5 per node, 16 owner classes; their reserve pods in NodeInfo) and 60 % of
+    the pods in an owner class.  Reservations hold no cpuset and no device (nodenumaresource/reservation.go and
+    deviceshare/reservation.go then restore nothing)."""
+    w = c3(seed=seed, n_nodes=n_nodes, n_pods=n_pods, policy_frac=policy_frac, policy=policy, **kw)
+    rng = np.random.Generator(np.random.PCG64(seed + 3))
+    for col in ("req_milli_cpu", "req_memory", "nonzero_milli_cpu", "nonzero_memory"):
+        setattr(w.nodes, col, getattr(w.nodes, col) // 2)
+    w.reservations = make_reservations(w.nodes, int(n_nodes * rsv_per_node), rng)
+    reservation_pods(w.pods, rng)
+    w.profile.reservation_weight = 5000
+    w.name = "C3-rsv"
+    return w
+
+
 def c3_bind(seed: int = SEED, n_nodes: int = 2000, n_pods: int = 4000, label_frac: float = 0.4,
             required_frac: float = 0.4, **kw) -> Workload:
     """C3 without NUMA topology policies, with node CPU bind policies and required pod bind policies

@@ -32,6 +32,7 @@ def assert_states_equal(a, b, label):
 
 
 def workloads(small=True):
-    """C2 (quota), C3 (devices, cpusets, SingleNUMANode nodes) and C4 (reservations), small sizes."""
+    """C2 (quota), C3 (devices, cpusets, SingleNUMANode nodes), C4 (reservations) and C3-rsv (the shipped profile's
+    Reservation + NodeNUMAResource + DeviceShare together), small sizes."""
     return [synth.c2(n_nodes=300, n_pods=200, n_quotas=8), synth.c3(n_nodes=200, n_pods=200),
-            synth.c4(n_nodes=300, n_reservations=700, n_pods=200)]
+            synth.c4(n_nodes=300, n_reservations=700, n_pods=200), synth.c3_rsv(n_nodes=200, n_pods=200)]

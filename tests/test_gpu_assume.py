@@ -27,7 +27,7 @@ def pick(total):
     return int(np.argmax(total))
 
 
-@pytest.mark.parametrize("wi", [0, 1, 2], ids=["c2", "c3", "c4"])
+@pytest.mark.parametrize("wi", [0, 1, 2, 3], ids=["c2", "c3", "c4", "c3rsv"])
 def test_eval_pick_assume_matches_oracle(runtime, oracle_lib, wi):
     w = workloads()[wi]
     ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
@@ -54,7 +54,7 @@ def test_eval_pick_assume_matches_oracle(runtime, oracle_lib, wi):
     orc.close()
 
 
-@pytest.mark.parametrize("wi", [0, 1, 2], ids=["c2", "c3", "c4"])
+@pytest.mark.parametrize("wi", [0, 1, 2, 3], ids=["c2", "c3", "c4", "c3rsv"])
 def test_schedule_then_unreserve(runtime, oracle_lib, wi):
     w = workloads()[wi]
     ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())

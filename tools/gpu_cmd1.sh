@@ -1,5 +1,5 @@
+# ad-hoc GPU batch of the session
 set -o pipefail
-mkdir -p gpurun_out/r5a
-timeout -k 10 400 python -u -m pytest tests/test_gpu_preempt.py tests/test_gpu_rccl.py -x -v --timeout 300 --timeout-method thread > gpurun_out/r5a/new.log 2>&1 || { tail -50 gpurun_out/r5a/new.log; exit 1; }
-tail -3 gpurun_out/r5a/new.log
-BENCH=1 BENCH_ARGS="--steps 10 --warmup 3" bash tools/gpu_tests.sh r5a
+mkdir -p gpurun_out/r5d
+timeout -k 10 600 python -u -m pytest tests/test_gpu_shipped_profile.py tests/test_gpu_reservation.py tests/test_gpu_deviceshare.py -v --timeout 300 --timeout-method thread > gpurun_out/r5d/new.log 2>&1
+grep -E "PASSED|FAILED|^E .*Error" gpurun_out/r5d/new.log | head -60
