@@ -52,9 +52,9 @@ METRIC = "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k no
 def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
 
-    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c3r"):
+    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f"):
         raise SystemExit(f"unknown config {name}")
-    fn = {"c2d": synth.c2_default, "c3r": synth.c3_rsv}.get(name) or getattr(synth, name)
+    fn = {"c2d": synth.c2_default, "c3r": synth.c3_rsv, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
 
@@ -474,7 +474,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c3r"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f"])
     ap.add_argument("--pods", type=int, default=0, help="pods per step (default: the config's own count)")
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)

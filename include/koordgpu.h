@@ -601,6 +601,9 @@ typedef struct ks_stats {
                               select too, the lists patched after the commit (monotone plugin sets) */
   int64_t pre_reserves;    /* Reserves whose NodeNUMAResource / DeviceShare allocation was computed ahead of the commit
                               (the pod's node ranked in its snapshot top) */
+  int64_t commit_lds_bytes; /* the commit kernel's LDS image for this context (of the CU's 160 KB) */
+  int64_t commit_helpers;   /* 1 = the NUMA-policy + DeviceShare commit ran its helper waves (their region fit the LDS
+                               next to the slot caches; 0 = wave 0 computed the device hints itself) */
 } ks_stats;
 
 /* ---- preemption: the ElasticQuota PostFilter ----

@@ -427,6 +427,8 @@ class KsStats(C.Structure):
         ("fixup_ms", C.c_double),
         ("pipelined", C.c_int64),
         ("pre_reserves", C.c_int64),
+        ("commit_lds_bytes", C.c_int64),
+        ("commit_helpers", C.c_int64),
     ]
 
 

@@ -3918,6 +3918,14 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   ctx->stats.bubble_passes = (int64_t)cnt[4];
   ctx->stats.pre_reserves = (int64_t)cnt[5];
   ctx->stats.pipelined = pipe ? (pipe->patch ? 2 : 1) : 0;
+  {
+    bool qc = false;
+    const int32_t rcap = commit_rcap(ctx, &qc);
+    const CommitLayout L = commit_layout(ctx->k, ctx->nchunks, qc, rsv_cache_bytes(ctx, rcap), dev_cache_bytes(ctx),
+                                         numa_cache_bytes(ctx), ctx->q.q, kernel_feat(ctx) == 0, commit_hint_variant(ctx));
+    ctx->stats.commit_lds_bytes = (int64_t)L.total;
+    ctx->stats.commit_helpers = L.hint ? 1 : 0;
+  }
   for (int i = 0; i < 8; ++i) ctx->stats.diag[i] = (int64_t)cnt[8 + i];
   for (size_t i = 0; i + 1 < evs.size(); i += 2) {
     float e = 0;

@@ -634,6 +634,29 @@ def with_static_plugins(w: Workload, seed: int = SEED + 7, weight_taint: int = 1
     return w
 
 
+def c3_full(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, n_quotas: int = 32, **kw) -> Workload:
+    """C3 (NUMA topology policies, cpuset pods, GPU / RDMA devices) under the rest of the shipped profile as well:
+    ElasticQuota (32 leaf quotas) and the v1beta2 default plugins TaintToleration, NodeAffinity and NodePorts -- the
+    combination whose commit kernel holds the NUMA slot cache, the device slot cache, the dictionary-plugin words and the
+    quota rows in one workgroup's LDS."""
+    w = c3(seed=seed, n_nodes=n_nodes, n_pods=n_pods, **kw)
+    rng = np.random.Generator(np.random.PCG64(seed + 5))
+    p = w.pods
+    batch = (p.flags & abi.KS_POD_PROD) == 0
+    p.quota[:] = rng.integers(0, n_quotas, p.n)
+    p.quota_req[QDIM_CPU] = p.req_milli_cpu
+    p.quota_req[QDIM_MEMORY] = p.req_memory
+    p.quota_req[QDIM_BATCH_CPU] = p.req_scalar[SLOT_BATCH_CPU]
+    p.quota_req[QDIM_BATCH_MEMORY] = p.req_scalar[SLOT_BATCH_MEMORY]
+    p.quota_mask[:] = np.where(batch, (1 << QDIM_BATCH_CPU) | (1 << QDIM_BATCH_MEMORY),
+                               (1 << QDIM_CPU) | (1 << QDIM_MEMORY)).astype(np.uint32)
+    w.quotas = make_quotas(p, n_quotas, rng)
+    w.profile.quota = ElasticQuotaArgs()
+    w = with_static_plugins(w, seed=seed + 6)
+    w.name = "C3-full"
+    return w
+
+
 def c2_default(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, **kw) -> Workload:
     """C2 under the v1beta2 default profile's upstream plugins as well: NodeResourcesBalancedAllocation,
     TaintToleration and NodeAffinity (weight 1 each) and NodePorts next to Fit + LoadAware + ElasticQuota."""

@@ -112,3 +112,42 @@ def test_shipped_profile_eval_pod(runtime, oracle_lib):
     finally:
         ev.close()
         orc.close()
+
+
+def test_c3_full_5k_nodes_quota_and_default_plugins(runtime, oracle_lib):
+    """SURVEY C3 at full size under the rest of the shipped profile too: NUMA policies + DeviceShare + ElasticQuota +
+    TaintToleration / NodeAffinity / NodePorts (synth.c3_full).  The commit kernel then holds the NUMA and device slot
+    caches, the dictionary-plugin words, the PodStat records and the quota rows in one workgroup's LDS; the stats say
+    how much of the CU's 160 KB that is and whether the helper waves' region still fit."""
+    w = synth.c3_full()
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    try:
+        got = ev.schedule(w.pods)
+        st = ev.stats()
+        cs_g = ev.fetch_cpusets(w.pods.n)
+        dev_g = ev.read_devices()
+        numa_g = ev.read_numa_nodes()
+        nodes_g = ev.read_nodes()
+        q_g = ev.read_quota_used()
+    finally:
+        ev.close()
+    print(f"c3-full: commit LDS {st['commit_lds_bytes']} B of 163840, helper waves {st['commit_helpers']}, "
+          f"passes {st['passes']}, cuts {st['cut_passes']}, pre-reserves {st['pre_reserves']}")
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), nthreads=8, **w.tables())
+    try:
+        want = orc.schedule(w.pods)
+        assert_same_results(got, want, "c3-full")
+        for k in ("gpu_minors", "rdma_minors"):
+            assert np.array_equal(got[k], want[k]), f"c3-full: {k} differ"
+        assert np.array_equal(cs_g, orc.fetch_cpusets(w.pods.n)), "c3-full: cpusets differ"
+        for g, o in zip(dev_g, orc.read_devices()):
+            assert np.array_equal(g, o), "c3-full: device state differs"
+        for g, o in zip(numa_g, orc.read_numa_nodes()):
+            assert np.array_equal(g, o), "c3-full: NUMA-node state differs"
+        assert np.array_equal(q_g, orc.read_quota_used()), "c3-full: quota used differs"
+        assert_same_state(nodes_g, orc.read_nodes(), "c3-full")
+    finally:
+        orc.close()
+    assert st["commit_lds_bytes"] <= 160 * 1024
+    rejected = int(((got["status"] & (abi.KS_S_QUOTA | abi.KS_S_QUOTA_NONPREEMPTIBLE)) != 0).sum())
+    assert rejected > 100 and int((got["gpu_minors"] != 0).sum()) > 1000, rejected
