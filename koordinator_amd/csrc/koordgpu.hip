@@ -105,6 +105,7 @@ __global__ void prep_nodes_kernel(DevNodes d, int64_t n, int32_t filter_expired)
   d.numa_amilli[i] = A;
   d.numa_off[i] = amp ? (int64_t)::ceil((double)A * ratio) - A : 0;
   if (amp) bits |= kNumaAmp;
+  if ((d.numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u) bits |= kNumaPolNode;
   if (d.numa_flags[i] & KS_NUMA_INVALID_RATIO) bits |= kNumaInvalid;
   // a score-term capacity outside the f64 path's range (ks_device.h term_least): the node scores in int64
   bool big = d.alloc_cpu[i] >= kBigCap || d.alloc_mem[i] >= kBigCap || d.alloc_eph[i] >= kBigCap ||
@@ -749,7 +750,7 @@ constexpr int kCpusetStage = 1024;
 __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* list, const int32_t* count_p,
                                                      const uint32_t* split, const PodRec* pods, CpuSet* out,
                                                      const uint32_t* numa_flags, uint32_t* cores, int32_t default_most,
-                                                     int64_t n) {
+                                                     int32_t* numa_free, int64_t numa_npad, int64_t n) {
   __shared__ int2 stage[kCpusetStage];
   const int64_t node = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int32_t count = *count_p;
@@ -811,8 +812,11 @@ __global__ __launch_bounds__(256) void cpuset_kernel(DevCpu cpu, const int2* lis
   }
   if (any && node < n) {
     const CpuTopo& t = cpu.topo[cpu.topo_id[node]];
-    cores[node] = cores_word(t, cs_andnot(cs_andnot(t.all, cpu.allocated[node]), cpu.reserved[node]),
-                             (numa_flags[node] >> KS_NUMA_CPU_BIND_SHIFT) & 3u);
+    const CpuSet av = cs_andnot(cs_andnot(t.all, cpu.allocated[node]), cpu.reserved[node]);
+    cores[node] = cores_word(t, av, (numa_flags[node] >> KS_NUMA_CPU_BIND_SHIFT) & 3u);
+    // the NUMA nodes' words too: the commit kept their CPU counts, the core counts follow the CPU ids chosen here
+    if (numa_free)
+      for (int k = 0; k < kNumaDev; ++k) numa_free[(int64_t)k * numa_npad + node] = numa_free_word(t, av, k);
   }
 }
 
@@ -833,16 +837,19 @@ __global__ void cores_kernel(DevCpu cpu, int32_t loaded, const uint32_t* numa_fl
   cores[i] = cores_word(tp, cs_andnot(cs_andnot(tp.all, cpu.allocated[i]), cpu.reserved[i]), label);
 }
 
-// CPUs of each NUMA node available to cpuset pods (topology CPUs of the node - allocated - reserved), for the NUMA
-// policy path's allocateCPUSet check; NUMA node k = the topology's k-th NUMA id (ids are 0..n-1, ks_load_cpu_state).
+// CPUs of each NUMA node available to cpuset pods (topology CPUs of the node - allocated - reserved) and its core
+// counts (numa_free_word), for the NUMA policy path's allocateCPUSet check and a required CPU bind policy's trim;
+// NUMA node k = the topology's k-th NUMA id (ids are 0..n-1, ks_load_cpu_state).
 __global__ void numa_free_kernel(DevCpu cpu, DevNuma nv, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t tid = cpu.topo_id[i];
   for (int k = 0; k < kNumaDev; ++k) {
     int32_t f = 0;
-    if (tid >= 0 && k < cpu.topo[tid].nnodes)
-      f = cs_count(cs_andnot(cs_andnot(cpu.topo[tid].node_mask[k], cpu.allocated[i]), cpu.reserved[i]));
+    if (tid >= 0) {
+      const CpuTopo& t = cpu.topo[tid];
+      f = numa_free_word(t, cs_andnot(cs_andnot(t.all, cpu.allocated[i]), cpu.reserved[i]), k);
+    }
     nv.free[(int64_t)k * nv.npad + i] = f;
   }
 }
@@ -1558,9 +1565,6 @@ static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
         KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: numa_flags 0x%x: encode the CPU bind / NUMA topology policy in its bits", (long long)i, f);
       if (label == 3u || (f >> (KS_NUMA_CPU_BIND_SHIFT + 2)))
         KS_FAIL(ctx, KS_EINVAL, "node %lld: numa_flags 0x%x invalid", (long long)i, f);
-      // the required policy on a NUMA-policy node runs through FilterByNUMANode's per-NUMA allocation: not modelled
-      if (label && ((f >> KS_NUMA_POLICY_SHIFT) & 3u))
-        KS_FAIL(ctx, KS_EUNSUPPORTED, "node %lld: a node CPU bind policy together with a NUMA topology policy is not supported", (long long)i);
     }
     for (int64_t i = 0; c->numa_cpuset_cpus && i < n; ++i)
       if (c->numa_cpuset_cpus[i] < 0 || c->numa_cpuset_cpus[i] > (1 << 20))
@@ -1637,6 +1641,9 @@ static int upload_prep_nodes(ks_ctx* ctx) {
 
 // CoresWord of every node (ks_device.h) after a load or delta of the node rows or the CPU state; the schedule
 // passes keep it current themselves (cpuset_kernel), as does ks_unreserve.
+// the NUMA-node words cpuset_kernel refreshes (DevNuma.free), or none without a NUMA-node table
+static int32_t* numa_words(const ks_ctx* ctx) { return (ctx->numa_blob && ctx->kc.numa_pol) ? ctx->nv.free : nullptr; }
+
 static int cores_refresh(ks_ctx* ctx) {
   if (!ctx->cfg.numa.enable || ctx->n == 0) return KS_OK;
   hipLaunchKernelGGL(cores_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
@@ -3057,9 +3064,6 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
       if ((pol != KS_CPU_BIND_FULL_PCPUS && pol != KS_CPU_BIND_SPREAD_BY_PCPUS) || ex > KS_CPU_EXCL_NUMA_NODE_LEVEL || (cb >> 5))
         KS_FAIL(ctx, KS_EINVAL, "pod %d: cpu_bind 0x%x invalid", i, cb);
       const bool req = (cb & KS_CPU_BIND_REQUIRED) != 0;
-      // a required policy on a NUMA-policy node runs through FilterByNUMANode's per-NUMA allocation: not modelled
-      if (req && ctx->numa_policy_nodes > 0)
-        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: a required CPU bind policy together with NUMA topology policies is not supported", i);
       any_req |= req;
       if (cpu <= 0 || cpu % 1000 != 0 || cpu / 1000 > KS_MAX_CPUS)
         KS_FAIL(ctx, KS_EINVAL, "pod %d: a cpu-bind pod needs a whole-CPU request in (0, %d] CPUs (PreFilter ErrInvalidRequestedCPUs)", i, KS_MAX_CPUS);
@@ -3775,7 +3779,8 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
                        (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
                        (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
-                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED),
+                       numa_words(ctx), ctx->nv.npad, ctx->n);
     HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
   }
   return KS_OK;
@@ -3901,7 +3906,8 @@ static int schedule_staged_impl(ks_ctx* ctx) {
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
                        (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
                        (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
-                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED),
+                       numa_words(ctx), ctx->nv.npad, ctx->n);
     HIPCHK(ctx, hipGetLastError());
   }
   HIPCHK(ctx, hipEventRecord(t1, ctx->stream));
@@ -4371,7 +4377,7 @@ __global__ void unreserve_kernel(UnreserveArgs a) {
           const int64_t o = (int64_t)k * a.nv.npad + n;
           const int32_t c1 = a.nv.cs[o] - ck;
           a.nv.cs[o] = c1;
-          a.nv.free[o] += ck;
+          a.nv.free[o] = numa_free_word(t, cs_andnot(cs_andnot(t.all, a.cpu.allocated[n]), a.cpu.reserved[n]), k);
           const int64_t m = (int64_t)c1 * 1000;
           a.nv.off[o] = ratio > 1.0 ? (int64_t)::ceil((double)m * ratio) - m : 0;
         }
@@ -4432,7 +4438,8 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
                        (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
                        (const PodRec*)ctx->ast.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
-                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED), ctx->n);
+                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED),
+                       numa_words(ctx), ctx->nv.npad, ctx->n);
     HIPCHK(ctx, hipGetLastError());
   }
   HIPCHK(ctx, hipMemcpyAsync(out, ctx->ast.results, sizeof(ks_result), hipMemcpyDeviceToHost, ctx->stream));

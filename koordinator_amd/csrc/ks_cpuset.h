@@ -433,6 +433,23 @@ __device__ inline CpuSet filter_required(const CpuTopo& t, const CpuSet& avail, 
   return r;
 }
 
+// NUMA node k's word of the NUMA-policy path (DevNuma.free, ks_numa.h): its available CPUs (bits 0-11), the cores
+// of the NUMA node whose CPUs are all available (bits 12-21: filterCPUsByRequiredCPUBindPolicy FullPCPUs keeps them)
+// and its cores with any available CPU (bits 22-31: SpreadByPCPUs keeps one CPU of each) -- trimNUMANodeResources
+// and allocateCPUSet of a required CPU bind policy read the latter two (resource_manager.go:144-167, :322-330).
+__device__ inline int32_t numa_free_word(const CpuTopo& t, const CpuSet& avail, int k) {
+  if (k >= t.nnodes) return 0;
+  const int32_t f = cs_count(cs_and(avail, t.node_mask[k]));
+  uint32_t full = 0, any = 0;
+  for (int c = 0; c < t.ncores; ++c) {
+    if (cs_count(cs_and(t.core_mask[c], t.node_mask[k])) == 0) continue;  // (a core lies in one NUMA node)
+    const int n = cs_count(cs_and(avail, t.core_mask[c]));
+    full += n == t.cpc ? 1u : 0u;
+    any += n > 0 ? 1u : 0u;
+  }
+  return (int32_t)((uint32_t)f | (full << 12) | (any << 22));
+}
+
 // CoresWord (ks_device.h) of a node whose available CPUs are `avail`.
 __device__ inline uint32_t cores_word(const CpuTopo& t, const CpuSet& avail, uint32_t label) {
   uint32_t full = 0, any = 0;

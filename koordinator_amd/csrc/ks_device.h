@@ -53,6 +53,7 @@ constexpr uint32_t kLaFailProd = 0x4u;      // Filter fails for prod pods when p
 constexpr int kLaReasonNonProdShift = 8;    // KS_R_LA_* reason bits for the non-prod case
 constexpr int kLaReasonProdShift = 20;      // KS_R_LA_* reason bits for the prod case
 constexpr uint32_t kNodeBigCap = 0x8u;      // a score-term capacity >= kBigCap: the node's terms take the int64 path
+constexpr uint32_t kNumaPolNode = 1u << 29; // NodeNUMAResource: the node has a NUMA topology policy (numa_flags bits 5-6)
 constexpr uint32_t kNumaAmp = 1u << 30;     // NodeNUMAResource: cpu amplification ratio > 1
 constexpr uint32_t kNumaInvalid = 1u << 31; // NodeNUMAResource: invalid amplification annotation
 
@@ -641,7 +642,10 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
   if (bind && rs == 0 && r.cpu_free < 0) rs = KS_R_NUMA_INVALID_TOPOLOGY;
   if (c.cores && bind && rs == 0) {
     // the Filter's required policy: the node's, else the pod's required one (plugin.go:303-312); FullPCPUs needs
-    // whole cores (:314-317); the trial Allocate keeps the cores the policy allows (resource_manager.go:322-335)
+    // whole cores (:314-317); the trial Allocate keeps the cores the policy allows (resource_manager.go:322-335) --
+    // only on a node without a NUMA topology policy (:318): on a policy node FilterByNUMANode's Allocate runs instead
+    // (numa_policy_eval)
+    const bool pol_node = c.numa_pol && (r.la_bits & kNumaPolNode);
     const bool preq = (p.flags & KS_POD_CPU_BIND) && (p.cpu_bind & KS_CPU_BIND_REQUIRED);
     const uint32_t ppol = p.cpu_bind & KS_CPU_BIND_POLICY_MASK;
     const uint32_t req = label ? label : (preq ? ppol : 0u);
@@ -651,8 +655,8 @@ __device__ __forceinline__ void numa_eval(const Cfg& c, const PodRec& p, const N
       const int32_t need = (int32_t)(p.cpu / 1000), cpc = max((int32_t)cores_cpc(r.cpu_cores), 1);
       if (req == KS_CPU_BIND_FULL_PCPUS) {
         if (need % cpc != 0) rs = KS_R_NUMA_SMT;
-        else if ((int32_t)cores_full(r.cpu_cores) * cpc < need) rs = KS_R_NUMA_CPUSET;
-      } else if ((int32_t)cores_any(r.cpu_cores) < need) {
+        else if (!pol_node && (int32_t)cores_full(r.cpu_cores) * cpc < need) rs = KS_R_NUMA_CPUSET;
+      } else if (!pol_node && (int32_t)cores_any(r.cpu_cores) < need) {
         rs = KS_R_NUMA_CPUSET;
       }
     }

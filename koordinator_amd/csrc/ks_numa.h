@@ -42,7 +42,8 @@ struct DevNuma {
   int64_t* used;         // [2][kNumaDev][npad] allocatedResources (raw; mutable)
   int64_t* off;          // [kNumaDev][npad] cpuset amplification of the allocated cpu: Amplify(cs) - cs (mutable)
   int32_t* cs;           // [kNumaDev][npad] allocated cpuset CPUs on the NUMA node (mutable)
-  int32_t* free;         // [kNumaDev][npad] CPUs of the NUMA node available to cpuset pods (mutable)
+  int32_t* free;         // [kNumaDev][npad] numa_free_word (ks_cpuset.h): CPUs of the NUMA node available to cpuset pods
+                         // (bits 0-11), its whole free cores (12-21) and cores with a free CPU (22-31) (mutable)
   uint32_t* present;     // [npad] bit k: an allocatedResources entry exists (mutable)
   const uint32_t* flags; // [npad] ks_node_cols.numa_flags (policy in bits 5-6)
   int64_t npad;
@@ -58,7 +59,8 @@ struct NumaGView {
   __device__ __forceinline__ int64_t total(int r, int k) const { return gld(d.total + ((int64_t)r * kNumaDev + k) * d.npad + n); }
   __device__ __forceinline__ int64_t used(int r, int k) const { return gld(d.used + ((int64_t)r * kNumaDev + k) * d.npad + n); }
   __device__ __forceinline__ int64_t off(int k) const { return gld(d.off + (int64_t)k * d.npad + n); }
-  __device__ __forceinline__ int32_t freec(int k) const { return gld(d.free + (int64_t)k * d.npad + n); }
+  __device__ __forceinline__ int32_t freew(int k) const { return gld(d.free + (int64_t)k * d.npad + n); }
+  __device__ __forceinline__ int32_t freec(int k) const { return freew(k) & 0xFFF; }
 };
 
 // LDS slot words: [2K total | 2K used | K off | K (cs << 32 | free) | meta (policy | count << 8 | present << 32)]
@@ -74,8 +76,15 @@ struct NumaLView {
   __device__ __forceinline__ int64_t total(int r, int k) const { return w[kNumaWTot + r * kNumaDev + k]; }
   __device__ __forceinline__ int64_t used(int r, int k) const { return w[kNumaWUsed + r * kNumaDev + k]; }
   __device__ __forceinline__ int64_t off(int k) const { return w[kNumaWOff + k]; }
-  __device__ __forceinline__ int32_t freec(int k) const { return (int32_t)(uint32_t)w[kNumaWCpu + k]; }
+  __device__ __forceinline__ int32_t freew(int k) const { return (int32_t)(uint32_t)w[kNumaWCpu + k]; }
+  __device__ __forceinline__ int32_t freec(int k) const { return freew(k) & 0xFFF; }
 };
+
+// a NUMA-node word's CPUs left by filterCPUsByRequiredCPUBindPolicy (resource_manager.go:595-627): FullPCPUs the CPUs
+// of the whole free cores, SpreadByPCPUs one CPU per core with a free CPU
+__device__ __forceinline__ int32_t numa_filtered(int32_t w, uint32_t policy, int32_t cpc) {
+  return policy == KS_CPU_BIND_FULL_PCPUS ? (int32_t)(((uint32_t)w >> 12) & 0x3FFu) * cpc : (int32_t)(((uint32_t)w >> 22) & 0x3FFu);
+}
 
 // node-level inputs of the policy path (NodeInfo and the node's cpuset state)
 struct NumaNodeCtx {
@@ -84,6 +93,7 @@ struct NumaNodeCtx {
   int64_t cs_milli; // the node's allocated cpuset CPUs x 1000
   int64_t cs_off;   // Amplify(cs_milli) - cs_milli
   int32_t cpu_free; // CPUs available to cpuset pods on the node (-1 = no valid CPU topology)
+  uint32_t cores;   // the node's CoresWord (Cfg.cores: core counts, CPUsPerCore, CPU bind label; ks_device.h)
 };
 
 struct NumaPolOut {
@@ -258,7 +268,15 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
   if (!LATE && dv) dh = dev_hints(c, p, *dv);
   const int pol = v.policy();
   const uint32_t pres = v.present();
-  const bool bind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
+  // requestCPUBind / getCPUBindPolicy on this node (util.go:85-122): a node CPU bind policy makes a whole-CPU pod
+  // cpu-bind with that policy required; else the pod's own policy, required or preferred (the Filter rejected a
+  // fractional request and a conflicting policy before: numa_eval)
+  const uint32_t label = c.cores ? cores_label(nc.cores) : 0u;
+  const bool pbind = c.cpuset && (p.flags & KS_POD_CPU_BIND);
+  const bool bind = pbind || (label != 0u && p.cpu > 0);
+  const uint32_t rpol = label ? label
+                              : ((pbind && (p.cpu_bind & KS_CPU_BIND_REQUIRED)) ? (p.cpu_bind & KS_CPU_BIND_POLICY_MASK) : 0u);
+  const int32_t cpc = max((int32_t)cores_cpc(nc.cores), 1);
   // used (with the cpuset amplification) is re-read for the score; total and available stay live
   auto used_of = [&](int r, int k) -> int64_t {
     return (k < K && ((pres >> k) & 1u)) ? v.used(r, k) + (r == 0 ? v.off(k) : 0) : 0;
@@ -271,6 +289,12 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
       tot[r][k] = k < K ? v.total(r, k) : 0;
       const int64_t a = tot[r][k] - used_of(r, k);
       av[r][k] = a < 0 ? 0 : a;
+    }
+    // trimNUMANodeResources (resource_manager.go:144-167): under a required policy a NUMA node offers at most the
+    // CPUs the policy leaves there (for the hints and for the allocation)
+    if (rpol && k < K && av[0][k] != 0) {
+      const int64_t fk = (int64_t)numa_filtered(v.freew(k), rpol, cpc) * 1000;
+      if (fk < av[0][k]) av[0][k] = fk;
     }
   }
   // options.requests: a cpu-bind pod's cpu amplified (hints and score); originalRequests for the allocation
@@ -458,8 +482,12 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
 #pragma unroll
       for (int i = 0; i < kNumaDev; ++i) {
         if (i >= nb) break;
-        // splitQuantity: a cpu-bind pod's cpu in whole CPUs (Quantity.Value() rounds up)
-        const int64_t split = (r == 0 && bind) ? ((q + 999) / 1000) / (nb - i) * 1000 : q / (nb - i);
+        // splitQuantity (:285-300): a cpu-bind pod's cpu in whole CPUs (Quantity.Value() rounds up); under a required
+        // FullPCPUs policy in whole cores
+        int64_t split = q / (nb - i);
+        if (r == 0 && bind)
+          split = rpol == KS_CPU_BIND_FULL_PCPUS ? ((q + 999) / 1000) / cpc / (nb - i) * cpc * 1000
+                                                 : ((q + 999) / 1000) / (nb - i) * 1000;
         int64_t a = 0;
 #pragma unroll
         for (int k = 0; k < kNumaDev; ++k) a = ord[i] == k ? av[r][k] : a;
@@ -479,22 +507,30 @@ __device__ __forceinline__ NumaPolOut numa_policy_eval(const Cfg& c, const PodRe
 #pragma unroll
   for (int k = 0; k < kNumaDev; ++k) any_alloc |= o.alloc[0][k] != 0 || o.alloc[1][k] != 0;
   if (bind) {
-    // allocateCPUSet: the node's available CPUs, then per allocated NUMA node min(available there, whole CPUs)
-    const int32_t need = (int32_t)(p.cpu_bind >> 8);
-    if (nc.cpu_free < need) {
+    // allocateCPUSet (:314-401): the node's available CPUs (under a required policy the ones it keeps), then per
+    // allocated NUMA node min(available there, whole CPUs); a required policy's satisfiedRequiredCPUBindPolicy on the
+    // union: FullPCPUs takes whole cores of a NUMA node only for a multiple of CPUsPerCore (SpreadByPCPUs' one CPU
+    // per core always satisfies it)
+    const int32_t need = pbind ? (int32_t)(p.cpu_bind >> 8) : (int32_t)(p.cpu / 1000);
+    const int32_t have = !rpol ? nc.cpu_free
+                               : (rpol == KS_CPU_BIND_FULL_PCPUS ? (int32_t)cores_full(nc.cores) * cpc
+                                                                 : (int32_t)cores_any(nc.cores));
+    if (nc.cpu_free < 0 || have < need) {
       o.reasons = KS_R_NUMA_CPUSET;
       return o;
     }
     if (any_alloc) {
       int32_t taken = 0;
+      bool whole = true;
 #pragma unroll
       for (int k = 0; k < kNumaDev; ++k) {
         if (o.alloc[0][k] == 0 && o.alloc[1][k] == 0) continue;
-        const int32_t f = v.freec(k), w = (int32_t)(o.alloc[0][k] / 1000);
+        const int32_t f = rpol ? numa_filtered(v.freew(k), rpol, cpc) : v.freec(k), w = (int32_t)(o.alloc[0][k] / 1000);
         o.cpus[k] = f < w ? f : w;
         taken += o.cpus[k];
+        whole = whole && (o.cpus[k] % cpc == 0);
       }
-      if (taken != need) {
+      if (taken != need || (rpol == KS_CPU_BIND_FULL_PCPUS && !whole)) {
         o.reasons = KS_R_NUMA_CPUSET;
         return o;
       }
@@ -555,6 +591,7 @@ __device__ __forceinline__ NumaNodeCtx numa_node_ctx(const NodeReg<NSC>& r) {
   nc.cs_milli = r.numa_A;
   nc.cs_off = r.numa_off;
   nc.cpu_free = r.cpu_free;
+  nc.cores = r.cpu_cores;
   return nc;
 }
 

@@ -1174,6 +1174,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       EvalOut o{};
       bool feas = false;
       bool unk = false;  // Cfg.cores: feasible only if the slot's core counts, changed in this pass, allow it
+      bool unk_pol = false;  // ... a NUMA-policy slot whose evaluation depends on them (numa_policy_eval)
       wait_rows(nslots >= 64 ? ~0ull : ((1ull << nslots) - 1));
       bool use_hw = false;
       if constexpr (HINTW) {
@@ -1305,9 +1306,17 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           o.araw = so.araw;
         }
         feas = o.reasons == 0;
-        if ((FEAT & 2) && cfg.cores && (cw & kCoresDirty) && feas)
-          unk = ((pod.flags & KS_POD_CPU_BIND) && (pod.cpu_bind & KS_CPU_BIND_REQUIRED)) ||
-                (cores_label(cw) != 0 && pod.cpu > 0);
+        const bool needs_cores = ((pod.flags & KS_POD_CPU_BIND) && (pod.cpu_bind & KS_CPU_BIND_REQUIRED)) ||
+                                 (cores_label(cw) != 0 && pod.cpu > 0);
+        if ((FEAT & 2) && cfg.cores && (cw & kCoresDirty) && feas) unk = needs_cores;
+        // on a node with a NUMA topology policy a required policy's NUMA-node core counts shape the hints, the
+        // allocation and the score, not only feasibility: a slot whose CPU ids are not chosen yet is unknown either way
+        if ((FEAT & 8) && cfg.cores && cfg.numa_pol && (cw & kCoresDirty) && (r.la_bits & kNumaPolNode) && needs_cores)
+          unk_pol = true;
+      }
+      if ((FEAT & 8) && cfg.cores && cfg.numa_pol && __ballot(unk_pol)) {
+        processed = j;  // the next pass sees the CPU ids cpuset_kernel chose
+        break;
       }
       if ((FEAT & 2) && DEV && (cfg.dev || cfg.stat) && cfg.cores && __ballot(unk)) {
         processed = j;  // a normalization max over the feasible nodes would depend on it
@@ -1685,6 +1694,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         nc.cs_off = snuma[4 * s + 1];
         nc.ratio = __longlong_as_double(snuma[4 * s + 2]);
         nc.cpu_free = (int32_t)snuma[4 * s + 3];
+        nc.cores = cfg.cores ? ((uint32_t)((uint64_t)snuma[4 * s + 3] >> 32) & ~kCoresDirty) : 0u;
         if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
           const DevLView dvl{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0};
           npr = numa_policy_eval<true>(cfg, pod, nl, nc, &dvl);  // the Filter passed on this state: DeviceShare follows
@@ -1979,6 +1989,7 @@ __global__ __launch_bounds__(64) void reserve_pre_kernel(CommitArgs a) {
         nc.cs_off = load_field(a.rowcols[RF_NUMA_OFF].p, a.rowcols[RF_NUMA_OFF].width, node);
         nc.ratio = __longlong_as_double(load_field(a.rowcols[RF_NUMA_RATIO].p, a.rowcols[RF_NUMA_RATIO].width, node));
         nc.cpu_free = (int32_t)load_field(a.rowcols[RF_CPU_FREE].p, a.rowcols[RF_CPU_FREE].width, node);
+        nc.cores = cfg.cores ? gld(a.dn->cpu_cores + node) : 0u;
         if (DEV && cfg.dev && (pflags & kPodHasGpu)) npr = numa_policy_eval<true>(cfg, pod, nv, nc, &dvg);
         else npr = numa_policy_eval(cfg, pod, nv, nc, (const DevGView*)nullptr);
         npol = true;

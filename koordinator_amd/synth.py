@@ -513,10 +513,10 @@ def c3_rsv(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, rsv_per_
 
 
 def c3_bind(seed: int = SEED, n_nodes: int = 2000, n_pods: int = 4000, label_frac: float = 0.4,
-            required_frac: float = 0.4, **kw) -> Workload:
-    """C3 without NUMA topology policies, with node CPU bind policies and required pod bind policies
-    (cpu_bind_policies)"""
-    w = c3(seed=seed, n_nodes=n_nodes, n_pods=n_pods, policy_frac=0.0, **kw)
+            required_frac: float = 0.4, policy_frac: float = 0.0, **kw) -> Workload:
+    """C3 with node CPU bind policies and required pod bind policies (cpu_bind_policies); without NUMA topology
+    policies by default, with policy_frac > 0 the labels and required policies meet NUMA-policy nodes too"""
+    w = c3(seed=seed, n_nodes=n_nodes, n_pods=n_pods, policy_frac=policy_frac, **kw)
     rng = np.random.Generator(np.random.PCG64(seed + 1))
     cpu_bind_policies(w.nodes, w.pods, rng, label_frac, required_frac)
     w.name = "C3-bind"

@@ -462,6 +462,7 @@ typedef struct {
 } ko_npol;
 
 static int cpu_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_npol *c, uint8_t *res);
+static void filter_required(const ko_topo *t, int policy, uint8_t *avail);
 
 static uint32_t numa_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_eff *e, const ko_npol *c) {
   if (p->reqzero) return 0; /* PreFilter skip */
@@ -613,6 +614,20 @@ static void dev_hints(const ko_sched *s, const ko_pod *p, int64_t n, ko_devhints
 static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t *raw, uint32_t allow);
 
 
+/* CPUs of NUMA node k (k < 0: of the node) that filterCPUsByRequiredCPUBindPolicy keeps of the available ones
+ * (resource_manager.go:595-627; trimNUMANodeResources :144-167 filters the NUMA node's available CPUs) */
+static int numa_filtered_cpus(const ko_sched *s, int64_t n, int k, int policy) {
+  if (!s->cpu_loaded || s->topo_of[n] < 0) return 0;
+  const ko_topo *t = &s->topos[s->topo_of[n]];
+  const uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
+  uint8_t av[KO_MAX_CPUS];
+  for (int i = 0; i < t->ncpus; i++) av[i] = !al[i] && !rs[i] && (k < 0 || t->node[i] == k);
+  filter_required(t, policy, av);
+  int c = 0;
+  for (int i = 0; i < t->ncpus; i++) c += av[i];
+  return c;
+}
+
 /* CPUs of NUMA node k available to cpuset pods: topology CPUs of the node minus allocated minus reserved */
 static int numa_free_cpus(const ko_sched *s, int64_t n, int k) {
   if (!s->cpu_loaded || s->topo_of[n] < 0) return 0;
@@ -737,6 +752,17 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
   numa_state(s, n, K, total, used, present, avail);
   const double ratio = s->nd.numa_ratio[n];
   const int bind = p->bind != 0;
+  /* getCPUBindPolicy (util.go:85-103): the pod's required policy or the node's CPU bind label (node_pod) */
+  const int rpol = (p->bind & KS_CPU_BIND_REQUIRED) ? (int)(p->bind & KS_CPU_BIND_POLICY_MASK) : 0;
+  const int cpc = (s->cpu_loaded && s->topo_of[n] >= 0 && s->topos[s->topo_of[n]].num_cores > 0)
+                      ? s->topos[s->topo_of[n]].ncpus / s->topos[s->topo_of[n]].num_cores
+                      : 1;
+  if (rpol) /* trimNUMANodeResources (resource_manager.go:144-167), for the hints and for the allocation */
+    for (int k = 0; k < K; k++) {
+      if (avail[k][0] == 0) continue;
+      const int64_t fk = (int64_t)numa_filtered_cpus(s, n, k, rpol) * 1000;
+      if (fk < avail[k][0]) avail[k][0] = fk;
+    }
   /* options.requests: a cpu-bind pod's cpu amplified (hints, score); originalRequests for the allocation */
   const int64_t req[2] = {bind ? amplify(p->cpu, ratio) : p->cpu, p->mem};
   const int64_t oreq[2] = {p->cpu, p->mem};
@@ -837,8 +863,13 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
         }
       int64_t q = oreq[r];
       for (int i = 0; i < nb; i++) {
-        /* splitQuantity: cpu of a cpu-bind pod in whole CPUs (Quantity.Value() rounds up), else milli / bytes */
-        const int64_t split = (r == 0 && bind) ? ((q + 999) / 1000) / (nb - i) * 1000 : q / (nb - i);
+        /* splitQuantity (:285-300): cpu of a cpu-bind pod in whole CPUs (Quantity.Value() rounds up), under a
+         * required FullPCPUs policy in whole cores; else milli / bytes */
+        int64_t split = q / (nb - i);
+        if (r == 0 && bind) {
+          const int64_t ncpus = (q + 999) / 1000;
+          split = rpol == KS_CPU_BIND_FULL_PCPUS ? ncpus / cpc / (nb - i) * cpc * 1000 : ncpus / (nb - i) * 1000;
+        }
         const int64_t a = avail[order[i]][r];
         const int64_t got = a > split ? split : a;
         if (got != 0) {
@@ -850,24 +881,19 @@ static uint32_t numa_policy_eval(const ko_sched *s, const ko_pod *p, int64_t n, 
     }
   }
   if (bind) {
-    /* allocateCPUSet: too few available CPUs on the node, or the allocated NUMA nodes' CPUs do not add up */
-    int free_total = 0, free_k[KS_MAX_NUMA];
-    for (int k = 0; k < K; k++) free_k[k] = numa_free_cpus(s, n, k);
-    if (s->cpu_loaded && s->topo_of[n] >= 0) { /* GetAvailableCPUs over the whole node */
-      const ko_topo *t = &s->topos[s->topo_of[n]];
-      const uint8_t *al = s->cpu_alloc + (size_t)n * KO_MAX_CPUS, *rs = s->cpu_resv + (size_t)n * KO_MAX_CPUS;
-      for (int i = 0; i < t->ncpus; i++) free_total += !al[i] && !rs[i];
-    }
-    if (free_total < p->needed) return KS_R_NUMA_CPUSET;
-    int any = 0, taken = 0;
+    /* allocateCPUSet (:314-401), run for real on the node's CPUs: per allocated NUMA node numCPUs = min(the available
+     * CPUs there -- the ones a required policy keeps --, the node's whole CPUs), takeCPUs on each, the total must be
+     * numCPUsNeeded, a required policy satisfied (cpu_allocate) */
     for (int k = 0; k < K; k++) {
       if (!out->alloc[k][0] && !out->alloc[k][1]) continue;
-      any = 1;
+      const int free_k = rpol ? numa_filtered_cpus(s, n, k, rpol) : numa_free_cpus(s, n, k);
       const int want_k = (int)(out->alloc[k][0] / 1000);
-      out->cpus[k] = free_k[k] < want_k ? free_k[k] : want_k;
-      taken += out->cpus[k];
+      out->cpus[k] = free_k < want_k ? free_k : want_k;
     }
-    if (any && taken != p->needed) return KS_R_NUMA_CPUSET;
+    ko_pod pt = *p;
+    ko_npol tc = {1, 0, 0, out};
+    uint8_t res[KO_MAX_CPUS];
+    if (cpu_allocate(s, &pt, n, &tc, res) != 0) return KS_R_NUMA_CPUSET;
   }
   /* DeviceShare's Allocate with the affinity */
   {

@@ -137,3 +137,32 @@ def allocate_cases():
         ("required SpreadByPCPUs and allocated", S, holes, [0, 2, 4, 6]),
         ("required SpreadByPCPUs and allocated: two cores", S, list(range(4, 104)), None),
     ]
+
+
+def policy_bind_cluster(topo, allocated=(), label=0, cpu_milli=4000, bind=None, required=False,
+                        policy=None):
+    """bind_policy_cluster's node with a NUMA topology policy (default SingleNUMANode) and its NodeResourceTopology
+    zones: one NUMA node per topology NUMA id, cpu = its CPUs x 1000, memory 2^39 each, allocatedResources cpu = the
+    allocated CPUs there.  Returns (cfg, nodes, cpu_state, pod, numa_nodes)."""
+    import numpy as np
+
+    from koordinator_amd import abi
+    from koordinator_amd.cluster import NumaNodes
+
+    cfg, nodes, st, pod = bind_policy_cluster(topo, allocated=allocated, label=label, cpu_milli=cpu_milli, bind=bind,
+                                              required=required)
+    pol = abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE if policy is None else policy
+    nodes.numa_flags[:] |= np.uint32(pol << abi.KS_NUMA_POLICY_SHIFT)
+    _, node, _ = build_topology(*topo)
+    K = max(node) + 1
+    nn = NumaNodes(1)
+    nn.count[0] = K
+    for k in range(K):
+        cpus = [i for i, v in enumerate(node) if v == k]
+        held = len([c for c in allocated if c in cpus])
+        nn.alloc_cpu[0, k] = len(cpus) * 1000
+        nn.alloc_memory[0, k] = 1 << 39
+        nn.cpuset_cpus[0, k] = held
+        nn.used_cpu[0, k] = held * 1000
+        nn.used_present[0, k] = 1 if held else 0
+    return cfg, nodes, st, pod, nn

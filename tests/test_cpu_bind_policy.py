@@ -5,7 +5,7 @@ pod cpu-bind only through the node's policy, count form of the trial Allocate)."
 import numpy as np
 import pytest
 
-from cpuset_util import allocate_cases, bind_policy_cluster, filter_cases
+from cpuset_util import allocate_cases, bind_policy_cluster, filter_cases, policy_bind_cluster
 from koordinator_amd import abi, synth
 from koordinator_amd.cluster import mask_cpus
 from oracle.oracle import Oracle
@@ -33,6 +33,58 @@ def test_reference_allocate_cases(case):
     else:
         assert r["status"][0] == abi.KS_S_SCHEDULED
         assert mask_cpus(o.fetch_cpusets(1)[0]) == want
+    o.close()
+
+
+@pytest.mark.parametrize("case", allocate_cases(), ids=[c[0] for c in allocate_cases()])
+def test_reference_allocate_cases_on_numa_policy_node(case):
+    """the same TestResourceManagerAllocate cases (their hint is NUMA node 0) on a SingleNUMANode node: the topology
+    manager admits NUMA node 0 (trimNUMANodeResources leaves node 1, whose CPUs are all allocated, no cpu), the NUMA
+    allocation is 4 CPUs there and allocateCPUSet takes the reference's CPUs; where the reference's Allocate fails, the
+    trimmed hints already leave nothing to admit"""
+    _, bind, allocated, want = case
+    cfg, nodes, st, pod, nn = policy_bind_cluster((2, 1, 26, 2), allocated=allocated, bind=bind, required=True)
+    o = Oracle(cfg, nodes, cpu_state=st, numa_nodes=nn)
+    r = o.schedule(pod)
+    if want is None:
+        assert r["status"][0] == abi.KS_S_UNSCHEDULABLE
+    else:
+        assert r["status"][0] == abi.KS_S_SCHEDULED
+        assert mask_cpus(o.fetch_cpusets(1)[0]) == want
+        na = o.fetch_numa_alloc(1)[0]
+        assert na[0][0] == 4000 and na[1][0] == 0  # NUMANodeResources: cpu 4 on NUMA node 0
+    o.close()
+
+
+def test_required_full_pcpus_split_over_two_numa_nodes():
+    """BestEffort node, 16 CPUs required FullPCPUs (no memory request: the cpu hints alone) on 2 x (4 cores x 2
+    threads): neither NUMA node alone has 16 CPUs, the {0, 1} hint splits in whole cores (splitQuantity :290-296:
+    8 + 8).  With CPU 0 taken and 14 CPUs: NUMA node 0 keeps 3 whole cores (trimNUMANodeResources: 7000 -> 6000),
+    the split gives 3 cores there and 4 on node 1, and allocateCPUSet takes cores 1-3 and 4-7.  (With a memory request
+    the memory list's single-NUMA hints narrow the merged affinity to {0}, whose allocation then fails: the
+    reference's merge prefers the narrower non-preferred hint.)"""
+    cfg, nodes, st, pod, nn = policy_bind_cluster((2, 1, 4, 2), allocated=[], bind=abi.KS_CPU_BIND_FULL_PCPUS,
+                                                  required=True, cpu_milli=16000,
+                                                  policy=abi.KS_NUMA_POLICY_BEST_EFFORT)
+    pod.req_memory[:] = 0
+    o = Oracle(cfg, nodes, cpu_state=st, numa_nodes=nn)
+    r = o.schedule(pod)
+    assert r["status"][0] == abi.KS_S_SCHEDULED and len(mask_cpus(o.fetch_cpusets(1)[0])) == 16
+    o.close()
+    pod.req_memory[:] = 1 << 30
+    o = Oracle(cfg, nodes, cpu_state=st, numa_nodes=nn)
+    assert o.schedule(pod)["status"][0] != abi.KS_S_SCHEDULED
+    o.close()
+    cfg, nodes, st, pod, nn = policy_bind_cluster((2, 1, 4, 2), allocated=[0], bind=abi.KS_CPU_BIND_FULL_PCPUS,
+                                                  required=True, cpu_milli=14000,
+                                                  policy=abi.KS_NUMA_POLICY_BEST_EFFORT)
+    pod.req_memory[:] = 0
+    o = Oracle(cfg, nodes, cpu_state=st, numa_nodes=nn)
+    r = o.schedule(pod)
+    # 14 CPUs = 7 cores: NUMA 0 keeps cores 1-3 (6 CPUs), NUMA 1 all 4 cores (8): split 3 + 4 cores ... 6 + 8 = 14
+    assert r["status"][0] == abi.KS_S_SCHEDULED
+    got = mask_cpus(o.fetch_cpusets(1)[0])
+    assert len(got) == 14 and 0 not in got and 1 not in got
     o.close()
 
 
