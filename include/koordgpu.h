@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 7
+#define KS_ABI_VERSION 8
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -176,6 +176,13 @@ extern "C" {
                                              NoExecute taint no toleration of the pod tolerates) */
 #define KS_R_NODE_AFFINITY 0x4000000u     /* upstream NodeAffinity Filter: "node(s) didn't match Pod's node affinity/selector" */
 #define KS_R_NODE_PORTS 0x8000000u        /* upstream NodePorts Filter: "node(s) didn't have free ports for the requested pod ports" */
+/* upstream PodTopologySpread Filter (ABI 8): "node(s) didn't match pod topology spread constraints" (ErrReasonConstraintsNotMatch)
+ * or its "(missing required label)" variant (ErrReasonNodeLabelNotMatch) */
+#define KS_R_TOPOLOGY_SPREAD 0x10000000u
+/* upstream InterPodAffinity Filter (ABI 8), the first failing check of the three in the plugin's order: */
+#define KS_R_POD_AFFINITY 0x20000000u          /* "node(s) didn't match pod affinity rules" */
+#define KS_R_POD_ANTI_AFFINITY 0x40000000u     /* "node(s) didn't match pod anti-affinity rules" */
+#define KS_R_EXISTING_ANTI_AFFINITY 0x80000000u /* "node(s) didn't satisfy existing pods anti-affinity rules" */
 
 /* ---- per-pod result status (ks_result.status) ---- */
 #define KS_S_SCHEDULED 0x0u
@@ -196,7 +203,9 @@ extern "C" {
 #define KS_SCORE_BALANCED 5    /* upstream NodeResourcesBalancedAllocation (balanced_allocation.go, v1.24) */
 #define KS_SCORE_TAINT 6       /* upstream TaintToleration after DefaultNormalizeScore(100, reverse) (v1.24) */
 #define KS_SCORE_NODE_AFFINITY 7 /* upstream NodeAffinity after DefaultNormalizeScore(100) (v1.24) */
-#define KS_NUM_SCORE_PLUGINS 8
+#define KS_SCORE_TOPOLOGY_SPREAD 8 /* upstream PodTopologySpread after its NormalizeScore (v1.24, ABI 8) */
+#define KS_SCORE_POD_AFFINITY 9    /* upstream InterPodAffinity after its NormalizeScore (v1.24, ABI 8) */
+#define KS_NUM_SCORE_PLUGINS 10
 
 /* ---- per-node DeviceShare flags (ks_device_cols.flags) ---- */
 #define KS_DEV_PRESENT 0x1u /* nodeDeviceCache.getNodeDevice != nil (deviceshare/plugin.go:286-289) */
@@ -325,6 +334,48 @@ typedef struct ks_static_plugin_args {
   int64_t plugin_weight;
 } ks_static_plugin_args;
 
+/* Upstream PodTopologySpread and InterPodAffinity (kube-scheduler v1.24.15 plugins/podtopologyspread,
+ * plugins/interpodaffinity; the v1beta2 default profile enables both, weights 2 and 1, with the system default
+ * spreading constraints and hardPodAffinityWeight 1).  Both count pods per topology domain.  The label selector
+ * matching runs on the host once per distinct selector / affinity term (koordinator_amd/topology_plugins.py,
+ * INTEGRATION.md "Pod topology spread and inter-pod affinity") and reaches the device as:
+ *   properties   <= KS_TOPO_PROPS predicates on pods (matches a spread constraint's selector in a namespace, matches
+ *                an affinity term, matches all required affinity terms of a pod, carries an anti-affinity term or a
+ *                weighted affinity term); ks_node_cols.topo_count[p] = the node's pods with property p (every Reserve
+ *                adds the pod's ks_pod_cols.topo_props, ks_unreserve removes them, ks_read_nodes reads them back);
+ *   domains      the hostname (each node its own) and one zonal key: ks_node_cols.topo_zone = the node's value
+ *                index 0..KS_TOPO_ZONES-1, -1 = label absent;
+ *   query terms  <= KS_TOPO_TERMS per pod (ks_pod_cols.topo_term, packed words, see KS_TOPO_K_*): what the two
+ *                plugins' PreFilter / Filter / PreScore / Score ask of the counters for that pod.
+ * A pod without query terms (KS_TOPO_DYN clear) never fails their Filters and scores 100 (PodTopologySpread's
+ * NormalizeScore with no constraint) and 0 everywhere; a pod with them is scheduled alone against the counters of
+ * every pod placed before it.  Not with ks_shard_init nranks > 1 or ks_preempt. */
+#define KS_TOPO_PROPS 16
+#define KS_TOPO_TERMS 8
+#define KS_TOPO_ZONES 64
+/* ks_pod_cols.topo_flags */
+#define KS_TOPO_DYN 0x1u           /* the pod has query terms */
+#define KS_TOPO_SELF_AFFINITY 0x2u /* podMatchesAllAffinityTerms(pod's own required affinity terms, pod) */
+#define KS_TOPO_SOFT_ALL_KEYS 0x4u /* PreScore requireAllTopologies: the soft constraints are the pod's own (not the
+                                      system defaults), so nodes without every soft key are ignored */
+/* topo_term word: kind (bits 0-7), property (8-15), key (16-23: 0 hostname, 1 zone), flags (24-31), param (32-63,
+ * int32: maxSkew, or the score weight with its sign) */
+#define KS_TOPO_K_SPREAD_HARD 1    /* DoNotSchedule constraint: skew = domain matches + self - min over domains */
+#define KS_TOPO_K_SPREAD_SOFT 2    /* ScheduleAnyway constraint (the pod's own or a system default) */
+#define KS_TOPO_K_AFFINITY 3       /* required affinity term (property: pods matching all of the pod's terms) */
+#define KS_TOPO_K_ANTI 4           /* required anti-affinity term */
+#define KS_TOPO_K_EXISTING_ANTI 5  /* a placed pod's required anti-affinity term that matches the pod */
+#define KS_TOPO_K_SCORE 6          /* weighted score term: weight x matching pods in the node's domain */
+#define KS_TOPO_T_SELF 0x1u        /* spread: the constraint's selector matches the pod itself */
+#define KS_TOPO_T_ELIG_ZONE 0x2u   /* spread: the constraint set (hard, or soft) has a zonal key (nodes without the
+                                      zone label are not eligible) */
+typedef struct ks_topology_args {
+  int32_t enable;
+  int32_t _pad0;
+  int64_t spread_weight;   /* PodTopologySpread profile weight (v1beta2 default 2) */
+  int64_t affinity_weight; /* InterPodAffinity profile weight (default 1) */
+} ks_topology_args;
+
 typedef struct ks_config {
   int32_t abi_version; /* = KS_ABI_VERSION */
   int32_t device;      /* HIP device ordinal */
@@ -342,6 +393,7 @@ typedef struct ks_config {
   ks_static_plugin_args taint;    /* ABI 6: upstream TaintToleration */
   ks_static_plugin_args affinity; /* ABI 6: upstream NodeAffinity */
   ks_static_plugin_args nodeports; /* ABI 6: upstream NodePorts (Filter only: enable_score / plugin_weight unused) */
+  ks_topology_args topology;       /* ABI 8: upstream PodTopologySpread + InterPodAffinity */
 } ks_config;
 
 /* Node snapshot, structure-of-arrays, one entry per node.  NodeInfo fields are
@@ -391,6 +443,9 @@ typedef struct ks_node_cols {
   /* NodePorts (ABI 6; NULL = 0): host-port dictionary bits in use on the node (NodeInfo.UsedPorts); every Reserve
    * adds the pod's bits while ks_config.nodeports is on (read back with ks_read_nodes) */
   const uint64_t *host_ports;
+  /* PodTopologySpread / InterPodAffinity (ABI 8; NULL = -1 / 0), see ks_topology_args */
+  const int32_t *topo_zone;                 /* zonal domain index, -1 = no zone label */
+  const int32_t *topo_count[KS_TOPO_PROPS]; /* the node's pods with property p */
 } ks_node_cols;
 
 /* Pending pods, queue order, structure-of-arrays. */
@@ -446,6 +501,10 @@ typedef struct ks_pod_cols {
    * 0.0.0.0) */
   const uint64_t *host_ports;
   const uint64_t *host_ports_conflict;
+  /* PodTopologySpread / InterPodAffinity (ABI 8; NULL = none), see ks_topology_args */
+  const uint32_t *topo_props;               /* bit p: the pod has property p (counted where it is placed) */
+  const uint32_t *topo_flags;               /* KS_TOPO_DYN | KS_TOPO_SELF_AFFINITY | KS_TOPO_SOFT_ALL_KEYS */
+  const uint64_t *topo_term[KS_TOPO_TERMS]; /* query terms, 0 = none (the used ones first) */
 } ks_pod_cols;
 
 #define KS_JOINT_NONE 0u
@@ -581,6 +640,7 @@ typedef struct ks_node_state {
   int64_t *la_prod_term_milli_cpu;
   int64_t *la_prod_term_memory;
   uint64_t *host_ports;  /* ABI 6: NodePorts dictionary bits in use (NULL = skip) */
+  int32_t *topo_count[KS_TOPO_PROPS]; /* ABI 8: the pods with each topology property (NULL = skip) */
 } ks_node_state;
 
 typedef struct ks_stats {

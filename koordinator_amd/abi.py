@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 7
+KS_ABI_VERSION = 8
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
@@ -108,6 +108,10 @@ KS_R_NUMA_SMT = 0x1000000
 KS_R_TAINT = 0x2000000
 KS_R_NODE_AFFINITY = 0x4000000
 KS_R_NODE_PORTS = 0x8000000
+KS_R_TOPOLOGY_SPREAD = 0x10000000
+KS_R_POD_AFFINITY = 0x20000000
+KS_R_POD_ANTI_AFFINITY = 0x40000000
+KS_R_EXISTING_ANTI_AFFINITY = 0x80000000
 
 KS_S_SCHEDULED = 0x0
 KS_S_QUOTA = 0x1
@@ -124,11 +128,27 @@ KS_SCORE_DEVICESHARE = 4
 KS_SCORE_BALANCED = 5
 KS_SCORE_TAINT = 6
 KS_SCORE_NODE_AFFINITY = 7
-KS_NUM_SCORE_PLUGINS = 8
+KS_SCORE_TOPOLOGY_SPREAD = 8
+KS_SCORE_POD_AFFINITY = 9
+KS_NUM_SCORE_PLUGINS = 10
 KS_AFFINITY_TERMS = 4
 KS_LABEL_NEVER = 1 << 63
 KS_BAL_CPU = 0x1
 KS_BAL_MEMORY = 0x2
+KS_TOPO_PROPS = 16
+KS_TOPO_TERMS = 8
+KS_TOPO_ZONES = 64
+KS_TOPO_DYN = 0x1
+KS_TOPO_SELF_AFFINITY = 0x2
+KS_TOPO_SOFT_ALL_KEYS = 0x4
+KS_TOPO_K_SPREAD_HARD = 1
+KS_TOPO_K_SPREAD_SOFT = 2
+KS_TOPO_K_AFFINITY = 3
+KS_TOPO_K_ANTI = 4
+KS_TOPO_K_EXISTING_ANTI = 5
+KS_TOPO_K_SCORE = 6
+KS_TOPO_T_SELF = 0x1
+KS_TOPO_T_ELIG_ZONE = 0x2
 
 KS_RSV_UNSCHEDULABLE = 0x1
 KS_RSV_ALLOCATE_ONCE = 0x2
@@ -197,6 +217,11 @@ class KsStaticPluginArgs(C.Structure):
     _fields_ = [("enable_filter", C.c_int32), ("enable_score", C.c_int32), ("plugin_weight", C.c_int64)]
 
 
+class KsTopologyArgs(C.Structure):
+    _fields_ = [("enable", C.c_int32), ("_pad0", C.c_int32), ("spread_weight", C.c_int64),
+                ("affinity_weight", C.c_int64)]
+
+
 class KsConfig(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32),
@@ -215,6 +240,7 @@ class KsConfig(C.Structure):
         ("taint", KsStaticPluginArgs),
         ("affinity", KsStaticPluginArgs),
         ("nodeports", KsStaticPluginArgs),
+        ("topology", KsTopologyArgs),
     ]
 
 
@@ -255,6 +281,8 @@ NODE_COLS = [
     ("taints_soft", C.POINTER(C.c_uint64)),
     ("labels", C.POINTER(C.c_uint64)),
     ("host_ports", C.POINTER(C.c_uint64)),
+    ("topo_zone", P32),
+    ("topo_count", P32 * KS_TOPO_PROPS),
 ]
 
 
@@ -293,6 +321,9 @@ POD_COLS = [
     ("affinity_weight", P32 * KS_AFFINITY_TERMS),
     ("host_ports", C.POINTER(C.c_uint64)),
     ("host_ports_conflict", C.POINTER(C.c_uint64)),
+    ("topo_props", PU32),
+    ("topo_flags", PU32),
+    ("topo_term", C.POINTER(C.c_uint64) * KS_TOPO_TERMS),
 ]
 
 
@@ -403,6 +434,7 @@ NODE_STATE_COLS = [
     ("la_prod_term_milli_cpu", P64),
     ("la_prod_term_memory", P64),
     ("host_ports", C.POINTER(C.c_uint64)),
+    ("topo_count", P32 * KS_TOPO_PROPS),
 ]
 
 

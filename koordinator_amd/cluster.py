@@ -121,6 +121,9 @@ class NodeTable(_Table):
         self.alloc_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.numa_cpu_amplification = np.zeros(self.n, np.float64)  # <= 1: not amplified
+        # PodTopologySpread / InterPodAffinity (topology_plugins.compile_topology)
+        self.topo_zone = np.full(self.n, -1, np.int32)
+        self.topo_count = np.zeros((abi.KS_TOPO_PROPS, self.n), np.int32)
 
     def copy(self) -> "NodeTable":
         t = NodeTable(self.n)
@@ -129,6 +132,8 @@ class NodeTable(_Table):
         t.alloc_scalar = self.alloc_scalar.copy()
         t.req_scalar = self.req_scalar.copy()
         t.numa_cpu_amplification = self.numa_cpu_amplification.copy()
+        t.topo_zone = self.topo_zone.copy()
+        t.topo_count = self.topo_count.copy()
         return t
 
     def rows(self, idx) -> "NodeTable":
@@ -139,6 +144,8 @@ class NodeTable(_Table):
         t.alloc_scalar = np.ascontiguousarray(self.alloc_scalar[:, idx])
         t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
         t.numa_cpu_amplification = np.ascontiguousarray(self.numa_cpu_amplification[idx])
+        t.topo_zone = np.ascontiguousarray(self.topo_zone[idx])
+        t.topo_count = np.ascontiguousarray(self.topo_count[:, idx])
         return t
 
     def check_range(self) -> None:
@@ -165,6 +172,11 @@ class NodeTable(_Table):
         for k in range(abi.KS_MAX_SCALARS):
             c.alloc_scalar[k] = _p64(self.alloc_scalar[k])
             c.req_scalar[k] = _p64(self.req_scalar[k])
+        self.topo_zone = np.ascontiguousarray(self.topo_zone, np.int32)
+        self.topo_count = np.ascontiguousarray(self.topo_count, np.int32)
+        c.topo_zone = _p32(self.topo_zone)
+        for p in range(abi.KS_TOPO_PROPS):
+            c.topo_count[p] = _p32(self.topo_count[p])
         c._keep = self  # keep arrays alive with the struct
         return c
 
@@ -186,6 +198,10 @@ class PodTable(_Table):
         self.affinity_required = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.uint64)
         self.affinity_preferred = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.uint64)
         self.affinity_weight = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.int32)
+        # PodTopologySpread / InterPodAffinity (topology_plugins.compile_topology)
+        self.topo_props = np.zeros(self.n, np.uint32)
+        self.topo_flags = np.zeros(self.n, np.uint32)
+        self.topo_term = np.zeros((abi.KS_TOPO_TERMS, self.n), np.uint64)
 
     def rows(self, idx) -> "PodTable":
         idx = np.asarray(idx)
@@ -194,8 +210,10 @@ class PodTable(_Table):
             setattr(t, k, np.ascontiguousarray(v[idx]))
         t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
         t.quota_req = np.ascontiguousarray(self.quota_req[:, idx])
-        for k in ("affinity_required", "affinity_preferred", "affinity_weight"):
+        for k in ("affinity_required", "affinity_preferred", "affinity_weight", "topo_term"):
             setattr(t, k, np.ascontiguousarray(getattr(self, k)[:, idx]))
+        t.topo_props = np.ascontiguousarray(self.topo_props[idx])
+        t.topo_flags = np.ascontiguousarray(self.topo_flags[idx])
         return t
 
     def ks(self) -> abi.KsPodCols:  # noqa: C901
@@ -225,6 +243,13 @@ class PodTable(_Table):
             c.affinity_required[t] = self.affinity_required[t].ctypes.data_as(C.POINTER(C.c_uint64))
             c.affinity_preferred[t] = self.affinity_preferred[t].ctypes.data_as(C.POINTER(C.c_uint64))
             c.affinity_weight[t] = _p32(self.affinity_weight[t])
+        self.topo_props = np.ascontiguousarray(self.topo_props, np.uint32)
+        self.topo_flags = np.ascontiguousarray(self.topo_flags, np.uint32)
+        self.topo_term = np.ascontiguousarray(self.topo_term, np.uint64)
+        c.topo_props = _pu32(self.topo_props)
+        c.topo_flags = _pu32(self.topo_flags)
+        for t in range(abi.KS_TOPO_TERMS):
+            c.topo_term[t] = self.topo_term[t].ctypes.data_as(C.POINTER(C.c_uint64))
         c._keep = self
         return c
 
@@ -586,6 +611,7 @@ class NodeState:
         self.pod_count = np.zeros(n, np.int32)
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, n), np.int64)
         self.host_ports = np.zeros(n, np.uint64)
+        self.topo_count = np.zeros((abi.KS_TOPO_PROPS, n), np.int32)
 
     def ks(self) -> abi.KsNodeState:
         s = abi.KsNodeState()
@@ -595,6 +621,8 @@ class NodeState:
         s.host_ports = self.host_ports.ctypes.data_as(C.POINTER(C.c_uint64))
         for k in range(abi.KS_MAX_SCALARS):
             s.req_scalar[k] = _p64(self.req_scalar[k])
+        for p in range(abi.KS_TOPO_PROPS):
+            s.topo_count[p] = _p32(self.topo_count[p])
         s._keep = self
         return s
 
@@ -603,6 +631,7 @@ class NodeState:
         d["pod_count"] = self.pod_count
         d["req_scalar"] = self.req_scalar
         d["host_ports"] = self.host_ports
+        d["topo_count"] = self.topo_count
         return d
 
 

@@ -163,6 +163,11 @@ class SchedulerProfile:
     node_affinity: bool = False
     node_affinity_weight: int = 1
     node_ports: bool = False  # upstream NodePorts (Filter only); host ports as dictionary bits (static_plugins)
+    # upstream PodTopologySpread / InterPodAffinity (v1beta2 default profile: weights 2 and 1); the host compiles
+    # selectors and affinity terms into per-node counters and per-pod query terms (topology_plugins.compile_topology)
+    topology: bool = False
+    topology_spread_weight: int = 2
+    inter_pod_affinity_weight: int = 1
     scalar_slots: tuple = (BATCH_CPU, BATCH_MEMORY)  # scalar resource name per ks slot
     batch_pods: int = 0
     candidates: int = 0
@@ -258,6 +263,10 @@ class SchedulerProfile:
             c.affinity.plugin_weight = self.node_affinity_weight
         if self.node_ports:
             c.nodeports.enable_filter = 1
+        if self.topology:
+            c.topology.enable = 1
+            c.topology.spread_weight = self.topology_spread_weight
+            c.topology.affinity_weight = self.inter_pod_affinity_weight
         if self.reservation_weight is not None:
             c.reservation.enable = 1
             c.reservation.plugin_weight = int(self.reservation_weight)

@@ -34,6 +34,7 @@
 #include "ks_pass.h"
 #include "ks_mono.h"
 #include "ks_debug.h"
+#include "ks_topo.h"
 #include "ks_preempt.h"
 
 using namespace ks;
@@ -126,6 +127,7 @@ struct DevPodCols {
   uint32_t* cpu_bind;
   uint8_t* joint;
   uint8_t* stat_dyn;  // per pod: 1 = a TaintToleration / NodeAffinity raw score can differ between nodes (host-built)
+  const TopoRec* topo;  // PodTopologySpread / InterPodAffinity records (NULL = off)
 };
 
 // estimatedUsedByResource (estimator/default_estimator.go:73-108)
@@ -194,6 +196,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   if (r.rdma > 0) r.flags |= kPodHasGpu;
   // a normalized score that can differ between nodes: DeviceShare (device requests), TaintToleration / NodeAffinity
   if ((r.flags & kPodHasGpu) || s.stat_dyn[i]) r.flags |= kPodNormDyn;
+  if (s.topo && (s.topo[i].flags & KS_TOPO_DYN)) r.flags |= kPodTopoDyn;
   r.cpu_bind = (r.flags & KS_POD_CPU_BIND) ? ((s.cpu_bind[i] & 0x1Fu) | ((uint32_t)(r.cpu / 1000) << 8)) : 0u;
   out[i] = r;
 }
@@ -935,6 +938,11 @@ struct PodStage {
   void* h_pack = nullptr;       // pinned, kPackPods pods
   size_t pack_bytes = 0;
   size_t col8 = 0, col4 = 0;    // device column strides of this stage
+  // PodTopologySpread / InterPodAffinity (ks_topo.h): the pods' query terms; ndyn = topology pods of the stage
+  TopoRec* topo = nullptr;
+  int32_t topo_cap = 0;
+  int32_t ndyn = 0;
+  std::vector<TopoRec> h_topo;
 };
 constexpr int32_t kPackPods = 64;
 
@@ -1091,6 +1099,18 @@ struct ks_ctx {
   uint8_t* pre_status = nullptr;   // [n]
   PreemptOut* pre_out = nullptr;
   int32_t* pre_victims = nullptr;  // [kPreemptMaxPods]
+  // PodTopologySpread / InterPodAffinity (ks_topo.h): node columns in the node blob (counters mutable, zone
+  // read-only), the normalizing-weight table, the topology step's scratch and one-candidate set
+  int32_t* topo_zone = nullptr;
+  int32_t* topo_count[KS_TOPO_PROPS] = {};
+  void* topo_blob = nullptr;
+  double* topo_lw = nullptr;
+  int32_t topo_nlw = 0;
+  TopoScratch* topo_scr = nullptr;
+  uint32_t* topo_cchunk = nullptr;
+  uint2* topo_ct = nullptr;
+  int32_t* topo_ccount = nullptr;
+  uint64_t *topo_cbound = nullptr, *topo_ctop = nullptr, *topo_csecond = nullptr;
   // stats
   ks_stats stats{};
   std::vector<hipEvent_t> ev_pool;
@@ -1424,6 +1444,11 @@ void ks_destroy(ks_ctx* ctx) {
   p = ctx->pipe; dev_free(p);
   p = ctx->pipe_top; dev_free(p);
   dev_free(ctx->npod_blob);
+  dev_free(ctx->topo_blob);
+  for (PodStage* ps : {&ctx->st, &ctx->est, &ctx->ast}) {
+    void* t = ps->topo;
+    dev_free(t);
+  }
   for (int i = 0; i < kPipeEvents; ++i) {
     if (ctx->pev_sel[i]) (void)hipEventDestroy(ctx->pev_sel[i]);
     if (ctx->pev_com[i]) (void)hipEventDestroy(ctx->pev_com[i]);
@@ -1456,6 +1481,8 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.cpu_free, 4, true);
   add(&d.cpu_cores, 4, true);
   add(&d.host_ports, 8, true);
+  if (ctx->cfg.topology.enable)
+    for (int q = 0; q < KS_TOPO_PROPS; ++q) add(&ctx->topo_count[q], 4, true);
   // read-only columns
   add(&d.alloc_cpu, 8, false);
   add(&d.alloc_mem, 8, false);
@@ -1481,10 +1508,11 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.taints_hard, 8, false);
   add(&d.taints_soft, 8, false);
   add(&d.labels, 8, false);
+  if (ctx->cfg.topology.enable) add(&ctx->topo_zone, 4, false);
 }
 
 // host source pointers in the same order as build_col_table (NULL = zeros)
-static std::vector<const void*> host_cols(const ks_node_cols* c) {
+static std::vector<const void*> host_cols(const ks_node_cols* c, bool topo) {
   std::vector<const void*> v;
   v.push_back(c->req_milli_cpu);
   v.push_back(c->req_memory);
@@ -1504,6 +1532,8 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(nullptr);  // cpu_free: ks_load_cpu_state (-1 = no CPU topology)
   v.push_back(nullptr);  // cpu_cores: cores_refresh
   v.push_back(c->host_ports);
+  if (topo)
+    for (int q = 0; q < KS_TOPO_PROPS; ++q) v.push_back(c->topo_count[q]);
   v.push_back(c->alloc_milli_cpu);
   v.push_back(c->alloc_memory);
   v.push_back(c->alloc_ephemeral);
@@ -1528,6 +1558,7 @@ static std::vector<const void*> host_cols(const ks_node_cols* c) {
   v.push_back(c->taints_hard);
   v.push_back(c->taints_soft);
   v.push_back(c->labels);
+  if (topo) v.push_back(c->topo_zone);  // NULL: -1 (set after the copy)
   return v;
 }
 
@@ -1540,6 +1571,14 @@ static int check_range64(ks_ctx* ctx, const int64_t* p, int64_t n, const char* w
 }
 
 static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
+  if (ctx->cfg.topology.enable) {
+    for (int64_t i = 0; c->topo_zone && i < n; ++i)
+      if (c->topo_zone[i] < -1 || c->topo_zone[i] >= KS_TOPO_ZONES)
+        KS_FAIL(ctx, KS_EINVAL, "topo_zone[%lld]=%d outside [-1, %d)", (long long)i, c->topo_zone[i], KS_TOPO_ZONES);
+    for (int q = 0; q < KS_TOPO_PROPS; ++q)
+      for (int64_t i = 0; c->topo_count[q] && i < n; ++i)
+        if (c->topo_count[q][i] < 0) KS_FAIL(ctx, KS_EINVAL, "topo_count[%d][%lld] < 0", q, (long long)i);
+  }
   if (!c->alloc_milli_cpu || !c->alloc_memory || !c->allowed_pods || !c->req_milli_cpu || !c->req_memory ||
       !c->pod_count || !c->nonzero_milli_cpu || !c->nonzero_memory || !c->la_flags)
     KS_FAIL(ctx, KS_EINVAL, "ks_node_cols: required column missing");
@@ -1666,6 +1705,43 @@ static int numa_install(ks_ctx* ctx, const ks_numa_node_cols* nc, const uint32_t
 static int check_dev_numa(ks_ctx* ctx);
 static int numa_refresh_free(ks_ctx* ctx);
 
+// PodTopologySpread / InterPodAffinity: the topologyNormalizingWeight table log(s + 2) for every topology size a
+// pod can see (s <= nodes; the host's libm, as the oracle), the topology step's scratch and one-candidate set
+static int topo_install(ks_ctx* ctx) {
+  dev_free(ctx->topo_blob);
+  const int32_t nlw = (int32_t)ctx->n + KS_TOPO_ZONES + 2;
+  const size_t b_lw = ((size_t)nlw * 8 + 255) / 256 * 256;
+  const size_t b_scr = (sizeof(TopoScratch) + 255) / 256 * 256;
+  const size_t b_cand = (size_t)kMaxBatch * kMaxCand * (4 + 8) + (size_t)kMaxBatch * (4 + 8 * 3);
+  if (dev_alloc(ctx, &ctx->topo_blob, b_lw + b_scr + b_cand) != KS_OK) return KS_ENOMEM;
+  char* b = (char*)ctx->topo_blob;
+  HIPCHK(ctx, hipMemsetAsync(b, 0, b_lw + b_scr + b_cand, ctx->stream));
+  ctx->topo_lw = (double*)b;
+  ctx->topo_nlw = nlw;
+  ctx->topo_scr = (TopoScratch*)(b + b_lw);
+  char* c = b + b_lw + b_scr;
+  ctx->topo_ct = (uint2*)c;
+  c += (size_t)kMaxBatch * kMaxCand * 8;
+  ctx->topo_cbound = (uint64_t*)c;
+  c += kMaxBatch * 8;
+  ctx->topo_ctop = (uint64_t*)c;
+  c += kMaxBatch * 8;
+  ctx->topo_csecond = (uint64_t*)c;
+  c += kMaxBatch * 8;
+  ctx->topo_cchunk = (uint32_t*)c;
+  c += (size_t)kMaxBatch * kMaxCand * 4;
+  ctx->topo_ccount = (int32_t*)c;
+  std::vector<double> lw((size_t)nlw);
+  for (int32_t i = 0; i < nlw; ++i) lw[(size_t)i] = log((double)(i + 2));
+  HIPCHK(ctx, hipMemcpyAsync(ctx->topo_lw, lw.data(), (size_t)nlw * 8, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // (pageable source)
+  return KS_OK;
+}
+
+static DevTopo dev_topo(const ks_ctx* ctx) {
+  return DevTopo{ctx->topo_zone, ctx->topo_count[0], ctx->npad, ctx->topo_lw, ctx->topo_nlw};
+}
+
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (!ctx || !nodes || n < 0 || n >= ((int64_t)1 << 31)) return ctx ? (ctx->err = "ks_load_nodes: bad args", KS_EINVAL) : KS_EINVAL;
   if (int rc = validate_nodes(ctx, nodes, n); rc != KS_OK) return rc;
@@ -1715,7 +1791,7 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (dev_alloc(ctx, &ctx->node_blob, total) != KS_OK) return KS_ENOMEM;
   HIPCHK(ctx, hipMemsetAsync(ctx->node_blob, 0, total, ctx->stream));
   char* base = (char*)ctx->node_blob;
-  std::vector<const void*> src = host_cols(nodes);
+  std::vector<const void*> src = host_cols(nodes, ctx->cfg.topology.enable != 0);
   for (size_t i = 0; i < ctx->cols.size(); ++i) {
     *ctx->cols[i].dev = base;
     if (src[i] && n > 0)
@@ -1723,6 +1799,10 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
     base += (size_t)ctx->npad * ctx->cols[i].width;
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->d.cpu_free, 0xFF, (size_t)ctx->npad * 4, ctx->stream));  // no CPU topology yet
+  if (ctx->cfg.topology.enable) {
+    if (!nodes->topo_zone) HIPCHK(ctx, hipMemsetAsync(ctx->topo_zone, 0xFF, (size_t)ctx->npad * 4, ctx->stream));
+    if (topo_install(ctx) != KS_OK) return KS_ENOMEM;
+  }
   ctx->cpu_loaded = false;
   // two sweep outputs: patched pipelined passes sweep pass k+1 while pass k's re-sweep still reads pass k's
   if (dev_alloc(ctx, &p, (size_t)2 * ctx->nchunks * 64 * 8) != KS_OK) return KS_ENOMEM;
@@ -2620,7 +2700,7 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
       KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: duplicate node index with reservations loaded");
   }
   if (int rc = validate_nodes(ctx, rows, m); rc != KS_OK) return rc;
-  std::vector<const void*> src = host_cols(rows);
+  std::vector<const void*> src = host_cols(rows, ctx->cfg.topology.enable != 0);
   std::vector<void*> dst;
   std::vector<int32_t> widths;
   std::vector<size_t> offs;
@@ -2957,7 +3037,11 @@ static int stage_cols_packed(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, i
 
 static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t p) {
   DevPodCols& s = st.cols;
-  if (p <= kPackPods && st.col8 && !ctx->kc.stat) return stage_cols_packed(ctx, st, pc, p);
+  if (p <= kPackPods && st.col8 && !ctx->kc.stat && !ctx->cfg.topology.enable) {
+    st.cols.topo = nullptr;
+    st.ndyn = 0;
+    return stage_cols_packed(ctx, st, pc, p);
+  }
   auto cp8 = [&](int64_t* d, const int64_t* h) -> hipError_t {
     if (h) return hipMemcpyAsync(d, h, (size_t)p * 8, hipMemcpyHostToDevice, ctx->stream);
     return hipMemsetAsync(d, 0, (size_t)p * 8, ctx->stream);
@@ -2993,7 +3077,36 @@ static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t 
   else HIPCHK(ctx, hipMemsetAsync(s.cpu_bind, 0, (size_t)p * 4, ctx->stream));
   // TaintToleration / NodeAffinity: the pods' PodStat records and normalization flags, built here from the columns
   // (a pod whose raw scores are 0 on every node normalizes the same under every max: not kPodNormDyn)
-  if (ctx->kc.stat) {
+  // PodTopologySpread / InterPodAffinity: the pods' query terms (TopoRec) next to the columns
+  st.cols.topo = nullptr;
+  st.ndyn = 0;
+  if (ctx->cfg.topology.enable) {
+    if (p > st.topo_cap || !st.topo) {
+      void* t = st.topo;
+      dev_free(t);
+      st.topo = nullptr;
+      st.topo_cap = 0;
+      const int32_t cap = std::max<int32_t>(p, 64);
+      if (dev_alloc(ctx, &t, (size_t)cap * sizeof(TopoRec)) != KS_OK) return KS_ENOMEM;
+      st.topo = (TopoRec*)t;
+      st.topo_cap = cap;
+    }
+    std::vector<TopoRec>& ht = st.h_topo;
+    ht.assign((size_t)p, TopoRec{});
+    for (int32_t i = 0; i < p; ++i) {
+      TopoRec& r = ht[(size_t)i];
+      r.props = pc->topo_props ? pc->topo_props[i] : 0;
+      r.flags = pc->topo_flags ? pc->topo_flags[i] : 0;
+      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+        r.term[t] = pc->topo_term[t] ? pc->topo_term[t][i] : 0;
+        r.nterms += r.term[t] != 0;
+      }
+      st.ndyn += (r.flags & KS_TOPO_DYN) ? 1 : 0;
+    }
+    if (p > 0) HIPCHK(ctx, hipMemcpyAsync(st.topo, ht.data(), (size_t)p * sizeof(TopoRec), hipMemcpyHostToDevice, ctx->stream));
+    st.cols.topo = st.topo;
+  }
+  if (ctx->kc.stat || ctx->cfg.topology.enable) {
     std::vector<PodStat>& hs = st.h_stat;
     std::vector<uint8_t>& hd = st.h_dyn;
     hs.assign((size_t)p, PodStat{});
@@ -3016,6 +3129,8 @@ static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t 
     if (p > 0) {
       HIPCHK(ctx, hipMemcpyAsync(st.stat, hs.data(), (size_t)p * sizeof(PodStat), hipMemcpyHostToDevice, ctx->stream));
       HIPCHK(ctx, hipMemcpyAsync(s.stat_dyn, hd.data(), (size_t)p, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (p > 0) {
       HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // pageable sources
     }
   } else {
@@ -3035,6 +3150,17 @@ static int prep_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
 }
 
 static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
+  for (int t = 0; ctx->cfg.topology.enable && t < KS_TOPO_TERMS; ++t)
+    for (int32_t i = 0; pc->topo_term[t] && i < p; ++i) {
+      const uint64_t w = pc->topo_term[t][i];
+      if (!w) continue;
+      const int kind = (int)(w & 0xFF), prop = (int)((w >> 8) & 0xFF), key = (int)((w >> 16) & 0xFF);
+      const int32_t param = (int32_t)(uint32_t)(w >> 32);
+      if (kind < KS_TOPO_K_SPREAD_HARD || kind > KS_TOPO_K_SCORE || prop >= KS_TOPO_PROPS || key > 1 ||
+          ((kind == KS_TOPO_K_SPREAD_HARD || kind == KS_TOPO_K_SPREAD_SOFT) && param < 1) ||
+          (kind == KS_TOPO_K_SCORE && (param < -1000000 || param > 1000000)))
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: topology term %d (%#llx) malformed", i, t, (unsigned long long)w);
+    }
   for (int32_t i = 0; pc->flags && i < p; ++i)
     if (pc->flags[i] & KS_POD_UNMODELLED)
       KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: requests the library does not model (FPGA, DeviceShare allocate hints, "
@@ -3293,6 +3419,12 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.pipe_after = nullptr;
   ca.top_reset = nullptr;
   ca.pre_rsv = nullptr;
+  ca.topo = ctx->cfg.topology.enable && st.topo ? 1 : 0;
+  ca.topo_const = (int32_t)(100 * ctx->cfg.topology.spread_weight);
+  ca.topo_rec = st.topo;
+  ca.topo_count = ctx->topo_count[0];
+  ca.topo_npad = ctx->npad;
+  ca.topo_best = ctx->topo_scr ? &ctx->topo_scr->best_total : nullptr;
   *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
                         ctx->q.q, kernel_feat(ctx) == 0, commit_hint_variant(ctx)).total;
   return ca;
@@ -3371,6 +3503,7 @@ static bool pipelined(const ks_ctx* ctx) {
   const int64_t mode = ctx->pipe_mode >= 0 ? ctx->pipe_mode : env_pipe;
   const int feat = kernel_feat(ctx);
   if (mode == 0 || !(feat == 0 || feat == 1) || ctx->kc.dev || ctx->kc.cores) return false;
+  if (ctx->cfg.topology.enable && ctx->st.ndyn > 0) return false;  // topology pods: the topology step between passes
   return mode == 2 || ctx->n >= env_min;
 }
 
@@ -3559,6 +3692,114 @@ struct PipeShape {
   bool patch;  // monotone plugin sets: select before the previous commit ends, re-evaluate the listed chunks after
 };
 
+// The per-node outputs of one pod's full evaluation (ks_eval_pod, the topology step) in a scratch buffer that lives
+// with the context (grown, never freed per call): reasons, the per-plugin score matrix, totals, raw scores
+struct EvBuf {
+  uint32_t* dr;
+  int64_t *ds, *dt;
+  int32_t *draw, *dhi, *ddraw, *dtraw, *daraw;
+};
+static int ev_buffers(ks_ctx* ctx, EvBuf& b) {
+  const int64_t n = ctx->n;
+  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4 + 8) + 64;
+  if (ctx->evbuf_bytes < bytes) {
+    dev_free(ctx->evbuf);
+    ctx->evbuf_bytes = 0;
+    if (dev_alloc(ctx, &ctx->evbuf, bytes) != KS_OK) return KS_ENOMEM;
+    ctx->evbuf_bytes = bytes;
+  }
+  void* buf = ctx->evbuf;
+  b.dr = (uint32_t*)buf;
+  b.ds = (int64_t*)((char*)buf + ((size_t)n * 4 + 15) / 16 * 16);
+  b.dt = b.ds + (size_t)n * KS_NUM_SCORE_PLUGINS;
+  b.draw = (int32_t*)(b.dt + n);
+  b.dhi = b.draw + n;
+  b.ddraw = b.dhi + n;
+  b.dtraw = b.ddraw + n;
+  b.daraw = b.dtraw + n;
+  return KS_OK;
+}
+
+// The topology kernels' arguments for stage st: the pod at *cursor (the batch step) or pod 0 (cursor NULL,
+// ks_eval_pod)
+static TopoKArgs topo_args(ks_ctx* ctx, PodStage& st, const int32_t* cursor, const EvBuf& eb) {
+  TopoKArgs a{};
+  a.t = dev_topo(ctx);
+  a.labels = ctx->d.labels;
+  a.recs = st.recs;
+  a.stat = st.stat;
+  a.trec = st.topo;
+  a.cursor = cursor;
+  a.total_pods = cursor ? ctx->np : 1;
+  a.n = ctx->n;
+  a.reasons = eb.dr;
+  a.scores = eb.ds;
+  a.total = eb.dt;
+  a.rraw = eb.draw;
+  a.rhi = eb.dhi;
+  a.draw = eb.ddraw;
+  a.traw = eb.dtraw;
+  a.araw = eb.daraw;
+  a.norm_others = cursor ? 1 : 0;
+  a.dev_on = ctx->kc.dev;
+  a.taint_on = (ctx->kc.taint & 2) != 0;
+  a.aff_on = (ctx->kc.aff & 2) != 0;
+  a.rsv_on = ctx->kc.rsv;
+  a.dev_w = ctx->cfg.deviceshare.plugin_weight;
+  a.taint_w = ctx->cfg.taint.plugin_weight;
+  a.aff_w = ctx->cfg.affinity.plugin_weight;
+  a.rsv_w = ctx->cfg.reservation.plugin_weight;
+  a.spread_w = ctx->cfg.topology.spread_weight;
+  a.ipa_w = ctx->cfg.topology.affinity_weight;
+  a.scr = ctx->topo_scr;
+  a.cand_chunk = ctx->topo_cchunk;
+  a.cand_t = ctx->topo_ct;
+  a.cand_count = ctx->topo_ccount;
+  a.cand_bound = ctx->topo_cbound;
+  a.cand_top = ctx->topo_ctop;
+  a.cand_second = ctx->topo_csecond;
+  return a;
+}
+
+// the pass's CPU ids (cores mode): exact per-node core counts for the next sweep (Cfg.cores)
+static int cores_pass_refresh(ks_ctx* ctx) {
+  if (!(ctx->kc.cores && ctx->cpu_loaded)) return KS_OK;
+  hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
+                     (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
+                     (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
+                     ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED),
+                     numa_words(ctx), ctx->nv.npad, ctx->n);
+  HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
+  return KS_OK;
+}
+
+// The topology step (ks_topo.h): when the pod at the cursor is a topology pod, every plugin's Filter / Score on every
+// node, the two plugins' PreFilter / Filter / PreScore / Score and every normalization, selectHost, and the commit of
+// that one pod on the chosen node (admission, every Reserve, the counters); otherwise every kernel returns at once.
+static int topo_step(ks_ctx* ctx) {
+  EvBuf eb;
+  if (ev_buffers(ctx, eb) != KS_OK) return KS_ENOMEM;
+  const int64_t n = ctx->n;
+  HIPCHK(ctx, launch_eval_debug(ctx->nsc, (int)((n + 255) / 256), ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv,
+                                ctx->kc, ctx->st.recs, n, eb.dr, eb.ds, eb.dt, eb.draw, eb.dhi, eb.ddraw, ctx->st.stat,
+                                eb.dtraw, eb.daraw, ctx->cursor, ctx->st.topo, ctx->np));
+  const TopoKArgs ta = topo_args(ctx, ctx->st, ctx->cursor, eb);
+  HIPCHK(ctx, launch_topo_filter(ctx->stream, ta));
+  HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
+  bool qcache = false;
+  size_t smem = 0;
+  CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, 1, &qcache, &smem);
+  ca.topo = 2;
+  ca.cand_chunk = ctx->topo_cchunk;
+  ca.cand_t = ctx->topo_ct;
+  ca.cand_count = ctx->topo_ccount;
+  ca.cand_bound = ctx->topo_cbound;
+  ca.cand_top = ctx->topo_ctop;
+  ca.cand_second = ctx->topo_csecond;
+  HIPCHK(ctx, pass_launcher(kernel_feat(ctx), ctx->nsc).commit(qcache, smem, ctx->stream, ca));
+  return cores_pass_refresh(ctx);
+}
+
 template <int NSC>
 static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeShape* pipe,
                        std::vector<std::pair<int, size_t>>* evs, size_t* evn) {
@@ -3585,6 +3826,12 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
     evs->push_back({kind, (*evn)++});
   };
   auto shard_lo = [&](int32_t sh) { return ctx->nchunks * sh / S; };
+  if (ctx->cfg.topology.enable && ctx->st.ndyn > 0 && !pipe) {
+    // a topology pod at the cursor is scheduled alone first (timed with the commits)
+    rec(2, ctx->stream);
+    if (int rc = topo_step(ctx); rc != KS_OK) return rc;
+    rec(2, ctx->stream);
+  }
   SweepArgs sa;
   sa.dn = ctx->dnodes;
   sa.rv = ctx->drv;
@@ -3774,16 +4021,8 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   rec(2, cs);
   if (pipe) HIPCHK(ctx, hipEventRecord(ctx->pev_com[k % kPipeEvents], cs));
   ctx->pipe_k = k + 1;
-  if (ctx->kc.cores && ctx->cpu_loaded) {
-    // the pass's CPU ids now, so that the next sweep sees exact per-node core counts (Cfg.cores)
-    hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
-                       (const int2*)ctx->cpuset_list, (const int32_t*)ctx->cpuset_n, (const uint32_t*)ctx->cpuset_split,
-                       (const PodRec*)ctx->st.recs, ctx->cpuset_out, (const uint32_t*)ctx->d.numa_flags,
-                       ctx->d.cpu_cores, (int32_t)(ctx->cfg.numa.numa_scoring_strategy == KS_MOST_ALLOCATED),
-                       numa_words(ctx), ctx->nv.npad, ctx->n);
-    HIPCHK(ctx, hipMemsetAsync(ctx->cpuset_n, 0, 4, ctx->stream));
-  }
-  return KS_OK;
+  // the pass's CPU ids now, so that the next sweep sees exact per-node core counts (Cfg.cores)
+  return cores_pass_refresh(ctx);
 }
 
 static int schedule_staged_impl(ks_ctx* ctx) {
@@ -4226,28 +4465,25 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
   if (ensure_stage(ctx, ctx->est, 1) != KS_OK) return KS_ENOMEM;
   if (stage_cols(ctx, ctx->est, pod, 1) != KS_OK || prep_stage(ctx, ctx->est, 1) != KS_OK) return KS_EHIP;
   const int64_t n = ctx->n;
-  // the per-node outputs in a scratch buffer that lives with the context (grown, never freed per call)
-  const size_t bytes = (size_t)(n > 0 ? n : 1) * (4 + 8 * KS_NUM_SCORE_PLUGINS + 8 + 8 + 4 + 8) + 64;
-  if (ctx->evbuf_bytes < bytes) {
-    dev_free(ctx->evbuf);
-    ctx->evbuf_bytes = 0;
-    if (dev_alloc(ctx, &ctx->evbuf, bytes) != KS_OK) return KS_ENOMEM;
-    ctx->evbuf_bytes = bytes;
-  }
-  void* buf = ctx->evbuf;
-  uint32_t* dr = (uint32_t*)buf;
-  int64_t* ds = (int64_t*)((char*)buf + ((size_t)n * 4 + 15) / 16 * 16);
-  int64_t* dt = ds + (size_t)n * KS_NUM_SCORE_PLUGINS;
-  int32_t* draw = (int32_t*)(dt + n);
-  int32_t* dhi = draw + n;
-  int32_t* ddraw = dhi + n;
-  int32_t* dtraw = ddraw + n;
-  int32_t* daraw = dtraw + n;
+  EvBuf eb;
+  if (ev_buffers(ctx, eb) != KS_OK) return KS_ENOMEM;
+  uint32_t* dr = eb.dr;
+  int64_t* ds = eb.ds;
+  int64_t* dt = eb.dt;
+  int32_t *draw = eb.draw, *dhi = eb.dhi, *ddraw = eb.ddraw, *dtraw = eb.dtraw, *daraw = eb.daraw;
   const int threads = 256;
   const int blocks = (int)((n + threads - 1) / threads);
   if (blocks > 0) {
     HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
                                   ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw));
+    // PodTopologySpread / InterPodAffinity: their Filters before every normalization (which run over the nodes all
+    // Filters leave), their scores after
+    TopoKArgs ta{};
+    const bool topo = ctx->cfg.topology.enable && ctx->est.topo;
+    if (topo) {
+      ta = topo_args(ctx, ctx->est, nullptr, eb);
+      HIPCHK(ctx, launch_topo_filter(ctx->stream, ta));
+    }
     if (ctx->kc.dev)
       hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,
                          ctx->cfg.deviceshare.plugin_weight);
@@ -4260,6 +4496,7 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
     if (ctx->kc.rsv)
       hipLaunchKernelGGL(rsv_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, draw, dhi, ds, dt,
                          ctx->cfg.reservation.plugin_weight);
+    if (topo) HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
   }
   HIPCHK(ctx, hipGetLastError());
   if (reasons && n) HIPCHK(ctx, hipMemcpyAsync(reasons, dr, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -4291,6 +4528,9 @@ struct UnreserveArgs {
   const uint64_t* cpuset;  // [KS_CPU_WORDS] the pod's CPUs
   const int64_t* nalloc;   // [2][kNumaDev] its NUMA-node allocation (cpu milli, memory)
   int32_t quota, dev, cpu_loaded, numa_pol, ratio_amp;
+  const TopoRec* topo;     // PodTopologySpread / InterPodAffinity: the pod's properties leave the node's counters
+  int32_t* topo_count;
+  int64_t topo_npad;
 };
 
 __global__ void unreserve_kernel(UnreserveArgs a) {
@@ -4324,6 +4564,9 @@ __global__ void unreserve_kernel(UnreserveArgs a) {
   }
   // NodeInfo.RemovePod: the pod's host ports (a used entry conflicts with itself, so no other pod holds it)
   if (a.c.ports & 1) d.host_ports[n] &= ~a.pstat[0].pwant;
+  if (a.topo)
+    for (uint32_t m = a.topo[0].props; m; m &= m - 1u)
+      a.topo_count[(int64_t)(__ffs((int)m) - 1) * a.topo_npad + n] -= 1;
   // reservationCache.forgetPod: Allocated -= Mask(requests, ResourceNames); the pod leaves the assigned set
   if (a.gi >= 0) {
     const uint32_t keys = rsv_keys(a.rv.meta[a.gi]);
@@ -4433,6 +4676,7 @@ int ks_assume(ks_ctx* ctx, const ks_pod_cols* pod, int32_t node, ks_result* out,
   size_t smem = 0;
   CommitArgs ca = commit_args(ctx, ctx->ast, 1, 1, &qcache, &smem);
   ca.force = 1;
+  if (ca.topo) ca.topo = 3;  // count the pod's properties on the node
   HIPCHK(ctx, pass_launcher(kernel_feat(ctx), ctx->nsc).commit(qcache, smem, ctx->stream, ca));
   if (ctx->cpu_loaded && ctx->n > 0) {
     hipLaunchKernelGGL(cpuset_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->cpu,
@@ -4522,6 +4766,9 @@ int ks_unreserve(ks_ctx* ctx, const ks_pod_cols* pod, const ks_result* r, const 
   ua.cpu_loaded = ctx->cpu_loaded;
   ua.numa_pol = ctx->kc.numa_pol && ctx->numa_blob;
   ua.ratio_amp = ctx->cfg.numa.enable;
+  ua.topo = ctx->cfg.topology.enable ? ctx->ast.topo : nullptr;
+  ua.topo_count = ctx->topo_count[0];
+  ua.topo_npad = ctx->npad;
   hipLaunchKernelGGL(unreserve_kernel, dim3(1), dim3(64), 0, ctx->stream, ua);
   HIPCHK(ctx, hipGetLastError());
   if (rb && rsv_launch_base(ctx, d_idx, 1, +1, 1) != KS_OK) return KS_EHIP;
@@ -4587,6 +4834,7 @@ int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
   HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, v.la_pterm_cpu, 8));
   HIPCHK(ctx, cp(o->la_prod_term_memory, v.la_pterm_mem, 8));
   HIPCHK(ctx, cp(o->host_ports, v.host_ports, 8));
+  for (int q = 0; ctx->cfg.topology.enable && q < KS_TOPO_PROPS; ++q) HIPCHK(ctx, cp(o->topo_count[q], ctx->topo_count[q], 4));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -4729,6 +4977,9 @@ int ks_preempt(ks_ctx* ctx, const ks_pod_cols* pod, int32_t priority, uint32_t f
     KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_preempt: the pod has no quota row (the reference's cloned PostFilterState has no "
                                   "QuotaInfo then)");
   if (nominated < -1 || nominated >= ctx->n) KS_FAIL(ctx, KS_EINVAL, "ks_preempt: nominated node %d out of range", nominated);
+  if (ctx->cfg.topology.enable && pod->topo_flags && (pod->topo_flags[0] & KS_TOPO_DYN))
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_preempt: the dry runs do not model PodTopologySpread / InterPodAffinity (the pod "
+                                  "has topology terms)");
   if (int rc = validate_pods(ctx, pod, 1); rc != KS_OK) return rc;
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ensure_stage(ctx, ctx->est, 1) != KS_OK) return KS_ENOMEM;
@@ -4832,6 +5083,8 @@ int ks_shard_init(ks_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* uniq
   if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || virtual_shards < 1 || nranks * virtual_shards > 1024)
     return ctx ? (ctx->err = "ks_shard_init: bad args", KS_EINVAL) : KS_EINVAL;
   if (nranks > 1 && !unique_id) KS_FAIL(ctx, KS_EINVAL, "ks_shard_init: nranks > 1 needs the rank-0 unique id");
+  if (nranks > 1 && ctx->cfg.topology.enable)
+    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_shard_init: PodTopologySpread / InterPodAffinity need every node on one rank");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ctx->comm) {
     (void)ncclCommDestroy(ctx->comm);
@@ -4860,6 +5113,8 @@ int ks_shard_init_loopback(ks_ctx* const* ctxs, int32_t nranks, int32_t virtual_
       if (ctxs[q] == ctxs[r]) KS_FAIL(ctxs[r], KS_EINVAL, "ks_shard_init_loopback: a context is given twice");
     if (ctxs[r]->n != ctxs[0]->n || ctxs[r]->k != ctxs[0]->k || ctxs[r]->batch != ctxs[0]->batch)
       KS_FAIL(ctxs[r], KS_EINVAL, "ks_shard_init_loopback: the ranks must load the same node count, batch and candidates");
+    if (ctxs[r]->cfg.topology.enable)
+      KS_FAIL(ctxs[r], KS_EUNSUPPORTED, "ks_shard_init_loopback: PodTopologySpread / InterPodAffinity need every node on one rank");
   }
   LoopGroup* g = new LoopGroup();
   g->n = nranks;

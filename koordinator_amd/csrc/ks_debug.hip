@@ -2,6 +2,7 @@
 // every node, no Reserve), in its own translation unit.
 #include "ks_pass.h"
 #include "ks_debug.h"
+#include "ks_topo.h"
 
 namespace ks {
 // ------------------------------------------------------------------------------------------
@@ -11,12 +12,20 @@ namespace ks {
 template <int NSC>
 __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n,
                                   uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
-                                  int32_t* draw, const PodStat* pstat, int32_t* traw, int32_t* araw) {
+                                  int32_t* draw, const PodStat* pstat, int32_t* traw, int32_t* araw,
+                                  const int32_t* cursor, const TopoRec* trec, int32_t total_pods) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // the topology step (ks_topo.h): the pod at the cursor, only if it is a topology pod
+  int64_t pi = 0;
+  if (cursor) {
+    pi = *cursor;
+    if (pi >= total_pods || !(trec[pi].flags & KS_TOPO_DYN)) return;
+  }
   NodeReg<NSC> r;
   load_node<NSC>(c, d, i, 1, r);
-  const PodRec p = *pod;
+  const PodRec p = pod[pi];
+  if (pstat) pstat += pi;
   RsvOut ro;
   EvalOut o = eval_full<NSC, true, false, 15>(
       c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
@@ -40,19 +49,22 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TAINT] = 0;
   scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = 0;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TOPOLOGY_SPREAD] = 0;
+  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_POD_AFFINITY] = 0;
 }
 
 
 hipError_t launch_eval_debug(int nsc, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,
                              const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
                              int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw,
-                             const PodStat* pstat, int32_t* traw, int32_t* araw) {
+                             const PodStat* pstat, int32_t* traw, int32_t* araw, const int32_t* cursor,
+                             const TopoRec* trec, int32_t total_pods) {
   if (nsc == 0)
-    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw);
+    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, cursor, trec, total_pods);
   else if (nsc == 2)
-    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw);
+    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, cursor, trec, total_pods);
   else
-    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw);
+    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, cursor, trec, total_pods);
   return hipGetLastError();
 }
 

@@ -208,7 +208,8 @@ __global__ __launch_bounds__(commit_threads(0)) void commit_mono_kernel(CommitAr
     return;
   }
   if (pipe_bubble(a, cursor0)) return;
-  const int32_t np = min(a.batch, a.total_pods - cursor0);
+  const int32_t np = topo_pass_pods(a, cursor0, min(a.batch, a.total_pods - cursor0));
+  if (np == 0) return;  // a topology pod at the cursor: the next topology step takes it
   const Cfg cfg = a.c;
 #if defined(KS_COMMIT_SEG) && !defined(KS_COMMIT_CAT)
 #define KS_COMMIT_CAT
@@ -544,7 +545,11 @@ __global__ __launch_bounds__(commit_threads(0)) void commit_mono_kernel(CommitAr
 #endif
   }
   // ---- write back: results, touched rows, quota usage ----
-  if (lane < processed) a.results[cursor0 + lane] = sres[lane];
+  if (lane < processed) {
+    ks_result r = sres[lane];
+    topo_writeback(a, cursor0 + lane, r);
+    a.results[cursor0 + lane] = r;
+  }
   if (lane < nslots) {
     const DevNodes d = *a.dn;
     const MonoRow& m = rows[srow];

@@ -13,6 +13,7 @@
 #include "ks_dev.h"
 #include "ks_cpuset.h"
 #include "ks_numa.h"
+#include "ks_topo.h"
 
 namespace ks {
 
@@ -371,6 +372,14 @@ struct CommitArgs {
   // NUMA topology policy variants: Reserve's NodeNUMAResource / DeviceShare allocations on each pod's snapshot-best
   // nodes, computed before the commit by reserve_pre_kernel ([64][kPreRsvM]); NULL = the commit computes every Reserve
   const struct PreRsv* pre_rsv;
+  // PodTopologySpread / InterPodAffinity (ks_topo.h): 0 off; 1 the pass ends before its first topology pod; 2 the
+  // topology step's one-pod commit; 3 ks_assume.  Every placed pod's properties are counted on its node.
+  int32_t topo;
+  int32_t topo_const;        // 100 x the PodTopologySpread weight: the score of a pod without query terms
+  const TopoRec* topo_rec;   // [pod] queue order
+  int32_t* topo_count;       // [KS_TOPO_PROPS][topo_npad]
+  int64_t topo_npad;
+  const int64_t* topo_best;  // mode 2: the topology step's total of the chosen node
 };
 
 // One pod's NodeNUMAResource + DeviceShare Reserve on one node of its snapshot ranking, computed on the snapshot state
@@ -785,7 +794,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     return;
   }
   if (pipe_bubble(a, cursor0)) return;
-  const int32_t np = min(a.batch, a.total_pods - cursor0);
+  const int32_t np = topo_pass_pods(a, cursor0, min(a.batch, a.total_pods - cursor0));
+  if (np == 0) return;  // a topology pod at the cursor: the next topology step takes it
 #ifdef KS_COMMIT_STAMPS
   uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tlast = __builtin_amdgcn_s_memtime();
@@ -1856,6 +1866,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   if (lane < processed) {
     ks_result r = sres[lane];
     if (RSV && r.reservation >= 0) r.reservation = a.rv->rowid[r.reservation];
+    topo_writeback(a, cursor0 + lane, r);
     a.results[cursor0 + lane] = r;
   }
   if (lane < nslots) {

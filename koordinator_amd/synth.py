@@ -634,6 +634,93 @@ def with_static_plugins(w: Workload, seed: int = SEED + 7, weight_taint: int = 1
     return w
 
 
+def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node=(0, 6), n_zones: int = 8,
+                   unzoned_frac: float = 0.1, spread_frac: float = 0.2, default_frac: float = 0.25,
+                   anti_frac: float = 0.08, affinity_frac: float = 0.06, pref_frac: float = 0.12):
+    """Zone labels (n_zones zones, unzoned_frac of the nodes without one), running pods (per_node) and pending pods
+    for the upstream PodTopologySpread / InterPodAffinity plugins (topology_plugins): four apps in namespace
+    "default" plus app-A pods in namespace "other"; pending pods with their own spread constraints (hostname / zone,
+    DoNotSchedule / ScheduleAnyway, skews 1-3), the system default constraints (an owner selector), a required
+    anti-affinity to app A per hostname, a required affinity to app D per zone, preferred (anti-)affinity terms;
+    running pods that carry the same terms, a few terminating.  Returns (node_labels, existing, pending)."""
+    from .topology_plugins import (HOSTNAME, SCHEDULE_ANYWAY, DO_NOT_SCHEDULE, ZONE, AffinityTerm, LabelSelector,
+                                   SpreadConstraint, TopoPod)
+    apps = ["A", "B", "C", "D"]
+    sel = {a: LabelSelector((("app", a),)) for a in apps}
+    anti_a = AffinityTerm(HOSTNAME, sel["A"])
+    aff_d = AffinityTerm(ZONE, sel["D"])
+    pref_c = (20, AffinityTerm(HOSTNAME, sel["C"]))
+    pref_b = (30, AffinityTerm(ZONE, sel["B"]))
+    node_labels = []
+    for i in range(n_nodes):
+        lab = {}
+        if rng.random() >= unzoned_frac:
+            lab[ZONE] = f"zone-{int(rng.integers(0, n_zones))}"
+        node_labels.append(lab)
+
+    def app_pod(ns="default"):
+        a = apps[int(rng.integers(0, len(apps)))]
+        return TopoPod(namespace=ns, labels={"app": a, "tier": str(rng.choice(["web", "batch"]))})
+
+    existing = []
+    for i in range(n_nodes):
+        for _ in range(int(rng.integers(per_node[0], per_node[1] + 1))):
+            p = app_pod("other" if rng.random() < 0.1 else "default")
+            p.terminating = rng.random() < 0.03
+            u = rng.random()
+            if u < 0.05 and p.namespace == "default":
+                p.anti_required = [anti_a]
+            elif u < 0.1 and p.namespace == "default":
+                p.affinity_required = [aff_d]
+            elif u < 0.16 and p.namespace == "default":
+                p.affinity_preferred = [pref_c]
+            elif u < 0.2 and p.namespace == "default":
+                p.anti_preferred = [pref_b]
+            existing.append((i, p))
+    pending = []
+    for i in range(n_pods):
+        p = app_pod("other" if rng.random() < 0.05 else "default")
+        u = rng.random()
+        own = LabelSelector((("app", p.labels["app"]),))
+        if u < spread_frac:
+            # (the API rejects two constraints with the same topologyKey and whenUnsatisfiable)
+            for key in ([HOSTNAME, ZONE] if rng.random() < 0.4 else [[HOSTNAME, ZONE][int(rng.integers(0, 2))]]):
+                when = DO_NOT_SCHEDULE if rng.random() < 0.5 else SCHEDULE_ANYWAY
+                s = own if rng.random() < 0.9 else sel[apps[int(rng.integers(0, 4))]]
+                p.spread.append(SpreadConstraint(int(rng.integers(1, 4)), key, when, s))
+        elif u < spread_frac + default_frac:
+            p.default_selector = own
+        u = rng.random()
+        if p.namespace == "default":
+            if u < anti_frac:
+                p.anti_required = [anti_a]
+            elif u < anti_frac + affinity_frac:
+                p.affinity_required = [aff_d]
+            elif u < anti_frac + affinity_frac + pref_frac and not p.spread:
+                if rng.random() < 0.5:
+                    p.affinity_preferred = [pref_c]
+                else:
+                    p.anti_preferred = [pref_b]
+        pending.append(p)
+    return node_labels, existing, pending
+
+
+def with_topology(w: Workload, seed: int = SEED + 8, spread_weight: int = 2, affinity_weight: int = 1,
+                  **kw) -> Workload:
+    """The workload with upstream PodTopologySpread and InterPodAffinity switched on and topology_specs compiled into
+    the node counters and pod query terms (topology_plugins.compile_topology); w.topo keeps the objects."""
+    from .topology_plugins import compile_topology, install
+    rng = np.random.Generator(np.random.PCG64(seed))
+    node_labels, existing, pending = topology_specs(w.nodes.n, w.pods.n, rng, **kw)
+    c = compile_topology(node_labels, existing, pending)
+    install(c, w.nodes, w.pods)
+    w.profile.topology = True
+    w.profile.topology_spread_weight = spread_weight
+    w.profile.inter_pod_affinity_weight = affinity_weight
+    w.topo = (node_labels, existing, pending)
+    return w
+
+
 def c3_full(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, n_quotas: int = 32, **kw) -> Workload:
     """C3 (NUMA topology policies, cpuset pods, GPU / RDMA devices) under the rest of the shipped profile as well:
     ElasticQuota (32 leaf quotas) and the v1beta2 default plugins TaintToleration, NodeAffinity and NodePorts -- the

@@ -1,0 +1,309 @@
+"""Host side of the upstream PodTopologySpread and InterPodAffinity plugins (kube-scheduler v1.24.15
+``plugins/podtopologyspread``, ``plugins/interpodaffinity``; the v1beta2 default profile enables both, weights 2 and
+1, and appends them to every koord-scheduler profile through ``defaultprofile.AppendDefaultPlugins``).
+
+Both plugins count *pods* per topology domain.  The label selector work -- which pods match which selector or affinity
+term -- runs here, once per distinct selector / term, and reaches the device as (``include/koordgpu.h``
+``ks_topology_args``):
+
+* properties (<= KS_TOPO_PROPS): predicates on pods.  ``sel``: in namespace ns, not terminating, matching a spread
+  constraint's selector (``countPodsMatchSelector``); ``term``: matching an affinity term (its namespaces and
+  selector, ``AffinityTerm.Matches``); ``all``: matching every required affinity term of one pod
+  (``podMatchesAllAffinityTerms``); ``carry``: carrying one required anti-affinity term, or one hard / preferred
+  (anti-)affinity term with its score weight.  Every node holds, per property, the number of its pods that have it
+  (``ks_node_cols.topo_count``, updated by every Reserve); every pod lists the properties it has
+  (``ks_pod_cols.topo_props``).
+* topology keys: the hostname (every node is its own domain) and one zonal key (``ks_node_cols.topo_zone``: the
+  node's zone index, -1 when the label is absent).
+* per pod <= KS_TOPO_TERMS query terms (``ks_pod_cols.topo_term``): what PreFilter / Filter / PreScore / Score of the
+  two plugins ask of the counters -- spread constraints (hard and soft, the system default constraints included),
+  required affinity / anti-affinity, the existing pods' anti-affinity terms that match the pod, and the score terms
+  (the pod's preferred terms, the existing pods' hard and preferred terms that match it, with their weights).
+
+A pod with no query term scores the constant 100 (PodTopologySpread's NormalizeScore with no constraint) and 0
+(InterPodAffinity) everywhere and never fails their Filters; the others are *topology pods* (KS_TOPO_DYN) and the
+device schedules each of them as the first pod of its pass.
+
+``oracle/topology_ref.py`` restates both plugins directly on these objects; the tests check that both agree.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi
+from .static_plugins import PodAffinitySpec, StaticPluginError
+
+HOSTNAME = "kubernetes.io/hostname"
+ZONE = "topology.kubernetes.io/zone"
+DO_NOT_SCHEDULE = "DoNotSchedule"
+SCHEDULE_ANYWAY = "ScheduleAnyway"
+SELECTOR_OPS = ("In", "NotIn", "Exists", "DoesNotExist")
+
+
+@dataclass(frozen=True)
+class LabelSelector:
+    """metav1.LabelSelector: matchLabels AND matchExpressions (In / NotIn / Exists / DoesNotExist)."""
+    match_labels: Tuple[Tuple[str, str], ...] = ()
+    match_expressions: Tuple[Tuple[str, str, Tuple[str, ...]], ...] = ()
+
+
+@dataclass(frozen=True)
+class SpreadConstraint:
+    max_skew: int
+    topology_key: str
+    when_unsatisfiable: str = DO_NOT_SCHEDULE
+    selector: Optional[LabelSelector] = None  # nil: matches nothing (LabelSelectorAsSelector(nil) = labels.Nothing())
+
+
+@dataclass(frozen=True)
+class AffinityTerm:
+    """PodAffinityTerm without a namespaceSelector: namespaces () = the owning pod's namespace."""
+    topology_key: str
+    selector: Optional[LabelSelector] = None
+    namespaces: Tuple[str, ...] = ()
+
+
+@dataclass
+class TopoPod:
+    """The parts of a pod the two plugins read."""
+    namespace: str = "default"
+    labels: Dict[str, str] = field(default_factory=dict)
+    terminating: bool = False  # DeletionTimestamp != nil (countPodsMatchSelector skips it)
+    spread: List[SpreadConstraint] = field(default_factory=list)
+    # the selector helper.DefaultSelector builds from the services / RCs / RSs / StatefulSets selecting the pod
+    # (None = none: no system default constraints)
+    default_selector: Optional[LabelSelector] = None
+    affinity_required: List[AffinityTerm] = field(default_factory=list)
+    affinity_preferred: List[Tuple[int, AffinityTerm]] = field(default_factory=list)
+    anti_required: List[AffinityTerm] = field(default_factory=list)
+    anti_preferred: List[Tuple[int, AffinityTerm]] = field(default_factory=list)
+    node_affinity: Optional[PodAffinitySpec] = None  # nodeSelector / required node affinity (spreading eligibility)
+
+
+# v1.24 podtopologyspread systemDefaultConstraints (plugins/podtopologyspread/plugin.go)
+SYSTEM_DEFAULT_CONSTRAINTS = ((HOSTNAME, 3), (ZONE, 5))
+
+
+def selector_matches(sel: Optional[LabelSelector], labels: Dict[str, str]) -> bool:
+    """labels.Selector.Matches of LabelSelectorAsSelector(sel); nil matches nothing, an empty selector everything"""
+    if sel is None:
+        return False
+    for k, v in sel.match_labels:
+        if labels.get(k) != v:
+            return False
+    for k, op, vals in sel.match_expressions:
+        has = k in labels
+        if op == "In":
+            if not has or labels[k] not in vals:
+                return False
+        elif op == "NotIn":
+            if has and labels[k] in vals:
+                return False
+        elif op == "Exists":
+            if not has:
+                return False
+        elif op == "DoesNotExist":
+            if has:
+                return False
+        else:
+            raise StaticPluginError(f"label selector operator {op!r}")
+    return True
+
+
+def term_namespaces(term: AffinityTerm, owner: TopoPod) -> Tuple[str, ...]:
+    """getNamespacesFromPodAffinityTerm: the term's namespaces, or the owner's namespace when it lists none"""
+    return tuple(sorted(set(term.namespaces))) if term.namespaces else (owner.namespace,)
+
+
+def term_matches(term: AffinityTerm, owner: TopoPod, pod: TopoPod) -> bool:
+    """AffinityTerm.Matches (framework/types.go): the pod's namespace among the term's and its labels selected"""
+    return pod.namespace in term_namespaces(term, owner) and selector_matches(term.selector, pod.labels)
+
+
+def spread_constraints(pod: TopoPod, hard: bool) -> List[SpreadConstraint]:
+    """filterTopologySpreadConstraints + the system defaults (buildDefaultConstraints) when the pod has none"""
+    want = DO_NOT_SCHEDULE if hard else SCHEDULE_ANYWAY
+    if pod.spread:
+        return [c for c in pod.spread if c.when_unsatisfiable == want]
+    if hard or pod.default_selector is None:
+        return []
+    sel = pod.default_selector
+    if not sel.match_labels and not sel.match_expressions:
+        return []  # an empty DefaultSelector: no default constraints
+    return [SpreadConstraint(skew, key, SCHEDULE_ANYWAY, sel) for key, skew in SYSTEM_DEFAULT_CONSTRAINTS]
+
+
+# ---- compilation to properties, counters and query terms ----
+
+KIND = {"spread_hard": 1, "spread_soft": 2, "affinity": 3, "anti": 4, "existing_anti": 5, "score": 6}
+
+
+@dataclass
+class Compiled:
+    props: List[tuple]                 # property identities, index = property
+    zones: List[str]                   # zone label values, index = zone
+    node_zone: np.ndarray              # [n] int32
+    node_count: np.ndarray             # [P][n] int32 pods with property p on node n
+    pod_props: np.ndarray              # [p] uint32 properties of each pending pod
+    pod_terms: np.ndarray              # [T][p] uint64 packed query terms (0 = none)
+    pod_flags: np.ndarray              # [p] uint32 KS_TOPO_*
+
+
+def _prop_has(prop: tuple, pod: TopoPod) -> bool:
+    kind = prop[0]
+    if kind == "sel":  # countPodsMatchSelector: not terminating, same namespace, selector
+        _, ns, sel = prop
+        return not pod.terminating and pod.namespace == ns and selector_matches(sel, pod.labels)
+    if kind == "term":
+        _, nss, sel = prop
+        return pod.namespace in nss and selector_matches(sel, pod.labels)
+    if kind == "all":
+        return all(pod.namespace in nss and selector_matches(sel, pod.labels) for nss, sel in prop[1])
+    if kind == "carry":
+        return prop in _carried(pod)
+    raise AssertionError(prop)
+
+
+def _carried(pod: TopoPod, hard_weight: int = 1) -> set:
+    """The carry properties of a pod: its required anti-affinity terms, and its hard / preferred (anti-)affinity terms
+    with their score weights (hard affinity terms weigh HardPodAffinityWeight)"""
+    out = set()
+    for t in pod.anti_required:
+        out.add(("carry", "anti", term_namespaces(t, pod), t.selector, t.topology_key, 0))
+    if hard_weight > 0:
+        for t in pod.affinity_required:
+            out.add(("carry", "score", term_namespaces(t, pod), t.selector, t.topology_key, hard_weight))
+    for w, t in pod.affinity_preferred:
+        out.add(("carry", "score", term_namespaces(t, pod), t.selector, t.topology_key, w))
+    for w, t in pod.anti_preferred:
+        out.add(("carry", "score", term_namespaces(t, pod), t.selector, t.topology_key, -w))
+    return out
+
+
+def pack_term(kind: int, prop: int, key: int, param: int, flags: int = 0) -> int:
+    """ks_pod_cols.topo_term word: kind (bits 0-7), property (8-15), topology key (16-23: 0 hostname, 1 zone),
+    flags (24-31: KS_TOPO_T_*), param (32-63, int32: maxSkew or the score weight)"""
+    return (kind & 0xFF) | ((prop & 0xFF) << 8) | ((key & 0xFF) << 16) | ((flags & 0xFF) << 24) | \
+        ((param & 0xFFFFFFFF) << 32)
+
+
+def compile_topology(node_labels: Sequence[Dict[str, str]], existing: Sequence[Tuple[int, TopoPod]],
+                     pending: Sequence[TopoPod], hard_weight: int = 1, zone_key: str = ZONE) -> Compiled:
+    """The properties, node counters and per-pod query terms of a cluster: node labels (every node has its hostname),
+    the running pods as (node row, pod), the pending pods in queue order.  Raises StaticPluginError for what the
+    device does not model (other topology keys, too many properties / terms / zones)."""
+    n = len(node_labels)
+    zones: List[str] = []
+    node_zone = np.full(n, -1, np.int32)
+    for i, lab in enumerate(node_labels):
+        if zone_key in lab:
+            if lab[zone_key] not in zones:
+                zones.append(lab[zone_key])
+            node_zone[i] = zones.index(lab[zone_key])
+    if len(zones) > abi.KS_TOPO_ZONES:
+        raise StaticPluginError(f"{len(zones)} zones (the device holds {abi.KS_TOPO_ZONES})")
+
+    def key_index(k: str) -> int:
+        if k == HOSTNAME:
+            return 0
+        if k == zone_key:
+            return 1
+        raise StaticPluginError(f"topology key {k!r} (the device models {HOSTNAME} and {zone_key})")
+
+    everyone = [p for _, p in existing] + list(pending)
+    carried_all = set()
+    for p in everyone:
+        carried_all |= _carried(p, hard_weight)
+    props: List[tuple] = []
+
+    def prop_index(pr: tuple) -> int:
+        if pr not in props:
+            props.append(pr)
+        return props.index(pr)
+
+    terms_per_pod: List[List[int]] = []
+    flags = np.zeros(len(pending), np.uint32)
+    for i, pod in enumerate(pending):
+        terms: List[int] = []
+        seen = set()
+        for c in pod.spread:
+            if (c.topology_key, c.when_unsatisfiable) in seen:
+                # ValidateTopologySpreadConstraints: a duplicate {topologyKey, whenUnsatisfiable} pair is invalid
+                raise StaticPluginError(f"pod {i}: duplicate spread constraint {c.topology_key}/{c.when_unsatisfiable}")
+            seen.add((c.topology_key, c.when_unsatisfiable))
+        hard = spread_constraints(pod, True)
+        soft = spread_constraints(pod, False)
+        hz = any(key_index(c.topology_key) == 1 for c in hard)
+        sz = any(key_index(c.topology_key) == 1 for c in soft)
+        for c in hard:
+            pi = prop_index(("sel", pod.namespace, c.selector))
+            self_match = abi.KS_TOPO_T_SELF if selector_matches(c.selector, pod.labels) else 0
+            terms.append(pack_term(KIND["spread_hard"], pi, key_index(c.topology_key), c.max_skew,
+                                   self_match | (abi.KS_TOPO_T_ELIG_ZONE if hz else 0)))
+        if soft and pod.spread:
+            flags[i] |= abi.KS_TOPO_SOFT_ALL_KEYS  # requireAllTopologies: the pod's own constraints
+        for c in soft:
+            pi = prop_index(("sel", pod.namespace, c.selector))
+            terms.append(pack_term(KIND["spread_soft"], pi, key_index(c.topology_key), c.max_skew,
+                                   abi.KS_TOPO_T_ELIG_ZONE if sz else 0))
+        if pod.affinity_required:
+            pi = prop_index(("all", tuple((term_namespaces(t, pod), t.selector) for t in pod.affinity_required)))
+            for t in pod.affinity_required:
+                terms.append(pack_term(KIND["affinity"], pi, key_index(t.topology_key), 0))
+            if all(term_matches(t, pod, pod) for t in pod.affinity_required):
+                flags[i] |= abi.KS_TOPO_SELF_AFFINITY
+        for t in pod.anti_required:
+            pi = prop_index(("term", term_namespaces(t, pod), t.selector))
+            terms.append(pack_term(KIND["anti"], pi, key_index(t.topology_key), 0))
+        for cp in sorted(carried_all, key=repr):
+            _, kind, nss, sel, key, w = cp
+            if not (pod.namespace in nss and selector_matches(sel, pod.labels)):
+                continue
+            if kind == "anti":
+                terms.append(pack_term(KIND["existing_anti"], prop_index(cp), key_index(key), 0))
+            else:
+                terms.append(pack_term(KIND["score"], prop_index(cp), key_index(key), w))
+        for w, t in pod.affinity_preferred:
+            terms.append(pack_term(KIND["score"], prop_index(("term", term_namespaces(t, pod), t.selector)),
+                                   key_index(t.topology_key), w))
+        for w, t in pod.anti_preferred:
+            terms.append(pack_term(KIND["score"], prop_index(("term", term_namespaces(t, pod), t.selector)),
+                                   key_index(t.topology_key), -w))
+        if len(terms) > abi.KS_TOPO_TERMS:
+            raise StaticPluginError(f"pod {i}: {len(terms)} topology terms (the device holds {abi.KS_TOPO_TERMS})")
+        if terms:
+            flags[i] |= abi.KS_TOPO_DYN
+        terms_per_pod.append(terms)
+    if len(props) > abi.KS_TOPO_PROPS:
+        raise StaticPluginError(f"{len(props)} topology properties (the device holds {abi.KS_TOPO_PROPS})")
+    P = len(props)
+    node_count = np.zeros((abi.KS_TOPO_PROPS, n), np.int32)
+    for nd, pod in existing:
+        for pi, pr in enumerate(props):
+            if _prop_has(pr, pod) if pr[0] != "carry" else pr in _carried(pod, hard_weight):
+                node_count[pi, nd] += 1
+    pod_props = np.zeros(len(pending), np.uint32)
+    for i, pod in enumerate(pending):
+        m = 0
+        for pi, pr in enumerate(props):
+            if (_prop_has(pr, pod) if pr[0] != "carry" else pr in _carried(pod, hard_weight)):
+                m |= 1 << pi
+        pod_props[i] = m
+    pod_terms = np.zeros((abi.KS_TOPO_TERMS, len(pending)), np.uint64)
+    for i, terms in enumerate(terms_per_pod):
+        for t, w in enumerate(terms):
+            pod_terms[t, i] = np.uint64(w)
+    assert P <= abi.KS_TOPO_PROPS
+    return Compiled(props, zones, node_zone, node_count, pod_props, pod_terms, flags)
+
+
+def install(c: Compiled, node_table, pod_table) -> None:
+    """Write the compiled columns into the tables (ks_node_cols.topo_zone / topo_count, ks_pod_cols.topo_*)."""
+    node_table.topo_zone[:] = c.node_zone
+    node_table.topo_count[:] = c.node_count
+    pod_table.topo_props[:] = c.pod_props
+    pod_table.topo_flags[:] = c.pod_flags
+    pod_table.topo_term[:] = c.pod_terms

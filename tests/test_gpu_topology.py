@@ -1,0 +1,167 @@
+"""GPU parity of upstream PodTopologySpread and InterPodAffinity (ks_topo.h / ks_topo.hip: a topology pod is scheduled
+alone by the topology step -- eval_debug_kernel, topo_filter_kernel, topo_norm_kernel, a one-pod commit -- and the
+regular passes end before it; every Reserve counts the pod's properties on its node) with the CPU oracle, which the
+CPU tests (tests/test_topology.py) check against the object-level restatement oracle/topology_ref.py.  Parity of the
+upstream plugins themselves is unpinned (kube-scheduler v1.24.15 is not on disk).  Per-node reasons / scores /
+totals through ks_eval_pod; whole queues through the pass loop -- with only the two plugins, C2-shaped under the
+v1beta2 default plugin set (ElasticQuota, BalancedAllocation, TaintToleration, NodeAffinity, NodePorts), with
+Reservation, with NUMA + DeviceShare (C3); the counters read back; ks_assume / ks_unreserve; the refusals."""
+import numpy as np
+import pytest
+
+from helpers import assert_same_results, assert_same_state
+from koordinator_amd import abi, synth
+from koordinator_amd.config import SchedulerProfile
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def runtime():
+    from koordinator_amd import runtime as rt
+
+    rt.lib()  # the in-tree HIP library; no fallback
+    return rt
+
+
+def run(runtime, oracle_lib, w, label):
+    cfg = w.cfg
+    ev = runtime.Evaluator(cfg, w.nodes.copy(), **w.tables())
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), nthreads=8, **w.tables())
+    try:
+        got = ev.schedule(w.pods)
+        st = ev.stats()
+        want = orc.schedule(w.pods)
+        assert_same_results(got, want, label)
+        assert_same_state(ev.read_nodes(), orc.read_nodes(), label)
+        for k in ("reservation", "gpu_minors", "rdma_minors"):
+            assert np.array_equal(got[k], want[k]), f"{label}: {k}"
+        if w.quotas is not None:
+            assert np.array_equal(ev.read_quota_used(), orc.read_quota_used()), f"{label}: quota used"
+    finally:
+        ev.close()
+        orc.close()
+    return got, st
+
+
+def topo_only(n_nodes, n_pods, seed, **kw):
+    w = synth.c1(n_nodes=n_nodes, n_pods=n_pods)
+    w = synth.with_topology(w, seed=seed, **kw)
+    return w
+
+
+def test_eval_pod(runtime, oracle_lib):
+    w = synth.with_topology(synth.with_static_plugins(synth.c1(n_nodes=700, n_pods=160), seed=31), seed=32)
+    cfg = w.cfg
+    ev = runtime.Evaluator(cfg, w.nodes.copy())
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy())
+    seen = 0
+    try:
+        for i in range(w.pods.n):
+            one = w.pods.rows([i])
+            r_g, s_g, t_g = ev.eval_pod(one)
+            r_o, s_o, t_o = orc.eval_pod(one)
+            assert np.array_equal(r_g, r_o), f"pod {i}: reasons at nodes {np.nonzero(r_g != r_o)[0][:5]}"
+            assert np.array_equal(s_g, s_o), f"pod {i}: scores at {np.argwhere(s_g != s_o)[:5].tolist()}"
+            assert np.array_equal(t_g, t_o), f"pod {i}: totals"
+            seen |= int(np.bitwise_or.reduce(r_g))
+    finally:
+        ev.close()
+        orc.close()
+    for bit in (abi.KS_R_TOPOLOGY_SPREAD, abi.KS_R_POD_AFFINITY, abi.KS_R_POD_ANTI_AFFINITY,
+                abi.KS_R_EXISTING_ANTI_AFFINITY):
+        assert seen & bit, hex(bit)
+
+
+def test_topology_only_queue(runtime, oracle_lib):
+    """the two plugins alone (Fit + LoadAware off): tight hostname / zone skews and anti-affinity decide placements"""
+    w = topo_only(60, 500, 41, per_node=(0, 2), spread_frac=0.35, anti_frac=0.15)
+    w.profile.fit = None
+    w.profile.loadaware = None
+    got, st = run(runtime, oracle_lib, w, "topology-only")
+    assert (got["status"] == abi.KS_S_UNSCHEDULABLE).sum() > 0
+
+
+@pytest.mark.parametrize("seed", [42, 43])
+def test_with_fit_loadaware(runtime, oracle_lib, seed):
+    w = topo_only(800, 2000, seed)
+    run(runtime, oracle_lib, w, f"fit+la+topology seed {seed}")
+
+
+def test_c2_default_with_topology(runtime, oracle_lib):
+    """C2 under the v1beta2 default plugin set with the two plugins as well (weights 2 / 1)"""
+    w = synth.with_topology(synth.c2_default(n_nodes=1500, n_pods=3000), seed=44)
+    got, st = run(runtime, oracle_lib, w, "c2-default+topology")
+    assert (got["status"] == abi.KS_S_SCHEDULED).sum() > 1000
+
+
+def test_reservation_with_topology(runtime, oracle_lib):
+    w = synth.with_topology(synth.c4(n_nodes=1000, n_reservations=2500, n_pods=2000), seed=45)
+    run(runtime, oracle_lib, w, "c4+topology")
+
+
+def test_c3_with_topology(runtime, oracle_lib):
+    """NUMA + DeviceShare (C3) with the two plugins: cpuset / device Reserves of topology pods in the one-pod commit"""
+    w = synth.with_topology(synth.c3(n_nodes=800, n_pods=1600), seed=46)
+    run(runtime, oracle_lib, w, "c3+topology")
+
+
+def test_assume_unreserve_counters(runtime, oracle_lib):
+    w = topo_only(300, 200, 47)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy())
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy())
+    try:
+        held = []
+        for i in range(120):
+            pod = w.pods.rows([i])
+            rg, _, tg = ev.eval_pod(pod)
+            ro, _, to = orc.eval_pod(pod)
+            assert np.array_equal(rg, ro) and np.array_equal(tg, to), f"pod {i}: eval"
+            if tg.max() < 0:
+                continue
+            node = int(np.argmax(tg))
+            a, _, _ = ev.assume(pod, node)
+            b, _, _ = orc.assume(pod, node)
+            assert a[0]["status"] == b[0]["status"]
+            held.append((i, a))
+        assert_same_state(ev.read_nodes(), orc.read_nodes(), "assumed")
+        for i, a in held[::2]:
+            pod = w.pods.rows([i])
+            ev.unreserve(pod, a)
+            orc.unreserve(pod, a)
+        assert_same_state(ev.read_nodes(), orc.read_nodes(), "half unreserved")
+        rest = w.pods.rows(list(range(120, 200)))
+        assert_same_results(ev.schedule(rest), orc.schedule(rest), "after unreserve")
+        assert_same_state(ev.read_nodes(), orc.read_nodes(), "after the queue")
+    finally:
+        ev.close()
+        orc.close()
+
+
+def test_checkpoint_restores_counters(runtime, oracle_lib):
+    w = topo_only(400, 600, 48)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy())
+    try:
+        ev.checkpoint()
+        first = ev.schedule(w.pods)
+        c1 = ev.read_nodes().topo_count.copy()
+        ev.restore()
+        assert np.array_equal(ev.read_nodes().topo_count, w.nodes.topo_count)
+        second = ev.schedule(w.pods)
+        assert_same_results(second, first, "after restore")
+        assert np.array_equal(ev.read_nodes().topo_count, c1)
+    finally:
+        ev.close()
+
+
+def test_refusals(runtime):
+    w = topo_only(64, 8, 49)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy())
+    try:
+        bad = w.pods.rows([0])
+        bad.topo_term[0, 0] = np.uint64(7)  # kind 7: no such term
+        with pytest.raises(runtime.KsError) as e:
+            ev.schedule(bad)
+        assert e.value.rc == abi.KS_EINVAL
+    finally:
+        ev.close()

@@ -1,0 +1,188 @@
+"""Upstream PodTopologySpread and InterPodAffinity (kube-scheduler v1.24.15 plugins/podtopologyspread,
+plugins/interpodaffinity; not on disk -- a go.mod dependency of the reference -- so parity is unpinned against
+reference fixtures).  CPU only:
+  * hand-worked cases of the host compiler (koordinator_amd/topology_plugins.py: properties, counters, query terms,
+    system default constraints, refusals);
+  * the C oracle's evaluation of the compiled form against oracle/topology_ref.py, which restates both plugins on the
+    pod objects (topology pairs, critical paths, affinity / anti-affinity counts, topologyScore maps): per-node Filter
+    verdicts, normalized scores and totals, alone, with node affinity, and next to NodeResourcesFit;
+  * whole queues: ko_schedule against a sequential loop over the restatement (each placed pod joins the running pods
+    of its node), and the counters ks_read_nodes reports after it."""
+import copy
+
+import numpy as np
+import pytest
+
+from koordinator_amd import abi, synth
+from koordinator_amd.config import SchedulerProfile
+from koordinator_amd.static_plugins import StaticPluginError
+from koordinator_amd.topology_plugins import (DO_NOT_SCHEDULE, HOSTNAME, KIND, SCHEDULE_ANYWAY, ZONE, AffinityTerm,
+                                              LabelSelector, SpreadConstraint, TopoPod, compile_topology, install)
+from oracle import topology_ref as ref
+from oracle.oracle import Oracle
+
+IPA_BITS = {"affinity": abi.KS_R_POD_AFFINITY, "anti": abi.KS_R_POD_ANTI_AFFINITY,
+            "existing": abi.KS_R_EXISTING_ANTI_AFFINITY}
+
+
+def _profile(fit=False, static=False):
+    kw = dict(topology=True, topology_spread_weight=2, inter_pod_affinity_weight=1, loadaware=None)
+    if not fit:
+        kw["fit"] = None
+    if static:
+        kw.update(node_affinity=True, node_affinity_weight=1)
+    return SchedulerProfile(**kw)
+
+
+def _workload(n_nodes, n_pods, seed, static=False, **kw):
+    w = synth.c1(n_nodes=n_nodes, n_pods=n_pods)
+    if static:
+        w = synth.with_static_plugins(w, seed=seed + 100)
+    return synth.with_topology(w, seed=seed, **kw)
+
+
+def _node_aff(w, i):
+    if not hasattr(w, "specs"):
+        return None
+    from oracle import static_plugins_ref as sref
+    nspec, pspec = w.specs
+    return lambda n: sref.affinity_filter(pspec[i], nspec[n])
+
+
+def _check_eval(w, profile, pods, base_profile=None, other_fn=None):
+    node_labels, existing, pending = w.topo
+    orc = Oracle(profile.to_ks_config(), w.nodes.copy())
+    base = Oracle(base_profile.to_ks_config(), w.nodes.copy()) if base_profile else None
+    try:
+        for i in pods:
+            one = w.pods.rows([i])
+            r, s, t = orc.eval_pod(one)
+            other = [True] * w.nodes.n if other_fn is None else [other_fn(i, n) for n in range(w.nodes.n)]
+            bt = None
+            if base is not None:
+                rb, sb, bt = base.eval_pod(one)
+                other = list(rb == 0)
+            pf, ipf, pn, inn, add = ref.evaluate(pending[i], node_labels, existing, other, node_aff=_node_aff(w, i))
+            for n in range(w.nodes.n):
+                assert bool(r[n] & abi.KS_R_TOPOLOGY_SPREAD) == pf[n], f"pod {i} node {n}: spread filter"
+                want = IPA_BITS.get(ipf[n], 0)
+                got = int(r[n]) & (abi.KS_R_POD_AFFINITY | abi.KS_R_POD_ANTI_AFFINITY | abi.KS_R_EXISTING_ANTI_AFFINITY)
+                assert got == want, f"pod {i} node {n}: inter-pod affinity filter {got:#x} vs {ipf[n]}"
+            assert list(s[:, abi.KS_SCORE_TOPOLOGY_SPREAD]) == pn, f"pod {i}: spread scores"
+            assert list(s[:, abi.KS_SCORE_POD_AFFINITY]) == inn, f"pod {i}: inter-pod affinity scores"
+            if base is None and other_fn is None:
+                assert list(t) == [a if a is not None else -1 for a in add], f"pod {i}: totals"
+    finally:
+        orc.close()
+        if base is not None:
+            base.close()
+
+
+def test_compile_hand_cases():
+    sel_a = LabelSelector((("app", "a"),))
+    nodes = [{ZONE: "z1"}, {ZONE: "z1"}, {ZONE: "z2"}, {}]
+    existing = [(0, TopoPod(labels={"app": "a"})), (0, TopoPod(labels={"app": "a"}, terminating=True)),
+                (2, TopoPod(labels={"app": "a"}, anti_required=[AffinityTerm(HOSTNAME, sel_a)]))]
+    pending = [
+        TopoPod(labels={"app": "a"}, spread=[SpreadConstraint(1, ZONE, DO_NOT_SCHEDULE, sel_a)]),
+        TopoPod(labels={"app": "b"}),                                        # nothing: not a topology pod
+        TopoPod(labels={"app": "b"}, default_selector=sel_a),                # system defaults: two soft terms
+        TopoPod(labels={"app": "a"}),                                        # matches the running anti term
+        TopoPod(namespace="x", labels={"app": "a"}),                         # other namespace: does not
+    ]
+    c = compile_topology(nodes, existing, pending)
+    assert list(c.node_zone) == [0, 0, 1, -1]
+    kinds = [[int(c.pod_terms[t, i]) & 0xFF for t in range(abi.KS_TOPO_TERMS) if c.pod_terms[t, i]]
+             for i in range(len(pending))]
+    # (pod 0 is app=a in namespace default too: the running pod's anti-affinity term applies to it)
+    assert kinds[0] == [KIND["spread_hard"], KIND["existing_anti"]] and kinds[1] == [] and kinds[2] == [KIND["spread_soft"]] * 2
+    assert kinds[3] == [KIND["existing_anti"]] and kinds[4] == []
+    assert [bool(f & abi.KS_TOPO_DYN) for f in c.pod_flags] == [True, False, True, True, False]
+    # the selector property of pod 0 counts app=a pods of namespace default that are not terminating
+    p0 = (int(c.pod_terms[0, 0]) >> 8) & 0xFF
+    assert list(c.node_count[p0, :4]) == [1, 0, 1, 0]
+    assert (int(c.pod_terms[0, 0]) >> 24) & abi.KS_TOPO_T_SELF and (int(c.pod_terms[0, 0]) >> 32) == 1
+    # the carried anti-affinity term: one pod on node 2; pod 3 and pod 0 (app=a, default) have it as a property
+    pa = (int(c.pod_terms[0, 3]) >> 8) & 0xFF
+    assert list(c.node_count[pa, :4]) == [0, 0, 1, 0]
+    assert (int(c.pod_props[3]) >> pa) & 1 == 0  # pod 3 does not carry the term itself
+    with pytest.raises(StaticPluginError):
+        compile_topology(nodes, [], [TopoPod(spread=[SpreadConstraint(1, "rack", DO_NOT_SCHEDULE, sel_a)])])
+    many = [TopoPod(labels={"app": str(k)}, spread=[SpreadConstraint(1, HOSTNAME, DO_NOT_SCHEDULE,
+                                                                      LabelSelector((("app", str(k)),)))])
+            for k in range(abi.KS_TOPO_PROPS + 1)]
+    with pytest.raises(StaticPluginError):
+        compile_topology(nodes, [], many)
+
+
+def test_hand_worked_spread_and_affinity():
+    """two zones; app=a pods: z1 holds 2 (nodes 0, 1), z2 holds 0; a DoNotSchedule zone constraint with maxSkew 1
+    rejects z1 (2 + 1 - 0 > 1); a required anti-affinity to app=a per hostname rejects nodes 0 and 1; a required
+    affinity to app=a per zone admits z1 only"""
+    sel_a = LabelSelector((("app", "a"),))
+    nodes = [{ZONE: "z1"}, {ZONE: "z1"}, {ZONE: "z2"}, {ZONE: "z2"}]
+    existing = [(0, TopoPod(labels={"app": "a"})), (1, TopoPod(labels={"app": "a"}))]
+    pending = [TopoPod(labels={"app": "a"}, spread=[SpreadConstraint(1, ZONE, DO_NOT_SCHEDULE, sel_a)]),
+               TopoPod(labels={"app": "b"}, anti_required=[AffinityTerm(HOSTNAME, sel_a)]),
+               TopoPod(labels={"app": "b"}, affinity_required=[AffinityTerm(ZONE, sel_a)]),
+               TopoPod(labels={"app": "b"}, affinity_preferred=[(50, AffinityTerm(HOSTNAME, sel_a))])]
+    w = synth.c1(n_nodes=4, n_pods=len(pending))
+    install(compile_topology(nodes, existing, pending), w.nodes, w.pods)
+    orc = Oracle(_profile().to_ks_config(), w.nodes.copy())
+    r, s, t = orc.eval_pod(w.pods.rows([0]))
+    assert list(r) == [abi.KS_R_TOPOLOGY_SPREAD] * 2 + [0, 0]
+    r, s, t = orc.eval_pod(w.pods.rows([1]))
+    assert list(r) == [abi.KS_R_POD_ANTI_AFFINITY] * 2 + [0, 0]
+    r, s, t = orc.eval_pod(w.pods.rows([2]))
+    assert list(r) == [0, 0] + [abi.KS_R_POD_AFFINITY] * 2
+    r, s, t = orc.eval_pod(w.pods.rows([3]))
+    # preferred affinity raw 50 / 50 / 0 / 0 -> 100 / 100 / 0 / 0; no spread constraint: 100 everywhere
+    assert list(s[:, abi.KS_SCORE_POD_AFFINITY]) == [100, 100, 0, 0]
+    assert list(s[:, abi.KS_SCORE_TOPOLOGY_SPREAD]) == [100] * 4
+    assert list(t) == [300, 300, 200, 200]
+    orc.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_oracle_against_restatement(seed):
+    w = _workload(120, 150, seed)
+    _check_eval(w, _profile(), range(150))
+
+
+def test_oracle_against_restatement_node_affinity():
+    """the pods' required node affinity decides which nodes count for spreading; NodeAffinity's Filter runs too"""
+    w = _workload(100, 120, 3, static=True)
+    _check_eval(w, _profile(static=True), range(120), other_fn=lambda i, n: _node_aff(w, i)(n))
+
+
+def test_oracle_against_restatement_with_fit():
+    """next to NodeResourcesFit: the normalizations run over the nodes every Filter leaves"""
+    w = _workload(90, 100, 4, per_node=(2, 9))
+    _check_eval(w, _profile(fit=True), range(100), base_profile=SchedulerProfile(loadaware=None))
+
+
+def test_schedule_against_restatement():
+    """ko_schedule with only the two plugins against a sequential loop over the restatement: max total, lowest
+    index; the placed pod joins its node's running pods (and its carried terms count from then on)"""
+    w = _workload(12, 160, 5, per_node=(0, 2), spread_frac=0.35, anti_frac=0.15)
+    node_labels, existing, pending = w.topo
+    existing = list(existing)
+    orc = Oracle(_profile().to_ks_config(), w.nodes.copy())
+    got = orc.schedule(w.pods)
+    st = orc.read_nodes()
+    orc.close()
+    for i, p in enumerate(pending):
+        _, _, _, _, add = ref.evaluate(p, node_labels, existing, [True] * len(node_labels))
+        totals = [a if a is not None else -1 for a in add]
+        best = max(totals)
+        want = totals.index(best) if best >= 0 else -1
+        assert int(got["node"][i]) == want, f"pod {i}"
+        if want >= 0:
+            assert int(got["score"][i]) == best, f"pod {i}: score"
+            existing.append((want, p))
+        else:
+            assert int(got["status"][i]) == abi.KS_S_UNSCHEDULABLE
+    # the counters after the queue are the compiled counters of the final pod set
+    c = compile_topology(node_labels, existing, pending)
+    assert np.array_equal(st.topo_count, c.node_count)
+    assert (got["status"] == abi.KS_S_UNSCHEDULABLE).sum() > 0
