@@ -52,8 +52,15 @@ METRIC = "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k no
 def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
 
-    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f"):
+    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f", "c2t"):
         raise SystemExit(f"unknown config {name}")
+    if name == "c2t":
+        # the complete v1beta2 default profile: c2d + PodTopologySpread (system default constraints for the pods owned
+        # by a ReplicaSet, own constraints) and InterPodAffinity (synth.topology_specs)
+        w = synth.c2_default(seed=seed, n_pods=n_pods) if n_pods else synth.c2_default(seed=seed)
+        w = synth.with_topology(w, seed=seed + 9)
+        w.name = "C2-default+topology"
+        return w
     fn = {"c2d": synth.c2_default, "c3r": synth.c3_rsv, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
@@ -466,7 +473,9 @@ def workload_desc(w):
             + (" + NodeNUMAResource(amplified CPUs, cpuset pods, NUMA topology policies) + DeviceShare(8 GPUs x 80GiB + 4 RDMA on"
                " 4 PCIe/2 NUMA per node, joint GPU+RDMA)" if w.devices is not None else "")
             + (" + upstream NodeResourcesBalancedAllocation + TaintToleration + NodeAffinity + NodePorts (v1beta2 default"
-               " plugins)" if w.profile.balanced is not None and w.profile.taint_toleration else ""))
+               " plugins)" if w.profile.balanced is not None and w.profile.taint_toleration else "")
+            + (" + upstream PodTopologySpread(weight 2, system default constraints) + InterPodAffinity(weight 1)"
+               f" ({int((w.pods.topo_flags & 1).sum())} topology pods)" if w.profile.topology else ""))
 
 
 def main():
@@ -474,7 +483,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f", "c2t"])
     ap.add_argument("--pods", type=int, default=0, help="pods per step (default: the config's own count)")
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)

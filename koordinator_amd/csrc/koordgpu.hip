@@ -223,6 +223,7 @@ struct SelectArgs {
   // equal, and then the next pass starts after its pods; otherwise (a bubble) the next pass starts at the cursor.
   int32_t* next_base;            // NULL = not pipelined
   const int32_t* real_cursor;
+  const PodRec* pods;            // a topology pod at the cursor: nothing to select (ks_topo.h)
 };
 
 
@@ -250,6 +251,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
     const int32_t rc = *a.real_cursor;
     *a.next_base = (cursor == rc && cursor < a.total_pods) ? cursor + min(a.batch, a.total_pods - cursor) : rc;
   }
+  if (cursor < a.total_pods && (__builtin_amdgcn_readfirstlane(a.pods[cursor].flags) & kPodTopoDyn)) return;
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
   const int32_t p = blockIdx.x;
@@ -3937,6 +3939,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   se.batch = ctx->batch;
   se.k = ctx->k;
   se.real_cursor = ctx->cursor;
+  se.pods = ctx->st.recs;
   const CandSlot L = cand_slot_layout(ctx->k);
   rec(1, ss);
   for (int32_t v = 0; v < ctx->vshards; ++v) {

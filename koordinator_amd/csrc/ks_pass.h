@@ -138,6 +138,8 @@ void sweep_kernel(SweepArgs a) {
   }
   const int32_t cursor = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor >= a.total_pods) return;
+  // a topology pod at the cursor (ks_topo.h): the topology step takes it and this pass commits nothing
+  if (__builtin_amdgcn_readfirstlane(a.pods[cursor].flags) & kPodTopoDyn) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
   const int32_t groups = (np + a.ppw - 1) / a.ppw;
   int64_t nitems = a.c1 - a.c0;
