@@ -1109,6 +1109,8 @@ struct ks_ctx {
   double* topo_lw = nullptr;
   int32_t topo_nlw = 0;
   TopoScratch* topo_scr = nullptr;
+  long long *topo_sraw = nullptr, *topo_iraw = nullptr;  // [npad] per-node raw scores of the step
+  int32_t topo_k = 1;  // topology steps per regular pass (queues of mostly topology pods run several in a row)
   uint32_t* topo_cchunk = nullptr;
   uint2* topo_ct = nullptr;
   int32_t* topo_ccount = nullptr;
@@ -1715,9 +1717,12 @@ static int topo_install(ks_ctx* ctx) {
   const size_t b_lw = ((size_t)nlw * 8 + 255) / 256 * 256;
   const size_t b_scr = (sizeof(TopoScratch) + 255) / 256 * 256;
   const size_t b_cand = (size_t)kMaxBatch * kMaxCand * (4 + 8) + (size_t)kMaxBatch * (4 + 8 * 3);
-  if (dev_alloc(ctx, &ctx->topo_blob, b_lw + b_scr + b_cand) != KS_OK) return KS_ENOMEM;
+  const size_t b_raw = (size_t)ctx->npad * 8 * 2;
+  if (dev_alloc(ctx, &ctx->topo_blob, b_lw + b_scr + b_cand + b_raw) != KS_OK) return KS_ENOMEM;
   char* b = (char*)ctx->topo_blob;
-  HIPCHK(ctx, hipMemsetAsync(b, 0, b_lw + b_scr + b_cand, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(b, 0, b_lw + b_scr + b_cand + b_raw, ctx->stream));
+  ctx->topo_sraw = (long long*)(b + b_lw + b_scr + b_cand);
+  ctx->topo_iraw = ctx->topo_sraw + ctx->npad;
   ctx->topo_lw = (double*)b;
   ctx->topo_nlw = nlw;
   ctx->topo_scr = (TopoScratch*)(b + b_lw);
@@ -1736,6 +1741,8 @@ static int topo_install(ks_ctx* ctx) {
   std::vector<double> lw((size_t)nlw);
   for (int32_t i = 0; i < nlw; ++i) lw[(size_t)i] = log((double)(i + 2));
   HIPCHK(ctx, hipMemcpyAsync(ctx->topo_lw, lw.data(), (size_t)nlw * 8, hipMemcpyHostToDevice, ctx->stream));
+  const TopoScratch init = topo_scratch_init();
+  HIPCHK(ctx, hipMemcpyAsync(ctx->topo_scr, &init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // (pageable source)
   return KS_OK;
 }
@@ -3728,7 +3735,6 @@ static TopoKArgs topo_args(ks_ctx* ctx, PodStage& st, const int32_t* cursor, con
   TopoKArgs a{};
   a.t = dev_topo(ctx);
   a.labels = ctx->d.labels;
-  a.recs = st.recs;
   a.stat = st.stat;
   a.trec = st.topo;
   a.cursor = cursor;
@@ -3742,7 +3748,8 @@ static TopoKArgs topo_args(ks_ctx* ctx, PodStage& st, const int32_t* cursor, con
   a.draw = eb.ddraw;
   a.traw = eb.dtraw;
   a.araw = eb.daraw;
-  a.norm_others = cursor ? 1 : 0;
+  a.sraw = ctx->topo_sraw;
+  a.iraw = ctx->topo_iraw;
   a.dev_on = ctx->kc.dev;
   a.taint_on = (ctx->kc.taint & 2) != 0;
   a.aff_on = (ctx->kc.aff & 2) != 0;
@@ -3754,12 +3761,14 @@ static TopoKArgs topo_args(ks_ctx* ctx, PodStage& st, const int32_t* cursor, con
   a.spread_w = ctx->cfg.topology.spread_weight;
   a.ipa_w = ctx->cfg.topology.affinity_weight;
   a.scr = ctx->topo_scr;
-  a.cand_chunk = ctx->topo_cchunk;
-  a.cand_t = ctx->topo_ct;
-  a.cand_count = ctx->topo_ccount;
-  a.cand_bound = ctx->topo_cbound;
-  a.cand_top = ctx->topo_ctop;
-  a.cand_second = ctx->topo_csecond;
+  if (cursor) {
+    a.cand_chunk = ctx->topo_cchunk;
+    a.cand_t = ctx->topo_ct;
+    a.cand_count = ctx->topo_ccount;
+    a.cand_bound = ctx->topo_cbound;
+    a.cand_top = ctx->topo_ctop;
+    a.cand_second = ctx->topo_csecond;
+  }
   return a;
 }
 
@@ -3782,15 +3791,22 @@ static int topo_step(ks_ctx* ctx) {
   EvBuf eb;
   if (ev_buffers(ctx, eb) != KS_OK) return KS_ENOMEM;
   const int64_t n = ctx->n;
+  const TopoKArgs ta = topo_args(ctx, ctx->st, ctx->cursor, eb);
+  HIPCHK(ctx, launch_topo_sums(ctx->stream, ta));
   HIPCHK(ctx, launch_eval_debug(ctx->nsc, (int)((n + 255) / 256), ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv,
                                 ctx->kc, ctx->st.recs, n, eb.dr, eb.ds, eb.dt, eb.draw, eb.dhi, eb.ddraw, ctx->st.stat,
-                                eb.dtraw, eb.daraw, ctx->cursor, ctx->st.topo, ctx->np));
-  const TopoKArgs ta = topo_args(ctx, ctx->st, ctx->cursor, eb);
-  HIPCHK(ctx, launch_topo_filter(ctx->stream, ta));
+                                eb.dtraw, eb.daraw, &ta));
+  HIPCHK(ctx, launch_topo_pts(ctx->stream, ta));
   HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
   bool qcache = false;
   size_t smem = 0;
   CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, 1, &qcache, &smem);
+  if (qcache) {
+    // one pod: the quota rows are read from HBM (copying the table into LDS would cost more than the pod's reads)
+    qcache = false;  // (the reservation cache that fit next to the quota rows fits without them)
+    smem = commit_layout(ctx->k, ctx->nchunks, false, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
+                         ctx->q.q, kernel_feat(ctx) == 0, commit_hint_variant(ctx)).total;
+  }
   ca.topo = 2;
   ca.cand_chunk = ctx->topo_cchunk;
   ca.cand_t = ctx->topo_ct;
@@ -3829,9 +3845,11 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
   };
   auto shard_lo = [&](int32_t sh) { return ctx->nchunks * sh / S; };
   if (ctx->cfg.topology.enable && ctx->st.ndyn > 0 && !pipe) {
-    // a topology pod at the cursor is scheduled alone first (timed with the commits)
+    // the topology pods at the cursor are scheduled alone first, up to topo_k of them in a row (timed with the
+    // commits); a step whose cursor pod is not one costs its launches only
     rec(2, ctx->stream);
-    if (int rc = topo_step(ctx); rc != KS_OK) return rc;
+    for (int32_t t = 0; t < ctx->topo_k; ++t)
+      if (int rc = topo_step(ctx); rc != KS_OK) return rc;
     rec(2, ctx->stream);
   }
   SweepArgs sa;
@@ -4063,6 +4081,11 @@ static int schedule_staged_impl(ks_ctx* ctx) {
       ctx->gather_bytes = gb;
     }
   }
+  // topology steps per regular pass: about the queue's topology pods per other pod (a regular pass that meets a
+  // topology pod at the cursor costs its launches for nothing), 1..8
+  ctx->topo_k = 1;
+  if (ctx->cfg.topology.enable && ctx->st.ndyn > 0)
+    ctx->topo_k = (int32_t)std::min<int64_t>(8, 1 + (int64_t)ctx->st.ndyn / std::max<int64_t>(1, (int64_t)np - ctx->st.ndyn));
   // pods per wave: aim for >= ~4096 waves per sweep
   const int64_t S = (int64_t)ctx->nranks * ctx->vshards;
   const int64_t local_chunks = ctx->nchunks * (ctx->rank + 1) * ctx->vshards / S - ctx->nchunks * ctx->rank * ctx->vshards / S;
@@ -4120,18 +4143,51 @@ static int schedule_staged_impl(ks_ctx* ctx) {
   size_t evn = 2;
   int32_t host_cursor = 0;
   int rounds = 0;
+  auto one_pass = [&](std::vector<std::pair<int, size_t>>* ev) -> int {
+    switch (ctx->nsc) {
+      case 0: return launch_pass<0>(ctx, ppw, sweep_blocks, pipe, ev, &evn);
+      case 2: return launch_pass<2>(ctx, ppw, sweep_blocks, pipe, ev, &evn);
+      default: return launch_pass<4>(ctx, ppw, sweep_blocks, pipe, ev, &evn);
+    }
+  };
+  // Topology pods (ks_topo.h): an iteration is topo_k topology steps + a regular pass, ~10 launches per pod, which the
+  // host's launch rate would bound; kGraphIters iterations are captured into one HIP graph and launched as one (not
+  // with per-kernel profiling events, not pipelined)
+  hipGraphExec_t gexec = nullptr;
+  static const int64_t env_graph = env_i64("KS_TOPO_GRAPH", 1, 0, 1);
+  constexpr int32_t kGraphIters = 4;
+  if (ctx->cfg.topology.enable && ctx->st.ndyn > 0 && !pipe && !ctx->cfg.profile && env_graph && !ctx->comm && !ctx->loop) {
+    EvBuf eb;
+    if (ev_buffers(ctx, eb) != KS_OK) return KS_ENOMEM;  // (allocated before the capture)
+    hipGraph_t graph = nullptr;
+    HIPCHK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    int rc = KS_OK;
+    for (int32_t i = 0; i < kGraphIters && rc == KS_OK; ++i) rc = one_pass(nullptr);
+    const hipError_t ee = hipStreamEndCapture(ctx->stream, &graph);
+    if (rc != KS_OK) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    HIPCHK(ctx, ee);
+    const hipError_t ie = hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(ctx, ie);
+  }
+  struct GraphGuard {
+    hipGraphExec_t& g;
+    ~GraphGuard() {
+      if (g) (void)hipGraphExecDestroy(g);
+    }
+  } graph_guard{gexec};
   while (host_cursor < np) {
     const int32_t remaining = np - host_cursor;
     const int32_t g = std::min<int32_t>((remaining + ctx->batch - 1) / ctx->batch, 256);
-    for (int32_t i = 0; i < g; ++i) {
-      auto* ev = ctx->cfg.profile ? &evs : nullptr;
-      int rc;
-      switch (ctx->nsc) {
-        case 0: rc = launch_pass<0>(ctx, ppw, sweep_blocks, pipe, ev, &evn); break;
-        case 2: rc = launch_pass<2>(ctx, ppw, sweep_blocks, pipe, ev, &evn); break;
-        default: rc = launch_pass<4>(ctx, ppw, sweep_blocks, pipe, ev, &evn); break;
+    for (int32_t i = 0; i < g; i += gexec ? kGraphIters : 1) {
+      if (gexec) {
+        HIPCHK(ctx, hipGraphLaunch(gexec, ctx->stream));
+        continue;
       }
-      if (rc != KS_OK) return rc;
+      if (int rc = one_pass(ctx->cfg.profile ? &evs : nullptr); rc != KS_OK) return rc;
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(&host_cursor, ctx->cursor, 4, hipMemcpyDeviceToHost, cs));
@@ -4476,17 +4532,18 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
   int32_t *draw = eb.draw, *dhi = eb.dhi, *ddraw = eb.ddraw, *dtraw = eb.dtraw, *daraw = eb.daraw;
   const int threads = 256;
   const int blocks = (int)((n + threads - 1) / threads);
-  if (blocks > 0) {
+  if (blocks > 0 && ctx->cfg.topology.enable && ctx->est.topo) {
+    // PodTopologySpread / InterPodAffinity: their PreFilter sums, every Filter (theirs folded into the evaluation
+    // kernel), then every normalization over the nodes all Filters leave (the topology step's kernels)
+    const TopoKArgs ta = topo_args(ctx, ctx->est, nullptr, eb);
+    HIPCHK(ctx, launch_topo_sums(ctx->stream, ta));
+    HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
+                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw, &ta));
+    HIPCHK(ctx, launch_topo_pts(ctx->stream, ta));
+    HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
+  } else if (blocks > 0) {
     HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
                                   ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw));
-    // PodTopologySpread / InterPodAffinity: their Filters before every normalization (which run over the nodes all
-    // Filters leave), their scores after
-    TopoKArgs ta{};
-    const bool topo = ctx->cfg.topology.enable && ctx->est.topo;
-    if (topo) {
-      ta = topo_args(ctx, ctx->est, nullptr, eb);
-      HIPCHK(ctx, launch_topo_filter(ctx->stream, ta));
-    }
     if (ctx->kc.dev)
       hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,
                          ctx->cfg.deviceshare.plugin_weight);
@@ -4499,7 +4556,6 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
     if (ctx->kc.rsv)
       hipLaunchKernelGGL(rsv_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, draw, dhi, ds, dt,
                          ctx->cfg.reservation.plugin_weight);
-    if (topo) HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
   }
   HIPCHK(ctx, hipGetLastError());
   if (reasons && n) HIPCHK(ctx, hipMemcpyAsync(reasons, dr, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));

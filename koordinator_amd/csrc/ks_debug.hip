@@ -13,58 +13,66 @@ template <int NSC>
 __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n,
                                   uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
                                   int32_t* draw, const PodStat* pstat, int32_t* traw, int32_t* araw,
-                                  const int32_t* cursor, const TopoRec* trec, int32_t total_pods) {
+                                  TopoKArgs tk, int32_t topo) {
+  __shared__ TopoLds tl;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const bool valid = i < n;
   // the topology step (ks_topo.h): the pod at the cursor, only if it is a topology pod
   int64_t pi = 0;
-  if (cursor) {
-    pi = *cursor;
-    if (pi >= total_pods || !(trec[pi].flags & KS_TOPO_DYN)) return;
+  TopoRec tr;
+  if (topo) {
+    pi = topo_pod(tk, tr);
+    if (pi < 0) return;
+    if (tr.flags & KS_TOPO_DYN) topo_stage(tk, tr, tl);
   }
-  NodeReg<NSC> r;
-  load_node<NSC>(c, d, i, 1, r);
-  const PodRec p = pod[pi];
-  if (pstat) pstat += pi;
-  RsvOut ro;
-  EvalOut o = eval_full<NSC, true, false, 15>(
-      c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
-      [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
-  if (c.stat) stat_eval(c, *pstat, d.taints_hard[i], d.taints_soft[i], d.labels[i], d.host_ports[i], o);
-  reasons[i] = o.reasons;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_BALANCED] = o.reasons ? 0 : o.bal;
-  // Fit + LoadAware + NUMA + BalancedAllocation part (the Reservation part is added by rsv_normalize_debug_kernel)
-  total[i] = o.reasons ? -1
-                       : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw +
-                             (int64_t)o.bal * c.bal_pw;
-  raw[i] = ro.raw;
-  hiord[i] = ro.hiord;
-  draw[i] = o.dev_raw;
-  traw[i] = o.traw;
-  araw[i] = o.araw;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TAINT] = 0;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = 0;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TOPOLOGY_SPREAD] = 0;
-  scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_POD_AFFINITY] = 0;
+  if (valid) {
+    NodeReg<NSC> r;
+    load_node<NSC>(c, d, i, 1, r);
+    const PodRec p = pod[pi];
+    const PodStat* ps = pstat ? pstat + pi : nullptr;
+    RsvOut ro;
+    EvalOut o = eval_full<NSC, true, false, 15>(
+        c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
+        [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
+    if (c.stat) stat_eval(c, *ps, d.taints_hard[i], d.taints_soft[i], d.labels[i], d.host_ports[i], o);
+    reasons[i] = o.reasons;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_BALANCED] = o.reasons ? 0 : o.bal;
+    // Fit + LoadAware + NUMA + BalancedAllocation part (the normalized plugins are added by the normalize kernels)
+    total[i] = o.reasons ? -1
+                         : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw +
+                               (int64_t)o.bal * c.bal_pw;
+    raw[i] = ro.raw;
+    hiord[i] = ro.hiord;
+    draw[i] = o.dev_raw;
+    traw[i] = o.traw;
+    araw[i] = o.araw;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TAINT] = 0;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = 0;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TOPOLOGY_SPREAD] = 0;
+    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_POD_AFFINITY] = 0;
+  }
+  // PodTopologySpread / InterPodAffinity Filters and the normalizations' reductions (every lane, converged)
+  if (topo) topo_eval_node(tk, tr, (int32_t)pi, i, valid, tl);
 }
 
 
 hipError_t launch_eval_debug(int nsc, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,
                              const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
                              int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw,
-                             const PodStat* pstat, int32_t* traw, int32_t* araw, const int32_t* cursor,
-                             const TopoRec* trec, int32_t total_pods) {
+                             const PodStat* pstat, int32_t* traw, int32_t* araw, const TopoKArgs* tk) {
+  const TopoKArgs t = tk ? *tk : TopoKArgs{};
+  const int32_t on = tk ? 1 : 0;
   if (nsc == 0)
-    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, cursor, trec, total_pods);
+    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
   else if (nsc == 2)
-    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, cursor, trec, total_pods);
+    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
   else
-    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, cursor, trec, total_pods);
+    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
   return hipGetLastError();
 }
 

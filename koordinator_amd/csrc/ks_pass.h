@@ -381,7 +381,7 @@ struct CommitArgs {
   const TopoRec* topo_rec;   // [pod] queue order
   int32_t* topo_count;       // [KS_TOPO_PROPS][topo_npad]
   int64_t topo_npad;
-  const int64_t* topo_best;  // mode 2: the topology step's total of the chosen node
+  const long long* topo_best;  // mode 2: the topology step's total of the chosen node
 };
 
 // One pod's NodeNUMAResource + DeviceShare Reserve on one node of its snapshot ranking, computed on the snapshot state

@@ -43,11 +43,22 @@ struct DevTopo {
   int32_t nlw;
 };
 
-// The topology step's scratch (HBM, one per context)
+// The topology step's reductions (HBM, one per context).  Every field is back at its initial value after each step
+// (topo_norm_kernel's last workgroup resets it; topo_install writes the initial image).
 struct TopoScratch {
-  int64_t zsum[KS_TOPO_TERMS][KS_TOPO_ZONES];  // per term: the zone's counted pods over the term's eligible nodes
-  unsigned long long zpres[KS_TOPO_TERMS];      // hard spread: zones with an eligible node
-  int64_t best_total;                           // the chosen node's total (the pod's result score)
+  long long zsum[KS_TOPO_TERMS][KS_TOPO_ZONES];  // per term: the zone's counted pods over the term's eligible nodes (0)
+  unsigned long long zpres[KS_TOPO_TERMS];        // hard spread: zones with an eligible node (0)
+  int hmin[KS_TOPO_TERMS];                        // hard spread, hostname: min count over the eligible nodes (INT_MAX)
+  int any_all;                                    // InterPodAffinity: affinityCounts is not empty (0)
+  unsigned long long hsize, zones;                // feasible non-ignored nodes, their zones (0)
+  int empty;                                      // a feasible non-ignored node without the zone label (0)
+  int dev_max, taint_max, aff_max;                // DeviceShare / TaintToleration / NodeAffinity raw maxima (0)
+  long long imin, imax;                           // InterPodAffinity raw extrema, from 0 (0)
+  long long smin, smax;                           // PodTopologySpread raw extrema over the non-ignored nodes (LLONG_MAX, 0)
+  unsigned long long rsv_pref, rsv_max;           // Reservation preferred-node key, raw max (0)
+  unsigned long long best;                        // selectHost key (total + 1) << 32 | ~node (0)
+  unsigned int done;                              // topo_norm_kernel workgroups finished (0)
+  long long best_total;                           // the chosen node's total (the pod's result score)
 };
 
 __device__ __forceinline__ int tp_kind(uint64_t w) { return (int)(w & 0xFF); }
@@ -100,9 +111,8 @@ __device__ __forceinline__ void topo_writeback(const A& a, int32_t pod, ks_resul
 struct TopoKArgs {
   DevTopo t;
   const uint64_t* labels;  // DevNodes.labels (required node affinity of the spread constraints)
-  const PodRec* recs;      // the stage, queue order
-  const PodStat* stat;     // NULL = no node affinity
-  const TopoRec* trec;
+  const PodStat* stat;     // the stage's PodStat records (NULL = no node affinity)
+  const TopoRec* trec;     // the stage's TopoRec records
   const int32_t* cursor;   // the pod at *cursor, only if it is a topology pod; NULL = pod 0, always (ks_eval_pod)
   int32_t total_pods;
   int64_t n;
@@ -114,19 +124,195 @@ struct TopoKArgs {
   const int32_t* draw;     // DeviceShare raw
   const int32_t* traw;     // TaintToleration raw
   const int32_t* araw;     // NodeAffinity raw
-  int32_t norm_others;     // topo_norm_kernel also runs the DeviceShare / TaintToleration / NodeAffinity /
-                           // Reservation normalizations (the batch step; ks_eval_pod launches their own kernels)
+  long long* sraw;         // [n] PodTopologySpread raw score (topo_pts_kernel)
+  long long* iraw;         // [n] InterPodAffinity raw score (eval_debug_kernel)
   int32_t dev_on, taint_on, aff_on, rsv_on;
   int64_t dev_w, taint_w, aff_w, rsv_w, spread_w, ipa_w;
   TopoScratch* scr;
-  // the batch step's one-candidate set of the chosen node (commit_kernel's lists, pod 0 of a one-pod pass)
+  // the batch step's one-candidate set of the chosen node (commit_kernel's lists, pod 0 of a one-pod pass); NULL in
+  // ks_eval_pod
   uint32_t* cand_chunk;
   uint2* cand_t;
   int32_t* cand_count;
   uint64_t *cand_bound, *cand_top, *cand_second;
 };
 
-hipError_t launch_topo_filter(hipStream_t s, const TopoKArgs& a);
+// the pod of the step (-1 = nothing to do: the cursor's pod is not a topology pod); rec = its record
+__device__ __forceinline__ int32_t topo_pod(const TopoKArgs& a, TopoRec& rec) {
+  int32_t pi = 0;
+  if (a.cursor) {
+    pi = *a.cursor;
+    if (pi >= a.total_pods) return -1;
+  }
+  rec = a.trec[pi];
+  if (a.cursor && !(rec.flags & KS_TOPO_DYN)) return -1;
+  return pi;
+}
+
+// the node counts for the term (hard spread: required node affinity + every hard key; soft spread: required node
+// affinity + every soft key when requireAllTopologies; InterPodAffinity: every node)
+__device__ __forceinline__ bool tp_eligible(uint64_t w, uint32_t pflags, bool aff, bool zone_ok) {
+  const int k = tp_kind(w);
+  if (k == KS_TOPO_K_SPREAD_HARD) return aff && (!(tp_flags(w) & KS_TOPO_T_ELIG_ZONE) || zone_ok);
+  if (k == KS_TOPO_K_SPREAD_SOFT)
+    return aff && (!((pflags & KS_TOPO_SOFT_ALL_KEYS) && (tp_flags(w) & KS_TOPO_T_ELIG_ZONE)) || zone_ok);
+  return true;
+}
+
+__device__ __forceinline__ long long wave_max_i64(long long v) {
+  return (long long)(wave_max_u64((uint64_t)v ^ (1ull << 63)) ^ (1ull << 63));
+}
+__device__ __forceinline__ long long wave_min_i64(long long v) {
+  return (long long)(~wave_max_u64(~((uint64_t)v ^ (1ull << 63))) ^ (1ull << 63));
+}
+
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, off, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), off, 64);
+    v |= ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// The block's LDS copy of the step's domain sums (TopoLds) and the hard spread constraints' minimum match count per
+// term (TpKeyToCriticalPaths[key][0].MatchNum; MaxInt32 when no domain is eligible), from what topo_sums_kernel left
+// in the scratch: one load per thread, the minima by LDS atomics.  Every thread of the block calls it.
+struct TopoLds {
+  long long zsum[KS_TOPO_TERMS][KS_TOPO_ZONES];
+  unsigned long long zpres[KS_TOPO_TERMS];
+  long long mins[KS_TOPO_TERMS];
+};
+__device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr, TopoLds& l) {
+  const int tid = threadIdx.x;
+  if (tid < KS_TOPO_TERMS) {
+    l.zpres[tid] = a.scr->zpres[tid];
+    l.mins[tid] = a.scr->hmin[tid];
+  }
+  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) (&l.zsum[0][0])[k] = (&a.scr->zsum[0][0])[k];
+  __syncthreads();
+  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) {
+    const int t = k / KS_TOPO_ZONES, z = k - t * KS_TOPO_ZONES;
+    if (tp_key(tr.term[t]) == 1 && ((l.zpres[t] >> z) & 1ull)) atomicMin(&l.mins[t], l.zsum[t][z]);
+  }
+  __syncthreads();
+}
+
+// eval_debug_kernel's topology part for node i (every lane of the wave calls it, converged; valid = a node of the
+// cluster): both plugins' Filters OR-ed into the node's reasons (total -1 and the score row zeroed when they fail),
+// InterPodAffinity's raw score, and the node's part of the normalizations' reductions (one global atomic per wave)
+__device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec& tr, int32_t pi, int64_t i, bool valid,
+                                               const TopoLds& l) {
+  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
+  bool soft_zone = false, need_aff = false;
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    const int k = tp_kind(tr.term[t]);
+    soft_zone |= k == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
+    need_aff |= k == KS_TOPO_K_SPREAD_HARD;
+  }
+  const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
+  bool feas = false, counted = false;
+  int32_t z = -1;
+  long long ir = 0;
+  int32_t dr = 0, trw = 0, arw = 0;
+  uint64_t pref = 0;
+  if (valid) {
+    const uint32_t base = a.reasons[i];
+    z = a.t.zone[i];
+    const bool has_zone = z >= 0;
+    uint32_t r = 0;
+    if (dyn) {
+      auto domain = [&](int t) -> long long {
+        const uint64_t w = tr.term[t];
+        return tp_key(w) == 1 ? l.zsum[t][z] : (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i];
+      };
+      const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, a.labels ? a.labels[i] : 0ull) : true;
+      // PodTopologySpread Filter: the first hard constraint that fails
+      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+        const uint64_t w = tr.term[t];
+        if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD) continue;
+        if (tp_key(w) == 1 && !has_zone) {  // ErrReasonNodeLabelNotMatch
+          r = KS_R_TOPOLOGY_SPREAD;
+          break;
+        }
+        long long match;
+        if (tp_key(w) == 1) match = ((l.zpres[t] >> z) & 1ull) ? l.zsum[t][z] : 0;
+        else match = tp_eligible(w, tr.flags, aff, has_zone) ? (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i] : 0;
+        const long long self = (tp_flags(w) & KS_TOPO_T_SELF) ? 1 : 0;
+        if (match + self - l.mins[t] > (long long)tp_param(w)) {  // ErrReasonConstraintsNotMatch
+          r = KS_R_TOPOLOGY_SPREAD;
+          break;
+        }
+      }
+      // InterPodAffinity Filter: affinity, anti-affinity, existing pods' anti-affinity -- the first that fails
+      bool aff_terms = false, missing = false, exist = true;
+      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+        if (tp_kind(tr.term[t]) != KS_TOPO_K_AFFINITY) continue;
+        aff_terms = true;
+        if (tp_key(tr.term[t]) == 1 && !has_zone) missing = true;
+        else if (domain(t) <= 0) exist = false;
+      }
+      uint32_t ipa = 0;
+      if (aff_terms && (missing || (!exist && !(a.scr->any_all == 0 && (tr.flags & KS_TOPO_SELF_AFFINITY))))) {
+        ipa = KS_R_POD_AFFINITY;
+      } else {
+        for (int t = 0; t < KS_TOPO_TERMS && !ipa; ++t) {
+          const uint64_t w = tr.term[t];
+          if (tp_kind(w) == KS_TOPO_K_ANTI && (tp_key(w) == 0 || has_zone) && domain(t) > 0) ipa = KS_R_POD_ANTI_AFFINITY;
+        }
+        for (int t = 0; t < KS_TOPO_TERMS && !ipa; ++t) {
+          const uint64_t w = tr.term[t];
+          if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && (tp_key(w) == 0 || has_zone) && domain(t) > 0)
+            ipa = KS_R_EXISTING_ANTI_AFFINITY;
+        }
+      }
+      r |= ipa;
+      if (r) {
+        a.reasons[i] = base | r;
+        a.total[i] = -1;
+        for (int k = 0; k < KS_NUM_SCORE_PLUGINS; ++k) a.scores[i * KS_NUM_SCORE_PLUGINS + k] = 0;
+      }
+      // InterPodAffinity Score: weight x matching pods in the node's domain, per score term
+      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+        const uint64_t w = tr.term[t];
+        if (tp_kind(w) == KS_TOPO_K_SCORE && (tp_key(w) == 0 || has_zone)) ir += (long long)tp_param(w) * domain(t);
+      }
+    }
+    feas = (base | r) == 0;
+    counted = feas && !(soft_all && soft_zone && !has_zone);  // initPreScoreState: not an ignored node
+    if (feas) {
+      a.iraw[i] = ir;
+      dr = a.draw[i];
+      trw = a.traw[i];
+      arw = a.araw[i];
+      if (a.rsv_on && a.rhi[i] > 0) pref = ((uint64_t)a.rhi[i] << 32) | (0xFFFFFFFFull - (uint64_t)i);
+    }
+  }
+  // the wave's part of every reduction, then one atomic per quantity
+  const int lane = threadIdx.x & 63;
+  const uint64_t cnt = __ballot(counted);
+  const uint64_t zbits = wave_or_u64(counted && z >= 0 ? (1ull << z) : 0ull);
+  const bool emp = __ballot(counted && z < 0) != 0;
+  const long long imn = wave_min_i64(feas ? ir : 0), imx = wave_max_i64(feas ? ir : 0);
+  const uint32_t dmx = wave_max_u32((uint32_t)dr), tmx = wave_max_u32((uint32_t)trw), amx = wave_max_u32((uint32_t)arw);
+  const uint64_t pmx = wave_max_u64(pref);
+  if (lane == 0) {
+    TopoScratch* s = a.scr;
+    if (cnt) atomicAdd(&s->hsize, (unsigned long long)__popcll(cnt));
+    if (zbits) atomicOr(&s->zones, zbits);
+    if (emp) atomicOr(&s->empty, 1);
+    if (imn < 0) atomicMin(&s->imin, imn);
+    if (imx > 0) atomicMax(&s->imax, imx);
+    if (dmx) atomicMax(&s->dev_max, (int)dmx);
+    if (tmx) atomicMax(&s->taint_max, (int)tmx);
+    if (amx) atomicMax(&s->aff_max, (int)amx);
+    if (pmx) atomicMax(&s->rsv_pref, (unsigned long long)pmx);
+  }
+}
+
+hipError_t launch_topo_sums(hipStream_t s, const TopoKArgs& a);
+hipError_t launch_topo_pts(hipStream_t s, const TopoKArgs& a);
 hipError_t launch_topo_norm(hipStream_t s, const TopoKArgs& a);
+TopoScratch topo_scratch_init();
 
 }  // namespace ks

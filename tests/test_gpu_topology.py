@@ -165,3 +165,22 @@ def test_refusals(runtime):
         assert e.value.rc == abi.KS_EINVAL
     finally:
         ev.close()
+
+
+def test_graph_and_direct_launches_agree(runtime, oracle_lib):
+    """the topology path's iterations run as one HIP graph per 4 iterations; with per-kernel profiling events on they
+    are launched one by one -- both give the oracle's schedule, and the step runs several topology steps per pass"""
+    w = synth.with_topology(synth.c2_default(n_nodes=600, n_pods=900), seed=50)
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), nthreads=8, **w.tables())
+    want = orc.schedule(w.pods)
+    orc.close()
+    for prof in (False, True):
+        ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+        try:
+            ev.set_profile(prof)
+            got = ev.schedule(w.pods)
+            assert_same_results(got, want, f"profile={prof}")
+            st = ev.stats()
+            assert st["passes"] > 0.8 * w.pods.n  # (every topology pod is a one-pod commit)
+        finally:
+            ev.close()
