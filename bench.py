@@ -12,8 +12,9 @@ The metric names 5k AND 100k nodes, so the same line carries ``c5``: configs[4] 
 Fit + LoadAware) timed the same way — on one GPU at N=1, node-sharded over the N ranks at N>1 (strong
 scaling: every rank sweeps its node range, one RCCL allgather of per-shard candidates per pass).
 At N=1 it also carries ``c3`` (configs[2]: NUMA + DeviceShare joint allocation, 5k nodes), ``c4`` (configs[3]:
-20k nodes with 50k Reservations) and ``c2d`` (C2 with the v1beta2 default profile's upstream plugins on as well:
-NodeResourcesBalancedAllocation, TaintToleration, NodeAffinity, NodePorts) and ``c3r`` (the shipped profile's
+20k nodes with 50k Reservations), ``c2d`` (C2 under the complete v1beta2 default profile's upstream plugins as well:
+NodeResourcesBalancedAllocation, TaintToleration, NodeAffinity, NodePorts, PodTopologySpread with the system default
+constraints, InterPodAffinity), ``c2s`` (c2d without the last two: the round-4 c2d) and ``c3r`` (the shipped profile's
 Reservation + NodeNUMAResource + DeviceShare together: C3's nodes with 12.5k reservations), each with its own CPU
 baseline, sample parity and roofline.
 
@@ -52,16 +53,16 @@ METRIC = "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k no
 def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
 
-    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f", "c2t"):
+    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c2s", "c3r", "c3f"):
         raise SystemExit(f"unknown config {name}")
-    if name == "c2t":
-        # the complete v1beta2 default profile: c2d + PodTopologySpread (system default constraints for the pods owned
-        # by a ReplicaSet, own constraints) and InterPodAffinity (synth.topology_specs)
+    if name == "c2d":
+        # the complete v1beta2 default profile: c2s's plugins + PodTopologySpread (system default constraints for the
+        # pods owned by a ReplicaSet, own constraints) and InterPodAffinity (synth.topology_specs)
         w = synth.c2_default(seed=seed, n_pods=n_pods) if n_pods else synth.c2_default(seed=seed)
         w = synth.with_topology(w, seed=seed + 9)
-        w.name = "C2-default+topology"
+        w.name = "C2-default"
         return w
-    fn = {"c2d": synth.c2_default, "c3r": synth.c3_rsv, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
+    fn = {"c2s": synth.c2_default, "c3r": synth.c3_rsv, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
 
@@ -483,7 +484,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c3r", "c3f", "c2t"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c2s", "c3r", "c3f"])
     ap.add_argument("--pods", type=int, default=0, help="pods per step (default: the config's own count)")
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
@@ -499,7 +500,7 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
     ap.add_argument("--c5-steps", type=int, default=3)
     ap.add_argument("--c5-warmup", type=int, default=1)
-    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d / c3r sub-records")
+    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d / c2s / c3r sub-records")
     ap.add_argument("--sub-steps", type=int, default=3)
     ap.add_argument("--sub-warmup", type=int, default=1)
     ap.add_argument("--no-preempt", action="store_true", help="skip the preempt (ElasticQuota PostFilter) record")
@@ -590,11 +591,11 @@ def main():
     if not args.no_sub and world == 1 and args.config == "c2":
         # SURVEY's C3 (NUMA + DeviceShare) and C4 (Reservation) workloads, each timed like the headline with its own
         # CPU baseline, sample parity and commit roofline (single GPU: neither is node-sharded)
-        # c2d: C2 under the v1beta2 default profile's upstream plugins as well (BalancedAllocation, TaintToleration,
-        # NodeAffinity, NodePorts)
         # c3r: the shipped profile's plugin set (Reservation + NodeNUMAResource + DeviceShare) on C3's nodes with C4-style
         # reservations (synth.c3_rsv)
-        for sub in ("c3", "c4", "c2d", "c3r"):
+        # c2d: C2 under the complete v1beta2 default profile (c2s + PodTopologySpread + InterPodAffinity); c2s: without
+        # those two (the round-4 c2d)
+        for sub in ("c3", "c4", "c2d", "c2s", "c3r"):
             ws = build_workload(sub, seed=20261015)
             rs, ress = run_config(ws, args, None, 1, 0, 0, False, args.sub_steps, args.sub_warmup, sub,
                                   not args.no_profile)

@@ -751,7 +751,7 @@ def c2_default(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10000, **kw)
     w = c2(seed=seed, n_nodes=n_nodes, n_pods=n_pods, **kw)
     w.profile.balanced = NodeResourcesBalancedAllocationArgs()
     w = with_static_plugins(w)
-    w.name = "C2-default"
+    w.name = "C2-static"
     return w
 
 

@@ -14,7 +14,7 @@ os.environ.setdefault("KS_LIB_PATH", os.path.join(os.path.dirname(os.path.dirnam
                                                       "libkoordgpu_split.so" if SPLIT else "libkoordgpu_diag.so"))))
 from koordinator_amd import runtime, synth
 which = sys.argv[1] if len(sys.argv) > 1 else "c2"
-w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4, "c2d": synth.c2_default,
+w = {"c2": synth.c2, "c3": synth.c3, "c4": synth.c4, "c2d": synth.c2_default, "c2s": synth.c2_default,
      "c5": lambda: synth.c5(n_pods=100_000)}[which]()
 cfg = w.cfg
 cfg.profile = 1
