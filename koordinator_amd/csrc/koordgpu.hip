@@ -3795,9 +3795,32 @@ static int topo_step(ks_ctx* ctx) {
   HIPCHK(ctx, launch_topo_sums(ctx->stream, ta));
   HIPCHK(ctx, launch_eval_debug(ctx->nsc, (int)((n + 255) / 256), ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv,
                                 ctx->kc, ctx->st.recs, n, eb.dr, eb.ds, eb.dt, eb.draw, eb.dhi, eb.ddraw, ctx->st.stat,
-                                eb.dtraw, eb.daraw, &ta));
+                                eb.dtraw, eb.daraw, &ta, kernel_feat(ctx)));
   HIPCHK(ctx, launch_topo_pts(ctx->stream, ta));
   HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
+  const int feat = kernel_feat(ctx);
+  if ((feat == 0 || feat == 4) && !ctx->kc.dev && !ctx->kc.rsv && !ctx->kc.numa && !ctx->cpu_loaded) {
+    // Reserve = NodeInfo.AddPod + the LoadAware assign cache + ElasticQuota: the lean one-wave commit
+    TopoCommitArgs tc;
+    tc.d = ctx->d;
+    tc.q = ctx->q;
+    tc.pq = ctx->st.pq;
+    tc.pods = ctx->st.recs;
+    tc.pstat = ctx->st.stat;
+    tc.trec = ctx->st.topo;
+    tc.cursor = ctx->cursor;
+    tc.total_pods = ctx->np;
+    tc.quota_enable = ctx->kc.quota_enable;
+    tc.quota_parent = ctx->kc.quota_parent;
+    tc.ports = ctx->kc.ports;
+    tc.results = ctx->st.results;
+    tc.counters = ctx->counters;
+    tc.topo_count = ctx->topo_count[0];
+    tc.topo_npad = ctx->npad;
+    tc.scr = ctx->topo_scr;
+    HIPCHK(ctx, launch_topo_commit(ctx->stream, tc));
+    return KS_OK;
+  }
   bool qcache = false;
   size_t smem = 0;
   CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, 1, &qcache, &smem);
@@ -4538,12 +4561,14 @@ int ks_eval_pod(ks_ctx* ctx, const ks_pod_cols* pod, uint32_t* reasons, int64_t*
     const TopoKArgs ta = topo_args(ctx, ctx->est, nullptr, eb);
     HIPCHK(ctx, launch_topo_sums(ctx->stream, ta));
     HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
-                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw, &ta));
+                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw, &ta,
+                                  kernel_feat(ctx)));
     HIPCHK(ctx, launch_topo_pts(ctx->stream, ta));
     HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
   } else if (blocks > 0) {
     HIPCHK(ctx, launch_eval_debug(ctx->nsc, blocks, ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv, ctx->kc,
-                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw));
+                                  ctx->est.recs, n, dr, ds, dt, draw, dhi, ddraw, ctx->est.stat, dtraw, daraw, nullptr,
+                                  kernel_feat(ctx)));
     if (ctx->kc.dev)
       hipLaunchKernelGGL(dev_normalize_debug_kernel, dim3(1), dim3(1024), 0, ctx->stream, n, dr, ddraw, ds, dt,
                          ctx->cfg.deviceshare.plugin_weight);

@@ -9,7 +9,7 @@ namespace ks {
 // debug evaluation of one pod over every node (no Reserve)
 // ------------------------------------------------------------------------------------------
 
-template <int NSC>
+template <int NSC, int FEAT>
 __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRsv* rv, const DevDev* dv, const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n,
                                   uint32_t* reasons, int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord,
                                   int32_t* draw, const PodStat* pstat, int32_t* traw, int32_t* araw,
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     const PodRec p = pod[pi];
     const PodStat* ps = pstat ? pstat + pi : nullptr;
     RsvOut ro;
-    EvalOut o = eval_full<NSC, true, false, 15>(
+    EvalOut o = eval_full<NSC, true, false, FEAT>(
         c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
         [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
     if (c.stat) stat_eval(c, *ps, d.taints_hard[i], d.taints_soft[i], d.labels[i], d.host_ports[i], o);
@@ -61,18 +61,31 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
 }
 
 
+// The plugin-set variant the context's kernels use (FEAT 0: Fit + LoadAware [+ quota], FEAT 4: + DeviceShare / the
+// dictionary plugins) or the generic one
+template <int NSC>
+static void launch_nsc(int feat, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,
+                       const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons, int64_t* scores,
+                       int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw, const PodStat* pstat, int32_t* traw,
+                       int32_t* araw, const TopoKArgs& t, int32_t on) {
+  if (feat == 0)
+    hipLaunchKernelGGL((eval_debug_kernel<NSC, 0>), dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+  else if (feat == 4)
+    hipLaunchKernelGGL((eval_debug_kernel<NSC, 4>), dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+  else
+    hipLaunchKernelGGL((eval_debug_kernel<NSC, 15>), dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+}
+
 hipError_t launch_eval_debug(int nsc, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,
                              const DevNuma* nv, Cfg c, const PodRec* pod, int64_t n, uint32_t* reasons,
                              int64_t* scores, int64_t* total, int32_t* raw, int32_t* hiord, int32_t* draw,
-                             const PodStat* pstat, int32_t* traw, int32_t* araw, const TopoKArgs* tk) {
+                             const PodStat* pstat, int32_t* traw, int32_t* araw, const TopoKArgs* tk, int feat) {
   const TopoKArgs t = tk ? *tk : TopoKArgs{};
   const int32_t on = tk ? 1 : 0;
-  if (nsc == 0)
-    hipLaunchKernelGGL(eval_debug_kernel<0>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
-  else if (nsc == 2)
-    hipLaunchKernelGGL(eval_debug_kernel<2>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
-  else
-    hipLaunchKernelGGL(eval_debug_kernel<4>, dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+  const int f = (feat == 0 || feat == 4) ? feat : 15;
+  if (nsc == 0) launch_nsc<0>(f, blocks, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+  else if (nsc == 2) launch_nsc<2>(f, blocks, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+  else launch_nsc<4>(f, blocks, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
   return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ struct TopoScratch {
   unsigned long long best;                        // selectHost key (total + 1) << 32 | ~node (0)
   unsigned int done;                              // topo_norm_kernel workgroups finished (0)
   long long best_total;                           // the chosen node's total (the pod's result score)
+  long long best_node;                            // ... the node (-1 = none feasible)
 };
 
 __device__ __forceinline__ int tp_kind(uint64_t w) { return (int)(w & 0xFF); }
@@ -310,6 +311,26 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
   }
 }
 
+// The lean one-pod commit of a topology pod for the plugin sets whose Reserve is NodeInfo.AddPod + the LoadAware
+// assign cache + ElasticQuota (kernel variants 0 and 4 without DeviceShare, Reservation, NodeNUMAResource)
+struct TopoCommitArgs {
+  DevNodes d;
+  DevQuotas q;
+  DevPodQuota pq;
+  const PodRec* pods;
+  const PodStat* pstat;
+  const TopoRec* trec;
+  int32_t* cursor;
+  int32_t total_pods;
+  int32_t quota_enable, quota_parent, ports;
+  ks_result* results;
+  unsigned long long* counters;
+  int32_t* topo_count;
+  int64_t topo_npad;
+  const TopoScratch* scr;
+};
+
+hipError_t launch_topo_commit(hipStream_t s, const TopoCommitArgs& a);
 hipError_t launch_topo_sums(hipStream_t s, const TopoKArgs& a);
 hipError_t launch_topo_pts(hipStream_t s, const TopoKArgs& a);
 hipError_t launch_topo_norm(hipStream_t s, const TopoKArgs& a);

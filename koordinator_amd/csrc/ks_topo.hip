@@ -24,6 +24,7 @@
 #include <climits>
 #include <cstring>
 
+#include "ks_pass.h"  // (quota_admit)
 #include "ks_topo.h"
 
 namespace ks {
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a) {
       a.cand_second[0] = 0;
     }
     s->best_total = b ? (long long)(b >> 32) - 1 : 0;
+    s->best_node = b ? (long long)(0xFFFFFFFFull - (b & 0xFFFFFFFFull)) : -1;
   }
   for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&s->zsum[0][0])[k] = 0;
   if (tid < KS_TOPO_TERMS) {
@@ -251,6 +253,65 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a) {
     s->best = 0;
     s->done = 0;
   }
+}
+
+// One wave: ElasticQuota PreFilter (quota_admit, lane = dimension), then on the step's chosen node the Reserve of the
+// plugin sets without DeviceShare / Reservation / NodeNUMAResource -- NodeInfo.AddPod (Requested, NonZeroRequested,
+// pod count, UsedPorts), podAssignCache.assign (the LoadAware estimate terms, prod too for a prod pod), the quota chain's
+// used (non-preemptible used) and the pod's topology properties -- the same column updates the commit kernel's
+// slot rows write back (ks_unreserve's inverse), then the cursor.
+__global__ __launch_bounds__(64) void topo_commit_kernel(TopoCommitArgs a) {
+  const int lane = threadIdx.x;
+  const int32_t c = *a.cursor;
+  if (c >= a.total_pods) return;
+  const TopoRec tr = a.trec[c];
+  if (!(tr.flags & KS_TOPO_DYN)) return;
+  const PodRec p = a.pods[c];
+  const uint32_t pmask = a.pq.mask[c];
+  const int64_t qreq = lane < KS_QUOTA_DIMS ? a.pq.req[lane][c] : 0;
+  uint32_t st = 0;
+  if (a.quota_enable && p.quota >= 0)
+    st = quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
+                     a.quota_parent != 0, p.quota, p.flags, pmask, qreq);
+  ks_result r{-1, st, 0, -1, 0, 0, 0};
+  const int64_t n = a.scr->best_node;
+  if (!st && n < 0) r.status = KS_S_UNSCHEDULABLE;
+  if (!st && n >= 0) {
+    r = ks_result{(int32_t)n, KS_S_SCHEDULED, a.scr->best_total, -1, 0, 0, 0};
+    if (a.quota_enable && p.quota >= 0 && lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u))
+      for (int32_t cur = p.quota; cur >= 0; cur = a.q.parent[cur]) {
+        a.q.used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+        if (p.flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
+      }
+    if (lane == 0) {
+      DevNodes& d = a.d;
+      d.req_cpu[n] += p.cpu;
+      d.req_mem[n] += p.mem;
+      d.req_eph[n] += p.eph;
+      for (int k = 0; k < KS_MAX_SCALARS; ++k) d.req_sc[k][n] += p.sc[k];
+      d.nz_cpu[n] += p.nzcpu;
+      d.nz_mem[n] += p.nzmem;
+      d.pod_count[n] += 1;
+      d.la_term_cpu[n] += p.est_cpu;
+      d.la_term_mem[n] += p.est_mem;
+      if (p.flags & KS_POD_PROD) {
+        d.la_pterm_cpu[n] += p.est_cpu;
+        d.la_pterm_mem[n] += p.est_mem;
+      }
+      if (a.ports & 1) d.host_ports[n] |= a.pstat[c].pwant;
+      for (uint32_t m = tr.props; m; m &= m - 1u) a.topo_count[(int64_t)(__ffs((int)m) - 1) * a.topo_npad + n] += 1;
+    }
+  }
+  if (lane == 0) {
+    a.results[c] = r;
+    *a.cursor = c + 1;
+    atomicAdd(&a.counters[0], 1ull);
+  }
+}
+
+hipError_t launch_topo_commit(hipStream_t s, const TopoCommitArgs& a) {
+  hipLaunchKernelGGL(topo_commit_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
 }
 
 static unsigned topo_blocks(const TopoKArgs& a) { return (unsigned)std::max<int64_t>(1, (a.n + kTopoThreads - 1) / kTopoThreads); }
