@@ -192,9 +192,12 @@ __device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr
   }
   for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) (&l.zsum[0][0])[k] = (&a.scr->zsum[0][0])[k];
   __syncthreads();
+  uint32_t zkey = 0;  // terms with the zonal key (a register mask: no dynamic index into the record)
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) zkey |= (tp_key(tr.term[t]) == 1 ? 1u : 0u) << t;
   for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) {
     const int t = k / KS_TOPO_ZONES, z = k - t * KS_TOPO_ZONES;
-    if (tp_key(tr.term[t]) == 1 && ((l.zpres[t] >> z) & 1ull)) atomicMin(&l.mins[t], l.zsum[t][z]);
+    if (((zkey >> t) & 1u) && ((l.zpres[t] >> z) & 1ull)) atomicMin(&l.mins[t], l.zsum[t][z]);
   }
   __syncthreads();
 }
@@ -206,6 +209,7 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
                                                const TopoLds& l) {
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
   bool soft_zone = false, need_aff = false;
+#pragma unroll
   for (int t = 0; t < KS_TOPO_TERMS; ++t) {
     const int k = tp_kind(tr.term[t]);
     soft_zone |= k == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
@@ -229,7 +233,8 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       };
       const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, a.labels ? a.labels[i] : 0ull) : true;
       // PodTopologySpread Filter: the first hard constraint that fails
-      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    #pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
         const uint64_t w = tr.term[t];
         if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD) continue;
         if (tp_key(w) == 1 && !has_zone) {  // ErrReasonNodeLabelNotMatch
@@ -247,7 +252,8 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       }
       // InterPodAffinity Filter: affinity, anti-affinity, existing pods' anti-affinity -- the first that fails
       bool aff_terms = false, missing = false, exist = true;
-      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    #pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
         if (tp_kind(tr.term[t]) != KS_TOPO_K_AFFINITY) continue;
         aff_terms = true;
         if (tp_key(tr.term[t]) == 1 && !has_zone) missing = true;
@@ -257,11 +263,15 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       if (aff_terms && (missing || (!exist && !(a.scr->any_all == 0 && (tr.flags & KS_TOPO_SELF_AFFINITY))))) {
         ipa = KS_R_POD_AFFINITY;
       } else {
-        for (int t = 0; t < KS_TOPO_TERMS && !ipa; ++t) {
+#pragma unroll
+        for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+          if (ipa) break;
           const uint64_t w = tr.term[t];
           if (tp_kind(w) == KS_TOPO_K_ANTI && (tp_key(w) == 0 || has_zone) && domain(t) > 0) ipa = KS_R_POD_ANTI_AFFINITY;
         }
-        for (int t = 0; t < KS_TOPO_TERMS && !ipa; ++t) {
+#pragma unroll
+        for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+          if (ipa) break;
           const uint64_t w = tr.term[t];
           if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && (tp_key(w) == 0 || has_zone) && domain(t) > 0)
             ipa = KS_R_EXISTING_ANTI_AFFINITY;
@@ -274,7 +284,8 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
         for (int k = 0; k < KS_NUM_SCORE_PLUGINS; ++k) a.scores[i * KS_NUM_SCORE_PLUGINS + k] = 0;
       }
       // InterPodAffinity Score: weight x matching pods in the node's domain, per score term
-      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    #pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
         const uint64_t w = tr.term[t];
         if (tp_kind(w) == KS_TOPO_K_SCORE && (tp_key(w) == 0 || has_zone)) ir += (long long)tp_param(w) * domain(t);
       }

@@ -649,7 +649,8 @@ def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node
     sel = {a: LabelSelector((("app", a),)) for a in apps}
     anti_a = AffinityTerm(HOSTNAME, sel["A"])
     aff_d = AffinityTerm(ZONE, sel["D"])
-    pref_c = (20, AffinityTerm(HOSTNAME, sel["C"]))
+    # (namespaceSelector {} = every namespace: app-C pods of "other" count too)
+    pref_c = (20, AffinityTerm(HOSTNAME, sel["C"], namespace_selector=LabelSelector()))
     pref_b = (30, AffinityTerm(ZONE, sel["B"]))
     node_labels = []
     for i in range(n_nodes):
@@ -705,6 +706,10 @@ def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node
     return node_labels, existing, pending
 
 
+# the namespaces' labels (the shim's namespace lister) for namespaceSelector terms
+TOPO_NAMESPACE_LABELS = {"default": {"team": "a"}, "other": {"team": "b"}}
+
+
 def with_topology(w: Workload, seed: int = SEED + 8, spread_weight: int = 2, affinity_weight: int = 1,
                   **kw) -> Workload:
     """The workload with upstream PodTopologySpread and InterPodAffinity switched on and topology_specs compiled into
@@ -712,7 +717,7 @@ def with_topology(w: Workload, seed: int = SEED + 8, spread_weight: int = 2, aff
     from .topology_plugins import compile_topology, install
     rng = np.random.Generator(np.random.PCG64(seed))
     node_labels, existing, pending = topology_specs(w.nodes.n, w.pods.n, rng, **kw)
-    c = compile_topology(node_labels, existing, pending)
+    c = compile_topology(node_labels, existing, pending, namespace_labels=TOPO_NAMESPACE_LABELS)
     install(c, w.nodes, w.pods)
     w.profile.topology = True
     w.profile.topology_spread_weight = spread_weight

@@ -60,10 +60,13 @@ class SpreadConstraint:
 
 @dataclass(frozen=True)
 class AffinityTerm:
-    """PodAffinityTerm without a namespaceSelector: namespaces () = the owning pod's namespace."""
+    """PodAffinityTerm: the pods of `namespaces` and of the namespaces `namespace_selector` selects (by the namespaces'
+    labels) whose labels `selector` selects; neither given = the owning pod's namespace (getNamespacesFromPodAffinityTerm).
+    A nil selector selects nothing, an empty one everything."""
     topology_key: str
     selector: Optional[LabelSelector] = None
     namespaces: Tuple[str, ...] = ()
+    namespace_selector: Optional[LabelSelector] = None
 
 
 @dataclass
@@ -113,14 +116,25 @@ def selector_matches(sel: Optional[LabelSelector], labels: Dict[str, str]) -> bo
     return True
 
 
-def term_namespaces(term: AffinityTerm, owner: TopoPod) -> Tuple[str, ...]:
-    """getNamespacesFromPodAffinityTerm: the term's namespaces, or the owner's namespace when it lists none"""
-    return tuple(sorted(set(term.namespaces))) if term.namespaces else (owner.namespace,)
+def term_namespaces(term: AffinityTerm, owner: TopoPod,
+                    namespace_labels: Optional[Dict[str, Dict[str, str]]] = None) -> Tuple[str, ...]:
+    """The namespaces whose pods the term can match: getNamespacesFromPodAffinityTerm (the term's namespaces, or the
+    owner's when it lists none and has no namespaceSelector) plus the namespaces its namespaceSelector selects
+    (AffinityTerm.Matches' NamespaceSelector.Matches(nsLabels) / mergeAffinityTermNamespacesIfNotEmpty), resolved over
+    the namespace labels the shim's namespace lister holds"""
+    if not term.namespaces and term.namespace_selector is None:
+        return (owner.namespace,)
+    out = set(term.namespaces)
+    for ns, lab in (namespace_labels or {}).items():
+        if selector_matches(term.namespace_selector, lab):
+            out.add(ns)
+    return tuple(sorted(out))
 
 
-def term_matches(term: AffinityTerm, owner: TopoPod, pod: TopoPod) -> bool:
+def term_matches(term: AffinityTerm, owner: TopoPod, pod: TopoPod,
+                 namespace_labels: Optional[Dict[str, Dict[str, str]]] = None) -> bool:
     """AffinityTerm.Matches (framework/types.go): the pod's namespace among the term's and its labels selected"""
-    return pod.namespace in term_namespaces(term, owner) and selector_matches(term.selector, pod.labels)
+    return pod.namespace in term_namespaces(term, owner, namespace_labels) and selector_matches(term.selector, pod.labels)
 
 
 def spread_constraints(pod: TopoPod, hard: bool) -> List[SpreadConstraint]:
@@ -152,7 +166,7 @@ class Compiled:
     pod_flags: np.ndarray              # [p] uint32 KS_TOPO_*
 
 
-def _prop_has(prop: tuple, pod: TopoPod) -> bool:
+def _prop_has(prop: tuple, pod: TopoPod, hard_weight: int = 1, nsl=None) -> bool:
     kind = prop[0]
     if kind == "sel":  # countPodsMatchSelector: not terminating, same namespace, selector
         _, ns, sel = prop
@@ -163,23 +177,23 @@ def _prop_has(prop: tuple, pod: TopoPod) -> bool:
     if kind == "all":
         return all(pod.namespace in nss and selector_matches(sel, pod.labels) for nss, sel in prop[1])
     if kind == "carry":
-        return prop in _carried(pod)
+        return prop in _carried(pod, hard_weight, nsl)
     raise AssertionError(prop)
 
 
-def _carried(pod: TopoPod, hard_weight: int = 1) -> set:
+def _carried(pod: TopoPod, hard_weight: int = 1, nsl=None) -> set:
     """The carry properties of a pod: its required anti-affinity terms, and its hard / preferred (anti-)affinity terms
     with their score weights (hard affinity terms weigh HardPodAffinityWeight)"""
     out = set()
     for t in pod.anti_required:
-        out.add(("carry", "anti", term_namespaces(t, pod), t.selector, t.topology_key, 0))
+        out.add(("carry", "anti", term_namespaces(t, pod, nsl), t.selector, t.topology_key, 0))
     if hard_weight > 0:
         for t in pod.affinity_required:
-            out.add(("carry", "score", term_namespaces(t, pod), t.selector, t.topology_key, hard_weight))
+            out.add(("carry", "score", term_namespaces(t, pod, nsl), t.selector, t.topology_key, hard_weight))
     for w, t in pod.affinity_preferred:
-        out.add(("carry", "score", term_namespaces(t, pod), t.selector, t.topology_key, w))
+        out.add(("carry", "score", term_namespaces(t, pod, nsl), t.selector, t.topology_key, w))
     for w, t in pod.anti_preferred:
-        out.add(("carry", "score", term_namespaces(t, pod), t.selector, t.topology_key, -w))
+        out.add(("carry", "score", term_namespaces(t, pod, nsl), t.selector, t.topology_key, -w))
     return out
 
 
@@ -191,10 +205,13 @@ def pack_term(kind: int, prop: int, key: int, param: int, flags: int = 0) -> int
 
 
 def compile_topology(node_labels: Sequence[Dict[str, str]], existing: Sequence[Tuple[int, TopoPod]],
-                     pending: Sequence[TopoPod], hard_weight: int = 1, zone_key: str = ZONE) -> Compiled:
+                     pending: Sequence[TopoPod], hard_weight: int = 1, zone_key: str = ZONE,
+                     namespace_labels: Optional[Dict[str, Dict[str, str]]] = None) -> Compiled:
     """The properties, node counters and per-pod query terms of a cluster: node labels (every node has its hostname),
-    the running pods as (node row, pod), the pending pods in queue order.  Raises StaticPluginError for what the
-    device does not model (other topology keys, too many properties / terms / zones)."""
+    the running pods as (node row, pod), the pending pods in queue order, the namespaces' labels (namespaceSelector).
+    Raises StaticPluginError for what the device does not model (other topology keys, too many properties / terms /
+    zones)."""
+    nsl = namespace_labels
     n = len(node_labels)
     zones: List[str] = []
     node_zone = np.full(n, -1, np.int32)
@@ -216,7 +233,7 @@ def compile_topology(node_labels: Sequence[Dict[str, str]], existing: Sequence[T
     everyone = [p for _, p in existing] + list(pending)
     carried_all = set()
     for p in everyone:
-        carried_all |= _carried(p, hard_weight)
+        carried_all |= _carried(p, hard_weight, nsl)
     props: List[tuple] = []
 
     def prop_index(pr: tuple) -> int:
@@ -250,13 +267,13 @@ def compile_topology(node_labels: Sequence[Dict[str, str]], existing: Sequence[T
             terms.append(pack_term(KIND["spread_soft"], pi, key_index(c.topology_key), c.max_skew,
                                    abi.KS_TOPO_T_ELIG_ZONE if sz else 0))
         if pod.affinity_required:
-            pi = prop_index(("all", tuple((term_namespaces(t, pod), t.selector) for t in pod.affinity_required)))
+            pi = prop_index(("all", tuple((term_namespaces(t, pod, nsl), t.selector) for t in pod.affinity_required)))
             for t in pod.affinity_required:
                 terms.append(pack_term(KIND["affinity"], pi, key_index(t.topology_key), 0))
-            if all(term_matches(t, pod, pod) for t in pod.affinity_required):
+            if all(term_matches(t, pod, pod, nsl) for t in pod.affinity_required):
                 flags[i] |= abi.KS_TOPO_SELF_AFFINITY
         for t in pod.anti_required:
-            pi = prop_index(("term", term_namespaces(t, pod), t.selector))
+            pi = prop_index(("term", term_namespaces(t, pod, nsl), t.selector))
             terms.append(pack_term(KIND["anti"], pi, key_index(t.topology_key), 0))
         for cp in sorted(carried_all, key=repr):
             _, kind, nss, sel, key, w = cp
@@ -267,10 +284,10 @@ def compile_topology(node_labels: Sequence[Dict[str, str]], existing: Sequence[T
             else:
                 terms.append(pack_term(KIND["score"], prop_index(cp), key_index(key), w))
         for w, t in pod.affinity_preferred:
-            terms.append(pack_term(KIND["score"], prop_index(("term", term_namespaces(t, pod), t.selector)),
+            terms.append(pack_term(KIND["score"], prop_index(("term", term_namespaces(t, pod, nsl), t.selector)),
                                    key_index(t.topology_key), w))
         for w, t in pod.anti_preferred:
-            terms.append(pack_term(KIND["score"], prop_index(("term", term_namespaces(t, pod), t.selector)),
+            terms.append(pack_term(KIND["score"], prop_index(("term", term_namespaces(t, pod, nsl), t.selector)),
                                    key_index(t.topology_key), -w))
         if len(terms) > abi.KS_TOPO_TERMS:
             raise StaticPluginError(f"pod {i}: {len(terms)} topology terms (the device holds {abi.KS_TOPO_TERMS})")
@@ -283,13 +300,13 @@ def compile_topology(node_labels: Sequence[Dict[str, str]], existing: Sequence[T
     node_count = np.zeros((abi.KS_TOPO_PROPS, n), np.int32)
     for nd, pod in existing:
         for pi, pr in enumerate(props):
-            if _prop_has(pr, pod) if pr[0] != "carry" else pr in _carried(pod, hard_weight):
+            if _prop_has(pr, pod, hard_weight, nsl):
                 node_count[pi, nd] += 1
     pod_props = np.zeros(len(pending), np.uint32)
     for i, pod in enumerate(pending):
         m = 0
         for pi, pr in enumerate(props):
-            if (_prop_has(pr, pod) if pr[0] != "carry" else pr in _carried(pod, hard_weight)):
+            if _prop_has(pr, pod, hard_weight, nsl):
                 m |= 1 << pi
         pod_props[i] = m
     pod_terms = np.zeros((abi.KS_TOPO_TERMS, len(pending)), np.uint64)

@@ -45,13 +45,13 @@ def _selector_matches(sel, labels: Dict[str, str]) -> bool:
     return True
 
 
-def _term_ns(term, owner) -> Tuple[str, ...]:
-    return tuple(term.namespaces) if term.namespaces else (owner.namespace,)
-
-
-def _term_matches(term, owner, pod) -> bool:
-    """framework.AffinityTerm.Matches without a namespaceSelector"""
-    return pod.namespace in _term_ns(term, owner) and _selector_matches(term.selector, pod.labels)
+def _term_matches(term, owner, pod, ns_labels) -> bool:
+    """framework.AffinityTerm.Matches(pod, nsLabels): Namespaces.Has(pod.Namespace) || NamespaceSelector.Matches(the
+    pod namespace's labels), then the term's selector; Namespaces = getNamespacesFromPodAffinityTerm (the owner's
+    namespace when the term lists none and has no namespaceSelector); a nil namespaceSelector selects nothing"""
+    nss = term.namespaces if (term.namespaces or term.namespace_selector is not None) else (owner.namespace,)
+    ns_ok = pod.namespace in nss or _selector_matches(term.namespace_selector, ns_labels.get(pod.namespace, {}))
+    return ns_ok and _selector_matches(term.selector, pod.labels)
 
 
 def _node_affinity_match(pod, i: int, node_aff) -> bool:
@@ -86,11 +86,12 @@ def _count_match(pods_on_node, sel, ns) -> int:
 
 
 def evaluate(pod, nodes: Sequence[Dict[str, str]], existing: Sequence[Tuple[int, object]], feasible_other: Sequence[bool],
-             spread_weight: int = 2, affinity_weight: int = 1, hard_weight: int = 1, node_aff=None):
+             spread_weight: int = 2, affinity_weight: int = 1, hard_weight: int = 1, node_aff=None, ns_labels=None):
     """One pod against the cluster: returns (pts_fail[n], ipa_fail[n] in {None, "affinity", "anti", "existing"},
     pts_norm[n], ipa_norm[n], totals_add[n]) where the scores are over the nodes feasible for every Filter
     (feasible_other and both plugins' Filters); node_aff(i) -> bool is the pod's required node affinity on node i."""
     N = len(nodes)
+    nsl = ns_labels or {}
     labels = [_labels(nodes[i], i) for i in range(N)]
     on_node: List[List[object]] = [[] for _ in range(N)]
     for nd, p in existing:
@@ -132,21 +133,21 @@ def evaluate(pod, nodes: Sequence[Dict[str, str]], existing: Sequence[Tuple[int,
         for ep in on_node[i]:
             # getExistingAntiAffinityCounts: the placed pods' required anti-affinity terms that match the pod
             for t in ep.anti_required:
-                if _term_matches(t, ep, pod) and t.topology_key in labels[i]:
+                if _term_matches(t, ep, pod, nsl) and t.topology_key in labels[i]:
                     pr = (t.topology_key, labels[i][t.topology_key])
                     exist_anti[pr] = exist_anti.get(pr, 0) + 1
             # getIncomingAffinityAntiAffinityCounts
-            if pod.affinity_required and all(_term_matches(t, pod, ep) for t in pod.affinity_required):
+            if pod.affinity_required and all(_term_matches(t, pod, ep, nsl) for t in pod.affinity_required):
                 for t in pod.affinity_required:
                     if t.topology_key in labels[i]:
                         pr = (t.topology_key, labels[i][t.topology_key])
                         aff_counts[pr] = aff_counts.get(pr, 0) + 1
             for t in pod.anti_required:
-                if _term_matches(t, pod, ep) and t.topology_key in labels[i]:
+                if _term_matches(t, pod, ep, nsl) and t.topology_key in labels[i]:
                     pr = (t.topology_key, labels[i][t.topology_key])
                     anti_counts[pr] = anti_counts.get(pr, 0) + 1
     aff_counts = {k: v for k, v in aff_counts.items() if v != 0}
-    self_all = bool(pod.affinity_required) and all(_term_matches(t, pod, pod) for t in pod.affinity_required)
+    self_all = bool(pod.affinity_required) and all(_term_matches(t, pod, pod, nsl) for t in pod.affinity_required)
     ipa_fail: List[Optional[str]] = [None] * N
     for i in range(N):
         ok = True
@@ -242,7 +243,7 @@ def evaluate(pod, nodes: Sequence[Dict[str, str]], existing: Sequence[Tuple[int,
     topo_score: Dict[str, Dict[str, int]] = {}
 
     def process(term, weight, check_pod, owner, node_i, mult):
-        if _term_matches(term, owner, check_pod) and term.topology_key in labels[node_i]:
+        if _term_matches(term, owner, check_pod, nsl) and term.topology_key in labels[node_i]:
             m = topo_score.setdefault(term.topology_key, {})
             v = labels[node_i][term.topology_key]
             m[v] = m.get(v, 0) + weight * mult

@@ -62,7 +62,8 @@ def _check_eval(w, profile, pods, base_profile=None, other_fn=None):
             if base is not None:
                 rb, sb, bt = base.eval_pod(one)
                 other = list(rb == 0)
-            pf, ipf, pn, inn, add = ref.evaluate(pending[i], node_labels, existing, other, node_aff=_node_aff(w, i))
+            pf, ipf, pn, inn, add = ref.evaluate(pending[i], node_labels, existing, other, node_aff=_node_aff(w, i),
+                                                 ns_labels=synth.TOPO_NAMESPACE_LABELS)
             for n in range(w.nodes.n):
                 assert bool(r[n] & abi.KS_R_TOPOLOGY_SPREAD) == pf[n], f"pod {i} node {n}: spread filter"
                 want = IPA_BITS.get(ipf[n], 0)
@@ -172,7 +173,8 @@ def test_schedule_against_restatement():
     st = orc.read_nodes()
     orc.close()
     for i, p in enumerate(pending):
-        _, _, _, _, add = ref.evaluate(p, node_labels, existing, [True] * len(node_labels))
+        _, _, _, _, add = ref.evaluate(p, node_labels, existing, [True] * len(node_labels),
+                                       ns_labels=synth.TOPO_NAMESPACE_LABELS)
         totals = [a if a is not None else -1 for a in add]
         best = max(totals)
         want = totals.index(best) if best >= 0 else -1
@@ -183,6 +185,33 @@ def test_schedule_against_restatement():
         else:
             assert int(got["status"][i]) == abi.KS_S_UNSCHEDULABLE
     # the counters after the queue are the compiled counters of the final pod set
-    c = compile_topology(node_labels, existing, pending)
+    c = compile_topology(node_labels, existing, pending, namespace_labels=synth.TOPO_NAMESPACE_LABELS)
     assert np.array_equal(st.topo_count, c.node_count)
     assert (got["status"] == abi.KS_S_UNSCHEDULABLE).sum() > 0
+
+
+def test_namespace_selector_cases():
+    """namespaceSelector: the term reaches the selected namespaces' pods (with or without listed namespaces); a nil
+    selector next to listed namespaces adds none; neither = the owner's namespace"""
+    from koordinator_amd.topology_plugins import term_namespaces
+    nsl = {"default": {"team": "a"}, "other": {"team": "b"}, "x": {}}
+    owner = TopoPod(namespace="default")
+    team_b = LabelSelector(match_expressions=(("team", "In", ("b",)),))
+    assert term_namespaces(AffinityTerm(HOSTNAME), owner, nsl) == ("default",)
+    assert term_namespaces(AffinityTerm(HOSTNAME, namespace_selector=LabelSelector()), owner, nsl) == ("default", "other", "x")
+    assert term_namespaces(AffinityTerm(HOSTNAME, namespace_selector=team_b), owner, nsl) == ("other",)
+    assert term_namespaces(AffinityTerm(HOSTNAME, namespaces=("x",), namespace_selector=team_b), owner, nsl) == ("other", "x")
+    assert term_namespaces(AffinityTerm(HOSTNAME, namespaces=("x",)), owner, nsl) == ("x",)
+    # through the oracle: anti-affinity to app=a of team b's namespaces rejects only the node holding other/app=a
+    sel_a = LabelSelector((("app", "a"),))
+    nodes = [{ZONE: "z1"}, {ZONE: "z1"}, {ZONE: "z2"}]
+    existing = [(0, TopoPod(namespace="default", labels={"app": "a"})), (1, TopoPod(namespace="other", labels={"app": "a"}))]
+    pending = [TopoPod(labels={"app": "b"}, anti_required=[AffinityTerm(HOSTNAME, sel_a, namespace_selector=team_b)])]
+    w = synth.c1(n_nodes=3, n_pods=1)
+    install(compile_topology(nodes, existing, pending, namespace_labels=nsl), w.nodes, w.pods)
+    orc = Oracle(_profile().to_ks_config(), w.nodes.copy())
+    r, _, _ = orc.eval_pod(w.pods.rows([0]))
+    orc.close()
+    assert list(r) == [0, abi.KS_R_POD_ANTI_AFFINITY, 0]
+    pf, ipf, _, _, _ = ref.evaluate(pending[0], nodes, existing, [True] * 3, ns_labels=nsl)
+    assert ipf == [None, "anti", None]
