@@ -3797,10 +3797,10 @@ static int topo_step(ks_ctx* ctx) {
                                 ctx->kc, ctx->st.recs, n, eb.dr, eb.ds, eb.dt, eb.draw, eb.dhi, eb.ddraw, ctx->st.stat,
                                 eb.dtraw, eb.daraw, &ta, kernel_feat(ctx)));
   HIPCHK(ctx, launch_topo_pts(ctx->stream, ta));
-  HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
   const int feat = kernel_feat(ctx);
   if ((feat == 0 || feat == 4) && !ctx->kc.dev && !ctx->kc.rsv && !ctx->kc.numa && !ctx->cpu_loaded) {
-    // Reserve = NodeInfo.AddPod + the LoadAware assign cache + ElasticQuota: the lean one-wave commit
+    // Reserve = NodeInfo.AddPod + the LoadAware assign cache + ElasticQuota: the lean commit, by the normalize
+    // kernel's last workgroup
     TopoCommitArgs tc;
     tc.d = ctx->d;
     tc.q = ctx->q;
@@ -3818,9 +3818,10 @@ static int topo_step(ks_ctx* ctx) {
     tc.topo_count = ctx->topo_count[0];
     tc.topo_npad = ctx->npad;
     tc.scr = ctx->topo_scr;
-    HIPCHK(ctx, launch_topo_commit(ctx->stream, tc));
+    HIPCHK(ctx, launch_topo_norm(ctx->stream, ta, &tc));
     return KS_OK;
   }
+  HIPCHK(ctx, launch_topo_norm(ctx->stream, ta));
   bool qcache = false;
   size_t smem = 0;
   CommitArgs ca = commit_args(ctx, ctx->st, ctx->np, 1, &qcache, &smem);

@@ -20,14 +20,14 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   // the topology step (ks_topo.h): the pod at the cursor, only if it is a topology pod
   int64_t pi = 0;
   TopoRec tr;
+  NodeReg<NSC> r;
+  load_node<NSC>(c, d, i, valid ? 1 : 0, r);  // (issued with the step's pod record)
   if (topo) {
-    pi = topo_pod(tk, tr);
+    pi = topo_cur(tk, tr);
     if (pi < 0) return;
     if (tr.flags & KS_TOPO_DYN) topo_stage(tk, tr, tl);
   }
   if (valid) {
-    NodeReg<NSC> r;
-    load_node<NSC>(c, d, i, 1, r);
     const PodRec p = pod[pi];
     const PodStat* ps = pstat ? pstat + pi : nullptr;
     RsvOut ro;

@@ -1119,6 +1119,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
                                 qlds->npused, true, qrow, 0u, pmask, req, /*skip_leaf=*/true);
         }
       }
+      KS_STAMP(6);  // (diagnostic builds: the admission part of the look-ahead)
       if (st_next) return;
       if (top && !((tw >> (tn & 63)) & 1ull)) {
         cn.fast = true;  // its row is in rawtop[j]
@@ -1127,6 +1128,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       }
     } else {
       st_next = a.force ? 0u : admit(j);
+      KS_STAMP(6);
       if (st_next) return;
       if (top && !((touched[tn >> 6] >> (tn & 63)) & 1ull)) {
         cn.fast = true;

@@ -18,6 +18,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include "ks_device.h"
 
 namespace ks {
@@ -60,6 +62,10 @@ struct TopoScratch {
   unsigned int done;                              // topo_norm_kernel workgroups finished (0)
   long long best_total;                           // the chosen node's total (the pod's result score)
   long long best_node;                            // ... the node (-1 = none feasible)
+  // the step's pod, written by topo_sums_kernel (the first kernel of a step) from *cursor: the later kernels read it
+  // with one load instead of the cursor -> record chain (-1 = the cursor's pod is not a topology pod)
+  int32_t cur_pi, _pad1[3];
+  TopoRec cur_rec;
 };
 
 __device__ __forceinline__ int tp_kind(uint64_t w) { return (int)(w & 0xFF); }
@@ -150,6 +156,12 @@ __device__ __forceinline__ int32_t topo_pod(const TopoKArgs& a, TopoRec& rec) {
   return pi;
 }
 
+// the step's pod as topo_sums_kernel left it (every later kernel of the step)
+__device__ __forceinline__ int32_t topo_cur(const TopoKArgs& a, TopoRec& rec) {
+  rec = a.scr->cur_rec;
+  return a.scr->cur_pi;
+}
+
 // the node counts for the term (hard spread: required node affinity + every hard key; soft spread: required node
 // affinity + every soft key when requireAllTopologies; InterPodAffinity: every node)
 __device__ __forceinline__ bool tp_eligible(uint64_t w, uint32_t pflags, bool aff, bool zone_ok) {
@@ -183,6 +195,7 @@ struct TopoLds {
   long long zsum[KS_TOPO_TERMS][KS_TOPO_ZONES];
   unsigned long long zpres[KS_TOPO_TERMS];
   long long mins[KS_TOPO_TERMS];
+  int any_all;  // affinityCounts is not empty
 };
 __device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr, TopoLds& l) {
   const int tid = threadIdx.x;
@@ -190,6 +203,7 @@ __device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr
     l.zpres[tid] = a.scr->zpres[tid];
     l.mins[tid] = a.scr->hmin[tid];
   }
+  if (tid == 0) l.any_all = a.scr->any_all;
   for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) (&l.zsum[0][0])[k] = (&a.scr->zsum[0][0])[k];
   __syncthreads();
   uint32_t zkey = 0;  // terms with the zonal key (a register mask: no dynamic index into the record)
@@ -260,7 +274,7 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
         else if (domain(t) <= 0) exist = false;
       }
       uint32_t ipa = 0;
-      if (aff_terms && (missing || (!exist && !(a.scr->any_all == 0 && (tr.flags & KS_TOPO_SELF_AFFINITY))))) {
+      if (aff_terms && (missing || (!exist && !(l.any_all == 0 && (tr.flags & KS_TOPO_SELF_AFFINITY))))) {
         ipa = KS_R_POD_AFFINITY;
       } else {
 #pragma unroll
@@ -341,10 +355,10 @@ struct TopoCommitArgs {
   const TopoScratch* scr;
 };
 
-hipError_t launch_topo_commit(hipStream_t s, const TopoCommitArgs& a);
 hipError_t launch_topo_sums(hipStream_t s, const TopoKArgs& a);
 hipError_t launch_topo_pts(hipStream_t s, const TopoKArgs& a);
-hipError_t launch_topo_norm(hipStream_t s, const TopoKArgs& a);
+// c != NULL: the last workgroup commits the pod (the lean commit); NULL: it leaves the one-candidate set
+hipError_t launch_topo_norm(hipStream_t s, const TopoKArgs& a, const TopoCommitArgs* c = nullptr);
 TopoScratch topo_scratch_init();
 
 }  // namespace ks

@@ -36,6 +36,7 @@ TopoScratch topo_scratch_init() {
   std::memset(&s, 0, sizeof(s));
   for (int t = 0; t < KS_TOPO_TERMS; ++t) s.hmin[t] = INT_MAX;  // newCriticalPaths: MatchNum math.MaxInt32
   s.smin = LLONG_MAX;
+  s.cur_pi = -1;
   return s;
 }
 
@@ -46,8 +47,12 @@ __global__ __launch_bounds__(kTopoThreads) void topo_sums_kernel(TopoKArgs a) {
   __shared__ int aa;
   TopoRec tr;
   const int32_t pi = topo_pod(a, tr);
-  if (pi < 0 || !(tr.flags & KS_TOPO_DYN)) return;
   const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) {
+    a.scr->cur_pi = pi;
+    a.scr->cur_rec = tr;
+  }
+  if (pi < 0 || !(tr.flags & KS_TOPO_DYN)) return;
   for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&zs[0][0])[k] = 0;
   if (tid < KS_TOPO_TERMS) {
     zp[tid] = 0;
@@ -97,47 +102,79 @@ __device__ __forceinline__ double topo_weight(const DevTopo& t, unsigned long lo
   return t.lw[size < (unsigned long long)t.nlw ? size : (unsigned long long)t.nlw - 1];
 }
 
-__global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
-  __shared__ long long zs[KS_TOPO_TERMS][KS_TOPO_ZONES];
-  TopoRec tr;
-  const int32_t pi = topo_pod(a, tr);
-  if (pi < 0) return;
-  const int tid = threadIdx.x;
-  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
-  const TopoScratch* s = a.scr;
-  if (dyn)
-    for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&zs[0][0])[k] = (&s->zsum[0][0])[k];
-  __syncthreads();
+// Issue the node's loads with the step's pod record, then wait once (a kernel of the step otherwise waits for the record,
+// branches, and only then loads its node)
+#define KS_TOPO_ISSUED(...) asm volatile("" ::__VA_ARGS__)
+
+// PodTopologySpread's raw score of a feasible node (PreScore's pair counts, Score's scoreForCount summed in term order,
+// math.Round); false = an ignored node (initPreScoreState: a soft zonal constraint with requireAllTopologies and no
+// zone label).  Every count is loaded before the f64 sum.
+__device__ __forceinline__ bool topo_spread_raw(const TopoKArgs& a, const TopoRec& tr, int64_t i, int32_t z, double hw,
+                                                double zw, bool ign_zoneless, long long& sr) {
+  // branch-free in the node: a zonal term of a node without the zone loads domain 0 and is not added
+  const bool has_zone = z >= 0;
+  const int zc = has_zone ? z : 0;
+  long long cnt[KS_TOPO_TERMS];
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    const uint64_t w = tr.term[t];
+    cnt[t] = 0;
+    if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) continue;  // (wave-uniform)
+    cnt[t] = tp_key(w) == 1 ? a.scr->zsum[t][zc] : (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i];
+  }
+  double score = 0.0;
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    const uint64_t w = tr.term[t];
+    if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) continue;
+    const double add = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt[t], tp_key(w) == 1 ? zw : hw), (double)(tp_param(w) - 1)));
+    score = (tp_key(w) == 1 && !has_zone) ? score : add;
+  }
+  const bool ignored = ign_zoneless && !has_zone;
+  sr = ignored ? 0 : (long long)::round(score);
+  return !ignored;
+}
+
+__device__ __forceinline__ bool topo_soft_zone(const TopoRec& tr) {
   bool soft_zone = false;
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t)
+    soft_zone |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
+  return soft_zone;
+}
+
+__global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kTopoThreads + tid;
+  const bool in = i < a.n;
+  const TopoScratch* s = a.scr;
+  const uint32_t rs = in ? a.reasons[i] : 1u;
+  const int32_t z = in ? a.t.zone[i] : -1;
+  const int32_t rr = (in && a.rsv_on) ? a.rraw[i] : 0;
+  const unsigned long long hs = s->hsize, zn = s->zones, rp = s->rsv_pref;
+  const int em = s->empty;
+  TopoRec tr;
+  const int32_t pi = topo_cur(a, tr);
+  KS_TOPO_ISSUED("v"(rs), "v"(z), "v"(rr));
+  if (pi < 0) return;
+  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
+  bool soft_zone = false;
+#pragma unroll
   for (int t = 0; t < KS_TOPO_TERMS; ++t)
     soft_zone |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
   const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
   // initPreScoreState's sizes: the hostname's the non-ignored feasible nodes, the zone's their distinct values (a node
   // without the label counts as the value "")
-  const double hw = topo_weight(a.t, s->hsize);
-  const double zw = topo_weight(a.t, (unsigned long long)__popcll(s->zones) + (s->empty ? 1ull : 0ull));
-  const int64_t pref = s->rsv_pref ? (int64_t)(0xFFFFFFFFull - (s->rsv_pref & 0xFFFFFFFFull)) : -1;
-  const int64_t i = (int64_t)blockIdx.x * kTopoThreads + tid;
+  const double hw = topo_weight(a.t, hs);
+  const double zw = topo_weight(a.t, (unsigned long long)__popcll(zn) + (em ? 1ull : 0ull));
+  const int64_t pref = rp ? (int64_t)(0xFFFFFFFFull - (rp & 0xFFFFFFFFull)) : -1;
   bool counted = false;
   long long sr = 0;
   uint64_t rmx = 0;
-  if (i < a.n && a.reasons[i] == 0) {
-    if (a.rsv_on) rmx = i == pref ? 1000ull : (uint64_t)(uint32_t)a.rraw[i];
+  if (in && rs == 0) {
+    if (a.rsv_on) rmx = i == pref ? 1000ull : (uint64_t)(uint32_t)rr;
     if (dyn) {
-      const int32_t z = a.t.zone[i];
-      const bool has_zone = z >= 0;
-      const bool ig = soft_all && soft_zone && !has_zone;
-      if (!ig) {
-        double score = 0.0;
-        for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-          const uint64_t w = tr.term[t];
-          if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || (tp_key(w) == 1 && !has_zone)) continue;
-          const long long cnt = tp_key(w) == 1 ? zs[t][z] : (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i];
-          score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, tp_key(w) == 1 ? zw : hw), (double)(tp_param(w) - 1)));
-        }
-        sr = (long long)::round(score);  // math.Round
-        counted = true;
-      }
+      counted = topo_spread_raw(a, tr, i, z, hw, zw, soft_all && soft_zone, sr);
       a.sraw[i] = sr;
     }
   }
@@ -151,140 +188,28 @@ __global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
   }
 }
 
-__global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a) {
-  __shared__ bool last;
-  TopoRec tr;
-  const int32_t pi = topo_pod(a, tr);
-  if (pi < 0) return;
-  const int tid = threadIdx.x;
-  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
-  TopoScratch* s = a.scr;
-  bool soft_zone = false;
-  for (int t = 0; t < KS_TOPO_TERMS; ++t)
-    soft_zone |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
-  const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
-  const int64_t dmx = s->dev_max, tmx = s->taint_max, amx = s->aff_max;
-  const int64_t rmx = (int64_t)s->rsv_max;
-  const int64_t pref = s->rsv_pref ? (int64_t)(0xFFFFFFFFull - (s->rsv_pref & 0xFFFFFFFFull)) : -1;
-  const long long smin = s->smin, smax = s->smax, imin = s->imin, imax = s->imax;
-  const int64_t i = (int64_t)blockIdx.x * kTopoThreads + tid;
-  uint64_t key = 0;
-  if (i < a.n && a.reasons[i] == 0) {
-    int64_t* sc = a.scores + i * KS_NUM_SCORE_PLUGINS;
-    int64_t tot = a.total[i];
-    // DefaultNormalizeScore (normalize_score.go:24-52): DeviceShare, TaintToleration (reverse), NodeAffinity
-    if (a.dev_on) {
-      const int64_t r = a.draw[i], v = dmx == 0 ? r : 100 * r / dmx;
-      sc[KS_SCORE_DEVICESHARE] = v;
-      tot += v * a.dev_w;
-    }
-    if (a.taint_on) {
-      const int64_t r = a.traw[i], v = tmx == 0 ? 100 : 100 - 100 * r / tmx;
-      sc[KS_SCORE_TAINT] = v;
-      tot += v * a.taint_w;
-    }
-    if (a.aff_on) {
-      const int64_t r = a.araw[i], v = amx == 0 ? r : 100 * r / amx;
-      sc[KS_SCORE_NODE_AFFINITY] = v;
-      tot += v * a.aff_w;
-    }
-    // Reservation: the preferred node scores mostPreferredScore (scoring.go:87-122), DefaultNormalizeScore
-    if (a.rsv_on) {
-      const int64_t r = i == pref ? 1000 : a.rraw[i], v = rmx == 0 ? r : 100 * r / rmx;
-      sc[KS_SCORE_RESERVATION] = v;
-      tot += v * a.rsv_w;
-    }
-    long long pts = 100, ipa = 0;  // no constraint: NormalizeScore's maxScore == 0 gives MaxNodeScore
-    if (dyn) {
-      const bool ig = soft_all && soft_zone && a.t.zone[i] < 0;
-      if (ig) pts = 0;
-      else if (smax != 0) pts = 100 * (smax + smin - a.sraw[i]) / smax;
-      const long long diff = imax - imin;
-      if (diff > 0) ipa = (long long)__dmul_rn(100.0, __ddiv_rn((double)(a.iraw[i] - imin), (double)diff));
-    }
-    sc[KS_SCORE_TOPOLOGY_SPREAD] = pts;
-    sc[KS_SCORE_POD_AFFINITY] = ipa;
-    tot += pts * a.spread_w + ipa * a.ipa_w;
-    a.total[i] = tot;
-    key = ((uint64_t)(tot + 1) << 32) | (0xFFFFFFFFull - (uint64_t)i);  // selectHost: max total, lowest index
-  }
-  const uint64_t km = wave_max_u64(key);
-  if ((tid & 63) == 0 && km) atomicMax(&s->best, (unsigned long long)km);
-  // the last workgroup: the one-candidate set, then the scratch back to its initial image
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) last = atomicAdd(&s->done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (tid == 0) {
-    const unsigned long long b = __hip_atomic_load(&s->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (a.cand_chunk) {
-      if (b) {
-        const int64_t node = (int64_t)(0xFFFFFFFFull - (b & 0xFFFFFFFFull));
-        a.cand_chunk[0] = (uint32_t)(node >> 6);
-        a.cand_t[0] = make_uint2((1u << 6) | (uint32_t)(63 - (node & 63)), 0u);  // an untouched node, key taken as is
-        a.cand_count[0] = 1;
-      } else {
-        a.cand_count[0] = 0;  // no feasible node: the commit reports the pod unschedulable
-      }
-      a.cand_bound[0] = 0;
-      a.cand_top[0] = 0;
-      a.cand_second[0] = 0;
-    }
-    s->best_total = b ? (long long)(b >> 32) - 1 : 0;
-    s->best_node = b ? (long long)(0xFFFFFFFFull - (b & 0xFFFFFFFFull)) : -1;
-  }
-  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&s->zsum[0][0])[k] = 0;
-  if (tid < KS_TOPO_TERMS) {
-    s->zpres[tid] = 0;
-    s->hmin[tid] = INT_MAX;
-  }
-  if (tid == 0) {
-    s->any_all = 0;
-    s->hsize = 0;
-    s->zones = 0;
-    s->empty = 0;
-    s->dev_max = s->taint_max = s->aff_max = 0;
-    s->imin = s->imax = 0;
-    s->smin = LLONG_MAX;
-    s->smax = 0;
-    s->rsv_pref = s->rsv_max = 0;
-    s->best = 0;
-    s->done = 0;
-  }
-}
-
-// One wave: ElasticQuota PreFilter (quota_admit, lane = dimension), then on the step's chosen node the Reserve of the
-// plugin sets without DeviceShare / Reservation / NodeNUMAResource -- NodeInfo.AddPod (Requested, NonZeroRequested,
+// One wave (lane = quota dimension): ElasticQuota PreFilter (quota_admit), then on the step's chosen node the Reserve of
+// the plugin sets without DeviceShare / Reservation / NodeNUMAResource -- NodeInfo.AddPod (Requested, NonZeroRequested,
 // pod count, UsedPorts), podAssignCache.assign (the LoadAware estimate terms, prod too for a prod pod), the quota chain's
-// used (non-preemptible used) and the pod's topology properties -- the same column updates the commit kernel's
-// slot rows write back (ks_unreserve's inverse), then the cursor.
-__global__ __launch_bounds__(64) void topo_commit_kernel(TopoCommitArgs a) {
-  const int lane = threadIdx.x;
-  const int32_t c = *a.cursor;
-  if (c >= a.total_pods) return;
-  const TopoRec tr = a.trec[c];
-  if (!(tr.flags & KS_TOPO_DYN)) return;
-  const PodRec p = a.pods[c];
-  const uint32_t pmask = a.pq.mask[c];
-  const int64_t qreq = lane < KS_QUOTA_DIMS ? a.pq.req[lane][c] : 0;
+// used (non-preemptible used) and the pod's topology properties -- the same column updates the commit kernel's slot rows
+// write back (ks_unreserve's inverse), then the cursor.  p / pmask / qreq: pod c's records, loaded ahead by the caller.
+__device__ __forceinline__ void topo_commit_one(const TopoCommitArgs& a, int lane, int32_t c, const TopoRec& tr,
+                                                const PodRec& p, uint32_t pmask, int64_t qreq, int64_t n, long long total) {
   uint32_t st = 0;
   if (a.quota_enable && p.quota >= 0)
     st = quota_admit(a.q.parent, a.q.limit_mask, a.q.min_mask, a.q.limit, a.q.used, a.q.min, a.q.npused,
                      a.quota_parent != 0, p.quota, p.flags, pmask, qreq);
   ks_result r{-1, st, 0, -1, 0, 0, 0};
-  const int64_t n = a.scr->best_node;
   if (!st && n < 0) r.status = KS_S_UNSCHEDULABLE;
   if (!st && n >= 0) {
-    r = ks_result{(int32_t)n, KS_S_SCHEDULED, a.scr->best_total, -1, 0, 0, 0};
+    r = ks_result{(int32_t)n, KS_S_SCHEDULED, total, -1, 0, 0, 0};
     if (a.quota_enable && p.quota >= 0 && lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u))
       for (int32_t cur = p.quota; cur >= 0; cur = a.q.parent[cur]) {
         a.q.used[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
         if (p.flags & KS_POD_NONPREEMPTIBLE) a.q.npused[(size_t)cur * KS_QUOTA_DIMS + lane] += qreq;
       }
     if (lane == 0) {
-      DevNodes& d = a.d;
+      const DevNodes& d = a.d;
       d.req_cpu[n] += p.cpu;
       d.req_mem[n] += p.mem;
       d.req_eph[n] += p.eph;
@@ -309,9 +234,130 @@ __global__ __launch_bounds__(64) void topo_commit_kernel(TopoCommitArgs a) {
   }
 }
 
-hipError_t launch_topo_commit(hipStream_t s, const TopoCommitArgs& a) {
-  hipLaunchKernelGGL(topo_commit_kernel, dim3(1), dim3(64), 0, s, a);
-  return hipGetLastError();
+// lean != 0: the last workgroup also commits the pod (topo_commit_one, the plugin sets whose Reserve is AddPod + the
+// assign cache + quota); else it leaves the one-candidate set and the chosen node for the general commit kernel
+__global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, TopoCommitArgs ca, int32_t lean) {
+  __shared__ bool last;
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kTopoThreads + tid;
+  const bool in = i < a.n;
+  TopoScratch* s = a.scr;
+  // the node's inputs and the reductions' results, issued with the step's pod record
+  const uint32_t rs = in ? a.reasons[i] : 1u;
+  const int64_t tot0 = in ? a.total[i] : 0;
+  const int32_t dr = (in && a.dev_on) ? a.draw[i] : 0, tr_ = (in && a.taint_on) ? a.traw[i] : 0,
+                ar = (in && a.aff_on) ? a.araw[i] : 0, rr = (in && a.rsv_on) ? a.rraw[i] : 0;
+  const long long sri = in ? a.sraw[i] : 0, iri = in ? a.iraw[i] : 0;
+  const int32_t z = in ? a.t.zone[i] : -1;
+  const int64_t dmx = s->dev_max, tmx = s->taint_max, amx = s->aff_max;
+  const int64_t rmx = (int64_t)s->rsv_max;
+  const unsigned long long rp = s->rsv_pref;
+  const long long smin = s->smin, smax = s->smax, imin = s->imin, imax = s->imax;
+  TopoRec tr;
+  const int32_t pi = topo_cur(a, tr);
+  KS_TOPO_ISSUED("v"(rs), "v"(tot0), "v"(dr), "v"(tr_), "v"(ar), "v"(rr), "v"(sri), "v"(iri), "v"(z));
+  if (pi < 0) return;
+  // the commit's pod records (wave 0 of every workgroup: the last one to finish uses them)
+  PodRec p{};
+  uint32_t pmask = 0;
+  int64_t qreq = 0;
+  if (lean && tid < 64) {
+    p = ca.pods[pi];
+    pmask = ca.pq.mask[pi];
+    qreq = tid < KS_QUOTA_DIMS ? ca.pq.req[tid][pi] : 0;
+  }
+  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
+  const bool soft_zone = topo_soft_zone(tr);
+  const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
+  const int64_t pref = rp ? (int64_t)(0xFFFFFFFFull - (rp & 0xFFFFFFFFull)) : -1;
+  uint64_t key = 0;
+  if (in && rs == 0) {
+    int64_t* sc = a.scores + i * KS_NUM_SCORE_PLUGINS;
+    int64_t tot = tot0;
+    // DefaultNormalizeScore (normalize_score.go:24-52): DeviceShare, TaintToleration (reverse), NodeAffinity
+    if (a.dev_on) {
+      const int64_t v = dmx == 0 ? dr : 100 * (int64_t)dr / dmx;
+      sc[KS_SCORE_DEVICESHARE] = v;
+      tot += v * a.dev_w;
+    }
+    if (a.taint_on) {
+      const int64_t v = tmx == 0 ? 100 : 100 - 100 * (int64_t)tr_ / tmx;
+      sc[KS_SCORE_TAINT] = v;
+      tot += v * a.taint_w;
+    }
+    if (a.aff_on) {
+      const int64_t v = amx == 0 ? ar : 100 * (int64_t)ar / amx;
+      sc[KS_SCORE_NODE_AFFINITY] = v;
+      tot += v * a.aff_w;
+    }
+    // Reservation: the preferred node scores mostPreferredScore (scoring.go:87-122), DefaultNormalizeScore
+    if (a.rsv_on) {
+      const int64_t r = i == pref ? 1000 : rr, v = rmx == 0 ? r : 100 * r / rmx;
+      sc[KS_SCORE_RESERVATION] = v;
+      tot += v * a.rsv_w;
+    }
+    long long pts = 100, ipa = 0;  // no constraint: NormalizeScore's maxScore == 0 gives MaxNodeScore
+    if (dyn) {
+      const bool ig = soft_all && soft_zone && z < 0;
+      if (ig) pts = 0;
+      else if (smax != 0) pts = 100 * (smax + smin - sri) / smax;
+      const long long diff = imax - imin;
+      if (diff > 0) ipa = (long long)__dmul_rn(100.0, __ddiv_rn((double)(iri - imin), (double)diff));
+    }
+    sc[KS_SCORE_TOPOLOGY_SPREAD] = pts;
+    sc[KS_SCORE_POD_AFFINITY] = ipa;
+    tot += pts * a.spread_w + ipa * a.ipa_w;
+    a.total[i] = tot;
+    key = ((uint64_t)(tot + 1) << 32) | (0xFFFFFFFFull - (uint64_t)i);  // selectHost: max total, lowest index
+  }
+  const uint64_t km = wave_max_u64(key);
+  if ((tid & 63) == 0 && km) atomicMax(&s->best, (unsigned long long)km);
+  // the last workgroup: the commit or the one-candidate set, then the scratch back to its initial image
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(&s->done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const unsigned long long b = __hip_atomic_load(&s->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long best_total = b ? (long long)(b >> 32) - 1 : 0;
+  const long long best_node = b ? (long long)(0xFFFFFFFFull - (b & 0xFFFFFFFFull)) : -1;
+  if (lean) {
+    if (tid < 64) topo_commit_one(ca, tid, pi, tr, p, pmask, qreq, best_node, best_total);
+  } else if (tid == 0) {
+    if (a.cand_chunk) {
+      if (b) {
+        a.cand_chunk[0] = (uint32_t)(best_node >> 6);
+        a.cand_t[0] = make_uint2((1u << 6) | (uint32_t)(63 - (best_node & 63)), 0u);  // an untouched node, key as is
+        a.cand_count[0] = 1;
+      } else {
+        a.cand_count[0] = 0;  // no feasible node: the commit reports the pod unschedulable
+      }
+      a.cand_bound[0] = 0;
+      a.cand_top[0] = 0;
+      a.cand_second[0] = 0;
+    }
+    s->best_total = best_total;
+    s->best_node = best_node;
+  }
+  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&s->zsum[0][0])[k] = 0;
+  if (tid < KS_TOPO_TERMS) {
+    s->zpres[tid] = 0;
+    s->hmin[tid] = INT_MAX;
+  }
+  if (tid == 0) {
+    s->any_all = 0;
+    s->hsize = 0;
+    s->zones = 0;
+    s->empty = 0;
+    s->dev_max = s->taint_max = s->aff_max = 0;
+    s->imin = s->imax = 0;
+    s->smin = LLONG_MAX;
+    s->smax = 0;
+    s->rsv_pref = s->rsv_max = 0;
+    s->best = 0;
+    s->done = 0;
+  }
 }
 
 static unsigned topo_blocks(const TopoKArgs& a) { return (unsigned)std::max<int64_t>(1, (a.n + kTopoThreads - 1) / kTopoThreads); }
@@ -326,8 +372,9 @@ hipError_t launch_topo_pts(hipStream_t s, const TopoKArgs& a) {
   return hipGetLastError();
 }
 
-hipError_t launch_topo_norm(hipStream_t s, const TopoKArgs& a) {
-  hipLaunchKernelGGL(topo_norm_kernel, dim3(topo_blocks(a)), dim3(kTopoThreads), 0, s, a);
+hipError_t launch_topo_norm(hipStream_t s, const TopoKArgs& a, const TopoCommitArgs* c) {
+  hipLaunchKernelGGL(topo_norm_kernel, dim3(topo_blocks(a)), dim3(kTopoThreads), 0, s, a, c ? *c : TopoCommitArgs{},
+                     (int32_t)(c != nullptr));
   return hipGetLastError();
 }
 

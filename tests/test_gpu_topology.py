@@ -184,3 +184,4 @@ def test_graph_and_direct_launches_agree(runtime, oracle_lib):
             assert st["passes"] > 0.8 * w.pods.n  # (every topology pod is a one-pod commit)
         finally:
             ev.close()
+
