@@ -281,6 +281,7 @@ __host__ __device__ inline CandSlot cand_slot_layout(int32_t k) {
 // Reserve, and the row of pod j+1's best untouched candidate is put in flight from HBM then.
 
 constexpr int kQuotaLdsRows = 128;  // quota tables up to this size are cached in LDS for the pass
+static_assert(kQuotaLdsRows < 0xFFFF && KS_QUOTA_DIMS <= 8, "commit_kernel's packed per-pod quota words");
 // Threads of a commit workgroup: its waves load the pass into LDS together, then wave 0 alone runs the sequential
 // loop.  The Fit + LoadAware [+ ElasticQuota] kernels fit 2 waves per SIMD (<= 256 VGPRs), so they load with 8 waves;
 // the other variants use every register of a SIMD (1 wave each).
@@ -870,6 +871,9 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   // wave 0, lane j: pod j's small per-pod values (read back with v_readlane in the loop)
   int32_t my_cnt = 0, my_quota = -1, my_cls = -1;
   uint32_t my_flags = 0, my_pmask = 0;
+  // QC: the pod's leaf quota row's static words -- parent (0xFFFF = none) | limit_mask << 16 | min_mask << 24 (the
+  // look-ahead's admission then reads only the per-dimension amounts from LDS, in one batch)
+  uint32_t my_qmeta = 0xFFFFu;
   uint64_t my_bound = 0, my_top = 0, my_second = 0;
   if (tid < 64 && lane < np) {
     my_cnt = a.cand_count[lane];
@@ -879,6 +883,11 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
 
     my_pmask = a.pq.mask[cursor0 + lane];
     my_quota = a.pods[cursor0 + lane].quota;
+    if (QC && my_quota >= 0) {
+      const int32_t pp = a.q.parent[my_quota];
+      my_qmeta = (uint32_t)(pp < 0 ? 0xFFFF : pp) | ((a.q.limit_mask[my_quota] & 0xFFu) << 16) |
+                 ((a.q.min_mask[my_quota] & 0xFFu) << 24);
+    }
     my_flags = a.pods[cursor0 + lane].flags;
     if (RSV) my_cls = a.pods[cursor0 + lane].rsv_class;
   }
@@ -1053,9 +1062,9 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   int32_t nslots = 0;
   int32_t processed = np;
   uint32_t rescans = 0, misses = 0, fast = 0, prehits = 0;
-  // speculative raw row of the next pod's best untouched candidate (lane f = field f)
-  int64_t spec_val = 0;
-  int32_t spec_node = -1;
+  // (no speculative row load of the next pod's best untouched candidate: the rows a new slot needs are nearly always
+  // the pass-start prefetches of its top / second-best node, and the in-flight load's registers, reused under the
+  // kernel's register pressure, put a wait on it into the next look-ahead -- C2 +2.9 % without it, C4 +0.7 %)
 
   auto admit = [&](int32_t j) -> uint32_t {
     const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
@@ -1095,12 +1104,12 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       const int ld = lane & (KS_QUOTA_DIMS - 1);
       const size_t o = (size_t)qr * KS_QUOTA_DIMS + ld;
       const int64_t req = pqreq[j * KS_QUOTA_DIMS + ld];
-      const uint32_t lm = qlds->limit_mask[qr];
       const int64_t u = qlds->used[o], l = qlds->limit[o];
-      // the leaf's min check (non-preemptible pods) and its parent, in the same batch of reads
-      const uint32_t mm = qlds->min_mask[qr];
+      // the leaf's min check (non-preemptible pods), in the same batch of reads; masks and parent from registers
       const int64_t nu = qlds->npused[o], mn = qlds->min[o];
-      const int32_t par = qlds->parent[qr];
+      const uint32_t qm = __builtin_amdgcn_readlane(my_qmeta, j);
+      const uint32_t lm = (qm >> 16) & 0xFFu, mm = qm >> 24;
+      const int32_t par = (qm & 0xFFFFu) == 0xFFFFu ? -1 : (int32_t)(qm & 0xFFFFu);
       const uint64_t tw = touched[tn >> 6];
       st_next = 0;
       par_next = par;
@@ -1141,17 +1150,6 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       cw_node = (int32_t)gkey_node(cn.umax);
       cw_next = gld(a.dn->cpu_cores + cw_node);
     }
-#ifndef KS_NO_SPEC
-    if (cn.umax) {
-      const int32_t node = (int32_t)gkey_node(cn.umax);
-      // (the top's and the second-best node's rows are in LDS already)
-      if (node != spec_node && node != (int32_t)gkey_node(readlane64(my_top, j)) &&
-          node != (int32_t)gkey_node(readlane64(my_second, j))) {
-        spec_node = node;
-        if (lane < RF_N) spec_val = load_field(my_col, my_w, node);
-      }
-    }
-#endif
   };
   lookahead(0);
   KS_STAMP(1);
@@ -1449,12 +1447,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       } else if (node == (int32_t)gkey_node(readlane64(my_second, j))) {
         src = rawrun + j * 32;  // prefetched at pass start
       } else {
-        int64_t v = spec_val;
-        if (node != spec_node) {
-          ++misses;
-          if (lane < RF_N) v = load_field(my_col, my_w, node);
-        }
-        if (lane < RF_N) raw[lane] = v;
+        ++misses;
+        if (lane < RF_N) raw[lane] = load_field(my_col, my_w, node);
       }
       if (HELP && src != raw) {
         // the row comes from a prefetched node row: wave 1 builds it
