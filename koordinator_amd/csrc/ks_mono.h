@@ -339,7 +339,7 @@ __global__ __launch_bounds__(commit_threads(0)) void commit_mono_kernel(CommitAr
   int32_t nslots = 0, ndyn = 0;
   int32_t processed = np;
   uint32_t rescans = 0, misses = 0, fast = 0;
-  int64_t spec_val = 0;  // raw row field `lane` of spec_node, in flight from HBM
+  FieldLd spec_val{0u, 0u, false};  // raw row field `lane` of spec_node, in flight from HBM (combined at its use)
   int32_t spec_node = -1;
 #ifdef KS_COMMIT_CAT
   tcat = __builtin_amdgcn_s_memtime();
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(commit_threads(0)) void commit_mono_kernel(CommitAr
           const int32_t un = (int32_t)gkey_node(cj.umax);
           if (un != spec_node && !__ballot(lane < np && my_tn == un)) {
             spec_node = un;
-            if (lane < RF_N) spec_val = load_field(my_col, my_w, un);
+            if (lane < RF_N) spec_val = field_issue(my_col, my_w, un);
           }
         }
         PodRec pod = spods[j];
@@ -483,10 +483,12 @@ __global__ __launch_bounds__(commit_threads(0)) void commit_mono_kernel(CommitAr
           ri = __ffsll((long long)own) - 1;
         } else {
           ri = kMaxBatch + ndyn++;
-          int64_t v = spec_val;
+          int64_t v = 0;
           if (node != spec_node) {
             ++misses;
             if (lane < RF_N) v = load_field(my_col, my_w, node);
+          } else {
+            v = field_value(spec_val);
           }
           if (lane < RF_N) raw1[lane] = v;
           if (lane < kRoles) mono_build(cfg, rows[ri], raw1, lane, ro);

@@ -562,10 +562,27 @@ __device__ __forceinline__ uint32_t quota_admit(P32 parent, PU32 limit_mask, PU3
   return 0;
 }
 
-// One row field of node `node`, lane f loading field f (4-byte columns zero-extended).
+// One row field of node `node`, lane f loading field f (4-byte columns zero-extended).  Two 32-bit loads and no branch:
+// the high word of a 4-byte column re-reads the low word and is dropped when the value is used.  (A per-lane
+// `w == 8 ? 64-bit load : 32-bit load + zero-extension` is a divergent branch whose extension sits right behind the
+// 32-bit load, so the compiler waits for that load on the spot: every prefetch through it was a synchronous load.)
+struct FieldLd {
+  uint32_t lo, hi;
+  bool wide;
+};
+__device__ __forceinline__ FieldLd field_issue(const void* p, int32_t w, int64_t node) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(static_cast<const char*>(p) + node * (int64_t)w);
+  FieldLd f;
+  f.wide = w == 8;
+  f.lo = gld(q);
+  f.hi = gld(q + (f.wide ? 1 : 0));
+  return f;
+}
+__device__ __forceinline__ int64_t field_value(const FieldLd& f) {
+  return (int64_t)(((uint64_t)(f.wide ? f.hi : 0u) << 32) | f.lo);
+}
 __device__ __forceinline__ int64_t load_field(const void* p, int32_t w, int64_t node) {
-  if (w == 8) return gld((const int64_t*)p + node);
-  return (int64_t)(uint64_t)gld((const uint32_t*)p + node);
+  return field_value(field_issue(p, w, node));
 }
 
 // NodeReg of one slot row (lane-private LDS reads).
@@ -699,22 +716,20 @@ __device__ __forceinline__ void lds_rawtop(int64_t* rawtop, const uint64_t* cand
 #pragma unroll
     for (int u = 0; u < kPro; ++u) {
       const int32_t i = i0 + u * NT;
-      t[u] = 0;
-      if (i < n) {
-        const int32_t p = i / RF_N, f = i - p * RF_N;
-        t[u] = cand_top[p];
-        rc[u] = rowcols[f];
-      }
+      const int32_t ii = i < n ? i : 0;  // (no branch: every load of the batch stays in flight together)
+      const int32_t p = ii / RF_N, f = ii - p * RF_N;
+      t[u] = i < n ? cand_top[p] : 0ull;
+      rc[u] = rowcols[f];
     }
-    int64_t v[kPro];
+    FieldLd v[kPro];
 #pragma unroll
-    for (int u = 0; u < kPro; ++u) v[u] = t[u] ? load_field(rc[u].p, rc[u].width, gkey_node(t[u])) : 0;
+    for (int u = 0; u < kPro; ++u) v[u] = field_issue(rc[u].p, rc[u].width, t[u] ? gkey_node(t[u]) : 0);
 #pragma unroll
     for (int u = 0; u < kPro; ++u) {
       const int32_t i = i0 + u * NT;
       if (i < n && t[u]) {
         const int32_t p = i / RF_N, f = i - p * RF_N;
-        rawtop[p * 32 + f] = v[u];
+        rawtop[p * 32 + f] = field_value(v[u]);
       }
     }
   }
