@@ -1094,6 +1094,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   };
   uint32_t st_next = 0;
   int32_t par_next = -1;  // QC: the quota parent of the pod the look-ahead ran for (read with its admission)
+  int64_t req_next = 0;   // QC: its request in dimension lane & 7 (the admission's read, reused by its usage update)
   // NUMA-policy variants: the node ids of the look-ahead pod's reserve_pre_kernel records (lane < kPreRsvM) and, with
   // Cfg.cores, the core word of its best untouched candidate; both loads in flight across the pod's slot evaluation
   int32_t pre_nodes = -1, cw_node = -1;
@@ -1119,6 +1120,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       const int ld = lane & (KS_QUOTA_DIMS - 1);
       const size_t o = (size_t)qr * KS_QUOTA_DIMS + ld;
       const int64_t req = pqreq[j * KS_QUOTA_DIMS + ld];
+      req_next = req;
       const int64_t u = qlds->used[o], l = qlds->limit[o];
       // the leaf's min check (non-preemptible pods), in the same batch of reads; masks and parent from registers
       const int64_t nu = qlds->npused[o], mn = qlds->min[o];
@@ -1176,6 +1178,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     const uint32_t st = st_next;
     const Cands cj = cn;
     const int32_t qpar = par_next;
+    const int64_t qreq_j = req_next;
     KS_CAT(0);
     if (st) {
       if (lane == 0) sres[j] = ks_result{-1, st, 0, -1, 0, 0, 0};
@@ -1835,7 +1838,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         const uint32_t pmask = __builtin_amdgcn_readlane(my_pmask, j);
         if (lane < KS_QUOTA_DIMS && ((pmask >> lane) & 1u)) {
           // updatePodUsedNoLock -> updateGroupDeltaUsedNoLock (group_quota_manager.go:620-655)
-          const int64_t qreq = pqreq[j * KS_QUOTA_DIMS + lane];
+          // (QC: the look-ahead's read of the pod's request; no LDS round trip in front of the atomics)
+          const int64_t qreq = QC ? qreq_j : pqreq[j * KS_QUOTA_DIMS + lane];
           const bool np_ = (pflags & KS_POD_NONPREEMPTIBLE) != 0;
           if (QC) {
             // LDS atomics: no read-back on the sequential path (the next pod's admission reads after them)
