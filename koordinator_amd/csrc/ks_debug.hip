@@ -22,11 +22,17 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   TopoRec tr;
   NodeReg<NSC> r;
   load_node<NSC>(c, d, i, valid ? 1 : 0, r);  // (issued with the step's pod record)
+  const int64_t i0 = valid ? i : 0;
+  const uint64_t th = c.stat ? d.taints_hard[i0] : 0ull, ts = c.stat ? d.taints_soft[i0] : 0ull,
+                 lb = c.stat ? d.labels[i0] : 0ull, hp = c.stat ? d.host_ports[i0] : 0ull;
+  TopoPre pre{};
   if (topo) {
     pi = topo_cur(tk, tr);
     if (pi < 0) return;
+    pre = topo_pre(tk, tr, i, valid);  // (in flight with the stage's loads)
     if (tr.flags & KS_TOPO_DYN) topo_stage(tk, tr, tl);
   }
+  TopoNodeIn tin{1u, 0, 0, 0, 0};
   if (valid) {
     const PodRec p = pod[pi];
     const PodStat* ps = pstat ? pstat + pi : nullptr;
@@ -34,7 +40,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     EvalOut o = eval_full<NSC, true, false, FEAT>(
         c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
         [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
-    if (c.stat) stat_eval(c, *ps, d.taints_hard[i], d.taints_soft[i], d.labels[i], d.host_ports[i], o);
+    if (c.stat) stat_eval(c, *ps, th, ts, lb, hp, o);
     reasons[i] = o.reasons;
     scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
     scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
@@ -55,9 +61,10 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = 0;
     scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TOPOLOGY_SPREAD] = 0;
     scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_POD_AFFINITY] = 0;
+    tin = TopoNodeIn{o.reasons, o.dev_raw, o.traw, o.araw, ro.hiord};
   }
   // PodTopologySpread / InterPodAffinity Filters and the normalizations' reductions (every lane, converged)
-  if (topo) topo_eval_node(tk, tr, (int32_t)pi, i, valid, tl);
+  if (topo) topo_eval_node(tk, tr, (int32_t)pi, i, valid, tl, pre, tin);
 }
 
 

@@ -216,11 +216,37 @@ __device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr
   __syncthreads();
 }
 
+// topo_eval_node's node inputs, loaded as soon as the step's pod record is known (with the stage's loads, ahead of
+// the plugin evaluation): the zone, the labels, the hostname-keyed terms' counts
+struct TopoPre {
+  int32_t z;
+  uint64_t lab;
+  int32_t cnt[KS_TOPO_TERMS];
+};
+__device__ __forceinline__ TopoPre topo_pre(const TopoKArgs& a, const TopoRec& tr, int64_t i, bool valid) {
+  TopoPre p;
+  const int64_t n = valid ? i : 0;
+  p.z = valid ? a.t.zone[n] : -1;
+  p.lab = a.labels ? a.labels[n] : 0ull;
+  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    const uint64_t w = tr.term[t];
+    p.cnt[t] = (dyn && w && tp_key(w) == 0) ? a.t.count[(int64_t)tp_prop(w) * a.t.npad + n] : 0;
+  }
+  return p;
+}
+// ... and the evaluation's results for the node (registers, not re-read from the buffers just written)
+struct TopoNodeIn {
+  uint32_t base;  // every other plugin's reasons
+  int32_t dr, trw, arw, rhi;
+};
+
 // eval_debug_kernel's topology part for node i (every lane of the wave calls it, converged; valid = a node of the
 // cluster): both plugins' Filters OR-ed into the node's reasons (total -1 and the score row zeroed when they fail),
 // InterPodAffinity's raw score, and the node's part of the normalizations' reductions (one global atomic per wave)
 __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec& tr, int32_t pi, int64_t i, bool valid,
-                                               const TopoLds& l) {
+                                               const TopoLds& l, const TopoPre& pre, const TopoNodeIn& in) {
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
   bool soft_zone = false, need_aff = false;
 #pragma unroll
@@ -236,16 +262,16 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
   int32_t dr = 0, trw = 0, arw = 0;
   uint64_t pref = 0;
   if (valid) {
-    const uint32_t base = a.reasons[i];
-    z = a.t.zone[i];
+    const uint32_t base = in.base;
+    z = pre.z;
     const bool has_zone = z >= 0;
     uint32_t r = 0;
     if (dyn) {
       auto domain = [&](int t) -> long long {
         const uint64_t w = tr.term[t];
-        return tp_key(w) == 1 ? l.zsum[t][z] : (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i];
+        return tp_key(w) == 1 ? l.zsum[t][z] : (long long)pre.cnt[t];
       };
-      const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, a.labels ? a.labels[i] : 0ull) : true;
+      const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, pre.lab) : true;
       // PodTopologySpread Filter: the first hard constraint that fails
     #pragma unroll
   for (int t = 0; t < KS_TOPO_TERMS; ++t) {
@@ -257,7 +283,7 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
         }
         long long match;
         if (tp_key(w) == 1) match = ((l.zpres[t] >> z) & 1ull) ? l.zsum[t][z] : 0;
-        else match = tp_eligible(w, tr.flags, aff, has_zone) ? (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i] : 0;
+        else match = tp_eligible(w, tr.flags, aff, has_zone) ? (long long)pre.cnt[t] : 0;
         const long long self = (tp_flags(w) & KS_TOPO_T_SELF) ? 1 : 0;
         if (match + self - l.mins[t] > (long long)tp_param(w)) {  // ErrReasonConstraintsNotMatch
           r = KS_R_TOPOLOGY_SPREAD;
@@ -308,10 +334,10 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
     counted = feas && !(soft_all && soft_zone && !has_zone);  // initPreScoreState: not an ignored node
     if (feas) {
       a.iraw[i] = ir;
-      dr = a.draw[i];
-      trw = a.traw[i];
-      arw = a.araw[i];
-      if (a.rsv_on && a.rhi[i] > 0) pref = ((uint64_t)a.rhi[i] << 32) | (0xFFFFFFFFull - (uint64_t)i);
+      dr = in.dr;
+      trw = in.trw;
+      arw = in.arw;
+      if (a.rsv_on && in.rhi > 0) pref = ((uint64_t)in.rhi << 32) | (0xFFFFFFFFull - (uint64_t)i);
     }
   }
   // the wave's part of every reduction, then one atomic per quantity

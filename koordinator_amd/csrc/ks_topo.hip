@@ -45,9 +45,13 @@ __global__ __launch_bounds__(kTopoThreads) void topo_sums_kernel(TopoKArgs a) {
   __shared__ unsigned long long zp[KS_TOPO_TERMS];
   __shared__ int hm[KS_TOPO_TERMS];
   __shared__ int aa;
+  const int tid = threadIdx.x;
+  const int64_t n = (int64_t)blockIdx.x * kTopoThreads + tid;
+  const int64_t n0 = n < a.n ? n : 0;
+  const int32_t z = a.t.zone[n0];  // (the node's loads issued with the cursor -> record chain)
+  const uint64_t lab = a.labels ? a.labels[n0] : 0ull;
   TopoRec tr;
   const int32_t pi = topo_pod(a, tr);
-  const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) {
     a.scr->cur_pi = pi;
     a.scr->cur_rec = tr;
@@ -61,29 +65,36 @@ __global__ __launch_bounds__(kTopoThreads) void topo_sums_kernel(TopoKArgs a) {
   if (tid == 0) aa = 0;
   __syncthreads();
   bool aff_host = false, need_aff = false;
+#pragma unroll
   for (int t = 0; t < KS_TOPO_TERMS; ++t) {
     aff_host |= tp_kind(tr.term[t]) == KS_TOPO_K_AFFINITY && tp_key(tr.term[t]) == 0;
     need_aff |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_HARD || tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT;
   }
-  const int64_t n = (int64_t)blockIdx.x * kTopoThreads + tid;
-  if (n < a.n) {
-    const int32_t z = a.t.zone[n];
-    const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, a.labels ? a.labels[n] : 0ull) : true;
-    for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-      const uint64_t w = tr.term[t];
-      if (!w || !tp_eligible(w, tr.flags, aff, z >= 0)) continue;
-      const int32_t cnt = a.t.count[(int64_t)tp_prop(w) * a.t.npad + n];
-      if (tp_key(w) == 1) {
-        if (z >= 0) {
-          if (cnt) atomicAdd((unsigned long long*)&zs[t][z], (unsigned long long)(long long)cnt);
-          atomicOr(&zp[t], 1ull << z);
-        }
-      } else if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD) {
-        atomicMin(&hm[t], cnt);
-      }
-      if (tp_kind(w) == KS_TOPO_K_AFFINITY && cnt > 0 && (aff_host || z >= 0)) aa = 1;
+  // every active term's count first (independent loads), then the node's part; the zones present and the hostname
+  // minima are reduced per wave (a same-address LDS atomic from every lane would serialize 64-way)
+  const bool in = n < a.n;
+  int32_t cnt[KS_TOPO_TERMS];
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) cnt[t] = tr.term[t] ? a.t.count[(int64_t)tp_prop(tr.term[t]) * a.t.npad + n0] : 0;
+  const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, lab) : true;
+  bool aav = false;
+#pragma unroll
+  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
+    const uint64_t w = tr.term[t];
+    if (!w) continue;  // (wave-uniform)
+    const bool el = in && tp_eligible(w, tr.flags, aff, z >= 0);
+    if (tp_key(w) == 1) {
+      const bool zd = el && z >= 0;
+      if (zd && cnt[t]) atomicAdd((unsigned long long*)&zs[t][z], (unsigned long long)(long long)cnt[t]);
+      const uint64_t o = wave_or_u64(zd ? (1ull << z) : 0ull);
+      if ((tid & 63) == 0 && o) atomicOr(&zp[t], o);
+    } else if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD) {
+      const uint32_t m = ~wave_max_u32(~(uint32_t)(el ? cnt[t] : INT_MAX));  // (counts are >= 0)
+      if ((tid & 63) == 0 && m != (uint32_t)INT_MAX) atomicMin(&hm[t], (int)m);
     }
+    if (tp_kind(w) == KS_TOPO_K_AFFINITY) aav |= el && cnt[t] > 0 && (aff_host || z >= 0);
   }
+  if (__ballot(aav) && (tid & 63) == 0) aa = 1;
   __syncthreads();
   TopoScratch* s = a.scr;
   for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) {
