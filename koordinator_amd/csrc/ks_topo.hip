@@ -323,13 +323,15 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   }
   const uint64_t km = wave_max_u64(key);
   if ((tid & 63) == 0 && km) atomicMax(&s->best, (unsigned long long)km);
-  // the last workgroup: the commit or the one-candidate set, then the scratch back to its initial image
-  __threadfence();
+  // the last workgroup: the commit or the one-candidate set, then the scratch back to its initial image.  The only
+  // value handed between workgroups is `best`, an agent-scope atomic performed at the memory side: each wave waits
+  // for its own atomic to complete before the workgroup's arrival (no L2 write-back fence: the scores and totals are
+  // read only after the kernel), and the last workgroup reads it with an agent-scope load.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) last = atomicAdd(&s->done, 1u) == gridDim.x - 1;
+  if (tid == 0) last = __hip_atomic_fetch_add(&s->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();
   const unsigned long long b = __hip_atomic_load(&s->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const long long best_total = b ? (long long)(b >> 32) - 1 : 0;
   const long long best_node = b ? (long long)(0xFFFFFFFFull - (b & 0xFFFFFFFFull)) : -1;
