@@ -1077,9 +1077,11 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   int32_t nslots = 0;
   int32_t processed = np;
   uint32_t rescans = 0, misses = 0, fast = 0, prehits = 0;
-  // (no speculative row load of the next pod's best untouched candidate: the rows a new slot needs are nearly always
-  // the pass-start prefetches of its top / second-best node, and the in-flight load's registers, reused under the
-  // kernel's register pressure, put a wait on it into the next look-ahead -- C2 +2.9 % without it, C4 +0.7 %)
+#ifdef KS_SPEC
+  // speculative raw row of the next pod's best untouched candidate (lane f = field f), two 32-bit halves in flight
+  FieldLd spec_val{0u, 0u, false};
+  int32_t spec_node = -1;
+#endif
 
   auto admit = [&](int32_t j) -> uint32_t {
     const int32_t qrow = __builtin_amdgcn_readlane(my_quota, j);
@@ -1167,6 +1169,17 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       cw_node = (int32_t)gkey_node(cn.umax);
       cw_next = gld(a.dn->cpu_cores + cw_node);
     }
+#ifdef KS_SPEC
+    if (cn.umax) {
+      const int32_t node = (int32_t)gkey_node(cn.umax);
+      // (the top's and the second-best node's rows are in LDS already)
+      if (node != spec_node && node != (int32_t)gkey_node(readlane64(my_top, j)) &&
+          node != (int32_t)gkey_node(readlane64(my_second, j))) {
+        spec_node = node;
+        if (lane < RF_N) spec_val = field_issue(my_col, my_w, node);
+      }
+    }
+#endif
   };
   lookahead(0);
   KS_STAMP(1);
@@ -1465,8 +1478,15 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       } else if (node == (int32_t)gkey_node(readlane64(my_second, j))) {
         src = rawrun + j * 32;  // prefetched at pass start
       } else {
-        ++misses;
-        if (lane < RF_N) raw[lane] = load_field(my_col, my_w, node);
+#ifdef KS_SPEC
+        if (node == spec_node) {
+          if (lane < RF_N) raw[lane] = field_value(spec_val);
+        } else
+#endif
+        {
+          ++misses;
+          if (lane < RF_N) raw[lane] = load_field(my_col, my_w, node);
+        }
       }
       if (HELP && src != raw) {
         // the row comes from a prefetched node row: wave 1 builds it
