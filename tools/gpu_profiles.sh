@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile evidence of the bench line's records, all from the library in this tree (each summary is stamped with its
-# sha256, which bench.py checks): per config (c2, c3, c4, c2d, c2s) the rocprofv3 kernel statistics of the bench command and
+# sha256, which bench.py checks): per config (c2, c3, c4, c2d, c2s, c3r) the rocprofv3 kernel statistics of the bench command and
 # the PMC HBM traffic (FETCH_SIZE / WRITE_SIZE passes) and VALU-issue summaries; for c5 the PMC passes on a 200k-pod
 # queue (sweep measured unpipelined, KS_PIPE=0: the same kernel without the list re-evaluation launches) and last the
 # pipelined kernel trace with its overlap summary (tools/trace_overlap.py).
@@ -11,14 +11,14 @@ set -o pipefail
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
 export TMPDIR=/tmp
-for CFG in ${CONFIGS:-c2 c3 c4 c2d c2s}; do
+for CFG in ${CONFIGS:-c2 c3 c4 c2d c2s c3r}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$CFG -o run -- python3 bench.py --config $CFG --no-c5 --no-sub --no-cpu-baseline > $OUT/prof_$CFG.json 2> $OUT/prof_$CFG.err || { echo "rocprof $CFG failed"; tail -30 $OUT/prof_$CFG.err; exit 1; }
   S=$(find $OUT/prof_$CFG -name '*kernel_stats.csv' | head -1)
   [ -n "$S" ] && cp $S $OUT/${CFG}_kernel_stats.csv
   rm -rf $OUT/prof_$CFG
-  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_traffic.sh $CFG $(basename $OUT)/traffic_$CFG > /dev/null || exit 1
+  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_traffic.sh $CFG ${OUT#gpurun_out/}/traffic_$CFG > /dev/null || exit 1
   cp $OUT/traffic_$CFG/traffic.json $OUT/${CFG}_traffic.json
-  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_valu.sh $CFG $(basename $OUT)/valu_$CFG > /dev/null || exit 1
+  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_valu.sh $CFG ${OUT#gpurun_out/}/valu_$CFG > /dev/null || exit 1
   cp $OUT/valu_$CFG/valu.json $OUT/${CFG}_valu.json
   rm -rf $OUT/traffic_$CFG $OUT/valu_$CFG
   echo "profiles $CFG done"
@@ -29,15 +29,15 @@ if [ "${PREEMPT:-1}" = 1 ]; then
   S=$(find $OUT/prof_preempt -name '*kernel_stats.csv' | head -1)
   [ -n "$S" ] && cp $S $OUT/preempt_kernel_stats.csv
   rm -rf $OUT/prof_preempt
-  bash tools/pmc_traffic.sh preempt $(basename $OUT)/traffic_preempt > /dev/null || exit 1
+  bash tools/pmc_traffic.sh preempt ${OUT#gpurun_out/}/traffic_preempt > /dev/null || exit 1
   cp $OUT/traffic_preempt/traffic.json $OUT/preempt_traffic.json
   rm -rf $OUT/traffic_preempt
   echo "profiles preempt done"
 fi
 if [ "${C5:-1}" = 1 ]; then
-  KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_traffic.sh c5 $(basename $OUT)/traffic_c5 > /dev/null || exit 1
+  KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_traffic.sh c5 ${OUT#gpurun_out/}/traffic_c5 > /dev/null || exit 1
   cp $OUT/traffic_c5/traffic.json $OUT/c5_traffic.json
-  KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_valu.sh c5 $(basename $OUT)/valu_c5 > /dev/null || exit 1
+  KS_PIPE=0 BENCH_ARGS="--no-c5 --pods 200000" bash tools/pmc_valu.sh c5 ${OUT#gpurun_out/}/valu_c5 > /dev/null || exit 1
   cp $OUT/valu_c5/valu.json $OUT/c5_valu.json
   rm -rf $OUT/traffic_c5 $OUT/valu_c5
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --no-c5 --no-cpu-baseline --pods 200000 --steps 2 --warmup 1 > $OUT/prof_c5.json 2> $OUT/prof_c5.err
