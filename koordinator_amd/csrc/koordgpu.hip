@@ -3791,10 +3791,11 @@ static int topo_step(ks_ctx* ctx) {
   EvBuf eb;
   if (ev_buffers(ctx, eb) != KS_OK) return KS_ENOMEM;
   const int64_t n = ctx->n;
-  const TopoKArgs ta = topo_args(ctx, ctx->st, ctx->cursor, eb);
+  TopoKArgs ta = topo_args(ctx, ctx->st, ctx->cursor, eb);
+  ta.scores = nullptr;  // (the batch step returns no per-plugin score matrix)
   HIPCHK(ctx, launch_topo_sums(ctx->stream, ta));
   HIPCHK(ctx, launch_eval_debug(ctx->nsc, (int)((n + 255) / 256), ctx->stream, ctx->d, ctx->drv, ctx->ddv, ctx->dnv,
-                                ctx->kc, ctx->st.recs, n, eb.dr, eb.ds, eb.dt, eb.draw, eb.dhi, eb.ddraw, ctx->st.stat,
+                                ctx->kc, ctx->st.recs, n, eb.dr, nullptr, eb.dt, eb.draw, eb.dhi, eb.ddraw, ctx->st.stat,
                                 eb.dtraw, eb.daraw, &ta, kernel_feat(ctx)));
   HIPCHK(ctx, launch_topo_pts(ctx->stream, ta));
   const int feat = kernel_feat(ctx);

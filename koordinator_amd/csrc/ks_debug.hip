@@ -42,11 +42,6 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
         [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
     if (c.stat) stat_eval(c, *ps, th, ts, lb, hp, o);
     reasons[i] = o.reasons;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = 0;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_BALANCED] = o.reasons ? 0 : o.bal;
     // Fit + LoadAware + NUMA + BalancedAllocation part (the normalized plugins are added by the normalize kernels)
     total[i] = o.reasons ? -1
                          : (int64_t)o.fit * c.fit_pw + (int64_t)o.la * c.la_pw + (int64_t)o.numa * c.numa_pw +
@@ -56,11 +51,19 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     draw[i] = o.dev_raw;
     traw[i] = o.traw;
     araw[i] = o.araw;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = 0;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TAINT] = 0;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_NODE_AFFINITY] = 0;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_TOPOLOGY_SPREAD] = 0;
-    scores[i * KS_NUM_SCORE_PLUGINS + KS_SCORE_POD_AFFINITY] = 0;
+    if (scores) {  // (NULL in the batch's topology step: only ks_eval_pod returns the per-plugin matrix)
+      int64_t* sc = scores + i * KS_NUM_SCORE_PLUGINS;
+      sc[KS_SCORE_FIT] = o.reasons ? 0 : o.fit;
+      sc[KS_SCORE_LOADAWARE] = o.reasons ? 0 : o.la;
+      sc[KS_SCORE_RESERVATION] = 0;
+      sc[KS_SCORE_NUMA] = o.reasons ? 0 : o.numa;
+      sc[KS_SCORE_BALANCED] = o.reasons ? 0 : o.bal;
+      sc[KS_SCORE_DEVICESHARE] = 0;
+      sc[KS_SCORE_TAINT] = 0;
+      sc[KS_SCORE_NODE_AFFINITY] = 0;
+      sc[KS_SCORE_TOPOLOGY_SPREAD] = 0;
+      sc[KS_SCORE_POD_AFFINITY] = 0;
+    }
     tin = TopoNodeIn{o.reasons, o.dev_raw, o.traw, o.araw, ro.hiord};
   }
   // PodTopologySpread / InterPodAffinity Filters and the normalizations' reductions (every lane, converged)

@@ -124,7 +124,7 @@ struct TopoKArgs {
   int32_t total_pods;
   int64_t n;
   uint32_t* reasons;       // [n] every plugin's KS_R_* (eval_debug_kernel's), topology bits OR-ed in
-  int64_t* scores;         // [n][KS_NUM_SCORE_PLUGINS]
+  int64_t* scores;         // [n][KS_NUM_SCORE_PLUGINS] (ks_eval_pod; NULL in the batch step: not written)
   int64_t* total;          // [n] weighted total, -1 = infeasible
   const int32_t* rraw;     // Reservation raw score, order rank (eval_debug_kernel's)
   const int32_t* rhi;
@@ -321,7 +321,8 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       if (r) {
         a.reasons[i] = base | r;
         a.total[i] = -1;
-        for (int k = 0; k < KS_NUM_SCORE_PLUGINS; ++k) a.scores[i * KS_NUM_SCORE_PLUGINS + k] = 0;
+        if (a.scores)
+          for (int k = 0; k < KS_NUM_SCORE_PLUGINS; ++k) a.scores[i * KS_NUM_SCORE_PLUGINS + k] = 0;
       }
       // InterPodAffinity Score: weight x matching pods in the node's domain, per score term
     #pragma unroll

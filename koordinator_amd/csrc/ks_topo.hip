@@ -283,28 +283,28 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   const int64_t pref = rp ? (int64_t)(0xFFFFFFFFull - (rp & 0xFFFFFFFFull)) : -1;
   uint64_t key = 0;
   if (in && rs == 0) {
-    int64_t* sc = a.scores + i * KS_NUM_SCORE_PLUGINS;
+    int64_t* sc = a.scores ? a.scores + i * KS_NUM_SCORE_PLUGINS : nullptr;  // (NULL: the batch step)
     int64_t tot = tot0;
     // DefaultNormalizeScore (normalize_score.go:24-52): DeviceShare, TaintToleration (reverse), NodeAffinity
     if (a.dev_on) {
       const int64_t v = dmx == 0 ? dr : 100 * (int64_t)dr / dmx;
-      sc[KS_SCORE_DEVICESHARE] = v;
+      if (sc) sc[KS_SCORE_DEVICESHARE] = v;
       tot += v * a.dev_w;
     }
     if (a.taint_on) {
       const int64_t v = tmx == 0 ? 100 : 100 - 100 * (int64_t)tr_ / tmx;
-      sc[KS_SCORE_TAINT] = v;
+      if (sc) sc[KS_SCORE_TAINT] = v;
       tot += v * a.taint_w;
     }
     if (a.aff_on) {
       const int64_t v = amx == 0 ? ar : 100 * (int64_t)ar / amx;
-      sc[KS_SCORE_NODE_AFFINITY] = v;
+      if (sc) sc[KS_SCORE_NODE_AFFINITY] = v;
       tot += v * a.aff_w;
     }
     // Reservation: the preferred node scores mostPreferredScore (scoring.go:87-122), DefaultNormalizeScore
     if (a.rsv_on) {
       const int64_t r = i == pref ? 1000 : rr, v = rmx == 0 ? r : 100 * r / rmx;
-      sc[KS_SCORE_RESERVATION] = v;
+      if (sc) sc[KS_SCORE_RESERVATION] = v;
       tot += v * a.rsv_w;
     }
     long long pts = 100, ipa = 0;  // no constraint: NormalizeScore's maxScore == 0 gives MaxNodeScore
@@ -315,8 +315,10 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
       const long long diff = imax - imin;
       if (diff > 0) ipa = (long long)__dmul_rn(100.0, __ddiv_rn((double)(iri - imin), (double)diff));
     }
-    sc[KS_SCORE_TOPOLOGY_SPREAD] = pts;
-    sc[KS_SCORE_POD_AFFINITY] = ipa;
+    if (sc) {
+      sc[KS_SCORE_TOPOLOGY_SPREAD] = pts;
+      sc[KS_SCORE_POD_AFFINITY] = ipa;
+    }
     tot += pts * a.spread_w + ipa * a.ipa_w;
     a.total[i] = tot;
     key = ((uint64_t)(tot + 1) << 32) | (0xFFFFFFFFull - (uint64_t)i);  // selectHost: max total, lowest index
