@@ -164,3 +164,19 @@ def test_c5_16k_pods_automatic_mode(runtime, oracle_lib):
     assert_same_results(got, orc.schedule(w.pods), "C5 16k")
     assert_same_state(state, orc.read_nodes(), "C5 16k")
     orc.close()
+
+
+def test_c5_64k_pods_automatic_mode(runtime, oracle_lib):
+    """100k nodes, 65,536 pods (1,024 pipelined passes, patched lists): bit-exact placements and node state against
+    the 16-thread oracle (~40 s of oracle time) -- four times the 16k sample, 6.6 % of the bench's 1M-pod queue."""
+    w = synth.c5(n_pods=65_536, seed=78)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy())
+    got = ev.schedule(w.pods)
+    st = ev.stats()
+    state = ev.read_nodes()
+    ev.close()
+    assert st["pipelined"] == 2 and st["passes"] >= 1024
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), nthreads=16)
+    assert_same_results(got, orc.schedule(w.pods), "C5 64k")
+    assert_same_state(state, orc.read_nodes(), "C5 64k")
+    orc.close()
