@@ -84,6 +84,14 @@ def test_c5_shape_20k_two_virtual_shards_per_rank(runtime, oracle_lib):
     assert st["pipelined"] == 2
 
 
+def test_c5_full_100k_nodes_two_ranks_two_vshards(runtime, oracle_lib):
+    """the bench's C5 node count (100k) over 2 ranks x 2 virtual shards (4 shards, the N = 4 layout of the bench's
+    sharded C5 on one GPU), pipelined with patched lists, 4,096 pods (64 passes)"""
+    w = synth.c5(n_pods=4096, seed=11)
+    st = run_ranks(runtime, oracle_lib, w.cfg, w.nodes, w.pods, "c5-100k-2x2", vshards=2, pipeline=2)
+    assert st["pipelined"] == 2 and st["passes"] >= 64
+
+
 def test_c5_shape_not_pipelined(runtime, oracle_lib):
     w = synth.c5(n_nodes=20_000, n_pods=1500, seed=9)
     st = run_ranks(runtime, oracle_lib, w.cfg, w.nodes, w.pods, "c5-20k-serial", pipeline=0)
