@@ -185,3 +185,21 @@ def test_graph_and_direct_launches_agree(runtime, oracle_lib):
         finally:
             ev.close()
 
+
+
+@pytest.mark.parametrize("label,kw", [
+    ("no zone labels", dict(unzoned_frac=1.0)),
+    ("one zone", dict(n_zones=1, unzoned_frac=0.0)),
+    ("64 zones", dict(n_zones=64, unzoned_frac=0.02)),
+    ("empty cluster", dict(per_node=(0, 0))),
+    ("anti-affinity heavy", dict(anti_frac=0.6, per_node=(0, 1))),
+    ("system defaults only", dict(default_frac=1.0, spread_frac=0.0, anti_frac=0.0, affinity_frac=0.0, pref_frac=0.0)),
+    ("hard spread heavy", dict(spread_frac=0.9, default_frac=0.0)),
+])
+def test_edge_shapes(runtime, oracle_lib, label, kw):
+    """the domain's edge shapes: nodes without the zonal key (every zonal constraint fails / is ignored), a single
+    domain, the 64-zone maximum, no placed pods, saturating anti-affinity, only the system default constraints, mostly
+    DoNotSchedule constraints -- placements, counters and node state equal the oracle's"""
+    w = topo_only(300, 400, 60 + len(label), **kw)
+    got, st = run(runtime, oracle_lib, w, label)
+    assert got["status"].shape[0] == 400

@@ -215,3 +215,21 @@ def test_namespace_selector_cases():
     assert list(r) == [0, abi.KS_R_POD_ANTI_AFFINITY, 0]
     pf, ipf, _, _, _ = ref.evaluate(pending[0], nodes, existing, [True] * 3, ns_labels=nsl)
     assert ipf == [None, "anti", None]
+
+
+EDGE_SHAPES = [
+    ("no zone labels", dict(unzoned_frac=1.0)),
+    ("one zone", dict(n_zones=1, unzoned_frac=0.0)),
+    ("64 zones", dict(n_zones=64, unzoned_frac=0.02)),
+    ("empty cluster", dict(per_node=(0, 0))),
+    ("anti-affinity heavy", dict(anti_frac=0.6, per_node=(0, 1))),
+    ("system defaults only", dict(default_frac=1.0, spread_frac=0.0, anti_frac=0.0, affinity_frac=0.0, pref_frac=0.0)),
+]
+
+
+@pytest.mark.parametrize("label,kw", EDGE_SHAPES)
+def test_oracle_against_restatement_edge_shapes(label, kw):
+    """the C oracle on the compiled form against the object-level restatement on the domain's edge shapes (the same
+    shapes tests/test_gpu_topology.py::test_edge_shapes runs on the device)"""
+    w = _workload(60, 24, 70 + len(label), **kw)
+    _check_eval(w, _profile(), range(w.pods.n))
