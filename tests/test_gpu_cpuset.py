@@ -171,3 +171,19 @@ def test_full_pcpus_split_cores(runtime, oracle_lib, seed):
             assert np.array_equal(a, b), label
         n_checked += int(want["status"][0] == abi.KS_S_SCHEDULED)
     assert n_checked > 10
+
+
+def test_full_pcpus_split_cores_hand_traced(runtime):
+    """the hand-traced split-core cases of tests/test_cpuset_golden.py on the device's accumulator"""
+    from test_cpuset_golden import SPLIT_CORE_CASES
+
+    for name, topo, alloc, needed, strategy, want in SPLIT_CORE_CASES:
+        c = {"topo": list(topo), "allocated": alloc, "allocated_excl": "None", "needed": needed, "bind": "FullPCPUs",
+             "excl": "None", "strategy": strategy}
+        cfg, nodes, st, pod = golden_cluster(c)
+        ev = runtime.Evaluator(cfg, nodes.copy(), cpu_state=st)
+        got = ev.schedule(pod)
+        cs = mask_cpus(ev.fetch_cpusets(1)[0])
+        ev.close()
+        assert got["status"][0] == abi.KS_S_SCHEDULED, name
+        assert cs == want, f"{name}: {cs} vs {want}"
