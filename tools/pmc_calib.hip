@@ -5,6 +5,12 @@
 // (every byte read or written exactly once, 256 MiB per read kernel so that the Infinity Cache holds nothing of it
 // from the previous launch); tools/pmc_calib.py divides the counters by it.
 //
+// The commit and select kernels do not stream: one lane of a wave loads a 4- or 8-byte field of a node row, a quota
+// row or a pod column, and stores a lone word.  The gather / scatter kernels reproduce that pattern on a known set of
+// 128-byte lines: every line of the buffer is touched exactly once, by one word, in a scrambled order (an odd
+// multiplier modulo a power of two is a bijection), by lane 0 of each wave (gather1 / scatter1) or by all 64 lanes at
+// 64 different lines (gather64).  Their factor is reported per touched line, not per algorithmic byte.
+//
 // build: hipcc -O3 --offload-arch=gfx950 -o build/pmc_calib tools/pmc_calib.hip
 // run:   rocprofv3 --pmc FETCH_SIZE -- build/pmc_calib   (and a second run with --pmc WRITE_SIZE)
 #include <hip/hip_runtime.h>
@@ -50,6 +56,33 @@ __global__ void write_kernel(T* __restrict__ dst, size_t n) {
   }
 }
 
+// lane 0 of each wave reads one T from each of nlines 128-byte lines, lines in scrambled order
+template <typename T>
+__global__ void gather1_kernel(const T* __restrict__ src, size_t nlines, unsigned long long* sink) {
+  const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  T acc{};
+  if ((threadIdx.x & 63) == 0)
+    for (size_t j = wave; j < nlines; j += nwaves) acc ^= src[((j * 0x9E3779B1ull) & (nlines - 1)) * (128 / sizeof(T))];
+  if (acc == (T)0x5a5a5a5a) sink[0] = 1;
+}
+
+// every lane reads one T from its own scrambled 128-byte line
+template <typename T>
+__global__ void gather64_kernel(const T* __restrict__ src, size_t nlines, unsigned long long* sink) {
+  T acc{};
+  for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < nlines; j += (size_t)gridDim.x * blockDim.x)
+    acc ^= src[((j * 0x9E3779B1ull) & (nlines - 1)) * (128 / sizeof(T))];
+  if (acc == (T)0x5a5a5a5a) sink[0] = 1;
+}
+
+// lane 0 of each wave stores one T into each of nlines 128-byte lines, lines in scrambled order
+template <typename T>
+__global__ void scatter1_kernel(T* __restrict__ dst, size_t nlines) {
+  const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (size_t j = wave; j < nlines; j += nwaves) dst[((j * 0x9E3779B1ull) & (nlines - 1)) * (128 / sizeof(T))] = T{};
+}
+
 int main() {
   const size_t bytes = (size_t)256 << 20;
   void* buf = nullptr;
@@ -68,9 +101,17 @@ int main() {
   hipLaunchKernelGGL(write_kernel<uint32_t>, grid, block, 0, 0, (uint32_t*)buf, wb / 4);
   hipLaunchKernelGGL(write_kernel<unsigned long long>, grid, block, 0, 0, (unsigned long long*)buf, wb / 8);
   hipLaunchKernelGGL(write_kernel<uint4>, grid, block, 0, 0, (uint4*)buf, wb / 16);
+  // scattered single words: 256 MiB of lines for the reads (2 Mi lines), 32 MiB for the stores (256 Ki lines)
+  const size_t rl = bytes / 128, wl = wb / 128;
+  hipLaunchKernelGGL(gather1_kernel<uint32_t>, grid, block, 0, 0, (const uint32_t*)buf, rl, sink);
+  hipLaunchKernelGGL(gather1_kernel<unsigned long long>, grid, block, 0, 0, (const unsigned long long*)buf, rl, sink);
+  hipLaunchKernelGGL(gather64_kernel<uint32_t>, grid, block, 0, 0, (const uint32_t*)buf, rl, sink);
+  hipLaunchKernelGGL(gather64_kernel<unsigned long long>, grid, block, 0, 0, (const unsigned long long*)buf, rl, sink);
+  hipLaunchKernelGGL(scatter1_kernel<uint32_t>, grid, block, 0, 0, (uint32_t*)buf, wl);
+  hipLaunchKernelGGL(scatter1_kernel<unsigned long long>, grid, block, 0, 0, (unsigned long long*)buf, wl);
   CHK(hipGetLastError());
   CHK(hipDeviceSynchronize());
-  printf("{\"read_bytes\": %zu, \"write_bytes\": %zu}\n", bytes, wb);
+  printf("{\"read_bytes\": %zu, \"write_bytes\": %zu, \"read_lines\": %zu, \"write_lines\": %zu}\n", bytes, wb, rl, wl);
   CHK(hipFree(buf));
   CHK(hipFree(sink));
   return 0;

@@ -36,6 +36,22 @@ def main():
         name = wn[d]
         if name.startswith("void write_kernel") or name.startswith("write_kernel"):
             out["write"][f"{width(name)}B/lane"] = {"write_size_bytes": int(v * 1024), "factor": round(WRITE / (v * 1024), 3)}
+    # scattered single words (the commit / select pattern): one word per 128-B line, READ / 128 lines read, WRITE / 128
+    # lines written; bytes_per_line = counter bytes / lines touched, so HBM bytes = lines x bytes_per_line
+    out["scattered"] = {"method": "one 4- or 8-B word per 128-B line, every line once, scrambled line order; gather1 / "
+                                  "scatter1: lane 0 of each wave, gather64: every lane its own line",
+                        "raw_counter_bytes_per_line": {}}
+    for src, total, lines, pre in ((fetch, READ, READ // 128, ("gather1", "gather64")), (write, WRITE, WRITE // 128, ("scatter1",))):
+        names = fn if src is fetch else wn
+        for d, v in src.items():
+            name = names[d].removeprefix("void ")
+            k = next((p for p in pre if name.startswith(p + "_kernel")), None)
+            if k is None:
+                continue
+            w = width(names[d])
+            out["scattered"]["raw_counter_bytes_per_line"][f"{k}/{w}B"] = {
+                "counter_bytes": int(v * 1024), "lines": lines, "counter_bytes_per_line": round(v * 1024 / lines, 2),
+                "algorithmic_bytes_per_line": w}
     print(json.dumps(out, indent=1))
 
 
