@@ -1385,6 +1385,16 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   ctx->counters = (unsigned long long*)p;
   if (dev_alloc(ctx, &p, kNormRows * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->dev_M = (unsigned long long*)p;
+  // empty candidate lists until a select writes them: a kernel that reads a list the pass did not write sees no node
+  // rather than whatever the allocation held
+  if (hipMemsetAsync(ctx->cand_count, 0, 2 * kMaxBatch * 4, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(ctx->cand_chunk, 0, cand_bytes * 4, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(ctx->cand_t, 0, cand_bytes * 8, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    g_create_error = "ks_create: cannot clear the candidate lists";
+    ks_destroy(ctx);
+    return KS_EHIP;
+  }
   *out = ctx;
   return KS_OK;
 fail:

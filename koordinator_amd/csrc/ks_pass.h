@@ -1980,7 +1980,10 @@ __global__ __launch_bounds__(64) void reserve_pre_kernel(CommitArgs a) {
   const int32_t j = blockIdx.x;
   const int32_t cursor0 = __builtin_amdgcn_readfirstlane(*a.cursor);
   if (cursor0 >= a.total_pods) return;
-  const int32_t np = min(a.batch, a.total_pods - cursor0);
+  // the pods the commit will take: with the topology plugins the pass ends before its first topology pod, and when the
+  // cursor's pod is one the sweep and the select return at once, so no list of this pass exists from that pod on (the
+  // lists there are an earlier pass's, or never written)
+  const int32_t np = topo_pass_pods(a, cursor0, min(a.batch, a.total_pods - cursor0));
   if (j >= np) return;
   const Cfg& cfg = a.c;
   const int32_t K = a.k, cnt = min(a.cand_count[j], K);

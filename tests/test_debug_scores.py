@@ -1,0 +1,55 @@
+"""The --debug-scores table (frameworkext/debug.go:61-108): the renderer against the reference's TestDebugScores golden
+(debug_test.go:91-176, tests/golden/debug_scores.json), and the weighting / feasibility host logic on the oracle's
+ks_eval_pod results.  The device run is tests/test_gpu_debug_scores.py."""
+import json
+import os
+
+import numpy as np
+
+from koordinator_amd import abi, synth
+from koordinator_amd.debug_scores import SCORE_PLUGINS, debug_scores, eval_debug_table, plugin_scores
+
+G = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "debug_scores.json")))
+
+
+def test_golden_table():
+    got = debug_scores(G["top_n"], G["pod"], G["plugin_to_node_scores"], G["nodes"])
+    assert got == "\n".join(G["want_lines"])
+
+
+def test_top_n_cuts_rows():
+    got = debug_scores(2, G["pod"], G["plugin_to_node_scores"], G["nodes"]).split("\n")
+    assert got == G["want_lines"][:4]
+    # more rows asked than nodes: every node once
+    assert debug_scores(9, G["pod"], G["plugin_to_node_scores"], G["nodes"]).split("\n") == G["want_lines"]
+
+
+def test_weights_and_feasibility(oracle_lib):
+    w = synth.with_topology(synth.with_static_plugins(synth.c1(n_nodes=60, n_pods=20), seed=31), seed=32)
+    cfg = w.cfg
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy())
+    try:
+        names = [f"node-{i}" for i in range(w.nodes.n)]
+        for i in range(6):
+            pod = w.pods.rows([i])
+            reasons, scores, total = orc.eval_pod(pod)
+            feas, per = plugin_scores(cfg, reasons, scores)
+            assert list(feas) == list(np.flatnonzero(reasons == 0))
+            assert sorted(per) == sorted(n for n, _, en, _ in SCORE_PLUGINS if en(cfg))
+            # the Score column is ks_eval_pod's weighted total
+            assert [sum(per[p][k] for p in per) for k in range(len(feas))] == [int(total[j]) for j in feas]
+            table = eval_debug_table(orc, cfg, pod, names, 3, f"default/pod-{i}")
+            if len(feas) < 2:
+                assert table is None
+                continue
+            rows = table.split("\n")[2:]
+            assert len(rows) == min(3, len(feas))
+            tot = [int(r.split(" | ")[3]) for r in rows]
+            assert tot == sorted(tot, reverse=True) and tot[0] == int(total[feas].max())
+        assert eval_debug_table(orc, cfg, w.pods.rows([0]), names, 0, "p") is None
+    finally:
+        orc.close()
+
+
+def test_score_columns_cover_the_abi():
+    assert sorted(c for _, c, _, _ in SCORE_PLUGINS) == list(range(abi.KS_NUM_SCORE_PLUGINS))

@@ -106,6 +106,24 @@ def test_c3_with_topology(runtime, oracle_lib):
     run(runtime, oracle_lib, w, "c3+topology")
 
 
+def test_c3_topology_queue_head_on_reused_memory(runtime, oracle_lib):
+    """A new context whose queue starts with more topology pods than one pass's topology steps take (C3: reserve_pre_kernel
+    runs ahead of every regular pass's commit), created on device memory that held other data: the regular pass that
+    meets a topology pod at the cursor has no candidate lists (its sweep and select return at once), and the Reserve
+    pre-pass must not read the lists' memory as nodes.  The released block is filled with large positive words first,
+    so a read of never-written lists would address far outside the cluster."""
+    import torch
+
+    junk = torch.full((96 << 20,), 0x3F3F3F3F, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    del junk
+    torch.cuda.empty_cache()
+    w = synth.with_topology(synth.c3(n_nodes=800, n_pods=1600), seed=46)
+    dyn = (w.pods.topo_flags & abi.KS_TOPO_DYN) != 0
+    assert dyn[:9].all()  # the queue's head: more topology pods in a row than the 8 topology steps of a pass
+    run(runtime, oracle_lib, w, "c3+topology, reused memory")
+
+
 def test_assume_unreserve_counters(runtime, oracle_lib):
     w = topo_only(300, 200, 47)
     ev = runtime.Evaluator(w.cfg, w.nodes.copy())
