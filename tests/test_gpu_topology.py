@@ -112,12 +112,14 @@ def test_c3_topology_queue_head_on_reused_memory(runtime, oracle_lib):
     meets a topology pod at the cursor has no candidate lists (its sweep and select return at once), and the Reserve
     pre-pass must not read the lists' memory as nodes.  The released block is filled with large positive words first,
     so a read of never-written lists would address far outside the cluster."""
-    import torch
+    import ctypes as C
 
-    junk = torch.full((96 << 20,), 0x3F3F3F3F, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()
-    del junk
-    torch.cuda.empty_cache()
+    hip = C.CDLL("libamdhip64.so")  # (the HIP runtime the library runs on)
+    junk = C.c_void_p()
+    size = C.c_size_t(384 << 20)
+    assert hip.hipMalloc(C.byref(junk), size) == 0
+    assert hip.hipMemset(junk, 0x3F, size) == 0 and hip.hipDeviceSynchronize() == 0
+    assert hip.hipFree(junk) == 0
     w = synth.with_topology(synth.c3(n_nodes=800, n_pods=1600), seed=46)
     dyn = (w.pods.topo_flags & abi.KS_TOPO_DYN) != 0
     assert dyn[:9].all()  # the queue's head: more topology pods in a row than the 8 topology steps of a pass
