@@ -53,3 +53,10 @@ def test_weights_and_feasibility(oracle_lib):
 
 def test_score_columns_cover_the_abi():
     assert sorted(c for _, c, _, _ in SCORE_PLUGINS) == list(range(abi.KS_NUM_SCORE_PLUGINS))
+
+
+def test_equal_totals_keep_node_order_and_no_rows():
+    s = {"A": [5, 5, 7], "B": [1, 1, 0]}
+    rows = debug_scores(3, "ns/p", s, ["n0", "n1", "n2"]).split("\n")[2:]
+    assert [r.split(" | ")[2] for r in rows] == ["n2", "n0", "n1"]  # 7, then the 6s in node order
+    assert debug_scores(0, "ns/p", s, ["n0", "n1", "n2"]).count("\n") == 1  # header and alignment row only
