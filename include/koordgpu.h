@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 8
+#define KS_ABI_VERSION 9
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -339,27 +339,30 @@ typedef struct ks_static_plugin_args {
  * spreading constraints and hardPodAffinityWeight 1).  Both count pods per topology domain.  The label selector
  * matching runs on the host once per distinct selector / affinity term (koordinator_amd/topology_plugins.py,
  * INTEGRATION.md "Pod topology spread and inter-pod affinity") and reaches the device as:
- *   properties   <= KS_TOPO_PROPS predicates on pods (matches a spread constraint's selector in a namespace, matches
- *                an affinity term, matches all required affinity terms of a pod, carries an anti-affinity term or a
- *                weighted affinity term); ks_node_cols.topo_count[p] = the node's pods with property p (every Reserve
- *                adds the pod's ks_pod_cols.topo_props, ks_unreserve removes them, ks_read_nodes reads them back);
- *   domains      the hostname (each node its own) and one zonal key: ks_node_cols.topo_zone = the node's value
- *                index 0..KS_TOPO_ZONES-1, -1 = label absent;
- *   query terms  <= KS_TOPO_TERMS per pod (ks_pod_cols.topo_term, packed words, see KS_TOPO_K_*): what the two
+ *   properties   ks_node_cols.topo_nprops (<= KS_TOPO_MAX_PROPS) predicates on pods (matches a spread constraint's
+ *                selector in a namespace, matches an affinity term, matches all required affinity terms of a pod,
+ *                carries an anti-affinity term or weighted affinity terms); ks_node_cols.topo_count[p * n + i] = node
+ *                i's pods with property p (every Reserve adds the pod's property list, ks_pod_cols.topo_props,
+ *                ks_unreserve removes it, ks_read_nodes reads the counters back);
+ *   domains      key 0 is the hostname (every node its own domain); keys 1..topo_nkeys (<= KS_TOPO_MAX_KEYS - 1) are
+ *                any other node labels: ks_node_cols.topo_domain[(k - 1) * n + i] = node i's value index of key k,
+ *                0..topo_ndomains-1, -1 = label absent;
+ *   query terms  <= KS_TOPO_MAX_TERMS per pod (ks_pod_cols.topo_terms, packed words, see KS_TOPO_K_*): what the two
  *                plugins' PreFilter / Filter / PreScore / Score ask of the counters for that pod.
  * A pod without query terms (KS_TOPO_DYN clear) never fails their Filters and scores 100 (PodTopologySpread's
  * NormalizeScore with no constraint) and 0 everywhere; a pod with them is scheduled alone against the counters of
- * every pod placed before it.  Not with ks_shard_init nranks > 1 or ks_preempt. */
-#define KS_TOPO_PROPS 16
-#define KS_TOPO_TERMS 8
-#define KS_TOPO_ZONES 64
+ * every pod placed before it, on every rank over the whole (replicated) node table under
+ * ks_shard_init.  Not with ks_preempt. */
+#define KS_TOPO_MAX_KEYS 256      /* topology keys, the hostname included */
+#define KS_TOPO_MAX_PROPS 65536   /* properties per context */
+#define KS_TOPO_MAX_TERMS 64      /* query terms per pod */
 /* ks_pod_cols.topo_flags */
 #define KS_TOPO_DYN 0x1u           /* the pod has query terms */
 #define KS_TOPO_SELF_AFFINITY 0x2u /* podMatchesAllAffinityTerms(pod's own required affinity terms, pod) */
 #define KS_TOPO_SOFT_ALL_KEYS 0x4u /* PreScore requireAllTopologies: the soft constraints are the pod's own (not the
                                       system defaults), so nodes without every soft key are ignored */
-/* topo_term word: kind (bits 0-7), property (8-15), key (16-23: 0 hostname, 1 zone), flags (24-31), param (32-63,
- * int32: maxSkew, or the score weight with its sign) */
+/* topo_terms word: kind (bits 0-3), flags (4-7), key (8-15: 0 hostname, k >= 1 topo_domain key k), property
+ * (16-31), param (32-63, int32: maxSkew, or the score weight with its sign) */
 #define KS_TOPO_K_SPREAD_HARD 1    /* DoNotSchedule constraint: skew = domain matches + self - min over domains */
 #define KS_TOPO_K_SPREAD_SOFT 2    /* ScheduleAnyway constraint (the pod's own or a system default) */
 #define KS_TOPO_K_AFFINITY 3       /* required affinity term (property: pods matching all of the pod's terms) */
@@ -367,8 +370,6 @@ typedef struct ks_static_plugin_args {
 #define KS_TOPO_K_EXISTING_ANTI 5  /* a placed pod's required anti-affinity term that matches the pod */
 #define KS_TOPO_K_SCORE 6          /* weighted score term: weight x matching pods in the node's domain */
 #define KS_TOPO_T_SELF 0x1u        /* spread: the constraint's selector matches the pod itself */
-#define KS_TOPO_T_ELIG_ZONE 0x2u   /* spread: the constraint set (hard, or soft) has a zonal key (nodes without the
-                                      zone label are not eligible) */
 typedef struct ks_topology_args {
   int32_t enable;
   int32_t _pad0;
@@ -443,9 +444,14 @@ typedef struct ks_node_cols {
   /* NodePorts (ABI 6; NULL = 0): host-port dictionary bits in use on the node (NodeInfo.UsedPorts); every Reserve
    * adds the pod's bits while ks_config.nodeports is on (read back with ks_read_nodes) */
   const uint64_t *host_ports;
-  /* PodTopologySpread / InterPodAffinity (ABI 8; NULL = -1 / 0), see ks_topology_args */
-  const int32_t *topo_zone;                 /* zonal domain index, -1 = no zone label */
-  const int32_t *topo_count[KS_TOPO_PROPS]; /* the node's pods with property p */
+  /* PodTopologySpread / InterPodAffinity (ABI 9; NULL = -1 / 0), see ks_topology_args.  The three sizes are fixed by
+   * ks_load_nodes; ks_update_nodes rows carry the same. */
+  int32_t topo_nkeys;            /* topology keys besides the hostname (keys 1..topo_nkeys) */
+  int32_t topo_ndomains;         /* value indices of every key are below this (>= 1 with keys) */
+  int32_t topo_nprops;           /* properties */
+  int32_t _topo_pad;
+  const int32_t *topo_domain;    /* [topo_nkeys][n]: key k's value index on node i at (k - 1) * n + i, -1 = absent */
+  const int32_t *topo_count;     /* [topo_nprops][n]: the node's pods with property p at p * n + i */
 } ks_node_cols;
 
 /* Pending pods, queue order, structure-of-arrays. */
@@ -501,10 +507,13 @@ typedef struct ks_pod_cols {
    * 0.0.0.0) */
   const uint64_t *host_ports;
   const uint64_t *host_ports_conflict;
-  /* PodTopologySpread / InterPodAffinity (ABI 8; NULL = none), see ks_topology_args */
-  const uint32_t *topo_props;               /* bit p: the pod has property p (counted where it is placed) */
-  const uint32_t *topo_flags;               /* KS_TOPO_DYN | KS_TOPO_SELF_AFFINITY | KS_TOPO_SOFT_ALL_KEYS */
-  const uint64_t *topo_term[KS_TOPO_TERMS]; /* query terms, 0 = none (the used ones first) */
+  /* PodTopologySpread / InterPodAffinity (ABI 9; NULL = none), see ks_topology_args.  Two CSR lists over the pods of
+   * the call: pod i's entries are [beg[i], beg[i + 1]) */
+  const uint32_t *topo_flags;     /* KS_TOPO_DYN | KS_TOPO_SELF_AFFINITY | KS_TOPO_SOFT_ALL_KEYS */
+  const int32_t *topo_prop_beg;   /* [p + 1] */
+  const int32_t *topo_props;      /* the pod's properties (counted where it is placed; each at most once) */
+  const int32_t *topo_term_beg;   /* [p + 1] (at most KS_TOPO_MAX_TERMS per pod) */
+  const uint64_t *topo_terms;     /* the pod's query terms */
 } ks_pod_cols;
 
 #define KS_JOINT_NONE 0u
@@ -640,7 +649,7 @@ typedef struct ks_node_state {
   int64_t *la_prod_term_milli_cpu;
   int64_t *la_prod_term_memory;
   uint64_t *host_ports;  /* ABI 6: NodePorts dictionary bits in use (NULL = skip) */
-  int32_t *topo_count[KS_TOPO_PROPS]; /* ABI 8: the pods with each topology property (NULL = skip) */
+  int32_t *topo_count;  /* ABI 9: [topo_nprops][n] the pods with each topology property (NULL = skip) */
 } ks_node_state;
 
 typedef struct ks_stats {

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 8
+KS_ABI_VERSION = 9
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
@@ -135,9 +135,9 @@ KS_AFFINITY_TERMS = 4
 KS_LABEL_NEVER = 1 << 63
 KS_BAL_CPU = 0x1
 KS_BAL_MEMORY = 0x2
-KS_TOPO_PROPS = 16
-KS_TOPO_TERMS = 8
-KS_TOPO_ZONES = 64
+KS_TOPO_MAX_KEYS = 256
+KS_TOPO_MAX_PROPS = 65536
+KS_TOPO_MAX_TERMS = 64
 KS_TOPO_DYN = 0x1
 KS_TOPO_SELF_AFFINITY = 0x2
 KS_TOPO_SOFT_ALL_KEYS = 0x4
@@ -148,7 +148,6 @@ KS_TOPO_K_ANTI = 4
 KS_TOPO_K_EXISTING_ANTI = 5
 KS_TOPO_K_SCORE = 6
 KS_TOPO_T_SELF = 0x1
-KS_TOPO_T_ELIG_ZONE = 0x2
 
 KS_RSV_UNSCHEDULABLE = 0x1
 KS_RSV_ALLOCATE_ONCE = 0x2
@@ -281,8 +280,12 @@ NODE_COLS = [
     ("taints_soft", C.POINTER(C.c_uint64)),
     ("labels", C.POINTER(C.c_uint64)),
     ("host_ports", C.POINTER(C.c_uint64)),
-    ("topo_zone", P32),
-    ("topo_count", P32 * KS_TOPO_PROPS),
+    ("topo_nkeys", C.c_int32),
+    ("topo_ndomains", C.c_int32),
+    ("topo_nprops", C.c_int32),
+    ("_topo_pad", C.c_int32),
+    ("topo_domain", P32),
+    ("topo_count", P32),
 ]
 
 
@@ -321,9 +324,11 @@ POD_COLS = [
     ("affinity_weight", P32 * KS_AFFINITY_TERMS),
     ("host_ports", C.POINTER(C.c_uint64)),
     ("host_ports_conflict", C.POINTER(C.c_uint64)),
-    ("topo_props", PU32),
     ("topo_flags", PU32),
-    ("topo_term", C.POINTER(C.c_uint64) * KS_TOPO_TERMS),
+    ("topo_prop_beg", P32),
+    ("topo_props", P32),
+    ("topo_term_beg", P32),
+    ("topo_terms", C.POINTER(C.c_uint64)),
 ]
 
 
@@ -434,7 +439,7 @@ NODE_STATE_COLS = [
     ("la_prod_term_milli_cpu", P64),
     ("la_prod_term_memory", P64),
     ("host_ports", C.POINTER(C.c_uint64)),
-    ("topo_count", P32 * KS_TOPO_PROPS),
+    ("topo_count", P32),
 ]
 
 

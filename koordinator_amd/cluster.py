@@ -121,9 +121,11 @@ class NodeTable(_Table):
         self.alloc_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, self.n), np.int64)
         self.numa_cpu_amplification = np.zeros(self.n, np.float64)  # <= 1: not amplified
-        # PodTopologySpread / InterPodAffinity (topology_plugins.compile_topology)
-        self.topo_zone = np.full(self.n, -1, np.int32)
-        self.topo_count = np.zeros((abi.KS_TOPO_PROPS, self.n), np.int32)
+        # PodTopologySpread / InterPodAffinity (topology_plugins.compile_topology): per key (besides the hostname) the
+        # node's value index (-1 = absent), per property the node's pods having it; values of every key < topo_ndomains
+        self.topo_domain = np.full((0, self.n), -1, np.int32)
+        self.topo_count = np.zeros((0, self.n), np.int32)
+        self.topo_ndomains = 1
 
     def copy(self) -> "NodeTable":
         t = NodeTable(self.n)
@@ -132,8 +134,9 @@ class NodeTable(_Table):
         t.alloc_scalar = self.alloc_scalar.copy()
         t.req_scalar = self.req_scalar.copy()
         t.numa_cpu_amplification = self.numa_cpu_amplification.copy()
-        t.topo_zone = self.topo_zone.copy()
+        t.topo_domain = self.topo_domain.copy()
         t.topo_count = self.topo_count.copy()
+        t.topo_ndomains = self.topo_ndomains
         return t
 
     def rows(self, idx) -> "NodeTable":
@@ -144,8 +147,9 @@ class NodeTable(_Table):
         t.alloc_scalar = np.ascontiguousarray(self.alloc_scalar[:, idx])
         t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
         t.numa_cpu_amplification = np.ascontiguousarray(self.numa_cpu_amplification[idx])
-        t.topo_zone = np.ascontiguousarray(self.topo_zone[idx])
+        t.topo_domain = np.ascontiguousarray(self.topo_domain[:, idx])
         t.topo_count = np.ascontiguousarray(self.topo_count[:, idx])
+        t.topo_ndomains = self.topo_ndomains
         return t
 
     def check_range(self) -> None:
@@ -172,13 +176,27 @@ class NodeTable(_Table):
         for k in range(abi.KS_MAX_SCALARS):
             c.alloc_scalar[k] = _p64(self.alloc_scalar[k])
             c.req_scalar[k] = _p64(self.req_scalar[k])
-        self.topo_zone = np.ascontiguousarray(self.topo_zone, np.int32)
-        self.topo_count = np.ascontiguousarray(self.topo_count, np.int32)
-        c.topo_zone = _p32(self.topo_zone)
-        for p in range(abi.KS_TOPO_PROPS):
-            c.topo_count[p] = _p32(self.topo_count[p])
+        self.topo_domain = np.ascontiguousarray(self.topo_domain, np.int32).reshape(-1, self.n)
+        self.topo_count = np.ascontiguousarray(self.topo_count, np.int32).reshape(-1, self.n)
+        c.topo_nkeys = self.topo_domain.shape[0]
+        c.topo_ndomains = int(self.topo_ndomains)
+        c.topo_nprops = self.topo_count.shape[0]
+        c.topo_domain = _p32(self.topo_domain) if self.topo_domain.size else None
+        c.topo_count = _p32(self.topo_count) if self.topo_count.size else None
         c._keep = self  # keep arrays alive with the struct
         return c
+
+
+def _csr_rows(beg: np.ndarray, vals: np.ndarray, idx: np.ndarray):
+    """rows idx of a CSR list: (new beg, new values)"""
+    idx = np.asarray(idx, np.int64)
+    beg = np.asarray(beg, np.int64)
+    cnt = beg[idx + 1] - beg[idx]
+    nb = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    if nb[-1] == 0:
+        return nb.astype(np.int32), vals[:0].copy()
+    pos = np.repeat(beg[idx] - nb[:-1], cnt) + np.arange(nb[-1])
+    return nb.astype(np.int32), np.ascontiguousarray(vals[pos])
 
 
 class PodTable(_Table):
@@ -198,10 +216,26 @@ class PodTable(_Table):
         self.affinity_required = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.uint64)
         self.affinity_preferred = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.uint64)
         self.affinity_weight = np.zeros((abi.KS_AFFINITY_TERMS, self.n), np.int32)
-        # PodTopologySpread / InterPodAffinity (topology_plugins.compile_topology)
-        self.topo_props = np.zeros(self.n, np.uint32)
+        # PodTopologySpread / InterPodAffinity (topology_plugins.compile_topology): flags, and the CSR lists of the
+        # pods' properties and query terms (pod i: [beg[i], beg[i + 1]))
         self.topo_flags = np.zeros(self.n, np.uint32)
-        self.topo_term = np.zeros((abi.KS_TOPO_TERMS, self.n), np.uint64)
+        self.topo_prop_beg = np.zeros(self.n + 1, np.int32)
+        self.topo_props = np.zeros(0, np.int32)
+        self.topo_term_beg = np.zeros(self.n + 1, np.int32)
+        self.topo_terms = np.zeros(0, np.uint64)
+
+    def set_topo(self, props, terms) -> None:
+        """The CSR lists from one list per pod (property indices; packed query terms)."""
+        assert len(props) == self.n and len(terms) == self.n
+        self.topo_prop_beg = np.concatenate([[0], np.cumsum([len(x) for x in props])]).astype(np.int32)
+        self.topo_props = np.array([v for x in props for v in x], np.int32)
+        self.topo_term_beg = np.concatenate([[0], np.cumsum([len(x) for x in terms])]).astype(np.int32)
+        self.topo_terms = np.array([v for x in terms for v in x], np.uint64)
+
+    def topo_lists(self, i: int):
+        """pod i's (properties, query terms)"""
+        return (self.topo_props[self.topo_prop_beg[i]:self.topo_prop_beg[i + 1]].tolist(),
+                self.topo_terms[self.topo_term_beg[i]:self.topo_term_beg[i + 1]].tolist())
 
     def rows(self, idx) -> "PodTable":
         idx = np.asarray(idx)
@@ -210,10 +244,11 @@ class PodTable(_Table):
             setattr(t, k, np.ascontiguousarray(v[idx]))
         t.req_scalar = np.ascontiguousarray(self.req_scalar[:, idx])
         t.quota_req = np.ascontiguousarray(self.quota_req[:, idx])
-        for k in ("affinity_required", "affinity_preferred", "affinity_weight", "topo_term"):
+        for k in ("affinity_required", "affinity_preferred", "affinity_weight"):
             setattr(t, k, np.ascontiguousarray(getattr(self, k)[:, idx]))
-        t.topo_props = np.ascontiguousarray(self.topo_props[idx])
         t.topo_flags = np.ascontiguousarray(self.topo_flags[idx])
+        t.topo_prop_beg, t.topo_props = _csr_rows(self.topo_prop_beg, self.topo_props, idx)
+        t.topo_term_beg, t.topo_terms = _csr_rows(self.topo_term_beg, self.topo_terms, idx)
         return t
 
     def ks(self) -> abi.KsPodCols:  # noqa: C901
@@ -243,13 +278,17 @@ class PodTable(_Table):
             c.affinity_required[t] = self.affinity_required[t].ctypes.data_as(C.POINTER(C.c_uint64))
             c.affinity_preferred[t] = self.affinity_preferred[t].ctypes.data_as(C.POINTER(C.c_uint64))
             c.affinity_weight[t] = _p32(self.affinity_weight[t])
-        self.topo_props = np.ascontiguousarray(self.topo_props, np.uint32)
         self.topo_flags = np.ascontiguousarray(self.topo_flags, np.uint32)
-        self.topo_term = np.ascontiguousarray(self.topo_term, np.uint64)
-        c.topo_props = _pu32(self.topo_props)
+        self.topo_prop_beg = np.ascontiguousarray(self.topo_prop_beg, np.int32)
+        self.topo_term_beg = np.ascontiguousarray(self.topo_term_beg, np.int32)
+        # (never a NULL list pointer: an empty list is one unused word)
+        self._props_buf = np.ascontiguousarray(self.topo_props if len(self.topo_props) else np.zeros(1), np.int32)
+        self._terms_buf = np.ascontiguousarray(self.topo_terms if len(self.topo_terms) else np.zeros(1), np.uint64)
         c.topo_flags = _pu32(self.topo_flags)
-        for t in range(abi.KS_TOPO_TERMS):
-            c.topo_term[t] = self.topo_term[t].ctypes.data_as(C.POINTER(C.c_uint64))
+        c.topo_prop_beg = _p32(self.topo_prop_beg)
+        c.topo_props = _p32(self._props_buf)
+        c.topo_term_beg = _p32(self.topo_term_beg)
+        c.topo_terms = self._terms_buf.ctypes.data_as(C.POINTER(C.c_uint64))
         c._keep = self
         return c
 
@@ -604,14 +643,14 @@ class NodePodTable:
 class NodeState:
     """Host buffers for ks_read_nodes / ko_read_nodes."""
 
-    def __init__(self, n: int):
+    def __init__(self, n: int, nprops: int = 0):
         self.n = n
         for name in STATE_I64:
             setattr(self, name, np.zeros(n, np.int64))
         self.pod_count = np.zeros(n, np.int32)
         self.req_scalar = np.zeros((abi.KS_MAX_SCALARS, n), np.int64)
         self.host_ports = np.zeros(n, np.uint64)
-        self.topo_count = np.zeros((abi.KS_TOPO_PROPS, n), np.int32)
+        self.topo_count = np.zeros((nprops, n), np.int32)
 
     def ks(self) -> abi.KsNodeState:
         s = abi.KsNodeState()
@@ -621,8 +660,7 @@ class NodeState:
         s.host_ports = self.host_ports.ctypes.data_as(C.POINTER(C.c_uint64))
         for k in range(abi.KS_MAX_SCALARS):
             s.req_scalar[k] = _p64(self.req_scalar[k])
-        for p in range(abi.KS_TOPO_PROPS):
-            s.topo_count[p] = _p32(self.topo_count[p])
+        s.topo_count = _p32(self.topo_count) if self.topo_count.size else None
         s._keep = self
         return s
 

@@ -54,6 +54,9 @@ static int64_t env_i64(const char* name, int64_t dflt, int64_t lo, int64_t hi) {
   return (int64_t)x;
 }
 
+// the candidate lists' initial fill byte (KS_TEST_POISON_LISTS=1: large words, for tests; else zeros)
+static int list_fill() { return env_i64("KS_TEST_POISON_LISTS", 0, 0, 1) ? 0x3F : 0; }
+
 // ------------------------------------------------------------------------------------------
 // prep kernels
 // ------------------------------------------------------------------------------------------
@@ -239,6 +242,7 @@ constexpr int kSelHistBins = 1024;
 constexpr int kSelThreads = 256;
 constexpr int kSelUnroll = 8;
 constexpr size_t kSelScratch = 128;  // cross-wave partials after the histogram
+constexpr int kSelBlocks = 2 * kMaxBatch;  // (select_kernel: pods 16x..16x+15 on the blocks of XCD x < 4)
 __host__ __device__ inline size_t select_smem(int64_t nc) { return (size_t)nc * sizeof(uint2) + kSelHistBins * 4 + kSelScratch; }
 
 __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
@@ -254,7 +258,12 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   if (cursor < a.total_pods && (__builtin_amdgcn_readfirstlane(a.pods[cursor].flags) & kPodTopoDyn)) return;
   if (cursor >= a.total_pods) return;
   const int32_t np = min(a.batch, a.total_pods - cursor);
-  const int32_t p = blockIdx.x;
+  // XCD-aware pod placement (blocks are dealt round-robin over the 8 XCDs): the 16 pods whose words share a 128-B line
+  // of a chunk row run on one XCD, so each line is fetched into one L2 once, not by every XCD (kSelBlocks blocks, those
+  // of XCDs 4-7 idle)
+  const int32_t xcd = (int32_t)(blockIdx.x & 7u);
+  if (xcd >= kMaxBatch / 16) return;
+  const int32_t p = xcd * 16 + (int32_t)(blockIdx.x >> 3);
   if (p >= np) return;
   const int32_t K = a.k;
   const int64_t nc = a.c1 - a.c0;  // LDS row index e <-> chunk c0 + e
@@ -940,9 +949,13 @@ struct PodStage {
   void* h_pack = nullptr;       // pinned, kPackPods pods
   size_t pack_bytes = 0;
   size_t col8 = 0, col4 = 0;    // device column strides of this stage
-  // PodTopologySpread / InterPodAffinity (ks_topo.h): the pods' query terms; ndyn = topology pods of the stage
+  // PodTopologySpread / InterPodAffinity (ks_topo.h): per pod its TopoRec, and the stage's query-term and property
+  // lists the records point into; ndyn = topology pods of the stage
   TopoRec* topo = nullptr;
+  uint64_t* topo_terms = nullptr;
+  int32_t* topo_props = nullptr;
   int32_t topo_cap = 0;
+  int64_t topo_tcap = 0, topo_pcap = 0;
   int32_t ndyn = 0;
   std::vector<TopoRec> h_topo;
 };
@@ -1103,8 +1116,13 @@ struct ks_ctx {
   int32_t* pre_victims = nullptr;  // [kPreemptMaxPods]
   // PodTopologySpread / InterPodAffinity (ks_topo.h): node columns in the node blob (counters mutable, zone
   // read-only), the normalizing-weight table, the topology step's scratch and one-candidate set
-  int32_t* topo_zone = nullptr;
-  int32_t* topo_count[KS_TOPO_PROPS] = {};
+  int32_t topo_nkeys = 0, topo_ndom = 1, topo_nprops = 0;
+  std::vector<int32_t*> topo_dom_v;    // [nkeys] column bases (contiguous, stride npad): key k + 1's value index
+  std::vector<int32_t*> topo_count_v;  // [nprops] (contiguous, stride npad, mutable): pods with property p
+  int32_t* topo_dom = nullptr;         // topo_dom_v[0]
+  int32_t* topo_count = nullptr;       // topo_count_v[0]
+  long long* topo_zsum = nullptr;      // the step's per-domain scratch (ks_topo.h DevTopo)
+  uint32_t *topo_zpres = nullptr, *topo_zsize = nullptr;
   void* topo_blob = nullptr;
   double* topo_lw = nullptr;
   int32_t topo_nlw = 0;
@@ -1386,10 +1404,11 @@ int ks_create(const ks_config* cfg, ks_ctx** out) {
   if (dev_alloc(ctx, &p, kNormRows * kMaxBatch * 8) != KS_OK) goto fail;
   ctx->dev_M = (unsigned long long*)p;
   // empty candidate lists until a select writes them: a kernel that reads a list the pass did not write sees no node
-  // rather than whatever the allocation held
-  if (hipMemsetAsync(ctx->cand_count, 0, 2 * kMaxBatch * 4, ctx->stream) != hipSuccess ||
-      hipMemsetAsync(ctx->cand_chunk, 0, cand_bytes * 4, ctx->stream) != hipSuccess ||
-      hipMemsetAsync(ctx->cand_t, 0, cand_bytes * 8, ctx->stream) != hipSuccess ||
+  // rather than whatever the allocation held.  KS_TEST_POISON_LISTS=1 (tests only) fills them with large words
+  // instead, so a test can check that no kernel reads a list its pass did not write as nodes
+  if (hipMemsetAsync(ctx->cand_count, list_fill(), 2 * kMaxBatch * 4, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(ctx->cand_chunk, list_fill(), cand_bytes * 4, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(ctx->cand_t, list_fill(), cand_bytes * 8, ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
     g_create_error = "ks_create: cannot clear the candidate lists";
     ks_destroy(ctx);
@@ -1462,6 +1481,10 @@ void ks_destroy(ks_ctx* ctx) {
   for (PodStage* ps : {&ctx->st, &ctx->est, &ctx->ast}) {
     void* t = ps->topo;
     dev_free(t);
+    t = ps->topo_terms;
+    dev_free(t);
+    t = ps->topo_props;
+    dev_free(t);
   }
   for (int i = 0; i < kPipeEvents; ++i) {
     if (ctx->pev_sel[i]) (void)hipEventDestroy(ctx->pev_sel[i]);
@@ -1495,8 +1518,9 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.cpu_free, 4, true);
   add(&d.cpu_cores, 4, true);
   add(&d.host_ports, 8, true);
-  if (ctx->cfg.topology.enable)
-    for (int q = 0; q < KS_TOPO_PROPS; ++q) add(&ctx->topo_count[q], 4, true);
+  ctx->topo_count_v.assign((size_t)(ctx->cfg.topology.enable ? ctx->topo_nprops : 0), nullptr);
+  ctx->topo_dom_v.assign((size_t)(ctx->cfg.topology.enable ? ctx->topo_nkeys : 0), nullptr);
+  for (int32_t*& c : ctx->topo_count_v) add(&c, 4, true);
   // read-only columns
   add(&d.alloc_cpu, 8, false);
   add(&d.alloc_mem, 8, false);
@@ -1522,11 +1546,11 @@ static void build_col_table(ks_ctx* ctx) {
   add(&d.taints_hard, 8, false);
   add(&d.taints_soft, 8, false);
   add(&d.labels, 8, false);
-  if (ctx->cfg.topology.enable) add(&ctx->topo_zone, 4, false);
+  for (int32_t*& c : ctx->topo_dom_v) add(&c, 4, false);
 }
 
-// host source pointers in the same order as build_col_table (NULL = zeros)
-static std::vector<const void*> host_cols(const ks_node_cols* c, bool topo) {
+// host source pointers in the same order as build_col_table (NULL = zeros); n = the rows of c
+static std::vector<const void*> host_cols(const ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
   std::vector<const void*> v;
   v.push_back(c->req_milli_cpu);
   v.push_back(c->req_memory);
@@ -1546,8 +1570,7 @@ static std::vector<const void*> host_cols(const ks_node_cols* c, bool topo) {
   v.push_back(nullptr);  // cpu_free: ks_load_cpu_state (-1 = no CPU topology)
   v.push_back(nullptr);  // cpu_cores: cores_refresh
   v.push_back(c->host_ports);
-  if (topo)
-    for (int q = 0; q < KS_TOPO_PROPS; ++q) v.push_back(c->topo_count[q]);
+  for (size_t q = 0; q < ctx->topo_count_v.size(); ++q) v.push_back(c->topo_count ? c->topo_count + (int64_t)q * n : nullptr);
   v.push_back(c->alloc_milli_cpu);
   v.push_back(c->alloc_memory);
   v.push_back(c->alloc_ephemeral);
@@ -1572,7 +1595,8 @@ static std::vector<const void*> host_cols(const ks_node_cols* c, bool topo) {
   v.push_back(c->taints_hard);
   v.push_back(c->taints_soft);
   v.push_back(c->labels);
-  if (topo) v.push_back(c->topo_zone);  // NULL: -1 (set after the copy)
+  // (NULL: -1, set after the copy)
+  for (size_t k = 0; k < ctx->topo_dom_v.size(); ++k) v.push_back(c->topo_domain ? c->topo_domain + (int64_t)k * n : nullptr);
   return v;
 }
 
@@ -1586,12 +1610,16 @@ static int check_range64(ks_ctx* ctx, const int64_t* p, int64_t n, const char* w
 
 static int validate_nodes(ks_ctx* ctx, const ks_node_cols* c, int64_t n) {
   if (ctx->cfg.topology.enable) {
-    for (int64_t i = 0; c->topo_zone && i < n; ++i)
-      if (c->topo_zone[i] < -1 || c->topo_zone[i] >= KS_TOPO_ZONES)
-        KS_FAIL(ctx, KS_EINVAL, "topo_zone[%lld]=%d outside [-1, %d)", (long long)i, c->topo_zone[i], KS_TOPO_ZONES);
-    for (int q = 0; q < KS_TOPO_PROPS; ++q)
-      for (int64_t i = 0; c->topo_count[q] && i < n; ++i)
-        if (c->topo_count[q][i] < 0) KS_FAIL(ctx, KS_EINVAL, "topo_count[%d][%lld] < 0", q, (long long)i);
+    if (c->topo_nkeys < 0 || c->topo_nkeys > KS_TOPO_MAX_KEYS - 1 || c->topo_nprops < 0 ||
+        c->topo_nprops > KS_TOPO_MAX_PROPS || c->topo_ndomains < 1 || c->topo_ndomains > (1 << 30))
+      KS_FAIL(ctx, KS_EINVAL, "topology sizes: %d keys (max %d), %d domains, %d properties (max %d)", c->topo_nkeys,
+              KS_TOPO_MAX_KEYS - 1, c->topo_ndomains, c->topo_nprops, KS_TOPO_MAX_PROPS);
+    const int64_t nk = c->topo_nkeys, np = c->topo_nprops;
+    for (int64_t i = 0; c->topo_domain && i < nk * n; ++i)
+      if (c->topo_domain[i] < -1 || c->topo_domain[i] >= c->topo_ndomains)
+        KS_FAIL(ctx, KS_EINVAL, "topo_domain[%lld]=%d outside [-1, %d)", (long long)i, c->topo_domain[i], c->topo_ndomains);
+    for (int64_t i = 0; c->topo_count && i < np * n; ++i)
+      if (c->topo_count[i] < 0) KS_FAIL(ctx, KS_EINVAL, "topo_count[%lld] < 0", (long long)i);
   }
   if (!c->alloc_milli_cpu || !c->alloc_memory || !c->allowed_pods || !c->req_milli_cpu || !c->req_memory ||
       !c->pod_count || !c->nonzero_milli_cpu || !c->nonzero_memory || !c->la_flags)
@@ -1723,16 +1751,23 @@ static int numa_refresh_free(ks_ctx* ctx);
 // pod can see (s <= nodes; the host's libm, as the oracle), the topology step's scratch and one-candidate set
 static int topo_install(ks_ctx* ctx) {
   dev_free(ctx->topo_blob);
-  const int32_t nlw = (int32_t)ctx->n + KS_TOPO_ZONES + 2;
+  // sizes a pod can see: the hostname's up to n nodes, another key's up to ndom values + ""
+  const int32_t nlw = (int32_t)std::max<int64_t>(ctx->n, ctx->topo_ndom + 1) + 2;
   const size_t b_lw = ((size_t)nlw * 8 + 255) / 256 * 256;
   const size_t b_scr = (sizeof(TopoScratch) + 255) / 256 * 256;
   const size_t b_cand = (size_t)kMaxBatch * kMaxCand * (4 + 8) + (size_t)kMaxBatch * (4 + 8 * 3);
   const size_t b_raw = (size_t)ctx->npad * 8 * 2;
-  if (dev_alloc(ctx, &ctx->topo_blob, b_lw + b_scr + b_cand + b_raw) != KS_OK) return KS_ENOMEM;
+  const size_t nw = ((size_t)ctx->topo_ndom + 31) / 32;
+  const size_t b_zsum = (size_t)kTopoTerms * (size_t)ctx->topo_ndom * 8, b_bits = (size_t)kTopoTerms * nw * 4;
+  const size_t tot = b_lw + b_scr + b_cand + b_raw + b_zsum + 2 * b_bits;
+  if (dev_alloc(ctx, &ctx->topo_blob, tot) != KS_OK) return KS_ENOMEM;
   char* b = (char*)ctx->topo_blob;
-  HIPCHK(ctx, hipMemsetAsync(b, 0, b_lw + b_scr + b_cand + b_raw, ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(b, 0, tot, ctx->stream));
   ctx->topo_sraw = (long long*)(b + b_lw + b_scr + b_cand);
   ctx->topo_iraw = ctx->topo_sraw + ctx->npad;
+  ctx->topo_zsum = (long long*)(b + b_lw + b_scr + b_cand + b_raw);
+  ctx->topo_zpres = (uint32_t*)(b + b_lw + b_scr + b_cand + b_raw + b_zsum);
+  ctx->topo_zsize = (uint32_t*)(b + b_lw + b_scr + b_cand + b_raw + b_zsum + b_bits);
   ctx->topo_lw = (double*)b;
   ctx->topo_nlw = nlw;
   ctx->topo_scr = (TopoScratch*)(b + b_lw);
@@ -1758,7 +1793,19 @@ static int topo_install(ks_ctx* ctx) {
 }
 
 static DevTopo dev_topo(const ks_ctx* ctx) {
-  return DevTopo{ctx->topo_zone, ctx->topo_count[0], ctx->npad, ctx->topo_lw, ctx->topo_nlw};
+  DevTopo t;
+  t.dom = ctx->topo_dom;
+  t.count = ctx->topo_count;
+  t.npad = ctx->npad;
+  t.nkeys = ctx->topo_nkeys;
+  t.ndom = ctx->topo_ndom;
+  t.lw = ctx->topo_lw;
+  t.nlw = ctx->topo_nlw;
+  t.nw = (ctx->topo_ndom + 31) / 32;
+  t.zsum = ctx->topo_zsum;
+  t.zpres = ctx->topo_zpres;
+  t.zsize = ctx->topo_zsize;
+  return t;
 }
 
 int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
@@ -1800,6 +1847,9 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   ctx->kc = make_cfg(ctx->cfg, ctx->nsc);
   ctx->soft_union = 0;
   for (int64_t i = 0; nodes->taints_soft && i < n; ++i) ctx->soft_union |= nodes->taints_soft[i];
+  ctx->topo_nkeys = ctx->cfg.topology.enable ? nodes->topo_nkeys : 0;
+  ctx->topo_ndom = ctx->cfg.topology.enable ? nodes->topo_ndomains : 1;
+  ctx->topo_nprops = ctx->cfg.topology.enable ? nodes->topo_nprops : 0;
   build_col_table(ctx);
   size_t total = 0, mut = 0;
   for (const Col& c : ctx->cols) {
@@ -1810,7 +1860,7 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   if (dev_alloc(ctx, &ctx->node_blob, total) != KS_OK) return KS_ENOMEM;
   HIPCHK(ctx, hipMemsetAsync(ctx->node_blob, 0, total, ctx->stream));
   char* base = (char*)ctx->node_blob;
-  std::vector<const void*> src = host_cols(nodes, ctx->cfg.topology.enable != 0);
+  std::vector<const void*> src = host_cols(ctx, nodes, n);
   for (size_t i = 0; i < ctx->cols.size(); ++i) {
     *ctx->cols[i].dev = base;
     if (src[i] && n > 0)
@@ -1819,7 +1869,10 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   }
   HIPCHK(ctx, hipMemsetAsync(ctx->d.cpu_free, 0xFF, (size_t)ctx->npad * 4, ctx->stream));  // no CPU topology yet
   if (ctx->cfg.topology.enable) {
-    if (!nodes->topo_zone) HIPCHK(ctx, hipMemsetAsync(ctx->topo_zone, 0xFF, (size_t)ctx->npad * 4, ctx->stream));
+    ctx->topo_dom = ctx->topo_dom_v.empty() ? nullptr : ctx->topo_dom_v[0];
+    ctx->topo_count = ctx->topo_count_v.empty() ? nullptr : ctx->topo_count_v[0];
+    if (!nodes->topo_domain && ctx->topo_dom)
+      HIPCHK(ctx, hipMemsetAsync(ctx->topo_dom, 0xFF, (size_t)ctx->npad * 4 * ctx->topo_nkeys, ctx->stream));
     if (topo_install(ctx) != KS_OK) return KS_ENOMEM;
   }
   ctx->cpu_loaded = false;
@@ -2719,7 +2772,11 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
       KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: duplicate node index with reservations loaded");
   }
   if (int rc = validate_nodes(ctx, rows, m); rc != KS_OK) return rc;
-  std::vector<const void*> src = host_cols(rows, ctx->cfg.topology.enable != 0);
+  if (ctx->cfg.topology.enable && (rows->topo_nkeys != ctx->topo_nkeys || rows->topo_nprops != ctx->topo_nprops ||
+                                   rows->topo_ndomains > ctx->topo_ndom))
+    KS_FAIL(ctx, KS_EINVAL, "ks_update_nodes: topology sizes differ from the loaded table's (%d keys, %d properties, "
+            "%d domains)", ctx->topo_nkeys, ctx->topo_nprops, ctx->topo_ndom);
+  std::vector<const void*> src = host_cols(ctx, rows, m);
   std::vector<void*> dst;
   std::vector<int32_t> widths;
   std::vector<size_t> offs;
@@ -3100,29 +3157,42 @@ static int stage_cols(ks_ctx* ctx, PodStage& st, const ks_pod_cols* pc, int32_t 
   st.cols.topo = nullptr;
   st.ndyn = 0;
   if (ctx->cfg.topology.enable) {
-    if (p > st.topo_cap || !st.topo) {
-      void* t = st.topo;
-      dev_free(t);
-      st.topo = nullptr;
-      st.topo_cap = 0;
-      const int32_t cap = std::max<int32_t>(p, 64);
-      if (dev_alloc(ctx, &t, (size_t)cap * sizeof(TopoRec)) != KS_OK) return KS_ENOMEM;
-      st.topo = (TopoRec*)t;
-      st.topo_cap = cap;
-    }
+    const int64_t nt = (pc->topo_term_beg && pc->topo_terms) ? pc->topo_term_beg[p] : 0;
+    const int64_t npr = (pc->topo_prop_beg && pc->topo_props) ? pc->topo_prop_beg[p] : 0;
+    auto grow = [&](void** buf, int64_t& cap, int64_t want, size_t elem) -> int {
+      if (want <= cap && *buf) return KS_OK;
+      dev_free(*buf);
+      *buf = nullptr;
+      cap = 0;
+      const int64_t c = std::max<int64_t>(want, 64);
+      if (dev_alloc(ctx, buf, (size_t)c * elem) != KS_OK) return KS_ENOMEM;
+      cap = c;
+      return KS_OK;
+    };
+    int64_t rcap = st.topo_cap;
+    if (grow((void**)&st.topo, rcap, p, sizeof(TopoRec)) != KS_OK || grow((void**)&st.topo_terms, st.topo_tcap, nt, 8) != KS_OK ||
+        grow((void**)&st.topo_props, st.topo_pcap, npr, 4) != KS_OK)
+      return KS_ENOMEM;
+    st.topo_cap = (int32_t)rcap;
     std::vector<TopoRec>& ht = st.h_topo;
     ht.assign((size_t)p, TopoRec{});
     for (int32_t i = 0; i < p; ++i) {
       TopoRec& r = ht[(size_t)i];
-      r.props = pc->topo_props ? pc->topo_props[i] : 0;
       r.flags = pc->topo_flags ? pc->topo_flags[i] : 0;
-      for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-        r.term[t] = pc->topo_term[t] ? pc->topo_term[t][i] : 0;
-        r.nterms += r.term[t] != 0;
+      if (nt) {
+        r.tbeg = pc->topo_term_beg[i];
+        r.nterms = pc->topo_term_beg[i + 1] - pc->topo_term_beg[i];
       }
+      if (npr) {
+        r.pbeg = pc->topo_prop_beg[i];
+        r.nprops = pc->topo_prop_beg[i + 1] - pc->topo_prop_beg[i];
+      }
+      if (r.nterms == 0) r.flags &= ~KS_TOPO_DYN;  // (no query term: nothing the step would ask)
       st.ndyn += (r.flags & KS_TOPO_DYN) ? 1 : 0;
     }
     if (p > 0) HIPCHK(ctx, hipMemcpyAsync(st.topo, ht.data(), (size_t)p * sizeof(TopoRec), hipMemcpyHostToDevice, ctx->stream));
+    if (nt) HIPCHK(ctx, hipMemcpyAsync(st.topo_terms, pc->topo_terms, (size_t)nt * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (npr) HIPCHK(ctx, hipMemcpyAsync(st.topo_props, pc->topo_props, (size_t)npr * 4, hipMemcpyHostToDevice, ctx->stream));
     st.cols.topo = st.topo;
   }
   if (ctx->kc.stat || ctx->cfg.topology.enable) {
@@ -3169,17 +3239,33 @@ static int prep_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
 }
 
 static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
-  for (int t = 0; ctx->cfg.topology.enable && t < KS_TOPO_TERMS; ++t)
-    for (int32_t i = 0; pc->topo_term[t] && i < p; ++i) {
-      const uint64_t w = pc->topo_term[t][i];
-      if (!w) continue;
-      const int kind = (int)(w & 0xFF), prop = (int)((w >> 8) & 0xFF), key = (int)((w >> 16) & 0xFF);
-      const int32_t param = (int32_t)(uint32_t)(w >> 32);
-      if (kind < KS_TOPO_K_SPREAD_HARD || kind > KS_TOPO_K_SCORE || prop >= KS_TOPO_PROPS || key > 1 ||
-          ((kind == KS_TOPO_K_SPREAD_HARD || kind == KS_TOPO_K_SPREAD_SOFT) && param < 1) ||
-          (kind == KS_TOPO_K_SCORE && (param < -1000000 || param > 1000000)))
-        KS_FAIL(ctx, KS_EINVAL, "pod %d: topology term %d (%#llx) malformed", i, t, (unsigned long long)w);
+  if (ctx->cfg.topology.enable) {
+    // the CSR lists: monotone offsets from 0, at most KS_TOPO_MAX_TERMS terms per pod, properties / keys in range
+    if ((pc->topo_term_beg == nullptr) != (pc->topo_terms == nullptr) || (pc->topo_prop_beg == nullptr) != (pc->topo_props == nullptr))
+      KS_FAIL(ctx, KS_EINVAL, "topology lists: an offset array without its list (or the reverse)");
+    for (int32_t i = 0; pc->topo_term_beg && i < p; ++i) {
+      const int32_t b = pc->topo_term_beg[i], e = pc->topo_term_beg[i + 1];
+      if ((i == 0 && b != 0) || e < b || e - b > KS_TOPO_MAX_TERMS)
+        KS_FAIL(ctx, KS_EINVAL, "pod %d: topology term offsets [%d, %d) (at most %d terms)", i, b, e, KS_TOPO_MAX_TERMS);
+      for (int32_t t = b; t < e; ++t) {
+        const uint64_t w = pc->topo_terms[t];
+        const int kind = (int)(w & 0xF), key = (int)((w >> 8) & 0xFF), prop = (int)((w >> 16) & 0xFFFF);
+        const int32_t param = (int32_t)(uint32_t)(w >> 32);
+        if (kind < KS_TOPO_K_SPREAD_HARD || kind > KS_TOPO_K_SCORE || prop >= ctx->topo_nprops || key > ctx->topo_nkeys ||
+            ((w >> 5) & 0x7) != 0 ||
+            ((kind == KS_TOPO_K_SPREAD_HARD || kind == KS_TOPO_K_SPREAD_SOFT) && param < 1) ||
+            (kind == KS_TOPO_K_SCORE && (param < -1000000 || param > 1000000)))
+          KS_FAIL(ctx, KS_EINVAL, "pod %d: topology term %d (%#llx) malformed", i, t - b, (unsigned long long)w);
+      }
     }
+    for (int32_t i = 0; pc->topo_prop_beg && i < p; ++i) {
+      const int32_t b = pc->topo_prop_beg[i], e = pc->topo_prop_beg[i + 1];
+      if ((i == 0 && b != 0) || e < b) KS_FAIL(ctx, KS_EINVAL, "pod %d: topology property offsets [%d, %d)", i, b, e);
+      for (int32_t k = b; k < e; ++k)
+        if (pc->topo_props[k] < 0 || pc->topo_props[k] >= ctx->topo_nprops)
+          KS_FAIL(ctx, KS_EINVAL, "pod %d: topology property %d outside [0, %d)", i, pc->topo_props[k], ctx->topo_nprops);
+    }
+  }
   for (int32_t i = 0; pc->flags && i < p; ++i)
     if (pc->flags[i] & KS_POD_UNMODELLED)
       KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: requests the library does not model (FPGA, DeviceShare allocate hints, "
@@ -3441,7 +3527,8 @@ static CommitArgs commit_args(ks_ctx* ctx, PodStage& st, int32_t total, int32_t 
   ca.topo = ctx->cfg.topology.enable && st.topo ? 1 : 0;
   ca.topo_const = (int32_t)(100 * ctx->cfg.topology.spread_weight);
   ca.topo_rec = st.topo;
-  ca.topo_count = ctx->topo_count[0];
+  ca.topo_props = st.topo_props;
+  ca.topo_count = ctx->topo_count;
   ca.topo_npad = ctx->npad;
   ca.topo_best = ctx->topo_scr ? &ctx->topo_scr->best_total : nullptr;
   *smem = commit_layout(ctx->k, ctx->nchunks, *qcache, (size_t)ca.rsv_bytes, (size_t)ca.dev_bytes, (size_t)ca.numa_bytes,
@@ -3747,6 +3834,7 @@ static TopoKArgs topo_args(ks_ctx* ctx, PodStage& st, const int32_t* cursor, con
   a.labels = ctx->d.labels;
   a.stat = st.stat;
   a.trec = st.topo;
+  a.terms = st.topo_terms;
   a.cursor = cursor;
   a.total_pods = cursor ? ctx->np : 1;
   a.n = ctx->n;
@@ -3819,6 +3907,7 @@ static int topo_step(ks_ctx* ctx) {
     tc.pods = ctx->st.recs;
     tc.pstat = ctx->st.stat;
     tc.trec = ctx->st.topo;
+    tc.props = ctx->st.topo_props;
     tc.cursor = ctx->cursor;
     tc.total_pods = ctx->np;
     tc.quota_enable = ctx->kc.quota_enable;
@@ -3826,7 +3915,7 @@ static int topo_step(ks_ctx* ctx) {
     tc.ports = ctx->kc.ports;
     tc.results = ctx->st.results;
     tc.counters = ctx->counters;
-    tc.topo_count = ctx->topo_count[0];
+    tc.topo_count = ctx->topo_count;
     tc.topo_npad = ctx->npad;
     tc.scr = ctx->topo_scr;
     HIPCHK(ctx, launch_topo_norm(ctx->stream, ta, &tc));
@@ -4018,7 +4107,7 @@ static int launch_pass(ks_ctx* ctx, int32_t ppw, int sweep_blocks, const PipeSha
       se.cand_count = (int32_t*)(b + L.count);
       se.cand_total = (int32_t*)(b + L.total);
     }
-    hipLaunchKernelGGL(select_kernel, dim3(ctx->batch), dim3(kSelThreads), select_smem(se.c1 - se.c0), ss, se);
+    hipLaunchKernelGGL(select_kernel, dim3(kSelBlocks), dim3(kSelThreads), select_smem(se.c1 - se.c0), ss, se);
   }
   if (S > 1) {
     if (ctx->comm || ctx->loop)  // every rank's candidate slots to every rank (one RCCL allgather per pass over xGMI)
@@ -4625,6 +4714,7 @@ struct UnreserveArgs {
   const int64_t* nalloc;   // [2][kNumaDev] its NUMA-node allocation (cpu milli, memory)
   int32_t quota, dev, cpu_loaded, numa_pol, ratio_amp;
   const TopoRec* topo;     // PodTopologySpread / InterPodAffinity: the pod's properties leave the node's counters
+  const int32_t* topo_props;
   int32_t* topo_count;
   int64_t topo_npad;
 };
@@ -4660,9 +4750,7 @@ __global__ void unreserve_kernel(UnreserveArgs a) {
   }
   // NodeInfo.RemovePod: the pod's host ports (a used entry conflicts with itself, so no other pod holds it)
   if (a.c.ports & 1) d.host_ports[n] &= ~a.pstat[0].pwant;
-  if (a.topo)
-    for (uint32_t m = a.topo[0].props; m; m &= m - 1u)
-      a.topo_count[(int64_t)(__ffs((int)m) - 1) * a.topo_npad + n] -= 1;
+  if (a.topo) topo_count_pod(a.topo_count, a.topo_npad, a.topo_props, a.topo[0], n, -1);
   // reservationCache.forgetPod: Allocated -= Mask(requests, ResourceNames); the pod leaves the assigned set
   if (a.gi >= 0) {
     const uint32_t keys = rsv_keys(a.rv.meta[a.gi]);
@@ -4863,7 +4951,8 @@ int ks_unreserve(ks_ctx* ctx, const ks_pod_cols* pod, const ks_result* r, const 
   ua.numa_pol = ctx->kc.numa_pol && ctx->numa_blob;
   ua.ratio_amp = ctx->cfg.numa.enable;
   ua.topo = ctx->cfg.topology.enable ? ctx->ast.topo : nullptr;
-  ua.topo_count = ctx->topo_count[0];
+  ua.topo_props = ctx->ast.topo_props;
+  ua.topo_count = ctx->topo_count;
   ua.topo_npad = ctx->npad;
   hipLaunchKernelGGL(unreserve_kernel, dim3(1), dim3(64), 0, ctx->stream, ua);
   HIPCHK(ctx, hipGetLastError());
@@ -4930,7 +5019,8 @@ int ks_read_nodes(ks_ctx* ctx, ks_node_state* o) {
   HIPCHK(ctx, cp(o->la_prod_term_milli_cpu, v.la_pterm_cpu, 8));
   HIPCHK(ctx, cp(o->la_prod_term_memory, v.la_pterm_mem, 8));
   HIPCHK(ctx, cp(o->host_ports, v.host_ports, 8));
-  for (int q = 0; ctx->cfg.topology.enable && q < KS_TOPO_PROPS; ++q) HIPCHK(ctx, cp(o->topo_count[q], ctx->topo_count[q], 4));
+  for (size_t q = 0; o->topo_count && q < ctx->topo_count_v.size(); ++q)
+    HIPCHK(ctx, cp(o->topo_count + q * n, ctx->topo_count_v[q], 4));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -5179,8 +5269,6 @@ int ks_shard_init(ks_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* uniq
   if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || virtual_shards < 1 || nranks * virtual_shards > 1024)
     return ctx ? (ctx->err = "ks_shard_init: bad args", KS_EINVAL) : KS_EINVAL;
   if (nranks > 1 && !unique_id) KS_FAIL(ctx, KS_EINVAL, "ks_shard_init: nranks > 1 needs the rank-0 unique id");
-  if (nranks > 1 && ctx->cfg.topology.enable)
-    KS_FAIL(ctx, KS_EUNSUPPORTED, "ks_shard_init: PodTopologySpread / InterPodAffinity need every node on one rank");
   HIPCHK(ctx, hipSetDevice(ctx->device));
   if (ctx->comm) {
     (void)ncclCommDestroy(ctx->comm);
@@ -5209,8 +5297,6 @@ int ks_shard_init_loopback(ks_ctx* const* ctxs, int32_t nranks, int32_t virtual_
       if (ctxs[q] == ctxs[r]) KS_FAIL(ctxs[r], KS_EINVAL, "ks_shard_init_loopback: a context is given twice");
     if (ctxs[r]->n != ctxs[0]->n || ctxs[r]->k != ctxs[0]->k || ctxs[r]->batch != ctxs[0]->batch)
       KS_FAIL(ctxs[r], KS_EINVAL, "ks_shard_init_loopback: the ranks must load the same node count, batch and candidates");
-    if (ctxs[r]->cfg.topology.enable)
-      KS_FAIL(ctxs[r], KS_EUNSUPPORTED, "ks_shard_init_loopback: PodTopologySpread / InterPodAffinity need every node on one rank");
   }
   LoopGroup* g = new LoopGroup();
   g->n = nranks;

@@ -25,11 +25,9 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   const int64_t i0 = valid ? i : 0;
   const uint64_t th = c.stat ? d.taints_hard[i0] : 0ull, ts = c.stat ? d.taints_soft[i0] : 0ull,
                  lb = c.stat ? d.labels[i0] : 0ull, hp = c.stat ? d.host_ports[i0] : 0ull;
-  TopoPre pre{};
   if (topo) {
     pi = topo_cur(tk, tr);
     if (pi < 0) return;
-    pre = topo_pre(tk, tr, i, valid);  // (in flight with the stage's loads)
     if (tr.flags & KS_TOPO_DYN) topo_stage(tk, tr, tl);
   }
   TopoNodeIn tin{1u, 0, 0, 0, 0};
@@ -67,7 +65,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     tin = TopoNodeIn{o.reasons, o.dev_raw, o.traw, o.araw, ro.hiord};
   }
   // PodTopologySpread / InterPodAffinity Filters and the normalizations' reductions (every lane, converged)
-  if (topo) topo_eval_node(tk, tr, (int32_t)pi, i, valid, tl, pre, tin);
+  if (topo) topo_eval_node(tk, tr, (int32_t)pi, i, valid, tl, tin);
 }
 
 

@@ -380,7 +380,8 @@ struct CommitArgs {
   int32_t topo;
   int32_t topo_const;        // 100 x the PodTopologySpread weight: the score of a pod without query terms
   const TopoRec* topo_rec;   // [pod] queue order
-  int32_t* topo_count;       // [KS_TOPO_PROPS][topo_npad]
+  const int32_t* topo_props; // the stage's property list (TopoRec.pbeg / nprops)
+  int32_t* topo_count;       // [nprops][topo_npad]
   int64_t topo_npad;
   const long long* topo_best;  // mode 2: the topology step's total of the chosen node
 };
@@ -1992,8 +1993,11 @@ __global__ __launch_bounds__(64) void reserve_pre_kernel(CommitArgs a) {
   if (lane < cnt) {
     const uint32_t ch = a.cand_chunk[j * K + lane];
     const uint2 t = a.cand_t[j * K + lane];
-    kb = local_gkey(t.x, ch);
-    kr = local_gkey(t.y, ch);
+    // (a list entry outside the cluster is not a node: never read as one, whatever the list memory holds)
+    if (ch < (uint32_t)a.nchunks) {
+      kb = local_gkey(t.x, ch);
+      kr = local_gkey(t.y, ch);
+    }
   }
   int32_t rb = 0, rr = 0;  // ranks: keys are distinct (the node is in the low word)
   for (int l = 0; l < 64; ++l) {
@@ -2020,6 +2024,7 @@ __global__ __launch_bounds__(64) void reserve_pre_kernel(CommitArgs a) {
   o.gminors = o.rminors = 0;
   o._pad[0] = o._pad[1] = 0;
   o.g_core = o.g_mem = o.g_ratio = o.g_rdma = 0;
+  if (o.node >= a.n) o.node = -1;
   if (o.node >= 0) {
     const int64_t node = o.node;
     const PodRec pod = a.pods[cursor0 + j];

@@ -6,14 +6,20 @@
 // A topology pod's Filter needs per-domain sums over every eligible node (PreFilter) and its Score a normalization
 // over every feasible node, so it cannot share a pass with other pods: the pass loop runs, before each regular pass,
 // a topology step that acts only when the pod at the cursor is one --
-//   eval_debug_kernel   every other plugin's Filter / Score on every node (ks_debug.hip, the ks_eval_pod path)
-//   topo_filter_kernel  PreFilter domain sums (one workgroup, LDS) + both plugins' Filters, OR-ed into the reasons
-//   topo_norm_kernel    the other plugins' normalizations, PodTopologySpread PreScore / Score / NormalizeScore and
-//                       InterPodAffinity Score / NormalizeScore over the feasible nodes, the best node (max total,
-//                       lowest index) as a one-candidate set
+//   topo_sums_kernel    PreFilter: per query term the domain sums over its eligible nodes
+//   eval_debug_kernel   every other plugin's Filter / Score on every node (ks_debug.hip, the ks_eval_pod path) with
+//                       both plugins' Filters and InterPodAffinity's raw score folded in (topo_eval_node)
+//   topo_pts_kernel     PodTopologySpread PreScore / Score
+//   topo_norm_kernel    every NormalizeScore, the weighted totals, the best node (max total, lowest index)
 //   commit_kernel       (CommitArgs.topo = 2) admission + every Reserve on that node, the counters of the pod's
-//                       properties
+//                       properties (or the lean commit in topo_norm_kernel's last workgroup)
 // -- and every regular pass ends before its first topology pod (CommitArgs.topo = 1).
+//
+// Sizes are the context's (ks_node_cols.topo_nkeys / topo_ndomains / topo_nprops): a query term names one of up to 256
+// topology keys (key 0 the hostname, whose domain is the node itself; key k >= 1 a node label whose value index is
+// DevTopo.dom) and one of up to 65,536 properties; a pod has up to KS_TOPO_MAX_TERMS terms and any number of
+// properties (CSR lists staged with the pod columns).  The per-domain sums of a step live in HBM ([term][domain],
+// DevTopo.zsum), reduced by wave-segmented atomics: one atomic per distinct domain of a wave.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -26,53 +32,64 @@ namespace ks {
 
 // internal pod flag (PodRec.flags): the pod has topology query terms (KS_TOPO_DYN)
 constexpr uint32_t kPodTopoDyn = 0x4000u;
+constexpr int kTopoTerms = KS_TOPO_MAX_TERMS;
 
-// Per pending pod, queue order (staged with the pod columns): the query terms and properties.
+// Per pending pod, queue order (staged with the pod columns): its query terms and properties in the stage's lists
 struct __attribute__((aligned(16))) TopoRec {
-  uint64_t term[KS_TOPO_TERMS];
-  uint32_t props, flags;
-  int32_t nterms, _pad;
+  int32_t tbeg, nterms;  // [tbeg, tbeg + nterms) of the stage's term list
+  int32_t pbeg, nprops;  // [pbeg, pbeg + nprops) of the stage's property list
+  uint32_t flags;        // KS_TOPO_*
+  int32_t _pad[3];
 };
-static_assert(sizeof(TopoRec) == 80, "TopoRec layout");
+static_assert(sizeof(TopoRec) == 32, "TopoRec layout");
 
-// Node side: zonal domain, per-property counters ([p][npad]), the topologyNormalizingWeight table
-// lw[s] = log(s + 2) for s in [0, nlw) (computed by the host's libm, the oracle's log)
+// Node side and the step's per-domain scratch.  lw[s] = log(s + 2) for s in [0, nlw) (the host's libm, the oracle's log).
 struct DevTopo {
-  int32_t* zone;
-  int32_t* count;
+  int32_t* dom;       // [nkeys][npad]: value index of key k + 1 (-1 = absent)
+  int32_t* count;     // [nprops][npad]: pods with property p
   int64_t npad;
+  int32_t nkeys, ndom;
   const double* lw;
   int32_t nlw;
+  int32_t nw;         // 32-bit words of a domain bit set: (ndom + 31) / 32
+  long long* zsum;    // [kTopoTerms][ndom]: per term the domain's counted pods over the term's eligible nodes (0)
+  uint32_t* zpres;    // [kTopoTerms][nw]: hard spread: domains with an eligible node (0)
+  uint32_t* zsize;    // [kTopoTerms][nw]: soft spread: domains of the counted nodes (initPreScoreState's topoSize) (0)
 };
 
 // The topology step's reductions (HBM, one per context).  Every field is back at its initial value after each step
-// (topo_norm_kernel's last workgroup resets it; topo_install writes the initial image).
+// (topo_norm_kernel resets it; topo_install writes the initial image).
 struct TopoScratch {
-  long long zsum[KS_TOPO_TERMS][KS_TOPO_ZONES];  // per term: the zone's counted pods over the term's eligible nodes (0)
-  unsigned long long zpres[KS_TOPO_TERMS];        // hard spread: zones with an eligible node (0)
-  int hmin[KS_TOPO_TERMS];                        // hard spread, hostname: min count over the eligible nodes (INT_MAX)
+  int hmin[kTopoTerms];                           // hard spread, hostname: min count over the eligible nodes (INT_MAX)
+  int tempty[kTopoTerms];                         // soft spread: a counted node without the key (the value "") (0)
   int any_all;                                    // InterPodAffinity: affinityCounts is not empty (0)
-  unsigned long long hsize, zones;                // feasible non-ignored nodes, their zones (0)
-  int empty;                                      // a feasible non-ignored node without the zone label (0)
-  int dev_max, taint_max, aff_max;                // DeviceShare / TaintToleration / NodeAffinity raw maxima (0)
+  int _pad0;
+  unsigned long long hsize;                       // feasible non-ignored nodes (0)
+  int dev_max, taint_max, aff_max, _pad1;         // DeviceShare / TaintToleration / NodeAffinity raw maxima (0)
   long long imin, imax;                           // InterPodAffinity raw extrema, from 0 (0)
   long long smin, smax;                           // PodTopologySpread raw extrema over the non-ignored nodes (LLONG_MAX, 0)
   unsigned long long rsv_pref, rsv_max;           // Reservation preferred-node key, raw max (0)
   unsigned long long best;                        // selectHost key (total + 1) << 32 | ~node (0)
-  unsigned int done;                              // topo_norm_kernel workgroups finished (0)
+  unsigned int done, _pad2;                       // topo_norm_kernel workgroups finished (0)
   long long best_total;                           // the chosen node's total (the pod's result score)
   long long best_node;                            // ... the node (-1 = none feasible)
   // the step's pod, written by topo_sums_kernel (the first kernel of a step) from *cursor: the later kernels read it
   // with one load instead of the cursor -> record chain (-1 = the cursor's pod is not a topology pod)
-  int32_t cur_pi, _pad1[3];
+  int32_t cur_pi, _pad3[3];
   TopoRec cur_rec;
 };
 
-__device__ __forceinline__ int tp_kind(uint64_t w) { return (int)(w & 0xFF); }
-__device__ __forceinline__ int tp_prop(uint64_t w) { return (int)((w >> 8) & 0xFF); }
-__device__ __forceinline__ int tp_key(uint64_t w) { return (int)((w >> 16) & 0xFF); }
-__device__ __forceinline__ uint32_t tp_flags(uint64_t w) { return (uint32_t)((w >> 24) & 0xFF); }
+__device__ __forceinline__ int tp_kind(uint64_t w) { return (int)(w & 0xF); }
+__device__ __forceinline__ uint32_t tp_flags(uint64_t w) { return (uint32_t)((w >> 4) & 0xF); }
+__device__ __forceinline__ int tp_key(uint64_t w) { return (int)((w >> 8) & 0xFF); }
+__device__ __forceinline__ int tp_prop(uint64_t w) { return (int)((w >> 16) & 0xFFFF); }
 __device__ __forceinline__ int32_t tp_param(uint64_t w) { return (int32_t)(uint32_t)(w >> 32); }
+
+// node n's value index of key k >= 1 (-1 = the label is absent)
+__device__ __forceinline__ int32_t tp_dom(const DevTopo& t, int k, int64_t n) { return t.dom[(int64_t)(k - 1) * t.npad + n]; }
+__device__ __forceinline__ int32_t tp_count(const DevTopo& t, uint64_t w, int64_t n) {
+  return t.count[(int64_t)tp_prop(w) * t.npad + n];
+}
 
 // nodeaffinity.GetRequiredNodeAffinity(pod).Match(node) over the label dictionary (NodeAffinity's Filter test)
 __device__ __forceinline__ bool tp_node_aff(const PodStat* s, uint64_t labels) {
@@ -97,6 +114,12 @@ __device__ __forceinline__ int32_t topo_pass_pods(const A& a, int32_t cursor0, i
   return dyn ? (int32_t)(__ffsll((long long)dyn) - 1) : np;
 }
 
+// NodeInfo.AddPod / RemovePod for the two plugins: the counters of the pod's properties on node n (delta +1 / -1)
+__device__ __forceinline__ void topo_count_pod(int32_t* count, int64_t npad, const int32_t* props, const TopoRec& t,
+                                               int64_t n, int32_t delta) {
+  for (int32_t k = 0; k < t.nprops; ++k) atomicAdd(count + (int64_t)props[t.pbeg + k] * npad + n, delta);
+}
+
 // Write-back of one result: the counters of the placed pod's properties (NodeInfo.AddPod), its score (the topology
 // step's total; a pod without query terms gets PodTopologySpread's constant 100 x weight on every node)
 template <typename A>
@@ -105,12 +128,7 @@ __device__ __forceinline__ void topo_writeback(const A& a, int32_t pod, ks_resul
   const TopoRec& t = a.topo_rec[pod];
   if (a.topo == 2) r.score = *a.topo_best;
   else if (a.topo == 1 && !(t.flags & KS_TOPO_DYN)) r.score += a.topo_const;
-  uint32_t m = t.props;
-  while (m) {
-    const int q = __ffs((int)m) - 1;
-    m &= m - 1u;
-    atomicAdd(a.topo_count + (int64_t)q * a.topo_npad + r.node, 1);
-  }
+  topo_count_pod(a.topo_count, a.topo_npad, a.topo_props, t, r.node, 1);
 }
 
 // ---- topology step kernels (ks_topo.hip) ----
@@ -120,6 +138,7 @@ struct TopoKArgs {
   const uint64_t* labels;  // DevNodes.labels (required node affinity of the spread constraints)
   const PodStat* stat;     // the stage's PodStat records (NULL = no node affinity)
   const TopoRec* trec;     // the stage's TopoRec records
+  const uint64_t* terms;   // the stage's query-term list
   const int32_t* cursor;   // the pod at *cursor, only if it is a topology pod; NULL = pod 0, always (ks_eval_pod)
   int32_t total_pods;
   int64_t n;
@@ -162,13 +181,25 @@ __device__ __forceinline__ int32_t topo_cur(const TopoKArgs& a, TopoRec& rec) {
   return a.scr->cur_pi;
 }
 
-// the node counts for the term (hard spread: required node affinity + every hard key; soft spread: required node
+// the step pod's term t (wave-uniform scalar load)
+__device__ __forceinline__ uint64_t topo_term(const TopoKArgs& a, const TopoRec& tr, int t) { return a.terms[tr.tbeg + t]; }
+
+// nodeLabelsMatchSpreadConstraints over the pod's constraints of one kind: node n has every key they name
+__device__ __forceinline__ bool topo_keys_ok(const TopoKArgs& a, const TopoRec& tr, int kind, int64_t n) {
+  bool ok = true;
+  for (int t = 0; t < tr.nterms; ++t) {
+    const uint64_t w = topo_term(a, tr, t);
+    if (tp_kind(w) == kind && tp_key(w) != 0) ok = ok && tp_dom(a.t, tp_key(w), n) >= 0;
+  }
+  return ok;
+}
+
+// the node counts for term w (hard spread: required node affinity + every hard key; soft spread: required node
 // affinity + every soft key when requireAllTopologies; InterPodAffinity: every node)
-__device__ __forceinline__ bool tp_eligible(uint64_t w, uint32_t pflags, bool aff, bool zone_ok) {
+__device__ __forceinline__ bool tp_eligible(uint64_t w, uint32_t pflags, bool aff, bool hard_keys, bool soft_keys) {
   const int k = tp_kind(w);
-  if (k == KS_TOPO_K_SPREAD_HARD) return aff && (!(tp_flags(w) & KS_TOPO_T_ELIG_ZONE) || zone_ok);
-  if (k == KS_TOPO_K_SPREAD_SOFT)
-    return aff && (!((pflags & KS_TOPO_SOFT_ALL_KEYS) && (tp_flags(w) & KS_TOPO_T_ELIG_ZONE)) || zone_ok);
+  if (k == KS_TOPO_K_SPREAD_HARD) return aff && hard_keys;
+  if (k == KS_TOPO_K_SPREAD_SOFT) return aff && (!(pflags & KS_TOPO_SOFT_ALL_KEYS) || soft_keys);
   return true;
 }
 
@@ -178,65 +209,61 @@ __device__ __forceinline__ long long wave_max_i64(long long v) {
 __device__ __forceinline__ long long wave_min_i64(long long v) {
   return (long long)(~wave_max_u64(~((uint64_t)v ^ (1ull << 63))) ^ (1ull << 63));
 }
-
-__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+__device__ __forceinline__ long long wave_sum_i64(long long v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    const uint32_t lo = __shfl_xor((int)(uint32_t)v, off, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), off, 64);
-    v |= ((uint64_t)hi << 32) | lo;
+    const uint32_t lo = __shfl_xor((int)(uint32_t)v, off, 64), hi = __shfl_xor((int)(uint32_t)((uint64_t)v >> 32), off, 64);
+    v += (long long)(((uint64_t)hi << 32) | lo);
   }
   return v;
 }
 
-// The block's LDS copy of the step's domain sums (TopoLds) and the hard spread constraints' minimum match count per
-// term (TpKeyToCriticalPaths[key][0].MatchNum; MaxInt32 when no domain is eligible), from what topo_sums_kernel left
-// in the scratch: one load per thread, the minima by LDS atomics.  Every thread of the block calls it.
+// Wave-segmented reduction into HBM (every lane calls it, converged): lanes with `on` add `v` to sum[z] and set bit z of
+// bits (either may be NULL); one atomic per distinct z of the wave
+__device__ __forceinline__ void topo_seg_add(long long* sum, uint32_t* bits, bool on, int32_t z, long long v) {
+  uint64_t act = __ballot(on);
+  while (act) {
+    const int l = __ffsll((long long)act) - 1;
+    const int32_t z0 = __shfl(z, l, 64);
+    const bool mine = on && z == z0;
+    const uint64_t m = __ballot(mine);
+    const long long s = sum ? wave_sum_i64(mine ? v : 0) : 0;
+    if ((threadIdx.x & 63) == l) {
+      if (sum && s) atomicAdd((unsigned long long*)(sum + z0), (unsigned long long)s);
+      if (bits) atomicOr(bits + (z0 >> 5), 1u << (z0 & 31));
+    }
+    act &= ~m;
+  }
+}
+
+// The block's LDS copy of the hard spread constraints' minimum match count per term (TpKeyToCriticalPaths[key][0]
+// .MatchNum; MaxInt32 when no domain is eligible) and affinityCounts' emptiness, from what topo_sums_kernel left in
+// the scratch.  Every thread of the block calls it.
 struct TopoLds {
-  long long zsum[KS_TOPO_TERMS][KS_TOPO_ZONES];
-  unsigned long long zpres[KS_TOPO_TERMS];
-  long long mins[KS_TOPO_TERMS];
-  int any_all;  // affinityCounts is not empty
+  long long mins[kTopoTerms];
+  int any_all;
 };
 __device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr, TopoLds& l) {
   const int tid = threadIdx.x;
-  if (tid < KS_TOPO_TERMS) {
-    l.zpres[tid] = a.scr->zpres[tid];
-    l.mins[tid] = a.scr->hmin[tid];
-  }
+  if (tid < kTopoTerms) l.mins[tid] = a.scr->hmin[tid];
   if (tid == 0) l.any_all = a.scr->any_all;
-  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) (&l.zsum[0][0])[k] = (&a.scr->zsum[0][0])[k];
   __syncthreads();
-  uint32_t zkey = 0;  // terms with the zonal key (a register mask: no dynamic index into the record)
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) zkey |= (tp_key(tr.term[t]) == 1 ? 1u : 0u) << t;
-  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += blockDim.x) {
-    const int t = k / KS_TOPO_ZONES, z = k - t * KS_TOPO_ZONES;
-    if (((zkey >> t) & 1u) && ((l.zpres[t] >> z) & 1ull)) atomicMin(&l.mins[t], l.zsum[t][z]);
+  for (int t = 0; t < tr.nterms; ++t) {
+    const uint64_t w = topo_term(a, tr, t);
+    if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD || tp_key(w) == 0) continue;  // (wave-uniform)
+    long long m = LLONG_MAX;
+    for (int z = tid; z < a.t.ndom; z += blockDim.x)
+      if ((a.t.zpres[(int64_t)t * a.t.nw + (z >> 5)] >> (z & 31)) & 1u) {
+        const long long v = a.t.zsum[(int64_t)t * a.t.ndom + z];
+        m = v < m ? v : m;
+      }
+    m = wave_min_i64(m);
+    if ((tid & 63) == 0 && m != LLONG_MAX) atomicMin(&l.mins[t], m);
   }
   __syncthreads();
 }
 
-// topo_eval_node's node inputs, loaded as soon as the step's pod record is known (with the stage's loads, ahead of
-// the plugin evaluation): the zone, the labels, the hostname-keyed terms' counts
-struct TopoPre {
-  int32_t z;
-  uint64_t lab;
-  int32_t cnt[KS_TOPO_TERMS];
-};
-__device__ __forceinline__ TopoPre topo_pre(const TopoKArgs& a, const TopoRec& tr, int64_t i, bool valid) {
-  TopoPre p;
-  const int64_t n = valid ? i : 0;
-  p.z = valid ? a.t.zone[n] : -1;
-  p.lab = a.labels ? a.labels[n] : 0ull;
-  const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-    const uint64_t w = tr.term[t];
-    p.cnt[t] = (dyn && w && tp_key(w) == 0) ? a.t.count[(int64_t)tp_prop(w) * a.t.npad + n] : 0;
-  }
-  return p;
-}
-// ... and the evaluation's results for the node (registers, not re-read from the buffers just written)
+// topo_eval_node's results of the other plugins for the node (registers, not re-read from the buffers just written)
 struct TopoNodeIn {
   uint32_t base;  // every other plugin's reasons
   int32_t dr, trw, arw, rhi;
@@ -244,46 +271,47 @@ struct TopoNodeIn {
 
 // eval_debug_kernel's topology part for node i (every lane of the wave calls it, converged; valid = a node of the
 // cluster): both plugins' Filters OR-ed into the node's reasons (total -1 and the score row zeroed when they fail),
-// InterPodAffinity's raw score, and the node's part of the normalizations' reductions (one global atomic per wave)
+// InterPodAffinity's raw score, the counted nodes' domains of the soft constraints (topology sizes), and the node's part
+// of the normalizations' reductions (one global atomic per wave)
 __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec& tr, int32_t pi, int64_t i, bool valid,
-                                               const TopoLds& l, const TopoPre& pre, const TopoNodeIn& in) {
+                                               const TopoLds& l, const TopoNodeIn& in) {
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
-  bool soft_zone = false, need_aff = false;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-    const int k = tp_kind(tr.term[t]);
-    soft_zone |= k == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
-    need_aff |= k == KS_TOPO_K_SPREAD_HARD;
-  }
   const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
+  const int64_t n = valid ? i : 0;
   bool feas = false, counted = false;
-  int32_t z = -1;
   long long ir = 0;
   int32_t dr = 0, trw = 0, arw = 0;
   uint64_t pref = 0;
   if (valid) {
     const uint32_t base = in.base;
-    z = pre.z;
-    const bool has_zone = z >= 0;
     uint32_t r = 0;
     if (dyn) {
-      auto domain = [&](int t) -> long long {
-        const uint64_t w = tr.term[t];
-        return tp_key(w) == 1 ? l.zsum[t][z] : (long long)pre.cnt[t];
+      const bool hard_keys = topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_HARD, n);
+      // the term's count in the node's domain (the node has the key's label)
+      auto domain = [&](int t, uint64_t w) -> long long {
+        if (tp_key(w) == 0) return (long long)tp_count(a.t, w, n);
+        return a.t.zsum[(int64_t)t * a.t.ndom + tp_dom(a.t, tp_key(w), n)];
       };
-      const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, pre.lab) : true;
       // PodTopologySpread Filter: the first hard constraint that fails
-    #pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-        const uint64_t w = tr.term[t];
+      bool aff = true, aff_done = false;
+      for (int t = 0; t < tr.nterms; ++t) {
+        const uint64_t w = topo_term(a, tr, t);
         if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD) continue;
-        if (tp_key(w) == 1 && !has_zone) {  // ErrReasonNodeLabelNotMatch
+        const int32_t z = tp_key(w) == 0 ? 0 : tp_dom(a.t, tp_key(w), n);
+        if (z < 0) {  // ErrReasonNodeLabelNotMatch
           r = KS_R_TOPOLOGY_SPREAD;
           break;
         }
         long long match;
-        if (tp_key(w) == 1) match = ((l.zpres[t] >> z) & 1ull) ? l.zsum[t][z] : 0;
-        else match = tp_eligible(w, tr.flags, aff, has_zone) ? (long long)pre.cnt[t] : 0;
+        if (tp_key(w) != 0) {
+          match = ((a.t.zpres[(int64_t)t * a.t.nw + (z >> 5)] >> (z & 31)) & 1u) ? a.t.zsum[(int64_t)t * a.t.ndom + z] : 0;
+        } else {
+          if (!aff_done) {
+            aff = tp_node_aff(a.stat ? a.stat + pi : nullptr, a.labels ? a.labels[n] : 0ull);
+            aff_done = true;
+          }
+          match = (aff && hard_keys) ? (long long)tp_count(a.t, w, n) : 0;
+        }
         const long long self = (tp_flags(w) & KS_TOPO_T_SELF) ? 1 : 0;
         if (match + self - l.mins[t] > (long long)tp_param(w)) {  // ErrReasonConstraintsNotMatch
           r = KS_R_TOPOLOGY_SPREAD;
@@ -292,28 +320,26 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       }
       // InterPodAffinity Filter: affinity, anti-affinity, existing pods' anti-affinity -- the first that fails
       bool aff_terms = false, missing = false, exist = true;
-    #pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-        if (tp_kind(tr.term[t]) != KS_TOPO_K_AFFINITY) continue;
+      for (int t = 0; t < tr.nterms; ++t) {
+        const uint64_t w = topo_term(a, tr, t);
+        if (tp_kind(w) != KS_TOPO_K_AFFINITY) continue;
         aff_terms = true;
-        if (tp_key(tr.term[t]) == 1 && !has_zone) missing = true;
-        else if (domain(t) <= 0) exist = false;
+        if (tp_key(w) != 0 && tp_dom(a.t, tp_key(w), n) < 0) missing = true;
+        else if (domain(t, w) <= 0) exist = false;
       }
       uint32_t ipa = 0;
       if (aff_terms && (missing || (!exist && !(l.any_all == 0 && (tr.flags & KS_TOPO_SELF_AFFINITY))))) {
         ipa = KS_R_POD_AFFINITY;
       } else {
-#pragma unroll
-        for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-          if (ipa) break;
-          const uint64_t w = tr.term[t];
-          if (tp_kind(w) == KS_TOPO_K_ANTI && (tp_key(w) == 0 || has_zone) && domain(t) > 0) ipa = KS_R_POD_ANTI_AFFINITY;
+        for (int t = 0; t < tr.nterms && !ipa; ++t) {
+          const uint64_t w = topo_term(a, tr, t);
+          if (tp_kind(w) == KS_TOPO_K_ANTI && (tp_key(w) == 0 || tp_dom(a.t, tp_key(w), n) >= 0) && domain(t, w) > 0)
+            ipa = KS_R_POD_ANTI_AFFINITY;
         }
-#pragma unroll
-        for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-          if (ipa) break;
-          const uint64_t w = tr.term[t];
-          if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && (tp_key(w) == 0 || has_zone) && domain(t) > 0)
+        for (int t = 0; t < tr.nterms && !ipa; ++t) {
+          const uint64_t w = topo_term(a, tr, t);
+          if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && (tp_key(w) == 0 || tp_dom(a.t, tp_key(w), n) >= 0) &&
+              domain(t, w) > 0)
             ipa = KS_R_EXISTING_ANTI_AFFINITY;
         }
       }
@@ -325,14 +351,16 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
           for (int k = 0; k < KS_NUM_SCORE_PLUGINS; ++k) a.scores[i * KS_NUM_SCORE_PLUGINS + k] = 0;
       }
       // InterPodAffinity Score: weight x matching pods in the node's domain, per score term
-    #pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-        const uint64_t w = tr.term[t];
-        if (tp_kind(w) == KS_TOPO_K_SCORE && (tp_key(w) == 0 || has_zone)) ir += (long long)tp_param(w) * domain(t);
-      }
+      if ((base | r) == 0)
+        for (int t = 0; t < tr.nterms; ++t) {
+          const uint64_t w = topo_term(a, tr, t);
+          if (tp_kind(w) == KS_TOPO_K_SCORE && (tp_key(w) == 0 || tp_dom(a.t, tp_key(w), n) >= 0))
+            ir += (long long)tp_param(w) * domain(t, w);
+        }
     }
     feas = (base | r) == 0;
-    counted = feas && !(soft_all && soft_zone && !has_zone);  // initPreScoreState: not an ignored node
+    // initPreScoreState: a node without every soft key is ignored under requireAllTopologies
+    counted = feas && !(dyn && soft_all && !topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, n));
     if (feas) {
       a.iraw[i] = ir;
       dr = in.dr;
@@ -341,19 +369,24 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       if (a.rsv_on && in.rhi > 0) pref = ((uint64_t)in.rhi << 32) | (0xFFFFFFFFull - (uint64_t)i);
     }
   }
-  // the wave's part of every reduction, then one atomic per quantity
+  // topology sizes of the soft constraints over the counted nodes: per term the domains (a node without the key: "")
+  if (dyn)
+    for (int t = 0; t < tr.nterms; ++t) {
+      const uint64_t w = topo_term(a, tr, t);
+      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) continue;  // (wave-uniform)
+      const int32_t z = counted ? tp_dom(a.t, tp_key(w), n) : -1;
+      topo_seg_add(nullptr, a.t.zsize + (int64_t)t * a.t.nw, counted && z >= 0, z, 0);
+      if (__ballot(counted && z < 0) && (threadIdx.x & 63) == 0) atomicOr(&a.scr->tempty[t], 1);
+    }
+  // the wave's part of every other reduction, then one atomic per quantity
   const int lane = threadIdx.x & 63;
   const uint64_t cnt = __ballot(counted);
-  const uint64_t zbits = wave_or_u64(counted && z >= 0 ? (1ull << z) : 0ull);
-  const bool emp = __ballot(counted && z < 0) != 0;
   const long long imn = wave_min_i64(feas ? ir : 0), imx = wave_max_i64(feas ? ir : 0);
   const uint32_t dmx = wave_max_u32((uint32_t)dr), tmx = wave_max_u32((uint32_t)trw), amx = wave_max_u32((uint32_t)arw);
   const uint64_t pmx = wave_max_u64(pref);
   if (lane == 0) {
     TopoScratch* s = a.scr;
     if (cnt) atomicAdd(&s->hsize, (unsigned long long)__popcll(cnt));
-    if (zbits) atomicOr(&s->zones, zbits);
-    if (emp) atomicOr(&s->empty, 1);
     if (imn < 0) atomicMin(&s->imin, imn);
     if (imx > 0) atomicMax(&s->imax, imx);
     if (dmx) atomicMax(&s->dev_max, (int)dmx);
@@ -372,6 +405,7 @@ struct TopoCommitArgs {
   const PodRec* pods;
   const PodStat* pstat;
   const TopoRec* trec;
+  const int32_t* props;  // the stage's property list
   int32_t* cursor;
   int32_t total_pods;
   int32_t quota_enable, quota_parent, ports;

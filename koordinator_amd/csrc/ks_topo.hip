@@ -1,13 +1,15 @@
 // ks_topo.hip — the topology step's kernels (ks_topo.h).  One thread per node, 256-thread workgroups over the
-// cluster; each workgroup pre-reduces in LDS / by wave and issues one global atomic per quantity, so a reduction
-// over 5k nodes is ~80 atomics to a handful of addresses rather than 5k.  The step's sequence:
-//   topo_sums_kernel   PreFilter: per term the zone sums, zones present, hostname minimum (eligible nodes only)
+// cluster; each wave pre-reduces (per quantity, or per distinct domain of its nodes) and issues one global atomic each,
+// so a reduction over 5k nodes is ~80 atomics per address rather than 5k.  The step's sequence:
+//   topo_sums_kernel   PreFilter: per term the domain sums, domains present, hostname minimum (eligible nodes only)
 //   eval_debug_kernel  every plugin's Filter / Score + topo_eval_node: both plugins' Filters, InterPodAffinity's raw
 //                      score, the other plugins' normalization maxima (ks_debug.hip)
-//   topo_pts_kernel    PodTopologySpread PreScore / Score: the topology sizes' weights, raw scores, their extrema;
+//   topo_pts_kernel    PodTopologySpread PreScore / Score: the topology sizes' weights (per soft constraint, from the
+//                      counted nodes' domains eval_debug_kernel marked), raw scores, their extrema;
 //                      the Reservation raw maximum (needs the preferred node)
-//   topo_norm_kernel   every NormalizeScore + weighted totals + selectHost; the last workgroup writes the one-candidate
-//                      set and puts the scratch back to its initial image
+//   topo_norm_kernel   every NormalizeScore + weighted totals + selectHost; the per-domain scratch zeroed by every
+//                      workgroup's slice; the last workgroup writes the one-candidate set (or commits) and puts the
+//                      scratch back to its initial image
 //
 // Upstream kube-scheduler v1.24.15 (not on disk: parity unpinned, restated on objects by oracle/topology_ref.py and on
 // the compiled form by oracle/koord_oracle.c tp_*):
@@ -34,22 +36,18 @@ constexpr int kTopoThreads = 256;
 TopoScratch topo_scratch_init() {
   TopoScratch s;
   std::memset(&s, 0, sizeof(s));
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) s.hmin[t] = INT_MAX;  // newCriticalPaths: MatchNum math.MaxInt32
+  for (int t = 0; t < kTopoTerms; ++t) s.hmin[t] = INT_MAX;  // newCriticalPaths: MatchNum math.MaxInt32
   s.smin = LLONG_MAX;
   s.cur_pi = -1;
   return s;
 }
 
 __global__ __launch_bounds__(kTopoThreads) void topo_sums_kernel(TopoKArgs a) {
-  __shared__ long long zs[KS_TOPO_TERMS][KS_TOPO_ZONES];
-  __shared__ unsigned long long zp[KS_TOPO_TERMS];
-  __shared__ int hm[KS_TOPO_TERMS];
-  __shared__ int aa;
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * kTopoThreads + tid;
-  const int64_t n0 = n < a.n ? n : 0;
-  const int32_t z = a.t.zone[n0];  // (the node's loads issued with the cursor -> record chain)
-  const uint64_t lab = a.labels ? a.labels[n0] : 0ull;
+  const bool in = n < a.n;
+  const int64_t n0 = in ? n : 0;
+  const uint64_t lab = a.labels ? a.labels[n0] : 0ull;  // (the node's loads issued with the cursor -> record chain)
   TopoRec tr;
   const int32_t pi = topo_pod(a, tr);
   if (blockIdx.x == 0 && tid == 0) {
@@ -57,55 +55,35 @@ __global__ __launch_bounds__(kTopoThreads) void topo_sums_kernel(TopoKArgs a) {
     a.scr->cur_rec = tr;
   }
   if (pi < 0 || !(tr.flags & KS_TOPO_DYN)) return;
-  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&zs[0][0])[k] = 0;
-  if (tid < KS_TOPO_TERMS) {
-    zp[tid] = 0;
-    hm[tid] = INT_MAX;
+  bool need_aff = false;
+  for (int t = 0; t < tr.nterms; ++t) {
+    const int k = tp_kind(topo_term(a, tr, t));
+    need_aff |= k == KS_TOPO_K_SPREAD_HARD || k == KS_TOPO_K_SPREAD_SOFT;
   }
-  if (tid == 0) aa = 0;
-  __syncthreads();
-  bool aff_host = false, need_aff = false;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-    aff_host |= tp_kind(tr.term[t]) == KS_TOPO_K_AFFINITY && tp_key(tr.term[t]) == 0;
-    need_aff |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_HARD || tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT;
-  }
-  // every active term's count first (independent loads), then the node's part; the zones present and the hostname
-  // minima are reduced per wave (a same-address LDS atomic from every lane would serialize 64-way)
-  const bool in = n < a.n;
-  int32_t cnt[KS_TOPO_TERMS];
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) cnt[t] = tr.term[t] ? a.t.count[(int64_t)tp_prop(tr.term[t]) * a.t.npad + n0] : 0;
   const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, lab) : true;
-  bool aav = false;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-    const uint64_t w = tr.term[t];
-    if (!w) continue;  // (wave-uniform)
-    const bool el = in && tp_eligible(w, tr.flags, aff, z >= 0);
-    if (tp_key(w) == 1) {
-      const bool zd = el && z >= 0;
-      if (zd && cnt[t]) atomicAdd((unsigned long long*)&zs[t][z], (unsigned long long)(long long)cnt[t]);
-      const uint64_t o = wave_or_u64(zd ? (1ull << z) : 0ull);
-      if ((tid & 63) == 0 && o) atomicOr(&zp[t], o);
-    } else if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD) {
-      const uint32_t m = ~wave_max_u32(~(uint32_t)(el ? cnt[t] : INT_MAX));  // (counts are >= 0)
-      if ((tid & 63) == 0 && m != (uint32_t)INT_MAX) atomicMin(&hm[t], (int)m);
-    }
-    if (tp_kind(w) == KS_TOPO_K_AFFINITY) aav |= el && cnt[t] > 0 && (aff_host || z >= 0);
-  }
-  if (__ballot(aav) && (tid & 63) == 0) aa = 1;
-  __syncthreads();
+  const bool hard_keys = topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_HARD, n0);
+  const bool soft_keys = topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, n0);
   TopoScratch* s = a.scr;
-  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) {
-    const long long v = (&zs[0][0])[k];
-    if (v) atomicAdd((unsigned long long*)&(&s->zsum[0][0])[k], (unsigned long long)v);
+  bool aav = false;
+  for (int t = 0; t < tr.nterms; ++t) {
+    const uint64_t w = topo_term(a, tr, t);  // (wave-uniform)
+    const bool el = in && tp_eligible(w, tr.flags, aff, hard_keys, soft_keys);
+    const int32_t cnt = el ? tp_count(a.t, w, n0) : 0;
+    int32_t z = 0;
+    if (tp_key(w) != 0) {
+      z = in ? tp_dom(a.t, tp_key(w), n0) : -1;
+      // the domain's sum, and for a hard constraint the domains with an eligible node (TpPairToMatchNum's keys)
+      topo_seg_add(a.t.zsum + (int64_t)t * a.t.ndom,
+                   tp_kind(w) == KS_TOPO_K_SPREAD_HARD ? a.t.zpres + (int64_t)t * a.t.nw : nullptr, el && z >= 0, z,
+                   (long long)cnt);
+    } else if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD) {
+      const uint32_t m = ~wave_max_u32(~(uint32_t)(el ? cnt : INT_MAX));  // (counts are >= 0)
+      if ((tid & 63) == 0 && m != (uint32_t)INT_MAX) atomicMin(&s->hmin[t], (int)m);
+    }
+    // affinityCounts: a pod matching every required term counts on each term's (key, value) the node has
+    if (tp_kind(w) == KS_TOPO_K_AFFINITY) aav |= el && cnt > 0 && z >= 0;
   }
-  if (tid < KS_TOPO_TERMS) {
-    if (zp[tid]) atomicOr(&s->zpres[tid], zp[tid]);
-    if (hm[tid] != INT_MAX) atomicMin(&s->hmin[tid], hm[tid]);
-  }
-  if (tid == 0 && aa) atomicOr(&s->any_all, 1);
+  if (__ballot(aav) && (tid & 63) == 0) atomicOr(&s->any_all, 1);
 }
 
 // topologyNormalizingWeight(size) = log(size + 2), from the host's table
@@ -117,67 +95,41 @@ __device__ __forceinline__ double topo_weight(const DevTopo& t, unsigned long lo
 // branches, and only then loads its node)
 #define KS_TOPO_ISSUED(...) asm volatile("" ::__VA_ARGS__)
 
-// PodTopologySpread's raw score of a feasible node (PreScore's pair counts, Score's scoreForCount summed in term order,
-// math.Round); false = an ignored node (initPreScoreState: a soft zonal constraint with requireAllTopologies and no
-// zone label).  Every count is loaded before the f64 sum.
-__device__ __forceinline__ bool topo_spread_raw(const TopoKArgs& a, const TopoRec& tr, int64_t i, int32_t z, double hw,
-                                                double zw, bool ign_zoneless, long long& sr) {
-  // branch-free in the node: a zonal term of a node without the zone loads domain 0 and is not added
-  const bool has_zone = z >= 0;
-  const int zc = has_zone ? z : 0;
-  long long cnt[KS_TOPO_TERMS];
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-    const uint64_t w = tr.term[t];
-    cnt[t] = 0;
-    if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) continue;  // (wave-uniform)
-    cnt[t] = tp_key(w) == 1 ? a.scr->zsum[t][zc] : (long long)a.t.count[(int64_t)tp_prop(w) * a.t.npad + i];
-  }
-  double score = 0.0;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t) {
-    const uint64_t w = tr.term[t];
-    if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) continue;
-    const double add = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt[t], tp_key(w) == 1 ? zw : hw), (double)(tp_param(w) - 1)));
-    score = (tp_key(w) == 1 && !has_zone) ? score : add;
-  }
-  const bool ignored = ign_zoneless && !has_zone;
-  sr = ignored ? 0 : (long long)::round(score);
-  return !ignored;
-}
-
-__device__ __forceinline__ bool topo_soft_zone(const TopoRec& tr) {
-  bool soft_zone = false;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t)
-    soft_zone |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
-  return soft_zone;
-}
-
 __global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
+  __shared__ double tw[kTopoTerms];
+  __shared__ unsigned int tsz[kTopoTerms];
   const int tid = threadIdx.x;
   const int64_t i = (int64_t)blockIdx.x * kTopoThreads + tid;
   const bool in = i < a.n;
   const TopoScratch* s = a.scr;
   const uint32_t rs = in ? a.reasons[i] : 1u;
-  const int32_t z = in ? a.t.zone[i] : -1;
   const int32_t rr = (in && a.rsv_on) ? a.rraw[i] : 0;
-  const unsigned long long hs = s->hsize, zn = s->zones, rp = s->rsv_pref;
-  const int em = s->empty;
+  const unsigned long long hs = s->hsize, rp = s->rsv_pref;
   TopoRec tr;
   const int32_t pi = topo_cur(a, tr);
-  KS_TOPO_ISSUED("v"(rs), "v"(z), "v"(rr));
-  if (pi < 0) return;
+  KS_TOPO_ISSUED("v"(rs), "v"(rr));
+  if (pi < 0) return;  // (grid-uniform)
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
-  bool soft_zone = false;
-#pragma unroll
-  for (int t = 0; t < KS_TOPO_TERMS; ++t)
-    soft_zone |= tp_kind(tr.term[t]) == KS_TOPO_K_SPREAD_SOFT && (tp_flags(tr.term[t]) & KS_TOPO_T_ELIG_ZONE);
   const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
-  // initPreScoreState's sizes: the hostname's the non-ignored feasible nodes, the zone's their distinct values (a node
-  // without the label counts as the value "")
-  const double hw = topo_weight(a.t, hs);
-  const double zw = topo_weight(a.t, (unsigned long long)__popcll(zn) + (em ? 1ull : 0ull));
+  // initPreScoreState's sizes per soft constraint: the hostname's the non-ignored feasible nodes, another key's their
+  // distinct values (a node without the label counts as the value "")
+  if (dyn) {
+    if (tid < kTopoTerms) tsz[tid] = 0u;
+    __syncthreads();
+    for (int t = 0; t < tr.nterms; ++t) {
+      const uint64_t w = topo_term(a, tr, t);
+      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) continue;
+      unsigned int c = 0;
+      for (int k = tid; k < a.t.nw; k += kTopoThreads) c += (unsigned int)__popc(a.t.zsize[(int64_t)t * a.t.nw + k]);
+      if (c) atomicAdd(&tsz[t], c);
+    }
+    __syncthreads();
+    if (tid < tr.nterms) {
+      const uint64_t w = topo_term(a, tr, tid);
+      tw[tid] = topo_weight(a.t, tp_key(w) == 0 ? hs : (unsigned long long)tsz[tid] + (s->tempty[tid] ? 1ull : 0ull));
+    }
+    __syncthreads();
+  }
   const int64_t pref = rp ? (int64_t)(0xFFFFFFFFull - (rp & 0xFFFFFFFFull)) : -1;
   bool counted = false;
   long long sr = 0;
@@ -185,7 +137,25 @@ __global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
   if (in && rs == 0) {
     if (a.rsv_on) rmx = i == pref ? 1000ull : (uint64_t)(uint32_t)rr;
     if (dyn) {
-      counted = topo_spread_raw(a, tr, i, z, hw, zw, soft_all && soft_zone, sr);
+      // PodTopologySpread's raw score (PreScore's pair counts, Score's scoreForCount summed in term order in Go's f64
+      // order, math.Round); an ignored node (requireAllTopologies, a soft key missing) scores 0 and is not counted
+      const bool ignored = soft_all && !topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, i);
+      double score = 0.0;
+      for (int t = 0; t < tr.nterms; ++t) {
+        const uint64_t w = topo_term(a, tr, t);
+        if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) continue;  // (wave-uniform)
+        long long cnt;
+        if (tp_key(w) == 0) {
+          cnt = (long long)tp_count(a.t, w, i);
+        } else {
+          const int32_t z = tp_dom(a.t, tp_key(w), i);
+          if (z < 0) continue;  // (a node without the key adds nothing)
+          cnt = a.t.zsum[(int64_t)t * a.t.ndom + z];
+        }
+        score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, tw[t]), (double)(tp_param(w) - 1)));
+      }
+      counted = !ignored;
+      sr = ignored ? 0 : (long long)::round(score);
       a.sraw[i] = sr;
     }
   }
@@ -235,8 +205,9 @@ __device__ __forceinline__ void topo_commit_one(const TopoCommitArgs& a, int lan
         d.la_pterm_mem[n] += p.est_mem;
       }
       if (a.ports & 1) d.host_ports[n] |= a.pstat[c].pwant;
-      for (uint32_t m = tr.props; m; m &= m - 1u) a.topo_count[(int64_t)(__ffs((int)m) - 1) * a.topo_npad + n] += 1;
     }
+    // the pod's properties (lanes over its list)
+    for (int32_t k = lane; k < tr.nprops; k += 64) atomicAdd(a.topo_count + (int64_t)a.props[tr.pbeg + k] * a.topo_npad + n, 1);
   }
   if (lane == 0) {
     a.results[c] = r;
@@ -244,6 +215,14 @@ __device__ __forceinline__ void topo_commit_one(const TopoCommitArgs& a, int lan
     atomicAdd(&a.counters[0], 1ull);
   }
 }
+
+// The last-workgroup hand-off below relies on gfx9's vmcnt covering non-returning atomics (each wave waits for its own
+// atomics before the workgroup's arrival) and on agent-scope atomics being performed at the memory side across XCDs,
+// so that the arrival ticket needs no L2 write-back fence.  Another ISA needs a release / acquire
+// ticket instead.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "topo_norm_kernel's fence-free arrival ticket is written for gfx950"
+#endif
 
 // lean != 0: the last workgroup also commits the pod (topo_commit_one, the plugin sets whose Reserve is AddPod + the
 // assign cache + quota); else it leaves the one-candidate set and the chosen node for the general commit kernel
@@ -259,14 +238,13 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   const int32_t dr = (in && a.dev_on) ? a.draw[i] : 0, tr_ = (in && a.taint_on) ? a.traw[i] : 0,
                 ar = (in && a.aff_on) ? a.araw[i] : 0, rr = (in && a.rsv_on) ? a.rraw[i] : 0;
   const long long sri = in ? a.sraw[i] : 0, iri = in ? a.iraw[i] : 0;
-  const int32_t z = in ? a.t.zone[i] : -1;
   const int64_t dmx = s->dev_max, tmx = s->taint_max, amx = s->aff_max;
   const int64_t rmx = (int64_t)s->rsv_max;
   const unsigned long long rp = s->rsv_pref;
   const long long smin = s->smin, smax = s->smax, imin = s->imin, imax = s->imax;
   TopoRec tr;
   const int32_t pi = topo_cur(a, tr);
-  KS_TOPO_ISSUED("v"(rs), "v"(tot0), "v"(dr), "v"(tr_), "v"(ar), "v"(rr), "v"(sri), "v"(iri), "v"(z));
+  KS_TOPO_ISSUED("v"(rs), "v"(tot0), "v"(dr), "v"(tr_), "v"(ar), "v"(rr), "v"(sri), "v"(iri));
   if (pi < 0) return;
   // the commit's pod records (wave 0 of every workgroup: the last one to finish uses them)
   PodRec p{};
@@ -278,7 +256,6 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
     qreq = tid < KS_QUOTA_DIMS ? ca.pq.req[tid][pi] : 0;
   }
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
-  const bool soft_zone = topo_soft_zone(tr);
   const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
   const int64_t pref = rp ? (int64_t)(0xFFFFFFFFull - (rp & 0xFFFFFFFFull)) : -1;
   uint64_t key = 0;
@@ -309,7 +286,7 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
     }
     long long pts = 100, ipa = 0;  // no constraint: NormalizeScore's maxScore == 0 gives MaxNodeScore
     if (dyn) {
-      const bool ig = soft_all && soft_zone && z < 0;
+      const bool ig = soft_all && !topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, i);
       if (ig) pts = 0;
       else if (smax != 0) pts = 100 * (smax + smin - sri) / smax;
       const long long diff = imax - imin;
@@ -325,6 +302,20 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   }
   const uint64_t km = wave_max_u64(key);
   if ((tid & 63) == 0 && km) atomicMax(&s->best, (unsigned long long)km);
+  // the step's per-domain scratch back to zero (read by no kernel after topo_pts_kernel): every workgroup a slice
+  if (dyn) {
+    const int64_t stride = (int64_t)gridDim.x * kTopoThreads;
+    const int64_t g = (int64_t)blockIdx.x * kTopoThreads + tid;
+    for (int t = 0; t < tr.nterms; ++t) {
+      const uint64_t w = topo_term(a, tr, t);
+      if (tp_key(w) == 0) continue;
+      for (int64_t z = g; z < a.t.ndom; z += stride) a.t.zsum[(int64_t)t * a.t.ndom + z] = 0;
+      for (int64_t k = g; k < a.t.nw; k += stride) {
+        a.t.zpres[(int64_t)t * a.t.nw + k] = 0u;
+        a.t.zsize[(int64_t)t * a.t.nw + k] = 0u;
+      }
+    }
+  }
   // the last workgroup: the commit or the one-candidate set, then the scratch back to its initial image.  The only
   // value handed between workgroups is `best`, an agent-scope atomic performed at the memory side: each wave waits
   // for its own atomic to complete before the workgroup's arrival (no L2 write-back fence: the scores and totals are
@@ -355,16 +346,13 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
     s->best_total = best_total;
     s->best_node = best_node;
   }
-  for (int k = tid; k < KS_TOPO_TERMS * KS_TOPO_ZONES; k += kTopoThreads) (&s->zsum[0][0])[k] = 0;
-  if (tid < KS_TOPO_TERMS) {
-    s->zpres[tid] = 0;
+  if (tid < kTopoTerms) {
     s->hmin[tid] = INT_MAX;
+    s->tempty[tid] = 0;
   }
   if (tid == 0) {
     s->any_all = 0;
     s->hsize = 0;
-    s->zones = 0;
-    s->empty = 0;
     s->dev_max = s->taint_max = s->aff_max = 0;
     s->imin = s->imax = 0;
     s->smin = LLONG_MAX;

@@ -230,6 +230,7 @@ class Evaluator:
         cols = nodes.ks()
         self._chk(self.L.ks_load_nodes(self.h, C.byref(cols), nodes.n))
         self.n = nodes.n
+        self.nprops = int(np.asarray(nodes.topo_count).shape[0])
 
     def update_nodes(self, idx, rows: NodeTable):
         idx = np.ascontiguousarray(idx, np.int32)
@@ -465,7 +466,7 @@ class Evaluator:
         return r
 
     def read_nodes(self) -> NodeState:
-        st = NodeState(self.n)
+        st = NodeState(self.n, getattr(self, 'nprops', 0))
         s = st.ks()
         self._chk(self.L.ks_read_nodes(self.h, C.byref(s)))
         return st

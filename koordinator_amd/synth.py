@@ -636,16 +636,23 @@ def with_static_plugins(w: Workload, seed: int = SEED + 7, weight_taint: int = 1
 
 def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node=(0, 6), n_zones: int = 8,
                    unzoned_frac: float = 0.1, spread_frac: float = 0.2, default_frac: float = 0.25,
-                   anti_frac: float = 0.08, affinity_frac: float = 0.06, pref_frac: float = 0.12):
+                   anti_frac: float = 0.08, affinity_frac: float = 0.06, pref_frac: float = 0.12,
+                   n_apps: int = 4, extra_keys=None, breadth_frac: float = 0.0, dup_frac: float = 0.0):
     """Zone labels (n_zones zones, unzoned_frac of the nodes without one), running pods (per_node) and pending pods
     for the upstream PodTopologySpread / InterPodAffinity plugins (topology_plugins): four apps in namespace
     "default" plus app-A pods in namespace "other"; pending pods with their own spread constraints (hostname / zone,
     DoNotSchedule / ScheduleAnyway, skews 1-3), the system default constraints (an owner selector), a required
     anti-affinity to app A per hostname, a required affinity to app D per zone, preferred (anti-)affinity terms;
-    running pods that carry the same terms, a few terminating.  Returns (node_labels, existing, pending)."""
+    running pods that carry the same terms, a few terminating.  Returns (node_labels, existing, pending).
+
+    Breadth (off by default): n_apps apps (one selector each), extra_keys {label key: values} further topology keys on
+    the nodes (a node misses each with probability unzoned_frac), breadth_frac of the pending pods with many terms over
+    every key (a spread constraint per key, anti-affinity / affinity / preferred terms on random keys and apps), and
+    dup_frac of the pods (running and pending) carrying one scored term twice (a required affinity term and the same
+    term preferred with weight 1, or one preferred term listed twice)."""
     from .topology_plugins import (HOSTNAME, SCHEDULE_ANYWAY, DO_NOT_SCHEDULE, ZONE, AffinityTerm, LabelSelector,
                                    SpreadConstraint, TopoPod)
-    apps = ["A", "B", "C", "D"]
+    apps = ["A", "B", "C", "D"] + [f"app{k}" for k in range(4, n_apps)]
     sel = {a: LabelSelector((("app", a),)) for a in apps}
     anti_a = AffinityTerm(HOSTNAME, sel["A"])
     aff_d = AffinityTerm(ZONE, sel["D"])
@@ -657,7 +664,26 @@ def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node
         lab = {}
         if rng.random() >= unzoned_frac:
             lab[ZONE] = f"zone-{int(rng.integers(0, n_zones))}"
+        for key, nv in (extra_keys or {}).items():
+            if rng.random() >= unzoned_frac:
+                lab[key] = f"{key}-{int(rng.integers(0, nv))}"
         node_labels.append(lab)
+    all_keys = [HOSTNAME, ZONE] + list(extra_keys or {})
+
+    def rkey():
+        return all_keys[int(rng.integers(0, len(all_keys)))]
+
+    def rsel():
+        return sel[apps[int(rng.integers(0, len(apps)))]]
+
+    def dup(p):
+        if rng.random() < 0.5:
+            t = AffinityTerm(rkey(), rsel())
+            p.affinity_required = p.affinity_required + [t]
+            p.affinity_preferred = p.affinity_preferred + [(1, t)]
+        else:
+            t = (int(rng.integers(1, 50)), AffinityTerm(rkey(), rsel()))
+            p.affinity_preferred = p.affinity_preferred + [t, t]
 
     def app_pod(ns="default"):
         a = apps[int(rng.integers(0, len(apps)))]
@@ -677,6 +703,8 @@ def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node
                 p.affinity_preferred = [pref_c]
             elif u < 0.2 and p.namespace == "default":
                 p.anti_preferred = [pref_b]
+            if dup_frac and p.namespace == "default" and rng.random() < dup_frac:
+                dup(p)
             existing.append((i, p))
     pending = []
     for i in range(n_pods):
@@ -702,6 +730,22 @@ def topology_specs(n_nodes: int, n_pods: int, rng: np.random.Generator, per_node
                     p.affinity_preferred = [pref_c]
                 else:
                     p.anti_preferred = [pref_b]
+        if breadth_frac and rng.random() < breadth_frac:
+            # many terms over every key: a spread constraint per key (no soft duplicates: one per key), required
+            # anti-affinity / affinity and preferred terms on random keys and apps
+            p.default_selector = None
+            p.spread = [SpreadConstraint(int(rng.integers(1, 5)), k,
+                                         DO_NOT_SCHEDULE if rng.random() < 0.3 else SCHEDULE_ANYWAY, rsel())
+                        for k in all_keys if rng.random() < 0.7]
+            p.anti_required = p.anti_required + [AffinityTerm(rkey(), rsel()) for _ in range(int(rng.integers(0, 3)))]
+            if rng.random() < 0.3:
+                p.affinity_required = [AffinityTerm(rkey(), LabelSelector((("tier", "web"),)))]
+            p.affinity_preferred = p.affinity_preferred + [(int(rng.integers(1, 100)), AffinityTerm(rkey(), rsel()))
+                                                           for _ in range(int(rng.integers(0, 4)))]
+            p.anti_preferred = p.anti_preferred + [(int(rng.integers(1, 100)), AffinityTerm(rkey(), rsel()))
+                                                   for _ in range(int(rng.integers(0, 3)))]
+        if dup_frac and p.namespace == "default" and rng.random() < dup_frac:
+            dup(p)
         pending.append(p)
     return node_labels, existing, pending
 
@@ -719,6 +763,7 @@ def with_topology(w: Workload, seed: int = SEED + 8, spread_weight: int = 2, aff
     node_labels, existing, pending = topology_specs(w.nodes.n, w.pods.n, rng, **kw)
     c = compile_topology(node_labels, existing, pending, namespace_labels=TOPO_NAMESPACE_LABELS)
     install(c, w.nodes, w.pods)
+    w.topo_compiled = c
     w.profile.topology = True
     w.profile.topology_spread_weight = spread_weight
     w.profile.inter_pod_affinity_weight = affinity_weight

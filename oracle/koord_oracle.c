@@ -119,8 +119,10 @@ typedef struct {
   uint32_t *numa_flags;
   uint64_t *taints_hard, *taints_soft, *labels; /* TaintToleration / NodeAffinity dictionary bits (ks_config.taint) */
   uint64_t *host_ports;                          /* NodePorts: NodeInfo.UsedPorts as host-port dictionary bits */
-  int32_t *tzone;                                /* PodTopologySpread / InterPodAffinity: zonal domain, -1 = none */
-  int32_t *tcount[KS_TOPO_PROPS];                /* ... pods with each topology property */
+  /* PodTopologySpread / InterPodAffinity: keys besides the hostname, value indices below tndom, properties */
+  int32_t tnkeys, tndom, tnprops;
+  int32_t *tdom;   /* [tnkeys][nn]: key k's value index on node i at (k - 1) * nn + i, -1 = absent */
+  int32_t *tcount; /* [tnprops][nn]: pods with property p on node i */
 } ko_nodes;
 
 typedef struct {
@@ -239,8 +241,12 @@ typedef struct {
   uint64_t req[KS_AFFINITY_TERMS], pref[KS_AFFINITY_TERMS];
   int32_t w[KS_AFFINITY_TERMS];
   uint64_t pwant, pconf; /* NodePorts: the pod's host-port bits, the bits any of them conflicts with */
-  uint32_t tprops, tflags; /* PodTopologySpread / InterPodAffinity: the pod's properties, KS_TOPO_* flags */
-  uint64_t tterm[KS_TOPO_TERMS];
+  /* PodTopologySpread / InterPodAffinity: KS_TOPO_* flags, the pod's properties and query terms (pointers into the
+   * caller's ks_pod_cols lists, valid for the call) */
+  uint32_t tflags;
+  int32_t ntprops, ntterms;
+  const int32_t *tprops;
+  const uint64_t *tterm;
 } ko_pod;
 
 /* NodeInfo values the Fit plugin reads, after the Reservation restore */
@@ -294,10 +300,20 @@ static void load_pod(const ko_sched *s, const ks_pod_cols *pc, int64_t i, ko_pod
   }
   p->pwant = pc->host_ports ? pc->host_ports[i] : 0;
   p->pconf = pc->host_ports_conflict ? pc->host_ports_conflict[i] : 0;
+  p->tflags = 0;
+  p->ntprops = p->ntterms = 0;
+  p->tprops = NULL;
+  p->tterm = NULL;
   if (s->cfg.topology.enable) {
-    p->tprops = pc->topo_props ? pc->topo_props[i] : 0;
     p->tflags = pc->topo_flags ? pc->topo_flags[i] : 0;
-    for (int t = 0; t < KS_TOPO_TERMS; t++) p->tterm[t] = pc->topo_term[t] ? pc->topo_term[t][i] : 0;
+    if (pc->topo_prop_beg && pc->topo_props) {
+      p->ntprops = pc->topo_prop_beg[i + 1] - pc->topo_prop_beg[i];
+      p->tprops = pc->topo_props + pc->topo_prop_beg[i];
+    }
+    if (pc->topo_term_beg && pc->topo_terms) {
+      p->ntterms = pc->topo_term_beg[i + 1] - pc->topo_term_beg[i];
+      p->tterm = pc->topo_terms + pc->topo_term_beg[i];
+    }
   }
 }
 
@@ -1746,8 +1762,7 @@ static void node_reserve(ko_sched *s, const ko_pod *p, int64_t n) {
   d->pod_count[n] += 1;
   if (s->cfg.nodeports.enable_filter) d->host_ports[n] |= p->pwant; /* NodeInfo.AddPod: UsedPorts */
   /* NodeInfo.AddPod: the pod counts in every topology domain of the node from now on */
-  for (int q = 0; q < KS_TOPO_PROPS; q++)
-    if ((p->tprops >> q) & 1u) d->tcount[q][n] += 1;
+  for (int q = 0; q < p->ntprops; q++) d->tcount[(size_t)p->tprops[q] * s->n + n] += 1;
   /* the freshly assigned pod has no PodMetric, so estimatedAssignedPodUsed counts
    * its estimate (load_aware.go:350-355) in every later Score on this node. */
   d->la_term_cpu[n] += p->est_cpu;
@@ -1901,8 +1916,11 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   s->nd.taints_soft = (uint64_t *)calloc(nn, 8);
   s->nd.labels = (uint64_t *)calloc(nn, 8);
   s->nd.host_ports = (uint64_t *)calloc(nn, 8);
-  s->nd.tzone = (int32_t *)calloc(nn, 4);
-  for (int q = 0; q < KS_TOPO_PROPS; q++) s->nd.tcount[q] = (int32_t *)calloc(nn, 4);
+  s->nd.tnkeys = nc->topo_nkeys > 0 ? nc->topo_nkeys : 0;
+  s->nd.tndom = nc->topo_ndomains;
+  s->nd.tnprops = nc->topo_nprops > 0 ? nc->topo_nprops : 0;
+  s->nd.tdom = (int32_t *)calloc(nn * (size_t)(s->nd.tnkeys ? s->nd.tnkeys : 1), 4);
+  s->nd.tcount = (int32_t *)calloc(nn * (size_t)(s->nd.tnprops ? s->nd.tnprops : 1), 4);
 #undef TAKE64
 #undef TAKE32
 #define CP64(dst, src) do { if (src) memcpy(s->nd.dst, src, (size_t)n * 8); } while (0)
@@ -1929,9 +1947,10 @@ ko_sched *ko_create(const ks_config *cfg, const ks_node_cols *nc, int64_t n, int
   if (nc->taints_soft) memcpy(s->nd.taints_soft, nc->taints_soft, (size_t)n * 8);
   if (nc->labels) memcpy(s->nd.labels, nc->labels, (size_t)n * 8);
   if (nc->host_ports) memcpy(s->nd.host_ports, nc->host_ports, (size_t)n * 8);
-  for (int64_t i = 0; i < n; i++) s->nd.tzone[i] = nc->topo_zone ? nc->topo_zone[i] : -1;
-  for (int q = 0; q < KS_TOPO_PROPS; q++)
-    if (nc->topo_count[q]) memcpy(s->nd.tcount[q], nc->topo_count[q], (size_t)n * 4);
+  for (int k = 0; k < s->nd.tnkeys; k++)
+    for (int64_t i = 0; i < n; i++) s->nd.tdom[(size_t)k * nn + i] = nc->topo_domain ? nc->topo_domain[(size_t)k * n + i] : -1;
+  for (int q = 0; q < s->nd.tnprops; q++)
+    if (nc->topo_count) memcpy(s->nd.tcount + (size_t)q * nn, nc->topo_count + (size_t)q * n, (size_t)n * 4);
 #undef CP64
 #undef CP32
   s->feasible = (uint8_t *)calloc(nn, 1);
@@ -1959,8 +1978,8 @@ void ko_destroy(ko_sched *s) {
   free(s->nd.taints_soft);
   free(s->nd.labels);
   free(s->nd.host_ports);
-  free(s->nd.tzone);
-  for (int q = 0; q < KS_TOPO_PROPS; q++) free(s->nd.tcount[q]);
+  free(s->nd.tdom);
+  free(s->nd.tcount);
   free(s->traw);
   free(s->araw);
   free(s->q);
@@ -2316,19 +2335,35 @@ static void rsv_normalize(ko_sched *s, int64_t *norm) {
  * satisfyPodAffinity / satisfyPodAntiAffinity / satisfyExistingPodsAntiAffinity, scoring.go processExistingPod /
  * Score / NormalizeScore) -- not on disk: parity unpinned, restated on objects by oracle/topology_ref.py -- over the
  * compiled form of koordinator_amd/topology_plugins.py (per-node property counters, per-pod query terms). */
-static int tp_kind(uint64_t w) { return (int)(w & 0xFF); }
-static int tp_prop(uint64_t w) { return (int)((w >> 8) & 0xFF); }
-static int tp_key(uint64_t w) { return (int)((w >> 16) & 0xFF); }
-static uint32_t tp_flags(uint64_t w) { return (uint32_t)((w >> 24) & 0xFF); }
+static int tp_kind(uint64_t w) { return (int)(w & 0xF); }
+static uint32_t tp_flags(uint64_t w) { return (uint32_t)((w >> 4) & 0xF); }
+static int tp_key(uint64_t w) { return (int)((w >> 8) & 0xFF); }
+static int tp_prop(uint64_t w) { return (int)((w >> 16) & 0xFFFF); }
 static int32_t tp_param(uint64_t w) { return (int32_t)(uint32_t)(w >> 32); }
 
-/* per pod: the PreFilter / PreScore domain counts */
+/* node n's value index of topology key k (key 0, the hostname: the node itself), -1 = the label is absent */
+static int64_t tp_dom(const ko_sched *s, int k, int64_t n) {
+  return k == 0 ? n : (int64_t)s->nd.tdom[(size_t)(k - 1) * (size_t)s->n + (size_t)n];
+}
+static int64_t tp_count(const ko_sched *s, uint64_t w, int64_t n) {
+  return s->nd.tcount[(size_t)tp_prop(w) * (size_t)s->n + (size_t)n];
+}
+
+/* per pod: the PreFilter / PreScore domain counts (per non-hostname term: [tndom] sums and presence) */
 typedef struct {
-  int64_t zsum[KS_TOPO_TERMS][KS_TOPO_ZONES]; /* per term: the zone's counted pods over the term's eligible nodes */
-  uint64_t zpres[KS_TOPO_TERMS];              /* hard spread: zones with an eligible node (TpPairToMatchNum keys) */
-  int64_t min[KS_TOPO_TERMS];                 /* hard spread: TpKeyToCriticalPaths[key][0].MatchNum */
-  int any_all;                                /* InterPodAffinity: len(affinityCounts) > 0 */
+  int nt, nd;
+  int64_t *zsum;   /* [nt][nd]: per term the domain's counted pods over the term's eligible nodes */
+  uint8_t *zpres;  /* [nt][nd]: hard spread: domains with an eligible node (TpPairToMatchNum keys) */
+  int64_t *min;    /* [nt]: hard spread: TpKeyToCriticalPaths[key][0].MatchNum */
+  int any_all;     /* InterPodAffinity: len(affinityCounts) > 0 */
 } ko_tctx;
+
+static void tp_ctx_free(ko_tctx *c) {
+  free(c->zsum);
+  free(c->zpres);
+  free(c->min);
+  memset(c, 0, sizeof(*c));
+}
 
 /* nodeaffinity.GetRequiredNodeAffinity(pod).Match(node): nodeSelector ANDed into each required term, OR over terms */
 static int tp_node_aff(const ko_sched *s, const ko_pod *p, int64_t n) {
@@ -2338,70 +2373,83 @@ static int tp_node_aff(const ko_sched *s, const ko_pod *p, int64_t n) {
   return 0;
 }
 
+/* nodeLabelsMatchSpreadConstraints over the pod's hard (kind KS_TOPO_K_SPREAD_HARD) or soft constraints: node n has
+ * every key they name */
+static int tp_keys_ok(const ko_sched *s, const ko_pod *p, int kind, int64_t n) {
+  for (int t = 0; t < p->ntterms; t++) {
+    const uint64_t w = p->tterm[t];
+    if (tp_kind(w) == kind && tp_key(w) != 0 && tp_dom(s, tp_key(w), n) < 0) return 0;
+  }
+  return 1;
+}
+
 /* the node counts for the term: hard spread -- calPreFilterState's nodes (required node affinity, every hard key);
  * soft spread -- PreScore's processAllNode (required node affinity, every soft key when requireAllTopologies);
  * InterPodAffinity -- every node (with the key's label) */
 static int tp_eligible(const ko_sched *s, const ko_pod *p, uint64_t w, int64_t n) {
   const int k = tp_kind(w);
-  const int zone_ok = s->nd.tzone[n] >= 0;
-  if (k == KS_TOPO_K_SPREAD_HARD) return tp_node_aff(s, p, n) && (!(tp_flags(w) & KS_TOPO_T_ELIG_ZONE) || zone_ok);
+  if (k == KS_TOPO_K_SPREAD_HARD) return tp_node_aff(s, p, n) && tp_keys_ok(s, p, KS_TOPO_K_SPREAD_HARD, n);
   if (k == KS_TOPO_K_SPREAD_SOFT)
     return tp_node_aff(s, p, n) &&
-           (!((p->tflags & KS_TOPO_SOFT_ALL_KEYS) && (tp_flags(w) & KS_TOPO_T_ELIG_ZONE)) || zone_ok);
+           (!(p->tflags & KS_TOPO_SOFT_ALL_KEYS) || tp_keys_ok(s, p, KS_TOPO_K_SPREAD_SOFT, n));
   return 1;
 }
 
 static void tp_prefilter(const ko_sched *s, const ko_pod *p, ko_tctx *c) {
   memset(c, 0, sizeof(*c));
-  int aff_host = 0;
-  for (int t = 0; t < KS_TOPO_TERMS; t++) {
-    c->min[t] = 2147483647; /* newCriticalPaths: MatchNum math.MaxInt32 */
-    if (tp_kind(p->tterm[t]) == KS_TOPO_K_AFFINITY && tp_key(p->tterm[t]) == 0) aff_host = 1;
-  }
+  c->nt = p->ntterms;
+  c->nd = s->nd.tndom > 0 ? s->nd.tndom : 1;
+  const size_t cells = (size_t)(c->nt > 0 ? c->nt : 1) * (size_t)c->nd;
+  c->zsum = (int64_t *)calloc(cells, 8);
+  c->zpres = (uint8_t *)calloc(cells, 1);
+  c->min = (int64_t *)calloc((size_t)(c->nt > 0 ? c->nt : 1), 8);
+  for (int t = 0; t < c->nt; t++) c->min[t] = 2147483647; /* newCriticalPaths: MatchNum math.MaxInt32 */
   for (int64_t n = 0; n < s->n; n++) {
-    const int32_t z = s->nd.tzone[n];
-    for (int t = 0; t < KS_TOPO_TERMS; t++) {
+    for (int t = 0; t < c->nt; t++) {
       const uint64_t w = p->tterm[t];
-      if (!w || !tp_eligible(s, p, w, n)) continue;
-      const int64_t cnt = s->nd.tcount[tp_prop(w)][n];
-      if (tp_key(w) == 1) {
-        if (z < 0) continue;
-        c->zsum[t][z] += cnt;
-        c->zpres[t] |= 1ull << z;
+      if (!tp_eligible(s, p, w, n)) continue;
+      const int64_t cnt = tp_count(s, w, n);
+      if (tp_key(w) != 0) {
+        const int64_t z = tp_dom(s, tp_key(w), n);
+        if (z >= 0) {
+          c->zsum[(size_t)t * c->nd + z] += cnt;
+          c->zpres[(size_t)t * c->nd + z] = 1;
+        }
       } else if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD && cnt < c->min[t]) {
         c->min[t] = cnt;
       }
-      if (tp_kind(w) == KS_TOPO_K_AFFINITY && cnt > 0 && (aff_host || z >= 0)) c->any_all = 1;
+      /* affinityCounts: a pod matching every required term counts on each term's (key, value) the node has */
+      if (tp_kind(w) == KS_TOPO_K_AFFINITY && cnt > 0 && (tp_key(w) == 0 || tp_dom(s, tp_key(w), n) >= 0)) c->any_all = 1;
     }
   }
-  for (int t = 0; t < KS_TOPO_TERMS; t++)
-    if (tp_kind(p->tterm[t]) == KS_TOPO_K_SPREAD_HARD && tp_key(p->tterm[t]) == 1)
-      for (int z = 0; z < KS_TOPO_ZONES; z++)
-        if (((c->zpres[t] >> z) & 1ull) && c->zsum[t][z] < c->min[t]) c->min[t] = c->zsum[t][z];
+  for (int t = 0; t < c->nt; t++)
+    if (tp_kind(p->tterm[t]) == KS_TOPO_K_SPREAD_HARD && tp_key(p->tterm[t]) != 0)
+      for (int z = 0; z < c->nd; z++)
+        if (c->zpres[(size_t)t * c->nd + z] && c->zsum[(size_t)t * c->nd + z] < c->min[t]) c->min[t] = c->zsum[(size_t)t * c->nd + z];
 }
 
 /* the term's count in the node's domain (the node has the key's label) */
 static int64_t tp_domain(const ko_sched *s, const ko_pod *p, const ko_tctx *c, int t, int64_t n) {
   const uint64_t w = p->tterm[t];
-  if (tp_key(w) == 1) return c->zsum[t][s->nd.tzone[n]];
-  return s->nd.tcount[tp_prop(w)][n];
+  if (tp_key(w) != 0) return c->zsum[(size_t)t * c->nd + tp_dom(s, tp_key(w), n)];
+  return tp_count(s, w, n);
 }
 
 /* PodTopologySpread Filter, then InterPodAffinity Filter (affinity, anti-affinity, existing pods' anti-affinity: the
  * first that fails) */
 static uint32_t tp_filter(const ko_sched *s, const ko_pod *p, const ko_tctx *c, int64_t n) {
   uint32_t r = 0;
-  const int has_zone = s->nd.tzone[n] >= 0;
-  for (int t = 0; t < KS_TOPO_TERMS; t++) {
+  for (int t = 0; t < p->ntterms; t++) {
     const uint64_t w = p->tterm[t];
     if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD) continue;
-    if (tp_key(w) == 1 && !has_zone) { /* ErrReasonNodeLabelNotMatch */
+    const int64_t z = tp_dom(s, tp_key(w), n);
+    if (z < 0) { /* ErrReasonNodeLabelNotMatch */
       r |= KS_R_TOPOLOGY_SPREAD;
       break;
     }
     int64_t match;
-    if (tp_key(w) == 1) match = ((c->zpres[t] >> s->nd.tzone[n]) & 1ull) ? c->zsum[t][s->nd.tzone[n]] : 0;
-    else match = tp_eligible(s, p, w, n) ? s->nd.tcount[tp_prop(w)][n] : 0;
+    if (tp_key(w) != 0) match = c->zpres[(size_t)t * c->nd + z] ? c->zsum[(size_t)t * c->nd + z] : 0;
+    else match = tp_eligible(s, p, w, n) ? tp_count(s, w, n) : 0;
     const int64_t self = (tp_flags(w) & KS_TOPO_T_SELF) ? 1 : 0;
     if (match + self - c->min[t] > tp_param(w)) { /* ErrReasonConstraintsNotMatch */
       r |= KS_R_TOPOLOGY_SPREAD;
@@ -2409,23 +2457,23 @@ static uint32_t tp_filter(const ko_sched *s, const ko_pod *p, const ko_tctx *c, 
     }
   }
   int aff_terms = 0, missing = 0, exist = 1;
-  for (int t = 0; t < KS_TOPO_TERMS; t++) {
+  for (int t = 0; t < p->ntterms; t++) {
     const uint64_t w = p->tterm[t];
     if (tp_kind(w) != KS_TOPO_K_AFFINITY) continue;
     aff_terms = 1;
-    if (tp_key(w) == 1 && !has_zone) missing = 1;
+    if (tp_dom(s, tp_key(w), n) < 0) missing = 1;
     else if (tp_domain(s, p, c, t, n) <= 0) exist = 0;
   }
   if (aff_terms && (missing || (!exist && !(!c->any_all && (p->tflags & KS_TOPO_SELF_AFFINITY)))))
     return r | KS_R_POD_AFFINITY;
-  for (int t = 0; t < KS_TOPO_TERMS; t++) {
+  for (int t = 0; t < p->ntterms; t++) {
     const uint64_t w = p->tterm[t];
-    if (tp_kind(w) == KS_TOPO_K_ANTI && (tp_key(w) == 0 || has_zone) && tp_domain(s, p, c, t, n) > 0)
+    if (tp_kind(w) == KS_TOPO_K_ANTI && tp_dom(s, tp_key(w), n) >= 0 && tp_domain(s, p, c, t, n) > 0)
       return r | KS_R_POD_ANTI_AFFINITY;
   }
-  for (int t = 0; t < KS_TOPO_TERMS; t++) {
+  for (int t = 0; t < p->ntterms; t++) {
     const uint64_t w = p->tterm[t];
-    if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && (tp_key(w) == 0 || has_zone) && tp_domain(s, p, c, t, n) > 0)
+    if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && tp_dom(s, tp_key(w), n) >= 0 && tp_domain(s, p, c, t, n) > 0)
       return r | KS_R_EXISTING_ANTI_AFFINITY;
   }
   return r;
@@ -2433,6 +2481,7 @@ static uint32_t tp_filter(const ko_sched *s, const ko_pod *p, const ko_tctx *c, 
 
 /* the filter pass over the nodes the other plugins left feasible (total >= 0) */
 static void tp_filter_all(ko_sched *s, const ko_pod *p, ko_tctx *c, uint32_t *reasons) {
+  memset(c, 0, sizeof(*c));
   if (!s->cfg.topology.enable || !(p->tflags & KS_TOPO_DYN)) return;
   tp_prefilter(s, p, c);
   for (int64_t n = 0; n < s->n; n++) {
@@ -2456,41 +2505,49 @@ static void tp_normalize(ko_sched *s, const ko_pod *p, const ko_tctx *c, int64_t
     }
     return;
   }
-  int soft_zone = 0, soft_all = 0;
-  for (int t = 0; t < KS_TOPO_TERMS; t++)
-    if (tp_kind(p->tterm[t]) == KS_TOPO_K_SPREAD_SOFT) {
-      if (tp_flags(p->tterm[t]) & KS_TOPO_T_ELIG_ZONE) soft_zone = 1;
-      soft_all = (p->tflags & KS_TOPO_SOFT_ALL_KEYS) != 0;
-    }
-  /* initPreScoreState: ignored nodes (requireAllTopologies and a soft key missing), the topology sizes */
+  const int soft_all = (p->tflags & KS_TOPO_SOFT_ALL_KEYS) != 0;
+  const size_t nn = (size_t)(s->n > 0 ? s->n : 1);
+  uint8_t *ign = (uint8_t *)calloc(nn, 1);
+  /* initPreScoreState: ignored nodes (requireAllTopologies and a soft key missing), the topology sizes per soft
+   * constraint (hostname: the non-ignored feasible nodes; another key: its distinct values there, "" for a node
+   * without the label) */
   int64_t hsize = 0;
-  uint64_t zones = 0;
-  int empty_zone = 0;
+  const int nt = p->ntterms, nd = c->nd > 0 ? c->nd : 1;
+  uint8_t *seen = (uint8_t *)calloc((size_t)(nt > 0 ? nt : 1) * (size_t)(nd + 1), 1);
+  int64_t *tsize = (int64_t *)calloc((size_t)(nt > 0 ? nt : 1), 8);
   for (int64_t n = 0; n < s->n; n++) {
     if (s->total[n] < 0) continue;
-    if (soft_all && soft_zone && s->nd.tzone[n] < 0) continue;
+    ign[n] = soft_all && !tp_keys_ok(s, p, KS_TOPO_K_SPREAD_SOFT, n);
+    if (ign[n]) continue;
     hsize++;
-    if (s->nd.tzone[n] >= 0) zones |= 1ull << s->nd.tzone[n];
-    else empty_zone = 1; /* the pair (zone, "") of a node without the label */
+    for (int t = 0; t < nt; t++) {
+      const uint64_t w = p->tterm[t];
+      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) continue;
+      const int64_t z = tp_dom(s, tp_key(w), n);
+      uint8_t *b = seen + (size_t)t * (size_t)(nd + 1) + (size_t)(z < 0 ? nd : z);
+      if (!*b) {
+        *b = 1;
+        tsize[t]++;
+      }
+    }
   }
-  const int64_t zsize = __builtin_popcountll(zones) + empty_zone;
   int64_t smin = INT64_MAX, smax = 0, imin = 0, imax = 0;
-  int64_t *sraw = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
-  int64_t *iraw = (int64_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 8);
+  int64_t *sraw = (int64_t *)calloc(nn, 8);
+  int64_t *iraw = (int64_t *)calloc(nn, 8);
   for (int64_t n = 0; n < s->n; n++) {
     if (s->total[n] < 0) continue;
-    const int has_zone = s->nd.tzone[n] >= 0;
-    const int ignored = soft_all && soft_zone && !has_zone;
+    const int ignored = ign[n];
     double score = 0.0;
     int64_t ir = 0;
-    for (int t = 0; t < KS_TOPO_TERMS; t++) {
+    for (int t = 0; t < nt; t++) {
       const uint64_t w = p->tterm[t];
       const int k = tp_kind(w);
-      if (k == KS_TOPO_K_SPREAD_SOFT && !ignored && (tp_key(w) == 0 || has_zone)) {
+      const int has = tp_dom(s, tp_key(w), n) >= 0;
+      if (k == KS_TOPO_K_SPREAD_SOFT && !ignored && has) {
         const int64_t cnt = tp_domain(s, p, c, t, n);
-        const double tw = log((double)((tp_key(w) == 1 ? zsize : hsize) + 2)); /* topologyNormalizingWeight */
-        score += (double)cnt * tw + (double)(tp_param(w) - 1);                  /* scoreForCount */
-      } else if (k == KS_TOPO_K_SCORE && (tp_key(w) == 0 || has_zone)) {
+        const double tw = log((double)((tp_key(w) != 0 ? tsize[t] : hsize) + 2)); /* topologyNormalizingWeight */
+        score += (double)cnt * tw + (double)(tp_param(w) - 1);                   /* scoreForCount */
+      } else if (k == KS_TOPO_K_SCORE && has) {
         ir += (int64_t)tp_param(w) * tp_domain(s, p, c, t, n);
       }
     }
@@ -2509,9 +2566,8 @@ static void tp_normalize(ko_sched *s, const ko_pod *p, const ko_tctx *c, int64_t
       if (inorm) inorm[n] = 0;
       continue;
     }
-    const int ignored = soft_all && soft_zone && s->nd.tzone[n] < 0;
     int64_t sn;
-    if (ignored) sn = 0;
+    if (ign[n]) sn = 0;
     else if (smax == 0) sn = MAX_NODE_SCORE;
     else sn = MAX_NODE_SCORE * (smax + smin - sraw[n]) / smax;
     const int64_t diff = imax - imin;
@@ -2523,6 +2579,9 @@ static void tp_normalize(ko_sched *s, const ko_pod *p, const ko_tctx *c, int64_t
   }
   free(sraw);
   free(iraw);
+  free(ign);
+  free(seen);
+  free(tsize);
 }
 
 /* NodeNUMAResource Reserve for a cpu-bind pod (plugin.go:376-429): resourceManager.Allocate ->
@@ -2711,6 +2770,7 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
     static_normalize(s, NULL, NULL);
     rsv_normalize(s, NULL);
     tp_normalize(s, &p, &tc, NULL, NULL);
+    tp_ctx_free(&tc);
     /* prioritizeNodes sum + selectHost: max score, lowest index on ties */
     int64_t best = -1, best_n = -1;
     for (int64_t n = 0; n < s->n; n++) {
@@ -2838,8 +2898,7 @@ int ko_unreserve(ko_sched *s, const ks_pod_cols *pc, const ks_result *r, const u
   d->nz_mem[n] -= p.nzmem;
   d->pod_count[n] -= 1;
   if (s->cfg.nodeports.enable_filter) d->host_ports[n] &= ~p.pwant;
-  for (int q = 0; q < KS_TOPO_PROPS; q++)
-    if ((p.tprops >> q) & 1u) d->tcount[q][n] -= 1;
+  for (int q = 0; q < p.ntprops; q++) d->tcount[(size_t)p.tprops[q] * s->n + n] -= 1;
   d->la_term_cpu[n] -= p.est_cpu;
   d->la_term_mem[n] -= p.est_mem;
   if (p.flags & KS_POD_PROD) {
@@ -2921,6 +2980,7 @@ int ko_eval_pod(ko_sched *s, const ks_pod_cols *pc, uint32_t *reasons, int64_t *
   static_normalize(s, tnorm, anorm);
   rsv_normalize(s, norm);
   tp_normalize(s, &p, &tc, snorm, inorm);
+  tp_ctx_free(&tc);
   for (int64_t n = 0; n < s->n; n++) {
     if (scores && s->cfg.reservation.enable) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_RESERVATION] = norm[n];
     if (scores) scores[n * KS_NUM_SCORE_PLUGINS + KS_SCORE_DEVICESHARE] = s->cfg.deviceshare.enable ? dnorm[n] : 0;
@@ -2969,8 +3029,8 @@ int ko_read_nodes(const ko_sched *s, ks_node_state *o) {
   if (o->la_prod_term_milli_cpu) memcpy(o->la_prod_term_milli_cpu, s->nd.la_pterm_cpu, b8);
   if (o->la_prod_term_memory) memcpy(o->la_prod_term_memory, s->nd.la_pterm_mem, b8);
   if (o->host_ports) memcpy(o->host_ports, s->nd.host_ports, b8);
-  for (int q = 0; q < KS_TOPO_PROPS; q++)
-    if (o->topo_count[q]) memcpy(o->topo_count[q], s->nd.tcount[q], b4);
+  for (int q = 0; o->topo_count && q < s->nd.tnprops; q++)
+    memcpy(o->topo_count + (size_t)q * s->n, s->nd.tcount + (size_t)q * s->n, b4);
   return 0;
 }
 

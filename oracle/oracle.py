@@ -155,6 +155,7 @@ class Oracle:
         self.L = lib()
         self.cfg = cfg
         self.n = nodes.n
+        self.nprops = int(np.asarray(nodes.topo_count).shape[0])
         self._cols = nodes.ks()
         self.h = self.L.ko_create(C.byref(cfg), C.byref(self._cols), nodes.n, int(nthreads))
         self.nq = 0
@@ -245,7 +246,7 @@ class Oracle:
         return lists.value, [(int(masks[i]), bool(prefs[i])) for i in range(nh.value)]
 
     def read_nodes(self) -> NodeState:
-        st = NodeState(self.n)
+        st = NodeState(self.n, getattr(self, 'nprops', 0))
         s = st.ks()
         self.L.ko_read_nodes(self.h, C.byref(s))
         return st

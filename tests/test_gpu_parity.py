@@ -127,6 +127,31 @@ def test_stress_filters_and_quota_chain(runtime, oracle_lib):
         check_run(runtime, oracle_lib, prof, nodes, pods, quotas, "stress")
 
 
+@pytest.mark.parametrize("batch", [64, 33, 8])
+def test_quota_admission_edges(runtime, oracle_lib, batch):
+    """ElasticQuota admission inside a pass (flat quotas): few quotas whose limits are crossed inside a pass, tight
+    non-preemptible mins, pods that pass the quota but fit no node (their requests never reach used), negative and
+    out-of-mask request words, pods without a quota."""
+    rng = np.random.Generator(np.random.PCG64(31 + batch))
+    nodes = stress_nodes(700, rng)
+    pods = stress_pods(1500, rng, n_quotas=3)
+    pods.req_milli_cpu[::11] = 10 ** 9  # admitted or not, never placed
+    pods.quota_req[0][::11] = pods.req_milli_cpu[::11] // 1000
+    pods.quota_req[5][::13] = -7  # a request word outside every quota's mask / a negative one
+    pods.quota_mask[::13] |= np.uint32(1 << 5)
+    pods.flags[rng.random(pods.n) < 0.3] |= abi.KS_POD_NONPREEMPTIBLE
+    quotas = synth.make_quotas(pods, 3, rng, admit_frac=0.35)
+    quotas.limit_mask[:] |= np.uint32(1 << 5)
+    quotas.limit[5][:] = 1 << 40
+    quotas.min_mask[:] = quotas.limit_mask
+    quotas.min[:, :] = quotas.limit // 3
+    got, _ = check_run(runtime, oracle_lib, profile(quota=True, batch_pods=batch), nodes, pods, quotas, f"cert-b{batch}")
+    st = got["status"]
+    assert ((st & abi.KS_S_QUOTA) != 0).sum() > 100
+    assert (st == abi.KS_S_QUOTA_NONPREEMPTIBLE).sum() > 0
+    assert (st == 0).sum() > 100
+
+
 def test_unschedulable_and_tiny_clusters(runtime, oracle_lib):
     rng = np.random.Generator(np.random.PCG64(14))
     for n in (1, 63, 64, 65, 130):

@@ -106,24 +106,18 @@ def test_c3_with_topology(runtime, oracle_lib):
     run(runtime, oracle_lib, w, "c3+topology")
 
 
-def test_c3_topology_queue_head_on_reused_memory(runtime, oracle_lib):
+def test_c3_topology_queue_head_on_poisoned_lists(runtime, oracle_lib, monkeypatch):
     """A new context whose queue starts with more topology pods than one pass's topology steps take (C3: reserve_pre_kernel
-    runs ahead of every regular pass's commit), created on device memory that held other data: the regular pass that
-    meets a topology pod at the cursor has no candidate lists (its sweep and select return at once), and the Reserve
-    pre-pass must not read the lists' memory as nodes.  The released block is filled with large positive words first,
-    so a read of never-written lists would address far outside the cluster."""
-    import ctypes as C
-
-    hip = C.CDLL("libamdhip64.so")  # (the HIP runtime the library runs on)
-    junk = C.c_void_p()
-    size = C.c_size_t(384 << 20)
-    assert hip.hipMalloc(C.byref(junk), size) == 0
-    assert hip.hipMemset(junk, 0x3F, size) == 0 and hip.hipDeviceSynchronize() == 0
-    assert hip.hipFree(junk) == 0
+    runs ahead of every regular pass's commit): the regular pass that meets a topology pod at the cursor has no candidate
+    lists (its sweep and select return at once), and the Reserve pre-pass must not read the lists' memory as nodes.
+    KS_TEST_POISON_LISTS=1 makes ks_create fill the lists with large words instead of zeros, so the condition is forced
+    rather than left to the allocator; the pre-pass stops where the commit stops (topo_pass_pods) and drops any list
+    entry outside the cluster."""
+    monkeypatch.setenv("KS_TEST_POISON_LISTS", "1")
     w = synth.with_topology(synth.c3(n_nodes=800, n_pods=1600), seed=46)
     dyn = (w.pods.topo_flags & abi.KS_TOPO_DYN) != 0
     assert dyn[:9].all()  # the queue's head: more topology pods in a row than the 8 topology steps of a pass
-    run(runtime, oracle_lib, w, "c3+topology, reused memory")
+    run(runtime, oracle_lib, w, "c3+topology, poisoned lists")
 
 
 def test_assume_unreserve_counters(runtime, oracle_lib):
@@ -178,10 +172,19 @@ def test_refusals(runtime):
     w = topo_only(64, 8, 49)
     ev = runtime.Evaluator(w.cfg, w.nodes.copy())
     try:
-        bad = w.pods.rows([0])
-        bad.topo_term[0, 0] = np.uint64(7)  # kind 7: no such term
+        for mutate in (lambda t: t.__setitem__(0, np.uint64(7)),                   # kind 7: no such term
+                       lambda t: t.__setitem__(0, t[0] | np.uint64(0xFFFF << 16)),  # property 65535: not loaded
+                       lambda t: t.__setitem__(0, t[0] | np.uint64(0xF0 << 8))):    # key 240: not loaded
+            bad = w.pods.rows([0])
+            assert len(bad.topo_terms) > 0
+            mutate(bad.topo_terms)
+            with pytest.raises(runtime.KsError) as e:
+                ev.schedule(bad)
+            assert e.value.rc == abi.KS_EINVAL
+        many = w.pods.rows([0])
+        many.set_topo([[]], [[int(many.topo_terms[0])] * (abi.KS_TOPO_MAX_TERMS + 1)])
         with pytest.raises(runtime.KsError) as e:
-            ev.schedule(bad)
+            ev.schedule(many)
         assert e.value.rc == abi.KS_EINVAL
     finally:
         ev.close()
@@ -211,6 +214,7 @@ def test_graph_and_direct_launches_agree(runtime, oracle_lib):
     ("no zone labels", dict(unzoned_frac=1.0)),
     ("one zone", dict(n_zones=1, unzoned_frac=0.0)),
     ("64 zones", dict(n_zones=64, unzoned_frac=0.02)),
+    ("1000 zones", dict(n_zones=1000, unzoned_frac=0.02)),
     ("empty cluster", dict(per_node=(0, 0))),
     ("anti-affinity heavy", dict(anti_frac=0.6, per_node=(0, 1))),
     ("system defaults only", dict(default_frac=1.0, spread_frac=0.0, anti_frac=0.0, affinity_frac=0.0, pref_frac=0.0)),
@@ -218,8 +222,70 @@ def test_graph_and_direct_launches_agree(runtime, oracle_lib):
 ])
 def test_edge_shapes(runtime, oracle_lib, label, kw):
     """the domain's edge shapes: nodes without the zonal key (every zonal constraint fails / is ignored), a single
-    domain, the 64-zone maximum, no placed pods, saturating anti-affinity, only the system default constraints, mostly
+    domain, 64 and 1000 values of a key (a wave's nodes in many domains), no placed pods, saturating anti-affinity, only the system default constraints, mostly
     DoNotSchedule constraints -- placements, counters and node state equal the oracle's"""
     w = topo_only(300, 400, 60 + len(label), **kw)
     got, st = run(runtime, oracle_lib, w, label)
     assert got["status"].shape[0] == 400
+
+
+# breadth: 240 apps (one selector each), region and rack keys besides the hostname and the zone, pods with many terms
+# over every key, pods carrying one scored term twice (DESIGN.md §2.13)
+BREADTH = dict(n_apps=240, extra_keys={"topology.kubernetes.io/region": 3, "example.com/rack": 40}, breadth_frac=0.3,
+               dup_frac=0.1)
+
+
+def test_breadth_eval_pod(runtime, oracle_lib):
+    w = topo_only(900, 200, 71, **BREADTH)
+    c = w.topo_compiled
+    assert len(c.keys) == 4 and len(c.props) > 200 and max(len(t) for t in c.pod_terms) > 8
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy())
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy())
+    try:
+        for i in range(w.pods.n):
+            one = w.pods.rows([i])
+            r_g, s_g, t_g = ev.eval_pod(one)
+            r_o, s_o, t_o = orc.eval_pod(one)
+            assert np.array_equal(r_g, r_o), f"pod {i}: reasons at nodes {np.nonzero(r_g != r_o)[0][:5]}"
+            assert np.array_equal(s_g, s_o), f"pod {i}: scores at {np.argwhere(s_g != s_o)[:5].tolist()}"
+            assert np.array_equal(t_g, t_o), f"pod {i}: totals"
+    finally:
+        ev.close()
+        orc.close()
+
+
+@pytest.mark.parametrize("seed", [72, 73])
+def test_breadth_queue(runtime, oracle_lib, seed):
+    w = topo_only(1200, 2500, seed, **BREADTH)
+    got, _ = run(runtime, oracle_lib, w, f"breadth seed {seed}")
+    assert (got["status"] == abi.KS_S_SCHEDULED).sum() > 500
+
+
+def test_breadth_c2_default(runtime, oracle_lib):
+    """the complete v1beta2 default profile (C2 shape) at breadth"""
+    w = synth.with_topology(synth.c2_default(n_nodes=1500, n_pods=3000), seed=74, **BREADTH)
+    run(runtime, oracle_lib, w, "c2-default breadth")
+
+
+@pytest.mark.parametrize("nranks,vshards", [(2, 1), (2, 2)])
+def test_sharded_topology(runtime, oracle_lib, nranks, vshards):
+    """node sharding with topology pods: every rank runs the topology steps over the whole (replicated) node table, the
+    regular passes are sharded and merged (the loopback transport of tests/test_gpu_shard_loopback.py)"""
+    w = synth.with_topology(synth.c2_default(n_nodes=1000, n_pods=1500), seed=75, **BREADTH)
+    cfg = w.cfg
+    tables = w.tables()
+    evs = [runtime.Evaluator(cfg, w.nodes.copy(), **{k: v.copy() for k, v in tables.items()}) for _ in range(nranks)]
+    try:
+        runtime.shard_loopback(evs, vshards)
+        outs = runtime.run_ranks(lambda ev: {"got": ev.schedule(w.pods), "state": ev.read_nodes()}, evs)
+    finally:
+        for ev in evs:
+            ev.close()
+    orc = oracle_lib.Oracle(cfg, w.nodes.copy(), nthreads=8, **tables)
+    want = orc.schedule(w.pods)
+    try:
+        for r, o in enumerate(outs):
+            assert_same_results(o["got"], want, f"rank {r}")
+            assert_same_state(o["state"], orc.read_nodes(), f"rank {r}")
+    finally:
+        orc.close()

@@ -17,7 +17,8 @@ from koordinator_amd import abi, synth
 from koordinator_amd.config import SchedulerProfile
 from koordinator_amd.static_plugins import StaticPluginError
 from koordinator_amd.topology_plugins import (DO_NOT_SCHEDULE, HOSTNAME, KIND, SCHEDULE_ANYWAY, ZONE, AffinityTerm,
-                                              LabelSelector, SpreadConstraint, TopoPod, compile_topology, install)
+                                              LabelSelector, SpreadConstraint, TopoPod, compile_topology, install,
+                                              unpack_term)
 from oracle import topology_ref as ref
 from oracle.oracle import Oracle
 
@@ -92,28 +93,48 @@ def test_compile_hand_cases():
         TopoPod(namespace="x", labels={"app": "a"}),                         # other namespace: does not
     ]
     c = compile_topology(nodes, existing, pending)
-    assert list(c.node_zone) == [0, 0, 1, -1]
-    kinds = [[int(c.pod_terms[t, i]) & 0xFF for t in range(abi.KS_TOPO_TERMS) if c.pod_terms[t, i]]
-             for i in range(len(pending))]
+    assert c.keys[0] == HOSTNAME and list(c.node_domain[c.keys.index(ZONE) - 1]) == [0, 0, 1, -1]
+    kinds = [[unpack_term(w)[0] for w in c.pod_terms[i]] for i in range(len(pending))]
     # (pod 0 is app=a in namespace default too: the running pod's anti-affinity term applies to it)
     assert kinds[0] == [KIND["spread_hard"], KIND["existing_anti"]] and kinds[1] == [] and kinds[2] == [KIND["spread_soft"]] * 2
     assert kinds[3] == [KIND["existing_anti"]] and kinds[4] == []
     assert [bool(f & abi.KS_TOPO_DYN) for f in c.pod_flags] == [True, False, True, True, False]
     # the selector property of pod 0 counts app=a pods of namespace default that are not terminating
-    p0 = (int(c.pod_terms[0, 0]) >> 8) & 0xFF
+    k0, p0, key0, param0, fl0 = unpack_term(c.pod_terms[0][0])
     assert list(c.node_count[p0, :4]) == [1, 0, 1, 0]
-    assert (int(c.pod_terms[0, 0]) >> 24) & abi.KS_TOPO_T_SELF and (int(c.pod_terms[0, 0]) >> 32) == 1
+    assert fl0 & abi.KS_TOPO_T_SELF and param0 == 1 and c.keys[key0] == ZONE
     # the carried anti-affinity term: one pod on node 2; pod 3 and pod 0 (app=a, default) have it as a property
-    pa = (int(c.pod_terms[0, 3]) >> 8) & 0xFF
+    pa = unpack_term(c.pod_terms[3][0])[1]
     assert list(c.node_count[pa, :4]) == [0, 0, 1, 0]
-    assert (int(c.pod_props[3]) >> pa) & 1 == 0  # pod 3 does not carry the term itself
-    with pytest.raises(StaticPluginError):
-        compile_topology(nodes, [], [TopoPod(spread=[SpreadConstraint(1, "rack", DO_NOT_SCHEDULE, sel_a)])])
-    many = [TopoPod(labels={"app": str(k)}, spread=[SpreadConstraint(1, HOSTNAME, DO_NOT_SCHEDULE,
-                                                                      LabelSelector((("app", str(k)),)))])
-            for k in range(abi.KS_TOPO_PROPS + 1)]
+    assert pa not in c.pod_props[3]  # pod 3 does not carry the term itself
+    # any other node label is a topology key of its own
+    c2 = compile_topology(nodes + [{"rack": "r1"}], [], [TopoPod(spread=[SpreadConstraint(1, "rack", DO_NOT_SCHEDULE, sel_a)])])
+    assert c2.keys == [HOSTNAME, "rack"] and list(c2.node_domain[0]) == [-1, -1, -1, -1, 0]
+    many = [TopoPod(labels={"app": "x"}, anti_preferred=[(1 + k, AffinityTerm(HOSTNAME, LabelSelector((("app", str(k)),))))
+                                                         for k in range(abi.KS_TOPO_MAX_TERMS + 1)])]
     with pytest.raises(StaticPluginError):
         compile_topology(nodes, [], many)
+
+
+def test_compile_duplicate_scored_terms():
+    """a running pod carrying the same scored term twice (a required affinity term and the same term preferred with
+    weight 1; one preferred term listed twice) counts it with the summed weight: one carry property of weight 2 / 2w"""
+    sel_a = LabelSelector((("app", "a"),))
+    t = AffinityTerm(HOSTNAME, sel_a)
+    nodes = [{ZONE: "z1"}, {ZONE: "z1"}]
+    existing = [(0, TopoPod(labels={"app": "b"}, affinity_required=[t], affinity_preferred=[(1, t)])),
+                (1, TopoPod(labels={"app": "b"}, affinity_preferred=[(7, t), (7, t)]))]
+    pending = [TopoPod(labels={"app": "a"})]
+    c = compile_topology(nodes, existing, pending)
+    params = sorted(unpack_term(w)[3] for w in c.pod_terms[0] if unpack_term(w)[0] == KIND["score"])
+    assert params == [2, 14]
+    _, _, _, inn, _ = ref.evaluate(pending[0], nodes, existing, [True, True])
+    w = synth.c1(n_nodes=2, n_pods=1)
+    install(c, w.nodes, w.pods)
+    orc = Oracle(_profile().to_ks_config(), w.nodes.copy())
+    _, s, _ = orc.eval_pod(w.pods.rows([0]))
+    orc.close()
+    assert list(s[:, abi.KS_SCORE_POD_AFFINITY]) == inn == [14, 100]
 
 
 def test_hand_worked_spread_and_affinity():
@@ -221,6 +242,7 @@ EDGE_SHAPES = [
     ("no zone labels", dict(unzoned_frac=1.0)),
     ("one zone", dict(n_zones=1, unzoned_frac=0.0)),
     ("64 zones", dict(n_zones=64, unzoned_frac=0.02)),
+    ("200 zones", dict(n_zones=200, unzoned_frac=0.02)),
     ("empty cluster", dict(per_node=(0, 0))),
     ("anti-affinity heavy", dict(anti_frac=0.6, per_node=(0, 1))),
     ("system defaults only", dict(default_frac=1.0, spread_frac=0.0, anti_frac=0.0, affinity_frac=0.0, pref_frac=0.0)),
@@ -233,3 +255,44 @@ def test_oracle_against_restatement_edge_shapes(label, kw):
     shapes tests/test_gpu_topology.py::test_edge_shapes runs on the device)"""
     w = _workload(60, 24, 70 + len(label), **kw)
     _check_eval(w, _profile(), range(w.pods.n))
+
+
+BREADTH = dict(n_apps=240, extra_keys={"topology.kubernetes.io/region": 3, "example.com/rack": 40}, breadth_frac=0.3,
+               dup_frac=0.1)
+
+
+def test_breadth_compiles_wide():
+    """>= 200 distinct selectors, two keys besides the hostname and the zone, pods with more than 8 terms"""
+    w = _workload(300, 400, 91, **BREADTH)
+    node_labels, existing, pending = w.topo
+    c = compile_topology(node_labels, existing, pending, namespace_labels=synth.TOPO_NAMESPACE_LABELS)
+    assert len(c.keys) == 4
+    assert len({p[2] for p in c.props if p[0] == "sel"} | {p[2] for p in c.props if p[0] == "term"}) >= 200
+    assert max(len(t) for t in c.pod_terms) > 8
+
+
+@pytest.mark.parametrize("seed", [92, 93])
+def test_oracle_against_restatement_breadth(seed):
+    w = _workload(80, 90, seed, **BREADTH)
+    _check_eval(w, _profile(), range(w.pods.n))
+
+
+def test_schedule_against_restatement_breadth():
+    w = _workload(16, 120, 94, per_node=(0, 2), **BREADTH)
+    node_labels, existing, pending = w.topo
+    existing = list(existing)
+    orc = Oracle(_profile().to_ks_config(), w.nodes.copy())
+    got = orc.schedule(w.pods)
+    st = orc.read_nodes()
+    orc.close()
+    for i, p in enumerate(pending):
+        _, _, _, _, add = ref.evaluate(p, node_labels, existing, [True] * len(node_labels),
+                                       ns_labels=synth.TOPO_NAMESPACE_LABELS)
+        totals = [a if a is not None else -1 for a in add]
+        best = max(totals)
+        want = totals.index(best) if best >= 0 else -1
+        assert int(got["node"][i]) == want, f"pod {i}"
+        if want >= 0:
+            existing.append((want, p))
+    c = compile_topology(node_labels, existing, pending, namespace_labels=synth.TOPO_NAMESPACE_LABELS)
+    assert np.array_equal(st.topo_count, c.node_count)
