@@ -3307,12 +3307,7 @@ static int validate_pods(ks_ctx* ctx, const ks_pod_cols* pc, int32_t p) {
     for (int32_t i = 0; i < p; ++i) {
       const uint8_t j = pc->joint[i];
       if (j > KS_JOINT_GPU_RDMA_SAME_PCIE) KS_FAIL(ctx, KS_EINVAL, "pod %d: joint %u invalid", i, (unsigned)j);
-      const bool gpu = (pc->gpu_core && pc->gpu_core[i]) || (pc->gpu_memory && pc->gpu_memory[i]) ||
-                       (pc->gpu_memory_ratio && pc->gpu_memory_ratio[i]);
-      // jointAllocate without an RDMA request allocates an RDMA device with a nil request
-      // (device_allocator.go:308-330): not modelled
-      if (j && gpu && !(pc->rdma && pc->rdma[i] > 0))
-        KS_FAIL(ctx, KS_EUNSUPPORTED, "pod %d: joint [gpu, rdma] allocation without an rdma request", i);
+      // (without an RDMA request jointAllocate still takes RDMA devices, with a nil request: ks_dev.h dev_eval)
     }
   }
   if (pc->rsv_class) {

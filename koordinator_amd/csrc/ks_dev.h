@@ -218,9 +218,11 @@ __device__ __forceinline__ bool dev_joint(const DevType& G, const DevType& R, co
   return true;
 }
 
-// tryJointAllocate -> allocateByTopology with DeviceTypes [gpu, rdma] (device_allocator.go:188-253)
+// tryJointAllocate -> allocateByTopology with DeviceTypes [gpu, rdma] (device_allocator.go:188-253).  rpref: the pod
+// requests RDMA -- only then is a switch or a NUMA-node group `preferred` (newDeviceTopologyGuide splits the free devices
+// per requested type, numa_topology.go:109-135; a joint pod without an RDMA request has no RDMA entry there)
 __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType& R, const GpuReq& g, bool same,
-                                                uint64_t meta, uint32_t& om, uint32_t& orm) {
+                                                uint64_t meta, uint32_t& om, uint32_t& orm, bool rpref = true) {
   uint32_t exist = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -231,7 +233,7 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
   uint32_t swpref = 0;
 #pragma unroll
   for (int p = 0; p < kPcie; ++p)
-    if (((exist >> p) & 1u) && (R.fit & dev_sub_of(R, kRdma, 1u << p))) swpref |= 1u << p;
+    if (rpref && ((exist >> p) & 1u) && (R.fit & dev_sub_of(R, kRdma, 1u << p))) swpref |= 1u << p;
   // freeNodeDevicesInPCIe: preferred switches first (a switch without a fitting RDMA fails jointAllocate)
   for (int p = 0; p < kPcie; ++p) {
     if (!((swpref >> p) & 1u)) continue;
@@ -252,7 +254,7 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
     uint32_t sw = 0;
     for (int q = p; q < kPcie; ++q)
       if (((exist >> q) & 1u) && ((uint32_t)(meta >> (8 * q)) & 0xFu) == node) sw |= 1u << q;
-    const bool pr = (R.fit & dev_sub_of(R, kRdma, sw)) != 0;
+    const bool pr = rpref && (R.fit & dev_sub_of(R, kRdma, sw)) != 0;
     gsw[ng] = sw;
     gkey[ng] = ((uint32_t)__builtin_popcount(sw & swpref) << 8) | (pr ? 16u : 0u) | (15u - node);
     ++ng;
@@ -306,9 +308,12 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   if (req_out) *req_out = g;
   if (o.reasons) return o;
   const bool has_gpu = (p.flags & kPodGpuReq) != 0, has_rdma = p.rdma > 0;
-  const bool joint = has_gpu && has_rdma && p.joint != KS_JOINT_NONE;
+  // jointAllocate's secondary type without an RDMA request (device_allocator.go:308-330): allocateDevices with a nil
+  // request per instance -- every RDMA device with non-zero free fits, none is used up, none scores the node
+  const bool jr = has_gpu && !has_rdma && p.joint != KS_JOINT_NONE;
+  const bool joint = has_gpu && (has_rdma || jr) && p.joint != KS_JOINT_NONE;
   const bool same = p.joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
-  // A best-effort joint pod asking for one RDMA device is feasible iff the per-type counts are: a joint
+  // A best-effort joint pod asking for one RDMA device (or none) is feasible iff the per-type counts are: a joint
   // success takes >= desired GPUs and one RDMA device, a joint failure falls back to allocateDevices.  Only
   // the allocation itself (Reserve) needs the walk then.
   const bool walk = joint && (ALLOC || same || g.rdesired > 1);
@@ -343,7 +348,7 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
     }
     raw += dev_score3(c, tsum, fsum, pod);
   }
-  if (has_rdma) {
+  if (has_rdma || (jr && walk)) {
     int64_t tsum = 0, fsum = 0;
 #pragma unroll
     for (int j = 0; j < kRdma; ++j) {
@@ -352,16 +357,16 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
       const int64_t f = t > u ? t - u : 0;
       tsum += t;
       fsum += f;
-      const bool fits = t != 0 && f != 0 && g.rdma <= f;
+      const bool fits = t != 0 && f != 0 && g.rdma <= f;  // (g.rdma == 0 without a request)
       R.fit |= fits ? (1u << j) : 0u;
       if (scores && fits) R.sc |= (uint64_t)dev_score1(c, t, f, g.rdma) << (8 * j);
     }
-    raw += dev_score1(c, tsum, fsum, g.rdma);
+    if (has_rdma) raw += dev_score1(c, tsum, fsum, g.rdma);
   }
   uint32_t om = 0, orm = 0;
   bool jdone = false;
   if (walk) {
-    if (dev_by_topology(G, R, g, same, (uint64_t)v.tot(kDevMetaW), om, orm)) {
+    if (dev_by_topology(G, R, g, same, (uint64_t)v.tot(kDevMetaW), om, orm, has_rdma)) {
       // validateJointAllocation (device_allocator.go:255-284)
       if (same && dev_pcies_of(G, kGpus, om) != dev_pcies_of(R, kRdma, orm)) {
         o.reasons = KS_R_DEV_JOINT;
@@ -400,7 +405,7 @@ struct DevFits {
   DevType G, R;
   GpuReq g;
   uint64_t meta;
-  bool walk, same, has_gpu, has_rdma;
+  bool walk, same, has_gpu, has_rdma, jr;
 };
 
 template <typename V>
@@ -409,7 +414,8 @@ __device__ __forceinline__ DevFits dev_fits(const Cfg& c, const PodRec& p, const
   f.g = g;
   f.has_gpu = (p.flags & kPodGpuReq) != 0;
   f.has_rdma = p.rdma > 0;
-  const bool joint = f.has_gpu && f.has_rdma && p.joint != KS_JOINT_NONE;
+  f.jr = f.has_gpu && !f.has_rdma && p.joint != KS_JOINT_NONE;  // (dev_eval: joint without an RDMA request)
+  const bool joint = f.has_gpu && (f.has_rdma || f.jr) && p.joint != KS_JOINT_NONE;
   f.same = p.joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
   f.walk = joint && (f.same || g.rdesired > 1);
   const uint64_t topo = (uint64_t)v.tot(kDevTopoW);
@@ -432,7 +438,7 @@ __device__ __forceinline__ DevFits dev_fits(const Cfg& c, const PodRec& p, const
       if (f.walk && fits) f.G.sc |= (uint64_t)dev_score3(c, t, fr, pod) << (8 * k);
     }
   }
-  if (f.has_rdma) {
+  if (f.has_rdma || (f.jr && f.walk)) {
 #pragma unroll
     for (int j = 0; j < kRdma; ++j) {
       const int64_t t = v.tot(kDevRdmaW + j), u = v.use(kDevRdmaW + j);
@@ -460,7 +466,7 @@ __device__ __forceinline__ bool dev_fits_ok(const DevFits& f, uint32_t gin, uint
   R.sc &= dev_byte_mask(R.fit);
   if (f.walk) {
     uint32_t om = 0, orm = 0;
-    if (dev_by_topology(G, R, f.g, f.same, f.meta, om, orm))
+    if (dev_by_topology(G, R, f.g, f.same, f.meta, om, orm, f.has_rdma))
       return !(f.same && dev_pcies_of(G, kGpus, om) != dev_pcies_of(R, kRdma, orm));
     if (f.same) return false;
   }

@@ -151,7 +151,8 @@ def device_allocated(gpu_minors: int = 0, gpu_core: Optional[int] = None, gpu_me
             rl[RESOURCE_GPU_CORE] = quantity_string(gpu_core or 0, "DecimalSI")
         alloc["gpu"] = [{"minor": m, "resources": rl} for m in ordered(gpu_minors, gpu_order)]
     if rdma_minors:
-        alloc["rdma"] = [{"minor": m, "resources": {RESOURCE_RDMA: quantity_string(rdma, "DecimalSI")}}
+        # (a joint [gpu, rdma] pod without an RDMA request gets RDMA devices with a nil request list: null)
+        alloc["rdma"] = [{"minor": m, "resources": {RESOURCE_RDMA: quantity_string(rdma, "DecimalSI")} if rdma else None}
                          for m in ordered(rdma_minors, rdma_order)]
     return _marshal(alloc)
 

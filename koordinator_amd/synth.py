@@ -274,10 +274,12 @@ def make_devices(nodes: NodeTable, rng: np.random.Generator, gpu_frac: float = 0
     return d
 
 
-def rdma_pods(pods: PodTable, rng: np.random.Generator, joint_frac: float = 0.5, rdma_only: float = 0.03) -> PodTable:
+def rdma_pods(pods: PodTable, rng: np.random.Generator, joint_frac: float = 0.5, rdma_only: float = 0.03,
+              joint_no_rdma: float = 0.0) -> PodTable:
     """Half of the whole-GPU pods also ask for koordinator.sh/rdma 1 with joint [gpu, rdma] allocation (half of
     those with RequiredScope SamePCIe, SURVEY C3's "GPU+RDMA joint SamePCIe" pods); a few pods ask for RDMA
-    only (1, 50 or 100 = one whole device)."""
+    only (1, 50 or 100 = one whole device).  joint_no_rdma: that fraction of the joint pods keeps the joint spec
+    without the RDMA request (jointAllocate then takes RDMA devices with a nil request)."""
     p = pods.n
     whole = (pods.gpu_core >= 100) & (pods.gpu_core % 100 == 0)
     j = whole & (rng.random(p) < joint_frac)
@@ -286,6 +288,8 @@ def rdma_pods(pods: PodTable, rng: np.random.Generator, joint_frac: float = 0.5,
     pods.joint[:] = np.where(j, np.where(same, abi.KS_JOINT_GPU_RDMA_SAME_PCIE, abi.KS_JOINT_GPU_RDMA), 0)
     only = (pods.gpu_core + pods.gpu_memory + pods.gpu_memory_ratio == 0) & (rng.random(p) < rdma_only)
     pods.rdma[:] = np.where(only, rng.choice(np.array([1, 50, 100], np.int64), p), pods.rdma)
+    if joint_no_rdma:
+        pods.rdma[:] = np.where(j & (rng.random(p) < joint_no_rdma), 0, pods.rdma)
     return pods
 
 

@@ -1555,7 +1555,8 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
     if (!((exist >> pc) & 1u)) continue;
     uint32_t sub[2];
     dev_sub_of(s, n, 1u << pc, sub);
-    swpref[pc] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
+    /* (a joint pod without an RDMA request: no RDMA entry in freeDevices, no switch is preferred) */
+    swpref[pc] = g->has[KO_T_RDMA] && dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
     sw[nsw++] = pc;
   }
   /* freeNodeDevicesInPCIe: sort.Slice by (preferred desc, socket, node); stable here (insertion sort for
@@ -1589,7 +1590,7 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
   for (int i = 0; i < ng; i++) {
     uint32_t sub[2];
     dev_sub_of(s, n, gp[grp[i]], sub);
-    gpref[grp[i]] = dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
+    gpref[grp[i]] = g->has[KO_T_RDMA] && dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
   }
   for (int i = 1; i < ng; i++)
     for (int j = i; j > 0; j--) {

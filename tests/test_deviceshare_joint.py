@@ -88,3 +88,35 @@ def test_rdma_only_and_scores():
     # the GPU + RDMA score is the sum of the per-type scoreNode values (can exceed 100 before normalize)
     reasons, scores, _ = o.eval_pod(joint_pod(1))
     assert reasons.tolist()[:2] == [0, 0]
+
+
+def test_joint_without_rdma_request():
+    """A [gpu, rdma] joint pod that requests no RDMA: jointAllocate still takes an RDMA device next to the GPUs, with a
+    nil request (device_allocator.go:308-330): any device with free resources fits, none is used up, none scores the
+    node; no switch is `preferred` (newDeviceTopologyGuide splits free devices only for requested types)."""
+    c = _case("allocate 3 GPU and 2 VF")
+    o = Oracle(dev_zero_weights(), plain_nodes(1), devices=joint_devices(c))
+    res = o.schedule(joint_pod(2, rdma=0))
+    assert minors(res["gpu_minors"][0]) == [0, 1] and minors(res["rdma_minors"][0]) == [1]
+    _, _, _, urd = o.read_devices()
+    assert np.array_equal(urd, joint_devices(c).used_rdma)  # nothing added to the RDMA devices
+    # RDMA 1 (switch 0) fully used: switch 0 cannot complete the joint allocation, switch 1 does
+    d = joint_devices(c)
+    d.used_rdma[1] = 100
+    o = Oracle(dev_zero_weights(), plain_nodes(1), devices=d)
+    res = o.schedule(joint_pod(2, rdma=0))
+    assert minors(res["gpu_minors"][0]) == [2, 3] and minors(res["rdma_minors"][0]) == [2]
+    # every RDMA device full: best effort falls back to the GPUs alone (no RDMA type in the request); SamePCIe fails
+    d = joint_devices(c)
+    d.used_rdma[1:5] = 100
+    o = Oracle(dev_zero_weights(), plain_nodes(1), devices=d)
+    res = o.schedule(joint_pod(2, rdma=0))
+    assert res["status"][0] == 0 and minors(res["gpu_minors"][0]) == [0, 1] and res["rdma_minors"][0] == 0
+    reasons, _, _ = o.eval_pod(joint_pod(2, rdma=0, joint=abi.KS_JOINT_GPU_RDMA_SAME_PCIE))
+    assert reasons.tolist() == [abi.KS_R_DEV_JOINT]
+    # a node without RDMA devices is no KS_R_DEV_NO_RDMA for it (the pod requests none)
+    d = joint_devices(c, n=2)
+    d.total_rdma[:, 1] = 0
+    o = Oracle(dev_default(), plain_nodes(2), devices=d)
+    reasons, _, _ = o.eval_pod(joint_pod(1, rdma=0))
+    assert reasons.tolist() == [0, 0]

@@ -56,10 +56,12 @@ def _same_pcie_devices():
 
 @pytest.mark.parametrize("gpus", [1, 2, 3, 4])
 @pytest.mark.parametrize("joint", [abi.KS_JOINT_GPU_RDMA, abi.KS_JOINT_GPU_RDMA_SAME_PCIE])
-def test_same_pcie_cases(runtime, oracle_lib, gpus, joint):
+@pytest.mark.parametrize("rdma", [1, 0])
+def test_same_pcie_cases(runtime, oracle_lib, gpus, joint, rdma):
+    """(rdma 0: the joint spec without an RDMA request -- jointAllocate takes RDMA devices with a nil request)"""
     for name, d in _same_pcie_devices():
         for cfg in (dev_zero_weights(), dev_default()):
-            pod = joint_pod(gpus, joint=joint)
+            pod = joint_pod(gpus, rdma=rdma, joint=joint)
             ev = runtime.Evaluator(cfg, plain_nodes(1), devices=d.copy())
             orc = oracle_lib.Oracle(cfg, plain_nodes(1), devices=d.copy())
             r_g, s_g, _ = ev.eval_pod(pod)
@@ -129,3 +131,14 @@ def test_schedule_tight_rdma_most_allocated(runtime, oracle_lib):
     w.pods.joint[w.pods.rdma > 0] = abi.KS_JOINT_GPU_RDMA_SAME_PCIE
     w.profile.deviceshare = DeviceShareArgs(strategy="MostAllocated")
     check(runtime, oracle_lib, w, "tight-most")
+
+
+@pytest.mark.parametrize("seed", [56, 57])
+def test_schedule_c3_joint_without_rdma_request(runtime, oracle_lib, seed):
+    """C3-shaped queues where a third of the joint pods keep the joint spec without the RDMA request"""
+    w = c3_small(seed)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    jr = (w.pods.joint != 0) & (rng.random(w.pods.n) < 0.35)
+    w.pods.rdma[jr] = 0
+    got = check(runtime, oracle_lib, w, f"c3-joint-nordma-{seed}")
+    assert ((got["rdma_minors"] != 0) & jr).sum() > 5
