@@ -176,8 +176,8 @@ class NodeTable(_Table):
         for k in range(abi.KS_MAX_SCALARS):
             c.alloc_scalar[k] = _p64(self.alloc_scalar[k])
             c.req_scalar[k] = _p64(self.req_scalar[k])
-        self.topo_domain = np.ascontiguousarray(self.topo_domain, np.int32).reshape(-1, self.n)
-        self.topo_count = np.ascontiguousarray(self.topo_count, np.int32).reshape(-1, self.n)
+        self.topo_domain = _rows2d(self.topo_domain, self.n)
+        self.topo_count = _rows2d(self.topo_count, self.n)
         c.topo_nkeys = self.topo_domain.shape[0]
         c.topo_ndomains = int(self.topo_ndomains)
         c.topo_nprops = self.topo_count.shape[0]
@@ -185,6 +185,14 @@ class NodeTable(_Table):
         c.topo_count = _p32(self.topo_count) if self.topo_count.size else None
         c._keep = self  # keep arrays alive with the struct
         return c
+
+
+def _rows2d(a, n: int) -> np.ndarray:
+    """[rows][n] int32, C-contiguous (a per-key / per-property block of node columns)"""
+    a = np.ascontiguousarray(a, np.int32)
+    if a.ndim != 2:
+        a = a.reshape(-1, n) if n else np.zeros((0, 0), np.int32)
+    return a
 
 
 def _csr_rows(beg: np.ndarray, vals: np.ndarray, idx: np.ndarray):

@@ -234,9 +234,12 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
 #pragma unroll
   for (int p = 0; p < kPcie; ++p)
     if (rpref && ((exist >> p) & 1u) && (R.fit & dev_sub_of(R, kRdma, 1u << p))) swpref |= 1u << p;
-  // freeNodeDevicesInPCIe: preferred switches first (a switch without a fitting RDMA fails jointAllocate)
+  // freeNodeDevicesInPCIe: preferred switches first (with an RDMA request a switch without a fitting RDMA device fails
+  // jointAllocate, so only those are tried); without one no switch is preferred and every switch is tried in
+  // (socket, node, pcie) = index order
+  const uint32_t tryset = rpref ? swpref : exist;
   for (int p = 0; p < kPcie; ++p) {
-    if (!((swpref >> p) & 1u)) continue;
+    if (!((tryset >> p) & 1u)) continue;
     if (__builtin_popcount(G.fit & dev_sub_of(G, kGpus, 1u << p)) >= g.desired &&
         dev_joint(G, R, g, same, 1u << p, 1u << p, om, orm))
       return true;
