@@ -148,7 +148,7 @@ __device__ __forceinline__ int64_t estimated_used(int64_t req, int64_t lim, int6
   return est;
 }
 
-__global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t sf_cpu, int64_t sf_mem) {
+__global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t sf_cpu, int64_t sf_mem, int32_t dev_on) {
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= np) return;
   PodRec r;
@@ -197,6 +197,7 @@ __global__ void prep_pods_kernel(DevPodCols s, PodRec* out, int32_t np, int64_t 
   r.joint = s.joint ? s.joint[i] : 0u;
   r._pad0 = 0;
   if (r.rdma > 0) r.flags |= kPodHasGpu;
+  if (dev_on && (r.flags & kPodHasGpu)) r.flags |= kPodDevNoNom;
   // a normalized score that can differ between nodes: DeviceShare (device requests), TaintToleration / NodeAffinity
   if ((r.flags & kPodHasGpu) || s.stat_dyn[i]) r.flags |= kPodNormDyn;
   if (s.topo && (s.topo[i].flags & KS_TOPO_DYN)) r.flags |= kPodTopoDyn;
@@ -3233,7 +3234,8 @@ static int prep_stage(ks_ctx* ctx, PodStage& st, int32_t p) {
   if (p <= 0) return KS_OK;
   const int threads = 256;
   hipLaunchKernelGGL(prep_pods_kernel, dim3((p + threads - 1) / threads), dim3(threads), 0, ctx->stream, st.cols,
-                     st.recs, p, ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory);
+                     st.recs, p, ctx->cfg.loadaware.scaling_cpu, ctx->cfg.loadaware.scaling_memory,
+                     (int32_t)(ctx->cfg.deviceshare.enable != 0));
   HIPCHK(ctx, hipGetLastError());
   return KS_OK;
 }

@@ -20,15 +20,18 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
   // the topology step (ks_topo.h): the pod at the cursor, only if it is a topology pod
   int64_t pi = 0;
   TopoRec tr;
+  TopoTerms tt;
   NodeReg<NSC> r;
   load_node<NSC>(c, d, i, valid ? 1 : 0, r);  // (issued with the step's pod record)
   const int64_t i0 = valid ? i : 0;
+  const TopoNodeDom nd = topo ? topo_node_dom(tk.t, i0) : TopoNodeDom{};
   const uint64_t th = c.stat ? d.taints_hard[i0] : 0ull, ts = c.stat ? d.taints_soft[i0] : 0ull,
                  lb = c.stat ? d.labels[i0] : 0ull, hp = c.stat ? d.host_ports[i0] : 0ull;
   if (topo) {
     pi = topo_cur(tk, tr);
+    tt = topo_terms_cur(tk);
     if (pi < 0) return;
-    if (tr.flags & KS_TOPO_DYN) topo_stage(tk, tr, tl);
+    if (tr.flags & KS_TOPO_DYN) topo_stage(tk, tr, tt, tl);
   }
   TopoNodeIn tin{1u, 0, 0, 0, 0};
   if (valid) {
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     tin = TopoNodeIn{o.reasons, o.dev_raw, o.traw, o.araw, ro.hiord};
   }
   // PodTopologySpread / InterPodAffinity Filters and the normalizations' reductions (every lane, converged)
-  if (topo) topo_eval_node(tk, tr, (int32_t)pi, i, valid, tl, tin);
+  if (topo) topo_eval_node(tk, tr, tt, nd, (int32_t)pi, i, valid, tl, tin);
 }
 
 

@@ -45,6 +45,10 @@ constexpr uint32_t kPodBigReq = 0x1000u;
 // internal pod flag: a normalized score (DeviceShare, TaintToleration, NodeAffinity) can differ between nodes for the
 // pod, so a commit may change its normalization max (the monotone fast path does not hold for it)
 constexpr uint32_t kPodNormDyn = 0x2000u;
+// internal pod flag: DeviceShare (enabled) has the pod's device requests, so its FilterReservation (plugin.go:322-358)
+// rejects every reservation holding no device -- every reservation the library models: none is nominated
+// (nominator.go:163-168), the pod is never assumed into one (reservation/plugin.go:546-560)
+constexpr uint32_t kPodDevNoNom = 0x8000u;
 
 // la_bits (prep_nodes_kernel output)
 constexpr uint32_t kLaZeroScore = 0x1u;     // Score returns 0 (no NodeMetric / expired)
@@ -720,6 +724,24 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   v = umax64(v, dpp64<0x141>(v));
   v = umax64(v, dpp64<0x140>(v));
   return umax64(umax64(readlane64(v, 0), readlane64(v, 16)), umax64(readlane64(v, 32), readlane64(v, 48)));
+}
+
+// DPP sum over the wave (the same exchange pattern as wave_max_u32: each step combines disjoint groups)
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp32<0xB1>(v);
+  v += dpp32<0x4E>(v);
+  v += dpp32<0x141>(v);
+  v += dpp32<0x140>(v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+
+__device__ __forceinline__ uint64_t wave_or_u64(uint64_t v) {
+  v |= dpp64<0xB1>(v);
+  v |= dpp64<0x4E>(v);
+  v |= dpp64<0x141>(v);
+  v |= dpp64<0x140>(v);
+  return readlane64(v, 0) | readlane64(v, 16) | readlane64(v, 32) | readlane64(v, 48);
 }
 
 __device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {

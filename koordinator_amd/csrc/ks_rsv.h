@@ -257,8 +257,14 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
   }
   o.nom = nom_o >= 0 ? nom_o : nom_s;
   o.raw = nom_o >= 0 ? raw_o : (nom_s >= 0 ? best_s : 0);
-  o.hi = hiord > 0 ? hiord : o.raw;
+  // the Reservation Filter passes on any satisfying reservation; the nomination also runs DeviceShare's
+  // FilterReservation, which rejects them all for a device pod (kPodDevNoNom)
   o.reasons = (aff && o.nom < 0) ? KS_R_RSV_NO_FIT : 0u;
+  if (p.flags & kPodDevNoNom) {
+    o.nom = -1;
+    o.raw = 0;
+  }
+  o.hi = hiord > 0 ? hiord : o.raw;
   return o;
 }
 

@@ -33,6 +33,7 @@ namespace ks {
 // internal pod flag (PodRec.flags): the pod has topology query terms (KS_TOPO_DYN)
 constexpr uint32_t kPodTopoDyn = 0x4000u;
 constexpr int kTopoTerms = KS_TOPO_MAX_TERMS;
+constexpr int kTopoInline = 8;  // the step pod's first terms, held in (wave-uniform) registers by every step kernel
 
 // Per pending pod, queue order (staged with the pod columns): its query terms and properties in the stage's lists
 struct __attribute__((aligned(16))) TopoRec {
@@ -77,6 +78,12 @@ struct TopoScratch {
   // with one load instead of the cursor -> record chain (-1 = the cursor's pod is not a topology pod)
   int32_t cur_pi, _pad3[3];
   TopoRec cur_rec;
+  uint64_t cur_terms[kTopoInline];  // ... and its first terms
+};
+
+// The step pod's first kTopoInline terms (registers); later ones are read from the stage's list
+struct TopoTerms {
+  uint64_t w[kTopoInline];
 };
 
 __device__ __forceinline__ int tp_kind(uint64_t w) { return (int)(w & 0xF); }
@@ -85,8 +92,25 @@ __device__ __forceinline__ int tp_key(uint64_t w) { return (int)((w >> 8) & 0xFF
 __device__ __forceinline__ int tp_prop(uint64_t w) { return (int)((w >> 16) & 0xFFFF); }
 __device__ __forceinline__ int32_t tp_param(uint64_t w) { return (int32_t)(uint32_t)(w >> 32); }
 
-// node n's value index of key k >= 1 (-1 = the label is absent)
-__device__ __forceinline__ int32_t tp_dom(const DevTopo& t, int k, int64_t n) { return t.dom[(int64_t)(k - 1) * t.npad + n]; }
+// A node's value indices of keys 1..kTopoPreKeys, loaded with the node's other inputs before the step's pod record
+// arrives (a kernel would otherwise wait for the record, then for the term, then for the domain)
+constexpr int kTopoPreKeys = 4;
+struct TopoNodeDom {
+  int32_t d[kTopoPreKeys];
+  int64_t n;
+};
+__device__ __forceinline__ TopoNodeDom topo_node_dom(const DevTopo& t, int64_t n) {
+  TopoNodeDom nd;
+#pragma unroll
+  for (int k = 0; k < kTopoPreKeys; ++k) nd.d[k] = k < t.nkeys ? t.dom[(int64_t)k * t.npad + n] : -1;
+  nd.n = n;
+  return nd;
+}
+// the node's value index of key k >= 1 (-1 = the label is absent); k is wave-uniform
+__device__ __forceinline__ int32_t tp_dom(const DevTopo& t, const TopoNodeDom& nd, int k) {
+  if (k <= kTopoPreKeys) return k == 1 ? nd.d[0] : k == 2 ? nd.d[1] : k == 3 ? nd.d[2] : nd.d[3];
+  return t.dom[(int64_t)(k - 1) * t.npad + nd.n];
+}
 __device__ __forceinline__ int32_t tp_count(const DevTopo& t, uint64_t w, int64_t n) {
   return t.count[(int64_t)tp_prop(w) * t.npad + n];
 }
@@ -184,14 +208,47 @@ __device__ __forceinline__ int32_t topo_cur(const TopoKArgs& a, TopoRec& rec) {
 // the step pod's term t (wave-uniform scalar load)
 __device__ __forceinline__ uint64_t topo_term(const TopoKArgs& a, const TopoRec& tr, int t) { return a.terms[tr.tbeg + t]; }
 
-// nodeLabelsMatchSpreadConstraints over the pod's constraints of one kind: node n has every key they name
-__device__ __forceinline__ bool topo_keys_ok(const TopoKArgs& a, const TopoRec& tr, int kind, int64_t n) {
-  bool ok = true;
-  for (int t = 0; t < tr.nterms; ++t) {
-    const uint64_t w = topo_term(a, tr, t);
-    if (tp_kind(w) == kind && tp_key(w) != 0) ok = ok && tp_dom(a.t, tp_key(w), n) >= 0;
-  }
-  return ok;
+__device__ __forceinline__ TopoTerms topo_terms_of(const TopoKArgs& a, const TopoRec& tr) {
+  TopoTerms tt;
+#pragma unroll
+  for (int t = 0; t < kTopoInline; ++t) tt.w[t] = t < tr.nterms ? a.terms[tr.tbeg + t] : 0ull;
+  return tt;
+}
+__device__ __forceinline__ TopoTerms topo_terms_cur(const TopoKArgs& a) {
+  TopoTerms tt;
+#pragma unroll
+  for (int t = 0; t < kTopoInline; ++t) tt.w[t] = a.scr->cur_terms[t];
+  return tt;
+}
+
+// f(t, w) over the step pod's terms in order (the first kTopoInline from registers: unrolled, no dynamic index);
+// f returns false to stop
+template <typename F>
+__device__ __forceinline__ void topo_each(const TopoKArgs& a, const TopoRec& tr, const TopoTerms& tt, F f) {
+#pragma unroll
+  for (int t = 0; t < kTopoInline; ++t)
+    if (t < tr.nterms && !f(t, tt.w[t])) return;
+  for (int t = kTopoInline; t < tr.nterms; ++t)
+    if (!f(t, topo_term(a, tr, t))) return;
+}
+
+// nodeLabelsMatchSpreadConstraints over the pod's hard and soft constraints: node n has every key they name
+struct TopoKeysOk {
+  bool hard, soft;
+};
+__device__ __forceinline__ TopoKeysOk topo_keys_ok(const TopoKArgs& a, const TopoRec& tr, const TopoTerms& tt,
+                                                   const TopoNodeDom& nd) {
+  TopoKeysOk k{true, true};
+  topo_each(a, tr, tt, [&](int, uint64_t w) {
+    const int kd = tp_kind(w);
+    if ((kd == KS_TOPO_K_SPREAD_HARD || kd == KS_TOPO_K_SPREAD_SOFT) && tp_key(w) != 0) {
+      const bool has = tp_dom(a.t, nd, tp_key(w)) >= 0;
+      if (kd == KS_TOPO_K_SPREAD_HARD) k.hard = k.hard && has;
+      else k.soft = k.soft && has;
+    }
+    return true;
+  });
+  return k;
 }
 
 // the node counts for term w (hard spread: required node affinity + every hard key; soft spread: required node
@@ -218,21 +275,35 @@ __device__ __forceinline__ long long wave_sum_i64(long long v) {
   return v;
 }
 
-// Wave-segmented reduction into HBM (every lane calls it, converged): lanes with `on` add `v` to sum[z] and set bit z of
-// bits (either may be NULL); one atomic per distinct z of the wave
-__device__ __forceinline__ void topo_seg_add(long long* sum, uint32_t* bits, bool on, int32_t z, long long v) {
+// Wave-segmented reduction into HBM (every lane calls it, converged): lanes with `on` add `v` (a node's pod count,
+// >= 0) to sum[z] and set bit z of bits (either may be NULL); one atomic per distinct z of the wave
+__device__ __forceinline__ void topo_seg_add(long long* sum, uint32_t* bits, bool on, int32_t z, int32_t v) {
   uint64_t act = __ballot(on);
   while (act) {
     const int l = __ffsll((long long)act) - 1;
-    const int32_t z0 = __shfl(z, l, 64);
+    const int32_t z0 = __builtin_amdgcn_readlane(z, l);
     const bool mine = on && z == z0;
     const uint64_t m = __ballot(mine);
-    const long long s = sum ? wave_sum_i64(mine ? v : 0) : 0;
+    const uint32_t s = sum ? wave_sum_u32(mine ? (uint32_t)v : 0u) : 0u;
     if ((threadIdx.x & 63) == l) {
       if (sum && s) atomicAdd((unsigned long long*)(sum + z0), (unsigned long long)s);
       if (bits) atomicOr(bits + (z0 >> 5), 1u << (z0 & 31));
     }
     act &= ~m;
+  }
+}
+
+// Wave-level domain bit set (bits: a [nw] word array; every lane calls it, converged): one 64-bit OR per wave when
+// every domain index fits a word pair, else one atomic per distinct domain of the wave
+__device__ __forceinline__ void topo_bits_or(uint32_t* bits, int32_t ndom, bool on, int32_t z) {
+  if (ndom <= 64) {
+    const uint64_t o = wave_or_u64(on ? (1ull << z) : 0ull);
+    if ((threadIdx.x & 63) == 0) {
+      if ((uint32_t)o) atomicOr(bits, (uint32_t)o);
+      if (o >> 32) atomicOr(bits + 1, (uint32_t)(o >> 32));
+    }
+  } else {
+    topo_seg_add(nullptr, bits, on, z, 0);
   }
 }
 
@@ -243,14 +314,13 @@ struct TopoLds {
   long long mins[kTopoTerms];
   int any_all;
 };
-__device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr, TopoLds& l) {
+__device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr, const TopoTerms& tt, TopoLds& l) {
   const int tid = threadIdx.x;
   if (tid < kTopoTerms) l.mins[tid] = a.scr->hmin[tid];
   if (tid == 0) l.any_all = a.scr->any_all;
   __syncthreads();
-  for (int t = 0; t < tr.nterms; ++t) {
-    const uint64_t w = topo_term(a, tr, t);
-    if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD || tp_key(w) == 0) continue;  // (wave-uniform)
+  topo_each(a, tr, tt, [&](int t, uint64_t w) {
+    if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD || tp_key(w) == 0) return true;  // (wave-uniform)
     long long m = LLONG_MAX;
     for (int z = tid; z < a.t.ndom; z += blockDim.x)
       if ((a.t.zpres[(int64_t)t * a.t.nw + (z >> 5)] >> (z & 31)) & 1u) {
@@ -259,7 +329,8 @@ __device__ __forceinline__ void topo_stage(const TopoKArgs& a, const TopoRec& tr
       }
     m = wave_min_i64(m);
     if ((tid & 63) == 0 && m != LLONG_MAX) atomicMin(&l.mins[t], m);
-  }
+    return true;
+  });
   __syncthreads();
 }
 
@@ -273,7 +344,8 @@ struct TopoNodeIn {
 // cluster): both plugins' Filters OR-ed into the node's reasons (total -1 and the score row zeroed when they fail),
 // InterPodAffinity's raw score, the counted nodes' domains of the soft constraints (topology sizes), and the node's part
 // of the normalizations' reductions (one global atomic per wave)
-__device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec& tr, int32_t pi, int64_t i, bool valid,
+__device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec& tr, const TopoTerms& tt,
+                                               const TopoNodeDom& nd, int32_t pi, int64_t i, bool valid,
                                                const TopoLds& l, const TopoNodeIn& in) {
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
   const bool soft_all = (tr.flags & KS_TOPO_SOFT_ALL_KEYS) != 0;
@@ -282,25 +354,26 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
   long long ir = 0;
   int32_t dr = 0, trw = 0, arw = 0;
   uint64_t pref = 0;
+  TopoKeysOk keys{true, true};
+  if (dyn) keys = topo_keys_ok(a, tr, tt, nd);
   if (valid) {
     const uint32_t base = in.base;
     uint32_t r = 0;
     if (dyn) {
-      const bool hard_keys = topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_HARD, n);
       // the term's count in the node's domain (the node has the key's label)
       auto domain = [&](int t, uint64_t w) -> long long {
         if (tp_key(w) == 0) return (long long)tp_count(a.t, w, n);
-        return a.t.zsum[(int64_t)t * a.t.ndom + tp_dom(a.t, tp_key(w), n)];
+        return a.t.zsum[(int64_t)t * a.t.ndom + tp_dom(a.t, nd, tp_key(w))];
       };
+      auto has_key = [&](uint64_t w) { return tp_key(w) == 0 || tp_dom(a.t, nd, tp_key(w)) >= 0; };
       // PodTopologySpread Filter: the first hard constraint that fails
       bool aff = true, aff_done = false;
-      for (int t = 0; t < tr.nterms; ++t) {
-        const uint64_t w = topo_term(a, tr, t);
-        if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD) continue;
-        const int32_t z = tp_key(w) == 0 ? 0 : tp_dom(a.t, tp_key(w), n);
+      topo_each(a, tr, tt, [&](int t, uint64_t w) {
+        if (tp_kind(w) != KS_TOPO_K_SPREAD_HARD) return true;
+        const int32_t z = tp_key(w) == 0 ? 0 : tp_dom(a.t, nd, tp_key(w));
         if (z < 0) {  // ErrReasonNodeLabelNotMatch
           r = KS_R_TOPOLOGY_SPREAD;
-          break;
+          return false;
         }
         long long match;
         if (tp_key(w) != 0) {
@@ -310,38 +383,37 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
             aff = tp_node_aff(a.stat ? a.stat + pi : nullptr, a.labels ? a.labels[n] : 0ull);
             aff_done = true;
           }
-          match = (aff && hard_keys) ? (long long)tp_count(a.t, w, n) : 0;
+          match = (aff && keys.hard) ? (long long)tp_count(a.t, w, n) : 0;
         }
         const long long self = (tp_flags(w) & KS_TOPO_T_SELF) ? 1 : 0;
         if (match + self - l.mins[t] > (long long)tp_param(w)) {  // ErrReasonConstraintsNotMatch
           r = KS_R_TOPOLOGY_SPREAD;
-          break;
+          return false;
         }
-      }
+        return true;
+      });
       // InterPodAffinity Filter: affinity, anti-affinity, existing pods' anti-affinity -- the first that fails
       bool aff_terms = false, missing = false, exist = true;
-      for (int t = 0; t < tr.nterms; ++t) {
-        const uint64_t w = topo_term(a, tr, t);
-        if (tp_kind(w) != KS_TOPO_K_AFFINITY) continue;
+      topo_each(a, tr, tt, [&](int t, uint64_t w) {
+        if (tp_kind(w) != KS_TOPO_K_AFFINITY) return true;
         aff_terms = true;
-        if (tp_key(w) != 0 && tp_dom(a.t, tp_key(w), n) < 0) missing = true;
+        if (!has_key(w)) missing = true;
         else if (domain(t, w) <= 0) exist = false;
-      }
+        return true;
+      });
       uint32_t ipa = 0;
       if (aff_terms && (missing || (!exist && !(l.any_all == 0 && (tr.flags & KS_TOPO_SELF_AFFINITY))))) {
         ipa = KS_R_POD_AFFINITY;
       } else {
-        for (int t = 0; t < tr.nterms && !ipa; ++t) {
-          const uint64_t w = topo_term(a, tr, t);
-          if (tp_kind(w) == KS_TOPO_K_ANTI && (tp_key(w) == 0 || tp_dom(a.t, tp_key(w), n) >= 0) && domain(t, w) > 0)
-            ipa = KS_R_POD_ANTI_AFFINITY;
-        }
-        for (int t = 0; t < tr.nterms && !ipa; ++t) {
-          const uint64_t w = topo_term(a, tr, t);
-          if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && (tp_key(w) == 0 || tp_dom(a.t, tp_key(w), n) >= 0) &&
-              domain(t, w) > 0)
-            ipa = KS_R_EXISTING_ANTI_AFFINITY;
-        }
+        topo_each(a, tr, tt, [&](int t, uint64_t w) {
+          if (tp_kind(w) == KS_TOPO_K_ANTI && has_key(w) && domain(t, w) > 0) ipa = KS_R_POD_ANTI_AFFINITY;
+          return ipa == 0;
+        });
+        if (!ipa)
+          topo_each(a, tr, tt, [&](int t, uint64_t w) {
+            if (tp_kind(w) == KS_TOPO_K_EXISTING_ANTI && has_key(w) && domain(t, w) > 0) ipa = KS_R_EXISTING_ANTI_AFFINITY;
+            return ipa == 0;
+          });
       }
       r |= ipa;
       if (r) {
@@ -352,15 +424,14 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
       }
       // InterPodAffinity Score: weight x matching pods in the node's domain, per score term
       if ((base | r) == 0)
-        for (int t = 0; t < tr.nterms; ++t) {
-          const uint64_t w = topo_term(a, tr, t);
-          if (tp_kind(w) == KS_TOPO_K_SCORE && (tp_key(w) == 0 || tp_dom(a.t, tp_key(w), n) >= 0))
-            ir += (long long)tp_param(w) * domain(t, w);
-        }
+        topo_each(a, tr, tt, [&](int t, uint64_t w) {
+          if (tp_kind(w) == KS_TOPO_K_SCORE && has_key(w)) ir += (long long)tp_param(w) * domain(t, w);
+          return true;
+        });
     }
     feas = (base | r) == 0;
     // initPreScoreState: a node without every soft key is ignored under requireAllTopologies
-    counted = feas && !(dyn && soft_all && !topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, n));
+    counted = feas && !(dyn && soft_all && !keys.soft);
     if (feas) {
       a.iraw[i] = ir;
       dr = in.dr;
@@ -371,13 +442,13 @@ __device__ __forceinline__ void topo_eval_node(const TopoKArgs& a, const TopoRec
   }
   // topology sizes of the soft constraints over the counted nodes: per term the domains (a node without the key: "")
   if (dyn)
-    for (int t = 0; t < tr.nterms; ++t) {
-      const uint64_t w = topo_term(a, tr, t);
-      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) continue;  // (wave-uniform)
-      const int32_t z = counted ? tp_dom(a.t, tp_key(w), n) : -1;
-      topo_seg_add(nullptr, a.t.zsize + (int64_t)t * a.t.nw, counted && z >= 0, z, 0);
+    topo_each(a, tr, tt, [&](int t, uint64_t w) {
+      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) return true;  // (wave-uniform)
+      const int32_t z = counted ? tp_dom(a.t, nd, tp_key(w)) : -1;
+      topo_bits_or(a.t.zsize + (int64_t)t * a.t.nw, a.t.ndom, counted && z >= 0, z);
       if (__ballot(counted && z < 0) && (threadIdx.x & 63) == 0) atomicOr(&a.scr->tempty[t], 1);
-    }
+      return true;
+    });
   // the wave's part of every other reduction, then one atomic per quantity
   const int lane = threadIdx.x & 63;
   const uint64_t cnt = __ballot(counted);

@@ -42,48 +42,87 @@ TopoScratch topo_scratch_init() {
   return s;
 }
 
+// LDS slots of a workgroup's domain sums ([term][domain], u32: a workgroup's nodes' counts): when the step's terms x
+// domains fit, each workgroup sums in LDS and issues one global atomic per non-zero slot; else one per distinct domain
+// of each wave (topo_seg_add)
+constexpr int kTopoLdsSums = 4096;
+
 __global__ __launch_bounds__(kTopoThreads) void topo_sums_kernel(TopoKArgs a) {
+  __shared__ uint32_t zl[kTopoLdsSums];
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)blockIdx.x * kTopoThreads + tid;
   const bool in = n < a.n;
   const int64_t n0 = in ? n : 0;
   const uint64_t lab = a.labels ? a.labels[n0] : 0ull;  // (the node's loads issued with the cursor -> record chain)
+  const TopoNodeDom nd = topo_node_dom(a.t, n0);
   TopoRec tr;
   const int32_t pi = topo_pod(a, tr);
-  if (blockIdx.x == 0 && tid == 0) {
-    a.scr->cur_pi = pi;
-    a.scr->cur_rec = tr;
+  const TopoTerms tt = pi >= 0 ? topo_terms_of(a, tr) : TopoTerms{};
+  if (blockIdx.x == 0 && tid < 64) {
+    if (tid == 0) {
+      a.scr->cur_pi = pi;
+      a.scr->cur_rec = tr;
+    }
+    if (tid < kTopoInline) a.scr->cur_terms[tid] = (pi >= 0 && tid < tr.nterms) ? a.terms[tr.tbeg + tid] : 0ull;
   }
-  if (pi < 0 || !(tr.flags & KS_TOPO_DYN)) return;
+  if (pi < 0 || !(tr.flags & KS_TOPO_DYN)) return;  // (grid-uniform)
+  // the first terms' counts and domains, loaded together
+  int32_t c8[kTopoInline], z8[kTopoInline];
+#pragma unroll
+  for (int t = 0; t < kTopoInline; ++t) {
+    const uint64_t w = tt.w[t];
+    c8[t] = t < tr.nterms ? tp_count(a.t, w, n0) : 0;
+    z8[t] = (t < tr.nterms && tp_key(w) != 0) ? tp_dom(a.t, nd, tp_key(w)) : 0;
+  }
+  const int32_t nslot = tr.nterms * a.t.ndom;
+  const bool lds = nslot <= kTopoLdsSums;  // (grid-uniform)
+  if (lds)
+    for (int k = tid; k < nslot; k += kTopoThreads) zl[k] = 0u;
   bool need_aff = false;
-  for (int t = 0; t < tr.nterms; ++t) {
-    const int k = tp_kind(topo_term(a, tr, t));
+  topo_each(a, tr, tt, [&](int, uint64_t w) {
+    const int k = tp_kind(w);
     need_aff |= k == KS_TOPO_K_SPREAD_HARD || k == KS_TOPO_K_SPREAD_SOFT;
-  }
+    return true;
+  });
   const bool aff = need_aff ? tp_node_aff(a.stat ? a.stat + pi : nullptr, lab) : true;
-  const bool hard_keys = topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_HARD, n0);
-  const bool soft_keys = topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, n0);
+  const TopoKeysOk keys = topo_keys_ok(a, tr, tt, nd);
   TopoScratch* s = a.scr;
   bool aav = false;
-  for (int t = 0; t < tr.nterms; ++t) {
-    const uint64_t w = topo_term(a, tr, t);  // (wave-uniform)
-    const bool el = in && tp_eligible(w, tr.flags, aff, hard_keys, soft_keys);
-    const int32_t cnt = el ? tp_count(a.t, w, n0) : 0;
+  __syncthreads();
+  auto term = [&](int t, uint64_t w, int32_t c, int32_t zn) {  // (wave-uniform)
+    const bool el = in && tp_eligible(w, tr.flags, aff, keys.hard, keys.soft);
+    const int32_t cnt = el ? c : 0;
     int32_t z = 0;
     if (tp_key(w) != 0) {
-      z = in ? tp_dom(a.t, tp_key(w), n0) : -1;
+      z = in ? zn : -1;
       // the domain's sum, and for a hard constraint the domains with an eligible node (TpPairToMatchNum's keys)
-      topo_seg_add(a.t.zsum + (int64_t)t * a.t.ndom,
-                   tp_kind(w) == KS_TOPO_K_SPREAD_HARD ? a.t.zpres + (int64_t)t * a.t.nw : nullptr, el && z >= 0, z,
-                   (long long)cnt);
+      const bool on = el && z >= 0;
+      if (lds) {
+        if (on && cnt) atomicAdd(&zl[t * a.t.ndom + z], (uint32_t)cnt);
+      } else {
+        topo_seg_add(a.t.zsum + (int64_t)t * a.t.ndom, nullptr, on, z, cnt);
+      }
+      if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD) topo_bits_or(a.t.zpres + (int64_t)t * a.t.nw, a.t.ndom, on, z);
     } else if (tp_kind(w) == KS_TOPO_K_SPREAD_HARD) {
       const uint32_t m = ~wave_max_u32(~(uint32_t)(el ? cnt : INT_MAX));  // (counts are >= 0)
       if ((tid & 63) == 0 && m != (uint32_t)INT_MAX) atomicMin(&s->hmin[t], (int)m);
     }
     // affinityCounts: a pod matching every required term counts on each term's (key, value) the node has
     if (tp_kind(w) == KS_TOPO_K_AFFINITY) aav |= el && cnt > 0 && z >= 0;
+  };
+#pragma unroll
+  for (int t = 0; t < kTopoInline; ++t)
+    if (t < tr.nterms) term(t, tt.w[t], c8[t], z8[t]);
+  for (int t = kTopoInline; t < tr.nterms; ++t) {
+    const uint64_t w = topo_term(a, tr, t);
+    term(t, w, tp_count(a.t, w, n0), tp_key(w) != 0 ? tp_dom(a.t, nd, tp_key(w)) : 0);
   }
   if (__ballot(aav) && (tid & 63) == 0) atomicOr(&s->any_all, 1);
+  if (lds) {  // the workgroup's sums: [term][domain] is zsum's layout
+    __syncthreads();
+    for (int k = tid; k < nslot; k += kTopoThreads)
+      if (zl[k]) atomicAdd((unsigned long long*)(a.t.zsum + k), (unsigned long long)zl[k]);
+  }
 }
 
 // topologyNormalizingWeight(size) = log(size + 2), from the host's table
@@ -105,8 +144,10 @@ __global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
   const uint32_t rs = in ? a.reasons[i] : 1u;
   const int32_t rr = (in && a.rsv_on) ? a.rraw[i] : 0;
   const unsigned long long hs = s->hsize, rp = s->rsv_pref;
+  const TopoNodeDom nd = topo_node_dom(a.t, in ? i : 0);
   TopoRec tr;
   const int32_t pi = topo_cur(a, tr);
+  const TopoTerms tt = topo_terms_cur(a);
   KS_TOPO_ISSUED("v"(rs), "v"(rr));
   if (pi < 0) return;  // (grid-uniform)
   const bool dyn = (tr.flags & KS_TOPO_DYN) != 0;
@@ -116,13 +157,14 @@ __global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
   if (dyn) {
     if (tid < kTopoTerms) tsz[tid] = 0u;
     __syncthreads();
-    for (int t = 0; t < tr.nterms; ++t) {
-      const uint64_t w = topo_term(a, tr, t);
-      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) continue;
+    topo_each(a, tr, tt, [&](int t, uint64_t w) {
+      if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT || tp_key(w) == 0) return true;
       unsigned int c = 0;
       for (int k = tid; k < a.t.nw; k += kTopoThreads) c += (unsigned int)__popc(a.t.zsize[(int64_t)t * a.t.nw + k]);
-      if (c) atomicAdd(&tsz[t], c);
-    }
+      c = wave_sum_u32(c);
+      if (c && (tid & 63) == 0) atomicAdd(&tsz[t], c);
+      return true;
+    });
     __syncthreads();
     if (tid < tr.nterms) {
       const uint64_t w = topo_term(a, tr, tid);
@@ -139,21 +181,21 @@ __global__ __launch_bounds__(kTopoThreads) void topo_pts_kernel(TopoKArgs a) {
     if (dyn) {
       // PodTopologySpread's raw score (PreScore's pair counts, Score's scoreForCount summed in term order in Go's f64
       // order, math.Round); an ignored node (requireAllTopologies, a soft key missing) scores 0 and is not counted
-      const bool ignored = soft_all && !topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, i);
+      const bool ignored = soft_all && !topo_keys_ok(a, tr, tt, nd).soft;
       double score = 0.0;
-      for (int t = 0; t < tr.nterms; ++t) {
-        const uint64_t w = topo_term(a, tr, t);
-        if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) continue;  // (wave-uniform)
+      topo_each(a, tr, tt, [&](int t, uint64_t w) {
+        if (tp_kind(w) != KS_TOPO_K_SPREAD_SOFT) return true;  // (wave-uniform)
         long long cnt;
         if (tp_key(w) == 0) {
           cnt = (long long)tp_count(a.t, w, i);
         } else {
-          const int32_t z = tp_dom(a.t, tp_key(w), i);
-          if (z < 0) continue;  // (a node without the key adds nothing)
+          const int32_t z = tp_dom(a.t, nd, tp_key(w));
+          if (z < 0) return true;  // (a node without the key adds nothing)
           cnt = a.t.zsum[(int64_t)t * a.t.ndom + z];
         }
         score = __dadd_rn(score, __dadd_rn(__dmul_rn((double)cnt, tw[t]), (double)(tp_param(w) - 1)));
-      }
+        return true;
+      });
       counted = !ignored;
       sr = ignored ? 0 : (long long)::round(score);
       a.sraw[i] = sr;
@@ -244,6 +286,7 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   const long long smin = s->smin, smax = s->smax, imin = s->imin, imax = s->imax;
   TopoRec tr;
   const int32_t pi = topo_cur(a, tr);
+  const TopoTerms tt = topo_terms_cur(a);
   KS_TOPO_ISSUED("v"(rs), "v"(tot0), "v"(dr), "v"(tr_), "v"(ar), "v"(rr), "v"(sri), "v"(iri));
   if (pi < 0) return;
   // the commit's pod records (wave 0 of every workgroup: the last one to finish uses them)
@@ -286,7 +329,7 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
     }
     long long pts = 100, ipa = 0;  // no constraint: NormalizeScore's maxScore == 0 gives MaxNodeScore
     if (dyn) {
-      const bool ig = soft_all && !topo_keys_ok(a, tr, KS_TOPO_K_SPREAD_SOFT, i);
+      const bool ig = soft_all && !topo_keys_ok(a, tr, tt, topo_node_dom(a.t, i)).soft;
       if (ig) pts = 0;
       else if (smax != 0) pts = 100 * (smax + smin - sri) / smax;
       const long long diff = imax - imin;
@@ -306,15 +349,15 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   if (dyn) {
     const int64_t stride = (int64_t)gridDim.x * kTopoThreads;
     const int64_t g = (int64_t)blockIdx.x * kTopoThreads + tid;
-    for (int t = 0; t < tr.nterms; ++t) {
-      const uint64_t w = topo_term(a, tr, t);
-      if (tp_key(w) == 0) continue;
+    topo_each(a, tr, tt, [&](int t, uint64_t w) {
+      if (tp_key(w) == 0) return true;
       for (int64_t z = g; z < a.t.ndom; z += stride) a.t.zsum[(int64_t)t * a.t.ndom + z] = 0;
       for (int64_t k = g; k < a.t.nw; k += stride) {
         a.t.zpres[(int64_t)t * a.t.nw + k] = 0u;
         a.t.zsize[(int64_t)t * a.t.nw + k] = 0u;
       }
-    }
+      return true;
+    });
   }
   // the last workgroup: the commit or the one-candidate set, then the scratch back to its initial image.  The only
   // value handed between workgroups is `best`, an agent-scope atomic performed at the memory side: each wave waits

@@ -1290,6 +1290,10 @@ static int32_t rsv_nominate(const ko_sched *s, const ko_pod *p, int64_t n, const
     }
   }
   if (node_order && mo != INT64_MAX) *node_order = mo;
+  /* RunReservationFilterPlugins also runs DeviceShare's FilterReservation (deviceshare/plugin.go:322-358): for a pod
+   * with device requests it fails for every reservation whose reserve pod holds no device (RestoreReservation's
+   * matched list, reservation.go:133-171, keeps only device-holding ones) -- every reservation modelled here */
+  if (s->cfg.deviceshare.enable && (p->has_gpu || p->rdma > 0)) return -1;
   return by_order >= 0 ? by_order : by_score;
 }
 

@@ -6,7 +6,9 @@ allocated NUMA nodes (calculateAllocatableAndRequested falls back to the restore
 DeviceShare's own RestoreReservation hooks (nodenumaresource/reservation.go:68-115, deviceshare/reservation.go) give
 nothing back for reservations that hold no cpuset and no device, which is what these reservations are.  Whole queues
 against the oracle: placements, scores, statuses, nominated reservations, GPU / RDMA minors, cpusets, and the node,
-reservation, device, CPU and NUMA-node state after every commit; single-pod Filter / Score parity."""
+reservation, device, CPU and NUMA-node state after every commit; single-pod Filter / Score parity.  A pod with device
+requests is never nominated into (nor assumed into) one of these reservations: DeviceShare's FilterReservation rejects
+a reservation that holds no device."""
 import numpy as np
 import pytest
 
@@ -65,14 +67,18 @@ def coverage(w, got):
     bind = (w.pods.flags & abi.KS_POD_CPU_BIND) != 0
     return {"placed": int(ok.sum()), "on_policy": int(onpol.sum()), "into_rsv": int(into.sum()),
             "into_rsv_on_policy": int((into & onpol).sum()), "dev_into_rsv": int((into & dev).sum()),
-            "bind_into_rsv": int((into & bind).sum())}
+            "bind_into_rsv": int((into & bind).sum()),
+            "dev_matched_placed": int((ok & dev & (w.pods.rsv_class >= 0)).sum())}
 
 
 def test_shipped_profile_5k_nodes(runtime, oracle_lib):
     """5k C3 nodes (half SingleNUMANode) with 12.5k reservations, 10k pods"""
     w = synth.c3_rsv()
     c = coverage(w, check(runtime, oracle_lib, w, "c3rsv-5k"))
-    assert c["into_rsv_on_policy"] > 300 and c["dev_into_rsv"] > 300 and c["bind_into_rsv"] > 300, c
+    # a device pod is never assumed into a reservation holding no device (DeviceShare's FilterReservation,
+    # deviceshare/plugin.go:322-358), though the restore still frees the matched reservations' resources for it
+    assert c["into_rsv_on_policy"] > 300 and c["bind_into_rsv"] > 300 and c["dev_matched_placed"] > 300, c
+    assert c["dev_into_rsv"] == 0, c
 
 
 @pytest.mark.parametrize("seed,policy", [

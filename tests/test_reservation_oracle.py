@@ -190,3 +190,25 @@ def test_score_with_order_cluster():
     assert scores[:, abi.KS_SCORE_RESERVATION].tolist() == [10, 10, 10, 100]
     res = o.schedule(pod)
     assert res["node"][0] == 3 and res["reservation"][0] == 3
+
+
+def test_device_pods_never_nominated_into_device_less_reservations():
+    """DeviceShare's FilterReservation (deviceshare/plugin.go:322-358) fails for a reservation whose reserve pod holds
+    no device when the pod has device requests, so NominateReservation (nominator.go:163-168) skips it and Reserve
+    (reservation/plugin.go:546-560) assumes the pod into none; with DeviceShare off the same pods go into them."""
+    from koordinator_amd import synth
+
+    w = synth.c3_rsv(seed=91, n_nodes=150, n_pods=400, policy_frac=0.3)
+    dev = (w.pods.gpu_core + w.pods.gpu_memory + w.pods.gpu_memory_ratio + w.pods.rdma) > 0
+    orc = Oracle(w.cfg, w.nodes.copy(), **w.tables())
+    got = orc.schedule(w.pods)
+    orc.close()
+    placed = got["status"] == abi.KS_S_SCHEDULED
+    assert (placed & dev & (w.pods.rsv_class >= 0)).sum() > 20
+    assert not (dev & (got["reservation"] >= 0)).any()
+    assert ((~dev) & (got["reservation"] >= 0)).sum() > 20
+    w.profile.deviceshare = None
+    orc = Oracle(w.cfg, w.nodes.copy(), **w.tables())
+    got2 = orc.schedule(w.pods)
+    orc.close()
+    assert (dev & (got2["reservation"] >= 0)).sum() > 10
