@@ -62,7 +62,9 @@ def build_workload(name: str, seed: int, n_pods: int = 0):
         w = synth.with_topology(w, seed=seed + 9)
         w.name = "C2-default"
         return w
-    fn = {"c2s": synth.c2_default, "c3r": synth.c3_rsv, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
+    # c3r: 70 % of the reservations on non-policy device nodes hold GPUs / RDMA (about a third of all of them)
+    c3r = lambda **kw: synth.c3_rsv(dev_rsv_frac=0.7, **kw)  # noqa: E731
+    fn = {"c2s": synth.c2_default, "c3r": c3r, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
 

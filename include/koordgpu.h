@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define KS_ABI_VERSION 9
+#define KS_ABI_VERSION 10
 
 #define KS_MAX_SCALARS 4 /* scalar (extended) resource slots, e.g. kubernetes.io/batch-cpu */
 #define KS_QUOTA_DIMS 8  /* resource dimensions tracked by ElasticQuota admission */
@@ -60,6 +60,10 @@ extern "C" {
 #define KS_MAX_RDMA 8     /* RDMA minors per node (ks_device_cols); minor = slot index */
 #define KS_MAX_PCIE 8     /* PCIe switches per node (ks_device_cols.pcie_*) */
 #define KS_PCIE_NONE 0xFFu /* device without topology (DeviceInfo.Topology == nil) */
+/* device words of one reservation's device resources (ks_reservation_cols.dev_*): GPU minor k's gpu-core at k,
+ * gpu-memory at KS_MAX_GPUS + k, gpu-memory-ratio at 2 * KS_MAX_GPUS + k; RDMA minor j's koordinator.sh/rdma at
+ * 3 * KS_MAX_GPUS + j */
+#define KS_DEV_WORDS (3 * KS_MAX_GPUS + KS_MAX_RDMA)
 #define KS_MAX_CPUS 256   /* logical CPUs per node topology (ks_cpu_topology); CPU ids 0..ncpus-1 */
 #define KS_CPU_WORDS 4    /* uint64 words of a CPU set (bit c = CPU c) */
 #define KS_MAX_NUMA 8     /* NUMA nodes per node (ks_numa_node_cols); the device evaluates up to 4 */
@@ -209,8 +213,11 @@ extern "C" {
 
 /* ---- per-node DeviceShare flags (ks_device_cols.flags) ---- */
 #define KS_DEV_PRESENT 0x1u /* nodeDeviceCache.getNodeDevice != nil (deviceshare/plugin.go:286-289) */
-#define KS_DEV_UNMODELLED 0x2u /* the node has preemptible device capacity (device_cache.go:314) or device-holding
-                                  reservations (deviceshare/reservation.go): ks_load_devices / ks_update_devices refuse it */
+#define KS_DEV_UNMODELLED 0x2u /* set by the shim for device state the library does not model on the node (FPGA or
+                                  VF-allocated devices): ks_load_devices / ks_update_devices refuse it.  Device-holding
+                                  reservations are modelled (ks_reservation_cols.dev_*); preemptible device capacity
+                                  (device_cache.go:314) exists only inside a preemption dry run, which ks_preempt refuses
+                                  with DeviceShare */
 
 /* ---- reservation flags (ks_reservation_cols.flags) ---- */
 #define KS_RSV_UNSCHEDULABLE 0x1u /* ReservationInfo.IsUnschedulable (transformer.go:113)              */
@@ -563,6 +570,13 @@ typedef struct ks_reservation_cols {
   const int32_t *assigned;        /* len(AssignedPods); NULL = 0 */
   const int64_t *reserve_nonzero_milli_cpu; /* reserve pod's NonZeroRequested; NULL = from allocatable */
   const int64_t *reserve_nonzero_memory;
+  /* DeviceShare (deviceshare/reservation.go:118-171): [r * KS_DEV_WORDS + w] the reserve pod's device allocation
+   * (nodeDeviceCache.getUsed of the reserve pod: the reservation's allocatable per minor; a minor with a non-zero word
+   * is one of its minors) and the allocations of its assigned pods on those minors (appendAllocatedByHints).  NULL =
+   * no reservation holds a device / nothing allocated.  The node's device used (ks_device_cols.used_*) counts both, as
+   * nodeDeviceCache does.  Reservations holding devices on a node with a NUMA topology policy are not supported. */
+  const int64_t *dev_allocatable;
+  const int64_t *dev_allocated;
 } ks_reservation_cols;
 
 /* Node GPU devices (nodeDeviceCache, deviceshare/device_cache.go): per minor k the device total and
@@ -813,6 +827,9 @@ int ks_add_reservations(ks_ctx *ctx, const ks_reservation_cols *rsv, int32_t r, 
 int ks_delete_reservations(ks_ctx *ctx, const int32_t *rows, int32_t m);
 /* Allocated (r*KS_RSV_DIMS, row-major) and len(AssignedPods) after commits; NULL = skip. */
 int ks_read_reservations(ks_ctx *ctx, int64_t *allocated, int32_t *assigned);
+/* The assigned pods' device allocations on each reservation's minors after commits ([r*KS_DEV_WORDS + w], the
+ * layout of ks_reservation_cols.dev_allocated; zeros without device-holding reservations) */
+int ks_read_reservation_devices(ks_ctx *ctx, int64_t *dev_allocated);
 
 /* RefreshRuntime for every quota of the tree at once, on the device
  * (replaces GroupQuotaManager.RefreshRuntime, group_quota_manager.go:259-326, with the request

@@ -8,12 +8,18 @@ from __future__ import annotations
 
 import ctypes as C
 
-KS_ABI_VERSION = 9
+KS_ABI_VERSION = 10
 KS_MAX_SCALARS = 4
 KS_QUOTA_DIMS = 8
 KS_MAX_GPUS = 8
 KS_MAX_RDMA = 8
 KS_MAX_PCIE = 8
+KS_DEV_WORDS = 3 * 8 + 8  # ks_reservation_cols.dev_*: GPU minor k core / memory / ratio at k, 8 + k, 16 + k; RDMA j at 24 + j
+
+
+def dev_word(kind: str, minor: int, q: int = 0) -> int:
+    """word of the KS_DEV_WORDS layout: kind "gpu" (q = 0 core, 1 memory, 2 ratio) or "rdma" """
+    return q * KS_MAX_GPUS + minor if kind == "gpu" else 3 * KS_MAX_GPUS + minor
 KS_PCIE_NONE = 0xFF
 KS_JOINT_NONE = 0
 KS_POD_UNMODELLED = 0x100
@@ -378,6 +384,8 @@ class KsReservationCols(C.Structure):
         ("assigned", P32),
         ("reserve_nonzero_milli_cpu", P64),
         ("reserve_nonzero_memory", P64),
+        ("dev_allocatable", P64),
+        ("dev_allocated", P64),
     ]
 
 
@@ -488,6 +496,7 @@ EXPORTED_SYMBOLS = [
     "ks_read_numa_nodes",
     "ks_load_reservations",
     "ks_read_reservations",
+    "ks_read_reservation_devices",
     "ks_refresh_quota_runtime",
     "ks_schedule",
     "ks_stage_pods",

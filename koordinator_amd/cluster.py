@@ -544,10 +544,14 @@ class NumaNodes:
 class ReservationTable:
     """Available reservations (ks_reservation_cols): one row per ReservationInfo
     (pkg/scheduler/frameworkext/reservation_info.go:37-115); resources [dim][row] with dims
-    cpu (milli), memory, ephemeral-storage, scalar[k]."""
+    cpu (milli), memory, ephemeral-storage, scalar[k].  DeviceShare (deviceshare/reservation.go): dev_allocatable /
+    dev_allocated [row][KS_DEV_WORDS] (abi.dev_word) are the reserve pod's device allocation and its assigned pods'
+    allocations on those minors; None = no reservation holds a device."""
 
     def __init__(self, r: int):
         self.r = int(r)
+        self.dev_allocatable = None
+        self.dev_allocated = None
         D = abi.KS_RSV_DIMS
         self.node = np.zeros(self.r, np.int32)
         self.owner_classes = np.zeros(self.r, np.uint64)
@@ -564,7 +568,17 @@ class ReservationTable:
         for k in ("node", "owner_classes", "flags", "policy", "order", "key_mask", "allocatable", "allocated",
                   "assigned"):
             setattr(t, k, getattr(self, k).copy())
+        for k in ("dev_allocatable", "dev_allocated"):
+            v = getattr(self, k)
+            setattr(t, k, None if v is None else v.copy())
         return t
+
+    def hold_devices(self) -> "ReservationTable":
+        """allocate the device columns (zeros)"""
+        if self.dev_allocatable is None:
+            self.dev_allocatable = np.zeros((self.r, abi.KS_DEV_WORDS), np.int64)
+            self.dev_allocated = np.zeros((self.r, abi.KS_DEV_WORDS), np.int64)
+        return self
 
     def ks(self) -> abi.KsReservationCols:
         c = abi.KsReservationCols()
@@ -582,6 +596,11 @@ class ReservationTable:
         for d in range(abi.KS_RSV_DIMS):
             c.allocatable[d] = _p64(self.allocatable[d])
             c.allocated[d] = _p64(self.allocated[d])
+        if self.dev_allocatable is not None:
+            self.dev_allocatable = np.ascontiguousarray(self.dev_allocatable, np.int64).reshape(self.r, abi.KS_DEV_WORDS)
+            self.dev_allocated = np.ascontiguousarray(self.dev_allocated, np.int64).reshape(self.r, abi.KS_DEV_WORDS)
+            c.dev_allocatable = _p64(self.dev_allocatable)
+            c.dev_allocated = _p64(self.dev_allocated)
         c._keep = self
         return c
 

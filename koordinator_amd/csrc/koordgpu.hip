@@ -1052,6 +1052,7 @@ struct ks_ctx {
     std::vector<uint32_t> flags, policy, key_mask;
     std::vector<int64_t> order, rnz_cpu, rnz_mem;
     std::vector<int64_t> alloc[kRsvDims], allocd[kRsvDims];
+    std::vector<int64_t> dal, dald;  // [row * KS_DEV_WORDS + w]
     std::vector<uint8_t> live;
   } rmir;
   // DeviceShare GPUs (ks_dev.h)
@@ -1090,6 +1091,9 @@ struct ks_ctx {
   std::vector<int32_t> h_dev_assumed, h_dev_assumed_ckpt;
   std::vector<int8_t> h_numa_k;    // per node: NUMA node count of a policy node (0 = no policy / none)
   std::vector<uint16_t> h_dev_ids; // per node: NUMA ids of the device topology (DeviceShare hints)
+  std::vector<uint8_t> h_pol;      // per node: a NUMA topology policy (numa_flags)
+  std::vector<uint8_t> h_dev_held; // per node: a reservation on it holds devices (kDevRsvHeld)
+  int64_t* rsv_dald_ckpt = nullptr;  // checkpoint of the reservations' device allocated
   std::vector<int8_t> h_cpu_nn;    // per node: NUMA nodes of its CPU topology (0 = none, -1 = ids not 0..n-1)
   std::vector<CpuTopo> h_topos;    // the loaded CPU topologies (ks_update_cpu_state refers to them)
   std::vector<int8_t> h_topo_dense;
@@ -1887,7 +1891,9 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
   // NUMA topology policies: an empty NUMA-node table until ks_load_numa_nodes
   ctx->numa_policy_nodes = 0;
   ctx->cpu_bind_labels = false;
+  ctx->h_pol.assign((size_t)n, 0);
   for (int64_t i = 0; ctx->cfg.numa.enable && nodes->numa_flags && i < n; ++i) {
+    ctx->h_pol[(size_t)i] = ((nodes->numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u) != 0;
     ctx->numa_policy_nodes += ((nodes->numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u) != 0;
     ctx->cpu_bind_labels |= ((nodes->numa_flags[i] >> KS_NUMA_CPU_BIND_SHIFT) & 3u) != 0;
   }
@@ -1901,6 +1907,27 @@ int ks_load_nodes(ks_ctx* ctx, const ks_node_cols* nodes, int64_t n) {
     ctx->kc.monotone_nd = 0;
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KS_OK;
+}
+
+// kDevRsvHeld into the device table's node flags from h_dev_held (after a reservation or a device install)
+__global__ void dev_held_kernel(uint32_t* flags, const uint8_t* held, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  flags[i] = (flags[i] & ~kDevRsvHeld) | (held[i] ? kDevRsvHeld : 0u);
+}
+
+static int dev_apply_held(ks_ctx* ctx) {
+  if (!ctx->dev_blob || ctx->n == 0) return KS_OK;
+  if (ctx->h_dev_held.size() != (size_t)ctx->n) ctx->h_dev_held.assign((size_t)ctx->n, 0);
+  void* p = nullptr;
+  if (dev_alloc(ctx, &p, (size_t)ctx->n) != KS_OK) return KS_ENOMEM;
+  HIPCHK(ctx, hipMemcpyAsync(p, ctx->h_dev_held.data(), (size_t)ctx->n, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(dev_held_kernel, dim3((unsigned)((ctx->n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     const_cast<uint32_t*>(ctx->dv.flags), (const uint8_t*)p, ctx->n);
+  HIPCHK(ctx, hipGetLastError());
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  dev_free(p);
   return KS_OK;
 }
 
@@ -1934,6 +1961,25 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
     if (check_range64(ctx, rc->reserve_nonzero_milli_cpu, nr, "reserve_nonzero_milli_cpu") != KS_OK) return KS_EINVAL;
     if (check_range64(ctx, rc->reserve_nonzero_memory, nr, "reserve_nonzero_memory") != KS_OK) return KS_EINVAL;
   }
+  // DeviceShare reservations (deviceshare/reservation.go): a reservation holding devices on a NUMA-policy node is
+  // refused (the topology hints would run tryAllocateFromReservation per NUMA mask)
+  std::vector<uint8_t> held((size_t)ctx->n, 0);
+  const bool devr = rc && rc->dev_allocatable;
+  if (devr) {
+    if (check_range64(ctx, rc->dev_allocatable, (int64_t)nr * KS_DEV_WORDS, "reservation dev_allocatable") != KS_OK ||
+        check_range64(ctx, rc->dev_allocated, (int64_t)nr * KS_DEV_WORDS, "reservation dev_allocated") != KS_OK)
+      return KS_EINVAL;
+    if (!ctx->cfg.deviceshare.enable) KS_FAIL(ctx, KS_ESTATE, "reservations hold devices but DeviceShare is not enabled");
+    for (int32_t r = 0; r < nr; ++r) {
+      bool h = false;
+      for (int w = 0; w < KS_DEV_WORDS; ++w) h |= rc->dev_allocatable[(size_t)r * KS_DEV_WORDS + w] != 0;
+      if (!h) continue;
+      if ((size_t)rc->node[r] < ctx->h_pol.size() && ctx->h_pol[(size_t)rc->node[r]])
+        KS_FAIL(ctx, KS_EUNSUPPORTED, "reservation %d holds devices on node %d, which has a NUMA topology policy", r,
+                rc->node[r]);
+      held[(size_t)rc->node[r]] = 1;
+    }
+  }
   // order labels -> composite ranks (smaller label = larger hi)
   std::vector<int64_t> ords;
   for (int32_t r = 0; r < nr; ++r)
@@ -1958,7 +2004,8 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
                o_ohi = o_meta + al16(m * 4), o_alloc = o_ohi + al16(m * 4), o_allocd = o_alloc + al16(D * m * 8),
                o_asg = o_allocd + al16(D * m * 8), o_rnz = o_asg + al16(m * 4), o_row = o_rnz + al16(2 * m * 8),
                o_ck_allocd = o_row + al16(m * 4), o_ck_asg = o_ck_allocd + al16(D * m * 8),
-               bytes = o_ck_asg + al16(m * 4);
+               o_dal = o_ck_asg + al16(m * 4), o_dald = o_dal + al16((size_t)kDevQW * m * 8),
+               o_ck_dald = o_dald + al16((size_t)kDevQW * m * 8), bytes = o_ck_dald + al16((size_t)kDevQW * m * 8);
   std::vector<char> h(bytes, 0);
   int32_t* beg = (int32_t*)(h.data() + o_beg);
   uint64_t* cls = (uint64_t*)(h.data() + o_cls);
@@ -1969,6 +2016,8 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
   int32_t* asg = (int32_t*)(h.data() + o_asg);
   int64_t* rnz = (int64_t*)(h.data() + o_rnz);
   int32_t* rowid = (int32_t*)(h.data() + o_row);
+  int64_t* dal = (int64_t*)(h.data() + o_dal);
+  int64_t* dald = (int64_t*)(h.data() + o_dald);
   for (int32_t i = 0; i < nr; ++i) beg[rc->node[perm[i]] + 1]++;
   for (int64_t n = 0; n < ctx->npad; ++n) beg[n + 1] += beg[n];
   ctx->h_rsv_gi.assign((size_t)ncaller, -1);
@@ -1985,6 +2034,15 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
     for (int d = 0; d < D; ++d)
       if ((rc->allocatable[d] && rc->allocatable[d][r]) || (rc->allocated[d] && rc->allocated[d][r])) nd = d + 1;
     meta[i] = flags | (pol << 4) | (rc->key_mask[r] << 8) | ((uint32_t)nd << 16);
+    if (devr) {
+      bool h = false;
+      for (int w = 0; w < kDevQW; ++w) {
+        dal[(size_t)w * m + i] = rc->dev_allocatable[(size_t)r * KS_DEV_WORDS + w];
+        dald[(size_t)w * m + i] = rc->dev_allocated ? rc->dev_allocated[(size_t)r * KS_DEV_WORDS + w] : 0;
+        h |= dal[(size_t)w * m + i] != 0;
+      }
+      if (h) meta[i] |= kRsvMetaDev;
+    }
     const int64_t o = rc->order ? rc->order[r] : 0;
     if (o != 0) {
       const int64_t rank = std::lower_bound(ords.begin(), ords.end(), o) - ords.begin();
@@ -2016,6 +2074,9 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
   rv.assigned = (int32_t*)(b + o_asg);
   rv.rnz = (const int64_t*)(b + o_rnz);
   rv.rowid = (const int32_t*)(b + o_row);
+  rv.dal = (const int64_t*)(b + o_dal);
+  rv.dald = (int64_t*)(b + o_dald);
+  ctx->rsv_dald_ckpt = (int64_t*)(b + o_ck_dald);
   rv.ncls = ctx->d.rsv_cls;
   rv.nr = (int64_t)m;  // row stride of the [dim][row] tables
   rv.w100 = 100 * ctx->cfg.reservation.plugin_weight;
@@ -2035,6 +2096,8 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
   if (upload_rowcols(ctx) != KS_OK) return KS_ENOMEM;  // row fields RF_RSV_BEG / RF_RSV_END
   if (rsv_launch_base(ctx, nullptr, ctx->n, +1, 1) != KS_OK) return KS_EHIP;
   ctx->rsv_based = true;
+  ctx->h_dev_held = held;
+  if (dev_apply_held(ctx) != KS_OK) return KS_EHIP;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   return KS_OK;
 }
@@ -2153,6 +2216,7 @@ static int dev_install(ks_ctx* ctx, const ks_device_cols* dc) {
   HIPCHK(ctx, hipMemcpyAsync(ctx->ddv, &ctx->dv, sizeof(DevDev), hipMemcpyHostToDevice, ctx->stream));
   ctx->dev_loaded = dc != nullptr;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (dev_apply_held(ctx) != KS_OK) return KS_EHIP;
   return check_dev_numa(ctx);
 }
 
@@ -2636,6 +2700,10 @@ static void rsv_mirror_append(ks_ctx* ctx, const ks_reservation_cols* rc, int32_
                                                       : ((keys & 1u) ? M.alloc[0].back() : kDefaultMilliCPU));
     M.rnz_mem.push_back(rc->reserve_nonzero_memory ? rc->reserve_nonzero_memory[r]
                                                    : ((keys & 2u) ? M.alloc[1].back() : kDefaultMemory));
+    for (int w = 0; w < KS_DEV_WORDS; ++w) {
+      M.dal.push_back(rc->dev_allocatable ? rc->dev_allocatable[(size_t)r * KS_DEV_WORDS + w] : 0);
+      M.dald.push_back(rc->dev_allocatable && rc->dev_allocated ? rc->dev_allocated[(size_t)r * KS_DEV_WORDS + w] : 0);
+    }
     M.live.push_back(1);
   }
 }
@@ -2666,11 +2734,14 @@ static int rsv_reinstall(ks_ctx* ctx) {
     std::vector<int32_t> as(m);
     HIPCHK(ctx, hipMemcpyAsync(ad.data(), ctx->rv.allocd, ad.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(as.data(), ctx->rv.assigned, m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<int64_t> dd((size_t)kDevQW * m);
+    HIPCHK(ctx, hipMemcpyAsync(dd.data(), ctx->rv.dald, dd.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     for (int32_t i = 0; i < ctx->rsv_live; ++i) {
       const int32_t r = ctx->rsv_perm[(size_t)i];
       for (int d = 0; d < kRsvDims; ++d) M.allocd[d][(size_t)r] = ad[(size_t)d * m + i];
       M.assigned[(size_t)r] = as[(size_t)i];
+      for (int w = 0; w < kDevQW; ++w) M.dald[(size_t)r * KS_DEV_WORDS + w] = dd[(size_t)w * m + i];
     }
   }
   std::vector<int32_t> caller;
@@ -2707,6 +2778,18 @@ static int rsv_reinstall(ks_ctx* ctx) {
     allocd[d] = pick64(M.allocd[d]);
     rc.allocatable[d] = alloc[d].data();
     rc.allocated[d] = allocd[d].data();
+  }
+  std::vector<int64_t> dal((size_t)nl * KS_DEV_WORDS), dald((size_t)nl * KS_DEV_WORDS);
+  bool anyd = false;
+  for (int32_t i = 0; i < nl; ++i)
+    for (int w = 0; w < KS_DEV_WORDS; ++w) {
+      dal[(size_t)i * KS_DEV_WORDS + w] = M.dal[(size_t)caller[(size_t)i] * KS_DEV_WORDS + w];
+      dald[(size_t)i * KS_DEV_WORDS + w] = M.dald[(size_t)caller[(size_t)i] * KS_DEV_WORDS + w];
+      anyd |= dal[(size_t)i * KS_DEV_WORDS + w] != 0;
+    }
+  if (anyd) {
+    rc.dev_allocatable = dal.data();
+    rc.dev_allocated = dald.data();
   }
   return rsv_install(ctx, &rc, nl, caller.data(), total);
 }
@@ -2760,8 +2843,27 @@ int ks_read_reservations(ks_ctx* ctx, int64_t* allocated, int32_t* assigned) {
   return KS_OK;
 }
 
+int ks_read_reservation_devices(ks_ctx* ctx, int64_t* dev_allocated) {
+  if (!ctx) return KS_EINVAL;
+  const int32_t nr = ctx->rsv_live;
+  if (!dev_allocated || nr == 0 || !ctx->rsv_blob) return KS_OK;
+  const size_t m = (size_t)ctx->rv.nr;
+  std::vector<int64_t> dd((size_t)kDevQW * m);
+  HIPCHK(ctx, hipMemcpyAsync(dd.data(), ctx->rv.dald, dd.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  for (int32_t i = 0; i < nr; ++i) {
+    const int32_t r = ctx->rsv_perm[(size_t)i];
+    for (int w = 0; w < KS_DEV_WORDS; ++w) dev_allocated[(size_t)r * KS_DEV_WORDS + w] = dd[(size_t)w * m + i];
+  }
+  return KS_OK;
+}
+
 int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, int64_t m) {
   if (!ctx || !idx || !rows || m < 0) return ctx ? (ctx->err = "ks_update_nodes: bad args", KS_EINVAL) : KS_EINVAL;
+  for (int64_t i = 0; ctx->cfg.numa.enable && rows->numa_flags && i < m; ++i)
+    if (idx[i] >= 0 && (size_t)idx[i] < ctx->h_dev_held.size() && ctx->h_dev_held[(size_t)idx[i]] &&
+        ((rows->numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u))
+      KS_FAIL(ctx, KS_EUNSUPPORTED, "node %d: a NUMA topology policy on a node whose reservations hold devices", idx[i]);
   if (!ctx->node_blob) KS_FAIL(ctx, KS_ESTATE, "ks_update_nodes before ks_load_nodes");
   if (m == 0) return KS_OK;
   for (int64_t i = 0; i < m; ++i)
@@ -2819,8 +2921,10 @@ int ks_update_nodes(ks_ctx* ctx, const int32_t* idx, const ks_node_cols* rows, i
   // the replaced rows are the reference's NodeInfo: add the reservation base restore again
   if (ctx->rsv_based && rsv_launch_base(ctx, (const int32_t*)((char*)dbuf + idx_off), m, +1, 0) != KS_OK) return KS_EHIP;
   if (upload_prep_nodes(ctx) != KS_OK) return KS_EHIP;
-  for (int64_t i = 0; ctx->cfg.numa.enable && rows->numa_flags && i < m; ++i)
+  for (int64_t i = 0; ctx->cfg.numa.enable && rows->numa_flags && i < m; ++i) {
     ctx->cpu_bind_labels |= ((rows->numa_flags[i] >> KS_NUMA_CPU_BIND_SHIFT) & 3u) != 0;
+    if ((size_t)idx[i] < ctx->h_pol.size()) ctx->h_pol[(size_t)idx[i]] = ((rows->numa_flags[i] >> KS_NUMA_POLICY_SHIFT) & 3u) != 0;
+  }
   // (the union only grows: a stale bit only withholds the fast path from a pod)
   for (int64_t i = 0; rows->taints_soft && i < m; ++i) ctx->soft_union |= rows->taints_soft[i];
   cores_mode(ctx);
@@ -4412,6 +4516,7 @@ int ks_checkpoint(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->numa_ckpt, ctx->nv.used, numa_mut_bytes((size_t)ctx->npad), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_allocd_ckpt, ctx->rv.allocd, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_dald_ckpt, ctx->rv.dald, (size_t)kDevQW * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rsv_assigned_ckpt, ctx->rv.assigned, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
   }
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -4435,6 +4540,7 @@ int ks_restore(ks_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->nv.used, ctx->numa_ckpt, numa_mut_bytes((size_t)ctx->npad), hipMemcpyDeviceToDevice, ctx->stream));
   if (ctx->rsv_blob) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.allocd, ctx->rsv_allocd_ckpt, (size_t)kRsvDims * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rv.dald, ctx->rsv_dald_ckpt, (size_t)kDevQW * ctx->rv.nr * 8, hipMemcpyDeviceToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rv.assigned, ctx->rsv_assigned_ckpt, (size_t)ctx->rv.nr * 4, hipMemcpyDeviceToDevice, ctx->stream));
   }
   ctx->h_dev_assumed = ctx->h_dev_assumed_ckpt;
@@ -4514,6 +4620,7 @@ int ks_update_devices(ks_ctx* ctx, const int32_t* idx, const ks_device_cols* row
     return KS_EHIP;
   for (int64_t i = 0; i < m; ++i) ctx->h_dev_ids[(size_t)ix[i]] = ids[(size_t)i];
   ctx->dev_loaded = true;
+  if (dev_apply_held(ctx) != KS_OK) return KS_EHIP;
   return check_dev_numa(ctx);
 }
 
@@ -4767,6 +4874,11 @@ __global__ void unreserve_kernel(UnreserveArgs a) {
       }
       for (int j = 0; j < kRdma; ++j)
         if ((a.rmin >> j) & 1u) a.dv.used[(int64_t)(kDevRdmaW + j) * a.dv.npad + n] -= g.rdma;
+      // the pod leaves its reservation's AssignedPods: its allocation on the reservation's minors too
+      if (a.gi >= 0 && (a.rv.meta[a.gi] & kRsvMetaDev)) {
+        const RsvG<true> gv(a.rv, n);
+        rsv_dev_assign(a.rv, gv, a.gi - gv.b, g, a.gmin, a.rmin, -1);
+      }
     }
   }
   // NodeAllocation.release (node_allocation.go:105-131): the CPUs (reference count 1 -> removed) and the

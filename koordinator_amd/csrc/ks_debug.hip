@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void eval_debug_kernel(DevNodes d, const DevRs
     const PodStat* ps = pstat ? pstat + pi : nullptr;
     RsvOut ro;
     EvalOut o = eval_full<NSC, true, false, FEAT>(
-        c, p, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*rv, i), p, r, dl); },
+        c, p, r, [&](auto&& f) { return f(RsvG<false>(*rv, i)); },
         [&]() { return DevGView{*dv, i}; }, [&]() { return NumaGView{*nv, i}; }, &ro);
     if (c.stat) stat_eval(c, *ps, th, ts, lb, hp, o);
     reasons[i] = o.reasons;

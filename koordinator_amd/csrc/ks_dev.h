@@ -37,9 +37,14 @@ constexpr int kDevQW = 3 * kGpus + kRdma;  // quantity words (totals and used)
 constexpr int kDevTopoW = kDevQW;
 constexpr int kDevMetaW = kDevQW + 1;
 constexpr int kDevTW = kDevQW + 2;  // total-table words
+static_assert(kDevQW == KS_DEV_WORDS, "the reservation device words (ks_reservation_cols.dev_*) are the quantity words");
+
+// internal node flag (DevDev.flags): a reservation on the node holds devices -- DeviceShare then runs with the
+// node's reservation restore state (ks_rsv.h dev_rsv_*)
+constexpr uint32_t kDevRsvHeld = 0x100u;
 
 struct DevDev {
-  const uint32_t* flags;  // [npad] KS_DEV_*
+  const uint32_t* flags;  // [npad] KS_DEV_* | kDevRsvHeld
   const int64_t* total;   // [kDevTW][npad]
   int64_t* used;          // [kDevQW][npad]  mutable (Reserve)
   int64_t npad;
@@ -50,7 +55,9 @@ struct DevGView {
   const DevDev& d;
   int64_t n;
   __device__ __forceinline__ bool present() const { return (gld(d.flags + n) & KS_DEV_PRESENT) != 0; }
+  __device__ __forceinline__ bool held() const { return (gld(d.flags + n) & kDevRsvHeld) != 0; }
   __device__ __forceinline__ int64_t tot(int w) const { return gld(d.total + (int64_t)w * d.npad + n); }
+  __device__ __forceinline__ int64_t ptot(int w) const { return tot(w); }  // (Prepare's unfiltered node device)
   __device__ __forceinline__ int64_t use(int w) const { return gld(d.used + (int64_t)w * d.npad + n); }
 };
 
@@ -60,11 +67,21 @@ constexpr int kDevLdsStride = kMaxBatch + 1;
 struct DevLView {
   const int64_t* t;  // word w at t[w * kDevLdsStride]  (kDevTW words)
   const int64_t* u;  // (kDevQW words)
-  bool pres;
-  __device__ __forceinline__ bool present() const { return pres; }
+  uint32_t fl;       // the node's flags
+  __device__ __forceinline__ bool present() const { return (fl & KS_DEV_PRESENT) != 0; }
+  __device__ __forceinline__ bool held() const { return (fl & kDevRsvHeld) != 0; }
   __device__ __forceinline__ int64_t tot(int w) const { return t[w * kDevLdsStride]; }
+  __device__ __forceinline__ int64_t ptot(int w) const { return tot(w); }
   __device__ __forceinline__ int64_t use(int w) const { return u[w * kDevLdsStride]; }
 };
+
+// defaultAllocateDevices' minor sets from a reservation (deviceshare/reservation.go:201-240): preferred minors per
+// type (0 = none: the preferred-PCIe order applies; non-empty they replace it, sortDeviceResourcesByMinor) and
+// required minors (0xFF = every minor)
+struct DevPick {
+  uint32_t gpref, rpref, greq, rreq;
+};
+constexpr DevPick kNoPick{0u, 0u, 0xFFu, 0xFFu};
 
 // The pod's request per instance and desired count per device type on one node.
 struct GpuReq {
@@ -81,7 +98,7 @@ __device__ __forceinline__ uint32_t dev_prepare(const PodRec& p, const V& v, Gpu
     int64_t total_mem = -1;
 #pragma unroll
     for (int k = kGpus - 1; k >= 0; --k) {  // the first healthy minor (all GPUs of a node are the same model)
-      const int64_t tc = v.tot(k), tm = v.tot(kGpus + k), tr = v.tot(2 * kGpus + k);
+      const int64_t tc = v.ptot(k), tm = v.ptot(kGpus + k), tr = v.ptot(2 * kGpus + k);
       if (tc || tm || tr) total_mem = tm;
     }
     if (total_mem < 0) return KS_R_DEV_NO_GPU;
@@ -103,7 +120,7 @@ __device__ __forceinline__ uint32_t dev_prepare(const PodRec& p, const V& v, Gpu
   if (p.rdma > 0) {
     bool any = false;
 #pragma unroll
-    for (int j = 0; j < kRdma; ++j) any |= v.tot(kDevRdmaW + j) != 0;
+    for (int j = 0; j < kRdma; ++j) any |= v.ptot(kDevRdmaW + j) != 0;
     if (!any) return KS_R_DEV_NO_RDMA;
     int64_t q = p.rdma;
     if (q > 100 && q % 100 == 0) {
@@ -158,15 +175,17 @@ struct DevType {
   __device__ __forceinline__ int score(int k) const { return (int)((sc >> (8 * k)) & 0xFFu); }
 };
 
-// defaultAllocateDevices over the fitting minors in `sub`: up to maxd minors in (preferred switch, score desc,
-// minor asc) order, at least `desired`; 0 = "Insufficient <type> devices"
-__device__ __forceinline__ uint32_t dev_take(const DevType& t, int nm, uint32_t sub, int desired, uint32_t pref) {
+// defaultAllocateDevices over the fitting minors in `sub` and the required set `rq`: up to maxd minors in (preferred,
+// score desc, minor asc) order -- preferred = the minor in `pm` when pm != 0, else its switch in `pref` --, at least
+// `desired`; 0 = "Insufficient <type> devices"
+__device__ __forceinline__ uint32_t dev_take(const DevType& t, int nm, uint32_t sub, int desired, uint32_t pref,
+                                             uint32_t pm = 0u, uint32_t rq = 0xFFu) {
   int maxd = desired;
   const int npref = __builtin_popcount(pref);
   maxd = npref > maxd ? npref : maxd;
   desired = desired == 0 ? 1 : desired;
   maxd = maxd < desired ? desired : maxd;
-  const uint32_t cand = t.fit & sub;
+  const uint32_t cand = t.fit & sub & rq;
   uint32_t mask = 0;
   int got = 0;
   for (int r = 0; r < maxd; ++r) {
@@ -176,7 +195,8 @@ __device__ __forceinline__ uint32_t dev_take(const DevType& t, int nm, uint32_t 
       if (k >= nm) break;
       const bool ok = ((cand >> k) & 1u) && !((mask >> k) & 1u);
       const uint32_t pc = t.pcie(k);
-      const int key = ((pc < 8u && ((pref >> pc) & 1u)) ? (1 << 12) : 0) | (t.score(k) << 4) | (15 - k);
+      const bool pr = pm ? ((pm >> k) & 1u) != 0 : (pc < 8u && ((pref >> pc) & 1u));
+      const int key = (pr ? (1 << 12) : 0) | (t.score(k) << 4) | (15 - k);
       best = (ok && key > bk) ? k : best;
       bk = (ok && key > bk) ? key : bk;
     }
@@ -205,13 +225,13 @@ __device__ __forceinline__ uint32_t dev_sub_of(const DevType& t, int nm, uint32_
 
 // jointAllocate (device_allocator.go:286-339) restricted to the switches `sw` (all minors if sw == ~0)
 __device__ __forceinline__ bool dev_joint(const DevType& G, const DevType& R, const GpuReq& g, bool same, uint32_t sw,
-                                          uint32_t pref, uint32_t& om, uint32_t& orm) {
+                                          uint32_t pref, uint32_t& om, uint32_t& orm, const DevPick& pk = kNoPick) {
   const uint32_t gs = sw == ~0u ? 0xFFu : dev_sub_of(G, kGpus, sw);
   const uint32_t rs = sw == ~0u ? 0xFFu : dev_sub_of(R, kRdma, sw);
-  const uint32_t prim = dev_take(G, kGpus, gs, g.desired, pref);
+  const uint32_t prim = dev_take(G, kGpus, gs, g.desired, pref, pk.gpref, pk.greq);
   if (!prim) return false;
   const uint32_t pc = dev_pcies_of(G, kGpus, prim);
-  const uint32_t sec = dev_take(R, kRdma, rs, same ? __builtin_popcount(pc) : 1, pc);
+  const uint32_t sec = dev_take(R, kRdma, rs, same ? __builtin_popcount(pc) : 1, pc, pk.rpref, pk.rreq);
   if (!sec) return false;
   om = prim;
   orm = sec;
@@ -222,7 +242,8 @@ __device__ __forceinline__ bool dev_joint(const DevType& G, const DevType& R, co
 // requests RDMA -- only then is a switch or a NUMA-node group `preferred` (newDeviceTopologyGuide splits the free devices
 // per requested type, numa_topology.go:109-135; a joint pod without an RDMA request has no RDMA entry there)
 __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType& R, const GpuReq& g, bool same,
-                                                uint64_t meta, uint32_t& om, uint32_t& orm, bool rpref = true) {
+                                                uint64_t meta, uint32_t& om, uint32_t& orm, bool rpref = true,
+                                                const DevPick& pk = kNoPick) {
   uint32_t exist = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -241,7 +262,7 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
   for (int p = 0; p < kPcie; ++p) {
     if (!((tryset >> p) & 1u)) continue;
     if (__builtin_popcount(G.fit & dev_sub_of(G, kGpus, 1u << p)) >= g.desired &&
-        dev_joint(G, R, g, same, 1u << p, 1u << p, om, orm))
+        dev_joint(G, R, g, same, 1u << p, 1u << p, om, orm, pk))
       return true;
   }
   // freeNodeDevicesInNode: one group per NUMA node, ordered by (|preferred switches| desc, preferred desc,
@@ -274,11 +295,11 @@ __device__ __forceinline__ bool dev_by_topology(const DevType& G, const DevType&
     done |= 1u << bi;
     const uint32_t sw = gsw[bi];
     if (__builtin_popcount(G.fit & dev_sub_of(G, kGpus, sw)) >= g.desired &&
-        dev_joint(G, R, g, same, sw, sw & swpref, om, orm))
+        dev_joint(G, R, g, same, sw, sw & swpref, om, orm, pk))
       return true;
   }
   // the whole node, preferring every preferred switch
-  return dev_joint(G, R, g, same, ~0u, swpref, om, orm);
+  return dev_joint(G, R, g, same, ~0u, swpref, om, orm, pk);
 }
 
 // The minors of each type on the NUMA nodes of `allow` (a bit per NUMA node id; ~0u = every minor): with a
@@ -303,7 +324,7 @@ __device__ __forceinline__ void dev_allowed(const V& v, uint32_t allow, uint32_t
 // NUMA affinity (dev_allowed).
 template <bool ALLOC, typename V>
 __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const V& v, GpuReq* req_out = nullptr,
-                                           uint32_t allow = ~0u) {
+                                           uint32_t allow = ~0u, const DevPick& pk = kNoPick) {
   DevOut o{0u, 0, 0u, 0u};
   if (!v.present()) return o;  // no device info: Filter passes, Score 0
   GpuReq g;
@@ -320,7 +341,8 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   // success takes >= desired GPUs and one RDMA device, a joint failure falls back to allocateDevices.  Only
   // the allocation itself (Reserve) needs the walk then.
   const bool walk = joint && (ALLOC || same || g.rdesired > 1);
-  const bool scores = ALLOC || walk;
+  // only Reserve's allocator has a scorer (deviceshare/plugin.go:404); Filter's walk sorts minors with score 0
+  const bool scores = ALLOC;
   uint32_t gin, rin;
   dev_allowed(v, allow, gin, rin);
   const uint64_t topo = (walk || ALLOC) ? (uint64_t)v.tot(kDevTopoW) : 0ull;
@@ -369,7 +391,7 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   uint32_t om = 0, orm = 0;
   bool jdone = false;
   if (walk) {
-    if (dev_by_topology(G, R, g, same, (uint64_t)v.tot(kDevMetaW), om, orm, has_rdma)) {
+    if (dev_by_topology(G, R, g, same, (uint64_t)v.tot(kDevMetaW), om, orm, has_rdma, pk)) {
       // validateJointAllocation (device_allocator.go:255-284)
       if (same && dev_pcies_of(G, kGpus, om) != dev_pcies_of(R, kRdma, orm)) {
         o.reasons = KS_R_DEV_JOINT;
@@ -383,13 +405,14 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
   }
   if (!jdone) {
     // allocateDevices per remaining type: feasibility is a count; the minors only with ALLOC
-    if ((has_gpu && __builtin_popcount(G.fit) < g.desired) || (has_rdma && __builtin_popcount(R.fit) < g.rdesired)) {
+    if ((has_gpu && __builtin_popcount(G.fit & pk.greq) < g.desired) ||
+        (has_rdma && __builtin_popcount(R.fit & pk.rreq) < g.rdesired)) {
       o.reasons = KS_R_DEV_INSUFFICIENT;
       return o;
     }
     if (ALLOC) {
-      om = has_gpu ? dev_take(G, kGpus, 0xFFu, g.desired, 0u) : 0u;
-      orm = has_rdma ? dev_take(R, kRdma, 0xFFu, g.rdesired, 0u) : 0u;
+      om = has_gpu ? dev_take(G, kGpus, 0xFFu, g.desired, 0u, pk.gpref, pk.greq) : 0u;
+      orm = has_rdma ? dev_take(R, kRdma, 0xFFu, g.rdesired, 0u, pk.rpref, pk.rreq) : 0u;
     }
   }
   o.raw = raw;
@@ -398,6 +421,41 @@ __device__ __forceinline__ DevOut dev_eval(const Cfg& c, const PodRec& p, const 
     o.rminors = orm;
   }
   return o;
+}
+
+// AutopilotAllocator.score alone (device_allocator.go:507-530): scoreNode per requested type over the view; a type
+// whose devices all have zero free is left out of the filtered node device (nodeDevice.filter, device_cache.go:351-353)
+template <typename V>
+__device__ __forceinline__ int32_t dev_raw(const Cfg& c, const PodRec& p, const V& v, const GpuReq& g) {
+  int32_t raw = 0;
+  if (p.flags & kPodGpuReq) {
+    const int64_t pod[3] = {g.core, g.mem, g.ratio};
+    int64_t tsum[3] = {0, 0, 0}, fsum[3] = {0, 0, 0};
+    bool anyf = false;
+    for (int k = 0; k < kGpus; ++k) {
+      const int64_t t[3] = {v.tot(k), v.tot(kGpus + k), v.tot(2 * kGpus + k)};
+      const int64_t u[3] = {v.use(k), v.use(kGpus + k), v.use(2 * kGpus + k)};
+      const bool exists = t[0] || t[1] || t[2];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int64_t f = t[q] > u[q] ? t[q] - u[q] : 0;
+        tsum[q] += exists ? t[q] : 0;
+        fsum[q] += exists ? f : 0;
+        anyf |= exists && f != 0;
+      }
+    }
+    if (anyf) raw += dev_score3(c, tsum, fsum, pod);
+  }
+  if (p.rdma > 0) {
+    int64_t tsum = 0, fsum = 0;
+    for (int j = 0; j < kRdma; ++j) {
+      const int64_t t = v.tot(kDevRdmaW + j), u = v.use(kDevRdmaW + j);
+      tsum += t;
+      fsum += t > u ? t - u : 0;
+    }
+    if (fsum) raw += dev_score1(c, tsum, fsum, g.rdma);
+  }
+  return raw;
 }
 
 // DeviceShare's Filter under several NUMA restrictions (generateTopologyHints' trial allocations): the per-minor
@@ -428,7 +486,6 @@ __device__ __forceinline__ DevFits dev_fits(const Cfg& c, const PodRec& p, const
   f.G.pcw = (uint32_t)topo;
   f.R.pcw = (uint32_t)(topo >> 32);
   if (f.has_gpu) {
-    const int64_t pod[3] = {g.core, g.mem, g.ratio};
 #pragma unroll
     for (int k = 0; k < kGpus; ++k) {
       const int64_t t[3] = {v.tot(k), v.tot(kGpus + k), v.tot(2 * kGpus + k)};
@@ -437,8 +494,7 @@ __device__ __forceinline__ DevFits dev_fits(const Cfg& c, const PodRec& p, const
       const bool exists = t[0] || t[1] || t[2];
       const bool fits = exists && (fr[0] || fr[1] || fr[2]) && (!g.has_core || g.core <= fr[0]) && g.mem <= fr[1] &&
                         g.ratio <= fr[2];
-      f.G.fit |= fits ? (1u << k) : 0u;
-      if (f.walk && fits) f.G.sc |= (uint64_t)dev_score3(c, t, fr, pod) << (8 * k);
+      f.G.fit |= fits ? (1u << k) : 0u;  // (the hints' trial allocator has no scorer: every minor scores 0)
     }
   }
   if (f.has_rdma || (f.jr && f.walk)) {
@@ -448,7 +504,6 @@ __device__ __forceinline__ DevFits dev_fits(const Cfg& c, const PodRec& p, const
       const int64_t fr = t > u ? t - u : 0;
       const bool fits = t != 0 && fr != 0 && g.rdma <= fr;
       f.R.fit |= fits ? (1u << j) : 0u;
-      if (f.walk && fits) f.R.sc |= (uint64_t)dev_score1(c, t, fr, g.rdma) << (8 * j);
     }
   }
   return f;

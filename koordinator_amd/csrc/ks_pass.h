@@ -125,7 +125,7 @@ void sweep_kernel(SweepArgs a) {
       }
       const PodRec pod = load_pod_uniform(a.pods + cursor + p);
       EvalOut o = eval_full<NSC, false, true, FEAT>(
-          a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+          a.c, pod, r, [&](auto&& f) { return f(RsvG<false>(*a.rv, node)); },
           [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
       const uint32_t key = o.reasons ? 0u : (((uint32_t)(key_total(a.c, o, NormM{0, 0, 0}) + 1) << 6) | (uint32_t)(63 - lane));
       t.x = wave_max_u32(key);
@@ -155,8 +155,8 @@ void sweep_kernel(SweepArgs a) {
     constexpr bool FIX = decltype(fixc)::value;
     for (int64_t w = wave; w < nwork; w += nwaves) {
       // (32-bit, with the divisor opaque per item: a hoisted reciprocal would be one more value live across the loop)
-      int32_t gdiv = groups;
-      asm volatile("" : "+s"(gdiv));
+      // (readfirstlane, not an "s" asm constraint: under SGPR pressure the allocator may keep the value in a VGPR)
+      const int32_t gdiv = __builtin_amdgcn_readfirstlane(groups);
       const int64_t lc = (int64_t)((uint32_t)w / (uint32_t)gdiv);  // chunk within this shard's range (or fix-list entry)
       const int64_t c = FIX ? (int64_t)(__builtin_amdgcn_readfirstlane(a.fix[1 + lc]) >> 6) : a.c0 + lc;
       if (FIX && (c < a.c0 || c >= a.c1)) continue;  // another shard's chunk
@@ -197,7 +197,7 @@ void sweep_kernel(SweepArgs a) {
       for (int32_t p = p0; p < p1; ++p) {
         const PodRec pod = load_pod_uniform(a.pods + cursor + p);
         EvalOut o = eval_full<NSC, false, true, FEAT>(
-            a.c, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+            a.c, pod, r, [&](auto&& f) { return f(RsvG<false>(*a.rv, node)); },
             [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
         if ((FEAT & 4) && a.c.stat) stat_eval(a.c, load_stat_uniform(a.pstat + cursor + p), st_hard, st_soft, st_lab, st_port, o);
         if ((FEAT & 4) && a.phase == 0) {
@@ -678,7 +678,7 @@ __device__ __forceinline__ uint64_t rescan_untouched(const CommitArgs& a, const 
     }
   }
   EvalOut o = eval_full<NSC, false, false, FEAT>(
-      cfg, pod, r, [&](RsvDelta<NSC>& dl) { return rsv_eval<NSC>(RsvG<false>(*a.rv, node), pod, r, dl); },
+      cfg, pod, r, [&](auto&& f) { return f(RsvG<false>(*a.rv, node)); },
       [&]() { return DevGView{*a.dv, node}; }, [&]() { return NumaGView{*a.nv, node}; });
   if ((FEAT & 4) && cfg.stat) stat_eval(cfg, *ps, sh, ss, sl, sp, o);
   const bool skip = o.reasons || ((touched_mask >> lane) & 1ull);
@@ -925,14 +925,22 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
   KS_STAMP(0);
   // Opaque copy of the profile: hipcc otherwise re-loads kernel-argument words inside the loop
   // (s_load + s_waitcnt lgkmcnt(0)), which would drain every LDS read in flight.
+  // (The Reservation + DeviceShare variants run at the SGPR limit, where an "s" constraint can meet a value the
+  // allocator keeps in a VGPR -- an illegal copy: they take readfirstlane, which stays legal.)
   Cfg cfg = a.c;
+  int32_t Kc = K;
   {
     int32_t* w = reinterpret_cast<int32_t*>(&cfg);
+    if constexpr ((FEAT & 5) == 5) {
 #pragma unroll
-    for (int i = 0; i < (int)(sizeof(Cfg) / 4); ++i) asm volatile("" : "+s"(w[i]));
+      for (int i = 0; i < (int)(sizeof(Cfg) / 4); ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
+      Kc = __builtin_amdgcn_readfirstlane(Kc);
+    } else {
+#pragma unroll
+      for (int i = 0; i < (int)(sizeof(Cfg) / 4); ++i) asm volatile("" : "+s"(w[i]));
+      asm volatile("" : "+s"(Kc));
+    }
   }
-  int32_t Kc = K;
-  asm volatile("" : "+s"(Kc));
 
   // ---- per-lane roles in slot construction and Reserve: lane t < ST_N owns slot term t ----
   // capacity / requested raw fields, the PodRec words of its Reserve delta (x1, x100), and whether a
@@ -1023,7 +1031,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           PodRec pod = spods[jj];
           pod.flags = __builtin_amdgcn_readfirstlane(pod.flags);
           pod.rsv_class = __builtin_amdgcn_readfirstlane(pod.rsv_class);
-          const DevLView v{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+          const DevLView v{sdev_tot + lane, sdev_use + lane, (uint32_t)sdev_pres[lane]};
           if (wv == 1) {
             shint[lane] = dev_hints(cfg, pod, v);
           } else {
@@ -1249,7 +1257,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         split_sink ^= (uint64_t)e.total ^ e.reasons;
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         split[0] += t1 - t0;
-        const DevLView dvl{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+        const DevLView dvl{sdev_tot + lane, sdev_use + lane, (uint32_t)sdev_pres[lane]};
         if ((FEAT & 8) && cfg.numa_pol && !(pod.flags & kPodReqZero)) {
           const NumaLView nl{snp + lane * kNumaSlotWords};
           if (nl.policy() != 0) {
@@ -1293,12 +1301,12 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
           cw = (uint32_t)((uint64_t)snuma[4 * lane + 3] >> 32);
           r.cpu_cores = (cw & kCoresDirty) ? (cw | kCoresCount | (kCoresCount << kCoresAnyShift)) : cw;
         }
-        auto rsvf = [&](RsvDelta<NSC>& dl) {
+        auto rsvf = [&](auto&& f) {
           const int32_t c = srcnt[lane];
-          if (c >= 0) return rsv_eval<NSC>(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane]}, pod, r, dl);
-          return rsv_eval<NSC>(RsvG<true>(*a.rv, snode), pod, r, dl);
+          if (c >= 0) return f(RsvL<RD>{srec + lane * a.rcap, c, srbeg[lane], a.rv});
+          return f(RsvG<true>(*a.rv, snode));
         };
-        auto devf = [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0}; };
+        auto devf = [&]() { return DevLView{sdev_tot + lane, sdev_use + lane, (uint32_t)sdev_pres[lane]}; };
         auto numaf = [&]() { return NumaLView{snp + lane * kNumaSlotWords}; };
         if constexpr (HINTW) {
           // the slot's DeviceShare hints: the hint wave's (use_hw), else computed here
@@ -1311,12 +1319,12 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
                 __builtin_amdgcn_s_sleep(1);
               }
             }
-            return dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0});
+            return dev_hints(cfg, pod, DevLView{sdev_tot + lane, sdev_use + lane, (uint32_t)sdev_pres[lane]});
           };
           // the slot's DeviceShare Filter / Score under `allow`: a helper wave's variant with the same allowed minors (the
           // result depends on the restriction only through them), else computed here
           auto dff = [&](uint32_t allow) -> DevOut {
-            const DevLView v{sdev_tot + lane, sdev_use + lane, sdev_pres[lane] != 0};
+            const DevLView v{sdev_tot + lane, sdev_use + lane, (uint32_t)sdev_pres[lane]};
             if (use_hw) {
               uint32_t gin, rin;
               dev_allowed(v, allow, gin, rin);
@@ -1470,7 +1478,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       if (DEV && cfg.dev) {
         const DevDev& dv = *a.dv;
         if (lane < DW) ld_dtot = gld(dv.total + (int64_t)lane * dv.npad + node);
-        else if (lane == DW) ld_dtot = (int64_t)(gld(dv.flags + node) & KS_DEV_PRESENT);
+        else if (lane == DW) ld_dtot = (int64_t)(gld(dv.flags + node) & (KS_DEV_PRESENT | kDevRsvHeld));
         if (lane < DU) ld_duse = gld(dv.used + (int64_t)lane * dv.npad + node);
       }
       const int64_t* src = raw;
@@ -1604,6 +1612,11 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     KS_STAMP(4);
     int32_t nom_row = -1;
     int64_t fitla_pref = -1;  // Fit + LoadAware total of a preferred (ordered) chosen node
+    // DeviceShare Reserve on a node whose reservations hold devices (computed with the nomination)
+    const bool want_dev0 = DEV && cfg.dev && (pflags & kPodHasGpu);
+    bool dev_rsv_done = false;
+    uint32_t gmin_rsv = 0, rmin_rsv = 0;
+    GpuReq g_rsv{};
     if (RSV && rsvc) {
       // NominateReservation on the pre-pod state, Reserve into it (AddAssignedPod), then the pod
       PodRec pod = spods[j];
@@ -1619,10 +1632,17 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       if ((FEAT & 2) && cfg.cores) nr.cpu_cores = (uint32_t)((uint64_t)snuma[4 * s + 3] >> 32);  // (score: the label)
       RsvDelta<NSC> dl;
       const int32_t mode = srcnt[s];
-      const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s]};
+      const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s], a.rv};
+      const DevLView sdv{sdev_tot + s, sdev_use + s, DEV && cfg.dev ? (uint32_t)sdev_pres[s] : 0u};
+      // DeviceShare's FilterReservation / ScoreReservation in the nomination (reservations holding devices)
+      auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
+        *ds = 0;
+        if constexpr (DEV) return sdv.held() && dev_rsv_candidate(cfg, pod, sdv, v, i, ds);
+        return false;
+      };
       RsvOut ro;
-      if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl);
-      else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl);
+      if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl, dnom);
+      else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl, dnom);
       const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);  // view index
       if (ro.hi >= kRsvOrderBase) {
         // the whole Filter / Score of the slot with this restore (eval_full: on a node with a NUMA topology policy the
@@ -1630,14 +1650,27 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         NodeReg<NSC> n2 = nr;
         EvalOut e2 = eval_full<NSC, false, false, FEAT>(
             cfg, pod, n2,
-            [&](RsvDelta<NSC>& d2) {
-              d2 = dl;
-              return ro;
+            [&](auto&& f) {
+              if (mode >= 0) return f(lv);
+              return f(RsvG<true>(*a.rv, node));
             },
-            [&]() { return DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}; },
+            [&]() { return DevLView{sdev_tot + s, sdev_use + s, (uint32_t)sdev_pres[s]}; },
             [&]() { return NumaLView{snp + s * kNumaSlotWords}; });
         if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[4 * s], sstat[4 * s + 1], sstat[4 * s + 2], sstat[4 * s + 3], e2);
         fitla_pref = e2.total + norm_terms(cfg, e2, Muse);
+      }
+      if (DEV && want_dev0 && sdv.held()) {
+        // DeviceShare Reserve on the cycle's restore state, before the Reservation plugin's own Reserve changes it
+        // (the ordered node's full evaluation above ran on the same state)
+        const DevOut rd = mode >= 0 ? dev_rsv_reserve(cfg, pod, sdv, lv, nom, &g_rsv)
+                                    : dev_rsv_reserve(cfg, pod, sdv, RsvG<true>(*a.rv, node), nom, &g_rsv);
+        gmin_rsv = __builtin_amdgcn_readfirstlane(rd.minors);
+        rmin_rsv = __builtin_amdgcn_readfirstlane(rd.rminors);
+        dev_rsv_done = true;
+        if (nom >= 0 && lane == 0) {
+          if (mode >= 0) rsv_dev_assign(*a.rv, lv, nom, g_rsv, gmin_rsv, rmin_rsv, +1);
+          else rsv_dev_assign(*a.rv, RsvG<true>(*a.rv, node), nom, g_rsv, gmin_rsv, rmin_rsv, +1);
+        }
       }
       int64_t dd = 0;
       if (nom >= 0) {
@@ -1706,7 +1739,8 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     const bool want_dev = DEV && cfg.dev && (pflags & kPodHasGpu);
     // a slot created by this pod holds the snapshot state: reserve_pre_kernel's allocation for the node, if it ranked
     const PreRsv* pre = nullptr;
-    if ((FEAT & 8) && a.pre_rsv && fresh && (want_npol || want_dev)) {
+    const bool held_here = DEV && cfg.dev && RSV && cfg.rsv && ((uint32_t)sdev_pres[s] & kDevRsvHeld);
+    if ((FEAT & 8) && a.pre_rsv && fresh && (want_npol || want_dev) && !held_here) {
       const uint64_t hit = __ballot(pre_nodes == node);  // (read by the look-ahead)
       if (hit) pre = a.pre_rsv + j * kPreRsvM + (__ffsll((long long)hit) - 1);
     }
@@ -1743,7 +1777,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         nc.cpu_free = (int32_t)snuma[4 * s + 3];
         nc.cores = cfg.cores ? ((uint32_t)((uint64_t)snuma[4 * s + 3] >> 32) & ~kCoresDirty) : 0u;
         if (DEV && cfg.dev && (pflags & kPodHasGpu)) {
-          const DevLView dvl{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0};
+          const DevLView dvl{sdev_tot + s, sdev_use + s, (uint32_t)sdev_pres[s]};
           npr = numa_policy_eval<true>(cfg, pod, nl, nc, &dvl);  // the Filter passed on this state: DeviceShare follows
         } else {
           npr = numa_policy_eval(cfg, pod, nl, nc, (const DevLView*)nullptr);
@@ -1754,10 +1788,24 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     const uint32_t dev_allow = (npol && npr.admitted && npr.affinity) ? npr.affinity : ~0u;
     if (want_dev) {
       // DeviceShare Reserve: allocate the minors on the pre-pod GPU state, add the request per instance
-      if (!pre) {
+      if (dev_rsv_done) {
+        gminors = gmin_rsv;
+        rminors = rmin_rsv;
+        g = g_rsv;
+      } else if (held_here) {
+        // reservations holding devices, none matching the pod: the unmatched ones' restore still applies
         PodRec pod = spods[j];
         pod.flags = pflags;
-        const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, sdev_pres[s] != 0}, &g, dev_allow);
+        const DevLView sdv{sdev_tot + s, sdev_use + s, (uint32_t)sdev_pres[s]};
+        const int32_t mode = srcnt[s];
+        const DevOut dd = mode >= 0 ? dev_rsv_reserve(cfg, pod, sdv, RsvL<RD>{srec + s * a.rcap, mode, srbeg[s], a.rv}, -1, &g)
+                                    : dev_rsv_reserve(cfg, pod, sdv, RsvG<true>(*a.rv, node), -1, &g);
+        gminors = __builtin_amdgcn_readfirstlane(dd.minors);
+        rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
+      } else if (!pre) {
+        PodRec pod = spods[j];
+        pod.flags = pflags;
+        const DevOut dd = dev_eval<true>(cfg, pod, DevLView{sdev_tot + s, sdev_use + s, (uint32_t)sdev_pres[s]}, &g, dev_allow);
         gminors = __builtin_amdgcn_readfirstlane(dd.minors);
         rminors = __builtin_amdgcn_readfirstlane(dd.rminors);
       }

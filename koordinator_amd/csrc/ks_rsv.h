@@ -35,7 +35,8 @@ constexpr int64_t kDefaultMilliCPU = 100;                 // schedutil.DefaultMi
 constexpr int64_t kDefaultMemory = 200ll * 1024 * 1024;   // schedutil.DefaultMemoryRequest
 constexpr int32_t kRsvOrderBase = 101;                    // hi of an ordered node > any raw score
 
-// meta word: flags (KS_RSV_*) | policy << 4 | key_mask << 8
+// meta word: flags (KS_RSV_*) | policy << 4 | key_mask << 8 | ndims << 16 | kRsvMetaDev
+constexpr uint32_t kRsvMetaDev = 1u << 20;  // the reservation holds devices (DevRsv.dal row non-zero)
 __device__ __forceinline__ uint32_t rsv_policy(uint32_t m) { return (m >> 4) & 0xfu; }
 __device__ __forceinline__ uint32_t rsv_keys(uint32_t m) { return (m >> 8) & 0xffu; }
 
@@ -51,6 +52,10 @@ struct DevRsv {
   const int64_t* rnz;     // [2][nr] reserve pod NonZeroRequested cpu / memory
   uint64_t* ncls;         // = DevNodes.rsv_cls
   const int32_t* rowid;   // CSR position -> caller row
+  // DeviceShare (deviceshare/reservation.go): the reserve pod's device allocation and its assigned pods' allocations
+  // on those minors, [kDevQW][nr] (ks_dev.h word layout); NULL when no reservation holds a device
+  const int64_t* dal;
+  int64_t* dald;          // mutable (Reserve)
   int64_t nr;
   int64_t w100;           // 100 * plugin weight
 };
@@ -103,6 +108,8 @@ struct RsvG {
   __device__ __forceinline__ int64_t allocd(int d, int64_t i) const { return rld<FRESH>(rv.allocd + d * rv.nr + b + i); }
   __device__ __forceinline__ int64_t rnz(int k, int64_t i) const { return gld(rv.rnz + k * rv.nr + b + i); }
   __device__ __forceinline__ int32_t csr(int64_t i) const { return (int32_t)(b + i); }
+  __device__ __forceinline__ int64_t dal(int w, int64_t i) const { return gld(rv.dal + (int64_t)w * rv.nr + b + i); }
+  __device__ __forceinline__ int64_t dald(int w, int64_t i) const { return rld<true>(rv.dald + (int64_t)w * rv.nr + b + i); }
 };
 
 template <int D>
@@ -118,6 +125,7 @@ template <int D>
 struct RsvL {
   const RsvRec<D>* rec;
   int32_t cnt, b;
+  const DevRsv* rvp;  // the device allocations stay in HBM
   __device__ __forceinline__ int64_t n() const { return cnt; }
   __device__ __forceinline__ uint32_t meta(int64_t i) const { return rec[i].meta; }
   __device__ __forceinline__ int32_t assigned(int64_t i) const { return rec[i].assigned; }
@@ -127,6 +135,10 @@ struct RsvL {
   __device__ __forceinline__ int64_t allocd(int d, int64_t i) const { return d < D ? rec[i].allocd[d] : 0; }
   __device__ __forceinline__ int64_t rnz(int k, int64_t i) const { return rec[i].rnz[k]; }
   __device__ __forceinline__ int32_t csr(int64_t i) const { return b + (int32_t)i; }
+  __device__ __forceinline__ int64_t dal(int w, int64_t i) const { return gld(rvp->dal + (int64_t)w * rvp->nr + b + i); }
+  __device__ __forceinline__ int64_t dald(int w, int64_t i) const {
+    return rld<true>(rvp->dald + (int64_t)w * rvp->nr + b + i);
+  }
 };
 
 // meta bits 16..19: 1 + the highest dimension with a non-zero allocatable / allocated (0 = none)
@@ -155,10 +167,226 @@ __device__ __forceinline__ int32_t rsv_score(const V& v, const PodRec& p, int64_
   return w ? s / w : 0;
 }
 
+// ---- DeviceShare with reservations holding devices (deviceshare/reservation.go) ----
+// RestoreReservation (:118-171) keeps the transformer's matched reservations that hold devices (allocatable = the
+// reserve pod's allocation, allocated = its assigned pods' on those minors, remained = allocatable - allocated) and the
+// unmatched ones with assigned pods; the allocator then sees used' = max(0, used - preemptible) (calcFreeWithPreemptible)
+// with preemptible = mergedUnmatchedUsed + mergedMatchedAllocatable (the node outside any reservation's preference) or
+// mergedUnmatchedUsed + mergedMatchedAllocated + remained(r) (allocating from reservation r).  The node columns hold
+// nodeDeviceCache's used (reserve pods and assigned pods both counted); the views below subtract the per-pod part.
+constexpr int kDrsFallback = 0, kDrsTry = 1;
+
+// a reservation the pod's restore treats as matched and holding devices
+template <typename V>
+__device__ __forceinline__ bool rsv_dev_matched(const V& v, int64_t i, int32_t cls) {
+  uint32_t meta;
+  int32_t a;
+  return cls >= 0 && cls < 64 && rsv_matches(v, i, cls, meta, a) && (meta & kRsvMetaDev);
+}
+
+// the reservation's minors of each type (newDeviceMinorMap(allocatable))
+template <typename V>
+__device__ __forceinline__ void rsv_dev_minors(const V& v, int64_t i, uint32_t& gm, uint32_t& rm) {
+  gm = rm = 0u;
+  for (int k = 0; k < kGpus; ++k)
+    gm |= (v.dal(k, i) | v.dal(kGpus + k, i) | v.dal(2 * kGpus + k, i)) != 0 ? (1u << k) : 0u;
+  for (int j = 0; j < kRdma; ++j) rm |= v.dal(kDevRdmaW + j, i) != 0 ? (1u << j) : 0u;
+}
+
+// The node device of one allocator call (see above).  r: the reservation allocated from (kDrsTry); gq / rq: the types
+// of requiredDeviceResources (calcRequiredDeviceResources, reservation.go:273-292) -- only those minors exist, with
+// free = r's remained (zero when `zero`: nothing remained anywhere).
+template <typename DV, typename V>
+struct DevRView {
+  const DV& d;
+  const V& v;
+  int32_t cls;
+  int64_t r;
+  int mode;
+  uint32_t gq, rq;
+  bool zero;
+  __device__ __forceinline__ bool present() const { return d.present(); }
+  __device__ __forceinline__ int64_t ptot(int w) const { return d.tot(w); }
+  // the word's required-type minor mask (0 = the type is not required)
+  __device__ __forceinline__ uint32_t req_of(int w, int& k) const {
+    if (w < kDevRdmaW) {
+      k = w % kGpus;
+      return gq;
+    }
+    k = w - kDevRdmaW;
+    return rq;
+  }
+  __device__ __forceinline__ int64_t tot(int w) const {
+    if (w >= kDevQW) return d.tot(w);  // (topology words)
+    int k;
+    const uint32_t q = req_of(w, k);
+    return (q && !((q >> k) & 1u)) ? 0 : d.tot(w);
+  }
+  __device__ __forceinline__ int64_t use(int w) const {
+    int k;
+    if (req_of(w, k)) {  // nodeDevice.filter: used = max(0, total - free)
+      const int64_t f = zero ? 0 : v.dal(w, r) - v.dald(w, r), u = d.tot(w) - f;
+      return u > 0 ? u : 0;
+    }
+    int64_t pre = 0;
+    for (int64_t i = 0; i < v.n(); ++i) {
+      const uint32_t meta = v.meta(i);
+      const int32_t a = v.assigned(i);
+      if (!(meta & kRsvMetaDev) || ((meta & KS_RSV_ALLOCATE_ONCE) && a > 0)) continue;
+      const bool matched = !(meta & KS_RSV_UNSCHEDULABLE) && cls >= 0 && cls < 64 && ((v.cls(i) >> cls) & 1ull);
+      if (matched) {
+        pre += mode == kDrsFallback ? v.dal(w, i) : v.dald(w, i) + (i == r ? v.dal(w, i) - v.dald(w, i) : 0);
+      } else if (a > 0) {
+        const int64_t x = v.dald(w, i);  // used = max(0, allocatable - remained)
+        pre += x > 0 ? x : 0;
+      }
+    }
+    const int64_t u = d.use(w) - pre;
+    return u > 0 ? u : 0;
+  }
+};
+
+// tryAllocateFromReservation's body for reservation i (reservation.go:201-240): Default / Aligned allocate with its
+// minors preferred; Restricted requires them, then allocates again with its remained as the free amounts.  ALLOC:
+// with Reserve's scorer and the minors.
+template <bool ALLOC, typename DV, typename V>
+__device__ __attribute__((noinline)) DevOut dev_rsv_try(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, GpuReq* req_out) {
+  const int32_t cls = p.rsv_class;
+  uint32_t gm, rm;
+  rsv_dev_minors(v, i, gm, rm);
+  DevPick pk{gm, rm, 0xFFu, 0xFFu};
+  const DevRView<DV, V> tv{dv, v, cls, i, kDrsTry, 0u, 0u, false};
+  const uint32_t pol = rsv_policy(v.meta(i));
+  if (pol == KS_RSV_POLICY_DEFAULT || pol == KS_RSV_POLICY_ALIGNED) return dev_eval<ALLOC>(c, p, tv, req_out, ~0u, pk);
+  if (pol != KS_RSV_POLICY_RESTRICTED) return DevOut{KS_R_DEV_INSUFFICIENT, 0, 0u, 0u};
+  pk.greq = gm;
+  pk.rreq = rm;
+  const DevOut d = dev_eval<false>(c, p, tv, nullptr, ~0u, pk);
+  if (d.reasons) return d;
+  // calcRequiredDeviceResources: the minors whose remained is not all-zero, else every minor with nothing
+  uint32_t gq = 0u, rq = 0u;
+  for (int k = 0; k < kGpus; ++k)
+    if ((gm >> k) & 1u) {
+      bool nz = false;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) nz |= v.dal(q * kGpus + k, i) != v.dald(q * kGpus + k, i);
+      gq |= nz ? (1u << k) : 0u;
+    }
+  for (int j = 0; j < kRdma; ++j)
+    if (((rm >> j) & 1u) && v.dal(kDevRdmaW + j, i) != v.dald(kDevRdmaW + j, i)) rq |= 1u << j;
+  const bool zero = !gq && !rq;
+  const DevRView<DV, V> qv{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero};
+  return dev_eval<ALLOC>(c, p, qv, req_out, ~0u, pk);
+}
+
+// scoreWithReservation (reservation.go:249-271) on reservation i's view, or (i < 0) the node outside every
+// reservation's preference -- DeviceShare Score (scoring.go:30-90)
+template <typename DV, typename V>
+__device__ __attribute__((noinline)) int32_t dev_rsv_score(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, const GpuReq& g) {
+  const int32_t cls = p.rsv_class;
+  if (i < 0) return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false}, g);
+  if (rsv_policy(v.meta(i)) != KS_RSV_POLICY_RESTRICTED)
+    return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, 0u, 0u, false}, g);
+  uint32_t gm, rm, gq = 0u, rq = 0u;
+  rsv_dev_minors(v, i, gm, rm);
+  for (int k = 0; k < kGpus; ++k)
+    if ((gm >> k) & 1u) {
+      bool nz = false;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) nz |= v.dal(q * kGpus + k, i) != v.dald(q * kGpus + k, i);
+      gq |= nz ? (1u << k) : 0u;
+    }
+  for (int j = 0; j < kRdma; ++j)
+    if (((rm >> j) & 1u) && v.dal(kDevRdmaW + j, i) != v.dald(kDevRdmaW + j, i)) rq |= 1u << j;
+  const bool zero = !gq && !rq;
+  return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero}, g);
+}
+
+// DeviceShare Filter + Score on a node whose reservations hold devices (deviceshare/plugin.go:271-320): a matched
+// reservation to allocate from (required for a reservation-affinity pod: KS_R_RSV_NO_FIT, "no reservation(s) to meet
+// the device requirements"), else the fallback view; the score on the nominated reservation's view (nom: view index)
+template <typename DV, typename V>
+__device__ __forceinline__ DevOut dev_rsv_eval(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int32_t nom) {
+  DevOut o{0u, 0, 0u, 0u};
+  if (!dv.present()) return o;
+  GpuReq g;
+  o.reasons = dev_prepare(p, dv, g);
+  if (o.reasons) return o;
+  const int32_t cls = p.rsv_class;
+  bool ok = false, any = false;
+  for (int64_t i = 0; i < v.n() && !ok; ++i) {
+    if (!rsv_dev_matched(v, i, cls)) continue;
+    any = true;
+    ok = dev_rsv_try<false>(c, p, dv, v, i, nullptr).reasons == 0;
+  }
+  if (!ok) {
+    if (any && (p.flags & KS_POD_RSV_AFFINITY)) {
+      o.reasons = KS_R_RSV_NO_FIT;
+      return o;
+    }
+    o.reasons = dev_eval<false>(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false}).reasons;
+    if (o.reasons) return o;
+  }
+  o.raw = dev_rsv_score(c, p, dv, v, (nom >= 0 && rsv_dev_matched(v, nom, cls)) ? nom : -1, g);
+  return o;
+}
+
+// DeviceShare's FilterReservation + ScoreReservation of reservation i (plugin.go:322-358, scoring.go:99-142): it holds
+// devices and tryAllocateFromReservation([i], required) allocates; *ds = its scoreWithReservation
+template <typename DV, typename V>
+__device__ __attribute__((noinline)) bool dev_rsv_candidate(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, int32_t* ds) {
+  *ds = 0;
+  if (!dv.present() || !rsv_dev_matched(v, i, p.rsv_class)) return false;
+  GpuReq g;
+  if (dev_prepare(p, dv, g)) return false;
+  if (dev_rsv_try<false>(c, p, dv, v, i, nullptr).reasons) return false;
+  *ds = dev_rsv_score(c, p, dv, v, i, g);
+  return true;
+}
+
+// Reserve (plugin.go:377-430): allocateWithNominatedReservation on the nominated reservation (view index nom), else
+// the fallback view, with the scorer; the minors in the result
+template <typename DV, typename V>
+__device__ __attribute__((noinline)) DevOut dev_rsv_reserve(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int32_t nom, GpuReq* req_out) {
+  if (nom >= 0 && rsv_dev_matched(v, nom, p.rsv_class)) {
+    const DevOut d = dev_rsv_try<true>(c, p, dv, v, nom, req_out);
+    if (d.reasons == 0) return d;
+  }
+  return dev_eval<true>(c, p, DevRView<DV, V>{dv, v, p.rsv_class, -1, kDrsFallback, 0u, 0u, false}, req_out);
+}
+
+// the assigned pod's allocation on reservation i's minors: allocated += (sign) the request per instance there
+template <typename V>
+__device__ __forceinline__ void rsv_dev_assign(const DevRsv& rv, const V& v, int64_t i, const GpuReq& g, uint32_t gmin,
+                                               uint32_t rmin, int64_t sign) {
+  uint32_t gm, rm;
+  rsv_dev_minors(v, i, gm, rm);
+  const int64_t col = v.csr(i);
+  for (int k = 0; k < kGpus; ++k)
+    if ((gm & gmin) >> k & 1u) {
+      rv.dald[(int64_t)(0 * kGpus + k) * rv.nr + col] += sign * g.core;
+      rv.dald[(int64_t)(1 * kGpus + k) * rv.nr + col] += sign * g.mem;
+      rv.dald[(int64_t)(2 * kGpus + k) * rv.nr + col] += sign * g.ratio;
+    }
+  for (int j = 0; j < kRdma; ++j)
+    if ((rm & rmin) >> j & 1u) rv.dald[(int64_t)(kDevRdmaW + j) * rv.nr + col] += sign * g.rdma;
+}
+
+// DeviceShare's FilterReservation where no reservation holds a device: it rejects every one for a pod it restores
+struct NoDevNom {
+  template <typename V>
+  __device__ __forceinline__ bool operator()(const V&, int64_t, int32_t* ds) const {
+    *ds = 0;
+    return false;
+  }
+};
+
 // BeforePreFilter restore + Reservation Filter + nomination for one (pod, node); r is the base row.
-// RsvOut.nom is the view index of the nominated reservation.
-template <int NSC, typename V>
-__device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const NodeReg<NSC>& r, RsvDelta<NSC>& dl) {
+// RsvOut.nom is the view index of the nominated reservation.  dn(v, i, &ds): DeviceShare's FilterReservation of
+// reservation i for a pod it restores (kPodDevNoNom), with its ScoreReservation in ds.
+template <int NSC, typename V, typename DN = NoDevNom>
+__device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const NodeReg<NSC>& r, RsvDelta<NSC>& dl,
+                                           DN dn = DN{}) {
   constexpr int D = 3 + NSC;
   const int32_t cls = p.rsv_class;
   const int64_t cnt = v.n();
@@ -212,12 +440,12 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
   slack[2] = r.free_eph - dpre[2] + ral[2];
 #pragma unroll
   for (int k = 0; k < NSC; ++k) slack[3 + k] = r.free_sc[k] - dpre[3 + k] + ral[3 + k];
-  int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0;
-  for (int64_t i = 0; i < cnt; ++i) {
-    uint32_t meta;
-    int32_t a;
-    if (!rsv_matches(v, i, cls, meta, a)) continue;
-    // filterWithReservations body for one reservation (plugin.go:386-422)
+  const bool dnom = (p.flags & kPodDevNoNom) != 0;
+  int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0, dmax = 0;
+  bool any_ok = false;
+  // filterWithReservations body for one reservation (plugin.go:386-422)
+  auto satisfies = [&](int64_t i) {
+    const uint32_t meta = v.meta(i);
     const uint32_t names = rsv_keys(meta) & p.rsv_keys;
     bool ok = names != 0 && !pods_bad;
     if (ok && !all_zero) {
@@ -241,8 +469,18 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
     } else if (pol != KS_RSV_POLICY_DEFAULT && pol != KS_RSV_POLICY_ALIGNED) {
       ok = false;
     }
-    if (!ok) continue;
-    // NominateReservation: lowest order label first (strict, table order), else best score
+    return ok;
+  };
+  for (int64_t i = 0; i < cnt; ++i) {
+    uint32_t meta;
+    int32_t a;
+    if (!rsv_matches(v, i, cls, meta, a)) continue;
+    if (!satisfies(i)) continue;
+    any_ok = true;
+    // NominateReservation: RunReservationFilterPlugins (Reservation's FilterReservation = the body above, then
+    // DeviceShare's for a pod it restores), lowest order label first (strict, table order), else the best score
+    int32_t ds = 0;
+    if (dnom && !dn(v, i, &ds)) continue;
     const int32_t oh = v.ohi(i);
     const int32_t sc = rsv_score(v, p, i);
     if (oh > best_o) {
@@ -250,20 +488,36 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
       nom_o = (int32_t)i;
       raw_o = sc;
     }
-    if (sc > best_s) {
+    dmax = max(dmax, ds);
+    if (!dnom && sc > best_s) {
       best_s = sc;
       nom_s = (int32_t)i;
     }
   }
-  o.nom = nom_o >= 0 ? nom_o : nom_s;
-  o.raw = nom_o >= 0 ? raw_o : (nom_s >= 0 ? best_s : 0);
-  // the Reservation Filter passes on any satisfying reservation; the nomination also runs DeviceShare's
-  // FilterReservation, which rejects them all for a device pod (kPodDevNoNom)
-  o.reasons = (aff && o.nom < 0) ? KS_R_RSV_NO_FIT : 0u;
-  if (p.flags & kPodDevNoNom) {
-    o.nom = -1;
-    o.raw = 0;
+  int32_t raw_s = best_s;
+  if (dnom && nom_o < 0) {
+    // prioritizeReservations (nominator.go:218-262): Reservation's ScoreReservation (no normalization) + DeviceShare's
+    // after DefaultReservationNormalizeScore(100); the highest sum, ties in table order
+    for (int64_t i = 0; i < cnt; ++i) {
+      uint32_t meta;
+      int32_t a;
+      if (!rsv_matches(v, i, cls, meta, a) || !satisfies(i)) continue;
+      int32_t ds = 0;
+      if (!dn(v, i, &ds)) continue;
+      const int32_t sc = rsv_score(v, p, i);
+      const int32_t t = sc + (dmax > 0 ? 100 * ds / dmax : ds);
+      if (t > best_s) {
+        best_s = t;
+        nom_s = (int32_t)i;
+        raw_s = sc;
+      }
+    }
   }
+  o.nom = nom_o >= 0 ? nom_o : nom_s;
+  o.raw = nom_o >= 0 ? raw_o : (nom_s >= 0 ? raw_s : 0);
+  // the Reservation Filter passes on any satisfying reservation (DeviceShare's FilterReservation runs in the
+  // nomination only)
+  o.reasons = (aff && !any_ok) ? KS_R_RSV_NO_FIT : 0u;
   o.hi = hiord > 0 ? hiord : o.raw;
   return o;
 }
@@ -290,8 +544,8 @@ __device__ __forceinline__ void rsv_apply(NodeReg<NSC>& r, const RsvDelta<NSC>& 
 
 // Filter + Score of one (pod, node) with the Reservation plugin: total = hi * F + Fit/LA total.
 // r must be the base row; with UNDO it is returned unchanged (the sweep reuses it across pods).
-// rsv(dl) runs rsv_eval on the node's reservation view; it is called only when the pod's class
-// matches one of them.
+// rsv(f) calls f on the node's reservation view (RsvG / RsvL): rsv_eval when the pod's class matches one of them,
+// DeviceShare's restore-state evaluation (dev_rsv_eval) on a node whose reservations hold devices.
 // FEAT: bit 0 Reservation, bit 1 NodeNUMAResource, bit 2 DeviceShare, bit 3 NUMA topology policies compiled in
 // (the Cfg flags switch them at run time).  devv() / numav() return the node's device view (ks_dev.h) and NUMA
 // view (ks_numa.h).  Filter order as in the profile: Fit, LoadAware, NodeNUMAResource (on a node with a NUMA
@@ -333,16 +587,7 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
     dpre = pr.dev;
     return allow;
   };
-  auto dev = [&](EvalOut& o, uint32_t allow) __attribute__((always_inline)) {
-    if (!dev_pod) return;
-    if (!DEBUG && o.reasons) return;
-    DevOut d;
-    if (dev_pre) {
-      d = dpre;
-    } else {
-      if constexpr (LateDevHints<DFF>::value) d = dff(allow);
-      else d = dev_eval<false>(c, p, devv(), nullptr, allow);
-    }
+  auto dev_apply = [&](EvalOut& o, const DevOut& d) __attribute__((always_inline)) {
     o.reasons |= DEBUG ? d.reasons : (d.reasons ? KS_R_FIT_PODS : 0u);
     o.dev_raw = d.raw;
     if (!DEBUG && dev_pol && d.reasons) {  // the deferred policy-path failure: no NUMA score (numa_policy_eval)
@@ -350,24 +595,55 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
       o.numa = 0;
     }
   };
+  auto dev = [&](EvalOut& o, uint32_t allow, int32_t nom) __attribute__((always_inline)) {
+    if (!dev_pod) return;
+    if (!DEBUG && o.reasons) return;
+    if constexpr (RSV) {
+      // reservations holding devices on the node (never one with a NUMA policy): the restore state's views
+      if (c.rsv) {
+        const auto dv = devv();
+        if (dv.held()) {
+          dev_apply(o, rsv([&](const auto& v) { return dev_rsv_eval(c, p, dv, v, nom); }));
+          return;
+        }
+      }
+    }
+    DevOut d;
+    if (dev_pre) {
+      d = dpre;
+    } else {
+      if constexpr (LateDevHints<DFF>::value) d = dff(allow);
+      else d = dev_eval<false>(c, p, devv(), nullptr, allow);
+    }
+    dev_apply(o, d);
+  };
   if (!RSV || !c.rsv || (p.rsv_class < 0 && !(p.flags & KS_POD_RSV_AFFINITY))) {
     if (info) *info = RsvOut{0u, 0, 0, 0, -1};
     EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
     const uint32_t allow = numa(o);
-    dev(o, allow);
+    dev(o, allow, -1);
     return o;
   }
   const bool slow = p.rsv_class >= 0 && p.rsv_class < 64 && ((r.rsv_cls >> p.rsv_class) & 1ull);
   RsvDelta<NSC> dl;
   RsvOut ro{(p.flags & KS_POD_RSV_AFFINITY) ? KS_R_RSV_AFFINITY : 0u, 0, 0, 0, -1};
   if (slow) {
-    ro = rsv(dl);
+    // DeviceShare's FilterReservation / ScoreReservation in the nomination (a pod it restores)
+    auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
+      *ds = 0;
+      if constexpr (DEV) {
+        const auto dv = devv();
+        return dv.held() && dev_rsv_candidate(c, p, dv, v, i, ds);
+      }
+      return false;
+    };
+    ro = rsv([&](const auto& v) { return rsv_eval<NSC>(v, p, r, dl, dnom); });
     rsv_apply<NSC>(r, dl, 1);
   }
   EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
   const uint32_t allow = numa(o);
   if (UNDO && slow) rsv_apply<NSC>(r, dl, -1);
-  dev(o, allow);
+  dev(o, allow, ro.nom);
   // a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
   // NodeNames, plugin.go:235-246) before any Filter plugin runs
   o.reasons = ro.reasons == KS_R_RSV_AFFINITY ? ro.reasons : (o.reasons | ro.reasons);

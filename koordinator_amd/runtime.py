@@ -62,6 +62,7 @@ def lib() -> C.CDLL:
     L.ks_load_quotas.argtypes = [vp, C.POINTER(abi.KsQuotaCols), C.c_int32]
     L.ks_load_reservations.argtypes = [vp, C.POINTER(abi.KsReservationCols), C.c_int32]
     L.ks_read_reservations.argtypes = [vp, abi.P64, abi.P32]
+    L.ks_read_reservation_devices.argtypes = [vp, abi.P64]
     L.ks_load_devices.argtypes = [vp, C.POINTER(abi.KsDeviceCols), C.c_int64]
     L.ks_read_devices.argtypes = [vp, abi.P64, abi.P64, abi.P64]
     L.ks_read_devices_rdma.argtypes = [vp, abi.P64]
@@ -318,6 +319,12 @@ class Evaluator:
         self._chk(self.L.ks_read_reservations(self.h, allocated.ctypes.data_as(abi.P64),
                                               assigned.ctypes.data_as(abi.P32)))
         return allocated[: self.nr * abi.KS_RSV_DIMS].reshape(self.nr, abi.KS_RSV_DIMS), assigned[: self.nr]
+
+    def read_reservation_devices(self):
+        """the assigned pods' device allocations on each reservation's minors [r][KS_DEV_WORDS] after commits"""
+        out = np.zeros(max(self.nr, 1) * abi.KS_DEV_WORDS, np.int64)
+        self._chk(self.L.ks_read_reservation_devices(self.h, out.ctypes.data_as(abi.P64)))
+        return out[: self.nr * abi.KS_DEV_WORDS].reshape(self.nr, abi.KS_DEV_WORDS)
 
     def shard(self, nranks: int = 1, rank: int = 0, unique_id: Optional[bytes] = None, virtual_shards: int = 1):
         """Node sharding: this rank sweeps its chunk range; candidates are exchanged by RCCL allgather."""

@@ -498,13 +498,55 @@ def c3(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, policy_frac:
     return Workload("C3", prof, nodes, pods, None, None, devs, cpus, numa)
 
 
+def device_reservations(w: Workload, rng: np.random.Generator, frac: float = 0.4) -> Workload:
+    """Reservations holding devices (deviceshare/reservation.go): frac of the reservations on nodes with device
+    information and no NUMA topology policy reserve one or two GPUs (a whole or half instance each) and, on half of
+    them, an RDMA device share; the reserve pod's allocation counts in the node's device used (nodeDeviceCache), and a
+    reservation with assigned pods has them use part of its first minor (counted in used a second time, as the
+    cache holds both the reserve pod and the assigned pods)."""
+    rs, dv = w.reservations, w.devices
+    rs.hold_devices()
+    pol = (w.nodes.numa_flags >> abi.KS_NUMA_POLICY_SHIFT) & 3
+    G = abi.KS_MAX_GPUS
+    for r in range(rs.r):
+        n = int(rs.node[r])
+        if not (dv.flags[n] & abi.KS_DEV_PRESENT) or pol[n] != 0 or rng.random() >= frac:
+            continue
+        minors = [k for k in range(G) if dv.total_ratio[k, n] > 0]
+        if not minors:
+            continue
+        pick = rng.choice(minors, min(len(minors), int(rng.integers(1, 3))), replace=False)
+        for i, k in enumerate(sorted(int(x) for x in pick)):
+            part = int(rng.choice([50, 100]))
+            mem = part * int(dv.total_memory[k, n]) // 100
+            for q, v in ((0, part), (1, mem), (2, part)):
+                rs.dev_allocatable[r, abi.dev_word("gpu", k, q)] = v
+            dv.used_core[k, n] += part
+            dv.used_memory[k, n] += mem
+            dv.used_ratio[k, n] += part
+            if i == 0 and rs.assigned[r] > 0:
+                use = part // 2
+                for q, v in ((0, use), (1, use * int(dv.total_memory[k, n]) // 100), (2, use)):
+                    rs.dev_allocated[r, abi.dev_word("gpu", k, q)] = v
+                dv.used_core[k, n] += use
+                dv.used_memory[k, n] += use * int(dv.total_memory[k, n]) // 100
+                dv.used_ratio[k, n] += use
+        rm = [j for j in range(abi.KS_MAX_RDMA) if dv.total_rdma[j, n] > 0]
+        if rm and rng.random() < 0.5:
+            j = int(rng.choice(rm))
+            rs.dev_allocatable[r, abi.dev_word("rdma", j)] = 50
+            dv.used_rdma[j, n] += 50
+    return w
+
+
 def c3_rsv(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, rsv_per_node: float = 2.5,
-           policy_frac: float = 0.5, policy: int = abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE, **kw) -> Workload:
+           policy_frac: float = 0.5, policy: int = abi.KS_NUMA_POLICY_SINGLE_NUMA_NODE, dev_rsv_frac: float = 0.0,
+           **kw) -> Workload:
     """The shipped koord-scheduler profile's plugin set (config/manager/scheduler-config.yaml:58-96: Reservation +
     NodeNUMAResource + DeviceShare next to Fit + LoadAware): C3's nodes (NUMA topology policies, cpuset pods, GPU /
     RDMA devices) with C4's reservations (~2.5 per node, 16 owner classes; their reserve pods in NodeInfo) and 60 % of
-    the pods in an owner class.  Reservations hold no cpuset and no device (nodenumaresource/reservation.go and
-    deviceshare/reservation.go then restore nothing)."""
+    the pods in an owner class.  Reservations hold no cpuset; with dev_rsv_frac > 0 that fraction of the
+    reservations on non-policy device nodes holds GPUs / RDMA (device_reservations, deviceshare/reservation.go)."""
     w = c3(seed=seed, n_nodes=n_nodes, n_pods=n_pods, policy_frac=policy_frac, policy=policy, **kw)
     rng = np.random.Generator(np.random.PCG64(seed + 3))
     for col in ("req_milli_cpu", "req_memory", "nonzero_milli_cpu", "nonzero_memory"):
@@ -513,6 +555,8 @@ def c3_rsv(seed: int = SEED, n_nodes: int = 5000, n_pods: int = 10_000, rsv_per_
     reservation_pods(w.pods, rng)
     w.profile.reservation_weight = 5000
     w.name = "C3-rsv"
+    if dev_rsv_frac > 0:
+        device_reservations(w, rng, dev_rsv_frac)
     return w
 
 

@@ -172,6 +172,10 @@ typedef struct {
   int64_t *order;
   int64_t *alloc, *allocd; /* nr * KO_D */
   int64_t *rnz;            /* nr * 2: reserve pod NonZeroRequested cpu, memory */
+  /* DeviceShare: the reserve pod's device allocation and its assigned pods' allocations on those minors
+   * ([nr][KS_DEV_WORDS], ks_reservation_cols.dev_*); dheld: the reservation holds a device */
+  int64_t *dal, *dald;
+  uint8_t *dheld;
 } ko_rsv;
 
 typedef struct ko_sched {
@@ -1264,36 +1268,61 @@ static int64_t rsv_score(const ko_rsv *rv, const ko_pod *p, int32_t r) {
   return w ? sum / w : 0;
 }
 
+static int rsv_dev_candidate(const ko_sched *s, const ko_pod *p, int64_t n, int32_t r, int64_t *ds_score);
+static int rsv_dev_pod(const ko_sched *s, const ko_pod *p);
+
 /* NominateReservation (nominator.go:134-192): FilterReservation survivors, lowest order label
  * first (findMostPreferredReservationByOrder), else the highest scoreReservation (ties: table
  * order).  Also returns the node's preferred order over every matched reservation (PreScore :65). */
 static int32_t rsv_nominate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_rstate *st, int64_t *node_order) {
   const ko_rsv *rv = &s->rv;
-  int64_t mo = INT64_MAX, bo = INT64_MAX, bs = -1;
-  int32_t by_order = -1, by_score = -1;
+  int64_t mo = INT64_MAX, bo = INT64_MAX;
+  int32_t by_order = -1;
   if (node_order) *node_order = 0;
   if (!st->has || st->nmatched == 0) return -1;
+  const int dev = rsv_dev_pod(s, p);
+  const int32_t cnt = rv->beg[n + 1] - rv->beg[n];
+  int32_t *surv = (int32_t *)calloc((size_t)(cnt > 0 ? cnt : 1), 4);
+  int64_t *rsc = (int64_t *)calloc((size_t)(cnt > 0 ? cnt : 1), 8), *dsc = (int64_t *)calloc((size_t)(cnt > 0 ? cnt : 1), 8);
+  int ns = 0;
+  int64_t dmax = 0;
   for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
     int32_t r = rv->row[i];
     if (!rsv_matched(rv, p, r)) continue;
     int64_t o = rv->order[r];
     if (o != 0 && mo > o) mo = o;
-    if (!rsv_satisfies(s, p, n, st, r)) continue; /* FilterReservation (plugin.go:503-530) */
+    /* RunReservationFilterPlugins: Reservation's FilterReservation (plugin.go:503-530), then DeviceShare's
+     * (deviceshare/plugin.go:322-358: a pod with device requests needs a reservation holding devices from which
+     * tryAllocateFromReservation allocates) */
+    if (!rsv_satisfies(s, p, n, st, r)) continue;
+    int64_t ds = 0;
+    if (dev && !rsv_dev_candidate(s, p, n, r, &ds)) continue;
     if (o != 0 && bo > o) {
       bo = o;
       by_order = r;
     }
-    int64_t sc = rsv_score(rv, p, r);
-    if (sc > bs) {
-      bs = sc;
-      by_score = r;
-    }
+    surv[ns] = r;
+    rsc[ns] = rsv_score(rv, p, r);
+    dsc[ns] = ds;
+    if (ds > dmax) dmax = ds;
+    ns++;
   }
   if (node_order && mo != INT64_MAX) *node_order = mo;
-  /* RunReservationFilterPlugins also runs DeviceShare's FilterReservation (deviceshare/plugin.go:322-358): for a pod
-   * with device requests it fails for every reservation whose reserve pod holds no device (RestoreReservation's
-   * matched list, reservation.go:133-171, keeps only device-holding ones) -- every reservation modelled here */
-  if (s->cfg.deviceshare.enable && (p->has_gpu || p->rdma > 0)) return -1;
+  /* prioritizeReservations (nominator.go:218-262): Reservation's ScoreReservation (no normalization) plus DeviceShare's
+   * (scoreWithReservation, DefaultReservationNormalizeScore(100): 100 * s / max when max > 0); the highest sum, ties in
+   * table order (sort.Slice is an insertion sort for <= 12 entries) */
+  int32_t by_score = -1;
+  int64_t bs = -1;
+  for (int i = 0; i < ns; i++) {
+    const int64_t t = rsc[i] + (dmax > 0 ? 100 * dsc[i] / dmax : dsc[i]);
+    if (t > bs) {
+      bs = t;
+      by_score = surv[i];
+    }
+  }
+  free(surv);
+  free(rsc);
+  free(dsc);
   return by_order >= 0 ? by_order : by_score;
 }
 
@@ -1319,6 +1348,35 @@ static const int64_t *dev_used(const ko_sched *s, int64_t n, int k) { return s->
  * Returns 0 for an absent minor (all-zero total). */
 static int dev_pcie(const ko_sched *s, int64_t n, int type, int k);
 
+/* The node device one AutopilotAllocator call sees (device_allocator.go:94-158, device_cache.go:314-395):
+ * allow -- the topology manager's NUMA affinity (KO_ALLOW_ALL = none); pre -- preemptibleDeviceResources per device
+ * word (KS_DEV_WORDS layout; calcFreeWithPreemptible: used' = max(0, used - pre), free = max(0, total - used')),
+ * NULL = none; reqtype[t] -- requiredDeviceResources has type t: only the minors reqm[t] exist, with free = req[w]
+ * (nodeDevice.filter: used = max(0, total - free)); required / preferred -- the required and preferred minor sets
+ * of defaultAllocateDevices (0 = none; preferred minors replace the preferred-PCIe order,
+ * sortDeviceResourcesByMinor); scored -- the allocator has a scorer (Reserve, Score, ScoreReservation; Filter,
+ * FilterReservation and the topology hints run without one, so every minor scores 0 there). */
+typedef struct {
+  uint32_t allow;
+  const int64_t *pre;
+  const int64_t *req;
+  int reqtype[KO_NTYPES];
+  uint32_t reqm[KO_NTYPES];
+  uint32_t required[KO_NTYPES], preferred[KO_NTYPES];
+  int scored;
+} ko_dctx;
+
+static ko_dctx dctx_plain(uint32_t allow, int scored) {
+  ko_dctx c;
+  memset(&c, 0, sizeof(c));
+  c.allow = allow;
+  c.scored = scored;
+  return c;
+}
+
+/* device word of (type, minor, resource q) in the KS_DEV_WORDS layout */
+static int dev_word(int type, int k, int q) { return type == KO_T_GPU ? q * KO_GPUS + k : 3 * KO_GPUS + k; }
+
 /* Minor k of `type` belongs to the node device the allocator sees: with a NUMA affinity (topology manager
  * store, deviceshare/plugin.go:292-303) filterNodeDevice keeps only devices whose topology NUMA node is in the
  * affinity (device_allocator.go:134-158); allow = bit per NUMA node id, KO_ALLOW_ALL = no affinity. */
@@ -1328,19 +1386,24 @@ static int dev_allowed(const ko_sched *s, int64_t n, int type, int k, uint32_t a
   return pc != KS_PCIE_NONE && ((allow >> s->dv.pnuma[(size_t)n * KO_PCIE + pc]) & 1u);
 }
 
-static int dev_minor(const ko_sched *s, int64_t n, int type, int k, int64_t tot[3], int64_t fre[3], uint32_t allow) {
+static int dev_minor(const ko_sched *s, int64_t n, int type, int k, int64_t tot[3], int64_t fre[3], const ko_dctx *c) {
   tot[0] = tot[1] = tot[2] = fre[0] = fre[1] = fre[2] = 0;
-  if (!dev_allowed(s, n, type, k, allow)) return 0;
-  if (type == KO_T_GPU) {
-    const int64_t *t = dev_total(s, n, k), *u = dev_used(s, n, k);
-    for (int q = 0; q < 3; q++) {
-      tot[q] = t[q];
-      fre[q] = t[q] > u[q] ? t[q] - u[q] : 0;
+  if (!dev_allowed(s, n, type, k, c ? c->allow : KO_ALLOW_ALL)) return 0;
+  if (c && c->reqtype[type] && !((c->reqm[type] >> k) & 1u)) return 0; /* not in requiredDeviceResources */
+  const int nq = type == KO_T_GPU ? 3 : 1;
+  for (int q = 0; q < nq; q++) {
+    const int64_t t = type == KO_T_GPU ? dev_total(s, n, k)[q] : s->dv.rtotal[(size_t)n * KO_RDMA + k];
+    int64_t u = type == KO_T_GPU ? dev_used(s, n, k)[q] : s->dv.rused[(size_t)n * KO_RDMA + k];
+    const int w = dev_word(type, k, q);
+    if (c && c->reqtype[type]) {
+      u = t - c->req[w];
+      if (u < 0) u = 0;
+    } else if (c && c->pre) {
+      u -= c->pre[w];
+      if (u < 0) u = 0;
     }
-  } else {
-    tot[0] = s->dv.rtotal[(size_t)n * KO_RDMA + k];
-    int64_t u = s->dv.rused[(size_t)n * KO_RDMA + k];
-    fre[0] = tot[0] > u ? tot[0] - u : 0;
+    tot[q] = t;
+    fre[q] = t > u ? t - u : 0;
   }
   return tot[0] != 0 || tot[1] != 0 || tot[2] != 0;
 }
@@ -1396,7 +1459,7 @@ static uint32_t dev_prepare(const ko_sched *s, const ko_pod *p, int64_t n, ko_de
     int any = 0;
     for (int k = 0; k < KO_RDMA; k++) {
       int64_t t[3], f[3];
-      any |= dev_minor(s, n, KO_T_RDMA, k, t, f, KO_ALLOW_ALL);
+      any |= dev_minor(s, n, KO_T_RDMA, k, t, f, NULL);
     }
     if (!any) return KS_R_DEV_NO_RDMA;
     int64_t q = p->rdma;
@@ -1441,11 +1504,11 @@ static int dev_fits(const ko_devreq *g, int type, const int64_t *fre) {
 }
 
 /* nodeDevice.split: how many minors of `sub` satisfy the request per instance (device_cache.go:419-433) */
-static int dev_split(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub, uint32_t allow) {
+static int dev_split(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub, const ko_dctx *dc) {
   int c = 0;
   for (int k = 0; k < dev_nminors(type); k++) {
     int64_t t[3], f[3];
-    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f, allow)) continue;
+    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f, dc)) continue;
     c += dev_fits(g, type, f);
   }
   return c;
@@ -1465,11 +1528,12 @@ static int pair_less(const ko_pair *a, const ko_pair *b) {
 }
 
 /* allocateDevices -> defaultAllocateDevices (device_allocator.go:360-462) over the minors `sub` of the
- * (filtered) node device: scoreDevices, sortDeviceResourcesByPreferredPCIe (pcie in `pref`), the first
- * maxDesiredCount = max(desired, |pref|) minors with non-zero free that satisfy the request.  Returns the
- * allocated minors as a mask (0 = "Insufficient <type> devices"). */
+ * (filtered) node device: scoreDevices (0 without a scorer), sortDeviceResourcesByPreferredPCIe (pcie in `pref`) then
+ * sortDeviceResourcesByMinor (the context's preferred minors, when any, replace the PCIe preference), the first
+ * maxDesiredCount = max(desired, |pref|) minors in the required set with non-zero free that satisfy the request.
+ * Returns the allocated minors as a mask (0 = "Insufficient <type> devices"). */
 static uint32_t dev_alloc_type(const ko_sched *s, int64_t n, const ko_devreq *g, int type, uint32_t sub, int desired,
-                               uint32_t pref, uint32_t allow) {
+                               uint32_t pref, const ko_dctx *dc) {
   int maxd = desired, npref = __builtin_popcount(pref);
   if (npref > maxd) maxd = npref;
   if (desired == 0) desired = 1;
@@ -1478,12 +1542,13 @@ static uint32_t dev_alloc_type(const ko_sched *s, int64_t n, const ko_devreq *g,
   int m = 0;
   for (int k = 0; k < dev_nminors(type); k++) {
     int64_t t[3], f[3];
-    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f, allow)) continue;
+    if (!((sub >> k) & 1u) || !dev_minor(s, n, type, k, t, f, dc)) continue;
     ko_pair *x = &r[m++];
     x->minor = k;
-    x->score = dev_scorer(s, type, t, f, g->req[type]);
+    x->score = dc->scored ? dev_scorer(s, type, t, f, g->req[type]) : 0;
     int pc = dev_pcie(s, n, type, k);
-    x->preferred = pc != KS_PCIE_NONE && ((pref >> pc) & 1u);
+    x->preferred = dc->preferred[type] ? (int)((dc->preferred[type] >> k) & 1u)
+                                       : (pc != KS_PCIE_NONE && ((pref >> pc) & 1u));
     memcpy(x->free, f, sizeof(f));
   }
   for (int i = 1; i < m; i++) /* insertion sort (a total order: minors are unique) */
@@ -1495,6 +1560,7 @@ static uint32_t dev_alloc_type(const ko_sched *s, int64_t n, const ko_devreq *g,
   uint32_t mask = 0;
   int got = 0;
   for (int i = 0; i < m && got < maxd; i++) {
+    if (dc->required[type] && !((dc->required[type] >> r[i].minor) & 1u)) continue;
     if (!r[i].free[0] && !r[i].free[1] && !r[i].free[2]) continue; /* zero resources */
     if (!dev_fits(g, type, r[i].free)) continue;
     mask |= 1u << r[i].minor;
@@ -1516,12 +1582,12 @@ static uint32_t dev_pcies_of(const ko_sched *s, int64_t n, int type, uint32_t ma
 /* jointAllocate (device_allocator.go:286-339) on the node device restricted to sub[]: the GPUs, then the
  * RDMA devices preferring the GPUs' PCIe switches.  0 = failed. */
 static int dev_joint_alloc(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, const uint32_t sub[2],
-                           uint32_t pref, uint32_t out[2], uint32_t allow) {
-  uint32_t prim = dev_alloc_type(s, n, g, KO_T_GPU, sub[KO_T_GPU], g->desired[KO_T_GPU], pref, allow);
+                           uint32_t pref, uint32_t out[2], const ko_dctx *dc) {
+  uint32_t prim = dev_alloc_type(s, n, g, KO_T_GPU, sub[KO_T_GPU], g->desired[KO_T_GPU], pref, dc);
   if (!prim) return 0;
   uint32_t pcies = dev_pcies_of(s, n, KO_T_GPU, prim);
   int desired = same_pcie ? __builtin_popcount(pcies) : 1;
-  uint32_t sec = dev_alloc_type(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], desired, pcies, allow);
+  uint32_t sec = dev_alloc_type(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], desired, pcies, dc);
   if (!sec) return 0;
   out[KO_T_GPU] = prim;
   out[KO_T_RDMA] = sec;
@@ -1543,14 +1609,14 @@ static void dev_sub_of(const ko_sched *s, int64_t n, uint32_t pcies, uint32_t su
  * per PCIe switch (newDeviceTopologyGuide / freeNodeDevicesInPCIe, numa_topology.go:109-175), per NUMA node
  * (freeNodeDevicesInNode :185-240), then the whole node.  Returns 1 with out[] on success. */
 static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int same_pcie, uint32_t out[2],
-                           uint32_t allow) {
+                           const ko_dctx *dc) {
   const uint32_t all[2] = {(1u << KO_GPUS) - 1u, (1u << KO_RDMA) - 1u};
   uint32_t exist = 0; /* switches that hold a device */
   for (int t = 0; t < KO_NTYPES; t++)
     for (int k = 0; k < dev_nminors(t); k++) {
       int64_t tt[3], ff[3];
       int pc = dev_pcie(s, n, t, k);
-      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff, allow)) exist |= 1u << pc;
+      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff, dc)) exist |= 1u << pc;
     }
   const uint8_t *pnuma = s->dv.pnuma + (size_t)n * KO_PCIE, *psock = s->dv.psock + (size_t)n * KO_PCIE;
   /* pcieSwitches in (socket, node, pcie) order = index order; preferred: free rdma instances on the switch */
@@ -1560,7 +1626,7 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
     uint32_t sub[2];
     dev_sub_of(s, n, 1u << pc, sub);
     /* (a joint pod without an RDMA request: no RDMA entry in freeDevices, no switch is preferred) */
-    swpref[pc] = g->has[KO_T_RDMA] && dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
+    swpref[pc] = g->has[KO_T_RDMA] && dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], dc) > 0;
     sw[nsw++] = pc;
   }
   /* freeNodeDevicesInPCIe: sort.Slice by (preferred desc, socket, node); stable here (insertion sort for
@@ -1576,8 +1642,8 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
   for (int i = 0; i < nsw; i++) {
     uint32_t sub[2];
     dev_sub_of(s, n, 1u << sw[i], sub);
-    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU], allow) >= g->desired[KO_T_GPU] &&
-        dev_joint_alloc(s, n, g, same_pcie, sub, 1u << sw[i], out, allow))
+    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU], dc) >= g->desired[KO_T_GPU] &&
+        dev_joint_alloc(s, n, g, same_pcie, sub, 1u << sw[i], out, dc))
       return 1;
   }
   /* groupedNodeDevices per NUMA node: preferredPCIes = the node's preferred switches */
@@ -1594,7 +1660,7 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
   for (int i = 0; i < ng; i++) {
     uint32_t sub[2];
     dev_sub_of(s, n, gp[grp[i]], sub);
-    gpref[grp[i]] = g->has[KO_T_RDMA] && dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], allow) > 0;
+    gpref[grp[i]] = g->has[KO_T_RDMA] && dev_split(s, n, g, KO_T_RDMA, sub[KO_T_RDMA], dc) > 0;
   }
   for (int i = 1; i < ng; i++)
     for (int j = i; j > 0; j--) {
@@ -1610,25 +1676,25 @@ static int dev_by_topology(const ko_sched *s, int64_t n, const ko_devreq *g, int
     uint32_t sub[2];
     dev_sub_of(s, n, gp[grp[i]], sub);
     union_pref |= gpref_pcies[grp[i]];
-    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU], allow) >= g->desired[KO_T_GPU] &&
-        dev_joint_alloc(s, n, g, same_pcie, sub, gpref_pcies[grp[i]], out, allow))
+    if (dev_split(s, n, g, KO_T_GPU, sub[KO_T_GPU], dc) >= g->desired[KO_T_GPU] &&
+        dev_joint_alloc(s, n, g, same_pcie, sub, gpref_pcies[grp[i]], out, dc))
       return 1;
   }
   /* the whole node, preferring every preferred switch */
-  return dev_joint_alloc(s, n, g, same_pcie, all, union_pref, out, allow);
+  return dev_joint_alloc(s, n, g, same_pcie, all, union_pref, out, dc);
 }
 
-/* AutopilotAllocator.Allocate (device_allocator.go:94-132) without hints, preemption or reservations:
+/* AutopilotAllocator.Allocate (device_allocator.go:94-132) without hints on the node device of `dc`:
  * tryJointAllocate, then allocateDevices for the types joint allocation did not cover.  Returns the
  * KS_R_DEV_* reason (0 = allocated, masks in out[]). */
 static uint32_t dev_allocate(const ko_sched *s, const ko_pod *p, int64_t n, const ko_devreq *g, uint32_t out[2],
-                             uint32_t allow) {
+                             const ko_dctx *dc) {
   const uint32_t all[2] = {(1u << KO_GPUS) - 1u, (1u << KO_RDMA) - 1u};
   out[0] = out[1] = 0;
   if (p->joint && g->has[KO_T_GPU]) {
     const int same = p->joint == KS_JOINT_GPU_RDMA_SAME_PCIE;
     uint32_t j[2] = {0, 0};
-    if (dev_by_topology(s, n, g, same, j, allow)) {
+    if (dev_by_topology(s, n, g, same, j, dc)) {
       /* validateJointAllocation (:255-284): the RDMA switches must equal the GPU switches */
       if (same && dev_pcies_of(s, n, KO_T_GPU, j[0]) != dev_pcies_of(s, n, KO_T_RDMA, j[1])) return KS_R_DEV_JOINT;
       out[0] = j[0];
@@ -1639,29 +1705,237 @@ static uint32_t dev_allocate(const ko_sched *s, const ko_pod *p, int64_t n, cons
   }
   for (int t = 0; t < KO_NTYPES; t++) {
     if (!g->has[t] || out[t]) continue;
-    out[t] = dev_alloc_type(s, n, g, t, all[t], g->desired[t], 0, allow);
+    out[t] = dev_alloc_type(s, n, g, t, all[t], g->desired[t], 0, dc);
     if (!out[t]) return KS_R_DEV_INSUFFICIENT;
   }
   return 0;
 }
 
-/* AutopilotAllocator.score (device_allocator.go:507-530): scoreNode per requested type, summed */
-static int64_t dev_node_score(const ko_sched *s, int64_t n, const ko_devreq *g, uint32_t allow) {
+/* AutopilotAllocator.score (device_allocator.go:507-530): scoreNode per requested type, summed; a type whose free
+ * devices are all zero is left out of the filtered node device (nodeDevice.filter, device_cache.go:351-353) */
+static int64_t dev_node_score(const ko_sched *s, int64_t n, const ko_devreq *g, const ko_dctx *dc) {
   int64_t sum = 0;
+  ko_dctx all = *dc;
+  all.allow = KO_ALLOW_ALL;
   for (int t = 0; t < KO_NTYPES; t++) {
     if (!g->has[t]) continue;
+    int anyfree = 0;
+    for (int k = 0; k < dev_nminors(t); k++) {
+      int64_t tt[3], ff[3];
+      dev_minor(s, n, t, k, tt, ff, &all);
+      anyfree |= ff[0] != 0 || ff[1] != 0 || ff[2] != 0;
+    }
+    if (!anyfree) continue;
     int64_t total[3] = {0, 0, 0}, free[3] = {0, 0, 0};
     for (int k = 0; k < dev_nminors(t); k++) {
       int64_t tt[3], ff[3];
-      if (!dev_minor(s, n, t, k, tt, ff, allow)) continue;
+      if (!dev_minor(s, n, t, k, tt, ff, dc)) continue;
       for (int q = 0; q < 3; q++) {
         total[q] += tt[q];
         free[q] += ff[q];
       }
     }
-    sum += dev_scorer(s, t, total, free, g->req[t]);
+    if (total[0] || total[1] || total[2]) sum += dev_scorer(s, t, total, free, g->req[t]);
   }
   return sum;
+}
+
+/* ---- DeviceShare with device-holding reservations (deviceshare/reservation.go) ----
+ * RestoreReservation (:118-171) per node the transformer processed: matched = the Reservation plugin's matched
+ * reservations holding devices (table order), unmatched = the other eligible ones with assigned pods holding devices;
+ * allocatable = the reserve pod's allocation, allocated = its assigned pods' allocations on its minors, remained =
+ * allocatable - allocated.  mergeReservationAllocations (:83-107): mergedUnmatchedUsed = sum of max(0, allocatable -
+ * remained) over unmatched, mergedMatchedAllocatable / mergedMatchedAllocated = sums over matched. */
+typedef struct {
+  int on;                    /* the node has a restore state */
+  int64_t uu[KS_DEV_WORDS];  /* mergedUnmatchedUsed */
+  int64_t mm[KS_DEV_WORDS];  /* mergedMatchedAllocated */
+  int64_t am[KS_DEV_WORDS];  /* mergedMatchedAllocatable */
+  int nm;                    /* matched reservations holding devices */
+} ko_drs;
+
+/* DeviceShare restores reservations for this pod: both plugins on, a pod with device requests (PreRestoreReservation
+ * skip = no device requests, reservation.go:109-116) */
+static int rsv_dev_pod(const ko_sched *s, const ko_pod *p) {
+  return s->cfg.reservation.enable && s->cfg.deviceshare.enable && (p->has_gpu || p->rdma > 0) && s->rv.nr > 0;
+}
+
+static void drs_build(const ko_sched *s, const ko_pod *p, int64_t n, ko_drs *d) {
+  memset(d, 0, sizeof(*d));
+  if (!rsv_dev_pod(s, p) || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return;
+  const ko_rsv *rv = &s->rv;
+  int nm = 0, nu = 0;
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    const int32_t r = rv->row[i];
+    if (!rsv_eligible(rv, r)) continue;
+    if (rsv_matched(rv, p, r)) nm++;
+    else if (rv->assigned[r] > 0) nu++;
+  }
+  /* transformer.go:123-135: nothing to restore, or a reservation-affinity pod without matched reservations */
+  if ((nm == 0 && nu == 0) || ((p->flags & KS_POD_RSV_AFFINITY) && nm == 0)) return;
+  d->on = 1;
+  for (int32_t i = rv->beg[n]; i < rv->beg[n + 1]; i++) {
+    const int32_t r = rv->row[i];
+    if (!rsv_eligible(rv, r) || !rv->dheld[r]) continue;
+    const int64_t *al = rv->dal + (size_t)r * KS_DEV_WORDS, *ad = rv->dald + (size_t)r * KS_DEV_WORDS;
+    if (rsv_matched(rv, p, r)) {
+      d->nm++;
+      for (int w = 0; w < KS_DEV_WORDS; w++) {
+        d->mm[w] += ad[w];
+        d->am[w] += al[w];
+      }
+    } else if (rv->assigned[r] > 0) {
+      for (int w = 0; w < KS_DEV_WORDS; w++) d->uu[w] += ad[w] > 0 ? ad[w] : 0;
+    }
+  }
+}
+
+/* newDeviceMinorMap(allocatable): the reservation's minors per type */
+static uint32_t rsv_dev_minors(const ko_rsv *rv, int32_t r, int type) {
+  const int64_t *al = rv->dal + (size_t)r * KS_DEV_WORDS;
+  uint32_t m = 0;
+  for (int k = 0; k < dev_nminors(type); k++) {
+    int nz = 0;
+    for (int q = 0; q < (type == KO_T_GPU ? 3 : 1); q++) nz |= al[dev_word(type, k, q)] != 0;
+    if (nz) m |= 1u << k;
+  }
+  return m;
+}
+
+/* calcRequiredDeviceResources (reservation.go:273-292): remained restricted to the reservation's minors (a minor whose
+ * remained is all-zero drops out); with nothing left at all, every minor of the reservation with no resources */
+static void drs_required(const ko_rsv *rv, int32_t r, ko_dctx *c, int64_t req[KS_DEV_WORDS]) {
+  const int64_t *al = rv->dal + (size_t)r * KS_DEV_WORDS, *ad = rv->dald + (size_t)r * KS_DEV_WORDS;
+  int any = 0;
+  memset(req, 0, sizeof(int64_t) * KS_DEV_WORDS);
+  for (int t = 0; t < KO_NTYPES; t++) {
+    const uint32_t pm = rsv_dev_minors(rv, r, t);
+    c->reqm[t] = 0;
+    for (int k = 0; k < dev_nminors(t); k++) {
+      if (!((pm >> k) & 1u)) continue;
+      int nz = 0;
+      for (int q = 0; q < (t == KO_T_GPU ? 3 : 1); q++) {
+        const int w = dev_word(t, k, q);
+        req[w] = al[w] - ad[w];
+        nz |= req[w] != 0;
+      }
+      if (nz) c->reqm[t] |= 1u << k;
+    }
+    c->reqtype[t] = c->reqm[t] != 0;
+    any |= c->reqtype[t];
+  }
+  if (!any) {
+    memset(req, 0, sizeof(int64_t) * KS_DEV_WORDS);
+    for (int t = 0; t < KO_NTYPES; t++) {
+      c->reqm[t] = rsv_dev_minors(rv, r, t);
+      c->reqtype[t] = c->reqm[t] != 0;
+    }
+  }
+  c->req = req;
+}
+
+/* preemptible of reservation r: mergedUnmatchedUsed + mergedMatchedAllocated + r's remained (reservation.go:199, 215) */
+static void drs_pre_of(const ko_rsv *rv, const ko_drs *d, int32_t r, int64_t pre[KS_DEV_WORDS]) {
+  const int64_t *al = rv->dal + (size_t)r * KS_DEV_WORDS, *ad = rv->dald + (size_t)r * KS_DEV_WORDS;
+  for (int w = 0; w < KS_DEV_WORDS; w++) pre[w] = d->uu[w] + d->mm[w] + al[w] - ad[w];
+}
+
+/* tryAllocateFromReservation's body for one reservation (reservation.go:201-240): Default / Aligned allocate with the
+ * reservation's minors preferred; Restricted requires them, first as minors, then with the remained resources as the
+ * devices' free amounts.  0 = allocated (out[]). */
+static uint32_t drs_try(const ko_sched *s, const ko_pod *p, int64_t n, const ko_devreq *g, const ko_drs *d, int32_t r,
+                        uint32_t allow, int scored, uint32_t out[2]) {
+  const ko_rsv *rv = &s->rv;
+  int64_t pre[KS_DEV_WORDS], req[KS_DEV_WORDS];
+  drs_pre_of(rv, d, r, pre);
+  ko_dctx c = dctx_plain(allow, scored);
+  c.pre = pre;
+  for (int t = 0; t < KO_NTYPES; t++) c.preferred[t] = rsv_dev_minors(rv, r, t);
+  const uint32_t pol = rv->policy[r];
+  if (pol == KS_RSV_POLICY_DEFAULT || pol == KS_RSV_POLICY_ALIGNED) return dev_allocate(s, p, n, g, out, &c);
+  if (pol != KS_RSV_POLICY_RESTRICTED) return KS_R_DEV_INSUFFICIENT;
+  for (int t = 0; t < KO_NTYPES; t++) c.required[t] = c.preferred[t];
+  const uint32_t rr = dev_allocate(s, p, n, g, out, &c);
+  if (rr) return rr;
+  drs_required(rv, r, &c, req);
+  return dev_allocate(s, p, n, g, out, &c);
+}
+
+/* the node device outside every reservation's preference: mergedUnmatchedUsed + mergedMatchedAllocatable */
+static void drs_fallback(const ko_drs *d, int64_t pre[KS_DEV_WORDS]) {
+  for (int w = 0; w < KS_DEV_WORDS; w++) pre[w] = d->uu[w] + d->am[w];
+}
+
+/* DeviceShare Filter with the restore state (deviceshare/plugin.go:271-320): tryAllocateFromReservation over the
+ * matched reservations (required from them for a reservation-affinity pod: KS_R_RSV_NO_FIT, "no reservation(s) to meet
+ * the device requirements"), else Allocate with the fallback preemptible.  0 = feasible. */
+static uint32_t drs_filter(const ko_sched *s, const ko_pod *p, int64_t n, const ko_devreq *g, const ko_drs *d,
+                           uint32_t allow) {
+  uint32_t out[2];
+  if (!d->on) {
+    const ko_dctx c = dctx_plain(allow, 0);
+    return dev_allocate(s, p, n, g, out, &c);
+  }
+  const ko_rsv *rv = &s->rv;
+  for (int32_t i = rv->beg[n]; d->nm && i < rv->beg[n + 1]; i++) {
+    const int32_t r = rv->row[i];
+    if (rsv_eligible(rv, r) && rv->dheld[r] && rsv_matched(rv, p, r) && drs_try(s, p, n, g, d, r, allow, 0, out) == 0) return 0;
+  }
+  if (d->nm && (p->flags & KS_POD_RSV_AFFINITY)) return KS_R_RSV_NO_FIT;
+  int64_t pre[KS_DEV_WORDS];
+  drs_fallback(d, pre);
+  ko_dctx c = dctx_plain(allow, 0);
+  c.pre = pre;
+  return dev_allocate(s, p, n, g, out, &c);
+}
+
+/* scoreWithReservation (reservation.go:249-271): the node score on reservation r's view (Restricted: its remained as
+ * the required resources) */
+static int64_t drs_score_rsv(const ko_sched *s, int64_t n, const ko_devreq *g, const ko_drs *d, int32_t r, uint32_t allow) {
+  int64_t pre[KS_DEV_WORDS], req[KS_DEV_WORDS];
+  drs_pre_of(&s->rv, d, r, pre);
+  ko_dctx c = dctx_plain(allow, 1);
+  c.pre = pre;
+  if (s->rv.policy[r] == KS_RSV_POLICY_RESTRICTED) drs_required(&s->rv, r, &c, req);
+  return dev_node_score(s, n, g, &c);
+}
+
+/* DeviceShare Score (scoring.go:30-90): with a nominated reservation its view, else the fallback view */
+static int64_t drs_score(const ko_sched *s, int64_t n, const ko_devreq *g, const ko_drs *d, int32_t nom, uint32_t allow) {
+  if (d->on && nom >= 0 && s->rv.dheld[nom]) return drs_score_rsv(s, n, g, d, nom, allow);
+  int64_t pre[KS_DEV_WORDS];
+  ko_dctx c = dctx_plain(allow, 1);
+  if (d->on) {
+    drs_fallback(d, pre);
+    c.pre = pre;
+  }
+  return dev_node_score(s, n, g, &c);
+}
+
+/* DeviceShare's FilterReservation + ScoreReservation for reservation r (plugin.go:322-358, scoring.go:99-142):
+ * the reservation holds devices and tryAllocateFromReservation([r], required) allocates; ds_score = its
+ * scoreWithReservation.  Returns 1 when r passes. */
+static int rsv_dev_candidate(const ko_sched *s, const ko_pod *p, int64_t n, int32_t r, int64_t *ds_score) {
+  *ds_score = 0;
+  if (!s->rv.dheld[r] || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT)) return 0;
+  ko_drs d;
+  drs_build(s, p, n, &d);
+  if (!d.on) return 0;
+  ko_devreq g;
+  if (dev_prepare(s, p, n, &g)) return 0;
+  uint32_t out[2];
+  if (drs_try(s, p, n, &g, &d, r, KO_ALLOW_ALL, 0, out)) return 0;
+  *ds_score = drs_score_rsv(s, n, &g, &d, r, KO_ALLOW_ALL);
+  return 1;
+}
+
+/* DeviceShare Score of a feasible node once the nomination is known (eval_node) */
+static int64_t dev_rsv_node_score(const ko_sched *s, const ko_pod *p, int64_t n, int32_t nom) {
+  ko_drs d;
+  drs_build(s, p, n, &d);
+  ko_devreq g;
+  if (!d.on || dev_prepare(s, p, n, &g)) return -1;
+  return drs_score(s, n, &g, &d, nom, KO_ALLOW_ALL);
 }
 
 /* DeviceShare Filter; *raw gets the node score (scoreNode) when feasible.  allow: the node's NUMA affinity from
@@ -1673,22 +1947,49 @@ static uint32_t dev_eval(const ko_sched *s, const ko_pod *p, int64_t n, int64_t 
   ko_devreq g;
   uint32_t r = dev_prepare(s, p, n, &g);
   if (r) return r;
-  uint32_t m[2];
-  r = dev_allocate(s, p, n, &g, m, allow);
+  ko_drs d;
+  drs_build(s, p, n, &d);
+  r = drs_filter(s, p, n, &g, &d, allow);
   if (r) return r;
-  *raw = dev_node_score(s, n, &g, allow);
+  *raw = drs_score(s, n, &g, &d, -1, allow); /* (eval_node re-scores once the nomination is known) */
   return 0;
 }
 
 /* Reserve -> nodeDevice.updateCacheUsed: used += the request per instance on each allocated minor */
-static void dev_reserve(ko_sched *s, const ko_pod *p, int64_t n, uint32_t *gpu_minors, uint32_t *rdma_minors,
+/* Reserve (plugin.go:377-430): allocateWithNominatedReservation (reservation.go:294-333: tryAllocateFromReservation on
+ * the nominated reservation), else Allocate with the fallback preemptible; with the scorer.  nom = the nominated
+ * reservation (-1); the restore state is the cycle's, i.e. before the Reservation plugin's own Reserve.  The pod's
+ * allocation on the nominated reservation's minors becomes part of its allocated (the reservation's AssignedPods). */
+static void dev_reserve(ko_sched *s, const ko_pod *p, int64_t n, int32_t nom, uint32_t *gpu_minors, uint32_t *rdma_minors,
                         uint32_t allow) {
   *gpu_minors = *rdma_minors = 0;
   if (!s->cfg.deviceshare.enable || !(p->has_gpu || p->rdma > 0) || !s->dv.loaded || !(s->dv.flags[n] & KS_DEV_PRESENT))
     return;
   ko_devreq g;
   uint32_t m[2];
-  if (dev_prepare(s, p, n, &g) || dev_allocate(s, p, n, &g, m, allow)) return;
+  if (dev_prepare(s, p, n, &g)) return;
+  ko_drs d;
+  drs_build(s, p, n, &d);
+  int done = 0;
+  if (d.on && nom >= 0 && s->rv.dheld[nom]) done = drs_try(s, p, n, &g, &d, nom, allow, 1, m) == 0;
+  if (!done) {
+    int64_t pre[KS_DEV_WORDS];
+    ko_dctx rc = dctx_plain(allow, 1);
+    if (d.on) {
+      drs_fallback(&d, pre);
+      rc.pre = pre;
+    }
+    if (dev_allocate(s, p, n, &g, m, &rc)) return;
+  }
+  if (nom >= 0 && s->cfg.reservation.enable && s->rv.dheld[nom]) {
+    int64_t *ad = s->rv.dald + (size_t)nom * KS_DEV_WORDS;
+    for (int t = 0; t < KO_NTYPES; t++) {
+      const uint32_t pm = rsv_dev_minors(&s->rv, nom, t) & m[t];
+      for (int k = 0; k < dev_nminors(t); k++)
+        if ((pm >> k) & 1u)
+          for (int q = 0; q < (t == KO_T_GPU ? 3 : 1); q++) ad[dev_word(t, k, q)] += g.req[t][q];
+    }
+  }
   for (int k = 0; k < KO_GPUS; k++) {
     if (!((m[0] >> k) & 1u)) continue;
     int64_t *u = s->dv.used + ((size_t)n * KO_GPUS + k) * 3;
@@ -1718,7 +2019,7 @@ static void dev_hints(const ko_sched *s, const ko_pod *p, int64_t n, ko_devhints
     for (int k = 0; k < dev_nminors(t); k++) {
       int64_t tt[3], ff[3];
       const int pc = dev_pcie(s, n, t, k);
-      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff, KO_ALLOW_ALL)) ids |= 1u << pnuma[pc];
+      if (pc != KS_PCIE_NONE && dev_minor(s, n, t, k, tt, ff, NULL)) ids |= 1u << pnuma[pc];
     }
   ko_devreq g;
   if (dev_prepare(s, p, n, &g)) return;
@@ -1737,7 +2038,7 @@ static void dev_hints(const ko_sched *s, const ko_pod *p, int64_t n, ko_devhints
       for (int k = 0; k < dev_nminors(t); k++) {
         int64_t tt[3], ff[3];
         const int pc = dev_pcie(s, n, t, k);
-        if (pc != KS_PCIE_NONE && ((mask >> pnuma[pc]) & 1u) && dev_minor(s, n, t, k, tt, ff, KO_ALLOW_ALL)) cnt[t]++;
+        if (pc != KS_PCIE_NONE && ((mask >> pnuma[pc]) & 1u) && dev_minor(s, n, t, k, tt, ff, NULL)) cnt[t]++;
       }
     int enough = 1;
     for (int t = 0; t < KO_NTYPES; t++)
@@ -1746,7 +2047,8 @@ static void dev_hints(const ko_sched *s, const ko_pod *p, int64_t n, ko_devhints
     if (minaff < 0) minaff = nid;
     if (__builtin_popcount(mask) < minaff) minaff = __builtin_popcount(mask);
     uint32_t out[2];
-    if (dev_allocate(s, p, n, &g, out, mask) == 0) h->mask[h->nh++] = mask;
+    const ko_dctx hc = dctx_plain(mask, 0);
+    if (dev_allocate(s, p, n, &g, out, &hc) == 0) h->mask[h->nh++] = mask;
   }
   if (minaff < 0) return;
   /* quotav1.ResourceNames(requestsPerInstance): gpu-core (requested, or the multi-device split), gpu-memory,
@@ -2001,6 +2303,7 @@ void ko_destroy(ko_sched *s) {
   ko_rsv *rv = &s->rv;
   free(rv->beg); free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
   free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
+  free(rv->dal); free(rv->dald); free(rv->dheld);
   npods_free(s);
   free(s);
 }
@@ -2010,7 +2313,11 @@ int ko_load_reservations(ko_sched *s, const ks_reservation_cols *rc, int32_t nr)
   ko_rsv *rv = &s->rv;
   free(rv->row); free(rv->node); free(rv->assigned); free(rv->cls); free(rv->flags);
   free(rv->policy); free(rv->keys); free(rv->order); free(rv->alloc); free(rv->allocd); free(rv->rnz);
+  free(rv->dal); free(rv->dald); free(rv->dheld);
   size_t m = (size_t)(nr > 0 ? nr : 1);
+  rv->dal = (int64_t *)calloc(m * KS_DEV_WORDS, 8);
+  rv->dald = (int64_t *)calloc(m * KS_DEV_WORDS, 8);
+  rv->dheld = (uint8_t *)calloc(m, 1);
   rv->nr = nr;
   rv->row = (int32_t *)calloc(m, 4);
   rv->node = (int32_t *)calloc(m, 4);
@@ -2043,6 +2350,12 @@ int ko_load_reservations(ko_sched *s, const ks_reservation_cols *rc, int32_t nr)
     nonzero_of(rv->alloc + (size_t)r * KO_D, rv->keys[r], nz);
     rv->rnz[2 * r] = rc->reserve_nonzero_milli_cpu ? rc->reserve_nonzero_milli_cpu[r] : nz[0];
     rv->rnz[2 * r + 1] = rc->reserve_nonzero_memory ? rc->reserve_nonzero_memory[r] : nz[1];
+    for (int w = 0; w < KS_DEV_WORDS; w++) {
+      const size_t o = (size_t)r * KS_DEV_WORDS + w;
+      rv->dal[o] = rc->dev_allocatable ? rc->dev_allocatable[o] : 0;
+      rv->dald[o] = rc->dev_allocated ? rc->dev_allocated[o] : 0;
+      rv->dheld[r] |= rv->dal[o] != 0;
+    }
   }
   for (int64_t n = 0; n < s->n; n++) rv->beg[n + 1] += rv->beg[n];
   int32_t *fill = (int32_t *)calloc((size_t)(s->n > 0 ? s->n : 1), 4);
@@ -2192,6 +2505,11 @@ int ko_read_reservations(const ko_sched *s, int64_t *allocated, int32_t *assigne
   return 0;
 }
 
+int ko_read_reservation_devices(const ko_sched *s, int64_t *dev_allocated) {
+  if (dev_allocated && s->rv.dald) memcpy(dev_allocated, s->rv.dald, (size_t)s->rv.nr * KS_DEV_WORDS * 8);
+  return 0;
+}
+
 int ko_load_quotas(ko_sched *s, const ks_quota_cols *qc, int32_t nq) {
   free(s->q);
   s->nq = nq;
@@ -2248,6 +2566,11 @@ static uint32_t eval_node(ko_sched *s, const ko_pod *p0, int64_t n, int64_t *fit
     int32_t nom = rsv_nominate(s, p, n, &st, &s->rord[n]);
     s->nom[n] = nom;
     s->rraw[n] = nom >= 0 ? rsv_score(&s->rv, p, nom) : 0;
+    /* DeviceShare Score runs after PreScore's nomination: on a restored node its view depends on it */
+    if (s->draw[n] >= 0 && s->cfg.deviceshare.enable && !npc.on) {
+      const int64_t ds = dev_rsv_node_score(s, p, n, nom);
+      if (ds >= 0) s->draw[n] = ds;
+    }
   }
   return 0;
 }
@@ -2807,11 +3130,11 @@ int ko_schedule(ko_sched *s, const ks_pod_cols *pc, int32_t np, ks_result *out) 
       out[i].score = 0;
       continue;
     }
+    dev_reserve(s, &p, best_n, s->nom[best_n], &out[i].gpu_minors, &out[i].rdma_minors, allow);
     if (s->nom[best_n] >= 0) {
       out[i].reservation = s->nom[best_n];
       rsv_reserve(s, &p, s->nom[best_n]);
     }
-    dev_reserve(s, &p, best_n, &out[i].gpu_minors, &out[i].rdma_minors, allow);
     numa_reserve(s, &p, best_n, &npc);
     if (npc.on && !npc.reasons) memcpy(s->numa_allocs + (size_t)i * KS_MAX_NUMA * 2, no.alloc, sizeof(no.alloc));
     node_reserve(s, &p, best_n);
@@ -2863,11 +3186,11 @@ int ko_assume(ko_sched *s, const ks_pod_cols *pc, int32_t node, ks_result *out, 
     int64_t ord = 0;
     nom = rsv_nominate(s, &p, n, &st0, &ord);
   }
+  dev_reserve(s, &p, n, nom, &out->gpu_minors, &out->rdma_minors, allow);
   if (nom >= 0) {
     out->reservation = nom;
     rsv_reserve(s, &p, nom);
   }
-  dev_reserve(s, &p, n, &out->gpu_minors, &out->rdma_minors, allow);
   numa_reserve(s, &p, n, &npc);
   node_reserve(s, &p, n);
   quota_reserve(s, &p);
@@ -2929,6 +3252,17 @@ int ko_unreserve(ko_sched *s, const ks_pod_cols *pc, const ks_result *r, const u
       }
       for (int k = 0; k < KO_RDMA; k++)
         if ((r->rdma_minors >> k) & 1u) s->dv.rused[(size_t)n * KO_RDMA + k] -= g.req[KO_T_RDMA][0];
+      /* the pod leaves its reservation's AssignedPods: its allocation on the reservation's minors too */
+      if (r->reservation >= 0 && s->cfg.reservation.enable && s->rv.dheld[r->reservation]) {
+        int64_t *ad = s->rv.dald + (size_t)r->reservation * KS_DEV_WORDS;
+        const uint32_t mm[2] = {r->gpu_minors, r->rdma_minors};
+        for (int t = 0; t < KO_NTYPES; t++) {
+          const uint32_t pm = rsv_dev_minors(&s->rv, r->reservation, t) & mm[t];
+          for (int k = 0; k < dev_nminors(t); k++)
+            if ((pm >> k) & 1u)
+              for (int q = 0; q < (t == KO_T_GPU ? 3 : 1); q++) ad[dev_word(t, k, q)] -= g.req[t][q];
+        }
+      }
     }
   }
   /* NodeAllocation.release: the CPUs (refcount 1 -> removed) and the NUMA-node resources
@@ -3398,4 +3732,45 @@ int ko_preempt(ko_sched *s, const ks_pod_cols *pc, int32_t prio, uint32_t pflags
   free(dry);
   free(cand);
   return 0;
+}
+
+/* ---- test hooks: DeviceShare's reservation restore and tryAllocateFromReservation on one node, pinned by
+ * deviceshare/reservation_test.go (tests/golden/deviceshare_reservation.json) ---- */
+
+/* RestoreReservation + mergeReservationAllocations for pod 0 of pc on `node` (reservation.go:83-171): the merged
+ * mergedUnmatchedUsed / mergedMatchedAllocated / mergedMatchedAllocatable ([KS_DEV_WORDS] each) and the number of
+ * matched reservations holding devices; -1 when the node has no restore state */
+int ko_test_device_restore(ko_sched *s, const ks_pod_cols *pc, int64_t node, int64_t *uu, int64_t *mm, int64_t *am) {
+  if (node < 0 || node >= s->n) return -1;
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  ko_drs d;
+  drs_build(s, &p, node, &d);
+  if (!d.on) return -1;
+  memcpy(uu, d.uu, sizeof(d.uu));
+  memcpy(mm, d.mm, sizeof(d.mm));
+  memcpy(am, d.am, sizeof(d.am));
+  return d.nm;
+}
+
+/* tryAllocateFromReservation (reservation.go:182-246) over the reservation rows rows[0..m) as the matched list, with
+ * the given mergedUnmatchedUsed (basic preemptible) and mergedMatchedAllocated, without a scorer (Filter).  Returns 1
+ * with the allocation in out[] (GPU, RDMA minor masks), 0 for no result (nil, nil), -1 for "node(s) no
+ * reservation(s) to meet the device requirements" (required). */
+int ko_test_try_reservation(ko_sched *s, const ks_pod_cols *pc, int64_t node, const int32_t *rows, int32_t m,
+                            const int64_t *uu, const int64_t *mm, int32_t required, uint32_t *out) {
+  if (node < 0 || node >= s->n) return -2;
+  ko_pod p;
+  load_pod(s, pc, 0, &p);
+  ko_devreq g;
+  if (dev_prepare(s, &p, node, &g)) return -2;
+  if (m == 0) return 0;
+  ko_drs d;
+  memset(&d, 0, sizeof(d));
+  d.on = 1;
+  memcpy(d.uu, uu, sizeof(d.uu));
+  memcpy(d.mm, mm, sizeof(d.mm));
+  for (int32_t i = 0; i < m; i++)
+    if (drs_try(s, &p, node, &g, &d, rows[i], KO_ALLOW_ALL, 0, out) == 0) return 1;
+  return required ? -1 : 0;
 }

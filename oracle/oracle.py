@@ -42,6 +42,7 @@ def lib():
         L.ko_load_quotas.argtypes = [C.c_void_p, C.POINTER(abi.KsQuotaCols), C.c_int32]
         L.ko_load_reservations.argtypes = [C.c_void_p, C.POINTER(abi.KsReservationCols), C.c_int32]
         L.ko_read_reservations.argtypes = [C.c_void_p, abi.P64, abi.P32]
+        L.ko_read_reservation_devices.argtypes = [C.c_void_p, abi.P64]
         L.ko_load_devices.argtypes = [C.c_void_p, C.POINTER(abi.KsDeviceCols)]
         L.ko_read_devices.argtypes = [C.c_void_p, abi.P64, abi.P64, abi.P64]
         L.ko_read_devices_rdma.argtypes = [C.c_void_p, abi.P64]
@@ -256,6 +257,11 @@ class Oracle:
         assigned = np.zeros(max(self.nr, 1), np.int32)
         self.L.ko_read_reservations(self.h, allocated.ctypes.data_as(abi.P64), assigned.ctypes.data_as(abi.P32))
         return allocated[: self.nr * abi.KS_RSV_DIMS].reshape(self.nr, abi.KS_RSV_DIMS), assigned[: self.nr]
+
+    def read_reservation_devices(self):
+        out = np.zeros(max(self.nr, 1) * abi.KS_DEV_WORDS, np.int64)
+        self.L.ko_read_reservation_devices(self.h, out.ctypes.data_as(abi.P64))
+        return out[: self.nr * abi.KS_DEV_WORDS].reshape(self.nr, abi.KS_DEV_WORDS)
 
     def read_devices(self):
         G = abi.KS_MAX_GPUS

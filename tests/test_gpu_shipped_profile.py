@@ -45,6 +45,10 @@ def check(runtime, oracle_lib, w, label, pipeline=None, vshards=0):
         assert bad.size == 0, f"{label}: cpusets differ for pods {bad[:8]}: {[mask_cpus(cs_g[i]) for i in bad[:2]]}"
         for a, b in zip(ev.read_reservations(), orc.read_reservations()):
             assert np.array_equal(a, b), f"{label}: reservations differ"
+        if w.reservations.dev_allocatable is not None:
+            rg, ro = ev.read_reservation_devices(), orc.read_reservation_devices()
+            bad = np.nonzero((rg != ro).any(axis=1))[0]
+            assert bad.size == 0, f"{label}: reservation device allocations differ at rows {bad[:8]}"
         for a, b in zip(ev.read_cpu_state(), orc.read_cpu_state()):
             assert np.array_equal(a, b), f"{label}: CPU state differs"
         for g, o in zip(ev.read_devices(), orc.read_devices()):
@@ -77,6 +81,7 @@ def test_shipped_profile_5k_nodes(runtime, oracle_lib):
     c = coverage(w, check(runtime, oracle_lib, w, "c3rsv-5k"))
     # a device pod is never assumed into a reservation holding no device (DeviceShare's FilterReservation,
     # deviceshare/plugin.go:322-358), though the restore still frees the matched reservations' resources for it
+    # (these reservations hold none: test_shipped_profile_device_reservations has ones that do)
     assert c["into_rsv_on_policy"] > 300 and c["bind_into_rsv"] > 300 and c["dev_matched_placed"] > 300, c
     assert c["dev_into_rsv"] == 0, c
 
@@ -87,6 +92,38 @@ def test_shipped_profile_policies(runtime, oracle_lib, seed, policy):
     w = synth.c3_rsv(seed=seed, n_nodes=700, n_pods=1500, policy=policy, policy_frac=0.7, rsv_per_node=3.0)
     c = coverage(w, check(runtime, oracle_lib, w, f"c3rsv-policy{policy}"))
     assert c["into_rsv_on_policy"] > 100, c
+
+
+@pytest.mark.parametrize("seed", [87, 88])
+def test_shipped_profile_device_reservations(runtime, oracle_lib, seed):
+    """Reservations holding GPUs / RDMA (deviceshare/reservation.go): on non-policy device nodes 70 % of the
+    reservations hold one or two GPU instances (whole or half) and half of those an RDMA share; the matched ones are
+    allocated from first (Default / Aligned prefer their minors, Restricted requires them), the unmatched ones' assigned
+    use is given back, device pods are nominated into them by FilterReservation / ScoreReservation"""
+    w = synth.c3_rsv(seed=seed, n_nodes=600, n_pods=1500, policy_frac=0.3, dev_rsv_frac=0.7)
+    held = (w.reservations.dev_allocatable != 0).any(axis=1)
+    assert held.mean() > 0.3
+    got = check(runtime, oracle_lib, w, f"c3rsv-devrsv{seed}")
+    c = coverage(w, got)
+    into = got["reservation"]
+    assert c["dev_into_rsv"] > 50 and held[into[into >= 0]].sum() > 50, c
+
+
+def test_shipped_profile_device_reservations_eval_pod(runtime, oracle_lib):
+    w = synth.c3_rsv(seed=89, n_nodes=300, n_pods=300, policy_frac=0.3, dev_rsv_frac=0.7)
+    ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
+    orc = oracle_lib.Oracle(w.cfg, w.nodes.copy(), **w.tables())
+    try:
+        for i in range(0, 300, 3):
+            one = w.pods.rows([i])
+            r_g, s_g, t_g = ev.eval_pod(one)
+            r_o, s_o, t_o = orc.eval_pod(one)
+            assert np.array_equal(r_g, r_o), f"pod {i}: reasons at nodes {np.nonzero(r_g != r_o)[0][:5]}"
+            assert np.array_equal(s_g, s_o), f"pod {i}: scores at nodes {np.nonzero((s_g != s_o).any(axis=1))[0][:5]}"
+            assert np.array_equal(t_g, t_o), f"pod {i}: totals"
+    finally:
+        ev.close()
+        orc.close()
 
 
 def test_shipped_profile_tight(runtime, oracle_lib):

@@ -212,3 +212,26 @@ def test_device_pods_never_nominated_into_device_less_reservations():
     got2 = orc.schedule(w.pods)
     orc.close()
     assert (dev & (got2["reservation"] >= 0)).sum() > 10
+
+
+def test_device_pods_into_device_holding_reservations():
+    """Reservations holding GPUs / RDMA (deviceshare/reservation.go): device pods are nominated only into them, and each
+    assigned pod's allocation on the reservation's minors joins its allocated (never outside its minors)."""
+    from koordinator_amd import synth
+
+    w = synth.c3_rsv(seed=92, n_nodes=200, n_pods=800, policy_frac=0.3, dev_rsv_frac=0.7)
+    rs = w.reservations
+    held = (rs.dev_allocatable != 0).any(axis=1)
+    dev = (w.pods.gpu_core + w.pods.gpu_memory + w.pods.gpu_memory_ratio + w.pods.rdma) > 0
+    orc = Oracle(w.cfg, w.nodes.copy(), **w.tables())
+    got = orc.schedule(w.pods)
+    dald = orc.read_reservation_devices()
+    orc.close()
+    into = got["reservation"]
+    di = dev & (into >= 0)
+    assert di.sum() > 10
+    assert held[into[di]].all()
+    grown = dald != rs.dev_allocated
+    assert grown.any()
+    assert not (grown & (rs.dev_allocatable == 0)).any()
+    assert (dald >= rs.dev_allocated).all()
