@@ -2005,7 +2005,8 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
                o_asg = o_allocd + al16(D * m * 8), o_rnz = o_asg + al16(m * 4), o_row = o_rnz + al16(2 * m * 8),
                o_ck_allocd = o_row + al16(m * 4), o_ck_asg = o_ck_allocd + al16(D * m * 8),
                o_dal = o_ck_asg + al16(m * 4), o_dald = o_dal + al16((size_t)kDevQW * m * 8),
-               o_ck_dald = o_dald + al16((size_t)kDevQW * m * 8), bytes = o_ck_dald + al16((size_t)kDevQW * m * 8);
+               o_ck_dald = o_dald + al16((size_t)kDevQW * m * 8), o_dmask = o_ck_dald + al16((size_t)kDevQW * m * 8),
+               bytes = o_dmask + al16(m * 4);
   std::vector<char> h(bytes, 0);
   int32_t* beg = (int32_t*)(h.data() + o_beg);
   uint64_t* cls = (uint64_t*)(h.data() + o_cls);
@@ -2018,6 +2019,7 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
   int32_t* rowid = (int32_t*)(h.data() + o_row);
   int64_t* dal = (int64_t*)(h.data() + o_dal);
   int64_t* dald = (int64_t*)(h.data() + o_dald);
+  uint32_t* dmask = (uint32_t*)(h.data() + o_dmask);
   for (int32_t i = 0; i < nr; ++i) beg[rc->node[perm[i]] + 1]++;
   for (int64_t n = 0; n < ctx->npad; ++n) beg[n + 1] += beg[n];
   ctx->h_rsv_gi.assign((size_t)ncaller, -1);
@@ -2040,6 +2042,7 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
         dal[(size_t)w * m + i] = rc->dev_allocatable[(size_t)r * KS_DEV_WORDS + w];
         dald[(size_t)w * m + i] = rc->dev_allocated ? rc->dev_allocated[(size_t)r * KS_DEV_WORDS + w] : 0;
         h |= dal[(size_t)w * m + i] != 0;
+        dmask[i] |= dal[(size_t)w * m + i] != 0 ? (1u << w) : 0u;
       }
       if (h) meta[i] |= kRsvMetaDev;
     }
@@ -2076,6 +2079,7 @@ static int rsv_install(ks_ctx* ctx, const ks_reservation_cols* rc, int32_t nr, c
   rv.rowid = (const int32_t*)(b + o_row);
   rv.dal = (const int64_t*)(b + o_dal);
   rv.dald = (int64_t*)(b + o_dald);
+  rv.dmask = (const uint32_t*)(b + o_dmask);
   ctx->rsv_dald_ckpt = (int64_t*)(b + o_ck_dald);
   rv.ncls = ctx->d.rsv_cls;
   rv.nr = (int64_t)m;  // row stride of the [dim][row] tables

@@ -1637,7 +1637,12 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       // DeviceShare's FilterReservation / ScoreReservation in the nomination (reservations holding devices)
       auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
         *ds = 0;
-        if constexpr (DEV) return sdv.held() && dev_rsv_candidate(cfg, pod, sdv, v, i, ds);
+        if constexpr (DEV) {
+          if (!sdv.held()) return false;
+          const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(cfg, pod), sdv, v, i);
+          *ds = (int32_t)(uint32_t)r;
+          return (r >> 32) != 0;
+        }
         return false;
       };
       RsvOut ro;

@@ -56,6 +56,7 @@ struct DevRsv {
   // on those minors, [kDevQW][nr] (ks_dev.h word layout); NULL when no reservation holds a device
   const int64_t* dal;
   int64_t* dald;          // mutable (Reserve)
+  const uint32_t* dmask;  // [nr] bit w: dal word w is non-zero (a device word the reservation holds)
   int64_t nr;
   int64_t w100;           // 100 * plugin weight
 };
@@ -109,6 +110,7 @@ struct RsvG {
   __device__ __forceinline__ int64_t rnz(int k, int64_t i) const { return gld(rv.rnz + k * rv.nr + b + i); }
   __device__ __forceinline__ int32_t csr(int64_t i) const { return (int32_t)(b + i); }
   __device__ __forceinline__ int64_t dal(int w, int64_t i) const { return gld(rv.dal + (int64_t)w * rv.nr + b + i); }
+  __device__ __forceinline__ uint32_t dmask(int64_t i) const { return gld(rv.dmask + b + i); }
   __device__ __forceinline__ int64_t dald(int w, int64_t i) const { return rld<true>(rv.dald + (int64_t)w * rv.nr + b + i); }
 };
 
@@ -136,6 +138,7 @@ struct RsvL {
   __device__ __forceinline__ int64_t rnz(int k, int64_t i) const { return rec[i].rnz[k]; }
   __device__ __forceinline__ int32_t csr(int64_t i) const { return b + (int32_t)i; }
   __device__ __forceinline__ int64_t dal(int w, int64_t i) const { return gld(rvp->dal + (int64_t)w * rvp->nr + b + i); }
+  __device__ __forceinline__ uint32_t dmask(int64_t i) const { return gld(rvp->dmask + b + i); }
   __device__ __forceinline__ int64_t dald(int w, int64_t i) const {
     return rld<true>(rvp->dald + (int64_t)w * rvp->nr + b + i);
   }
@@ -193,6 +196,14 @@ __device__ __forceinline__ void rsv_dev_minors(const V& v, int64_t i, uint32_t& 
   for (int j = 0; j < kRdma; ++j) rm |= v.dal(kDevRdmaW + j, i) != 0 ? (1u << j) : 0u;
 }
 
+// the device words held by any reservation of the view
+template <typename V>
+__device__ __forceinline__ uint32_t rsv_dev_words(const V& v) {
+  uint32_t m = 0u;
+  for (int64_t i = 0; i < v.n(); ++i) m |= v.dmask(i);
+  return m;
+}
+
 // The node device of one allocator call (see above).  r: the reservation allocated from (kDrsTry); gq / rq: the types
 // of requiredDeviceResources (calcRequiredDeviceResources, reservation.go:273-292) -- only those minors exist, with
 // free = r's remained (zero when `zero`: nothing remained anywhere).
@@ -205,6 +216,7 @@ struct DevRView {
   int mode;
   uint32_t gq, rq;
   bool zero;
+  uint32_t hm;  // device words any of the node's reservations holds (others need no restore)
   __device__ __forceinline__ bool present() const { return d.present(); }
   __device__ __forceinline__ int64_t ptot(int w) const { return d.tot(w); }
   // the word's required-type minor mask (0 = the type is not required)
@@ -228,6 +240,7 @@ struct DevRView {
       const int64_t f = zero ? 0 : v.dal(w, r) - v.dald(w, r), u = d.tot(w) - f;
       return u > 0 ? u : 0;
     }
+    if (!((hm >> w) & 1u)) return d.use(w);
     int64_t pre = 0;
     for (int64_t i = 0; i < v.n(); ++i) {
       const uint32_t meta = v.meta(i);
@@ -250,17 +263,18 @@ struct DevRView {
 // minors preferred; Restricted requires them, then allocates again with its remained as the free amounts.  ALLOC:
 // with Reserve's scorer and the minors.
 template <bool ALLOC, typename DV, typename V>
-__device__ __attribute__((noinline)) DevOut dev_rsv_try(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, GpuReq* req_out) {
+__device__ __forceinline__ DevOut dev_rsv_try(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, GpuReq* req_out) {
   const int32_t cls = p.rsv_class;
   uint32_t gm, rm;
   rsv_dev_minors(v, i, gm, rm);
   DevPick pk{gm, rm, 0xFFu, 0xFFu};
-  const DevRView<DV, V> tv{dv, v, cls, i, kDrsTry, 0u, 0u, false};
+  const uint32_t hm = rsv_dev_words(v);
+  const DevRView<DV, V> tv{dv, v, cls, i, kDrsTry, 0u, 0u, false, hm};
   const uint32_t pol = rsv_policy(v.meta(i));
   if (pol == KS_RSV_POLICY_DEFAULT || pol == KS_RSV_POLICY_ALIGNED) return dev_eval<ALLOC>(c, p, tv, req_out, ~0u, pk);
   if (pol != KS_RSV_POLICY_RESTRICTED) return DevOut{KS_R_DEV_INSUFFICIENT, 0, 0u, 0u};
-  pk.greq = gm;
-  pk.rreq = rm;
+  pk.greq = gm ? gm : 0xFFu;  // (a type the reservation holds none of is not required: an empty minor set)
+  pk.rreq = rm ? rm : 0xFFu;
   const DevOut d = dev_eval<false>(c, p, tv, nullptr, ~0u, pk);
   if (d.reasons) return d;
   // calcRequiredDeviceResources: the minors whose remained is not all-zero, else every minor with nothing
@@ -275,18 +289,18 @@ __device__ __attribute__((noinline)) DevOut dev_rsv_try(const Cfg& c, const PodR
   for (int j = 0; j < kRdma; ++j)
     if (((rm >> j) & 1u) && v.dal(kDevRdmaW + j, i) != v.dald(kDevRdmaW + j, i)) rq |= 1u << j;
   const bool zero = !gq && !rq;
-  const DevRView<DV, V> qv{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero};
+  const DevRView<DV, V> qv{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero, hm};
   return dev_eval<ALLOC>(c, p, qv, req_out, ~0u, pk);
 }
 
 // scoreWithReservation (reservation.go:249-271) on reservation i's view, or (i < 0) the node outside every
 // reservation's preference -- DeviceShare Score (scoring.go:30-90)
 template <typename DV, typename V>
-__device__ __attribute__((noinline)) int32_t dev_rsv_score(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, const GpuReq& g) {
+__device__ __forceinline__ int32_t dev_rsv_score(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, const GpuReq& g) {
   const int32_t cls = p.rsv_class;
-  if (i < 0) return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false}, g);
+  if (i < 0) return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false, rsv_dev_words(v)}, g);
   if (rsv_policy(v.meta(i)) != KS_RSV_POLICY_RESTRICTED)
-    return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, 0u, 0u, false}, g);
+    return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, 0u, 0u, false, rsv_dev_words(v)}, g);
   uint32_t gm, rm, gq = 0u, rq = 0u;
   rsv_dev_minors(v, i, gm, rm);
   for (int k = 0; k < kGpus; ++k)
@@ -299,7 +313,7 @@ __device__ __attribute__((noinline)) int32_t dev_rsv_score(const Cfg& c, const P
   for (int j = 0; j < kRdma; ++j)
     if (((rm >> j) & 1u) && v.dal(kDevRdmaW + j, i) != v.dald(kDevRdmaW + j, i)) rq |= 1u << j;
   const bool zero = !gq && !rq;
-  return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero}, g);
+  return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero, rsv_dev_words(v)}, g);
 }
 
 // DeviceShare Filter + Score on a node whose reservations hold devices (deviceshare/plugin.go:271-320): a matched
@@ -324,8 +338,13 @@ __device__ __forceinline__ DevOut dev_rsv_eval(const Cfg& c, const PodRec& p, co
       o.reasons = KS_R_RSV_NO_FIT;
       return o;
     }
-    o.reasons = dev_eval<false>(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false}).reasons;
+    const DevOut f = dev_eval<false>(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false, rsv_dev_words(v)});
+    o.reasons = f.reasons;
     if (o.reasons) return o;
+    if (!(nom >= 0 && rsv_dev_matched(v, nom, cls))) {
+      o.raw = f.raw;  // (the Score's view is this one: its raw is the Filter's)
+      return o;
+    }
   }
   o.raw = dev_rsv_score(c, p, dv, v, (nom >= 0 && rsv_dev_matched(v, nom, cls)) ? nom : -1, g);
   return o;
@@ -334,7 +353,7 @@ __device__ __forceinline__ DevOut dev_rsv_eval(const Cfg& c, const PodRec& p, co
 // DeviceShare's FilterReservation + ScoreReservation of reservation i (plugin.go:322-358, scoring.go:99-142): it holds
 // devices and tryAllocateFromReservation([i], required) allocates; *ds = its scoreWithReservation
 template <typename DV, typename V>
-__device__ __attribute__((noinline)) bool dev_rsv_candidate(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, int32_t* ds) {
+__device__ __forceinline__ bool dev_rsv_candidate(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, int32_t* ds) {
   *ds = 0;
   if (!dv.present() || !rsv_dev_matched(v, i, p.rsv_class)) return false;
   GpuReq g;
@@ -347,12 +366,12 @@ __device__ __attribute__((noinline)) bool dev_rsv_candidate(const Cfg& c, const 
 // Reserve (plugin.go:377-430): allocateWithNominatedReservation on the nominated reservation (view index nom), else
 // the fallback view, with the scorer; the minors in the result
 template <typename DV, typename V>
-__device__ __attribute__((noinline)) DevOut dev_rsv_reserve(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int32_t nom, GpuReq* req_out) {
+__device__ __forceinline__ DevOut dev_rsv_reserve(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int32_t nom, GpuReq* req_out) {
   if (nom >= 0 && rsv_dev_matched(v, nom, p.rsv_class)) {
     const DevOut d = dev_rsv_try<true>(c, p, dv, v, nom, req_out);
     if (d.reasons == 0) return d;
   }
-  return dev_eval<true>(c, p, DevRView<DV, V>{dv, v, p.rsv_class, -1, kDrsFallback, 0u, 0u, false}, req_out);
+  return dev_eval<true>(c, p, DevRView<DV, V>{dv, v, p.rsv_class, -1, kDrsFallback, 0u, 0u, false, rsv_dev_words(v)}, req_out);
 }
 
 // the assigned pod's allocation on reservation i's minors: allocated += (sign) the request per instance there
@@ -471,6 +490,9 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
     }
     return ok;
   };
+  // DeviceShare's verdicts of the first 8 reservations, kept for the second pass (ok bit, 8-bit score: <= 200)
+  uint32_t dok = 0u;
+  uint64_t dsv = 0ull;
   for (int64_t i = 0; i < cnt; ++i) {
     uint32_t meta;
     int32_t a;
@@ -480,7 +502,14 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
     // NominateReservation: RunReservationFilterPlugins (Reservation's FilterReservation = the body above, then
     // DeviceShare's for a pod it restores), lowest order label first (strict, table order), else the best score
     int32_t ds = 0;
-    if (dnom && !dn(v, i, &ds)) continue;
+    if (dnom) {
+      const bool pass = dn(v, i, &ds);
+      if (i < 8 && pass) {
+        dok |= 1u << i;
+        dsv |= (uint64_t)(uint32_t)ds << (8 * i);
+      }
+      if (!pass) continue;
+    }
     const int32_t oh = v.ohi(i);
     const int32_t sc = rsv_score(v, p, i);
     if (oh > best_o) {
@@ -503,7 +532,12 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
       int32_t a;
       if (!rsv_matches(v, i, cls, meta, a) || !satisfies(i)) continue;
       int32_t ds = 0;
-      if (!dn(v, i, &ds)) continue;
+      if (i < 8) {
+        if (!((dok >> i) & 1u)) continue;
+        ds = (int32_t)((dsv >> (8 * i)) & 0xFFull);
+      } else if (!dn(v, i, &ds)) {
+        continue;
+      }
       const int32_t sc = rsv_score(v, p, i);
       const int32_t t = sc + (dmax > 0 ? 100 * ds / dmax : ds);
       if (t > best_s) {
@@ -520,6 +554,54 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
   o.reasons = (aff && !any_ok) ? KS_R_RSV_NO_FIT : 0u;
   o.hi = hiord > 0 ? hiord : o.raw;
   return o;
+}
+
+// ---- the restore path's call boundary: these run out of line (one instance per view pair) with their inputs by
+// value, so the kernels keep their registers and nothing is copied to the stack per call ----
+struct DevRsvArgs {
+  int32_t dev_most, dw_core, dw_mem, dw_ratio, dw_rdma;
+  uint32_t flags;
+  int32_t rsv_class;
+  uint32_t joint;
+  int64_t gpu_core, gpu_mem, gpu_ratio, rdma;
+};
+__device__ __forceinline__ DevRsvArgs dev_rsv_args(const Cfg& c, const PodRec& p) {
+  return DevRsvArgs{c.dev_most, c.dw_core, c.dw_mem, c.dw_ratio, c.dw_rdma, p.flags, p.rsv_class, p.joint,
+                    p.gpu_core, p.gpu_mem, p.gpu_ratio, p.rdma};
+}
+__device__ __forceinline__ void dev_rsv_unpack(const DevRsvArgs& x, Cfg& c, PodRec& p) {
+  c = Cfg{};
+  c.dev = 1;
+  c.dev_most = x.dev_most;
+  c.dw_core = x.dw_core;
+  c.dw_mem = x.dw_mem;
+  c.dw_ratio = x.dw_ratio;
+  c.dw_rdma = x.dw_rdma;
+  p = PodRec{};
+  p.flags = x.flags;
+  p.rsv_class = x.rsv_class;
+  p.joint = x.joint;
+  p.gpu_core = x.gpu_core;
+  p.gpu_mem = x.gpu_mem;
+  p.gpu_ratio = x.gpu_ratio;
+  p.rdma = x.rdma;
+}
+template <typename DV, typename V>
+__device__ __attribute__((noinline)) DevOut dev_rsv_eval_x(DevRsvArgs x, DV dv, V v, int32_t nom) {
+  Cfg c;
+  PodRec p;
+  dev_rsv_unpack(x, c, p);
+  return dev_rsv_eval(c, p, dv, v, nom);
+}
+// (ok << 32) | ds
+template <typename DV, typename V>
+__device__ __attribute__((noinline)) uint64_t dev_rsv_candidate_x(DevRsvArgs x, DV dv, V v, int64_t i) {
+  Cfg c;
+  PodRec p;
+  dev_rsv_unpack(x, c, p);
+  int32_t ds = 0;
+  const bool ok = dev_rsv_candidate(c, p, dv, v, i, &ds);
+  return ((uint64_t)(ok ? 1u : 0u) << 32) | (uint32_t)ds;
 }
 
 // base row <-> the pod's restored row (sign = +1 apply, -1 undo; exact in int64)
@@ -603,7 +685,7 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
       if (c.rsv) {
         const auto dv = devv();
         if (dv.held()) {
-          dev_apply(o, rsv([&](const auto& v) { return dev_rsv_eval(c, p, dv, v, nom); }));
+          dev_apply(o, rsv([&](const auto& v) { return dev_rsv_eval_x(dev_rsv_args(c, p), dv, v, nom); }));
           return;
         }
       }
@@ -633,7 +715,10 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
       *ds = 0;
       if constexpr (DEV) {
         const auto dv = devv();
-        return dv.held() && dev_rsv_candidate(c, p, dv, v, i, ds);
+        if (!dv.held()) return false;
+        const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(c, p), dv, v, i);
+        *ds = (int32_t)(uint32_t)r;
+        return (r >> 32) != 0;
       }
       return false;
     };
