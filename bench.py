@@ -53,7 +53,7 @@ METRIC = "pods scheduled/sec + node-evals/sec (% HBM roofline) at 5k and 100k no
 def build_workload(name: str, seed: int, n_pods: int = 0):
     from koordinator_amd import synth
 
-    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c2s", "c3r", "c3f"):
+    if name not in ("c1", "c2", "c3", "c4", "c5", "c2d", "c2s", "c3r", "c3rd", "c3f"):
         raise SystemExit(f"unknown config {name}")
     if name == "c2d":
         # the complete v1beta2 default profile: c2s's plugins + PodTopologySpread (system default constraints for the
@@ -62,9 +62,9 @@ def build_workload(name: str, seed: int, n_pods: int = 0):
         w = synth.with_topology(w, seed=seed + 9)
         w.name = "C2-default"
         return w
-    # c3r: 70 % of the reservations on non-policy device nodes hold GPUs / RDMA (about a third of all of them)
-    c3r = lambda **kw: synth.c3_rsv(dev_rsv_frac=0.7, **kw)  # noqa: E731
-    fn = {"c2s": synth.c2_default, "c3r": c3r, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
+    # c3rd: c3r where 70 % of the reservations on non-policy device nodes hold GPUs / RDMA (about a third of all of them)
+    c3rd = lambda **kw: synth.c3_rsv(dev_rsv_frac=0.7, **kw)  # noqa: E731
+    fn = {"c2s": synth.c2_default, "c3r": synth.c3_rsv, "c3rd": c3rd, "c3f": synth.c3_full}.get(name) or getattr(synth, name)
     return fn(seed=seed, n_pods=n_pods) if n_pods else fn(seed=seed)
 
 
@@ -486,7 +486,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c2s", "c3r", "c3f"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "c2d", "c2s", "c3r", "c3rd", "c3f"])
     ap.add_argument("--pods", type=int, default=0, help="pods per step (default: the config's own count)")
     ap.add_argument("--batch-pods", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
@@ -502,7 +502,7 @@ def main():
     ap.add_argument("--c5-pods", type=int, default=1_000_000)
     ap.add_argument("--c5-steps", type=int, default=3)
     ap.add_argument("--c5-warmup", type=int, default=1)
-    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d / c2s / c3r sub-records")
+    ap.add_argument("--no-sub", action="store_true", help="skip the c3 / c4 / c2d / c2s / c3r / c3rd sub-records")
     ap.add_argument("--sub-steps", type=int, default=3)
     ap.add_argument("--sub-warmup", type=int, default=1)
     ap.add_argument("--no-preempt", action="store_true", help="skip the preempt (ElasticQuota PostFilter) record")
@@ -594,10 +594,10 @@ def main():
         # SURVEY's C3 (NUMA + DeviceShare) and C4 (Reservation) workloads, each timed like the headline with its own
         # CPU baseline, sample parity and commit roofline (single GPU: neither is node-sharded)
         # c3r: the shipped profile's plugin set (Reservation + NodeNUMAResource + DeviceShare) on C3's nodes with C4-style
-        # reservations (synth.c3_rsv)
+        # reservations (synth.c3_rsv); c3rd: c3r with reservations holding GPUs / RDMA (DeviceShare's restore state)
         # c2d: C2 under the complete v1beta2 default profile (c2s + PodTopologySpread + InterPodAffinity); c2s: without
         # those two (the round-4 c2d)
-        for sub in ("c3", "c4", "c2d", "c2s", "c3r"):
+        for sub in ("c3", "c4", "c2d", "c2s", "c3r", "c3rd"):
             ws = build_workload(sub, seed=20261015)
             rs, ress = run_config(ws, args, None, 1, 0, 0, False, args.sub_steps, args.sub_warmup, sub,
                                   not args.no_profile)

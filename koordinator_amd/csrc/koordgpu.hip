@@ -1093,6 +1093,7 @@ struct ks_ctx {
   std::vector<uint16_t> h_dev_ids; // per node: NUMA ids of the device topology (DeviceShare hints)
   std::vector<uint8_t> h_pol;      // per node: a NUMA topology policy (numa_flags)
   std::vector<uint8_t> h_dev_held; // per node: a reservation on it holds devices (kDevRsvHeld)
+  bool dev_held_any = false;       // ... on some node (the pass kernels' FEAT bit 16)
   int64_t* rsv_dald_ckpt = nullptr;  // checkpoint of the reservations' device allocated
   std::vector<int8_t> h_cpu_nn;    // per node: NUMA nodes of its CPU topology (0 = none, -1 = ids not 0..n-1)
   std::vector<CpuTopo> h_topos;    // the loaded CPU topologies (ks_update_cpu_state refers to them)
@@ -1918,8 +1919,10 @@ __global__ void dev_held_kernel(uint32_t* flags, const uint8_t* held, int64_t n)
 }
 
 static int dev_apply_held(ks_ctx* ctx) {
+  ctx->dev_held_any = false;
   if (!ctx->dev_blob || ctx->n == 0) return KS_OK;
   if (ctx->h_dev_held.size() != (size_t)ctx->n) ctx->h_dev_held.assign((size_t)ctx->n, 0);
+  for (uint8_t h : ctx->h_dev_held) ctx->dev_held_any = ctx->dev_held_any || h != 0;
   void* p = nullptr;
   if (dev_alloc(ctx, &p, (size_t)ctx->n) != KS_OK) return KS_ENOMEM;
   HIPCHK(ctx, hipMemcpyAsync(p, ctx->h_dev_held.data(), (size_t)ctx->n, hipMemcpyHostToDevice, ctx->stream));
@@ -3499,18 +3502,20 @@ static bool commit_qcache(const ks_ctx* ctx) {
 }
 
 // Kernel variant (FEAT bits, ks_pass.h): 1 Reservation, 2 NodeNUMAResource, 4 the normalized plugins (DeviceShare,
-// TaintToleration / NodeAffinity / NodePorts), 8 NUMA topology policies (with 2).  A context runs the smallest built
+// TaintToleration / NodeAffinity / NodePorts), 8 NUMA topology policies (with 2), 16 reservations holding devices (with
+// 1 and 4: DeviceShare's restore state, ks_rsv.h; without it the restore code costs the 7 / 15 kernels ~30 % at c3r,
+// though no node runs it).  A context runs the smallest built
 // variant whose bits cover the plugins it enables: a bit that is compiled in but unused still costs registers -- the
 // variants with Reservation and the normalized plugins together spill 180-320 B/lane in the commit kernel, those
 // without Reservation (4, 6, 14) none (hipcc -Rpass-analysis=kernel-resource-usage).
-constexpr int kBuiltFeats[] = {0, 1, 3, 4, 6, 7, 11, 14, 15};  // ascending (koordinator_amd/csrc/Makefile FEATS)
+constexpr int kBuiltFeats[] = {0, 1, 3, 4, 6, 7, 11, 14, 15, 23, 31};  // ascending (koordinator_amd/csrc/Makefile FEATS)
 
 static int kernel_feat(const ks_ctx* ctx) {
   const int need = (ctx->kc.rsv ? 1 : 0) | (ctx->kc.numa ? 2 : 0) | ((ctx->kc.dev || ctx->kc.stat) ? 4 : 0) |
-                   (ctx->kc.numa_pol ? 10 : 0);
+                   (ctx->kc.numa_pol ? 10 : 0) | ((ctx->kc.rsv && ctx->kc.dev && ctx->dev_held_any) ? 21 : 0);
   for (int f : kBuiltFeats)
     if ((f & need) == need) return f;
-  return 15;
+  return 31;
 }
 
 // the slot device region of the commit kernel: GPU state (DeviceShare), then the TaintToleration / NodeAffinity words
@@ -3559,6 +3564,8 @@ static int32_t commit_rcap(const ks_ctx* ctx, bool* qcache) {
 static PassLaunch pass_launcher(int feat, int nsc) {
 #define KS_PICK(F) return nsc == 0 ? pass_launch_f##F##_n0() : (nsc == 2 ? pass_launch_f##F##_n2() : pass_launch_f##F##_n4())
   switch (feat) {
+    case 31: KS_PICK(31);
+    case 23: KS_PICK(23);
     case 15: KS_PICK(15);
     case 14: KS_PICK(14);
     case 11: KS_PICK(11);

@@ -84,7 +84,7 @@ static void launch_nsc(int feat, int blocks, hipStream_t s, DevNodes d, const De
   else if (feat == 4)
     hipLaunchKernelGGL((eval_debug_kernel<NSC, 4>), dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
   else
-    hipLaunchKernelGGL((eval_debug_kernel<NSC, 15>), dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
+    hipLaunchKernelGGL((eval_debug_kernel<NSC, 31>), dim3(blocks), dim3(256), 0, s, d, rv, dv, nv, c, pod, n, reasons, scores, total, raw, hiord, draw, pstat, traw, araw, t, on);
 }
 
 hipError_t launch_eval_debug(int nsc, int blocks, hipStream_t s, DevNodes d, const DevRsv* rv, const DevDev* dv,

@@ -1637,7 +1637,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       // DeviceShare's FilterReservation / ScoreReservation in the nomination (reservations holding devices)
       auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
         *ds = 0;
-        if constexpr (DEV) {
+        if constexpr (DEV && (FEAT & 16) != 0) {
           if (!sdv.held()) return false;
           const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(cfg, pod), sdv, v, i);
           *ds = (int32_t)(uint32_t)r;
@@ -1664,7 +1664,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[4 * s], sstat[4 * s + 1], sstat[4 * s + 2], sstat[4 * s + 3], e2);
         fitla_pref = e2.total + norm_terms(cfg, e2, Muse);
       }
-      if (DEV && want_dev0 && sdv.held()) {
+      if ((FEAT & 16) && DEV && want_dev0 && sdv.held()) {
         // DeviceShare Reserve on the cycle's restore state, before the Reservation plugin's own Reserve changes it
         // (the ordered node's full evaluation above ran on the same state)
         const DevOut rd = mode >= 0 ? dev_rsv_reserve(cfg, pod, sdv, lv, nom, &g_rsv)
@@ -1744,7 +1744,7 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
     const bool want_dev = DEV && cfg.dev && (pflags & kPodHasGpu);
     // a slot created by this pod holds the snapshot state: reserve_pre_kernel's allocation for the node, if it ranked
     const PreRsv* pre = nullptr;
-    const bool held_here = DEV && cfg.dev && RSV && cfg.rsv && ((uint32_t)sdev_pres[s] & kDevRsvHeld);
+    const bool held_here = (FEAT & 16) && DEV && cfg.dev && RSV && cfg.rsv && ((uint32_t)sdev_pres[s] & kDevRsvHeld);
     if ((FEAT & 8) && a.pre_rsv && fresh && (want_npol || want_dev) && !held_here) {
       const uint64_t hit = __ballot(pre_nodes == node);  // (read by the look-ahead)
       if (hit) pre = a.pre_rsv + j * kPreRsvM + (__ffsll((long long)hit) - 1);
@@ -2150,6 +2150,8 @@ KS_DECLARE_VARIANT(7)
 KS_DECLARE_VARIANT(11)
 KS_DECLARE_VARIANT(14)
 KS_DECLARE_VARIANT(15)
+KS_DECLARE_VARIANT(23)
+KS_DECLARE_VARIANT(31)
 #undef KS_DECLARE_VARIANT
 
 }  // namespace ks

@@ -89,6 +89,8 @@ struct RsvOut {
   int32_t raw;       // scoreReservation of the nominated reservation (0 = none)
   int32_t hiord;     // kRsvOrderBase+... of the node's best order label over matched (0 = none)
   int32_t nom;       // nominated reservation, CSR position (-1 = none)
+  int32_t dds;       // 1 + DeviceShare's ScoreReservation of the nominated reservation when its FilterReservation
+                     // nominated it (a reservation holding devices the pod allocates from), else 0
 };
 
 // ---- views of one node's reservations ----
@@ -196,12 +198,33 @@ __device__ __forceinline__ void rsv_dev_minors(const V& v, int64_t i, uint32_t& 
   for (int j = 0; j < kRdma; ++j) rm |= v.dal(kDevRdmaW + j, i) != 0 ? (1u << j) : 0u;
 }
 
-// the device words held by any reservation of the view
+// The node's reservations as one pod's restore sees them, classified once per call: mm = the matched ones holding
+// devices (rsv_dev_matched), um = the unmatched ones holding devices with assigned pods, hm = the device words any
+// reservation holds (other words need no restore).  View positions >= 64 are classified on the spot (drs_matched).
+struct DrsSet {
+  uint64_t mm, um;
+  uint32_t hm;
+};
 template <typename V>
-__device__ __forceinline__ uint32_t rsv_dev_words(const V& v) {
-  uint32_t m = 0u;
-  for (int64_t i = 0; i < v.n(); ++i) m |= v.dmask(i);
-  return m;
+__device__ __forceinline__ DrsSet drs_set(const V& v, int32_t cls) {
+  DrsSet s{0ull, 0ull, 0u};
+  const int64_t n = v.n();
+  for (int64_t i = 0; i < n; ++i) {
+    s.hm |= v.dmask(i);
+    if (i >= 64) continue;
+    const uint32_t meta = v.meta(i);
+    if (!(meta & kRsvMetaDev)) continue;
+    const int32_t a = v.assigned(i);
+    if ((meta & KS_RSV_ALLOCATE_ONCE) && a > 0) continue;  // (not restored at all)
+    const bool matched = !(meta & KS_RSV_UNSCHEDULABLE) && cls >= 0 && cls < 64 && ((v.cls(i) >> cls) & 1ull);
+    s.mm |= matched ? (1ull << i) : 0ull;
+    s.um |= (!matched && a > 0) ? (1ull << i) : 0ull;
+  }
+  return s;
+}
+template <typename V>
+__device__ __forceinline__ bool drs_matched(const DrsSet& s, const V& v, int64_t i, int32_t cls) {
+  return i < 64 ? ((s.mm >> i) & 1ull) != 0 : rsv_dev_matched(v, i, cls);
 }
 
 // The node device of one allocator call (see above).  r: the reservation allocated from (kDrsTry); gq / rq: the types
@@ -216,7 +239,7 @@ struct DevRView {
   int mode;
   uint32_t gq, rq;
   bool zero;
-  uint32_t hm;  // device words any of the node's reservations holds (others need no restore)
+  const DrsSet& s;
   __device__ __forceinline__ bool present() const { return d.present(); }
   __device__ __forceinline__ int64_t ptot(int w) const { return d.tot(w); }
   // the word's required-type minor mask (0 = the type is not required)
@@ -240,9 +263,20 @@ struct DevRView {
       const int64_t f = zero ? 0 : v.dal(w, r) - v.dald(w, r), u = d.tot(w) - f;
       return u > 0 ? u : 0;
     }
-    if (!((hm >> w) & 1u)) return d.use(w);
+    if (!((s.hm >> w) & 1u)) return d.use(w);
+    // preemptible: the matched ones' allocatable (fallback) or allocated plus r's remained (kDrsTry), the unmatched
+    // ones' allocated (their assigned pods' part of the reserve pod's use)
     int64_t pre = 0;
-    for (int64_t i = 0; i < v.n(); ++i) {
+    for (uint64_t m = s.mm; m; m &= m - 1ull) {
+      const int i = __builtin_ctzll(m);
+      pre += mode == kDrsFallback ? v.dal(w, i) : v.dald(w, i);
+    }
+    if (mode == kDrsTry && r < 64) pre += v.dal(w, r) - v.dald(w, r);
+    for (uint64_t m = s.um; m; m &= m - 1ull) {
+      const int64_t x = v.dald(w, __builtin_ctzll(m));
+      pre += x > 0 ? x : 0;
+    }
+    for (int64_t i = 64; i < v.n(); ++i) {
       const uint32_t meta = v.meta(i);
       const int32_t a = v.assigned(i);
       if (!(meta & kRsvMetaDev) || ((meta & KS_RSV_ALLOCATE_ONCE) && a > 0)) continue;
@@ -263,13 +297,13 @@ struct DevRView {
 // minors preferred; Restricted requires them, then allocates again with its remained as the free amounts.  ALLOC:
 // with Reserve's scorer and the minors.
 template <bool ALLOC, typename DV, typename V>
-__device__ __forceinline__ DevOut dev_rsv_try(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, GpuReq* req_out) {
+__device__ __forceinline__ DevOut dev_rsv_try(const Cfg& c, const PodRec& p, const DV& dv, const V& v, const DrsSet& s,
+                                              int64_t i, GpuReq* req_out) {
   const int32_t cls = p.rsv_class;
   uint32_t gm, rm;
   rsv_dev_minors(v, i, gm, rm);
   DevPick pk{gm, rm, 0xFFu, 0xFFu};
-  const uint32_t hm = rsv_dev_words(v);
-  const DevRView<DV, V> tv{dv, v, cls, i, kDrsTry, 0u, 0u, false, hm};
+  const DevRView<DV, V> tv{dv, v, cls, i, kDrsTry, 0u, 0u, false, s};
   const uint32_t pol = rsv_policy(v.meta(i));
   if (pol == KS_RSV_POLICY_DEFAULT || pol == KS_RSV_POLICY_ALIGNED) return dev_eval<ALLOC>(c, p, tv, req_out, ~0u, pk);
   if (pol != KS_RSV_POLICY_RESTRICTED) return DevOut{KS_R_DEV_INSUFFICIENT, 0, 0u, 0u};
@@ -289,18 +323,19 @@ __device__ __forceinline__ DevOut dev_rsv_try(const Cfg& c, const PodRec& p, con
   for (int j = 0; j < kRdma; ++j)
     if (((rm >> j) & 1u) && v.dal(kDevRdmaW + j, i) != v.dald(kDevRdmaW + j, i)) rq |= 1u << j;
   const bool zero = !gq && !rq;
-  const DevRView<DV, V> qv{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero, hm};
+  const DevRView<DV, V> qv{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero, s};
   return dev_eval<ALLOC>(c, p, qv, req_out, ~0u, pk);
 }
 
 // scoreWithReservation (reservation.go:249-271) on reservation i's view, or (i < 0) the node outside every
 // reservation's preference -- DeviceShare Score (scoring.go:30-90)
 template <typename DV, typename V>
-__device__ __forceinline__ int32_t dev_rsv_score(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, const GpuReq& g) {
+__device__ __forceinline__ int32_t dev_rsv_score(const Cfg& c, const PodRec& p, const DV& dv, const V& v, const DrsSet& s,
+                                                int64_t i, const GpuReq& g) {
   const int32_t cls = p.rsv_class;
-  if (i < 0) return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false, rsv_dev_words(v)}, g);
+  if (i < 0) return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false, s}, g);
   if (rsv_policy(v.meta(i)) != KS_RSV_POLICY_RESTRICTED)
-    return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, 0u, 0u, false, rsv_dev_words(v)}, g);
+    return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, 0u, 0u, false, s}, g);
   uint32_t gm, rm, gq = 0u, rq = 0u;
   rsv_dev_minors(v, i, gm, rm);
   for (int k = 0; k < kGpus; ++k)
@@ -313,7 +348,7 @@ __device__ __forceinline__ int32_t dev_rsv_score(const Cfg& c, const PodRec& p, 
   for (int j = 0; j < kRdma; ++j)
     if (((rm >> j) & 1u) && v.dal(kDevRdmaW + j, i) != v.dald(kDevRdmaW + j, i)) rq |= 1u << j;
   const bool zero = !gq && !rq;
-  return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero, rsv_dev_words(v)}, g);
+  return dev_raw(c, p, DevRView<DV, V>{dv, v, cls, i, kDrsTry, zero ? gm : gq, zero ? rm : rq, zero, s}, g);
 }
 
 // DeviceShare Filter + Score on a node whose reservations hold devices (deviceshare/plugin.go:271-320): a matched
@@ -327,26 +362,27 @@ __device__ __forceinline__ DevOut dev_rsv_eval(const Cfg& c, const PodRec& p, co
   o.reasons = dev_prepare(p, dv, g);
   if (o.reasons) return o;
   const int32_t cls = p.rsv_class;
+  const DrsSet s = drs_set(v, cls);
   bool ok = false, any = false;
   for (int64_t i = 0; i < v.n() && !ok; ++i) {
-    if (!rsv_dev_matched(v, i, cls)) continue;
+    if (!drs_matched(s, v, i, cls)) continue;
     any = true;
-    ok = dev_rsv_try<false>(c, p, dv, v, i, nullptr).reasons == 0;
+    ok = dev_rsv_try<false>(c, p, dv, v, s, i, nullptr).reasons == 0;
   }
   if (!ok) {
     if (any && (p.flags & KS_POD_RSV_AFFINITY)) {
       o.reasons = KS_R_RSV_NO_FIT;
       return o;
     }
-    const DevOut f = dev_eval<false>(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false, rsv_dev_words(v)});
+    const DevOut f = dev_eval<false>(c, p, DevRView<DV, V>{dv, v, cls, -1, kDrsFallback, 0u, 0u, false, s});
     o.reasons = f.reasons;
     if (o.reasons) return o;
-    if (!(nom >= 0 && rsv_dev_matched(v, nom, cls))) {
+    if (!(nom >= 0 && drs_matched(s, v, nom, cls))) {
       o.raw = f.raw;  // (the Score's view is this one: its raw is the Filter's)
       return o;
     }
   }
-  o.raw = dev_rsv_score(c, p, dv, v, (nom >= 0 && rsv_dev_matched(v, nom, cls)) ? nom : -1, g);
+  o.raw = dev_rsv_score(c, p, dv, v, s, (nom >= 0 && drs_matched(s, v, nom, cls)) ? nom : -1, g);
   return o;
 }
 
@@ -358,8 +394,9 @@ __device__ __forceinline__ bool dev_rsv_candidate(const Cfg& c, const PodRec& p,
   if (!dv.present() || !rsv_dev_matched(v, i, p.rsv_class)) return false;
   GpuReq g;
   if (dev_prepare(p, dv, g)) return false;
-  if (dev_rsv_try<false>(c, p, dv, v, i, nullptr).reasons) return false;
-  *ds = dev_rsv_score(c, p, dv, v, i, g);
+  const DrsSet s = drs_set(v, p.rsv_class);
+  if (dev_rsv_try<false>(c, p, dv, v, s, i, nullptr).reasons) return false;
+  *ds = dev_rsv_score(c, p, dv, v, s, i, g);
   return true;
 }
 
@@ -367,11 +404,12 @@ __device__ __forceinline__ bool dev_rsv_candidate(const Cfg& c, const PodRec& p,
 // the fallback view, with the scorer; the minors in the result
 template <typename DV, typename V>
 __device__ __forceinline__ DevOut dev_rsv_reserve(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int32_t nom, GpuReq* req_out) {
-  if (nom >= 0 && rsv_dev_matched(v, nom, p.rsv_class)) {
-    const DevOut d = dev_rsv_try<true>(c, p, dv, v, nom, req_out);
+  const DrsSet s = drs_set(v, p.rsv_class);
+  if (nom >= 0 && drs_matched(s, v, nom, p.rsv_class)) {
+    const DevOut d = dev_rsv_try<true>(c, p, dv, v, s, nom, req_out);
     if (d.reasons == 0) return d;
   }
-  return dev_eval<true>(c, p, DevRView<DV, V>{dv, v, p.rsv_class, -1, kDrsFallback, 0u, 0u, false, rsv_dev_words(v)}, req_out);
+  return dev_eval<true>(c, p, DevRView<DV, V>{dv, v, p.rsv_class, -1, kDrsFallback, 0u, 0u, false, s}, req_out);
 }
 
 // the assigned pod's allocation on reservation i's minors: allocated += (sign) the request per instance there
@@ -460,7 +498,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
 #pragma unroll
   for (int k = 0; k < NSC; ++k) slack[3 + k] = r.free_sc[k] - dpre[3 + k] + ral[3 + k];
   const bool dnom = (p.flags & kPodDevNoNom) != 0;
-  int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0, dmax = 0;
+  int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0, dmax = 0, ds_o = 0, ds_s = 0;
   bool any_ok = false;
   // filterWithReservations body for one reservation (plugin.go:386-422)
   auto satisfies = [&](int64_t i) {
@@ -516,6 +554,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
       best_o = oh;
       nom_o = (int32_t)i;
       raw_o = sc;
+      ds_o = ds;
     }
     dmax = max(dmax, ds);
     if (!dnom && sc > best_s) {
@@ -544,11 +583,13 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
         best_s = t;
         nom_s = (int32_t)i;
         raw_s = sc;
+        ds_s = ds;
       }
     }
   }
   o.nom = nom_o >= 0 ? nom_o : nom_s;
   o.raw = nom_o >= 0 ? raw_o : (nom_s >= 0 ? raw_s : 0);
+  o.dds = (dnom && o.nom >= 0) ? 1 + (nom_o >= 0 ? ds_o : ds_s) : 0;
   // the Reservation Filter passes on any satisfying reservation (DeviceShare's FilterReservation runs in the
   // nomination only)
   o.reasons = (aff && !any_ok) ? KS_R_RSV_NO_FIT : 0u;
@@ -640,6 +681,7 @@ template <int NSC, bool DEBUG, bool UNDO, int FEAT, typename F, typename G, type
 __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, NodeReg<NSC>& r, F&& rsv, G&& devv,
                                              H&& numav, RsvOut* info = nullptr, DHF dhf = DHF{}, DFF dff = DFF{}) {
   constexpr bool RSV = (FEAT & 1) != 0, NUMA = (FEAT & 2) != 0, DEV = (FEAT & 4) != 0, POL = (FEAT & 8) != 0;
+  constexpr bool HELD = RSV && DEV && (FEAT & 16) != 0;  // reservations holding devices (DeviceShare's restore state)
   const bool dev_pod = DEV && c.dev && (p.flags & kPodHasGpu);
   // NodeNUMAResource (policy None part, then the topology-manager path on a policy node); returns DeviceShare's
   // NUMA restriction
@@ -677,15 +719,18 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
       o.numa = 0;
     }
   };
-  auto dev = [&](EvalOut& o, uint32_t allow, int32_t nom) __attribute__((always_inline)) {
+  auto dev = [&](EvalOut& o, uint32_t allow, int32_t nom, int32_t dds) __attribute__((always_inline)) {
     if (!dev_pod) return;
     if (!DEBUG && o.reasons) return;
-    if constexpr (RSV) {
+    if constexpr (HELD) {
       // reservations holding devices on the node (never one with a NUMA policy): the restore state's views
       if (c.rsv) {
         const auto dv = devv();
         if (dv.held()) {
-          dev_apply(o, rsv([&](const auto& v) { return dev_rsv_eval_x(dev_rsv_args(c, p), dv, v, nom); }));
+          // a reservation DeviceShare's FilterReservation nominated: the pod allocates from it (Filter passes) and
+          // the Score is its ScoreReservation's view, both computed in the nomination
+          if (dds > 0) dev_apply(o, DevOut{0u, dds - 1, 0u, 0u});
+          else dev_apply(o, rsv([&](const auto& v) { return dev_rsv_eval_x(dev_rsv_args(c, p), dv, v, nom); }));
           return;
         }
       }
@@ -703,7 +748,7 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
     if (info) *info = RsvOut{0u, 0, 0, 0, -1};
     EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
     const uint32_t allow = numa(o);
-    dev(o, allow, -1);
+    dev(o, allow, -1, 0);
     return o;
   }
   const bool slow = p.rsv_class >= 0 && p.rsv_class < 64 && ((r.rsv_cls >> p.rsv_class) & 1ull);
@@ -713,7 +758,7 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
     // DeviceShare's FilterReservation / ScoreReservation in the nomination (a pod it restores)
     auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
       *ds = 0;
-      if constexpr (DEV) {
+      if constexpr (HELD) {
         const auto dv = devv();
         if (!dv.held()) return false;
         const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(c, p), dv, v, i);
@@ -728,7 +773,7 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
   EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);
   const uint32_t allow = numa(o);
   if (UNDO && slow) rsv_apply<NSC>(r, dl, -1);
-  dev(o, allow, ro.nom);
+  dev(o, allow, ro.nom, ro.dds);
   // a node without matched reservations is cut by the Reservation PreFilter (PreFilterResult
   // NodeNames, plugin.go:235-246) before any Filter plugin runs
   o.reasons = ro.reasons == KS_R_RSV_AFFINITY ? ro.reasons : (o.reasons | ro.reasons);

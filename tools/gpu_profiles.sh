@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile evidence of the bench line's records, all from the library in this tree (each summary is stamped with its
-# sha256, which bench.py checks): per config (c2, c3, c4, c2d, c2s, c3r) the rocprofv3 kernel statistics of the bench command and
+# sha256, which bench.py checks): per config (c2, c3, c4, c2d, c2s, c3r, c3rd) the rocprofv3 kernel statistics of the bench command and
 # the PMC HBM traffic (FETCH_SIZE / WRITE_SIZE passes) and VALU-issue summaries; for c5 the PMC passes on a 200k-pod
 # queue (sweep measured unpipelined, KS_PIPE=0: the same kernel without the list re-evaluation launches) and last the
 # pipelined kernel trace with its overlap summary (tools/trace_overlap.py).
@@ -11,8 +11,11 @@ set -o pipefail
 OUT=gpurun_out/${1:-prof}
 mkdir -p $OUT
 export TMPDIR=/tmp
-for CFG in ${CONFIGS:-c2 c3 c4 c2d c2s c3r}; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$CFG -o run -- python3 bench.py --config $CFG --no-c5 --no-sub --no-cpu-baseline > $OUT/prof_$CFG.json 2> $OUT/prof_$CFG.err || { echo "rocprof $CFG failed"; tail -30 $OUT/prof_$CFG.err; exit 1; }
+for CFG in ${CONFIGS:-c2 c3 c4 c2d c2s c3r c3rd}; do
+  # (c2d: the topology loop without its HIP graph -- rocprofv3's CSV kernel trace of the captured loop died in the
+  # HIP runtime in round 5)
+  G=1; [ "$CFG" = c2d ] && G=0
+  KS_TOPO_GRAPH=$G timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$CFG -o run -- python3 bench.py --config $CFG --no-c5 --no-sub --no-cpu-baseline > $OUT/prof_$CFG.json 2> $OUT/prof_$CFG.err || { echo "rocprof $CFG failed"; tail -30 $OUT/prof_$CFG.err; exit 1; }
   S=$(find $OUT/prof_$CFG -name '*kernel_stats.csv' | head -1)
   [ -n "$S" ] && cp $S $OUT/${CFG}_kernel_stats.csv
   rm -rf $OUT/prof_$CFG
