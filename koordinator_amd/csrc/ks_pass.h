@@ -1646,19 +1646,24 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
         return false;
       };
       RsvOut ro;
-      if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl, dnom);
-      else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl, dnom);
+      if constexpr ((FEAT & 16) != 0) {
+        if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl, dnom);
+        else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl, dnom);
+      } else {
+        if (mode >= 0) ro = rsv_eval<NSC>(lv, pod, nr, dl);
+        else ro = rsv_eval<NSC>(RsvG<true>(*a.rv, node), pod, nr, dl);
+      }
       const int32_t nom = __builtin_amdgcn_readfirstlane(ro.nom);  // view index
       if (ro.hi >= kRsvOrderBase) {
         // the whole Filter / Score of the slot with this restore (eval_full: on a node with a NUMA topology policy the
         // score over the allocated NUMA nodes and DeviceShare under the admitted affinity, not the policy-None parts)
         NodeReg<NSC> n2 = nr;
+        auto rv2 = [&](auto&& f) {
+          if (mode >= 0) return f(lv);
+          return f(RsvG<true>(*a.rv, node));
+        };
         EvalOut e2 = eval_full<NSC, false, false, FEAT>(
-            cfg, pod, n2,
-            [&](auto&& f) {
-              if (mode >= 0) return f(lv);
-              return f(RsvG<true>(*a.rv, node));
-            },
+            cfg, pod, n2, RsvWithOut<NSC, decltype(rv2)>{rv2, ro, dl},
             [&]() { return DevLView{sdev_tot + s, sdev_use + s, (uint32_t)sdev_pres[s]}; },
             [&]() { return NumaLView{snp + s * kNumaSlotWords}; });
         if (DEV && cfg.stat) stat_eval(cfg, pst, sstat[4 * s], sstat[4 * s + 1], sstat[4 * s + 2], sstat[4 * s + 3], e2);

@@ -25,6 +25,8 @@
 // is the preferred node) and (Fit+LA) otherwise.
 #pragma once
 
+#include <type_traits>
+
 #include "ks_device.h"
 #include "ks_numa.h"
 
@@ -497,6 +499,8 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
   slack[2] = r.free_eph - dpre[2] + ral[2];
 #pragma unroll
   for (int k = 0; k < NSC; ++k) slack[3 + k] = r.free_sc[k] - dpre[3 + k] + ral[3 + k];
+  // DeviceShare's FilterReservation for a pod it restores: dn, or (NoDevNom) none of them passes
+  constexpr bool DSN = !std::is_same<DN, NoDevNom>::value;
   const bool dnom = (p.flags & kPodDevNoNom) != 0;
   int32_t best_o = 0, best_s = -1, nom_o = -1, nom_s = -1, raw_o = 0, dmax = 0, ds_o = 0, ds_s = 0;
   bool any_ok = false;
@@ -541,6 +545,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
     // DeviceShare's for a pod it restores), lowest order label first (strict, table order), else the best score
     int32_t ds = 0;
     if (dnom) {
+      if constexpr (!DSN) continue;
       const bool pass = dn(v, i, &ds);
       if (i < 8 && pass) {
         dok |= 1u << i;
@@ -563,7 +568,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
     }
   }
   int32_t raw_s = best_s;
-  if (dnom && nom_o < 0) {
+  if (DSN && dnom && nom_o < 0) {
     // prioritizeReservations (nominator.go:218-262): Reservation's ScoreReservation (no normalization) + DeviceShare's
     // after DefaultReservationNormalizeScore(100); the highest sum, ties in table order
     for (int64_t i = 0; i < cnt; ++i) {
@@ -589,7 +594,7 @@ __device__ __forceinline__ RsvOut rsv_eval(const V& v, const PodRec& p, const No
   }
   o.nom = nom_o >= 0 ? nom_o : nom_s;
   o.raw = nom_o >= 0 ? raw_o : (nom_s >= 0 ? raw_s : 0);
-  o.dds = (dnom && o.nom >= 0) ? 1 + (nom_o >= 0 ? ds_o : ds_s) : 0;
+  o.dds = (DSN && dnom && o.nom >= 0) ? 1 + (nom_o >= 0 ? ds_o : ds_s) : 0;
   // the Reservation Filter passes on any satisfying reservation (DeviceShare's FilterReservation runs in the
   // nomination only)
   o.reasons = (aff && !any_ok) ? KS_R_RSV_NO_FIT : 0u;
@@ -644,6 +649,22 @@ __device__ __attribute__((noinline)) uint64_t dev_rsv_candidate_x(DevRsvArgs x, 
   const bool ok = dev_rsv_candidate(c, p, dv, v, i, &ds);
   return ((uint64_t)(ok ? 1u : 0u) << 32) | (uint32_t)ds;
 }
+
+// A reservation visitor with the pod's rsv_eval on it already computed (the commit's nomination, reused by eval_full)
+template <int NSC, typename F>
+struct RsvWithOut {
+  F f;
+  RsvOut ro;
+  RsvDelta<NSC> dl;
+  template <typename G>
+  __device__ __forceinline__ auto operator()(G&& g) const {
+    return f(g);
+  }
+};
+template <typename T>
+struct RsvKnown : std::false_type {};
+template <int NSC, typename F>
+struct RsvKnown<RsvWithOut<NSC, F>> : std::true_type {};
 
 // base row <-> the pod's restored row (sign = +1 apply, -1 undo; exact in int64)
 template <int NSC>
@@ -767,7 +788,14 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
       }
       return false;
     };
-    ro = rsv([&](const auto& v) { return rsv_eval<NSC>(v, p, r, dl, dnom); });
+    if constexpr (RsvKnown<std::decay_t<F>>::value) {
+      ro = rsv.ro;  // (the caller's nomination on the same row)
+      dl = rsv.dl;
+    } else if constexpr (HELD) {
+      ro = rsv([&](const auto& v) { return rsv_eval<NSC>(v, p, r, dl, dnom); });
+    } else {
+      ro = rsv([&](const auto& v) { return rsv_eval<NSC>(v, p, r, dl); });
+    }
     rsv_apply<NSC>(r, dl, 1);
   }
   EvalOut o = eval_pod_node<NSC, DEBUG>(c, p, r);

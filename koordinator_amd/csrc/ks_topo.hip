@@ -362,7 +362,12 @@ __global__ __launch_bounds__(kTopoThreads) void topo_norm_kernel(TopoKArgs a, To
   // the last workgroup: the commit or the one-candidate set, then the scratch back to its initial image.  The only
   // value handed between workgroups is `best`, an agent-scope atomic performed at the memory side: each wave waits
   // for its own atomic to complete before the workgroup's arrival (no L2 write-back fence: the scores and totals are
-  // read only after the kernel), and the last workgroup reads it with an agent-scope load.
+  // read only after the kernel), and the last workgroup reads it with an agent-scope load.  This relies on gfx9's
+  // counters: vmcnt also covers the non-returning atomicMax (gfx10+ split the store counter off), so other targets
+  // must not build it (the error below) and need a release / acquire pair on `done` instead.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "topo_norm_kernel's fence-free hand-over is written for gfx950's vmcnt semantics"
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) last = __hip_atomic_fetch_add(&s->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;

@@ -109,6 +109,18 @@ def test_shipped_profile_device_reservations(runtime, oracle_lib, seed):
     assert c["dev_into_rsv"] > 50 and held[into[into >= 0]].sum() > 50, c
 
 
+def test_shipped_profile_device_reservations_full_size(runtime, oracle_lib):
+    """the bench's c3rd record itself (bench.py build_workload, sub-record seed): 10k pods x 5k nodes, about a third of
+    the reservations holding GPUs / RDMA, every result and the final reservation / device / CPU state vs the oracle"""
+    w = synth.c3_rsv(seed=20261015, dev_rsv_frac=0.7)
+    assert w.nodes.n == 5000 and w.pods.n == 10_000
+    held = (w.reservations.dev_allocatable != 0).any(axis=1)
+    assert held.mean() > 0.3
+    got = check(runtime, oracle_lib, w, "c3rd")
+    into = got["reservation"]
+    assert held[into[into >= 0]].sum() > 200
+
+
 def test_shipped_profile_device_reservations_eval_pod(runtime, oracle_lib):
     w = synth.c3_rsv(seed=89, n_nodes=300, n_pods=300, policy_frac=0.3, dev_rsv_frac=0.7)
     ev = runtime.Evaluator(w.cfg, w.nodes.copy(), **w.tables())
