@@ -19,9 +19,11 @@ for CFG in ${CONFIGS:-c2 c3 c4 c2d c2s c3r c3rd}; do
   S=$(find $OUT/prof_$CFG -name '*kernel_stats.csv' | head -1)
   [ -n "$S" ] && cp $S $OUT/${CFG}_kernel_stats.csv
   rm -rf $OUT/prof_$CFG
-  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_traffic.sh $CFG ${OUT#gpurun_out/}/traffic_$CFG > /dev/null || exit 1
+  # (c2d's PMC passes on 1,000 pods: --pmc serializes each of the ~4 dispatches per topology pod)
+  PARGS="--no-c5 --no-sub"; [ "$CFG" = c2d ] && PARGS="$PARGS --pods 1000"
+  BENCH_ARGS="$PARGS" bash tools/pmc_traffic.sh $CFG ${OUT#gpurun_out/}/traffic_$CFG > /dev/null || exit 1
   cp $OUT/traffic_$CFG/traffic.json $OUT/${CFG}_traffic.json
-  BENCH_ARGS="--no-c5 --no-sub" bash tools/pmc_valu.sh $CFG ${OUT#gpurun_out/}/valu_$CFG > /dev/null || exit 1
+  BENCH_ARGS="$PARGS" bash tools/pmc_valu.sh $CFG ${OUT#gpurun_out/}/valu_$CFG > /dev/null || exit 1
   cp $OUT/valu_$CFG/valu.json $OUT/${CFG}_valu.json
   rm -rf $OUT/traffic_$CFG $OUT/valu_$CFG
   echo "profiles $CFG done"
