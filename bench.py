@@ -15,8 +15,9 @@ At N=1 it also carries ``c3`` (configs[2]: NUMA + DeviceShare joint allocation, 
 20k nodes with 50k Reservations), ``c2d`` (C2 under the complete v1beta2 default profile's upstream plugins as well:
 NodeResourcesBalancedAllocation, TaintToleration, NodeAffinity, NodePorts, PodTopologySpread with the system default
 constraints, InterPodAffinity), ``c2s`` (c2d without the last two: the round-4 c2d) and ``c3r`` (the shipped profile's
-Reservation + NodeNUMAResource + DeviceShare together: C3's nodes with 12.5k reservations), each with its own CPU
-baseline, sample parity and roofline.
+Reservation + NodeNUMAResource + DeviceShare together: C3's nodes with 12.5k reservations) and ``c3rd`` (c3r where
+31.6 % of the reservations hold GPUs / RDMA: DeviceShare's reservation restore state), each with its own CPU baseline,
+sample parity and roofline.
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): one process per GPU.  ``value`` at N>1 is C2 node-sharded
 over the N ranks (strong scaling: one cluster, one queue, every rank sweeps its node range and the per-shard
