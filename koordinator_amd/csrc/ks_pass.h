@@ -1634,12 +1634,19 @@ __global__ __launch_bounds__(commit_threads(FEAT)) void commit_kernel(CommitArgs
       const int32_t mode = srcnt[s];
       const RsvL<RD> lv{srec + s * a.rcap, mode, srbeg[s], a.rv};
       const DevLView sdv{sdev_tot + s, sdev_use + s, DEV && cfg.dev ? (uint32_t)sdev_pres[s] : 0u};
-      // DeviceShare's FilterReservation / ScoreReservation in the nomination (reservations holding devices)
+      // DeviceShare's FilterReservation / ScoreReservation in the nomination (reservations holding devices); the
+      // view's classification once per nomination
+      DrsSet dset{0ull, 0ull, 0u};
+      bool dset_on = false;
       auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
         *ds = 0;
         if constexpr (DEV && (FEAT & 16) != 0) {
           if (!sdv.held()) return false;
-          const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(cfg, pod), sdv, v, i);
+          if (!dset_on) {
+            dset = drs_set(v, pod.rsv_class);
+            dset_on = true;
+          }
+          const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(cfg, pod), sdv, v, dset, i);
           *ds = (int32_t)(uint32_t)r;
           return (r >> 32) != 0;
         }

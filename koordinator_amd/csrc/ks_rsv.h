@@ -115,7 +115,7 @@ struct RsvG {
   __device__ __forceinline__ int32_t csr(int64_t i) const { return (int32_t)(b + i); }
   __device__ __forceinline__ int64_t dal(int w, int64_t i) const { return gld(rv.dal + (int64_t)w * rv.nr + b + i); }
   __device__ __forceinline__ uint32_t dmask(int64_t i) const { return gld(rv.dmask + b + i); }
-  __device__ __forceinline__ int64_t dald(int w, int64_t i) const { return rld<true>(rv.dald + (int64_t)w * rv.nr + b + i); }
+  __device__ __forceinline__ int64_t dald(int w, int64_t i) const { return rld<FRESH>(rv.dald + (int64_t)w * rv.nr + b + i); }
 };
 
 template <int D>
@@ -391,12 +391,12 @@ __device__ __forceinline__ DevOut dev_rsv_eval(const Cfg& c, const PodRec& p, co
 // DeviceShare's FilterReservation + ScoreReservation of reservation i (plugin.go:322-358, scoring.go:99-142): it holds
 // devices and tryAllocateFromReservation([i], required) allocates; *ds = its scoreWithReservation
 template <typename DV, typename V>
-__device__ __forceinline__ bool dev_rsv_candidate(const Cfg& c, const PodRec& p, const DV& dv, const V& v, int64_t i, int32_t* ds) {
+__device__ __forceinline__ bool dev_rsv_candidate(const Cfg& c, const PodRec& p, const DV& dv, const V& v, const DrsSet& s,
+                                                  int64_t i, int32_t* ds) {
   *ds = 0;
   if (!dv.present() || !rsv_dev_matched(v, i, p.rsv_class)) return false;
   GpuReq g;
   if (dev_prepare(p, dv, g)) return false;
-  const DrsSet s = drs_set(v, p.rsv_class);
   if (dev_rsv_try<false>(c, p, dv, v, s, i, nullptr).reasons) return false;
   *ds = dev_rsv_score(c, p, dv, v, s, i, g);
   return true;
@@ -641,12 +641,12 @@ __device__ __attribute__((noinline)) DevOut dev_rsv_eval_x(DevRsvArgs x, DV dv, 
 }
 // (ok << 32) | ds
 template <typename DV, typename V>
-__device__ __attribute__((noinline)) uint64_t dev_rsv_candidate_x(DevRsvArgs x, DV dv, V v, int64_t i) {
+__device__ __attribute__((noinline)) uint64_t dev_rsv_candidate_x(DevRsvArgs x, DV dv, V v, DrsSet s, int64_t i) {
   Cfg c;
   PodRec p;
   dev_rsv_unpack(x, c, p);
   int32_t ds = 0;
-  const bool ok = dev_rsv_candidate(c, p, dv, v, i, &ds);
+  const bool ok = dev_rsv_candidate(c, p, dv, v, s, i, &ds);
   return ((uint64_t)(ok ? 1u : 0u) << 32) | (uint32_t)ds;
 }
 
@@ -776,13 +776,20 @@ __device__ __forceinline__ EvalOut eval_full(const Cfg& c, const PodRec& p, Node
   RsvDelta<NSC> dl;
   RsvOut ro{(p.flags & KS_POD_RSV_AFFINITY) ? KS_R_RSV_AFFINITY : 0u, 0, 0, 0, -1};
   if (slow) {
-    // DeviceShare's FilterReservation / ScoreReservation in the nomination (a pod it restores)
+    // DeviceShare's FilterReservation / ScoreReservation in the nomination (a pod it restores); the view's
+    // classification once per nomination
+    DrsSet dset{0ull, 0ull, 0u};
+    bool dset_on = false;
     auto dnom = [&](const auto& v, int64_t i, int32_t* ds) -> bool {
       *ds = 0;
       if constexpr (HELD) {
         const auto dv = devv();
         if (!dv.held()) return false;
-        const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(c, p), dv, v, i);
+        if (!dset_on) {
+          dset = drs_set(v, p.rsv_class);
+          dset_on = true;
+        }
+        const uint64_t r = dev_rsv_candidate_x(dev_rsv_args(c, p), dv, v, dset, i);
         *ds = (int32_t)(uint32_t)r;
         return (r >> 32) != 0;
       }
