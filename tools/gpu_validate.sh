@@ -1,5 +1,6 @@
 #!/bin/bash
-# One library's validation on one MI355X: the -m gpu parity suite, then the c3r / c3rd wall-clock timer (tools/c3r_time.py).
+# One library's validation on one MI355X: the -m gpu parity suite, then the c3r / c3rd wall-clock timer
+# (tools/c3r_time.py).  Round-end evidence (smoke, bench line, profiles) is tools/gpu_final.sh.
 set -o pipefail
 O=gpurun_out/${1:-val}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
